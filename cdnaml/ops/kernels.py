@@ -1,0 +1,491 @@
+"""Tensor-level entry points for every native kernel (SURVEY §2.10 K1–K15).
+
+Each op dispatches on the device of its inputs:
+
+* device tensors (ROCm/HIP) -> the hand-written gfx950 kernel in
+  ``csrc/kernels`` via :mod:`cdnaml.ops._lib` (fails loudly if the library
+  cannot be built/loaded);
+* CPU tensors -> a plain PyTorch reference implementation of the same op.
+  These references define the semantics and are the oracles of the GPU
+  numerics tests (tests/test_kernels_gpu.py).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import philox as _philox
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(dev: torch.device):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _native(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# --------------------------------------------------------------------- K1
+def gram(X: torch.Tensor, y: Optional[torch.Tensor] = None, shift: Optional[torch.Tensor] = None,
+         yshift: float = 0.0, bf16: bool = False) -> torch.Tensor:
+    """Return A^T A (float64, (d+2)x(d+2)) for A = [X - shift | 1 | y - yshift].
+
+    Column d is the intercept column of ones; column d+1 is y (zeros if None).
+    """
+    n, d = X.shape
+    if X.dtype != torch.float32:
+        X = X.float()
+    if _native(X) and d + 2 <= 512:
+        X = X if X.stride(1) == 1 else X.contiguous()
+        y32 = None if y is None else y.float().contiguous()
+        sh = None if shift is None else shift.float().contiguous()
+        L = _lib.lib()
+        ws_n = L.cdna_gram_workspace(n, d, int(bf16))
+        ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=X.device)
+        out = torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
+        _lib.check(L.cdna_gram(_ptr(X), n, d, X.stride(0), _ptr(y32), _ptr(sh), float(yshift), _ptr(out), _ptr(ws),
+                               int(bf16), _stream(X.device)), "cdna_gram")
+        return out
+    A = torch.empty((n, d + 2), dtype=torch.float32, device=X.device)
+    A[:, :d] = X if shift is None else X - shift.float()
+    A[:, d] = 1.0
+    A[:, d + 1] = 0.0 if y is None else (y.float() - yshift)
+    if bf16:
+        A = A.to(torch.bfloat16)
+    A = A.double()
+    return A.T @ A
+
+
+# -------------------------------------------------------------------- K15
+def uniform(n: int, seed: int, offset: int = 0, stream: int = 0, device=None) -> torch.Tensor:
+    """Philox uniform doubles keyed by (seed, offset+i, stream)."""
+    device = torch.device(device) if device is not None else torch.device("cpu")
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    if device.type == "cuda":
+        out = torch.empty(n, dtype=torch.float64, device=device)
+        _lib.check(_lib.lib().cdna_uniform(_ptr(out), n, seed, int(offset), int(stream) & 0xFFFFFFFF,
+                                           _stream(device)), "cdna_uniform")
+        return out
+    return torch.from_numpy(_philox.uniform(n, seed, int(offset), int(stream)))
+
+
+def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=None) -> torch.Tensor:
+    """uint8 [T, n] Poisson(rate) bootstrap multiplicities, tree t on stream 0x100+t."""
+    device = torch.device(device) if device is not None else torch.device("cpu")
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    if device.type == "cuda":
+        out = torch.empty((T, n), dtype=torch.uint8, device=device)
+        _lib.check(_lib.lib().cdna_poisson(_ptr(out), T, n, seed, int(offset), float(rate), _stream(device)),
+                   "cdna_poisson")
+        return out
+    return torch.from_numpy(_philox.poisson(T, n, seed, int(offset), float(rate)))
+
+
+# --------------------------------------------------------------------- K4
+def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor) -> torch.Tensor:
+    """Raw features -> uint8 bins in feature-group-major layout [G, n, 8].
+
+    Continuous feature f: bin = #{thr[f, :nthr[f]] < x}; NaN -> nthr[f].
+    Categorical feature (nthr[f] < 0): bin = clamp(int(x), 0, 255).
+    """
+    n, d = X.shape
+    G = (d + 7) // 8
+    tmax = thr.shape[1] if thr.dim() == 2 else 0
+    if _native(X):
+        X = X.float()
+        X = X if X.stride(1) == 1 else X.contiguous()
+        thr = thr.float().contiguous()
+        nthr = nthr.int().contiguous()
+        out = torch.empty((G, n, 8), dtype=torch.uint8, device=X.device)
+        if n:
+            _lib.check(_lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, _ptr(out),
+                                              _stream(X.device)), "cdna_binize")
+        return out
+    out = torch.zeros((G, n, 8), dtype=torch.uint8)
+    Xf = X.float()
+    for f in range(d):
+        nt = int(nthr[f])
+        x = Xf[:, f]
+        if nt < 0:
+            b = torch.clamp(x.to(torch.int64), 0, 255)
+        else:
+            b = torch.searchsorted(thr[f, :nt].float().contiguous(), x.contiguous(), right=False)
+            b = torch.where(torch.isnan(x), torch.full_like(b, nt), b)
+        out[f // 8, :, f % 8] = b.to(torch.uint8)
+    return out
+
+
+def bins_to_matrix(bins: torch.Tensor, d: int) -> torch.Tensor:
+    """[G, n, 8] -> [n, d] (int64) view helper for reference code."""
+    G, n, _ = bins.shape
+    return bins.permute(1, 0, 2).reshape(n, G * 8)[:, :d].to(torch.int64)
+
+
+# --------------------------------------------------------------------- K5
+def _slot_groups(slot_tree: np.ndarray, SB: int):
+    S = len(slot_tree)
+    s0, t0, t1 = [], [], []
+    for a in range(0, S, SB):
+        b = min(S, a + SB)
+        s0.append(a)
+        t0.append(int(slot_tree[a]))
+        t1.append(int(slot_tree[b - 1]))
+    return np.array(s0, np.int32), np.array(t0, np.int32), np.array(t1, np.int32)
+
+
+def _plan_chunks(n: int, G: int, ngroups: int, target_blocks: int = 2048) -> int:
+    per = max(1, target_blocks // max(1, G * ngroups))
+    return int(max(1, min(per, (n + 4095) // 4096)))
+
+
+def hist_moments(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optional[torch.Tensor],
+                 v0: Optional[torch.Tensor], v1: torch.Tensor, build_slot: torch.Tensor, slot_tree: np.ndarray,
+                 feat_mask: Optional[torch.Tensor], B: int, lds_budget: int = 64 * 1024) -> torch.Tensor:
+    """Per-slot (feature, bin) weighted moments: out[S, d, B, 2] (float64).
+
+    out[s, f, b, 0] = sum w_t(r) * v0(r), out[s, f, b, 1] = sum w_t(r) * v1(r) over
+    rows r whose active node in tree t maps to build slot s and bin_f(r) == b,
+    restricted to features enabled in feat_mask[s] (bit f).
+    """
+    S = len(slot_tree)
+    G, n, _ = bins.shape
+    T = node.shape[0]
+    out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
+    if S == 0 or n == 0:
+        return out
+    if _native(bins):
+        SB = max(1, min(S, lds_budget // (8 * B * 2 * 4)))
+        s0, t0, t1 = _slot_groups(np.asarray(slot_tree), SB)
+        ng = len(s0)
+        grp = torch.from_numpy(np.concatenate([s0, t0, t1])).to(bins.device)
+        nchunk = _plan_chunks(n, G, ng)
+        mw = 0 if feat_mask is None else feat_mask.shape[1]
+        fm = None if feat_mask is None else feat_mask.int().contiguous()
+        node = node.int().contiguous()
+        weight = None if weight is None else weight.to(torch.uint8).contiguous()
+        v0 = None if v0 is None else v0.float().contiguous()
+        v1 = v1.float().contiguous()
+        build_slot = build_slot.int().contiguous()
+        _lib.check(_lib.lib().cdna_hist_moments(
+            _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0), _ptr(v1), _ptr(build_slot), _ptr(fm), mw, S,
+            B, SB, ng, _ptr(grp), _ptr(grp) + 4 * ng, _ptr(grp) + 8 * ng, nchunk, _ptr(out), _stream(bins.device)),
+            "cdna_hist_moments")
+        return out
+    bm = bins_to_matrix(bins, d)
+    a0 = torch.ones(n, dtype=torch.float64) if v0 is None else v0.double()
+    a1 = v1.double()
+    fr = torch.arange(d)
+    flat = out.view(-1, 2)
+    for t in range(T):
+        ids = node[t].long()
+        ok = ids >= 0
+        slot = torch.full_like(ids, -1)
+        slot[ok] = build_slot.long()[ids[ok]]
+        ok = slot >= 0
+        w = torch.ones(n, dtype=torch.float64) if weight is None else weight[t].double()
+        ok = ok & (w != 0)
+        if not ok.any():
+            continue
+        rs = slot[ok]
+        idx = (rs[:, None] * d + fr[None, :]) * B + bm[ok]
+        msk = torch.ones_like(idx, dtype=torch.bool)
+        if feat_mask is not None:
+            words = feat_mask.long()[rs]  # [m, MW]
+            bits = (words[:, fr // 32] >> (fr % 32)) & 1
+            msk = bits.bool()
+        wx0 = (w[ok] * a0[ok])[:, None].expand_as(idx)
+        wx1 = (w[ok] * a1[ok])[:, None].expand_as(idx)
+        flat[:, 0] += torch.bincount(idx[msk], weights=wx0[msk], minlength=flat.shape[0])
+        flat[:, 1] += torch.bincount(idx[msk], weights=wx1[msk], minlength=flat.shape[0])
+    return out
+
+
+def hist_classes(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optional[torch.Tensor],
+                 label: torch.Tensor, C: int, build_slot: torch.Tensor, slot_tree: np.ndarray,
+                 feat_mask: Optional[torch.Tensor], B: int, lds_budget: int = 64 * 1024) -> torch.Tensor:
+    """Per-slot (feature, bin) weighted class counts: out[S, d, B, C] (float64)."""
+    S = len(slot_tree)
+    G, n, _ = bins.shape
+    T = node.shape[0]
+    out = torch.zeros((S, d, B, C), dtype=torch.float64, device=bins.device)
+    if S == 0 or n == 0:
+        return out
+    if _native(bins):
+        SB = max(1, min(S, lds_budget // (8 * B * C * 4)))
+        if 8 * B * C * 4 > 160 * 1024:
+            raise ValueError("too many classes x bins for the LDS histogram")
+        s0, t0, t1 = _slot_groups(np.asarray(slot_tree), SB)
+        ng = len(s0)
+        grp = torch.from_numpy(np.concatenate([s0, t0, t1])).to(bins.device)
+        nchunk = _plan_chunks(n, G, ng)
+        mw = 0 if feat_mask is None else feat_mask.shape[1]
+        fm = None if feat_mask is None else feat_mask.int().contiguous()
+        lab = label.int().contiguous()
+        node = node.int().contiguous()
+        weight = None if weight is None else weight.to(torch.uint8).contiguous()
+        build_slot = build_slot.int().contiguous()
+        _lib.check(_lib.lib().cdna_hist_classes(
+            _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(lab), C, _ptr(build_slot), _ptr(fm), mw, S, B, SB,
+            ng, _ptr(grp), _ptr(grp) + 4 * ng, _ptr(grp) + 8 * ng, nchunk, _ptr(out), _stream(bins.device)),
+            "cdna_hist_classes")
+        return out
+    bm = bins_to_matrix(bins, d)
+    lab = label.long()
+    fr = torch.arange(d)
+    flat = out.view(-1)
+    for t in range(T):
+        ids = node[t].long()
+        ok = ids >= 0
+        slot = torch.full_like(ids, -1)
+        slot[ok] = build_slot.long()[ids[ok]]
+        w = torch.ones(n, dtype=torch.float64) if weight is None else weight[t].double()
+        ok = (slot >= 0) & (w != 0) & (lab >= 0) & (lab < C)
+        if not ok.any():
+            continue
+        rs = slot[ok]
+        idx = ((rs[:, None] * d + fr[None, :]) * B + bm[ok]) * C + lab[ok][:, None]
+        msk = torch.ones_like(idx, dtype=torch.bool)
+        if feat_mask is not None:
+            words = feat_mask.long()[rs]
+            msk = ((words[:, fr // 32] >> (fr % 32)) & 1).bool()
+        wx = w[ok][:, None].expand_as(idx)
+        flat += torch.bincount(idx[msk], weights=wx[msk], minlength=flat.shape[0])
+    return out
+
+
+# --------------------------------------------------------------------- K7
+def partition(bins: torch.Tensor, node: torch.Tensor, split_feat: torch.Tensor, split_bin: torch.Tensor,
+              cat_off: torch.Tensor, cat_mask: torch.Tensor, child: torch.Tensor) -> None:
+    """In-place: move each row of each tree from its active node to the chosen child."""
+    G, n, _ = bins.shape
+    T = node.shape[0]
+    if n == 0 or T == 0:
+        return
+    if _native(bins):
+        cm = cat_mask.int().contiguous() if cat_mask.numel() else torch.zeros(8, dtype=torch.int32,
+                                                                                 device=bins.device)
+        assert node.dtype == torch.int32 and node.is_contiguous()
+        split_feat, split_bin = split_feat.int().contiguous(), split_bin.int().contiguous()
+        cat_off, child = cat_off.int().contiguous(), child.int().contiguous()
+        _lib.check(_lib.lib().cdna_partition(_ptr(bins), n, T, _ptr(node), _ptr(split_feat), _ptr(split_bin),
+                                             _ptr(cat_off), _ptr(cm), _ptr(child), _stream(bins.device)),
+                   "cdna_partition")
+        return
+    d = G * 8
+    bm = bins_to_matrix(bins, d)
+    sf = split_feat.long()
+    sb = split_bin.long()
+    co = cat_off.long()
+    cm = cat_mask.long() & 0xFFFFFFFF
+    ch = child.long().view(-1, 2)
+    rows = torch.arange(n)
+    for t in range(T):
+        ids = node[t].long()
+        ok = ids >= 0
+        if not ok.any():
+            continue
+        i = ids[ok]
+        f = sf[i]
+        leaf = f < 0
+        fb = bm[rows[ok], f.clamp(min=0)]
+        cat = co[i] >= 0
+        words = cm[(co[i].clamp(min=0) * 8 + (fb >> 5))] if cm.numel() else torch.zeros_like(fb)
+        left = torch.where(cat, ((words >> (fb & 31)) & 1).bool(), fb <= sb[i])
+        nxt = torch.where(left, ch[i, 0], ch[i, 1])
+        nxt = torch.where(leaf, torch.full_like(nxt, -1), nxt)
+        new = ids.clone()
+        new[ok] = nxt
+        node[t] = new.to(node.dtype)
+
+
+# --------------------------------------------------------------------- K8
+def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree_w: torch.Tensor,
+                 values: torch.Tensor, masks: torch.Tensor, K: int, base: Optional[torch.Tensor] = None
+                 ) -> torch.Tensor:
+    """Ensemble prediction on raw features -> float32 [n, K].
+
+    nodes: int32 [N, 4] packed as documented in trees.hip.
+    """
+    n, d = X.shape
+    T = roots.numel()
+    if _native(X):
+        X = X.float()
+        X = X if X.stride(1) == 1 else X.contiguous()
+        out = torch.empty((n, K), dtype=torch.float32, device=X.device)
+        if n:
+            m = masks.int().contiguous() if masks.numel() else torch.zeros(8, dtype=torch.int32, device=X.device)
+            nodes, roots = nodes.int().contiguous(), roots.int().contiguous()
+            tree_w, values = tree_w.float().contiguous(), values.float().contiguous()
+            base = None if base is None else base.float().contiguous()
+            _lib.check(_lib.lib().cdna_tree_predict(_ptr(X), n, d, X.stride(0), _ptr(nodes), _ptr(roots),
+                                                    _ptr(tree_w), T, _ptr(values), _ptr(m), K, _ptr(base), _ptr(out),
+                                                    _stream(X.device)), "cdna_tree_predict")
+        return out
+    Xf = X.float()
+    out = torch.zeros((n, K), dtype=torch.float32)
+    if base is not None:
+        out += base.float()[None, :]
+    nd = nodes.long()
+    vals = values.float()
+    mk = masks.long() & 0xFFFFFFFF
+    rows = torch.arange(n)
+    for t in range(T):
+        cur = torch.full((n,), int(roots[t]), dtype=torch.long)
+        for _ in range(64):
+            nv = nd[cur]
+            internal = nv[:, 0] != -1
+            if not internal.any():
+                break
+            f = nv[:, 0]
+            cont = f >= 0
+            fi = torch.where(cont, f, -f - 2).clamp(min=0)
+            x = Xf[rows, fi]
+            thr = nv[:, 1].to(torch.int32).view(torch.float32)
+            c = x.to(torch.int64)
+            okc = (c >= 0) & (c < 256)
+            cc = c.clamp(0, 255)
+            moff = torch.where(cont, torch.zeros_like(f), nv[:, 1]).clamp(min=0)
+            words = mk[(moff * 8 + (cc >> 5))] if mk.numel() else torch.zeros_like(cc)
+            catleft = okc & ((words >> (cc & 31)) & 1).bool()
+            left = torch.where(cont, x <= thr, catleft)
+            nxt = torch.where(left, nv[:, 2], nv[:, 3])
+            cur = torch.where(internal, nxt, cur)
+        off = nd[cur][:, 1]
+        idx = off[:, None] + torch.arange(K)[None, :]
+        out += float(tree_w[t]) * vals[idx]
+    return out
+
+
+def predict_binned_add(bins: torch.Tensor, nodes: torch.Tensor, root: int, values: torch.Tensor,
+                       masks: torch.Tensor, scale: float, out: torch.Tensor) -> None:
+    """out[r] += scale * leaf value of a bin-threshold tree (GBDT margin update)."""
+    G, n, _ = bins.shape
+    if n == 0:
+        return
+    if _native(bins):
+        m = masks.int().contiguous() if masks.numel() else torch.zeros(8, dtype=torch.int32, device=bins.device)
+        nodes, values = nodes.int().contiguous(), values.float().contiguous()
+        assert out.dtype == torch.float32 and out.is_contiguous()
+        _lib.check(_lib.lib().cdna_predict_binned_add(_ptr(bins), n, _ptr(nodes), int(root), _ptr(values), _ptr(m),
+                                                      float(scale), _ptr(out), _stream(bins.device)),
+                   "cdna_predict_binned_add")
+        return
+    bm = bins_to_matrix(bins, G * 8)
+    nd = nodes.long()
+    mk = masks.long() & 0xFFFFFFFF
+    rows = torch.arange(n)
+    cur = torch.full((n,), int(root), dtype=torch.long)
+    for _ in range(64):
+        nv = nd[cur]
+        internal = nv[:, 0] != -1
+        if not internal.any():
+            break
+        f = nv[:, 0]
+        cont = f >= 0
+        fi = torch.where(cont, f, -f - 2).clamp(min=0)
+        b = bm[rows, fi]
+        moff = torch.where(cont, torch.zeros_like(f), nv[:, 1]).clamp(min=0)
+        words = mk[(moff * 8 + (b >> 5))] if mk.numel() else torch.zeros_like(b)
+        left = torch.where(cont, b <= nv[:, 1], ((words >> (b & 31)) & 1).bool())
+        cur = torch.where(internal, torch.where(left, nv[:, 2], nv[:, 3]), cur)
+    out += scale * values.float()[nd[cur][:, 1]]
+
+
+# -------------------------------------------------------------------- K13
+def reg_metrics(y: torch.Tensor, p: torch.Tensor, w: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[Σw, Σw e², Σw|e|, Σw y, Σw y², Σw p, Σw p², Σw y p] as float64[8] (local)."""
+    y = y.double().contiguous()
+    p = p.double().contiguous()
+    w = None if w is None else w.double().contiguous()
+    if _native(y):
+        acc = torch.zeros(8, dtype=torch.float64, device=y.device)
+        _lib.check(_lib.lib().cdna_reg_metrics(_ptr(y), _ptr(p), _ptr(w), y.numel(), _ptr(acc), _stream(y.device)),
+                   "cdna_reg_metrics")
+        return acc
+    ww = torch.ones_like(y) if w is None else w
+    e = y - p
+    return torch.stack([ww.sum(), (ww * e * e).sum(), (ww * e.abs()).sum(), (ww * y).sum(), (ww * y * y).sum(),
+                        (ww * p).sum(), (ww * p * p).sum(), (ww * y * p).sum()])
+
+
+# -------------------------------------------------------------------- K14
+def score_hist(score: torch.Tensor, label: torch.Tensor, lo: float, hi: float, nb: int) -> torch.Tensor:
+    score = score.double().contiguous()
+    label = label.double().contiguous()
+    if _native(score):
+        h = torch.zeros((nb, 2), dtype=torch.float64, device=score.device)
+        _lib.check(_lib.lib().cdna_score_hist(_ptr(score), _ptr(label), score.numel(), float(lo), float(hi), nb,
+                                              _ptr(h), _stream(score.device)), "cdna_score_hist")
+        return h
+    scale = nb / (hi - lo) if hi > lo else 0.0
+    b = ((score - lo) * scale).floor().long().clamp(0, nb - 1)
+    pos = (label > 0.5).long()
+    h = torch.zeros(nb * 2, dtype=torch.float64)
+    h.index_add_(0, b * 2 + pos, torch.ones_like(score))
+    return h.view(nb, 2)
+
+
+# -------------------------------------------------------------------- K10
+def kmeans_step(X: torch.Tensor, C: torch.Tensor, with_sums: bool = True):
+    """Assign rows to nearest centre; return (assign, sums[k,d], counts[k], cost) (local)."""
+    n, d = X.shape
+    k = C.shape[0]
+    if _native(X) and (2 * k * d + k) * 4 <= 64 * 1024:
+        X = X.float()
+        X = X if X.stride(1) == 1 else X.contiguous()
+        Cf = C.float().contiguous()
+        assign = torch.empty(n, dtype=torch.int32, device=X.device)
+        sums = torch.zeros((k, d), dtype=torch.float64, device=X.device)
+        counts = torch.zeros(k, dtype=torch.float64, device=X.device)
+        cost = torch.zeros(1, dtype=torch.float64, device=X.device)
+        if n:
+            _lib.check(_lib.lib().cdna_kmeans_step(_ptr(X), n, d, X.stride(0), _ptr(Cf), k, _ptr(assign),
+                                                   _ptr(sums) if with_sums else None,
+                                                   _ptr(counts) if with_sums else None, _ptr(cost),
+                                                   _stream(X.device)), "cdna_kmeans_step")
+        return assign, sums, counts, cost[0]
+    Xf = X.float()
+    dist = torch.cdist(Xf, C.float()) ** 2
+    best, assign = dist.min(dim=1)
+    sums = torch.zeros((k, d), dtype=torch.float64, device=X.device)
+    sums.index_add_(0, assign, Xf.double())
+    counts = torch.bincount(assign, minlength=k).double()
+    return assign.int(), sums, counts, best.double().sum()
+
+
+# -------------------------------------------------------------------- K11
+def logistic_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b: float,
+                  wt: Optional[torch.Tensor] = None):
+    """Binary logistic loss and gradient (local sums): returns (grad[d+1], loss)."""
+    n, d = X.shape
+    y = y.double().contiguous()
+    wt = None if wt is None else wt.double().contiguous()
+    if _native(X) and d <= 512:
+        X = X.float()
+        X = X if X.stride(1) == 1 else X.contiguous()
+        wd = w.double().contiguous()
+        grad = torch.zeros(d + 1, dtype=torch.float64, device=X.device)
+        loss = torch.zeros(1, dtype=torch.float64, device=X.device)
+        if n:
+            _lib.check(_lib.lib().cdna_logistic_grad(_ptr(X), n, d, X.stride(0), _ptr(y), _ptr(wt), _ptr(wd),
+                                                     float(b), _ptr(grad), _ptr(loss), _stream(X.device)),
+                       "cdna_logistic_grad")
+        return grad, loss[0]
+    Xd = X.double()
+    m = Xd @ w.double() + b
+    p = torch.sigmoid(m)
+    ww = torch.ones_like(y) if wt is None else wt
+    res = ww * (p - y)
+    g = torch.empty(d + 1, dtype=torch.float64, device=X.device)
+    g[:d] = Xd.T @ res
+    g[d] = res.sum()
+    loss = (ww * (torch.nn.functional.softplus(m) - y * m)).sum()
+    return g, loss

@@ -1,0 +1,291 @@
+// K1 gram_xtx — fused [X-s | 1 | y-ys]ᵀ[X-s | 1 | y-ys] on MFMA.
+//
+// One pass over the row-major feature matrix produces every sufficient
+// statistic LinearRegression / standardisation needs (XᵀX, Xᵀy, column sums,
+// n, yᵀy) without materialising the augmented matrix.  Reference behaviour:
+// LinearRegression "normal" solver, ML 02 - Linear Regression I.py:84-123,
+// Labs/ML 02L:68-79.
+//
+// Mapping (v_mfma_f32_32x32x2_f32, exact f32): the reduction axis of the
+// Gram is the ROW axis, so for an output tile (I,J) lane l supplies
+//   A[i=l&31][k=l>>5] = Â[k0 + (l>>5)][32I + (l&31)]
+//   B[k=l>>5][j=l&31] = Â[k0 + (l>>5)][32J + (l&31)]
+// i.e. each half-wave reads 128 contiguous bytes of one row: fully coalesced
+// global loads straight into the MFMA operands, no LDS staging needed.
+// Each wave owns a contiguous row range and P upper-triangular tiles; the 4
+// waves of a block are folded through LDS atomics and each block writes one
+// f32 partial slab, reduced deterministically in f64 by gram_reduce_kernel.
+//
+// bf16 variant: inputs rounded to bf16 and fed to v_mfma_f32_32x32x16_bf16
+// through an LDS transpose (ds_read of 8 consecutive rows per lane).
+#include "common.h"
+
+namespace {
+
+constexpr int kMaxPairs = 160;
+struct PairTable {
+  int16_t I[kMaxPairs];
+  int16_t J[kMaxPairs];
+};
+
+__device__ __forceinline__ float aug_val(const float* __restrict__ X, const float* __restrict__ y,
+                                         int64_t r, int c, int d, int64_t ldx, float s, bool valid) {
+  if (!valid) return 0.f;
+  if (c < d) return X[r * ldx + c] - s;
+  if (c == d) return 1.f;
+  if (c == d + 1 && y != nullptr) return y[r] - s;
+  return 0.f;
+}
+
+__device__ __forceinline__ float col_shift(const float* __restrict__ shift, float yshift, int c, int d) {
+  if (c < d) return shift ? shift[c] : 0.f;
+  if (c == d + 1) return yshift;
+  return 0.f;
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void gram_f32_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                       const float* __restrict__ y, const float* __restrict__ shift,
+                                                       float yshift, PairTable tab, int npairs,
+                                                       float* __restrict__ partial, int64_t rows_per_wave) {
+  __shared__ float red[P * 1024];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < P * 1024; i += 256) red[i] = 0.f;
+
+  const int pbase = blockIdx.y * P;
+  int ca[P], cb[P];
+  float sa[P], sb[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int gp = pbase + p < npairs ? pbase + p : npairs - 1;
+    ca[p] = tab.I[gp] * 32 + (lane & 31);
+    cb[p] = tab.J[gp] * 32 + (lane & 31);
+    sa[p] = col_shift(shift, yshift, ca[p], d);
+    sb[p] = col_shift(shift, yshift, cb[p], d);
+  }
+  f32x16 acc[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[p][e] = 0.f;
+
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wid;
+  const int64_t r0 = gw * rows_per_wave;
+  int64_t r1 = r0 + rows_per_wave;
+  if (r1 > n) r1 = n;
+  const int half = lane >> 5;
+  for (int64_t k0 = r0; k0 < r1; k0 += 4) {
+    // two MFMA k-steps (4 rows) per iteration: issue all loads first
+    const int64_t ra = k0 + half, rb = k0 + 2 + half;
+    const bool va = ra < r1, vb = rb < r1;
+    float a0[P], b0[P], a1[P], b1[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      a0[p] = aug_val(X, y, ra, ca[p], d, ldx, sa[p], va);
+      b0[p] = aug_val(X, y, ra, cb[p], d, ldx, sb[p], va);
+      a1[p] = aug_val(X, y, rb, ca[p], d, ldx, sa[p], vb);
+      b1[p] = aug_val(X, y, rb, cb[p], d, ldx, sb[p], vb);
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[p], b0[p], acc[p], 0, 0, 0);
+      acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[p], b1[p], acc[p], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  const int col = lane & 31;
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * half;
+      atomicAdd(&red[p * 1024 + row * 32 + col], acc[p][e]);
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < P * 1024; i += 256) {
+    const int p = i >> 10;
+    if (pbase + p < npairs) partial[((int64_t)blockIdx.x * npairs + pbase + p) * 1024 + (i & 1023)] = red[i];
+  }
+}
+
+// bf16 inputs / f32 accumulate: 16 rows per MFMA. A 64-row tile of the
+// augmented matrix is converted to bf16 and stored TRANSPOSED in LDS
+// (tile[c][r], 64 rows -> 128 B per column) so each lane's 8-row fragment of
+// one column is one 16-byte ds_read.
+template <int P>
+__global__ __launch_bounds__(256) void gram_bf16_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                        const float* __restrict__ y, const float* __restrict__ shift,
+                                                        float yshift, PairTable tab, int npairs, int Dpad,
+                                                        float* __restrict__ partial, int64_t rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // column stride 64 rows * 2 B = 128 B, padded by 16 B to spread banks
+  constexpr int kColStride = 72;  // in bf16 elements (144 B)
+  uint16_t* tile = reinterpret_cast<uint16_t*>(smem);
+  float* red = reinterpret_cast<float*>(smem + (size_t)Dpad * kColStride * 2);
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < P * 1024; i += 256) red[i] = 0.f;
+  const int pbase = blockIdx.y * P;
+  int ta[P], tb[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int gp = pbase + p < npairs ? pbase + p : npairs - 1;
+    ta[p] = tab.I[gp];
+    tb[p] = tab.J[gp];
+  }
+  f32x16 acc[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[p][e] = 0.f;
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  const int64_t rb0 = (int64_t)blockIdx.x * rows_per_block;
+  int64_t rb1 = rb0 + rows_per_block;
+  if (rb1 > n) rb1 = n;
+  const int half = lane >> 5;
+  for (int64_t t0 = rb0; t0 < rb1; t0 += 64) {
+    __syncthreads();
+    // stage: element e -> (row r = e / Dpad, col c = e % Dpad); coalesced along c
+    for (int e = threadIdx.x; e < 64 * Dpad; e += 256) {
+      const int r = e / Dpad, c = e - r * Dpad;
+      const int64_t gr = t0 + r;
+      const float v = aug_val(X, y, gr, c, d, ldx, col_shift(shift, yshift, c, d), gr < rb1);
+      const __bf16 b = (__bf16)v;  // RNE, lowers to v_cvt_pk_bf16_f32
+      tile[c * kColStride + r] = __builtin_bit_cast(uint16_t, b);
+    }
+    __syncthreads();
+    // each wave takes a 16-row k-slice of the 64-row tile
+    const int kr = wid * 16 + 8 * half;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&tile[(ta[p] * 32 + (lane & 31)) * kColStride + kr]);
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(&tile[(tb[p] * 32 + (lane & 31)) * kColStride + kr]);
+      acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[p], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  const int col = lane & 31;
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * half;
+      atomicAdd(&red[p * 1024 + row * 32 + col], acc[p][e]);
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < P * 1024; i += 256) {
+    const int p = i >> 10;
+    if (pbase + p < npairs) partial[((int64_t)blockIdx.x * npairs + pbase + p) * 1024 + (i & 1023)] = red[i];
+  }
+}
+
+__global__ void gram_reduce_kernel(const float* __restrict__ partial, int nblk, int npairs, PairTable tab, int D,
+                                   double* __restrict__ out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)npairs * 1024) return;
+  const int gp = (int)(idx >> 10), e = (int)(idx & 1023);
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += (double)partial[((int64_t)b * npairs + gp) * 1024 + e];
+  const int i = tab.I[gp] * 32 + (e >> 5), j = tab.J[gp] * 32 + (e & 31);
+  if (i < D && j < D) {
+    out[(int64_t)i * D + j] = s;
+    out[(int64_t)j * D + i] = s;
+  }
+}
+
+struct GramPlan {
+  PairTable tab;
+  int npairs, P, ngroups, nblk, D;
+  int64_t rows_per_unit;
+};
+
+GramPlan make_plan(int64_t n, int d, bool bf16) {
+  GramPlan pl{};
+  pl.D = d + 2;
+  const int T = (pl.D + 31) / 32;
+  int k = 0;
+  for (int i = 0; i < T; ++i)
+    for (int j = i; j < T; ++j) {
+      pl.tab.I[k] = (int16_t)i;
+      pl.tab.J[k] = (int16_t)j;
+      ++k;
+    }
+  pl.npairs = k;
+  const int maxP = bf16 ? 4 : 8;
+  pl.ngroups = (k + maxP - 1) / maxP;
+  pl.P = (k + pl.ngroups - 1) / pl.ngroups;
+  int64_t nb = (n + 8191) / 8192;
+  if (nb > 256) nb = 256;
+  if (nb < 1) nb = 1;
+  pl.nblk = (int)nb;
+  if (bf16) {
+    int64_t rpb = (n + nb - 1) / nb;
+    rpb = (rpb + 63) / 64 * 64;
+    pl.rows_per_unit = rpb;
+  } else {
+    const int64_t waves = nb * 4;
+    int64_t rpw = (n + waves - 1) / waves;
+    rpw = (rpw + 3) / 4 * 4;
+    if (rpw < 4) rpw = 4;
+    pl.rows_per_unit = rpw;
+  }
+  return pl;
+}
+
+template <int P>
+void launch_f32(const GramPlan& pl, const float* X, int64_t n, int d, int64_t ldx, const float* y, const float* shift,
+                float yshift, float* ws, hipStream_t st) {
+  hipLaunchKernelGGL(gram_f32_kernel<P>, dim3(pl.nblk, pl.ngroups), dim3(256), 0, st, X, n, d, ldx, y, shift, yshift,
+                     pl.tab, pl.npairs, ws, pl.rows_per_unit);
+}
+template <int P>
+void launch_bf16(const GramPlan& pl, const float* X, int64_t n, int d, int64_t ldx, const float* y,
+                 const float* shift, float yshift, float* ws, hipStream_t st) {
+  const int Dpad = ((pl.D + 31) / 32) * 32;
+  const size_t lds = (size_t)Dpad * 72 * 2 + (size_t)P * 1024 * 4;
+  hipLaunchKernelGGL(gram_bf16_kernel<P>, dim3(pl.nblk, pl.ngroups), dim3(256), lds, st, X, n, d, ldx, y, shift,
+                     yshift, pl.tab, pl.npairs, Dpad, ws, pl.rows_per_unit);
+}
+
+}  // namespace
+
+// Workspace (in floats) needed by cdna_gram for an n×d problem.
+CDNA_API int64_t cdna_gram_workspace(int64_t n, int d, int bf16) {
+  GramPlan pl = make_plan(n, d, bf16 != 0);
+  return (int64_t)pl.nblk * pl.npairs * 1024;
+}
+
+// out: (d+2)×(d+2) f64, row-major.  Column d is the all-ones column, column
+// d+1 is y (zeros if y == nullptr).  Supports d+2 <= 512 (160 tile pairs).
+CDNA_API int cdna_gram(const float* X, int64_t n, int d, int64_t ldx, const float* y, const float* shift, float yshift,
+                       double* out, float* ws, int bf16, hipStream_t st) {
+  if (d + 2 > 32 * 17) return (int)hipErrorInvalidValue;
+  GramPlan pl = make_plan(n, d, bf16 != 0);
+  if (pl.npairs > kMaxPairs) return (int)hipErrorInvalidValue;
+  if (bf16) {
+    switch (pl.P) {
+      case 1: launch_bf16<1>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      case 2: launch_bf16<2>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      case 3: launch_bf16<3>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      default: launch_bf16<4>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+    }
+  } else {
+    switch (pl.P) {
+      case 1: launch_f32<1>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      case 2: launch_f32<2>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      case 3: launch_f32<3>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      case 4: launch_f32<4>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      case 5: launch_f32<5>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      case 6: launch_f32<6>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      case 7: launch_f32<7>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      default: launch_f32<8>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+    }
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const int64_t tot = (int64_t)pl.npairs * 1024;
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ws, pl.nblk,
+                     pl.npairs, pl.tab, pl.D, out);
+  return (int)hipGetLastError();
+}

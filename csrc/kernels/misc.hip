@@ -1,0 +1,235 @@
+// K15 philox_rng, K13 reg_metrics, K10 kmeans_step, K11 logistic loss/grad,
+// K14 auc score histogram.
+#include "common.h"
+
+namespace {
+
+inline unsigned grid_for(int64_t n, int per, unsigned cap) {
+  int64_t g = (n + per - 1) / per;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// ---------------------------------------------------------------- K15 RNG
+__global__ void uniform_kernel(double* __restrict__ out, int64_t n, uint64_t seed, uint64_t offset, uint32_t stream) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = cdna::philox_uniform(seed, offset + (uint64_t)i, stream);
+}
+
+// Poisson(rate) bootstrap multiplicities for T trees: out[t][i], stream = t + 1
+// (rate >= 1 with no bootstrap is handled on the host as all-ones).
+__global__ void poisson_kernel(uint8_t* __restrict__ out, int T, int64_t n, uint64_t seed, uint64_t offset,
+                               double rate) {
+  const int t = blockIdx.y;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double u = cdna::philox_uniform(seed, offset + (uint64_t)i, 0x100u + (uint32_t)t);
+    out[(int64_t)t * n + i] = (uint8_t)cdna::poisson_from_uniform(u, rate);
+  }
+}
+
+// ------------------------------------------------------- K13 reg metrics
+// acc: [0]=w [1]=Σw e² [2]=Σw|e| [3]=Σw y [4]=Σw y² [5]=Σw p [6]=Σw p² [7]=Σw y p
+__global__ __launch_bounds__(256) void reg_metrics_kernel(const double* __restrict__ y, const double* __restrict__ p,
+                                                          const double* __restrict__ w, int64_t n,
+                                                          double* __restrict__ acc) {
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double yy = y[i], pp = p[i], ww = w ? w[i] : 1.0;
+    const double e = yy - pp;
+    s[0] += ww;
+    s[1] += ww * e * e;
+    s[2] += ww * fabs(e);
+    s[3] += ww * yy;
+    s[4] += ww * yy * yy;
+    s[5] += ww * pp;
+    s[6] += ww * pp * pp;
+    s[7] += ww * yy * pp;
+  }
+  __shared__ double red[4][8];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const double v = cdna::wave_sum(s[k]);
+    if (lane == 0) red[wid][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const double v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(&acc[threadIdx.x], v);
+  }
+}
+
+// ------------------------------------------------ K14 AUC score histogram
+// Scores are mapped into `nb` equal-width buckets over [lo, hi]; per bucket
+// the weighted positive and negative counts are accumulated (f64).
+__global__ __launch_bounds__(256) void score_hist_kernel(const double* __restrict__ score,
+                                                         const double* __restrict__ label, int64_t n, double lo,
+                                                         double hi, int nb, double* __restrict__ hist) {
+  const double scale = hi > lo ? (double)nb / (hi - lo) : 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    int b = (int)((score[i] - lo) * scale);
+    b = b < 0 ? 0 : (b >= nb ? nb - 1 : b);
+    atomicAdd(&hist[b * 2 + (label[i] > 0.5 ? 1 : 0)], 1.0);
+  }
+}
+
+// -------------------------------------------------------- K10 k-means step
+// assign each row to its nearest centre; accumulate per-centre sums/counts
+// (LDS-privatised, f64 flush).  centres/sums staged in LDS (k*d <= 8192).
+__global__ __launch_bounds__(256) void kmeans_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                     const float* __restrict__ C, int k, int* __restrict__ assign,
+                                                     double* __restrict__ sums, double* __restrict__ counts,
+                                                     double* __restrict__ cost) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* sc = sm;               // [k][d]
+  float* ss = sm + k * d;       // [k][d]
+  float* scnt = ss + k * d;     // [k]
+  for (int i = threadIdx.x; i < k * d; i += 256) {
+    sc[i] = C[i];
+    ss[i] = 0.f;
+  }
+  for (int i = threadIdx.x; i < k; i += 256) scnt[i] = 0.f;
+  __syncthreads();
+  double mycost = 0.0;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
+    const float* x = X + r * ldx;
+    float best = 3.4e38f;
+    int bi = 0;
+    for (int c = 0; c < k; ++c) {
+      float dist = 0.f;
+      for (int f = 0; f < d; ++f) {
+        const float df = x[f] - sc[c * d + f];
+        dist += df * df;
+      }
+      if (dist < best) {
+        best = dist;
+        bi = c;
+      }
+    }
+    assign[r] = bi;
+    mycost += best;
+    if (sums) {
+      for (int f = 0; f < d; ++f) atomicAdd(&ss[bi * d + f], x[f]);
+      atomicAdd(&scnt[bi], 1.f);
+    }
+  }
+  __syncthreads();
+  if (sums) {
+    for (int i = threadIdx.x; i < k * d; i += 256)
+      if (ss[i] != 0.f) atomicAdd(&sums[i], (double)ss[i]);
+    for (int i = threadIdx.x; i < k; i += 256)
+      if (scnt[i] != 0.f) atomicAdd(&counts[i], (double)scnt[i]);
+  }
+  if (cost) {
+    const double v = cdna::wave_sum(mycost);
+    if ((threadIdx.x & 63) == 0) atomicAdd(cost, v);
+  }
+}
+
+// ------------------------------------------- K11 binary logistic loss/grad
+// margin m = x·w + b ; loss += wt*(log1p(exp(m)) - y m) ; grad += wt*(σ(m)-y)·[x, 1]
+// One wave per row group; lanes span features (coalesced row reads), the dot
+// product is a wave butterfly, gradient accumulates lane-local then is folded
+// once per block (f64 global atomics).  grad has d+1 entries (+ intercept).
+__global__ __launch_bounds__(256) void logistic_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                       const double* __restrict__ y, const double* __restrict__ wt,
+                                                       const double* __restrict__ w, double b,
+                                                       double* __restrict__ grad, double* __restrict__ loss) {
+  extern __shared__ __attribute__((aligned(16))) double gsm[];  // [d+1]
+  for (int i = threadIdx.x; i <= d; i += 256) gsm[i] = 0.0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wid, nw = (int64_t)gridDim.x * 4;
+  constexpr int FPL = 8;  // features per lane handled in registers (d <= 512)
+  double gacc[FPL];
+  float wl[FPL];
+#pragma unroll
+  for (int q = 0; q < FPL; ++q) {
+    gacc[q] = 0.0;
+    const int f = lane + 64 * q;
+    wl[q] = f < d ? (float)w[f] : 0.f;
+  }
+  double gb = 0.0, ls = 0.0;
+  for (int64_t r = gw; r < n; r += nw) {
+    const float* x = X + r * ldx;
+    float xv[FPL];
+    float dot = 0.f;
+#pragma unroll
+    for (int q = 0; q < FPL; ++q) {
+      const int f = lane + 64 * q;
+      xv[q] = f < d ? x[f] : 0.f;
+      dot += xv[q] * wl[q];
+    }
+    const double m = (double)cdna::wave_sum(dot) + b;
+    const double yy = y[r], ww = wt ? wt[r] : 1.0;
+    const double p = 1.0 / (1.0 + exp(-m));
+    const double res = ww * (p - yy);
+#pragma unroll
+    for (int q = 0; q < FPL; ++q) gacc[q] += res * (double)xv[q];
+    if (lane == 0) {
+      gb += res;
+      ls += ww * ((m > 0 ? m + log1p(exp(-m)) : log1p(exp(m))) - yy * m);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < FPL; ++q) {
+    const int f = lane + 64 * q;
+    if (f < d) atomicAdd(&gsm[f], gacc[q]);
+  }
+  if (lane == 0) atomicAdd(&gsm[d], gb);
+  __syncthreads();
+  for (int i = threadIdx.x; i <= d; i += 256) atomicAdd(&grad[i], gsm[i]);
+  if (lane == 0) atomicAdd(loss, ls);
+}
+
+}  // namespace
+
+CDNA_API int cdna_uniform(double* out, int64_t n, uint64_t seed, uint64_t offset, uint32_t stream, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(uniform_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, out, n, seed, offset, stream);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_t offset, double rate,
+                          hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  hipLaunchKernelGGL(poisson_kernel, dim3(grid_for(n, 256, 2048), T), dim3(256), 0, st, out, T, n, seed, offset,
+                     rate);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_reg_metrics(const double* y, const double* p, const double* w, int64_t n, double* acc,
+                              hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(reg_metrics_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, y, p, w, n, acc);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_score_hist(const double* score, const double* label, int64_t n, double lo, double hi, int nb,
+                             double* hist, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(score_hist_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, score, label, n, lo, hi, nb,
+                     hist);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_kmeans_step(const float* X, int64_t n, int d, int64_t ldx, const float* C, int k, int* assign,
+                              double* sums, double* counts, double* cost, hipStream_t st) {
+  if (n <= 0) return 0;
+  if ((size_t)(2 * k * d + k) * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)(2 * k * d + k) * 4;
+  hipLaunchKernelGGL(kmeans_kernel, dim3(grid_for(n, 256, 2048)), dim3(256), lds, st, X, n, d, ldx, C, k, assign,
+                     sums, counts, cost);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_logistic_grad(const float* X, int64_t n, int d, int64_t ldx, const double* y, const double* wt,
+                                const double* w, double b, double* grad, double* loss, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (d > 512) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)(d + 1) * 8;
+  hipLaunchKernelGGL(logistic_kernel, dim3(grid_for(n, 64, 1024)), dim3(256), lds, st, X, n, d, ldx, y, wt, w, b,
+                     grad, loss);
+  return (int)hipGetLastError();
+}

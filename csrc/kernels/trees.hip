@@ -1,0 +1,406 @@
+// Histogram tree learning on CDNA4 (SURVEY §2.10 K4 binize, K5 hist_build,
+// K7 row_partition, K8 tree_predict).  Shared by DecisionTree*, RandomForest*
+// and the XGBoost-style GBDT.
+//
+// Reference behaviour: MLlib's PLANET-style learner — per-partition split
+// statistics for every (node, feature, bin), tree-reduced once per level,
+// best split chosen on the driver (ML 06 - Decision Trees.py:96-118,
+// Labs/ML 07L:19); maxBins bounds the bin count (ML 07:41).
+//
+// Data layout (chosen for the histogram kernel, the hot loop):
+//   bins   : uint8, feature-group-major  [G = ceil(d/8)][n][8]
+//            -> one 8-byte load per (row, group); a wave reads 512 contiguous B
+//   node   : int32 [T][n]   active-node id of the row in tree t (-1 = in a leaf)
+//   weight : uint8 [T][n]   Poisson bootstrap multiplicity (nullptr = 1)
+//   stats  : f32 v0[n], v1[n] (RF regression: 1, y; GBDT: g, h)
+// Histogram accumulation is LDS-privatised per block (ds_add_f32), flushed
+// once per block with f64 global atomics; blocks are mapped XCD-aware so the
+// G feature-group blocks of one row chunk share an XCD's L2 for node/weight
+// re-reads.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// K4 binize: raw f32 [n][d] -> uint8 bins [G][n][8]
+// continuous: bin = #thresholds strictly below x  (x <= thr[b] goes left of split b)
+// categorical (nthr[f] < 0): bin = (int)x
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void binize_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                     const float* __restrict__ thr, const int* __restrict__ nthr,
+                                                     int tmax, int use_lds, uint64_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int G = (d + 7) / 8;
+  const int dp = G * 8;
+  uint8_t* tile = reinterpret_cast<uint8_t*>(smem);                 // [256][dp]
+  float* sthr = reinterpret_cast<float*>(smem + ((256 * dp + 15) / 16) * 16);
+  const float* T = thr;
+  if (use_lds) {
+    for (int i = threadIdx.x; i < d * tmax; i += 256) sthr[i] = thr[i];
+    T = sthr;
+  }
+  __syncthreads();
+  for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < n; r0 += (int64_t)gridDim.x * 256) {
+    const int rows = (int)((n - r0) < 256 ? (n - r0) : 256);
+    for (int e = threadIdx.x; e < rows * dp; e += 256) {
+      const int r = e / dp, f = e - r * dp;
+      uint8_t b = 0;
+      if (f < d) {
+        const float x = X[(r0 + r) * ldx + f];
+        const int nt = nthr[f];
+        if (nt < 0) {
+          int c = (int)x;
+          b = (uint8_t)(c < 0 ? 0 : (c > 255 ? 255 : c));
+        } else {
+          const float* tf = T + (int64_t)f * tmax;
+          int lo = 0, hi = nt;  // first index with tf[idx] >= x
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (tf[mid] < x) lo = mid + 1; else hi = mid;
+          }
+          if (x != x) lo = nt;  // NaN -> last bin
+          b = (uint8_t)lo;
+        }
+      }
+      tile[r * dp + f] = b;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < rows * G; e += 256) {
+      const int g = e / rows, r = e - g * rows;
+      out[(int64_t)g * n + r0 + r] = *reinterpret_cast<const uint64_t*>(&tile[r * dp + g * 8]);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K5 hist_build (moments): hist[slot][f][bin][2] += w * (v0, v1)
+// grid: linear; decoded (after XCD remap) as g fastest, then row chunk, then
+// slot group.  Slot group k covers slots [grp_s0[k], grp_s0[k]+SB) which all
+// live in trees [grp_t0[k], grp_t1[k]].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void hist_moments_kernel(
+    const uint64_t* __restrict__ bins, int64_t n, int d, int T, const int* __restrict__ node,
+    const uint8_t* __restrict__ weight, const float* __restrict__ v0, const float* __restrict__ v1,
+    const int* __restrict__ build_slot, const uint32_t* __restrict__ feat_mask, int mask_words, int S, int B,
+    int SB, const int* __restrict__ grp_s0, const int* __restrict__ grp_t0, const int* __restrict__ grp_t1,
+    int nchunk, int64_t rows_per_chunk, double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float lh[];  // [SB][8][B][2]
+  const int G = (d + 7) / 8;
+  const uint32_t nblk = gridDim.x;
+  const uint32_t w = cdna::xcd_remap(blockIdx.x, nblk);
+  const int g = (int)(w % G);
+  const int chunk = (int)((w / G) % nchunk);
+  const int grp = (int)(w / ((uint32_t)G * nchunk));
+  const int s0 = grp_s0[grp], t0 = grp_t0[grp], t1 = grp_t1[grp];
+  const int hsz = SB * 8 * B * 2;
+  for (int i = threadIdx.x; i < hsz; i += 256) lh[i] = 0.f;
+  __syncthreads();
+  const int64_t rb = (int64_t)chunk * rows_per_chunk;
+  int64_t re = rb + rows_per_chunk;
+  if (re > n) re = n;
+  const int fbase = g * 8;
+  const int mword = fbase >> 5, mshift = fbase & 31;
+  for (int64_t r = rb + threadIdx.x; r < re; r += 256) {
+    const uint64_t b8 = bins[(int64_t)g * n + r];
+    const float a0 = v0 ? v0[r] : 1.f;
+    const float a1 = v1[r];
+    for (int t = t0; t <= t1; ++t) {
+      const int id = node[(int64_t)t * n + r];
+      if (id < 0) continue;
+      const int ls = build_slot[id] - s0;
+      if (ls < 0 || ls >= SB) continue;
+      const float wt = weight ? (float)weight[(int64_t)t * n + r] : 1.f;
+      if (wt == 0.f) continue;
+      uint32_t m = 0xFFu;
+      if (feat_mask) m = (feat_mask[(int64_t)(ls + s0) * mask_words + mword] >> mshift) & 0xFFu;
+      const float x0 = wt * a0, x1 = wt * a1;
+      float* base = lh + (int64_t)ls * 8 * B * 2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if ((m >> j) & 1u) {
+          const int bin = (int)((b8 >> (8 * j)) & 0xFFu);
+          float* p = base + (j * B + bin) * 2;
+          atomicAdd(p, x0);
+          atomicAdd(p + 1, x1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < hsz; i += 256) {
+    const float v = lh[i];
+    if (v == 0.f) continue;
+    const int k = i & 1;
+    const int bin = (i >> 1) % B;
+    const int j = ((i >> 1) / B) & 7;
+    const int ls = (i >> 1) / (B * 8);
+    const int f = fbase + j;
+    const int slot = s0 + ls;
+    if (f < d && slot < S) atomicAdd(&out[(((int64_t)slot * d + f) * B + bin) * 2 + k], (double)v);
+  }
+}
+
+// K5 (classification): hist[slot][f][bin][c] += w for label class c
+__global__ __launch_bounds__(256) void hist_classes_kernel(
+    const uint64_t* __restrict__ bins, int64_t n, int d, int T, const int* __restrict__ node,
+    const uint8_t* __restrict__ weight, const int* __restrict__ label, int C, const int* __restrict__ build_slot,
+    const uint32_t* __restrict__ feat_mask, int mask_words, int S, int B, int SB, const int* __restrict__ grp_s0,
+    const int* __restrict__ grp_t0, const int* __restrict__ grp_t1, int nchunk, int64_t rows_per_chunk,
+    double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float lh[];  // [SB][8][B][C]
+  const int G = (d + 7) / 8;
+  const uint32_t w = cdna::xcd_remap(blockIdx.x, gridDim.x);
+  const int g = (int)(w % G);
+  const int chunk = (int)((w / G) % nchunk);
+  const int grp = (int)(w / ((uint32_t)G * nchunk));
+  const int s0 = grp_s0[grp], t0 = grp_t0[grp], t1 = grp_t1[grp];
+  const int hsz = SB * 8 * B * C;
+  for (int i = threadIdx.x; i < hsz; i += 256) lh[i] = 0.f;
+  __syncthreads();
+  const int64_t rb = (int64_t)chunk * rows_per_chunk;
+  int64_t re = rb + rows_per_chunk;
+  if (re > n) re = n;
+  const int fbase = g * 8;
+  const int mword = fbase >> 5, mshift = fbase & 31;
+  for (int64_t r = rb + threadIdx.x; r < re; r += 256) {
+    const uint64_t b8 = bins[(int64_t)g * n + r];
+    const int c = label[r];
+    if (c < 0 || c >= C) continue;
+    for (int t = t0; t <= t1; ++t) {
+      const int id = node[(int64_t)t * n + r];
+      if (id < 0) continue;
+      const int ls = build_slot[id] - s0;
+      if (ls < 0 || ls >= SB) continue;
+      const float wt = weight ? (float)weight[(int64_t)t * n + r] : 1.f;
+      if (wt == 0.f) continue;
+      uint32_t m = 0xFFu;
+      if (feat_mask) m = (feat_mask[(int64_t)(ls + s0) * mask_words + mword] >> mshift) & 0xFFu;
+      float* base = lh + (int64_t)ls * 8 * B * C;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if ((m >> j) & 1u) {
+          const int bin = (int)((b8 >> (8 * j)) & 0xFFu);
+          atomicAdd(base + (j * B + bin) * C + c, wt);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < hsz; i += 256) {
+    const float v = lh[i];
+    if (v == 0.f) continue;
+    const int c = i % C;
+    const int bin = (i / C) % B;
+    const int j = (i / (C * B)) & 7;
+    const int ls = i / (C * B * 8);
+    const int f = fbase + j;
+    const int slot = s0 + ls;
+    if (f < d && slot < S) atomicAdd(&out[(((int64_t)slot * d + f) * B + bin) * C + c], (double)v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K7 row_partition: move every row of every tree to its child for the level.
+// split_feat[id] : -1 -> node became a leaf (row leaves the active set)
+// split_bin[id]  : continuous: left iff bin <= split_bin
+// cat_off[id]    : >= 0 -> categorical, left iff bit bin of cat_mask[cat_off..+8]
+// child[id*2+{0,1}] : next-level active id or -1
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void partition_kernel(const uint64_t* __restrict__ bins, int64_t n, int T,
+                                                        int* __restrict__ node, const int* __restrict__ split_feat,
+                                                        const int* __restrict__ split_bin,
+                                                        const int* __restrict__ cat_off,
+                                                        const uint32_t* __restrict__ cat_mask,
+                                                        const int* __restrict__ child) {
+  const int t = blockIdx.y;
+  const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bins);
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
+    const int64_t o = (int64_t)t * n + r;
+    const int id = node[o];
+    if (id < 0) continue;
+    const int f = split_feat[id];
+    if (f < 0) {
+      node[o] = -1;
+      continue;
+    }
+    const int bin = b8[((int64_t)(f >> 3) * n + r) * 8 + (f & 7)];
+    const int co = cat_off[id];
+    bool left;
+    if (co >= 0) left = (cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u;
+    else left = bin <= split_bin[id];
+    node[o] = child[id * 2 + (left ? 0 : 1)];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K8 tree_predict on raw features.  Packed node = int4:
+//   continuous : {f, float_bits(thr), left, right}      left iff x <= thr
+//   categorical: {-(f+2), mask_off, left, right}        left iff bit (int)x
+//   leaf       : {-1, value_off, 0, 0}                  values[value_off .. +K]
+// out[r][k] = base[k] + sum_t tree_w[t] * leafval_t(r)[k]
+// Block = 256 threads = 64 rows x 4 tree lanes; the 64-row tile of X is
+// staged in LDS with coalesced loads, per-tree-lane partial sums folded in LDS.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void predict_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                      const int4* __restrict__ nodes, const int* __restrict__ roots,
+                                                      const float* __restrict__ tree_w, int T,
+                                                      const float* __restrict__ values, const uint32_t* __restrict__ masks,
+                                                      int K, const float* __restrict__ base, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float sx[];  // [64][d+1] then [4][64][K]
+  const int dp = d + 1;
+  float* part = sx + 64 * dp;
+  const int tl = threadIdx.x >> 6, row = threadIdx.x & 63;
+  for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < n; r0 += (int64_t)gridDim.x * 64) {
+    const int rows = (int)((n - r0) < 64 ? (n - r0) : 64);
+    for (int e = threadIdx.x; e < rows * d; e += 256) {
+      const int r = e / d, f = e - r * d;
+      sx[r * dp + f] = X[(r0 + r) * ldx + f];
+    }
+    for (int e = threadIdx.x; e < 4 * 64 * K; e += 256) part[e] = 0.f;
+    __syncthreads();
+    if (row < rows) {
+      const float* xr = sx + row * dp;
+      float* pr = part + (tl * 64 + row) * K;
+      for (int t = tl; t < T; t += 4) {
+        int nd = roots[t];
+        int4 nv = nodes[nd];
+        while (nv.x != -1) {
+          bool left;
+          if (nv.x >= 0) {
+            left = xr[nv.x] <= __int_as_float(nv.y);
+          } else {
+            const int c = (int)xr[-nv.x - 2];
+            left = (c >= 0 && c < 256) ? ((masks[nv.y * 8 + (c >> 5)] >> (c & 31)) & 1u) : false;
+          }
+          nd = left ? nv.z : nv.w;
+          nv = nodes[nd];
+        }
+        const float tw = tree_w[t];
+        const float* v = values + nv.y;
+        for (int k = 0; k < K; ++k) pr[k] += tw * v[k];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < rows * K; e += 256) {
+      const int r = e / K, k = e - r * K;
+      float s = base ? base[k] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s += part[(q * 64 + r) * K + k];
+      out[(r0 + r) * K + k] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// Leaf lookup on binned data (for GBDT training-set margin updates):
+// out[r] += scale * value(leaf(r)) for a single tree in the compact
+// level-array form used during training (split on bins).
+__global__ __launch_bounds__(256) void predict_binned_kernel(const uint64_t* __restrict__ bins, int64_t n,
+                                                             const int4* __restrict__ nodes, int root,
+                                                             const float* __restrict__ values,
+                                                             const uint32_t* __restrict__ masks, float scale,
+                                                             float* __restrict__ out) {
+  const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bins);
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
+    int nd = root;
+    int4 nv = nodes[nd];
+    while (nv.x != -1) {
+      bool left;
+      if (nv.x >= 0) {
+        const int bin = b8[((int64_t)(nv.x >> 3) * n + r) * 8 + (nv.x & 7)];
+        left = bin <= nv.y;
+      } else {
+        const int f = -nv.x - 2;
+        const int bin = b8[((int64_t)(f >> 3) * n + r) * 8 + (f & 7)];
+        left = (masks[nv.y * 8 + (bin >> 5)] >> (bin & 31)) & 1u;
+      }
+      nd = left ? nv.z : nv.w;
+      nv = nodes[nd];
+    }
+    out[r] += scale * values[nv.y];
+  }
+}
+
+inline unsigned grid_for(int64_t n, int per, unsigned cap) {
+  int64_t g = (n + per - 1) / per;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+}  // namespace
+
+CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const float* thr, const int* nthr, int tmax,
+                         uint64_t* out, hipStream_t st) {
+  if (n <= 0) return 0;
+  const int G = (d + 7) / 8;
+  const size_t tile = ((size_t)256 * G * 8 + 15) / 16 * 16;
+  const size_t tbytes = (size_t)d * (tmax > 0 ? tmax : 1) * 4;
+  const int use_lds = (tile + tbytes) <= 96 * 1024 ? 1 : 0;
+  const size_t lds = tile + (use_lds ? tbytes : 0);
+  if (tile > 120 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(binize_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
+                     tmax, use_lds, out);
+  return (int)hipGetLastError();
+}
+
+// ngroups slot groups of SB slots (host-planned); out must be zeroed.
+CDNA_API int cdna_hist_moments(const uint64_t* bins, int64_t n, int d, int T, const int* node, const uint8_t* weight,
+                               const float* v0, const float* v1, const int* build_slot, const uint32_t* feat_mask,
+                               int mask_words, int S, int B, int SB, int ngroups, const int* grp_s0,
+                               const int* grp_t0, const int* grp_t1, int nchunk, double* out, hipStream_t st) {
+  if (n <= 0 || S <= 0) return 0;
+  const int G = (d + 7) / 8;
+  const int64_t rpc = (n + nchunk - 1) / nchunk;
+  const size_t lds = (size_t)SB * 8 * B * 2 * 4;
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  const unsigned nblk = (unsigned)G * nchunk * ngroups;
+  hipLaunchKernelGGL(hist_moments_kernel, dim3(nblk), dim3(256), lds, st, bins, n, d, T, node, weight, v0, v1,
+                     build_slot, feat_mask, mask_words, S, B, SB, grp_s0, grp_t0, grp_t1, nchunk, rpc, out);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_hist_classes(const uint64_t* bins, int64_t n, int d, int T, const int* node, const uint8_t* weight,
+                               const int* label, int C, const int* build_slot, const uint32_t* feat_mask,
+                               int mask_words, int S, int B, int SB, int ngroups, const int* grp_s0,
+                               const int* grp_t0, const int* grp_t1, int nchunk, double* out, hipStream_t st) {
+  if (n <= 0 || S <= 0) return 0;
+  const int G = (d + 7) / 8;
+  const int64_t rpc = (n + nchunk - 1) / nchunk;
+  const size_t lds = (size_t)SB * 8 * B * C * 4;
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  const unsigned nblk = (unsigned)G * nchunk * ngroups;
+  hipLaunchKernelGGL(hist_classes_kernel, dim3(nblk), dim3(256), lds, st, bins, n, d, T, node, weight, label, C,
+                     build_slot, feat_mask, mask_words, S, B, SB, grp_s0, grp_t0, grp_t1, nchunk, rpc, out);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_partition(const uint64_t* bins, int64_t n, int T, int* node, const int* split_feat,
+                            const int* split_bin, const int* cat_off, const uint32_t* cat_mask, const int* child,
+                            hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  hipLaunchKernelGGL(partition_kernel, dim3(grid_for(n, 256, 2048), T), dim3(256), 0, st, bins, n, T, node,
+                     split_feat, split_bin, cat_off, cat_mask, child);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_tree_predict(const float* X, int64_t n, int d, int64_t ldx, const int4* nodes, const int* roots,
+                               const float* tree_w, int T, const float* values, const uint32_t* masks, int K,
+                               const float* base, float* out, hipStream_t st) {
+  if (n <= 0) return 0;
+  const size_t lds = ((size_t)64 * (d + 1) + (size_t)4 * 64 * K) * 4;
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(predict_kernel, dim3(grid_for(n, 64, 8192)), dim3(256), lds, st, X, n, d, ldx, nodes, roots,
+                     tree_w, T, values, masks, K, base, out);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_predict_binned_add(const uint64_t* bins, int64_t n, const int4* nodes, int root,
+                                     const float* values, const uint32_t* masks, float scale, float* out,
+                                     hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(predict_binned_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, bins, n, nodes, root,
+                     values, masks, scale, out);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,235 @@
+"""Numerics of every native HIP kernel vs its plain-PyTorch CPU reference."""
+import numpy as np
+import pytest
+import torch
+
+from cdnaml.ops import _lib, kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _lib.lib()  # must load: no silent fallback on a GPU box
+    return torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("n,d", [(1000, 5), (4097, 30), (20000, 100), (333, 200)])
+def test_gram_f32(dev, n, d):
+    g = torch.Generator().manual_seed(n + d)
+    X = torch.randn(n, d, generator=g) * 3 + 1
+    y = torch.randn(n, generator=g)
+    sh = X[:64].mean(0)
+    ref = K.gram(X, y, sh, 0.25)
+    out = K.gram(X.to(dev), y.to(dev), sh.to(dev), 0.25).cpu()
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-3 * n ** 0.5)
+
+
+def test_gram_asymmetric_identity(dev):
+    # A = I-check with asymmetric data: catches row/col swaps in the C layout
+    n, d = 64, 40
+    X = torch.arange(n * d, dtype=torch.float32).reshape(n, d) % 7 - (torch.arange(d) % 5)[None, :]
+    ref = K.gram(X)
+    out = K.gram(X.to(dev)).cpu()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("n,d", [(5000, 100), (100, 7)])
+def test_gram_bf16(dev, n, d):
+    g = torch.Generator().manual_seed(7)
+    X = torch.randn(n, d, generator=g)
+    y = torch.randn(n, generator=g)
+    ref = K.gram(X, y, None, 0.0, bf16=True)
+    out = K.gram(X.to(dev), y.to(dev), None, 0.0, bf16=True).cpu()
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-2)
+
+
+def test_uniform_bit_identical(dev):
+    a = K.uniform(100000, 42, 12345, 3)
+    b = K.uniform(100000, 42, 12345, 3, device=dev).cpu()
+    assert torch.equal(a, b)
+
+
+def test_poisson_matches(dev):
+    a = K.poisson_weights(4, 50000, 7, 1000, 1.0)
+    b = K.poisson_weights(4, 50000, 7, 1000, 1.0, device=dev).cpu()
+    assert (a != b).sum().item() <= 2  # libm exp() may differ in the last ulp
+
+
+def _thresholds(X, maxb):
+    d = X.shape[1]
+    thr = torch.zeros(d, maxb - 1)
+    nthr = torch.zeros(d, dtype=torch.int32)
+    for f in range(d):
+        q = torch.quantile(X[:2000, f], torch.linspace(0, 1, maxb + 1)[1:-1]).unique()
+        thr[f, : len(q)] = q
+        nthr[f] = len(q)
+    return thr, nthr
+
+
+def test_binize(dev):
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(3000, 21, generator=g)
+    X[:, 3] = torch.randint(0, 9, (3000,), generator=g).float()
+    thr, nthr = _thresholds(X, 40)
+    nthr[3] = -1
+    X[5, 2] = float("nan")
+    ref = K.binize(X, thr, nthr)
+    out = K.binize(X.to(dev), thr.to(dev), nthr.to(dev)).cpu()
+    assert torch.equal(out, ref)
+
+
+def _tree_state(n, T, A, seed):
+    g = torch.Generator().manual_seed(seed)
+    node = torch.randint(-1, A, (T, n), generator=g, dtype=torch.int32)
+    build = torch.randint(-1, 3, (A,), generator=g, dtype=torch.int32)
+    # slots must be tree-major: remap per tree (ids are tree-major: A/T ids per tree)
+    per = A // T
+    slot_tree = []
+    s = 0
+    for i in range(A):
+        if build[i] >= 0:
+            build[i] = s
+            slot_tree.append(i // per)
+            s += 1
+    for t in range(T):
+        lo, hi = t * per, (t + 1) * per
+        m = node[t] >= 0
+        node[t][m] = lo + (node[t][m] % per)
+    return node, build, np.array(slot_tree, np.int32)
+
+
+@pytest.mark.parametrize("B", [40, 256])
+def test_hist_moments(dev, B):
+    n, d, T, A = 20000, 19, 3, 12
+    g = torch.Generator().manual_seed(B)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    bins = K.binize(X, thr, nthr)
+    node, build, slot_tree = _tree_state(n, T, A, 3)
+    S = len(slot_tree)
+    w = K.poisson_weights(T, n, 5, 0, 1.0)
+    y = torch.randn(n, generator=g)
+    mw = (d + 31) // 32
+    fm = torch.randint(0, 2 ** 31 - 1, (S, mw), generator=g, dtype=torch.int64).to(torch.int32)
+    ref = K.hist_moments(bins, d, node, w, None, y, build, slot_tree, fm, B)
+    out = K.hist_moments(bins.to(dev), d, node.to(dev), w.to(dev), None, y.to(dev), build.to(dev), slot_tree,
+                         fm.to(dev), B, lds_budget=8 * 1024).cpu()
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-4)
+
+
+def test_hist_classes(dev):
+    n, d, T, A, C, B = 10000, 10, 2, 8, 3, 32
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    bins = K.binize(X, thr, nthr)
+    node, build, slot_tree = _tree_state(n, T, A, 4)
+    w = K.poisson_weights(T, n, 5, 0, 1.0)
+    lab = torch.randint(0, C, (n,), generator=g, dtype=torch.int32)
+    ref = K.hist_classes(bins, d, node, w, lab, C, build, slot_tree, None, B)
+    out = K.hist_classes(bins.to(dev), d, node.to(dev), w.to(dev), lab.to(dev), C, build.to(dev), slot_tree, None,
+                         B).cpu()
+    assert torch.allclose(out, ref)
+
+
+def test_partition(dev):
+    n, d, T, A = 5000, 12, 2, 6
+    g = torch.Generator().manual_seed(2)
+    X = torch.randn(n, d, generator=g)
+    X[:, 4] = torch.randint(0, 20, (n,), generator=g).float()
+    thr, nthr = _thresholds(X, 32)
+    nthr[4] = -1
+    bins = K.binize(X, thr, nthr)
+    node, _, _ = _tree_state(n, T, A, 9)
+    sf = torch.tensor([0, 4, -1, 7, 4, 11], dtype=torch.int32)
+    sb = torch.tensor([10, 0, 0, 3, 0, 20], dtype=torch.int32)
+    co = torch.tensor([-1, 0, -1, -1, 1, -1], dtype=torch.int32)
+    cm = torch.randint(0, 2 ** 31 - 1, (16,), generator=g, dtype=torch.int64).to(torch.int32)
+    child = torch.arange(12, dtype=torch.int32) - 2
+    a = node.clone()
+    K.partition(bins, a, sf, sb, co, cm, child)
+    b = node.to(dev)
+    K.partition(bins.to(dev), b, sf.to(dev), sb.to(dev), co.to(dev), cm.to(dev), child.to(dev))
+    assert torch.equal(a, b.cpu())
+
+
+def _random_forest_arrays(T, depth, d, K_, seed):
+    g = torch.Generator().manual_seed(seed)
+    nodes, values, roots = [], [], []
+    masks = torch.randint(0, 2 ** 31 - 1, (4 * 8,), generator=g, dtype=torch.int64).to(torch.int32)
+    for t in range(T):
+        roots.append(len(nodes))
+        base = len(nodes)
+        nint = 2 ** depth - 1
+        for i in range(nint):
+            l, r = base + 2 * i + 1, base + 2 * i + 2
+            if i % 5 == 4:
+                nodes.append([-(int(torch.randint(0, d, (1,), generator=g)) + 2), i % 4, l, r])
+            else:
+                thr = float(torch.randn(1, generator=g))
+                nodes.append([int(torch.randint(0, d, (1,), generator=g)),
+                              int(torch.tensor([thr], dtype=torch.float32).view(torch.int32)), l, r])
+        for i in range(2 ** depth):
+            nodes.append([-1, len(values), 0, 0])
+            values.extend(torch.randn(K_, generator=g).tolist())
+    return (torch.tensor(nodes, dtype=torch.int32), torch.tensor(roots, dtype=torch.int32),
+            torch.tensor(values, dtype=torch.float32), masks)
+
+
+@pytest.mark.parametrize("K_", [1, 3])
+def test_tree_predict(dev, K_):
+    n, d, T = 3000, 17, 7
+    g = torch.Generator().manual_seed(K_)
+    X = torch.randn(n, d, generator=g)
+    X[:, 3] = torch.randint(0, 40, (n,), generator=g).float()
+    nodes, roots, values, masks = _random_forest_arrays(T, 4, d, K_, 5)
+    # categorical nodes use feature 3 only
+    cat = nodes[:, 0] < -1
+    nodes[cat, 0] = -(3 + 2)
+    tw = torch.rand(T, generator=g)
+    base = torch.randn(K_, generator=g)
+    ref = K.tree_predict(X, nodes, roots, tw, values, masks, K_, base)
+    out = K.tree_predict(X.to(dev), nodes.to(dev), roots.to(dev), tw.to(dev), values.to(dev), masks.to(dev), K_,
+                         base.to(dev)).cpu()
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_reg_metrics(dev):
+    g = torch.Generator().manual_seed(3)
+    y = torch.randn(100001, generator=g, dtype=torch.float64)
+    p = y + 0.1 * torch.randn(100001, generator=g, dtype=torch.float64)
+    ref = K.reg_metrics(y, p)
+    out = K.reg_metrics(y.to(dev), p.to(dev)).cpu()
+    assert torch.allclose(out, ref, rtol=1e-10)
+
+
+def test_kmeans_step(dev):
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(10000, 4, generator=g)
+    C = torch.randn(5, 4, generator=g)
+    a1, s1, c1, cost1 = K.kmeans_step(X, C)
+    a2, s2, c2, cost2 = K.kmeans_step(X.to(dev), C.to(dev))
+    assert torch.equal(a1, a2.cpu())
+    assert torch.allclose(s1, s2.cpu(), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(c1, c2.cpu())
+
+
+def test_logistic_grad(dev):
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(20000, 37, generator=g)
+    y = (torch.rand(20000, generator=g) > 0.5).double()
+    w = torch.randn(37, generator=g, dtype=torch.float64) * 0.1
+    g1, l1 = K.logistic_grad(X, y, w, 0.3)
+    g2, l2 = K.logistic_grad(X.to(dev), y.to(dev), w.to(dev), 0.3)
+    assert torch.allclose(g1, g2.cpu(), rtol=1e-4, atol=1e-3)
+    assert abs(float(l1) - float(l2)) < 1e-3 * abs(float(l1))
+
+
+def test_score_hist(dev):
+    g = torch.Generator().manual_seed(3)
+    s = torch.rand(50000, generator=g, dtype=torch.float64)
+    lab = (torch.rand(50000, generator=g) > 0.3).double()
+    assert torch.equal(K.score_hist(s, lab, 0.0, 1.0, 1000), K.score_hist(s.to(dev), lab.to(dev), 0.0, 1.0, 1000).cpu())
