@@ -1,0 +1,607 @@
+"""Level-wise distributed histogram tree learner (SURVEY §2.5.3 A3–A6, §2.9 P2/P9).
+
+One engine for DecisionTree*, RandomForest*, GBT* and the XGBoost-style
+GBDT.  Per tree level, for all trees of a forest at once:
+
+  1. ``hist_moments`` / ``hist_classes`` (HIP, LDS-privatised) build the
+     per-(node, feature, bin) statistics of this rank's rows;
+  2. ONE fused RCCL all-reduce of the level's histogram over xGMI
+     (PLANET's treeAggregate, ML 06 - Decision Trees.py:108-110);
+  3. the best split of every active node is found on device (prefix sums
+     over bins, impurity gain, categorical centroid ordering);
+  4. ``partition`` (HIP) moves every row of every tree to its child.
+
+Because the all-reduced histograms are bit-identical on every rank, every
+rank makes identical decisions and ends with the same model; no broadcast is
+needed.  Bins come from a global quantile sample (all-gathered), so they do
+not depend on the GPU count.  Bootstrap weights are Philox-Poisson keyed by
+the GLOBAL row id: a forest trained on 1 or 8 GPUs is the same forest.
+
+Two histogram strategies:
+  * masked  — per-node feature subsets (RF): only the node's sampled
+              features are accumulated, no sibling subtraction;
+  * subtract — all features (DT/GBDT): only the smaller child of each
+              split is built, its sibling is parent − child.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ...ops import kernels as K
+from ..util import IllegalArgumentException
+
+
+@dataclass
+class TreeParams:
+    max_depth: int = 5
+    max_bins: int = 32
+    min_instances: float = 1.0
+    min_info_gain: float = 0.0
+    impurity: str = "variance"          # variance | gini | entropy | xgb
+    num_classes: int = 0
+    feature_subset: Optional[int] = None  # features per node (None = all)
+    bootstrap: bool = False
+    subsampling_rate: float = 1.0
+    seed: int = 0
+    reg_lambda: float = 1.0
+    gamma: float = 0.0
+    min_child_weight: float = 1.0
+    min_weight_fraction: float = 0.0
+
+
+# ============================================================ binning (K3/K4)
+@dataclass
+class BinnedData:
+    X: torch.Tensor
+    bins: torch.Tensor
+    thresholds: np.ndarray            # [d, B-1] float64 raw thresholds
+    nthr: np.ndarray                  # [d] int (-1 categorical)
+    categorical: Dict[int, int]
+    n_local: int
+    n_global: int
+    row_offset: int
+    d: int
+    B: int
+
+
+def find_thresholds(sample: np.ndarray, d: int, max_bins: int, categorical: Dict[int, int]):
+    """Per-feature split thresholds from a (global) sample (Spark findSplits semantics)."""
+    thr = np.zeros((d, max(max_bins - 1, 1)), dtype=np.float64)
+    nthr = np.zeros(d, dtype=np.int32)
+    for f in range(d):
+        if f in categorical:
+            nthr[f] = -1
+            continue
+        col = sample[:, f]
+        col = col[~np.isnan(col)]
+        if col.size == 0:
+            continue
+        vals, counts = np.unique(col, return_counts=True)
+        if len(vals) <= 1:
+            continue
+        if len(vals) <= max_bins:
+            cand = (vals[:-1] + vals[1:]) / 2.0
+        else:
+            cum = np.cumsum(counts)
+            total = cum[-1]
+            targets = total * np.arange(1, max_bins) / max_bins
+            idx = np.searchsorted(cum, targets, side="left")
+            idx = np.unique(np.clip(idx, 0, len(vals) - 2))
+            cand = (vals[idx] + vals[idx + 1]) / 2.0
+        cand = np.unique(cand)[: max_bins - 1]
+        thr[f, : len(cand)] = cand
+        nthr[f] = len(cand)
+    return thr, nthr
+
+
+def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins: int, seed: int,
+                row_offset: int, n_global: int) -> BinnedData:
+    d = X.shape[1]
+    for f, k in categorical.items():
+        if k > max_bins:
+            raise IllegalArgumentException(
+                f"requirement failed: DecisionTree requires maxBins (= {max_bins}) to be at least as large as the "
+                f"number of values in each categorical feature, but categorical feature {f} has {k} values. "
+                f"Consider removing this and other categorical features with a large number of values, or add "
+                f"more training examples.")
+    if max_bins > 256:
+        raise IllegalArgumentException("maxBins must be <= 256 on this engine (uint8 bins)")
+    comm = session.comm
+    n = X.shape[0]
+    target = max(max_bins * max_bins, 10000)
+    frac = min(1.0, target / max(n_global, 1))
+    if frac < 1.0:
+        u = K.uniform(n, seed ^ 0x5BD1E995, row_offset, 3, device=X.device)
+        samp = X[u < frac]
+    else:
+        samp = X
+    if comm.distributed:
+        samp = torch.cat(comm.all_gather_varlen(samp.contiguous()))
+    sample = samp.double().cpu().numpy()
+    thr, nthr = find_thresholds(sample, d, max_bins, categorical)
+    thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
+    nthr_t = torch.from_numpy(nthr).to(X.device)
+    bins = K.binize(X, thr_t, nthr_t)
+    return BinnedData(X, bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins)
+
+
+# ============================================================ forest storage
+class Forest:
+    """Struct-of-arrays node store for an ensemble (host), + cached device arrays."""
+
+    def __init__(self, K_: int):
+        self.K = K_
+        self.feat: List[int] = []
+        self.thr: List[float] = []
+        self.bin: List[int] = []
+        self.left: List[int] = []
+        self.right: List[int] = []
+        self.catmask: List[np.ndarray] = []
+        self.is_cat: List[bool] = []
+        self.value: List[np.ndarray] = []
+        self.weight: List[float] = []
+        self.gain: List[float] = []
+        self.impurity: List[float] = []
+        self.depth: List[int] = []
+        self.roots: List[int] = []
+        self._dev = {}
+
+    def add(self, value, weight, depth, impurity=float("nan")) -> int:
+        i = len(self.feat)
+        self.feat.append(-1)
+        self.thr.append(0.0)
+        self.bin.append(0)
+        self.left.append(-1)
+        self.right.append(-1)
+        self.catmask.append(np.zeros(8, dtype=np.uint32))
+        self.is_cat.append(False)
+        self.value.append(np.asarray(value, dtype=np.float64).reshape(-1))
+        self.weight.append(float(weight))
+        self.gain.append(0.0)
+        self.impurity.append(float(impurity))
+        self.depth.append(depth)
+        return i
+
+    @property
+    def num_nodes(self):
+        return len(self.feat)
+
+    def tree_nodes(self, t: int) -> List[int]:
+        out, stack = [], [self.roots[t]]
+        while stack:
+            i = stack.pop()
+            out.append(i)
+            if self.feat[i] >= 0:
+                stack.extend([self.right[i], self.left[i]])
+        return out
+
+    def tree_depth(self, t: int) -> int:
+        return max(self.depth[i] for i in self.tree_nodes(t)) - self.depth[self.roots[t]]
+
+    # ----------------------------------------------------------- device
+    def device_arrays(self, device, values_kind: str = "value"):
+        key = (str(device), values_kind)
+        if key in self._dev:
+            return self._dev[key]
+        N = self.num_nodes
+        nodes = np.zeros((N, 4), dtype=np.int32)
+        vals = []
+        masks = []
+        for i in range(N):
+            if self.feat[i] < 0:
+                off = len(vals)
+                v = self.value[i] if values_kind == "value" else self.value[i] * self.weight[i]
+                vals.extend(v.tolist())
+                nodes[i] = (-1, off, 0, 0)
+            elif self.is_cat[i]:
+                nodes[i] = (-(self.feat[i] + 2), len(masks), self.left[i], self.right[i])
+                masks.append(self.catmask[i].view(np.int32))
+            else:
+                nodes[i] = (self.feat[i], np.array([self.thr[i]], dtype=np.float32).view(np.int32)[0],
+                            self.left[i], self.right[i])
+        out = (torch.from_numpy(nodes).to(device),
+               torch.tensor(self.roots, dtype=torch.int32, device=device),
+               torch.tensor(vals if vals else [0.0], dtype=torch.float32, device=device),
+               torch.from_numpy(np.concatenate(masks) if masks else np.zeros(8, np.int32)).to(device))
+        self._dev[key] = out
+        return out
+
+    def binned_arrays(self, device, tree: int):
+        """Single tree with bin thresholds (GBDT training-set margin update)."""
+        key = ("bin", str(device), tree)
+        if key in self._dev:
+            return self._dev[key]
+        idx = self.tree_nodes(tree)
+        pos = {g: j for j, g in enumerate(idx)}
+        nodes = np.zeros((len(idx), 4), dtype=np.int32)
+        vals, masks = [], []
+        for j, g in enumerate(idx):
+            if self.feat[g] < 0:
+                nodes[j] = (-1, len(vals), 0, 0)
+                vals.append(float(self.value[g][0]))
+            elif self.is_cat[g]:
+                nodes[j] = (-(self.feat[g] + 2), len(masks), pos[self.left[g]], pos[self.right[g]])
+                masks.append(self.catmask[g].view(np.int32))
+            else:
+                nodes[j] = (self.feat[g], self.bin[g], pos[self.left[g]], pos[self.right[g]])
+        out = (torch.from_numpy(nodes).to(device), torch.tensor(vals, dtype=torch.float32, device=device),
+               torch.from_numpy(np.concatenate(masks) if masks else np.zeros(8, np.int32)).to(device))
+        self._dev[key] = out
+        return out
+
+    def predict(self, X: torch.Tensor, tree_w: np.ndarray, base=None, values_kind="value") -> torch.Tensor:
+        nodes, roots, vals, masks = self.device_arrays(X.device, values_kind)
+        tw = torch.tensor(np.asarray(tree_w, np.float32), device=X.device)
+        b = None if base is None else torch.tensor(np.asarray(base, np.float32).reshape(-1), device=X.device)
+        return K.tree_predict(X, nodes, roots, tw, vals, masks, self.K, b)
+
+    def predict_leaf_index(self, X: torch.Tensor) -> torch.Tensor:
+        """Host reference traversal returning leaf ids [n, T] (small inputs only)."""
+        Xn = X.double().cpu().numpy()
+        out = np.zeros((Xn.shape[0], len(self.roots)), dtype=np.int64)
+        for t, r in enumerate(self.roots):
+            for i in range(Xn.shape[0]):
+                j = r
+                while self.feat[j] >= 0:
+                    x = Xn[i, self.feat[j]]
+                    if self.is_cat[j]:
+                        c = int(x)
+                        go_left = 0 <= c < 256 and (int(self.catmask[j][c >> 5]) >> (c & 31)) & 1
+                    else:
+                        go_left = x <= self.thr[j]
+                    j = self.left[j] if go_left else self.right[j]
+                out[i, t] = j
+        return torch.from_numpy(out)
+
+    # ----------------------------------------------------------- persistence
+    def state(self, prefix="forest_"):
+        catm = np.stack(self.catmask) if self.catmask else np.zeros((0, 8), np.uint32)
+        vals = np.stack(self.value) if self.value else np.zeros((0, self.K))
+        return {
+            prefix + "feat": torch.tensor(self.feat, dtype=torch.int32),
+            prefix + "thr": torch.tensor(self.thr, dtype=torch.float64),
+            prefix + "bin": torch.tensor(self.bin, dtype=torch.int32),
+            prefix + "left": torch.tensor(self.left, dtype=torch.int32),
+            prefix + "right": torch.tensor(self.right, dtype=torch.int32),
+            prefix + "catmask": torch.from_numpy(catm.view(np.int32).copy()),
+            prefix + "is_cat": torch.tensor(self.is_cat, dtype=torch.bool),
+            prefix + "value": torch.from_numpy(vals),
+            prefix + "weight": torch.tensor(self.weight, dtype=torch.float64),
+            prefix + "gain": torch.tensor(self.gain, dtype=torch.float64),
+            prefix + "impurity": torch.tensor(self.impurity, dtype=torch.float64),
+            prefix + "depth": torch.tensor(self.depth, dtype=torch.int32),
+            prefix + "roots": torch.tensor(self.roots, dtype=torch.int32),
+        }
+
+    @classmethod
+    def from_state(cls, st, prefix="forest_"):
+        vals = st[prefix + "value"].numpy()
+        f = cls(vals.shape[1] if vals.ndim == 2 else 1)
+        f.feat = st[prefix + "feat"].tolist()
+        f.thr = st[prefix + "thr"].tolist()
+        f.bin = st[prefix + "bin"].tolist()
+        f.left = st[prefix + "left"].tolist()
+        f.right = st[prefix + "right"].tolist()
+        f.catmask = [r.view(np.uint32).copy() for r in st[prefix + "catmask"].numpy()]
+        f.is_cat = st[prefix + "is_cat"].tolist()
+        f.value = [v for v in vals]
+        f.weight = st[prefix + "weight"].tolist()
+        f.gain = st[prefix + "gain"].tolist()
+        f.impurity = st[prefix + "impurity"].tolist()
+        f.depth = st[prefix + "depth"].tolist()
+        f.roots = st[prefix + "roots"].tolist()
+        return f
+
+    def feature_importances(self, d: int, trees: Optional[List[int]] = None) -> np.ndarray:
+        """Spark semantics: per-tree gain×count, normalised per tree, averaged, normalised."""
+        total = np.zeros(d)
+        trees = range(len(self.roots)) if trees is None else trees
+        for t in trees:
+            imp = np.zeros(d)
+            for i in self.tree_nodes(t):
+                if self.feat[i] >= 0:
+                    imp[self.feat[i]] += self.gain[i] * self.weight[i]
+            s = imp.sum()
+            if s > 0:
+                imp /= s
+            total += imp
+        s = total.sum()
+        return total / s if s > 0 else total
+
+
+# ============================================================ trainer
+def _impurity_from_counts(c: torch.Tensor, kind: str) -> torch.Tensor:
+    W = c.sum(-1)
+    p = c / W.clamp_min(1e-300).unsqueeze(-1)
+    if kind == "gini":
+        return 1.0 - (p * p).sum(-1)
+    lp = torch.where(p > 0, torch.log2(p.clamp_min(1e-300)), torch.zeros_like(p))
+    return -(p * lp).sum(-1)
+
+
+class ForestTrainer:
+    """Trains T trees level-synchronously over one BinnedData shard per rank."""
+
+    def __init__(self, session, data: BinnedData, params: TreeParams):
+        self.session = session
+        self.data = data
+        self.p = params
+        self.comm = session.comm
+        self.device = data.bins.device
+        self.classification = params.impurity in ("gini", "entropy")
+        self.C = params.num_classes if self.classification else 0
+        self.stats_k = self.C if self.classification else 2
+
+    # ------------------------------------------------------------ helpers
+    def _feature_mask(self, t: int, node_key: int) -> Optional[np.ndarray]:
+        k = self.p.feature_subset
+        d = self.data.d
+        if k is None or k >= d:
+            return None
+        rng = np.random.default_rng([self.p.seed & 0xFFFFFFFF, t, node_key])
+        feats = rng.choice(d, size=k, replace=False)
+        words = np.zeros((d + 31) // 32, dtype=np.uint32)
+        for f in feats:
+            words[f >> 5] |= np.uint32(1) << np.uint32(f & 31)
+        return words
+
+    def _node_stats(self, H: torch.Tensor, fmask_any: torch.Tensor) -> torch.Tensor:
+        """Node totals [A, k] from per-feature bin sums (masked features are zero)."""
+        per_f = H.sum(2)  # [A, d, k]
+        w = per_f[..., 0] if not self.classification else per_f.sum(-1)
+        best_f = torch.argmax(w, dim=1)
+        return per_f[torch.arange(H.shape[0], device=H.device), best_f]
+
+    def _leaf_value(self, st: np.ndarray) -> np.ndarray:
+        if self.classification:
+            W = st.sum()
+            return st / W if W > 0 else np.full(self.C, 1.0 / max(self.C, 1))
+        if self.p.impurity == "xgb":
+            H, G = st[0], st[1]
+            return np.array([-G / (H + self.p.reg_lambda)])
+        W, S = st[0], st[1]
+        return np.array([S / W if W > 0 else 0.0])
+
+    def _weight(self, st: np.ndarray) -> float:
+        return float(st.sum()) if self.classification else float(st[0])
+
+    def _impurity(self, st: np.ndarray) -> float:
+        if self.classification:
+            t = torch.from_numpy(st)[None]
+            return float(_impurity_from_counts(t, self.p.impurity)[0])
+        return float("nan")
+
+    # ------------------------------------------------------------ split scan
+    def _best_splits(self, H: torch.Tensor, tot: torch.Tensor, masks: torch.Tensor):
+        """H [A, d, B, k] (f64) -> per node (gain, feat, bin, left stats, right stats, cat order)."""
+        A, d, B, k = H.shape
+        p = self.p
+        nthr = torch.from_numpy(self.data.nthr).to(H.device)
+        cat_feats = sorted(self.data.categorical)
+        Hs = H
+        order = None
+        if cat_feats:
+            cf = torch.tensor(cat_feats, device=H.device)
+            Hc = H[:, cf]  # [A, nc, B, k]
+            if self.classification:
+                W = Hc.sum(-1)
+                if self.C == 2:
+                    cent = Hc[..., 1] / W.clamp_min(1e-300)
+                else:
+                    cent = _impurity_from_counts(Hc, p.impurity)
+            elif p.impurity == "xgb":
+                W = Hc[..., 0]
+                cent = Hc[..., 1] / (W + p.reg_lambda)
+            else:
+                W = Hc[..., 0]
+                cent = Hc[..., 1] / W.clamp_min(1e-300)
+            cent = torch.where(W > 0, cent, torch.full_like(cent, float("inf")))
+            order = torch.argsort(cent, dim=-1, stable=True)  # [A, nc, B]
+            Hs = H.clone()
+            Hs[:, cf] = torch.gather(Hc, 2, order.unsqueeze(-1).expand(-1, -1, -1, k))
+        cum = Hs.cumsum(2)
+        left = cum
+        right = tot[:, None, None, :] - cum
+        if self.classification:
+            WL, WR = left.sum(-1), right.sum(-1)
+            Wt = tot.sum(-1)[:, None, None]
+            imp_p = _impurity_from_counts(tot, p.impurity)[:, None, None]
+            gain = imp_p - WL / Wt * _impurity_from_counts(left, p.impurity) - \
+                WR / Wt * _impurity_from_counts(right, p.impurity)
+            valid = (WL >= max(p.min_instances, 1e-12)) & (WR >= max(p.min_instances, 1e-12))
+        elif p.impurity == "xgb":
+            HL, GL = left[..., 0], left[..., 1]
+            HR, GR = right[..., 0], right[..., 1]
+            Ht, Gt = tot[:, 0][:, None, None], tot[:, 1][:, None, None]
+            lam = p.reg_lambda
+            gain = 0.5 * (GL * GL / (HL + lam) + GR * GR / (HR + lam) - Gt * Gt / (Ht + lam)) - p.gamma
+            valid = (HL >= p.min_child_weight) & (HR >= p.min_child_weight) & (HL > 0) & (HR > 0)
+        else:
+            WL, SL = left[..., 0], left[..., 1]
+            WR, SR = right[..., 0], right[..., 1]
+            Wt, St = tot[:, 0][:, None, None], tot[:, 1][:, None, None]
+            gain = (SL * SL / WL.clamp_min(1e-300) + SR * SR / WR.clamp_min(1e-300) - St * St /
+                    Wt.clamp_min(1e-300)) / Wt.clamp_min(1e-300)
+            valid = (WL >= max(p.min_instances, 1e-12)) & (WR >= max(p.min_instances, 1e-12))
+        # legal split positions per feature
+        bpos = torch.arange(B, device=H.device)[None, :]
+        limit = torch.where(nthr >= 0, nthr, torch.full_like(nthr, 0))[:, None]  # continuous: b < nthr
+        legal = bpos < limit  # [d, B]
+        if cat_feats:
+            nonempty = (Hc.sum(-1) if self.classification else Hc[..., 0]) > 0  # [A, nc, B]
+            ncnt = nonempty.sum(-1)  # [A, nc]
+            legal_c = bpos[None, None, :] < (ncnt - 1).unsqueeze(-1)  # [A, nc, B]
+            legal_full = legal[None].expand(A, -1, -1).clone()
+            legal_full[:, cf] = legal_c
+            legal = legal_full
+        else:
+            legal = legal[None].expand(A, -1, -1)
+        valid = valid & legal
+        if masks is not None:
+            fm = ((masks[:, (torch.arange(d, device=H.device) >> 5)] >>
+                   (torch.arange(d, device=H.device) & 31).to(masks.dtype)) & 1).bool()  # [A, d]
+            valid = valid & fm[:, :, None]
+        gain = torch.where(valid & torch.isfinite(gain), gain, torch.full_like(gain, float("-inf")))
+        flat = gain.reshape(A, -1)
+        best = torch.argmax(flat, dim=1)
+        bgain = flat[torch.arange(A, device=H.device), best]
+        bf = best // B
+        bb = best % B
+        ar = torch.arange(A, device=H.device)
+        lstats = left[ar, bf, bb]
+        rstats = right[ar, bf, bb]
+        return bgain, bf, bb, lstats, rstats, order, cat_feats
+
+    # ------------------------------------------------------------ training
+    def train(self, num_trees: int, stats_rows: Dict[str, torch.Tensor], weights: Optional[torch.Tensor],
+              forest: Optional[Forest] = None) -> Forest:
+        """Grow ``num_trees`` trees. stats_rows: {'v0','v1'} (moments) or {'label'} (classes)."""
+        p = self.p
+        data = self.data
+        dev = self.device
+        n, d, B = data.n_local, data.d, data.B
+        T = num_trees
+        forest = forest or Forest(self.C if self.classification else 1)
+        masked = p.feature_subset is not None and p.feature_subset < d
+        subtract = not masked
+        node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
+            torch.zeros((T, 0), dtype=torch.int32, device=dev)
+        # active entries: dict(tree, fid (forest node idx), key, mask, parent_hist_idx, build, stats)
+        active = [{"tree": t, "fid": None, "key": 1, "depth": 0, "stats": None, "sib": None, "parent": None}
+                  for t in range(T)]
+        prev_hist = None  # [A_prev, d, B, k] histograms of last level's split nodes
+        mw = (d + 31) // 32
+        root_ids = [None] * T
+        for depth in range(p.max_depth + 1):
+            if not active:
+                break
+            A = len(active)
+            # ---- decide which active nodes get a histogram built
+            if subtract:
+                build = [True] * A
+                for a, e in enumerate(active):
+                    s = e["sib"]
+                    if s is not None and e["parent"] is not None:
+                        # build only the smaller of two active siblings
+                        if self._weight(e["stats"]) > self._weight(active[s]["stats"]) or \
+                                (self._weight(e["stats"]) == self._weight(active[s]["stats"]) and a > s):
+                            build[a] = False
+            else:
+                build = [True] * A
+            build_ids = [a for a in range(A) if build[a]]
+            slot_of = np.full(A, -1, dtype=np.int32)
+            slot_of[build_ids] = np.arange(len(build_ids), dtype=np.int32)
+            slot_tree = np.array([active[a]["tree"] for a in build_ids], dtype=np.int32)
+            masks_np = None
+            if masked:
+                masks_np = np.stack([self._feature_mask(e["tree"], e["key"]) for e in active])
+            fm_build = None
+            if masks_np is not None:
+                fm_build = torch.from_numpy(masks_np[build_ids].view(np.int32)).to(dev)
+            build_slot = torch.from_numpy(slot_of).to(dev)
+            if self.classification:
+                Hb = K.hist_classes(data.bins, d, node, weights, stats_rows["label"], self.C, build_slot, slot_tree,
+                                    fm_build, B)
+            else:
+                Hb = K.hist_moments(data.bins, d, node, weights, stats_rows.get("v0"), stats_rows["v1"],
+                                    build_slot, slot_tree, fm_build, B)
+            self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
+            # ---- assemble every active node's histogram
+            H = torch.empty((A, d, B, self.stats_k), dtype=torch.float64, device=dev)
+            if build_ids:
+                H[torch.tensor(build_ids, device=dev)] = Hb
+            derived = [a for a in range(A) if not build[a]]
+            if derived:
+                di = torch.tensor(derived, device=dev)
+                par = torch.tensor([active[a]["parent"] for a in derived], device=dev)
+                sib = torch.tensor([active[a]["sib"] for a in derived], device=dev)
+                H[di] = prev_hist[par] - H[sib]
+            tot = self._node_stats(H, None)
+            if depth == 0:
+                for a, e in enumerate(active):
+                    st = tot[a].cpu().numpy()
+                    e["stats"] = st
+            masks_t = torch.from_numpy(masks_np.view(np.int32)).to(dev) if masks_np is not None else None
+            gain, bf, bb, lst, rst, order, cat_feats = self._best_splits(H, tot, masks_t)
+            gain_h, bf_h, bb_h = gain.cpu().numpy(), bf.cpu().numpy(), bb.cpu().numpy()
+            lst_h, rst_h = lst.cpu().numpy(), rst.cpu().numpy()
+            order_h = order.cpu().numpy() if order is not None else None
+            # ---- create forest nodes for the active set, decide splits
+            split_feat = np.full(A, -1, dtype=np.int32)
+            split_bin = np.zeros(A, dtype=np.int32)
+            cat_off = np.full(A, -1, dtype=np.int32)
+            cat_masks = []
+            child = np.full(2 * A, -1, dtype=np.int32)
+            nxt = []
+            for a, e in enumerate(active):
+                st = e["stats"]
+                if e["fid"] is None:
+                    fid = forest.add(self._leaf_value(st), self._weight(st), depth, self._impurity(st))
+                    e["fid"] = fid
+                    if depth == 0:
+                        root_ids[e["tree"]] = fid
+                fid = e["fid"]
+                g = float(gain_h[a])
+                W = self._weight(st)
+                can_split = depth < p.max_depth and np.isfinite(g) and g > 0 and g >= p.min_info_gain and \
+                    W >= 2 * p.min_instances
+                if not can_split:
+                    continue
+                f = int(bf_h[a])
+                b = int(bb_h[a])
+                forest.feat[fid] = f
+                forest.gain[fid] = g
+                if f in self.data.categorical:
+                    ci = cat_feats.index(f)
+                    left_cats = order_h[a, ci, : b + 1]
+                    m = np.zeros(8, dtype=np.uint32)
+                    for c in left_cats:
+                        m[int(c) >> 5] |= np.uint32(1) << np.uint32(int(c) & 31)
+                    forest.is_cat[fid] = True
+                    forest.catmask[fid] = m
+                    cat_off[a] = len(cat_masks)
+                    cat_masks.append(m)
+                else:
+                    forest.bin[fid] = b
+                    forest.thr[fid] = float(self.data.thresholds[f, b])
+                    split_bin[a] = b
+                split_feat[a] = f
+                ls, rs = lst_h[a], rst_h[a]
+                lid = forest.add(self._leaf_value(ls), self._weight(ls), depth + 1, self._impurity(ls))
+                rid = forest.add(self._leaf_value(rs), self._weight(rs), depth + 1, self._impurity(rs))
+                forest.left[fid], forest.right[fid] = lid, rid
+                for side, (cid, cst) in enumerate(((lid, ls), (rid, rs))):
+                    cw = self._weight(cst)
+                    leaf = depth + 1 >= p.max_depth or cw < 2 * p.min_instances
+                    if self.classification and not leaf:
+                        leaf = int((cst > 0).sum()) <= 1  # pure node
+                    if not leaf:
+                        child[2 * a + side] = len(nxt)
+                        nxt.append({"tree": e["tree"], "fid": cid, "key": e["key"] * 2 + side, "depth": depth + 1,
+                                    "stats": cst, "sib": None, "parent": a, "side": side})
+            # siblings (both children active) for subtraction
+            by_parent: Dict[int, List[int]] = {}
+            for i, e in enumerate(nxt):
+                by_parent.setdefault(e["parent"], []).append(i)
+            for par, kids in by_parent.items():
+                if len(kids) == 2:
+                    nxt[kids[0]]["sib"], nxt[kids[1]]["sib"] = kids[1], kids[0]
+                else:
+                    nxt[kids[0]]["sib"] = None
+                    if subtract:
+                        nxt[kids[0]]["parent"] = None  # single child: build directly
+            if nxt:
+                cm = np.stack(cat_masks).view(np.int32) if cat_masks else np.zeros((0, 8), np.int32)
+                K.partition(data.bins, node, torch.from_numpy(split_feat).to(dev),
+                            torch.from_numpy(split_bin).to(dev), torch.from_numpy(cat_off).to(dev),
+                            torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child).to(dev))
+            prev_hist = H if subtract else None
+            active = nxt
+        forest.roots.extend(root_ids)
+        forest._dev = {}
+        return forest

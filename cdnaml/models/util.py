@@ -1,0 +1,122 @@
+"""Shared helpers for estimators: device matrices, ML attributes, errors."""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..sql import types as T
+from ..sql.batch import Batch, ColumnData, concat_batches
+from ..sql.dataframe import MapPlan
+
+
+class IllegalArgumentException(ValueError):
+    pass
+
+
+_VECTOR_SQL = "struct<type:tinyint,size:int,indices:array<int>,values:array<double>>"
+
+
+def require_vector(df, col: str):
+    f = df.schema[col] if col in df.columns else None
+    if f is None:
+        raise IllegalArgumentException(f"Field \"{col}\" does not exist.\nAvailable fields: {', '.join(df.columns)}")
+    if not isinstance(f.dataType, (T.VectorUDT, T.ArrayType)):
+        raise IllegalArgumentException(
+            f"requirement failed: Column {col} must be of type {_VECTOR_SQL} but was actually "
+            f"{f.dataType.simpleString()}.")
+
+
+def require_numeric(df, col: str):
+    f = df.schema[col]
+    if not (f.dataType.is_numeric or isinstance(f.dataType, T.BooleanType)):
+        raise IllegalArgumentException(
+            f"requirement failed: Column {col} must be of type numeric but was actually of type "
+            f"{f.dataType.simpleString()}.")
+
+
+def local_batch(df, cols: List[str]) -> Batch:
+    parts = df.select(*cols)._plan.execute()
+    if not parts:
+        from ..sql.batch import empty_batch
+        return empty_batch(df.select(*cols).schema, df._session.device)
+    return concat_batches(parts)
+
+
+def local_xyw(df, features_col: str, label_col: Optional[str] = None, weight_col: Optional[str] = None,
+              drop_null_label: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor], Optional[torch.Tensor]]:
+    """This rank's rows as device tensors: X f32 [n, d], y f64 [n], w f64 [n]."""
+    require_vector(df, features_col)
+    cols = [features_col] + ([label_col] if label_col else []) + ([weight_col] if weight_col else [])
+    b = local_batch(df, cols)
+    X = b.columns[features_col].values
+    if X.dtype != torch.float32:
+        X = X.float()
+    y = w = None
+    keep = None
+    if label_col:
+        yc = b.columns[label_col]
+        y = yc.values.to(torch.float64)
+        if yc.valid is not None and drop_null_label:
+            keep = yc.valid
+    if weight_col:
+        w = b.columns[weight_col].values.to(torch.float64)
+    if keep is not None and not bool(keep.all()):
+        X = X[keep]
+        y = y[keep]
+        w = None if w is None else w[keep]
+    return X, y, w
+
+
+def vector_attrs(meta: dict, width: int, name: str) -> List[dict]:
+    """Per-slot attributes of a vector column (names, nominal arity)."""
+    ma = (meta or {}).get("ml_attr")
+    if ma and "attrs" in ma:
+        attrs = list(ma["attrs"])
+        if len(attrs) == width:
+            return attrs
+    return [{"idx": i, "name": f"{name}_{i}", "type": "numeric"} for i in range(width)]
+
+
+def scalar_attr(meta: dict, name: str) -> dict:
+    ma = (meta or {}).get("ml_attr")
+    if ma and "type" in ma:
+        a = dict(ma)
+        a.setdefault("name", name)
+        return a
+    return {"name": name, "type": "numeric"}
+
+
+def with_prediction(df, name: str, fn, out_type: T.DataType = None, meta_fn=None):
+    """Append a column computed per partition by ``fn(batch) -> ColumnData``."""
+    def per(b: Batch, ctx):
+        c = fn(b)
+        return b.with_column(name, c)
+    return df._new(MapPlan(df._plan, f"Transform -> {name}", per))
+
+
+def categorical_info(meta: dict, width: int, name: str) -> dict:
+    """{feature index: arity} for nominal/binary vector slots (Spark categoricalFeaturesInfo)."""
+    out = {}
+    for i, a in enumerate(vector_attrs(meta, width, name)):
+        t = a.get("type")
+        if t == "nominal":
+            k = a.get("num_vals") or (len(a["vals"]) if "vals" in a else None)
+            if k:
+                out[i] = int(k)
+        elif t == "binary":
+            out[i] = 2
+    return out
+
+
+def global_count(session, n_local: int) -> int:
+    return int(session.comm.all_reduce_scalar(float(n_local)))
+
+
+def global_offset(session, n_local: int) -> int:
+    comm = session.comm
+    if not comm.distributed:
+        return 0
+    counts = comm.all_gather_object(int(n_local))
+    return int(sum(counts[: comm.rank]))

@@ -352,7 +352,7 @@ def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree
             c = x.to(torch.int64)
             okc = (c >= 0) & (c < 256)
             cc = c.clamp(0, 255)
-            moff = torch.where(cont, torch.zeros_like(f), nv[:, 1]).clamp(min=0)
+            moff = torch.where(f <= -2, nv[:, 1], torch.zeros_like(f)).clamp(min=0)
             words = mk[(moff * 8 + (cc >> 5))] if mk.numel() else torch.zeros_like(cc)
             catleft = okc & ((words >> (cc & 31)) & 1).bool()
             left = torch.where(cont, x <= thr, catleft)
@@ -392,7 +392,7 @@ def predict_binned_add(bins: torch.Tensor, nodes: torch.Tensor, root: int, value
         cont = f >= 0
         fi = torch.where(cont, f, -f - 2).clamp(min=0)
         b = bm[rows, fi]
-        moff = torch.where(cont, torch.zeros_like(f), nv[:, 1]).clamp(min=0)
+        moff = torch.where(f <= -2, nv[:, 1], torch.zeros_like(f)).clamp(min=0)
         words = mk[(moff * 8 + (b >> 5))] if mk.numel() else torch.zeros_like(b)
         left = torch.where(cont, b <= nv[:, 1], ((words >> (b & 31)) & 1).bool())
         cur = torch.where(internal, torch.where(left, nv[:, 2], nv[:, 3]), cur)

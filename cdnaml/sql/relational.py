@@ -1,0 +1,379 @@
+"""Partition-local relational algorithms on device tensors.
+
+Group-by / join / distinct / sort all start from dense integer *key codes*:
+each key column is reduced to a code (string dictionary code, or the
+``torch.unique`` inverse of numeric values), codes are combined mixed-radix
+into one int64 and densified again — after that every operator is a sort,
+``searchsorted`` or a segmented ``scatter_reduce`` on the GPU.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import types as T
+from .batch import Batch, ColumnData, column_from_numpy, concat_columns, unify_dictionaries
+
+
+def column_codes(c: ColumnData) -> Tuple[torch.Tensor, int]:
+    """Dense int64 codes (nulls -> 0, values -> 1..k) and cardinality k+1."""
+    v = c.values
+    if v.dim() == 2:
+        _, inv = torch.unique(v, dim=0, return_inverse=True)
+        codes = inv + 1
+    elif isinstance(c.dtype, T.StringType):
+        codes = v.long() + 1
+        if codes.numel():
+            uniq, inv = torch.unique(codes, return_inverse=True)
+            codes = inv + 1
+    else:
+        x = v
+        if x.dtype.is_floating_point:
+            x = torch.where(x == 0, torch.zeros_like(x), x)  # -0.0 == 0.0
+        _, inv = torch.unique(x, return_inverse=True)
+        codes = inv + 1
+    if c.valid is not None:
+        codes = torch.where(c.valid, codes, torch.zeros_like(codes))
+    k = int(codes.max()) + 1 if codes.numel() else 1
+    return codes, k
+
+
+def combine_codes(cols: List[ColumnData], n: int, device) -> Tuple[torch.Tensor, int]:
+    """Dense group id per row for the tuple of key columns; returns (gid, ngroups)."""
+    if not cols:
+        return torch.zeros(n, dtype=torch.int64, device=device), (1 if n else 0)
+    combined = None
+    for c in cols:
+        codes, k = column_codes(c)
+        if combined is None:
+            combined = codes
+        else:
+            combined = combined * k + codes
+            if combined.numel() and int(combined.max()) > 2 ** 60 // max(k, 1):
+                _, combined = torch.unique(combined, return_inverse=True)
+    uniq, gid = torch.unique(combined, return_inverse=True)
+    return gid, int(uniq.numel())
+
+
+def first_index_per_group(gid: torch.Tensor, ngroups: int) -> torch.Tensor:
+    n = gid.numel()
+    idx = torch.arange(n, device=gid.device)
+    first = torch.full((ngroups,), n, dtype=torch.int64, device=gid.device)
+    first.scatter_reduce_(0, gid, idx, reduce="amin", include_self=True)
+    return first
+
+
+# ----------------------------------------------------------------- aggregation
+def aggregate(batch: Batch, keys: List[str], aggs: List[Tuple[str, object]]) -> Batch:
+    """Local hash aggregation: keys + one output column per (name, AggExpr)."""
+    from .column import EvalContext
+    n = batch.n
+    dev = batch.device
+    gid, G = combine_codes([batch.columns[k] for k in keys], n, dev)
+    if not keys:
+        gid = torch.zeros(n, dtype=torch.int64, device=dev)
+        G = 1
+    first = first_index_per_group(gid, G) if G else torch.zeros(0, dtype=torch.int64, device=dev)
+    out: Dict[str, ColumnData] = {}
+    if keys and G:
+        for k in keys:
+            out[k] = batch.columns[k].take(first)
+    elif keys:
+        for k in keys:
+            out[k] = batch.columns[k].slice(0, 0)
+    ctx = EvalContext()
+    for name, agg in aggs:
+        out[name] = _agg_one(batch, agg, gid, G, first, ctx)
+    return Batch(out, G, dev)
+
+
+def _seg_sum(vals, gid, G, dtype=torch.float64):
+    s = torch.zeros(G, dtype=dtype, device=vals.device)
+    s.index_add_(0, gid, vals.to(dtype))
+    return s
+
+
+def _agg_one(batch: Batch, agg, gid, G, first, ctx) -> ColumnData:
+    kind = agg.kind
+    dev = batch.device
+    if agg.x is None:  # count(*)
+        cnt = torch.bincount(gid, minlength=G).to(torch.int64) if batch.n else torch.zeros(G, dtype=torch.int64,
+                                                                                           device=dev)
+        return ColumnData(cnt[:G], T.LongType())
+    c = agg.x.eval(batch, ctx)
+    valid = c.valid_mask()
+    if agg.distinct:
+        # dedupe (gid, value) pairs first
+        vcodes, k = column_codes(c)
+        pair = gid * k + vcodes
+        keep = valid.clone()
+        if batch.n:
+            u, inv = torch.unique(pair, return_inverse=True)
+            fi = first_index_per_group(inv, u.numel())
+            mask = torch.zeros(batch.n, dtype=torch.bool, device=dev)
+            mask[fi] = True
+            keep = keep & mask
+        valid = keep
+    if kind == "count":
+        cnt = torch.zeros(G, dtype=torch.int64, device=dev)
+        cnt.index_add_(0, gid, valid.to(torch.int64))
+        return ColumnData(cnt, T.LongType())
+    if kind in ("first", "last"):
+        idx = torch.arange(batch.n, device=dev)
+        if kind == "first":
+            pos = torch.full((G,), batch.n, dtype=torch.int64, device=dev)
+            pos.scatter_reduce_(0, gid, idx, reduce="amin", include_self=True)
+        else:
+            pos = torch.full((G,), -1, dtype=torch.int64, device=dev)
+            pos.scatter_reduce_(0, gid, idx, reduce="amax", include_self=True)
+        return c.take(pos.clamp(0, max(batch.n - 1, 0))) if batch.n else c.slice(0, 0)
+    if kind in ("collect_list", "collect_set"):
+        vals = c.to_numpy()
+        g = gid.cpu().numpy()
+        lists = [[] for _ in range(G)]
+        vm = valid.cpu().numpy()
+        for i in range(batch.n):
+            if vm[i]:
+                lists[g[i]].append(vals[i])
+        if kind == "collect_set":
+            lists = [list(dict.fromkeys(x)) for x in lists]
+        return ColumnData(torch.zeros(G, device=dev), T.ArrayType(c.dtype), meta={"_py": lists})
+    if isinstance(c.dtype, T.StringType) and kind in ("min", "max"):
+        v = c.values.long()
+        fill = 2 ** 40 if kind == "min" else -1
+        v = torch.where(valid, v, torch.full_like(v, fill))
+        r = torch.full((G,), fill, dtype=torch.int64, device=dev)
+        r.scatter_reduce_(0, gid, v, reduce="amin" if kind == "min" else "amax", include_self=True)
+        ok = (r != fill)
+        return ColumnData(torch.where(ok, r, torch.zeros_like(r)).to(torch.int32), c.dtype,
+                          None if bool(ok.all()) else ok, c.dictionary)
+    x = c.values.to(torch.float64) if c.values.dim() == 1 else c.values.to(torch.float64)
+    xz = torch.where(valid, x, torch.zeros_like(x))
+    cnt = torch.zeros(G, dtype=torch.float64, device=dev)
+    cnt.index_add_(0, gid, valid.to(torch.float64))
+    nonempty = cnt > 0
+    vnull = None if bool(nonempty.all()) else nonempty
+    if kind == "sum":
+        s = _seg_sum(xz, gid, G)
+        if isinstance(c.dtype, T.IntegralType):
+            return ColumnData(s.to(torch.int64), T.LongType(), vnull)
+        return ColumnData(s, T.DoubleType(), vnull)
+    if kind == "avg":
+        s = _seg_sum(xz, gid, G)
+        return ColumnData(s / cnt.clamp_min(1), T.DoubleType(), vnull)
+    if kind in ("min", "max"):
+        fill = float("inf") if kind == "min" else float("-inf")
+        xv = torch.where(valid, x, torch.full_like(x, fill))
+        r = torch.full((G,), fill, dtype=torch.float64, device=dev)
+        r.scatter_reduce_(0, gid, xv, reduce="amin" if kind == "min" else "amax", include_self=True)
+        r = torch.where(nonempty, r, torch.zeros_like(r))
+        dt = c.dtype
+        if isinstance(dt, (T.IntegralType, T.DateType, T.TimestampType, T.BooleanType)):
+            return ColumnData(r.to(dt.torch_dtype), dt, vnull)
+        return ColumnData(r.to(c.values.dtype), dt, vnull)
+    if kind in ("stddev", "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop", "skewness", "kurtosis"):
+        s = _seg_sum(xz, gid, G)
+        mu = s / cnt.clamp_min(1)
+        dev2 = torch.where(valid, x - mu[gid], torch.zeros_like(x))
+        m2 = _seg_sum(dev2 * dev2, gid, G)
+        if kind in ("skewness", "kurtosis"):
+            m3 = _seg_sum(dev2 ** 3, gid, G)
+            m4 = _seg_sum(dev2 ** 4, gid, G)
+            nn = cnt.clamp_min(1)
+            if kind == "skewness":
+                r = torch.sqrt(nn) * m3 / m2.clamp_min(1e-300) ** 1.5
+            else:
+                r = nn * m4 / (m2 * m2).clamp_min(1e-300) - 3.0
+            return ColumnData(r, T.DoubleType(), vnull)
+        pop = kind in ("stddev_pop", "var_pop")
+        denom = cnt if pop else cnt - 1
+        var = m2 / denom.clamp_min(1)
+        ok = denom > 0
+        var = torch.where(ok, var, torch.full_like(var, float("nan")))
+        r = torch.sqrt(var) if kind.startswith("stddev") else var
+        return ColumnData(r, T.DoubleType(), vnull)
+    if kind == "percentile":
+        qs = agg.param
+        multi = isinstance(qs, (list, tuple))
+        qlist = list(qs) if multi else [qs]
+        order = torch.argsort(torch.where(valid, x, torch.full_like(x, float("inf"))), stable=True)
+        order = order[torch.argsort(gid[order], stable=True)]
+        gs = gid[order]
+        starts = torch.zeros(G + 1, dtype=torch.int64, device=dev)
+        starts[1:] = torch.cumsum(cnt.to(torch.int64), 0)
+        gcount_all = torch.bincount(gs, minlength=G)
+        gstart_all = torch.zeros(G, dtype=torch.int64, device=dev)
+        gstart_all[1:] = torch.cumsum(gcount_all, 0)[:-1]
+        res = []
+        for q in qlist:
+            # Spark percentile_approx: smallest value with rank >= ceil(q * n)
+            rk = torch.ceil(q * cnt).to(torch.int64).clamp_min(1) - 1
+            pos = gstart_all + rk.clamp_min(0)
+            pos = pos.clamp(0, max(batch.n - 1, 0))
+            res.append(x[order][pos] if batch.n else torch.zeros(G, dtype=torch.float64, device=dev))
+        if multi:
+            return ColumnData(torch.stack(res, 1), T.ArrayType(T.DoubleType()), vnull)
+        return ColumnData(res[0], T.DoubleType(), vnull)
+    raise ValueError(f"unsupported aggregate {kind}")
+
+
+# ----------------------------------------------------------------------- sort
+def sort_indices(batch: Batch, orders) -> torch.Tensor:
+    """Stable multi-key sort permutation. orders: list of (ColumnData, ascending, nulls_first)."""
+    n = batch.n
+    perm = torch.arange(n, device=batch.device)
+    for c, asc, nulls_first in reversed(orders):
+        c = c.take(perm)
+        if isinstance(c.dtype, T.StringType):
+            key = c.values.to(torch.float64)
+        elif c.values.dim() == 2:
+            key = c.values[:, 0].to(torch.float64)
+        else:
+            key = c.values.to(torch.float64)
+        if key.dtype.is_floating_point:
+            nan = torch.isnan(key)
+            # Spark: NaN is larger than any other value
+            key = torch.where(nan, torch.full_like(key, float("inf")), key)
+        if not asc:
+            key = -key
+        valid = c.valid_mask()
+        big = float("inf")
+        nullkey = torch.full_like(key, -big if nulls_first else big)
+        key = torch.where(valid, key, nullkey)
+        # tie-break by null flag explicitly (inf ties)
+        nulls = (~valid).to(torch.int8)
+        if nulls_first:
+            nulls = -nulls
+        p1 = torch.argsort(key, stable=True)
+        p2 = torch.argsort(nulls[p1], stable=True)
+        perm = perm[p1][p2]
+    return perm
+
+
+# ----------------------------------------------------------------------- join
+def join(left: Batch, right: Batch, lkeys: List[str], rkeys: List[str], how: str,
+         drop_right_keys: bool = True) -> Batch:
+    """Local equi-join of two partitions (keys already co-partitioned)."""
+    dev = left.device
+    how = {"inner": "inner", "left": "left", "leftouter": "left", "left_outer": "left", "right": "right",
+           "rightouter": "right", "right_outer": "right", "outer": "full", "full": "full", "fullouter": "full",
+           "full_outer": "full", "semi": "semi", "leftsemi": "semi", "left_semi": "semi", "anti": "anti",
+           "leftanti": "anti", "left_anti": "anti", "cross": "cross"}[how.lower()]
+    nl, nr = left.n, right.n
+    if how == "cross":
+        li = torch.arange(nl, device=dev).repeat_interleave(nr)
+        ri = torch.arange(nr, device=dev).repeat(nl)
+        return _assemble(left, right, li, ri, None, None, [], drop_right_keys=False)
+    # shared key codes across both sides
+    lk, rk = [], []
+    for a, b in zip(lkeys, rkeys):
+        ca, cb = left.columns[a], right.columns[b]
+        if isinstance(ca.dtype, T.StringType) or isinstance(cb.dtype, T.StringType):
+            from .column import _cast
+            ca = ca if isinstance(ca.dtype, T.StringType) else _cast(ca, T.StringType())
+            cb = cb if isinstance(cb.dtype, T.StringType) else _cast(cb, T.StringType())
+            ca, cb = unify_dictionaries([ca, cb])
+        elif ca.values.dtype != cb.values.dtype:
+            ca = ColumnData(ca.values.to(torch.float64), T.DoubleType(), ca.valid)
+            cb = ColumnData(cb.values.to(torch.float64), T.DoubleType(), cb.valid)
+        both = concat_columns([ca, cb])
+        lk.append(both)
+    gid, G = combine_codes(lk, nl + nr, dev)
+    # null keys never match
+    nullany = torch.zeros(nl + nr, dtype=torch.bool, device=dev)
+    for c in lk:
+        nullany |= ~c.valid_mask()
+    lg, rg = gid[:nl], gid[nl:]
+    lnull, rnull = nullany[:nl], nullany[nl:]
+    rg_eff = torch.where(rnull, torch.full_like(rg, -1), rg)
+    rorder = torch.argsort(rg_eff, stable=True)
+    rsorted = rg_eff[rorder]
+    lo = torch.searchsorted(rsorted, lg, right=False)
+    hi = torch.searchsorted(rsorted, lg, right=True)
+    cnt = torch.where(lnull, torch.zeros_like(hi), hi - lo)
+    if how == "semi":
+        return left.filter(cnt > 0)
+    if how == "anti":
+        return left.filter(cnt == 0)
+    li = torch.arange(nl, device=dev).repeat_interleave(cnt)
+    start = torch.repeat_interleave(lo, cnt)
+    off = torch.arange(li.numel(), device=dev) - torch.repeat_interleave(torch.cumsum(cnt, 0) - cnt, cnt)
+    ri = rorder[start + off] if li.numel() else torch.zeros(0, dtype=torch.int64, device=dev)
+    lmiss = rmiss = None
+    if how in ("left", "full"):
+        lmiss = torch.nonzero(cnt == 0).flatten()
+    if how in ("right", "full"):
+        matched = torch.zeros(nr, dtype=torch.bool, device=dev)
+        if ri.numel():
+            matched[ri] = True
+        rmiss = torch.nonzero(~matched).flatten()
+    return _assemble(left, right, li, ri, lmiss, rmiss, list(zip(lkeys, rkeys)), drop_right_keys, how)
+
+
+def _assemble(left, right, li, ri, lmiss, rmiss, keypairs, drop_right_keys, how="inner"):
+    dev = left.device
+    cols = {}
+    nmatch = li.numel()
+    nlm = 0 if lmiss is None else lmiss.numel()
+    nrm = 0 if rmiss is None else rmiss.numel()
+    total = nmatch + nlm + nrm
+    rkeys = {b: a for a, b in keypairs} if drop_right_keys else {}
+
+    def gather(c: ColumnData, idx, present_mask_len, side_present):
+        parts_v, parts_m = [], []
+        taken = c.take(idx)
+        parts_v.append(taken.values)
+        parts_m.append(taken.valid_mask())
+        return taken
+
+    for name, c in left.columns.items():
+        pieces = [c.take(li)]
+        if nlm:
+            pieces.append(c.take(lmiss))
+        if nrm:
+            # right-only rows: left side null, but keys come from right
+            rname = next((b for a, b in keypairs if a == name), None)
+            if rname is not None and drop_right_keys:
+                rc = right.columns[rname]
+                if isinstance(c.dtype, T.StringType):
+                    pieces.append(rc.take(rmiss))
+                else:
+                    t = rc.take(rmiss)
+                    pieces.append(ColumnData(t.values.to(c.values.dtype), c.dtype, t.valid))
+            else:
+                pieces.append(_null_like(c, nrm))
+        cols[name] = concat_columns(pieces) if len(pieces) > 1 else pieces[0]
+    for name, c in right.columns.items():
+        if name in rkeys:
+            continue
+        outname = name
+        if outname in cols:
+            outname = name  # Spark keeps duplicate names; we suffix to stay addressable
+            k = 1
+            while outname in cols:
+                outname = f"{name}_{k}"
+                k += 1
+        pieces = [c.take(ri)]
+        if nlm:
+            pieces.append(_null_like(c, nlm))
+        if nrm:
+            pieces.append(c.take(rmiss))
+        cols[outname] = concat_columns(pieces) if len(pieces) > 1 else pieces[0]
+    return Batch(cols, total, dev)
+
+
+def _null_like(c: ColumnData, n: int) -> ColumnData:
+    shape = (n,) + tuple(c.values.shape[1:])
+    return ColumnData(torch.zeros(shape, dtype=c.values.dtype, device=c.device), c.dtype,
+                      torch.zeros(n, dtype=torch.bool, device=c.device), c.dictionary, c.meta)
+
+
+# ------------------------------------------------------------------- distinct
+def dedup_indices(batch: Batch, keys: List[str]) -> torch.Tensor:
+    gid, G = combine_codes([batch.columns[k] for k in keys], batch.n, batch.device)
+    if batch.n == 0:
+        return torch.zeros(0, dtype=torch.int64, device=batch.device)
+    first = first_index_per_group(gid, G)
+    return torch.sort(first).values

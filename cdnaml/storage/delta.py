@@ -1,0 +1,310 @@
+"""Versioned ("Delta-style") tables: JSON commit log + Parquet parts.
+
+Behaviour pinned by ML 00c - Delta Review.py:57-254 and Labs/ML 05L:54-75:
+``_delta_log/000…N.json`` commits with protocol/metaData/add/remove/commitInfo
+actions, ``mode("overwrite")``/``append``, ``partitionBy`` directories,
+``mergeSchema`` / ``overwriteSchema`` evolution, time travel with
+``versionAsOf`` / ``timestampAsOf``, ``DESCRIBE HISTORY``, and ``vacuum``
+which refuses short retention unless
+``spark.databricks.delta.retentionDurationCheck.enabled`` is false — after
+which vacuumed versions can no longer be read.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import json
+import os
+import time
+import uuid
+from typing import Dict, List, Optional
+
+import pandas as pd
+
+from ..sql import types as T
+from ..sql.dataframe import DataFrame
+
+LOG = "_delta_log"
+
+
+class DeltaError(Exception):
+    pass
+
+
+def _log_dir(path):
+    return os.path.join(path, LOG)
+
+
+def _versions(path) -> List[int]:
+    d = _log_dir(path)
+    if not os.path.isdir(d):
+        return []
+    return sorted(int(f[:-5]) for f in os.listdir(d) if f.endswith(".json") and f[:-5].isdigit())
+
+
+def is_delta_table(path) -> bool:
+    return bool(_versions(path))
+
+
+def _read_commit(path, v) -> List[dict]:
+    with open(os.path.join(_log_dir(path), f"{v:020d}.json")) as f:
+        return [json.loads(l) for l in f if l.strip()]
+
+
+class Snapshot:
+    def __init__(self, path, version):
+        self.path = path
+        self.version = version
+        self.files: Dict[str, dict] = {}
+        self.metadata: Optional[dict] = None
+        for v in range(0, version + 1):
+            if not os.path.exists(os.path.join(_log_dir(path), f"{v:020d}.json")):
+                continue
+            for a in _read_commit(path, v):
+                if "metaData" in a:
+                    self.metadata = a["metaData"]
+                elif "add" in a:
+                    self.files[a["add"]["path"]] = a["add"]
+                elif "remove" in a:
+                    self.files.pop(a["remove"]["path"], None)
+
+    @property
+    def schema(self) -> T.StructType:
+        return T.StructType.fromJson(self.metadata["schemaString"])
+
+    @property
+    def partition_columns(self) -> List[str]:
+        return self.metadata.get("partitionColumns", []) if self.metadata else []
+
+
+def _commit_timestamp(path, v) -> int:
+    for a in _read_commit(path, v):
+        if "commitInfo" in a:
+            return int(a["commitInfo"]["timestamp"])
+    return int(os.path.getmtime(os.path.join(_log_dir(path), f"{v:020d}.json")) * 1000)
+
+
+def _parse_ts(ts) -> int:
+    if isinstance(ts, (int, float)):
+        return int(ts)
+    t = pd.Timestamp(ts)
+    if t.tzinfo is None:
+        t = t.tz_localize(_dt.datetime.now().astimezone().tzinfo)
+    return int(t.timestamp() * 1000)
+
+
+def resolve_version(path, options) -> int:
+    vs = _versions(path)
+    if not vs:
+        raise DeltaError(f"`{path}` is not a Delta table.")
+    if "versionasof" in options:
+        v = int(options["versionasof"])
+        if v not in vs:
+            raise DeltaError(f"Cannot time travel Delta table to version {v}. Available versions: [{vs[0]}, {vs[-1]}].")
+        return v
+    if "timestampasof" in options:
+        ts = _parse_ts(options["timestampasof"])
+        cands = [v for v in vs if _commit_timestamp(path, v) <= ts]
+        if not cands:
+            raise DeltaError(f"The provided timestamp ({options['timestampasof']}) is before the earliest version "
+                             f"available to this table.")
+        return cands[-1]
+    return vs[-1]
+
+
+def read_delta(session, path, options=None) -> DataFrame:
+    from ..sql.readwriter import _strip_dbfs, scan_parquet_files
+    options = {k.lower(): v for k, v in (options or {}).items()}
+    path = _strip_dbfs(path)
+    v = resolve_version(path, options)
+    snap = Snapshot(path, v)
+    files = [os.path.join(path, p) for p in sorted(snap.files)]
+    missing = [f for f in files if not os.path.exists(f)]
+    if missing:
+        raise DeltaError(f"FileNotFoundException: {missing[0]} — the file was deleted (e.g. by VACUUM); "
+                         f"version {v} can no longer be read.")
+    schema = snap.schema
+    if not files:
+        return session.createDataFrame(pd.DataFrame({f.name: [] for f in schema.fields}), schema)
+    df = scan_parquet_files(session, files, [path] * len(files), schema, name=f"DeltaScan v{v}")
+    return df
+
+
+def _now_ms():
+    return int(time.time() * 1000)
+
+
+def _write_commit(path, version, actions):
+    os.makedirs(_log_dir(path), exist_ok=True)
+    fp = os.path.join(_log_dir(path), f"{version:020d}.json")
+    if os.path.exists(fp):
+        raise DeltaError(f"ConcurrentModificationException: version {version} already committed")
+    tmp = fp + f".tmp{uuid.uuid4().hex}"
+    with open(tmp, "w") as f:
+        for a in actions:
+            f.write(json.dumps(a) + "\n")
+    os.replace(tmp, fp)
+
+
+def write_delta(df: DataFrame, path: str, mode: str, options: dict, partition_by: List[str],
+                operation: str = "WRITE"):
+    from ..sql.readwriter import write_files
+    session = df._session
+    comm = session.comm
+    vs = _versions(path)
+    exists = bool(vs)
+    new_schema = df.schema
+    if exists and mode in ("error", "errorifexists", "default"):
+        raise DeltaError(f"Table already exists at {path}")
+    if exists and mode == "ignore":
+        return
+    snap = Snapshot(path, vs[-1]) if exists else None
+    schema = new_schema
+    merge = options.get("mergeschema", "false") == "true"
+    overwrite_schema = options.get("overwriteschema", "false") == "true"
+    if snap is not None:
+        old = snap.schema
+        if partition_by and partition_by != snap.partition_columns and mode == "overwrite" and not overwrite_schema:
+            raise DeltaError("AnalysisException: partition columns do not match the table; use "
+                             "option('overwriteSchema', 'true') to change them")
+        if not partition_by:
+            partition_by = snap.partition_columns if not overwrite_schema else []
+        if [(f.name, f.dataType) for f in old.fields] != [(f.name, f.dataType) for f in new_schema.fields]:
+            if mode == "overwrite" and overwrite_schema:
+                schema = new_schema
+            elif merge:
+                fields = list(old.fields)
+                names = {f.name for f in fields}
+                for f in new_schema.fields:
+                    if f.name not in names:
+                        fields.append(f)
+                schema = T.StructType(fields)
+            else:
+                raise DeltaError(
+                    "AnalysisException: A schema mismatch detected when writing to the Delta table. To enable "
+                    "schema migration using DataFrameWriter or DataStreamWriter, please set: "
+                    "'.option(\"mergeSchema\", \"true\")'. For other operations, set the session configuration "
+                    "spark.databricks.delta.schema.autoMerge.enabled to \"true\".\n"
+                    f"Table schema: {old.simpleString()}\nData schema: {new_schema.simpleString()}")
+    # data files go under the table root; write_files with append semantics (never deletes old files)
+    written = write_files(df, path, "parquet", "append", {"compression": "snappy"}, partition_by)
+    allw = comm.all_gather_object(written) if comm.distributed else [written]
+    if comm.rank == 0:
+        version = vs[-1] + 1 if exists else 0
+        ts = _now_ms()
+        actions = [{"commitInfo": {"timestamp": ts, "operation": "CREATE TABLE AS SELECT" if not exists and
+                                   operation == "WRITE" and False else operation,
+                                   "operationParameters": {"mode": {"overwrite": "Overwrite", "append": "Append"}
+                                                           .get(mode, "ErrorIfExists"),
+                                                           "partitionBy": json.dumps(partition_by)},
+                                   "isBlindAppend": mode == "append", "readVersion": vs[-1] if exists else None,
+                                   "operationMetrics": {"numFiles": str(sum(len(w) for w in allw))}}}]
+        if not exists:
+            actions.append({"protocol": {"minReaderVersion": 1, "minWriterVersion": 2}})
+        if not exists or schema is not new_schema or snap is None or schema.json() != snap.schema.json() or \
+                partition_by != snap.partition_columns:
+            actions.append({"metaData": {"id": (snap.metadata["id"] if snap else str(uuid.uuid4())),
+                                         "format": {"provider": "parquet", "options": {}},
+                                         "schemaString": schema.json(), "partitionColumns": partition_by,
+                                         "configuration": {}, "createdTime": ts}})
+        if mode == "overwrite" and snap is not None:
+            for p in snap.files:
+                actions.append({"remove": {"path": p, "deletionTimestamp": ts, "dataChange": True}})
+        for w in allw:
+            for fp in w:
+                rel = os.path.relpath(fp, path)
+                pv = {}
+                for part in os.path.dirname(rel).split(os.sep):
+                    if "=" in part:
+                        k, v = part.split("=", 1)
+                        pv[k] = v
+                actions.append({"add": {"path": rel, "partitionValues": pv, "size": os.path.getsize(fp),
+                                        "modificationTime": ts, "dataChange": True}})
+        _write_commit(path, version, actions)
+    comm.barrier()
+
+
+def history(path) -> List[dict]:
+    out = []
+    for v in reversed(_versions(path)):
+        ci = next((a["commitInfo"] for a in _read_commit(path, v) if "commitInfo" in a), {})
+        out.append({"version": v, "timestamp": _dt.datetime.fromtimestamp(ci.get("timestamp", 0) / 1000),
+                    "operation": ci.get("operation", "WRITE"),
+                    "operationParameters": json.dumps(ci.get("operationParameters", {})),
+                    "readVersion": ci.get("readVersion"), "isBlindAppend": ci.get("isBlindAppend"),
+                    "operationMetrics": json.dumps(ci.get("operationMetrics", {}))})
+    return out
+
+
+class DeltaTable:
+    """``delta.tables.DeltaTable`` subset used by the course."""
+
+    def __init__(self, session, path):
+        self._session = session
+        self._path = path
+
+    @classmethod
+    def forPath(cls, session, path):
+        from ..sql.readwriter import _strip_dbfs
+        path = _strip_dbfs(path)
+        if not is_delta_table(path):
+            raise DeltaError(f"`{path}` is not a Delta table.")
+        return cls(session, path)
+
+    @classmethod
+    def forName(cls, session, name):
+        info = session.catalog._table_info(name)
+        return cls(session, info["location"])
+
+    @classmethod
+    def isDeltaTable(cls, session, path):
+        return is_delta_table(path)
+
+    def toDF(self) -> DataFrame:
+        return read_delta(self._session, self._path)
+
+    def history(self, limit=None) -> DataFrame:
+        h = history(self._path)
+        if limit:
+            h = h[:limit]
+        return self._session.createDataFrame(pd.DataFrame(h))
+
+    def vacuum(self, retentionHours: float = 168.0):
+        conf = self._session.conf
+        check = conf.get("spark.databricks.delta.retentionDurationCheck.enabled", "true") == "true"
+        if check and retentionHours < 168:
+            raise DeltaError(
+                "requirement failed: Are you sure you would like to vacuum files with such a low retention period? "
+                "If you have writers that are currently writing to this table, there is a risk that you may "
+                "corrupt the state of your Delta table. If you are certain that there are no operations being "
+                "performed on this table, such as insert/upsert/delete/optimize, then you may turn off this check "
+                "by setting: spark.databricks.delta.retentionDurationCheck.enabled = false")
+        comm = self._session.comm
+        if comm.rank == 0:
+            vs = _versions(self._path)
+            live = set(Snapshot(self._path, vs[-1]).files)
+            cutoff = _now_ms() - retentionHours * 3600 * 1000
+            for root, dirs, files in os.walk(self._path):
+                if LOG in root.split(os.sep):
+                    continue
+                for f in files:
+                    if f.startswith(("_", ".")):
+                        continue
+                    full = os.path.join(root, f)
+                    rel = os.path.relpath(full, self._path)
+                    if rel not in live and os.path.getmtime(full) * 1000 <= cutoff + 1:
+                        os.remove(full)
+        comm.barrier()
+        return self._session.createDataFrame(pd.DataFrame({"path": [self._path]}))
+
+    def delete(self, condition=None):
+        from ..sql.column import Column
+        df = self.toDF()
+        if condition is not None:
+            from ..sql.parser import parse_expression
+            cond = parse_expression(condition) if isinstance(condition, str) else condition
+            keep = df.filter(~cond | cond.isNull())
+        else:
+            keep = df.limit(0)
+        keep = keep.cache()
+        keep.count()
+        write_delta(keep, self._path, "overwrite", {}, [], operation="DELETE")
