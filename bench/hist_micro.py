@@ -1,0 +1,103 @@
+"""Histogram-kernel microbenchmark: one tree level of an RF, timed per variant.
+
+    python bench/hist_micro.py --rows 1e7 [--variants all]
+
+Builds binned synthetic data, a level state (node ids / bootstrap weights /
+feature masks for T trees with L active nodes each) and times the histogram
+kernel alone with HIP events, reporting ms and lane-updates/s.
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cdnaml.ops import kernels as K  # noqa: E402
+
+
+def make_state(n, d, T, L, B, masked, seed=0, dev="cuda"):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    X = torch.randn((n, d), generator=g, device=dev)
+    thr = torch.linspace(-2, 2, B - 1, device=dev)[None, :].expand(d, -1).contiguous()
+    nthr = torch.full((d,), B - 1, dtype=torch.int32, device=dev)
+    bins = K.binize(X, thr, nthr)
+    del X
+    # active ids: tree-major, L per tree; rows spread uniformly over a tree's nodes
+    node = (torch.randint(0, L, (T, n), generator=g, device=dev, dtype=torch.int32) +
+            (torch.arange(T, device=dev, dtype=torch.int32) * L)[:, None]).contiguous()
+    A = T * L
+    build = torch.arange(A, dtype=torch.int32, device=dev)
+    slot_tree = np.repeat(np.arange(T), L).astype(np.int32)
+    id_tree = slot_tree.copy()
+    w = K.poisson_weights(T, n, 1, 0, 1.0, device=dev)
+    fm = None
+    if masked:
+        rng = np.random.default_rng(0)
+        words = np.zeros((A, (d + 31) // 32), dtype=np.uint32)
+        k = int(np.ceil(d / 3))
+        for a in range(A):
+            for f in rng.choice(d, k, replace=False):
+                words[a, f >> 5] |= np.uint32(1) << np.uint32(f & 31)
+        fm = torch.from_numpy(words.view(np.int32)).to(dev)
+    y = torch.randn(n, generator=g, device=dev)
+    return bins, node, w, y, build, slot_tree, id_tree, fm
+
+
+def timeit(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return min(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=float, default=1e7)
+    ap.add_argument("--d", type=int, default=100)
+    ap.add_argument("--B", type=int, default=40)
+    ap.add_argument("--variants", default="all")
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    n, d, B = int(args.rows), args.d, args.B
+    configs = [
+        # (name, T, L, masked, weights, version, lds)
+        ("L0 T20 masked w v3", 20, 1, True, True, 3, 65536),
+        ("L0 T20 full   w v3", 20, 1, False, True, 3, 65536),
+        ("L4 T20 masked w v3", 20, 16, True, True, 3, 65536),
+        ("L4 T20 masked w v3 128K", 20, 16, True, True, 3, 131072),
+        ("L4 T20 full   w v3", 20, 16, False, True, 3, 65536),
+        ("L0 T20 masked w v2", 20, 1, True, True, 2, 65536),
+        ("L0 T20 full   w v2", 20, 1, False, True, 2, 65536),
+        ("L0 T20 full  nw v2", 20, 1, False, False, 2, 65536),
+        ("L0 T1  full  nw v2", 1, 1, False, False, 2, 65536),
+        ("L4 T20 masked w v2", 20, 16, True, True, 2, 65536),
+        ("L4 T20 masked w v2 128K", 20, 16, True, True, 2, 131072),
+        ("L4 T20 full   w v2", 20, 16, False, True, 2, 65536),
+    ]
+    for name, T, L, masked, wts, ver, lds in configs:
+        bins, node, w, y, build, st, it, fm = make_state(n, d, T, L, B, masked)
+        K.HIST_VERSION = ver
+        fn = lambda: K.hist_moments(bins, d, node, w if wts else None, None, y, build, st, fm, B,  # noqa: E731
+                                    lds_budget=lds, id_tree=it if ver >= 2 else None)
+        ms = timeit(fn, args.reps)
+        frac_w = float((w > 0).float().mean()) if wts else 1.0
+        feats = int(np.ceil(d / 3)) if masked else d
+        upd = n * T * frac_w * feats
+        print(f"{name:28s} {ms:9.2f} ms  {upd / ms * 1e3:9.3e} upd/s  ({upd:.2e} row-tree-feature updates)",
+              flush=True)
+        del bins, node, w, y
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -27,7 +27,7 @@ class Estimator(Params, MLWritable, MLReadable):
         if isinstance(params, (list, tuple)):
             return [self.fit(dataset, p) for p in params]
         est = self.copy(params) if params else self
-        from ..tracking import autolog as _al
+        from ..tracking import autologging as _al
         return _al.wrap_fit(est, dataset)
 
     def fitMultiple(self, dataset, paramMaps):

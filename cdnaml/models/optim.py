@@ -1,0 +1,103 @@
+"""Host-side quasi-Newton optimisers (L-BFGS and OWL-QN) driving device loss/grad passes.
+
+Each objective evaluation is one fused device pass (e.g. the K11
+logistic loss/grad kernel) + one RCCL all-reduce of d+2 doubles; the
+optimiser state (d-sized) lives on the host in float64 — the same split
+as MLlib's driver-side Breeze optimiser (MLE 03 - Logistic Regression
+Lab.py:99-158 uses elasticNetParam in {0, 0.5, 1}, so L1 needs OWL-QN).
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Tuple
+
+import numpy as np
+
+
+def minimize(fg: Callable[[np.ndarray], Tuple[float, np.ndarray]], x0: np.ndarray, max_iter: int = 100,
+             tol: float = 1e-6, m: int = 10, l1: Optional[np.ndarray] = None) -> Tuple[np.ndarray, List[float], int]:
+    """Minimise f(x) (+ sum l1_i |x_i| if l1 given, via OWL-QN). Returns (x, history, iters)."""
+    x = np.array(x0, dtype=np.float64)
+    owl = l1 is not None and np.any(l1 > 0)
+    l1 = np.zeros_like(x) if l1 is None else np.asarray(l1, dtype=np.float64)
+
+    def full(xv):
+        f, g = fg(xv)
+        if owl:
+            f = f + float(np.sum(l1 * np.abs(xv)))
+        return f, g
+
+    def pseudo_grad(xv, g):
+        if not owl:
+            return g
+        pg = g.copy()
+        pos = xv > 0
+        neg = xv < 0
+        zero = ~(pos | neg)
+        pg[pos] += l1[pos]
+        pg[neg] -= l1[neg]
+        gp = g[zero] + l1[zero]
+        gm = g[zero] - l1[zero]
+        pz = np.zeros(zero.sum())
+        pz[gm > 0] = gm[gm > 0]
+        pz[gp < 0] = gp[gp < 0]
+        pg[zero] = pz
+        return pg
+
+    f, g = full(x)
+    hist = [f]
+    S: List[np.ndarray] = []
+    Y: List[np.ndarray] = []
+    it = 0
+    for it in range(1, max_iter + 1):
+        pg = pseudo_grad(x, g)
+        if np.linalg.norm(pg) <= 1e-12 * max(1.0, np.linalg.norm(x)):
+            break
+        # two-loop recursion
+        q = pg.copy()
+        alphas = []
+        for s, y in reversed(list(zip(S, Y))):
+            rho = 1.0 / max(y @ s, 1e-300)
+            a = rho * (s @ q)
+            alphas.append(a)
+            q -= a * y
+        if S:
+            gamma = (S[-1] @ Y[-1]) / max(Y[-1] @ Y[-1], 1e-300)
+            q *= gamma
+        for (s, y), a in zip(zip(S, Y), reversed(alphas)):
+            rho = 1.0 / max(y @ s, 1e-300)
+            b = rho * (y @ q)
+            q += (a - b) * s
+        d = -q
+        if owl:
+            d = np.where(d * pg < 0, d, 0.0)  # keep descent direction consistent with pseudo-gradient
+            orthant = np.where(x != 0, np.sign(x), -np.sign(pg))
+        if d @ pg >= 0:
+            d = -pg
+            S.clear()
+            Y.clear()
+        step = 1.0 if S else min(1.0, 1.0 / max(np.linalg.norm(pg), 1e-12))
+        ok = False
+        for _ in range(40):
+            xn = x + step * d
+            if owl:
+                xn = np.where(np.sign(xn) == orthant, xn, 0.0)
+            fn, gn = full(xn)
+            if fn <= f + 1e-4 * (pg @ (xn - x)):
+                ok = True
+                break
+            step *= 0.5
+        if not ok:
+            break
+        s_, y_ = xn - x, gn - g
+        if s_ @ y_ > 1e-12:
+            S.append(s_)
+            Y.append(y_)
+            if len(S) > m:
+                S.pop(0)
+                Y.pop(0)
+        rel = abs(f - fn) / max(abs(fn), abs(f), 1e-12)
+        x, f, g = xn, fn, gn
+        hist.append(f)
+        if rel < tol:
+            break
+    return x, hist, it

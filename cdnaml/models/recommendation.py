@@ -1,0 +1,240 @@
+"""Alternating least squares.
+
+Ratings are row-sharded across ranks; user/item factor tables (small) are
+replicated.  Each half-iteration every rank accumulates, for the ratings it
+holds, the per-entity normal equations Σ v vᵀ and Σ r v with one batched
+outer-product scatter on device; the partial systems are summed with one
+RCCL all-reduce and solved as a BATCH on the GPU — Cholesky for the default
+path, batched coordinate-descent NNLS when ``nonnegative=True``
+(MLE 01 - Collaborative Filtering Lab.py:136-202).  Regularisation follows
+MLlib's ALS-WR scaling (λ · n_u).  ``coldStartStrategy="drop"`` removes
+rows with unknown users/items from ``transform`` output.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..sql import types as T
+from ..sql.batch import ColumnData
+from ..sql.dataframe import MapPlan
+from .base import Estimator, Model
+from .param import NO_DEFAULT, TypeConverters as TC, keyword_init
+from .regression import _default_seed
+from .util import local_batch
+
+
+class ALS(Estimator):
+    _params = {
+        "rank": ("rank of the factorization", 10, TC.toInt),
+        "maxIter": ("max number of iterations (>= 0)", 10, TC.toInt),
+        "regParam": ("regularization parameter (>= 0)", 0.1, TC.toFloat),
+        "numUserBlocks": ("number of user blocks", 10, TC.toInt),
+        "numItemBlocks": ("number of item blocks", 10, TC.toInt),
+        "implicitPrefs": ("whether to use implicit preference", False, TC.toBoolean),
+        "alpha": ("alpha for implicit preference", 1.0, TC.toFloat),
+        "userCol": ("column name for user ids. Ids must be within the integer value range.", "user", TC.toString),
+        "itemCol": ("column name for item ids. Ids must be within the integer value range.", "item", TC.toString),
+        "ratingCol": ("column name for ratings", "rating", TC.toString),
+        "predictionCol": ("prediction column name", "prediction", TC.toString),
+        "nonnegative": ("whether to use nonnegative constraint for least squares", False, TC.toBoolean),
+        "checkpointInterval": ("checkpoint interval", 10, TC.toInt),
+        "seed": ("random seed", None, TC.toInt),
+        "intermediateStorageLevel": ("storage level for intermediate datasets", "MEMORY_AND_DISK", TC.toString),
+        "finalStorageLevel": ("storage level for ALS model factors", "MEMORY_AND_DISK", TC.toString),
+        "coldStartStrategy": ("strategy for dealing with unknown or new users/items at prediction time: nan, drop",
+                              "nan", TC.toString),
+        "blockSize": ("block size for stacking input data in matrices", 4096, TC.toInt),
+    }
+
+    def __init__(self, **kwargs):
+        super().__init__()
+        keyword_init(self, kwargs)
+
+    @staticmethod
+    def _solve(A: torch.Tensor, b: torch.Tensor, nonneg: bool) -> torch.Tensor:
+        """Batched SPD solve [E, r, r] x = [E, r] on device."""
+        if not nonneg:
+            L, info = torch.linalg.cholesky_ex(A)
+            x = torch.cholesky_solve(b.unsqueeze(-1), L).squeeze(-1)
+            bad = info != 0
+            if bool(bad.any()):
+                x[bad] = torch.linalg.lstsq(A[bad], b[bad].unsqueeze(-1)).solution.squeeze(-1)
+            return x
+        # batched coordinate-descent NNLS (exact per-coordinate minimisation)
+        E, r = b.shape
+        x = torch.zeros_like(b)
+        diag = torch.diagonal(A, dim1=1, dim2=2).clamp_min(1e-12)
+        for _ in range(40):
+            for j in range(r):
+                g = b[:, j] - (A[:, j, :] * x).sum(1) + A[:, j, j] * x[:, j]
+                x[:, j] = torch.clamp(g / diag[:, j], min=0.0)
+        return x
+
+    def _half_step(self, comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha):
+        rank = F_src.shape[1]
+        dev = F_src.device
+        A = torch.zeros((n_dst, rank, rank), dtype=torch.float64, device=dev)
+        bvec = torch.zeros((n_dst, rank), dtype=torch.float64, device=dev)
+        cnt = torch.zeros(n_dst, dtype=torch.float64, device=dev)
+        chunk = 1 << 20
+        for a in range(0, src_idx.numel(), chunk):
+            s, d_, rr = src_idx[a:a + chunk], dst_idx[a:a + chunk], r[a:a + chunk]
+            V = F_src[s]
+            if implicit:
+                c = 1.0 + alpha * rr.abs()
+                p = (rr > 0).double()
+                A.index_add_(0, d_, (c - 1.0)[:, None, None] * V[:, :, None] * V[:, None, :])
+                bvec.index_add_(0, d_, (c * p)[:, None] * V)
+            else:
+                A.index_add_(0, d_, V[:, :, None] * V[:, None, :])
+                bvec.index_add_(0, d_, rr[:, None] * V)
+            cnt.index_add_(0, d_, torch.ones_like(rr))
+        comm.all_reduce_many([A.view(-1), bvec.view(-1), cnt])
+        eye = torch.eye(rank, dtype=torch.float64, device=dev)
+        if implicit:
+            YtY = F_src.T @ F_src
+            A = A + YtY[None]
+            A = A + lam * cnt.clamp_min(1)[:, None, None] * eye
+        else:
+            A = A + (lam * cnt)[:, None, None] * eye
+        has = cnt > 0
+        out = torch.zeros((n_dst, rank), dtype=torch.float64, device=dev)
+        if bool(has.any()):
+            out[has] = self._solve(A[has], bvec[has], nonneg)
+        return out
+
+    def _fit(self, dataset):
+        uc, ic, rc = self.getUserCol(), self.getItemCol(), self.getRatingCol()
+        session = dataset._session
+        comm = session.comm
+        b = local_batch(dataset, [uc, ic, rc])
+        u = b.columns[uc].values.long()
+        i = b.columns[ic].values.long()
+        r = b.columns[rc].values.double()
+        ok = torch.ones_like(r, dtype=torch.bool)
+        for c in (b.columns[uc], b.columns[ic], b.columns[rc]):
+            if c.valid is not None:
+                ok &= c.valid
+        u, i, r = u[ok], i[ok], r[ok]
+        uid = torch.unique(u)
+        iid = torch.unique(i)
+        if comm.distributed:
+            uid = torch.unique(torch.cat(comm.all_gather_varlen(uid)))
+            iid = torch.unique(torch.cat(comm.all_gather_varlen(iid)))
+        ui = torch.searchsorted(uid, u)
+        ii = torch.searchsorted(iid, i)
+        k = self.getRank()
+        seed = self.getSeed() if self.getSeed() is not None else _default_seed(type(self))
+        g = torch.Generator().manual_seed(int(seed) & 0x7FFFFFFF)
+        # MLlib initialises factors with |N(0,1)| / sqrt(rank)-normalised rows
+        U = torch.randn((uid.numel(), k), generator=g, dtype=torch.float64).abs()
+        V = torch.randn((iid.numel(), k), generator=g, dtype=torch.float64).abs()
+        U = (U / torch.linalg.vector_norm(U, dim=1, keepdim=True)).to(u.device)
+        V = (V / torch.linalg.vector_norm(V, dim=1, keepdim=True)).to(u.device)
+        lam, nonneg = self.getRegParam(), self.getNonnegative()
+        implicit, alpha = self.getImplicitPrefs(), self.getAlpha()
+        for _ in range(self.getMaxIter()):
+            U = self._half_step(comm, ii, ui, r, V, uid.numel(), lam, nonneg, implicit, alpha)
+            V = self._half_step(comm, ui, ii, r, U, iid.numel(), lam, nonneg, implicit, alpha)
+        model = ALSModel(uid.cpu().numpy(), U.float().cpu().numpy(), iid.cpu().numpy(), V.float().cpu().numpy())
+        return model
+
+
+class ALSModel(Model):
+    _params = {k: v for k, v in ALS._params.items() if k != "rank"}  # ALSModel.rank is a property
+
+    def __init__(self, user_ids=None, user_factors=None, item_ids=None, item_factors=None):
+        super().__init__()
+        self._uid = np.asarray(user_ids if user_ids is not None else [], dtype=np.int64)
+        self._U = np.asarray(user_factors if user_factors is not None else np.zeros((0, 0)), dtype=np.float32)
+        self._iid = np.asarray(item_ids if item_ids is not None else [], dtype=np.int64)
+        self._V = np.asarray(item_factors if item_factors is not None else np.zeros((0, 0)), dtype=np.float32)
+
+    @property
+    def rank(self):
+        return int(self._U.shape[1]) if self._U.ndim == 2 else 0
+
+    def _factor_df(self, ids, F):
+        import pandas as pd
+        from ..session import SparkSession
+        s = SparkSession.getActiveSession()
+        return s.createDataFrame(pd.DataFrame({"id": ids.astype(np.int32), "features": [list(map(float, f)) for f in F]}),
+                                 schema="id int, features array<float>")
+
+    @property
+    def userFactors(self):
+        return self._factor_df(self._uid, self._U)
+
+    @property
+    def itemFactors(self):
+        return self._factor_df(self._iid, self._V)
+
+    def _lookup(self, ids: torch.Tensor, table: np.ndarray):
+        t = torch.from_numpy(table).to(ids.device)
+        if t.numel() == 0:
+            return torch.zeros_like(ids), torch.zeros_like(ids, dtype=torch.bool)
+        pos = torch.searchsorted(t, ids).clamp(max=t.numel() - 1)
+        return pos, t[pos] == ids
+
+    def _transform(self, dataset):
+        uc, ic, pc = self.getUserCol(), self.getItemCol(), self.getPredictionCol()
+        drop = self.getColdStartStrategy() == "drop"
+        U, V = torch.from_numpy(self._U), torch.from_numpy(self._V)
+        model = self
+
+        def fn(b, ctx):
+            u = b.columns[uc].values.long()
+            i = b.columns[ic].values.long()
+            pu, oku = model._lookup(u, model._uid)
+            pi, oki = model._lookup(i, model._iid)
+            Ud, Vd = U.to(u.device), V.to(u.device)
+            ok = oku & oki
+            for c in (b.columns[uc], b.columns[ic]):
+                if c.valid is not None:
+                    ok &= c.valid
+            pred = (Ud[pu] * Vd[pi]).sum(1).double() if u.numel() else torch.zeros(0, dtype=torch.float64,
+                                                                                     device=u.device)
+            pred = torch.where(ok, pred, torch.full_like(pred, float("nan")))
+            nb = b.with_column(pc, ColumnData(pred.float(), T.FloatType()))
+            return nb.filter(ok) if drop else nb
+        return dataset._new(MapPlan(dataset._plan, "ALSModel", fn))
+
+    def _recommend(self, src_ids, S, dst_ids, D, k, src_name, dst_name):
+        import pandas as pd
+        from ..session import SparkSession
+        s = SparkSession.getActiveSession()
+        dev = s.device
+        St, Dt = torch.from_numpy(S).to(dev), torch.from_numpy(D).to(dev)
+        scores = St @ Dt.T
+        kk = min(k, Dt.shape[0])
+        top = torch.topk(scores, kk, dim=1)
+        idx, val = top.indices.cpu().numpy(), top.values.cpu().numpy()
+        recs = [[{dst_name: int(dst_ids[j]), "rating": float(v)} for j, v in zip(ri, rv)] for ri, rv in zip(idx, val)]
+        pdf = pd.DataFrame({src_name: src_ids.astype(np.int32), "recommendations": [str(r) for r in recs]})
+        df = s.createDataFrame(pdf)
+        df._recs = recs
+        return df
+
+    def recommendForAllUsers(self, numItems):
+        return self._recommend(self._uid, self._U, self._iid, self._V, numItems, self.getUserCol(),
+                               self.getItemCol())
+
+    def recommendForAllItems(self, numUsers):
+        return self._recommend(self._iid, self._V, self._uid, self._U, numUsers, self.getItemCol(),
+                               self.getUserCol())
+
+    def recommendForUserSubset(self, dataset, numItems):
+        ids = np.array([r[0] for r in dataset.select(self.getUserCol()).distinct().collect()], dtype=np.int64)
+        pos = np.searchsorted(self._uid, ids)
+        ok = (pos < len(self._uid)) & (self._uid[np.minimum(pos, len(self._uid) - 1)] == ids)
+        return self._recommend(ids[ok], self._U[pos[ok]], self._iid, self._V, numItems, self.getUserCol(),
+                               self.getItemCol())
+
+    def _save_state(self):
+        return {}, {"uid": torch.from_numpy(self._uid), "U": torch.from_numpy(self._U),
+                    "iid": torch.from_numpy(self._iid), "V": torch.from_numpy(self._V)}
+
+    def _load_state(self, extra, tensors, stages):
+        self._uid, self._U = tensors["uid"].numpy(), tensors["U"].numpy()
+        self._iid, self._V = tensors["iid"].numpy(), tensors["V"].numpy()

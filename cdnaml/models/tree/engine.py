@@ -35,6 +35,8 @@ import torch
 from ...ops import kernels as K
 from ..util import IllegalArgumentException
 
+HIST_MODE = __import__("os").environ.get("CDNAML_RF_HIST", "masked")
+
 
 @dataclass
 class TreeParams:
@@ -467,7 +469,10 @@ class ForestTrainer:
         n, d, B = data.n_local, data.d, data.B
         T = num_trees
         forest = forest or Forest(self.C if self.classification else 1)
-        masked = p.feature_subset is not None and p.feature_subset < d
+        need_masks = p.feature_subset is not None and p.feature_subset < d
+        # "masked": accumulate only each node's sampled features (fewer atomics, no subtraction);
+        # "full": accumulate all features, derive larger siblings by subtraction, mask at split time.
+        masked = need_masks and HIST_MODE == "masked"
         subtract = not masked
         node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
             torch.zeros((T, 0), dtype=torch.int32, device=dev)
@@ -498,18 +503,19 @@ class ForestTrainer:
             slot_of[build_ids] = np.arange(len(build_ids), dtype=np.int32)
             slot_tree = np.array([active[a]["tree"] for a in build_ids], dtype=np.int32)
             masks_np = None
-            if masked:
+            if need_masks:
                 masks_np = np.stack([self._feature_mask(e["tree"], e["key"]) for e in active])
             fm_build = None
-            if masks_np is not None:
+            if masked:
                 fm_build = torch.from_numpy(masks_np[build_ids].view(np.int32)).to(dev)
             build_slot = torch.from_numpy(slot_of).to(dev)
+            id_tree = np.array([e["tree"] for e in active], dtype=np.int32)
             if self.classification:
                 Hb = K.hist_classes(data.bins, d, node, weights, stats_rows["label"], self.C, build_slot, slot_tree,
-                                    fm_build, B)
+                                    fm_build, B, id_tree=id_tree)
             else:
                 Hb = K.hist_moments(data.bins, d, node, weights, stats_rows.get("v0"), stats_rows["v1"],
-                                    build_slot, slot_tree, fm_build, B)
+                                    build_slot, slot_tree, fm_build, B, id_tree=id_tree)
             self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
             # ---- assemble every active node's histogram
             H = torch.empty((A, d, B, self.stats_k), dtype=torch.float64, device=dev)

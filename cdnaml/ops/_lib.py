@@ -72,6 +72,9 @@ _SIGS = {
     "cdna_hist_classes": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                            c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p], c_int),
+    "cdna_hist2": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                    c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p,
+                    c_void_p], c_int),
     "cdna_partition": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p], c_int),
     "cdna_tree_predict": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_void_p,

@@ -146,9 +146,57 @@ def _plan_chunks(n: int, G: int, ngroups: int, target_blocks: int = 2048) -> int
     return int(max(1, min(per, (n + 4095) // 4096)))
 
 
+HIST_LDS_BUDGET = int(__import__("os").environ.get("CDNAML_HIST_LDS", str(64 * 1024)))
+HIST_VERSION = int(__import__("os").environ.get("CDNAML_HIST_VERSION", "3"))
+
+
+def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_tree, id_tree, feat_mask, B,
+           lds_budget, out):
+    """Launch the v2 histogram kernel (csrc/kernels/hist2.hip)."""
+    S = len(slot_tree)
+    G, n, _ = bins.shape
+    T = node.shape[0]
+    Kst = 2 if mode == 0 else C
+    per_slot = Kst * 8 * B * 4
+    SB = max(1, min(S, lds_budget // per_slot))
+    if per_slot > 150 * 1024:
+        raise ValueError("histogram too large for LDS (classes x bins)")
+    slot_tree = np.asarray(slot_tree)
+    id_tree = np.asarray(id_tree)
+    rows = []
+    for a in range(0, S, SB):
+        b = min(S, a + SB)
+        t0, t1 = int(slot_tree[a]), int(slot_tree[b - 1])
+        i0 = int(np.searchsorted(id_tree, t0, side="left"))
+        i1 = int(np.searchsorted(id_tree, t1, side="right"))
+        rows.append((a, t0, t1, i0, i1))
+    grp = torch.tensor(rows, dtype=torch.int32, device=bins.device).reshape(-1)
+    ng = len(rows)
+    span = max(r[4] - r[3] for r in rows)
+    lds_left = 150 * 1024 - ((SB * per_slot + 15) // 16) * 16 - SB - 16
+    id_span_max = int(min(span, max(0, lds_left // 4), 16384))
+    # 2 x 512-thread blocks per CU when LDS allows; enough chunks to fill 256 CUs
+    target = 1024
+    nchunk = int(max(1, min((target + G * ng - 1) // (G * ng), (n + 8191) // 8192)))
+    mw = 0 if feat_mask is None else feat_mask.shape[1]
+    fm = None if feat_mask is None else feat_mask.int().contiguous()
+    node = node.int().contiguous()
+    weight = None if weight is None else weight.to(torch.uint8).contiguous()
+    v0 = None if v0 is None else v0.float().contiguous()
+    v1 = None if v1 is None else v1.float().contiguous()
+    label = None if label is None else label.int().contiguous()
+    build_slot = build_slot.int().contiguous()
+    kmode = mode | (2 if HIST_VERSION >= 3 else 0)
+    _lib.check(_lib.lib().cdna_hist2(kmode, _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0), _ptr(v1),
+                                     _ptr(label), int(C), _ptr(build_slot), _ptr(fm), mw, S, B, SB, _ptr(grp), ng,
+                                     nchunk, id_span_max, _ptr(out), _stream(bins.device)), "cdna_hist2")
+    return out
+
+
 def hist_moments(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optional[torch.Tensor],
                  v0: Optional[torch.Tensor], v1: torch.Tensor, build_slot: torch.Tensor, slot_tree: np.ndarray,
-                 feat_mask: Optional[torch.Tensor], B: int, lds_budget: int = 64 * 1024) -> torch.Tensor:
+                 feat_mask: Optional[torch.Tensor], B: int, lds_budget: Optional[int] = None,
+                 id_tree: Optional[np.ndarray] = None) -> torch.Tensor:
     """Per-slot (feature, bin) weighted moments: out[S, d, B, 2] (float64).
 
     out[s, f, b, 0] = sum w_t(r) * v0(r), out[s, f, b, 1] = sum w_t(r) * v1(r) over
@@ -161,7 +209,11 @@ def hist_moments(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optiona
     out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
     if S == 0 or n == 0:
         return out
+    if _native(bins) and id_tree is not None and HIST_VERSION >= 2:
+        return _hist2(0, bins, d, node, weight, v0, v1, None, 0, build_slot, slot_tree, id_tree, feat_mask, B,
+                      lds_budget or HIST_LDS_BUDGET, out)
     if _native(bins):
+        lds_budget = lds_budget or 64 * 1024
         SB = max(1, min(S, lds_budget // (8 * B * 2 * 4)))
         s0, t0, t1 = _slot_groups(np.asarray(slot_tree), SB)
         ng = len(s0)
@@ -210,7 +262,8 @@ def hist_moments(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optiona
 
 def hist_classes(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optional[torch.Tensor],
                  label: torch.Tensor, C: int, build_slot: torch.Tensor, slot_tree: np.ndarray,
-                 feat_mask: Optional[torch.Tensor], B: int, lds_budget: int = 64 * 1024) -> torch.Tensor:
+                 feat_mask: Optional[torch.Tensor], B: int, lds_budget: Optional[int] = None,
+                 id_tree: Optional[np.ndarray] = None) -> torch.Tensor:
     """Per-slot (feature, bin) weighted class counts: out[S, d, B, C] (float64)."""
     S = len(slot_tree)
     G, n, _ = bins.shape
@@ -218,7 +271,11 @@ def hist_classes(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optiona
     out = torch.zeros((S, d, B, C), dtype=torch.float64, device=bins.device)
     if S == 0 or n == 0:
         return out
+    if _native(bins) and id_tree is not None and HIST_VERSION >= 2:
+        return _hist2(1, bins, d, node, weight, None, None, label, C, build_slot, slot_tree, id_tree, feat_mask, B,
+                      lds_budget or HIST_LDS_BUDGET, out)
     if _native(bins):
+        lds_budget = lds_budget or 64 * 1024
         SB = max(1, min(S, lds_budget // (8 * B * C * 4)))
         if 8 * B * C * 4 > 160 * 1024:
             raise ValueError("too many classes x bins for the LDS histogram")

@@ -102,7 +102,8 @@ def _tree_state(n, T, A, seed):
 
 
 @pytest.mark.parametrize("B", [40, 256])
-def test_hist_moments(dev, B):
+@pytest.mark.parametrize("ver", [1, 2, 3])
+def test_hist_moments(dev, B, ver):
     n, d, T, A = 20000, 19, 3, 12
     g = torch.Generator().manual_seed(B)
     X = torch.randn(n, d, generator=g)
@@ -114,13 +115,16 @@ def test_hist_moments(dev, B):
     y = torch.randn(n, generator=g)
     mw = (d + 31) // 32
     fm = torch.randint(0, 2 ** 31 - 1, (S, mw), generator=g, dtype=torch.int64).to(torch.int32)
+    id_tree = np.arange(A) // (A // T) if ver >= 2 else None
+    K.HIST_VERSION = max(ver, 2)
     ref = K.hist_moments(bins, d, node, w, None, y, build, slot_tree, fm, B)
     out = K.hist_moments(bins.to(dev), d, node.to(dev), w.to(dev), None, y.to(dev), build.to(dev), slot_tree,
-                         fm.to(dev), B, lds_budget=8 * 1024).cpu()
+                         fm.to(dev), B, lds_budget=8 * 1024, id_tree=id_tree).cpu()
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-4)
 
 
-def test_hist_classes(dev):
+@pytest.mark.parametrize("ver", [1, 2, 3])
+def test_hist_classes(dev, ver):
     n, d, T, A, C, B = 10000, 10, 2, 8, 3, 32
     g = torch.Generator().manual_seed(11)
     X = torch.randn(n, d, generator=g)
@@ -130,8 +134,10 @@ def test_hist_classes(dev):
     w = K.poisson_weights(T, n, 5, 0, 1.0)
     lab = torch.randint(0, C, (n,), generator=g, dtype=torch.int32)
     ref = K.hist_classes(bins, d, node, w, lab, C, build, slot_tree, None, B)
+    id_tree = np.arange(A) // (A // T) if ver >= 2 else None
+    K.HIST_VERSION = max(ver, 2)
     out = K.hist_classes(bins.to(dev), d, node.to(dev), w.to(dev), lab.to(dev), C, build.to(dev), slot_tree, None,
-                         B).cpu()
+                         B, id_tree=id_tree).cpu()
     assert torch.allclose(out, ref)
 
 
