@@ -70,23 +70,25 @@ def main():
     args = ap.parse_args()
     n, d, B = int(args.rows), args.d, args.B
     configs = [
-        # (name, T, L, masked, weights, version, lds)
-        ("L0 T20 masked w v3", 20, 1, True, True, 3, 65536),
-        ("L0 T20 full   w v3", 20, 1, False, True, 3, 65536),
-        ("L4 T20 masked w v3", 20, 16, True, True, 3, 65536),
-        ("L4 T20 masked w v3 128K", 20, 16, True, True, 3, 131072),
-        ("L4 T20 full   w v3", 20, 16, False, True, 3, 65536),
-        ("L0 T20 masked w v2", 20, 1, True, True, 2, 65536),
-        ("L0 T20 full   w v2", 20, 1, False, True, 2, 65536),
-        ("L0 T20 full  nw v2", 20, 1, False, False, 2, 65536),
-        ("L0 T1  full  nw v2", 1, 1, False, False, 2, 65536),
-        ("L4 T20 masked w v2", 20, 16, True, True, 2, 65536),
-        ("L4 T20 masked w v2 128K", 20, 16, True, True, 2, 131072),
-        ("L4 T20 full   w v2", 20, 16, False, True, 2, 65536),
+        # (name, T, L, masked, weights, version, lane map, lds bytes)
+        ("L0 T20 masked w v4", 20, 1, True, True, 4, 2, 65536),
+        ("L0 T20 masked w v4 m3", 20, 1, True, True, 4, 3, 65536),
+        ("L0 T20 full   w v4", 20, 1, False, True, 4, 2, 65536),
+        ("L0 T20 full   w v4 m3", 20, 1, False, True, 4, 3, 65536),
+        ("L4 T20 masked w v4", 20, 16, True, True, 4, 2, 65536),
+        ("L4 T20 masked w v4 m3", 20, 16, True, True, 4, 3, 65536),
+        ("L4 T20 masked w v4 40K", 20, 16, True, True, 4, 2, 40960),
+        ("L4 T20 masked w v4 128K", 20, 16, True, True, 4, 2, 131072),
+        ("L4 T20 full   w v4", 20, 16, False, True, 4, 2, 65536),
+        ("L0 T20 masked w v2", 20, 1, True, True, 2, 2, 65536),
+        ("L4 T20 masked w v2", 20, 16, True, True, 2, 2, 65536),
     ]
-    for name, T, L, masked, wts, ver, lds in configs:
+    if args.variants != "all":
+        configs = [c for c in configs if any(v in c[0] for v in args.variants.split(","))]
+    for name, T, L, masked, wts, ver, lmap, lds in configs:
         bins, node, w, y, build, st, it, fm = make_state(n, d, T, L, B, masked)
         K.HIST_VERSION = ver
+        K.HIST_MAP = lmap
         fn = lambda: K.hist_moments(bins, d, node, w if wts else None, None, y, build, st, fm, B,  # noqa: E731
                                     lds_budget=lds, id_tree=it if ver >= 2 else None)
         ms = timeit(fn, args.reps)

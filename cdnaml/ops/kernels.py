@@ -147,17 +147,36 @@ def _plan_chunks(n: int, G: int, ngroups: int, target_blocks: int = 2048) -> int
 
 
 HIST_LDS_BUDGET = int(__import__("os").environ.get("CDNAML_HIST_LDS", str(64 * 1024)))
-HIST_VERSION = int(__import__("os").environ.get("CDNAML_HIST_VERSION", "3"))
+HIST_VERSION = int(__import__("os").environ.get("CDNAML_HIST_VERSION", "4"))
+HIST_MAP = int(__import__("os").environ.get("CDNAML_HIST_MAP", "2"))  # 2: lane = row; 3: lane = 8*row + feature
+
+
+def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int) -> float:
+    """Power-of-two fixed-point scale so that sum_r w_r * |round(v_r * s)| < 2^62 over n rows."""
+    if v is None or v.numel() == 0:
+        return 1.0
+    m = float(v.abs().max().item())
+    if not math.isfinite(m):
+        raise ValueError("histogram statistic contains NaN/Inf")
+    if m == 0.0:
+        return 1.0
+    e = 62 - math.ceil(math.log2(max(1, n) * max(1, wmax) * m)) - 1
+    return float(2.0 ** max(-120, min(100, e)))
 
 
 def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_tree, id_tree, feat_mask, B,
            lds_budget, out):
-    """Launch the v2 histogram kernel (csrc/kernels/hist2.hip)."""
+    """Launch the LDS histogram kernel: v4 integer (hist4.hip, default) or v2/v3 float (hist2.hip)."""
     S = len(slot_tree)
     G, n, _ = bins.shape
     T = node.shape[0]
     Kst = 2 if mode == 0 else C
-    per_slot = Kst * 8 * B * 4
+    v4 = HIST_VERSION >= 4
+    if v4:
+        kbits = mode | (4 if (mode == 0 and v0 is not None) else 0)
+        per_slot = 8 * B * int(_lib.lib().cdna_hist4_bytes_per_bin(kbits, int(C)))
+    else:
+        per_slot = Kst * 8 * B * 4
     SB = max(1, min(S, lds_budget // per_slot))
     if per_slot > 150 * 1024:
         raise ValueError("histogram too large for LDS (classes x bins)")
@@ -178,6 +197,7 @@ def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_
     # 2 x 512-thread blocks per CU when LDS allows; enough chunks to fill 256 CUs
     target = 1024
     nchunk = int(max(1, min((target + G * ng - 1) // (G * ng), (n + 8191) // 8192)))
+    nchunk = max(nchunk, -(-n // (1 << 23)))  # u32 LDS counts: rows/chunk * 255 < 2^32
     mw = 0 if feat_mask is None else feat_mask.shape[1]
     fm = None if feat_mask is None else feat_mask.int().contiguous()
     node = node.int().contiguous()
@@ -186,10 +206,26 @@ def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_
     v1 = None if v1 is None else v1.float().contiguous()
     label = None if label is None else label.int().contiguous()
     build_slot = build_slot.int().contiguous()
-    kmode = mode | (2 if HIST_VERSION >= 3 else 0)
-    _lib.check(_lib.lib().cdna_hist2(kmode, _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0), _ptr(v1),
-                                     _ptr(label), int(C), _ptr(build_slot), _ptr(fm), mw, S, B, SB, _ptr(grp), ng,
-                                     nchunk, id_span_max, _ptr(out), _stream(bins.device)), "cdna_hist2")
+    vmode = 2 if HIST_VERSION == 3 or HIST_MAP == 3 else 0
+    if not v4:
+        _lib.check(_lib.lib().cdna_hist2(mode | vmode, _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0),
+                                         _ptr(v1), _ptr(label), int(C), _ptr(build_slot), _ptr(fm), mw, S, B, SB,
+                                         _ptr(grp), ng, nchunk, id_span_max, _ptr(out), _stream(bins.device)),
+                   "cdna_hist2")
+        return out
+    wmax = 255 if weight is not None else 1
+    qs0 = _fixed_scale(v0, n, wmax)
+    qs1 = _fixed_scale(v1, n, wmax)
+    iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
+    _lib.check(_lib.lib().cdna_hist4(kbits | vmode, _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0),
+                                     _ptr(v1), _ptr(label), int(C), _ptr(build_slot), _ptr(fm), mw, S, B, SB,
+                                     _ptr(grp), ng, nchunk, id_span_max, qs0, qs1, _ptr(iout),
+                                     _stream(bins.device)), "cdna_hist4")
+    out.copy_(iout)
+    if mode == 0:
+        if v0 is not None:
+            out[..., 0] /= qs0
+        out[..., 1] /= qs1
     return out
 
 

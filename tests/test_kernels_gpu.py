@@ -101,9 +101,15 @@ def _tree_state(n, T, A, seed):
     return node, build, np.array(slot_tree, np.int32)
 
 
+def _set_hist_version(monkeypatch, ver):
+    """ver: 1..4 kernel generation; 43 = v4 integer kernel with the v3 lane mapping."""
+    monkeypatch.setattr(K, "HIST_VERSION", 4 if ver == 43 else max(ver, 2))
+    monkeypatch.setattr(K, "HIST_MAP", 3 if ver == 43 else 2)
+
+
 @pytest.mark.parametrize("B", [40, 256])
-@pytest.mark.parametrize("ver", [1, 2, 3])
-def test_hist_moments(dev, B, ver):
+@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43])
+def test_hist_moments(dev, B, ver, monkeypatch):
     n, d, T, A = 20000, 19, 3, 12
     g = torch.Generator().manual_seed(B)
     X = torch.randn(n, d, generator=g)
@@ -116,15 +122,15 @@ def test_hist_moments(dev, B, ver):
     mw = (d + 31) // 32
     fm = torch.randint(0, 2 ** 31 - 1, (S, mw), generator=g, dtype=torch.int64).to(torch.int32)
     id_tree = np.arange(A) // (A // T) if ver >= 2 else None
-    K.HIST_VERSION = max(ver, 2)
+    _set_hist_version(monkeypatch, ver)
     ref = K.hist_moments(bins, d, node, w, None, y, build, slot_tree, fm, B)
     out = K.hist_moments(bins.to(dev), d, node.to(dev), w.to(dev), None, y.to(dev), build.to(dev), slot_tree,
                          fm.to(dev), B, lds_budget=8 * 1024, id_tree=id_tree).cpu()
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("ver", [1, 2, 3])
-def test_hist_classes(dev, ver):
+@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43])
+def test_hist_classes(dev, ver, monkeypatch):
     n, d, T, A, C, B = 10000, 10, 2, 8, 3, 32
     g = torch.Generator().manual_seed(11)
     X = torch.randn(n, d, generator=g)
@@ -135,10 +141,45 @@ def test_hist_classes(dev, ver):
     lab = torch.randint(0, C, (n,), generator=g, dtype=torch.int32)
     ref = K.hist_classes(bins, d, node, w, lab, C, build, slot_tree, None, B)
     id_tree = np.arange(A) // (A // T) if ver >= 2 else None
-    K.HIST_VERSION = max(ver, 2)
+    _set_hist_version(monkeypatch, ver)
     out = K.hist_classes(bins.to(dev), d, node.to(dev), w.to(dev), lab.to(dev), C, build.to(dev), slot_tree, None,
                          B, id_tree=id_tree).cpu()
     assert torch.allclose(out, ref)
+
+
+@pytest.mark.parametrize("ver", [2, 4])
+def test_hist_moments_v0(dev, ver, monkeypatch):
+    """Moments with a real-valued v0 plane (XGBoost hessians) and no bootstrap weights."""
+    n, d, T, A, B = 30000, 13, 2, 6, 64
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    bins = K.binize(X, thr, nthr)
+    node, build, slot_tree = _tree_state(n, T, A, 6)
+    v0 = torch.rand(n, generator=g) * 0.25
+    v1 = torch.randn(n, generator=g) * 100.0
+    _set_hist_version(monkeypatch, ver)
+    ref = K.hist_moments(bins, d, node, None, v0, v1, build, slot_tree, None, B)
+    out = K.hist_moments(bins.to(dev), d, node.to(dev), None, v0.to(dev), v1.to(dev), build.to(dev), slot_tree,
+                         None, B, id_tree=np.arange(A) // (A // T)).cpu()
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-3)
+
+
+def test_hist_v4_deterministic(dev, monkeypatch):
+    """Integer histograms are bit-identical across launches with different chunkings."""
+    n, d, T, A, B = 50000, 16, 2, 4, 32
+    g = torch.Generator().manual_seed(8)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    bins = K.binize(X, thr, nthr).to(dev)
+    node, build, slot_tree = _tree_state(n, T, A, 2)
+    y = torch.randn(n, generator=g).to(dev)
+    _set_hist_version(monkeypatch, 4)
+    it = np.arange(A) // (A // T)
+    a = K.hist_moments(bins, d, node.to(dev), None, None, y, build.to(dev), slot_tree, None, B, id_tree=it)
+    b = K.hist_moments(bins, d, node.to(dev), None, None, y, build.to(dev), slot_tree, None, B, lds_budget=4096,
+                       id_tree=it)
+    assert torch.equal(a, b)
 
 
 def test_partition(dev):
