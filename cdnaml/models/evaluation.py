@@ -102,7 +102,7 @@ def _auc_from_counts(tp, fp, metric):
             return float("nan")
         tpr = np.r_[0.0, tp / P, 1.0]
         fpr = np.r_[0.0, fp / N, 1.0]
-        return float(np.trapz(tpr, fpr))
+        return float(np.trapezoid(tpr, fpr))
     if metric == "areaUnderPR":
         if P == 0:
             return float("nan")
@@ -110,7 +110,7 @@ def _auc_from_counts(tp, fp, metric):
         prec = tp / np.maximum(tp + fp, 1e-300)
         rec = np.r_[0.0, rec]
         prec = np.r_[prec[0] if len(prec) else 1.0, prec]
-        return float(np.trapz(prec, rec))
+        return float(np.trapezoid(prec, rec))
     raise IllegalArgumentException(f"unsupported metric {metric}")
 
 

@@ -659,6 +659,8 @@ class StandardScalerModel(Model):
 
         def fn(b, ctx):
             X = b.columns[ic].values.float()
+            if X.shape[0] == 0:
+                X = X.new_zeros((0, len(mu)))
             Y = X
             if wm:
                 Y = Y - mu.to(b.device)

@@ -156,7 +156,8 @@ class Comm:
             flat = flat.to(torch.uint8)
         fw = self._dev_tensor(flat)
         out = torch.empty(sum(recv_counts) * inner, dtype=fw.dtype, device=fw.device)
-        dist.all_to_all_single(out, fw, [int(c.shape[0]) * inner for c in chunks], [r * inner for r in recv_counts])
+        dist.all_to_all_single(out, fw, output_split_sizes=[r * inner for r in recv_counts],
+                               input_split_sizes=[int(c.shape[0]) * inner for c in chunks])
         self.calls += 2
         self.bytes_reduced += flat.numel() * flat.element_size()
         out = out.to(ref.device)

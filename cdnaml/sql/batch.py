@@ -64,8 +64,12 @@ class ColumnData:
                           self.dictionary, self.meta)
 
     # ------------------------------------------------------------ host
-    def to_numpy(self):
-        """Host values as a numpy/pandas-friendly array (object for strings/vectors)."""
+    def to_numpy(self, nulls_as_nan: bool = False):
+        """Host values as a numpy/pandas-friendly array (object for strings/vectors).
+
+        ``nulls_as_nan``: numeric nulls become NaN in a float64 array (what Spark's
+        Arrow ``toPandas`` produces); otherwise they are ``None`` in an object array.
+        """
         v = self.values.detach().cpu()
         valid = None if self.valid is None else self.valid.cpu().numpy()
         dt = self.dtype
@@ -104,6 +108,10 @@ class ColumnData:
             return a
         a = v.numpy()
         if valid is not None and not valid.all():
+            if nulls_as_nan and not isinstance(dt, T.BooleanType):
+                a = a.astype(np.float64)
+                a[~valid] = np.nan
+                return a
             if isinstance(dt, (T.FloatType, T.DoubleType)):
                 a = a.astype(np.float64)
                 a[~valid] = np.nan
@@ -234,7 +242,7 @@ class Batch:
     def to_pandas(self) -> pd.DataFrame:
         data = {}
         for k, c in self.columns.items():
-            data[k] = c.to_numpy()
+            data[k] = c.to_numpy(nulls_as_nan=True)
         return pd.DataFrame(data, columns=self.names)
 
 
@@ -449,5 +457,12 @@ def batch_from_pandas(pdf: pd.DataFrame, schema: Optional[T.StructType], device)
 
 def empty_batch(schema: T.StructType, device, widths: Optional[dict] = None) -> Batch:
     widths = widths or {}
-    cols = {f.name: empty_column(f.dataType, device, widths.get(f.name, 0), f.metadata) for f in schema.fields}
+
+    def width(f):
+        if f.name in widths:
+            return widths[f.name]
+        ma = (f.metadata or {}).get("ml_attr") or {}
+        return int(ma.get("num_attrs") or 0)
+
+    cols = {f.name: empty_column(f.dataType, device, width(f), f.metadata) for f in schema.fields}
     return Batch(cols, 0, device)

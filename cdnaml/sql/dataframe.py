@@ -471,9 +471,13 @@ class DataFrame:
         return local
 
     def collect(self) -> List[T.Row]:
-        pdf = self.toPandas()
-        names = list(pdf.columns)
-        cols = [self._py_column(pdf[c]) for c in names]
+        b = self._local_concat()
+        names = list(self.columns)
+        cols = [b.columns[c].to_pylist() for c in names]
+        if self._session.comm.distributed:
+            parts = self._session.comm.all_gather_object(cols)
+            cols = [sum((p[i] for p in parts), []) for i in range(len(names))]
+        cols = [[v.item() if isinstance(v, np.generic) else v for v in c] for c in cols]
         return [T.Row._make(names, vals) for vals in zip(*cols)] if names else []
 
     @staticmethod
@@ -890,16 +894,20 @@ class DataFrame:
                 if s == "count":
                     aggs.append(F.count(c))
                 elif s == "mean":
-                    aggs.append(F.avg(c) if not is_str else F.lit(None))
+                    aggs.append(F.avg(c) if not is_str else None)
                 elif s == "stddev":
-                    aggs.append(F.stddev(c) if not is_str else F.lit(None))
+                    aggs.append(F.stddev(c) if not is_str else None)
                 elif s in ("min", "max"):
                     aggs.append(F.min(c) if s == "min" else F.max(c))
                 elif s.endswith("%"):
-                    aggs.append(F.percentile_approx(c, float(s[:-1]) / 100.0) if not is_str else F.lit(None))
+                    aggs.append(F.percentile_approx(c, float(s[:-1]) / 100.0) if not is_str else None)
                 else:
                     raise ValueError(s)
-            vals = self.agg(*[a.alias(f"_s{i}") for i, a in enumerate(aggs)]).collect()[0]
+            live = [(i, a) for i, a in enumerate(aggs) if a is not None]
+            got = self.agg(*[a.alias(f"_s{i}") for i, a in live]).collect()[0]
+            vals = [None] * len(aggs)
+            for (i, _), v in zip(live, got):
+                vals[i] = v
             for s, v in zip(stats, vals):
                 rows[s].append(None if v is None else (str(int(v)) if s == "count" else _num_str(v)))
         pdf = pd.DataFrame({"summary": stats, **{f.name: [rows[s][i] for s in stats] for i, f in enumerate(fields)}})

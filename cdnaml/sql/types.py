@@ -228,10 +228,17 @@ class StructType(DataType):
     def __repr__(self):
         return "StructType([" + ", ".join(repr(f) for f in self.fields) + "])"
 
-    def json(self):
-        return json.dumps({"type": "struct", "fields": [
+    def jsonValue(self):
+        return {"type": "struct", "fields": [
             {"name": f.name, "type": f.dataType.simpleString(), "nullable": f.nullable, "metadata": f.metadata}
-            for f in self.fields]})
+            for f in self.fields]}
+
+    def json(self):
+        return json.dumps(self.jsonValue())
+
+    @classmethod
+    def fromDDL(cls, ddl: str) -> "StructType":
+        return _parse_datatype_string(ddl)
 
     @staticmethod
     def fromJson(s):

@@ -1,0 +1,160 @@
+"""CPU reference paths of the kernel library + property tests.
+
+The HIP kernels are checked against these same references on the GPU in
+tests/test_kernels_gpu.py; here the references themselves are pinned against
+brute-force numpy loops, and the framework-level invariants are property-tested.
+"""
+import numpy as np
+import pytest
+import torch
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from cdnaml.ops import kernels as K
+from cdnaml.ops import philox
+
+
+def test_philox_known_answer():
+    # Philox4x32-10 known-answer vector (Random123 kat_vectors: counter 0, key 0)
+    c = philox.philox4x32_10(np.uint32(0), np.uint32(0), np.uint32(0), np.uint32(0), 0, 0)
+    assert [int(x) for x in c] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+
+
+def test_uniform_offsets_are_consistent():
+    a = philox.uniform(1000, seed=7)
+    b = philox.uniform(300, seed=7, offset=700)
+    np.testing.assert_array_equal(a[700:], b)
+    assert ((a >= 0) & (a < 1)).all()
+    assert abs(a.mean() - 0.5) < 0.05
+    t = K.uniform(1000, 7)
+    np.testing.assert_array_equal(t.numpy(), a)
+
+
+def test_poisson_weights_mean():
+    w = K.poisson_weights(4, 20000, seed=3, offset=0, rate=1.0)
+    assert w.shape == (4, 20000) and w.dtype == torch.uint8
+    m = w.float().mean(1)
+    assert torch.all((m - 1.0).abs() < 0.03)
+    assert 0.35 < float((w == 0).float().mean()) < 0.39  # e^-1
+
+
+def _bins(n=500, d=11, B=16, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, d, generator=g)
+    q = torch.linspace(0.05, 0.95, B - 1)
+    thr = torch.quantile(X, q, dim=0).T.contiguous()
+    nthr = torch.full((d,), B - 1, dtype=torch.int32)
+    return X, thr, nthr, K.binize(X, thr, nthr)
+
+
+def test_binize_matches_searchsorted():
+    X, thr, nthr, bins = _bins()
+    bm = K.bins_to_matrix(bins, X.shape[1])
+    for f in range(X.shape[1]):
+        ref = torch.searchsorted(thr[f], X[:, f].contiguous(), right=False)
+        assert torch.equal(bm[:, f].long(), ref)
+
+
+def test_hist_moments_bruteforce():
+    X, thr, nthr, bins = _bins(n=300, d=5, B=8)
+    n, d, B = 300, 5, 8
+    T, A = 2, 4
+    g = torch.Generator().manual_seed(1)
+    node = torch.randint(0, 2, (T, n), generator=g, dtype=torch.int32) + torch.tensor([[0], [2]], dtype=torch.int32)
+    build = torch.tensor([0, -1, 1, 2], dtype=torch.int32)
+    slot_tree = np.array([0, 1, 1])
+    w = K.poisson_weights(T, n, 1, 0, 1.0)
+    y = torch.randn(n, generator=g)
+    out = K.hist_moments(bins, d, node, w, None, y, build, slot_tree, None, B)
+    bm = K.bins_to_matrix(bins, d)
+    ref = np.zeros((3, d, B, 2))
+    for t in range(T):
+        for r in range(n):
+            s = int(build[node[t, r]])
+            if s < 0:
+                continue
+            for f in range(d):
+                ref[s, f, int(bm[r, f]), 0] += float(w[t, r])
+                ref[s, f, int(bm[r, f]), 1] += float(w[t, r]) * float(y[r])
+    np.testing.assert_allclose(out.numpy(), ref, rtol=1e-10, atol=1e-10)
+
+
+def test_fixed_point_scale_bounds():
+    v = torch.tensor([1e3, -5.0])
+    s = K._fixed_scale(v, 10 ** 8, 255)
+    assert 1e8 * 255 * 1e3 * s < 2 ** 62
+    assert s >= 2 ** 10
+    assert K._fixed_scale(torch.zeros(3), 10, 1) == 1.0
+    with pytest.raises(ValueError):
+        K._fixed_scale(torch.tensor([float("nan")]), 10, 1)
+
+
+def test_reg_metrics_and_score_hist():
+    g = torch.Generator().manual_seed(0)
+    y = torch.randn(1000, generator=g, dtype=torch.float64)
+    p = y + 0.1 * torch.randn(1000, generator=g, dtype=torch.float64)
+    s = K.reg_metrics(y, p)
+    e = (y - p)
+    np.testing.assert_allclose(float(s[0]), 1000)
+    np.testing.assert_allclose(float(s[1]), float((e * e).sum()), rtol=1e-10)
+    lab = (y > 0).double()
+    h = K.score_hist(p, lab, -4.0, 4.0, 64)
+    assert float(h.sum()) == 1000
+
+
+def test_kmeans_step_reference():
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(200, 3, generator=g)
+    C = X[:4].clone()
+    assign, sums, counts, cost = K.kmeans_step(X, C)
+    d2 = ((X[:, None, :] - C[None]) ** 2).sum(-1)
+    assert torch.equal(assign.long(), d2.argmin(1))
+    np.testing.assert_allclose(float(cost), float(d2.min(1).values.sum()), rtol=1e-5)
+    assert int(counts.sum()) == 200
+
+
+def test_gram_reference():
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(100, 6, generator=g)
+    y = torch.randn(100, generator=g)
+    G = K.gram(X, y)
+    A = torch.cat([X.double(), torch.ones(100, 1, dtype=torch.float64), y.double()[:, None]], 1)
+    np.testing.assert_allclose(G.numpy(), (A.T @ A).numpy(), rtol=1e-9, atol=1e-9)
+
+
+# ----------------------------------------------------------- property tests
+@settings(max_examples=25, deadline=None)
+@given(n=st.integers(1, 3000), parts=st.integers(1, 9), seed=st.integers(0, 2 ** 31 - 1))
+def test_uniform_partition_invariant(n, parts, seed):
+    """Counter-based RNG: generating in any number of pieces gives the same stream."""
+    whole = philox.uniform(n, seed)
+    cuts = np.linspace(0, n, parts + 1).astype(int)
+    pieces = np.concatenate([philox.uniform(b - a, seed, offset=a) for a, b in zip(cuts[:-1], cuts[1:])])
+    np.testing.assert_array_equal(whole, pieces)
+
+
+@settings(max_examples=15, deadline=None)
+@given(n=st.integers(20, 400), split=st.integers(1, 19), seed=st.integers(0, 1000))
+def test_histogram_is_additive(n, split, seed):
+    """Histograms of row shards sum to the histogram of the whole (the all-reduce contract)."""
+    X, thr, nthr, bins = _bins(n=n, d=3, B=8, seed=seed)
+    cut = max(1, n * split // 20)
+    node = torch.zeros((1, n), dtype=torch.int32)
+    build = torch.tensor([0], dtype=torch.int32)
+    y = torch.randn(n, generator=torch.Generator().manual_seed(seed))
+    whole = K.hist_moments(bins, 3, node, None, None, y, build, np.array([0]), None, 8)
+    a = K.hist_moments(bins[:, :cut].contiguous(), 3, node[:, :cut].contiguous(), None, None, y[:cut], build,
+                       np.array([0]), None, 8)
+    b = K.hist_moments(bins[:, cut:].contiguous(), 3, node[:, cut:].contiguous(), None, None, y[cut:], build,
+                       np.array([0]), None, 8)
+    np.testing.assert_allclose((a + b).numpy(), whole.numpy(), rtol=1e-9, atol=1e-9)
+
+
+@settings(max_examples=10, deadline=None)
+@given(seed=st.integers(0, 10000), frac=st.floats(0.1, 0.9))
+def test_random_split_partition_count_invariant(seed, frac):
+    import cdnaml
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    a = spark.range(0, 2000, numPartitions=1).randomSplit([frac, 1 - frac], seed=seed)[0]
+    b = spark.range(0, 2000, numPartitions=6).randomSplit([frac, 1 - frac], seed=seed)[0]
+    assert set(a.toPandas().id) == set(b.toPandas().id)
