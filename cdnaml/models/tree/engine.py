@@ -54,6 +54,7 @@ class TreeParams:
     gamma: float = 0.0
     min_child_weight: float = 1.0
     min_weight_fraction: float = 0.0
+    subset_scope: str = "node"          # "node" (Spark / colsample_bynode) or "tree" (colsample_bytree)
 
 
 # ============================================================ binning (K3/K4)
@@ -69,6 +70,7 @@ class BinnedData:
     row_offset: int
     d: int
     B: int
+    missing_bin: bool = False         # bin 0 holds missing values (XGBoost sparsity-aware splits)
 
 
 def find_thresholds(sample: np.ndarray, d: int, max_bins: int, categorical: Dict[int, int]):
@@ -102,8 +104,26 @@ def find_thresholds(sample: np.ndarray, d: int, max_bins: int, categorical: Dict
 
 
 def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins: int, seed: int,
-                row_offset: int, n_global: int) -> BinnedData:
+                row_offset: int, n_global: int, missing: Optional[float] = None) -> BinnedData:
+    """Global-sample quantile thresholds + device binning.
+
+    ``missing`` (XGBoost semantics, ML 11:67 ``missing=0``): NaN and values equal
+    to ``missing`` go to a dedicated bin 0; the remaining ``max_bins - 1`` bins
+    hold the observed values, so every split can route missing rows either way.
+    """
     d = X.shape[1]
+    if missing is not None:
+        miss = torch.isnan(X)
+        if not math.isnan(missing):
+            miss |= X == float(missing)
+        Xm = torch.where(miss, torch.full_like(X, float("-inf")), X)
+        inner = make_binned(session, torch.where(miss, torch.full_like(X, float("nan")), X), {}, max_bins - 1,
+                            seed, row_offset, n_global, None) if max_bins > 2 else None
+        thr = np.concatenate([np.full((d, 1), -np.finfo(np.float32).max), inner.thresholds], 1)
+        nthr = inner.nthr + 1
+        thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
+        bins = K.binize(Xm, thr_t, torch.from_numpy(nthr).to(X.device))
+        return BinnedData(X, bins, thr, nthr, {}, X.shape[0], n_global, row_offset, d, max_bins, True)
     for f, k in categorical.items():
         if k > max_bins:
             raise IllegalArgumentException(
@@ -345,7 +365,8 @@ class ForestTrainer:
         d = self.data.d
         if k is None or k >= d:
             return None
-        rng = np.random.default_rng([self.p.seed & 0xFFFFFFFF, t, node_key])
+        key = 1 if self.p.subset_scope == "tree" else node_key
+        rng = np.random.default_rng([self.p.seed & 0xFFFFFFFF, t, key])
         feats = rng.choice(d, size=k, replace=False)
         words = np.zeros((d + 31) // 32, dtype=np.uint32)
         for f in feats:
@@ -430,6 +451,16 @@ class ForestTrainer:
             gain = (SL * SL / WL.clamp_min(1e-300) + SR * SR / WR.clamp_min(1e-300) - St * St /
                     Wt.clamp_min(1e-300)) / Wt.clamp_min(1e-300)
             valid = (WL >= max(p.min_instances, 1e-12)) & (WR >= max(p.min_instances, 1e-12))
+        miss2 = None
+        if p.impurity == "xgb" and self.data.missing_bin:
+            # option 2: missing rows (bin 0) go RIGHT: left = bins 1..b
+            left2 = cum - Hs[:, :, 0:1, :]
+            right2 = tot[:, None, None, :] - left2
+            HL2, GL2 = left2[..., 0], left2[..., 1]
+            HR2, GR2 = right2[..., 0], right2[..., 1]
+            gain2 = 0.5 * (GL2 * GL2 / (HL2 + lam) + GR2 * GR2 / (HR2 + lam) - Gt * Gt / (Ht + lam)) - p.gamma
+            valid2 = (HL2 >= p.min_child_weight) & (HR2 >= p.min_child_weight) & (HL2 > 0) & (HR2 > 0)
+            miss2 = (gain2, valid2, left2, right2)
         # legal split positions per feature
         bpos = torch.arange(B, device=H.device)[None, :]
         limit = torch.where(nthr >= 0, nthr, torch.full_like(nthr, 0))[:, None]  # continuous: b < nthr
@@ -449,15 +480,30 @@ class ForestTrainer:
                    (torch.arange(d, device=H.device) & 31).to(masks.dtype)) & 1).bool()  # [A, d]
             valid = valid & fm[:, :, None]
         gain = torch.where(valid & torch.isfinite(gain), gain, torch.full_like(gain, float("-inf")))
+        ar = torch.arange(A, device=H.device)
+        if miss2 is not None:
+            gain2, valid2, left2, right2 = miss2
+            valid2 = valid2 & legal & (bpos >= 1)
+            if masks is not None:
+                valid2 = valid2 & fm[:, :, None]
+            gain2 = torch.where(valid2 & torch.isfinite(gain2), gain2, torch.full_like(gain2, float("-inf")))
+            both = torch.cat([gain.reshape(A, -1), gain2.reshape(A, -1)], 1)
+            best = torch.argmax(both, dim=1)
+            bgain = both[ar, best]
+            mr = best >= d * B
+            best = best % (d * B)
+            bf, bb = best // B, best % B
+            lstats = torch.where(mr[:, None], left2[ar, bf, bb], left[ar, bf, bb])
+            rstats = torch.where(mr[:, None], right2[ar, bf, bb], right[ar, bf, bb])
+            return bgain, bf, bb, lstats, rstats, order, cat_feats, mr
         flat = gain.reshape(A, -1)
         best = torch.argmax(flat, dim=1)
-        bgain = flat[torch.arange(A, device=H.device), best]
+        bgain = flat[ar, best]
         bf = best // B
         bb = best % B
-        ar = torch.arange(A, device=H.device)
         lstats = left[ar, bf, bb]
         rstats = right[ar, bf, bb]
-        return bgain, bf, bb, lstats, rstats, order, cat_feats
+        return bgain, bf, bb, lstats, rstats, order, cat_feats, None
 
     # ------------------------------------------------------------ training
     def train(self, num_trees: int, stats_rows: Dict[str, torch.Tensor], weights: Optional[torch.Tensor],
@@ -533,7 +579,8 @@ class ForestTrainer:
                     st = tot[a].cpu().numpy()
                     e["stats"] = st
             masks_t = torch.from_numpy(masks_np.view(np.int32)).to(dev) if masks_np is not None else None
-            gain, bf, bb, lst, rst, order, cat_feats = self._best_splits(H, tot, masks_t)
+            gain, bf, bb, lst, rst, order, cat_feats, miss_right = self._best_splits(H, tot, masks_t)
+            mr_h = miss_right.cpu().numpy() if miss_right is not None else None
             gain_h, bf_h, bb_h = gain.cpu().numpy(), bf.cpu().numpy(), bb.cpu().numpy()
             lst_h, rst_h = lst.cpu().numpy(), rst.cpu().numpy()
             order_h = order.cpu().numpy() if order is not None else None
@@ -570,6 +617,17 @@ class ForestTrainer:
                         m[int(c) >> 5] |= np.uint32(1) << np.uint32(int(c) & 31)
                     forest.is_cat[fid] = True
                     forest.catmask[fid] = m
+                    cat_off[a] = len(cat_masks)
+                    cat_masks.append(m)
+                elif mr_h is not None and mr_h[a]:
+                    # missing (bin 0) goes right: left = bins 1..b, expressed as a bin-set split
+                    m = np.zeros(8, dtype=np.uint32)
+                    for c in range(1, b + 1):
+                        m[c >> 5] |= np.uint32(1) << np.uint32(c & 31)
+                    forest.is_cat[fid] = True
+                    forest.catmask[fid] = m
+                    forest.bin[fid] = b
+                    forest.thr[fid] = float(self.data.thresholds[f, b])
                     cat_off[a] = len(cat_masks)
                     cat_masks.append(m)
                 else:

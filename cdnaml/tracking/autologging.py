@@ -30,3 +30,7 @@ def wrap_fit(est, dataset):
         except Exception:  # autolog must never break a fit
             pass
     return model
+
+
+def is_enabled() -> bool:
+    return bool(_state["enabled"])

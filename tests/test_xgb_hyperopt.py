@@ -1,0 +1,162 @@
+"""XGBoost-style GBDT (ML 11) and hyperopt (T3/T4; ML 08, L08)."""
+import functools
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from cdnaml.hyperopt import STATUS_OK, SparkTrials, Trials, anneal, fmin, hp, rand, space_eval, tpe
+from cdnaml.ml import Pipeline, PipelineModel
+from cdnaml.ml.evaluation import BinaryClassificationEvaluator, MulticlassClassificationEvaluator, \
+    RegressionEvaluator
+from cdnaml.ml.feature import StringIndexer, VectorAssembler
+from cdnaml.ml.regression import RandomForestRegressor
+from cdnaml.ml.xgboost import XgboostClassifier, XgboostRegressor
+from cdnaml.sql import functions as F
+
+
+def _reg(spark, n=3000, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, 4))
+    X[rng.uniform(size=n) < 0.25, 0] = 0.0
+    y = np.where(X[:, 0] == 0, 6.0, 2 * X[:, 0]) + X[:, 1] ** 2 + 0.1 * rng.normal(size=n)
+    pdf = pd.DataFrame(X, columns=list("abcd"))
+    pdf["label"] = y
+    return VectorAssembler(inputCols=list("abcd"), outputCol="features").transform(spark.createDataFrame(pdf)), X, y
+
+
+def test_xgb_regressor_learns_missing_direction(spark, tmp_path):
+    df, X, y = _reg(spark)
+    m = XgboostRegressor(n_estimators=100, learning_rate=0.1, max_depth=4, random_state=42, missing=0).fit(df)
+    pred = m.transform(df)
+    rmse = RegressionEvaluator().evaluate(pred)
+    assert rmse < 0.25
+    p = pred.toPandas()
+    zero = X[:, 0] == 0
+    # rows with a[0] == missing get the learned default branch: prediction near 6 + b^2
+    assert np.abs(p.prediction.values[zero] - (6 + X[zero, 1] ** 2)).mean() < 0.4
+    # save / load in a pipeline
+    pm = Pipeline(stages=[XgboostRegressor(n_estimators=20, max_depth=3, missing=0)]).fit(df)
+    path = str(tmp_path / "xgb")
+    pm.write().overwrite().save(path)
+    a = pm.transform(df).select("prediction").toPandas().prediction.values
+    b = PipelineModel.load(path).transform(df).select("prediction").toPandas().prediction.values
+    np.testing.assert_array_equal(a, b)
+    assert m.get_booster().get_score(importance_type="gain")
+
+
+def test_xgb_matches_sklearn_hist_gbdt_quality(spark):
+    from sklearn.ensemble import HistGradientBoostingRegressor
+
+    df, X, y = _reg(spark, seed=3)
+    m = XgboostRegressor(n_estimators=60, learning_rate=0.2, max_depth=4, reg_lambda=1.0).fit(df)
+    ours = RegressionEvaluator().evaluate(m.transform(df))
+    sk = HistGradientBoostingRegressor(max_iter=60, learning_rate=0.2, max_depth=4, l2_regularization=1.0,
+                                       early_stopping=False).fit(X, y)
+    ref = float(np.sqrt(np.mean((sk.predict(X) - y) ** 2)))
+    assert ours < 1.5 * ref + 0.05  # parity unpinned (xgboost not installed): same-quality bound vs sklearn
+
+
+def test_xgb_pipeline_log_label(spark):
+    """ML 11:36-103: StringIndexer + VectorAssembler + XgboostRegressor on log(price), exp back."""
+    rng = np.random.default_rng(1)
+    n = 2000
+    hood = rng.choice(["a", "b", "c", "d"], n)
+    acc = rng.integers(1, 8, n).astype(float)
+    price = np.exp(3 + 0.2 * acc + (hood == "a") * 0.5 + 0.05 * rng.normal(size=n))
+    df = spark.createDataFrame(pd.DataFrame({"hood": hood, "acc": acc, "price": price}))
+    df = df.withColumn("label", F.log(F.col("price")))
+    si = StringIndexer(inputCols=["hood"], outputCols=["hoodIdx"], handleInvalid="skip")
+    va = VectorAssembler(inputCols=["hoodIdx", "acc"], outputCol="features")
+    xgb = XgboostRegressor(n_estimators=100, learning_rate=0.1, max_depth=4, random_state=42, missing=0)
+    pm = Pipeline(stages=[si, va, xgb]).fit(df)
+    pred = pm.transform(df).withColumn("prediction", F.exp(F.col("prediction")))
+    r2 = RegressionEvaluator(labelCol="price", metricName="r2").evaluate(pred)
+    assert r2 > 0.95
+
+
+def test_xgb_classifier_binary_multiclass_early_stop(spark):
+    rng = np.random.default_rng(0)
+    n = 3000
+    X = rng.normal(size=(n, 3))
+    yb = (X[:, 0] + X[:, 1] > 0).astype(float)
+    ym = np.digitize(X[:, 0], [-0.5, 0.5]).astype(float)
+    val = rng.uniform(size=n) < 0.2
+    pdf = pd.DataFrame(X, columns=list("abc"))
+    pdf["yb"], pdf["ym"], pdf["val"] = yb, ym, val
+    df = VectorAssembler(inputCols=list("abc"), outputCol="features").transform(spark.createDataFrame(pdf))
+    mb = XgboostClassifier(n_estimators=50, max_depth=3, labelCol="yb").fit(df)
+    auc = BinaryClassificationEvaluator(labelCol="yb").evaluate(mb.transform(df))
+    assert auc > 0.97
+    mm = XgboostClassifier(n_estimators=30, max_depth=3, labelCol="ym").fit(df)
+    acc = MulticlassClassificationEvaluator(labelCol="ym", metricName="accuracy").evaluate(mm.transform(df))
+    assert acc > 0.95 and mm.numClasses == 3
+    es = XgboostClassifier(n_estimators=500, learning_rate=0.3, max_depth=3, labelCol="yb",
+                           validationIndicatorCol="val", early_stopping_rounds=5).fit(df)
+    assert len(es._forest.roots) < 500
+
+
+def test_hyperopt_fmin_tpe_and_space_eval():
+    space = {"x": hp.uniform("x", -5, 5), "q": hp.quniform("q", 2, 10, 1),
+             "c": hp.choice("c", ["a", "b", "c"]), "lr": hp.loguniform("lr", np.log(1e-4), 0.0)}
+
+    def f(p):
+        return (p["x"] - 1.3) ** 2 + 0.1 * (p["q"] - 7) ** 2 + {"a": 1, "b": 0, "c": 2}[p["c"]] + \
+            abs(np.log10(p["lr"]) + 2)
+
+    trials = Trials()
+    best = fmin(f, space, algo=functools.partial(tpe.suggest, n_startup_jobs=5), max_evals=60, trials=trials,
+                rstate=np.random.default_rng(42))
+    assert best["c"] == 1  # choice -> index (Labs/ML 08L:118)
+    assert space_eval(space, best)["c"] == "b"
+    assert float(best["q"]).is_integer()
+    assert min(trials.losses()) < 0.6
+    # deterministic given rstate
+    again = fmin(f, space, algo=functools.partial(tpe.suggest, n_startup_jobs=5), max_evals=60,
+                 rstate=np.random.default_rng(42))
+    assert again == best
+    r = fmin(f, space, algo=rand.suggest, max_evals=30, rstate=np.random.RandomState(0))
+    a = fmin(f, space, algo=anneal.suggest, max_evals=30, rstate=np.random.RandomState(0))
+    assert set(r) == set(a) == {"x", "q", "c", "lr"}
+
+
+def test_hyperopt_dict_results_failures_and_spark_trials():
+    calls = []
+
+    def f(p):
+        calls.append(p)
+        if p["x"] > 4.5:
+            raise RuntimeError("boom")
+        return {"loss": (p["x"] - 2) ** 2, "status": STATUS_OK}
+
+    st = SparkTrials(parallelism=3)
+    best = fmin(f, {"x": hp.uniform("x", 0, 5)}, algo=tpe.suggest, max_evals=24, trials=st,
+                rstate=np.random.default_rng(1))
+    assert len(st) == 24 and abs(best["x"] - 2) < 0.7
+    assert st.best_trial["result"]["status"] == STATUS_OK
+    with pytest.raises(ZeroDivisionError):  # plain Trials re-raise objective errors
+        fmin(lambda p: 1 / 0, {"x": hp.uniform("x", 0, 1)}, max_evals=2)
+
+
+def test_hyperopt_over_distributed_mllib(spark):
+    """ML 08:78-170: objective builds pipeline.copy({rf.maxDepth: q, rf.numTrees: q}) and returns RMSE."""
+    rng = np.random.default_rng(0)
+    n = 1500
+    X = rng.normal(size=(n, 3))
+    y = np.sin(2 * X[:, 0]) * 3 + X[:, 1]
+    pdf = pd.DataFrame(X, columns=list("abc"))
+    pdf["price"] = y
+    df = spark.createDataFrame(pdf)
+    train, val = df.randomSplit([0.8, 0.2], seed=42)
+    va = VectorAssembler(inputCols=list("abc"), outputCol="features")
+    rf = RandomForestRegressor(labelCol="price", maxBins=40, seed=42)
+    pipeline = Pipeline(stages=[va, rf])
+    ev = RegressionEvaluator(labelCol="price")
+
+    def objective(params):
+        est = pipeline.copy({rf.maxDepth: params["max_depth"], rf.numTrees: params["num_trees"]})
+        return ev.evaluate(est.fit(train).transform(val))
+
+    space = {"max_depth": hp.quniform("max_depth", 2, 5, 1), "num_trees": hp.quniform("num_trees", 10, 30, 1)}
+    best = fmin(objective, space, algo=tpe.suggest, max_evals=4, trials=Trials(), rstate=np.random.default_rng(42))
+    assert 2 <= best["max_depth"] <= 5 and 10 <= best["num_trees"] <= 30
