@@ -126,6 +126,7 @@ def read_delta(session, path, options=None) -> DataFrame:
     if not files:
         return session.createDataFrame(pd.DataFrame({f.name: [] for f in schema.fields}), schema)
     df = scan_parquet_files(session, files, [path] * len(files), schema, name=f"DeltaScan v{v}")
+    df._plan.source_paths = [path]
     return df
 
 
