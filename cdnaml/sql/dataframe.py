@@ -671,6 +671,26 @@ class DataFrame:
             return T.StructType(s.fields + [T.StructField(name, T.DoubleType())])
         return self._new(PartitionsPlan(session, "AttachRowUniform", [self._plan], fn, sfn))
 
+    def _with_sequence_id(self, name: str) -> "DataFrame":
+        """Attach a consecutive 0..N-1 int64 id in global row order (one counts all-gather)."""
+        session = self._session
+
+        def fn(parts):
+            comm = session.comm
+            local = sum(p.n for p in parts)
+            counts = comm.all_gather_object(local) if comm.distributed else [local]
+            off = sum(counts[: comm.rank])
+            out = []
+            for p in parts:
+                ids = torch.arange(off, off + p.n, dtype=torch.int64, device=p.device)
+                off += p.n
+                out.append(p.with_column(name, ColumnData(ids, T.LongType())))
+            return out
+
+        def sfn(s):
+            return T.StructType(s.fields + [T.StructField(name, T.LongType(), False)])
+        return self._new(PartitionsPlan(session, "AttachSequenceId", [self._plan], fn, sfn))
+
     def randomSplit(self, weights: List[float], seed: Optional[int] = None) -> List["DataFrame"]:
         """Split by Philox(seed, global row id): independent of the GPU count.
 
