@@ -499,11 +499,123 @@ def _mix(h: torch.Tensor) -> torch.Tensor:
     return h ^ (h >> 16)
 
 
+# ---- Spark-compatible Murmur3_x86_32 (seed 42, column hashes chained) ----
+_M32 = 0xFFFFFFFF
+
+
+def _rotl(x: torch.Tensor, r: int) -> torch.Tensor:
+    return ((x << r) | (x >> (32 - r))) & _M32
+
+
+def _mix_k1(k: torch.Tensor) -> torch.Tensor:
+    k = (k * 0xCC9E2D51) & _M32
+    k = _rotl(k, 15)
+    return (k * 0x1B873593) & _M32
+
+
+def _mix_h1(h: torch.Tensor, k: torch.Tensor) -> torch.Tensor:
+    h = (h ^ k) & _M32
+    h = _rotl(h, 13)
+    return (h * 5 + 0xE6546B64) & _M32
+
+
+def _fmix(h: torch.Tensor, length: int) -> torch.Tensor:
+    h = h ^ length
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & _M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & _M32
+    return h ^ (h >> 16)
+
+
+def _murmur_int(v: torch.Tensor, seed: torch.Tensor) -> torch.Tensor:
+    return _fmix(_mix_h1(seed, _mix_k1(v & _M32)), 4)
+
+
+def _murmur_long(v: torch.Tensor, seed: torch.Tensor) -> torch.Tensor:
+    lo = v & _M32
+    hi = (v >> 32) & _M32
+    h = _mix_h1(seed, _mix_k1(lo))
+    h = _mix_h1(h, _mix_k1(hi))
+    return _fmix(h, 8)
+
+
+def _murmur_bytes_py(b: bytes, seed: int) -> int:
+    """Spark's Murmur3_x86_32.hashUnsafeBytes (trailing bytes mixed one by one, signed)."""
+    def mk(k):
+        k = (k * 0xCC9E2D51) & _M32
+        k = ((k << 15) | (k >> 17)) & _M32
+        return (k * 0x1B873593) & _M32
+
+    def mh(h, k):
+        h ^= k
+        h = ((h << 13) | (h >> 19)) & _M32
+        return (h * 5 + 0xE6546B64) & _M32
+    h = seed & _M32
+    n = len(b)
+    aligned = n - n % 4
+    for i in range(0, aligned, 4):
+        h = mh(h, mk(int.from_bytes(b[i:i + 4], "little")))
+    for i in range(aligned, n):
+        x = b[i] - 256 if b[i] >= 128 else b[i]
+        h = mh(h, mk(x & _M32))
+    h ^= n
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & _M32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & _M32
+    return h ^ (h >> 16)
+
+
+def _spark_hash_column(c: ColumnData, seed: torch.Tensor) -> torch.Tensor:
+    dt = c.dtype
+    v = c.values
+    if isinstance(dt, T.StringType):
+        d = c.dictionary if c.dictionary is not None else np.array([], dtype=object)
+        codes = c.values.long()
+        uniq_seeds = torch.unique(seed)
+        if uniq_seeds.numel() == 1:
+            s0 = int(uniq_seeds[0])
+            lut = torch.tensor([_murmur_bytes_py(x.encode("utf-8"), s0) for x in d.tolist()] + [s0],
+                               dtype=torch.int64, device=c.device)
+            h = lut[torch.where(codes < 0, torch.full_like(codes, len(d)), codes)]
+        else:
+            sd, cd = seed.cpu().tolist(), codes.cpu().tolist()
+            h = torch.tensor([_murmur_bytes_py(d[k].encode("utf-8"), s) if k >= 0 else s for k, s in zip(cd, sd)],
+                             dtype=torch.int64, device=c.device)
+    elif isinstance(dt, (T.LongType, T.TimestampType)):
+        h = _murmur_long(v.long(), seed)
+    elif isinstance(dt, T.DoubleType):
+        x = torch.where(v == 0, torch.zeros_like(v), v.double())  # -0.0 -> 0.0
+        x = torch.where(torch.isnan(x), torch.full_like(x, float("nan")), x)
+        h = _murmur_long(x.view(torch.int64), seed)
+    elif isinstance(dt, T.FloatType):
+        x = torch.where(v == 0, torch.zeros_like(v), v.float())
+        h = _murmur_int(x.view(torch.int32).long(), seed)
+    elif isinstance(dt, (T.VectorUDT, T.ArrayType)):
+        et = dt.elementType if isinstance(dt, T.ArrayType) else T.DoubleType()
+        h = seed
+        for j in range(v.shape[1]):
+            if isinstance(et, (T.IntegerType, T.ShortType, T.ByteType)):
+                h = _murmur_int(v[:, j].round().long(), h)
+            elif isinstance(et, T.LongType):
+                h = _murmur_long(v[:, j].round().long(), h)
+            else:
+                h = _murmur_long(v[:, j].double().view(torch.int64), h)
+        return h
+    else:  # int / short / byte / boolean / date -> hashInt
+        h = _murmur_int(v.long(), seed)
+    if c.valid is not None:
+        h = torch.where(c.valid, h, seed)  # nulls leave the running hash unchanged
+    return h
+
+
 def hash(*cols) -> Column:  # noqa: A001
+    """Spark ``hash``: Murmur3_x86_32, seed 42, chained over the columns (bit-compatible)."""
     def ev(b, ctx, args):
         h = torch.full((b.n,), 42, dtype=torch.int64, device=b.device)
         for a in args:
-            h = _mix(h * 31 + _hash_column(a)) & 0xFFFFFFFF
+            h = _spark_hash_column(a, h)
         h = torch.where(h >= 2 ** 31, h - 2 ** 32, h)
         return ColumnData(h.to(torch.int32), T.IntegerType())
     return Column(Func("hash", ev, [_ce(c) for c in cols]))
@@ -518,7 +630,14 @@ def struct(*cols):
 
 def array(*cols) -> Column:
     def ev(b, ctx, args):
-        return ColumnData(torch.stack([a.values.float() for a in args], dim=1), T.ArrayType(T.DoubleType()))
+        kinds = [a.dtype for a in args]
+        if kinds and all(isinstance(k, (T.IntegerType, T.ShortType, T.ByteType)) for k in kinds):
+            et = T.IntegerType()
+        elif kinds and all(isinstance(k, T.IntegralType) for k in kinds):
+            et = T.LongType()
+        else:
+            et = T.DoubleType()
+        return ColumnData(torch.stack([a.values.float() for a in args], dim=1), T.ArrayType(et))
     return Column(Func("array", ev, [_ce(c) for c in cols]))
 
 

@@ -1,0 +1,173 @@
+"""Course harness helpers (Includes/Class-Utility-Methods.py,
+Includes/Classroom-Setup.py).
+
+``setup(lesson)`` resolves the same names the notebooks rely on —
+``username``, ``cleaned_username``, ``userhome``, ``course_dir``,
+``working_dir``, ``datasets_dir`` — creates the directories, installs the
+synthetic datasets (H2) and the per-user database (H5).  The answer
+validator hashes answers with Spark's ``abs(hash(value))`` exactly like the
+course (UTIL:161-165) — our ``hash`` is bit-compatible Murmur3 — so the
+expected constants in the labs check against this engine unchanged.
+"""
+from __future__ import annotations
+
+import csv
+import getpass
+import os
+import re
+import time
+from typing import Any, Dict, List, Optional
+
+from .dbutils import dbutils, to_local
+
+COURSE = "scalable-machine-learning-with-apache-spark"
+
+
+class Classroom:
+    def __init__(self, spark=None, course: str = COURSE, lesson: Optional[str] = None, root: Optional[str] = None,
+                 install: bool = True, dataset_scale: float = 1.0):
+        from ..session import SparkSession
+        self.spark = spark or SparkSession.builder.getOrCreate()
+        self.username = get_username(self.spark)
+        self.cleaned_username = re.sub(r"[^a-zA-Z0-9]", "_", self.username).lower()
+        self.userhome = f"dbfs:/user/{self.username}/dbacademy"
+        self.course_dir = f"{self.userhome}/{course}"
+        self.datasets_dir = f"{self.course_dir}/datasets"
+        self.lesson = lesson or os.environ.get("CDNAML_LESSON", "lesson")
+        clean_lesson = re.sub(r"[^a-zA-Z0-9]", "_", self.lesson).lower()
+        self.working_dir = f"{self.course_dir}/{clean_lesson}"
+        self.test_results: Dict[str, Dict[str, Any]] = {}
+        if root is not None:
+            os.environ["CDNAML_DBFS_ROOT"] = root
+        dbutils.fs.mkdirs(self.working_dir)
+        if install:
+            from .datasets import install_datasets
+            install_datasets(to_local(self.datasets_dir), self.spark, scale=dataset_scale)
+        self.database = create_user_database(self.spark, self.cleaned_username, COURSE, self.lesson)
+        self.spark.conf.set("com.databricks.training.module-name", "ml")
+
+    # ------------------------------------------------------------ H3 answers
+    def validate_your_answer(self, what: str, expected_hash: int, answer) -> bool:
+        s = "null" if answer is None else "true" if answer is True else "false" if answer is False else str(answer)
+        h = to_hash(self.spark, s)
+        ok = h == int(expected_hash)
+        self.test_results[what] = {"passed": ok, "answer": s, "hash": h}
+        return ok
+
+    validateYourAnswer = validate_your_answer
+
+    def summarize_your_results(self) -> str:
+        rows = [f"<tr><th>{k}</th><td>{'passed' if v['passed'] else 'FAILED'}</td></tr>"
+                for k, v in self.test_results.items()]
+        return "<table>" + "".join(rows) + "</table>"
+
+    summarizeYourResults = summarize_your_results
+
+    def log_your_test(self, path: str, name: str, value) -> None:
+        p = to_local(path)
+        os.makedirs(os.path.dirname(os.path.abspath(p)), exist_ok=True)
+        with open(p, "a", newline="") as f:
+            csv.writer(f).writerow([name, value])
+
+    logYourTest = log_your_test
+
+    def load_your_test_results(self, path: str) -> Dict[str, str]:
+        with open(to_local(path)) as f:
+            return {r[0]: r[1] for r in csv.reader(f) if r}
+
+    loadYourTestResults = load_your_test_results
+
+    def clear_your_results(self):
+        self.test_results.clear()
+
+    clearYourResults = clear_your_results
+
+    # ------------------------------------------------------------ H10 streams
+    def until_stream_is_ready(self, name: str, progressions: int = 3, timeout: float = 60.0):
+        """Busy-wait until the named query reports progress (SETUP:96-110)."""
+        t0 = time.time()
+        while True:
+            qs = [q for q in self.spark.streams.active if q.name == name]
+            if qs and len(qs[0].recentProgress) >= progressions:
+                return qs[0]
+            if time.time() - t0 > timeout:
+                raise TimeoutError(f"stream {name!r} made no progress in {timeout}s")
+            time.sleep(0.2)
+
+    untilStreamIsReady = until_stream_is_ready
+
+    # ------------------------------------------------------------ H11 reset
+    def reset(self):
+        dbutils.fs.rm(self.course_dir, True)
+
+    def names(self) -> Dict[str, str]:
+        return {"username": self.username, "cleaned_username": self.cleaned_username, "userhome": self.userhome,
+                "course_dir": self.course_dir, "datasets_dir": self.datasets_dir, "working_dir": self.working_dir}
+
+
+def get_username(spark=None) -> str:
+    """``SELECT current_user()`` (UTIL:51-60); env ``CDNAML_USER`` overrides."""
+    u = os.environ.get("CDNAML_USER")
+    if u:
+        return u
+    try:
+        u = getpass.getuser()
+    except Exception:  # noqa: BLE001
+        u = "user"
+    return f"{u}@cdnaml.local"
+
+
+def to_hash(spark, value) -> int:
+    """``abs(hash(str(value)))`` cast to int, computed by the engine (UTIL:161-165)."""
+    from ..sql import functions as F
+    df = spark.createDataFrame([(str(value),)], ["value"])
+    return int(df.select(F.abs(F.hash(F.col("value"))).cast("int").alias("h")).first().h)
+
+
+def create_user_database(spark, username: str, course: str, lesson: str) -> str:
+    """Per-user database (UTIL:134-150)."""
+    name = re.sub(r"[^a-zA-Z0-9]", "_", f"{username}_{course[:12]}").lower()
+    spark.sql(f"CREATE DATABASE IF NOT EXISTS {name}")
+    spark.sql(f"USE {name}")
+    return name
+
+
+def delete_tables(spark, database: str):
+    spark.sql(f"DROP DATABASE IF EXISTS {database} CASCADE")
+
+
+def path_exists(path: str) -> bool:
+    return os.path.exists(to_local(path))
+
+
+def delete_path(path: str) -> bool:
+    return dbutils.fs.rm(path, True)
+
+
+def platform_info() -> Dict[str, Any]:
+    """Runtime / device introspection (H8): ROCm + GPU details instead of DBR tags."""
+    import torch
+    info = {"runtime": f"cdnaml {__import__('cdnaml').__version__}", "torch": torch.__version__,
+            "hip": getattr(torch.version, "hip", None), "gpus": 0, "devices": []}
+    if torch.cuda.is_available():
+        info["gpus"] = torch.cuda.device_count()
+        info["devices"] = [torch.cuda.get_device_properties(i).name for i in range(info["gpus"])]
+    return info
+
+
+def init_tracking_as_job(job_id: Optional[str] = None):
+    """H9: when run as a job, route experiments to ``/Curriculum/Test Results/Experiments/{jobId}``."""
+    from .. import tracking
+    jid = job_id or dbutils.notebook.getContext().tags().get("jobId")
+    if jid:
+        return tracking.set_experiment(f"/Curriculum/Test Results/Experiments/{jid}")
+    return None
+
+
+class FILL_IN:  # noqa: N801 - course placeholder (UTIL:356-363)
+    VALUE = None
+    LIST = []
+    SCHEMA = None
+    ROW = None
+    INT = 0
+    DATAFRAME = None
