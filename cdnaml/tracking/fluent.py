@@ -46,6 +46,8 @@ def _comm():
 
 # ---------------------------------------------------------------- tracking uri
 def set_tracking_uri(uri: str):
+    if uri != _global["uri"]:
+        _global["experiment_id"] = None  # experiment ids are per store
     _global["uri"] = uri
 
 
