@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--bins", type=int, default=40)
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--trace", default="", help="after timing, run one traced step; write a Chrome trace here")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -72,9 +73,13 @@ def main():
     rf = RandomForestRegressor(labelCol="label", featuresCol="features", numTrees=args.trees,
                                maxDepth=args.depth, maxBins=args.bins, seed=args.seed)
 
+    from cdnaml.utils import tracing
+
     def step():
-        model = rf.fit(df)
-        parts = model.transform(df)._plan.execute()  # materialise predictions on device
+        with tracing.span("rf.fit"):
+            model = rf.fit(df)
+        with tracing.span("rf.transform"):
+            parts = model.transform(df)._plan.execute()  # materialise predictions on device
         return model, parts
 
     for i in range(args.warmup):
@@ -103,6 +108,15 @@ def main():
     corr = float(torch.corrcoef(torch.stack([p[:1000000], y[:1000000]]))[0, 1]) if n > 1 else float("nan")
     log(f"step {ms:.1f} ms, {rows_per_s:.3e} rows/s, pred finite={ok}, corr(pred,label)={corr:.3f}, "
         f"nodes={model.totalNumNodes}")
+    if args.trace:
+        tracing.reset()
+        tracing.enable()
+        step()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        tracing.disable()
+        log("traced step (untimed):\n" + tracing.summary())
+        tracing.export_chrome_trace(args.trace if W == 1 else f"{args.trace}.rank{rank}")
     if rank == 0:
         print(json.dumps({
             "metric": "rows/sec fit+transform, RandomForestRegressor 1e8×100 synthetic, 1/2/4/8 GPU",

@@ -72,6 +72,10 @@ def main():
     configs = [
         # (name, T, L, masked, weights, version, lane map, lds bytes)
         ("L0 T20 masked w v4", 20, 1, True, True, 4, 2, 65536),
+        ("L0 T20 masked w v4 rot", 20, 1, True, True, 4, 4, 65536),
+        ("L0 T20 full   w v4 rot", 20, 1, False, True, 4, 4, 65536),
+        ("L4 T20 masked w v4 rot", 20, 16, True, True, 4, 4, 65536),
+        ("L4 T20 full   w v4 rot", 20, 16, False, True, 4, 4, 65536),
         ("L0 T20 masked w v4 m3", 20, 1, True, True, 4, 3, 65536),
         ("L0 T20 full   w v4", 20, 1, False, True, 4, 2, 65536),
         ("L0 T20 full   w v4 m3", 20, 1, False, True, 4, 3, 65536),

@@ -33,9 +33,10 @@ import numpy as np
 import torch
 
 from ...ops import kernels as K
+from ...utils import tracing as _tr
 from ..util import IllegalArgumentException
 
-HIST_MODE = __import__("os").environ.get("CDNAML_RF_HIST", "masked")
+HIST_MODE = __import__("os").environ.get("CDNAML_RF_HIST", "full")
 
 
 @dataclass
@@ -145,10 +146,12 @@ def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins:
     if comm.distributed:
         samp = torch.cat(comm.all_gather_varlen(samp.contiguous()))
     sample = samp.double().cpu().numpy()
-    thr, nthr = find_thresholds(sample, d, max_bins, categorical)
+    with _tr.span("tree.find_thresholds", cat="host"):
+        thr, nthr = find_thresholds(sample, d, max_bins, categorical)
     thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
     nthr_t = torch.from_numpy(nthr).to(X.device)
-    bins = K.binize(X, thr_t, nthr_t)
+    with _tr.span("tree.binize"):
+        bins = K.binize(X, thr_t, nthr_t)
     return BinnedData(X, bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins)
 
 
@@ -556,13 +559,17 @@ class ForestTrainer:
                 fm_build = torch.from_numpy(masks_np[build_ids].view(np.int32)).to(dev)
             build_slot = torch.from_numpy(slot_of).to(dev)
             id_tree = np.array([e["tree"] for e in active], dtype=np.int32)
-            if self.classification:
-                Hb = K.hist_classes(data.bins, d, node, weights, stats_rows["label"], self.C, build_slot, slot_tree,
-                                    fm_build, B, id_tree=id_tree)
-            else:
-                Hb = K.hist_moments(data.bins, d, node, weights, stats_rows.get("v0"), stats_rows["v1"],
-                                    build_slot, slot_tree, fm_build, B, id_tree=id_tree)
-            self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
+            with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
+                if self.classification:
+                    Hb = K.hist_classes(data.bins, d, node, weights, stats_rows["label"], self.C, build_slot,
+                                        slot_tree, fm_build, B, id_tree=id_tree)
+                else:
+                    Hb = K.hist_moments(data.bins, d, node, weights, stats_rows.get("v0"), stats_rows["v1"],
+                                        build_slot, slot_tree, fm_build, B, id_tree=id_tree)
+            with _tr.span("tree.allreduce", cat="comm", bytes=Hb.numel() * 8):
+                self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
+            _split_span = _tr.span("tree.split", depth=depth)
+            _split_span.__enter__()
             # ---- assemble every active node's histogram
             H = torch.empty((A, d, B, self.stats_k), dtype=torch.float64, device=dev)
             if build_ids:
@@ -584,6 +591,7 @@ class ForestTrainer:
             gain_h, bf_h, bb_h = gain.cpu().numpy(), bf.cpu().numpy(), bb.cpu().numpy()
             lst_h, rst_h = lst.cpu().numpy(), rst.cpu().numpy()
             order_h = order.cpu().numpy() if order is not None else None
+            _split_span.__exit__(None, None, None)
             # ---- create forest nodes for the active set, decide splits
             split_feat = np.full(A, -1, dtype=np.int32)
             split_bin = np.zeros(A, dtype=np.int32)
@@ -661,9 +669,10 @@ class ForestTrainer:
                         nxt[kids[0]]["parent"] = None  # single child: build directly
             if nxt:
                 cm = np.stack(cat_masks).view(np.int32) if cat_masks else np.zeros((0, 8), np.int32)
-                K.partition(data.bins, node, torch.from_numpy(split_feat).to(dev),
-                            torch.from_numpy(split_bin).to(dev), torch.from_numpy(cat_off).to(dev),
-                            torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child).to(dev))
+                with _tr.span("tree.partition", depth=depth):
+                    K.partition(data.bins, node, torch.from_numpy(split_feat).to(dev),
+                                torch.from_numpy(split_bin).to(dev), torch.from_numpy(cat_off).to(dev),
+                                torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child).to(dev))
             prev_hist = H if subtract else None
             active = nxt
         forest.roots.extend(root_ids)

@@ -148,7 +148,8 @@ def _plan_chunks(n: int, G: int, ngroups: int, target_blocks: int = 2048) -> int
 
 HIST_LDS_BUDGET = int(__import__("os").environ.get("CDNAML_HIST_LDS", str(64 * 1024)))
 HIST_VERSION = int(__import__("os").environ.get("CDNAML_HIST_VERSION", "4"))
-HIST_MAP = int(__import__("os").environ.get("CDNAML_HIST_MAP", "2"))  # 2: lane = row; 3: lane = 8*row + feature
+# lane mapping: 2 = lane per row; 3 = lane = 8*row + feature; 4 = lane per row, rotated features + pipelined loads
+HIST_MAP = int(__import__("os").environ.get("CDNAML_HIST_MAP", "4"))
 
 
 def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int) -> float:
@@ -206,7 +207,7 @@ def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_
     v1 = None if v1 is None else v1.float().contiguous()
     label = None if label is None else label.int().contiguous()
     build_slot = build_slot.int().contiguous()
-    vmode = 2 if HIST_VERSION == 3 or HIST_MAP == 3 else 0
+    vmode = 2 if HIST_VERSION == 3 or HIST_MAP == 3 else (8 if HIST_MAP == 4 and HIST_VERSION >= 4 else 0)
     if not v4:
         _lib.check(_lib.lib().cdna_hist2(mode | vmode, _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0),
                                          _ptr(v1), _ptr(label), int(C), _ptr(build_slot), _ptr(fm), mw, S, B, SB,

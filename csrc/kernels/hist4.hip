@@ -184,10 +184,189 @@ __global__ __launch_bounds__(kThreads) void hist4_kernel(const Hist4Args a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// MAP 2: rotated features + software-pipelined row loads.
+// rocprofv3 on MAP 0 (1e8 rows, 20 trees): SQ_LDS_BANK_CONFLICT ~ 55 % of
+// SQ_LDS_IDX_ACTIVE and SQ_WAIT_ANY ~ 62 % of SQ_WAVE_CYCLES.  Two causes:
+//   * every lane of an instruction updates the SAME feature, so 64 rows land
+//     on ~40 bins: same-word collisions serialise the atomic.  Here lane l
+//     visits feature (j + l) & 7 at step j, so one instruction spreads over
+//     8 features x B bins;
+//   * each row's loads (bins word, v1, node id + weight per tree) are waited
+//     on right before use.  Here the next row's loads are issued before the
+//     current row's atomics, hiding HBM/L2 latency behind LDS work.
+// ---------------------------------------------------------------------------
 template <int MODE, bool V0>
-void launch(const Hist4Args& a, unsigned nblk, size_t lds, bool v3, hipStream_t st) {
-  if (v3)
+__global__ __launch_bounds__(kThreads) void hist4r_kernel(const Hist4Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int G = (a.d + 7) / 8;
+  const int plane = a.SB * 8 * a.B;
+  unsigned long long* h64 = reinterpret_cast<unsigned long long*>(smem);
+  uint32_t* h32 = reinterpret_cast<uint32_t*>(h64 + (size_t)a.n64 * plane);
+  const int hwords = a.n32 * plane;
+  int* lslot = reinterpret_cast<int*>(h32 + ((hwords + 3) & ~3));
+  uint8_t* lmask = reinterpret_cast<uint8_t*>(lslot + a.id_span_max);
+
+  const uint32_t w = cdna::xcd_remap(blockIdx.x, gridDim.x);
+  const int g = (int)(w % G);
+  const int grp = (int)((w / G) % a.ngroups);
+  const int chunk = (int)(w / ((uint32_t)G * a.ngroups));
+  const int s0 = a.grp[grp * 5 + 0], t0 = a.grp[grp * 5 + 1], t1 = a.grp[grp * 5 + 2];
+  const int id0 = a.grp[grp * 5 + 3], id1 = a.grp[grp * 5 + 4];
+  const int span = id1 - id0;
+  const bool lds_slot = span <= a.id_span_max;
+  const int fbase = g * 8;
+  const int rot = threadIdx.x & 7;
+
+  for (int i = threadIdx.x; i < a.n64 * plane; i += kThreads) h64[i] = 0ull;
+  for (int i = threadIdx.x; i < hwords; i += kThreads) h32[i] = 0u;
+  if (lds_slot)
+    for (int i = threadIdx.x; i < span; i += kThreads) lslot[i] = a.build_slot[id0 + i];
+  for (int i = threadIdx.x; i < a.SB; i += kThreads) {
+    uint32_t m = 0xFFu;
+    const int slot = s0 + i;
+    if (a.feat_mask != nullptr && slot < a.S)
+      m = (a.feat_mask[(int64_t)slot * a.mask_words + (fbase >> 5)] >> (fbase & 31)) & 0xFFu;
+    const int valid = a.d - fbase;
+    if (valid < 8) m &= (1u << (valid > 0 ? valid : 0)) - 1u;
+    lmask[i] = (uint8_t)m;
+  }
+  __syncthreads();
+
+  const int64_t rb = (int64_t)chunk * a.rows_per_chunk;
+  int64_t re = rb + a.rows_per_chunk;
+  if (re > a.n) re = a.n;
+  const int64_t n = a.n;
+  const int nt_head = t1 - t0 + 1 < 4 ? t1 - t0 + 1 : 4;  // trees whose loads are pipelined
+
+  // row r's inputs, loaded one iteration ahead
+  uint64_t b8 = 0;
+  float x0 = 1.f, x1 = 0.f;
+  int lab = 0;
+  int ids[4] = {-1, -1, -1, -1};
+  int wt[4] = {0, 0, 0, 0};
+  auto load_row = [&](int64_t rr, uint64_t& ob8, float& ox0, float& ox1, int& olab, int* oids, int* owt) {
+    ob8 = a.bins[(int64_t)g * n + rr];
+    if (MODE == 0) {
+      if (V0) ox0 = a.v0[rr];
+      ox1 = a.v1[rr];
+    } else {
+      olab = a.label[rr];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = k < nt_head;
+      oids[k] = ok ? a.node[(int64_t)(t0 + k) * n + rr] : -1;
+      owt[k] = (ok && a.weight) ? (int)a.weight[(int64_t)(t0 + k) * n + rr] : 1;
+    }
+  };
+  int64_t r = rb + threadIdx.x;
+  if (r < re) load_row(r, b8, x0, x1, lab, ids, wt);
+
+  for (; r < re; r += kThreads) {
+    // issue the next row's loads first
+    uint64_t nb8 = 0;
+    float nx0 = 1.f, nx1 = 0.f;
+    int nlab = 0;
+    int nids[4] = {-1, -1, -1, -1};
+    int nwt[4] = {0, 0, 0, 0};
+    const int64_t rn = r + kThreads;
+    if (rn < re) load_row(rn, nb8, nx0, nx1, nlab, nids, nwt);
+
+    long long q0 = 1, q1 = 0;
+    bool row_ok = true;
+    if (MODE == 0) {
+      if (V0) q0 = llrintf(x0 * a.qs0);
+      q1 = llrintf(x1 * a.qs1);
+    } else {
+      row_ok = lab >= 0 && lab < a.C;
+    }
+    if (row_ok) {
+      for (int t = t0; t <= t1; t += 4) {
+        int cid[4], cwt[4];
+        if (t == t0) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { cid[k] = ids[k]; cwt[k] = wt[k]; }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int tt = t + k;
+            const bool ok = tt <= t1;
+            cid[k] = ok ? a.node[(int64_t)tt * n + r] : -1;
+            cwt[k] = (ok && a.weight) ? (int)a.weight[(int64_t)tt * n + r] : 1;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int id = cid[k];
+          if (id < id0 || id >= id1 || cwt[k] == 0) continue;
+          const int sl = lds_slot ? lslot[id - id0] : a.build_slot[id];
+          const int ls = sl - s0;
+          if (ls < 0 || ls >= a.SB) continue;
+          const uint32_t m = lmask[ls];
+          const int off = (ls * 8) * a.B;
+          const long long y1 = (long long)cwt[k] * q1;
+          const long long y0 = V0 ? (long long)cwt[k] * q0 : 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int jj = (j + rot) & 7;
+            if ((m >> jj) & 1u) {
+              const int idx = off + jj * a.B + (int)((b8 >> (8 * jj)) & 0xFFu);
+              if (MODE == 0) {
+                if (V0) {
+                  lds_add64(h64 + idx, y0);
+                  lds_add64(h64 + plane + idx, y1);
+                } else {
+                  atomicAdd(h32 + idx, (uint32_t)cwt[k]);
+                  lds_add64(h64 + idx, y1);
+                }
+              } else {
+                atomicAdd(h32 + lab * plane + idx, (uint32_t)cwt[k]);
+              }
+            }
+          }
+        }
+      }
+    }
+    b8 = nb8;
+    x0 = nx0;
+    x1 = nx1;
+    lab = nlab;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { ids[k] = nids[k]; wt[k] = nwt[k]; }
+  }
+  __syncthreads();
+  const int total = (a.n64 + a.n32) * plane;
+  for (int i = threadIdx.x; i < total; i += kThreads) {
+    const bool is64 = i < a.n64 * plane;
+    const int p = is64 ? i / plane : (i - a.n64 * plane) / plane;
+    const int rem = i - (is64 ? p : a.n64 + p) * plane;
+    long long v;
+    int k;
+    if (is64) {
+      v = (long long)h64[i];
+      k = (MODE == 0 && !V0) ? 1 : p;
+    } else {
+      v = (long long)h32[i - a.n64 * plane];
+      k = p;
+    }
+    if (v == 0) continue;
+    const int ls = rem / (8 * a.B);
+    const int jj = (rem / a.B) & 7;
+    const int bn = rem % a.B;
+    const int f = fbase + jj;
+    const int slot = s0 + ls;
+    if (f < a.d && slot < a.S)
+      atomicAdd(&a.out[(((int64_t)slot * a.d + f) * a.B + bn) * a.K + k], (unsigned long long)v);
+  }
+}
+
+template <int MODE, bool V0>
+void launch(const Hist4Args& a, unsigned nblk, size_t lds, int map, hipStream_t st) {
+  if (map == 1)
     hipLaunchKernelGGL((hist4_kernel<MODE, V0, 1>), dim3(nblk), dim3(kThreads), lds, st, a);
+  else if (map == 2)
+    hipLaunchKernelGGL((hist4r_kernel<MODE, V0>), dim3(nblk), dim3(kThreads), lds, st, a);
   else
     hipLaunchKernelGGL((hist4_kernel<MODE, V0, 0>), dim3(nblk), dim3(kThreads), lds, st, a);
 }
@@ -201,7 +380,8 @@ CDNA_API int cdna_hist4_bytes_per_bin(int mode, int C) {
   return (mode & 4) ? 16 : 12;
 }
 
-// mode bit0: classes; bit1: v3 lane mapping; bit2: v0 present (moments).
+// mode bit0: classes; bit1: v3 lane mapping; bit2: v0 present (moments);
+// bit3: rotated features + pipelined row loads (MAP 2).
 // `out` (int64 [S][d][B][K]) must be zeroed.  Result in fixed point: plane k
 // scaled by qs_k (counts unscaled).
 CDNA_API int cdna_hist4(int mode, const uint64_t* bins, int64_t n, int d, int T, const int* node,
@@ -246,9 +426,9 @@ CDNA_API int cdna_hist4(int mode, const uint64_t* bins, int64_t n, int d, int T,
   const size_t lds = plane * 8 * a.n64 + ((plane * a.n32 + 3) & ~(size_t)3) * 4 + (size_t)id_span_max * 4 + SB + 16;
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   const unsigned nblk = (unsigned)G * ngroups * nchunk;
-  const bool v3 = (mode & 2) != 0;
-  if (classes) launch<1, false>(a, nblk, lds, v3, st);
-  else if (has_v0) launch<0, true>(a, nblk, lds, v3, st);
-  else launch<0, false>(a, nblk, lds, v3, st);
+  const int map = (mode & 2) ? 1 : ((mode & 8) ? 2 : 0);
+  if (classes) launch<1, false>(a, nblk, lds, map, st);
+  else if (has_v0) launch<0, true>(a, nblk, lds, map, st);
+  else launch<0, false>(a, nblk, lds, map, st);
   return (int)hipGetLastError();
 }

@@ -102,13 +102,13 @@ def _tree_state(n, T, A, seed):
 
 
 def _set_hist_version(monkeypatch, ver):
-    """ver: 1..4 kernel generation; 43 = v4 integer kernel with the v3 lane mapping."""
-    monkeypatch.setattr(K, "HIST_VERSION", 4 if ver == 43 else max(ver, 2))
-    monkeypatch.setattr(K, "HIST_MAP", 3 if ver == 43 else 2)
+    """ver: 1..4 kernel generation; 43 / 44 = v4 integer kernel with the v3 / rotated lane mapping."""
+    monkeypatch.setattr(K, "HIST_VERSION", 4 if ver in (43, 44) else max(ver, 2))
+    monkeypatch.setattr(K, "HIST_MAP", {43: 3, 44: 4}.get(ver, 2))
 
 
 @pytest.mark.parametrize("B", [40, 256])
-@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43])
+@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43, 44])
 def test_hist_moments(dev, B, ver, monkeypatch):
     n, d, T, A = 20000, 19, 3, 12
     g = torch.Generator().manual_seed(B)
@@ -129,7 +129,7 @@ def test_hist_moments(dev, B, ver, monkeypatch):
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43])
+@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43, 44])
 def test_hist_classes(dev, ver, monkeypatch):
     n, d, T, A, C, B = 10000, 10, 2, 8, 3, 32
     g = torch.Generator().manual_seed(11)
@@ -147,7 +147,7 @@ def test_hist_classes(dev, ver, monkeypatch):
     assert torch.allclose(out, ref)
 
 
-@pytest.mark.parametrize("ver", [2, 4])
+@pytest.mark.parametrize("ver", [2, 4, 44])
 def test_hist_moments_v0(dev, ver, monkeypatch):
     """Moments with a real-valued v0 plane (XGBoost hessians) and no bootstrap weights."""
     n, d, T, A, B = 30000, 13, 2, 6, 64
