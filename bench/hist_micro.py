@@ -72,6 +72,16 @@ def main():
     configs = [
         # (name, T, L, masked, weights, version, lane map, lds bytes)
         ("L0 T20 masked w v4", 20, 1, True, True, 4, 2, 65536),
+        ("L0 T20 full   w v4 fast", 20, 1, False, True, 4, 5, 65536),
+        ("L1 T20 full   w v4 fast", 20, 2, False, True, 4, 5, 65536),
+        ("L4 T20 full   w v4 fast", 20, 16, False, True, 4, 5, 65536),
+        ("L0 T20 masked w v4 fast", 20, 1, True, True, 4, 5, 65536),
+        ("L4 T20 masked w v4 fast", 20, 16, True, True, 4, 5, 65536),
+        ("L4 T20 full   w v4 fast 96K", 20, 16, False, True, 4, 5, 98304),
+        ("L0 T20 full   w v5 packed", 20, 1, False, True, 5, 4, 65536),
+        ("L4 T20 full   w v5 packed", 20, 16, False, True, 5, 4, 65536),
+        ("L0 T20 masked w v5 packed", 20, 1, True, True, 5, 4, 65536),
+        ("L4 T20 masked w v5 packed", 20, 16, True, True, 5, 4, 65536),
         ("L0 T20 masked w v4 rot", 20, 1, True, True, 4, 4, 65536),
         ("L0 T20 full   w v4 rot", 20, 1, False, True, 4, 4, 65536),
         ("L4 T20 masked w v4 rot", 20, 16, True, True, 4, 4, 65536),
@@ -91,7 +101,8 @@ def main():
         configs = [c for c in configs if any(v in c[0] for v in args.variants.split(","))]
     for name, T, L, masked, wts, ver, lmap, lds in configs:
         bins, node, w, y, build, st, it, fm = make_state(n, d, T, L, B, masked)
-        K.HIST_VERSION = ver
+        K.HIST_VERSION = min(ver, 4)
+        K.HIST_PACKED = ver == 5
         K.HIST_MAP = lmap
         fn = lambda: K.hist_moments(bins, d, node, w if wts else None, None, y, build, st, fm, B,  # noqa: E731
                                     lds_budget=lds, id_tree=it if ver >= 2 else None)

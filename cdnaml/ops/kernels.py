@@ -148,12 +148,16 @@ def _plan_chunks(n: int, G: int, ngroups: int, target_blocks: int = 2048) -> int
 
 HIST_LDS_BUDGET = int(__import__("os").environ.get("CDNAML_HIST_LDS", str(64 * 1024)))
 HIST_VERSION = int(__import__("os").environ.get("CDNAML_HIST_VERSION", "4"))
-# lane mapping: 2 = lane per row; 3 = lane = 8*row + feature; 4 = lane per row, rotated features + pipelined loads
-HIST_MAP = int(__import__("os").environ.get("CDNAML_HIST_MAP", "4"))
+# lane mapping: 2 = lane per row; 3 = lane = 8*row + feature; 4 = lane per row, rotated features + pipelined
+# loads; 5 = 4 with the per-update VALU work hoisted (hist4f_kernel)
+HIST_MAP = int(__import__("os").environ.get("CDNAML_HIST_MAP", "5"))
+# regression histograms: one packed (count | offset sum) ds_add_u64 per update (hist4.hip hist4p_kernel)
+HIST_PACKED = __import__("os").environ.get("CDNAML_HIST_PACKED", "0") != "0"
 
 
-def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int) -> float:
-    """Power-of-two fixed-point scale so that sum_r w_r * |round(v_r * s)| < 2^62 over n rows."""
+def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int, qmax_bits: int = 62) -> float:
+    """Power-of-two fixed-point scale so that sum_r w_r * |round(v_r * s)| < 2^62 over n rows
+    (and |round(v_r * s)| < 2^qmax_bits for kernels that quantise in 32 bits)."""
     if v is None or v.numel() == 0:
         return 1.0
     m = float(v.abs().max().item())
@@ -162,6 +166,18 @@ def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int) -> float:
     if m == 0.0:
         return 1.0
     e = 62 - math.ceil(math.log2(max(1, n) * max(1, wmax) * m)) - 1
+    e = min(e, qmax_bits - math.ceil(math.log2(m)) - 1)
+    return float(2.0 ** max(-120, min(100, e)))
+
+
+def _packed_scale(v: torch.Tensor) -> float:
+    """Power-of-two scale with |round(v * s)| <= 2^23 (packed count|sum LDS words)."""
+    m = float(v.abs().max().item()) if v.numel() else 0.0
+    if not math.isfinite(m):
+        raise ValueError("histogram statistic contains NaN/Inf")
+    if m == 0.0:
+        return 1.0
+    e = math.floor(math.log2((2 ** 23) / m))
     return float(2.0 ** max(-120, min(100, e)))
 
 
@@ -173,9 +189,12 @@ def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_
     T = node.shape[0]
     Kst = 2 if mode == 0 else C
     v4 = HIST_VERSION >= 4
+    packed = v4 and HIST_PACKED and mode == 0 and v0 is None and HIST_MAP != 5
     if v4:
-        kbits = mode | (4 if (mode == 0 and v0 is not None) else 0)
+        kbits = mode | (4 if (mode == 0 and v0 is not None) else 0) | (16 if packed else 0)
         per_slot = 8 * B * int(_lib.lib().cdna_hist4_bytes_per_bin(kbits, int(C)))
+        if packed:
+            lds_budget = min(lds_budget, 8192 * 8)  # register drain holds <= 16 cells per thread
     else:
         per_slot = Kst * 8 * B * 4
     SB = max(1, min(S, lds_budget // per_slot))
@@ -208,6 +227,8 @@ def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_
     label = None if label is None else label.int().contiguous()
     build_slot = build_slot.int().contiguous()
     vmode = 2 if HIST_VERSION == 3 or HIST_MAP == 3 else (8 if HIST_MAP == 4 and HIST_VERSION >= 4 else 0)
+    if HIST_MAP == 5 and v4 and v0 is None and id_span_max >= span:
+        vmode = 32  # fast rotated kernel (LDS slot table must hold the whole id span)
     if not v4:
         _lib.check(_lib.lib().cdna_hist2(mode | vmode, _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0),
                                          _ptr(v1), _ptr(label), int(C), _ptr(build_slot), _ptr(fm), mw, S, B, SB,
@@ -216,9 +237,9 @@ def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_
         return out
     wmax = 255 if weight is not None else 1
     qs0 = _fixed_scale(v0, n, wmax)
-    qs1 = _fixed_scale(v1, n, wmax)
+    qs1 = _packed_scale(v1) if packed else _fixed_scale(v1, n, wmax, qmax_bits=30 if vmode == 32 else 62)
     iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
-    _lib.check(_lib.lib().cdna_hist4(kbits | vmode, _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0),
+    _lib.check(_lib.lib().cdna_hist4(kbits | (vmode if not packed else 0), _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0),
                                      _ptr(v1), _ptr(label), int(C), _ptr(build_slot), _ptr(fm), mw, S, B, SB,
                                      _ptr(grp), ng, nchunk, id_span_max, qs0, qs1, _ptr(iout),
                                      _stream(bins.device)), "cdna_hist4")

@@ -102,13 +102,15 @@ def _tree_state(n, T, A, seed):
 
 
 def _set_hist_version(monkeypatch, ver):
-    """ver: 1..4 kernel generation; 43 / 44 = v4 integer kernel with the v3 / rotated lane mapping."""
-    monkeypatch.setattr(K, "HIST_VERSION", 4 if ver in (43, 44) else max(ver, 2))
-    monkeypatch.setattr(K, "HIST_MAP", {43: 3, 44: 4}.get(ver, 2))
+    """ver: 1..4 kernel generation; 43 / 44 = v4 integer kernel with the v3 / rotated lane mapping;
+    45 = packed single-atomic regression kernel; 46 = fast rotated kernel (hist4f)."""
+    monkeypatch.setattr(K, "HIST_VERSION", 4 if ver in (43, 44, 45, 46) else max(ver, 2))
+    monkeypatch.setattr(K, "HIST_MAP", {43: 3, 44: 4, 45: 4, 46: 5}.get(ver, 2))
+    monkeypatch.setattr(K, "HIST_PACKED", ver == 45)
 
 
 @pytest.mark.parametrize("B", [40, 256])
-@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43, 44])
+@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43, 44, 45, 46])
 def test_hist_moments(dev, B, ver, monkeypatch):
     n, d, T, A = 20000, 19, 3, 12
     g = torch.Generator().manual_seed(B)
@@ -129,7 +131,7 @@ def test_hist_moments(dev, B, ver, monkeypatch):
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43, 44])
+@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43, 44, 46])
 def test_hist_classes(dev, ver, monkeypatch):
     n, d, T, A, C, B = 10000, 10, 2, 8, 3, 32
     g = torch.Generator().manual_seed(11)
@@ -165,7 +167,8 @@ def test_hist_moments_v0(dev, ver, monkeypatch):
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-3)
 
 
-def test_hist_v4_deterministic(dev, monkeypatch):
+@pytest.mark.parametrize("ver", [4, 45, 46])
+def test_hist_v4_deterministic(dev, ver, monkeypatch):
     """Integer histograms are bit-identical across launches with different chunkings."""
     n, d, T, A, B = 50000, 16, 2, 4, 32
     g = torch.Generator().manual_seed(8)
@@ -174,7 +177,7 @@ def test_hist_v4_deterministic(dev, monkeypatch):
     bins = K.binize(X, thr, nthr).to(dev)
     node, build, slot_tree = _tree_state(n, T, A, 2)
     y = torch.randn(n, generator=g).to(dev)
-    _set_hist_version(monkeypatch, 4)
+    _set_hist_version(monkeypatch, ver)
     it = np.arange(A) // (A // T)
     a = K.hist_moments(bins, d, node.to(dev), None, None, y, build.to(dev), slot_tree, None, B, id_tree=it)
     b = K.hist_moments(bins, d, node.to(dev), None, None, y, build.to(dev), slot_tree, None, B, lds_budget=4096,
