@@ -99,7 +99,44 @@ def main():
     ]
     if args.variants != "all":
         configs = [c for c in configs if any(v in c[0] for v in args.variants.split(","))]
+    configs = [("L0 T20 full   codes pk4", 20, 1, False, True, 7, 4, 65536),
+               ("L4 T20 full   codes pk4", 20, 16, False, True, 7, 4, 65536),
+               ("L0 T20 full   codes pk8 48K", 20, 1, False, True, 7, 8, 49152),
+               ("L0 T20 full   codes pk8", 20, 1, False, True, 7, 8, 65536),
+               ("L0 T20 full   codes pk16", 20, 1, False, True, 7, 16, 65536),
+               ("L1 T20 full   codes pk8", 20, 2, False, True, 7, 8, 65536),
+               ("L4 T20 full   codes pk8", 20, 16, False, True, 7, 8, 65536),
+               ("L4 T20 masked codes pk8", 20, 16, True, True, 7, 8, 65536),
+               ("L0 T20 full   codes", 20, 1, False, True, 6, 0, 65536),
+               ("L1 T20 full   codes", 20, 2, False, True, 6, 0, 65536),
+               ("L4 T20 full   codes", 20, 16, False, True, 6, 0, 65536),
+               ("L0 T20 masked codes", 20, 1, True, True, 6, 0, 65536),
+               ("L4 T20 masked codes", 20, 16, True, True, 6, 0, 65536)] + configs
+    if args.variants != "all":
+        configs = [c for c in configs if any(v in c[0] for v in args.variants.split(","))]
     for name, T, L, masked, wts, ver, lmap, lds in configs:
+        if ver in (6, 7):
+            K.HIST5_PACKED = ver == 7
+            K.HIST5_PACKED_MAXT = lmap if ver == 7 else 8
+            bins, node, w, y, build, st, it, fm = make_state(n, d, T, L, B, masked)
+            codes = K.codes_init(w, T, n, "cuda")
+            loc = node - (torch.arange(T, device="cuda", dtype=torch.int32) * L)[:, None]
+            c = codes.to(torch.int32) & 0xFFFF
+            loc = torch.where((c & 0xFF) == 0xFF, torch.full_like(loc, 0xFF), loc)
+            codes = ((c & 0xFF00) | loc).to(torch.int16).contiguous()
+            tfirst = torch.arange(T, dtype=torch.int32) * L
+            del node
+            fn = lambda: K.hist_codes(0, bins, d, codes, tfirst, None, y, None, 0, build, st, it, fm, B,  # noqa: E731
+                                      lds_budget=lds)
+            ms = timeit(fn, args.reps)
+            frac_w = float((w > 0).float().mean())
+            feats = int(np.ceil(d / 3)) if masked else d
+            upd = n * T * frac_w * feats
+            print(f"{name:28s} {ms:9.2f} ms  {upd / ms * 1e3:9.3e} upd/s  ({upd:.2e} row-tree-feature updates)",
+                  flush=True)
+            del bins, codes, w, y
+            torch.cuda.empty_cache()
+            continue
         bins, node, w, y, build, st, it, fm = make_state(n, d, T, L, B, masked)
         K.HIST_VERSION = min(ver, 4)
         K.HIST_PACKED = ver == 5

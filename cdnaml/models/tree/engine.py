@@ -37,6 +37,8 @@ from ...utils import tracing as _tr
 from ..util import IllegalArgumentException
 
 HIST_MODE = __import__("os").environ.get("CDNAML_RF_HIST", "full")
+# compact uint16 row records (hist5.hip) instead of int32 node ids + uint8 weights
+USE_CODES = __import__("os").environ.get("CDNAML_TREE_CODES", "1") != "0"
 
 
 @dataclass
@@ -523,8 +525,14 @@ class ForestTrainer:
         # "full": accumulate all features, derive larger siblings by subtraction, mask at split time.
         masked = need_masks and HIST_MODE == "masked"
         subtract = not masked
-        node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
-            torch.zeros((T, 0), dtype=torch.int32, device=dev)
+        # row records (uint16 weight<<8 | local node) when every level fits 255 nodes per tree
+        use_codes = USE_CODES and p.max_depth <= 8
+        if use_codes:
+            codes = K.codes_init(weights, T, n, dev)
+            node = None
+        else:
+            node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
+                torch.zeros((T, 0), dtype=torch.int32, device=dev)
         # active entries: dict(tree, fid (forest node idx), key, mask, parent_hist_idx, build, stats)
         active = [{"tree": t, "fid": None, "key": 1, "depth": 0, "stats": None, "sib": None, "parent": None}
                   for t in range(T)]
@@ -559,8 +567,13 @@ class ForestTrainer:
                 fm_build = torch.from_numpy(masks_np[build_ids].view(np.int32)).to(dev)
             build_slot = torch.from_numpy(slot_of).to(dev)
             id_tree = np.array([e["tree"] for e in active], dtype=np.int32)
+            tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
-                if self.classification:
+                if use_codes:
+                    Hb = K.hist_codes(1 if self.classification else 0, data.bins, d, codes, tfirst,
+                                      stats_rows.get("v0"), stats_rows.get("v1"), stats_rows.get("label"), self.C,
+                                      build_slot, slot_tree, id_tree, fm_build, B)
+                elif self.classification:
                     Hb = K.hist_classes(data.bins, d, node, weights, stats_rows["label"], self.C, build_slot,
                                         slot_tree, fm_build, B, id_tree=id_tree)
                 else:
@@ -670,9 +683,17 @@ class ForestTrainer:
             if nxt:
                 cm = np.stack(cat_masks).view(np.int32) if cat_masks else np.zeros((0, 8), np.int32)
                 with _tr.span("tree.partition", depth=depth):
-                    K.partition(data.bins, node, torch.from_numpy(split_feat).to(dev),
-                                torch.from_numpy(split_bin).to(dev), torch.from_numpy(cat_off).to(dev),
-                                torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child).to(dev))
+                    if use_codes:
+                        nxt_tree = np.array([e["tree"] for e in nxt], dtype=np.int32)
+                        tfirst_next = torch.from_numpy(
+                            np.searchsorted(nxt_tree, np.arange(T), side="left").astype(np.int32))
+                        K.partition_codes(data.bins, codes, tfirst, tfirst_next, torch.from_numpy(split_feat),
+                                          torch.from_numpy(split_bin), torch.from_numpy(cat_off),
+                                          torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child))
+                    else:
+                        K.partition(data.bins, node, torch.from_numpy(split_feat).to(dev),
+                                    torch.from_numpy(split_bin).to(dev), torch.from_numpy(cat_off).to(dev),
+                                    torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child).to(dev))
             prev_hist = H if subtract else None
             active = nxt
         forest.roots.extend(root_ids)

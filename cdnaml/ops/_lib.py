@@ -79,6 +79,12 @@ _SIGS = {
                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,
                     c_void_p, c_void_p], c_int),
     "cdna_hist4_bytes_per_bin": ([c_int, c_int], c_int),
+    "cdna_hist5": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                    c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,
+                    c_void_p, c_void_p], c_int),
+    "cdna_hist5_max_trees": ([], c_int),
+    "cdna_partition5": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p], c_int),
     "cdna_partition": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p], c_int),
     "cdna_tree_predict": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_void_p,

@@ -153,6 +153,9 @@ HIST_VERSION = int(__import__("os").environ.get("CDNAML_HIST_VERSION", "4"))
 HIST_MAP = int(__import__("os").environ.get("CDNAML_HIST_MAP", "5"))
 # regression histograms: one packed (count | offset sum) ds_add_u64 per update (hist4.hip hist4p_kernel)
 HIST_PACKED = __import__("os").environ.get("CDNAML_HIST_PACKED", "0") != "0"
+# hist v5 (row records): packed single-atomic regression histograms, trees per block group when packed
+HIST5_PACKED = __import__("os").environ.get("CDNAML_HIST5_PACKED", "1") != "0"
+HIST5_PACKED_MAXT = int(__import__("os").environ.get("CDNAML_HIST5_PACKED_MAXT", "8"))
 
 
 def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int, qmax_bits: int = 62) -> float:
@@ -374,6 +377,134 @@ def hist_classes(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optiona
         wx = w[ok][:, None].expand_as(idx)
         flat += torch.bincount(idx[msk], weights=wx[msk], minlength=flat.shape[0])
     return out
+
+
+# ------------------------------------------------------------ K5/K7 on row records
+CODE_DONE = 0xFF
+
+
+def codes_init(weights: Optional[torch.Tensor], T: int, n: int, device) -> torch.Tensor:
+    """Row records for level 0: code[r, t] = weight << 8 | local (0 = the root, 255 = done).
+
+    Returned as int16 [T, n] holding the uint16 bit patterns (hist5.hip)."""
+    if weights is None:
+        w = torch.ones((T, n), dtype=torch.int32, device=device)
+    else:
+        w = weights.to(device=device).to(torch.int32)
+    c = (w << 8) | torch.where(w == 0, torch.full_like(w, CODE_DONE), torch.zeros_like(w))
+    return c.to(torch.int16).contiguous()
+
+
+def decode_codes(codes: torch.Tensor, tfirst: torch.Tensor):
+    """codes [T, n] -> (node ids int32 [T, n] with -1 = done, weights uint8 [T, n])."""
+    c = codes.to(torch.int32) & 0xFFFF
+    loc = c & 0xFF
+    w = (c >> 8).to(torch.uint8)
+    ids = tfirst.to(c.device).to(torch.int32)[:, None] + loc
+    ids = torch.where((loc == CODE_DONE) | (w == 0), torch.full_like(ids, -1), ids)
+    return ids.contiguous(), w.contiguous()
+
+
+def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirst: torch.Tensor,
+               v0: Optional[torch.Tensor], v1: Optional[torch.Tensor], label: Optional[torch.Tensor], C: int,
+               build_slot: torch.Tensor, slot_tree: np.ndarray, id_tree: np.ndarray,
+               feat_mask: Optional[torch.Tensor], B: int, lds_budget: Optional[int] = None) -> torch.Tensor:
+    """Histograms from row records (hist5.hip).  mode 0: moments [S, d, B, 2]; 1: classes [S, d, B, C]."""
+    S = len(slot_tree)
+    G, n, _ = bins.shape
+    T = codes.shape[0] if codes.dim() == 2 else 0
+    K_ = 2 if mode == 0 else C
+    out = torch.zeros((S, d, B, K_), dtype=torch.float64, device=bins.device)
+    if S == 0 or n == 0:
+        return out
+    if not _native(bins):
+        node, w = decode_codes(codes, tfirst)
+        if mode == 0:
+            return hist_moments(bins, d, node, w, v0, v1, build_slot, slot_tree, feat_mask, B)
+        return hist_classes(bins, d, node, w, label, C, build_slot, slot_tree, feat_mask, B)
+    lib = _lib.lib()
+    maxt = int(lib.cdna_hist5_max_trees())
+    packed = HIST5_PACKED and mode == 0 and v0 is None
+    kbits = mode | (4 if (mode == 0 and v0 is not None) else 0) | (16 if packed else 0)
+    per_slot = 8 * B * int(lib.cdna_hist4_bytes_per_bin(kbits, int(C)))
+    if per_slot > 150 * 1024:
+        raise ValueError("histogram too large for LDS (classes x bins)")
+    budget = lds_budget or HIST_LDS_BUDGET
+    if packed:
+        budget = min(budget, 8192 * 8)  # register drain: <= 16 cells per thread
+        maxt = min(maxt, HIST5_PACKED_MAXT)
+    SB = max(1, min(S, budget // per_slot))
+    slot_tree = np.asarray(slot_tree)
+    id_tree = np.asarray(id_tree)
+    rows = []
+    a = 0
+    while a < S:
+        b = min(S, a + SB)
+        # at most `maxt` trees per group (prefetched row record)
+        t0 = int(slot_tree[a])
+        b = min(b, int(np.searchsorted(slot_tree, t0 + maxt, side="left")))
+        t1 = int(slot_tree[b - 1])
+        i0 = int(np.searchsorted(id_tree, t0, side="left"))
+        i1 = int(np.searchsorted(id_tree, t1, side="right"))
+        rows.append((a, t0, t1, i0, i1))
+        a = b
+    grp = torch.tensor(rows, dtype=torch.int32, device=bins.device).reshape(-1)
+    ng = len(rows)
+    max_nt = max(r[2] - r[1] + 1 for r in rows)
+    bucket = 1 if max_nt <= 1 else 2 if max_nt <= 2 else 4 if max_nt <= 4 else 8 if max_nt <= 8 else 16
+    lds_used = ((SB * per_slot + 15) // 16) * 16 + bucket * 512 + SB + 16
+    if lds_used > 160 * 1024:
+        raise ValueError("local-node tables do not fit in LDS next to the histogram")
+    nchunk = int(max(1, min((1024 + G * ng - 1) // (G * ng), (n + 8191) // 8192)))
+    nchunk = max(nchunk, -(-n // (1 << 23)))
+    mw = 0 if feat_mask is None else feat_mask.shape[1]
+    fm = None if feat_mask is None else feat_mask.int().contiguous()
+    v0 = None if v0 is None else v0.float().contiguous()
+    v1 = None if v1 is None else v1.float().contiguous()
+    label = None if label is None else label.int().contiguous()
+    wmax = 255
+    qs0 = _fixed_scale(v0, n, wmax, qmax_bits=30)
+    qs1 = _packed_scale(v1) if packed else _fixed_scale(v1, n, wmax, qmax_bits=30)
+    iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
+    assert codes.dtype == torch.int16 and codes.is_contiguous() and codes.shape[1] == n
+    tf = tfirst.to(device=bins.device, dtype=torch.int32).contiguous()
+    bs = build_slot.int().contiguous()
+    _lib.check(lib.cdna_hist5(kbits, _ptr(bins), n, d, T, _ptr(codes), _ptr(tf), _ptr(v0), _ptr(v1), _ptr(label),
+                              int(C), _ptr(bs), _ptr(fm), mw, S, B, SB, _ptr(grp), ng, nchunk, max_nt, qs0, qs1,
+                              _ptr(iout), _stream(bins.device)), "cdna_hist5")
+    out.copy_(iout)
+    if mode == 0:
+        if v0 is not None:
+            out[..., 0] /= qs0
+        out[..., 1] /= qs1
+    return out
+
+
+def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tensor, tfirst_next: torch.Tensor,
+                    split_feat: torch.Tensor, split_bin: torch.Tensor, cat_off: torch.Tensor,
+                    cat_mask: torch.Tensor, child: torch.Tensor) -> None:
+    """In place: every row's code moves to the chosen child's local index (255 = done)."""
+    G, n, _ = bins.shape
+    T = codes.shape[0]
+    if n == 0 or T == 0:
+        return
+    if _native(bins):
+        cm = cat_mask.int().contiguous() if cat_mask.numel() else torch.zeros(8, dtype=torch.int32,
+                                                                                 device=bins.device)
+        args = [t.to(device=bins.device, dtype=torch.int32).contiguous()
+                for t in (tfirst, tfirst_next, split_feat, split_bin, cat_off, child)]
+        _lib.check(_lib.lib().cdna_partition5(_ptr(bins), n, T, _ptr(codes), _ptr(args[0]), _ptr(args[1]),
+                                              _ptr(args[2]), _ptr(args[3]), _ptr(args[4]), _ptr(cm),
+                                              _ptr(args[5]), _stream(bins.device)), "cdna_partition5")
+        return
+    node, w = decode_codes(codes, tfirst)
+    live = node >= 0
+    partition(bins, node, split_feat, split_bin, cat_off, cat_mask, child)
+    tn = tfirst_next.to(torch.int32)[:, None]
+    loc = torch.where(node >= 0, node - tn, torch.full_like(node, CODE_DONE))
+    loc = torch.where(live, loc, torch.full_like(loc, CODE_DONE))
+    c = (w.to(torch.int32) << 8) | loc
+    codes.copy_(c.to(torch.int16))
 
 
 # --------------------------------------------------------------------- K7

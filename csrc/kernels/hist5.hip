@@ -1,0 +1,587 @@
+// K5/K7 on compact row records: hist v5 + partition over uint16 "codes".
+//
+// v4 (hist4f) loaded, per (row, tree) and per 8-feature block, a 4-byte node id
+// and a 1-byte bootstrap weight from two [T][n] arrays: at level 0 with 20
+// trees that is 13 feature blocks x 20 x 5 B = 1.3 KB of loads per row, the
+// dominant traffic of the kernel (profiles/pmc_hist4_1e8.csv: 62 % of wave
+// time waiting on vector memory).  v5 keeps ONE uint16 per (row, tree):
+//
+//     code = weight << 8 | local        local = node index within its tree's
+//                                       active set at this level, 255 = done
+//
+// stored tree-major ([T][n], like the int32 node ids it replaces) so every
+// per-tree load of a wave is one coalesced 128-byte line (a row-major record
+// was measured slower at deep levels, where a block touches only 1-2 trees).
+// The global active id is tfirst[t] + local (tfirst = first active id of
+// tree t, a per-level table).  Rows with zero
+// bootstrap weight are "done" from the start and never touch LDS.  The
+// histogram inner loop is hist4f's (rotated features, hoisted VALU work,
+// batched slot-table reads); the next row's record is prefetched.
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 512;
+constexpr int kMaxTrees = 16;  // trees per block group (host splits larger groups)
+
+struct Hist5Args {
+  const uint64_t* bins;  // [G][n] 8 bins per word
+  int64_t n;
+  int d, T;
+  const uint16_t* codes;  // [T][n]
+  const int* tfirst;      // [T] first active id of each tree at this level
+  const float* v0;
+  const float* v1;
+  const int* label;
+  int C;
+  const int* build_slot;  // [A] slot or -1
+  const uint32_t* feat_mask;
+  int mask_words, S, B, SB, K;
+  const int* grp;  // [ngroups][5] = s0, t0, t1, id0, id1
+  int ngroups, nchunk;
+  int64_t rows_per_chunk;
+  float qs0, qs1;
+  int n64, n32;
+  unsigned long long* out;  // [S][d][B][K]
+};
+
+// MODE 0: moments (count u32 + sum u64, or with V0 two u64 sums); MODE 1: class counts (u32).
+template <int MODE, bool MASKED, bool V0, int NT>
+__global__ __launch_bounds__(kThreads) void hist5_kernel(const Hist5Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int G = (a.d + 7) / 8;
+  const int plane = a.SB * 8 * a.B;
+  unsigned long long* h64 = reinterpret_cast<unsigned long long*>(smem);
+  uint32_t* h32 = reinterpret_cast<uint32_t*>(h64 + (size_t)a.n64 * plane);
+  const int hwords = a.n32 * plane;
+  // per-tree local-node -> slot table: lt[k][loc] = slot - s0 or -1 (loc 255 = done)
+  int16_t* lt = reinterpret_cast<int16_t*>(h32 + ((hwords + 3) & ~3));
+  const uint32_t w = cdna::xcd_remap(blockIdx.x, gridDim.x);
+  const int g = (int)(w % G);
+  const int grp = (int)((w / G) % a.ngroups);
+  const int chunk = (int)(w / ((uint32_t)G * a.ngroups));
+  const int s0 = a.grp[grp * 5 + 0], t0 = a.grp[grp * 5 + 1], t1 = a.grp[grp * 5 + 2];
+  const int id1 = a.grp[grp * 5 + 4];
+  const int nt = t1 - t0 + 1;  // <= kMaxTrees (host-checked)
+  uint8_t* lmask = reinterpret_cast<uint8_t*>(lt + NT * 256);
+  const int fbase = g * 8;
+  const int rot = threadIdx.x & 7;
+
+  for (int i = threadIdx.x; i < a.n64 * plane; i += kThreads) h64[i] = 0ull;
+  for (int i = threadIdx.x; i < hwords; i += kThreads) h32[i] = 0u;
+  for (int i = threadIdx.x; i < NT * 256; i += kThreads) {
+    const int k = i >> 8, loc = i & 255;
+    int v = -1;
+    const int id = k < nt ? a.tfirst[t0 + k] + loc : 0;
+    const int idend = k + 1 < nt ? a.tfirst[t0 + k + 1] : id1;
+    if (k < nt && loc != 255 && id < idend) {
+      const int sl = a.build_slot[id];
+      if (sl >= s0 && sl < s0 + a.SB) v = sl - s0;
+    }
+    lt[i] = (int16_t)v;
+  }
+  if (MASKED) {
+    for (int i = threadIdx.x; i < a.SB; i += kThreads) {
+      const int slot = s0 + i;
+      uint32_t m = 0u;
+      if (slot < a.S) m = (a.feat_mask[(int64_t)slot * a.mask_words + (fbase >> 5)] >> (fbase & 31)) & 0xFFu;
+      const int valid = a.d - fbase;
+      if (valid < 8) m &= (1u << (valid > 0 ? valid : 0)) - 1u;
+      lmask[i] = (uint8_t)m;
+    }
+  }
+  int fsel[8], fsh[8], foff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int jj = (j + rot) & 7;
+    fsel[j] = jj >> 2;
+    fsh[j] = (jj & 3) * 8;
+    foff[j] = jj * a.B;
+  }
+  // features beyond d in the last block
+  const int valid_f = a.d - fbase;
+  uint32_t fvalid = valid_f >= 8 ? 0xFFu : ((1u << (valid_f > 0 ? valid_f : 0)) - 1u);
+  const uint32_t frot = ((fvalid >> rot) | (fvalid << (8 - rot))) & 0xFFu;
+  __syncthreads();
+
+  const int64_t rb = (int64_t)chunk * a.rows_per_chunk;
+  int64_t re = rb + a.rows_per_chunk;
+  if (re > a.n) re = a.n;
+  const int64_t n = a.n;
+  const int slot_cells = 8 * a.B;
+
+  uint64_t b8 = 0;
+  float x0 = 1.f, x1 = 0.f;
+  int lab = 0;
+  uint32_t cd[NT];
+  // trees past nt read a valid row (their tables are all -1, so they never add)
+  const int64_t tstride = (int64_t)n;
+  auto load_row = [&](int64_t rr, uint64_t& ob8, float& ox0, float& ox1, int& olab, uint32_t* ocd) {
+    ob8 = a.bins[(int64_t)g * n + rr];
+    if (MODE == 0) {
+      if (V0) ox0 = a.v0[rr];
+      ox1 = a.v1[rr];
+    } else {
+      olab = a.label[rr];
+    }
+    const uint16_t* cp = a.codes + (int64_t)t0 * n + rr;
+#pragma unroll
+    for (int k = 0; k < NT; ++k) ocd[k] = (uint32_t)cp[(k < nt ? k : 0) * tstride];
+  };
+  int64_t r = rb + threadIdx.x;
+  if (r < re) load_row(r, b8, x0, x1, lab, cd);
+  else {
+#pragma unroll
+    for (int k = 0; k < NT; ++k) cd[k] = 0xFFu;
+  }
+
+  for (; r < re; r += kThreads) {
+    uint64_t nb8 = 0;
+    float nx0 = 1.f, nx1 = 0.f;
+    int nlab = 0;
+    uint32_t ncd[NT];
+    const int64_t rn = r + kThreads;
+    if (rn < re) load_row(rn, nb8, nx0, nx1, nlab, ncd);
+    else {
+#pragma unroll
+      for (int k = 0; k < NT; ++k) ncd[k] = 0xFFu;
+    }
+
+    const uint32_t lo = (uint32_t)b8, hi = (uint32_t)(b8 >> 32);
+    int cell[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      cell[j] = foff[j] + (int)__builtin_amdgcn_ubfe(fsel[j] ? hi : lo, (uint32_t)fsh[j], 8u);
+    int q0 = 1, q1 = 0;
+    bool row_ok = true;
+    if (MODE == 0) {
+      if (V0) q0 = (int)rintf(x0 * a.qs0);
+      q1 = (int)rintf(x1 * a.qs1);
+    } else {
+      row_ok = lab >= 0 && lab < a.C;
+    }
+    const uint32_t cbase_lab = MODE == 1 ? (uint32_t)(lab * plane) : 0u;
+    if (row_ok) {
+      constexpr int KB = NT;  // all slot-table reads of the row first: one LDS wait per row
+#pragma unroll
+      for (int kb = 0; kb < NT; kb += KB) {
+        int lsk[KB];
+        uint32_t mk[KB];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          lsk[k] = lt[(kb + k) * 256 + (int)(cd[kb + k] & 0xFFu)];  // -1: done / not built here
+          if (MASKED) mk[k] = lmask[lsk[k] < 0 ? 0 : lsk[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const int ls = lsk[k];
+          if (ls < 0) continue;
+          const uint32_t wv = cd[kb + k] >> 8;
+          const uint32_t base = (uint32_t)(ls * slot_cells) + cbase_lab;
+          uint32_t mrot = frot;
+          if (MASKED) mrot &= ((mk[k] >> rot) | (mk[k] << (8 - rot))) & 0xFFu;
+          const long long y1 = (long long)wv * (long long)q1;
+          const long long y0 = V0 ? (long long)wv * (long long)q0 : 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if (!((mrot >> j) & 1u)) continue;
+            const uint32_t c = base + (uint32_t)cell[j];
+            if (MODE == 1) {
+              atomicAdd(h32 + c, wv);
+            } else if (V0) {
+              atomicAdd(h64 + c, (unsigned long long)y0);
+              atomicAdd(h64 + plane + c, (unsigned long long)y1);
+            } else {
+              atomicAdd(h32 + c, wv);
+              atomicAdd(h64 + c, (unsigned long long)y1);
+            }
+          }
+        }
+      }
+    }
+    b8 = nb8;
+    x0 = nx0;
+    x1 = nx1;
+    lab = nlab;
+#pragma unroll
+    for (int k = 0; k < NT; ++k) cd[k] = ncd[k];
+  }
+  __syncthreads();
+  // flush: 64-bit planes first (k = 1 for count+sum moments, k = p with V0), then 32-bit planes
+  const int total = (a.n64 + a.n32) * plane;
+  for (int i = threadIdx.x; i < total; i += kThreads) {
+    const bool is64 = i < a.n64 * plane;
+    const int p = is64 ? i / plane : (i - a.n64 * plane) / plane;
+    const int rem = i - (is64 ? p : a.n64 + p) * plane;
+    long long v;
+    int k;
+    if (is64) {
+      v = (long long)h64[i];
+      k = (MODE == 0 && !V0) ? 1 : p;
+    } else {
+      v = (long long)h32[i - a.n64 * plane];
+      k = p;
+    }
+    if (v == 0) continue;
+    const int ls = rem / (8 * a.B);
+    const int jj = (rem / a.B) & 7;
+    const int bn = rem % a.B;
+    const int f = fbase + jj;
+    const int slot = s0 + ls;
+    if (f < a.d && slot < a.S)
+      atomicAdd(&a.out[(((int64_t)slot * a.d + f) * a.B + bn) * a.K + k], (unsigned long long)v);
+  }
+}
+
+// Packed regression variant (measured motive: the two-atomic kernel reaches
+// ~3.5 of the ~4 LDS atomic lane-ops/clk/CU at full levels): ONE ds_add_u64
+// per update holding count (bits 44..63) | sum of w * (q + 2^23) (bits 0..43).
+// Every kPackIters * 512 = 4096 rows the block drains its words into
+// per-thread registers (uint32 count, int64 sum), so count <= 255 * 4096 < 2^20
+// and the offset sum < 4096 * 255 * 2^24 = 2^44: no field can overflow.
+constexpr int kPackShift = 44;
+constexpr int kPackQ = 1 << 23;
+constexpr int kPackIters = 8;
+constexpr int kPackCells = 16;  // plane <= 16 * 512 = 8192 cells (64 KB)
+
+template <bool MASKED, int NT>
+__global__ __launch_bounds__(kThreads) void hist5p_kernel(const Hist5Args a) {
+  constexpr int MODE = 0;
+  constexpr bool V0 = false;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int G = (a.d + 7) / 8;
+  const int plane = a.SB * 8 * a.B;
+  unsigned long long* h64 = reinterpret_cast<unsigned long long*>(smem);
+  uint32_t* h32 = reinterpret_cast<uint32_t*>(h64 + (size_t)plane);
+  const int hwords = 0;
+  // per-tree local-node -> slot table: lt[k][loc] = slot - s0 or -1 (loc 255 = done)
+  int16_t* lt = reinterpret_cast<int16_t*>(h32 + ((hwords + 3) & ~3));
+  const uint32_t w = cdna::xcd_remap(blockIdx.x, gridDim.x);
+  const int g = (int)(w % G);
+  const int grp = (int)((w / G) % a.ngroups);
+  const int chunk = (int)(w / ((uint32_t)G * a.ngroups));
+  const int s0 = a.grp[grp * 5 + 0], t0 = a.grp[grp * 5 + 1], t1 = a.grp[grp * 5 + 2];
+  const int id1 = a.grp[grp * 5 + 4];
+  const int nt = t1 - t0 + 1;  // <= kMaxTrees (host-checked)
+  uint8_t* lmask = reinterpret_cast<uint8_t*>(lt + NT * 256);
+  const int fbase = g * 8;
+  const int rot = threadIdx.x & 7;
+
+  for (int i = threadIdx.x; i < plane; i += kThreads) h64[i] = 0ull;
+  uint32_t acc_c[kPackCells];
+  long long acc_s[kPackCells];
+#pragma unroll
+  for (int i = 0; i < kPackCells; ++i) {
+    acc_c[i] = 0u;
+    acc_s[i] = 0;
+  }
+  for (int i = threadIdx.x; i < hwords; i += kThreads) h32[i] = 0u;
+  for (int i = threadIdx.x; i < NT * 256; i += kThreads) {
+    const int k = i >> 8, loc = i & 255;
+    int v = -1;
+    const int id = k < nt ? a.tfirst[t0 + k] + loc : 0;
+    const int idend = k + 1 < nt ? a.tfirst[t0 + k + 1] : id1;
+    if (k < nt && loc != 255 && id < idend) {
+      const int sl = a.build_slot[id];
+      if (sl >= s0 && sl < s0 + a.SB) v = sl - s0;
+    }
+    lt[i] = (int16_t)v;
+  }
+  if (MASKED) {
+    for (int i = threadIdx.x; i < a.SB; i += kThreads) {
+      const int slot = s0 + i;
+      uint32_t m = 0u;
+      if (slot < a.S) m = (a.feat_mask[(int64_t)slot * a.mask_words + (fbase >> 5)] >> (fbase & 31)) & 0xFFu;
+      const int valid = a.d - fbase;
+      if (valid < 8) m &= (1u << (valid > 0 ? valid : 0)) - 1u;
+      lmask[i] = (uint8_t)m;
+    }
+  }
+  int fsel[8], fsh[8], foff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int jj = (j + rot) & 7;
+    fsel[j] = jj >> 2;
+    fsh[j] = (jj & 3) * 8;
+    foff[j] = jj * a.B;
+  }
+  // features beyond d in the last block
+  const int valid_f = a.d - fbase;
+  uint32_t fvalid = valid_f >= 8 ? 0xFFu : ((1u << (valid_f > 0 ? valid_f : 0)) - 1u);
+  const uint32_t frot = ((fvalid >> rot) | (fvalid << (8 - rot))) & 0xFFu;
+  __syncthreads();
+
+  const int64_t rb = (int64_t)chunk * a.rows_per_chunk;
+  int64_t re = rb + a.rows_per_chunk;
+  if (re > a.n) re = a.n;
+  const int64_t n = a.n;
+  const int slot_cells = 8 * a.B;
+
+  uint64_t b8 = 0;
+  float x0 = 1.f, x1 = 0.f;
+  int lab = 0;
+  uint32_t cd[NT];
+  // trees past nt read a valid row (their tables are all -1, so they never add)
+  const int64_t tstride = (int64_t)n;
+  auto load_row = [&](int64_t rr, uint64_t& ob8, float& ox0, float& ox1, int& olab, uint32_t* ocd) {
+    ob8 = a.bins[(int64_t)g * n + rr];
+    if (MODE == 0) {
+      if (V0) ox0 = a.v0[rr];
+      ox1 = a.v1[rr];
+    } else {
+      olab = a.label[rr];
+    }
+    const uint16_t* cp = a.codes + (int64_t)t0 * n + rr;
+#pragma unroll
+    for (int k = 0; k < NT; ++k) ocd[k] = (uint32_t)cp[(k < nt ? k : 0) * tstride];
+  };
+  auto drain = [&]() {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPackCells; ++i) {
+      const int idx = (int)threadIdx.x + i * kThreads;
+      if (idx < plane) {
+        const unsigned long long v = h64[idx];
+        if (v) {
+          const uint32_t c = (uint32_t)(v >> kPackShift);
+          acc_c[i] += c;
+          acc_s[i] += (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)c;
+          h64[idx] = 0ull;
+        }
+      }
+    }
+    __syncthreads();
+  };
+  int64_t r = rb + threadIdx.x;
+  if (r < re) load_row(r, b8, x0, x1, lab, cd);
+  else {
+#pragma unroll
+    for (int k = 0; k < NT; ++k) cd[k] = 0xFFu;
+  }
+
+  int iter = 0;
+  for (int64_t rbase = rb; rbase < re; rbase += kThreads, r += kThreads, ++iter) {
+    if (r >= re) {
+#pragma unroll
+      for (int k = 0; k < NT; ++k) cd[k] = 0xFFu;  // tail lanes: no work, but keep the block in step
+    }
+    uint64_t nb8 = 0;
+    float nx0 = 1.f, nx1 = 0.f;
+    int nlab = 0;
+    uint32_t ncd[NT];
+    const int64_t rn = r + kThreads;
+    if (rn < re) load_row(rn, nb8, nx0, nx1, nlab, ncd);
+    else {
+#pragma unroll
+      for (int k = 0; k < NT; ++k) ncd[k] = 0xFFu;
+    }
+
+    const uint32_t lo = (uint32_t)b8, hi = (uint32_t)(b8 >> 32);
+    int cell[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      cell[j] = foff[j] + (int)__builtin_amdgcn_ubfe(fsel[j] ? hi : lo, (uint32_t)fsh[j], 8u);
+    int q1 = (int)rintf(x1 * a.qs1);
+    q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+    const unsigned long long qoff = (unsigned long long)(q1 + kPackQ);
+    const bool row_ok = true;
+    const uint32_t cbase_lab = MODE == 1 ? (uint32_t)(lab * plane) : 0u;
+    if (row_ok) {
+      constexpr int KB = NT;  // all slot-table reads of the row first: one LDS wait per row
+#pragma unroll
+      for (int kb = 0; kb < NT; kb += KB) {
+        int lsk[KB];
+        uint32_t mk[KB];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          lsk[k] = lt[(kb + k) * 256 + (int)(cd[kb + k] & 0xFFu)];  // -1: done / not built here
+          if (MASKED) mk[k] = lmask[lsk[k] < 0 ? 0 : lsk[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const int ls = lsk[k];
+          if (ls < 0) continue;
+          const uint32_t wv = cd[kb + k] >> 8;
+          const uint32_t base = (uint32_t)(ls * slot_cells) + cbase_lab;
+          uint32_t mrot = frot;
+          if (MASKED) mrot &= ((mk[k] >> rot) | (mk[k] << (8 - rot))) & 0xFFu;
+          const unsigned long long add = ((unsigned long long)wv << kPackShift) + (unsigned long long)wv * qoff;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if (!((mrot >> j) & 1u)) continue;
+            atomicAdd(h64 + base + (uint32_t)cell[j], add);
+          }
+        }
+      }
+    }
+    b8 = nb8;
+    x0 = nx0;
+    x1 = nx1;
+    lab = nlab;
+#pragma unroll
+    for (int k = 0; k < NT; ++k) cd[k] = ncd[k];
+    if ((iter + 1) % kPackIters == 0) drain();
+  }
+  drain();
+#pragma unroll
+  for (int i = 0; i < kPackCells; ++i) {
+    const int idx = (int)threadIdx.x + i * kThreads;
+    if (idx >= plane || acc_c[i] == 0u) continue;
+    const int ls = idx / (8 * a.B);
+    const int jj = (idx / a.B) & 7;
+    const int bn = idx % a.B;
+    const int f = fbase + jj;
+    const int slot = s0 + ls;
+    if (f < a.d && slot < a.S) {
+      unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+      atomicAdd(o, (unsigned long long)acc_c[i]);
+      atomicAdd(o + 1, (unsigned long long)acc_s[i]);
+    }
+  }
+}
+
+
+// Row-record partition: every row moves, in every tree, from its active node to
+// the chosen child (or finishes).  grid.y = tree, coalesced 2-byte codes.
+__global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restrict__ bins, int64_t n, int T,
+                                                         uint16_t* __restrict__ codes,
+                                                         const int* __restrict__ tfirst,
+                                                         const int* __restrict__ tfirst_next,
+                                                         const int* __restrict__ split_feat,
+                                                         const int* __restrict__ split_bin,
+                                                         const int* __restrict__ cat_off,
+                                                         const uint32_t* __restrict__ cat_mask,
+                                                         const int* __restrict__ child) {
+  const int t = blockIdx.y;
+  const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bins);
+  const int tf = tfirst[t], tfn = tfirst_next[t];
+  uint16_t* rec = codes + (int64_t)t * n;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
+    const uint32_t c = rec[r];
+    const uint32_t loc = c & 0xFFu;
+    if (loc == 0xFFu) continue;
+    const int id = tf + (int)loc;
+    const int f = split_feat[id];
+    uint32_t nloc = 0xFFu;
+    if (f >= 0) {
+      const int bin = b8[((int64_t)(f >> 3) * n + r) * 8 + (f & 7)];
+      const int co = cat_off[id];
+      const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u
+                                : bin <= split_bin[id];
+      const int ch = child[id * 2 + (left ? 0 : 1)];
+      if (ch >= 0) nloc = (uint32_t)(ch - tfn);
+    }
+    rec[r] = (uint16_t)((c & 0xFF00u) | nloc);
+  }
+}
+
+inline unsigned grid_for(int64_t n, int per, unsigned cap) {
+  int64_t b = (n + per - 1) / per;
+  return (unsigned)(b < (int64_t)cap ? (b < 1 ? 1 : b) : cap);
+}
+
+template <int MODE, bool MASKED, bool V0>
+void launch5(const Hist5Args& a, int nt_max, unsigned nblk, size_t lds, hipStream_t st) {
+  if (nt_max <= 1) hipLaunchKernelGGL((hist5_kernel<MODE, MASKED, V0, 1>), dim3(nblk), dim3(kThreads), lds, st, a);
+  else if (nt_max <= 2)
+    hipLaunchKernelGGL((hist5_kernel<MODE, MASKED, V0, 2>), dim3(nblk), dim3(kThreads), lds, st, a);
+  else if (nt_max <= 4)
+    hipLaunchKernelGGL((hist5_kernel<MODE, MASKED, V0, 4>), dim3(nblk), dim3(kThreads), lds, st, a);
+  else if (nt_max <= 8)
+    hipLaunchKernelGGL((hist5_kernel<MODE, MASKED, V0, 8>), dim3(nblk), dim3(kThreads), lds, st, a);
+  else
+    hipLaunchKernelGGL((hist5_kernel<MODE, MASKED, V0, 16>), dim3(nblk), dim3(kThreads), lds, st, a);
+}
+
+template <bool MASKED>
+void launch5p(const Hist5Args& a, int nt_max, unsigned nblk, size_t lds, hipStream_t st) {
+  if (nt_max <= 1) hipLaunchKernelGGL((hist5p_kernel<MASKED, 1>), dim3(nblk), dim3(kThreads), lds, st, a);
+  else if (nt_max <= 2) hipLaunchKernelGGL((hist5p_kernel<MASKED, 2>), dim3(nblk), dim3(kThreads), lds, st, a);
+  else if (nt_max <= 4) hipLaunchKernelGGL((hist5p_kernel<MASKED, 4>), dim3(nblk), dim3(kThreads), lds, st, a);
+  else if (nt_max <= 8) hipLaunchKernelGGL((hist5p_kernel<MASKED, 8>), dim3(nblk), dim3(kThreads), lds, st, a);
+  else hipLaunchKernelGGL((hist5p_kernel<MASKED, 16>), dim3(nblk), dim3(kThreads), lds, st, a);
+}
+
+inline int nt_bucket(int nt) { return nt <= 1 ? 1 : nt <= 2 ? 2 : nt <= 4 ? 4 : nt <= 8 ? 8 : 16; }
+
+}  // namespace
+
+CDNA_API int cdna_hist5_max_trees() { return kMaxTrees; }
+
+// mode bit0: classes; bit2: v0 present; bit4: packed single-atomic regression
+// (|v * qs1| <= 2^23, plane <= 8192 cells).  grp rows must satisfy t1 - t0 < 16;
+// `id_span_max` = max trees per group (sizes the LDS local -> slot tables).
+CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T, const uint16_t* codes,
+                        const int* tfirst, const float* v0, const float* v1, const int* label, int C,
+                        const int* build_slot, const uint32_t* feat_mask, int mask_words, int S, int B, int SB,
+                        const int* grp, int ngroups, int nchunk, int id_span_max, float qs0, float qs1,
+                        unsigned long long* out, hipStream_t st) {
+  if (n <= 0 || S <= 0) return 0;
+  Hist5Args a;
+  a.bins = bins;
+  a.n = n;
+  a.d = d;
+  a.T = T;
+  a.codes = codes;
+  a.tfirst = tfirst;
+  a.v0 = v0;
+  a.v1 = v1;
+  a.label = label;
+  a.C = C;
+  a.build_slot = build_slot;
+  a.feat_mask = feat_mask;
+  a.mask_words = mask_words;
+  a.S = S;
+  a.B = B;
+  a.SB = SB;
+  const bool classes = (mode & 1) != 0, has_v0 = (mode & 4) != 0;
+  a.K = classes ? C : 2;
+  a.n64 = classes ? 0 : (has_v0 ? 2 : 1);
+  a.n32 = classes ? C : (has_v0 ? 0 : 1);
+  a.grp = grp;
+  a.ngroups = ngroups;
+  a.nchunk = nchunk;
+  a.rows_per_chunk = (n + nchunk - 1) / nchunk;
+  if (a.rows_per_chunk * 255 >= (int64_t)1 << 32) return (int)hipErrorInvalidValue;
+  a.qs0 = qs0;
+  a.qs1 = qs1;
+  a.out = out;
+  const int G = (d + 7) / 8;
+  const size_t plane = (size_t)SB * 8 * B;
+  // id_span_max carries the max trees per group here (local -> slot tables of 256 int16 each)
+  const size_t lds = plane * 8 * a.n64 + ((plane * a.n32 + 3) & ~(size_t)3) * 4 +
+                     (size_t)nt_bucket(id_span_max) * 512 + SB + 16;
+  if (lds > 160 * 1024 || id_span_max > kMaxTrees) return (int)hipErrorInvalidValue;
+  const unsigned nblk = (unsigned)G * ngroups * nchunk;
+  const bool masked = feat_mask != nullptr;
+  const int ntm = id_span_max;
+  if (mode & 16) {  // packed single-atomic regression
+    if (classes || has_v0 || plane > (size_t)kPackCells * kThreads) return (int)hipErrorInvalidValue;
+    a.n64 = 1;
+    a.n32 = 0;
+    const size_t lds_p = plane * 8 + (size_t)nt_bucket(ntm) * 512 + SB + 16;
+    if (masked) launch5p<true>(a, ntm, nblk, lds_p, st);
+    else launch5p<false>(a, ntm, nblk, lds_p, st);
+    return (int)hipGetLastError();
+  }
+  if (classes) {
+    if (masked) launch5<1, true, false>(a, ntm, nblk, lds, st);
+    else launch5<1, false, false>(a, ntm, nblk, lds, st);
+  } else if (has_v0) {
+    if (masked) launch5<0, true, true>(a, ntm, nblk, lds, st);
+    else launch5<0, false, true>(a, ntm, nblk, lds, st);
+  } else {
+    if (masked) launch5<0, true, false>(a, ntm, nblk, lds, st);
+    else launch5<0, false, false>(a, ntm, nblk, lds, st);
+  }
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_partition5(const uint64_t* bins, int64_t n, int T, uint16_t* codes, const int* tfirst,
+                             const int* tfirst_next, const int* split_feat, const int* split_bin, const int* cat_off,
+                             const uint32_t* cat_mask, const int* child, hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  hipLaunchKernelGGL(partition5_kernel, dim3(grid_for(n, 256, 2048), T), dim3(256), 0, st, bins, n, T, codes, tfirst,
+                     tfirst_next, split_feat, split_bin, cat_off, cat_mask, child);
+  return (int)hipGetLastError();
+}

@@ -283,3 +283,76 @@ def test_score_hist(dev):
     s = torch.rand(50000, generator=g, dtype=torch.float64)
     lab = (torch.rand(50000, generator=g) > 0.3).double()
     assert torch.equal(K.score_hist(s, lab, 0.0, 1.0, 1000), K.score_hist(s.to(dev), lab.to(dev), 0.0, 1.0, 1000).cpu())
+
+
+def _codes_state(n, T, per, seed):
+    """Random row records: T trees with `per` active nodes each (tree-major ids)."""
+    g = torch.Generator().manual_seed(seed)
+    w = K.poisson_weights(T, n, seed, 0, 1.0)
+    codes = K.codes_init(w, T, n, "cpu")
+    loc = torch.randint(0, per, (T, n), generator=g, dtype=torch.int32)
+    done = torch.rand((T, n), generator=g) < 0.1
+    c = codes.to(torch.int32) & 0xFFFF
+    loc = torch.where(done | ((c & 0xFF) == 0xFF), torch.full_like(loc, 0xFF), loc)
+    codes = ((c & 0xFF00) | loc).to(torch.int16).contiguous()
+    tfirst = torch.arange(T, dtype=torch.int32) * per
+    A = T * per
+    build = torch.randint(-1, 2, (A,), generator=g, dtype=torch.int32)
+    slot_tree, s = [], 0
+    for i in range(A):
+        if build[i] >= 0:
+            build[i] = s
+            slot_tree.append(i // per)
+            s += 1
+    id_tree = np.arange(A) // per
+    return codes, tfirst, build, np.array(slot_tree, dtype=np.int32), id_tree
+
+
+@pytest.mark.parametrize("kind", ["moments", "moments_v0", "classes", "masked", "packed", "packed_masked"])
+def test_hist_codes(dev, kind, monkeypatch):
+    n, d, T, per, B, C = 30000, 21, 18, 5, 40, 3
+    g = torch.Generator().manual_seed(7)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    bins = K.binize(X, thr, nthr)
+    codes, tfirst, build, slot_tree, id_tree = _codes_state(n, T, per, 3)
+    S = len(slot_tree)
+    y = torch.randn(n, generator=g) * 10
+    h = torch.rand(n, generator=g)
+    lab = torch.randint(0, C, (n,), generator=g, dtype=torch.int32)
+    fm = None
+    monkeypatch.setattr(K, "HIST5_PACKED", kind.startswith("packed"))
+    if kind.endswith("masked"):
+        fm = torch.randint(0, 2 ** 31 - 1, (S, (d + 31) // 32), generator=g, dtype=torch.int64).to(torch.int32)
+    mode = 1 if kind == "classes" else 0
+    v0 = h if kind == "moments_v0" else None
+    ref = K.hist_codes(mode, bins, d, codes, tfirst, v0, y, lab, C, build, slot_tree, id_tree, fm, B)
+    out = K.hist_codes(mode, bins.to(dev), d, codes.to(dev), tfirst, None if v0 is None else v0.to(dev), y.to(dev),
+                       lab.to(dev), C, build.to(dev), slot_tree, id_tree, None if fm is None else fm.to(dev), B,
+                       lds_budget=16 * 1024).cpu()
+    assert torch.allclose(out, ref, rtol=1e-6, atol=1e-3)
+
+
+def test_partition_codes(dev):
+    n, d, T, per = 20000, 12, 6, 4
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(n, d, generator=g)
+    X[:, 3] = torch.randint(0, 20, (n,), generator=g).float()
+    thr, nthr = _thresholds(X, 32)
+    nthr[3] = -1
+    bins = K.binize(X, thr, nthr)
+    codes, tfirst, _, _, _ = _codes_state(n, T, per, 9)
+    A = T * per
+    sf = torch.randint(-1, d, (A,), generator=g, dtype=torch.int32)
+    sb = torch.randint(0, 30, (A,), generator=g, dtype=torch.int32)
+    co = torch.where(sf == 3, torch.arange(A, dtype=torch.int32) % 2, torch.full((A,), -1, dtype=torch.int32))
+    cm = torch.randint(0, 2 ** 31 - 1, (16,), generator=g, dtype=torch.int64).to(torch.int32)
+    # next level: 2 children per node, some finished
+    child = torch.arange(2 * A, dtype=torch.int32)
+    child[torch.rand(2 * A, generator=g) < 0.2] = -1
+    tfirst_next = torch.arange(T, dtype=torch.int32) * (2 * per)
+    a = codes.clone()
+    K.partition_codes(bins, a, tfirst, tfirst_next, sf, sb, co, cm, child)
+    b = codes.to(dev)
+    K.partition_codes(bins.to(dev), b, tfirst, tfirst_next, sf, sb, co, cm.to(dev), child)
+    assert torch.equal(a, b.cpu())
