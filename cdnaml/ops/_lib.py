@@ -83,11 +83,11 @@ _SIGS = {
                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,
                     c_void_p, c_void_p], c_int),
     "cdna_hist5_max_trees": ([], c_int),
-    "cdna_partition5": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_partition5": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_partition": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p], c_int),
-    "cdna_tree_predict": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+    "cdna_tree_predict": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p,
                            c_void_p, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_predict_binned_add": ([c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p,
                                  c_void_p], c_int),

@@ -493,7 +493,8 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
                                                                                  device=bins.device)
         args = [t.to(device=bins.device, dtype=torch.int32).contiguous()
                 for t in (tfirst, tfirst_next, split_feat, split_bin, cat_off, child)]
-        _lib.check(_lib.lib().cdna_partition5(_ptr(bins), n, T, _ptr(codes), _ptr(args[0]), _ptr(args[1]),
+        A = int(split_feat.numel())
+        _lib.check(_lib.lib().cdna_partition5(_ptr(bins), n, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]),
                                               _ptr(args[2]), _ptr(args[3]), _ptr(args[4]), _ptr(cm),
                                               _ptr(args[5]), _stream(bins.device)), "cdna_partition5")
         return
@@ -571,7 +572,8 @@ def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree
             nodes, roots = nodes.int().contiguous(), roots.int().contiguous()
             tree_w, values = tree_w.float().contiguous(), values.float().contiguous()
             base = None if base is None else base.float().contiguous()
-            _lib.check(_lib.lib().cdna_tree_predict(_ptr(X), n, d, X.stride(0), _ptr(nodes), _ptr(roots),
+            _lib.check(_lib.lib().cdna_tree_predict(_ptr(X), n, d, X.stride(0), _ptr(nodes), int(nodes.shape[0]),
+                                                    _ptr(roots),
                                                     _ptr(tree_w), T, _ptr(values), _ptr(m), K, _ptr(base), _ptr(out),
                                                     _stream(X.device)), "cdna_tree_predict")
         return out

@@ -74,6 +74,114 @@ __global__ __launch_bounds__(256) void binize_kernel(const float* __restrict__ X
 }
 
 // ---------------------------------------------------------------------------
+// binize v2.  v1 (above) spent 55 ms on 1e8 x 100 (profiles/, traced step):
+// one thread per (row, feature) element with integer divisions, a
+// data-dependent binary-search loop and byte-wide LDS tile writes.  v2 stages a
+// tile of rows with coalesced float4 loads, gives each thread (row, 8-feature
+// group) tasks so the result is ONE uint64 store (coalesced along rows for a
+// fixed group), and runs a fixed-trip branchless search over the LDS
+// thresholds (every lane executes the same 6-7 steps; no divergence).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                      const float* __restrict__ thr, const int* __restrict__ nthr,
+                                                      int tmax, int rows_per_tile, int steps,
+                                                      uint64_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  const int G = (d + 7) / 8;
+  float* sx = smf;                                  // [rows_per_tile][d]
+  float* sthr = smf + (size_t)rows_per_tile * d;    // [d][tmax]
+  int* snt = reinterpret_cast<int*>(sthr + (size_t)d * tmax);
+  for (int i = threadIdx.x; i < d * tmax; i += 256) sthr[i] = thr[i];
+  for (int i = threadIdx.x; i < d; i += 256) snt[i] = nthr[i];
+  const bool contiguous = ldx == d && (d % 4) == 0;
+  // register double buffer: the next tile's float4s are in flight while the
+  // current tile is binned (rocprofv3: the single-buffered loop spent 69 % of
+  // wave time waiting on memory)
+  constexpr int kPre = 8;  // float4 per thread per tile (64 rows x d <= 128 floats x ... / 256 threads)
+  float4 pre[kPre];
+  const int64_t stride = (int64_t)gridDim.x * rows_per_tile;
+  auto fetch = [&](int64_t r0) {
+    if (!contiguous || r0 >= n) return;
+    const int rows = (int)((n - r0) < rows_per_tile ? (n - r0) : rows_per_tile);
+    const float4* src = reinterpret_cast<const float4*>(X + r0 * ldx);
+    const int nv = rows * d / 4;
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int i = threadIdx.x + k * 256;
+      if (i < nv) pre[k] = src[i];
+    }
+  };
+  const bool use_pre = contiguous && rows_per_tile * d / 4 <= kPre * 256;
+  if (use_pre) fetch((int64_t)blockIdx.x * rows_per_tile);
+  for (int64_t r0 = (int64_t)blockIdx.x * rows_per_tile; r0 < n; r0 += stride) {
+    const int rows = (int)((n - r0) < rows_per_tile ? (n - r0) : rows_per_tile);
+    __syncthreads();
+    if (use_pre) {
+      float4* dst = reinterpret_cast<float4*>(sx);
+      const int nv = rows * d / 4;
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < nv) dst[i] = pre[k];
+      }
+    } else if (contiguous) {
+      const float4* src = reinterpret_cast<const float4*>(X + r0 * ldx);
+      float4* dst = reinterpret_cast<float4*>(sx);
+      const int nv = rows * d / 4;
+      for (int i = threadIdx.x; i < nv; i += 256) dst[i] = src[i];
+    } else {
+      for (int i = threadIdx.x; i < rows * d; i += 256) {
+        const int r = i / d, f = i - r * d;
+        sx[i] = X[(r0 + r) * ldx + f];
+      }
+    }
+    __syncthreads();
+    if (use_pre) fetch(r0 + stride);
+    for (int task = threadIdx.x; task < rows * G; task += 256) {
+      const int g = task / rows, r = task - g * rows;
+      // the 8 searches of a bins word advance in lockstep: 8 independent LDS
+      // reads per step instead of one dependent chain per feature (the
+      // dependent version left the waves idle on LDS latency)
+      float x[8];
+      int nt[8], lo[8], toff[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int f = g * 8 + j < d ? g * 8 + j : d - 1;
+        x[j] = sx[r * d + f];
+        nt[j] = g * 8 + j < d ? snt[f] : 0;
+        toff[j] = f * tmax - 1;
+        lo[j] = 0;
+      }
+#pragma unroll
+      for (int s2 = 7; s2 >= 0; --s2) {
+        if (s2 >= steps) continue;  // block-uniform
+        const int step = 1 << s2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int cand = lo[j] + step;
+          const float tv = cand <= nt[j] ? sthr[toff[j] + cand] : __builtin_inff();
+          lo[j] = tv < x[j] ? cand : lo[j];
+        }
+      }
+      uint64_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint32_t b;
+        if (nt[j] < 0) {
+          const int c = (int)x[j];
+          b = (uint32_t)(c < 0 ? 0 : (c > 255 ? 255 : c));
+        } else {
+          b = (x[j] != x[j]) ? (uint32_t)nt[j] : (uint32_t)lo[j];
+        }
+        if (g * 8 + j >= d) b = 0;
+        word |= (uint64_t)b << (8 * j);
+      }
+      out[(int64_t)g * n + r0 + r] = word;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K5 hist_build (moments): hist[slot][f][bin][2] += w * (v0, v1)
 // grid: linear; decoded (after XCD remap) as g fastest, then row chunk, then
 // slot group.  Slot group k covers slots [grp_s0[k], grp_s0[k]+SB) which all
@@ -246,50 +354,93 @@ __global__ __launch_bounds__(256) void predict_kernel(const float* __restrict__ 
                                                       const int4* __restrict__ nodes, const int* __restrict__ roots,
                                                       const float* __restrict__ tree_w, int T,
                                                       const float* __restrict__ values, const uint32_t* __restrict__ masks,
-                                                      int K, const float* __restrict__ base, float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float sx[];  // [64][d+1] then [4][64][K]
+                                                      int K, const float* __restrict__ base, float* __restrict__ out,
+                                                      int n_nodes_lds) {
+  // LDS: [n_nodes_lds] int4 forest (when it fits), then X tile [64][d+1], then [4][64][K] partials.
+  // rocprofv3 on the global-node version: 78 % of wave time waiting on the
+  // dependent node loads of each root-to-leaf walk; walking an LDS copy of the
+  // forest turns each step into a ~100-cycle ds_read_b128.
+  extern __shared__ __attribute__((aligned(16))) float sx_all[];
+  int4* snodes = reinterpret_cast<int4*>(sx_all);
+  float* sx = sx_all + (size_t)n_nodes_lds * 4;
   const int dp = d + 1;
   float* part = sx + 64 * dp;
+  const int4* nd_src = n_nodes_lds > 0 ? snodes : nodes;
+  for (int i = threadIdx.x; i < n_nodes_lds; i += 256) snodes[i] = nodes[i];
   const int tl = threadIdx.x >> 6, row = threadIdx.x & 63;
+  const bool vec = ldx == d && (d % 4) == 0;
   for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < n; r0 += (int64_t)gridDim.x * 64) {
     const int rows = (int)((n - r0) < 64 ? (n - r0) : 64);
-    for (int e = threadIdx.x; e < rows * d; e += 256) {
-      const int r = e / d, f = e - r * d;
-      sx[r * dp + f] = X[(r0 + r) * ldx + f];
+    __syncthreads();
+    if (vec) {
+      const float4* src = reinterpret_cast<const float4*>(X + r0 * ldx);
+      const int nv = rows * d / 4;
+      for (int i = threadIdx.x; i < nv; i += 256) {
+        const float4 v = src[i];
+        const int e = i * 4, r = e / d, f = e - r * d;  // d % 4 == 0: a float4 never crosses a row
+        float* dst = sx + r * dp + f;
+        dst[0] = v.x;
+        dst[1] = v.y;
+        dst[2] = v.z;
+        dst[3] = v.w;
+      }
+    } else {
+      for (int e = threadIdx.x; e < rows * d; e += 256) {
+        const int r = e / d, f = e - r * d;
+        sx[r * dp + f] = X[(r0 + r) * ldx + f];
+      }
     }
     for (int e = threadIdx.x; e < 4 * 64 * K; e += 256) part[e] = 0.f;
     __syncthreads();
     if (row < rows) {
       const float* xr = sx + row * dp;
       float* pr = part + (tl * 64 + row) * K;
-      for (int t = tl; t < T; t += 4) {
-        int nd = roots[t];
-        int4 nv = nodes[nd];
-        while (nv.x != -1) {
-          bool left;
-          if (nv.x >= 0) {
-            left = xr[nv.x] <= __int_as_float(nv.y);
-          } else {
-            const int c = (int)xr[-nv.x - 2];
-            left = (c >= 0 && c < 256) ? ((masks[nv.y * 8 + (c >> 5)] >> (c & 31)) & 1u) : false;
-          }
-          nd = left ? nv.z : nv.w;
-          nv = nodes[nd];
+      // up to 8 of this lane's trees walk in lockstep: independent node
+      // reads per level instead of one dependent chain per tree
+      constexpr int W = 8;
+      for (int tb = tl; tb < T; tb += 4 * W) {
+        int4 nv[W];
+        bool live[W];
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+          const int t = tb + 4 * u;
+          live[u] = t < T;
+          nv[u] = live[u] ? nd_src[roots[t]] : make_int4(-1, 0, 0, 0);
         }
-        const float tw = tree_w[t];
-        const float* v = values + nv.y;
-        for (int k = 0; k < K; ++k) pr[k] += tw * v[k];
+        bool any = true;
+        while (any) {
+          any = false;
+#pragma unroll
+          for (int u = 0; u < W; ++u) {
+            if (nv[u].x == -1) continue;
+            bool left;
+            if (nv[u].x >= 0) {
+              left = xr[nv[u].x] <= __int_as_float(nv[u].y);
+            } else {
+              const int c = (int)xr[-nv[u].x - 2];
+              left = (c >= 0 && c < 256) ? ((masks[nv[u].y * 8 + (c >> 5)] >> (c & 31)) & 1u) : false;
+            }
+            nv[u] = nd_src[left ? nv[u].z : nv[u].w];
+            any = true;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+          if (!live[u]) continue;
+          const float tw = tree_w[tb + 4 * u];
+          const float* v = values + nv[u].y;
+          for (int k = 0; k < K; ++k) pr[k] += tw * v[k];
+        }
       }
     }
     __syncthreads();
     for (int e = threadIdx.x; e < rows * K; e += 256) {
       const int r = e / K, k = e - r * K;
-      float s = base ? base[k] : 0.f;
+      float sacc = base ? base[k] : 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) s += part[(q * 64 + r) * K + k];
-      out[(r0 + r) * K + k] = s;
+      for (int q = 0; q < 4; ++q) sacc += part[(q * 64 + r) * K + k];
+      out[(r0 + r) * K + k] = sacc;
     }
-    __syncthreads();
   }
 }
 
@@ -334,6 +485,20 @@ inline unsigned grid_for(int64_t n, int per, unsigned cap) {
 CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const float* thr, const int* nthr, int tmax,
                          uint64_t* out, hipStream_t st) {
   if (n <= 0) return 0;
+  {
+    // v2: tile of rows in LDS next to the thresholds (<= 64 KB per block)
+    const size_t tb = (size_t)d * (tmax > 0 ? tmax : 1) * 4 + (size_t)d * 4;
+    int rpt = 64;
+    while (rpt > 4 && ((size_t)rpt * d * 4 + tb > 64 * 1024 || (size_t)rpt * d > 8192)) rpt /= 2;
+    if ((size_t)rpt * d * 4 + tb <= 64 * 1024) {
+      int steps = 0;
+      while ((1 << steps) <= tmax) ++steps;
+      const size_t lds = (size_t)rpt * d * 4 + tb;
+      hipLaunchKernelGGL(binize2_kernel, dim3(grid_for(n, rpt, 8192)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
+                         tmax > 0 ? tmax : 1, rpt, steps, out);
+      return (int)hipGetLastError();
+    }
+  }
   const int G = (d + 7) / 8;
   const size_t tile = ((size_t)256 * G * 8 + 15) / 16 * 16;
   const size_t tbytes = (size_t)d * (tmax > 0 ? tmax : 1) * 4;
@@ -385,14 +550,19 @@ CDNA_API int cdna_partition(const uint64_t* bins, int64_t n, int T, int* node, c
   return (int)hipGetLastError();
 }
 
-CDNA_API int cdna_tree_predict(const float* X, int64_t n, int d, int64_t ldx, const int4* nodes, const int* roots,
-                               const float* tree_w, int T, const float* values, const uint32_t* masks, int K,
-                               const float* base, float* out, hipStream_t st) {
+CDNA_API int cdna_tree_predict(const float* X, int64_t n, int d, int64_t ldx, const int4* nodes, int64_t n_nodes_total,
+                               const int* roots, const float* tree_w, int T, const float* values,
+                               const uint32_t* masks, int K, const float* base, float* out, hipStream_t st) {
   if (n <= 0) return 0;
-  const size_t lds = ((size_t)64 * (d + 1) + (size_t)4 * 64 * K) * 4;
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  const size_t lds0 = ((size_t)64 * (d + 1) + (size_t)4 * 64 * K) * 4;
+  if (lds0 > 160 * 1024) return (int)hipErrorInvalidValue;
+  // forest copy in LDS when it fits next to the tile (<= 64 KB per block keeps 2 blocks / CU)
+  int n_nodes = 0;
+  const size_t room = lds0 < 64 * 1024 ? 64 * 1024 - lds0 : 0;
+  n_nodes = n_nodes_total <= (int64_t)(room / 16) ? (int)n_nodes_total : 0;
+  const size_t lds = lds0 + (size_t)n_nodes * 16;
   hipLaunchKernelGGL(predict_kernel, dim3(grid_for(n, 64, 8192)), dim3(256), lds, st, X, n, d, ldx, nodes, roots,
-                     tree_w, T, values, masks, K, base, out);
+                     tree_w, T, values, masks, K, base, out, n_nodes);
   return (int)hipGetLastError();
 }
 
