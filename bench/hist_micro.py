@@ -99,7 +99,14 @@ def main():
     ]
     if args.variants != "all":
         configs = [c for c in configs if any(v in c[0] for v in args.variants.split(","))]
-    configs = [("L0 T20 full   codes pk4", 20, 1, False, True, 7, 4, 65536),
+    configs = [("L2 T20 full   codes pk8 128K", 20, 4, False, True, 7, 8, 131072),
+               ("L3 T20 full   codes pk8 128K", 20, 8, False, True, 7, 8, 131072),
+               ("L1 T20 full   codes pk8 128K", 20, 2, False, True, 7, 8, 131072),
+               ("L4 T20 full   codes pk8 128K", 20, 16, False, True, 7, 8, 131072),
+               ("L0 T20 full   codes pk8 128K", 20, 1, False, True, 7, 8, 131072),
+               ("L4 T20 full   codes pk16 128K", 20, 16, False, True, 7, 16, 131072),
+               ("L4 T20 masked codes pk8 128K", 20, 16, True, True, 7, 8, 131072),
+               ("L0 T20 full   codes pk4", 20, 1, False, True, 7, 4, 65536),
                ("L4 T20 full   codes pk4", 20, 16, False, True, 7, 4, 65536),
                ("L0 T20 full   codes pk8 48K", 20, 1, False, True, 7, 8, 49152),
                ("L0 T20 full   codes pk8", 20, 1, False, True, 7, 8, 65536),

@@ -156,6 +156,7 @@ HIST_PACKED = __import__("os").environ.get("CDNAML_HIST_PACKED", "0") != "0"
 # hist v5 (row records): packed single-atomic regression histograms, trees per block group when packed
 HIST5_PACKED = __import__("os").environ.get("CDNAML_HIST5_PACKED", "1") != "0"
 HIST5_PACKED_MAXT = int(__import__("os").environ.get("CDNAML_HIST5_PACKED_MAXT", "8"))
+HIST5_PACKED_LDS = int(__import__("os").environ.get("CDNAML_HIST5_PACKED_LDS", str(128 * 1024)))
 
 
 def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int, qmax_bits: int = 62) -> float:
@@ -431,7 +432,8 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
         raise ValueError("histogram too large for LDS (classes x bins)")
     budget = lds_budget or HIST_LDS_BUDGET
     if packed:
-        budget = min(budget, 8192 * 8)  # register drain: <= 16 cells per thread
+        # register drain holds <= 16 cells per thread: 512 threads -> 64 KB, 1024 threads -> 128 KB
+        budget = min(HIST5_PACKED_LDS if lds_budget is None else lds_budget, 16384 * 8)
         maxt = min(maxt, HIST5_PACKED_MAXT)
     SB = max(1, min(S, budget // per_slot))
     slot_tree = np.asarray(slot_tree)
@@ -450,12 +452,15 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
         a = b
     grp = torch.tensor(rows, dtype=torch.int32, device=bins.device).reshape(-1)
     ng = len(rows)
+    # the tree cap can leave groups smaller than the LDS budget allows: size LDS to the largest group
+    SB = max(min(SB, (rows[i + 1][0] if i + 1 < ng else S) - rows[i][0]) for i in range(ng))
     max_nt = max(r[2] - r[1] + 1 for r in rows)
     bucket = 1 if max_nt <= 1 else 2 if max_nt <= 2 else 4 if max_nt <= 4 else 8 if max_nt <= 8 else 16
     lds_used = ((SB * per_slot + 15) // 16) * 16 + bucket * 512 + SB + 16
     if lds_used > 160 * 1024:
         raise ValueError("local-node tables do not fit in LDS next to the histogram")
-    nchunk = int(max(1, min((1024 + G * ng - 1) // (G * ng), (n + 8191) // 8192)))
+    target_blocks = 512 if (packed and SB * per_slot > 8192 * 8) else 1024  # 1024-thread blocks: 1 per CU
+    nchunk = int(max(1, min((target_blocks + G * ng - 1) // (G * ng), (n + 8191) // 8192)))
     nchunk = max(nchunk, -(-n // (1 << 23)))
     mw = 0 if feat_mask is None else feat_mask.shape[1]
     fm = None if feat_mask is None else feat_mask.int().contiguous()

@@ -244,8 +244,9 @@ constexpr int kPackQ = 1 << 23;
 constexpr int kPackIters = 8;
 constexpr int kPackCells = 16;  // plane <= 16 * 512 = 8192 cells (64 KB)
 
-template <bool MASKED, int NT>
-__global__ __launch_bounds__(kThreads) void hist5p_kernel(const Hist5Args a) {
+template <bool MASKED, int NT, int TH>
+__global__ __launch_bounds__(TH) void hist5p_kernel(const Hist5Args a) {
+  constexpr int kPackItersT = 4096 / TH;  // rows between drains stay 4096 (count field < 2^20)
   constexpr int MODE = 0;
   constexpr bool V0 = false;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(kThreads) void hist5p_kernel(const Hist5Args a) {
   const int fbase = g * 8;
   const int rot = threadIdx.x & 7;
 
-  for (int i = threadIdx.x; i < plane; i += kThreads) h64[i] = 0ull;
+  for (int i = threadIdx.x; i < plane; i += TH) h64[i] = 0ull;
   uint32_t acc_c[kPackCells];
   long long acc_s[kPackCells];
 #pragma unroll
@@ -275,8 +276,8 @@ __global__ __launch_bounds__(kThreads) void hist5p_kernel(const Hist5Args a) {
     acc_c[i] = 0u;
     acc_s[i] = 0;
   }
-  for (int i = threadIdx.x; i < hwords; i += kThreads) h32[i] = 0u;
-  for (int i = threadIdx.x; i < NT * 256; i += kThreads) {
+  for (int i = threadIdx.x; i < hwords; i += TH) h32[i] = 0u;
+  for (int i = threadIdx.x; i < NT * 256; i += TH) {
     const int k = i >> 8, loc = i & 255;
     int v = -1;
     const int id = k < nt ? a.tfirst[t0 + k] + loc : 0;
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(kThreads) void hist5p_kernel(const Hist5Args a) {
     lt[i] = (int16_t)v;
   }
   if (MASKED) {
-    for (int i = threadIdx.x; i < a.SB; i += kThreads) {
+    for (int i = threadIdx.x; i < a.SB; i += TH) {
       const int slot = s0 + i;
       uint32_t m = 0u;
       if (slot < a.S) m = (a.feat_mask[(int64_t)slot * a.mask_words + (fbase >> 5)] >> (fbase & 31)) & 0xFFu;
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(kThreads) void hist5p_kernel(const Hist5Args a) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kPackCells; ++i) {
-      const int idx = (int)threadIdx.x + i * kThreads;
+      const int idx = (int)threadIdx.x + i * TH;
       if (idx < plane) {
         const unsigned long long v = h64[idx];
         if (v) {
@@ -360,7 +361,7 @@ __global__ __launch_bounds__(kThreads) void hist5p_kernel(const Hist5Args a) {
   }
 
   int iter = 0;
-  for (int64_t rbase = rb; rbase < re; rbase += kThreads, r += kThreads, ++iter) {
+  for (int64_t rbase = rb; rbase < re; rbase += TH, r += TH, ++iter) {
     if (r >= re) {
 #pragma unroll
       for (int k = 0; k < NT; ++k) cd[k] = 0xFFu;  // tail lanes: no work, but keep the block in step
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(kThreads) void hist5p_kernel(const Hist5Args a) {
     float nx0 = 1.f, nx1 = 0.f;
     int nlab = 0;
     uint32_t ncd[NT];
-    const int64_t rn = r + kThreads;
+    const int64_t rn = r + TH;
     if (rn < re) load_row(rn, nb8, nx0, nx1, nlab, ncd);
     else {
 #pragma unroll
@@ -420,12 +421,12 @@ __global__ __launch_bounds__(kThreads) void hist5p_kernel(const Hist5Args a) {
     lab = nlab;
 #pragma unroll
     for (int k = 0; k < NT; ++k) cd[k] = ncd[k];
-    if ((iter + 1) % kPackIters == 0) drain();
+    if ((iter + 1) % kPackItersT == 0) drain();
   }
   drain();
 #pragma unroll
   for (int i = 0; i < kPackCells; ++i) {
-    const int idx = (int)threadIdx.x + i * kThreads;
+    const int idx = (int)threadIdx.x + i * TH;
     if (idx >= plane || acc_c[i] == 0u) continue;
     const int ls = idx / (8 * a.B);
     const int jj = (idx / a.B) & 7;
@@ -569,13 +570,29 @@ void launch5(const Hist5Args& a, int nt_max, unsigned nblk, size_t lds, hipStrea
     hipLaunchKernelGGL((hist5_kernel<MODE, MASKED, V0, 16>), dim3(nblk), dim3(kThreads), lds, st, a);
 }
 
+template <typename K>
+void go(K kern, unsigned nblk, int th, size_t lds, hipStream_t st, const Hist5Args& a) {
+  // blocks above 64 KB of dynamic LDS must opt in (gfx950 has 160 KB per CU)
+  if (lds > 64 * 1024) hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(th), lds, st, a);
+}
+
+template <bool MASKED, int TH>
+void launch5p_t(const Hist5Args& a, int nt_max, unsigned nblk, size_t lds, hipStream_t st) {
+  if (nt_max <= 1) go(hist5p_kernel<MASKED, 1, TH>, nblk, TH, lds, st, a);
+  else if (nt_max <= 2) go(hist5p_kernel<MASKED, 2, TH>, nblk, TH, lds, st, a);
+  else if (nt_max <= 4) go(hist5p_kernel<MASKED, 4, TH>, nblk, TH, lds, st, a);
+  else if (nt_max <= 8) go(hist5p_kernel<MASKED, 8, TH>, nblk, TH, lds, st, a);
+  else go(hist5p_kernel<MASKED, 16, TH>, nblk, TH, lds, st, a);
+}
+
+// 1024-thread blocks hold 16384 packed cells (128 KB): one block per CU with
+// the same 16 waves as two 512-thread blocks, but twice the slots per pass.
 template <bool MASKED>
-void launch5p(const Hist5Args& a, int nt_max, unsigned nblk, size_t lds, hipStream_t st) {
-  if (nt_max <= 1) hipLaunchKernelGGL((hist5p_kernel<MASKED, 1>), dim3(nblk), dim3(kThreads), lds, st, a);
-  else if (nt_max <= 2) hipLaunchKernelGGL((hist5p_kernel<MASKED, 2>), dim3(nblk), dim3(kThreads), lds, st, a);
-  else if (nt_max <= 4) hipLaunchKernelGGL((hist5p_kernel<MASKED, 4>), dim3(nblk), dim3(kThreads), lds, st, a);
-  else if (nt_max <= 8) hipLaunchKernelGGL((hist5p_kernel<MASKED, 8>), dim3(nblk), dim3(kThreads), lds, st, a);
-  else hipLaunchKernelGGL((hist5p_kernel<MASKED, 16>), dim3(nblk), dim3(kThreads), lds, st, a);
+void launch5p(const Hist5Args& a, int nt_max, unsigned nblk, size_t lds, bool big, hipStream_t st) {
+  if (big) launch5p_t<MASKED, 1024>(a, nt_max, nblk, lds, st);
+  else launch5p_t<MASKED, 512>(a, nt_max, nblk, lds, st);
 }
 
 inline int nt_bucket(int nt) { return nt <= 1 ? 1 : nt <= 2 ? 2 : nt <= 4 ? 4 : nt <= 8 ? 8 : 16; }
@@ -627,17 +644,20 @@ CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T,
   // id_span_max carries the max trees per group here (local -> slot tables of 256 int16 each)
   const size_t lds = plane * 8 * a.n64 + ((plane * a.n32 + 3) & ~(size_t)3) * 4 +
                      (size_t)nt_bucket(id_span_max) * 512 + SB + 16;
-  if (lds > 160 * 1024 || id_span_max > kMaxTrees) return (int)hipErrorInvalidValue;
+  if (id_span_max > kMaxTrees) return (int)hipErrorInvalidValue;
+  if (lds > 160 * 1024 && !(mode & 16)) return (int)hipErrorInvalidValue;
   const unsigned nblk = (unsigned)G * ngroups * nchunk;
   const bool masked = feat_mask != nullptr;
   const int ntm = id_span_max;
   if (mode & 16) {  // packed single-atomic regression
-    if (classes || has_v0 || plane > (size_t)kPackCells * kThreads) return (int)hipErrorInvalidValue;
+    const bool big = plane > (size_t)kPackCells * 512;
+    if (classes || has_v0 || plane > (size_t)kPackCells * 1024) return (int)hipErrorInvalidValue;
     a.n64 = 1;
     a.n32 = 0;
     const size_t lds_p = plane * 8 + (size_t)nt_bucket(ntm) * 512 + SB + 16;
-    if (masked) launch5p<true>(a, ntm, nblk, lds_p, st);
-    else launch5p<false>(a, ntm, nblk, lds_p, st);
+    if (lds_p > 160 * 1024) return (int)hipErrorInvalidValue;
+    if (masked) launch5p<true>(a, ntm, nblk, lds_p, big, st);
+    else launch5p<false>(a, ntm, nblk, lds_p, big, st);
     return (int)hipGetLastError();
   }
   if (classes) {
