@@ -133,8 +133,9 @@ def main():
             codes = ((c & 0xFF00) | loc).to(torch.int16).contiguous()
             tfirst = torch.arange(T, dtype=torch.int32) * L
             del node
+            wmax = int(w.max().item())
             fn = lambda: K.hist_codes(0, bins, d, codes, tfirst, None, y, None, 0, build, st, it, fm, B,  # noqa: E731
-                                      lds_budget=lds)
+                                      lds_budget=lds, wmax=wmax)
             ms = timeit(fn, args.reps)
             frac_w = float((w > 0).float().mean())
             feats = int(np.ceil(d / 3)) if masked else d

@@ -529,6 +529,7 @@ class ForestTrainer:
         use_codes = USE_CODES and p.max_depth <= 8
         if use_codes:
             codes = K.codes_init(weights, T, n, dev)
+            wmax = int(weights.max().item()) if (weights is not None and weights.numel()) else 1
             node = None
         else:
             node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
@@ -572,7 +573,7 @@ class ForestTrainer:
                 if use_codes:
                     Hb = K.hist_codes(1 if self.classification else 0, data.bins, d, codes, tfirst,
                                       stats_rows.get("v0"), stats_rows.get("v1"), stats_rows.get("label"), self.C,
-                                      build_slot, slot_tree, id_tree, fm_build, B)
+                                      build_slot, slot_tree, id_tree, fm_build, B, wmax=wmax)
                 elif self.classification:
                     Hb = K.hist_classes(data.bins, d, node, weights, stats_rows["label"], self.C, build_slot,
                                         slot_tree, fm_build, B, id_tree=id_tree)

@@ -81,7 +81,7 @@ _SIGS = {
     "cdna_hist4_bytes_per_bin": ([c_int, c_int], c_int),
     "cdna_hist5": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,
-                    c_void_p, c_void_p], c_int),
+                    c_int, c_void_p, c_void_p], c_int),
     "cdna_hist5_max_trees": ([], c_int),
     "cdna_partition5": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p], c_int),

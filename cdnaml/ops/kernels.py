@@ -409,8 +409,11 @@ def decode_codes(codes: torch.Tensor, tfirst: torch.Tensor):
 def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirst: torch.Tensor,
                v0: Optional[torch.Tensor], v1: Optional[torch.Tensor], label: Optional[torch.Tensor], C: int,
                build_slot: torch.Tensor, slot_tree: np.ndarray, id_tree: np.ndarray,
-               feat_mask: Optional[torch.Tensor], B: int, lds_budget: Optional[int] = None) -> torch.Tensor:
-    """Histograms from row records (hist5.hip).  mode 0: moments [S, d, B, 2]; 1: classes [S, d, B, C]."""
+               feat_mask: Optional[torch.Tensor], B: int, lds_budget: Optional[int] = None,
+               wmax: int = 255) -> torch.Tensor:
+    """Histograms from row records (hist5.hip).  mode 0: moments [S, d, B, 2]; 1: classes [S, d, B, C].
+
+    ``wmax``: largest row weight in ``codes`` (bounds the packed kernel's drain interval)."""
     S = len(slot_tree)
     G, n, _ = bins.shape
     T = codes.shape[0] if codes.dim() == 2 else 0
@@ -467,7 +470,7 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
     v0 = None if v0 is None else v0.float().contiguous()
     v1 = None if v1 is None else v1.float().contiguous()
     label = None if label is None else label.int().contiguous()
-    wmax = 255
+    wmax = int(max(1, min(255, wmax)))
     qs0 = _fixed_scale(v0, n, wmax, qmax_bits=30)
     qs1 = _packed_scale(v1) if packed else _fixed_scale(v1, n, wmax, qmax_bits=30)
     iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
@@ -476,7 +479,7 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
     bs = build_slot.int().contiguous()
     _lib.check(lib.cdna_hist5(kbits, _ptr(bins), n, d, T, _ptr(codes), _ptr(tf), _ptr(v0), _ptr(v1), _ptr(label),
                               int(C), _ptr(bs), _ptr(fm), mw, S, B, SB, _ptr(grp), ng, nchunk, max_nt, qs0, qs1,
-                              _ptr(iout), _stream(bins.device)), "cdna_hist5")
+                              int(max(1, min(255, wmax))), _ptr(iout), _stream(bins.device)), "cdna_hist5")
     out.copy_(iout)
     if mode == 0:
         if v0 is not None:

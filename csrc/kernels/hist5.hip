@@ -42,6 +42,7 @@ struct Hist5Args {
   int64_t rows_per_chunk;
   float qs0, qs1;
   int n64, n32;
+  int drain_iters;          // packed kernel: row iterations between register drains
   unsigned long long* out;  // [S][d][B][K]
 };
 
@@ -246,7 +247,8 @@ constexpr int kPackCells = 16;  // plane <= 16 * 512 = 8192 cells (64 KB)
 
 template <bool MASKED, int NT, int TH>
 __global__ __launch_bounds__(TH) void hist5p_kernel(const Hist5Args a) {
-  constexpr int kPackItersT = 4096 / TH;  // rows between drains stay 4096 (count field < 2^20)
+  // rows between drains: (rows x max weight) < 2^20 keeps both packed fields in range
+  const int drain_iters = a.drain_iters;
   constexpr int MODE = 0;
   constexpr bool V0 = false;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(TH) void hist5p_kernel(const Hist5Args a) {
     lab = nlab;
 #pragma unroll
     for (int k = 0; k < NT; ++k) cd[k] = ncd[k];
-    if ((iter + 1) % kPackItersT == 0) drain();
+    if ((iter + 1) % drain_iters == 0) drain();
   }
   drain();
 #pragma unroll
@@ -607,7 +609,7 @@ CDNA_API int cdna_hist5_max_trees() { return kMaxTrees; }
 CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T, const uint16_t* codes,
                         const int* tfirst, const float* v0, const float* v1, const int* label, int C,
                         const int* build_slot, const uint32_t* feat_mask, int mask_words, int S, int B, int SB,
-                        const int* grp, int ngroups, int nchunk, int id_span_max, float qs0, float qs1,
+                        const int* grp, int ngroups, int nchunk, int id_span_max, float qs0, float qs1, int wmax,
                         unsigned long long* out, hipStream_t st) {
   if (n <= 0 || S <= 0) return 0;
   Hist5Args a;
@@ -651,6 +653,11 @@ CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T,
   const int ntm = id_span_max;
   if (mode & 16) {  // packed single-atomic regression
     const bool big = plane > (size_t)kPackCells * 512;
+    {
+      const int th = big ? 1024 : 512;
+      const int64_t rows_ok = ((int64_t)1 << 20) / (wmax > 0 ? wmax + 1 : 1);  // rows * wmax < 2^20
+      a.drain_iters = (int)(rows_ok / th > 0 ? rows_ok / th : 1);
+    }
     if (classes || has_v0 || plane > (size_t)kPackCells * 1024) return (int)hipErrorInvalidValue;
     a.n64 = 1;
     a.n32 = 0;

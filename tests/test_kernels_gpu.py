@@ -308,7 +308,8 @@ def _codes_state(n, T, per, seed):
     return codes, tfirst, build, np.array(slot_tree, dtype=np.int32), id_tree
 
 
-@pytest.mark.parametrize("kind", ["moments", "moments_v0", "classes", "masked", "packed", "packed_masked"])
+@pytest.mark.parametrize("kind", ["moments", "moments_v0", "classes", "masked", "packed", "packed_masked",
+                                  "packed_wmax"])
 def test_hist_codes(dev, kind, monkeypatch):
     n, d, T, per, B, C = 30000, 21, 18, 5, 40, 3
     g = torch.Generator().manual_seed(7)
@@ -327,9 +328,10 @@ def test_hist_codes(dev, kind, monkeypatch):
     mode = 1 if kind == "classes" else 0
     v0 = h if kind == "moments_v0" else None
     ref = K.hist_codes(mode, bins, d, codes, tfirst, v0, y, lab, C, build, slot_tree, id_tree, fm, B)
+    wmax = int(((codes.to(torch.int32) & 0xFFFF) >> 8).max()) if kind == "packed_wmax" else 255
     out = K.hist_codes(mode, bins.to(dev), d, codes.to(dev), tfirst, None if v0 is None else v0.to(dev), y.to(dev),
                        lab.to(dev), C, build.to(dev), slot_tree, id_tree, None if fm is None else fm.to(dev), B,
-                       lds_budget=16 * 1024).cpu()
+                       lds_budget=16 * 1024, wmax=wmax).cpu()
     assert torch.allclose(out, ref, rtol=1e-6, atol=1e-3)
 
 
