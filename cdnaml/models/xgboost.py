@@ -161,7 +161,7 @@ class _XgbEstimatorBase(Estimator):
                           min_child_weight=self.getMin_child_weight(),
                           subset_scope="node" if cb_node < 1.0 else "tree")
 
-    def _boost(self, session, data, grad_hess, F, seed, n_out, val_mask, y, metric_fn):
+    def _boost(self, session, data, grad_hess, F, seed, n_out, val_mask, y, metric_fn, unit_hess=False):
         """Rounds of K trees (one per output); F [n, n_out] float32 margins (in place)."""
         dev = data.bins.device
         n = data.n_local
@@ -183,7 +183,10 @@ class _XgbEstimatorBase(Estimator):
                 bag = train_w if bag is None else bag * train_w
             for k in range(n_out):
                 trainer.p.seed = (seed * 1000003 + m * 131 + k) & 0x7FFFFFFF
-                trainer.train(1, {"v0": h[:, k].float().contiguous(), "v1": g[:, k].float().contiguous()},
+                # unit hessians (squared error, unweighted): H = row count, so the histogram
+                # takes the single-statistic (packed count|sum) path
+                v0 = None if unit_hess else h[:, k].float().contiguous()
+                trainer.train(1, {"v0": v0, "v1": g[:, k].float().contiguous()},
                               None if bag is None else bag[None, :].contiguous(), forest)
                 t = len(forest.roots) - 1
                 self._apply_l1(forest, t)
@@ -270,7 +273,8 @@ class XgboostRegressor(_XgbEstimatorBase):
             session.comm.all_reduce(s)
             return math.sqrt(float(s[0]) / max(float(s[1]), 1.0))
 
-        forest, hist = self._boost(session, data, grad_hess, F, seed, 1, val, y, metric)
+        unit = obj in ("reg:squarederror", "reg:linear", "reg:absoluteerror") and wf is None
+        forest, hist = self._boost(session, data, grad_hess, F, seed, 1, val, y, metric, unit_hess=unit)
         model = XgboostRegressorModel(forest, data.d, base_margin, data.thresholds, data.nthr, obj)
         model._copyValues_from(self)
         model.evals_result_ = {"validation": hist}
