@@ -19,6 +19,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -142,8 +143,14 @@ def bench_infer(spark, args):
     bufs = [torch.randn((chunk, 100), generator=g, dtype=torch.float32, device=dev) for _ in range(2)]
     outs = [None, None]
 
+    from cdnaml.ops import kernels as K
+    nodes, roots, vals, masks = forest.device_arrays(dev, "value")
+    tw_d = torch.tensor(np.asarray(tw, np.float32), device=dev)
+    masks = masks.int().contiguous() if masks.numel() else torch.zeros(8, dtype=torch.int32, device=dev)
+
     def run_chunk(j):
-        outs[j] = forest.predict(bufs[j], tw, [0.0])
+        # device-resident forest arrays, no host->device traffic: capturable in a HIP graph
+        outs[j] = K.tree_predict(bufs[j], nodes, roots, tw_d, vals, masks, forest.K, None)
     graphs = None
     if dev.type == "cuda" and not args.no_graph:
         s = torch.cuda.Stream()

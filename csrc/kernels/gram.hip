@@ -17,7 +17,9 @@
 // f32 partial slab, reduced deterministically in f64 by gram_reduce_kernel.
 //
 // bf16 variant: inputs rounded to bf16 and fed to v_mfma_f32_32x32x16_bf16
-// through an LDS transpose (ds_read of 8 consecutive rows per lane).
+// through an LDS transpose (ds_read of 8 consecutive rows per lane).  The
+// streaming form (gram_bf16s_kernel) reads X once with all tile pairs per
+// block; gram_bf16_kernel remains for unaligned / wide inputs.
 #include "common.h"
 
 namespace {
@@ -180,6 +182,123 @@ __global__ __launch_bounds__(256) void gram_bf16_kernel(const float* __restrict_
   }
 }
 
+// Streaming bf16 Gram (d % 4 == 0, 16-byte aligned rows, D <= 160): one pass
+// over X with every tile pair in the same block, so X is read exactly once.
+//  * rows stream through a double-buffered LDS tile (64 rows, stored column-
+//    major as bf16 so a lane's 8-row MFMA fragment is one 16-byte ds_read);
+//  * the next tile's float4 loads are issued into registers before the MFMAs
+//    on the current tile, and land in the other LDS buffer after them: one
+//    __syncthreads per tile;
+//  * wave w owns tile pairs w, w+4, ...; its accumulators go straight to the
+//    block's partial slab (no cross-wave fold).
+// Each thread's (row, column-quad) items are fixed for the whole kernel, so
+// their global and LDS offsets are computed once.
+template <int PW, int NI>
+__global__ __launch_bounds__(256) void gram_bf16s_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                         const float* __restrict__ y,
+                                                         const float* __restrict__ shift, float yshift,
+                                                         PairTable tab, int npairs, int Dpad,
+                                                         float* __restrict__ partial, int64_t rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int kCS = 72;  // column stride in bf16 elements (64 rows + 8 pad)
+  uint16_t* buf = reinterpret_cast<uint16_t*>(smem);
+  const int tsz = Dpad * kCS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, half = lane >> 5;
+  const int d4 = d >> 2;
+  const int items = 64 * d4;
+  // zero both buffers once: padding columns d+2..Dpad-1 stay zero forever
+  for (int i = tid; i < 2 * tsz / 2; i += 256) reinterpret_cast<uint32_t*>(buf)[i] = 0u;
+  int goff[NI], loff[NI], rr[NI];
+  float4 sh[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int e = tid + 256 * i;
+    const int r = e < items ? e / d4 : 0, c4 = e < items ? e - (e / d4) * d4 : 0;
+    goff[i] = e < items ? (int)(r * ldx) + 4 * c4 : -1;
+    loff[i] = 4 * c4 * kCS + r;
+    rr[i] = r;
+    sh[i] = shift ? *reinterpret_cast<const float4*>(shift + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  int pr[PW];
+#pragma unroll
+  for (int j = 0; j < PW; ++j) pr[j] = wid + 4 * j;
+  f32x16 acc[PW];
+#pragma unroll
+  for (int j = 0; j < PW; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+
+  const int64_t rb0 = (int64_t)blockIdx.x * rows_per_block;
+  int64_t rb1 = rb0 + rows_per_block;
+  if (rb1 > n) rb1 = n;
+  float4 v[NI];
+  float yv = 0.f;
+// next tile's rows -> registers (rows past rb1 load the shift, i.e. become 0)
+#define GRAM_LOAD(T0)                                                                      \
+  {                                                                                        \
+    const int64_t lim_ = rb1 - (T0);                                                       \
+    _Pragma("unroll") for (int i = 0; i < NI; ++i) {                                       \
+      const bool ok_ = goff[i] >= 0 && rr[i] < lim_;                                       \
+      v[i] = ok_ ? *reinterpret_cast<const float4*>(X + (T0) * ldx + goff[i]) : sh[i];     \
+    }                                                                                      \
+    if (tid < 64) yv = (y != nullptr && tid < lim_) ? y[(T0) + tid] - yshift : 0.f;        \
+  }
+// registers -> bf16 column-major LDS tile
+#define GRAM_STORE(TB, T0)                                                                 \
+  {                                                                                        \
+    _Pragma("unroll") for (int i = 0; i < NI; ++i) {                                       \
+      if (goff[i] >= 0) {                                                                  \
+        uint16_t* p_ = (TB) + loff[i];                                                     \
+        p_[0] = __builtin_bit_cast(uint16_t, (__bf16)(v[i].x - sh[i].x));                  \
+        p_[kCS] = __builtin_bit_cast(uint16_t, (__bf16)(v[i].y - sh[i].y));                \
+        p_[2 * kCS] = __builtin_bit_cast(uint16_t, (__bf16)(v[i].z - sh[i].z));            \
+        p_[3 * kCS] = __builtin_bit_cast(uint16_t, (__bf16)(v[i].w - sh[i].w));            \
+      }                                                                                    \
+    }                                                                                      \
+    if (tid < 64) {                                                                        \
+      (TB)[d * kCS + tid] = __builtin_bit_cast(uint16_t, (__bf16)((T0) + tid < rb1 ? 1.f : 0.f)); \
+      (TB)[(d + 1) * kCS + tid] = __builtin_bit_cast(uint16_t, (__bf16)yv);                \
+    }                                                                                      \
+  }
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  __syncthreads();
+  int cur = 0;
+  if (rb0 < rb1) {
+    GRAM_LOAD(rb0);
+    GRAM_STORE(buf, rb0);
+  }
+  for (int64_t t0 = rb0; t0 < rb1; t0 += 64) {
+    const bool more = t0 + 64 < rb1;
+    if (more) GRAM_LOAD(t0 + 64);
+    __syncthreads();
+    const uint16_t* tc = buf + cur * tsz;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kr = ks * 16 + 8 * half;
+#pragma unroll
+      for (int j = 0; j < PW; ++j) {
+        if (pr[j] >= npairs) continue;
+        const int ti = tab.I[pr[j]], tj = tab.J[pr[j]];
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&tc[(ti * 32 + (lane & 31)) * kCS + kr]);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&tc[(tj * 32 + (lane & 31)) * kCS + kr]);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[j], 0, 0, 0);
+      }
+    }
+    if (more) GRAM_STORE(buf + (cur ^ 1) * tsz, t0 + 64);
+    cur ^= 1;
+  }
+  const int col = lane & 31;
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    if (pr[j] >= npairs) continue;
+    float* dst = partial + ((int64_t)blockIdx.x * npairs + pr[j]) * 1024;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dst[((e & 3) + 8 * (e >> 2) + 4 * half) * 32 + col] = acc[j][e];
+  }
+}
+#undef GRAM_LOAD
+#undef GRAM_STORE
+
 __global__ void gram_reduce_kernel(const float* __restrict__ partial, int nblk, int npairs, PairTable tab, int D,
                                    double* __restrict__ out) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -233,6 +352,43 @@ GramPlan make_plan(int64_t n, int d, bool bf16) {
   return pl;
 }
 
+constexpr int kStreamMaxD = 160;
+
+bool stream_ok(const float* X, int d, int64_t ldx, const float* shift) {
+  return d % 4 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(shift) & 15) == 0 && d + 2 <= kStreamMaxD;
+}
+
+GramPlan make_stream_plan(int64_t n, int d) {
+  GramPlan pl = make_plan(n, d, true);
+  pl.ngroups = 1;
+  int64_t nb = (n + 4095) / 4096;
+  if (nb > 1024) nb = 1024;  // 4 resident blocks x 256 CUs
+  if (nb < 1) nb = 1;
+  pl.nblk = (int)nb;
+  int64_t rpb = (n + nb - 1) / nb;
+  pl.rows_per_unit = (rpb + 63) / 64 * 64;
+  return pl;
+}
+
+template <int PW, int NI>
+void launch_stream(const GramPlan& pl, const float* X, int64_t n, int d, int64_t ldx, const float* y,
+                   const float* shift, float yshift, float* ws, hipStream_t st) {
+  const int Dpad = ((pl.D + 31) / 32) * 32;
+  const size_t lds = (size_t)2 * Dpad * 72 * 2;
+  hipLaunchKernelGGL((gram_bf16s_kernel<PW, NI>), dim3(pl.nblk), dim3(256), lds, st, X, n, d, ldx, y, shift, yshift,
+                     pl.tab, pl.npairs, Dpad, ws, pl.rows_per_unit);
+}
+
+template <int PW>
+void launch_stream_ni(const GramPlan& pl, const float* X, int64_t n, int d, int64_t ldx, const float* y,
+                      const float* shift, float yshift, float* ws, hipStream_t st) {
+  const int ni = (64 * (d / 4) + 255) / 256;
+  if (ni <= 4) launch_stream<PW, 4>(pl, X, n, d, ldx, y, shift, yshift, ws, st);
+  else if (ni <= 7) launch_stream<PW, 7>(pl, X, n, d, ldx, y, shift, yshift, ws, st);
+  else launch_stream<PW, 10>(pl, X, n, d, ldx, y, shift, yshift, ws, st);
+}
+
 template <int P>
 void launch_f32(const GramPlan& pl, const float* X, int64_t n, int d, int64_t ldx, const float* y, const float* shift,
                 float yshift, float* ws, hipStream_t st) {
@@ -253,7 +409,13 @@ void launch_bf16(const GramPlan& pl, const float* X, int64_t n, int d, int64_t l
 // Workspace (in floats) needed by cdna_gram for an n×d problem.
 CDNA_API int64_t cdna_gram_workspace(int64_t n, int d, int bf16) {
   GramPlan pl = make_plan(n, d, bf16 != 0);
-  return (int64_t)pl.nblk * pl.npairs * 1024;
+  int64_t w = (int64_t)pl.nblk * pl.npairs * 1024;
+  if (bf16 && d + 2 <= kStreamMaxD) {
+    GramPlan ps = make_stream_plan(n, d);
+    const int64_t w2 = (int64_t)ps.nblk * ps.npairs * 1024;
+    if (w2 > w) w = w2;
+  }
+  return w;
 }
 
 // out: (d+2)×(d+2) f64, row-major.  Column d is the all-ones column, column
@@ -263,7 +425,16 @@ CDNA_API int cdna_gram(const float* X, int64_t n, int d, int64_t ldx, const floa
   if (d + 2 > 32 * 17) return (int)hipErrorInvalidValue;
   GramPlan pl = make_plan(n, d, bf16 != 0);
   if (pl.npairs > kMaxPairs) return (int)hipErrorInvalidValue;
-  if (bf16) {
+  if (bf16 && stream_ok(X, d, ldx, shift)) {
+    pl = make_stream_plan(n, d);
+    const int pw = (pl.npairs + 3) / 4;
+    switch (pw) {
+      case 1: launch_stream_ni<1>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      case 2: launch_stream_ni<2>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      case 3: launch_stream_ni<3>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+      default: launch_stream_ni<4>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
+    }
+  } else if (bf16) {
     switch (pl.P) {
       case 1: launch_bf16<1>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
       case 2: launch_bf16<2>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;

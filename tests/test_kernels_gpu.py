@@ -36,14 +36,21 @@ def test_gram_asymmetric_identity(dev):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("n,d", [(5000, 100), (100, 7)])
-def test_gram_bf16(dev, n, d):
-    g = torch.Generator().manual_seed(7)
-    X = torch.randn(n, d, generator=g)
-    y = torch.randn(n, generator=g)
-    ref = K.gram(X, y, None, 0.0, bf16=True)
-    out = K.gram(X.to(dev), y.to(dev), None, 0.0, bf16=True).cpu()
-    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-2)
+@pytest.mark.parametrize("n,d,shifted,ldx", [(5000, 100, False, None), (100, 7, False, None),
+                                             (70001, 128, True, None), (200003, 64, True, None), (3, 4, True, None),
+                                             (9000, 100, True, 101), (131, 156, False, None)])
+def test_gram_bf16(dev, n, d, shifted, ldx):
+    # d % 4 == 0 with aligned rows takes the streaming kernel; ldx=101 / d=7 the tiled fallback
+    g = torch.Generator().manual_seed(7 + n)
+    X = torch.randn(n, ldx or d, generator=g) * 2 + 0.5
+    y = torch.randn(n, generator=g) + 3
+    sh = X[:64, :d].mean(0) if shifted else None
+    ys = 2.5 if shifted else 0.0
+    Xd = X.to(dev)[:, :d]
+    X = X[:, :d]
+    ref = K.gram(X.contiguous(), y, sh, ys, bf16=True)
+    out = K.gram(Xd, y.to(dev), None if sh is None else sh.to(dev), ys, bf16=True).cpu()
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-2 * max(1.0, n / 20000))
 
 
 def test_uniform_bit_identical(dev):
