@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cdnaml.ops import kernels as K  # noqa: E402
 
 
-def make_state(n, d, T, L, B, masked, seed=0, dev="cuda"):
+def make_state(n, d, T, L, B, masked, seed=0, dev="cuda", sub=False):
     g = torch.Generator(device=dev).manual_seed(seed)
     X = torch.randn((n, d), generator=g, device=dev)
     thr = torch.linspace(-2, 2, B - 1, device=dev)[None, :].expand(d, -1).contiguous()
@@ -29,6 +29,13 @@ def make_state(n, d, T, L, B, masked, seed=0, dev="cuda"):
     node = (torch.randint(0, L, (T, n), generator=g, device=dev, dtype=torch.int32) +
             (torch.arange(T, device=dev, dtype=torch.int32) * L)[:, None]).contiguous()
     A = T * L
+    if sub and L > 1:
+        # full+subtract: only one child of each sibling pair is built (even local ids here)
+        loc = np.tile(np.arange(L), T)
+        bs = np.where(loc % 2 == 0, np.cumsum(loc % 2 == 0) - 1, -1).astype(np.int32)
+        build = torch.from_numpy(bs).to(dev)
+        slot_tree = np.repeat(np.arange(T), L // 2).astype(np.int32)
+        return _finish(n, d, T, L, B, masked, g, bins, node, build, slot_tree, np.repeat(np.arange(T), L), dev)
     build = torch.arange(A, dtype=torch.int32, device=dev)
     slot_tree = np.repeat(np.arange(T), L).astype(np.int32)
     id_tree = slot_tree.copy()
@@ -44,6 +51,22 @@ def make_state(n, d, T, L, B, masked, seed=0, dev="cuda"):
         fm = torch.from_numpy(words.view(np.int32)).to(dev)
     y = torch.randn(n, generator=g, device=dev)
     return bins, node, w, y, build, slot_tree, id_tree, fm
+
+
+def _finish(n, d, T, L, B, masked, g, bins, node, build, slot_tree, id_tree, dev):
+    w = K.poisson_weights(T, n, 1, 0, 1.0, device=dev)
+    S = len(slot_tree)
+    fm = None
+    if masked:
+        rng = np.random.default_rng(0)
+        words = np.zeros((S, (d + 31) // 32), dtype=np.uint32)
+        k = int(np.ceil(d / 3))
+        for a in range(S):
+            for f in rng.choice(d, k, replace=False):
+                words[a, f >> 5] |= np.uint32(1) << np.uint32(f & 31)
+        fm = torch.from_numpy(words.view(np.int32)).to(dev)
+    y = torch.randn(n, generator=g, device=dev)
+    return bins, node, w, y, build, slot_tree, id_tree.astype(np.int32), fm
 
 
 def timeit(fn, reps=3):
@@ -99,7 +122,15 @@ def main():
     ]
     if args.variants != "all":
         configs = [c for c in configs if any(v in c[0] for v in args.variants.split(","))]
-    configs = [("L2 T20 full   codes pk8 128K", 20, 4, False, True, 7, 8, 131072),
+    sub_cfgs = []
+    for lvl in range(5):
+        for ver, tag in ((7, "pk8"), (8, "pkq")):
+            sub_cfgs.append((f"L{lvl} T20 sub    codes {tag} 128K", 20, 1 << lvl, False, True, ver, 8, 131072))
+    sub_cfgs.append(("L4 T20 sub msk codes pk8 128K", 20, 16, True, True, 7, 8, 131072))
+    sub_cfgs.append(("L4 T20 sub msk codes pkq 128K", 20, 16, True, True, 8, 8, 131072))
+    sub_cfgs.append(("L7 T1  sub    codes pk8 128K B256", 1, 128, False, True, 7, 8, 131072))
+    sub_cfgs.append(("L7 T1  sub    codes pkq 128K B256", 1, 128, False, True, 8, 8, 131072))
+    configs = sub_cfgs + [("L2 T20 full   codes pk8 128K", 20, 4, False, True, 7, 8, 131072),
                ("L3 T20 full   codes pk8 128K", 20, 8, False, True, 7, 8, 131072),
                ("L1 T20 full   codes pk8 128K", 20, 2, False, True, 7, 8, 131072),
                ("L4 T20 full   codes pk8 128K", 20, 16, False, True, 7, 8, 131072),
@@ -122,10 +153,13 @@ def main():
     if args.variants != "all":
         configs = [c for c in configs if any(v in c[0] for v in args.variants.split(","))]
     for name, T, L, masked, wts, ver, lmap, lds in configs:
-        if ver in (6, 7):
-            K.HIST5_PACKED = ver == 7
-            K.HIST5_PACKED_MAXT = lmap if ver == 7 else 8
-            bins, node, w, y, build, st, it, fm = make_state(n, d, T, L, B, masked)
+        if ver in (6, 7, 8):
+            K.HIST5_PACKED = ver >= 7
+            K.HIST5_COMPACT = 2 if ver == 8 else 0
+            K.HIST5_PACKED_MAXT = lmap if ver >= 7 else 8
+            Bc = 256 if "B256" in name else B
+            sub = " sub " in name
+            bins, node, w, y, build, st, it, fm = make_state(n, d, T, L, Bc, masked, sub=sub)
             codes = K.codes_init(w, T, n, "cuda")
             loc = node - (torch.arange(T, device="cuda", dtype=torch.int32) * L)[:, None]
             c = codes.to(torch.int32) & 0xFFFF
@@ -134,12 +168,12 @@ def main():
             tfirst = torch.arange(T, dtype=torch.int32) * L
             del node
             wmax = int(w.max().item())
-            fn = lambda: K.hist_codes(0, bins, d, codes, tfirst, None, y, None, 0, build, st, it, fm, B,  # noqa: E731
+            fn = lambda: K.hist_codes(0, bins, d, codes, tfirst, None, y, None, 0, build, st, it, fm, Bc,  # noqa: E731
                                       lds_budget=lds, wmax=wmax)
             ms = timeit(fn, args.reps)
             frac_w = float((w > 0).float().mean())
             feats = int(np.ceil(d / 3)) if masked else d
-            upd = n * T * frac_w * feats
+            upd = n * T * frac_w * feats * (0.5 if (sub and L > 1) else 1.0)
             print(f"{name:28s} {ms:9.2f} ms  {upd / ms * 1e3:9.3e} upd/s  ({upd:.2e} row-tree-feature updates)",
                   flush=True)
             del bins, codes, w, y

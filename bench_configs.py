@@ -61,8 +61,20 @@ def _data(spark, n_total, d, seed=42, cls=False):
     return spark.createDataFrameFromLocalTensors({"features": X, "label": y}), n
 
 
+TRACE = None
+
+
 def _timed(spark, fn, steps, warmup):
     dev = spark.device
+    if TRACE:
+        from cdnaml.utils import tracing
+        tracing.reset()
+        tracing.enable()
+        fn()
+        _sync(dev)
+        tracing.disable()
+        _log("traced run (untimed):\n" + tracing.summary())
+        tracing.export_chrome_trace(TRACE)
     for _ in range(warmup):
         fn()
     _sync(dev)
@@ -212,7 +224,10 @@ def main():
     ap.add_argument("--chunk", type=float, default=2.5e7)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--trace", default="", help="run one traced (untimed) step first; Chrome trace path")
     args = ap.parse_args()
+    global TRACE
+    TRACE = args.trace or None
     import cdnaml
     spark = cdnaml.SparkSession.builder.appName("bench_configs").getOrCreate()
     {"lr": bench_lr, "cv": bench_cv, "gbdt": bench_gbdt, "infer": bench_infer, "airbnb": bench_airbnb}[

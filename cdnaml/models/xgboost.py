@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from ..ops import kernels as K
+from ..utils import tracing as _tr
 from ..sql import types as T
 from ..sql.batch import ColumnData
 from ..sql.dataframe import MapPlan
@@ -173,7 +174,8 @@ class _XgbEstimatorBase(Estimator):
         best, best_round, history = float("inf"), -1, []
         train_w = None if val_mask is None else (~val_mask).to(torch.uint8)
         for m in range(self.getN_estimators()):
-            g, h = grad_hess(F)  # [n, n_out] each
+            with _tr.span("xgb.grad_hess", round=m):
+                g, h = grad_hess(F)  # [n, n_out] each
             bag = None
             rate = self.getSubsample()
             if rate < 1.0:
@@ -189,11 +191,12 @@ class _XgbEstimatorBase(Estimator):
                 trainer.train(1, {"v0": v0, "v1": g[:, k].float().contiguous()},
                               None if bag is None else bag[None, :].contiguous(), forest)
                 t = len(forest.roots) - 1
-                self._apply_l1(forest, t)
-                nodes, vals, masks = forest.binned_arrays(dev, t)
-                col = F[:, k].contiguous()
-                K.predict_binned_add(data.bins, nodes, 0, vals, masks, eta, col)
-                F[:, k] = col
+                with _tr.span("xgb.update_margin", round=m):
+                    self._apply_l1(forest, t)
+                    nodes, vals, masks = forest.binned_arrays(dev, t)
+                    col = F[:, k].contiguous()
+                    K.predict_binned_add(data.bins, nodes, 0, vals, masks, eta, col)
+                    F[:, k] = col
             if val_mask is not None and metric_fn is not None:
                 v = metric_fn(F, val_mask)
                 history.append(v)

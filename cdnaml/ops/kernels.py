@@ -157,6 +157,9 @@ HIST_PACKED = __import__("os").environ.get("CDNAML_HIST_PACKED", "0") != "0"
 HIST5_PACKED = __import__("os").environ.get("CDNAML_HIST5_PACKED", "1") != "0"
 HIST5_PACKED_MAXT = int(__import__("os").environ.get("CDNAML_HIST5_PACKED_MAXT", "8"))
 HIST5_PACKED_LDS = int(__import__("os").environ.get("CDNAML_HIST5_PACKED_LDS", str(128 * 1024)))
+# wave-compacted packed kernel (hist5q): full-wave LDS atomic rounds over sparse (row, tree) work
+# 0 off, 1 where it pays (deep levels), 2 always (tests)
+HIST5_COMPACT = int(__import__("os").environ.get("CDNAML_HIST5_COMPACT", "1"))
 
 
 def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int, qmax_bits: int = 62) -> float:
@@ -429,7 +432,8 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
     lib = _lib.lib()
     maxt = int(lib.cdna_hist5_max_trees())
     packed = HIST5_PACKED and mode == 0 and v0 is None
-    kbits = mode | (4 if (mode == 0 and v0 is not None) else 0) | (16 if packed else 0)
+    compact = packed and HIST5_COMPACT
+    kbits = mode | (4 if (mode == 0 and v0 is not None) else 0) | (16 if packed else 0) | (64 if compact else 0)
     per_slot = 8 * B * int(lib.cdna_hist4_bytes_per_bin(kbits, int(C)))
     if per_slot > 150 * 1024:
         raise ValueError("histogram too large for LDS (classes x bins)")
@@ -459,10 +463,17 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
     SB = max(min(SB, (rows[i + 1][0] if i + 1 < ng else S) - rows[i][0]) for i in range(ng))
     max_nt = max(r[2] - r[1] + 1 for r in rows)
     bucket = 1 if max_nt <= 1 else 2 if max_nt <= 2 else 4 if max_nt <= 4 else 8 if max_nt <= 8 else 16
-    lds_used = ((SB * per_slot + 15) // 16) * 16 + bucket * 512 + SB + 16
+    big = packed and SB * per_slot > 8192 * 8  # 1024-thread blocks: 1 per CU
+    # wave compaction pays once the plane needs 1024-thread blocks and several trees share
+    # a pass (measured per level: profiles/hist_micro_1e8_compact.txt); below that the
+    # lane-per-row kernel's fewer LDS instructions win
+    compact = compact and (HIST5_COMPACT >= 2 or (big and max_nt >= 2))
+    kbits = kbits if compact else (kbits & ~64)
+    rbuf = 16 * 128 * 12 if compact else 0
+    lds_used = ((SB * per_slot + 15) // 16) * 16 + rbuf + bucket * 512 + SB + 16
     if lds_used > 160 * 1024:
         raise ValueError("local-node tables do not fit in LDS next to the histogram")
-    target_blocks = 512 if (packed and SB * per_slot > 8192 * 8) else 1024  # 1024-thread blocks: 1 per CU
+    target_blocks = 512 if big else 1024
     nchunk = int(max(1, min((target_blocks + G * ng - 1) // (G * ng), (n + 8191) // 8192)))
     nchunk = max(nchunk, -(-n // (1 << 23)))
     mw = 0 if feat_mask is None else feat_mask.shape[1]

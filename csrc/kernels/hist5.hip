@@ -312,6 +312,7 @@ __global__ __launch_bounds__(TH) void hist5p_kernel(const Hist5Args a) {
   const int valid_f = a.d - fbase;
   uint32_t fvalid = valid_f >= 8 ? 0xFFu : ((1u << (valid_f > 0 ? valid_f : 0)) - 1u);
   const uint32_t frot = ((fvalid >> rot) | (fvalid << (8 - rot))) & 0xFFu;
+  const bool all8 = valid_f >= 8;
   __syncthreads();
 
   const int64_t rb = (int64_t)chunk * a.rows_per_chunk;
@@ -409,10 +410,15 @@ __global__ __launch_bounds__(TH) void hist5p_kernel(const Hist5Args a) {
           uint32_t mrot = frot;
           if (MASKED) mrot &= ((mk[k] >> rot) | (mk[k] << (8 - rot))) & 0xFFu;
           const unsigned long long add = ((unsigned long long)wv << kPackShift) + (unsigned long long)wv * qoff;
+          if (!MASKED && all8) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            if (!((mrot >> j) & 1u)) continue;
-            atomicAdd(h64 + base + (uint32_t)cell[j], add);
+            for (int j = 0; j < 8; ++j) atomicAdd(h64 + base + (uint32_t)cell[j], add);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              if (!((mrot >> j) & 1u)) continue;
+              atomicAdd(h64 + base + (uint32_t)cell[j], add);
+            }
           }
         }
       }
@@ -443,6 +449,251 @@ __global__ __launch_bounds__(TH) void hist5p_kernel(const Hist5Args a) {
   }
 }
 
+
+
+// Wave-compacted packed kernel.  An LDS atomic costs the same whatever
+// fraction of the wave is active (profiles/lds_mask_bench_mi355x.txt: 16 clk
+// per ds_add_u64 per CU at 64, 32 or 8 active lanes), and (row, tree) work is
+// sparse: bootstrap zeros leave 37 % of lanes idle at level 0 and, below it,
+// only rows of the smaller child of each sibling pair are built.  So each
+// wave queues its active (row, tree) items and issues the 8 feature atomics
+// only for full 64-item rounds:
+//   * the row's bins word and offset value go once per row-iteration to a
+//     per-wave LDS row buffer (two parities, so items of the previous
+//     iteration stay readable);
+//   * an item is one word (source lane | parity | weight | slot), moved into
+//     queue position with one ds_permute_b32 whose destinations form a full
+//     permutation (inactive lanes fill the tail positions);
+//   * two register slots hold up to 127 pending items; a round drains 64.
+// Leftover items of iteration i-1 are flushed (a partial round) at the end
+// of iteration i before their row-buffer parity is reused.
+template <bool MASKED, int NT, int TH>
+__global__ __launch_bounds__(TH) void hist5q_kernel(const Hist5Args a) {
+  const int drain_iters = a.drain_iters;
+  constexpr int NW = TH / 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int G = (a.d + 7) / 8;
+  const int plane = a.SB * 8 * a.B;
+  unsigned long long* h64 = reinterpret_cast<unsigned long long*>(smem);
+  uint2* rbuf_b = reinterpret_cast<uint2*>(h64 + (size_t)plane);  // [NW][2][64] bins words
+  uint32_t* rbuf_q = reinterpret_cast<uint32_t*>(rbuf_b + NW * 128);  // [NW][2][64] q + 2^23
+  int16_t* lt = reinterpret_cast<int16_t*>(rbuf_q + NW * 128);
+  uint8_t* lmask = reinterpret_cast<uint8_t*>(lt + NT * 256);
+  const uint32_t w = cdna::xcd_remap(blockIdx.x, gridDim.x);
+  const int g = (int)(w % G);
+  const int grp = (int)((w / G) % a.ngroups);
+  const int chunk = (int)(w / ((uint32_t)G * a.ngroups));
+  const int s0 = a.grp[grp * 5 + 0], t0 = a.grp[grp * 5 + 1], t1 = a.grp[grp * 5 + 2];
+  const int id1 = a.grp[grp * 5 + 4];
+  const int nt = t1 - t0 + 1;
+  const int fbase = g * 8;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int rot = lane & 7;
+
+  for (int i = threadIdx.x; i < plane; i += TH) h64[i] = 0ull;
+  uint32_t acc_c[kPackCells];
+  long long acc_s[kPackCells];
+#pragma unroll
+  for (int i = 0; i < kPackCells; ++i) {
+    acc_c[i] = 0u;
+    acc_s[i] = 0;
+  }
+  for (int i = threadIdx.x; i < NT * 256; i += TH) {
+    const int k = i >> 8, loc = i & 255;
+    int v = -1;
+    const int id = k < nt ? a.tfirst[t0 + k] + loc : 0;
+    const int idend = k + 1 < nt ? a.tfirst[t0 + k + 1] : id1;
+    if (k < nt && loc != 255 && id < idend) {
+      const int sl = a.build_slot[id];
+      if (sl >= s0 && sl < s0 + a.SB) v = sl - s0;
+    }
+    lt[i] = (int16_t)v;
+  }
+  if (MASKED) {
+    for (int i = threadIdx.x; i < a.SB; i += TH) {
+      const int slot = s0 + i;
+      uint32_t m = 0u;
+      if (slot < a.S) m = (a.feat_mask[(int64_t)slot * a.mask_words + (fbase >> 5)] >> (fbase & 31)) & 0xFFu;
+      const int valid = a.d - fbase;
+      if (valid < 8) m &= (1u << (valid > 0 ? valid : 0)) - 1u;
+      lmask[i] = (uint8_t)m;
+    }
+  }
+  int fsel[8], fsh[8], foff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int jj = (j + rot) & 7;
+    fsel[j] = jj >> 2;
+    fsh[j] = (jj & 3) * 8;
+    foff[j] = jj * a.B;
+  }
+  const int valid_f = a.d - fbase;
+  const uint32_t fvalid = valid_f >= 8 ? 0xFFu : ((1u << (valid_f > 0 ? valid_f : 0)) - 1u);
+  const uint32_t frot = ((fvalid >> rot) | (fvalid << (8 - rot))) & 0xFFu;
+  const bool all8 = valid_f >= 8;  // block-uniform: no per-feature guards in the atomic rounds
+  __syncthreads();
+
+  const int64_t rb = (int64_t)chunk * a.rows_per_chunk;
+  int64_t re = rb + a.rows_per_chunk;
+  if (re > a.n) re = a.n;
+  const int64_t n = a.n;
+  const int slot_cells = 8 * a.B;
+  uint2* my_b = rbuf_b + wid * 128;
+  uint32_t* my_q = rbuf_q + wid * 128;
+
+// one queue round: lanes with VALID take the item in word IT
+#define H5Q_ROUND(IT, VALID)                                                                    \
+  if (VALID) {                                                                                  \
+    const uint32_t it_ = (IT);                                                                  \
+    const int src_ = (int)(it_ & 127u);                                                         \
+    const uint2 bw_ = my_b[src_];                                                               \
+    const unsigned long long qo_ = my_q[src_];                                                  \
+    const uint32_t wv_ = (it_ >> 7) & 255u;                                                     \
+    const int ls_ = (int)(it_ >> 15);                                                           \
+    uint32_t mr_ = frot;                                                                        \
+    if (MASKED) {                                                                               \
+      const uint32_t mk_ = lmask[ls_];                                                          \
+      mr_ &= ((mk_ >> rot) | (mk_ << (8 - rot))) & 0xFFu;                                       \
+    }                                                                                           \
+    const unsigned long long add_ = ((unsigned long long)wv_ << kPackShift) + wv_ * qo_;        \
+    unsigned long long* hb_ = h64 + ls_ * slot_cells;                                           \
+    if (!MASKED && all8) {                                                                      \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j)                                             \
+        atomicAdd(hb_ + foff[j] + (int)__builtin_amdgcn_ubfe(fsel[j] ? bw_.y : bw_.x,           \
+                                                               (uint32_t)fsh[j], 8u), add_);    \
+    } else {                                                                                    \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                           \
+        if ((mr_ >> j) & 1u)                                                                    \
+          atomicAdd(hb_ + foff[j] + (int)__builtin_amdgcn_ubfe(fsel[j] ? bw_.y : bw_.x,         \
+                                                                 (uint32_t)fsh[j], 8u), add_);  \
+      }                                                                                         \
+    }                                                                                           \
+  }
+
+  auto drain = [&]() {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPackCells; ++i) {
+      const int idx = (int)threadIdx.x + i * TH;
+      if (idx < plane) {
+        const unsigned long long v = h64[idx];
+        if (v) {
+          const uint32_t c = (uint32_t)(v >> kPackShift);
+          acc_c[i] += c;
+          acc_s[i] += (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)c;
+          h64[idx] = 0ull;
+        }
+      }
+    }
+    __syncthreads();
+  };
+
+  uint64_t b8 = 0;
+  float x1 = 0.f;
+  uint32_t cd[NT];
+  const int64_t tstride = (int64_t)n;
+  int64_t r = rb + threadIdx.x;
+  if (r < re) {
+    b8 = a.bins[(int64_t)g * n + r];
+    x1 = a.v1[r];
+    const uint16_t* cp = a.codes + (int64_t)t0 * n + r;
+#pragma unroll
+    for (int k = 0; k < NT; ++k) cd[k] = (uint32_t)cp[(k < nt ? k : 0) * tstride];
+  } else {
+#pragma unroll
+    for (int k = 0; k < NT; ++k) cd[k] = 0xFFu;
+  }
+
+  uint32_t qa = 0u, qb = 0u;  // queue slots: positions [0, 64) and [64, 128)
+  int cnt = 0, prev = 0, par = 0;
+  int iter = 0;
+  for (int64_t rbase = rb; rbase < re; rbase += TH, r += TH, ++iter) {
+    if (r >= re) {
+#pragma unroll
+      for (int k = 0; k < NT; ++k) cd[k] = 0xFFu;
+    }
+    uint64_t nb8 = 0;
+    float nx1 = 0.f;
+    uint32_t ncd[NT];
+    const int64_t rn = r + TH;
+    if (rn < re) {
+      nb8 = a.bins[(int64_t)g * n + rn];
+      nx1 = a.v1[rn];
+      const uint16_t* cp = a.codes + (int64_t)t0 * n + rn;
+#pragma unroll
+      for (int k = 0; k < NT; ++k) ncd[k] = (uint32_t)cp[(k < nt ? k : 0) * tstride];
+    } else {
+#pragma unroll
+      for (int k = 0; k < NT; ++k) ncd[k] = 0xFFu;
+    }
+    int q1 = (int)rintf(x1 * a.qs1);
+    q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+    my_b[par * 64 + lane] = make_uint2((uint32_t)b8, (uint32_t)(b8 >> 32));
+    my_q[par * 64 + lane] = (uint32_t)(q1 + kPackQ);
+    int lsk[NT];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) lsk[k] = lt[k * 256 + (int)(cd[k] & 0xFFu)];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      const bool act = lsk[k] >= 0;
+      const uint64_t mask = __builtin_amdgcn_ballot_w64(act);
+      if (mask == 0ull) continue;
+      const int m = __builtin_popcountll(mask);
+      const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+      const uint32_t item = (uint32_t)(par * 64 + lane) | (((cd[k] >> 8) & 255u) << 7) |
+                            ((uint32_t)(act ? lsk[k] : 0) << 15);
+      const int pos = act ? rank : m + lane - rank;
+      const uint32_t rcv = (uint32_t)__builtin_amdgcn_ds_permute(((cnt + pos) & 63) * 4, (int)item);
+      const int rel = (lane - cnt) & 63;
+      if (rel < m) {
+        if (lane >= cnt) qa = rcv;
+        else qb = rcv;
+      }
+      cnt += m;
+      if (cnt >= 64) {
+        H5Q_ROUND(qa, true);
+        qa = qb;
+        cnt -= 64;
+        prev = 0;
+      }
+    }
+    if (prev > 0) {  // items of the previous iteration: their row-buffer parity is reused next
+      H5Q_ROUND(qa, lane < cnt);
+      cnt = 0;
+    }
+    prev = cnt;
+    par ^= 1;
+    b8 = nb8;
+    x1 = nx1;
+#pragma unroll
+    for (int k = 0; k < NT; ++k) cd[k] = ncd[k];
+    if ((iter + 1) % drain_iters == 0) {
+      H5Q_ROUND(qa, lane < cnt);
+      cnt = 0;
+      prev = 0;
+      drain();
+    }
+  }
+  H5Q_ROUND(qa, lane < cnt);
+  drain();
+#undef H5Q_ROUND
+#pragma unroll
+  for (int i = 0; i < kPackCells; ++i) {
+    const int idx = (int)threadIdx.x + i * TH;
+    if (idx >= plane || acc_c[i] == 0u) continue;
+    const int ls = idx / (8 * a.B);
+    const int jj = (idx / a.B) & 7;
+    const int bn = idx % a.B;
+    const int f = fbase + jj;
+    const int slot = s0 + ls;
+    if (f < a.d && slot < a.S) {
+      unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+      atomicAdd(o, (unsigned long long)acc_c[i]);
+      atomicAdd(o + 1, (unsigned long long)acc_s[i]);
+    }
+  }
+}
 
 // Row-record partition: every row moves, in every tree, from its active node to
 // the chosen child (or finishes).  grid.y = tree.  The tree's split table
@@ -597,6 +848,22 @@ void launch5p(const Hist5Args& a, int nt_max, unsigned nblk, size_t lds, bool bi
   else launch5p_t<MASKED, 512>(a, nt_max, nblk, lds, st);
 }
 
+template <bool MASKED, int TH>
+void launch5q_t(const Hist5Args& a, int nt_max, unsigned nblk, size_t lds, hipStream_t st) {
+  if (nt_max <= 1) go(hist5q_kernel<MASKED, 1, TH>, nblk, TH, lds, st, a);
+  else if (nt_max <= 2) go(hist5q_kernel<MASKED, 2, TH>, nblk, TH, lds, st, a);
+  else if (nt_max <= 4) go(hist5q_kernel<MASKED, 4, TH>, nblk, TH, lds, st, a);
+  else if (nt_max <= 8) go(hist5q_kernel<MASKED, 8, TH>, nblk, TH, lds, st, a);
+  else go(hist5q_kernel<MASKED, 16, TH>, nblk, TH, lds, st, a);
+}
+
+// compacted kernel: always 1024-thread blocks (16 waves per CU; a 512-thread
+// block at >128 VGPRs would run 8)
+template <bool MASKED>
+void launch5q(const Hist5Args& a, int nt_max, unsigned nblk, size_t lds, hipStream_t st) {
+  launch5q_t<MASKED, 1024>(a, nt_max, nblk, lds, st);
+}
+
 inline int nt_bucket(int nt) { return nt <= 1 ? 1 : nt <= 2 ? 2 : nt <= 4 ? 4 : nt <= 8 ? 8 : 16; }
 
 }  // namespace
@@ -604,7 +871,8 @@ inline int nt_bucket(int nt) { return nt <= 1 ? 1 : nt <= 2 ? 2 : nt <= 4 ? 4 : 
 CDNA_API int cdna_hist5_max_trees() { return kMaxTrees; }
 
 // mode bit0: classes; bit2: v0 present; bit4: packed single-atomic regression
-// (|v * qs1| <= 2^23, plane <= 8192 cells).  grp rows must satisfy t1 - t0 < 16;
+// (|v * qs1| <= 2^23, plane <= 16384 cells); bit6 (with bit4): wave-compacted
+// packed kernel.  grp rows must satisfy t1 - t0 < 16;
 // `id_span_max` = max trees per group (sizes the LDS local -> slot tables).
 CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T, const uint16_t* codes,
                         const int* tfirst, const float* v0, const float* v1, const int* label, int C,
@@ -652,7 +920,8 @@ CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T,
   const bool masked = feat_mask != nullptr;
   const int ntm = id_span_max;
   if (mode & 16) {  // packed single-atomic regression
-    const bool big = plane > (size_t)kPackCells * 512;
+    const bool compact = (mode & 64) != 0;
+    const bool big = compact || plane > (size_t)kPackCells * 512;
     {
       const int th = big ? 1024 : 512;
       const int64_t rows_ok = ((int64_t)1 << 20) / (wmax > 0 ? wmax + 1 : 1);  // rows * wmax < 2^20
@@ -661,10 +930,16 @@ CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T,
     if (classes || has_v0 || plane > (size_t)kPackCells * 1024) return (int)hipErrorInvalidValue;
     a.n64 = 1;
     a.n32 = 0;
-    const size_t lds_p = plane * 8 + (size_t)nt_bucket(ntm) * 512 + SB + 16;
+    const size_t rbuf = compact ? (size_t)16 * 128 * 12 : 0;  // per-wave row buffers
+    const size_t lds_p = plane * 8 + rbuf + (size_t)nt_bucket(ntm) * 512 + SB + 16;
     if (lds_p > 160 * 1024) return (int)hipErrorInvalidValue;
-    if (masked) launch5p<true>(a, ntm, nblk, lds_p, big, st);
-    else launch5p<false>(a, ntm, nblk, lds_p, big, st);
+    if (compact) {
+      if (masked) launch5q<true>(a, ntm, nblk, lds_p, st);
+      else launch5q<false>(a, ntm, nblk, lds_p, st);
+    } else {
+      if (masked) launch5p<true>(a, ntm, nblk, lds_p, big, st);
+      else launch5p<false>(a, ntm, nblk, lds_p, big, st);
+    }
     return (int)hipGetLastError();
   }
   if (classes) {

@@ -1,0 +1,10 @@
+#!/bin/bash
+# hist tests + micro (compact vs lane-per-row) + headline bench with the automatic choice
+set -o pipefail
+mkdir -p gpurun_out/compact
+O=gpurun_out/compact
+timeout -k 10 300 python -m pytest tests/test_kernels_gpu.py -q -x -k "hist_codes or partition" > $O/test.log 2>&1 &&
+timeout -k 10 400 python bench.py --steps 3 --warmup 1 --trace $O/trace.json > $O/bench.json 2> $O/bench.log
+rc=$?
+tail -3 $O/test.log; grep -v amdgpu.ids $O/bench.log | tail -14; cat $O/bench.json
+exit $rc

@@ -316,8 +316,12 @@ def _codes_state(n, T, per, seed):
 
 
 @pytest.mark.parametrize("kind", ["moments", "moments_v0", "classes", "masked", "packed", "packed_masked",
-                                  "packed_wmax"])
+                                  "packed_wmax", "packed_nc", "packed_nc_masked", "packed_big", "packed_big_masked",
+                                  "packed_q", "packed_q_masked", "packed_q_wmax"])
 def test_hist_codes(dev, kind, monkeypatch):
+    # packed_q_*: wave-compacted kernel (hist5q) forced; packed_nc_*: lane-per-row packed kernel
+    # (hist5p) only; packed / packed_big: automatic choice (*_big: 128 KB plane -> 1024-thread blocks,
+    # where the compacted kernel is chosen)
     n, d, T, per, B, C = 30000, 21, 18, 5, 40, 3
     g = torch.Generator().manual_seed(7)
     X = torch.randn(n, d, generator=g)
@@ -330,15 +334,17 @@ def test_hist_codes(dev, kind, monkeypatch):
     lab = torch.randint(0, C, (n,), generator=g, dtype=torch.int32)
     fm = None
     monkeypatch.setattr(K, "HIST5_PACKED", kind.startswith("packed"))
+    monkeypatch.setattr(K, "HIST5_COMPACT", 0 if kind.startswith("packed_nc") else
+                        2 if kind.startswith("packed_q") else 1)
     if kind.endswith("masked"):
         fm = torch.randint(0, 2 ** 31 - 1, (S, (d + 31) // 32), generator=g, dtype=torch.int64).to(torch.int32)
     mode = 1 if kind == "classes" else 0
     v0 = h if kind == "moments_v0" else None
     ref = K.hist_codes(mode, bins, d, codes, tfirst, v0, y, lab, C, build, slot_tree, id_tree, fm, B)
-    wmax = int(((codes.to(torch.int32) & 0xFFFF) >> 8).max()) if kind == "packed_wmax" else 255
+    wmax = int(((codes.to(torch.int32) & 0xFFFF) >> 8).max()) if kind.endswith("wmax") else 255
     out = K.hist_codes(mode, bins.to(dev), d, codes.to(dev), tfirst, None if v0 is None else v0.to(dev), y.to(dev),
                        lab.to(dev), C, build.to(dev), slot_tree, id_tree, None if fm is None else fm.to(dev), B,
-                       lds_budget=16 * 1024, wmax=wmax).cpu()
+                       lds_budget=(128 if "big" in kind else 16) * 1024, wmax=wmax).cpu()
     assert torch.allclose(out, ref, rtol=1e-6, atol=1e-3)
 
 
