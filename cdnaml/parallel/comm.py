@@ -13,6 +13,17 @@ Collectives used by the engine:
   * all_gather (fixed / variable length) — quantile sketches, dictionaries;
   * all_to_all_v — hash shuffles (groupBy / join / dropDuplicates / repartition);
   * broadcast — model parameters, tuning trial configs.
+
+Failure handling:
+  * every collective runs inside ``_guard``: a failure surfaces as
+    :class:`CommError` naming the rank, the collective and its call number;
+  * watchdog: the process group is created with ``CDNAML_COMM_TIMEOUT``
+    seconds (default 1800), so a peer that died or hangs turns a blocked
+    collective into an error instead of a silent hang;
+  * fault injection: ``CDNAML_FAULT=rank:op:n`` makes ``rank`` fail its n-th
+    ``op`` call (op = all_reduce, all_gather, broadcast, all_to_all, barrier
+    or ``*``) before anything is sent; the failing rank tears its process
+    group down so peers error out promptly.
 """
 from __future__ import annotations
 
@@ -23,6 +34,49 @@ from typing import Any, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
+
+
+class CommError(RuntimeError):
+    """A collective failed on this rank (injected, a peer died, or the watchdog timed out)."""
+
+    def __init__(self, rank: int, op: str, call: int, cause: str):
+        super().__init__(f"[rank {rank}] collective {op} (call #{call}) failed: {cause}")
+        self.rank, self.op, self.call = rank, op, call
+
+
+def _parse_fault(spec: Optional[str]):
+    if not spec:
+        return None
+    try:
+        r, op, n = spec.split(":")
+        return int(r), op, int(n)
+    except ValueError:
+        raise ValueError(f"CDNAML_FAULT must be rank:op:n, got {spec!r}") from None
+
+
+class _Guard:
+    def __init__(self, comm: "Comm", op: str):
+        self.comm, self.op = comm, op
+
+    def __enter__(self):
+        c = self.comm
+        c.op_calls[self.op] = c.op_calls.get(self.op, 0) + 1
+        self.n = c.op_calls[self.op]
+        f = c.fault
+        if f is not None and f[0] == c.rank and f[1] in (self.op, "*"):
+            k = self.n if f[1] == self.op else sum(c.op_calls.values())
+            if k == f[2]:
+                c.fault = None
+                err = CommError(c.rank, self.op, self.n, "injected fault (CDNAML_FAULT)")
+                c.abort()
+                raise err
+        return self
+
+    def __exit__(self, et, ev, tb):
+        if ev is not None and not isinstance(ev, CommError) and isinstance(ev, (RuntimeError, ConnectionError,
+                                                                                  OSError)):
+            raise CommError(self.comm.rank, self.op, self.n, f"{type(ev).__name__}: {ev}") from ev
+        return False
 
 
 class Comm:
@@ -36,6 +90,20 @@ class Comm:
         self.backend = dist.get_backend() if self.initialized else "local"
         self.bytes_reduced = 0
         self.calls = 0
+        self.op_calls = {}
+        self.fault = _parse_fault(os.environ.get("CDNAML_FAULT"))
+
+    def _guard(self, op: str) -> _Guard:
+        return _Guard(self, op)
+
+    def abort(self) -> None:
+        """Tear this rank's process group down (peers' pending collectives then fail)."""
+        if self.initialized and dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:  # noqa: BLE001 - best effort during failure handling
+                pass
+            self.initialized = False
 
     # ----------------------------------------------------------------- info
     @property
@@ -59,7 +127,8 @@ class Comm:
         w = self._dev_tensor(t)
         if not w.is_contiguous():
             w = w.contiguous()
-        dist.all_reduce(w, op=rop)
+        with self._guard("all_reduce"):
+            dist.all_reduce(w, op=rop)
         if w.data_ptr() != t.data_ptr():
             t.copy_(w)
         return t
@@ -90,14 +159,16 @@ class Comm:
         if not self.distributed:
             return [obj]
         out = [None] * self.world_size
-        dist.all_gather_object(out, obj)
+        with self._guard("all_gather"):
+            dist.all_gather_object(out, obj)
         return out
 
     def broadcast_object(self, obj: Any, src: int = 0) -> Any:
         if not self.distributed:
             return obj
         box = [obj]
-        dist.broadcast_object_list(box, src=src)
+        with self._guard("broadcast"):
+            dist.broadcast_object_list(box, src=src)
         return box[0]
 
     def all_gather_varlen(self, t: torch.Tensor) -> List[torch.Tensor]:
@@ -108,21 +179,24 @@ class Comm:
         sizes = [torch.zeros_like(n) for _ in range(self.world_size)]
         n_w = self._dev_tensor(n)
         sizes_w = [self._dev_tensor(s) for s in sizes]
-        dist.all_gather(sizes_w, n_w)
+        with self._guard("all_gather"):
+            dist.all_gather(sizes_w, n_w)
         sizes = [int(s.item()) for s in sizes_w]
         mx = max(sizes)
         pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
         pad_w = self._dev_tensor(pad)
         bufs = [torch.empty_like(pad_w) for _ in range(self.world_size)]
-        dist.all_gather(bufs, pad_w)
+        with self._guard("all_gather"):
+            dist.all_gather(bufs, pad_w)
         return [b[:s].to(t.device) for b, s in zip(bufs, sizes)]
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if not self.distributed:
             return t
         w = self._dev_tensor(t)
-        dist.broadcast(w, src=src)
+        with self._guard("broadcast"):
+            dist.broadcast(w, src=src)
         if w.data_ptr() != t.data_ptr():
             t.copy_(w)
         return t
@@ -146,7 +220,8 @@ class Comm:
         send_n = torch.tensor([c.shape[0] for c in chunks], dtype=torch.int64)
         recv_n = torch.empty(W, dtype=torch.int64)
         s_w, r_w = self._dev_tensor(send_n), self._dev_tensor(recv_n)
-        dist.all_to_all_single(r_w, s_w)
+        with self._guard("all_to_all"):
+            dist.all_to_all_single(r_w, s_w)
         recv_counts = [int(x) for x in r_w.cpu().tolist()]
         flat = torch.cat([c.reshape(-1) for c in chunks]) if any(c.numel() for c in chunks) else \
             torch.empty(0, dtype=ref.dtype, device=ref.device)
@@ -156,8 +231,9 @@ class Comm:
             flat = flat.to(torch.uint8)
         fw = self._dev_tensor(flat)
         out = torch.empty(sum(recv_counts) * inner, dtype=fw.dtype, device=fw.device)
-        dist.all_to_all_single(out, fw, output_split_sizes=[r * inner for r in recv_counts],
-                               input_split_sizes=[int(c.shape[0]) * inner for c in chunks])
+        with self._guard("all_to_all"):
+            dist.all_to_all_single(out, fw, output_split_sizes=[r * inner for r in recv_counts],
+                                   input_split_sizes=[int(c.shape[0]) * inner for c in chunks])
         self.calls += 2
         self.bytes_reduced += flat.numel() * flat.element_size()
         out = out.to(ref.device)
@@ -171,17 +247,21 @@ class Comm:
 
     def barrier(self):
         if self.distributed:
-            if self.backend == "nccl":
-                dist.barrier(device_ids=[self.device.index])
-            else:
-                dist.barrier()
+            with self._guard("barrier"):
+                if self.backend == "nccl":
+                    dist.barrier(device_ids=[self.device.index])
+                else:
+                    dist.barrier()
 
 
-def init_from_env(device_type: Optional[str] = None, timeout_s: float = 1800.0) -> None:
+def init_from_env(device_type: Optional[str] = None, timeout_s: Optional[float] = None) -> None:
     """Initialise torch.distributed from torchrun-style env vars (idempotent).
 
-    MASTER_ADDR should be 127.0.0.1 for single-node runs.
+    MASTER_ADDR should be 127.0.0.1 for single-node runs.  The collective
+    watchdog timeout is ``timeout_s`` or ``CDNAML_COMM_TIMEOUT`` (seconds).
     """
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("CDNAML_COMM_TIMEOUT", "1800"))
     if not dist.is_available() or dist.is_initialized():
         return
     ws = int(os.environ.get("WORLD_SIZE", "1"))

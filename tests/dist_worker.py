@@ -76,7 +76,25 @@ def scenario_ml(spark):
     return out
 
 
-SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml}
+def scenario_fault(spark):
+    """CDNAML_FAULT=1:all_reduce:2 -> rank 1 fails its 2nd all-reduce; every rank must see a
+    CommError naming a rank and the collective instead of hanging (watchdog CDNAML_COMM_TIMEOUT)."""
+    import time
+    from cdnaml.models.regression import LinearRegression
+    from cdnaml.models.feature import VectorAssembler
+    from cdnaml.parallel.comm import CommError
+    df = VectorAssembler(inputCols=["x0", "x1", "x2", "x3"], outputCol="features").transform(_data(spark))
+    t0 = time.time()
+    try:
+        for _ in range(3):
+            LinearRegression().fit(df)
+        return {"rank": spark.comm.rank, "error": None}
+    except CommError as e:
+        return {"rank": spark.comm.rank, "error": str(e), "err_rank": e.rank, "op": e.op,
+                "seconds": time.time() - t0}
+
+
+SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault}
 
 
 def run(name):
@@ -86,6 +104,10 @@ def run(name):
 
 if __name__ == "__main__":
     res = run(sys.argv[1])
-    if int(os.environ.get("RANK", "0")) == 0:
+    rank = int(os.environ.get("RANK", "0"))
+    if sys.argv[1] == "fault":  # every rank reports (its own failure mode)
+        with open(f"{sys.argv[2]}.rank{rank}", "w") as f:
+            json.dump(res, f)
+    elif rank == 0:
         with open(sys.argv[2], "w") as f:
             json.dump(res, f)
