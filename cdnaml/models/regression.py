@@ -693,7 +693,17 @@ def boost(session, data, y_target_fn, grad_fn, T_rounds, est, seed, init_margin,
     forest = Forest(1)
     F = torch.full((n,), float(init_margin), dtype=torch.float32, device=dev)
     weights = []
-    for m in range(T_rounds):
+    # checkpointInterval + SparkContext.setCheckpointDir: resume from the last saved round
+    from .tree.checkpoint import RoundCheckpointer
+    ck = RoundCheckpointer(session, est, data.n_global, data.d,
+                           est.getCheckpointInterval() if est.hasParam("checkpointInterval") else None)
+    start = 0
+    resumed = ck.load()
+    if resumed is not None:
+        start, forest, Fm, extra = resumed
+        F = Fm.to(dev)
+        weights = list(extra["weights"])
+    for m in range(start, T_rounds):
         target = y_target_fn(F) if (m == 0 and first_weight_one) else grad_fn(F)
         bag = _bag_weights(data, 1, False, est.getSubsamplingRate(), seed + m)
         trainer.p.seed = seed + m
@@ -702,6 +712,7 @@ def boost(session, data, y_target_fn, grad_fn, T_rounds, est, seed, init_margin,
         nodes, vals, masks = forest.binned_arrays(dev, m)
         K.predict_binned_add(data.bins, nodes, 0, vals, masks, wgt, F)
         weights.append(wgt)
+        ck.maybe_save(m + 1, forest, F, {"weights": weights})
     return forest, np.asarray(weights)
 
 

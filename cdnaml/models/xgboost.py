@@ -63,6 +63,8 @@ _XGB = {
     "objective": ("learning objective", None, TC.toString),
     "num_workers": ("number of data-parallel workers (= GPUs of the SPMD job)", 1, TC.toInt),
     "use_gpu": ("train on the GPU (always true when one is present)", False, TC.toBoolean),
+    "checkpoint_interval": ("save the booster every N rounds under SparkContext.setCheckpointDir and resume "
+                            "an interrupted fit from it (-1: off)", -1, TC.toInt),
     "early_stopping_rounds": ("stop when the validation metric has not improved for this many rounds", None,
                               TC.toInt),
     "eval_metric": ("validation metric (rmse / logloss / mlogloss / error)", None, TC.toString),
@@ -173,7 +175,15 @@ class _XgbEstimatorBase(Estimator):
         esr = self.getEarly_stopping_rounds()
         best, best_round, history = float("inf"), -1, []
         train_w = None if val_mask is None else (~val_mask).to(torch.uint8)
-        for m in range(self.getN_estimators()):
+        from .tree.checkpoint import RoundCheckpointer
+        ck = RoundCheckpointer(session, self, data.n_global, data.d, self.getCheckpoint_interval())
+        start = 0
+        resumed = ck.load()
+        if resumed is not None:
+            start, forest, Fm, extra = resumed
+            F.copy_(Fm.to(F.device).view_as(F))
+            best, best_round, history = extra["best"], extra["best_round"], list(extra["history"])
+        for m in range(start, self.getN_estimators()):
             with _tr.span("xgb.grad_hess", round=m):
                 g, h = grad_hess(F)  # [n, n_out] each
             bag = None
@@ -206,6 +216,7 @@ class _XgbEstimatorBase(Estimator):
                     keep = (best_round + 1) * n_out
                     forest = _truncate(forest, keep)
                     break
+            ck.maybe_save(m + 1, forest, F, {"best": best, "best_round": best_round, "history": history})
         return forest, history
 
     def _apply_l1(self, forest: Forest, t: int):

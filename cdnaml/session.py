@@ -79,6 +79,15 @@ class SparkContext:
     def setLogLevel(self, level):
         pass
 
+    def setCheckpointDir(self, dirName: str) -> None:
+        """Directory for iterative-fit checkpoints (GBT / XGBoost every `checkpointInterval` rounds)."""
+        import os
+        os.makedirs(dirName, exist_ok=True)
+        self._session.conf.set("cdnaml.checkpoint.dir", dirName)
+
+    def getCheckpointDir(self):
+        return self._session.conf.getAll().get("cdnaml.checkpoint.dir")
+
     def parallelize(self, data, numSlices=None):
         return self._session.createDataFrame([(x,) if not isinstance(x, (tuple, list)) else x for x in data])
 

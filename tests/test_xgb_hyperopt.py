@@ -160,3 +160,51 @@ def test_hyperopt_over_distributed_mllib(spark):
     space = {"max_depth": hp.quniform("max_depth", 2, 5, 1), "num_trees": hp.quniform("num_trees", 10, 30, 1)}
     best = fmin(objective, space, algo=tpe.suggest, max_evals=4, trials=Trials(), rstate=np.random.default_rng(42))
     assert 2 <= best["max_depth"] <= 5 and 10 <= best["num_trees"] <= 30
+
+
+class _Crash(Exception):
+    pass
+
+
+@pytest.mark.parametrize("kind", ["xgb", "gbt"])
+def test_boosting_checkpoint_resume_is_exact(spark, tmp_path, monkeypatch, kind):
+    """a boosting fit interrupted after round 8 resumes from its round-8 checkpoint
+    (SparkContext.setCheckpointDir + checkpoint interval 4) and gives the uninterrupted model."""
+    from cdnaml.ml.regression import GBTRegressor
+    from cdnaml.models.tree import checkpoint as ckm
+    df, X, y = _reg(spark, n=1500, seed=5)
+    spark.sparkContext.setCheckpointDir(str(tmp_path / "ck"))
+
+    def make():
+        if kind == "xgb":
+            return XgboostRegressor(n_estimators=12, max_depth=3, learning_rate=0.3, subsample=0.8,
+                                    random_state=7, checkpoint_interval=4)
+        return GBTRegressor(maxIter=12, maxDepth=3, subsamplingRate=0.8, seed=7, checkpointInterval=4)
+
+    full = make().fit(df).transform(df).select("prediction").toPandas().prediction.values
+    import shutil
+    shutil.rmtree(tmp_path / "ck")
+    spark.sparkContext.setCheckpointDir(str(tmp_path / "ck"))
+    orig = ckm.RoundCheckpointer.maybe_save
+
+    def crashing(self, rounds_done, *a, **k):
+        orig(self, rounds_done, *a, **k)
+        if rounds_done == 10:
+            raise _Crash()
+    monkeypatch.setattr(ckm.RoundCheckpointer, "maybe_save", crashing)
+    with pytest.raises(_Crash):
+        make().fit(df)
+    monkeypatch.setattr(ckm.RoundCheckpointer, "maybe_save", orig)
+    seen = []
+    orig_load = ckm.RoundCheckpointer.load
+
+    def recording_load(self):
+        r = orig_load(self)
+        seen.append(None if r is None else r[0])
+        return r
+    monkeypatch.setattr(ckm.RoundCheckpointer, "load", recording_load)
+    resumed_model = make().fit(df)
+    assert seen == [8]  # resumed from the last complete interval before the crash
+    resumed = resumed_model.transform(df).select("prediction").toPandas().prediction.values
+    np.testing.assert_array_equal(full, resumed)
+    spark.conf.unset("cdnaml.checkpoint.dir")
