@@ -39,6 +39,8 @@ from ..util import IllegalArgumentException
 HIST_MODE = __import__("os").environ.get("CDNAML_RF_HIST", "full")
 # compact uint16 row records (hist5.hip) instead of int32 node ids + uint8 weights
 USE_CODES = __import__("os").environ.get("CDNAML_TREE_CODES", "1") != "0"
+# single-tree regression fits (boosting rounds, DecisionTree): rows kept grouped by node (seg.hip)
+USE_SEG = __import__("os").environ.get("CDNAML_TREE_SEG", "1") != "0"
 
 
 @dataclass
@@ -74,6 +76,12 @@ class BinnedData:
     d: int
     B: int
     missing_bin: bool = False         # bin 0 holds missing values (XGBoost sparsity-aware splits)
+    bins_rm: Optional[torch.Tensor] = None  # lazily built row-major copy [n, G, 8] (segment-mode histograms)
+
+    def row_major_bins(self) -> torch.Tensor:
+        if self.bins_rm is None:
+            self.bins_rm = self.bins.permute(1, 0, 2).contiguous()
+        return self.bins_rm
 
 
 def find_thresholds(sample: np.ndarray, d: int, max_bins: int, categorical: Dict[int, int]):
@@ -525,9 +533,23 @@ class ForestTrainer:
         # "full": accumulate all features, derive larger siblings by subtraction, mask at split time.
         masked = need_masks and HIST_MODE == "masked"
         subtract = not masked
+        # one regression tree: rows grouped by node in a permutation (segment mode)
+        use_seg = USE_SEG and T == 1 and not self.classification and not masked
         # row records (uint16 weight<<8 | local node) when every level fits 255 nodes per tree
-        use_codes = USE_CODES and p.max_depth <= 8
-        if use_codes:
+        use_codes = USE_CODES and p.max_depth <= 8 and not use_seg
+        if use_seg:
+            w1 = None if weights is None else weights.reshape(-1)
+            wmax = int(w1.max().item()) if (w1 is not None and w1.numel()) else 1
+            perm = (torch.arange(n, dtype=torch.int32, device=dev) if w1 is None else
+                    torch.nonzero(w1 > 0).flatten().to(torch.int32))
+            pl = perm.long()
+            v1p = stats_rows["v1"].float()[pl].contiguous()
+            v0p = None if stats_rows.get("v0") is None else stats_rows["v0"].float()[pl].contiguous()
+            wp = None if (w1 is None or wmax <= 1) else w1[pl].to(torch.uint8).contiguous()
+            seg_scales = K.seg_scales(v0p, v1p, wmax, n) if perm.numel() else (1.0, 1.0)
+            segs = np.array([[0, perm.numel()]], dtype=np.int64)
+            node = None
+        elif use_codes:
             codes = K.codes_init(weights, T, n, dev)
             wmax = int(weights.max().item()) if (weights is not None and weights.numel()) else 1
             node = None
@@ -570,7 +592,14 @@ class ForestTrainer:
             id_tree = np.array([e["tree"] for e in active], dtype=np.int32)
             tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
-                if use_codes:
+                if use_seg:
+                    sb = np.array([[segs[a, 0], segs[a, 1], slot_of[a]] for a in build_ids], dtype=np.int64)
+                    Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax, seg_scales,
+                                    # sparse node segments (>= 4 built nodes) gather whole rows from the
+                                    # row-major copy; dense shallow levels stream the [G][n] layout
+                                    bins_rm=data.row_major_bins() if (K.SEG_ROW_MAJOR and dev.type == "cuda"
+                                                                      and len(build_ids) >= 4) else None)
+                elif use_codes:
                     Hb = K.hist_codes(1 if self.classification else 0, data.bins, d, codes, tfirst,
                                       stats_rows.get("v0"), stats_rows.get("v1"), stats_rows.get("label"), self.C,
                                       build_slot, slot_tree, id_tree, fm_build, B, wmax=wmax)
@@ -684,7 +713,11 @@ class ForestTrainer:
             if nxt:
                 cm = np.stack(cat_masks).view(np.int32) if cat_masks else np.zeros((0, 8), np.int32)
                 with _tr.span("tree.partition", depth=depth):
-                    if use_codes:
+                    if use_seg:
+                        perm, v0p, v1p, wp, segs = K.seg_partition(data.bins, perm, v0p, v1p, wp, segs, split_feat,
+                                                                    split_bin, cat_off, cm.reshape(-1), child,
+                                                                    len(nxt))
+                    elif use_codes:
                         nxt_tree = np.array([e["tree"] for e in nxt], dtype=np.int32)
                         tfirst_next = torch.from_numpy(
                             np.searchsorted(nxt_tree, np.arange(T), side="left").astype(np.int32))

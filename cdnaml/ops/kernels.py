@@ -756,3 +756,173 @@ def logistic_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b: float,
     g[d] = res.sum()
     loss = (ww * (torch.nn.functional.softplus(m) - y * m)).sum()
     return g, loss
+
+
+# ------------------------------------------------------------ segment mode (seg.hip)
+SEG_HIST_CHUNK = 262144
+# row-major bins copy for segment histograms (one cache line per row instead of one per 8-feature group)
+SEG_ROW_MAJOR = __import__("os").environ.get("CDNAML_SEG_ROW_MAJOR", "1") != "0"
+SEG_PART_CHUNK = 8192
+
+
+def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_global: int):
+    """Fixed-point scales for one tree's statistics (packed when there is no v0)."""
+    if v0p is None:
+        return 1.0, _packed_scale(v1p)
+    return (_fixed_scale(v0p, n_global, wmax, qmax_bits=30), _fixed_scale(v1p, n_global, wmax, qmax_bits=30))
+
+
+def _seg_work(segs: np.ndarray, chunk: int) -> np.ndarray:
+    """segs [k, 3] {start, len, tag} -> work items [m, 3] of at most `chunk` rows each."""
+    segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
+    segs = segs[segs[:, 1] > 0]
+    if len(segs) == 0:
+        return np.zeros((0, 3), dtype=np.int32)
+    k = (segs[:, 1] + chunk - 1) // chunk
+    rep = np.repeat(np.arange(len(segs)), k)
+    j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
+    st = segs[rep, 0] + j * chunk
+    ln = np.minimum(chunk, segs[rep, 1] - j * chunk)
+    return np.stack([st, ln, segs[rep, 2]], 1).astype(np.int32)
+
+
+def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
+             v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
+             scales=None, bins_rm: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
+
+    segs: [k, 3] {start, len, slot}.  [..., 0] = sum w*v0 (or sum w when v0p is None), [..., 1] = sum w*v1.
+    """
+    G, n, _ = bins.shape
+    out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
+    segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
+    if S == 0 or len(segs) == 0:
+        return out
+    if not _native(bins):
+        flat = bins.permute(1, 0, 2).reshape(n, G * 8)[:, :d].long()
+        for s, ln, slot in segs:
+            if ln <= 0:
+                continue
+            rows = perm[s:s + ln].long()
+            w = torch.ones(ln, dtype=torch.float64) if wp is None else wp[s:s + ln].double()
+            a0 = w if v0p is None else w * v0p[s:s + ln].double()
+            a1 = w * v1p[s:s + ln].double()
+            bb = flat[rows]  # [ln, d]
+            idx = (torch.arange(d)[None, :] * B + bb).reshape(-1)
+            out[slot, :, :, 0] += torch.zeros(d * B, dtype=torch.float64).index_add_(
+                0, idx, a0[:, None].expand(-1, d).reshape(-1)).view(d, B)
+            out[slot, :, :, 1] += torch.zeros(d * B, dtype=torch.float64).index_add_(
+                0, idx, a1[:, None].expand(-1, d).reshape(-1)).view(d, B)
+        return out
+    packed = v0p is None
+    wm = int(max(1, min(255, wmax)))
+    chunk = SEG_HIST_CHUNK if not packed else min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1))
+    work = _seg_work(segs, chunk)
+    if len(work) == 0:
+        return out
+    qs0, qs1 = scales if scales is not None else seg_scales(v0p, v1p, wm, n)
+    wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
+    iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
+    mode = (1 if packed else 0) | (2 if wp is not None else 0) | (4 if bins_rm is not None else 0)
+    if bins_rm is not None:
+        assert bins_rm.shape == (n, G, 8) and bins_rm.is_contiguous()
+    src = bins if bins_rm is None else bins_rm
+    _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(src), n, d, B, _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp),
+                                        _ptr(wt), len(work), float(qs0), float(qs1), _ptr(iout),
+                                        _stream(bins.device)), "cdna_seg_hist")
+    out.copy_(iout)
+    if not packed:
+        out[..., 0] /= qs0
+    out[..., 1] /= qs1
+    return out
+
+
+def seg_partition(bins: torch.Tensor, perm: torch.Tensor, v0p: Optional[torch.Tensor], v1p: torch.Tensor,
+                  wp: Optional[torch.Tensor], segs: np.ndarray, split_feat: np.ndarray, split_bin: np.ndarray,
+                  cat_off: np.ndarray, cat_mask: np.ndarray, child: np.ndarray, n_next: int):
+    """Stable split of every node segment into its children's segments (rows of leaves dropped).
+
+    segs [A, 2] {start, len} of the active nodes (in active order); child [2A] next-level node index
+    or -1; n_next = number of next-level nodes.  Returns (perm, v0p, v1p, wp, segs_next [n_next, 2]).
+    """
+    G, n, _ = bins.shape
+    segs = np.asarray(segs, dtype=np.int64).reshape(-1, 2)
+    A = len(segs)
+    dev = perm.device
+    sf = np.asarray(split_feat, dtype=np.int32)
+    if not _native(bins):
+        flat = bins.permute(1, 0, 2).reshape(n, G * 8)
+        lefts = np.zeros(A, dtype=np.int64)
+        pieces = [[] for _ in range(max(n_next, 0))]
+        for a in range(A):
+            s, ln = segs[a]
+            if ln == 0 or sf[a] < 0:
+                continue
+            idx = torch.arange(int(s), int(s + ln))
+            rows = perm[idx].long()
+            bv = flat[rows, int(sf[a])].long()
+            if cat_off[a] >= 0:
+                m = torch.from_numpy(np.asarray(cat_mask, dtype=np.int64).reshape(-1, 8)[cat_off[a]] & 0xFFFFFFFF)
+                left = ((m[bv >> 5] >> (bv & 31)) & 1).bool()
+            else:
+                left = bv <= int(split_bin[a])
+            for side, sel in ((0, left), (1, ~left)):
+                c = int(child[2 * a + side])
+                if c >= 0:
+                    pieces[c].append(idx[sel])
+        order = [torch.cat(p) if p else torch.zeros(0, dtype=torch.long) for p in pieces]
+        lens = np.array([len(o) for o in order], dtype=np.int64)
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if n_next else np.zeros(0, np.int64)
+        cat = torch.cat(order) if order else torch.zeros(0, dtype=torch.long)
+        return (perm[cat].contiguous(), None if v0p is None else v0p[cat].contiguous(), v1p[cat].contiguous(),
+                None if wp is None else wp[cat].contiguous(), np.stack([starts, lens], 1))
+    # native: pass 1 counts left rows per chunk, host computes output offsets, pass 2 scatters
+    tags = np.arange(A, dtype=np.int64)
+    work = _seg_work(np.concatenate([segs, tags[:, None]], 1), SEG_PART_CHUNK)
+    nw = len(work)
+    L = _lib.lib()
+    sf_t = torch.from_numpy(sf).to(dev)
+    sb_t = torch.from_numpy(np.asarray(split_bin, dtype=np.int32)).to(dev)
+    co_t = torch.from_numpy(np.asarray(cat_off, dtype=np.int32)).to(dev)
+    cm = np.asarray(cat_mask, dtype=np.int32).reshape(-1)
+    cm_t = torch.from_numpy(cm if cm.size else np.zeros(8, np.int32)).to(dev)
+    wt = torch.from_numpy(work.reshape(-1)).to(dev)
+    lc = torch.zeros(max(nw, 1), dtype=torch.int32, device=dev)
+    if nw:
+        _lib.check(L.cdna_seg_partition(1, _ptr(bins), n, _ptr(perm), None, None, None, _ptr(wt), nw, _ptr(sf_t),
+                                        _ptr(sb_t), _ptr(co_t), _ptr(cm_t), None, None, _ptr(lc), None, None, None,
+                                        None, _stream(dev)), "cdna_seg_partition(count)")
+    lc_h = lc.cpu().numpy()[:nw].astype(np.int64)
+    wseg = work[:, 2].astype(np.int64)
+    wlen = work[:, 1].astype(np.int64)
+    rc_h = wlen - lc_h
+    child = np.asarray(child, dtype=np.int64)
+    # child sizes
+    lens = np.zeros(n_next, dtype=np.int64)
+    cl, cr = child[2 * wseg], child[2 * wseg + 1]
+    splits = sf[wseg] >= 0
+    np.add.at(lens, cl[splits & (cl >= 0)], lc_h[splits & (cl >= 0)])
+    np.add.at(lens, cr[splits & (cr >= 0)], rc_h[splits & (cr >= 0)])
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if n_next else np.zeros(0, np.int64)
+    # per-chunk offsets: child start + rows of the same child in earlier chunks of the segment
+    # (work items are in segment order: exclusive scans restart at each segment's first chunk)
+    first = np.searchsorted(wseg, wseg, side="left")
+    ex_l = np.cumsum(lc_h) - lc_h
+    ex_r = np.cumsum(rc_h) - rc_h
+    off_l = ex_l - ex_l[first]
+    off_r = ex_r - ex_r[first]
+    lb = np.where(splits & (cl >= 0), starts[np.maximum(cl, 0)] + off_l, -1) if n_next else np.full(nw, -1)
+    rb = np.where(splits & (cr >= 0), starts[np.maximum(cr, 0)] + off_r, -1) if n_next else np.full(nw, -1)
+    total = int(lens.sum())
+    perm_o = torch.empty(total, dtype=torch.int32, device=dev)
+    v1_o = torch.empty(total, dtype=torch.float32, device=dev)
+    v0_o = None if v0p is None else torch.empty(total, dtype=torch.float32, device=dev)
+    w_o = None if wp is None else torch.empty(total, dtype=torch.uint8, device=dev)
+    if nw and total:
+        lb_t = torch.from_numpy(lb.astype(np.int32)).to(dev)
+        rb_t = torch.from_numpy(rb.astype(np.int32)).to(dev)
+        _lib.check(L.cdna_seg_partition(2, _ptr(bins), n, _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp), _ptr(wt), nw,
+                                        _ptr(sf_t), _ptr(sb_t), _ptr(co_t), _ptr(cm_t), _ptr(lb_t), _ptr(rb_t),
+                                        None, _ptr(perm_o), _ptr(v0_o), _ptr(v1_o), _ptr(w_o), _stream(dev)),
+                   "cdna_seg_partition(scatter)")
+    return perm_o, v0_o, v1_o, w_o, np.stack([starts, lens], 1)

@@ -1,0 +1,396 @@
+// Single-tree "segment" mode: rows kept sorted by tree node (K5 + K7 for T = 1).
+//
+// Boosting grows one tree at a time (XGBoost / GBT: SURVEY A6, P9; DecisionTree
+// A3).  The multi-tree row-record kernels (hist5.hip) scan EVERY row per pass
+// and skip rows outside the pass's slot group; for one tree at depth 7 with
+// 256 bins a pass holds 8 of the 64 built nodes, so the level re-reads all rows
+// 8 x 13 times (36 ms of a 115 ms tree at 1e8 rows).  Here the active rows are
+// a permutation `perm` grouped by node (one contiguous segment per active node)
+// with the per-row statistics stored in the same order, so
+//   * hist: a block owns (a chunk of ONE node's segment, one 8-feature group):
+//     its LDS plane is a single node's 8 x B cells; it gathers the row's 8-bin
+//     word through perm and reads the statistics contiguously;
+//   * partition: a stable two-pass split of every segment into its children's
+//     segments (pass 1 counts left rows per chunk, the host turns the counts
+//     into output offsets, pass 2 scatters perm + statistics); rows of nodes
+//     that became leaves are dropped, so perm shrinks level by level.
+// Counts/sums are the same fixed-point integers as hist5 (bit-reproducible).
+#include "common.h"
+
+namespace {
+
+constexpr int kSegThreads = 256;
+constexpr int kPackShift = 44;
+constexpr int kPackQ = 1 << 23;
+
+// work item: {start in perm, length, slot (hist) / segment (partition)}
+struct SegHistArgs {
+  const uint64_t* bins;  // [G][n]
+  int64_t n;
+  int d, B;
+  const int* perm;
+  const float* v0p;
+  const float* v1p;
+  const uint8_t* wp;
+  const int* work;
+  float qs0, qs1;
+  unsigned long long* out;  // [S][d][B][2]
+};
+
+// PACKED: one u64 atomic per update (count << 44 | sum of w * (q + 2^23)); the
+// host bounds chunk length x max weight below 2^20 so neither field overflows.
+// !PACKED: two u64 sums (w * q0, w * q1).
+template <bool PACKED, bool HAS_W>
+__global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const SegHistArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long h[];
+  const int g = blockIdx.y;
+  const int fbase = g * 8;
+  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
+  const int plane = 8 * a.B;
+  const int nplanes = PACKED ? 1 : 2;
+  for (int i = threadIdx.x; i < plane * nplanes; i += kSegThreads) h[i] = 0ull;
+  const int rot = threadIdx.x & 7;
+  int fsel[8], fsh[8], foff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int jj = (j + rot) & 7;
+    fsel[j] = jj >> 2;
+    fsh[j] = (jj & 3) * 8;
+    foff[j] = jj * a.B;
+  }
+  const int valid_f = a.d - fbase;
+  const bool all8 = valid_f >= 8;
+  const uint32_t fvalid = all8 ? 0xFFu : ((1u << (valid_f > 0 ? valid_f : 0)) - 1u);
+  const uint32_t frot = ((fvalid >> rot) | (fvalid << (8 - rot))) & 0xFFu;
+  __syncthreads();
+  const uint64_t* bg = a.bins + (int64_t)g * a.n;
+  const int* pp = a.perm + start;
+  constexpr int U = 4;  // rows in flight per thread: perm loads, then gathers, then atomics
+  for (int i0 = threadIdx.x; i0 < len; i0 += kSegThreads * U) {
+    uint64_t b8[U];
+    float x0[U], x1[U];
+    uint32_t w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * kSegThreads;
+      const bool ok = i < len;
+      const int row = ok ? pp[i] : 0;
+      b8[u] = ok ? bg[row] : 0ull;
+      x1[u] = ok ? a.v1p[start + i] : 0.f;
+      x0[u] = (!PACKED && ok) ? a.v0p[start + i] : 0.f;
+      w[u] = ok ? (HAS_W ? (uint32_t)a.wp[start + i] : 1u) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (w[u] == 0u) continue;
+      const uint32_t lo = (uint32_t)b8[u], hi = (uint32_t)(b8[u] >> 32);
+      int cell[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        cell[j] = foff[j] + (int)__builtin_amdgcn_ubfe(fsel[j] ? hi : lo, (uint32_t)fsh[j], 8u);
+      if (PACKED) {
+        int q1 = (int)rintf(x1[u] * a.qs1);
+        q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+        const unsigned long long add =
+            ((unsigned long long)w[u] << kPackShift) + (unsigned long long)w[u] * (unsigned long long)(q1 + kPackQ);
+        if (all8) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) atomicAdd(h + cell[j], add);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if ((frot >> j) & 1u) atomicAdd(h + cell[j], add);
+        }
+      } else {
+        const long long y0 = (long long)w[u] * (long long)(int)rintf(x0[u] * a.qs0);
+        const long long y1 = (long long)w[u] * (long long)(int)rintf(x1[u] * a.qs1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (!all8 && !((frot >> j) & 1u)) continue;
+          atomicAdd(h + cell[j], (unsigned long long)y0);
+          atomicAdd(h + plane + cell[j], (unsigned long long)y1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < plane; c += kSegThreads) {
+    const int jj = c / a.B, bn = c - jj * a.B;
+    const int f = fbase + jj;
+    if (f >= a.d) continue;
+    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+    if (PACKED) {
+      const unsigned long long v = h[c];
+      if (!v) continue;
+      const unsigned long long cnt = v >> kPackShift;
+      const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+      atomicAdd(o, cnt);
+      atomicAdd(o + 1, (unsigned long long)sum);
+    } else {
+      const unsigned long long v0 = h[c], v1 = h[plane + c];
+      if (v0) atomicAdd(o, v0);
+      if (v1) atomicAdd(o + 1, v1);
+    }
+  }
+}
+
+// Row-major variant: bins_rm[row][G] (a row's 8-bin words contiguous, one
+// 128-byte line for up to 16 groups).  At deep levels a node's rows are sparse
+// in row order, so the [G][n] layout costs one cache line PER GROUP per row
+// (13 lines at d = 100) while only 8 bytes of each are used; here 8 lanes share
+// a row (lane & 7 = group within the block's group range) and read its words
+// with one coalesced access.  Blocks cover up to 8 groups (128 KB planes at
+// B = 256, 1024 threads); rot = row-within-wave spreads LDS banks.
+template <bool PACKED, bool HAS_W>
+__global__ __launch_bounds__(1024) void seg_hist_rm_kernel(const SegHistArgs a, const uint64_t* __restrict__ bins_rm,
+                                                           int G, int ngb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long h[];
+  constexpr int TH = 1024;
+  const int g0 = blockIdx.y * ngb;
+  const int ng = G - g0 < ngb ? G - g0 : ngb;
+  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
+  const int plane_g = 8 * a.B;
+  const int plane = ng * plane_g;
+  const int nplanes = PACKED ? 1 : 2;
+  for (int i = threadIdx.x; i < plane * nplanes; i += TH) h[i] = 0ull;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int gi = lane & 7, rsub = lane >> 3;
+  const bool lane_on = gi < ng;
+  const int g = g0 + (lane_on ? gi : 0);
+  const int fbase = g * 8;
+  const int rot = rsub;
+  int fsel[8], fsh[8], foff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int jj = (j + rot) & 7;
+    fsel[j] = jj >> 2;
+    fsh[j] = (jj & 3) * 8;
+    foff[j] = gi * plane_g + jj * a.B;
+  }
+  const int valid_f = a.d - fbase;
+  const bool all8 = valid_f >= 8;
+  const uint32_t fvalid = all8 ? 0xFFu : ((1u << (valid_f > 0 ? valid_f : 0)) - 1u);
+  const uint32_t frot = ((fvalid >> rot) | (fvalid << (8 - rot))) & 0xFFu;
+  __syncthreads();
+  constexpr int RPI = TH / 8;  // rows per block iteration
+  constexpr int U = 2;
+  for (int i0 = wid * 8 + rsub; i0 < len; i0 += RPI * U) {
+    uint64_t b8[U];
+    float x0[U], x1[U];
+    uint32_t w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * RPI;
+      const bool ok = i < len && lane_on;
+      const int row = ok ? a.perm[start + i] : 0;
+      b8[u] = ok ? bins_rm[(int64_t)row * G + g] : 0ull;
+      x1[u] = ok ? a.v1p[start + i] : 0.f;
+      x0[u] = (!PACKED && ok) ? a.v0p[start + i] : 0.f;
+      w[u] = ok ? (HAS_W ? (uint32_t)a.wp[start + i] : 1u) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (w[u] == 0u) continue;
+      const uint32_t lo = (uint32_t)b8[u], hi = (uint32_t)(b8[u] >> 32);
+      int cell[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        cell[j] = foff[j] + (int)__builtin_amdgcn_ubfe(fsel[j] ? hi : lo, (uint32_t)fsh[j], 8u);
+      if (PACKED) {
+        int q1 = (int)rintf(x1[u] * a.qs1);
+        q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+        const unsigned long long add =
+            ((unsigned long long)w[u] << kPackShift) + (unsigned long long)w[u] * (unsigned long long)(q1 + kPackQ);
+        if (all8) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) atomicAdd(h + cell[j], add);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if ((frot >> j) & 1u) atomicAdd(h + cell[j], add);
+        }
+      } else {
+        const long long y0 = (long long)w[u] * (long long)(int)rintf(x0[u] * a.qs0);
+        const long long y1 = (long long)w[u] * (long long)(int)rintf(x1[u] * a.qs1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (!all8 && !((frot >> j) & 1u)) continue;
+          atomicAdd(h + cell[j], (unsigned long long)y0);
+          atomicAdd(h + plane + cell[j], (unsigned long long)y1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < plane; c += TH) {
+    const int gq = c / plane_g, rem = c - gq * plane_g;
+    const int jj = rem / a.B, bn = rem - jj * a.B;
+    const int f = (g0 + gq) * 8 + jj;
+    if (f >= a.d) continue;
+    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+    if (PACKED) {
+      const unsigned long long v = h[c];
+      if (!v) continue;
+      const unsigned long long cnt = v >> kPackShift;
+      const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+      atomicAdd(o, cnt);
+      atomicAdd(o + 1, (unsigned long long)sum);
+    } else {
+      const unsigned long long v0 = h[c], v1 = h[plane + c];
+      if (v0) atomicAdd(o, v0);
+      if (v1) atomicAdd(o + 1, v1);
+    }
+  }
+}
+
+struct SegPartArgs {
+  const uint64_t* bins;
+  int64_t n;
+  const int* perm;
+  const float* v0p;
+  const float* v1p;
+  const uint8_t* wp;
+  const int* work;        // {start, len, seg}
+  const int* split_feat;  // [A] (-1: leaf, rows dropped)
+  const int* split_bin;
+  const int* cat_off;     // [A] (-1: ordered split)
+  const uint32_t* cat_mask;  // [*][8]
+  const int* left_base;   // [chunks] output offset of this chunk's first left row (-1: child is a leaf)
+  const int* right_base;
+  int* left_cnt;          // pass 1 output [chunks]
+  int* perm_out;
+  float* v0_out;
+  float* v1_out;
+  uint8_t* w_out;
+};
+
+__device__ __forceinline__ bool seg_left(const SegPartArgs& a, int seg, int row) {
+  const int f = a.split_feat[seg];
+  const int bin = (int)reinterpret_cast<const uint8_t*>(a.bins)[((int64_t)(f >> 3) * a.n + row) * 8 + (f & 7)];
+  const int co = a.cat_off[seg];
+  return co >= 0 ? ((a.cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u : bin <= a.split_bin[seg];
+}
+
+__global__ __launch_bounds__(kSegThreads) void seg_count_kernel(const SegPartArgs a) {
+  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], seg = a.work[3 * blockIdx.x + 2];
+  __shared__ int red[kSegThreads / 64];
+  int c = 0;
+  if (a.split_feat[seg] >= 0)
+    for (int i = threadIdx.x; i < len; i += kSegThreads) c += seg_left(a, seg, a.perm[start + i]) ? 1 : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < kSegThreads / 64; ++k) s += red[k];
+    a.left_cnt[blockIdx.x] = s;
+  }
+}
+
+// Stable scatter: rounds of 256 rows; a row's rank among this chunk's left
+// (right) rows = ballot prefix within the wave + the earlier waves' totals.
+__global__ __launch_bounds__(kSegThreads) void seg_scatter_kernel(const SegPartArgs a) {
+  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], seg = a.work[3 * blockIdx.x + 2];
+  if (a.split_feat[seg] < 0) return;
+  const int lb = a.left_base[blockIdx.x], rbase = a.right_base[blockIdx.x];
+  __shared__ int wl[kSegThreads / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int done_l = 0, done_r = 0;
+  for (int i0 = 0; i0 < len; i0 += kSegThreads) {
+    const int i = i0 + threadIdx.x;
+    const bool ok = i < len;
+    const int row = ok ? a.perm[start + i] : 0;
+    const bool left = ok && seg_left(a, seg, row);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(left);
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) wl[wid] = __builtin_popcountll(m);
+    __syncthreads();
+    int before = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kSegThreads / 64; ++k) {
+      before += k < wid ? wl[k] : 0;
+      tot += wl[k];
+    }
+    __syncthreads();
+    const int rank_l = done_l + before + below;                       // among left rows of this chunk
+    const int rank_r = done_r + (wid * 64 + lane) - (before + below);  // among right rows
+    if (ok) {
+      int dst = -1;
+      if (left) dst = lb >= 0 ? lb + rank_l : -1;
+      else dst = rbase >= 0 ? rbase + rank_r : -1;
+      if (dst >= 0) {
+        a.perm_out[dst] = row;
+        a.v1_out[dst] = a.v1p[start + i];
+        if (a.v0p) a.v0_out[dst] = a.v0p[start + i];
+        if (a.wp) a.w_out[dst] = a.wp[start + i];
+      }
+    }
+    const int nrows = len - i0 < kSegThreads ? len - i0 : kSegThreads;
+    done_l += tot;
+    done_r += nrows - tot;
+  }
+}
+
+}  // namespace
+
+// mode bit0: packed (no v0; count | sum in one atomic); bit1: per-row weights wp present;
+// bit2: bins are row-major [n][G] words (seg_hist_rm_kernel).
+// work: [nwork][3] {start, len, slot}; grid = nwork x ceil(d / 8).
+CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int B, const int* perm, const float* v0p,
+                           const float* v1p, const uint8_t* wp, const int* work, int nwork, float qs0, float qs1,
+                           unsigned long long* out, hipStream_t st) {
+  if (nwork <= 0) return 0;
+  SegHistArgs a{bins, n, d, B, perm, v0p, v1p, wp, work, qs0, qs1, out};
+  const bool packed = (mode & 1) != 0, has_w = (mode & 2) != 0;
+  if (mode & 4) {  // bins is row-major [n][G]
+    const int G = (d + 7) / 8;
+    const int cells_max = 16384 / (packed ? 1 : 2);  // 128 KB of u64 planes
+    int ngb = cells_max / (8 * B);
+    if (ngb > 8) ngb = 8;
+    if (ngb < 1) return (int)hipErrorInvalidValue;
+    const int nblk_g = (G + ngb - 1) / ngb;
+    ngb = (G + nblk_g - 1) / nblk_g;  // balance the group blocks
+    const size_t lds = (size_t)ngb * 8 * B * 8 * (packed ? 1 : 2);
+    const dim3 grid((unsigned)nwork, (unsigned)nblk_g);
+    auto launch = [&](auto kern) {
+      if (lds > 64 * 1024)
+        hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(kern, grid, dim3(1024), lds, st, a, bins, G, ngb);
+    };
+    if (packed) {
+      if (has_w) launch(seg_hist_rm_kernel<true, true>);
+      else launch(seg_hist_rm_kernel<true, false>);
+    } else {
+      if (has_w) launch(seg_hist_rm_kernel<false, true>);
+      else launch(seg_hist_rm_kernel<false, false>);
+    }
+    return (int)hipGetLastError();
+  }
+  const size_t lds = (size_t)8 * B * 8 * (packed ? 1 : 2);
+  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)nwork, (unsigned)((d + 7) / 8));
+  if (packed) {
+    if (has_w) hipLaunchKernelGGL((seg_hist_kernel<true, true>), grid, dim3(kSegThreads), lds, st, a);
+    else hipLaunchKernelGGL((seg_hist_kernel<true, false>), grid, dim3(kSegThreads), lds, st, a);
+  } else {
+    if (has_w) hipLaunchKernelGGL((seg_hist_kernel<false, true>), grid, dim3(kSegThreads), lds, st, a);
+    else hipLaunchKernelGGL((seg_hist_kernel<false, false>), grid, dim3(kSegThreads), lds, st, a);
+  }
+  return (int)hipGetLastError();
+}
+
+// pass 1 (left_cnt != null, outputs unused) or pass 2 (scatter) of the segment partition.
+CDNA_API int cdna_seg_partition(int pass, const uint64_t* bins, int64_t n, const int* perm, const float* v0p,
+                                const float* v1p, const uint8_t* wp, const int* work, int nwork,
+                                const int* split_feat, const int* split_bin, const int* cat_off,
+                                const uint32_t* cat_mask, const int* left_base, const int* right_base, int* left_cnt,
+                                int* perm_out, float* v0_out, float* v1_out, uint8_t* w_out, hipStream_t st) {
+  if (nwork <= 0) return 0;
+  SegPartArgs a{bins,     n,         perm,       v0p,        v1p,      wp,       work,   split_feat, split_bin,
+                cat_off,  cat_mask,  left_base,  right_base, left_cnt, perm_out, v0_out, v1_out,     w_out};
+  if (pass == 1) hipLaunchKernelGGL(seg_count_kernel, dim3((unsigned)nwork), dim3(kSegThreads), 0, st, a);
+  else hipLaunchKernelGGL(seg_scatter_kernel, dim3((unsigned)nwork), dim3(kSegThreads), 0, st, a);
+  return (int)hipGetLastError();
+}

@@ -371,3 +371,81 @@ def test_partition_codes(dev):
     b = codes.to(dev)
     K.partition_codes(bins.to(dev), b, tfirst, tfirst_next, sf, sb, co, cm.to(dev), child)
     assert torch.equal(a, b.cpu())
+
+
+def _seg_state(n, d, B, nseg, seed, weights):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    bins = K.binize(X, thr, nthr)
+    keep = torch.rand(n, generator=g) < 0.8
+    perm = torch.nonzero(keep).flatten().int()
+    perm = perm[torch.randperm(perm.numel(), generator=g)]
+    m = perm.numel()
+    cuts = np.sort(np.random.default_rng(seed).choice(np.arange(1, m), nseg - 1, replace=False))
+    starts = np.concatenate([[0], cuts])
+    lens = np.diff(np.concatenate([starts, [m]]))
+    v1 = torch.randn(m, generator=g) * 5
+    v0 = torch.rand(m, generator=g)
+    wp = torch.randint(0, 4, (m,), generator=g, dtype=torch.uint8) if weights else None
+    return bins, perm, v0, v1, wp, np.stack([starts, lens], 1)
+
+
+@pytest.mark.parametrize("packed,weights,B,d", [(True, False, 256, 100), (True, True, 40, 21), (False, False, 64, 13),
+                                                 (False, True, 256, 9)])
+@pytest.mark.parametrize("row_major", [False, True])
+def test_seg_hist(dev, packed, weights, B, d, row_major):
+    bins, perm, v0, v1, wp, segs = _seg_state(30000, d, B, 7, 3, weights)
+    build = [0, 2, 3, 6]
+    sb = np.array([[segs[a, 0], segs[a, 1], i] for i, a in enumerate(build)])
+    v0a = None if packed else v0
+    ref = K.seg_hist(bins, d, B, perm, v0a, v1, wp, sb, len(build), 3)
+    bd = bins.to(dev)
+    out = K.seg_hist(bd, d, B, perm.to(dev), None if v0a is None else v0a.to(dev), v1.to(dev),
+                     None if wp is None else wp.to(dev), sb, len(build), 3,
+                     bins_rm=bd.permute(1, 0, 2).contiguous() if row_major else None).cpu()
+    assert torch.allclose(out, ref, rtol=1e-6, atol=1e-3)
+
+
+@pytest.mark.parametrize("with_v0,weights", [(False, False), (True, True)])
+def test_seg_partition(dev, with_v0, weights):
+    n, d, B = 40000, 12, 32
+    bins, perm, v0, v1, wp, segs = _seg_state(n, d, B, 5, 9, weights)
+    # segment 1 is a leaf (rows dropped); segment 3 is a categorical-mask split; others ordered splits
+    sf = np.array([2, -1, 5, 0, 11], dtype=np.int32)
+    sbin = np.array([10, 0, 3, 20, 15], dtype=np.int32)
+    co = np.array([-1, -1, -1, 0, -1], dtype=np.int32)
+    cm = np.random.default_rng(1).integers(0, 2 ** 31 - 1, 8).astype(np.int32)
+    # children: seg0 -> (0, 1), seg2 -> (2, leaf), seg3 -> (3, 4), seg4 -> (leaf, 5)
+    child = np.array([0, 1, -1, -1, 2, -1, 3, 4, -1, 5], dtype=np.int32)
+    v0a = v0 if with_v0 else None
+    ref = K.seg_partition(bins, perm, v0a, v1, wp, segs, sf, sbin, co, cm, child, 6)
+    out = K.seg_partition(bins.to(dev), perm.to(dev), None if v0a is None else v0a.to(dev), v1.to(dev),
+                          None if wp is None else wp.to(dev), segs, sf, sbin, co, cm, child, 6)
+    np.testing.assert_array_equal(ref[4], out[4])
+    assert torch.equal(ref[0].int(), out[0].cpu())  # stable: same order as the reference
+    assert torch.equal(ref[2], out[2].cpu())
+    if with_v0:
+        assert torch.equal(ref[1], out[1].cpu())
+    if weights:
+        assert torch.equal(ref[3], out[3].cpu())
+
+
+def test_seg_mode_matches_codes_mode(dev, monkeypatch):
+    """One-tree fits (XGBoost rounds, DecisionTree) through the segment kernels give the codes-mode model."""
+    import cdnaml
+    from cdnaml.models.tree import engine as E
+    from cdnaml.ml.feature import VectorAssembler
+    from cdnaml.ml.regression import DecisionTreeRegressor
+    from cdnaml.ml.xgboost import XgboostRegressor
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn((200000, 20), generator=g, device=dev)
+    y = (X[:, 0] * 2 + torch.sin(X[:, 1] * 3) + (X[:, 2] > 0.5).float()).double()
+    df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
+    for mk in (lambda: DecisionTreeRegressor(maxDepth=7), lambda: XgboostRegressor(n_estimators=4, max_depth=6)):
+        preds = []
+        for seg in (False, True):
+            monkeypatch.setattr(E, "USE_SEG", seg)
+            preds.append(mk().fit(df).transform(df).select("prediction").toPandas().prediction.values)
+        assert np.abs(preds[0] - preds[1]).max() < 1e-3
