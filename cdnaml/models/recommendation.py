@@ -24,6 +24,9 @@ from .regression import _default_seed
 from .util import local_batch
 
 
+# K12 HIP path (als.hip) for ranks <= 32 on the GPU; the torch path is the reference
+ALS_NATIVE = True
+
 class ALS(Estimator):
     _params = {
         "rank": ("rank of the factorization", 10, TC.toInt),
@@ -71,9 +74,60 @@ class ALS(Estimator):
                 x[:, j] = torch.clamp(g / diag[:, j], min=0.0)
         return x
 
-    def _half_step(self, comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha):
+    @staticmethod
+    def _csr(dst_idx: torch.Tensor, n_dst: int):
+        """Ratings sorted by destination: (order, offsets[n_dst + 1])."""
+        order = torch.argsort(dst_idx, stable=True)
+        counts = torch.bincount(dst_idx, minlength=n_dst)
+        off = torch.zeros(n_dst + 1, dtype=torch.int64, device=dst_idx.device)
+        off[1:] = torch.cumsum(counts, 0)
+        return order, off
+
+    def _half_step_native(self, comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha, csr):
+        """K12 on the GPU (als.hip): per-destination Gram accumulation without an [nnz, r, r]
+        temporary, one fused all-reduce, then batched in-LDS Cholesky / NNLS solves."""
+        from ..ops import _lib
+        from ..ops.kernels import _ptr, _stream
         rank = F_src.shape[1]
         dev = F_src.device
+        order, off = csr
+        src_s = src_idx[order].int().contiguous()
+        r_s = r[order].double().contiguous()
+        Fd = F_src.double().contiguous()
+        A = torch.empty((n_dst, rank, rank), dtype=torch.float64, device=dev)
+        bvec = torch.empty((n_dst, rank), dtype=torch.float64, device=dev)
+        cnt = torch.empty(n_dst, dtype=torch.float64, device=dev)
+        L = _lib.lib()
+        _lib.check(L.cdna_als_accumulate(n_dst, _ptr(off), _ptr(src_s), _ptr(r_s), _ptr(Fd), rank, int(implicit),
+                                         float(alpha), _ptr(A), _ptr(bvec), _ptr(cnt), _stream(dev)),
+                   "cdna_als_accumulate")
+        comm.all_reduce_many([A.view(-1), bvec.view(-1), cnt])
+        has = cnt > 0
+        out = torch.zeros((n_dst, rank), dtype=torch.float64, device=dev)
+        hi = torch.nonzero(has).flatten()
+        E = int(hi.numel())
+        if E == 0:
+            return out
+        Ah, bh = A[hi].contiguous(), bvec[hi].contiguous()
+        diag = (lam * cnt[hi].clamp_min(1)) if implicit else (lam * cnt[hi])
+        G = (Fd.T @ Fd).contiguous() if implicit else None
+        x = torch.empty((E, rank), dtype=torch.float64, device=dev)
+        info = torch.empty(E, dtype=torch.int32, device=dev)
+        _lib.check(L.cdna_als_solve(E, rank, _ptr(Ah), _ptr(bh), _ptr(diag.contiguous()), _ptr(G), int(nonneg), 40,
+                                    _ptr(x), _ptr(info), _stream(dev)), "cdna_als_solve")
+        bad = info != 0
+        if bool(bad.any()):
+            eye = torch.eye(rank, dtype=torch.float64, device=dev)
+            Mb = Ah[bad] + diag[bad][:, None, None] * eye + (G[None] if G is not None else 0)
+            x[bad] = torch.linalg.lstsq(Mb, bh[bad].unsqueeze(-1)).solution.squeeze(-1)
+        out[hi] = x
+        return out
+
+    def _half_step(self, comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha, csr=None):
+        rank = F_src.shape[1]
+        dev = F_src.device
+        if csr is not None:
+            return self._half_step_native(comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha, csr)
         A = torch.zeros((n_dst, rank, rank), dtype=torch.float64, device=dev)
         bvec = torch.zeros((n_dst, rank), dtype=torch.float64, device=dev)
         cnt = torch.zeros(n_dst, dtype=torch.float64, device=dev)
@@ -134,9 +188,12 @@ class ALS(Estimator):
         V = (V / torch.linalg.vector_norm(V, dim=1, keepdim=True)).to(u.device)
         lam, nonneg = self.getRegParam(), self.getNonnegative()
         implicit, alpha = self.getImplicitPrefs(), self.getAlpha()
+        native = ALS_NATIVE and u.device.type == "cuda" and k <= 32
+        csr_u = self._csr(ui, uid.numel()) if native else None
+        csr_i = self._csr(ii, iid.numel()) if native else None
         for _ in range(self.getMaxIter()):
-            U = self._half_step(comm, ii, ui, r, V, uid.numel(), lam, nonneg, implicit, alpha)
-            V = self._half_step(comm, ui, ii, r, U, iid.numel(), lam, nonneg, implicit, alpha)
+            U = self._half_step(comm, ii, ui, r, V, uid.numel(), lam, nonneg, implicit, alpha, csr_u)
+            V = self._half_step(comm, ui, ii, r, U, iid.numel(), lam, nonneg, implicit, alpha, csr_i)
         model = ALSModel(uid.cpu().numpy(), U.float().cpu().numpy(), iid.cpu().numpy(), V.float().cpu().numpy())
         return model
 

@@ -449,3 +449,27 @@ def test_seg_mode_matches_codes_mode(dev, monkeypatch):
             monkeypatch.setattr(E, "USE_SEG", seg)
             preds.append(mk().fit(df).transform(df).select("prediction").toPandas().prediction.values)
         assert np.abs(preds[0] - preds[1]).max() < 1e-3
+
+
+@pytest.mark.parametrize("nonneg,implicit,rank", [(False, False, 12), (True, False, 4), (False, True, 8),
+                                                  (True, True, 20)])
+def test_als_native_matches_torch_path(dev, monkeypatch, nonneg, implicit, rank):
+    """K12 (als.hip accumulate + batched Cholesky/NNLS) against the torch reference half-steps."""
+    import cdnaml
+    import pandas as pd
+    from cdnaml.models import recommendation as R
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    rng = np.random.default_rng(3)
+    nu, ni, nnz = 300, 200, 6000
+    u = rng.integers(0, nu, nnz)
+    i = rng.integers(0, ni, nnz)
+    Ut, Vt = rng.normal(size=(nu, 3)), rng.normal(size=(ni, 3))
+    rt = np.clip((Ut[u] * Vt[i]).sum(1) + 3 + 0.3 * rng.normal(size=nnz), 0.5, 5.0)
+    df = spark.createDataFrame(pd.DataFrame({"userId": u, "movieId": i, "rating": rt}))
+    preds = []
+    for native in (False, True):
+        monkeypatch.setattr(R, "ALS_NATIVE", native)
+        m = R.ALS(userCol="userId", itemCol="movieId", ratingCol="rating", rank=rank, maxIter=5, regParam=0.1,
+                  nonnegative=nonneg, implicitPrefs=implicit, seed=42).fit(df)
+        preds.append(np.asarray(m.itemFactors.toPandas().features.tolist(), dtype=np.float64))
+    np.testing.assert_allclose(preds[1], preds[0], rtol=1e-4, atol=1e-5)
