@@ -93,10 +93,13 @@ def main():
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
+    marks = []
     for i in range(args.steps):
         model, parts = step()
+        marks.append(time.perf_counter())
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    marks.append(time.perf_counter())
     comm.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = comm.all_reduce_scalar(elapsed, "max")
@@ -108,6 +111,7 @@ def main():
     corr = float(torch.corrcoef(torch.stack([p[:1000000], y[:1000000]]))[0, 1]) if n > 1 else float("nan")
     log(f"step {ms:.1f} ms, {rows_per_s:.3e} rows/s, pred finite={ok}, corr(pred,label)={corr:.3f}, "
         f"nodes={model.totalNumNodes}")
+    log("host step marks (ms): " + " ".join(f"{(b - a) * 1e3:.1f}" for a, b in zip([t0] + marks[:-1], marks)))
     if args.trace:
         tracing.reset()
         tracing.enable()

@@ -550,8 +550,7 @@ class ForestTrainer:
             segs = np.array([[0, perm.numel()]], dtype=np.int64)
             node = None
         elif use_codes:
-            codes = K.codes_init(weights, T, n, dev)
-            wmax = int(weights.max().item()) if (weights is not None and weights.numel()) else 1
+            codes, wmax = K.codes_init_max(weights, T, n, dev)
             node = None
         else:
             node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \

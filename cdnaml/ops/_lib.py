@@ -93,6 +93,7 @@ _SIGS = {
                              c_void_p, c_void_p, c_void_p], c_int),
     "cdna_als_solve": ([c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                         c_void_p], c_int),
+    "cdna_codes_init": ([c_void_p, c_int64, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_partition5": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_partition": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -391,12 +391,25 @@ def codes_init(weights: Optional[torch.Tensor], T: int, n: int, device) -> torch
     """Row records for level 0: code[r, t] = weight << 8 | local (0 = the root, 255 = done).
 
     Returned as int16 [T, n] holding the uint16 bit patterns (hist5.hip)."""
+    return codes_init_max(weights, T, n, device)[0]
+
+
+def codes_init_max(weights: Optional[torch.Tensor], T: int, n: int, device):
+    """(codes, largest weight).  On the GPU one kernel writes the codes and reduces the max."""
+    if weights is not None and _native(weights) and weights.dtype == torch.uint8 and weights.is_contiguous() \
+            and weights.data_ptr() % 16 == 0:
+        codes = torch.empty((T, n), dtype=torch.int16, device=weights.device)
+        wm = torch.zeros(1, dtype=torch.int32, device=weights.device)
+        _lib.check(_lib.lib().cdna_codes_init(_ptr(weights), T * n, _ptr(codes), _ptr(wm), _stream(weights.device)),
+                   "cdna_codes_init")
+        return codes, max(1, int(wm.item()))
     if weights is None:
         w = torch.ones((T, n), dtype=torch.int32, device=device)
     else:
         w = weights.to(device=device).to(torch.int32)
     c = (w << 8) | torch.where(w == 0, torch.full_like(w, CODE_DONE), torch.zeros_like(w))
-    return c.to(torch.int16).contiguous()
+    wmax = int(w.max().item()) if w.numel() else 1
+    return c.to(torch.int16).contiguous(), max(1, wmax)
 
 
 def decode_codes(codes: torch.Tensor, tfirst: torch.Tensor):

@@ -19,12 +19,23 @@ __global__ void uniform_kernel(double* __restrict__ out, int64_t n, uint64_t see
 
 // Poisson(rate) bootstrap multiplicities for T trees: out[t][i], stream = t + 1
 // (rate >= 1 with no bootstrap is handled on the host as all-ones).
+// The CDF F_0..F_{kCdf-1} of poisson_from_uniform's recurrence is tabulated on
+// the host (same double operations in the same order, so every draw is
+// bit-identical to the loop): the kernel does compares only, no exp / divide.
+constexpr int kCdf = 32;
+struct PoissonCdf {
+  double F[kCdf];
+};
+
 __global__ void poisson_kernel(uint8_t* __restrict__ out, int T, int64_t n, uint64_t seed, uint64_t offset,
-                               double rate) {
+                               double rate, PoissonCdf cdf) {
   const int t = blockIdx.y;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double u = cdna::philox_uniform(seed, offset + (uint64_t)i, 0x100u + (uint32_t)t);
-    out[(int64_t)t * n + i] = (uint8_t)cdna::poisson_from_uniform(u, rate);
+    uint32_t k = 0;
+    while (k < kCdf && u > cdf.F[k]) ++k;
+    if (k == kCdf) k = cdna::poisson_from_uniform(u, rate);  // tail beyond the table: exact loop
+    out[(int64_t)t * n + i] = (uint8_t)k;
   }
 }
 
@@ -191,11 +202,67 @@ CDNA_API int cdna_uniform(double* out, int64_t n, uint64_t seed, uint64_t offset
   return (int)hipGetLastError();
 }
 
+// Level-0 row records from bootstrap weights: code = w << 8 | (w ? 0 : 255)
+// (hist5.hip), 16 rows per thread per trip, and the largest weight (drain
+// interval of the packed histogram) folded into one atomicMax per block.
+__global__ __launch_bounds__(256) void codes_init_kernel(const uint8_t* __restrict__ w, int64_t total,
+                                                         uint16_t* __restrict__ codes, unsigned* __restrict__ wmax) {
+  unsigned m = 0u;
+  const int64_t n16 = total / 16;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n16; q += (int64_t)gridDim.x * 256) {
+    const uint4 v = reinterpret_cast<const uint4*>(w)[q];
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+    uint4 o[2];
+    uint32_t* ow = reinterpret_cast<uint32_t*>(o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t b0 = (wd[k] >> (16 * h)) & 0xFFu, b1 = (wd[k] >> (16 * h + 8)) & 0xFFu;
+        const uint32_t c0 = (b0 << 8) | (b0 ? 0u : 0xFFu), c1 = (b1 << 8) | (b1 ? 0u : 0xFFu);
+        ow[2 * k + h] = c0 | (c1 << 16);
+        m = max(m, max(b0, b1));
+      }
+    }
+    reinterpret_cast<uint4*>(codes)[2 * q] = o[0];
+    reinterpret_cast<uint4*>(codes)[2 * q + 1] = o[1];
+  }
+  for (int64_t i = n16 * 16 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const uint32_t b = w[i];
+    codes[i] = (uint16_t)((b << 8) | (b ? 0u : 0xFFu));
+    m = max(m, b);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+  __shared__ unsigned red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(wmax, max(max(red[0], red[1]), max(red[2], red[3])));
+}
+
+CDNA_API int cdna_codes_init(const uint8_t* w, int64_t total, uint16_t* codes, unsigned* wmax, hipStream_t st) {
+  if (total <= 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(w) & 15) || (reinterpret_cast<uintptr_t>(codes) & 15))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(codes_init_kernel, dim3(grid_for(total / 16 + 1, 256, 4096)), dim3(256), 0, st, w, total, codes,
+                     wmax);
+  return (int)hipGetLastError();
+}
+
 CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_t offset, double rate,
                           hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
+  PoissonCdf cdf;
+  {
+    double p = exp(-rate), F = p;
+    for (int k = 0; k < kCdf; ++k) {
+      cdf.F[k] = F;  // F after k loop iterations
+      p *= rate / (double)(k + 1);
+      F += p;
+    }
+  }
   hipLaunchKernelGGL(poisson_kernel, dim3(grid_for(n, 256, 2048), T), dim3(256), 0, st, out, T, n, seed, offset,
-                     rate);
+                     rate, cdf);
   return (int)hipGetLastError();
 }
 

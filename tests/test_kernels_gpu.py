@@ -59,9 +59,10 @@ def test_uniform_bit_identical(dev):
     assert torch.equal(a, b)
 
 
-def test_poisson_matches(dev):
-    a = K.poisson_weights(4, 50000, 7, 1000, 1.0)
-    b = K.poisson_weights(4, 50000, 7, 1000, 1.0, device=dev).cpu()
+@pytest.mark.parametrize("rate", [1.0, 0.63, 2.5])
+def test_poisson_matches(dev, rate):
+    a = K.poisson_weights(4, 50000, 7, 1000, rate)
+    b = K.poisson_weights(4, 50000, 7, 1000, rate, device=dev).cpu()
     assert (a != b).sum().item() <= 2  # libm exp() may differ in the last ulp
 
 
@@ -473,3 +474,11 @@ def test_als_native_matches_torch_path(dev, monkeypatch, nonneg, implicit, rank)
                   nonnegative=nonneg, implicitPrefs=implicit, seed=42).fit(df)
         preds.append(np.asarray(m.itemFactors.toPandas().features.tolist(), dtype=np.float64))
     np.testing.assert_allclose(preds[1], preds[0], rtol=1e-4, atol=1e-5)
+
+
+def test_codes_init_kernel(dev):
+    w = torch.randint(0, 7, (5, 10007), dtype=torch.uint8)
+    w[2, 5] = 200
+    ref, ref_max = K.codes_init_max(w, 5, 10007, "cpu")
+    out, mx = K.codes_init_max(w.to(dev), 5, 10007, dev)
+    assert torch.equal(ref, out.cpu()) and mx == ref_max == 200
