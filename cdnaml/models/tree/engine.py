@@ -41,6 +41,8 @@ HIST_MODE = __import__("os").environ.get("CDNAML_RF_HIST", "full")
 USE_CODES = __import__("os").environ.get("CDNAML_TREE_CODES", "1") != "0"
 # single-tree regression fits (boosting rounds, DecisionTree): rows kept grouped by node (seg.hip)
 USE_SEG = __import__("os").environ.get("CDNAML_TREE_SEG", "1") != "0"
+# multi-tree regression forests: level 0 on row records, then rows grouped by (tree, node) segments
+USE_MSEG = __import__("os").environ.get("CDNAML_TREE_MSEG", "0") != "0"
 
 
 @dataclass
@@ -535,6 +537,10 @@ class ForestTrainer:
         subtract = not masked
         # one regression tree: rows grouped by node in a permutation (segment mode)
         use_seg = USE_SEG and T == 1 and not self.classification and not masked
+        # several regression trees: level 0 on row records (one pass over the bins serves every tree), then
+        # one permutation segment per (tree, node) so deep levels touch only the rows of the nodes they build
+        use_mseg = (USE_MSEG and USE_CODES and T > 1 and not self.classification and not masked and
+                    p.max_depth <= 8 and T * n < 2 ** 31 and n > 0)
         # row records (uint16 weight<<8 | local node) when every level fits 255 nodes per tree
         use_codes = USE_CODES and p.max_depth <= 8 and not use_seg
         if use_seg:
@@ -590,6 +596,8 @@ class ForestTrainer:
             build_slot = torch.from_numpy(slot_of).to(dev)
             id_tree = np.array([e["tree"] for e in active], dtype=np.int32)
             tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
+            if use_mseg and depth == 1:
+                use_codes, use_seg = False, True  # rows now live in per-(tree, node) segments
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
                 if use_seg:
                     sb = np.array([[segs[a, 0], segs[a, 1], slot_of[a]] for a in build_ids], dtype=np.int64)
@@ -597,7 +605,8 @@ class ForestTrainer:
                                     # sparse node segments (>= 4 built nodes) gather whole rows from the
                                     # row-major copy; dense shallow levels stream the [G][n] layout
                                     bins_rm=data.row_major_bins() if (K.SEG_ROW_MAJOR and dev.type == "cuda"
-                                                                      and len(build_ids) >= 4) else None)
+                                                                      and len(build_ids) >= 4) else None,
+                                    interleave=use_mseg)
                 elif use_codes:
                     Hb = K.hist_codes(1 if self.classification else 0, data.bins, d, codes, tfirst,
                                       stats_rows.get("v0"), stats_rows.get("v1"), stats_rows.get("label"), self.C,
@@ -712,7 +721,19 @@ class ForestTrainer:
             if nxt:
                 cm = np.stack(cat_masks).view(np.int32) if cat_masks else np.zeros((0, 8), np.int32)
                 with _tr.span("tree.partition", depth=depth):
-                    if use_seg:
+                    if use_mseg and depth == 0:
+                        # level 0 -> per-(tree, child) segments; weight-0 (out-of-bag) rows are dropped here
+                        wts = weights if weights is not None else \
+                            torch.ones((T, n), dtype=torch.uint8, device=dev)
+                        wts = wts.to(torch.uint8).contiguous()
+                        v1 = stats_rows["v1"].float().contiguous()
+                        v0 = None if stats_rows.get("v0") is None else stats_rows["v0"].float().contiguous()
+                        segs0 = np.stack([np.arange(T, dtype=np.int64) * n, np.full(T, n, np.int64)], 1)
+                        perm, v0p, v1p, wp, segs = K.seg_partition(data.bins, None, v0, v1, wts, segs0, split_feat,
+                                                                   split_bin, cat_off, cm.reshape(-1), child, len(nxt))
+                        seg_scales = K.seg_scales(v0, v1, wmax, n)
+                        codes = None
+                    elif use_seg:
                         perm, v0p, v1p, wp, segs = K.seg_partition(data.bins, perm, v0p, v1p, wp, segs, split_feat,
                                                                     split_bin, cat_off, cm.reshape(-1), child,
                                                                     len(nxt))

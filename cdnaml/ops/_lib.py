@@ -87,7 +87,7 @@ _SIGS = {
                        c_int, c_float, c_float, c_void_p, c_void_p], c_int),
     "cdna_seg_partition": ([c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                            c_void_p, c_void_p, c_void_p], c_int),
+                            c_void_p, c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "cdna_als_max_rank": ([], c_int),
     "cdna_als_accumulate": ([c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p,
                              c_void_p, c_void_p, c_void_p], c_int),

@@ -801,10 +801,13 @@ def _seg_work(segs: np.ndarray, chunk: int) -> np.ndarray:
 
 def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
              v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
-             scales=None, bins_rm: Optional[torch.Tensor] = None) -> torch.Tensor:
+             scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False) -> torch.Tensor:
     """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
 
     segs: [k, 3] {start, len, slot}.  [..., 0] = sum w*v0 (or sum w when v0p is None), [..., 1] = sum w*v1.
+    interleave: order the work items by their relative position inside their segment, so that segments
+    of different trees (whose rows are all sorted by row id) gather the same region of the bins at the
+    same time and share it through L2 / MALL.
     """
     G, n, _ = bins.shape
     out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
@@ -833,6 +836,11 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
     work = _seg_work(segs, chunk)
     if len(work) == 0:
         return out
+    if interleave and len(segs) > 1:
+        sg = segs[segs[:, 1] > 0]
+        k = (sg[:, 1] + chunk - 1) // chunk
+        j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
+        work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
     qs0, qs1 = scales if scales is not None else seg_scales(v0p, v1p, wm, n)
     wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
     iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
@@ -850,29 +858,42 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
     return out
 
 
-def seg_partition(bins: torch.Tensor, perm: torch.Tensor, v0p: Optional[torch.Tensor], v1p: torch.Tensor,
+def seg_partition(bins: torch.Tensor, perm: Optional[torch.Tensor], v0p: Optional[torch.Tensor], v1p: torch.Tensor,
                   wp: Optional[torch.Tensor], segs: np.ndarray, split_feat: np.ndarray, split_bin: np.ndarray,
                   cat_off: np.ndarray, cat_mask: np.ndarray, child: np.ndarray, n_next: int):
     """Stable split of every node segment into its children's segments (rows of leaves dropped).
 
     segs [A, 2] {start, len} of the active nodes (in active order); child [2A] next-level node index
     or -1; n_next = number of next-level nodes.  Returns (perm, v0p, v1p, wp, segs_next [n_next, 2]).
+
+    ``perm=None`` is the level-0 entry of multi-tree segment mode: active node a is the root of tree
+    a over all n rows, ``wp`` is the [T, n] bootstrap weight matrix, ``v0p``/``v1p`` are the unpermuted
+    per-row statistics, and rows whose weight in that tree is 0 are dropped.
     """
     G, n, _ = bins.shape
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 2)
     A = len(segs)
-    dev = perm.device
+    dev = v1p.device
     sf = np.asarray(split_feat, dtype=np.int32)
+    implicit = perm is None
+    if implicit:
+        assert wp is not None and wp.shape == (A, n) and wp.is_contiguous(), "implicit entry needs [T, n] weights"
+        assert np.array_equal(segs[:, 0], np.arange(A) * n) and np.all(segs[:, 1] == n)
+        assert A * n < 2 ** 31, "multi-tree segment mode indexes rows with int32"
     if not _native(bins):
         flat = bins.permute(1, 0, 2).reshape(n, G * 8)
-        lefts = np.zeros(A, dtype=np.int64)
         pieces = [[] for _ in range(max(n_next, 0))]
         for a in range(A):
             s, ln = segs[a]
             if ln == 0 or sf[a] < 0:
                 continue
             idx = torch.arange(int(s), int(s + ln))
-            rows = perm[idx].long()
+            if implicit:
+                rows = idx - a * n
+                keep = wp[a].cpu() > 0
+                idx, rows = idx[keep], rows[keep]
+            else:
+                rows = perm[idx].long()
             bv = flat[rows, int(sf[a])].long()
             if cat_off[a] >= 0:
                 m = torch.from_numpy(np.asarray(cat_mask, dtype=np.int64).reshape(-1, 8)[cat_off[a]] & 0xFFFFFFFF)
@@ -887,9 +908,13 @@ def seg_partition(bins: torch.Tensor, perm: torch.Tensor, v0p: Optional[torch.Te
         lens = np.array([len(o) for o in order], dtype=np.int64)
         starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if n_next else np.zeros(0, np.int64)
         cat = torch.cat(order) if order else torch.zeros(0, dtype=torch.long)
+        if implicit:
+            rows = cat % n
+            return (rows.to(torch.int32).contiguous(), None if v0p is None else v0p[rows].contiguous(),
+                    v1p[rows].contiguous(), wp.reshape(-1)[cat].contiguous(), np.stack([starts, lens], 1))
         return (perm[cat].contiguous(), None if v0p is None else v0p[cat].contiguous(), v1p[cat].contiguous(),
                 None if wp is None else wp[cat].contiguous(), np.stack([starts, lens], 1))
-    # native: pass 1 counts left rows per chunk, host computes output offsets, pass 2 scatters
+    # native: pass 1 counts left/right rows per chunk, host computes output offsets, pass 2 scatters
     tags = np.arange(A, dtype=np.int64)
     work = _seg_work(np.concatenate([segs, tags[:, None]], 1), SEG_PART_CHUNK)
     nw = len(work)
@@ -900,15 +925,16 @@ def seg_partition(bins: torch.Tensor, perm: torch.Tensor, v0p: Optional[torch.Te
     cm = np.asarray(cat_mask, dtype=np.int32).reshape(-1)
     cm_t = torch.from_numpy(cm if cm.size else np.zeros(8, np.int32)).to(dev)
     wt = torch.from_numpy(work.reshape(-1)).to(dev)
-    lc = torch.zeros(max(nw, 1), dtype=torch.int32, device=dev)
+    lrc = torch.zeros((2, max(nw, 1)), dtype=torch.int32, device=dev)
+    impl_n = n if implicit else 0
     if nw:
-        _lib.check(L.cdna_seg_partition(1, _ptr(bins), n, _ptr(perm), None, None, None, _ptr(wt), nw, _ptr(sf_t),
-                                        _ptr(sb_t), _ptr(co_t), _ptr(cm_t), None, None, _ptr(lc), None, None, None,
-                                        None, _stream(dev)), "cdna_seg_partition(count)")
-    lc_h = lc.cpu().numpy()[:nw].astype(np.int64)
+        _lib.check(L.cdna_seg_partition(1, _ptr(bins), n, _ptr(perm), None, None, _ptr(wp) if implicit else None,
+                                        _ptr(wt), nw, _ptr(sf_t), _ptr(sb_t), _ptr(co_t), _ptr(cm_t), None, None,
+                                        _ptr(lrc[0]), None, None, None, None, impl_n, _ptr(lrc[1]), _stream(dev)),
+                   "cdna_seg_partition(count)")
+    lrc_h = lrc.cpu().numpy()[:, :nw].astype(np.int64)
+    lc_h, rc_h = lrc_h[0], lrc_h[1]
     wseg = work[:, 2].astype(np.int64)
-    wlen = work[:, 1].astype(np.int64)
-    rc_h = wlen - lc_h
     child = np.asarray(child, dtype=np.int64)
     # child sizes
     lens = np.zeros(n_next, dtype=np.int64)
@@ -927,6 +953,7 @@ def seg_partition(bins: torch.Tensor, perm: torch.Tensor, v0p: Optional[torch.Te
     lb = np.where(splits & (cl >= 0), starts[np.maximum(cl, 0)] + off_l, -1) if n_next else np.full(nw, -1)
     rb = np.where(splits & (cr >= 0), starts[np.maximum(cr, 0)] + off_r, -1) if n_next else np.full(nw, -1)
     total = int(lens.sum())
+    assert total < 2 ** 31
     perm_o = torch.empty(total, dtype=torch.int32, device=dev)
     v1_o = torch.empty(total, dtype=torch.float32, device=dev)
     v0_o = None if v0p is None else torch.empty(total, dtype=torch.float32, device=dev)
@@ -936,6 +963,6 @@ def seg_partition(bins: torch.Tensor, perm: torch.Tensor, v0p: Optional[torch.Te
         rb_t = torch.from_numpy(rb.astype(np.int32)).to(dev)
         _lib.check(L.cdna_seg_partition(2, _ptr(bins), n, _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp), _ptr(wt), nw,
                                         _ptr(sf_t), _ptr(sb_t), _ptr(co_t), _ptr(cm_t), _ptr(lb_t), _ptr(rb_t),
-                                        None, _ptr(perm_o), _ptr(v0_o), _ptr(v1_o), _ptr(w_o), _stream(dev)),
-                   "cdna_seg_partition(scatter)")
+                                        None, _ptr(perm_o), _ptr(v0_o), _ptr(v1_o), _ptr(w_o), impl_n, None,
+                                        _stream(dev)), "cdna_seg_partition(scatter)")
     return perm_o, v0_o, v1_o, w_o, np.stack([starts, lens], 1)

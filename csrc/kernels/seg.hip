@@ -262,7 +262,23 @@ struct SegPartArgs {
   float* v0_out;
   float* v1_out;
   uint8_t* w_out;
+  // implicit_n > 0: level-0 multi-tree entry.  Segment s is tree s over rows
+  // [0, n): perm is the identity (row = start + i - s * n), wp is the [T][n]
+  // bootstrap weight matrix (indexed like the virtual perm), v0p/v1p are the
+  // unpermuted per-row statistics (indexed by row), and weight-0 rows are dropped.
+  int64_t implicit_n;
+  int* right_cnt;         // pass 1 output [chunks] (rows kept on the right)
 };
+
+struct SegRow {
+  int row;
+  bool keep;
+};
+
+__device__ __forceinline__ SegRow seg_row(const SegPartArgs& a, int seg, int64_t idx) {
+  if (a.implicit_n > 0) return SegRow{(int)(idx - (int64_t)seg * a.implicit_n), a.wp[idx] != 0};
+  return SegRow{a.perm[idx], true};
+}
 
 __device__ __forceinline__ bool seg_left(const SegPartArgs& a, int seg, int row) {
   const int f = a.split_feat[seg];
@@ -274,18 +290,35 @@ __device__ __forceinline__ bool seg_left(const SegPartArgs& a, int seg, int row)
 __global__ __launch_bounds__(kSegThreads) void seg_count_kernel(const SegPartArgs a) {
   const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], seg = a.work[3 * blockIdx.x + 2];
   __shared__ int red[kSegThreads / 64];
-  int c = 0;
+  __shared__ int redr[kSegThreads / 64];
+  int c = 0, r = 0;
   if (a.split_feat[seg] >= 0)
-    for (int i = threadIdx.x; i < len; i += kSegThreads) c += seg_left(a, seg, a.perm[start + i]) ? 1 : 0;
+    for (int i = threadIdx.x; i < len; i += kSegThreads) {
+      const SegRow sr = seg_row(a, seg, (int64_t)start + i);
+      if (!sr.keep) continue;
+      const bool l = seg_left(a, seg, sr.row);
+      c += l ? 1 : 0;
+      r += l ? 0 : 1;
+    }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    r += __shfl_xor(r, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = c;
+    redr[threadIdx.x >> 6] = r;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int s = 0;
+    int s = 0, sr = 0;
 #pragma unroll
-    for (int k = 0; k < kSegThreads / 64; ++k) s += red[k];
+    for (int k = 0; k < kSegThreads / 64; ++k) {
+      s += red[k];
+      sr += redr[k];
+    }
     a.left_cnt[blockIdx.x] = s;
+    if (a.right_cnt) a.right_cnt[blockIdx.x] = sr;
   }
 }
 
@@ -296,40 +329,50 @@ __global__ __launch_bounds__(kSegThreads) void seg_scatter_kernel(const SegPartA
   if (a.split_feat[seg] < 0) return;
   const int lb = a.left_base[blockIdx.x], rbase = a.right_base[blockIdx.x];
   __shared__ int wl[kSegThreads / 64];
+  __shared__ int wr[kSegThreads / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bool implicit = a.implicit_n > 0;
   int done_l = 0, done_r = 0;
   for (int i0 = 0; i0 < len; i0 += kSegThreads) {
     const int i = i0 + threadIdx.x;
     const bool ok = i < len;
-    const int row = ok ? a.perm[start + i] : 0;
-    const bool left = ok && seg_left(a, seg, row);
+    const SegRow sr = ok ? seg_row(a, seg, (int64_t)start + i) : SegRow{0, false};
+    const int row = sr.row;
+    const bool left = sr.keep && seg_left(a, seg, row);
+    const bool right = sr.keep && !left;
     const uint64_t m = __builtin_amdgcn_ballot_w64(left);
+    const uint64_t mr = __builtin_amdgcn_ballot_w64(right);
     const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (lane == 0) wl[wid] = __builtin_popcountll(m);
+    const int below_r =
+        (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mr >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mr, 0u));
+    if (lane == 0) {
+      wl[wid] = __builtin_popcountll(m);
+      wr[wid] = __builtin_popcountll(mr);
+    }
     __syncthreads();
-    int before = 0, tot = 0;
+    int before = 0, tot = 0, before_r = 0, tot_r = 0;
 #pragma unroll
     for (int k = 0; k < kSegThreads / 64; ++k) {
       before += k < wid ? wl[k] : 0;
       tot += wl[k];
+      before_r += k < wid ? wr[k] : 0;
+      tot_r += wr[k];
     }
     __syncthreads();
-    const int rank_l = done_l + before + below;                       // among left rows of this chunk
-    const int rank_r = done_r + (wid * 64 + lane) - (before + below);  // among right rows
-    if (ok) {
-      int dst = -1;
-      if (left) dst = lb >= 0 ? lb + rank_l : -1;
-      else dst = rbase >= 0 ? rbase + rank_r : -1;
+    if (left || right) {
+      const int dst = left ? (lb >= 0 ? lb + done_l + before + below : -1)
+                           : (rbase >= 0 ? rbase + done_r + before_r + below_r : -1);
       if (dst >= 0) {
+        const int64_t src = (int64_t)start + i;
+        const int64_t sidx = implicit ? (int64_t)row : src;  // statistics: per row (implicit) or permuted
         a.perm_out[dst] = row;
-        a.v1_out[dst] = a.v1p[start + i];
-        if (a.v0p) a.v0_out[dst] = a.v0p[start + i];
-        if (a.wp) a.w_out[dst] = a.wp[start + i];
+        a.v1_out[dst] = a.v1p[sidx];
+        if (a.v0p) a.v0_out[dst] = a.v0p[sidx];
+        if (a.wp) a.w_out[dst] = a.wp[src];
       }
     }
-    const int nrows = len - i0 < kSegThreads ? len - i0 : kSegThreads;
     done_l += tot;
-    done_r += nrows - tot;
+    done_r += tot_r;
   }
 }
 
@@ -381,15 +424,20 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
   return (int)hipGetLastError();
 }
 
-// pass 1 (left_cnt != null, outputs unused) or pass 2 (scatter) of the segment partition.
+// pass 1 (left_cnt / right_cnt, outputs unused) or pass 2 (scatter) of the segment partition.
+// implicit_n > 0: level-0 entry of multi-tree segment mode (see SegPartArgs).
 CDNA_API int cdna_seg_partition(int pass, const uint64_t* bins, int64_t n, const int* perm, const float* v0p,
                                 const float* v1p, const uint8_t* wp, const int* work, int nwork,
                                 const int* split_feat, const int* split_bin, const int* cat_off,
                                 const uint32_t* cat_mask, const int* left_base, const int* right_base, int* left_cnt,
-                                int* perm_out, float* v0_out, float* v1_out, uint8_t* w_out, hipStream_t st) {
+                                int* perm_out, float* v0_out, float* v1_out, uint8_t* w_out, int64_t implicit_n,
+                                int* right_cnt, hipStream_t st) {
   if (nwork <= 0) return 0;
+  if (implicit_n > 0 && (perm != nullptr || wp == nullptr)) return (int)hipErrorInvalidValue;
+  if (implicit_n <= 0 && perm == nullptr) return (int)hipErrorInvalidValue;
   SegPartArgs a{bins,     n,         perm,       v0p,        v1p,      wp,       work,   split_feat, split_bin,
-                cat_off,  cat_mask,  left_base,  right_base, left_cnt, perm_out, v0_out, v1_out,     w_out};
+                cat_off,  cat_mask,  left_base,  right_base, left_cnt, perm_out, v0_out, v1_out,     w_out,
+                implicit_n, right_cnt};
   if (pass == 1) hipLaunchKernelGGL(seg_count_kernel, dim3((unsigned)nwork), dim3(kSegThreads), 0, st, a);
   else hipLaunchKernelGGL(seg_scatter_kernel, dim3((unsigned)nwork), dim3(kSegThreads), 0, st, a);
   return (int)hipGetLastError();

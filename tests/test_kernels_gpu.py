@@ -432,6 +432,46 @@ def test_seg_partition(dev, with_v0, weights):
         assert torch.equal(ref[3], out[3].cpu())
 
 
+def test_seg_partition_implicit_level0(dev):
+    """Multi-tree entry: tree t's root segment is every row, weight-0 rows are dropped (stable)."""
+    n, d, B, T = 30000, 12, 32, 5
+    bins = _seg_state(n, d, B, 1, 4, False)[0]
+    gen = torch.Generator().manual_seed(11)
+    v0, v1 = torch.rand(n, generator=gen), torch.randn(n, generator=gen) * 5
+    w = torch.from_numpy(np.random.default_rng(5).poisson(1.0, (T, n)).clip(0, 255).astype(np.uint8))
+    segs = np.stack([np.arange(T) * n, np.full(T, n)], 1)
+    sf = np.array([2, -1, 5, 0, 11], dtype=np.int32)
+    sbin = np.array([10, 0, 3, 20, 15], dtype=np.int32)
+    co = np.array([-1, -1, -1, 0, -1], dtype=np.int32)
+    cm = np.random.default_rng(1).integers(0, 2 ** 31 - 1, 8).astype(np.int32)
+    child = np.array([0, 1, -1, -1, 2, -1, 3, 4, -1, 5], dtype=np.int32)
+    ref = K.seg_partition(bins, None, v0, v1, w, segs, sf, sbin, co, cm, child, 6)
+    out = K.seg_partition(bins.to(dev), None, v0.to(dev), v1.to(dev), w.to(dev), segs, sf, sbin, co, cm, child, 6)
+    np.testing.assert_array_equal(ref[4], out[4])
+    assert torch.equal(ref[0].int(), out[0].cpu())
+    assert torch.equal(ref[1], out[1].cpu()) and torch.equal(ref[2], out[2].cpu())
+    assert torch.equal(ref[3], out[3].cpu())
+    assert int(ref[3].min()) > 0  # out-of-bag rows dropped
+
+
+def test_mseg_forest_matches_codes_forest(dev, monkeypatch):
+    """RandomForest through multi-tree segment mode builds the codes-mode forest."""
+    import cdnaml
+    from cdnaml.models.tree import engine as E
+    from cdnaml.ml.regression import RandomForestRegressor
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn((300000, 24), generator=g, device=dev)
+    y = (X[:, 0] * 2 + torch.sin(X[:, 1] * 3) + (X[:, 2] > 0.5).float()).double()
+    df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
+    preds = []
+    for mseg in (False, True):
+        monkeypatch.setattr(E, "USE_MSEG", mseg)
+        m = RandomForestRegressor(numTrees=8, maxDepth=6, maxBins=40, seed=7).fit(df)
+        preds.append(m.transform(df).select("prediction").toPandas().prediction.values)
+    assert np.abs(preds[0] - preds[1]).max() < 1e-3
+
+
 def test_seg_mode_matches_codes_mode(dev, monkeypatch):
     """One-tree fits (XGBoost rounds, DecisionTree) through the segment kernels give the codes-mode model."""
     import cdnaml
