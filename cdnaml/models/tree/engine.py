@@ -42,7 +42,8 @@ USE_CODES = __import__("os").environ.get("CDNAML_TREE_CODES", "1") != "0"
 # single-tree regression fits (boosting rounds, DecisionTree): rows kept grouped by node (seg.hip)
 USE_SEG = __import__("os").environ.get("CDNAML_TREE_SEG", "1") != "0"
 # multi-tree regression forests: level 0 on row records, then rows grouped by (tree, node) segments
-USE_MSEG = __import__("os").environ.get("CDNAML_TREE_MSEG", "0") != "0"
+USE_MSEG = __import__("os").environ.get("CDNAML_TREE_MSEG", "1") != "0"
+MSEG_L0 = __import__("os").environ.get("CDNAML_MSEG_L0", "1") != "0"  # level 0 through segments too
 
 
 @dataclass
@@ -82,7 +83,7 @@ class BinnedData:
 
     def row_major_bins(self) -> torch.Tensor:
         if self.bins_rm is None:
-            self.bins_rm = self.bins.permute(1, 0, 2).contiguous()
+            self.bins_rm = K.bins_row_major(self.bins)
         return self.bins_rm
 
 
@@ -537,8 +538,9 @@ class ForestTrainer:
         subtract = not masked
         # one regression tree: rows grouped by node in a permutation (segment mode)
         use_seg = USE_SEG and T == 1 and not self.classification and not masked
-        # several regression trees: level 0 on row records (one pass over the bins serves every tree), then
-        # one permutation segment per (tree, node) so deep levels touch only the rows of the nodes they build
+        # several regression trees: row records for every level (one dense pass partitions all trees), and from
+        # level 1 on the rows of the nodes a level builds are gathered into slot segments first, so the
+        # histogram touches only those rows (level 0 streams the bins once for every tree instead)
         use_mseg = (USE_MSEG and USE_CODES and T > 1 and not self.classification and not masked and
                     p.max_depth <= 8 and T * n < 2 ** 31 and n > 0)
         # row records (uint16 weight<<8 | local node) when every level fits 255 nodes per tree
@@ -558,6 +560,9 @@ class ForestTrainer:
         elif use_codes:
             codes, wmax = K.codes_init_max(weights, T, n, dev)
             node = None
+            if use_mseg:
+                mseg_scales = K.seg_scales(None if stats_rows.get("v0") is None else stats_rows["v0"].float(),
+                                           stats_rows["v1"].float(), wmax, n)
         else:
             node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
                 torch.zeros((T, 0), dtype=torch.int32, device=dev)
@@ -596,10 +601,17 @@ class ForestTrainer:
             build_slot = torch.from_numpy(slot_of).to(dev)
             id_tree = np.array([e["tree"] for e in active], dtype=np.int32)
             tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
-            if use_mseg and depth == 1:
-                use_codes, use_seg = False, True  # rows now live in per-(tree, node) segments
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
-                if use_seg:
+                if use_mseg and (depth >= 1 or MSEG_L0):
+                    # gather the rows of the built nodes into slot segments, then segment histograms
+                    perm, v0p, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, len(build_ids),
+                                                             stats_rows.get("v0"), stats_rows["v1"])
+                    sb = np.concatenate([sg, np.arange(len(build_ids), dtype=np.int64)[:, None]], 1)
+                    Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax, mseg_scales,
+                                    bins_rm=data.row_major_bins() if dev.type == "cuda" else None,
+                                    interleave=True)
+                    del perm, v0p, v1p, wp
+                elif use_seg:
                     sb = np.array([[segs[a, 0], segs[a, 1], slot_of[a]] for a in build_ids], dtype=np.int64)
                     Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax, seg_scales,
                                     # sparse node segments (>= 4 built nodes) gather whole rows from the
@@ -721,19 +733,7 @@ class ForestTrainer:
             if nxt:
                 cm = np.stack(cat_masks).view(np.int32) if cat_masks else np.zeros((0, 8), np.int32)
                 with _tr.span("tree.partition", depth=depth):
-                    if use_mseg and depth == 0:
-                        # level 0 -> per-(tree, child) segments; weight-0 (out-of-bag) rows are dropped here
-                        wts = weights if weights is not None else \
-                            torch.ones((T, n), dtype=torch.uint8, device=dev)
-                        wts = wts.to(torch.uint8).contiguous()
-                        v1 = stats_rows["v1"].float().contiguous()
-                        v0 = None if stats_rows.get("v0") is None else stats_rows["v0"].float().contiguous()
-                        segs0 = np.stack([np.arange(T, dtype=np.int64) * n, np.full(T, n, np.int64)], 1)
-                        perm, v0p, v1p, wp, segs = K.seg_partition(data.bins, None, v0, v1, wts, segs0, split_feat,
-                                                                   split_bin, cat_off, cm.reshape(-1), child, len(nxt))
-                        seg_scales = K.seg_scales(v0, v1, wmax, n)
-                        codes = None
-                    elif use_seg:
+                    if use_seg:
                         perm, v0p, v1p, wp, segs = K.seg_partition(data.bins, perm, v0p, v1p, wp, segs, split_feat,
                                                                     split_bin, cat_off, cm.reshape(-1), child,
                                                                     len(nxt))

@@ -88,6 +88,12 @@ _SIGS = {
     "cdna_seg_partition": ([c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_int64, c_void_p, c_void_p], c_int),
+    "cdna_codes_compact": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_bins_row_major": ([c_void_p, c_int64, c_int, c_void_p, c_void_p], c_int),
+    "cdna_codes_compact_w": ([c_int, c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+                             c_int),
     "cdna_als_max_rank": ([], c_int),
     "cdna_als_accumulate": ([c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p,
                              c_void_p, c_void_p, c_void_p], c_int),

@@ -966,3 +966,125 @@ def seg_partition(bins: torch.Tensor, perm: Optional[torch.Tensor], v0p: Optiona
                                         None, _ptr(perm_o), _ptr(v0_o), _ptr(v1_o), _ptr(w_o), impl_n, None,
                                         _stream(dev)), "cdna_seg_partition(scatter)")
     return perm_o, v0_o, v1_o, w_o, np.stack([starts, lens], 1)
+
+
+def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndarray, S: int,
+                  v0: Optional[torch.Tensor], v1: torch.Tensor):
+    """Rows of the nodes a level builds, gathered into one segment per histogram slot.
+
+    codes [T, n] row records (weight << 8 | local node); tfirst [T] first active index per tree;
+    build_slot [A] slot of active node a (-1: not built).  Returns (perm int32, v0p, v1p, wp uint8,
+    segs [S, 2] {start, len}).  Row order inside a segment is unspecified (the segment histograms
+    are exact fixed-point sums, so it does not change any result).
+    """
+    T, n = codes.shape
+    dev = codes.device
+    A = len(build_slot)
+    bs = np.asarray(build_slot, dtype=np.int32)
+    if not _native(codes):
+        c = codes.to(torch.int32) & 0xFFFF
+        loc = c & 0xFF
+        ids = tfirst.to(torch.int64).to(dev)[:, None] + loc.long()
+        slot_t = torch.from_numpy(np.concatenate([bs, [-1]])).to(dev)
+        ids = torch.where(loc == CODE_DONE, torch.full_like(ids, A), ids).clamp_max(A)
+        slot = slot_t[ids]  # [T, n]
+        flat = slot.reshape(-1)
+        keep = torch.nonzero(flat >= 0).flatten()
+        order = keep[torch.argsort(flat[keep], stable=True)]
+        rows = order % n
+        lens = np.bincount(flat[keep].numpy(), minlength=S)[:S].astype(np.int64)
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if S else np.zeros(0, np.int64)
+        return (rows.to(torch.int32), None if v0 is None else v0[rows].float(), v1[rows].float(),
+                (c.reshape(-1)[order] >> 8).to(torch.uint8), np.stack([starts, lens], 1))
+    L = _lib.lib()
+    assert tfirst.numel() == T
+    tf = tfirst.to(device=dev, dtype=torch.int32)
+    # built nodes per tree -> wave-owned kernel when few (stable, no atomics)
+    tf_h = tfirst.cpu().numpy().astype(np.int64)
+    tree_of = np.searchsorted(tf_h, np.arange(A), side="right") - 1
+    built = bs >= 0
+    nb_t = np.bincount(tree_of[built], minlength=T) if A else np.zeros(T, np.int64)
+    kb_need = int(nb_t.max()) if T else 0
+    if 0 < kb_need <= 16 and COMPACT_W:
+        return _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1)
+    bs_t = torch.from_numpy(bs).to(dev)
+    v1c = v1.float().contiguous()
+    v0c = None if v0 is None else v0.float().contiguous()
+    cnt = torch.zeros(max(S, 1), dtype=torch.int32, device=dev)
+    _lib.check(L.cdna_codes_compact(1, _ptr(codes), n, T, A, _ptr(tf), _ptr(bs_t), _ptr(v0c), _ptr(v1c), _ptr(cnt),
+                                    None, None, None, None, _stream(dev)), "cdna_codes_compact(count)")
+    lens = cnt.cpu().numpy()[:S].astype(np.int64)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if S else np.zeros(0, np.int64)
+    total = int(lens.sum())
+    assert total < 2 ** 31
+    perm = torch.empty(total, dtype=torch.int32, device=dev)
+    v1p = torch.empty(total, dtype=torch.float32, device=dev)
+    v0p = None if v0 is None else torch.empty(total, dtype=torch.float32, device=dev)
+    wp = torch.empty(total, dtype=torch.uint8, device=dev)
+    if total:
+        cur = torch.from_numpy(np.concatenate([starts, [0]]).astype(np.int32)).to(dev)
+        _lib.check(L.cdna_codes_compact(2, _ptr(codes), n, T, A, _ptr(tf), _ptr(bs_t), _ptr(v0c), _ptr(v1c),
+                                        _ptr(cur), _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp), _stream(dev)),
+                   "cdna_codes_compact(scatter)")
+    return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
+
+
+COMPACT_W = __import__("os").environ.get("CDNAML_COMPACT_W", "1") != "0"
+
+
+def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1):
+    T, n = codes.shape
+    dev = codes.device
+    A = len(bs)
+    KB = 1
+    while KB < kb_need:
+        KB *= 2
+    # k of each built node inside its tree (slots are numbered tree-major, so slot = first slot of tree + k)
+    kmap = np.full(A, -1, dtype=np.int32)
+    first_slot = np.zeros(T, dtype=np.int64)
+    first_slot[1:] = np.cumsum(nb_t)[:-1]
+    kmap[built] = bs[built] - first_slot[tree_of[built]]
+    assert np.all(kmap[built] >= 0) and np.all(kmap[built] < KB)
+    per_wave = max(256, -(-n // (2048 * 256)) * 256)
+    Wv = -(-n // per_wave)
+    L = _lib.lib()
+    kmap_t = torch.from_numpy(kmap).to(dev)
+    v1c = v1.float().contiguous()
+    v0c = None if v0 is None else v0.float().contiguous()
+    wcnt = torch.empty((T, Wv, KB), dtype=torch.int32, device=dev)
+    _lib.check(L.cdna_codes_compact_w(1, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
+                                      per_wave, Wv, _ptr(wcnt), None, None, None, None, None, _stream(dev)),
+               "cdna_codes_compact_w(count)")
+    tot = wcnt.sum(1, dtype=torch.int64)                      # [T, KB]
+    tot_h = tot.cpu().numpy()
+    lens = np.zeros(S, dtype=np.int64)
+    sl = (first_slot[:, None] + np.arange(KB)[None, :])        # slot of (t, k)
+    valid = np.arange(KB)[None, :] < nb_t[:, None]
+    lens[sl[valid]] = tot_h[valid]
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if S else np.zeros(0, np.int64)
+    total = int(lens.sum())
+    assert total < 2 ** 31
+    perm = torch.empty(total, dtype=torch.int32, device=dev)
+    v1p = torch.empty(total, dtype=torch.float32, device=dev)
+    v0p = None if v0 is None else torch.empty(total, dtype=torch.float32, device=dev)
+    wp = torch.empty(total, dtype=torch.uint8, device=dev)
+    if total:
+        kstart = np.zeros((T, KB), dtype=np.int64)
+        kstart[valid] = starts[sl[valid]]
+        woff = (torch.from_numpy(kstart).to(dev)[:, None, :] + torch.cumsum(wcnt, 1, dtype=torch.int64) - wcnt)
+        woff = woff.to(torch.int32).contiguous()
+        _lib.check(L.cdna_codes_compact_w(2, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
+                                          per_wave, Wv, None, _ptr(woff), _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp),
+                                          _stream(dev)), "cdna_codes_compact_w(scatter)")
+    return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
+
+
+def bins_row_major(bins: torch.Tensor) -> torch.Tensor:
+    """[G, n, 8] feature-group-major bins -> row-major [n, G, 8] copy."""
+    G, n, _ = bins.shape
+    if not _native(bins):
+        return bins.permute(1, 0, 2).contiguous()
+    out = torch.empty((n, G, 8), dtype=torch.uint8, device=bins.device)
+    _lib.check(_lib.lib().cdna_bins_row_major(_ptr(bins), n, G, _ptr(out), _stream(bins.device)),
+               "cdna_bins_row_major")
+    return out

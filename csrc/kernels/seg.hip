@@ -243,6 +243,80 @@ __global__ __launch_bounds__(1024) void seg_hist_rm_kernel(const SegHistArgs a, 
   }
 }
 
+// Flat row-major variant (packed statistics, all G groups in one block): the
+// lanes of a wave take consecutive (row, group) PAIRS, so with G = 13 groups
+// every lane is busy (the 8-lanes-per-row mapping above leaves 3 of every 16
+// lanes idle at G = 13, and every idle lane still costs its share of each
+// ds_add wave instruction).  A lane's 8 cells are updated in a rotated order;
+// the partial last group (d % 8 != 0) masks its missing features per j, so the
+// wave issues exactly 8 atomic instructions per pair round.
+template <bool HAS_W>
+__global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a, const uint64_t* __restrict__ bins_rm,
+                                                             int G) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long h[];
+  constexpr int TH = 1024;
+  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
+  const int plane_g = 8 * a.B;
+  const int plane = G * plane_g;
+  for (int i = threadIdx.x; i < plane; i += TH) h[i] = 0ull;
+  const int rot = threadIdx.x & 7;
+  __syncthreads();
+  const uint32_t total = (uint32_t)len * (uint32_t)G;
+  const uint32_t Gu = (uint32_t)G;
+  constexpr int U = 2;
+  for (uint32_t q0 = threadIdx.x; q0 < total; q0 += TH * U) {
+    uint64_t b8[U];
+    float x1[U];
+    uint32_t w[U];
+    int g_[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t q = q0 + u * TH;
+      const bool ok = q < total;
+      const uint32_t i = ok ? q / Gu : 0u;
+      const int g = ok ? (int)(q - i * Gu) : 0;
+      g_[u] = g;
+      const int row = ok ? a.perm[start + i] : 0;
+      b8[u] = ok ? bins_rm[(int64_t)row * G + g] : 0ull;
+      x1[u] = ok ? a.v1p[start + i] : 0.f;
+      w[u] = ok ? (HAS_W ? (uint32_t)a.wp[start + i] : 1u) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int g = g_[u];
+      const int valid_f = a.d - g * 8;
+      const uint32_t fvalid = w[u] == 0u ? 0u : (valid_f >= 8 ? 0xFFu : ((1u << (valid_f > 0 ? valid_f : 0)) - 1u));
+      const uint32_t frot = ((fvalid >> rot) | (fvalid << (8 - rot))) & 0xFFu;
+      const uint32_t lo = (uint32_t)b8[u], hi = (uint32_t)(b8[u] >> 32);
+      int q1 = (int)rintf(x1[u] * a.qs1);
+      q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+      const unsigned long long add =
+          ((unsigned long long)w[u] << kPackShift) + (unsigned long long)w[u] * (unsigned long long)(q1 + kPackQ);
+      const int gbase = g * plane_g;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int jj = (j + rot) & 7;
+        const int cell = gbase + jj * a.B + (int)__builtin_amdgcn_ubfe(jj >= 4 ? hi : lo, (uint32_t)((jj & 3) * 8), 8u);
+        if ((frot >> j) & 1u) atomicAdd(h + cell, add);
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < plane; c += TH) {
+    const int gq = c / plane_g, rem = c - gq * plane_g;
+    const int jj = rem / a.B, bn = rem - jj * a.B;
+    const int f = gq * 8 + jj;
+    if (f >= a.d) continue;
+    const unsigned long long v = h[c];
+    if (!v) continue;
+    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+    const unsigned long long cnt = v >> kPackShift;
+    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    atomicAdd(o, cnt);
+    atomicAdd(o + 1, (unsigned long long)sum);
+  }
+}
+
 struct SegPartArgs {
   const uint64_t* bins;
   int64_t n;
@@ -376,10 +450,278 @@ __global__ __launch_bounds__(kSegThreads) void seg_scatter_kernel(const SegPartA
   }
 }
 
+// ---------------------------------------------------------------------------
+// Multi-tree forests keep the dense row records (hist5.hip codes, cheap to
+// partition: one coalesced pass) and, before each level >= 1 histogram, gather
+// the rows of the nodes that level BUILDS (the smaller sibling of each pair)
+// into per-slot segments: perm / statistics / weight, so the segment
+// histogram touches only those rows (the codes kernels scan every (row, tree)
+// record and idle on the skipped ones: 54 ms vs ~37 ms per level at 1e8 x 20
+// trees).  Pass 1 counts rows per slot; the host turns counts into segment
+// starts; pass 2 scatters.  Within a wave the rows of one slot are ranked by
+// peeling (one ballot per distinct slot in the wave), so the LDS atomics are
+// one per (wave, slot), not one per row.  Segment order is block-arbitrary;
+// the fixed-point histogram sums do not depend on it.
+struct CompactArgs {
+  const uint16_t* codes;  // [T][n]  weight << 8 | local node (0xFF = done)
+  int64_t n;
+  int T, A;
+  const int* tfirst;      // [T] first active index of tree t (active order is tree-major)
+  const int* build_slot;  // [A] histogram slot of the active node, -1 = not built
+  const float* v0;        // [n] or null
+  const float* v1;        // [n]
+  int* cnt;               // pass 1: [S] row totals; pass 2: [S] write cursors (pre-set to segment starts)
+  int* perm_out;
+  float* v0_out;
+  float* v1_out;
+  uint8_t* w_out;
+};
+
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void codes_compact_kernel(const CompactArgs a) {
+  __shared__ int s_slot[256], s_cnt[256], s_base[256];
+  const int t = blockIdx.y;
+  const int tf = a.tfirst[t];
+  const int nloc = (t + 1 < a.T ? a.tfirst[t + 1] : a.A) - tf;
+  for (int i = threadIdx.x; i < 256; i += 256) {
+    s_slot[i] = i < nloc ? a.build_slot[tf + i] : -1;
+    s_cnt[i] = 0;
+  }
+  __syncthreads();
+  const uint16_t* rec = a.codes + (int64_t)t * a.n;
+  const int64_t per = ((a.n + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
+  const int64_t r0 = (int64_t)blockIdx.x * per;
+  const int64_t r1 = r0 + per < a.n ? r0 + per : a.n;
+  const int lane = threadIdx.x & 63;
+  constexpr int U = 8;  // code loads in flight per thread (one dependent load per trip was latency-bound)
+  // sweep 1: per-slot counts of this block's range (wave-aggregated LDS atomics)
+  for (int64_t rb = r0; rb < r1; rb += 256 * U) {
+    uint32_t cu[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = rb + u * 256 + threadIdx.x;
+      cu[u] = r < r1 ? (uint32_t)rec[r] : 0xFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+    const uint32_t c = cu[u];
+    const uint32_t loc = c & 0xFFu;
+    bool want = loc != 0xFFu && s_slot[loc] >= 0;
+    while (true) {
+      const uint64_t act = __builtin_amdgcn_ballot_w64(want);
+      if (!act) break;
+      const int leader = __builtin_ctzll(act);
+      const uint32_t lloc = (uint32_t)__shfl((int)loc, leader);
+      const uint64_t m = __builtin_amdgcn_ballot_w64(want && loc == lloc);
+      if (lane == leader) atomicAdd(&s_cnt[lloc], __builtin_popcountll(m));
+      if (loc == lloc) want = false;
+    }
+    }
+  }
+  __syncthreads();
+  if (!SCATTER) {
+    for (int i = threadIdx.x; i < nloc; i += 256)
+      if (s_cnt[i]) atomicAdd(&a.cnt[s_slot[i]], s_cnt[i]);
+    return;
+  }
+  for (int i = threadIdx.x; i < nloc; i += 256) {
+    s_base[i] = s_cnt[i] ? atomicAdd(&a.cnt[s_slot[i]], s_cnt[i]) : 0;
+    s_cnt[i] = 0;
+  }
+  __syncthreads();
+  // sweep 2: scatter (row, statistics, weight) to the slot segments
+  for (int64_t rb = r0; rb < r1; rb += 256 * U) {
+    uint32_t cu[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = rb + u * 256 + threadIdx.x;
+      cu[u] = r < r1 ? (uint32_t)rec[r] : 0xFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+    const int64_t r = rb + u * 256 + threadIdx.x;
+    const uint32_t c = cu[u];
+    const uint32_t loc = c & 0xFFu;
+    bool want = loc != 0xFFu && s_slot[loc] >= 0;
+    int pos = -1;
+    while (true) {
+      const uint64_t act = __builtin_amdgcn_ballot_w64(want);
+      if (!act) break;
+      const int leader = __builtin_ctzll(act);
+      const uint32_t lloc = (uint32_t)__shfl((int)loc, leader);
+      const uint64_t m = __builtin_amdgcn_ballot_w64(want && loc == lloc);
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&s_cnt[lloc], __builtin_popcountll(m));
+      base = __shfl(base, leader);
+      if (want && loc == lloc) {
+        const int below =
+            (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        pos = s_base[lloc] + base + below;
+        want = false;
+      }
+    }
+    if (pos >= 0) {
+      a.perm_out[pos] = (int)r;
+      a.v1_out[pos] = a.v1[r];
+      if (a.v0) a.v0_out[pos] = a.v0[r];
+      a.w_out[pos] = (uint8_t)(c >> 8);
+    }
+    }
+  }
+}
+
+// Wave-owned variant for few built nodes per tree (KB <= 16, every RF level of
+// depth <= 5 and the shallow levels of deeper forests).  rocprofv3 on the
+// peeling kernel: ~80 wave instructions per 64 records and 71 % of wave time
+// waiting (3.8 + 10.3 ms per level at 1e8 x 20 trees).  Here each wave owns a
+// fixed contiguous row range and counts its records per built node in
+// registers (pass 1 writes [T][waves][KB] counts, no atomics); the host scans
+// the counts into per-wave output offsets; pass 2 re-reads the range and
+// ranks a lane's (up to 4) records per node with 3 ballots (the count 0..4 in
+// binary).  Output order is the row order: stable and deterministic.
+struct CompactWArgs {
+  const uint16_t* codes;
+  int64_t n;
+  int T, A;
+  const int* tfirst;
+  const int* kmap;        // [A] index of the active node among its tree's built nodes, -1 = not built
+  const float* v0;
+  const float* v1;
+  int64_t per_wave;       // rows per wave (multiple of 256)
+  int Wv;                 // waves per tree
+  int* wcnt;              // pass 1: [T][Wv][KB] counts
+  const int* woff;        // pass 2: [T][Wv][KB] output offsets
+  int* perm_out;
+  float* v0_out;
+  float* v1_out;
+  uint8_t* w_out;
+};
+
+__device__ __forceinline__ bool v_aligned(const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <int KB, bool SCATTER>
+__global__ __launch_bounds__(256) void codes_compact_w_kernel(const CompactWArgs a) {
+  __shared__ int s_k[256];
+  const int t = blockIdx.y;
+  const int tf = a.tfirst[t];
+  const int nloc = (t + 1 < a.T ? a.tfirst[t + 1] : a.A) - tf;
+  for (int i = threadIdx.x; i < 256; i += 256) s_k[i] = (i < nloc && i < 255) ? a.kmap[tf + i] : -1;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= a.Wv) return;
+  const int64_t r_begin = (int64_t)w * a.per_wave;
+  const int64_t r_end = r_begin + a.per_wave < a.n ? r_begin + a.per_wave : a.n;
+  const uint16_t* rec = a.codes + (int64_t)t * a.n;
+  const int64_t cb = ((int64_t)t * a.Wv + w) * KB;
+  int acc[KB];
+#pragma unroll
+  for (int k = 0; k < KB; ++k) acc[k] = SCATTER ? a.woff[cb + k] : 0;
+  // 2 x 4 records per lane per trip, codes (and, in pass 2, the statistics) loaded up front as vectors:
+  // the one-group loop waited on each trip's dependent load chain (codes -> LDS map -> v1 -> store)
+  const bool vec = (a.n & 3) == 0 && (reinterpret_cast<uintptr_t>(a.codes) & 7u) == 0 && v_aligned(a.v1) && (a.v0 == nullptr || v_aligned(a.v0));
+  constexpr int NG = 2;
+  for (int64_t rb = r_begin; rb < r_end; rb += 256 * NG) {
+    uint32_t cc[NG][4];
+    float x1[NG][4], x0[NG][4];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      const int64_t r = rb + q * 256 + lane * 4;
+      if (vec && r + 3 < r_end) {
+        const uint2 c4 = *reinterpret_cast<const uint2*>(rec + r);
+        cc[q][0] = c4.x & 0xFFFFu;
+        cc[q][1] = c4.x >> 16;
+        cc[q][2] = c4.y & 0xFFFFu;
+        cc[q][3] = c4.y >> 16;
+        if (SCATTER) {
+          const float4 f = *reinterpret_cast<const float4*>(a.v1 + r);
+          x1[q][0] = f.x, x1[q][1] = f.y, x1[q][2] = f.z, x1[q][3] = f.w;
+          if (a.v0) {
+            const float4 g = *reinterpret_cast<const float4*>(a.v0 + r);
+            x0[q][0] = g.x, x0[q][1] = g.y, x0[q][2] = g.z, x0[q][3] = g.w;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = r + j < r_end;
+          cc[q][j] = ok ? (uint32_t)rec[r + j] : 0xFFu;
+          if (SCATTER) {
+            x1[q][j] = ok ? a.v1[r + j] : 0.f;
+            if (a.v0) x0[q][j] = ok ? a.v0[r + j] : 0.f;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+    const int64_t r = rb + q * 256 + lane * 4;
+    int kk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) kk[j] = s_k[cc[q][j] & 0xFFu];
+    if (!SCATTER) {
+#pragma unroll
+      for (int k = 0; k < KB; ++k)
+        acc[k] += (kk[0] == k) + (kk[1] == k) + (kk[2] == k) + (kk[3] == k);
+    } else {
+      int pos[4] = {-1, -1, -1, -1};
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const int c = (kk[0] == k) + (kk[1] == k) + (kk[2] == k) + (kk[3] == k);
+        const uint64_t b0 = __builtin_amdgcn_ballot_w64((c & 1) != 0);
+        const uint64_t b1 = __builtin_amdgcn_ballot_w64((c & 2) != 0);
+        const uint64_t b2 = __builtin_amdgcn_ballot_w64((c & 4) != 0);
+        if ((b0 | b1 | b2) == 0ull) continue;  // wave-uniform
+        auto below = [&](uint64_t m) {
+          return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        };
+        int p = acc[k] + below(b0) + 2 * below(b1) + 4 * below(b2);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (kk[j] == k) pos[j] = p++;
+        acc[k] += __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (pos[j] < 0) continue;
+        a.perm_out[pos[j]] = (int)(r + j);
+        a.v1_out[pos[j]] = x1[q][j];
+        if (a.v0) a.v0_out[pos[j]] = x0[q][j];
+        a.w_out[pos[j]] = (uint8_t)(cc[q][j] >> 8);
+      }
+    }
+    }
+  }
+  if (!SCATTER) {
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      int v = acc[k];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) a.wcnt[cb + k] = v;
+    }
+  }
+}
+
+// [G][n] 8-feature bin words -> row-major [n][G] (one row's words contiguous),
+// staged through LDS so both the reads and the writes are coalesced.
+__global__ __launch_bounds__(256) void bins_row_major_kernel(const uint64_t* __restrict__ bins, int64_t n, int G,
+                                                             uint64_t* __restrict__ out) {
+  extern __shared__ uint64_t tile[];  // [256][G] (odd G strides spread the banks)
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  const int rows = n - r0 < 256 ? (int)(n - r0) : 256;
+  for (int g = 0; g < G; ++g)
+    if (threadIdx.x < rows) tile[threadIdx.x * G + g] = bins[(int64_t)g * n + r0 + threadIdx.x];
+  __syncthreads();
+  uint64_t* o = out + r0 * G;
+  for (int i = threadIdx.x; i < rows * G; i += 256) o[i] = tile[i];
+}
+
 }  // namespace
 
 // mode bit0: packed (no v0; count | sum in one atomic); bit1: per-row weights wp present;
-// bit2: bins are row-major [n][G] words (seg_hist_rm_kernel).
+// bit2: bins are row-major [n][G] words (seg_hist_flat_kernel when packed and all groups fit 128 KB of LDS,
+// else seg_hist_rm_kernel); bit3: force seg_hist_rm_kernel.
 // work: [nwork][3] {start, len, slot}; grid = nwork x ceil(d / 8).
 CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int B, const int* perm, const float* v0p,
                            const float* v1p, const uint8_t* wp, const int* work, int nwork, float qs0, float qs1,
@@ -387,6 +729,20 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
   if (nwork <= 0) return 0;
   SegHistArgs a{bins, n, d, B, perm, v0p, v1p, wp, work, qs0, qs1, out};
   const bool packed = (mode & 1) != 0, has_w = (mode & 2) != 0;
+  if ((mode & 4) && packed && (size_t)((d + 7) / 8) * 8 * B * 8 <= 128 * 1024 && !(mode & 8)) {
+    // all groups of a row in one block, lanes over (row, group) pairs
+    const int G = (d + 7) / 8;
+    const size_t lds = (size_t)G * 8 * B * 8;
+    auto launch = [&](auto kern) {
+      if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+      hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), lds, st, a, bins, G);
+    };
+    if (has_w) launch(seg_hist_flat_kernel<true>);
+    else launch(seg_hist_flat_kernel<false>);
+    return (int)hipGetLastError();
+  }
   if (mode & 4) {  // bins is row-major [n][G]
     const int G = (d + 7) / 8;
     const int cells_max = 16384 / (packed ? 1 : 2);  // 128 KB of u64 planes
@@ -440,5 +796,53 @@ CDNA_API int cdna_seg_partition(int pass, const uint64_t* bins, int64_t n, const
                 implicit_n, right_cnt};
   if (pass == 1) hipLaunchKernelGGL(seg_count_kernel, dim3((unsigned)nwork), dim3(kSegThreads), 0, st, a);
   else hipLaunchKernelGGL(seg_scatter_kernel, dim3((unsigned)nwork), dim3(kSegThreads), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// Gather the rows of built nodes into slot segments (see CompactArgs).  pass 1: cnt = per-slot
+// totals (must be zeroed); pass 2: cnt = per-slot write cursors initialised to the segment starts.
+CDNA_API int cdna_codes_compact(int pass, const uint16_t* codes, int64_t n, int T, int A, const int* tfirst,
+                                const int* build_slot, const float* v0, const float* v1, int* cnt, int* perm_out,
+                                float* v0_out, float* v1_out, uint8_t* w_out, hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  CompactArgs a{codes, n, T, A, tfirst, build_slot, v0, v1, cnt, perm_out, v0_out, v1_out, w_out};
+  int64_t nb = (n + 4095) / 4096;
+  const int per_tree = (int)(nb < 512 ? nb : 512);
+  const dim3 grid((unsigned)per_tree, (unsigned)T);
+  if (pass == 1) hipLaunchKernelGGL(codes_compact_kernel<false>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(codes_compact_kernel<true>, grid, dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_bins_row_major(const uint64_t* bins, int64_t n, int G, uint64_t* out, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (G <= 0 || G > 32) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bins_row_major_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), (size_t)256 * G * 8, st,
+                     bins, n, G, out);
+  return (int)hipGetLastError();
+}
+
+// Wave-owned compaction (KB = max built nodes per tree, <= 16).  pass 1 writes wcnt, pass 2 scatters
+// from woff.  per_wave must be a multiple of 256; Wv = ceil(n / per_wave).
+CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64_t n, int T, int A,
+                                  const int* tfirst, const int* kmap, const float* v0, const float* v1,
+                                  int64_t per_wave, int Wv, int* wcnt, const int* woff, int* perm_out, float* v0_out,
+                                  float* v1_out, uint8_t* w_out, hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  if (per_wave % 256 != 0 || (int64_t)Wv * per_wave < n) return (int)hipErrorInvalidValue;
+  CompactWArgs a{codes, n, T, A, tfirst, kmap, v0, v1, per_wave, Wv, wcnt, woff, perm_out, v0_out, v1_out, w_out};
+  const dim3 grid((unsigned)((Wv + 3) / 4), (unsigned)T);
+  auto go = [&](auto k1, auto k2) {
+    if (pass == 1) hipLaunchKernelGGL(k1, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k2, grid, dim3(256), 0, st, a);
+  };
+  switch (KB) {
+    case 1: go(codes_compact_w_kernel<1, false>, codes_compact_w_kernel<1, true>); break;
+    case 2: go(codes_compact_w_kernel<2, false>, codes_compact_w_kernel<2, true>); break;
+    case 4: go(codes_compact_w_kernel<4, false>, codes_compact_w_kernel<4, true>); break;
+    case 8: go(codes_compact_w_kernel<8, false>, codes_compact_w_kernel<8, true>); break;
+    case 16: go(codes_compact_w_kernel<16, false>, codes_compact_w_kernel<16, true>); break;
+    default: return (int)hipErrorInvalidValue;
+  }
   return (int)hipGetLastError();
 }

@@ -88,8 +88,11 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
                                                       uint64_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int G = (d + 7) / 8;
-  float* sx = smf;                                  // [rows_per_tile][d]
-  float* sthr = smf + (size_t)rows_per_tile * d;    // [d][tmax]
+  // [rows_per_tile][dp]: an odd row stride keeps the per-task x reads (lanes = rows) conflict-free; with
+  // stride d = 100 (4 banks apart) 8 lanes shared each bank
+  const int dp = d | 1;
+  float* sx = smf;                                  // [rows_per_tile][dp]
+  float* sthr = smf + (size_t)rows_per_tile * dp;   // [d][tmax]
   int* snt = reinterpret_cast<int*>(sthr + (size_t)d * tmax);
   for (int i = threadIdx.x; i < d * tmax; i += 256) sthr[i] = thr[i];
   for (int i = threadIdx.x; i < d; i += 256) snt[i] = nthr[i];
@@ -117,22 +120,35 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
     const int rows = (int)((n - r0) < rows_per_tile ? (n - r0) : rows_per_tile);
     __syncthreads();
     if (use_pre) {
-      float4* dst = reinterpret_cast<float4*>(sx);
       const int nv = rows * d / 4;
 #pragma unroll
       for (int k = 0; k < kPre; ++k) {
         const int i = threadIdx.x + k * 256;
-        if (i < nv) dst[i] = pre[k];
+        if (i < nv) {
+          const int e = i * 4, r = e / d, f = e - r * d;  // d % 4 == 0: a float4 never crosses a row
+          float* dst = sx + r * dp + f;
+          dst[0] = pre[k].x;
+          dst[1] = pre[k].y;
+          dst[2] = pre[k].z;
+          dst[3] = pre[k].w;
+        }
       }
     } else if (contiguous) {
       const float4* src = reinterpret_cast<const float4*>(X + r0 * ldx);
-      float4* dst = reinterpret_cast<float4*>(sx);
       const int nv = rows * d / 4;
-      for (int i = threadIdx.x; i < nv; i += 256) dst[i] = src[i];
+      for (int i = threadIdx.x; i < nv; i += 256) {
+        const float4 v = src[i];
+        const int e = i * 4, r = e / d, f = e - r * d;
+        float* dst = sx + r * dp + f;
+        dst[0] = v.x;
+        dst[1] = v.y;
+        dst[2] = v.z;
+        dst[3] = v.w;
+      }
     } else {
       for (int i = threadIdx.x; i < rows * d; i += 256) {
         const int r = i / d, f = i - r * d;
-        sx[i] = X[(r0 + r) * ldx + f];
+        sx[r * dp + f] = X[(r0 + r) * ldx + f];
       }
     }
     __syncthreads();
@@ -147,7 +163,7 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int f = g * 8 + j < d ? g * 8 + j : d - 1;
-        x[j] = sx[r * d + f];
+        x[j] = sx[r * dp + f];
         nt[j] = g * 8 + j < d ? snt[f] : 0;
         toff[j] = f * tmax - 1;
         lo[j] = 0;
@@ -369,10 +385,42 @@ __global__ __launch_bounds__(256) void predict_kernel(const float* __restrict__ 
   for (int i = threadIdx.x; i < n_nodes_lds; i += 256) snodes[i] = nodes[i];
   const int tl = threadIdx.x >> 6, row = threadIdx.x & 63;
   const bool vec = ldx == d && (d % 4) == 0;
-  for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < n; r0 += (int64_t)gridDim.x * 64) {
+  // register double buffer: the next tile's float4s are in flight while this
+  // tile's trees are walked (the single-buffered loop read X at ~1.8 TB/s)
+  constexpr int kPre = 8;
+  float4 pre[kPre];
+  const int64_t stride = (int64_t)gridDim.x * 64;
+  const bool use_pre = vec && 64 * d / 4 <= kPre * 256;
+  auto fetch = [&](int64_t r0) {
+    if (r0 >= n) return;
+    const int rows = (int)((n - r0) < 64 ? (n - r0) : 64);
+    const float4* src = reinterpret_cast<const float4*>(X + r0 * ldx);
+    const int nv = rows * d / 4;
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int i = threadIdx.x + k * 256;
+      if (i < nv) pre[k] = src[i];
+    }
+  };
+  if (use_pre) fetch((int64_t)blockIdx.x * 64);
+  for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < n; r0 += stride) {
     const int rows = (int)((n - r0) < 64 ? (n - r0) : 64);
     __syncthreads();
-    if (vec) {
+    if (use_pre) {
+      const int nv = rows * d / 4;
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < nv) {
+          const int e = i * 4, r = e / d, f = e - r * d;
+          float* dst = sx + r * dp + f;
+          dst[0] = pre[k].x;
+          dst[1] = pre[k].y;
+          dst[2] = pre[k].z;
+          dst[3] = pre[k].w;
+        }
+      }
+    } else if (vec) {
       const float4* src = reinterpret_cast<const float4*>(X + r0 * ldx);
       const int nv = rows * d / 4;
       for (int i = threadIdx.x; i < nv; i += 256) {
@@ -392,6 +440,7 @@ __global__ __launch_bounds__(256) void predict_kernel(const float* __restrict__ 
     }
     for (int e = threadIdx.x; e < 4 * 64 * K; e += 256) part[e] = 0.f;
     __syncthreads();
+    if (use_pre) fetch(r0 + stride);
     if (row < rows) {
       const float* xr = sx + row * dp;
       float* pr = part + (tl * 64 + row) * K;
@@ -488,12 +537,13 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
   {
     // v2: tile of rows in LDS next to the thresholds (<= 64 KB per block)
     const size_t tb = (size_t)d * (tmax > 0 ? tmax : 1) * 4 + (size_t)d * 4;
+    const size_t dp = (size_t)(d | 1);
     int rpt = 64;
-    while (rpt > 4 && ((size_t)rpt * d * 4 + tb > 64 * 1024 || (size_t)rpt * d > 8192)) rpt /= 2;
-    if ((size_t)rpt * d * 4 + tb <= 64 * 1024) {
+    while (rpt > 4 && ((size_t)rpt * dp * 4 + tb > 64 * 1024 || (size_t)rpt * d > 8192)) rpt /= 2;
+    if ((size_t)rpt * dp * 4 + tb <= 64 * 1024) {
       int steps = 0;
       while ((1 << steps) <= tmax) ++steps;
-      const size_t lds = (size_t)rpt * d * 4 + tb;
+      const size_t lds = (size_t)rpt * dp * 4 + tb;
       hipLaunchKernelGGL(binize2_kernel, dim3(grid_for(n, rpt, 8192)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
                          tmax > 0 ? tmax : 1, rpt, steps, out);
       return (int)hipGetLastError();

@@ -392,7 +392,7 @@ def _seg_state(n, d, B, nseg, seed, weights):
     return bins, perm, v0, v1, wp, np.stack([starts, lens], 1)
 
 
-@pytest.mark.parametrize("packed,weights,B,d", [(True, False, 256, 100), (True, True, 40, 21), (False, False, 64, 13),
+@pytest.mark.parametrize("packed,weights,B,d", [(True, False, 256, 100), (True, True, 40, 21), (True, True, 40, 100), (False, False, 64, 13),
                                                  (False, True, 256, 9)])
 @pytest.mark.parametrize("row_major", [False, True])
 def test_seg_hist(dev, packed, weights, B, d, row_major):
@@ -452,6 +452,44 @@ def test_seg_partition_implicit_level0(dev):
     assert torch.equal(ref[1], out[1].cpu()) and torch.equal(ref[2], out[2].cpu())
     assert torch.equal(ref[3], out[3].cpu())
     assert int(ref[3].min()) > 0  # out-of-bag rows dropped
+
+
+@pytest.mark.parametrize("wave_owned", [True, False])
+def test_codes_compact(dev, monkeypatch, wave_owned):
+    """Rows of built nodes gathered into slot segments: same (row, v1, w) multiset per slot as the reference
+    (the wave-owned kernel is also stable: exactly the reference order)."""
+    monkeypatch.setattr(K, "COMPACT_W", wave_owned)
+    T, n = 6, 50000
+    rng = np.random.default_rng(2)
+    nloc = rng.integers(1, 9, T)
+    tfirst = torch.from_numpy(np.concatenate([[0], np.cumsum(nloc)[:-1]]).astype(np.int32))
+    A = int(nloc.sum())
+    loc = rng.integers(0, 9, (T, n))
+    loc = np.where(loc >= nloc[:, None], 0xFF, loc)
+    w = rng.integers(1, 5, (T, n))
+    codes = torch.from_numpy(((w << 8) | loc).astype(np.uint16).view(np.int16))
+    build = rng.random(A) < 0.6
+    slot_of = np.full(A, -1, np.int32)
+    slot_of[build] = np.arange(build.sum())
+    S = int(build.sum())
+    v1 = torch.randn(n)
+    ref = K.codes_compact(codes, tfirst, slot_of, S, None, v1)
+    out = K.codes_compact(codes.to(dev), tfirst, slot_of, S, None, v1.to(dev))
+    np.testing.assert_array_equal(ref[4], out[4])
+    for s_, (st, ln) in enumerate(ref[4]):
+        key_r = sorted(zip(ref[0][st:st + ln].tolist(), ref[3][st:st + ln].tolist()))
+        key_o = sorted(zip(out[0][st:st + ln].cpu().tolist(), out[3][st:st + ln].cpu().tolist()))
+        assert key_r == key_o
+        rows = out[0][st:st + ln].long().cpu()
+        assert torch.equal(out[2][st:st + ln].cpu(), v1[rows])
+    if wave_owned:
+        assert torch.equal(out[0].cpu(), ref[0]) and torch.equal(out[3].cpu(), ref[3])
+
+
+def test_bins_row_major(dev):
+    bins = torch.randint(0, 255, (13, 100003, 8), dtype=torch.uint8)
+    out = K.bins_row_major(bins.to(dev)).cpu()
+    assert torch.equal(out, bins.permute(1, 0, 2).contiguous())
 
 
 def test_mseg_forest_matches_codes_forest(dev, monkeypatch):
