@@ -44,6 +44,10 @@ USE_SEG = __import__("os").environ.get("CDNAML_TREE_SEG", "1") != "0"
 # multi-tree regression forests: level 0 on row records, then rows grouped by (tree, node) segments
 USE_MSEG = __import__("os").environ.get("CDNAML_TREE_MSEG", "1") != "0"
 MSEG_L0 = __import__("os").environ.get("CDNAML_MSEG_L0", "1") != "0"  # level 0 through segments too
+# feature-subset forests: accumulate only each node's sampled features in segment mode.  Opt-in: measured
+# 5-8x slower (profiles/pmc_seg_hist_subset.txt): both children must be built, and every row gather of the
+# row-major bins (one or two 64 B lines) then feeds 34 atomics instead of 104
+MSEG_SUBSET = __import__("os").environ.get("CDNAML_MSEG_SUBSET", "0") != "0"
 
 
 @dataclass
@@ -117,6 +121,59 @@ def find_thresholds(sample: np.ndarray, d: int, max_bins: int, categorical: Dict
     return thr, nthr
 
 
+def find_thresholds_t(samp: torch.Tensor, max_bins: int, categorical: Dict[int, int]):
+    """``find_thresholds`` on a [s, d] float64 tensor, vectorised over features (runs on the sample's device).
+
+    Features with more distinct values than ``max_bins`` (the common continuous case) take the batched
+    quantile path: one sort of the whole sample, the quantile positions, and a batched searchsorted for
+    the next distinct value.  Categorical / few-distinct / empty features fall back to the per-feature host
+    code on their (already sorted) column.  Bit-identical to ``find_thresholds``.
+    """
+    s, d = samp.shape
+    thr = np.zeros((d, max(max_bins - 1, 1)), dtype=np.float64)
+    nthr = np.zeros(d, dtype=np.int32)
+    if s == 0 or d == 0:
+        for f in categorical:
+            nthr[f] = -1
+        return thr, nthr
+    dev = samp.device
+    S = torch.sort(samp.t().contiguous(), dim=1).values          # [d, s], NaN last
+    nn = (~torch.isnan(S)).sum(1)                                 # non-NaN count per feature
+    Sf = torch.where(torch.isnan(S), torch.full_like(S, float("inf")), S)
+    ar = torch.arange(s, device=dev)
+    valid = ar[None, :] < nn[:, None]
+    newv = torch.ones_like(valid)
+    newv[:, 1:] = Sf[:, 1:] != Sf[:, :-1]
+    k = (newv & valid).sum(1)                                     # distinct non-NaN values
+    cat = torch.zeros(d, dtype=torch.bool, device=dev)
+    if categorical:
+        cat[torch.tensor(sorted(categorical), device=dev)] = True
+    fast = (k > max_bins) & ~cat
+    if max_bins > 1 and bool(fast.any()):
+        j = torch.arange(1, max_bins, device=dev, dtype=torch.int64)
+        tgt = (nn[:, None] * j[None, :]).double() / max_bins      # same operations as the host code
+        pos = (torch.ceil(tgt).long() - 1).clamp_min(0)
+        pos = torch.minimum(pos, (nn - 1).clamp_min(0)[:, None])
+        v = Sf.gather(1, pos)
+        vmax = Sf.gather(1, (nn - 1).clamp_min(0)[:, None])
+        first_max = torch.searchsorted(Sf, vmax, right=False)
+        prev_max = Sf.gather(1, (first_max - 1).clamp_min(0))
+        v = torch.where(v == vmax, prev_max, v)                  # idx clipped to len(vals) - 2
+        nxt = Sf.gather(1, torch.searchsorted(Sf, v, right=True).clamp_max(s - 1))
+        cand = ((v + nxt) / 2.0).cpu().numpy()
+        for f in torch.nonzero(fast).flatten().tolist():
+            c = np.unique(cand[f])[: max_bins - 1]
+            thr[f, : len(c)] = c
+            nthr[f] = len(c)
+    slow = torch.nonzero(~fast).flatten().tolist()
+    if slow:
+        cols = S[slow].t().cpu().numpy()
+        t2, n2 = find_thresholds(cols, len(slow), max_bins,
+                                 {i: categorical[f] for i, f in enumerate(slow) if f in categorical})
+        thr[slow], nthr[slow] = t2, n2
+    return thr, nthr
+
+
 def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins: int, seed: int,
                 row_offset: int, n_global: int, missing: Optional[float] = None) -> BinnedData:
     """Global-sample quantile thresholds + device binning.
@@ -158,9 +215,8 @@ def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins:
         samp = X
     if comm.distributed:
         samp = torch.cat(comm.all_gather_varlen(samp.contiguous()))
-    sample = samp.double().cpu().numpy()
-    with _tr.span("tree.find_thresholds", cat="host"):
-        thr, nthr = find_thresholds(sample, d, max_bins, categorical)
+    with _tr.span("tree.find_thresholds"):
+        thr, nthr = find_thresholds_t(samp.double(), max_bins, categorical)
     thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
     nthr_t = torch.from_numpy(nthr).to(X.device)
     with _tr.span("tree.binize"):
@@ -362,6 +418,24 @@ def _impurity_from_counts(c: torch.Tensor, kind: str) -> torch.Tensor:
     return -(p * lp).sum(-1)
 
 
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _mask_feature_lists(words: np.ndarray, d: int) -> Optional[np.ndarray]:
+    """Feature-subset bit words [S, ceil(d/32)] -> feature ids [S, m] (None if m differs between nodes)."""
+    f = np.arange(d)
+    bits = ((words[:, f >> 5] >> (f & 31).astype(np.uint32)) & 1).astype(bool)
+    cnt = bits.sum(1)
+    if len(cnt) == 0 or cnt.min() != cnt.max() or cnt[0] == 0:
+        return None
+    return np.nonzero(bits)[1].reshape(len(cnt), int(cnt[0])).astype(np.int32)
+
+
 class ForestTrainer:
     """Trains T trees level-synchronously over one BinnedData shard per rank."""
 
@@ -376,17 +450,30 @@ class ForestTrainer:
         self.stats_k = self.C if self.classification else 2
 
     # ------------------------------------------------------------ helpers
-    def _feature_mask(self, t: int, node_key: int) -> Optional[np.ndarray]:
+    def _feature_masks(self, trees: np.ndarray, node_keys: np.ndarray) -> np.ndarray:
+        """Feature-subset bit words [A, ceil(d/32)] for a level's nodes (featureSubsetStrategy).
+
+        Node (tree t, heap key) keeps the k features with the smallest splitmix64 hash of
+        (seed, t, key, feature): a uniform k-subset per node, drawn for the whole level in a few
+        vectorised numpy ops (the per-node Generator took ~40 us per node: 6 ms of host time at
+        160 nodes, idling the GPU between levels).  Identical on every rank.
+        """
         k = self.p.feature_subset
         d = self.data.d
-        if k is None or k >= d:
-            return None
-        key = 1 if self.p.subset_scope == "tree" else node_key
-        rng = np.random.default_rng([self.p.seed & 0xFFFFFFFF, t, key])
-        feats = rng.choice(d, size=k, replace=False)
-        words = np.zeros((d + 31) // 32, dtype=np.uint32)
-        for f in feats:
-            words[f >> 5] |= np.uint32(1) << np.uint32(f & 31)
+        A = len(trees)
+        words = np.zeros((A, (d + 31) // 32), dtype=np.uint32)
+        if k is None or k >= d or A == 0:
+            return words
+        keys = np.ones(A, dtype=np.uint64) if self.p.subset_scope == "tree" else node_keys.astype(np.uint64)
+        with np.errstate(over="ignore"):
+            base = (np.uint64(self.p.seed & 0xFFFFFFFFFFFF) * np.uint64(0x9E3779B97F4A7C15)
+                    + trees.astype(np.uint64) * np.uint64(0xBF58476D1CE4E5B9)
+                    + keys * np.uint64(0x94D049BB133111EB))
+            h = _splitmix64(base[:, None] + np.arange(d, dtype=np.uint64)[None, :] * np.uint64(0xD6E8FEB86659FD93))
+        feats = np.argpartition(h, k - 1, axis=1)[:, :k]
+        rows = np.repeat(np.arange(A), k)
+        f = feats.reshape(-1)
+        np.bitwise_or.at(words, (rows, f >> 5), (np.uint32(1) << (f & 31).astype(np.uint32)))
         return words
 
     def _node_stats(self, H: torch.Tensor, fmask_any: torch.Tensor) -> torch.Tensor:
@@ -534,15 +621,19 @@ class ForestTrainer:
         need_masks = p.feature_subset is not None and p.feature_subset < d
         # "masked": accumulate only each node's sampled features (fewer atomics, no subtraction);
         # "full": accumulate all features, derive larger siblings by subtraction, mask at split time.
-        masked = need_masks and HIST_MODE == "masked"
+        # several regression trees: row records for every level (one dense pass partitions all trees); before
+        # each level's histogram the rows of the nodes it builds are gathered into slot segments, so the
+        # histogram touches only those rows
+        mseg_ok = (USE_MSEG and USE_CODES and T > 1 and not self.classification and p.max_depth <= 8 and
+                   T * n < 2 ** 31 and n > 0)
+        # ... and with per-node feature subsets (RandomForest) only each node's sampled features are
+        # accumulated (packed statistics only: no v0)
+        subset_seg = mseg_ok and need_masks and MSEG_SUBSET and stats_rows.get("v0") is None
+        masked = need_masks and (HIST_MODE == "masked" or subset_seg)
         subtract = not masked
         # one regression tree: rows grouped by node in a permutation (segment mode)
         use_seg = USE_SEG and T == 1 and not self.classification and not masked
-        # several regression trees: row records for every level (one dense pass partitions all trees), and from
-        # level 1 on the rows of the nodes a level builds are gathered into slot segments first, so the
-        # histogram touches only those rows (level 0 streams the bins once for every tree instead)
-        use_mseg = (USE_MSEG and USE_CODES and T > 1 and not self.classification and not masked and
-                    p.max_depth <= 8 and T * n < 2 ** 31 and n > 0)
+        use_mseg = mseg_ok and (not masked or subset_seg)
         # row records (uint16 weight<<8 | local node) when every level fits 255 nodes per tree
         use_codes = USE_CODES and p.max_depth <= 8 and not use_seg
         if use_seg:
@@ -594,7 +685,8 @@ class ForestTrainer:
             slot_tree = np.array([active[a]["tree"] for a in build_ids], dtype=np.int32)
             masks_np = None
             if need_masks:
-                masks_np = np.stack([self._feature_mask(e["tree"], e["key"]) for e in active])
+                masks_np = self._feature_masks(np.array([e["tree"] for e in active], dtype=np.uint64),
+                                               np.array([e["key"] for e in active], dtype=np.uint64))
             fm_build = None
             if masked:
                 fm_build = torch.from_numpy(masks_np[build_ids].view(np.int32)).to(dev)
@@ -607,9 +699,16 @@ class ForestTrainer:
                     perm, v0p, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, len(build_ids),
                                                              stats_rows.get("v0"), stats_rows["v1"])
                     sb = np.concatenate([sg, np.arange(len(build_ids), dtype=np.int64)[:, None]], 1)
-                    Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax, mseg_scales,
-                                    bins_rm=data.row_major_bins() if dev.type == "cuda" else None,
-                                    interleave=True)
+                    if subset_seg:
+                        feats = _mask_feature_lists(masks_np[build_ids], d)
+                    if subset_seg and feats is not None:
+                        Hb = K.seg_hist_subset(data.bins, d, B, perm, v1p, wp, sb, len(build_ids), wmax, feats,
+                                               mseg_scales, bins_rm=data.row_major_bins() if dev.type == "cuda"
+                                               else None, interleave=True)
+                    else:
+                        Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax,
+                                        mseg_scales, bins_rm=data.row_major_bins() if dev.type == "cuda" else None,
+                                        interleave=True)
                     del perm, v0p, v1p, wp
                 elif use_seg:
                     sb = np.array([[segs[a, 0], segs[a, 1], slot_of[a]] for a in build_ids], dtype=np.int64)

@@ -91,6 +91,8 @@ _SIGS = {
     "cdna_codes_compact": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_bins_row_major": ([c_void_p, c_int64, c_int, c_void_p, c_void_p], c_int),
+    "cdna_seg_hist_subset": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                              c_float, c_void_p, c_int, c_void_p, c_void_p], c_int),
     "cdna_codes_compact_w": ([c_int, c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
                              c_int),
@@ -101,11 +103,11 @@ _SIGS = {
                         c_void_p], c_int),
     "cdna_codes_init": ([c_void_p, c_int64, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_partition5": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+                         c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
     "cdna_partition": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p], c_int),
     "cdna_tree_predict": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p,
-                           c_void_p, c_int, c_void_p, c_void_p, c_void_p], c_int),
+                           c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p], c_int),
     "cdna_predict_binned_add": ([c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p,
                                  c_void_p], c_int),
     "cdna_uniform": ([c_void_p, c_int64, c_uint64, c_uint64, c_uint32, c_void_p], c_int),

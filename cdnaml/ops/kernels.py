@@ -514,8 +514,10 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
 
 def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tensor, tfirst_next: torch.Tensor,
                     split_feat: torch.Tensor, split_bin: torch.Tensor, cat_off: torch.Tensor,
-                    cat_mask: torch.Tensor, child: torch.Tensor) -> None:
-    """In place: every row's code moves to the chosen child's local index (255 = done)."""
+                    cat_mask: torch.Tensor, child: torch.Tensor, bins_rm: Optional[torch.Tensor] = None) -> None:
+    """In place: every row's code moves to the chosen child's local index (255 = done).
+
+    bins_rm: optional row-major copy [n, G, 8] of the bins, read instead of ``bins`` when given."""
     G, n, _ = bins.shape
     T = codes.shape[0]
     if n == 0 or T == 0:
@@ -526,9 +528,13 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
         args = [t.to(device=bins.device, dtype=torch.int32).contiguous()
                 for t in (tfirst, tfirst_next, split_feat, split_bin, cat_off, child)]
         A = int(split_feat.numel())
-        _lib.check(_lib.lib().cdna_partition5(_ptr(bins), n, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]),
+        src, rm_bytes = bins, 0
+        if bins_rm is not None:
+            assert bins_rm.shape == (n, G, 8) and bins_rm.is_contiguous()
+            src, rm_bytes = bins_rm, G * 8
+        _lib.check(_lib.lib().cdna_partition5(_ptr(src), n, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]),
                                               _ptr(args[2]), _ptr(args[3]), _ptr(args[4]), _ptr(cm),
-                                              _ptr(args[5]), _stream(bins.device)), "cdna_partition5")
+                                              _ptr(args[5]), rm_bytes, _stream(bins.device)), "cdna_partition5")
         return
     node, w = decode_codes(codes, tfirst)
     live = node >= 0
@@ -607,7 +613,7 @@ def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree
             _lib.check(_lib.lib().cdna_tree_predict(_ptr(X), n, d, X.stride(0), _ptr(nodes), int(nodes.shape[0]),
                                                     _ptr(roots),
                                                     _ptr(tree_w), T, _ptr(values), _ptr(m), K, _ptr(base), _ptr(out),
-                                                    _stream(X.device)), "cdna_tree_predict")
+                                                    int(values.numel()), _stream(X.device)), "cdna_tree_predict")
         return out
     Xf = X.float()
     out = torch.zeros((n, K), dtype=torch.float32)
@@ -854,6 +860,52 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
     out.copy_(iout)
     if not packed:
         out[..., 0] /= qs0
+    out[..., 1] /= qs1
+    return out
+
+
+def seg_hist_subset(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v1p: torch.Tensor,
+                    wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int, feats: np.ndarray,
+                    scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False) -> torch.Tensor:
+    """Packed segment histograms [S, d, B, 2] over each slot's sampled features only (others stay 0).
+
+    feats: [S, m] feature ids of slot s (RandomForest per-node feature subsets).
+    """
+    G, n, _ = bins.shape
+    feats = np.asarray(feats, dtype=np.int32).reshape(S, -1)
+    m = feats.shape[1]
+    if not _native(bins):
+        out = seg_hist(bins, d, B, perm, None, v1p, wp, segs, S, wmax, scales)
+        keep = torch.zeros((S, d), dtype=torch.bool)
+        if S:
+            keep[torch.arange(S)[:, None], torch.from_numpy(feats).long()] = True
+        return out * keep[:, :, None, None]
+    out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
+    segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
+    if S == 0 or len(segs) == 0:
+        return out
+    wm = int(max(1, min(255, wmax)))
+    chunk = min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1), ((1 << 24) - 1) // max(m, 1))  # pair index < 2^24
+    work = _seg_work(segs, chunk)
+    if len(work) == 0:
+        return out
+    if interleave and len(segs) > 1:
+        sg = segs[segs[:, 1] > 0]
+        k = (sg[:, 1] + chunk - 1) // chunk
+        j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
+        work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
+    qs1 = (scales if scales is not None else seg_scales(None, v1p, wm, n))[1]
+    if bins_rm is None:
+        bins_rm = bins_row_major(bins)
+    assert bins_rm.shape == (n, G, 8) and bins_rm.is_contiguous()
+    dev = bins.device
+    wt = torch.from_numpy(work.reshape(-1)).to(dev)
+    ft = torch.from_numpy(feats.reshape(-1)).to(dev)
+    iout = torch.zeros(out.shape, dtype=torch.int64, device=dev)
+    _lib.check(_lib.lib().cdna_seg_hist_subset(_ptr(bins_rm), n, G * 8, d, B, _ptr(perm), _ptr(v1p), _ptr(wp),
+                                               _ptr(wt), len(work), float(qs1), _ptr(ft), m, _ptr(iout),
+                                               _stream(dev)), "cdna_seg_hist_subset")
+    out.copy_(iout)
     out[..., 1] /= qs1
     return out
 

@@ -709,7 +709,7 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
                                                          const int* __restrict__ split_bin,
                                                          const int* __restrict__ cat_off,
                                                          const uint32_t* __restrict__ cat_mask,
-                                                         const int* __restrict__ child) {
+                                                         const int* __restrict__ child, int rm_row_bytes) {
   __shared__ int s_f[256], s_b[256], s_co[256], s_ch[512];
   const int t = blockIdx.y;
   const int tf = tfirst[t];
@@ -729,6 +729,11 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
   }
   __syncthreads();
   const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bins);
+  // rm_row_bytes > 0: bins is the row-major copy [n][G*8] (a row's bytes share 1-2 cache lines, so the
+  // up-to-255 different split features of a tree's rows do not each pull a line of their own group)
+  auto bidx = [&](int64_t r, int f) -> int64_t {
+    return rm_row_bytes > 0 ? r * rm_row_bytes + f : ((int64_t)(f >> 3) * n + r) * 8 + (f & 7);
+  };
   uint16_t* rec = codes + (int64_t)t * n;
   const int64_t n4 = n / 4;
   auto move = [&](int64_t r, uint32_t c) -> uint32_t {
@@ -737,7 +742,7 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
     const int f = s_f[loc];
     uint32_t nl = 0xFFu;
     if (f >= 0) {
-      const int bin = b8[((int64_t)(f >> 3) * n + r) * 8 + (f & 7)];
+      const int bin = b8[bidx(r, f)];
       const int co = s_co[loc];
       const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u : bin <= s_b[loc];
       nl = (uint32_t)s_ch[2 * loc + (left ? 0 : 1)];
@@ -767,7 +772,7 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
           const uint32_t loc = c & 0xFFu;
           const int f = loc == 0xFFu ? -1 : s_f[loc];
           const int64_t r = (q0 + u * stride) * 4 + k;
-          bins_[u][k] = f >= 0 ? (int)b8[((int64_t)(f >> 3) * n + r) * 8 + (f & 7)] : 0;
+          bins_[u][k] = f >= 0 ? (int)b8[bidx(r, f)] : 0;
         }
       }
 #pragma unroll
@@ -957,10 +962,10 @@ CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T,
 
 CDNA_API int cdna_partition5(const uint64_t* bins, int64_t n, int T, int A, uint16_t* codes, const int* tfirst,
                              const int* tfirst_next, const int* split_feat, const int* split_bin, const int* cat_off,
-                             const uint32_t* cat_mask, const int* child, hipStream_t st) {
+                             const uint32_t* cat_mask, const int* child, int rm_row_bytes, hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
   hipLaunchKernelGGL(partition5_kernel, dim3(grid_for(n / 4 + 1, 256, 1024), T), dim3(256), 0, st, bins, n, T, A,
                      codes, tfirst,
-                     tfirst_next, split_feat, split_bin, cat_off, cat_mask, child);
+                     tfirst_next, split_feat, split_bin, cat_off, cat_mask, child, rm_row_bytes);
   return (int)hipGetLastError();
 }

@@ -317,6 +317,71 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
   }
 }
 
+// Feature-subset variant (RandomForest featureSubsetStrategy): a node's split
+// only considers its m sampled features (ML 07 / Spark "onethird" = 34 of 100),
+// so only those are accumulated.  Lanes take consecutive (row, sampled feature)
+// PAIRS: one byte gather from the row-major bins and one packed atomic per
+// lane, every lane busy.  Both children of a split are built (no sibling
+// subtraction: the parent's histogram only holds the parent's features); at
+// m = 34 that is 2 x 34 = 68 atomics per parent row instead of 104 for the
+// smaller child alone, and 34 instead of 104 at the root.
+template <bool HAS_W>
+__global__ __launch_bounds__(1024) void seg_hist_subset_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins_rm,
+                                                               int row_bytes, const int* __restrict__ feats, int m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long h[];  // [m][B]
+  constexpr int TH = 1024;
+  int* s_f = reinterpret_cast<int*>(h + (size_t)m * a.B);
+  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
+  const int plane = m * a.B;
+  for (int i = threadIdx.x; i < plane; i += TH) h[i] = 0ull;
+  for (int i = threadIdx.x; i < m; i += TH) s_f[i] = feats[(int64_t)slot * m + i];
+  __syncthreads();
+  const uint32_t total = (uint32_t)len * (uint32_t)m;
+  const int mi = m;
+  const float inv_m = 1.0f / (float)m;
+  // 16 pairs in flight per lane: each pair is a dependent perm -> byte-gather chain, so a few pairs per
+  // trip left the waves waiting on memory (U = 4 ran 5x slower than the flat kernel)
+  constexpr int U = 16;
+  for (uint32_t q0 = threadIdx.x; q0 < total; q0 += TH * U) {
+    int cell[U];
+    unsigned long long add[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t q = q0 + u * TH;
+      const bool ok = q < total;
+      // q < 2^24 (host-bounded chunk x m): float quotient, one correction step
+      int i = (int)((float)q * inv_m);
+      int fi = (int)q - i * mi;
+      if (fi < 0) { --i; fi += mi; }
+      if (fi >= mi) { ++i; fi -= mi; }
+      if (!ok) { i = 0; fi = 0; }
+      const int row = ok ? a.perm[start + i] : 0;
+      const int f = s_f[fi];
+      const int bin = ok ? (int)bins_rm[(int64_t)row * row_bytes + f] : 0;
+      const uint32_t w = ok ? (HAS_W ? (uint32_t)a.wp[start + i] : 1u) : 0u;
+      int q1 = ok ? (int)rintf(a.v1p[start + i] * a.qs1) : 0;
+      q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+      add[u] = ((unsigned long long)w << kPackShift) + (unsigned long long)w * (unsigned long long)(q1 + kPackQ);
+      cell[u] = fi * a.B + bin;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (add[u]) atomicAdd(h + cell[u], add[u]);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < plane; c += TH) {
+    const int fi = c / a.B, bn = c - fi * a.B;
+    const unsigned long long v = h[c];
+    if (!v) continue;
+    const int f = s_f[fi];
+    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+    const unsigned long long cnt = v >> kPackShift;
+    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    atomicAdd(o, cnt);
+    atomicAdd(o + 1, (unsigned long long)sum);
+  }
+}
+
 struct SegPartArgs {
   const uint64_t* bins;
   int64_t n;
@@ -844,5 +909,26 @@ CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64
     case 16: go(codes_compact_w_kernel<16, false>, codes_compact_w_kernel<16, true>); break;
     default: return (int)hipErrorInvalidValue;
   }
+  return (int)hipGetLastError();
+}
+
+// Packed (count | sum) segment histograms over each slot's m sampled features only.
+// feats [S][m] (slot-major feature ids); bins_rm row-major [n][row_bytes]; out [S][d][B][2] zeroed.
+CDNA_API int cdna_seg_hist_subset(const uint8_t* bins_rm, int64_t n, int row_bytes, int d, int B, const int* perm,
+                                  const float* v1p, const uint8_t* wp, const int* work, int nwork, float qs1,
+                                  const int* feats, int m, unsigned long long* out, hipStream_t st) {
+  if (nwork <= 0) return 0;
+  if (m <= 0 || m > d) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)m * B * 8 + (size_t)m * 4;
+  if (lds > 128 * 1024) return (int)hipErrorInvalidValue;
+  SegHistArgs a{nullptr, n, d, B, perm, nullptr, v1p, wp, work, 1.f, qs1, out};
+  auto launch = [&](auto kern) {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), lds, st, a, bins_rm, row_bytes, feats, m);
+  };
+  if (wp) launch(seg_hist_subset_kernel<true>);
+  else launch(seg_hist_subset_kernel<false>);
   return (int)hipGetLastError();
 }

@@ -371,18 +371,34 @@ __global__ __launch_bounds__(256) void predict_kernel(const float* __restrict__ 
                                                       const float* __restrict__ tree_w, int T,
                                                       const float* __restrict__ values, const uint32_t* __restrict__ masks,
                                                       int K, const float* __restrict__ base, float* __restrict__ out,
-                                                      int n_nodes_lds) {
+                                                      int n_nodes_lds, int n_vals_lds) {
   // LDS: [n_nodes_lds] int4 forest (when it fits), then X tile [64][d+1], then [4][64][K] partials.
   // rocprofv3 on the global-node version: 78 % of wave time waiting on the
   // dependent node loads of each root-to-leaf walk; walking an LDS copy of the
   // forest turns each step into a ~100-cycle ds_read_b128.
   extern __shared__ __attribute__((aligned(16))) float sx_all[];
+  // n_vals_lds > 0: the leaf values, roots and tree weights are staged next to the forest (rocprofv3: with
+  // them in global memory every tree's walk ended in three dependent global loads, 70 % of wave time waiting)
   int4* snodes = reinterpret_cast<int4*>(sx_all);
-  float* sx = sx_all + (size_t)n_nodes_lds * 4;
+  float* svals = sx_all + (size_t)n_nodes_lds * 4;
+  const int nv_pad = n_vals_lds > 0 ? ((n_vals_lds + 3) & ~3) + ((2 * T + 3) & ~3) : 0;
+  int* sroots = reinterpret_cast<int*>(svals + ((n_vals_lds + 3) & ~3));
+  float* stw = reinterpret_cast<float*>(sroots + T);
+  float* sx = svals + nv_pad;
   const int dp = d + 1;
   float* part = sx + 64 * dp;
   const int4* nd_src = n_nodes_lds > 0 ? snodes : nodes;
   for (int i = threadIdx.x; i < n_nodes_lds; i += 256) snodes[i] = nodes[i];
+  if (n_vals_lds > 0) {
+    for (int i = threadIdx.x; i < n_vals_lds; i += 256) svals[i] = values[i];
+    for (int i = threadIdx.x; i < T; i += 256) {
+      sroots[i] = roots[i];
+      stw[i] = tree_w[i];
+    }
+    values = svals;
+    roots = sroots;
+    tree_w = stw;
+  }
   const int tl = threadIdx.x >> 6, row = threadIdx.x & 63;
   const bool vec = ldx == d && (d % 4) == 0;
   // register double buffer: the next tile's float4s are in flight while this
@@ -602,17 +618,20 @@ CDNA_API int cdna_partition(const uint64_t* bins, int64_t n, int T, int* node, c
 
 CDNA_API int cdna_tree_predict(const float* X, int64_t n, int d, int64_t ldx, const int4* nodes, int64_t n_nodes_total,
                                const int* roots, const float* tree_w, int T, const float* values,
-                               const uint32_t* masks, int K, const float* base, float* out, hipStream_t st) {
+                               const uint32_t* masks, int K, const float* base, float* out, int64_t n_values,
+                               hipStream_t st) {
   if (n <= 0) return 0;
   const size_t lds0 = ((size_t)64 * (d + 1) + (size_t)4 * 64 * K) * 4;
   if (lds0 > 160 * 1024) return (int)hipErrorInvalidValue;
   // forest copy in LDS when it fits next to the tile (<= 64 KB per block keeps 2 blocks / CU)
-  int n_nodes = 0;
+  int n_nodes = 0, n_vals = 0;
   const size_t room = lds0 < 64 * 1024 ? 64 * 1024 - lds0 : 0;
   n_nodes = n_nodes_total <= (int64_t)(room / 16) ? (int)n_nodes_total : 0;
-  const size_t lds = lds0 + (size_t)n_nodes * 16;
+  const size_t vbytes = (size_t)(((n_values + 3) & ~3) + ((2 * T + 3) & ~3)) * 4;
+  if (n_nodes > 0 && n_values > 0 && (size_t)n_nodes * 16 + vbytes <= room) n_vals = (int)n_values;
+  const size_t lds = lds0 + (size_t)n_nodes * 16 + (n_vals > 0 ? vbytes : 0);
   hipLaunchKernelGGL(predict_kernel, dim3(grid_for(n, 64, 8192)), dim3(256), lds, st, X, n, d, ldx, nodes, roots,
-                     tree_w, T, values, masks, K, base, out, n_nodes);
+                     tree_w, T, values, masks, K, base, out, n_nodes, n_vals);
   return (int)hipGetLastError();
 }
 

@@ -158,3 +158,31 @@ def test_random_split_partition_count_invariant(seed, frac):
     a = spark.range(0, 2000, numPartitions=1).randomSplit([frac, 1 - frac], seed=seed)[0]
     b = spark.range(0, 2000, numPartitions=6).randomSplit([frac, 1 - frac], seed=seed)[0]
     assert set(a.toPandas().id) == set(b.toPandas().id)
+
+
+def test_find_thresholds_vectorised_matches_host():
+    """The batched (device) split-candidate finder is bit-identical to the per-feature host finder
+    (Spark findSplits semantics: midpoints of distinct values, or of quantile cut points)."""
+    import torch
+    from cdnaml.models.tree.engine import find_thresholds, find_thresholds_t
+    rng = np.random.default_rng(0)
+    for trial in range(20):
+        s, d = int(rng.integers(1, 2000)), int(rng.integers(1, 10))
+        X = rng.normal(size=(s, d))
+        for f in range(d):
+            kind = rng.integers(0, 5)
+            if kind == 1:
+                X[:, f] = rng.integers(0, rng.integers(1, 60), s)
+            elif kind == 2:
+                X[rng.random(s) < 0.3, f] = np.nan
+            elif kind == 3:
+                X[:, f] = np.round(X[:, f], 1)
+            elif kind == 4:
+                X[:, f] = 1.0
+        cat = {f: int(np.nanmax(np.abs(X[:, f])) + 1) for f in range(d)
+               if rng.random() < 0.15 and not np.isnan(X[:, f]).any()}
+        for B in (2, 5, 40, 256):
+            a = find_thresholds(X, d, B, cat)
+            b = find_thresholds_t(torch.from_numpy(X), B, cat)
+            np.testing.assert_array_equal(a[1], b[1])
+            np.testing.assert_array_equal(a[0], b[0])
