@@ -743,15 +743,26 @@ class ForestTrainer:
                 sib = torch.tensor([active[a]["sib"] for a in derived], device=dev)
                 H[di] = prev_hist[par] - H[sib]
             tot = self._node_stats(H, None)
-            if depth == 0:
-                for a, e in enumerate(active):
-                    st = tot[a].cpu().numpy()
-                    e["stats"] = st
             masks_t = torch.from_numpy(masks_np.view(np.int32)).to(dev) if masks_np is not None else None
             gain, bf, bb, lst, rst, order, cat_feats, miss_right = self._best_splits(H, tot, masks_t)
-            mr_h = miss_right.cpu().numpy() if miss_right is not None else None
-            gain_h, bf_h, bb_h = gain.cpu().numpy(), bf.cpu().numpy(), bb.cpu().numpy()
-            lst_h, rst_h = lst.cpu().numpy(), rst.cpu().numpy()
+            # one device->host transfer for the whole level's decisions (ids < 2^53 are exact in f64)
+            kk = lst.shape[1]
+            cols = [gain[:, None], bf[:, None].double(), bb[:, None].double(), lst, rst]
+            if miss_right is not None:
+                cols.append(miss_right[:, None].double())
+            if depth == 0:
+                cols.append(tot)
+            host = torch.cat(cols, 1).cpu().numpy()
+            gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
+            lst_h, rst_h = host[:, 3:3 + kk], host[:, 3 + kk:3 + 2 * kk]
+            c0 = 3 + 2 * kk
+            mr_h = None
+            if miss_right is not None:
+                mr_h = host[:, c0] != 0
+                c0 += 1
+            if depth == 0:
+                for a, e in enumerate(active):
+                    e["stats"] = host[a, c0:c0 + tot.shape[1]].copy()
             order_h = order.cpu().numpy() if order is not None else None
             _split_span.__exit__(None, None, None)
             # ---- create forest nodes for the active set, decide splits
