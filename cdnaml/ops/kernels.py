@@ -1140,3 +1140,85 @@ def bins_row_major(bins: torch.Tensor) -> torch.Tensor:
     _lib.check(_lib.lib().cdna_bins_row_major(_ptr(bins), n, G, _ptr(out), _stream(bins.device)),
                "cdna_bins_row_major")
     return out
+
+
+# ------------------------------------------------------------ K20 / K16 (relational.hip)
+def _merge_moments(part: torch.Tensor) -> torch.Tensor:
+    """Chan merge of per-block moments [nb, d, 5] (count, mean, M2, min, max) -> [d, 5]."""
+    cnt, mean, m2 = part[..., 0], part[..., 1], part[..., 2]
+    N = cnt.sum(0)
+    w = torch.where(N > 0, cnt / N.clamp_min(1), torch.zeros_like(cnt))
+    mu = torch.where(cnt > 0, mean, torch.zeros_like(mean))
+    M = (w * mu).sum(0)
+    dev2 = torch.where(cnt > 0, cnt * (mu - M) ** 2, torch.zeros_like(mu))
+    M2 = torch.where(cnt > 0, m2, torch.zeros_like(m2)).sum(0) + dev2.sum(0)
+    has = cnt > 0
+    inf = torch.full_like(mean, float("inf"))
+    mn = torch.where(has, part[..., 3], inf).amin(0)
+    mxs = torch.where(has, part[..., 4], -inf)
+    mx = torch.where(torch.isnan(mxs).any(0), torch.full_like(M, float("nan")), mxs.amax(0))
+    nanmean = torch.isnan(torch.where(has, mean, torch.zeros_like(mean))).any(0)
+    M = torch.where(nanmean, torch.full_like(M, float("nan")), M)
+    return torch.stack([N, M, M2, mn, mx], 1)
+
+
+def col_moments(X: torch.Tensor, valid: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K20: per-column (count, mean, M2, min, max) of X [n, d] in fp64, skipping entries with valid == 0.
+
+    NaNs are values (mean NaN, max NaN, min ignores them) as in Spark's describe/summary."""
+    n, d = X.shape
+    if n == 0 or d == 0:
+        out = torch.zeros((d, 5), dtype=torch.float64, device=X.device)
+        out[:, 3], out[:, 4] = float("inf"), float("-inf")
+        return out
+    if _native(X):
+        Xc = X if X.dtype in (torch.float32, torch.float64) else X.double()
+        if Xc.stride(1) != 1:
+            Xc = Xc.contiguous()
+        v = None
+        if valid is not None:
+            v = valid.to(torch.uint8)
+            v = v if v.stride(1) == 1 else v.contiguous()
+        rpb = max(256, -(-n // 4096))
+        nb = -(-n // rpb)
+        part = torch.empty((nb, d, 5), dtype=torch.float64, device=X.device)
+        _lib.check(_lib.lib().cdna_col_moments(0 if Xc.dtype == torch.float32 else 1, _ptr(Xc), n, d, Xc.stride(0),
+                                               _ptr(v), 0 if v is None else v.stride(0), rpb, _ptr(part),
+                                               _stream(X.device)), "cdna_col_moments")
+        return _merge_moments(part)
+    x = X.double()
+    ok = torch.ones_like(x, dtype=torch.bool) if valid is None else valid.bool()
+    cnt = ok.sum(0).double()
+    xs = torch.where(ok, x, torch.zeros_like(x))
+    mean = xs.sum(0) / cnt.clamp_min(1)
+    m2 = torch.where(ok, (x - mean) ** 2, torch.zeros_like(x)).sum(0)
+    mn = torch.where(ok & ~torch.isnan(x), x, torch.full_like(x, float("inf"))).amin(0)
+    mx = torch.where(ok, x, torch.full_like(x, float("-inf")))
+    mx = torch.where((torch.isnan(mx)).any(0), torch.full_like(mean, float("nan")), mx.nan_to_num(float("-inf")).amax(0))
+    return torch.stack([cnt, mean, m2, mn, mx], 1)
+
+
+def partition_dest(dest: torch.Tensor, W: int):
+    """K16: stable counting sort of rows by destination bucket in [0, W).
+
+    Returns (perm int64 [n] = stable argsort of dest, counts [W] int64)."""
+    n = dest.numel()
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int64, device=dest.device), torch.zeros(W, dtype=torch.int64,
+                                                                                 device=dest.device)
+    if _native(dest) and W <= 8192:
+        d32 = dest.to(torch.int32).contiguous()
+        rpb = max(1024, -(-n // 2048))
+        nb = -(-n // rpb)
+        counts = torch.empty((W, nb), dtype=torch.int32, device=dest.device)
+        L = _lib.lib()
+        _lib.check(L.cdna_partition_dest(1, _ptr(d32), n, W, rpb, _ptr(counts), None, None, _stream(dest.device)),
+                   "cdna_partition_dest(count)")
+        flat = counts.reshape(-1).long()
+        offs = (torch.cumsum(flat, 0) - flat).contiguous()
+        perm = torch.empty(n, dtype=torch.int64, device=dest.device)
+        _lib.check(L.cdna_partition_dest(2, _ptr(d32), n, W, rpb, None, _ptr(offs), _ptr(perm),
+                                         _stream(dest.device)), "cdna_partition_dest(scatter)")
+        return perm, counts.long().sum(1)
+    perm = torch.argsort(dest.long(), stable=True)
+    return perm, torch.bincount(dest.long(), minlength=W)

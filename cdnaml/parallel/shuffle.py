@@ -40,8 +40,9 @@ def exchange(comm, batch: Batch, dest: torch.Tensor) -> Batch:
         return batch
     W = comm.world_size
     batch = unify_global_dictionaries(comm, batch)
-    order = torch.argsort(dest.long(), stable=True)
-    counts = torch.bincount(dest.long(), minlength=W).cpu().tolist()
+    from ..ops import kernels as K
+    order, counts = K.partition_dest(dest, W)  # K16 stable counting sort (HIP on the GPU)
+    counts = counts.cpu().tolist()
     sorted_b = batch.take(order)
     out_cols = {}
     recv_n = None

@@ -9,6 +9,8 @@ partitions resident in HBM (ML 00b:88-104).
 """
 from __future__ import annotations
 
+import math
+
 import itertools
 from typing import Callable, Dict, List, Optional, Sequence, Union
 
@@ -164,6 +166,33 @@ class DataFrameNaFunctions:
 class DataFrameStatFunctions:
     def __init__(self, df):
         self.df = df
+
+    def _column_moments(self, names) -> dict:
+        """{name: (count, mean, M2, min, max)} over all partitions of all ranks (K20 + Chan merge)."""
+        from ..ops import kernels as K
+        session = self._session
+        parts = self._plan.execute()
+        k = len(names)
+        locs = []
+        for b in parts:
+            if b.n == 0:
+                continue
+            cols = [b.columns[nm] for nm in names]
+            X = torch.stack([c.values.double() for c in cols], 1)
+            v = None
+            if any(c.valid is not None for c in cols):
+                v = torch.stack([c.valid_mask() for c in cols], 1)
+            locs.append(K.col_moments(X, v))
+        dev = session.device
+        if locs:
+            part = torch.stack(locs).to(dev)
+        else:
+            part = torch.zeros((1, k, 5), dtype=torch.float64, device=dev)
+            part[..., 3], part[..., 4] = float("inf"), float("-inf")
+        if session.comm.distributed:
+            part = torch.cat(session.comm.all_gather_varlen(part.contiguous()))
+        tot = K._merge_moments(part).cpu().numpy()
+        return {nm: tuple(float(x) for x in tot[i]) for i, nm in enumerate(names)}
 
     def approxQuantile(self, col, probabilities, relativeError):
         return self.df.approxQuantile(col, probabilities, relativeError)
@@ -906,12 +935,21 @@ class DataFrame:
         fields = [f for f in self.schema.fields
                   if (not flat or f.name in flat) and (f.dataType.is_numeric or isinstance(f.dataType, T.StringType))]
         rows = {s: [] for s in stats}
+        # count / mean / stddev / min / max of every numeric column: one K20 pass (col_moments) per local
+        # partition, per-rank partials merged with Chan's formula (one all-gather), instead of one
+        # aggregation job per column
+        moment_stats = {"count", "mean", "stddev", "min", "max"}
+        num_fields = [f for f in fields if f.dataType.is_numeric and not isinstance(f.dataType, T.BooleanType)]
+        mom = self._column_moments([f.name for f in num_fields]) if num_fields and \
+            any(s in moment_stats for s in stats) else {}
         for f in fields:
             c = F.col(f.name)
             is_str = isinstance(f.dataType, T.StringType)
             aggs = []
             for s in stats:
-                if s == "count":
+                if f.name in mom and s in moment_stats:
+                    aggs.append(None)
+                elif s == "count":
                     aggs.append(F.count(c))
                 elif s == "mean":
                     aggs.append(F.avg(c) if not is_str else None)
@@ -924,15 +962,57 @@ class DataFrame:
                 else:
                     raise ValueError(s)
             live = [(i, a) for i, a in enumerate(aggs) if a is not None]
-            got = self.agg(*[a.alias(f"_s{i}") for i, a in live]).collect()[0]
+            got = self.agg(*[a.alias(f"_s{i}") for i, a in live]).collect()[0] if live else []
             vals = [None] * len(aggs)
             for (i, _), v in zip(live, got):
                 vals[i] = v
+            if f.name in mom:
+                cnt, mean, m2, mn, mx = mom[f.name]
+                integral = isinstance(f.dataType, (T.IntegerType, T.LongType, T.ShortType, T.ByteType))
+                for i, s in enumerate(stats):
+                    if s == "count":
+                        vals[i] = int(cnt)
+                    elif cnt == 0:
+                        vals[i] = None
+                    elif s == "mean":
+                        vals[i] = mean
+                    elif s == "stddev":
+                        vals[i] = math.sqrt(m2 / (cnt - 1)) if cnt > 1 else float("nan")
+                    elif s in ("min", "max"):
+                        v = mn if s == "min" else mx
+                        vals[i] = int(v) if (integral and math.isfinite(v)) else v
             for s, v in zip(stats, vals):
                 rows[s].append(None if v is None else (str(int(v)) if s == "count" else _num_str(v)))
         pdf = pd.DataFrame({"summary": stats, **{f.name: [rows[s][i] for s in stats] for i, f in enumerate(fields)}})
         return self._session.createDataFrame(pdf, schema=T.StructType(
             [T.StructField("summary", T.StringType())] + [T.StructField(f.name, T.StringType()) for f in fields]))
+
+    def _column_moments(self, names) -> dict:
+        """{name: (count, mean, M2, min, max)} over all partitions of all ranks (K20 + Chan merge)."""
+        from ..ops import kernels as K
+        session = self._session
+        parts = self._plan.execute()
+        k = len(names)
+        locs = []
+        for b in parts:
+            if b.n == 0:
+                continue
+            cols = [b.columns[nm] for nm in names]
+            X = torch.stack([c.values.double() for c in cols], 1)
+            v = None
+            if any(c.valid is not None for c in cols):
+                v = torch.stack([c.valid_mask() for c in cols], 1)
+            locs.append(K.col_moments(X, v))
+        dev = session.device
+        if locs:
+            part = torch.stack(locs).to(dev)
+        else:
+            part = torch.zeros((1, k, 5), dtype=torch.float64, device=dev)
+            part[..., 3], part[..., 4] = float("inf"), float("-inf")
+        if session.comm.distributed:
+            part = torch.cat(session.comm.all_gather_varlen(part.contiguous()))
+        tot = K._merge_moments(part).cpu().numpy()
+        return {nm: tuple(float(x) for x in tot[i]) for i, nm in enumerate(names)}
 
     def approxQuantile(self, col, probabilities, relativeError):
         """Exact quantiles (relativeError = 0 semantics, which satisfies any bound)."""

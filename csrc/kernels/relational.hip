@@ -1,0 +1,172 @@
+// DataFrame-engine kernels (SURVEY §2.10 K16 hash_partition, K20 col_stats).
+//
+// K20 col_moments: count / mean / M2 / min / max of every column of a [n][d]
+// row-major matrix in ONE pass (describe(), summary(), StandardScaler,
+// Summarizer).  A block owns a row chunk and a group of <= 64 columns: lanes
+// are (row lane, column), so a wave reads 64 consecutive columns of a row —
+// coalesced for the row-major layout — and each lane runs Welford in fp64 over
+// its rows.  Lanes of the same column are merged in LDS with Chan's pairwise
+// formula; per-block partials [nblk][d][5] are merged on the device the same
+// way (cdnaml/ops/kernels.py col_moments), so the result does not depend on
+// the block schedule.  Null entries (valid == 0) are skipped, NaNs are values
+// (Spark: a NaN in a column makes its mean NaN).
+//
+// K16 partition_by_dest: stable counting sort of rows by destination rank /
+// bucket (the all-to-all shuffle of groupBy / join / dropDuplicates /
+// repartition, Spark "shuffle write").  Pass 1 counts each block's rows per
+// bucket in LDS; the host-side exclusive scan of [bucket][block] gives every
+// block its output offsets; pass 2 re-reads the block's rows and scatters
+// their indices in row order (wave ballots rank rows of equal bucket), so the
+// permutation equals a stable argsort of dest without a radix sort.
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+struct Moments {
+  double n, mean, m2, mn, mx;
+};
+
+__device__ __forceinline__ Moments merge(const Moments& a, const Moments& b) {
+  if (a.n == 0.0) return b;
+  if (b.n == 0.0) return a;
+  Moments r;
+  r.n = a.n + b.n;
+  const double delta = b.mean - a.mean;
+  r.mean = a.mean + delta * (b.n / r.n);
+  r.m2 = a.m2 + b.m2 + delta * delta * (a.n * b.n / r.n);
+  // Spark orders NaN above every value: min skips NaNs (fmin), max is NaN once any NaN was seen
+  r.mn = fmin(a.mn, b.mn);
+  r.mx = (a.mx != a.mx || b.mx != b.mx) ? __builtin_nan("") : fmax(a.mx, b.mx);
+  return r;
+}
+
+template <typename TV>
+__global__ __launch_bounds__(kThreads) void col_moments_kernel(const TV* __restrict__ X, int64_t n, int d,
+                                                               int64_t ldx, const uint8_t* __restrict__ valid,
+                                                               int64_t ldv, int64_t rows_per_block,
+                                                               double* __restrict__ part) {
+  __shared__ Moments sm[kThreads];
+  const int cg = d - (int)blockIdx.y * 64 < 64 ? d - (int)blockIdx.y * 64 : 64;  // columns in this group
+  const int rl = kThreads / cg;                                                   // row lanes
+  const int c = threadIdx.x % cg, lane_r = threadIdx.x / cg;
+  const int col = blockIdx.y * 64 + c;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+  Moments m{0.0, 0.0, 0.0, __builtin_inf(), -__builtin_inf()};
+  bool nan_seen = false;
+  if (lane_r < rl) {
+    for (int64_t r = r0 + lane_r; r < r1; r += rl) {
+      if (valid && !valid[r * ldv + col]) continue;
+      const double x = (double)X[r * ldx + col];
+      if (x != x) nan_seen = true;
+      m.n += 1.0;
+      const double delta = x - m.mean;
+      m.mean += delta / m.n;
+      m.m2 += delta * (x - m.mean);
+      m.mn = fmin(m.mn, x);
+      m.mx = fmax(m.mx, x);
+    }
+  }
+  if (nan_seen) m.mx = __builtin_nan("");
+  sm[threadIdx.x] = m;
+  __syncthreads();
+  if (lane_r == 0) {
+    Moments acc = sm[c];
+    for (int k = 1; k < rl; ++k) acc = merge(acc, sm[k * cg + c]);
+    double* o = part + ((int64_t)blockIdx.x * d + col) * 5;
+    o[0] = acc.n;
+    o[1] = acc.mean;
+    o[2] = acc.m2;
+    o[3] = acc.mn;
+    o[4] = acc.mx;
+  }
+}
+
+// dest values must lie in [0, W).  counts: [W][nblk] (bucket-major, so one
+// flat exclusive scan gives every (bucket, block) its output offset).
+template <bool SCATTER>
+__global__ __launch_bounds__(kThreads) void partition_dest_kernel(const int* __restrict__ dest, int64_t n, int W,
+                                                                  int64_t rows_per_block, int* __restrict__ counts,
+                                                                  const int64_t* __restrict__ offsets,
+                                                                  int64_t* __restrict__ perm) {
+  extern __shared__ int s_cnt[];  // [W] counts (pass 1) / cursors (pass 2)
+  const int nblk = gridDim.x;
+  for (int i = threadIdx.x; i < W; i += kThreads) s_cnt[i] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+  if (!SCATTER) {
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += kThreads) atomicAdd(&s_cnt[dest[r]], 1);
+    __syncthreads();
+    for (int i = threadIdx.x; i < W; i += kThreads) counts[(int64_t)i * nblk + blockIdx.x] = s_cnt[i];
+    return;
+  }
+  // stable: rounds of 256 rows in order; within a round, waves in order; within a wave, lanes in order
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t rb = r0; rb < r1; rb += kThreads) {
+    const int64_t r = rb + threadIdx.x;
+    const bool ok = r < r1;
+    const int b = ok ? dest[r] : -1;
+    // waves take turns so earlier waves' rows get lower positions
+    for (int w = 0; w < kThreads / 64; ++w) {
+      if (wid == w) {
+        bool want = ok;
+        while (true) {
+          const uint64_t act = __builtin_amdgcn_ballot_w64(want);
+          if (!act) break;
+          const int leader = __builtin_ctzll(act);
+          const int lb = __shfl(b, leader);
+          const uint64_t m = __builtin_amdgcn_ballot_w64(want && b == lb);
+          int base = 0;
+          if (lane == leader) {
+            base = s_cnt[lb];
+            s_cnt[lb] = base + __builtin_popcountll(m);
+          }
+          base = __shfl(base, leader);
+          if (want && b == lb) {
+            const int below =
+                (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            perm[offsets[(int64_t)lb * nblk + blockIdx.x] + base + below] = r;
+            want = false;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+}  // namespace
+
+// dtype: 0 = f32, 1 = f64.  part: [nblk][d][5] (count, mean, M2, min, max); nblk = ceil(n / rows_per_block).
+CDNA_API int cdna_col_moments(int dtype, const void* X, int64_t n, int d, int64_t ldx, const uint8_t* valid,
+                              int64_t ldv, int64_t rows_per_block, double* part, hipStream_t st) {
+  if (n <= 0 || d <= 0) return 0;
+  if (rows_per_block <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((n + rows_per_block - 1) / rows_per_block), (unsigned)((d + 63) / 64));
+  if (dtype == 0)
+    hipLaunchKernelGGL(col_moments_kernel<float>, grid, dim3(kThreads), 0, st, (const float*)X, n, d, ldx, valid,
+                       ldv, rows_per_block, part);
+  else
+    hipLaunchKernelGGL(col_moments_kernel<double>, grid, dim3(kThreads), 0, st, (const double*)X, n, d, ldx, valid,
+                       ldv, rows_per_block, part);
+  return (int)hipGetLastError();
+}
+
+// pass 1: counts [W][nblk]; pass 2: perm [n] from offsets [W][nblk] (exclusive scan of counts).
+CDNA_API int cdna_partition_dest(int pass, const int* dest, int64_t n, int W, int64_t rows_per_block, int* counts,
+                                 const int64_t* offsets, int64_t* perm, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (W <= 0 || W > 8192 || rows_per_block <= 0) return (int)hipErrorInvalidValue;
+  const unsigned nblk = (unsigned)((n + rows_per_block - 1) / rows_per_block);
+  const size_t lds = (size_t)W * 4;
+  if (pass == 1)
+    hipLaunchKernelGGL(partition_dest_kernel<false>, dim3(nblk), dim3(kThreads), lds, st, dest, n, W,
+                       rows_per_block, counts, offsets, perm);
+  else
+    hipLaunchKernelGGL(partition_dest_kernel<true>, dim3(nblk), dim3(kThreads), lds, st, dest, n, W, rows_per_block,
+                       counts, offsets, perm);
+  return (int)hipGetLastError();
+}

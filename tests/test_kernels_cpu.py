@@ -186,3 +186,16 @@ def test_find_thresholds_vectorised_matches_host():
             b = find_thresholds_t(torch.from_numpy(X), B, cat)
             np.testing.assert_array_equal(a[1], b[1])
             np.testing.assert_array_equal(a[0], b[0])
+
+
+def test_col_moments_reference_semantics():
+    """K20 reference path: Spark describe semantics (nulls skipped, NaN propagates to mean/max)."""
+    X = torch.tensor([[1.0, 2.0], [3.0, float("nan")], [5.0, 4.0]], dtype=torch.float64)
+    v = torch.tensor([[True, True], [True, True], [False, True]])
+    m = K.col_moments(X, v)
+    assert m[0, 0] == 2 and m[0, 1] == 2.0 and m[0, 2] == 2.0 and m[0, 3] == 1.0 and m[0, 4] == 3.0
+    assert m[1, 0] == 3 and torch.isnan(m[1, 1]) and m[1, 3] == 2.0 and torch.isnan(m[1, 4])
+    parts = torch.stack([K.col_moments(X[:2]), K.col_moments(X[2:])])
+    merged = K._merge_moments(parts)
+    full = K.col_moments(X)
+    assert torch.allclose(merged[0], full[0])

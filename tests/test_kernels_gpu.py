@@ -576,3 +576,29 @@ def test_codes_init_kernel(dev):
     ref, ref_max = K.codes_init_max(w, 5, 10007, "cpu")
     out, mx = K.codes_init_max(w.to(dev), 5, 10007, dev)
     assert torch.equal(ref, out.cpu()) and mx == ref_max == 200
+
+
+@pytest.mark.parametrize("dtype,d,with_valid", [(torch.float32, 100, False), (torch.float64, 3, True),
+                                                (torch.float64, 70, True)])
+def test_col_moments(dev, dtype, d, with_valid):
+    """K20 one-pass column moments vs the fp64 torch reference (nulls skipped, NaN max/mean)."""
+    g = torch.Generator().manual_seed(1)
+    n = 200003
+    X = (torch.randn(n, d, generator=g, dtype=torch.float64) * 3 + 1).to(dtype)
+    X[5, 0] = float("nan") if d == 3 else X[5, 0]
+    v = (torch.rand(n, d, generator=g) > 0.1) if with_valid else None
+    ref = K.col_moments(X, v)
+    out = K.col_moments(X.to(dev), None if v is None else v.to(dev)).cpu()
+    assert torch.equal(out[:, 0], ref[:, 0])
+    assert torch.allclose(out[:, 1:3], ref[:, 1:3], rtol=1e-9, atol=1e-9, equal_nan=True)
+    assert torch.equal(out[:, 3:], ref[:, 3:]) or torch.allclose(out[:, 3:], ref[:, 3:], equal_nan=True)
+
+
+@pytest.mark.parametrize("W", [2, 8, 37, 1000])
+def test_partition_dest(dev, W):
+    """K16 stable counting sort == stable argsort of the destination bucket."""
+    g = torch.Generator().manual_seed(W)
+    dest = torch.randint(0, W, (300001,), generator=g)
+    perm, counts = K.partition_dest(dest.to(dev), W)
+    assert torch.equal(perm.cpu(), torch.argsort(dest, stable=True))
+    assert torch.equal(counts.cpu(), torch.bincount(dest, minlength=W))
