@@ -91,6 +91,8 @@ _SIGS = {
     "cdna_codes_compact": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_bins_row_major": ([c_void_p, c_int64, c_int, c_void_p, c_void_p], c_int),
+    "cdna_partition6": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_col_moments": ([c_int, c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_void_p],
                          c_int),
     "cdna_partition_dest": ([c_int, c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],

@@ -512,6 +512,12 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
     return out
 
 
+# all trees per row chunk over an LDS copy of the chunk's bins (partition6) instead of one tree per grid row.
+# Opt-in: measured 7.8 ms per level at 1e8 x 20 trees at every depth, the same as partition5 (both move
+# 8 GB of row records plus the bins at ~2.4 TB/s), so the bins re-reads were not the bound
+PARTITION6 = __import__("os").environ.get("CDNAML_PARTITION6", "0") != "0"
+
+
 def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tensor, tfirst_next: torch.Tensor,
                     split_feat: torch.Tensor, split_bin: torch.Tensor, cat_off: torch.Tensor,
                     cat_mask: torch.Tensor, child: torch.Tensor, bins_rm: Optional[torch.Tensor] = None) -> None:
@@ -528,6 +534,11 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
         args = [t.to(device=bins.device, dtype=torch.int32).contiguous()
                 for t in (tfirst, tfirst_next, split_feat, split_bin, cat_off, child)]
         A = int(split_feat.numel())
+        if PARTITION6 and G <= 32 and A <= 1024 and T <= 64 and bins_rm is None:
+            _lib.check(_lib.lib().cdna_partition6(_ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]),
+                                                  _ptr(args[1]), _ptr(args[2]), _ptr(args[3]), _ptr(args[4]),
+                                                  _ptr(cm), _ptr(args[5]), _stream(bins.device)), "cdna_partition6")
+            return
         src, rm_bytes = bins, 0
         if bins_rm is not None:
             assert bins_rm.shape == (n, G, 8) and bins_rm.is_contiguous()

@@ -810,6 +810,80 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
   }
 }
 
+// Row-record partition, all trees per row chunk (partition6).  partition5 runs
+// one tree per grid.y and re-gathers, for every (row, tree), one byte from the
+// [G][n] bins: with up to 2^depth split features per tree, 20 trees re-read
+// the whole bins matrix from L2/HBM per level (5-10 ms at 1e8 x 100).  Here a
+// block stages its 256-row slice of ALL feature groups in LDS once (26 KB at
+// d = 100) and walks every tree over it: the bins cross HBM once per level,
+// and each tree's split table is staged in LDS per tree.
+constexpr int kP6Rows = 256;
+constexpr int kP6MaxA = 1024;  // active nodes of the level (all trees) staged in LDS
+constexpr int kP6MaxT = 64;
+__global__ __launch_bounds__(256) void partition6_kernel(const uint64_t* __restrict__ bins, int64_t n, int G, int T,
+                                                         int A, uint16_t* __restrict__ codes,
+                                                         const int* __restrict__ tfirst,
+                                                         const int* __restrict__ tfirst_next,
+                                                         const int* __restrict__ split_feat,
+                                                         const int* __restrict__ split_bin,
+                                                         const int* __restrict__ cat_off,
+                                                         const uint32_t* __restrict__ cat_mask,
+                                                         const int* __restrict__ child) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t tile[];  // [G][kP6Rows]
+  __shared__ int s_f[kP6MaxA], s_b[kP6MaxA], s_co[kP6MaxA];
+  __shared__ uint8_t s_ch[2 * kP6MaxA];
+  __shared__ int s_tf[kP6MaxT];
+  const int64_t r0 = (int64_t)blockIdx.x * kP6Rows;
+  const int rows = n - r0 < kP6Rows ? (int)(n - r0) : kP6Rows;
+  for (int i = threadIdx.x; i < G * kP6Rows; i += 256) {
+    const int g = i / kP6Rows, r = i - g * kP6Rows;
+    tile[i] = r < rows ? bins[(int64_t)g * n + r0 + r] : 0ull;
+  }
+  for (int i = threadIdx.x; i < T; i += 256) s_tf[i] = tfirst[i];
+  for (int i = threadIdx.x; i < A; i += 256) {
+    s_f[i] = split_feat[i];
+    s_b[i] = split_bin[i];
+    s_co[i] = cat_off[i];
+    // the tree of active node i: largest t with tfirst[t] <= i (tfirst is non-decreasing)
+    int lo = 0, hi = T - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tfirst[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const int tfn = tfirst_next[lo];
+    const int c0 = child[i * 2], c1 = child[i * 2 + 1];
+    s_ch[2 * i] = (uint8_t)(c0 >= 0 ? c0 - tfn : 0xFF);
+    s_ch[2 * i + 1] = (uint8_t)(c1 >= 0 ? c1 - tfn : 0xFF);
+  }
+  __syncthreads();
+  const uint8_t* tb = reinterpret_cast<const uint8_t*>(tile);
+  const int r = threadIdx.x;
+  if (r >= rows) return;
+  uint16_t* rec = codes + r0 + r;
+  // 8 trees' records in flight per thread, then their moves (one dependent load per tree was latency-bound)
+  constexpr int TB = 8;
+  for (int t0 = 0; t0 < T; t0 += TB) {
+    uint32_t c[TB];
+#pragma unroll
+    for (int u = 0; u < TB; ++u) c[u] = t0 + u < T ? (uint32_t)rec[(int64_t)(t0 + u) * n] : 0xFFu;
+#pragma unroll
+    for (int u = 0; u < TB; ++u) {
+      const uint32_t loc = c[u] & 0xFFu;
+      if (loc == 0xFFu) continue;
+      const int id = s_tf[t0 + u] + (int)loc;
+      const int f = s_f[id];
+      uint32_t nl = 0xFFu;
+      if (f >= 0) {
+        const int bin = tb[((f >> 3) * kP6Rows + r) * 8 + (f & 7)];
+        const int co = s_co[id];
+        const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u : bin <= s_b[id];
+        nl = s_ch[2 * id + (left ? 0 : 1)];
+      }
+      rec[(int64_t)(t0 + u) * n] = (uint16_t)((c[u] & 0xFF00u) | nl);
+    }
+  }
+}
+
 inline unsigned grid_for(int64_t n, int per, unsigned cap) {
   int64_t b = (n + per - 1) / per;
   return (unsigned)(b < (int64_t)cap ? (b < 1 ? 1 : b) : cap);
@@ -957,6 +1031,21 @@ CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T,
     if (masked) launch5<0, true, false>(a, ntm, nblk, lds, st);
     else launch5<0, false, false>(a, ntm, nblk, lds, st);
   }
+  return (int)hipGetLastError();
+}
+
+// all trees per 256-row chunk with the chunk's bins in LDS (G * 2 KB; G <= 32, A <= 1024, T <= 64)
+CDNA_API int cdna_partition6(const uint64_t* bins, int64_t n, int G, int T, int A, uint16_t* codes,
+                             const int* tfirst, const int* tfirst_next, const int* split_feat, const int* split_bin,
+                             const int* cat_off, const uint32_t* cat_mask, const int* child, hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  if (G <= 0 || G > 32 || A > kP6MaxA || T > kP6MaxT) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)G * kP6Rows * 8;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(partition6_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(partition6_kernel, dim3((unsigned)((n + kP6Rows - 1) / kP6Rows)), dim3(256), lds, st, bins, n,
+                     G, T, A, codes, tfirst, tfirst_next, split_feat, split_bin, cat_off, cat_mask, child);
   return (int)hipGetLastError();
 }
 

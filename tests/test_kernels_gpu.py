@@ -349,8 +349,10 @@ def test_hist_codes(dev, kind, monkeypatch):
     assert torch.allclose(out, ref, rtol=1e-6, atol=1e-3)
 
 
-def test_partition_codes(dev):
-    n, d, T, per = 20000, 12, 6, 4
+@pytest.mark.parametrize("p6,n", [(True, 20000), (False, 20000), (True, 20001)])
+def test_partition_codes(dev, monkeypatch, p6, n):
+    monkeypatch.setattr(K, "PARTITION6", p6)
+    d, T, per = 12, 6, 4
     g = torch.Generator().manual_seed(5)
     X = torch.randn(n, d, generator=g)
     X[:, 3] = torch.randint(0, 20, (n,), generator=g).float()
