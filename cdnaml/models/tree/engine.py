@@ -44,6 +44,8 @@ USE_SEG = __import__("os").environ.get("CDNAML_TREE_SEG", "1") != "0"
 # multi-tree regression forests: level 0 on row records, then rows grouped by (tree, node) segments
 USE_MSEG = __import__("os").environ.get("CDNAML_TREE_MSEG", "1") != "0"
 MSEG_L0 = __import__("os").environ.get("CDNAML_MSEG_L0", "1") != "0"  # level 0 through segments too
+# single-output forests of depth <= 8 predict from a heap layout (8-byte nodes, fixed-step walks)
+HEAP_PREDICT = __import__("os").environ.get("CDNAML_HEAP_PREDICT", "1") != "0"
 # feature-subset forests: accumulate only each node's sampled features in segment mode.  Opt-in: measured
 # 5-8x slower (profiles/pmc_seg_hist_subset.txt): both children must be built, and every row gather of the
 # row-major bins (one or two 64 B lines) then feeds 34 atomics instead of 104
@@ -328,9 +330,50 @@ class Forest:
         self._dev[key] = out
         return out
 
+    def heap_arrays(self, device, values_kind: str = "value"):
+        """Single-output forests of depth <= 8: heap layout [T, 2^(D+1)-1, 2] int32 (children of slot i at
+        2i+1 / 2i+2; {feature | -1 leaf | -(f+2) categorical, threshold / leaf value / mask-offset bits})
+        plus the categorical masks, or None."""
+        key = ("heap", str(device), values_kind)
+        if key in self._dev:
+            return self._dev[key]
+        res = None
+        D = max((self.tree_depth(t) for t in range(len(self.roots))), default=0)
+        if self.K == 1 and self.roots and D <= 8:
+            S = 2 ** (D + 1) - 1
+            heap = np.zeros((len(self.roots), S, 2), dtype=np.int32)
+            heap[:, :, 0] = -1
+            masks = []
+            for t, r in enumerate(self.roots):
+                stack = [(r, 0)]
+                while stack:
+                    i, h = stack.pop()
+                    if self.feat[i] < 0:
+                        v = self.value[i][0] if values_kind == "value" else self.value[i][0] * self.weight[i]
+                        heap[t, h] = (-1, np.array([v], dtype=np.float32).view(np.int32)[0])
+                        continue
+                    if self.is_cat[i]:
+                        heap[t, h] = (-(self.feat[i] + 2), len(masks))
+                        masks.append(self.catmask[i].view(np.int32))
+                    else:
+                        heap[t, h] = (self.feat[i], np.array([self.thr[i]], dtype=np.float32).view(np.int32)[0])
+                    stack.append((self.left[i], 2 * h + 1))
+                    stack.append((self.right[i], 2 * h + 2))
+            res = (torch.from_numpy(heap).to(device), D,
+                   torch.from_numpy(np.concatenate(masks) if masks else np.zeros(8, np.int32)).to(device))
+        self._dev[key] = res
+        return res
+
     def predict(self, X: torch.Tensor, tree_w: np.ndarray, base=None, values_kind="value") -> torch.Tensor:
-        nodes, roots, vals, masks = self.device_arrays(X.device, values_kind)
         tw = torch.tensor(np.asarray(tree_w, np.float32), device=X.device)
+        if self.K == 1 and X.device.type == "cuda" and HEAP_PREDICT:
+            ha = self.heap_arrays(X.device, values_kind)
+            if ha is not None:
+                b0 = 0.0 if base is None else float(np.asarray(base, np.float64).reshape(-1)[0])
+                out = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], b0)
+                if out is not None:
+                    return out
+        nodes, roots, vals, masks = self.device_arrays(X.device, values_kind)
         b = None if base is None else torch.tensor(np.asarray(base, np.float32).reshape(-1), device=X.device)
         return K.tree_predict(X, nodes, roots, tw, vals, masks, self.K, b)
 

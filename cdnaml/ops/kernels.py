@@ -603,6 +603,30 @@ def partition(bins: torch.Tensor, node: torch.Tensor, split_feat: torch.Tensor, 
 
 
 # --------------------------------------------------------------------- K8
+def tree_predict_heap(X: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: torch.Tensor,
+                      masks: torch.Tensor, base: float = 0.0) -> Optional[torch.Tensor]:
+    """Single-output ensemble prediction over a heap-laid-out forest (int32 [T, S, 2], S = 2^(depth+1)-1).
+
+    Returns None when the forest does not fit the kernel's LDS budget (use ``tree_predict``)."""
+    n, d = X.shape
+    T, S, _ = heap.shape
+    if not _native(X):
+        return None
+    X = X.float()
+    X = X if X.stride(1) == 1 else X.contiguous()
+    out = torch.empty((n, 1), dtype=torch.float32, device=X.device)
+    if n == 0:
+        return out
+    m = masks.int().contiguous() if masks.numel() else torch.zeros(8, dtype=torch.int32, device=X.device)
+    rc = _lib.lib().cdna_tree_predict_heap(_ptr(X), n, d, X.stride(0), _ptr(heap), S, depth,
+                                           _ptr(tree_w.float().contiguous()), T, _ptr(m), float(base), _ptr(out),
+                                           _stream(X.device))
+    if rc == 1:  # hipErrorInvalidValue: over the LDS budget
+        return None
+    _lib.check(rc, "cdna_tree_predict_heap")
+    return out
+
+
 def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree_w: torch.Tensor,
                  values: torch.Tensor, masks: torch.Tensor, K: int, base: Optional[torch.Tensor] = None
                  ) -> torch.Tensor:

@@ -509,6 +509,107 @@ __global__ __launch_bounds__(256) void predict_kernel(const float* __restrict__ 
   }
 }
 
+// K8 on a heap-laid-out forest (single output, every tree depth <= 8): node i
+// of a tree has children 2i+1 / 2i+2, so a node is 8 bytes {feature | -1 leaf
+// | -(f+2) categorical, threshold / leaf value / mask offset} and a walk is
+// exactly `depth` steps with no child loads or termination test (leaves stay
+// put).  The forest is ~2x smaller in LDS than the int4 form (20 trees of
+// depth 5: 10 KB), so 4 blocks fit a CU instead of 3; the walk is
+// branch-uniform.  Same semantics as predict_kernel: left iff x <= thr (NaN
+// goes right), categorical left iff the category's mask bit is set.
+__global__ __launch_bounds__(256) void predict_heap_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                           const int2* __restrict__ heap, int S, int depth,
+                                                           const float* __restrict__ tree_w, int T,
+                                                           const uint32_t* __restrict__ masks, float base,
+                                                           float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  int2* sheap = reinterpret_cast<int2*>(sm);
+  float* stw = sm + (size_t)T * S * 2;
+  float* sx = stw + ((T + 3) & ~3);
+  const int dp = d + 1;
+  float* part = sx + 64 * dp;
+  for (int i = threadIdx.x; i < T * S; i += 256) sheap[i] = heap[i];
+  for (int i = threadIdx.x; i < T; i += 256) stw[i] = tree_w[i];
+  const int tl = threadIdx.x >> 6, row = threadIdx.x & 63;
+  const bool vec = ldx == d && (d % 4) == 0;
+  constexpr int kPre = 8;
+  float4 pre[kPre];
+  const int64_t stride = (int64_t)gridDim.x * 64;
+  const bool use_pre = vec && 64 * d / 4 <= kPre * 256;
+  auto fetch = [&](int64_t r0) {
+    if (r0 >= n) return;
+    const int rows = (int)((n - r0) < 64 ? (n - r0) : 64);
+    const float4* src = reinterpret_cast<const float4*>(X + r0 * ldx);
+    const int nv = rows * d / 4;
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int i = threadIdx.x + k * 256;
+      if (i < nv) pre[k] = src[i];
+    }
+  };
+  if (use_pre) fetch((int64_t)blockIdx.x * 64);
+  for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < n; r0 += stride) {
+    const int rows = (int)((n - r0) < 64 ? (n - r0) : 64);
+    __syncthreads();
+    if (use_pre) {
+      const int nv = rows * d / 4;
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < nv) {
+          const int e = i * 4, r = e / d, f = e - r * d;
+          float* dst = sx + r * dp + f;
+          dst[0] = pre[k].x;
+          dst[1] = pre[k].y;
+          dst[2] = pre[k].z;
+          dst[3] = pre[k].w;
+        }
+      }
+    } else {
+      for (int e = threadIdx.x; e < rows * d; e += 256) {
+        const int r = e / d, f = e - r * d;
+        sx[r * dp + f] = X[(r0 + r) * ldx + f];
+      }
+    }
+    __syncthreads();
+    if (use_pre) fetch(r0 + stride);
+    float acc = 0.f;
+    if (row < rows) {
+      const float* xr = sx + row * dp;
+      constexpr int W = 8;
+      for (int tb = tl; tb < T; tb += 4 * W) {
+        int idx[W];
+#pragma unroll
+        for (int u = 0; u < W; ++u) idx[u] = 0;
+        for (int s = 0; s < depth; ++s) {
+#pragma unroll
+          for (int u = 0; u < W; ++u) {
+            const int t = tb + 4 * u;
+            if (t >= T) continue;
+            const int2 nd = sheap[t * S + idx[u]];
+            if (nd.x >= 0) {
+              idx[u] = 2 * idx[u] + (xr[nd.x] <= __int_as_float(nd.y) ? 1 : 2);
+            } else if (nd.x < -1) {
+              const int c = (int)xr[-nd.x - 2];
+              const bool left = (c >= 0 && c < 256) ? ((masks[nd.y * 8 + (c >> 5)] >> (c & 31)) & 1u) : false;
+              idx[u] = 2 * idx[u] + (left ? 1 : 2);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+          const int t = tb + 4 * u;
+          if (t < T) acc += stw[t] * __int_as_float(sheap[t * S + idx[u]].y);
+        }
+      }
+    }
+    part[tl * 64 + row] = acc;
+    __syncthreads();
+    if (threadIdx.x < rows) out[r0 + threadIdx.x] = base + part[threadIdx.x] + part[64 + threadIdx.x] +
+                                                    part[128 + threadIdx.x] + part[192 + threadIdx.x];
+  }
+}
+
 // Leaf lookup on binned data (for GBDT training-set margin updates):
 // out[r] += scale * value(leaf(r)) for a single tree in the compact
 // level-array form used during training (split on bins).
@@ -641,5 +742,18 @@ CDNA_API int cdna_predict_binned_add(const uint64_t* bins, int64_t n, const int4
   if (n <= 0) return 0;
   hipLaunchKernelGGL(predict_binned_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, bins, n, nodes, root,
                      values, masks, scale, out);
+  return (int)hipGetLastError();
+}
+
+// heap forest [T][S] int2 (S = 2^(depth+1) - 1), single output; returns hipErrorInvalidValue when it
+// does not fit the LDS budget (the caller then uses cdna_tree_predict).
+CDNA_API int cdna_tree_predict_heap(const float* X, int64_t n, int d, int64_t ldx, const int2* heap, int S, int depth,
+                                    const float* tree_w, int T, const uint32_t* masks, float base, float* out,
+                                    hipStream_t st) {
+  if (n <= 0) return 0;
+  const size_t lds = (size_t)T * S * 8 + (size_t)((T + 3) & ~3) * 4 + ((size_t)64 * (d + 1) + 256) * 4;
+  if (lds > 64 * 1024 || depth < 0 || depth > 12) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(predict_heap_kernel, dim3(grid_for(n, 64, 8192)), dim3(256), lds, st, X, n, d, ldx, heap, S,
+                     depth, tree_w, T, masks, base, out);
   return (int)hipGetLastError();
 }

@@ -604,3 +604,27 @@ def test_partition_dest(dev, W):
     perm, counts = K.partition_dest(dest.to(dev), W)
     assert torch.equal(perm.cpu(), torch.argsort(dest, stable=True))
     assert torch.equal(counts.cpu(), torch.bincount(dest, minlength=W))
+
+
+def test_heap_predict_matches_node_predict(dev, monkeypatch):
+    """K8 heap-layout walk == int4-node walk (categorical splits, NaN features, GBT weighted leaves)."""
+    import cdnaml
+    from cdnaml.models.tree import engine as E
+    from cdnaml.ml.regression import RandomForestRegressor, GBTRegressor
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator(device=dev).manual_seed(3)
+    X = torch.randn((50000, 12), generator=g, device=dev)
+    X[:, 4] = torch.randint(0, 9, (50000,), generator=g, device=dev).float()
+    y = (X[:, 0] * 2 + torch.sin(X[:, 1] * 3) + (X[:, 4] == 3).float() * 2).double()
+    df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
+    Xq = X.clone()
+    Xq[::97, 0] = float("nan")
+    for est in (RandomForestRegressor(numTrees=7, maxDepth=6, seed=1), GBTRegressor(maxIter=5, maxDepth=4)):
+        m = est.fit(df)
+        f = m._forest
+        tw = m._tree_w if hasattr(m, "_tree_w") and len(m._tree_w) else np.full(len(f.roots), 1.0 / len(f.roots))
+        outs = []
+        for heap in (True, False):
+            monkeypatch.setattr(E, "HEAP_PREDICT", heap)
+            outs.append(f.predict(Xq, tw).cpu())
+        assert torch.allclose(outs[0], outs[1], rtol=1e-6, atol=1e-5)
