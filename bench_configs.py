@@ -160,9 +160,12 @@ def bench_infer(spark, args):
     tw_d = torch.tensor(np.asarray(tw, np.float32), device=dev)
     masks = masks.int().contiguous() if masks.numel() else torch.zeros(8, dtype=torch.int32, device=dev)
 
+    heap = forest.heap_arrays(dev, "value") if dev.type == "cuda" else None
+
     def run_chunk(j):
         # device-resident forest arrays, no host->device traffic: capturable in a HIP graph
-        outs[j] = K.tree_predict(bufs[j], nodes, roots, tw_d, vals, masks, forest.K, None)
+        out = K.tree_predict_heap(bufs[j], heap[0], heap[1], tw_d, heap[2]) if heap is not None else None
+        outs[j] = out if out is not None else K.tree_predict(bufs[j], nodes, roots, tw_d, vals, masks, forest.K, None)
     graphs = None
     if dev.type == "cuda" and not args.no_graph:
         s = torch.cuda.Stream()

@@ -568,10 +568,30 @@ def _train_forest_regression(est, dataset, num_trees, subset, bootstrap, rate, i
     return forest, data.d
 
 
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev):
+    s = _SIDE_STREAMS.get(dev.index)
+    if s is None:
+        s = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
 def _bag_weights(data, T_, bootstrap, rate, seed):
     n = data.n_local
     dev = data.bins.device
     if bootstrap and T_ > 1:
+        if dev.type == "cuda":
+            # compute-bound Philox draws on a side stream, overlapping the memory-bound binning kernel that
+            # make_binned has just queued on the current stream (the draws depend on nothing queued there)
+            main = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            with torch.cuda.stream(side):
+                wts = K.poisson_weights(T_, n, seed, data.row_offset, rate, device=dev)
+            main.wait_stream(side)
+            wts.record_stream(main)
+            return wts
         return K.poisson_weights(T_, n, seed, data.row_offset, rate, device=dev)
     if rate < 1.0:
         u = torch.stack([K.uniform(n, seed, data.row_offset, 0x200 + t, device=dev) for t in range(T_)])

@@ -252,17 +252,20 @@ __global__ __launch_bounds__(1024) void seg_hist_rm_kernel(const SegHistArgs a, 
 // wave issues exactly 8 atomic instructions per pair round.
 template <bool HAS_W>
 __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a, const uint64_t* __restrict__ bins_rm,
-                                                             int G) {
+                                                             int G, int ngb) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long h[];
   constexpr int TH = 1024;
   const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
+  // block y covers groups [g0, g0 + ng) (all of them when they fit 128 KB of LDS; B = 256 needs 2 blocks)
+  const int g0 = blockIdx.y * ngb;
+  const int ng = G - g0 < ngb ? G - g0 : ngb;
   const int plane_g = 8 * a.B;
-  const int plane = G * plane_g;
+  const int plane = ng * plane_g;
   for (int i = threadIdx.x; i < plane; i += TH) h[i] = 0ull;
   const int rot = threadIdx.x & 7;
   __syncthreads();
-  const uint32_t total = (uint32_t)len * (uint32_t)G;
-  const uint32_t Gu = (uint32_t)G;
+  const uint32_t total = (uint32_t)len * (uint32_t)ng;
+  const uint32_t Gu = (uint32_t)ng;
   constexpr int U = 2;
   for (uint32_t q0 = threadIdx.x; q0 < total; q0 += TH * U) {
     uint64_t b8[U];
@@ -274,17 +277,17 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
       const uint32_t q = q0 + u * TH;
       const bool ok = q < total;
       const uint32_t i = ok ? q / Gu : 0u;
-      const int g = ok ? (int)(q - i * Gu) : 0;
+      const int g = ok ? (int)(q - i * Gu) : 0;  // group within the block's range
       g_[u] = g;
       const int row = ok ? a.perm[start + i] : 0;
-      b8[u] = ok ? bins_rm[(int64_t)row * G + g] : 0ull;
+      b8[u] = ok ? bins_rm[(int64_t)row * G + g0 + g] : 0ull;
       x1[u] = ok ? a.v1p[start + i] : 0.f;
       w[u] = ok ? (HAS_W ? (uint32_t)a.wp[start + i] : 1u) : 0u;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int g = g_[u];
-      const int valid_f = a.d - g * 8;
+      const int valid_f = a.d - (g0 + g) * 8;
       const uint32_t fvalid = w[u] == 0u ? 0u : (valid_f >= 8 ? 0xFFu : ((1u << (valid_f > 0 ? valid_f : 0)) - 1u));
       const uint32_t frot = ((fvalid >> rot) | (fvalid << (8 - rot))) & 0xFFu;
       const uint32_t lo = (uint32_t)b8[u], hi = (uint32_t)(b8[u] >> 32);
@@ -305,7 +308,7 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
   for (int c = threadIdx.x; c < plane; c += TH) {
     const int gq = c / plane_g, rem = c - gq * plane_g;
     const int jj = rem / a.B, bn = rem - jj * a.B;
-    const int f = gq * 8 + jj;
+    const int f = (g0 + gq) * 8 + jj;
     if (f >= a.d) continue;
     const unsigned long long v = h[c];
     if (!v) continue;
@@ -794,15 +797,19 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
   if (nwork <= 0) return 0;
   SegHistArgs a{bins, n, d, B, perm, v0p, v1p, wp, work, qs0, qs1, out};
   const bool packed = (mode & 1) != 0, has_w = (mode & 2) != 0;
-  if ((mode & 4) && packed && (size_t)((d + 7) / 8) * 8 * B * 8 <= 128 * 1024 && !(mode & 8)) {
-    // all groups of a row in one block, lanes over (row, group) pairs
+  if ((mode & 4) && packed && (size_t)8 * B * 8 <= 128 * 1024 && !(mode & 8)) {
+    // lanes over (row, group) pairs; the groups are split over as few blocks as fit 128 KB of LDS
     const int G = (d + 7) / 8;
-    const size_t lds = (size_t)G * 8 * B * 8;
+    int ngb = (128 * 1024) / (8 * B * 8);
+    if (ngb > G) ngb = G;
+    const int nblk_g = (G + ngb - 1) / ngb;
+    ngb = (G + nblk_g - 1) / nblk_g;  // balance
+    const size_t lds = (size_t)ngb * 8 * B * 8;
     auto launch = [&](auto kern) {
       if (lds > 64 * 1024)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
-      hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), lds, st, a, bins, G);
+      hipLaunchKernelGGL(kern, dim3((unsigned)nwork, (unsigned)nblk_g), dim3(1024), lds, st, a, bins, G, ngb);
     };
     if (has_w) launch(seg_hist_flat_kernel<true>);
     else launch(seg_hist_flat_kernel<false>);
