@@ -44,6 +44,8 @@ USE_SEG = __import__("os").environ.get("CDNAML_TREE_SEG", "1") != "0"
 # multi-tree regression forests: level 0 on row records, then rows grouped by (tree, node) segments
 USE_MSEG = __import__("os").environ.get("CDNAML_TREE_MSEG", "1") != "0"
 MSEG_L0 = __import__("os").environ.get("CDNAML_MSEG_L0", "1") != "0"  # level 0 through segments too
+# segment-mode forests carry one packed 8-byte record per gathered row (row | weight | quantised label)
+MSEG_REC = __import__("os").environ.get("CDNAML_MSEG_REC", "1") != "0"
 # single-output forests of depth <= 8 predict from a heap layout (8-byte nodes, fixed-step walks)
 HEAP_PREDICT = __import__("os").environ.get("CDNAML_HEAP_PREDICT", "1") != "0"
 # feature-subset forests: accumulate only each node's sampled features in segment mode.  Opt-in: measured
@@ -739,8 +741,12 @@ class ForestTrainer:
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
                 if use_mseg and (depth >= 1 or MSEG_L0):
                     # gather the rows of the built nodes into slot segments, then segment histograms
+                    rec_ok = (MSEG_REC and dev.type == "cuda" and stats_rows.get("v0") is None and
+                              not subset_seg and 8 * B * 8 <= 128 * 1024)
                     perm, v0p, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, len(build_ids),
-                                                             stats_rows.get("v0"), stats_rows["v1"])
+                                                             stats_rows.get("v0"), stats_rows["v1"],
+                                                             rec_scale=mseg_scales[1] if rec_ok else None)
+                    is_rec = rec_ok and v1p is None
                     sb = np.concatenate([sg, np.arange(len(build_ids), dtype=np.int64)[:, None]], 1)
                     if subset_seg:
                         feats = _mask_feature_lists(masks_np[build_ids], d)
@@ -751,7 +757,7 @@ class ForestTrainer:
                     else:
                         Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax,
                                         mseg_scales, bins_rm=data.row_major_bins() if dev.type == "cuda" else None,
-                                        interleave=True)
+                                        interleave=True, rec=is_rec)
                     del perm, v0p, v1p, wp
                 elif use_seg:
                     sb = np.array([[segs[a, 0], segs[a, 1], slot_of[a]] for a in build_ids], dtype=np.int64)

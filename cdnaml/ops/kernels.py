@@ -842,7 +842,49 @@ def _seg_work(segs: np.ndarray, chunk: int) -> np.ndarray:
 
 def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
              v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
-             scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False) -> torch.Tensor:
+             scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False,
+             rec: bool = False) -> torch.Tensor:
+    """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
+
+    rec: ``perm`` holds packed int64 item records from ``codes_compact(rec_scale=scales[1])`` (v1p/wp unused;
+    GPU with ``bins_rm`` only)."""
+    if rec:
+        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave)
+    return _seg_hist(bins, d, B, perm, v0p, v1p, wp, segs, S, wmax, scales, bins_rm, interleave)
+
+
+def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave):
+    G, n, _ = bins.shape
+    out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
+    segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
+    if S == 0 or len(segs) == 0:
+        return out
+    assert _native(bins) and bins_rm is not None and rec.dtype == torch.int64
+    wm = int(max(1, min(255, wmax)))
+    chunk = min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1))
+    work = _seg_work(segs, chunk)
+    if len(work) == 0:
+        return out
+    if interleave and len(segs) > 1:
+        sg = segs[segs[:, 1] > 0]
+        k = (sg[:, 1] + chunk - 1) // chunk
+        j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
+        work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
+    qs1 = float(scales[1])
+    wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
+    iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
+    assert bins_rm.shape == (n, G, 8) and bins_rm.is_contiguous()
+    _lib.check(_lib.lib().cdna_seg_hist(1 | 4 | 16, _ptr(bins_rm), n, d, B, _ptr(rec), None, None, None,
+                                        _ptr(wt), len(work), 1.0, qs1, _ptr(iout), _stream(bins.device)),
+               "cdna_seg_hist(rec)")
+    out.copy_(iout)
+    out[..., 1] /= qs1
+    return out
+
+
+def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
+              v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
+              scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False) -> torch.Tensor:
     """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
 
     segs: [k, 3] {start, len, slot}.  [..., 0] = sum w*v0 (or sum w when v0p is None), [..., 1] = sum w*v1.
@@ -1056,13 +1098,16 @@ def seg_partition(bins: torch.Tensor, perm: Optional[torch.Tensor], v0p: Optiona
 
 
 def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndarray, S: int,
-                  v0: Optional[torch.Tensor], v1: torch.Tensor):
+                  v0: Optional[torch.Tensor], v1: torch.Tensor, rec_scale: Optional[float] = None):
     """Rows of the nodes a level builds, gathered into one segment per histogram slot.
 
     codes [T, n] row records (weight << 8 | local node); tfirst [T] first active index per tree;
     build_slot [A] slot of active node a (-1: not built).  Returns (perm int32, v0p, v1p, wp uint8,
     segs [S, 2] {start, len}).  Row order inside a segment is unspecified (the segment histograms
     are exact fixed-point sums, so it does not change any result).
+
+    rec_scale (GPU, no v0, wave-owned path only): return packed int64 item records instead, as
+    (rec, None, None, None, segs) with rec = row | w << 31 | (clamp(rint(v1 * rec_scale), +-2^23) + 2^23) << 39.
     """
     T, n = codes.shape
     dev = codes.device
@@ -1093,7 +1138,8 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
     nb_t = np.bincount(tree_of[built], minlength=T) if A else np.zeros(T, np.int64)
     kb_need = int(nb_t.max()) if T else 0
     if 0 < kb_need <= 16 and COMPACT_W:
-        return _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1)
+        return _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1,
+                                rec_scale if (v0 is None and n < 2 ** 31) else None)
     bs_t = torch.from_numpy(bs).to(dev)
     v1c = v1.float().contiguous()
     v0c = None if v0 is None else v0.float().contiguous()
@@ -1119,7 +1165,7 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
 COMPACT_W = __import__("os").environ.get("CDNAML_COMPACT_W", "1") != "0"
 
 
-def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1):
+def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1, rec_scale=None):
     T, n = codes.shape
     dev = codes.device
     A = len(bs)
@@ -1140,8 +1186,8 @@ def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1):
     v0c = None if v0 is None else v0.float().contiguous()
     wcnt = torch.empty((T, Wv, KB), dtype=torch.int32, device=dev)
     _lib.check(L.cdna_codes_compact_w(1, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
-                                      per_wave, Wv, _ptr(wcnt), None, None, None, None, None, _stream(dev)),
-               "cdna_codes_compact_w(count)")
+                                      per_wave, Wv, _ptr(wcnt), None, None, None, None, None, None, 0.0,
+                                      _stream(dev)), "cdna_codes_compact_w(count)")
     tot = wcnt.sum(1, dtype=torch.int64)                      # [T, KB]
     tot_h = tot.cpu().numpy()
     lens = np.zeros(S, dtype=np.int64)
@@ -1151,18 +1197,25 @@ def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1):
     starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if S else np.zeros(0, np.int64)
     total = int(lens.sum())
     assert total < 2 ** 31
-    perm = torch.empty(total, dtype=torch.int32, device=dev)
-    v1p = torch.empty(total, dtype=torch.float32, device=dev)
-    v0p = None if v0 is None else torch.empty(total, dtype=torch.float32, device=dev)
-    wp = torch.empty(total, dtype=torch.uint8, device=dev)
+    rec = rec_scale is not None
+    if rec:
+        perm = torch.empty(total, dtype=torch.int64, device=dev)
+        v1p = v0p = wp = None
+    else:
+        perm = torch.empty(total, dtype=torch.int32, device=dev)
+        v1p = torch.empty(total, dtype=torch.float32, device=dev)
+        v0p = None if v0 is None else torch.empty(total, dtype=torch.float32, device=dev)
+        wp = torch.empty(total, dtype=torch.uint8, device=dev)
     if total:
         kstart = np.zeros((T, KB), dtype=np.int64)
         kstart[valid] = starts[sl[valid]]
         woff = (torch.from_numpy(kstart).to(dev)[:, None, :] + torch.cumsum(wcnt, 1, dtype=torch.int64) - wcnt)
         woff = woff.to(torch.int32).contiguous()
         _lib.check(L.cdna_codes_compact_w(2, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
-                                          per_wave, Wv, None, _ptr(woff), _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp),
-                                          _stream(dev)), "cdna_codes_compact_w(scatter)")
+                                          per_wave, Wv, None, _ptr(woff), None if rec else _ptr(perm), _ptr(v0p),
+                                          _ptr(v1p), _ptr(wp), _ptr(perm) if rec else None,
+                                          float(rec_scale) if rec else 0.0, _stream(dev)),
+                   "cdna_codes_compact_w(scatter)")
     return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
 
 

@@ -35,6 +35,8 @@ struct SegHistArgs {
   const int* work;
   float qs0, qs1;
   unsigned long long* out;  // [S][d][B][2]
+  // optional packed item records (flat kernel, REC): row | weight << 31 | (q1 + 2^23) << 39 (see CompactWArgs)
+  const uint64_t* rec = nullptr;
 };
 
 // PACKED: one u64 atomic per update (count << 44 | sum of w * (q + 2^23)); the
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(1024) void seg_hist_rm_kernel(const SegHistArgs a, 
 // ds_add wave instruction).  A lane's 8 cells are updated in a rotated order;
 // the partial last group (d % 8 != 0) masks its missing features per j, so the
 // wave issues exactly 8 atomic instructions per pair round.
-template <bool HAS_W>
+template <bool HAS_W, bool REC = false>
 __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a, const uint64_t* __restrict__ bins_rm,
                                                              int G, int ngb) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long h[];
@@ -279,10 +281,19 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
       const uint32_t i = ok ? q / Gu : 0u;
       const int g = ok ? (int)(q - i * Gu) : 0;  // group within the block's range
       g_[u] = g;
-      const int row = ok ? a.perm[start + i] : 0;
-      b8[u] = ok ? bins_rm[(int64_t)row * G + g0 + g] : 0ull;
-      x1[u] = ok ? a.v1p[start + i] : 0.f;
-      w[u] = ok ? (HAS_W ? (uint32_t)a.wp[start + i] : 1u) : 0u;
+      if (REC) {
+        // one 8-byte record per item instead of perm / v1p / wp: fewer, wider loads
+        const uint64_t rc = ok ? a.rec[start + i] : 0ull;
+        const int row = (int)(rc & 0x7FFFFFFFull);
+        b8[u] = ok ? bins_rm[(int64_t)row * G + g0 + g] : 0ull;
+        w[u] = (uint32_t)(rc >> 31) & 0xFFu;
+        x1[u] = __int_as_float((int)(uint32_t)(rc >> 39));  // carries q1 + 2^23 (bit pattern, not a float)
+      } else {
+        const int row = ok ? a.perm[start + i] : 0;
+        b8[u] = ok ? bins_rm[(int64_t)row * G + g0 + g] : 0ull;
+        x1[u] = ok ? a.v1p[start + i] : 0.f;
+        w[u] = ok ? (HAS_W ? (uint32_t)a.wp[start + i] : 1u) : 0u;
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -291,10 +302,16 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
       const uint32_t fvalid = w[u] == 0u ? 0u : (valid_f >= 8 ? 0xFFu : ((1u << (valid_f > 0 ? valid_f : 0)) - 1u));
       const uint32_t frot = ((fvalid >> rot) | (fvalid << (8 - rot))) & 0xFFu;
       const uint32_t lo = (uint32_t)b8[u], hi = (uint32_t)(b8[u] >> 32);
-      int q1 = (int)rintf(x1[u] * a.qs1);
-      q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+      uint32_t qb;  // q1 + 2^23
+      if (REC) {
+        qb = (uint32_t)__float_as_int(x1[u]);
+      } else {
+        int q1 = (int)rintf(x1[u] * a.qs1);
+        q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+        qb = (uint32_t)(q1 + kPackQ);
+      }
       const unsigned long long add =
-          ((unsigned long long)w[u] << kPackShift) + (unsigned long long)w[u] * (unsigned long long)(q1 + kPackQ);
+          ((unsigned long long)w[u] << kPackShift) + (unsigned long long)w[u] * (unsigned long long)qb;
       const int gbase = g * plane_g;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -663,6 +680,10 @@ struct CompactWArgs {
   float* v0_out;
   float* v1_out;
   uint8_t* w_out;
+  // rec_out != null: one packed record per item instead of perm / v1 / w:
+  // row (31 bits) | weight << 31 (8 bits) | (clamp(rint(v1 * qs1), +-2^23) + 2^23) << 39 (25 bits)
+  uint64_t* rec_out;
+  float qs1;
 };
 
 __device__ __forceinline__ bool v_aligned(const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -752,6 +773,13 @@ __global__ __launch_bounds__(256) void codes_compact_w_kernel(const CompactWArgs
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (pos[j] < 0) continue;
+        if (a.rec_out) {
+          int q1 = (int)rintf(x1[q][j] * a.qs1);
+          q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+          a.rec_out[pos[j]] = (uint64_t)(r + j) | ((uint64_t)(cc[q][j] >> 8) << 31) |
+                              ((uint64_t)(uint32_t)(q1 + kPackQ) << 39);
+          continue;
+        }
         a.perm_out[pos[j]] = (int)(r + j);
         a.v1_out[pos[j]] = x1[q][j];
         if (a.v0) a.v0_out[pos[j]] = x0[q][j];
@@ -788,6 +816,7 @@ __global__ __launch_bounds__(256) void bins_row_major_kernel(const uint64_t* __r
 }  // namespace
 
 // mode bit0: packed (no v0; count | sum in one atomic); bit1: per-row weights wp present;
+// bit4: `perm` holds packed 8-byte item records (row | w << 31 | (q1 + 2^23) << 39; flat kernel only).
 // bit2: bins are row-major [n][G] words (seg_hist_flat_kernel when packed and all groups fit 128 KB of LDS,
 // else seg_hist_rm_kernel); bit3: force seg_hist_rm_kernel.
 // work: [nwork][3] {start, len, slot}; grid = nwork x ceil(d / 8).
@@ -797,6 +826,8 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
   if (nwork <= 0) return 0;
   SegHistArgs a{bins, n, d, B, perm, v0p, v1p, wp, work, qs0, qs1, out};
   const bool packed = (mode & 1) != 0, has_w = (mode & 2) != 0;
+  if ((mode & 16) && !((mode & 4) && packed && (size_t)8 * B * 8 <= 128 * 1024 && !(mode & 8)))
+    return (int)hipErrorInvalidValue;
   if ((mode & 4) && packed && (size_t)8 * B * 8 <= 128 * 1024 && !(mode & 8)) {
     // lanes over (row, group) pairs; the groups are split over as few blocks as fit 128 KB of LDS
     const int G = (d + 7) / 8;
@@ -811,8 +842,14 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
                                   (int)lds);
       hipLaunchKernelGGL(kern, dim3((unsigned)nwork, (unsigned)nblk_g), dim3(1024), lds, st, a, bins, G, ngb);
     };
-    if (has_w) launch(seg_hist_flat_kernel<true>);
-    else launch(seg_hist_flat_kernel<false>);
+    if (mode & 16) {  // perm holds packed item records
+      a.rec = reinterpret_cast<const uint64_t*>(perm);
+      launch(seg_hist_flat_kernel<true, true>);
+    } else if (has_w) {
+      launch(seg_hist_flat_kernel<true>);
+    } else {
+      launch(seg_hist_flat_kernel<false>);
+    }
     return (int)hipGetLastError();
   }
   if (mode & 4) {  // bins is row-major [n][G]
@@ -899,10 +936,12 @@ CDNA_API int cdna_bins_row_major(const uint64_t* bins, int64_t n, int G, uint64_
 CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64_t n, int T, int A,
                                   const int* tfirst, const int* kmap, const float* v0, const float* v1,
                                   int64_t per_wave, int Wv, int* wcnt, const int* woff, int* perm_out, float* v0_out,
-                                  float* v1_out, uint8_t* w_out, hipStream_t st) {
+                                  float* v1_out, uint8_t* w_out, uint64_t* rec_out, float qs1, hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
   if (per_wave % 256 != 0 || (int64_t)Wv * per_wave < n) return (int)hipErrorInvalidValue;
-  CompactWArgs a{codes, n, T, A, tfirst, kmap, v0, v1, per_wave, Wv, wcnt, woff, perm_out, v0_out, v1_out, w_out};
+  if (rec_out && (n >= (int64_t)1 << 31 || v0)) return (int)hipErrorInvalidValue;
+  CompactWArgs a{codes, n, T, A, tfirst, kmap, v0, v1, per_wave, Wv, wcnt, woff, perm_out, v0_out, v1_out, w_out,
+                 rec_out, qs1};
   const dim3 grid((unsigned)((Wv + 3) / 4), (unsigned)T);
   auto go = [&](auto k1, auto k2) {
     if (pass == 1) hipLaunchKernelGGL(k1, grid, dim3(256), 0, st, a);

@@ -628,3 +628,34 @@ def test_heap_predict_matches_node_predict(dev, monkeypatch):
             monkeypatch.setattr(E, "HEAP_PREDICT", heap)
             outs.append(f.predict(Xq, tw).cpu())
         assert torch.allclose(outs[0], outs[1], rtol=1e-6, atol=1e-5)
+
+
+def test_compact_records_histogram(dev):
+    """Packed item records (row | w | quantised label) give the same segment histograms as perm/v1/w."""
+    T, n, d, B = 5, 60000, 21, 40
+    rng = np.random.default_rng(8)
+    nloc = np.full(T, 2)
+    tfirst = torch.from_numpy(np.arange(T, dtype=np.int32) * 2)
+    loc = rng.integers(0, 3, (T, n))
+    loc = np.where(loc == 2, 0xFF, loc)
+    w = rng.integers(0, 6, (T, n))
+    loc = np.where(w == 0, 0xFF, loc)
+    codes = torch.from_numpy(((w << 8) | loc).astype(np.uint16).view(np.int16)).to(dev)
+    slot_of = np.array([0, -1, 1, -1, -1, 2, 3, 4, 5, -1], dtype=np.int32)
+    S = 6
+    g = torch.Generator().manual_seed(2)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    bins = K.binize(X.to(dev), thr.to(dev), nthr.to(dev))
+    rm = K.bins_row_major(bins)
+    v1 = (torch.randn(n, generator=g) * 3).to(dev)
+    sc = K.seg_scales(None, v1, 5, n)
+    p0, _, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, S, None, v1)
+    r1, _, nv, nw, sg1 = K.codes_compact(codes, tfirst, slot_of, S, None, v1, rec_scale=sc[1])
+    assert nv is None and r1.dtype == torch.int64
+    np.testing.assert_array_equal(sg, sg1)
+    assert torch.equal(r1 & 0x7FFFFFFF, p0.long())
+    sb = np.concatenate([sg, np.arange(S)[:, None]], 1)
+    a = K.seg_hist(bins, d, B, p0, None, v1p, wp, sb, S, 5, sc, bins_rm=rm)
+    b = K.seg_hist(bins, d, B, r1, None, None, None, sb, S, 5, sc, bins_rm=rm, rec=True)
+    assert torch.equal(a, b)
