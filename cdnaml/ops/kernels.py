@@ -90,6 +90,50 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
 
 
 # --------------------------------------------------------------------- K4
+# binize v3 (LUT-narrowed search).  Opt-in: measured 38.8 ms vs 27.4 ms for the plain lockstep search at
+# 1e8 x 100 x 40 bins -- binize2 is not bound by its threshold reads (rocprofv3: 36 % of its LDS cycles are
+# bank conflicts of the tile stores, half of wave time waits on memory)
+BINIZE_LUT = __import__("os").environ.get("CDNAML_BINIZE_LUT", "0") != "0"
+
+
+def _binize_lut(thr: torch.Tensor, nthr: torch.Tensor):
+    """Cell tables for binize v3: per continuous feature, C uniform f32 cells over [t_0, t_last] and the
+    number of thresholds in earlier cells (the same f32 cell function as the kernel).  Picks the C in
+    (64, 128, 256) with the fewest in-cell search steps (ceil(log2(fullest cell + 1))), the smallest on ties;
+    None when that still needs more than 5 steps (the plain search is then as good)."""
+    T = thr.detach().float().cpu().numpy().reshape(len(nthr), -1) if thr.numel() else np.zeros((len(nthr), 1),
+                                                                                                np.float32)
+    nt = nthr.detach().cpu().numpy().astype(np.int64)
+    d = len(nt)
+    best = None
+    for C in (64, 128, 256):
+        lut = np.zeros((d, C + 1), dtype=np.uint8)
+        lo = np.zeros(d, dtype=np.float32)
+        sc = np.zeros(d, dtype=np.float32)
+        M = 0
+        for f in range(d):
+            k = int(nt[f])
+            if k <= 0:
+                continue
+            t = T[f, :k].astype(np.float32)
+            lo[f] = t[0]
+            span = np.float32(t[-1]) - np.float32(t[0])
+            sc[f] = np.float32(C) / span if span > 0 else np.float32(0.0)
+            with np.errstate(invalid="ignore", over="ignore"):
+                cf = (t - lo[f]) * sc[f]
+            cf = np.minimum(np.maximum(np.nan_to_num(cf, nan=0.0), np.float32(0.0)), np.float32(C - 1))
+            cells = cf.astype(np.int64)
+            lut[f] = np.searchsorted(cells, np.arange(C + 1), side="left")
+            M = max(M, int(np.diff(lut[f].astype(np.int64)).max()))
+        steps = int(M).bit_length()
+        if best is None or steps < best[3]:
+            best = (lut, np.concatenate([lo, sc]), C, steps)
+    if best is None or best[3] > 5:
+        return None
+    dev = thr.device
+    return (torch.from_numpy(best[0]).to(dev), torch.from_numpy(best[1]).to(dev), best[2], best[3])
+
+
 def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor) -> torch.Tensor:
     """Raw features -> uint8 bins in feature-group-major layout [G, n, 8].
 
@@ -106,6 +150,15 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor) -> torch.Tens
         nthr = nthr.int().contiguous()
         out = torch.empty((G, n, 8), dtype=torch.uint8, device=X.device)
         if n:
+            lut = _binize_lut(thr, nthr) if BINIZE_LUT else None
+            if lut is not None:
+                lut_t, losc_t, C, M = lut
+                rc = _lib.lib().cdna_binize_lut(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax,
+                                                _ptr(lut_t), _ptr(losc_t), C, M, _ptr(out), _stream(X.device))
+                if rc == 0:
+                    return out
+                if rc != 1:  # 1 = hipErrorInvalidValue: LDS budget, use the search kernel
+                    _lib.check(rc, "cdna_binize_lut")
             _lib.check(_lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, _ptr(out),
                                               _stream(X.device)), "cdna_binize")
         return out

@@ -659,3 +659,23 @@ def test_compact_records_histogram(dev):
     a = K.seg_hist(bins, d, B, p0, None, v1p, wp, sb, S, 5, sc, bins_rm=rm)
     b = K.seg_hist(bins, d, B, r1, None, None, None, sb, S, 5, sc, bins_rm=rm, rec=True)
     assert torch.equal(a, b)
+
+
+def test_binize_lut_matches_reference(dev, monkeypatch):
+    """binize v3 (LUT-narrowed search) == torch.searchsorted reference, incl. +-inf, NaN, ties at thresholds."""
+    from cdnaml.models.tree.engine import find_thresholds
+    g = torch.Generator().manual_seed(4)
+    n, d = 50000, 24
+    X = torch.randn(n, d, generator=g, dtype=torch.float64) * 3
+    X[:, 5] = torch.round(X[:, 5])
+    X[:, 6] = X[:, 6] ** 3
+    X[7, 1], X[8, 1], X[9, 2] = float("inf"), float("-inf"), float("nan")
+    thr, nthr = find_thresholds(X[:5000].numpy(), d, 40, {})
+    X[:100, 0] = torch.from_numpy(thr[0, :100 if thr.shape[1] > 100 else thr.shape[1]]).repeat(3)[:100]
+    thr_t = torch.from_numpy(thr.astype(np.float32))
+    nthr_t = torch.from_numpy(nthr)
+    monkeypatch.setattr(K, "BINIZE_LUT", True)
+    assert K._binize_lut(thr_t, nthr_t) is not None
+    ref = K.binize(X.float(), thr_t, nthr_t)
+    out = K.binize(X.float().to(dev), thr_t.to(dev), nthr_t.to(dev)).cpu()
+    assert torch.equal(out, ref)
