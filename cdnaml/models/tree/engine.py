@@ -44,6 +44,8 @@ USE_SEG = __import__("os").environ.get("CDNAML_TREE_SEG", "1") != "0"
 # multi-tree regression forests: level 0 on row records, then rows grouped by (tree, node) segments
 USE_MSEG = __import__("os").environ.get("CDNAML_TREE_MSEG", "1") != "0"
 MSEG_L0 = __import__("os").environ.get("CDNAML_MSEG_L0", "1") != "0"  # level 0 through segments too
+# single-tree packed fits (boosting rounds with unit hessians, DecisionTree) through row records + compaction
+MSEG_T1 = __import__("os").environ.get("CDNAML_MSEG_T1", "1") != "0"
 # segment-mode forests carry one packed 8-byte record per gathered row (row | weight | quantised label)
 MSEG_REC = __import__("os").environ.get("CDNAML_MSEG_REC", "1") != "0"
 # single-output forests of depth <= 8 predict from a heap layout (8-byte nodes, fixed-step walks)
@@ -669,16 +671,16 @@ class ForestTrainer:
         # several regression trees: row records for every level (one dense pass partitions all trees); before
         # each level's histogram the rows of the nodes it builds are gathered into slot segments, so the
         # histogram touches only those rows
-        mseg_ok = (USE_MSEG and USE_CODES and T > 1 and not self.classification and p.max_depth <= 8 and
-                   T * n < 2 ** 31 and n > 0)
+        mseg_ok = (USE_MSEG and USE_CODES and (T > 1 or (MSEG_T1 and stats_rows.get("v0") is None)) and
+                   not self.classification and p.max_depth <= 8 and T * n < 2 ** 31 and n > 0)
         # ... and with per-node feature subsets (RandomForest) only each node's sampled features are
         # accumulated (packed statistics only: no v0)
         subset_seg = mseg_ok and need_masks and MSEG_SUBSET and stats_rows.get("v0") is None
         masked = need_masks and (HIST_MODE == "masked" or subset_seg)
         subtract = not masked
         # one regression tree: rows grouped by node in a permutation (segment mode)
-        use_seg = USE_SEG and T == 1 and not self.classification and not masked
         use_mseg = mseg_ok and (not masked or subset_seg)
+        use_seg = USE_SEG and T == 1 and not self.classification and not masked and not use_mseg
         # row records (uint16 weight<<8 | local node) when every level fits 255 nodes per tree
         use_codes = USE_CODES and p.max_depth <= 8 and not use_seg
         if use_seg:

@@ -906,6 +906,17 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
     return _seg_hist(bins, d, B, perm, v0p, v1p, wp, segs, S, wmax, scales, bins_rm, interleave)
 
 
+# Bank-conflict experiments on the flat segment histogram (rocprofv3: 67 % of its LDS cycles are conflicts
+# of random bins).  Both opt-in, both measured slower on the headline (profiles/README.md):
+#  * SEG_PRIV: one 8-feature group per block with 16 interleaved copies (conflict-free atomics) -- 111 ms
+#    per level vs 25: the per-lane 8-byte row gathers no longer coalesce (one cache line per lane);
+#  * SEG_SPLIT4: all groups with 4 interleaved copies -- 286 vs 238 ms/step: 160 KB blocks halve occupancy.
+SEG_PRIV = __import__("os").environ.get("CDNAML_SEG_PRIV", "0") != "0"
+# flat kernel with 4 interleaved bank-split copies per cell (all groups must fit 160 KB)
+SEG_SPLIT4 = __import__("os").environ.get("CDNAML_SEG_SPLIT4", "0") != "0"
+SEG_PRIV_CHUNK = int(__import__("os").environ.get("CDNAML_SEG_PRIV_CHUNK", "65536"))
+
+
 def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave):
     G, n, _ = bins.shape
     out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
@@ -914,7 +925,10 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave):
         return out
     assert _native(bins) and bins_rm is not None and rec.dtype == torch.int64
     wm = int(max(1, min(255, wmax)))
-    chunk = min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1))
+    priv = SEG_PRIV and B <= 64
+    split4 = SEG_SPLIT4 and not priv and -(-d // 8) * 8 * B * 8 * 4 <= 160 * 1024
+    # bank-private planes: each of the 16 copies sees 1/16 of a chunk's rows (count field headroom)
+    chunk = min(SEG_PRIV_CHUNK if priv else SEG_HIST_CHUNK, ((1 << 20) // (wm + 1)) * (16 if priv else 1))
     work = _seg_work(segs, chunk)
     if len(work) == 0:
         return out
@@ -927,7 +941,9 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave):
     wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
     iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
     assert bins_rm.shape == (n, G, 8) and bins_rm.is_contiguous()
-    _lib.check(_lib.lib().cdna_seg_hist(1 | 4 | 16, _ptr(bins_rm), n, d, B, _ptr(rec), None, None, None,
+    _lib.check(_lib.lib().cdna_seg_hist(1 | 4 | 16 | (32 if priv else 0) | (64 if split4 else 0), _ptr(bins_rm), n,
+                                        d, B, _ptr(rec), None,
+                                        None, None,
                                         _ptr(wt), len(work), 1.0, qs1, _ptr(iout), _stream(bins.device)),
                "cdna_seg_hist(rec)")
     out.copy_(iout)

@@ -542,10 +542,13 @@ def test_seg_mode_matches_codes_mode(dev, monkeypatch):
     df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
     for mk in (lambda: DecisionTreeRegressor(maxDepth=7), lambda: XgboostRegressor(n_estimators=4, max_depth=6)):
         preds = []
-        for seg in (False, True):
+        # codes-only, node-segment partition, row records + per-level compaction
+        for seg, t1 in ((False, False), (True, False), (False, True)):
             monkeypatch.setattr(E, "USE_SEG", seg)
+            monkeypatch.setattr(E, "MSEG_T1", t1)
             preds.append(mk().fit(df).transform(df).select("prediction").toPandas().prediction.values)
         assert np.abs(preds[0] - preds[1]).max() < 1e-3
+        assert np.abs(preds[0] - preds[2]).max() < 1e-3
 
 
 @pytest.mark.parametrize("nonneg,implicit,rank", [(False, False, 12), (True, False, 4), (False, True, 8),
