@@ -89,7 +89,7 @@ _SIGS = {
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "cdna_codes_compact": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p], c_int),
     "cdna_bins_row_major": ([c_void_p, c_int64, c_int, c_void_p, c_void_p], c_int),
     "cdna_partition6": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p], c_int),

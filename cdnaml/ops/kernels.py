@@ -457,7 +457,8 @@ def codes_init_max(weights: Optional[torch.Tensor], T: int, n: int, device):
                    "cdna_codes_init")
         return codes, max(1, int(wm.item()))
     if weights is None:
-        w = torch.ones((T, n), dtype=torch.int32, device=device)
+        # every row in every tree with weight 1 at the root (local node 0): one fill, no elementwise chain
+        return torch.full((T, n), 1 << 8, dtype=torch.int16, device=device), 1
     else:
         w = weights.to(device=device).to(torch.int32)
     c = (w << 8) | torch.where(w == 0, torch.full_like(w, CODE_DONE), torch.zeros_like(w))
@@ -1214,20 +1215,26 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
     v0c = None if v0 is None else v0.float().contiguous()
     cnt = torch.zeros(max(S, 1), dtype=torch.int32, device=dev)
     _lib.check(L.cdna_codes_compact(1, _ptr(codes), n, T, A, _ptr(tf), _ptr(bs_t), _ptr(v0c), _ptr(v1c), _ptr(cnt),
-                                    None, None, None, None, _stream(dev)), "cdna_codes_compact(count)")
+                                    None, None, None, None, None, 0.0, _stream(dev)), "cdna_codes_compact(count)")
     lens = cnt.cpu().numpy()[:S].astype(np.int64)
     starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if S else np.zeros(0, np.int64)
     total = int(lens.sum())
     assert total < 2 ** 31
-    perm = torch.empty(total, dtype=torch.int32, device=dev)
-    v1p = torch.empty(total, dtype=torch.float32, device=dev)
-    v0p = None if v0 is None else torch.empty(total, dtype=torch.float32, device=dev)
-    wp = torch.empty(total, dtype=torch.uint8, device=dev)
+    rec = rec_scale is not None and v0 is None and n < 2 ** 31
+    if rec:
+        perm = torch.empty(total, dtype=torch.int64, device=dev)
+        v1p = v0p = wp = None
+    else:
+        perm = torch.empty(total, dtype=torch.int32, device=dev)
+        v1p = torch.empty(total, dtype=torch.float32, device=dev)
+        v0p = None if v0 is None else torch.empty(total, dtype=torch.float32, device=dev)
+        wp = torch.empty(total, dtype=torch.uint8, device=dev)
     if total:
         cur = torch.from_numpy(np.concatenate([starts, [0]]).astype(np.int32)).to(dev)
         _lib.check(L.cdna_codes_compact(2, _ptr(codes), n, T, A, _ptr(tf), _ptr(bs_t), _ptr(v0c), _ptr(v1c),
-                                        _ptr(cur), _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp), _stream(dev)),
-                   "cdna_codes_compact(scatter)")
+                                        _ptr(cur), None if rec else _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp),
+                                        _ptr(perm) if rec else None, float(rec_scale) if rec else 0.0,
+                                        _stream(dev)), "cdna_codes_compact(scatter)")
     return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
 
 
@@ -1278,8 +1285,11 @@ def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1, re
     if total:
         kstart = np.zeros((T, KB), dtype=np.int64)
         kstart[valid] = starts[sl[valid]]
-        woff = (torch.from_numpy(kstart).to(dev)[:, None, :] + torch.cumsum(wcnt, 1, dtype=torch.int64) - wcnt)
-        woff = woff.to(torch.int32).contiguous()
+        # exclusive scan over each (tree, node)'s waves, as an inner-dim scan on the [T, KB, Wv] transpose
+        # (torch's outer-dim scan kernel took 0.37 ms per call on [1, 2048, KB])
+        wt_ = wcnt.permute(0, 2, 1).contiguous()
+        ex = torch.cumsum(wt_, 2, dtype=torch.int64) - wt_
+        woff = (torch.from_numpy(kstart).to(dev)[:, :, None] + ex).to(torch.int32).permute(0, 2, 1).contiguous()
         _lib.check(L.cdna_codes_compact_w(2, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
                                           per_wave, Wv, None, _ptr(woff), None if rec else _ptr(perm), _ptr(v0p),
                                           _ptr(v1p), _ptr(wp), _ptr(perm) if rec else None,

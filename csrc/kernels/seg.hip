@@ -643,6 +643,8 @@ struct CompactArgs {
   float* v0_out;
   float* v1_out;
   uint8_t* w_out;
+  uint64_t* rec_out;  // optional packed records (see CompactWArgs)
+  float qs1;
 };
 
 template <bool SCATTER>
@@ -674,16 +676,9 @@ __global__ __launch_bounds__(256) void codes_compact_kernel(const CompactArgs a)
     for (int u = 0; u < U; ++u) {
     const uint32_t c = cu[u];
     const uint32_t loc = c & 0xFFu;
-    bool want = loc != 0xFFu && s_slot[loc] >= 0;
-    while (true) {
-      const uint64_t act = __builtin_amdgcn_ballot_w64(want);
-      if (!act) break;
-      const int leader = __builtin_ctzll(act);
-      const uint32_t lloc = (uint32_t)__shfl((int)loc, leader);
-      const uint64_t m = __builtin_amdgcn_ballot_w64(want && loc == lloc);
-      if (lane == leader) atomicAdd(&s_cnt[lloc], __builtin_popcountll(m));
-      if (loc == lloc) want = false;
-    }
+    // this kernel serves levels with many built nodes per tree (the wave-owned kernel covers <= 16):
+    // plain per-lane LDS atomics; peeling one ballot round per distinct node in the wave cost up to 64 rounds
+    if (loc != 0xFFu && s_slot[loc] >= 0) atomicAdd(&s_cnt[loc], 1);
     }
   }
   __syncthreads();
@@ -710,29 +705,18 @@ __global__ __launch_bounds__(256) void codes_compact_kernel(const CompactArgs a)
     const int64_t r = rb + u * 256 + threadIdx.x;
     const uint32_t c = cu[u];
     const uint32_t loc = c & 0xFFu;
-    bool want = loc != 0xFFu && s_slot[loc] >= 0;
-    int pos = -1;
-    while (true) {
-      const uint64_t act = __builtin_amdgcn_ballot_w64(want);
-      if (!act) break;
-      const int leader = __builtin_ctzll(act);
-      const uint32_t lloc = (uint32_t)__shfl((int)loc, leader);
-      const uint64_t m = __builtin_amdgcn_ballot_w64(want && loc == lloc);
-      int base = 0;
-      if (lane == leader) base = atomicAdd(&s_cnt[lloc], __builtin_popcountll(m));
-      base = __shfl(base, leader);
-      if (want && loc == lloc) {
-        const int below =
-            (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        pos = s_base[lloc] + base + below;
-        want = false;
-      }
-    }
+    const int pos = (loc != 0xFFu && s_slot[loc] >= 0) ? s_base[loc] + atomicAdd(&s_cnt[loc], 1) : -1;
     if (pos >= 0) {
-      a.perm_out[pos] = (int)r;
-      a.v1_out[pos] = a.v1[r];
-      if (a.v0) a.v0_out[pos] = a.v0[r];
-      a.w_out[pos] = (uint8_t)(c >> 8);
+      if (a.rec_out) {
+        int q1 = (int)rintf(a.v1[r] * a.qs1);
+        q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+        a.rec_out[pos] = (uint64_t)r | ((uint64_t)(c >> 8) << 31) | ((uint64_t)(uint32_t)(q1 + kPackQ) << 39);
+      } else {
+        a.perm_out[pos] = (int)r;
+        a.v1_out[pos] = a.v1[r];
+        if (a.v0) a.v0_out[pos] = a.v0[r];
+        a.w_out[pos] = (uint8_t)(c >> 8);
+      }
     }
     }
   }
@@ -1012,9 +996,11 @@ CDNA_API int cdna_seg_partition(int pass, const uint64_t* bins, int64_t n, const
 // totals (must be zeroed); pass 2: cnt = per-slot write cursors initialised to the segment starts.
 CDNA_API int cdna_codes_compact(int pass, const uint16_t* codes, int64_t n, int T, int A, const int* tfirst,
                                 const int* build_slot, const float* v0, const float* v1, int* cnt, int* perm_out,
-                                float* v0_out, float* v1_out, uint8_t* w_out, hipStream_t st) {
+                                float* v0_out, float* v1_out, uint8_t* w_out, uint64_t* rec_out, float qs1,
+                                hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
-  CompactArgs a{codes, n, T, A, tfirst, build_slot, v0, v1, cnt, perm_out, v0_out, v1_out, w_out};
+  if (rec_out && (n >= (int64_t)1 << 31 || v0)) return (int)hipErrorInvalidValue;
+  CompactArgs a{codes, n, T, A, tfirst, build_slot, v0, v1, cnt, perm_out, v0_out, v1_out, w_out, rec_out, qs1};
   int64_t nb = (n + 4095) / 4096;
   const int per_tree = (int)(nb < 512 ? nb : 512);
   const dim3 grid((unsigned)per_tree, (unsigned)T);
