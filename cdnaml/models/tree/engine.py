@@ -46,6 +46,8 @@ USE_MSEG = __import__("os").environ.get("CDNAML_TREE_MSEG", "1") != "0"
 MSEG_L0 = __import__("os").environ.get("CDNAML_MSEG_L0", "1") != "0"  # level 0 through segments too
 # single-tree packed fits (boosting rounds with unit hessians, DecisionTree) through row records + compaction
 MSEG_T1 = __import__("os").environ.get("CDNAML_MSEG_T1", "1") != "0"
+# K6 split search in one HIP kernel (split.hip) where it applies; else the torch formulation
+NATIVE_SPLIT = __import__("os").environ.get("CDNAML_NATIVE_SPLIT", "1") != "0"
 # segment-mode forests carry one packed 8-byte record per gathered row (row | weight | quantised label)
 MSEG_REC = __import__("os").environ.get("CDNAML_MSEG_REC", "1") != "0"
 # single-output forests of depth <= 8 predict from a heap layout (8-byte nodes, fixed-step walks)
@@ -550,6 +552,17 @@ class ForestTrainer:
         return float("nan")
 
     # ------------------------------------------------------------ split scan
+    def _native_split(self, dev) -> bool:
+        """K6 kernel for regression variance / XGBoost gains without categorical or missing-value bins."""
+        return (NATIVE_SPLIT and dev.type == "cuda" and not self.classification and not self.data.categorical and
+                not (self.p.impurity == "xgb" and self.data.missing_bin) and self.stats_k == 2)
+
+    def _nthr_dev(self, dev):
+        t = getattr(self, "_nthr_t", None)
+        if t is None:
+            t = self._nthr_t = torch.from_numpy(np.asarray(self.data.nthr, dtype=np.int32)).to(dev)
+        return t
+
     def _best_splits(self, H: torch.Tensor, tot: torch.Tensor, masks: torch.Tensor):
         """H [A, d, B, k] (f64) -> per node (gain, feat, bin, left stats, right stats, cat order)."""
         A, d, B, k = H.shape
@@ -793,9 +806,17 @@ class ForestTrainer:
                 par = torch.tensor([active[a]["parent"] for a in derived], device=dev)
                 sib = torch.tensor([active[a]["sib"] for a in derived], device=dev)
                 H[di] = prev_hist[par] - H[sib]
-            tot = self._node_stats(H, None)
             masks_t = torch.from_numpy(masks_np.view(np.int32)).to(dev) if masks_np is not None else None
-            gain, bf, bb, lst, rst, order, cat_feats, miss_right = self._best_splits(H, tot, masks_t)
+            if self._native_split(dev):
+                # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
+                so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
+                                       p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight)
+                gain, bf, bb = so[:, 0], so[:, 1].long(), so[:, 2].long()
+                lst, rst = so[:, 3:5], so[:, 5:7]
+                order, cat_feats, miss_right = None, [], None
+            else:
+                tot = self._node_stats(H, None)
+                gain, bf, bb, lst, rst, order, cat_feats, miss_right = self._best_splits(H, tot, masks_t)
             # one device->host transfer for the whole level's decisions (ids < 2^53 are exact in f64)
             kk = lst.shape[1]
             cols = [gain[:, None], bf[:, None].double(), bb[:, None].double(), lst, rst]

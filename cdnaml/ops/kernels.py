@@ -1389,3 +1389,24 @@ def partition_dest(dest: torch.Tensor, W: int):
         return perm, counts.long().sum(1)
     perm = torch.argsort(dest.long(), stable=True)
     return perm, torch.bincount(dest.long(), minlength=W)
+
+
+# ------------------------------------------------------------ K6 (split.hip)
+def split_scan(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor], kind: int, min_inst: float,
+               reg_lambda: float = 1.0, gamma: float = 0.0, min_child_weight: float = 1.0):
+    """Best split per node of level histograms H [A, d, B, 2] (fp64) -> (out [A, 8], tot [A, 2]).
+
+    out = (gain, feature, bin, left0, left1, right0, right1, 0); gain -inf when no legal split.
+    kind 0: variance gain on (weight, sum); kind 1: XGBoost gain on (hess, grad)."""
+    A, d, B, k = H.shape
+    assert k == 2 and H.dtype == torch.float64 and _native(H)
+    Hc = H.contiguous()
+    out = torch.empty((A, 8), dtype=torch.float64, device=H.device)
+    tot = torch.empty((A, 2), dtype=torch.float64, device=H.device)
+    nt = nthr.to(device=H.device, dtype=torch.int32).contiguous()
+    m = None if masks is None else masks.to(device=H.device, dtype=torch.int32).contiguous()
+    mw = 0 if m is None else m.shape[1]
+    _lib.check(_lib.lib().cdna_split_scan(_ptr(Hc), _ptr(nt), _ptr(m), mw, A, d, B, kind, float(min_inst),
+                                          float(reg_lambda), float(gamma), float(min_child_weight), _ptr(out),
+                                          _ptr(tot), _stream(H.device)), "cdna_split_scan")
+    return out, tot

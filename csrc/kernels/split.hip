@@ -1,0 +1,157 @@
+// K6 split_scan: best split of every active node from its level histogram, in
+// one kernel (PLANET's per-level "find best splits" on the
+// driver, ML 06 - Decision Trees.py:96-118).
+//
+// The torch formulation (prefix sums, gains, masks, argmax over [A, d, B])
+// launches ~30 small kernels per tree level, ~0.65 ms of a level at any data
+// size -- 3 ms of a 46 ms fit at the 8-GPU strong-scaling point (1.25e7 rows
+// per GPU).  Here one block owns one node: a thread per feature sums its bins
+// (node totals = the feature with the largest weight, as the torch path),
+// then scans them left to right in fp64, evaluating the impurity gain of
+// every legal threshold; a block argmax picks the best (gain, feature, bin)
+// with ties going to the lowest flat index f * B + b (torch.argmax order).
+//
+// Regression variance gain and XGBoost's second-order gain are covered;
+// categorical features, classification impurities and missing-value
+// directions stay on the torch path (cdnaml/models/tree/engine.py).
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 128;
+
+struct SplitArgs {
+  const double* H;       // [A][d][B][2]
+  const int* nthr;       // [d]  legal thresholds b < nthr[f]
+  const uint32_t* mask;  // [A][mw] feature-subset bits (null: all features)
+  int mw;
+  int A, d, B;
+  int kind;              // 0 variance (stats: weight, sum), 1 xgb (stats: hess, grad)
+  double min_inst, lambda, gamma, mcw;
+  double* out;           // [A][8]: gain, f, b, left0, left1, right0, right1, -
+  double* tot_out;       // [A][2] node totals
+};
+
+__device__ __forceinline__ double gain_of(const SplitArgs& a, double l0, double l1, double r0, double r1, double t0,
+                                          double t1, bool* ok) {
+  if (a.kind == 0) {
+    const double lo = a.min_inst > 1e-12 ? a.min_inst : 1e-12;
+    *ok = l0 >= lo && r0 >= lo;
+    const double wl = l0 > 1e-300 ? l0 : 1e-300, wr = r0 > 1e-300 ? r0 : 1e-300, wt = t0 > 1e-300 ? t0 : 1e-300;
+    return (l1 * l1 / wl + r1 * r1 / wr - t1 * t1 / wt) / wt;
+  }
+  *ok = l0 >= a.mcw && r0 >= a.mcw && l0 > 0.0 && r0 > 0.0;
+  return 0.5 * (l1 * l1 / (l0 + a.lambda) + r1 * r1 / (r0 + a.lambda) - t1 * t1 / (t0 + a.lambda)) - a.gamma;
+}
+
+__global__ __launch_bounds__(kThreads) void split_scan_kernel(const SplitArgs a) {
+  __shared__ double s_w[kThreads], s_t0[kThreads], s_t1[kThreads], s_g[kThreads];
+  __shared__ int s_f[kThreads], s_k[kThreads];
+  const int node = blockIdx.x;
+  const double* Hn = a.H + (int64_t)node * a.d * a.B * 2;
+  // pass 1: per-feature totals; node totals = those of the feature with the most weight (first on ties)
+  double bw = -1.0, b0 = 0.0, b1 = 0.0;
+  int bf = 0x7FFFFFFF;
+  for (int f = threadIdx.x; f < a.d; f += kThreads) {
+    double t0 = 0.0, t1 = 0.0;
+    const double* hf = Hn + (int64_t)f * a.B * 2;
+    for (int b = 0; b < a.B; ++b) {
+      t0 += hf[2 * b];
+      t1 += hf[2 * b + 1];
+    }
+    if (t0 > bw) {
+      bw = t0;
+      b0 = t0;
+      b1 = t1;
+      bf = f;
+    }
+  }
+  s_w[threadIdx.x] = bw;
+  s_t0[threadIdx.x] = b0;
+  s_t1[threadIdx.x] = b1;
+  s_f[threadIdx.x] = bf;
+  __syncthreads();
+  for (int o = kThreads / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const int j = threadIdx.x + o;
+      if (s_w[j] > s_w[threadIdx.x] || (s_w[j] == s_w[threadIdx.x] && s_f[j] < s_f[threadIdx.x])) {
+        s_w[threadIdx.x] = s_w[j];
+        s_t0[threadIdx.x] = s_t0[j];
+        s_t1[threadIdx.x] = s_t1[j];
+        s_f[threadIdx.x] = s_f[j];
+      }
+    }
+    __syncthreads();
+  }
+  const double t0 = s_t0[0], t1 = s_t1[0];
+  __syncthreads();
+  // pass 2: every legal threshold of every (sampled) feature
+  double best = -__builtin_inf();
+  int bk = 0x7FFFFFFF;
+  for (int f = threadIdx.x; f < a.d; f += kThreads) {
+    if (a.mask && !((a.mask[(int64_t)node * a.mw + (f >> 5)] >> (f & 31)) & 1u)) continue;
+    const int lim = a.nthr[f] < 0 ? 0 : a.nthr[f];
+    const double* hf = Hn + (int64_t)f * a.B * 2;
+    double l0 = 0.0, l1 = 0.0;
+    for (int b = 0; b < a.B && b < lim; ++b) {
+      l0 += hf[2 * b];
+      l1 += hf[2 * b + 1];
+      bool ok;
+      const double g = gain_of(a, l0, l1, t0 - l0, t1 - l1, t0, t1, &ok);
+      if (ok && g == g && g != __builtin_inf() && g != -__builtin_inf() && g > best) {
+        best = g;
+        bk = f * a.B + b;
+      }
+    }
+  }
+  s_g[threadIdx.x] = best;
+  s_k[threadIdx.x] = bk;
+  __syncthreads();
+  for (int o = kThreads / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const int j = threadIdx.x + o;
+      if (s_g[j] > s_g[threadIdx.x] || (s_g[j] == s_g[threadIdx.x] && s_k[j] < s_k[threadIdx.x])) {
+        s_g[threadIdx.x] = s_g[j];
+        s_k[threadIdx.x] = s_k[j];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double* o = a.out + (int64_t)node * 8;
+    const int k = s_k[0];
+    const bool found = k != 0x7FFFFFFF;
+    const int f = found ? k / a.B : 0, b = found ? k - (k / a.B) * a.B : 0;
+    double l0 = 0.0, l1 = 0.0;
+    if (found) {
+      const double* hf = Hn + (int64_t)f * a.B * 2;
+      for (int q = 0; q <= b; ++q) {
+        l0 += hf[2 * q];
+        l1 += hf[2 * q + 1];
+      }
+    }
+    o[0] = found ? s_g[0] : -__builtin_inf();
+    o[1] = f;
+    o[2] = b;
+    o[3] = l0;
+    o[4] = l1;
+    o[5] = t0 - l0;
+    o[6] = t1 - l1;
+    o[7] = 0.0;
+    a.tot_out[node * 2] = t0;
+    a.tot_out[node * 2 + 1] = t1;
+  }
+}
+
+}  // namespace
+
+// kind: 0 = variance (regression trees), 1 = XGBoost gain.  out [A][8], tot_out [A][2] (fp64).
+CDNA_API int cdna_split_scan(const double* H, const int* nthr, const uint32_t* mask, int mw, int A, int d, int B,
+                             int kind, double min_inst, double lambda, double gamma, double mcw, double* out,
+                             double* tot_out, hipStream_t st) {
+  if (A <= 0) return 0;
+  if (d <= 0 || B <= 0 || (kind != 0 && kind != 1)) return (int)hipErrorInvalidValue;
+  SplitArgs a{H, nthr, mask, mw, A, d, B, kind, min_inst, lambda, gamma, mcw, out, tot_out};
+  hipLaunchKernelGGL(split_scan_kernel, dim3((unsigned)A), dim3(kThreads), 0, st, a);
+  return (int)hipGetLastError();
+}

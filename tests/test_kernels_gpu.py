@@ -682,3 +682,24 @@ def test_binize_lut_matches_reference(dev, monkeypatch):
     ref = K.binize(X.float(), thr_t, nthr_t)
     out = K.binize(X.float().to(dev), thr_t.to(dev), nthr_t.to(dev)).cpu()
     assert torch.equal(out, ref)
+
+
+def test_native_split_scan_matches_torch(dev, monkeypatch):
+    """K6 split kernel == torch split search: RF (feature subsets), DecisionTree, XGBoost (lambda/gamma)."""
+    import cdnaml
+    from cdnaml.models.tree import engine as E
+    from cdnaml.ml.regression import DecisionTreeRegressor, RandomForestRegressor
+    from cdnaml.ml.xgboost import XgboostRegressor
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator(device=dev).manual_seed(5)
+    X = torch.randn((100000, 16), generator=g, device=dev)
+    y = (X[:, 0] * 2 + torch.sin(X[:, 1] * 3) + (X[:, 2] > 0.5).float()).double()
+    df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
+    for mk in (lambda: RandomForestRegressor(numTrees=6, maxDepth=6, seed=3),
+               lambda: DecisionTreeRegressor(maxDepth=7, minInstancesPerNode=20),
+               lambda: XgboostRegressor(n_estimators=3, max_depth=5, reg_lambda=2.0, gamma=0.1)):
+        preds = []
+        for native in (False, True):
+            monkeypatch.setattr(E, "NATIVE_SPLIT", native)
+            preds.append(mk().fit(df).transform(df).select("prediction").toPandas().prediction.values)
+        assert np.abs(preds[0] - preds[1]).max() < 1e-4
