@@ -95,6 +95,7 @@ _SIGS = {
                          c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_double, c_double, c_double,
                          c_double, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_compact_mask": ([c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_col_moments": ([c_int, c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_void_p],
                          c_int),
     "cdna_partition_dest": ([c_int, c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],

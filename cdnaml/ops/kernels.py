@@ -1410,3 +1410,26 @@ def split_scan(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor
                                           float(reg_lambda), float(gamma), float(min_child_weight), _ptr(out),
                                           _ptr(tot), _stream(H.device)), "cdna_split_scan")
     return out, tot
+
+
+def compact_mask(mask: torch.Tensor) -> torch.Tensor:
+    """K19: int64 indices of the True entries of a 1-D mask, in order (== torch.nonzero(mask).flatten())."""
+    n = mask.numel()
+    if not _native(mask) or n == 0:
+        return torch.nonzero(mask.reshape(-1), as_tuple=False).flatten()
+    m8 = mask.reshape(-1).to(torch.uint8).contiguous()
+    rpb = max(4096, -(-n // 4096))
+    nb = -(-n // rpb)
+    counts = torch.empty(nb, dtype=torch.int32, device=mask.device)
+    L = _lib.lib()
+    _lib.check(L.cdna_compact_mask(1, _ptr(m8), n, rpb, _ptr(counts), None, None, _stream(mask.device)),
+               "cdna_compact_mask(count)")
+    c64 = counts.long()
+    csum = torch.cumsum(c64, 0)
+    total = int(csum[-1].item())
+    idx = torch.empty(total, dtype=torch.int64, device=mask.device)
+    if total:
+        offs = (csum - c64).contiguous()
+        _lib.check(L.cdna_compact_mask(2, _ptr(m8), n, rpb, None, _ptr(offs), _ptr(idx), _stream(mask.device)),
+                   "cdna_compact_mask(write)")
+    return idx

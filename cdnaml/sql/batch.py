@@ -225,7 +225,8 @@ class Batch:
                      else int(idx.sum()), self.device)
 
     def filter(self, mask: torch.Tensor) -> "Batch":
-        idx = torch.nonzero(mask, as_tuple=False).flatten()
+        from ..ops import kernels as K
+        idx = K.compact_mask(mask)  # K19 stream compaction (HIP on the GPU)
         return self.take(idx)
 
     def slice(self, a: int, b: int) -> "Batch":

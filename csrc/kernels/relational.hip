@@ -1,4 +1,4 @@
-// DataFrame-engine kernels (SURVEY §2.10 K16 hash_partition, K20 col_stats).
+// DataFrame-engine kernels (SURVEY §2.10 K16 hash_partition, K19 compact, K20 col_stats).
 //
 // K20 col_moments: count / mean / M2 / min / max of every column of a [n][d]
 // row-major matrix in ONE pass (describe(), summary(), StandardScaler,
@@ -138,6 +138,45 @@ __global__ __launch_bounds__(kThreads) void partition_dest_kernel(const int* __r
   }
 }
 
+// K19 compact: indices of the rows whose mask byte is non-zero, in row order
+// (filter / handleInvalid="skip" / coldStartStrategy="drop").  Pass 1 counts
+// each block's kept rows with wave ballots; the host-side exclusive scan gives
+// block offsets; pass 2 writes each kept row's index at offset + rank (rank =
+// kept rows of earlier waves of the round + mbcnt within the wave).
+template <bool WRITE>
+__global__ __launch_bounds__(kThreads) void compact_mask_kernel(const uint8_t* __restrict__ mask, int64_t n,
+                                                                int64_t rows_per_block, int* __restrict__ counts,
+                                                                const int64_t* __restrict__ offsets,
+                                                                int64_t* __restrict__ idx) {
+  __shared__ int s_w[kThreads / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+  int64_t base = WRITE ? offsets[blockIdx.x] : 0;
+  int total = 0;
+  for (int64_t rb = r0; rb < r1; rb += kThreads) {
+    const int64_t r = rb + threadIdx.x;
+    const bool keep = r < r1 && mask[r] != 0;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
+    if (lane == 0) s_w[wid] = __builtin_popcountll(m);
+    __syncthreads();
+    int before = 0, round = 0;
+#pragma unroll
+    for (int k = 0; k < kThreads / 64; ++k) {
+      before += k < wid ? s_w[k] : 0;
+      round += s_w[k];
+    }
+    __syncthreads();
+    if (WRITE && keep) {
+      const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      idx[base + before + below] = r;
+    }
+    base += round;
+    total += round;
+  }
+  if (!WRITE && threadIdx.x == 0) counts[blockIdx.x] = total;
+}
+
 }  // namespace
 
 // dtype: 0 = f32, 1 = f64.  part: [nblk][d][5] (count, mean, M2, min, max); nblk = ceil(n / rows_per_block).
@@ -168,5 +207,20 @@ CDNA_API int cdna_partition_dest(int pass, const int* dest, int64_t n, int W, in
   else
     hipLaunchKernelGGL(partition_dest_kernel<true>, dim3(nblk), dim3(kThreads), lds, st, dest, n, W, rows_per_block,
                        counts, offsets, perm);
+  return (int)hipGetLastError();
+}
+
+// K19: pass 1 counts [nblk] kept rows per block; pass 2 writes idx from offsets [nblk] (exclusive scan).
+CDNA_API int cdna_compact_mask(int pass, const uint8_t* mask, int64_t n, int64_t rows_per_block, int* counts,
+                               const int64_t* offsets, int64_t* idx, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (rows_per_block <= 0) return (int)hipErrorInvalidValue;
+  const unsigned nblk = (unsigned)((n + rows_per_block - 1) / rows_per_block);
+  if (pass == 1)
+    hipLaunchKernelGGL(compact_mask_kernel<false>, dim3(nblk), dim3(kThreads), 0, st, mask, n, rows_per_block, counts,
+                       offsets, idx);
+  else
+    hipLaunchKernelGGL(compact_mask_kernel<true>, dim3(nblk), dim3(kThreads), 0, st, mask, n, rows_per_block, counts,
+                       offsets, idx);
   return (int)hipGetLastError();
 }

@@ -703,3 +703,11 @@ def test_native_split_scan_matches_torch(dev, monkeypatch):
             monkeypatch.setattr(E, "NATIVE_SPLIT", native)
             preds.append(mk().fit(df).transform(df).select("prediction").toPandas().prediction.values)
         assert np.abs(preds[0] - preds[1]).max() < 1e-4
+
+
+@pytest.mark.parametrize("n,p", [(1000003, 0.3), (4097, 0.0), (50000, 1.0)])
+def test_compact_mask(dev, n, p):
+    """K19 stream compaction == torch.nonzero order."""
+    g = torch.Generator().manual_seed(n)
+    m = torch.rand(n, generator=g) < p
+    assert torch.equal(K.compact_mask(m.to(dev)).cpu(), torch.nonzero(m).flatten())
