@@ -880,6 +880,16 @@ def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_glob
     return (_fixed_scale(v0p, n_global, wmax, qmax_bits=30), _fixed_scale(v1p, n_global, wmax, qmax_bits=30))
 
 
+SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "1024"))
+
+
+def _fill_chunk(segs: np.ndarray, chunk: int) -> int:
+    """Shrink the rows-per-block chunk so a level with few rows still launches ~SEG_MIN_BLOCKS blocks
+    (at 1.25e7 rows per GPU a level's 95K-row chunks made only ~100 blocks for 256 CUs)."""
+    total = int(np.asarray(segs, dtype=np.int64).reshape(-1, 3)[:, 1].clip(min=0).sum())
+    return int(min(chunk, max(8192, -(-total // max(1, SEG_MIN_BLOCKS)))))
+
+
 def _seg_work(segs: np.ndarray, chunk: int) -> np.ndarray:
     """segs [k, 3] {start, len, tag} -> work items [m, 3] of at most `chunk` rows each."""
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
@@ -930,6 +940,7 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave):
     split4 = SEG_SPLIT4 and not priv and -(-d // 8) * 8 * B * 8 * 4 <= 160 * 1024
     # bank-private planes: each of the 16 copies sees 1/16 of a chunk's rows (count field headroom)
     chunk = min(SEG_PRIV_CHUNK if priv else SEG_HIST_CHUNK, ((1 << 20) // (wm + 1)) * (16 if priv else 1))
+    chunk = _fill_chunk(segs, chunk)
     work = _seg_work(segs, chunk)
     if len(work) == 0:
         return out
@@ -986,6 +997,7 @@ def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optio
     packed = v0p is None
     wm = int(max(1, min(255, wmax)))
     chunk = SEG_HIST_CHUNK if not packed else min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1))
+    chunk = _fill_chunk(segs, chunk)
     work = _seg_work(segs, chunk)
     if len(work) == 0:
         return out
