@@ -712,8 +712,12 @@ class ForestTrainer:
             codes, wmax = K.codes_init_max(weights, T, n, dev)
             node = None
             if use_mseg:
-                mseg_scales = K.seg_scales(None if stats_rows.get("v0") is None else stats_rows["v0"].float(),
-                                           stats_rows["v1"].float(), wmax, n)
+                if stats_rows.get("v0") is None:
+                    # one quantisation scale for every rank: the int64 level histograms then all-reduce to
+                    # the same sums on 1 or N GPUs (the forest does not depend on the GPU count)
+                    mseg_scales = (1.0, K.packed_scale_global(stats_rows["v1"].float(), self.comm))
+                else:
+                    mseg_scales = K.seg_scales(stats_rows["v0"].float(), stats_rows["v1"].float(), wmax, n)
         else:
             node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
                 torch.zeros((T, 0), dtype=torch.int32, device=dev)
@@ -753,6 +757,7 @@ class ForestTrainer:
             build_slot = torch.from_numpy(slot_of).to(dev)
             id_tree = np.array([e["tree"] for e in active], dtype=np.int32)
             tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
+            hist_raw_scale = None
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
                 if use_mseg and (depth >= 1 or MSEG_L0):
                     # gather the rows of the built nodes into slot segments, then segment histograms
@@ -772,7 +777,8 @@ class ForestTrainer:
                     else:
                         Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax,
                                         mseg_scales, bins_rm=data.row_major_bins() if dev.type == "cuda" else None,
-                                        interleave=True, rec=is_rec)
+                                        interleave=True, rec=is_rec, raw=is_rec)
+                        hist_raw_scale = mseg_scales[1] if is_rec else None
                     del perm, v0p, v1p, wp
                 elif use_seg:
                     sb = np.array([[segs[a, 0], segs[a, 1], slot_of[a]] for a in build_ids], dtype=np.int64)
@@ -794,6 +800,10 @@ class ForestTrainer:
                                         build_slot, slot_tree, fm_build, B, id_tree=id_tree)
             with _tr.span("tree.allreduce", cat="comm", bytes=Hb.numel() * 8):
                 self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
+            if Hb.dtype == torch.int64:  # exact fixed-point sums (count, sum * scale) -> fp64 moments
+                Hf = Hb.double()
+                Hf[..., 1] /= hist_raw_scale
+                Hb = Hf
             _split_span = _tr.span("tree.split", depth=depth)
             _split_span.__enter__()
             # ---- assemble every active node's histogram

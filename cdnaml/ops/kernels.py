@@ -230,6 +230,19 @@ def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int, qmax_bits: int = 
     return float(2.0 ** max(-120, min(100, e)))
 
 
+def packed_scale_global(v: torch.Tensor, comm) -> float:
+    """``_packed_scale`` from the max |v| over all ranks: every rank quantises identically, so integer
+    histograms all-reduce to the same sums whatever the number of GPUs."""
+    m = float(v.abs().max().item()) if v.numel() else 0.0
+    m = comm.all_reduce_scalar(m, "max") if comm is not None else m
+    if not math.isfinite(m):
+        raise ValueError("histogram statistic contains NaN/Inf")
+    if m == 0.0:
+        return 1.0
+    e = math.floor(math.log2((2 ** 23) / m))
+    return float(2.0 ** max(-120, min(100, e)))
+
+
 def _packed_scale(v: torch.Tensor) -> float:
     """Power-of-two scale with |round(v * s)| <= 2^23 (packed count|sum LDS words)."""
     m = float(v.abs().max().item()) if v.numel() else 0.0
@@ -907,13 +920,14 @@ def _seg_work(segs: np.ndarray, chunk: int) -> np.ndarray:
 def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
              v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
              scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False,
-             rec: bool = False) -> torch.Tensor:
+             rec: bool = False, raw: bool = False) -> torch.Tensor:
     """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
 
     rec: ``perm`` holds packed int64 item records from ``codes_compact(rec_scale=scales[1])`` (v1p/wp unused;
-    GPU with ``bins_rm`` only)."""
+    GPU with ``bins_rm`` only).  raw (with rec): return the exact int64 fixed-point sums (count, sum * scales[1])
+    instead of fp64 moments, so ranks can all-reduce integers."""
     if rec:
-        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave)
+        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw)
     return _seg_hist(bins, d, B, perm, v0p, v1p, wp, segs, S, wmax, scales, bins_rm, interleave)
 
 
@@ -928,9 +942,9 @@ SEG_SPLIT4 = __import__("os").environ.get("CDNAML_SEG_SPLIT4", "0") != "0"
 SEG_PRIV_CHUNK = int(__import__("os").environ.get("CDNAML_SEG_PRIV_CHUNK", "65536"))
 
 
-def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave):
+def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False):
     G, n, _ = bins.shape
-    out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
+    out = torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
     if S == 0 or len(segs) == 0:
         return out
@@ -958,6 +972,8 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave):
                                         None, None,
                                         _ptr(wt), len(work), 1.0, qs1, _ptr(iout), _stream(bins.device)),
                "cdna_seg_hist(rec)")
+    if raw:
+        return iout
     out.copy_(iout)
     out[..., 1] /= qs1
     return out
