@@ -182,6 +182,23 @@ def find_thresholds_t(samp: torch.Tensor, max_bins: int, categorical: Dict[int, 
     return thr, nthr
 
 
+def _global_sample(session, X: torch.Tensor, max_bins: int, seed: int, row_offset: int, n_global: int):
+    """Rows sampled by Philox keyed on the GLOBAL row id (the same rows whatever the GPU count), gathered
+    from every rank: the split-candidate sample."""
+    comm = session.comm
+    n = X.shape[0]
+    target = max(max_bins * max_bins, 10000)
+    frac = min(1.0, target / max(n_global, 1))
+    if frac < 1.0:
+        u = K.uniform(n, seed ^ 0x5BD1E995, row_offset, 3, device=X.device)
+        samp = X[K.compact_mask(u < frac)]
+    else:
+        samp = X
+    if comm.distributed:
+        samp = torch.cat(comm.all_gather_varlen(samp.contiguous()))
+    return samp
+
+
 def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins: int, seed: int,
                 row_offset: int, n_global: int, missing: Optional[float] = None) -> BinnedData:
     """Global-sample quantile thresholds + device binning.
@@ -192,16 +209,21 @@ def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins:
     """
     d = X.shape[1]
     if missing is not None:
-        miss = torch.isnan(X)
-        if not math.isnan(missing):
-            miss |= X == float(missing)
-        Xm = torch.where(miss, torch.full_like(X, float("-inf")), X)
-        inner = make_binned(session, torch.where(miss, torch.full_like(X, float("nan")), X), {}, max_bins - 1,
-                            seed, row_offset, n_global, None) if max_bins > 2 else None
-        thr = np.concatenate([np.full((d, 1), -np.finfo(np.float32).max), inner.thresholds], 1)
-        nthr = inner.nthr + 1
+        # thresholds of the observed values from the (missing -> NaN) global sample; the binning kernel maps
+        # missing values to -inf -> bin 0 on the fly (no masked copies of the full matrix)
+        samp = _global_sample(session, X, max_bins - 1, seed, row_offset, n_global)
+        sm = torch.isnan(samp) if math.isnan(missing) else (torch.isnan(samp) | (samp == float(missing)))
+        samp = torch.where(sm, torch.full_like(samp, float("nan")), samp)
+        if max_bins > 2:
+            with _tr.span("tree.find_thresholds"):
+                ithr, inthr = find_thresholds_t(samp.double(), max_bins - 1, {})
+        else:
+            ithr, inthr = np.zeros((d, 0)), np.zeros(d, dtype=np.int32)
+        thr = np.concatenate([np.full((d, 1), -np.finfo(np.float32).max), ithr], 1)
+        nthr = inthr + 1
         thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
-        bins = K.binize(Xm, thr_t, torch.from_numpy(nthr).to(X.device))
+        with _tr.span("tree.binize"):
+            bins = K.binize(X, thr_t, torch.from_numpy(nthr).to(X.device), missing=float(missing))
         return BinnedData(X, bins, thr, nthr, {}, X.shape[0], n_global, row_offset, d, max_bins, True)
     for f, k in categorical.items():
         if k > max_bins:
@@ -212,17 +234,8 @@ def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins:
                 f"more training examples.")
     if max_bins > 256:
         raise IllegalArgumentException("maxBins must be <= 256 on this engine (uint8 bins)")
-    comm = session.comm
     n = X.shape[0]
-    target = max(max_bins * max_bins, 10000)
-    frac = min(1.0, target / max(n_global, 1))
-    if frac < 1.0:
-        u = K.uniform(n, seed ^ 0x5BD1E995, row_offset, 3, device=X.device)
-        samp = X[u < frac]
-    else:
-        samp = X
-    if comm.distributed:
-        samp = torch.cat(comm.all_gather_varlen(samp.contiguous()))
+    samp = _global_sample(session, X, max_bins, seed, row_offset, n_global)
     with _tr.span("tree.find_thresholds"):
         thr, nthr = find_thresholds_t(samp.double(), max_bins, categorical)
     thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
@@ -553,9 +566,9 @@ class ForestTrainer:
 
     # ------------------------------------------------------------ split scan
     def _native_split(self, dev) -> bool:
-        """K6 kernel for regression variance / XGBoost gains without categorical or missing-value bins."""
+        """K6 kernel for regression variance / XGBoost gains (incl. missing-value bins), no categoricals."""
         return (NATIVE_SPLIT and dev.type == "cuda" and not self.classification and not self.data.categorical and
-                not (self.p.impurity == "xgb" and self.data.missing_bin) and self.stats_k == 2)
+                self.stats_k == 2)
 
     def _nthr_dev(self, dev):
         t = getattr(self, "_nthr_t", None)
@@ -819,11 +832,12 @@ class ForestTrainer:
             masks_t = torch.from_numpy(masks_np.view(np.int32)).to(dev) if masks_np is not None else None
             if self._native_split(dev):
                 # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
+                mb = p.impurity == "xgb" and self.data.missing_bin
                 so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
-                                       p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight)
+                                       p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight, missing_bin=mb)
                 gain, bf, bb = so[:, 0], so[:, 1].long(), so[:, 2].long()
                 lst, rst = so[:, 3:5], so[:, 5:7]
-                order, cat_feats, miss_right = None, [], None
+                order, cat_feats, miss_right = None, [], (so[:, 7] > 0.5 if mb else None)
             else:
                 tot = self._node_stats(H, None)
                 gain, bf, bb, lst, rst, order, cat_feats, miss_right = self._best_splits(H, tot, masks_t)

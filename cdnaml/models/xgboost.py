@@ -333,12 +333,7 @@ class _XgbModelBase(Model):
             self._dev[key] = (thr, torch.from_numpy(self._nthr).to(dev))
         thr, nthr = self._dev[key]
         Xf = X.float()
-        mv = self.getMissing()
-        miss = torch.isnan(Xf)
-        if not math.isnan(mv):
-            miss |= Xf == float(mv)
-        Xm = torch.where(miss, torch.full_like(Xf, float("-inf")), Xf).contiguous()
-        bins = K.binize(Xm, thr, nthr)
+        bins = K.binize(Xf, thr, nthr, missing=float(self.getMissing()))  # missing -> bin 0 inside the kernel
         eta = self.getLearning_rate()
         F = torch.full((n, self._n_out), self._base, dtype=torch.float32, device=dev)
         for t in range(len(self._forest.roots)):

@@ -65,7 +65,8 @@ _SIGS = {
     "cdna_gram_workspace": ([c_int64, c_int, c_int], c_int64),
     "cdna_gram": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int,
                    c_void_p], c_int),
-    "cdna_binize": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_int, c_void_p, c_void_p], c_int),
+    "cdna_binize": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p],
+                    c_int),
     "cdna_hist_moments": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p], c_int),
@@ -93,8 +94,8 @@ _SIGS = {
     "cdna_bins_row_major": ([c_void_p, c_int64, c_int, c_void_p, c_void_p], c_int),
     "cdna_partition6": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p], c_int),
-    "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_double, c_double, c_double,
-                         c_double, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double,
+                         c_double, c_double, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_compact_mask": ([c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_col_moments": ([c_int, c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_void_p],
                          c_int),

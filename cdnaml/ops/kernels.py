@@ -134,11 +134,13 @@ def _binize_lut(thr: torch.Tensor, nthr: torch.Tensor):
     return (torch.from_numpy(best[0]).to(dev), torch.from_numpy(best[1]).to(dev), best[2], best[3])
 
 
-def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor) -> torch.Tensor:
+def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Optional[float] = None) -> torch.Tensor:
     """Raw features -> uint8 bins in feature-group-major layout [G, n, 8].
 
     Continuous feature f: bin = #{thr[f, :nthr[f]] < x}; NaN -> nthr[f].
     Categorical feature (nthr[f] < 0): bin = clamp(int(x), 0, 255).
+    missing (XGBoost): values that are NaN or equal ``missing`` are binned as -inf (bin 0 when the
+    thresholds start at -FLT_MAX), without materialising a masked copy of X.
     """
     n, d = X.shape
     G = (d + 7) // 8
@@ -149,8 +151,10 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor) -> torch.Tens
         thr = thr.float().contiguous()
         nthr = nthr.int().contiguous()
         out = torch.empty((G, n, 8), dtype=torch.uint8, device=X.device)
+        miss_on = missing is not None
+        miss_val = float("nan") if (missing is None or math.isnan(missing)) else float(missing)
         if n:
-            lut = _binize_lut(thr, nthr) if BINIZE_LUT else None
+            lut = _binize_lut(thr, nthr) if (BINIZE_LUT and not miss_on) else None
             if lut is not None:
                 lut_t, losc_t, C, M = lut
                 rc = _lib.lib().cdna_binize_lut(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax,
@@ -159,11 +163,14 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor) -> torch.Tens
                     return out
                 if rc != 1:  # 1 = hipErrorInvalidValue: LDS budget, use the search kernel
                     _lib.check(rc, "cdna_binize_lut")
-            _lib.check(_lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, _ptr(out),
-                                              _stream(X.device)), "cdna_binize")
+            _lib.check(_lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, int(miss_on),
+                                              miss_val, _ptr(out), _stream(X.device)), "cdna_binize")
         return out
     out = torch.zeros((G, n, 8), dtype=torch.uint8)
     Xf = X.float()
+    if missing is not None:
+        miss = torch.isnan(Xf) if math.isnan(missing) else (torch.isnan(Xf) | (Xf == float(missing)))
+        Xf = torch.where(miss, torch.full_like(Xf, float("-inf")), Xf)
     for f in range(d):
         nt = int(nthr[f])
         x = Xf[:, f]
@@ -1421,10 +1428,11 @@ def partition_dest(dest: torch.Tensor, W: int):
 
 # ------------------------------------------------------------ K6 (split.hip)
 def split_scan(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor], kind: int, min_inst: float,
-               reg_lambda: float = 1.0, gamma: float = 0.0, min_child_weight: float = 1.0):
+               reg_lambda: float = 1.0, gamma: float = 0.0, min_child_weight: float = 1.0,
+               missing_bin: bool = False):
     """Best split per node of level histograms H [A, d, B, 2] (fp64) -> (out [A, 8], tot [A, 2]).
 
-    out = (gain, feature, bin, left0, left1, right0, right1, 0); gain -inf when no legal split.
+    out = (gain, feature, bin, left0, left1, right0, right1, missing-goes-right); gain -inf when no legal split.
     kind 0: variance gain on (weight, sum); kind 1: XGBoost gain on (hess, grad)."""
     A, d, B, k = H.shape
     assert k == 2 and H.dtype == torch.float64 and _native(H)
@@ -1434,7 +1442,8 @@ def split_scan(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor
     nt = nthr.to(device=H.device, dtype=torch.int32).contiguous()
     m = None if masks is None else masks.to(device=H.device, dtype=torch.int32).contiguous()
     mw = 0 if m is None else m.shape[1]
-    _lib.check(_lib.lib().cdna_split_scan(_ptr(Hc), _ptr(nt), _ptr(m), mw, A, d, B, kind, float(min_inst),
+    _lib.check(_lib.lib().cdna_split_scan(_ptr(Hc), _ptr(nt), _ptr(m), mw, A, d, B, kind, int(missing_bin),
+                                          float(min_inst),
                                           float(reg_lambda), float(gamma), float(min_child_weight), _ptr(out),
                                           _ptr(tot), _stream(H.device)), "cdna_split_scan")
     return out, tot

@@ -11,9 +11,10 @@
 // every legal threshold; a block argmax picks the best (gain, feature, bin)
 // with ties going to the lowest flat index f * B + b (torch.argmax order).
 //
-// Regression variance gain and XGBoost's second-order gain are covered;
-// categorical features, classification impurities and missing-value
-// directions stay on the torch path (cdnaml/models/tree/engine.py).
+// Regression variance gain and XGBoost's second-order gain (with the
+// sparsity-aware missing direction: bin 0 = missing, tried on both sides)
+// are covered; categorical features and classification impurities stay on
+// the torch path (cdnaml/models/tree/engine.py).
 #include "common.h"
 
 namespace {
@@ -27,6 +28,7 @@ struct SplitArgs {
   int mw;
   int A, d, B;
   int kind;              // 0 variance (stats: weight, sum), 1 xgb (stats: hess, grad)
+  int missing_bin;       // xgb: bin 0 holds missing values; also try sending them right (left = bins 1..b)
   double min_inst, lambda, gamma, mcw;
   double* out;           // [A][8]: gain, f, b, left0, left1, right0, right1, -
   double* tot_out;       // [A][2] node totals
@@ -86,12 +88,16 @@ __global__ __launch_bounds__(kThreads) void split_scan_kernel(const SplitArgs a)
   const double t0 = s_t0[0], t1 = s_t1[0];
   __syncthreads();
   // pass 2: every legal threshold of every (sampled) feature
+  // candidate keys: f * B + b (missing rows left with bin 0), then d * B + f * B + b (missing rows right);
+  // ties go to the lower key, as torch.argmax over the concatenated gains
   double best = -__builtin_inf();
   int bk = 0x7FFFFFFF;
+  const int off2 = a.d * a.B;
   for (int f = threadIdx.x; f < a.d; f += kThreads) {
     if (a.mask && !((a.mask[(int64_t)node * a.mw + (f >> 5)] >> (f & 31)) & 1u)) continue;
     const int lim = a.nthr[f] < 0 ? 0 : a.nthr[f];
     const double* hf = Hn + (int64_t)f * a.B * 2;
+    const double m0 = hf[0], m1 = hf[1];  // bin 0 (missing values when missing_bin)
     double l0 = 0.0, l1 = 0.0;
     for (int b = 0; b < a.B && b < lim; ++b) {
       l0 += hf[2 * b];
@@ -101,6 +107,14 @@ __global__ __launch_bounds__(kThreads) void split_scan_kernel(const SplitArgs a)
       if (ok && g == g && g != __builtin_inf() && g != -__builtin_inf() && g > best) {
         best = g;
         bk = f * a.B + b;
+      }
+      if (a.missing_bin && b >= 1) {
+        const double q0 = l0 - m0, q1 = l1 - m1;
+        const double g2 = gain_of(a, q0, q1, t0 - q0, t1 - q1, t0, t1, &ok);
+        if (ok && g2 == g2 && g2 != __builtin_inf() && g2 != -__builtin_inf() && g2 > best) {
+          best = g2;
+          bk = off2 + f * a.B + b;
+        }
       }
     }
   }
@@ -119,8 +133,10 @@ __global__ __launch_bounds__(kThreads) void split_scan_kernel(const SplitArgs a)
   }
   if (threadIdx.x == 0) {
     double* o = a.out + (int64_t)node * 8;
-    const int k = s_k[0];
-    const bool found = k != 0x7FFFFFFF;
+    const int k0 = s_k[0];
+    const bool found = k0 != 0x7FFFFFFF;
+    const bool mr = found && k0 >= off2;
+    const int k = mr ? k0 - off2 : k0;
     const int f = found ? k / a.B : 0, b = found ? k - (k / a.B) * a.B : 0;
     double l0 = 0.0, l1 = 0.0;
     if (found) {
@@ -128,6 +144,10 @@ __global__ __launch_bounds__(kThreads) void split_scan_kernel(const SplitArgs a)
       for (int q = 0; q <= b; ++q) {
         l0 += hf[2 * q];
         l1 += hf[2 * q + 1];
+      }
+      if (mr) {
+        l0 -= hf[0];
+        l1 -= hf[1];
       }
     }
     o[0] = found ? s_g[0] : -__builtin_inf();
@@ -137,7 +157,7 @@ __global__ __launch_bounds__(kThreads) void split_scan_kernel(const SplitArgs a)
     o[4] = l1;
     o[5] = t0 - l0;
     o[6] = t1 - l1;
-    o[7] = 0.0;
+    o[7] = mr ? 1.0 : 0.0;
     a.tot_out[node * 2] = t0;
     a.tot_out[node * 2 + 1] = t1;
   }
@@ -147,11 +167,12 @@ __global__ __launch_bounds__(kThreads) void split_scan_kernel(const SplitArgs a)
 
 // kind: 0 = variance (regression trees), 1 = XGBoost gain.  out [A][8], tot_out [A][2] (fp64).
 CDNA_API int cdna_split_scan(const double* H, const int* nthr, const uint32_t* mask, int mw, int A, int d, int B,
-                             int kind, double min_inst, double lambda, double gamma, double mcw, double* out,
-                             double* tot_out, hipStream_t st) {
+                             int kind, int missing_bin, double min_inst, double lambda, double gamma, double mcw,
+                             double* out, double* tot_out, hipStream_t st) {
   if (A <= 0) return 0;
-  if (d <= 0 || B <= 0 || (kind != 0 && kind != 1)) return (int)hipErrorInvalidValue;
-  SplitArgs a{H, nthr, mask, mw, A, d, B, kind, min_inst, lambda, gamma, mcw, out, tot_out};
+  if (d <= 0 || B <= 0 || (kind != 0 && kind != 1) || (missing_bin && kind != 1)) return (int)hipErrorInvalidValue;
+  if ((int64_t)2 * d * B >= 0x7FFFFFFF) return (int)hipErrorInvalidValue;
+  SplitArgs a{H, nthr, mask, mw, A, d, B, kind, missing_bin, min_inst, lambda, gamma, mcw, out, tot_out};
   hipLaunchKernelGGL(split_scan_kernel, dim3((unsigned)A), dim3(kThreads), 0, st, a);
   return (int)hipGetLastError();
 }

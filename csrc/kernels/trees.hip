@@ -29,7 +29,8 @@ namespace {
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void binize_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                      const float* __restrict__ thr, const int* __restrict__ nthr,
-                                                     int tmax, int use_lds, uint64_t* __restrict__ out) {
+                                                     int tmax, int use_lds, int miss_on, float miss_val,
+                                                     uint64_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int G = (d + 7) / 8;
   const int dp = G * 8;
@@ -47,7 +48,8 @@ __global__ __launch_bounds__(256) void binize_kernel(const float* __restrict__ X
       const int r = e / dp, f = e - r * dp;
       uint8_t b = 0;
       if (f < d) {
-        const float x = X[(r0 + r) * ldx + f];
+        float x = X[(r0 + r) * ldx + f];
+        if (miss_on && (x != x || x == miss_val)) x = -__builtin_inff();
         const int nt = nthr[f];
         if (nt < 0) {
           int c = (int)x;
@@ -85,8 +87,8 @@ __global__ __launch_bounds__(256) void binize_kernel(const float* __restrict__ X
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                       const float* __restrict__ thr, const int* __restrict__ nthr,
-                                                      int tmax, int rows_per_tile, int steps,
-                                                      uint64_t* __restrict__ out) {
+                                                      int tmax, int rows_per_tile, int steps, int miss_on,
+                                                      float miss_val, uint64_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int G = (d + 7) / 8;
   // [rows_per_tile][dp]: an odd row stride keeps the per-task x reads (lanes = rows) conflict-free; with
@@ -165,6 +167,8 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
       for (int j = 0; j < 8; ++j) {
         const int f = g * 8 + j < d ? g * 8 + j : d - 1;
         x[j] = sx[r * dp + f];
+        // XGBoost missing values (NaN or == missing) -> -inf -> bin 0 (thresholds start at -FLT_MAX)
+        if (miss_on && (x[j] != x[j] || x[j] == miss_val)) x[j] = -__builtin_inff();
         nt[j] = g * 8 + j < d ? snt[f] : 0;
         toff[j] = f * tmax - 1;
         lo[j] = 0;
@@ -761,8 +765,9 @@ inline unsigned grid_for(int64_t n, int per, unsigned cap) {
 
 }  // namespace
 
+// miss_on: values that are NaN or equal miss_val are binned as -inf (XGBoost missing-value bin 0).
 CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const float* thr, const int* nthr, int tmax,
-                         uint64_t* out, hipStream_t st) {
+                         int miss_on, float miss_val, uint64_t* out, hipStream_t st) {
   if (n <= 0) return 0;
   {
     // v2: tile of rows in LDS next to the thresholds (<= 64 KB per block)
@@ -788,7 +793,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(binize2_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(binize2_kernel, dim3(grid_for(n, rpt, 8192)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
-                         tmax > 0 ? tmax : 1, rpt, steps, out);
+                         tmax > 0 ? tmax : 1, rpt, steps, miss_on, miss_val, out);
       return (int)hipGetLastError();
     }
   }
@@ -799,7 +804,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
   const size_t lds = tile + (use_lds ? tbytes : 0);
   if (tile > 120 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(binize_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
-                     tmax, use_lds, out);
+                     tmax, use_lds, miss_on, miss_val, out);
   return (int)hipGetLastError();
 }
 

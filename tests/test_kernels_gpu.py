@@ -711,3 +711,19 @@ def test_compact_mask(dev, n, p):
     g = torch.Generator().manual_seed(n)
     m = torch.rand(n, generator=g) < p
     assert torch.equal(K.compact_mask(m.to(dev)).cpu(), torch.nonzero(m).flatten())
+
+
+@pytest.mark.parametrize("missing", [float("nan"), 0.0])
+def test_binize_missing_in_kernel(dev, missing):
+    """XGBoost missing values (NaN, or == missing) go to bin 0 inside the binning kernel."""
+    g = torch.Generator().manual_seed(6)
+    X = torch.randn(20000, 13, generator=g)
+    X[::7, 2] = float("nan")
+    X[::5, 3] = 0.0
+    thr, nthr = _thresholds(X.nan_to_num(0.0), 30)
+    thr = torch.cat([torch.full((13, 1), -torch.finfo(torch.float32).max), thr], 1)
+    nthr = nthr + 1
+    ref = K.binize(X, thr, nthr, missing=missing)
+    out = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), missing=missing).cpu()
+    assert torch.equal(out, ref)
+    assert int(out[0, ::7, 2].max()) == 0
