@@ -85,13 +85,13 @@ _SIGS = {
                     c_int, c_void_p, c_void_p], c_int),
     "cdna_hist5_max_trees": ([], c_int),
     "cdna_seg_hist": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                       c_int, c_float, c_float, c_void_p, c_void_p], c_int),
+                       c_int, c_float, c_float, c_void_p, c_int, c_void_p], c_int),
     "cdna_seg_partition": ([c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "cdna_codes_compact": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p], c_int),
-    "cdna_bins_row_major": ([c_void_p, c_int64, c_int, c_void_p, c_void_p], c_int),
+    "cdna_bins_row_major": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p], c_int),
     "cdna_partition6": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double,

@@ -615,8 +615,8 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
             return
         src, rm_bytes = bins, 0
         if bins_rm is not None:
-            assert bins_rm.shape == (n, G, 8) and bins_rm.is_contiguous()
-            src, rm_bytes = bins_rm, G * 8
+            assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
+            src, rm_bytes = bins_rm, bins_rm.shape[1] * 8
         _lib.check(_lib.lib().cdna_partition5(_ptr(src), n, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]),
                                               _ptr(args[2]), _ptr(args[3]), _ptr(args[4]), _ptr(cm),
                                               _ptr(args[5]), rm_bytes, _stream(bins.device)), "cdna_partition5")
@@ -973,12 +973,12 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
     qs1 = float(scales[1])
     wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
     iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
-    assert bins_rm.shape == (n, G, 8) and bins_rm.is_contiguous()
+    assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
     _lib.check(_lib.lib().cdna_seg_hist(1 | 4 | 16 | (32 if priv else 0) | (64 if split4 else 0), _ptr(bins_rm), n,
                                         d, B, _ptr(rec), None,
                                         None, None,
-                                        _ptr(wt), len(work), 1.0, qs1, _ptr(iout), _stream(bins.device)),
-               "cdna_seg_hist(rec)")
+                                        _ptr(wt), len(work), 1.0, qs1, _ptr(iout), bins_rm.shape[1],
+                                        _stream(bins.device)), "cdna_seg_hist(rec)")
     if raw:
         return iout
     out.copy_(iout)
@@ -1034,11 +1034,12 @@ def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optio
     iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
     mode = (1 if packed else 0) | (2 if wp is not None else 0) | (4 if bins_rm is not None else 0)
     if bins_rm is not None:
-        assert bins_rm.shape == (n, G, 8) and bins_rm.is_contiguous()
+        assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
     src = bins if bins_rm is None else bins_rm
     _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(src), n, d, B, _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp),
                                         _ptr(wt), len(work), float(qs0), float(qs1), _ptr(iout),
-                                        _stream(bins.device)), "cdna_seg_hist")
+                                        0 if bins_rm is None else bins_rm.shape[1], _stream(bins.device)),
+               "cdna_seg_hist")
     out.copy_(iout)
     if not packed:
         out[..., 0] /= qs0
@@ -1079,12 +1080,12 @@ def seg_hist_subset(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v1p:
     qs1 = (scales if scales is not None else seg_scales(None, v1p, wm, n))[1]
     if bins_rm is None:
         bins_rm = bins_row_major(bins)
-    assert bins_rm.shape == (n, G, 8) and bins_rm.is_contiguous()
+    assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
     dev = bins.device
     wt = torch.from_numpy(work.reshape(-1)).to(dev)
     ft = torch.from_numpy(feats.reshape(-1)).to(dev)
     iout = torch.zeros(out.shape, dtype=torch.int64, device=dev)
-    _lib.check(_lib.lib().cdna_seg_hist_subset(_ptr(bins_rm), n, G * 8, d, B, _ptr(perm), _ptr(v1p), _ptr(wp),
+    _lib.check(_lib.lib().cdna_seg_hist_subset(_ptr(bins_rm), n, bins_rm.shape[1] * 8, d, B, _ptr(perm), _ptr(v1p), _ptr(wp),
                                                _ptr(wt), len(work), float(qs1), _ptr(ft), m, _ptr(iout),
                                                _stream(dev)), "cdna_seg_hist_subset")
     out.copy_(iout)
@@ -1333,13 +1334,21 @@ def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1, re
     return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
 
 
-def bins_row_major(bins: torch.Tensor) -> torch.Tensor:
-    """[G, n, 8] feature-group-major bins -> row-major [n, G, 8] copy."""
+BINS_RM_PAD = __import__("os").environ.get("CDNAML_BINS_RM_PAD", "1") != "0"
+
+
+def bins_row_major(bins: torch.Tensor, pad: Optional[bool] = None) -> torch.Tensor:
+    """[G, n, 8] feature-group-major bins -> row-major [n, Gs, 8] copy.
+
+    pad (default on the GPU when G <= 16): Gs = 16, zero-filled, so every row is one aligned 128-byte line
+    (a gathered 104-byte row at d = 100 touched ~1.8 lines)."""
     G, n, _ = bins.shape
     if not _native(bins):
         return bins.permute(1, 0, 2).contiguous()
-    out = torch.empty((n, G, 8), dtype=torch.uint8, device=bins.device)
-    _lib.check(_lib.lib().cdna_bins_row_major(_ptr(bins), n, G, _ptr(out), _stream(bins.device)),
+    pad = BINS_RM_PAD if pad is None else pad
+    Gs = 16 if (pad and G <= 16) else G
+    out = torch.empty((n, Gs, 8), dtype=torch.uint8, device=bins.device)
+    _lib.check(_lib.lib().cdna_bins_row_major(_ptr(bins), n, G, Gs, _ptr(out), _stream(bins.device)),
                "cdna_bins_row_major")
     return out
 

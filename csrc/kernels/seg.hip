@@ -37,6 +37,7 @@ struct SegHistArgs {
   unsigned long long* out;  // [S][d][B][2]
   // optional packed item records (flat kernel, REC): row | weight << 31 | (q1 + 2^23) << 39 (see CompactWArgs)
   const uint64_t* rec = nullptr;
+  int rs = 0;  // row stride of the row-major bins in 8-byte words (0: G); 16 = one 128-byte line per row
 };
 
 // PACKED: one u64 atomic per update (count << 44 | sum of w * (q + 2^23)); the
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(1024) void seg_hist_rm_kernel(const SegHistArgs a, 
       const int i = i0 + u * RPI;
       const bool ok = i < len && lane_on;
       const int row = ok ? a.perm[start + i] : 0;
-      b8[u] = ok ? bins_rm[(int64_t)row * G + g] : 0ull;
+      b8[u] = ok ? bins_rm[(int64_t)row * (a.rs ? a.rs : G) + g] : 0ull;
       x1[u] = ok ? a.v1p[start + i] : 0.f;
       x0[u] = (!PACKED && ok) ? a.v0p[start + i] : 0.f;
       w[u] = ok ? (HAS_W ? (uint32_t)a.wp[start + i] : 1u) : 0u;
@@ -288,12 +289,12 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
         // one 8-byte record per item instead of perm / v1p / wp: fewer, wider loads
         const uint64_t rc = ok ? a.rec[start + i] : 0ull;
         const int row = (int)(rc & 0x7FFFFFFFull);
-        b8[u] = ok ? bins_rm[(int64_t)row * G + g0 + g] : 0ull;
+        b8[u] = ok ? bins_rm[(int64_t)row * (a.rs ? a.rs : G) + g0 + g] : 0ull;
         w[u] = (uint32_t)(rc >> 31) & 0xFFu;
         x1[u] = __int_as_float((int)(uint32_t)(rc >> 39));  // carries q1 + 2^23 (bit pattern, not a float)
       } else {
         const int row = ok ? a.perm[start + i] : 0;
-        b8[u] = ok ? bins_rm[(int64_t)row * G + g0 + g] : 0ull;
+        b8[u] = ok ? bins_rm[(int64_t)row * (a.rs ? a.rs : G) + g0 + g] : 0ull;
         x1[u] = ok ? a.v1p[start + i] : 0.f;
         w[u] = ok ? (HAS_W ? (uint32_t)a.wp[start + i] : 1u) : 0u;
       }
@@ -445,7 +446,7 @@ __global__ __launch_bounds__(256) void seg_hist_priv_kernel(const SegHistArgs a,
       const bool ok = i < len;
       const uint64_t rc = ok ? a.rec[start + i] : 0ull;
       const int row = (int)(rc & 0x7FFFFFFFull);
-      b8[u] = ok ? bins_rm[(int64_t)row * G + g] : 0ull;
+      b8[u] = ok ? bins_rm[(int64_t)row * (a.rs ? a.rs : G) + g] : 0ull;
       w[u] = (uint32_t)(rc >> 31) & 0xFFu;
       qb[u] = (uint32_t)(rc >> 39);
     }
@@ -869,15 +870,20 @@ __global__ __launch_bounds__(256) void codes_compact_w_kernel(const CompactWArgs
 // [G][n] 8-feature bin words -> row-major [n][G] (one row's words contiguous),
 // staged through LDS so both the reads and the writes are coalesced.
 __global__ __launch_bounds__(256) void bins_row_major_kernel(const uint64_t* __restrict__ bins, int64_t n, int G,
-                                                             uint64_t* __restrict__ out) {
+                                                             int Gs, uint64_t* __restrict__ out) {
   extern __shared__ uint64_t tile[];  // [256][G] (odd G strides spread the banks)
   const int64_t r0 = (int64_t)blockIdx.x * 256;
   const int rows = n - r0 < 256 ? (int)(n - r0) : 256;
   for (int g = 0; g < G; ++g)
     if (threadIdx.x < rows) tile[threadIdx.x * G + g] = bins[(int64_t)g * n + r0 + threadIdx.x];
   __syncthreads();
-  uint64_t* o = out + r0 * G;
-  for (int i = threadIdx.x; i < rows * G; i += 256) o[i] = tile[i];
+  // output rows are Gs >= G words (Gs = 16 at d <= 128: every row is one aligned 128-byte line, so a
+  // gathered row costs one line instead of ~1.8 for 104-byte rows)
+  uint64_t* o = out + r0 * Gs;
+  for (int i = threadIdx.x; i < rows * Gs; i += 256) {
+    const int r = i / Gs, g = i - r * Gs;
+    o[i] = g < G ? tile[r * G + g] : 0ull;
+  }
 }
 
 }  // namespace
@@ -890,9 +896,11 @@ __global__ __launch_bounds__(256) void bins_row_major_kernel(const uint64_t* __r
 // work: [nwork][3] {start, len, slot}; grid = nwork x ceil(d / 8).
 CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int B, const int* perm, const float* v0p,
                            const float* v1p, const uint8_t* wp, const int* work, int nwork, float qs0, float qs1,
-                           unsigned long long* out, hipStream_t st) {
+                           unsigned long long* out, int rm_stride, hipStream_t st) {
   if (nwork <= 0) return 0;
+  if (rm_stride != 0 && rm_stride < (d + 7) / 8) return (int)hipErrorInvalidValue;
   SegHistArgs a{bins, n, d, B, perm, v0p, v1p, wp, work, qs0, qs1, out};
+  a.rs = rm_stride;
   const bool packed = (mode & 1) != 0, has_w = (mode & 2) != 0;
   if ((mode & 16) && (mode & 32) && (mode & 4) && packed && B <= 64) {
     // bank-private planes: one 8-feature group per block, 16 interleaved copies
@@ -1009,11 +1017,11 @@ CDNA_API int cdna_codes_compact(int pass, const uint16_t* codes, int64_t n, int 
   return (int)hipGetLastError();
 }
 
-CDNA_API int cdna_bins_row_major(const uint64_t* bins, int64_t n, int G, uint64_t* out, hipStream_t st) {
+CDNA_API int cdna_bins_row_major(const uint64_t* bins, int64_t n, int G, int Gs, uint64_t* out, hipStream_t st) {
   if (n <= 0) return 0;
-  if (G <= 0 || G > 32) return (int)hipErrorInvalidValue;
+  if (G <= 0 || G > 32 || Gs < G) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bins_row_major_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), (size_t)256 * G * 8, st,
-                     bins, n, G, out);
+                     bins, n, G, Gs, out);
   return (int)hipGetLastError();
 }
 

@@ -396,7 +396,7 @@ def _seg_state(n, d, B, nseg, seed, weights):
 
 @pytest.mark.parametrize("packed,weights,B,d", [(True, False, 256, 100), (True, True, 40, 21), (True, True, 40, 100), (False, False, 64, 13),
                                                  (False, True, 256, 9)])
-@pytest.mark.parametrize("row_major", [False, True])
+@pytest.mark.parametrize("row_major", [False, True, "pad"])
 def test_seg_hist(dev, packed, weights, B, d, row_major):
     bins, perm, v0, v1, wp, segs = _seg_state(30000, d, B, 7, 3, weights)
     build = [0, 2, 3, 6]
@@ -406,7 +406,8 @@ def test_seg_hist(dev, packed, weights, B, d, row_major):
     bd = bins.to(dev)
     out = K.seg_hist(bd, d, B, perm.to(dev), None if v0a is None else v0a.to(dev), v1.to(dev),
                      None if wp is None else wp.to(dev), sb, len(build), 3,
-                     bins_rm=bd.permute(1, 0, 2).contiguous() if row_major else None).cpu()
+                     bins_rm=(K.bins_row_major(bd, pad=True) if row_major == "pad" else
+                              bd.permute(1, 0, 2).contiguous() if row_major else None)).cpu()
     assert torch.allclose(out, ref, rtol=1e-6, atol=1e-3)
 
 
@@ -506,8 +507,11 @@ def test_codes_compact(dev, monkeypatch, wave_owned):
 
 def test_bins_row_major(dev):
     bins = torch.randint(0, 255, (13, 100003, 8), dtype=torch.uint8)
-    out = K.bins_row_major(bins.to(dev)).cpu()
-    assert torch.equal(out, bins.permute(1, 0, 2).contiguous())
+    ref = bins.permute(1, 0, 2).contiguous()
+    assert torch.equal(K.bins_row_major(bins.to(dev), pad=False).cpu(), ref)
+    padded = K.bins_row_major(bins.to(dev), pad=True).cpu()
+    assert padded.shape == (100003, 16, 8)
+    assert torch.equal(padded[:, :13], ref) and int(padded[:, 13:].abs().sum()) == 0
 
 
 def test_mseg_forest_matches_codes_forest(dev, monkeypatch):
