@@ -887,7 +887,7 @@ def logistic_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b: float,
 
 
 # ------------------------------------------------------------ segment mode (seg.hip)
-SEG_HIST_CHUNK = 262144
+SEG_HIST_CHUNK = int(__import__("os").environ.get("CDNAML_SEG_HIST_CHUNK", "262144"))
 # row-major bins copy for segment histograms (one cache line per row instead of one per 8-feature group)
 SEG_ROW_MAJOR = __import__("os").environ.get("CDNAML_SEG_ROW_MAJOR", "1") != "0"
 SEG_PART_CHUNK = 8192
