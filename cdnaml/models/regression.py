@@ -470,7 +470,7 @@ class _TreeModelBase(Model):
 
     @property
     def depth(self):
-        return max((self._forest.tree_depth(t) for t in range(len(self._forest.roots))), default=0)
+        return int(self._forest.tree_depths().max()) if self._forest.roots else 0
 
     def toDebugString_tree(self, t, names=None):
         f = self._forest

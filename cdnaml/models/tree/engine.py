@@ -282,6 +282,38 @@ class Forest:
         self.depth.append(depth)
         return i
 
+    def add_many(self, values: np.ndarray, weights: np.ndarray, depth: int, impurity: np.ndarray) -> np.ndarray:
+        """Append N leaf nodes at once (values [N, k]); returns their ids."""
+        i0, N = len(self.feat), len(weights)
+        values = np.asarray(values, dtype=np.float64).reshape(N, -1)
+        self.feat.extend([-1] * N)
+        self.thr.extend([0.0] * N)
+        self.bin.extend([0] * N)
+        self.left.extend([-1] * N)
+        self.right.extend([-1] * N)
+        self.catmask.extend(list(np.zeros((N, 8), dtype=np.uint32)))
+        self.is_cat.extend([False] * N)
+        self.value.extend(list(values))
+        self.weight.extend(np.asarray(weights, dtype=np.float64).tolist())
+        self.gain.extend([0.0] * N)
+        self.impurity.extend(np.asarray(impurity, dtype=np.float64).tolist())
+        self.depth.extend([depth] * N)
+        return np.arange(i0, i0 + N, dtype=np.int64)
+
+    def set_splits(self, fids, feats, gains, bins, thrs, has_thr, lefts, rights) -> None:
+        """Turn leaves ``fids`` into split nodes (numeric ones, ``has_thr``, also get bin + threshold)."""
+        for fid, f, g, b, t, h, l_, r_ in zip(np.asarray(fids).tolist(), np.asarray(feats).tolist(),
+                                              np.asarray(gains).tolist(), np.asarray(bins).tolist(),
+                                              np.asarray(thrs).tolist(), np.asarray(has_thr).tolist(),
+                                              np.asarray(lefts).tolist(), np.asarray(rights).tolist()):
+            self.feat[fid] = f
+            self.gain[fid] = g
+            self.left[fid] = l_
+            self.right[fid] = r_
+            if h:
+                self.bin[fid] = b
+                self.thr[fid] = t
+
     @property
     def num_nodes(self):
         return len(self.feat)
@@ -294,6 +326,40 @@ class Forest:
             if self.feat[i] >= 0:
                 stack.extend([self.right[i], self.left[i]])
         return out
+
+    def _layout(self):
+        """Per node: tree index (-1 if unreachable), heap slot (root 0, children 2i+1 / 2i+2) and, per tree,
+        its depth -- one vectorised sweep per level instead of a Python walk per node."""
+        N = len(self.feat)
+        tree_of = np.full(N, -1, dtype=np.int64)
+        slot = np.zeros(N, dtype=np.int64)
+        T = len(self.roots)
+        dep = np.zeros(T, dtype=np.int64)
+        if T == 0:
+            return tree_of, slot, dep
+        feat = np.asarray(self.feat, dtype=np.int64)
+        left = np.asarray(self.left, dtype=np.int64)
+        right = np.asarray(self.right, dtype=np.int64)
+        fr = np.asarray(self.roots, dtype=np.int64)
+        tree_of[fr] = np.arange(T)
+        level = 0
+        while len(fr):
+            dep[tree_of[fr]] = level
+            inner = fr[feat[fr] >= 0]
+            if not len(inner):
+                break
+            lc, rc = left[inner], right[inner]
+            tree_of[lc] = tree_of[inner]
+            tree_of[rc] = tree_of[inner]
+            if level < 62:
+                slot[lc] = 2 * slot[inner] + 1
+                slot[rc] = 2 * slot[inner] + 2
+            fr = np.concatenate([lc, rc])
+            level += 1
+        return tree_of, slot, dep
+
+    def tree_depths(self) -> np.ndarray:
+        return self._layout()[2]
 
     def tree_depth(self, t: int) -> int:
         return max(self.depth[i] for i in self.tree_nodes(t)) - self.depth[self.roots[t]]
@@ -357,27 +423,31 @@ class Forest:
         if key in self._dev:
             return self._dev[key]
         res = None
-        D = max((self.tree_depth(t) for t in range(len(self.roots))), default=0)
+        tree_of, slot, dep = self._layout()
+        D = int(dep.max()) if self.roots else 0
         if self.K == 1 and self.roots and D <= 8:
             S = 2 ** (D + 1) - 1
             heap = np.zeros((len(self.roots), S, 2), dtype=np.int32)
             heap[:, :, 0] = -1
-            masks = []
-            for t, r in enumerate(self.roots):
-                stack = [(r, 0)]
-                while stack:
-                    i, h = stack.pop()
-                    if self.feat[i] < 0:
-                        v = self.value[i][0] if values_kind == "value" else self.value[i][0] * self.weight[i]
-                        heap[t, h] = (-1, np.array([v], dtype=np.float32).view(np.int32)[0])
-                        continue
-                    if self.is_cat[i]:
-                        heap[t, h] = (-(self.feat[i] + 2), len(masks))
-                        masks.append(self.catmask[i].view(np.int32))
-                    else:
-                        heap[t, h] = (self.feat[i], np.array([self.thr[i]], dtype=np.float32).view(np.int32)[0])
-                    stack.append((self.left[i], 2 * h + 1))
-                    stack.append((self.right[i], 2 * h + 2))
+            feat = np.asarray(self.feat, dtype=np.int32)
+            live = np.nonzero(tree_of >= 0)[0]
+            lt, ls = tree_of[live], slot[live]
+            fl = feat[live]
+            leaf = fl < 0
+            v = np.array([self.value[i][0] for i in live[leaf].tolist()], dtype=np.float64)
+            if values_kind != "value":
+                v = v * np.asarray(self.weight, dtype=np.float64)[live[leaf]]
+            heap[lt[leaf], ls[leaf], 1] = v.astype(np.float32).view(np.int32)
+            sp = ~leaf
+            isc = np.asarray(self.is_cat, dtype=bool)[live] & sp
+            num = sp & ~isc
+            heap[lt[num], ls[num], 0] = fl[num]
+            heap[lt[num], ls[num], 1] = np.asarray(self.thr, dtype=np.float64)[live[num]].astype(
+                np.float32).view(np.int32)
+            cat_ids = live[isc]
+            masks = [self.catmask[i].view(np.int32) for i in cat_ids.tolist()]
+            heap[lt[isc], ls[isc], 0] = -(fl[isc] + 2)
+            heap[lt[isc], ls[isc], 1] = np.arange(len(cat_ids), dtype=np.int32)
             res = (torch.from_numpy(heap).to(device), D,
                    torch.from_numpy(np.concatenate(masks) if masks else np.zeros(8, np.int32)).to(device))
         self._dev[key] = res
@@ -554,6 +624,31 @@ class ForestTrainer:
             return np.array([-G / (H + self.p.reg_lambda)])
         W, S = st[0], st[1]
         return np.array([S / W if W > 0 else 0.0])
+
+    def _weights_v(self, st: np.ndarray) -> np.ndarray:
+        """Node weights of stats rows [N, k]."""
+        if st.shape[0] == 0:
+            return np.zeros(0)
+        return st.sum(1) if self.classification else st[:, 0].astype(np.float64)
+
+    def _leaf_values_v(self, st: np.ndarray) -> np.ndarray:
+        """``_leaf_value`` of stats rows [N, k] -> [N, k_out]."""
+        N = st.shape[0]
+        if self.classification:
+            W = st.sum(1, keepdims=True)
+            with np.errstate(invalid="ignore", divide="ignore"):
+                return np.where(W > 0, st / np.where(W > 0, W, 1.0), 1.0 / max(self.C, 1))
+        if N == 0:
+            return np.zeros((0, 1))
+        if self.p.impurity == "xgb":
+            return (-st[:, 1] / (st[:, 0] + self.p.reg_lambda))[:, None]
+        W, S = st[:, 0], st[:, 1]
+        return np.where(W > 0, S / np.where(W > 0, W, 1.0), 0.0)[:, None]
+
+    def _impurities_v(self, st: np.ndarray) -> np.ndarray:
+        if self.classification and st.shape[0]:
+            return _impurity_from_counts(torch.from_numpy(np.ascontiguousarray(st)), self.p.impurity).double().numpy()
+        return np.full(st.shape[0], np.nan)
 
     def _weight(self, st: np.ndarray) -> float:
         return float(st.sum()) if self.classification else float(st[0])
@@ -734,41 +829,43 @@ class ForestTrainer:
         else:
             node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
                 torch.zeros((T, 0), dtype=torch.int32, device=dev)
-        # active entries: dict(tree, fid (forest node idx), key, mask, parent_hist_idx, build, stats)
-        active = [{"tree": t, "fid": None, "key": 1, "depth": 0, "stats": None, "sib": None, "parent": None}
-                  for t in range(T)]
+        # the level's active nodes as a struct of arrays (host): tree, forest id, heap key, stats [A, k],
+        # sibling / parent positions (-1 = none).  The per-level host work between the split decisions'
+        # device->host copy and the next level's launches is a few vectorised numpy ops, not a per-node
+        # Python loop (that loop idled the GPU for 0.2-2.5 ms per level at 20 trees x 2^L nodes)
+        a_tree = np.arange(T, dtype=np.int32)
+        a_fid = np.full(T, -1, dtype=np.int64)
+        a_key = np.ones(T, dtype=np.uint64)
+        a_stats = np.zeros((T, 0))
+        a_sib = np.full(T, -1, dtype=np.int64)
+        a_parent = np.full(T, -1, dtype=np.int64)
         prev_hist = None  # [A_prev, d, B, k] histograms of last level's split nodes
-        mw = (d + 31) // 32
         root_ids = [None] * T
         for depth in range(p.max_depth + 1):
-            if not active:
+            A = len(a_tree)
+            if A == 0:
                 break
-            A = len(active)
             # ---- decide which active nodes get a histogram built
-            if subtract:
-                build = [True] * A
-                for a, e in enumerate(active):
-                    s = e["sib"]
-                    if s is not None and e["parent"] is not None:
-                        # build only the smaller of two active siblings
-                        if self._weight(e["stats"]) > self._weight(active[s]["stats"]) or \
-                                (self._weight(e["stats"]) == self._weight(active[s]["stats"]) and a > s):
-                            build[a] = False
-            else:
-                build = [True] * A
-            build_ids = [a for a in range(A) if build[a]]
+            build = np.ones(A, dtype=bool)
+            if subtract and depth > 0:
+                # build only the smaller of two active siblings (ties: the first one)
+                has = np.nonzero((a_sib >= 0) & (a_parent >= 0))[0]
+                w_all = self._weights_v(a_stats)
+                wa, ws = w_all[has], w_all[a_sib[has]]
+                lose = (wa > ws) | ((wa == ws) & (has > a_sib[has]))
+                build[has[lose]] = False
+            build_ids = np.nonzero(build)[0]
             slot_of = np.full(A, -1, dtype=np.int32)
             slot_of[build_ids] = np.arange(len(build_ids), dtype=np.int32)
-            slot_tree = np.array([active[a]["tree"] for a in build_ids], dtype=np.int32)
+            slot_tree = a_tree[build_ids]
             masks_np = None
             if need_masks:
-                masks_np = self._feature_masks(np.array([e["tree"] for e in active], dtype=np.uint64),
-                                               np.array([e["key"] for e in active], dtype=np.uint64))
+                masks_np = self._feature_masks(a_tree.astype(np.uint64), a_key)
             fm_build = None
             if masked:
-                fm_build = torch.from_numpy(masks_np[build_ids].view(np.int32)).to(dev)
+                fm_build = torch.from_numpy(np.ascontiguousarray(masks_np[build_ids]).view(np.int32)).to(dev)
             build_slot = torch.from_numpy(slot_of).to(dev)
-            id_tree = np.array([e["tree"] for e in active], dtype=np.int32)
+            id_tree = a_tree
             tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
             hist_raw_scale = None
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
@@ -794,7 +891,7 @@ class ForestTrainer:
                         hist_raw_scale = mseg_scales[1] if is_rec else None
                     del perm, v0p, v1p, wp
                 elif use_seg:
-                    sb = np.array([[segs[a, 0], segs[a, 1], slot_of[a]] for a in build_ids], dtype=np.int64)
+                    sb = np.stack([segs[build_ids, 0], segs[build_ids, 1], slot_of[build_ids].astype(np.int64)], 1)
                     Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax, seg_scales,
                                     # sparse node segments (>= 4 built nodes) gather whole rows from the
                                     # row-major copy; dense shallow levels stream the [G][n] layout
@@ -820,14 +917,16 @@ class ForestTrainer:
             _split_span = _tr.span("tree.split", depth=depth)
             _split_span.__enter__()
             # ---- assemble every active node's histogram
-            H = torch.empty((A, d, B, self.stats_k), dtype=torch.float64, device=dev)
-            if build_ids:
-                H[torch.tensor(build_ids, device=dev)] = Hb
-            derived = [a for a in range(A) if not build[a]]
-            if derived:
-                di = torch.tensor(derived, device=dev)
-                par = torch.tensor([active[a]["parent"] for a in derived], device=dev)
-                sib = torch.tensor([active[a]["sib"] for a in derived], device=dev)
+            derived = np.nonzero(~build)[0]
+            if len(derived) == 0:
+                H = Hb
+            else:
+                H = torch.empty((A, d, B, self.stats_k), dtype=torch.float64, device=dev)
+                if len(build_ids):
+                    H[torch.from_numpy(build_ids).to(dev)] = Hb
+                di = torch.from_numpy(derived).to(dev)
+                par = torch.from_numpy(a_parent[derived]).to(dev)
+                sib = torch.from_numpy(a_sib[derived]).to(dev)
                 H[di] = prev_hist[par] - H[sib]
             masks_t = torch.from_numpy(masks_np.view(np.int32)).to(dev) if masks_np is not None else None
             if self._native_split(dev):
@@ -857,96 +956,97 @@ class ForestTrainer:
                 mr_h = host[:, c0] != 0
                 c0 += 1
             if depth == 0:
-                for a, e in enumerate(active):
-                    e["stats"] = host[a, c0:c0 + tot.shape[1]].copy()
+                a_stats = host[:, c0:c0 + tot.shape[1]].copy()
             order_h = order.cpu().numpy() if order is not None else None
             _split_span.__exit__(None, None, None)
             # ---- create forest nodes for the active set, decide splits
+            if depth == 0:
+                a_fid = forest.add_many(self._leaf_values_v(a_stats), self._weights_v(a_stats), depth,
+                                        self._impurities_v(a_stats))
+                for t_, fid_ in zip(a_tree.tolist(), a_fid.tolist()):
+                    root_ids[t_] = fid_
+            W_a = self._weights_v(a_stats)
+            with np.errstate(invalid="ignore"):
+                can = np.isfinite(gain_h) & (gain_h > 0) & (gain_h >= p.min_info_gain) & \
+                    (W_a >= 2 * p.min_instances)
+            if depth >= p.max_depth:
+                can[:] = False
+            sp = np.nonzero(can)[0]
             split_feat = np.full(A, -1, dtype=np.int32)
             split_bin = np.zeros(A, dtype=np.int32)
             cat_off = np.full(A, -1, dtype=np.int32)
             cat_masks = []
             child = np.full(2 * A, -1, dtype=np.int32)
-            nxt = []
-            for a, e in enumerate(active):
-                st = e["stats"]
-                if e["fid"] is None:
-                    fid = forest.add(self._leaf_value(st), self._weight(st), depth, self._impurity(st))
-                    e["fid"] = fid
-                    if depth == 0:
-                        root_ids[e["tree"]] = fid
-                fid = e["fid"]
-                g = float(gain_h[a])
-                W = self._weight(st)
-                can_split = depth < p.max_depth and np.isfinite(g) and g > 0 and g >= p.min_info_gain and \
-                    W >= 2 * p.min_instances
-                if not can_split:
-                    continue
-                f = int(bf_h[a])
-                b = int(bb_h[a])
-                forest.feat[fid] = f
-                forest.gain[fid] = g
-                if f in self.data.categorical:
-                    ci = cat_feats.index(f)
-                    left_cats = order_h[a, ci, : b + 1]
-                    m = np.zeros(8, dtype=np.uint32)
-                    for c in left_cats:
-                        m[int(c) >> 5] |= np.uint32(1) << np.uint32(int(c) & 31)
-                    forest.is_cat[fid] = True
-                    forest.catmask[fid] = m
+            f_sp, b_sp, fid_sp = bf_h[sp], bb_h[sp], a_fid[sp]
+            thr_sp = np.zeros(len(sp))
+            plain = np.ones(len(sp), dtype=bool)
+            if self.data.categorical or mr_h is not None:
+                for j, a in enumerate(sp.tolist()):
+                    f, b = int(f_sp[j]), int(b_sp[j])
+                    if f in self.data.categorical:
+                        ci = cat_feats.index(f)
+                        m = np.zeros(8, dtype=np.uint32)
+                        for c in order_h[a, ci, : b + 1]:
+                            m[int(c) >> 5] |= np.uint32(1) << np.uint32(int(c) & 31)
+                    elif mr_h is not None and mr_h[a]:
+                        # missing (bin 0) goes right: left = bins 1..b, expressed as a bin-set split
+                        m = np.zeros(8, dtype=np.uint32)
+                        for c in range(1, b + 1):
+                            m[c >> 5] |= np.uint32(1) << np.uint32(c & 31)
+                        forest.bin[int(fid_sp[j])] = b
+                        thr_sp[j] = float(self.data.thresholds[f, b])
+                    else:
+                        continue
+                    plain[j] = False
+                    forest.is_cat[int(fid_sp[j])] = True
+                    forest.catmask[int(fid_sp[j])] = m
                     cat_off[a] = len(cat_masks)
                     cat_masks.append(m)
-                elif mr_h is not None and mr_h[a]:
-                    # missing (bin 0) goes right: left = bins 1..b, expressed as a bin-set split
-                    m = np.zeros(8, dtype=np.uint32)
-                    for c in range(1, b + 1):
-                        m[c >> 5] |= np.uint32(1) << np.uint32(c & 31)
-                    forest.is_cat[fid] = True
-                    forest.catmask[fid] = m
-                    forest.bin[fid] = b
-                    forest.thr[fid] = float(self.data.thresholds[f, b])
-                    cat_off[a] = len(cat_masks)
-                    cat_masks.append(m)
-                else:
-                    forest.bin[fid] = b
-                    forest.thr[fid] = float(self.data.thresholds[f, b])
-                    split_bin[a] = b
-                split_feat[a] = f
-                ls, rs = lst_h[a], rst_h[a]
-                lid = forest.add(self._leaf_value(ls), self._weight(ls), depth + 1, self._impurity(ls))
-                rid = forest.add(self._leaf_value(rs), self._weight(rs), depth + 1, self._impurity(rs))
-                forest.left[fid], forest.right[fid] = lid, rid
-                for side, (cid, cst) in enumerate(((lid, ls), (rid, rs))):
-                    cw = self._weight(cst)
-                    leaf = depth + 1 >= p.max_depth or cw < 2 * p.min_instances
-                    if self.classification and not leaf:
-                        leaf = int((cst > 0).sum()) <= 1  # pure node
-                    if not leaf:
-                        child[2 * a + side] = len(nxt)
-                        nxt.append({"tree": e["tree"], "fid": cid, "key": e["key"] * 2 + side, "depth": depth + 1,
-                                    "stats": cst, "sib": None, "parent": a, "side": side})
-            # siblings (both children active) for subtraction
-            by_parent: Dict[int, List[int]] = {}
-            for i, e in enumerate(nxt):
-                by_parent.setdefault(e["parent"], []).append(i)
-            for par, kids in by_parent.items():
-                if len(kids) == 2:
-                    nxt[kids[0]]["sib"], nxt[kids[1]]["sib"] = kids[1], kids[0]
-                else:
-                    nxt[kids[0]]["sib"] = None
-                    if subtract:
-                        nxt[kids[0]]["parent"] = None  # single child: build directly
-            if nxt:
+            cat_f = np.array([f in self.data.categorical for f in f_sp.tolist()], dtype=bool) if \
+                self.data.categorical else np.zeros(len(sp), dtype=bool)
+            num = ~cat_f  # numeric splits carry a bin threshold (missing-right ones too)
+            if num.any():
+                thr_sp[num] = self.data.thresholds[f_sp[num], b_sp[num]]
+            split_bin[sp[plain]] = b_sp[plain]
+            split_feat[sp] = f_sp
+            # children in (node, side) order: ids base + 2j (left), base + 2j + 1 (right)
+            k_st = lst_h.shape[1]
+            ch_st = np.stack([lst_h[sp], rst_h[sp]], 1).reshape(-1, k_st)
+            ch_ids = forest.add_many(self._leaf_values_v(ch_st), self._weights_v(ch_st), depth + 1,
+                                     self._impurities_v(ch_st))
+            forest.set_splits(fid_sp, f_sp, gain_h[sp], b_sp, thr_sp, num, ch_ids[0::2], ch_ids[1::2])
+            cw = self._weights_v(ch_st)
+            leaf = (cw < 2 * p.min_instances) | (depth + 1 >= p.max_depth)
+            if self.classification:
+                leaf |= (ch_st > 0).sum(1) <= 1  # pure node
+            nl = np.nonzero(~leaf)[0]
+            ch_par = np.repeat(sp, 2)
+            child[2 * ch_par[nl] + (nl & 1)] = np.arange(len(nl), dtype=np.int32)
+            n_tree = a_tree[ch_par[nl]]
+            n_fid = ch_ids[nl]
+            n_key = a_key[ch_par[nl]] * np.uint64(2) + (nl & 1).astype(np.uint64)
+            n_stats = ch_st[nl]
+            n_parent = ch_par[nl].astype(np.int64)
+            # siblings (both children active) for subtraction; a single active child is built directly
+            pos = np.full(2 * len(sp), -1, dtype=np.int64)
+            pos[nl] = np.arange(len(nl))
+            lp, rp = pos[0::2], pos[1::2]
+            both = (lp >= 0) & (rp >= 0)
+            n_sib = np.full(len(nl), -1, dtype=np.int64)
+            n_sib[lp[both]] = rp[both]
+            n_sib[rp[both]] = lp[both]
+            if subtract:
+                n_parent[n_sib < 0] = -1
+            if len(nl):
                 cm = np.stack(cat_masks).view(np.int32) if cat_masks else np.zeros((0, 8), np.int32)
                 with _tr.span("tree.partition", depth=depth):
                     if use_seg:
                         perm, v0p, v1p, wp, segs = K.seg_partition(data.bins, perm, v0p, v1p, wp, segs, split_feat,
                                                                     split_bin, cat_off, cm.reshape(-1), child,
-                                                                    len(nxt))
+                                                                    len(nl))
                     elif use_codes:
-                        nxt_tree = np.array([e["tree"] for e in nxt], dtype=np.int32)
                         tfirst_next = torch.from_numpy(
-                            np.searchsorted(nxt_tree, np.arange(T), side="left").astype(np.int32))
+                            np.searchsorted(n_tree, np.arange(T), side="left").astype(np.int32))
                         K.partition_codes(data.bins, codes, tfirst, tfirst_next, torch.from_numpy(split_feat),
                                           torch.from_numpy(split_bin), torch.from_numpy(cat_off),
                                           torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child))
@@ -955,7 +1055,7 @@ class ForestTrainer:
                                     torch.from_numpy(split_bin).to(dev), torch.from_numpy(cat_off).to(dev),
                                     torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child).to(dev))
             prev_hist = H if subtract else None
-            active = nxt
+            a_tree, a_fid, a_key, a_stats, a_sib, a_parent = n_tree, n_fid, n_key, n_stats, n_sib, n_parent
         forest.roots.extend(root_ids)
         forest._dev = {}
         return forest
