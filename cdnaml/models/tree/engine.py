@@ -223,8 +223,9 @@ def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins:
         nthr = inthr + 1
         thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
         with _tr.span("tree.binize"):
-            bins = K.binize(X, thr_t, torch.from_numpy(nthr).to(X.device), missing=float(missing))
-        return BinnedData(X, bins, thr, nthr, {}, X.shape[0], n_global, row_offset, d, max_bins, True)
+            bins, rm = K.binize(X, thr_t, torch.from_numpy(nthr).to(X.device), missing=float(missing),
+                                want_rm=True)
+        return BinnedData(X, bins, thr, nthr, {}, X.shape[0], n_global, row_offset, d, max_bins, True, rm)
     for f, k in categorical.items():
         if k > max_bins:
             raise IllegalArgumentException(
@@ -241,8 +242,9 @@ def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins:
     thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
     nthr_t = torch.from_numpy(nthr).to(X.device)
     with _tr.span("tree.binize"):
-        bins = K.binize(X, thr_t, nthr_t)
-    return BinnedData(X, bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins)
+        # the row-major copy (segment histograms' row gathers) comes out of the same kernel
+        bins, rm = K.binize(X, thr_t, nthr_t, want_rm=True)
+    return BinnedData(X, bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins, False, rm)
 
 
 # ============================================================ forest storage

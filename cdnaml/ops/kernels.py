@@ -134,8 +134,12 @@ def _binize_lut(thr: torch.Tensor, nthr: torch.Tensor):
     return (torch.from_numpy(best[0]).to(dev), torch.from_numpy(best[1]).to(dev), best[2], best[3])
 
 
-def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Optional[float] = None) -> torch.Tensor:
+def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Optional[float] = None,
+           want_rm: bool = False):
     """Raw features -> uint8 bins in feature-group-major layout [G, n, 8].
+
+    want_rm: return ``(bins, rm)`` where ``rm`` is the row-major copy of ``bins_row_major`` written by the
+    same kernel (GPU search kernel only; otherwise None and the caller transposes lazily).
 
     Continuous feature f: bin = #{thr[f, :nthr[f]] < x}; NaN -> nthr[f].
     Categorical feature (nthr[f] < 0): bin = clamp(int(x), 0, 255).
@@ -151,6 +155,8 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Opti
         thr = thr.float().contiguous()
         nthr = nthr.int().contiguous()
         out = torch.empty((G, n, 8), dtype=torch.uint8, device=X.device)
+        Gs = 16 if (BINS_RM_PAD and G <= 16) else G
+        rm = torch.empty((n, Gs, 8), dtype=torch.uint8, device=X.device) if want_rm else None
         miss_on = missing is not None
         miss_val = float("nan") if (missing is None or math.isnan(missing)) else float(missing)
         if n:
@@ -160,12 +166,17 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Opti
                 rc = _lib.lib().cdna_binize_lut(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax,
                                                 _ptr(lut_t), _ptr(losc_t), C, M, _ptr(out), _stream(X.device))
                 if rc == 0:
-                    return out
+                    return (out, None) if want_rm else out
                 if rc != 1:  # 1 = hipErrorInvalidValue: LDS budget, use the search kernel
                     _lib.check(rc, "cdna_binize_lut")
-            _lib.check(_lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, int(miss_on),
-                                              miss_val, _ptr(out), _stream(X.device)), "cdna_binize")
-        return out
+            rc = _lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, int(miss_on),
+                                        miss_val, _ptr(out), _ptr(rm) if rm is not None else None, Gs,
+                                        _stream(X.device))
+            if rc == 2:  # the fallback kernel ran: no row-major copy
+                rm = None
+            else:
+                _lib.check(rc, "cdna_binize")
+        return (out, rm) if want_rm else out
     out = torch.zeros((G, n, 8), dtype=torch.uint8)
     Xf = X.float()
     if missing is not None:
@@ -180,7 +191,7 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Opti
             b = torch.searchsorted(thr[f, :nt].float().contiguous(), x.contiguous(), right=False)
             b = torch.where(torch.isnan(x), torch.full_like(b, nt), b)
         out[f // 8, :, f % 8] = b.to(torch.uint8)
-    return out
+    return (out, None) if want_rm else out
 
 
 def bins_to_matrix(bins: torch.Tensor, d: int) -> torch.Tensor:

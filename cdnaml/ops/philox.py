@@ -69,9 +69,24 @@ def poisson_from_uniform(u: np.ndarray, lam: float) -> np.ndarray:
     return k
 
 
+def uniform32(n: int, seed: int, offset: int = 0, stream: int = 0) -> np.ndarray:
+    """32-bit uniforms (as doubles in [0,1)) for elements offset..offset+n-1: one Philox call per quad of
+    consecutive global indices (index >> 2), word index & 3 (``poisson_kernel`` in misc.hip)."""
+    seed &= 0xFFFFFFFFFFFFFFFF
+    if n <= 0:
+        return np.zeros(0)
+    q0, q1 = offset >> 2, (offset + n - 1) >> 2
+    q = np.arange(q0, q1 + 1, dtype=np.uint64)
+    lo = (q & _MASK32).astype(np.uint32)
+    hi = (q >> np.uint64(32)).astype(np.uint32)
+    r = philox4x32_10(lo, hi, np.uint32(stream & 0xFFFFFFFF), np.uint32(0xB00F), seed & 0xFFFFFFFF, seed >> 32)
+    words = np.stack(r, 1).reshape(-1)[offset - 4 * q0: offset - 4 * q0 + n]
+    return words.astype(np.float64) * (1.0 / 4294967296.0)
+
+
 def poisson(T: int, n: int, seed: int, offset: int, rate: float) -> np.ndarray:
     out = np.empty((T, n), dtype=np.uint8)
     for t in range(T):
-        u = uniform(n, seed, offset, 0x100 + t)
+        u = uniform32(n, seed, offset, 0x100 + t)
         out[t] = np.minimum(poisson_from_uniform(u, rate), 255).astype(np.uint8)
     return out

@@ -88,7 +88,8 @@ __global__ __launch_bounds__(256) void binize_kernel(const float* __restrict__ X
 __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                       const float* __restrict__ thr, const int* __restrict__ nthr,
                                                       int tmax, int rows_per_tile, int steps, int miss_on,
-                                                      float miss_val, uint64_t* __restrict__ out) {
+                                                      float miss_val, uint64_t* __restrict__ out,
+                                                      uint64_t* __restrict__ rm, int Gs) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int G = (d + 7) / 8;
   // [rows_per_tile][dp]: an odd row stride keeps the per-task x reads (lanes = rows) conflict-free; with
@@ -198,6 +199,14 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
         word |= (uint64_t)b << (8 * j);
       }
       out[(int64_t)g * n + r0 + r] = word;
+      if (rm) {
+        // row-major copy [n][Gs] written from the same registers (saves the separate transpose kernel's
+        // re-read of the [G][n] bins); the row's padding words are zeroed by its last group's task
+        uint64_t* rrow = rm + (r0 + r) * Gs;
+        rrow[g] = word;
+        if (g == G - 1)
+          for (int gp = G; gp < Gs; ++gp) rrow[gp] = 0;
+      }
     }
   }
 }
@@ -766,8 +775,11 @@ inline unsigned grid_for(int64_t n, int per, unsigned cap) {
 }  // namespace
 
 // miss_on: values that are NaN or equal miss_val are binned as -inf (XGBoost missing-value bin 0).
+// rm (optional): also write the row-major copy [n][Gs] (Gs >= G words per row).  Returns 2 when the v1 kernel
+// ran instead (rm not written).
 CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const float* thr, const int* nthr, int tmax,
-                         int miss_on, float miss_val, uint64_t* out, hipStream_t st) {
+                         int miss_on, float miss_val, uint64_t* out, uint64_t* rm, int Gs, hipStream_t st) {
+  if (rm && Gs < (d + 7) / 8) return (int)hipErrorInvalidValue;
   if (n <= 0) return 0;
   {
     // v2: tile of rows in LDS next to the thresholds (<= 64 KB per block)
@@ -793,7 +805,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(binize2_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(binize2_kernel, dim3(grid_for(n, rpt, 8192)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
-                         tmax > 0 ? tmax : 1, rpt, steps, miss_on, miss_val, out);
+                         tmax > 0 ? tmax : 1, rpt, steps, miss_on, miss_val, out, rm, Gs);
       return (int)hipGetLastError();
     }
   }
@@ -805,7 +817,8 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
   if (tile > 120 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(binize_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
                      tmax, use_lds, miss_on, miss_val, out);
-  return (int)hipGetLastError();
+  const int e = (int)hipGetLastError();
+  return e != 0 ? e : (rm ? 2 : 0);
 }
 
 // ngroups slot groups of SB slots (host-planned); out must be zeroed.

@@ -89,6 +89,20 @@ def test_binize(dev):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("d", [21, 100])
+def test_binize_row_major_copy(dev, d):
+    """The binning kernel's row-major copy equals the standalone transpose (padding words zeroed)."""
+    g = torch.Generator().manual_seed(2)
+    X = torch.randn(4099, d, generator=g)
+    thr, nthr = _thresholds(X, 40)
+    bins, rm = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), want_rm=True)
+    assert rm is not None
+    ref = K.bins_row_major(bins)
+    assert rm.shape == ref.shape
+    assert torch.equal(rm.cpu(), ref.cpu())
+    assert torch.equal(bins.cpu(), K.binize(X, thr, nthr))
+
+
 def _tree_state(n, T, A, seed):
     g = torch.Generator().manual_seed(seed)
     node = torch.randint(-1, A, (T, n), generator=g, dtype=torch.int32)
