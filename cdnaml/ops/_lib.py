@@ -63,6 +63,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
 _SIGS = {
     # name: (argtypes, restype)
     "cdna_gram_workspace": ([c_int64, c_int, c_int], c_int64),
+    "cdna_quantile_thresholds": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+                                 c_int),
     "cdna_gram": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int,
                    c_void_p], c_int),
     "cdna_binize": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,

@@ -89,6 +89,31 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
     return torch.from_numpy(_philox.poisson(T, n, seed, int(offset), float(rate)))
 
 
+# --------------------------------------------------------------------- K3
+QUANTILE_MAX_S = 16384  # sample rows a quantile block sorts in LDS (fp64)
+
+
+def quantile_thresholds(samp: torch.Tensor, max_bins: int):
+    """K3 on the GPU: per-feature quantile split candidates of a [s, d] sample in one kernel (quantile.hip).
+
+    Returns host arrays (thr [d, max_bins-1], nthr [d], kdist [d]) and the device tensor of sorted columns
+    [d, s] (NaN last), or None when the kernel does not apply (CPU tensor, s > QUANTILE_MAX_S, max_bins < 2).
+    Features with kdist <= max_bins (and categorical ones) need the host path on their sorted column."""
+    s, d = samp.shape
+    if not _native(samp) or s == 0 or s > QUANTILE_MAX_S or not (2 <= max_bins <= 257):
+        return None
+    samp = samp.double().contiguous()
+    dev = samp.device
+    sorted_ = torch.empty((d, s), dtype=torch.float64, device=dev)
+    thr = torch.empty((d, max_bins - 1), dtype=torch.float64, device=dev)
+    ints = torch.empty((2, d), dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().cdna_quantile_thresholds(_ptr(samp), s, d, max_bins, _ptr(sorted_), _ptr(thr),
+                                                   _ptr(ints[0]), _ptr(ints[1]), _stream(dev)),
+               "cdna_quantile_thresholds")
+    ih = ints.cpu().numpy()
+    return thr.cpu().numpy(), ih[0].copy(), ih[1].copy(), sorted_
+
+
 # --------------------------------------------------------------------- K4
 # binize v3 (LUT-narrowed search).  Opt-in: measured 38.8 ms vs 27.4 ms for the plain lockstep search at
 # 1e8 x 100 x 40 bins -- binize2 is not bound by its threshold reads (rocprofv3: 36 % of its LDS cycles are

@@ -89,6 +89,28 @@ def test_binize(dev):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("max_bins,s", [(40, 10000), (256, 16384), (2, 3000), (32, 777)])
+def test_quantile_thresholds_kernel(dev, max_bins, s):
+    """K3 quantile kernel == the host findSplits reference (NaNs, +-inf, few-distinct and categorical columns)."""
+    from cdnaml.models.tree.engine import find_thresholds, find_thresholds_t
+    g = torch.Generator().manual_seed(max_bins)
+    samp = torch.randn(s, 37, generator=g, dtype=torch.float64)
+    samp[:, 3] = torch.randint(0, 6, (s,), generator=g).double()       # categorical
+    samp[:, 4] = torch.round(samp[:, 4] * 3)                             # few distinct values
+    samp[::5, 7] = float("nan")
+    samp[::11, 8] = float("inf")
+    samp[::13, 8] = -float("inf")
+    samp[:, 9] = float("nan")                                            # empty column
+    samp[: s // 2, 10] = 2.5                                             # heavy tie at one value
+    cats = {3: 6}
+    q = K.quantile_thresholds(samp.to(dev), max_bins)
+    assert q is not None
+    thr_d, nthr_d = find_thresholds_t(samp.to(dev), max_bins, cats)
+    thr_h, nthr_h = find_thresholds(samp.numpy(), 37, max_bins, cats)
+    assert np.array_equal(nthr_d, nthr_h)
+    assert np.array_equal(thr_d, thr_h, equal_nan=True)
+
+
 @pytest.mark.parametrize("d", [21, 100])
 def test_binize_row_major_copy(dev, d):
     """The binning kernel's row-major copy equals the standalone transpose (padding words zeroed)."""
