@@ -263,6 +263,8 @@ class XgboostRegressor(_XgbEstimatorBase):
             F[:, 0] += bm.float()
 
         def grad_hess(F):
+            if F.is_cuda and obj in K.GRAD_HESS_OBJ:
+                return K.grad_hess(F, yf, wf, K.GRAD_HESS_OBJ[obj])  # K9 HIP kernel
             f = F[:, 0]
             if obj in ("reg:squarederror", "reg:linear"):
                 g, h = f - yf, torch.ones_like(f)
@@ -408,6 +410,8 @@ class XgboostClassifier(_XgbEstimatorBase):
             F += bm.float()[:, None]
 
         def grad_hess(F):
+            if F.is_cuda:
+                return K.grad_hess(F, yi.float(), wf, 4 if n_out == 1 else 5)  # K9 HIP kernel
             if n_out == 1:
                 pr = _sigmoid(F[:, 0])
                 g = pr - yi.float()

@@ -89,6 +89,25 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
     return torch.from_numpy(_philox.poisson(T, n, seed, int(offset), float(rate)))
 
 
+# --------------------------------------------------------------------- K9
+GRAD_HESS_OBJ = {"reg:squarederror": 0, "reg:linear": 0, "reg:absoluteerror": 1, "reg:pseudohubererror": 2,
+                 "count:poisson": 3, "binary:logistic": 4, "multi:softprob": 5}
+
+
+def grad_hess(F: torch.Tensor, y: torch.Tensor, w: Optional[torch.Tensor], obj: int):
+    """K9: gradient and hessian [n, K] of objective code ``obj`` (GRAD_HESS_OBJ) at margin F [n, K] (GPU).
+    y: float labels (class index for softmax); w: optional float row weights."""
+    n, Kc = F.shape
+    F = F.float().contiguous()
+    y = y.float().contiguous()
+    w = None if w is None else w.float().contiguous()
+    g = torch.empty_like(F)
+    h = torch.empty_like(F)
+    _lib.check(_lib.lib().cdna_grad_hess(_ptr(F), _ptr(y), _ptr(w), n, Kc, int(obj), _ptr(g), _ptr(h),
+                                         _stream(F.device)), "cdna_grad_hess")
+    return g, h
+
+
 # --------------------------------------------------------------------- K3
 QUANTILE_MAX_S = 16384  # sample rows a quantile block sorts in LDS (fp64)
 

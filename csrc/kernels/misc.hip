@@ -56,6 +56,60 @@ __global__ __launch_bounds__(256) void poisson_kernel(uint8_t* __restrict__ out,
   }
 }
 
+// ------------------------------------------------------- K9 grad / hess
+// Per-row gradient and hessian of the boosting objective at the current margin
+// F [n][K] (one pass: F, label, weight in; g, h out).  obj: 0 squared error,
+// 1 absolute error, 2 pseudo-Huber, 3 Poisson (hessian * exp(max_delta_step
+// 0.7), XGBoost), 4 binary logistic, 5 softmax over K classes (label = class
+// index).  Same f32 formulas as the torch path in cdnaml/models/xgboost.py.
+__global__ __launch_bounds__(256) void grad_hess_kernel(const float* __restrict__ F, const float* __restrict__ y,
+                                                        const float* __restrict__ w, int64_t n, int K, int obj,
+                                                        float* __restrict__ g, float* __restrict__ h) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float yy = y[i];
+    const float ww = w ? w[i] : 1.0f;
+    if (obj == 5) {
+      const float* f = F + i * K;
+      float m = f[0];
+      for (int k = 1; k < K; ++k) m = fmaxf(m, f[k]);
+      float z = 0.0f;
+      for (int k = 0; k < K; ++k) z += expf(f[k] - m);
+      const int c = (int)yy;
+      for (int k = 0; k < K; ++k) {
+        const float p = expf(f[k] - m) / z;
+        g[i * K + k] = (p - (k == c ? 1.0f : 0.0f)) * ww;
+        h[i * K + k] = fmaxf(2.0f * p * (1.0f - p), 1e-16f) * ww;
+      }
+      continue;
+    }
+    const float f = F[i * K];
+    float gg, hh;
+    if (obj == 0) {
+      gg = f - yy;
+      hh = 1.0f;
+    } else if (obj == 1) {
+      const float r = f - yy;
+      gg = (float)((r > 0.0f) - (r < 0.0f));
+      hh = 1.0f;
+    } else if (obj == 2) {
+      const float r = f - yy;
+      const float sq = sqrtf(1.0f + r * r);
+      gg = r / sq;
+      hh = 1.0f / (sq * sq * sq);
+    } else if (obj == 3) {
+      const float e = expf(f);
+      gg = e - yy;
+      hh = e * 2.0137527074704766f;  // exp(0.7)
+    } else {
+      const float p = 1.0f / (1.0f + expf(-f));
+      gg = p - yy;
+      hh = fmaxf(p * (1.0f - p), 1e-16f);
+    }
+    g[i] = gg * ww;
+    h[i] = hh * ww;
+  }
+}
+
 // ------------------------------------------------------- K13 reg metrics
 // acc: [0]=w [1]=Σw e² [2]=Σw|e| [3]=Σw y [4]=Σw y² [5]=Σw p [6]=Σw p² [7]=Σw y p
 __global__ __launch_bounds__(256) void reg_metrics_kernel(const double* __restrict__ y, const double* __restrict__ p,
@@ -315,5 +369,13 @@ CDNA_API int cdna_logistic_grad(const float* X, int64_t n, int d, int64_t ldx, c
   const size_t lds = (size_t)(d + 1) * 8;
   hipLaunchKernelGGL(logistic_kernel, dim3(grid_for(n, 64, 1024)), dim3(256), lds, st, X, n, d, ldx, y, wt, w, b,
                      grad, loss);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_grad_hess(const float* F, const float* y, const float* w, int64_t n, int K, int obj, float* g,
+                            float* h, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (obj < 0 || obj > 5 || K < 1 || (obj != 5 && K != 1)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(grad_hess_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, F, y, w, n, K, obj, g, h);
   return (int)hipGetLastError();
 }

@@ -767,3 +767,47 @@ def test_binize_missing_in_kernel(dev, missing):
     out = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), missing=missing).cpu()
     assert torch.equal(out, ref)
     assert int(out[0, ::7, 2].max()) == 0
+
+
+@pytest.mark.parametrize("obj", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_grad_hess_kernel(dev, obj, weighted):
+    """K9 gradient/hessian kernel vs the fp32 torch formulas of every supported objective."""
+    g0 = torch.Generator().manual_seed(obj)
+    n, C = 5003, (4 if obj == 5 else 1)
+    F = torch.randn(n, C, generator=g0)
+    if obj == 5:
+        y = torch.randint(0, C, (n,), generator=g0).float()
+    elif obj == 4:
+        y = torch.randint(0, 2, (n,), generator=g0).float()
+    elif obj == 3:
+        y = torch.randint(0, 5, (n,), generator=g0).float()
+    else:
+        y = torch.randn(n, generator=g0)
+    w = torch.rand(n, generator=g0) * 3 if weighted else None
+    f = F[:, 0]
+    if obj == 0:
+        g, h = f - y, torch.ones_like(f)
+    elif obj == 1:
+        g, h = torch.sign(f - y), torch.ones_like(f)
+    elif obj == 2:
+        r = f - y
+        s = torch.sqrt(1 + r * r)
+        g, h = r / s, 1 / (s * s * s)
+    elif obj == 3:
+        e = torch.exp(f)
+        g, h = e - y, e * np.exp(0.7)
+    elif obj == 4:
+        p = torch.sigmoid(f)
+        g, h = p - y, (p * (1 - p)).clamp_min(1e-16)
+    if obj == 5:
+        p = torch.softmax(F, 1)
+        g = p - torch.nn.functional.one_hot(y.long(), C).float()
+        h = (2 * p * (1 - p)).clamp_min(1e-16)
+    else:
+        g, h = g[:, None], h[:, None]
+    if w is not None:
+        g, h = g * w[:, None], h * w[:, None]
+    gd, hd = K.grad_hess(F.to(dev), y.to(dev), None if w is None else w.to(dev), obj)
+    torch.testing.assert_close(gd.cpu(), g, rtol=2e-6, atol=2e-6)
+    torch.testing.assert_close(hd.cpu(), h, rtol=2e-6, atol=2e-6)
