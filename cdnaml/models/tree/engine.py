@@ -52,6 +52,8 @@ NATIVE_SPLIT = __import__("os").environ.get("CDNAML_NATIVE_SPLIT", "1") != "0"
 MSEG_REC = __import__("os").environ.get("CDNAML_MSEG_REC", "1") != "0"
 # single-output forests of depth <= 8 predict from a heap layout (8-byte nodes, fixed-step walks)
 HEAP_PREDICT = __import__("os").environ.get("CDNAML_HEAP_PREDICT", "1") != "0"
+# row-record partition gathers split bins from the row-major copy (one line per row) instead of [G][n]
+PARTITION_RM = __import__("os").environ.get("CDNAML_PARTITION_RM", "0") != "0"
 # feature-subset forests: accumulate only each node's sampled features in segment mode.  Opt-in: measured
 # 5-8x slower (profiles/pmc_seg_hist_subset.txt): both children must be built, and every row gather of the
 # row-major bins (one or two 64 B lines) then feeds 34 atomics instead of 104
@@ -1071,7 +1073,9 @@ class ForestTrainer:
                             np.searchsorted(n_tree, np.arange(T), side="left").astype(np.int32))
                         K.partition_codes(data.bins, codes, tfirst, tfirst_next, torch.from_numpy(split_feat),
                                           torch.from_numpy(split_bin), torch.from_numpy(cat_off),
-                                          torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child))
+                                          torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child),
+                                          bins_rm=data.row_major_bins() if (PARTITION_RM and dev.type == "cuda")
+                                          else None)
                     else:
                         K.partition(data.bins, node, torch.from_numpy(split_feat).to(dev),
                                     torch.from_numpy(split_bin).to(dev), torch.from_numpy(cat_off).to(dev),

@@ -97,6 +97,10 @@ _SIGS = {
     "cdna_bins_row_major": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p], c_int),
     "cdna_partition6": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_partition7": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_partition8": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double,
                          c_double, c_double, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_compact_mask": ([c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p], c_int),

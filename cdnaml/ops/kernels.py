@@ -645,6 +645,11 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
 # Opt-in: measured 7.8 ms per level at 1e8 x 20 trees at every depth, the same as partition5 (both move
 # 8 GB of row records plus the bins at ~2.4 TB/s), so the bins re-reads were not the bound
 PARTITION6 = __import__("os").environ.get("CDNAML_PARTITION6", "0") != "0"
+# persistent partition (tables staged once per block, coalesced bins words, all trees' codes in flight)
+PARTITION7 = __import__("os").environ.get("CDNAML_PARTITION7", "1") != "0"
+# ... two adjacent rows per lane (even n): half the memory instructions.  Opt-in: measured equal to partition7
+# (5.09 vs 5.00 ms per level at 1e8 x 20 trees; both stream ~18 GB per level: bins once, codes read + write)
+PARTITION8 = __import__("os").environ.get("CDNAML_PARTITION8", "0") != "0"
 
 
 def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tensor, tfirst_next: torch.Tensor,
@@ -663,6 +668,17 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
         args = [t.to(device=bins.device, dtype=torch.int32).contiguous()
                 for t in (tfirst, tfirst_next, split_feat, split_bin, cat_off, child)]
         A = int(split_feat.numel())
+        if PARTITION7 and not PARTITION6 and G <= 16 and A <= 1024 and T <= 64 and bins_rm is None:
+            if PARTITION8 and n % 2 == 0 and codes.is_contiguous() and bins.data_ptr() % 16 == 0:
+                _lib.check(_lib.lib().cdna_partition8(_ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]),
+                                                      _ptr(args[1]), _ptr(args[2]), _ptr(args[3]), _ptr(args[4]),
+                                                      _ptr(cm), _ptr(args[5]), _stream(bins.device)),
+                           "cdna_partition8")
+                return
+            _lib.check(_lib.lib().cdna_partition7(_ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]),
+                                                  _ptr(args[1]), _ptr(args[2]), _ptr(args[3]), _ptr(args[4]),
+                                                  _ptr(cm), _ptr(args[5]), _stream(bins.device)), "cdna_partition7")
+            return
         if PARTITION6 and G <= 32 and A <= 1024 and T <= 64 and bins_rm is None:
             _lib.check(_lib.lib().cdna_partition6(_ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]),
                                                   _ptr(args[1]), _ptr(args[2]), _ptr(args[3]), _ptr(args[4]),

@@ -884,6 +884,190 @@ __global__ __launch_bounds__(256) void partition6_kernel(const uint64_t* __restr
   }
 }
 
+// Row-record partition, persistent (partition7).  partition5 (grid.y = tree)
+// re-gathers one byte per (row, tree) from the [G][n] planes, so 20 trees pull
+// the bins planes through HBM up to 20 times per level (4.7 -> 9.5 ms per level
+// at 1e8 x 20 trees as the split features diversify); partition6 fixed that
+// but re-staged every split table per 256-row chunk and ran one short pass per
+// block (latency-bound, 8 ms flat).  Here ~4 blocks per CU stay resident: the
+// level's split tables (all trees) are staged in LDS ONCE per block, and each
+// thread owns one row per trip: its G bins words are read with coalesced
+// 8-byte loads (once per level), parked in the thread's own LDS column (no
+// block barrier), and the row's codes of up to kP7TB trees are all in flight
+// before any is moved.
+constexpr int kP7MaxA = 1024;
+constexpr int kP7MaxT = 64;
+constexpr int kP7MaxG = 16;  // MAXG template: 8 / 13 / 16 words per row (registers sized to the row)
+constexpr int kP7TB = 24;
+template <int MAXG>
+__global__ __launch_bounds__(256) void partition7_kernel(const uint64_t* __restrict__ bins, int64_t n, int G, int T,
+                                                         int A, uint16_t* __restrict__ codes,
+                                                         const int* __restrict__ tfirst,
+                                                         const int* __restrict__ tfirst_next,
+                                                         const int* __restrict__ split_feat,
+                                                         const int* __restrict__ split_bin,
+                                                         const int* __restrict__ cat_off,
+                                                         const uint32_t* __restrict__ cat_mask,
+                                                         const int* __restrict__ child) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t tile7[];  // [G][256]
+  __shared__ int s_fb[kP7MaxA], s_co[kP7MaxA];  // feature (0xFFFF: leaf) | bin << 16
+  __shared__ uint8_t s_ch[2 * kP7MaxA];
+  __shared__ int s_tf[kP7MaxT];
+  for (int i = threadIdx.x; i < T; i += 256) s_tf[i] = tfirst[i];
+  for (int i = threadIdx.x; i < A; i += 256) {
+    const int f = split_feat[i];
+    s_fb[i] = (f >= 0 ? f : 0xFFFF) | (split_bin[i] << 16);
+    s_co[i] = cat_off[i];
+    int lo = 0, hi = T - 1;  // the tree of active node i: largest t with tfirst[t] <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tfirst[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const int tfn = tfirst_next[lo];
+    const int c0 = child[i * 2], c1 = child[i * 2 + 1];
+    s_ch[2 * i] = (uint8_t)(c0 >= 0 ? c0 - tfn : 0xFF);
+    s_ch[2 * i + 1] = (uint8_t)(c1 >= 0 ? c1 - tfn : 0xFF);
+  }
+  __syncthreads();
+  const uint8_t* tb = reinterpret_cast<const uint8_t*>(tile7);
+  const int lr = threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  // one row: park its bins words in this thread's LDS column (no barrier), move every tree's code
+  auto move_row = [&](int64_t r, const uint64_t (&w)[MAXG], const uint32_t (&cc)[kP7TB], int half) {
+    uint32_t c[kP7TB];
+#pragma unroll
+    for (int u = 0; u < kP7TB; ++u) c[u] = (cc[u] >> (16 * half)) & 0xFFFFu;
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g)
+      if (g < G) tile7[g * 256 + lr] = w[g];
+    for (int t0 = 0; t0 < T; t0 += kP7TB) {
+      if (t0 > 0) {
+#pragma unroll
+        for (int u = 0; u < kP7TB; ++u) c[u] = t0 + u < T ? (uint32_t)codes[(int64_t)(t0 + u) * n + r] : 0xFFu;
+      }
+#pragma unroll
+      for (int u = 0; u < kP7TB; ++u) {
+        const uint32_t loc = c[u] & 0xFFu;
+        if (t0 + u >= T || loc == 0xFFu) continue;
+        const int id = s_tf[t0 + u] + (int)loc;
+        const int fb = s_fb[id];
+        const int f = fb & 0xFFFF;
+        uint32_t nl = 0xFFu;
+        if (f != 0xFFFF) {
+          const int bin = tb[((f >> 3) * 256 + lr) * 8 + (f & 7)];
+          const int co = s_co[id];
+          const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u : bin <= (fb >> 16);
+          nl = s_ch[2 * id + (left ? 0 : 1)];
+        }
+        codes[(int64_t)(t0 + u) * n + r] = (uint16_t)((c[u] & 0xFF00u) | nl);
+      }
+    }
+  };
+  for (int64_t r = (int64_t)blockIdx.x * 256 + lr; r < n; r += stride) {
+    uint64_t w[MAXG];
+    uint32_t cc[kP7TB];
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g)
+      if (g < G) w[g] = bins[(int64_t)g * n + r];
+#pragma unroll
+    for (int u = 0; u < kP7TB; ++u) cc[u] = u < T ? (uint32_t)codes[(int64_t)u * n + r] : 0xFFu;
+    move_row(r, w, cc, 0);
+  }
+}
+
+// partition8: partition7 with two adjacent rows per lane (n even): one 16-byte
+// load per bins group and one 4-byte load / store per tree cover both rows
+// (half the memory instructions of partition7, whose 2-byte code accesses
+// bounded it), and the split bin is picked from the row's registers by a
+// select ladder instead of an LDS tile (tables only in LDS: more resident
+// blocks).
+template <int MAXG>
+__global__ __launch_bounds__(256) void partition8_kernel(const uint64_t* __restrict__ bins, int64_t n, int G, int T,
+                                                         int A, uint16_t* __restrict__ codes,
+                                                         const int* __restrict__ tfirst,
+                                                         const int* __restrict__ tfirst_next,
+                                                         const int* __restrict__ split_feat,
+                                                         const int* __restrict__ split_bin,
+                                                         const int* __restrict__ cat_off,
+                                                         const uint32_t* __restrict__ cat_mask,
+                                                         const int* __restrict__ child) {
+  __shared__ int s_fb[kP7MaxA], s_co[kP7MaxA];  // feature (0xFFFF: leaf) | bin << 16
+  __shared__ uint8_t s_ch[2 * kP7MaxA];
+  __shared__ int s_tf[kP7MaxT];
+  for (int i = threadIdx.x; i < T; i += 256) s_tf[i] = tfirst[i];
+  for (int i = threadIdx.x; i < A; i += 256) {
+    const int f = split_feat[i];
+    s_fb[i] = (f >= 0 ? f : 0xFFFF) | (split_bin[i] << 16);
+    s_co[i] = cat_off[i];
+    int lo = 0, hi = T - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tfirst[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const int tfn = tfirst_next[lo];
+    const int c0 = child[i * 2], c1 = child[i * 2 + 1];
+    s_ch[2 * i] = (uint8_t)(c0 >= 0 ? c0 - tfn : 0xFF);
+    s_ch[2 * i + 1] = (uint8_t)(c1 >= 0 ? c1 - tfn : 0xFF);
+  }
+  __syncthreads();
+  const int64_t np = n >> 1;
+  const uint32_t* codes2 = reinterpret_cast<const uint32_t*>(codes);
+  uint32_t* codes2w = reinterpret_cast<uint32_t*>(codes);
+  const int64_t n2 = n >> 1;  // row pairs per tree plane
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < np; q += (int64_t)gridDim.x * 256) {
+    // words[k][2g + h]: 32-bit half h of group g of row 2q + k
+    uint32_t wd[2][2 * MAXG];
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g) {
+      if (g < G) {
+        const uint4 v = *reinterpret_cast<const uint4*>(bins + (int64_t)g * n + 2 * q);
+        wd[0][2 * g] = v.x;
+        wd[0][2 * g + 1] = v.y;
+        wd[1][2 * g] = v.z;
+        wd[1][2 * g + 1] = v.w;
+      } else {
+        wd[0][2 * g] = wd[0][2 * g + 1] = wd[1][2 * g] = wd[1][2 * g + 1] = 0u;
+      }
+    }
+    for (int t0 = 0; t0 < T; t0 += kP7TB) {
+      uint32_t cc[kP7TB];
+#pragma unroll
+      for (int u = 0; u < kP7TB; ++u) cc[u] = t0 + u < T ? codes2[(int64_t)(t0 + u) * n2 + q] : 0x00FF00FFu;
+#pragma unroll
+      for (int u = 0; u < kP7TB; ++u) {
+        if (t0 + u >= T || (cc[u] & 0x00FF00FFu) == 0x00FF00FFu) continue;  // both rows done in this tree
+        uint32_t o = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const uint32_t c = (cc[u] >> (16 * k)) & 0xFFFFu;
+          const uint32_t loc = c & 0xFFu;
+          uint32_t res = c;
+          if (loc != 0xFFu) {
+            const int id = s_tf[t0 + u] + (int)loc;
+            const int fb = s_fb[id];
+            const int f = fb & 0xFFFF;
+            uint32_t nl = 0xFFu;
+            if (f != 0xFFFF) {
+              const int wi = f >> 2;
+              uint32_t word = wd[k][0];
+#pragma unroll
+              for (int j = 1; j < 2 * MAXG; ++j) word = wi == j ? wd[k][j] : word;
+              const int bin = (int)((word >> ((f & 3) * 8)) & 0xFFu);
+              const int co = s_co[id];
+              const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u
+                                        : bin <= (fb >> 16);
+              nl = s_ch[2 * id + (left ? 0 : 1)];
+            }
+            res = (c & 0xFF00u) | nl;
+          }
+          o |= res << (16 * k);
+        }
+        codes2w[(int64_t)(t0 + u) * n2 + q] = o;
+      }
+    }
+  }
+}
+
 inline unsigned grid_for(int64_t n, int per, unsigned cap) {
   int64_t b = (n + per - 1) / per;
   return (unsigned)(b < (int64_t)cap ? (b < 1 ? 1 : b) : cap);
@@ -1046,6 +1230,51 @@ CDNA_API int cdna_partition6(const uint64_t* bins, int64_t n, int G, int T, int 
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(partition6_kernel, dim3((unsigned)((n + kP6Rows - 1) / kP6Rows)), dim3(256), lds, st, bins, n,
                      G, T, A, codes, tfirst, tfirst_next, split_feat, split_bin, cat_off, cat_mask, child);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_partition7(const uint64_t* bins, int64_t n, int G, int T, int A, uint16_t* codes,
+                             const int* tfirst, const int* tfirst_next, const int* split_feat, const int* split_bin,
+                             const int* cat_off, const uint32_t* cat_mask, const int* child, hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  if (G <= 0 || G > kP7MaxG || A > kP7MaxA || T > kP7MaxT || G * 8 > 0xFFFF) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)G * 256 * 8;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  // exactly the resident blocks (one round): a 4-per-CU grid with only 3 resident per CU (LDS) ran a
+  // second, quarter-full round
+  auto launch = [&](auto kern) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1) per_cu = 2;
+    const dim3 grid(grid_for(n, 256, (unsigned)(per_cu * ncu)));
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, bins, n, G, T, A, codes, tfirst, tfirst_next, split_feat,
+                       split_bin, cat_off, cat_mask, child);
+  };
+  if (G <= 8) launch(partition7_kernel<8>);
+  else if (G <= 13) launch(partition7_kernel<13>);
+  else launch(partition7_kernel<16>);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_partition8(const uint64_t* bins, int64_t n, int G, int T, int A, uint16_t* codes,
+                             const int* tfirst, const int* tfirst_next, const int* split_feat, const int* split_bin,
+                             const int* cat_off, const uint32_t* cat_mask, const int* child, hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  if ((n & 1) || G <= 0 || G > kP7MaxG || A > kP7MaxA || T > kP7MaxT) return (int)hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(bins) & 15) || (reinterpret_cast<uintptr_t>(codes) & 3))
+    return (int)hipErrorInvalidValue;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  auto launch = [&](auto kern) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+    const dim3 grid(grid_for(n / 2, 256, (unsigned)(per_cu * ncu)));
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, bins, n, G, T, A, codes, tfirst, tfirst_next, split_feat,
+                       split_bin, cat_off, cat_mask, child);
+  };
+  if (G <= 8) launch(partition8_kernel<8>);
+  else if (G <= 13) launch(partition8_kernel<13>);
+  else launch(partition8_kernel<16>);
   return (int)hipGetLastError();
 }
 

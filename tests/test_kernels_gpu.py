@@ -385,10 +385,14 @@ def test_hist_codes(dev, kind, monkeypatch):
     assert torch.allclose(out, ref, rtol=1e-6, atol=1e-3)
 
 
-@pytest.mark.parametrize("p6,n", [(True, 20000), (False, 20000), (True, 20001)])
-def test_partition_codes(dev, monkeypatch, p6, n):
-    monkeypatch.setattr(K, "PARTITION6", p6)
-    d, T, per = 12, 6, 4
+@pytest.mark.parametrize("variant,n,T,d", [("p6", 20000, 6, 12), ("p5", 20000, 6, 12), ("p6", 20001, 6, 12),
+                                           ("p7", 20001, 6, 12), ("p7", 70001, 30, 100), ("p8", 70000, 30, 100),
+                                           ("p8", 20000, 6, 12), ("p8", 4000, 3, 130)])
+def test_partition_codes(dev, monkeypatch, variant, n, T, d):
+    monkeypatch.setattr(K, "PARTITION6", variant == "p6")
+    monkeypatch.setattr(K, "PARTITION7", variant in ("p7", "p8"))
+    monkeypatch.setattr(K, "PARTITION8", variant == "p8")
+    per = 4
     g = torch.Generator().manual_seed(5)
     X = torch.randn(n, d, generator=g)
     X[:, 3] = torch.randint(0, 20, (n,), generator=g).float()
