@@ -647,6 +647,7 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
 PARTITION6 = __import__("os").environ.get("CDNAML_PARTITION6", "0") != "0"
 # persistent partition (tables staged once per block, coalesced bins words, all trees' codes in flight)
 PARTITION7 = __import__("os").environ.get("CDNAML_PARTITION7", "1") != "0"
+PARTITION7_MIN_T = int(__import__("os").environ.get("CDNAML_PARTITION7_MIN_T", "16"))
 # ... two adjacent rows per lane (even n): half the memory instructions.  Opt-in: measured equal to partition7
 # (5.09 vs 5.00 ms per level at 1e8 x 20 trees; both stream ~18 GB per level: bins once, codes read + write)
 PARTITION8 = __import__("os").environ.get("CDNAML_PARTITION8", "0") != "0"
@@ -668,7 +669,11 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
         args = [t.to(device=bins.device, dtype=torch.int32).contiguous()
                 for t in (tfirst, tfirst_next, split_feat, split_bin, cat_off, child)]
         A = int(split_feat.numel())
-        if PARTITION7 and not PARTITION6 and G <= 16 and A <= 1024 and T <= 64 and bins_rm is None:
+        # partition7 streams every bins word of every row once per level (10 GB at 1e8 x 100): it pays when
+        # many trees share that pass; for few trees partition5's per-(row, tree) byte gathers move less (GBDT,
+        # T = 1: 57.9 vs 40.6 ms per boosting round with partition7; CV grid with 5 / 10 trees: 2.18 vs 1.34 s)
+        if PARTITION7 and not PARTITION6 and T >= PARTITION7_MIN_T and G <= 16 and A <= 1024 and T <= 64 and \
+                bins_rm is None:
             if PARTITION8 and n % 2 == 0 and codes.is_contiguous() and bins.data_ptr() % 16 == 0:
                 _lib.check(_lib.lib().cdna_partition8(_ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]),
                                                       _ptr(args[1]), _ptr(args[2]), _ptr(args[3]), _ptr(args[4]),

@@ -392,6 +392,7 @@ def test_partition_codes(dev, monkeypatch, variant, n, T, d):
     monkeypatch.setattr(K, "PARTITION6", variant == "p6")
     monkeypatch.setattr(K, "PARTITION7", variant in ("p7", "p8"))
     monkeypatch.setattr(K, "PARTITION8", variant == "p8")
+    monkeypatch.setattr(K, "PARTITION7_MIN_T", 1)
     per = 4
     g = torch.Generator().manual_seed(5)
     X = torch.randn(n, d, generator=g)
