@@ -934,24 +934,29 @@ class ForestTrainer:
                                         build_slot, slot_tree, fm_build, B, id_tree=id_tree)
             with _tr.span("tree.allreduce", cat="comm", bytes=Hb.numel() * 8):
                 self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
-            if Hb.dtype == torch.int64:  # exact fixed-point sums (count, sum * scale) -> fp64 moments
-                Hf = Hb.double()
-                Hf[..., 1] /= hist_raw_scale
-                Hb = Hf
             _split_span = _tr.span("tree.split", depth=depth)
             _split_span.__enter__()
             # ---- assemble every active node's histogram
             derived = np.nonzero(~build)[0]
-            if len(derived) == 0:
-                H = Hb
+            is_raw = Hb.dtype == torch.int64
+            if dev.type == "cuda" and (is_raw or len(derived)):
+                # one kernel: fixed-point -> fp64 and parent - sibling for the derived nodes
+                H = K.hist_assemble(Hb, hist_raw_scale if is_raw else None, prev_hist if len(derived) else None,
+                                    slot_of, a_parent, a_sib)
             else:
-                H = torch.empty((A, d, B, self.stats_k), dtype=torch.float64, device=dev)
-                if len(build_ids):
-                    H[torch.from_numpy(build_ids).to(dev)] = Hb
-                di = torch.from_numpy(derived).to(dev)
-                par = torch.from_numpy(a_parent[derived]).to(dev)
-                sib = torch.from_numpy(a_sib[derived]).to(dev)
-                H[di] = prev_hist[par] - H[sib]
+                if is_raw:  # exact fixed-point sums (count, sum * scale) -> fp64 moments
+                    Hb = Hb.double()
+                    Hb[..., 1] /= hist_raw_scale
+                if len(derived) == 0:
+                    H = Hb
+                else:
+                    H = torch.empty((A, d, B, self.stats_k), dtype=torch.float64, device=dev)
+                    if len(build_ids):
+                        H[torch.from_numpy(build_ids).to(dev)] = Hb
+                    di = torch.from_numpy(derived).to(dev)
+                    par = torch.from_numpy(a_parent[derived]).to(dev)
+                    sib = torch.from_numpy(a_sib[derived]).to(dev)
+                    H[di] = prev_hist[par] - H[sib]
             masks_t = torch.from_numpy(masks_np.view(np.int32)).to(dev) if masks_np is not None else None
             if self._native_split(dev):
                 # K6 in one kernel: node totals, prefix scans, gains, masks, argmax

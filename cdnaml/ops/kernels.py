@@ -89,6 +89,28 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
     return torch.from_numpy(_philox.poisson(T, n, seed, int(offset), float(rate)))
 
 
+# ------------------------------------------------------- level histogram assembly
+def hist_assemble(Hb: torch.Tensor, raw_scale: Optional[float], prev: Optional[torch.Tensor], slot: np.ndarray,
+                  parent: np.ndarray, sib: np.ndarray) -> torch.Tensor:
+    """fp64 histograms [A, d, B, K] of a level's active nodes in one launch (split.hip): built node a copies
+    Hb[slot[a]] (int64 fixed point divided by raw_scale in stat 1 when raw_scale is given); a derived node
+    (slot -1) is prev[parent[a]] - (its sibling's built histogram)."""
+    A = len(slot)
+    nb, d, B, Kc = Hb.shape
+    dev = Hb.device
+    H = torch.empty((A, d, B, Kc), dtype=torch.float64, device=dev)
+    m = torch.from_numpy(np.stack([slot, parent, sib], 1).astype(np.int32).reshape(-1)).to(dev)
+    raw = raw_scale is not None
+    src = Hb.contiguous() if raw else Hb.double().contiguous()
+    if raw:
+        assert Hb.dtype == torch.int64
+    pv = None if prev is None else prev.contiguous()
+    _lib.check(_lib.lib().cdna_hist_assemble(_ptr(src), int(raw), float(raw_scale) if raw else 1.0, _ptr(pv),
+                                             _ptr(m), A, d * B * Kc, Kc, _ptr(H), _stream(dev)),
+               "cdna_hist_assemble")
+    return H
+
+
 # --------------------------------------------------------------------- K9
 GRAD_HESS_OBJ = {"reg:squarederror": 0, "reg:linear": 0, "reg:absoluteerror": 1, "reg:pseudohubererror": 2,
                  "count:poisson": 3, "binary:logistic": 4, "multi:softprob": 5}

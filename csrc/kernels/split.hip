@@ -176,3 +176,40 @@ CDNA_API int cdna_split_scan(const double* H, const int* nthr, const uint32_t* m
   hipLaunchKernelGGL(split_scan_kernel, dim3((unsigned)A), dim3(kThreads), 0, st, a);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Level histogram assembly (one launch instead of ~8 small torch ops + 3 copies
+// per level): every active node's fp64 moments [A][d][B][K] from the level's
+// built histograms Hb [nb][d][B][K] -- exact int64 fixed-point sums (raw = 1:
+// stat 1 divided by `scale`) or fp64 -- and, for the larger sibling, parent
+// minus sibling from the previous level's assembled histograms.
+// map [A][3] = (build slot or -1, parent position, sibling position).
+// ---------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(256) void hist_assemble_kernel(const void* __restrict__ Hb, int raw, double scale,
+                                                            const double* __restrict__ prev,
+                                                            const int* __restrict__ map, int64_t cells, int K,
+                                                            double* __restrict__ H) {
+  const int a = blockIdx.y;
+  const int slot = map[3 * a], par = map[3 * a + 1], sib = map[3 * a + 2];
+  const int src = slot >= 0 ? slot : map[3 * sib];
+  for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += (int64_t)gridDim.x * 256) {
+    const int64_t i = (int64_t)src * cells + c;
+    double v = raw ? (double)reinterpret_cast<const long long*>(Hb)[i] : reinterpret_cast<const double*>(Hb)[i];
+    if (raw && (c % K) == 1) v = v / scale;
+    if (slot < 0) v = prev[(int64_t)par * cells + c] - v;
+    H[(int64_t)a * cells + c] = v;
+  }
+}
+}  // namespace
+
+CDNA_API int cdna_hist_assemble(const void* Hb, int raw, double scale, const double* prev, const int* map, int A,
+                                int64_t cells, int K, double* H, hipStream_t st) {
+  if (A <= 0 || cells <= 0) return 0;
+  if (A > 65535) return (int)hipErrorInvalidValue;
+  int64_t gx = (cells + 255) / 256;
+  if (gx > 64) gx = 64;
+  hipLaunchKernelGGL(hist_assemble_kernel, dim3((unsigned)gx, (unsigned)A), dim3(256), 0, st, Hb, raw, scale, prev,
+                     map, cells, K, H);
+  return (int)hipGetLastError();
+}

@@ -816,3 +816,30 @@ def test_grad_hess_kernel(dev, obj, weighted):
     gd, hd = K.grad_hess(F.to(dev), y.to(dev), None if w is None else w.to(dev), obj)
     torch.testing.assert_close(gd.cpu(), g, rtol=2e-6, atol=2e-6)
     torch.testing.assert_close(hd.cpu(), h, rtol=2e-6, atol=2e-6)
+
+
+@pytest.mark.parametrize("raw", [True, False])
+def test_hist_assemble(dev, raw):
+    """Level histogram assembly kernel == the torch sequence (fixed-point scale, parent - sibling)."""
+    g = torch.Generator().manual_seed(11)
+    d, B, Kc = 7, 40, 2
+    # 6 active nodes: siblings 0/1 (0 built), siblings 2/3 (3 built), 4 and 5 built without a sibling
+    slot = np.array([0, -1, -1, 1, 2, 3], dtype=np.int64)
+    parent = np.array([0, 0, 1, 1, -1, -1], dtype=np.int64)
+    sib = np.array([1, 0, 3, 2, -1, -1], dtype=np.int64)
+    if raw:
+        Hb = torch.randint(-2 ** 40, 2 ** 40, (4, d, B, Kc), generator=g, dtype=torch.int64)
+        scale = 2.0 ** 17
+        Hf = Hb.double()
+        Hf[..., 1] /= scale
+    else:
+        Hb = torch.randn(4, d, B, Kc, generator=g, dtype=torch.float64)
+        scale, Hf = None, Hb
+    prev = torch.randn(2, d, B, Kc, generator=g, dtype=torch.float64)
+    ref = torch.empty(6, d, B, Kc, dtype=torch.float64)
+    built = np.nonzero(slot >= 0)[0]
+    ref[torch.from_numpy(built)] = Hf[torch.from_numpy(slot[built])]
+    for a in np.nonzero(slot < 0)[0]:
+        ref[a] = prev[parent[a]] - ref[sib[a]]
+    out = K.hist_assemble(Hb.to(dev), scale, prev.to(dev), slot, parent, sib).cpu()
+    assert torch.equal(out, ref)
