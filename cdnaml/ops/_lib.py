@@ -112,7 +112,8 @@ _SIGS = {
                               c_float, c_void_p, c_int, c_void_p, c_void_p], c_int),
     "cdna_codes_compact_w": ([c_int, c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                              c_float, c_void_p], c_int),
+                              c_float, c_void_p, c_void_p], c_int),
+    "cdna_wave_scan": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
     "cdna_als_max_rank": ([], c_int),
     "cdna_als_accumulate": ([c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p,
                              c_void_p, c_void_p, c_void_p], c_int),

@@ -1404,9 +1404,11 @@ def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1, re
     v0c = None if v0 is None else v0.float().contiguous()
     wcnt = torch.empty((T, Wv, KB), dtype=torch.int32, device=dev)
     _lib.check(L.cdna_codes_compact_w(1, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
-                                      per_wave, Wv, _ptr(wcnt), None, None, None, None, None, None, 0.0,
+                                      per_wave, Wv, _ptr(wcnt), None, None, None, None, None, None, 0.0, None,
                                       _stream(dev)), "cdna_codes_compact_w(count)")
-    tot = wcnt.sum(1, dtype=torch.int64)                      # [T, KB]
+    # per-(tree, node) exclusive scan over the waves in place + node totals, one launch
+    tot = torch.empty((T, KB), dtype=torch.int64, device=dev)
+    _lib.check(L.cdna_wave_scan(_ptr(wcnt), T, Wv, KB, _ptr(tot), _stream(dev)), "cdna_wave_scan")
     tot_h = tot.cpu().numpy()
     lens = np.zeros(S, dtype=np.int64)
     sl = (first_slot[:, None] + np.arange(KB)[None, :])        # slot of (t, k)
@@ -1427,15 +1429,12 @@ def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1, re
     if total:
         kstart = np.zeros((T, KB), dtype=np.int64)
         kstart[valid] = starts[sl[valid]]
-        # exclusive scan over each (tree, node)'s waves, as an inner-dim scan on the [T, KB, Wv] transpose
-        # (torch's outer-dim scan kernel took 0.37 ms per call on [1, 2048, KB])
-        wt_ = wcnt.permute(0, 2, 1).contiguous()
-        ex = torch.cumsum(wt_, 2, dtype=torch.int64) - wt_
-        woff = (torch.from_numpy(kstart).to(dev)[:, :, None] + ex).to(torch.int32).permute(0, 2, 1).contiguous()
+        kstart_t = torch.from_numpy(kstart).to(dev)
+        # wcnt now holds the per-wave exclusive offsets; the scatter pass adds each node's segment start
         _lib.check(L.cdna_codes_compact_w(2, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
-                                          per_wave, Wv, None, _ptr(woff), None if rec else _ptr(perm), _ptr(v0p),
+                                          per_wave, Wv, None, _ptr(wcnt), None if rec else _ptr(perm), _ptr(v0p),
                                           _ptr(v1p), _ptr(wp), _ptr(perm) if rec else None,
-                                          float(rec_scale) if rec else 0.0, _stream(dev)),
+                                          float(rec_scale) if rec else 0.0, _ptr(kstart_t), _stream(dev)),
                    "cdna_codes_compact_w(scatter)")
     return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
 

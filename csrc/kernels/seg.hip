@@ -752,6 +752,7 @@ struct CompactWArgs {
   // row (31 bits) | weight << 31 (8 bits) | (clamp(rint(v1 * qs1), +-2^23) + 2^23) << 39 (25 bits)
   uint64_t* rec_out;
   float qs1;
+  const int64_t* kstart;  // pass 2, optional: [T][KB] segment start added to the per-wave offsets
 };
 
 __device__ __forceinline__ bool v_aligned(const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -773,7 +774,8 @@ __global__ __launch_bounds__(256) void codes_compact_w_kernel(const CompactWArgs
   const int64_t cb = ((int64_t)t * a.Wv + w) * KB;
   int acc[KB];
 #pragma unroll
-  for (int k = 0; k < KB; ++k) acc[k] = SCATTER ? a.woff[cb + k] : 0;
+  for (int k = 0; k < KB; ++k)
+    acc[k] = SCATTER ? a.woff[cb + k] + (a.kstart ? (int)a.kstart[(int64_t)t * KB + k] : 0) : 0;
   // 2 x 4 records per lane per trip, codes (and, in pass 2, the statistics) loaded up front as vectors:
   // the one-group loop waited on each trip's dependent load chain (codes -> LDS map -> v1 -> store)
   const bool vec = (a.n & 3) == 0 && (reinterpret_cast<uintptr_t>(a.codes) & 7u) == 0 && v_aligned(a.v1) && (a.v0 == nullptr || v_aligned(a.v0));
@@ -865,6 +867,38 @@ __global__ __launch_bounds__(256) void codes_compact_w_kernel(const CompactWArgs
       if (lane == 0) a.wcnt[cb + k] = v;
     }
   }
+}
+
+// Per (tree, built node): exclusive prefix of the per-wave counts [T][Wv][KB] in place and the node's total
+// (one launch instead of the torch permute / cumsum / subtract / add / cast / permute chain per level).
+__global__ __launch_bounds__(256) void wave_scan_kernel(int* __restrict__ wcnt, int Wv, int KB,
+                                                        int64_t* __restrict__ tot) {
+  const int t = blockIdx.x / KB, k = blockIdx.x - t * KB;
+  int* base = wcnt + (int64_t)t * Wv * KB + k;
+  const int per = (Wv + 255) / 256;
+  const int w0 = threadIdx.x * per;
+  int s = 0;
+  for (int j = 0; j < per; ++j)
+    if (w0 + j < Wv) s += base[(int64_t)(w0 + j) * KB];
+  __shared__ int sh[256];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
+    const int v = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+    __syncthreads();
+    sh[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = sh[threadIdx.x] - s;
+  for (int j = 0; j < per; ++j) {
+    if (w0 + j < Wv) {
+      int* p = base + (int64_t)(w0 + j) * KB;
+      const int c = *p;
+      *p = run;
+      run += c;
+    }
+  }
+  if (threadIdx.x == 255) tot[blockIdx.x] = sh[255];
 }
 
 // [G][n] 8-feature bin words -> row-major [n][G] (one row's words contiguous),
@@ -1030,12 +1064,13 @@ CDNA_API int cdna_bins_row_major(const uint64_t* bins, int64_t n, int G, int Gs,
 CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64_t n, int T, int A,
                                   const int* tfirst, const int* kmap, const float* v0, const float* v1,
                                   int64_t per_wave, int Wv, int* wcnt, const int* woff, int* perm_out, float* v0_out,
-                                  float* v1_out, uint8_t* w_out, uint64_t* rec_out, float qs1, hipStream_t st) {
+                                  float* v1_out, uint8_t* w_out, uint64_t* rec_out, float qs1,
+                                  const int64_t* kstart, hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
   if (per_wave % 256 != 0 || (int64_t)Wv * per_wave < n) return (int)hipErrorInvalidValue;
   if (rec_out && (n >= (int64_t)1 << 31 || v0)) return (int)hipErrorInvalidValue;
   CompactWArgs a{codes, n, T, A, tfirst, kmap, v0, v1, per_wave, Wv, wcnt, woff, perm_out, v0_out, v1_out, w_out,
-                 rec_out, qs1};
+                 rec_out, qs1, kstart};
   const dim3 grid((unsigned)((Wv + 3) / 4), (unsigned)T);
   auto go = [&](auto k1, auto k2) {
     if (pass == 1) hipLaunchKernelGGL(k1, grid, dim3(256), 0, st, a);
@@ -1070,5 +1105,12 @@ CDNA_API int cdna_seg_hist_subset(const uint8_t* bins_rm, int64_t n, int row_byt
   };
   if (wp) launch(seg_hist_subset_kernel<true>);
   else launch(seg_hist_subset_kernel<false>);
+  return (int)hipGetLastError();
+}
+
+// In place: wcnt [T][Wv][KB] -> exclusive per-(tree, node) prefix over waves; tot [T][KB] = node totals.
+CDNA_API int cdna_wave_scan(int* wcnt, int T, int Wv, int KB, int64_t* tot, hipStream_t st) {
+  if (T <= 0 || Wv <= 0 || KB <= 0) return 0;
+  hipLaunchKernelGGL(wave_scan_kernel, dim3((unsigned)(T * KB)), dim3(256), 0, st, wcnt, Wv, KB, tot);
   return (int)hipGetLastError();
 }
