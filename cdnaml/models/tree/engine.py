@@ -963,29 +963,36 @@ class ForestTrainer:
                 mb = p.impurity == "xgb" and self.data.missing_bin
                 so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
                                        p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight, missing_bin=mb)
-                gain, bf, bb = so[:, 0], so[:, 1].long(), so[:, 2].long()
-                lst, rst = so[:, 3:5], so[:, 5:7]
-                order, cat_feats, miss_right = None, [], (so[:, 7] > 0.5 if mb else None)
+                # so [A, 8] = gain, feature, bin, left (2), right (2), missing-goes-right: copied to the host as is
+                # (plus the node totals at level 0), no per-column device ops
+                sw = so.shape[1]
+                host = (torch.cat([so, tot], 1) if depth == 0 else so).cpu().numpy()
+                gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
+                lst_h, rst_h = host[:, 3:5], host[:, 5:7]
+                mr_h = host[:, 7] > 0.5 if mb else None
+                if depth == 0:
+                    a_stats = host[:, sw:sw + tot.shape[1]].copy()
+                order, cat_feats = None, []
             else:
                 tot = self._node_stats(H, None)
                 gain, bf, bb, lst, rst, order, cat_feats, miss_right = self._best_splits(H, tot, masks_t)
-            # one device->host transfer for the whole level's decisions (ids < 2^53 are exact in f64)
-            kk = lst.shape[1]
-            cols = [gain[:, None], bf[:, None].double(), bb[:, None].double(), lst, rst]
-            if miss_right is not None:
-                cols.append(miss_right[:, None].double())
-            if depth == 0:
-                cols.append(tot)
-            host = torch.cat(cols, 1).cpu().numpy()
-            gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
-            lst_h, rst_h = host[:, 3:3 + kk], host[:, 3 + kk:3 + 2 * kk]
-            c0 = 3 + 2 * kk
-            mr_h = None
-            if miss_right is not None:
-                mr_h = host[:, c0] != 0
-                c0 += 1
-            if depth == 0:
-                a_stats = host[:, c0:c0 + tot.shape[1]].copy()
+                # one device->host transfer for the whole level's decisions (ids < 2^53 are exact in f64)
+                kk = lst.shape[1]
+                cols = [gain[:, None], bf[:, None].double(), bb[:, None].double(), lst, rst]
+                if miss_right is not None:
+                    cols.append(miss_right[:, None].double())
+                if depth == 0:
+                    cols.append(tot)
+                host = torch.cat(cols, 1).cpu().numpy()
+                gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
+                lst_h, rst_h = host[:, 3:3 + kk], host[:, 3 + kk:3 + 2 * kk]
+                c0 = 3 + 2 * kk
+                mr_h = None
+                if miss_right is not None:
+                    mr_h = host[:, c0] != 0
+                    c0 += 1
+                if depth == 0:
+                    a_stats = host[:, c0:c0 + tot.shape[1]].copy()
             order_h = order.cpu().numpy() if order is not None else None
             _split_span.__exit__(None, None, None)
             # ---- create forest nodes for the active set, decide splits

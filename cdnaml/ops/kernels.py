@@ -1057,10 +1057,9 @@ SEG_PRIV_CHUNK = int(__import__("os").environ.get("CDNAML_SEG_PRIV_CHUNK", "6553
 
 def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False):
     G, n, _ = bins.shape
-    out = torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
     if S == 0 or len(segs) == 0:
-        return out
+        return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
     assert _native(bins) and bins_rm is not None and rec.dtype == torch.int64
     wm = int(max(1, min(255, wmax)))
     priv = SEG_PRIV and B <= 64
@@ -1070,7 +1069,7 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
     chunk = _fill_chunk(segs, chunk)
     work = _seg_work(segs, chunk)
     if len(work) == 0:
-        return out
+        return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
     if interleave and len(segs) > 1:
         sg = segs[segs[:, 1] > 0]
         k = (sg[:, 1] + chunk - 1) // chunk
@@ -1078,7 +1077,7 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
     qs1 = float(scales[1])
     wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
-    iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
+    iout = torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
     assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
     _lib.check(_lib.lib().cdna_seg_hist(1 | 4 | 16 | (32 if priv else 0) | (64 if split4 else 0), _ptr(bins_rm), n,
                                         d, B, _ptr(rec), None,
@@ -1087,7 +1086,7 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
                                         _stream(bins.device)), "cdna_seg_hist(rec)")
     if raw:
         return iout
-    out.copy_(iout)
+    out = iout.double()
     out[..., 1] /= qs1
     return out
 
