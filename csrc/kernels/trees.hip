@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
                                                       const float* __restrict__ thr, const int* __restrict__ nthr,
                                                       int tmax, int rows_per_tile, int steps, int miss_on,
                                                       float miss_val, uint64_t* __restrict__ out,
-                                                      uint64_t* __restrict__ rm, int Gs) {
+                                                      uint64_t* __restrict__ rm, int Gs, int tpad) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int G = (d + 7) / 8;
   // [rows_per_tile][dp]: an odd row stride keeps the per-task x reads (lanes = rows) conflict-free; with
@@ -97,8 +97,18 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
   const int dp = d | 1;
   float* sx = smf;                                  // [rows_per_tile][dp]
   float* sthr = smf + (size_t)rows_per_tile * dp;   // [d][tmax]
-  int* snt = reinterpret_cast<int*>(sthr + (size_t)d * tmax);
-  for (int i = threadIdx.x; i < d * tmax; i += 256) sthr[i] = thr[i];
+  int* snt = reinterpret_cast<int*>(sthr + (size_t)d * (tpad > 0 ? tpad : tmax));
+  // tpad > 0: each feature's table padded with +inf to tpad = 2^steps entries, so the search reads
+  // sthr[f * tpad + cand - 1] unconditionally (no per-step bound test / select)
+  const int tst = tpad > 0 ? tpad : tmax;
+  if (tpad > 0) {
+    for (int i = threadIdx.x; i < d * tpad; i += 256) {
+      const int f = i / tpad, c = i - f * tpad;
+      sthr[i] = c < nthr[f] ? thr[f * tmax + c] : __builtin_inff();
+    }
+  } else {
+    for (int i = threadIdx.x; i < d * tmax; i += 256) sthr[i] = thr[i];
+  }
   for (int i = threadIdx.x; i < d; i += 256) snt[i] = nthr[i];
   const bool contiguous = ldx == d && (d % 4) == 0;
   // register double buffer: the next tile's float4s are in flight while the
@@ -171,7 +181,7 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
         // XGBoost missing values (NaN or == missing) -> -inf -> bin 0 (thresholds start at -FLT_MAX)
         if (miss_on && (x[j] != x[j] || x[j] == miss_val)) x[j] = -__builtin_inff();
         nt[j] = g * 8 + j < d ? snt[f] : 0;
-        toff[j] = f * tmax - 1;
+        toff[j] = f * tst - 1;
         lo[j] = 0;
       }
 #pragma unroll
@@ -181,7 +191,7 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int cand = lo[j] + step;
-          const float tv = cand <= nt[j] ? sthr[toff[j] + cand] : __builtin_inff();
+          const float tv = tpad > 0 ? sthr[toff[j] + cand] : (cand <= nt[j] ? sthr[toff[j] + cand] : __builtin_inff());
           lo[j] = tv < x[j] ? cand : lo[j];
         }
       }
@@ -783,7 +793,16 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
   if (n <= 0) return 0;
   {
     // v2: tile of rows in LDS next to the thresholds (<= 64 KB per block)
-    const size_t tb = (size_t)d * (tmax > 0 ? tmax : 1) * 4 + (size_t)d * 4;
+    // CDNAML_BINIZE_PAD=1: +inf-padded power-of-two threshold tables (branch-free search steps).  Opt-in:
+    // measured equal (28.5 ms either way at 1e8 x 100 x 40 bins), so the per-step bound test is not the limit
+    static const bool pad_on = [] {
+      const char* e = getenv("CDNAML_BINIZE_PAD");
+      return e && atoi(e) != 0;
+    }();
+    int steps0 = 0;
+    while ((1 << steps0) <= tmax) ++steps0;
+    const int tpad = (pad_on && tmax > 0) ? (1 << steps0) : 0;
+    const size_t tb = (size_t)d * (tpad > 0 ? tpad : (tmax > 0 ? tmax : 1)) * 4 + (size_t)d * 4;
     const size_t dp = (size_t)(d | 1);
     // up to 64 KB per block (2+ blocks per CU); large threshold tables (maxBins 256 at d = 100: 100 KB)
     // opt in to 150 KB rather than falling back to v1 (253 ms at 1e8 x 100 x 256 bins)
@@ -805,7 +824,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(binize2_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(binize2_kernel, dim3(grid_for(n, rpt, 8192)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
-                         tmax > 0 ? tmax : 1, rpt, steps, miss_on, miss_val, out, rm, Gs);
+                         tmax > 0 ? tmax : 1, rpt, steps, miss_on, miss_val, out, rm, Gs, tpad);
       return (int)hipGetLastError();
     }
   }
