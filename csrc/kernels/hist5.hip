@@ -899,7 +899,7 @@ constexpr int kP7MaxA = 1024;
 constexpr int kP7MaxT = 64;
 constexpr int kP7MaxG = 16;  // MAXG template: 8 / 13 / 16 words per row (registers sized to the row)
 constexpr int kP7TB = 24;
-template <int MAXG>
+template <int MAXG, bool LADDER>
 __global__ __launch_bounds__(256) void partition7_kernel(const uint64_t* __restrict__ bins, int64_t n, int G, int T,
                                                          int A, uint16_t* __restrict__ codes,
                                                          const int* __restrict__ tfirst,
@@ -937,9 +937,11 @@ __global__ __launch_bounds__(256) void partition7_kernel(const uint64_t* __restr
     uint32_t c[kP7TB];
 #pragma unroll
     for (int u = 0; u < kP7TB; ++u) c[u] = (cc[u] >> (16 * half)) & 0xFFFFu;
+    if (!LADDER) {
 #pragma unroll
-    for (int g = 0; g < MAXG; ++g)
-      if (g < G) tile7[g * 256 + lr] = w[g];
+      for (int g = 0; g < MAXG; ++g)
+        if (g < G) tile7[g * 256 + lr] = w[g];
+    }
     for (int t0 = 0; t0 < T; t0 += kP7TB) {
       if (t0 > 0) {
 #pragma unroll
@@ -954,7 +956,21 @@ __global__ __launch_bounds__(256) void partition7_kernel(const uint64_t* __restr
         const int f = fb & 0xFFFF;
         uint32_t nl = 0xFFu;
         if (f != 0xFFFF) {
-          const int bin = tb[((f >> 3) * 256 + lr) * 8 + (f & 7)];
+          int bin;
+          if (LADDER) {
+            // LADDER (opt-in CDNAML_PARTITION7_LADDER): the bin byte is selected from the row's registers (no LDS
+            // tile: 7 instead of 4 resident waves per SIMD); measured slower, 26.9 vs 19.9 ms per step at 1e8
+            const int wi = f >> 2;
+            uint32_t word = (uint32_t)w[0];
+#pragma unroll
+            for (int jj = 1; jj < 2 * MAXG; ++jj) {
+              const uint32_t v = (jj & 1) ? (uint32_t)(w[jj >> 1] >> 32) : (uint32_t)w[jj >> 1];
+              word = wi == jj ? v : word;
+            }
+            bin = (int)((word >> ((f & 3) * 8)) & 0xFFu);
+          } else {
+            bin = tb[((f >> 3) * 256 + lr) * 8 + (f & 7)];
+          }
           const int co = s_co[id];
           const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u : bin <= (fb >> 16);
           nl = s_ch[2 * id + (left ? 0 : 1)];
@@ -1238,7 +1254,7 @@ CDNA_API int cdna_partition7(const uint64_t* bins, int64_t n, int G, int T, int 
                              const int* cat_off, const uint32_t* cat_mask, const int* child, hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
   if (G <= 0 || G > kP7MaxG || A > kP7MaxA || T > kP7MaxT || G * 8 > 0xFFFF) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)G * 256 * 8;
+  size_t lds = (size_t)G * 256 * 8;
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   // exactly the resident blocks (one round): a 4-per-CU grid with only 3 resident per CU (LDS) ran a
@@ -1250,9 +1266,20 @@ CDNA_API int cdna_partition7(const uint64_t* bins, int64_t n, int G, int T, int 
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, bins, n, G, T, A, codes, tfirst, tfirst_next, split_feat,
                        split_bin, cat_off, cat_mask, child);
   };
-  if (G <= 8) launch(partition7_kernel<8>);
-  else if (G <= 13) launch(partition7_kernel<13>);
-  else launch(partition7_kernel<16>);
+  static const bool ladder = [] {
+    const char* e = getenv("CDNAML_PARTITION7_LADDER");
+    return e && atoi(e) != 0;
+  }();
+  if (ladder) {
+    const size_t lds0 = lds;
+    lds = 0;
+    if (G <= 8) launch(partition7_kernel<8, true>);
+    else if (G <= 13) launch(partition7_kernel<13, true>);
+    else launch(partition7_kernel<16, true>);
+    lds = lds0;
+  } else if (G <= 8) launch(partition7_kernel<8, false>);
+  else if (G <= 13) launch(partition7_kernel<13, false>);
+  else launch(partition7_kernel<16, false>);
   return (int)hipGetLastError();
 }
 
