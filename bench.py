@@ -58,13 +58,10 @@ def main():
     d = args.features
     log(f"world={W} device={dev} rows/rank={n} features={d}")
 
-    # ---- synthetic data, generated in HBM (rank-disjoint streams)
-    g = torch.Generator(device=dev).manual_seed(args.seed * 1000 + rank)
-    X = torch.randn((n, d), generator=g, device=dev, dtype=torch.float32)
-    wvec = torch.randn(d, generator=torch.Generator(device=dev).manual_seed(args.seed), device=dev)
-    y = (X @ wvec).double()
-    y += 2.0 * torch.sin(X[:, 0].double() * 2.0) + (X[:, 1] > 0.5).double() * 3.0
-    y += 0.1 * torch.randn(n, generator=g, device=dev, dtype=torch.float64)
+    # ---- synthetic data, generated in HBM, keyed by GLOBAL row id (Philox): the 1e8-row table is the same
+    # whatever the GPU count, so every N trains the identical forest (same nodes / digest)
+    from cdnaml.utils.synthetic import forest_digest, regression_shard
+    X, y, _ = regression_shard(n_total, d, args.seed, rank, W, dev)
     df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -110,7 +107,7 @@ def main():
     ok = bool(torch.isfinite(p).all())
     corr = float(torch.corrcoef(torch.stack([p[:1000000], y[:1000000]]))[0, 1]) if n > 1 else float("nan")
     log(f"step {ms:.1f} ms, {rows_per_s:.3e} rows/s, pred finite={ok}, corr(pred,label)={corr:.3f}, "
-        f"nodes={model.totalNumNodes}")
+        f"nodes={model.totalNumNodes} digest={forest_digest(model._forest)}")
     log("host step marks (ms): " + " ".join(f"{(b - a) * 1e3:.1f}" for a, b in zip([t0] + marks[:-1], marks)))
     if args.trace:
         tracing.reset()
@@ -134,7 +131,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (HBM-generated gaussian features, nonlinear label)",
+            "data": "synthetic (Philox gaussian features keyed by global row id, generated in HBM; nonlinear label)",
             "config": {"model": f"RandomForestRegressor(numTrees={args.trees},maxDepth={args.depth},"
                                 f"maxBins={args.bins})",
                        "global_batch": n_total, "seq_len": None, "num_features": d,

@@ -715,8 +715,9 @@ def boost(session, data, y_target_fn, grad_fn, T_rounds, est, seed, init_margin,
     weights = []
     # checkpointInterval + SparkContext.setCheckpointDir: resume from the last saved round
     from .tree.checkpoint import RoundCheckpointer
-    ck = RoundCheckpointer(session, est, data.n_global, data.d,
-                           est.getCheckpointInterval() if est.hasParam("checkpointInterval") else None)
+    ck = RoundCheckpointer(session, est, data,
+                           est.getCheckpointInterval() if est.hasParam("checkpointInterval") else None,
+                           labels=y_target_fn(F))
     start = 0
     resumed = ck.load()
     if resumed is not None:
@@ -733,6 +734,7 @@ def boost(session, data, y_target_fn, grad_fn, T_rounds, est, seed, init_margin,
         K.predict_binned_add(data.bins, nodes, 0, vals, masks, wgt, F)
         weights.append(wgt)
         ck.maybe_save(m + 1, forest, F, {"weights": weights})
+    ck.finish()
     return forest, np.asarray(weights)
 
 

@@ -604,6 +604,10 @@ class ForestTrainer:
         self.classification = params.impurity in ("gini", "entropy")
         self.C = params.num_classes if self.classification else 0
         self.stats_k = self.C if self.classification else 2
+        # the largest shard over all ranks: every histogram-path decision below is made from values all ranks
+        # agree on, so every rank issues the same collectives (count, dtype) whatever its own row count
+        self.n_max = data.n_local if not self.comm.distributed else int(
+            self.comm.all_reduce_scalar(float(data.n_local), "max"))
 
     # ------------------------------------------------------------ helpers
     def _feature_masks(self, trees: np.ndarray, node_keys: np.ndarray) -> np.ndarray:
@@ -817,7 +821,7 @@ class ForestTrainer:
         # each level's histogram the rows of the nodes it builds are gathered into slot segments, so the
         # histogram touches only those rows
         mseg_ok = (USE_MSEG and USE_CODES and (T > 1 or (MSEG_T1 and stats_rows.get("v0") is None)) and
-                   not self.classification and p.max_depth <= 8 and T * n < 2 ** 31 and n > 0)
+                   not self.classification and p.max_depth <= 8 and T * self.n_max < 2 ** 31 and data.n_global > 0)
         # ... and with per-node feature subsets (RandomForest) only each node's sampled features are
         # accumulated (packed statistics only: no v0)
         subset_seg = mseg_ok and need_masks and MSEG_SUBSET and stats_rows.get("v0") is None
@@ -837,19 +841,22 @@ class ForestTrainer:
             v1p = stats_rows["v1"].float()[pl].contiguous()
             v0p = None if stats_rows.get("v0") is None else stats_rows["v0"].float()[pl].contiguous()
             wp = None if (w1 is None or wmax <= 1) else w1[pl].to(torch.uint8).contiguous()
-            seg_scales = K.seg_scales(v0p, v1p, wmax, n) if perm.numel() else (1.0, 1.0)
+            # scales agreed over all ranks (max |v|, max weight, global row count): the int64 fixed-point
+            # level histograms all-reduce exactly, so the tree does not depend on the GPU count
+            seg_scales = K.seg_scales(v0p, v1p, wmax, data.n_global, self.comm)
+            seg_raw = seg_scales if v0p is not None else seg_scales[1]
             segs = np.array([[0, perm.numel()]], dtype=np.int64)
             node = None
         elif use_codes:
             codes, wmax = K.codes_init_max(weights, T, n, dev)
             node = None
             if use_mseg:
-                if stats_rows.get("v0") is None:
-                    # one quantisation scale for every rank: the int64 level histograms then all-reduce to
-                    # the same sums on 1 or N GPUs (the forest does not depend on the GPU count)
-                    mseg_scales = (1.0, K.packed_scale_global(stats_rows["v1"].float(), self.comm))
-                else:
-                    mseg_scales = K.seg_scales(stats_rows["v0"].float(), stats_rows["v1"].float(), wmax, n)
+                # one quantisation scale for every rank: the int64 level histograms then all-reduce to
+                # the same sums on 1 or N GPUs (the forest does not depend on the GPU count)
+                v0s = stats_rows.get("v0")
+                mseg_scales = K.seg_scales(None if v0s is None else v0s.float(), stats_rows["v1"].float(), wmax,
+                                           data.n_global, self.comm)
+                mseg_raw = mseg_scales[1] if v0s is None else mseg_scales
         else:
             node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
                 torch.zeros((T, 0), dtype=torch.int32, device=dev)
@@ -895,8 +902,10 @@ class ForestTrainer:
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
                 if use_mseg and (depth >= 1 or MSEG_L0):
                     # gather the rows of the built nodes into slot segments, then segment histograms
-                    rec_ok = (MSEG_REC and dev.type == "cuda" and stats_rows.get("v0") is None and
-                              not subset_seg and 8 * B * 8 <= 128 * 1024)
+                    # packed item records on every device (the CPU emulates the HIP compaction + flat histogram
+                    # exactly, so gloo ranks traverse the integer path RCCL ranks take)
+                    rec_ok = (MSEG_REC and stats_rows.get("v0") is None and not subset_seg and
+                              8 * B * 8 <= 128 * 1024)
                     perm, v0p, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, len(build_ids),
                                                              stats_rows.get("v0"), stats_rows["v1"],
                                                              rec_scale=mseg_scales[1] if rec_ok else None)
@@ -911,8 +920,8 @@ class ForestTrainer:
                     else:
                         Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax,
                                         mseg_scales, bins_rm=data.row_major_bins() if dev.type == "cuda" else None,
-                                        interleave=True, rec=is_rec, raw=is_rec)
-                        hist_raw_scale = mseg_scales[1] if is_rec else None
+                                        interleave=True, rec=is_rec, raw=True)
+                        hist_raw_scale = mseg_raw
                     del perm, v0p, v1p, wp
                 elif use_seg:
                     sb = np.stack([segs[build_ids, 0], segs[build_ids, 1], slot_of[build_ids].astype(np.int64)], 1)
@@ -921,7 +930,8 @@ class ForestTrainer:
                                     # row-major copy; dense shallow levels stream the [G][n] layout
                                     bins_rm=data.row_major_bins() if (K.SEG_ROW_MAJOR and dev.type == "cuda"
                                                                       and len(build_ids) >= 4) else None,
-                                    interleave=use_mseg)
+                                    interleave=use_mseg, raw=True)
+                    hist_raw_scale = seg_raw
                 elif use_codes:
                     Hb = K.hist_codes(1 if self.classification else 0, data.bins, d, codes, tfirst,
                                       stats_rows.get("v0"), stats_rows.get("v1"), stats_rows.get("label"), self.C,
@@ -939,24 +949,12 @@ class ForestTrainer:
             # ---- assemble every active node's histogram
             derived = np.nonzero(~build)[0]
             is_raw = Hb.dtype == torch.int64
-            if dev.type == "cuda" and (is_raw or len(derived)):
-                # one kernel: fixed-point -> fp64 and parent - sibling for the derived nodes
+            if is_raw or len(derived):
+                # one kernel (CPU: the same arithmetic in torch): fixed-point -> fp64 and parent - sibling
                 H = K.hist_assemble(Hb, hist_raw_scale if is_raw else None, prev_hist if len(derived) else None,
                                     slot_of, a_parent, a_sib)
             else:
-                if is_raw:  # exact fixed-point sums (count, sum * scale) -> fp64 moments
-                    Hb = Hb.double()
-                    Hb[..., 1] /= hist_raw_scale
-                if len(derived) == 0:
-                    H = Hb
-                else:
-                    H = torch.empty((A, d, B, self.stats_k), dtype=torch.float64, device=dev)
-                    if len(build_ids):
-                        H[torch.from_numpy(build_ids).to(dev)] = Hb
-                    di = torch.from_numpy(derived).to(dev)
-                    par = torch.from_numpy(a_parent[derived]).to(dev)
-                    sib = torch.from_numpy(a_sib[derived]).to(dev)
-                    H[di] = prev_hist[par] - H[sib]
+                H = Hb
             masks_t = torch.from_numpy(masks_np.view(np.int32)).to(dev) if masks_np is not None else None
             if self._native_split(dev):
                 # K6 in one kernel: node totals, prefix scans, gains, masks, argmax

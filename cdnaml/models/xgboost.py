@@ -176,7 +176,7 @@ class _XgbEstimatorBase(Estimator):
         best, best_round, history = float("inf"), -1, []
         train_w = None if val_mask is None else (~val_mask).to(torch.uint8)
         from .tree.checkpoint import RoundCheckpointer
-        ck = RoundCheckpointer(session, self, data.n_global, data.d, self.getCheckpoint_interval())
+        ck = RoundCheckpointer(session, self, data, self.getCheckpoint_interval(), labels=y)
         start = 0
         resumed = ck.load()
         if resumed is not None:
@@ -217,6 +217,7 @@ class _XgbEstimatorBase(Estimator):
                     forest = _truncate(forest, keep)
                     break
             ck.maybe_save(m + 1, forest, F, {"best": best, "best_round": best_round, "history": history})
+        ck.finish()
         return forest, history
 
     def _apply_l1(self, forest: Forest, t: int):
@@ -275,8 +276,8 @@ class XgboostRegressor(_XgbEstimatorBase):
                 s = torch.sqrt(1 + r * r)
                 g, h = r / s, 1 / (s * s * s)
             elif obj == "count:poisson":
-                e = torch.exp(f)
-                g, h = e - yf, e * math.exp(0.7)
+                e = torch.exp(f.double())
+                g, h = (e - yf.double()).float(), (e * math.exp(0.7)).float()
             else:
                 raise IllegalArgumentException(f"unsupported objective {obj}")
             if wf is not None:
@@ -412,16 +413,18 @@ class XgboostClassifier(_XgbEstimatorBase):
         def grad_hess(F):
             if F.is_cuda:
                 return K.grad_hess(F, yi.float(), wf, 4 if n_out == 1 else 5)  # K9 HIP kernel
+            # host path in fp64, rounded once to fp32: vectorised and scalar-tail transcendentals then agree,
+            # so a row's gradient does not depend on where the shard boundary puts it (any world size)
             if n_out == 1:
-                pr = _sigmoid(F[:, 0])
-                g = pr - yi.float()
-                h = (pr * (1 - pr)).clamp_min(1e-16)
+                pr = _sigmoid(F[:, 0].double())
+                g = (pr - yi.double()).float()
+                h = (pr * (1 - pr)).clamp_min(1e-16).float()
                 g, h = g[:, None], h[:, None]
             else:
-                pr = torch.softmax(F, dim=1)
-                oh = torch.nn.functional.one_hot(yi.clamp(0, C - 1), C).float()
-                g = pr - oh
-                h = (2.0 * pr * (1 - pr)).clamp_min(1e-16)
+                pr = torch.softmax(F.double(), dim=1)
+                oh = torch.nn.functional.one_hot(yi.clamp(0, C - 1), C).double()
+                g = (pr - oh).float()
+                h = (2.0 * pr * (1 - pr)).clamp_min(1e-16).float()
             if wf is not None:
                 g, h = g * wf[:, None], h * wf[:, None]
             return g, h

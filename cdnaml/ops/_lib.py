@@ -50,12 +50,36 @@ def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     srcs = sorted(glob.glob(os.path.join(_SRC_DIR, "*.hip")))
     tmp = LIB_PATH + f".tmp{os.getpid()}"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-o", tmp] + srcs
-    if verbose:
-        print(" ".join(cmd))
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed building {LIB_PATH}:\n{res.stderr[-4000:]}")
+    objdir = os.path.join(_OUT_DIR, f".obj{os.getpid()}")
+    os.makedirs(objdir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = [hipcc] + flags + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr[-4000:]}")
+        return obj
+
+    # one translation unit per kernel file, compiled in parallel, then one link
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+    try:
+        with ThreadPoolExecutor(jobs) as ex:
+            objs = list(ex.map(compile_one, srcs))
+        cmd = [hipcc] + flags + ["-shared", "-o", tmp] + objs
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"hipcc link failed building {LIB_PATH}:\n{res.stderr[-4000:]}")
+    finally:
+        for f in glob.glob(os.path.join(objdir, "*")):
+            os.remove(f)
+        os.rmdir(objdir)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 
@@ -138,8 +162,8 @@ _SIGS = {
     "cdna_score_hist": ([c_void_p, c_void_p, c_int64, c_double, c_double, c_int, c_void_p, c_void_p], c_int),
     "cdna_kmeans_step": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_void_p], c_int),
-    "cdna_hist_assemble": ([c_void_p, c_int, c_double, c_void_p, c_void_p, c_int, c_int64, c_int, c_void_p,
-                            c_void_p], c_int),
+    "cdna_hist_assemble": ([c_void_p, c_int, c_double, c_double, c_void_p, c_void_p, c_int, c_int64, c_int,
+                            c_void_p, c_void_p], c_int),
     "cdna_grad_hess": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_logistic_grad": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_double, c_void_p,
                             c_void_p, c_void_p], c_int),

@@ -90,25 +90,52 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
 
 
 # ------------------------------------------------------- level histogram assembly
-def hist_assemble(Hb: torch.Tensor, raw_scale: Optional[float], prev: Optional[torch.Tensor], slot: np.ndarray,
+def hist_assemble(Hb: torch.Tensor, raw_scale, prev: Optional[torch.Tensor], slot: np.ndarray,
                   parent: np.ndarray, sib: np.ndarray) -> torch.Tensor:
     """fp64 histograms [A, d, B, K] of a level's active nodes in one launch (split.hip): built node a copies
-    Hb[slot[a]] (int64 fixed point divided by raw_scale in stat 1 when raw_scale is given); a derived node
-    (slot -1) is prev[parent[a]] - (its sibling's built histogram)."""
+    Hb[slot[a]] (int64 fixed point when ``raw_scale`` is given: a float divides stat 1, a pair (s0, s1)
+    divides stats 0 and 1); a derived node (slot -1) is prev[parent[a]] - (its sibling's built histogram)."""
     A = len(slot)
     nb, d, B, Kc = Hb.shape
     dev = Hb.device
+    s0, s1 = raw_scales(raw_scale)
+    raw = raw_scale is not None
+    if not _native(Hb):
+        src = Hb.double()
+        if raw:
+            src = src.clone()
+            src[..., 0] /= s0
+            src[..., 1] /= s1
+        H = torch.empty((A, d, B, Kc), dtype=torch.float64, device=dev)
+        sl = torch.from_numpy(np.asarray(slot, dtype=np.int64))
+        built = sl >= 0
+        if bool(built.any()):
+            H[built] = src[sl[built]]
+        der = torch.nonzero(~built).flatten()
+        if der.numel():
+            par = torch.from_numpy(np.asarray(parent, dtype=np.int64))[der]
+            sib_ = torch.from_numpy(np.asarray(sib, dtype=np.int64))[der]
+            H[der] = prev[par] - src[sl[sib_]]
+        return H
     H = torch.empty((A, d, B, Kc), dtype=torch.float64, device=dev)
     m = torch.from_numpy(np.stack([slot, parent, sib], 1).astype(np.int32).reshape(-1)).to(dev)
-    raw = raw_scale is not None
     src = Hb.contiguous() if raw else Hb.double().contiguous()
     if raw:
         assert Hb.dtype == torch.int64
     pv = None if prev is None else prev.contiguous()
-    _lib.check(_lib.lib().cdna_hist_assemble(_ptr(src), int(raw), float(raw_scale) if raw else 1.0, _ptr(pv),
+    _lib.check(_lib.lib().cdna_hist_assemble(_ptr(src), int(raw), float(s0), float(s1), _ptr(pv),
                                              _ptr(m), A, d * B * Kc, Kc, _ptr(H), _stream(dev)),
                "cdna_hist_assemble")
     return H
+
+
+def raw_scales(raw_scale):
+    """(scale of stat 0, scale of stat 1) of an int64 fixed-point histogram (1.0 = unscaled)."""
+    if raw_scale is None:
+        return 1.0, 1.0
+    if isinstance(raw_scale, (tuple, list)):
+        return float(raw_scale[0]), float(raw_scale[1])
+    return 1.0, float(raw_scale)
 
 
 # --------------------------------------------------------------------- K9
@@ -999,11 +1026,20 @@ SEG_ROW_MAJOR = __import__("os").environ.get("CDNAML_SEG_ROW_MAJOR", "1") != "0"
 SEG_PART_CHUNK = 8192
 
 
-def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_global: int):
-    """Fixed-point scales for one tree's statistics (packed when there is no v0)."""
+def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_global: int, comm=None):
+    """Fixed-point scales for one tree's statistics (packed when there is no v0).
+
+    With ``comm`` the max |v|, the max weight and ``n_global`` are agreed over every rank first: all ranks
+    then quantise identically and their int64 histograms all-reduce to the same sums on 1 or N GPUs."""
     if v0p is None:
-        return 1.0, _packed_scale(v1p)
-    return (_fixed_scale(v0p, n_global, wmax, qmax_bits=30), _fixed_scale(v1p, n_global, wmax, qmax_bits=30))
+        return 1.0, (packed_scale_global(v1p, comm) if comm is not None else _packed_scale(v1p))
+    if comm is None or not comm.distributed:
+        return (_fixed_scale(v0p, n_global, wmax, qmax_bits=30), _fixed_scale(v1p, n_global, wmax, qmax_bits=30))
+    m = torch.tensor([float(v0p.abs().max()) if v0p.numel() else 0.0,
+                      float(v1p.abs().max()) if v1p.numel() else 0.0, float(wmax)], dtype=torch.float64)
+    comm.all_reduce(m, "max")
+    w = int(m[2])
+    return (_fixed_scale(m[0:1], n_global, w, qmax_bits=30), _fixed_scale(m[1:2], n_global, w, qmax_bits=30))
 
 
 SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "1024"))
@@ -1038,21 +1074,56 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
 
     rec: ``perm`` holds packed int64 item records from ``codes_compact(rec_scale=scales[1])`` (v1p/wp unused;
     GPU with ``bins_rm`` only).  raw (with rec): return the exact int64 fixed-point sums (count, sum * scales[1])
-    instead of fp64 moments, so ranks can all-reduce integers."""
+    instead of fp64 moments, so ranks can all-reduce integers (also without rec: (sum w*q0 | count, sum w*q1)).
+    CPU: the same fixed-point integers as the HIP kernels (fp32 quantisation, int64 sums), so CPU ranks
+    traverse the exact arithmetic of the GPU path."""
     if rec:
         return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw)
-    return _seg_hist(bins, d, B, perm, v0p, v1p, wp, segs, S, wmax, scales, bins_rm, interleave)
+    return _seg_hist(bins, d, B, perm, v0p, v1p, wp, segs, S, wmax, scales, bins_rm, interleave, raw)
 
 
-# Bank-conflict experiments on the flat segment histogram (rocprofv3: 67 % of its LDS cycles are conflicts
-# of random bins).  Both opt-in, both measured slower on the headline (profiles/README.md):
-#  * SEG_PRIV: one 8-feature group per block with 16 interleaved copies (conflict-free atomics) -- 111 ms
-#    per level vs 25: the per-lane 8-byte row gathers no longer coalesce (one cache line per lane);
-#  * SEG_SPLIT4: all groups with 4 interleaved copies -- 286 vs 238 ms/step: 160 KB blocks halve occupancy.
-SEG_PRIV = __import__("os").environ.get("CDNAML_SEG_PRIV", "0") != "0"
-# flat kernel with 4 interleaved bank-split copies per cell (all groups must fit 160 KB)
-SEG_SPLIT4 = __import__("os").environ.get("CDNAML_SEG_SPLIT4", "0") != "0"
-SEG_PRIV_CHUNK = int(__import__("os").environ.get("CDNAML_SEG_PRIV_CHUNK", "65536"))
+def _seg_flat_index(bins: torch.Tensor, d: int, B: int, rows: torch.Tensor, slot: torch.Tensor) -> torch.Tensor:
+    """CPU: flat cell index slot * d * B + f * B + bin(row, f) of every (row, feature) pair, [m, d]."""
+    G, n, _ = bins.shape
+    flat = bins.permute(1, 0, 2).reshape(n, G * 8)[:, :d].long()
+    return slot[:, None] * (d * B) + torch.arange(d)[None, :] * B + flat[rows]
+
+
+def _int_hist_cpu(bins, d, B, S, rows, slot, a0, a1) -> torch.Tensor:
+    """CPU: exact int64 sums of per-item integers a0 / a1 into cells [S, d, B, 2]."""
+    out = torch.zeros(S * d * B * 2, dtype=torch.int64)
+    if rows.numel():
+        idx = _seg_flat_index(bins, d, B, rows, slot) * 2
+        out.index_add_(0, idx.reshape(-1), a0[:, None].expand(-1, d).reshape(-1))
+        out.index_add_(0, idx.reshape(-1) + 1, a1[:, None].expand(-1, d).reshape(-1))
+    return out.view(S, d, B, 2)
+
+
+def _seg_items(segs: np.ndarray):
+    """segs [k, 3] {start, len, slot} -> (item positions, item slots) as int64 tensors."""
+    segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
+    segs = segs[segs[:, 1] > 0]
+    if len(segs) == 0:
+        return torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64)
+    ln = segs[:, 1]
+    pos = np.repeat(segs[:, 0], ln) + (np.arange(int(ln.sum())) - np.repeat(np.cumsum(ln) - ln, ln))
+    return torch.from_numpy(pos), torch.from_numpy(np.repeat(segs[:, 2], ln))
+
+
+def _quant(v: torch.Tensor, scale: float, clamp: bool) -> torch.Tensor:
+    """The kernels' fixed-point quantisation: rintf(v * scale) in fp32 (clamped to +-2^23 when packed)."""
+    q = torch.round(v.float() * torch.tensor(scale, dtype=torch.float32)).to(torch.int64)
+    return q.clamp(-(1 << 23), 1 << 23) if clamp else q
+
+
+def rec_decode(rec: torch.Tensor):
+    """Packed item records -> (row, weight, quantised label) int64 tensors."""
+    r = rec.to(torch.int64)
+    return r & ((1 << 31) - 1), (r >> 31) & 0xFF, ((r >> 39) & ((1 << 25) - 1)) - (1 << 23)
+
+
+def rec_encode(rows: torch.Tensor, w: torch.Tensor, q: torch.Tensor) -> torch.Tensor:
+    return rows.to(torch.int64) | (w.to(torch.int64) << 31) | ((q.to(torch.int64) + (1 << 23)) << 39)
 
 
 def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False):
@@ -1060,30 +1131,29 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
     if S == 0 or len(segs) == 0:
         return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
-    assert _native(bins) and bins_rm is not None and rec.dtype == torch.int64
-    wm = int(max(1, min(255, wmax)))
-    priv = SEG_PRIV and B <= 64
-    split4 = SEG_SPLIT4 and not priv and -(-d // 8) * 8 * B * 8 * 4 <= 160 * 1024
-    # bank-private planes: each of the 16 copies sees 1/16 of a chunk's rows (count field headroom)
-    chunk = min(SEG_PRIV_CHUNK if priv else SEG_HIST_CHUNK, ((1 << 20) // (wm + 1)) * (16 if priv else 1))
-    chunk = _fill_chunk(segs, chunk)
-    work = _seg_work(segs, chunk)
-    if len(work) == 0:
-        return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
-    if interleave and len(segs) > 1:
-        sg = segs[segs[:, 1] > 0]
-        k = (sg[:, 1] + chunk - 1) // chunk
-        j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
-        work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
     qs1 = float(scales[1])
-    wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
-    iout = torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
-    assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
-    _lib.check(_lib.lib().cdna_seg_hist(1 | 4 | 16 | (32 if priv else 0) | (64 if split4 else 0), _ptr(bins_rm), n,
-                                        d, B, _ptr(rec), None,
-                                        None, None,
-                                        _ptr(wt), len(work), 1.0, qs1, _ptr(iout), bins_rm.shape[1],
-                                        _stream(bins.device)), "cdna_seg_hist(rec)")
+    if not _native(bins):
+        pos, slot = _seg_items(segs)
+        rows, w, q = rec_decode(rec[pos])
+        iout = _int_hist_cpu(bins, d, B, S, rows, slot, w, w * q)
+    else:
+        assert bins_rm is not None and rec.dtype == torch.int64
+        wm = int(max(1, min(255, wmax)))
+        chunk = _fill_chunk(segs, min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1)))
+        work = _seg_work(segs, chunk)
+        if len(work) == 0:
+            return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
+        if interleave and len(segs) > 1:
+            sg = segs[segs[:, 1] > 0]
+            k = (sg[:, 1] + chunk - 1) // chunk
+            j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
+            work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
+        wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
+        iout = torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
+        assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
+        _lib.check(_lib.lib().cdna_seg_hist(1 | 4 | 16, _ptr(bins_rm), n, d, B, _ptr(rec), None, None, None,
+                                            _ptr(wt), len(work), 1.0, qs1, _ptr(iout), bins_rm.shape[1],
+                                            _stream(bins.device)), "cdna_seg_hist(rec)")
     if raw:
         return iout
     out = iout.double()
@@ -1093,59 +1163,58 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
 
 def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
               v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
-              scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False) -> torch.Tensor:
+              scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False,
+              raw: bool = False) -> torch.Tensor:
     """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
 
     segs: [k, 3] {start, len, slot}.  [..., 0] = sum w*v0 (or sum w when v0p is None), [..., 1] = sum w*v1.
     interleave: order the work items by their relative position inside their segment, so that segments
     of different trees (whose rows are all sorted by row id) gather the same region of the bins at the
     same time and share it through L2 / MALL.
+    raw: return the int64 fixed-point sums (stat k scaled by ``scales[k]``; stat 0 unscaled when packed).
     """
     G, n, _ = bins.shape
-    out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
-    if S == 0 or len(segs) == 0:
-        return out
-    if not _native(bins):
-        flat = bins.permute(1, 0, 2).reshape(n, G * 8)[:, :d].long()
-        for s, ln, slot in segs:
-            if ln <= 0:
-                continue
-            rows = perm[s:s + ln].long()
-            w = torch.ones(ln, dtype=torch.float64) if wp is None else wp[s:s + ln].double()
-            a0 = w if v0p is None else w * v0p[s:s + ln].double()
-            a1 = w * v1p[s:s + ln].double()
-            bb = flat[rows]  # [ln, d]
-            idx = (torch.arange(d)[None, :] * B + bb).reshape(-1)
-            out[slot, :, :, 0] += torch.zeros(d * B, dtype=torch.float64).index_add_(
-                0, idx, a0[:, None].expand(-1, d).reshape(-1)).view(d, B)
-            out[slot, :, :, 1] += torch.zeros(d * B, dtype=torch.float64).index_add_(
-                0, idx, a1[:, None].expand(-1, d).reshape(-1)).view(d, B)
-        return out
     packed = v0p is None
     wm = int(max(1, min(255, wmax)))
-    chunk = SEG_HIST_CHUNK if not packed else min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1))
-    chunk = _fill_chunk(segs, chunk)
-    work = _seg_work(segs, chunk)
-    if len(work) == 0:
-        return out
-    if interleave and len(segs) > 1:
-        sg = segs[segs[:, 1] > 0]
-        k = (sg[:, 1] + chunk - 1) // chunk
-        j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
-        work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
+    zero = lambda: torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64,  # noqa: E731
+                               device=bins.device)
+    if S == 0 or len(segs) == 0:
+        return zero()
     qs0, qs1 = scales if scales is not None else seg_scales(v0p, v1p, wm, n)
-    wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
-    iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
-    mode = (1 if packed else 0) | (2 if wp is not None else 0) | (4 if bins_rm is not None else 0)
-    if bins_rm is not None:
-        assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
-    src = bins if bins_rm is None else bins_rm
-    _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(src), n, d, B, _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp),
-                                        _ptr(wt), len(work), float(qs0), float(qs1), _ptr(iout),
-                                        0 if bins_rm is None else bins_rm.shape[1], _stream(bins.device)),
-               "cdna_seg_hist")
-    out.copy_(iout)
+    if not _native(bins):
+        pos, slot = _seg_items(segs)
+        rows = perm[pos].long()
+        w = torch.ones(len(pos), dtype=torch.int64) if wp is None else wp[pos].to(torch.int64)
+        if packed:
+            a0, a1 = w, w * _quant(v1p[pos], qs1, True)
+        else:
+            a0, a1 = w * _quant(v0p[pos], qs0, False), w * _quant(v1p[pos], qs1, False)
+        iout = _int_hist_cpu(bins, d, B, S, rows, slot, a0, a1)
+    else:
+        chunk = SEG_HIST_CHUNK if not packed else min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1))
+        chunk = _fill_chunk(segs, chunk)
+        work = _seg_work(segs, chunk)
+        if len(work) == 0:
+            return zero()
+        if interleave and len(segs) > 1:
+            sg = segs[segs[:, 1] > 0]
+            k = (sg[:, 1] + chunk - 1) // chunk
+            j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
+            work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
+        wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
+        iout = torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
+        mode = (1 if packed else 0) | (2 if wp is not None else 0) | (4 if bins_rm is not None else 0)
+        if bins_rm is not None:
+            assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
+        src = bins if bins_rm is None else bins_rm
+        _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(src), n, d, B, _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp),
+                                            _ptr(wt), len(work), float(qs0), float(qs1), _ptr(iout),
+                                            0 if bins_rm is None else bins_rm.shape[1], _stream(bins.device)),
+                   "cdna_seg_hist")
+    if raw:
+        return iout
+    out = iout.double()
     if not packed:
         out[..., 0] /= qs0
     out[..., 1] /= qs1
@@ -1337,8 +1406,13 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
         rows = order % n
         lens = np.bincount(flat[keep].numpy(), minlength=S)[:S].astype(np.int64)
         starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if S else np.zeros(0, np.int64)
+        wts = c.reshape(-1)[order] >> 8
+        if rec_scale is not None and v0 is None and n < 2 ** 31:
+            # the packed item records of the HIP compaction (same fp32 quantisation)
+            return rec_encode(rows, wts, _quant(v1[rows], rec_scale, True)), None, None, None, \
+                np.stack([starts, lens], 1)
         return (rows.to(torch.int32), None if v0 is None else v0[rows].float(), v1[rows].float(),
-                (c.reshape(-1)[order] >> 8).to(torch.uint8), np.stack([starts, lens], 1))
+                wts.to(torch.uint8), np.stack([starts, lens], 1))
     L = _lib.lib()
     assert tfirst.numel() == T
     tf = tfirst.to(device=dev, dtype=torch.int32)

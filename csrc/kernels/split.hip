@@ -181,35 +181,42 @@ CDNA_API int cdna_split_scan(const double* H, const int* nthr, const uint32_t* m
 // Level histogram assembly (one launch instead of ~8 small torch ops + 3 copies
 // per level): every active node's fp64 moments [A][d][B][K] from the level's
 // built histograms Hb [nb][d][B][K] -- exact int64 fixed-point sums (raw = 1:
-// stat 1 divided by `scale`) or fp64 -- and, for the larger sibling, parent
-// minus sibling from the previous level's assembled histograms.
+// stat 0 divided by `scale0`, stat 1 by `scale1`) or fp64 -- and, for the
+// larger sibling, parent minus sibling from the previous level's histograms.
 // map [A][3] = (build slot or -1, parent position, sibling position).
+// Nodes are strided over gridDim.y (any A: deep levels of many trees exceed
+// the 65535 limit of one grid dimension).
 // ---------------------------------------------------------------------------
 namespace {
-__global__ __launch_bounds__(256) void hist_assemble_kernel(const void* __restrict__ Hb, int raw, double scale,
-                                                            const double* __restrict__ prev,
-                                                            const int* __restrict__ map, int64_t cells, int K,
+__global__ __launch_bounds__(256) void hist_assemble_kernel(const void* __restrict__ Hb, int raw, double scale0,
+                                                            double scale1, const double* __restrict__ prev,
+                                                            const int* __restrict__ map, int A, int64_t cells, int K,
                                                             double* __restrict__ H) {
-  const int a = blockIdx.y;
-  const int slot = map[3 * a], par = map[3 * a + 1], sib = map[3 * a + 2];
-  const int src = slot >= 0 ? slot : map[3 * sib];
-  for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += (int64_t)gridDim.x * 256) {
-    const int64_t i = (int64_t)src * cells + c;
-    double v = raw ? (double)reinterpret_cast<const long long*>(Hb)[i] : reinterpret_cast<const double*>(Hb)[i];
-    if (raw && (c % K) == 1) v = v / scale;
-    if (slot < 0) v = prev[(int64_t)par * cells + c] - v;
-    H[(int64_t)a * cells + c] = v;
+  for (int a = blockIdx.y; a < A; a += gridDim.y) {
+    const int slot = map[3 * a], par = map[3 * a + 1], sib = map[3 * a + 2];
+    const int src = slot >= 0 ? slot : map[3 * sib];
+    for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += (int64_t)gridDim.x * 256) {
+      const int64_t i = (int64_t)src * cells + c;
+      double v = raw ? (double)reinterpret_cast<const long long*>(Hb)[i] : reinterpret_cast<const double*>(Hb)[i];
+      if (raw) {
+        const int k = (int)(c % K);
+        if (k == 0 && scale0 != 1.0) v = v / scale0;
+        if (k == 1) v = v / scale1;
+      }
+      if (slot < 0) v = prev[(int64_t)par * cells + c] - v;
+      H[(int64_t)a * cells + c] = v;
+    }
   }
 }
 }  // namespace
 
-CDNA_API int cdna_hist_assemble(const void* Hb, int raw, double scale, const double* prev, const int* map, int A,
-                                int64_t cells, int K, double* H, hipStream_t st) {
+CDNA_API int cdna_hist_assemble(const void* Hb, int raw, double scale0, double scale1, const double* prev,
+                                const int* map, int A, int64_t cells, int K, double* H, hipStream_t st) {
   if (A <= 0 || cells <= 0) return 0;
-  if (A > 65535) return (int)hipErrorInvalidValue;
   int64_t gx = (cells + 255) / 256;
   if (gx > 64) gx = 64;
-  hipLaunchKernelGGL(hist_assemble_kernel, dim3((unsigned)gx, (unsigned)A), dim3(256), 0, st, Hb, raw, scale, prev,
-                     map, cells, K, H);
+  const int gy = A < 65535 ? A : 65535;
+  hipLaunchKernelGGL(hist_assemble_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, Hb, raw, scale0,
+                     scale1, prev, map, A, cells, K, H);
   return (int)hipGetLastError();
 }

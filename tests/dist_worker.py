@@ -94,7 +94,88 @@ def scenario_fault(spark):
                 "seconds": time.time() - t0}
 
 
-SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault}
+def _tree_df(spark, n=4000, d=12, seed=3, uneven=None):
+    """Partition-invariant regression/classification table (features keyed by global row id)."""
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, d))
+    y = X[:, 0] * 2.0 - X[:, 1] + np.sin(2 * X[:, 2]) + 0.1 * rng.normal(size=n)
+    pdf = pd.DataFrame({"idx": np.arange(n), "label": y, "cls": (y > 0).astype(float)})
+    from cdnaml.ml.feature import VectorAssembler
+    for i in range(d):
+        pdf[f"x{i}"] = X[:, i]
+    df = spark.createDataFrame(pdf)
+    if uneven is not None:
+        # keep a prefix of the global rows: rank shards become empty / imbalanced (filter keeps placement)
+        from cdnaml.sql import functions as F
+        df = df.filter(F.col("idx") < int(n * uneven))
+    return VectorAssembler(inputCols=[f"x{i}" for i in range(d)], outputCol="features").transform(df)
+
+
+def _tree_digests(df):
+    from cdnaml.ml.classification import RandomForestClassifier
+    from cdnaml.ml.regression import DecisionTreeRegressor, GBTRegressor, RandomForestRegressor
+    from cdnaml.ml.xgboost import XgboostClassifier, XgboostRegressor
+    from cdnaml.utils.synthetic import forest_digest
+    out = {}
+    fits = {
+        "rf20": RandomForestRegressor(numTrees=20, maxDepth=5, maxBins=40, seed=42),
+        "dt": DecisionTreeRegressor(maxDepth=6, maxBins=32),
+        "gbt": GBTRegressor(maxIter=5, maxDepth=4, seed=1),
+        "xgb_reg": XgboostRegressor(n_estimators=5, max_depth=4, learning_rate=0.3, random_state=42, missing=0.0),
+        "xgb_cls": XgboostClassifier(n_estimators=4, max_depth=3, random_state=7, labelCol="cls"),
+        "rf_cls": RandomForestClassifier(numTrees=5, maxDepth=4, seed=11, labelCol="cls"),
+    }
+    for k, est in fits.items():
+        m = est.fit(df)
+        out[k] = forest_digest(m._forest)
+        out[k + "_nodes"] = int(sum(len(m._forest.tree_nodes(t)) for t in range(len(m._forest.roots))))
+    return out
+
+
+def scenario_trees(spark):
+    """Every tree learner's fitted model is bit-identical at any world size (int64 fixed-point histograms
+    all-reduced exactly, scales agreed over ranks, data keyed by global row id)."""
+    return _tree_digests(_tree_df(spark))
+
+
+def scenario_trees_uneven(spark):
+    """Same with imbalanced shards: the first 30 % of the global rows only (at W >= 4 some ranks are
+    empty): every rank must still issue the same collectives and reach the 1-rank model."""
+    return _tree_digests(_tree_df(spark, uneven=0.3))
+
+
+def scenario_cv(spark):
+    from cdnaml.ml.evaluation import RegressionEvaluator
+    from cdnaml.ml.regression import RandomForestRegressor
+    from cdnaml.ml.tuning import CrossValidator, ParamGridBuilder
+    df = _tree_df(spark, n=3000, d=6)
+    rf = RandomForestRegressor(maxBins=32, seed=42)
+    grid = ParamGridBuilder().addGrid(rf.maxDepth, [2, 4]).addGrid(rf.numTrees, [3, 6]).build()
+    cv = CrossValidator(estimator=rf, estimatorParamMaps=grid, evaluator=RegressionEvaluator(), numFolds=3,
+                        seed=42, parallelism=2)
+    m = cv.fit(df)
+    from cdnaml.utils.synthetic import forest_digest
+    return {"avg": [round(float(v), 9) for v in m.avgMetrics], "best": forest_digest(m.bestModel._forest)}
+
+
+def scenario_als(spark):
+    from cdnaml.ml.recommendation import ALS
+    rng = np.random.default_rng(5)
+    nu, ni, r = 60, 40, 3
+    U, V = rng.normal(size=(nu, r)), rng.normal(size=(ni, r))
+    pairs = rng.choice(nu * ni, size=1500, replace=False)
+    u, i = pairs // ni, pairs % ni
+    pdf = pd.DataFrame({"userId": u, "movieId": i, "rating": (U[u] * V[i]).sum(1) + 3.0})
+    df = spark.createDataFrame(pdf)
+    m = ALS(rank=3, maxIter=5, regParam=0.05, seed=42, userCol="userId", itemCol="movieId",
+            ratingCol="rating").fit(df)
+    uf = m.userFactors.orderBy("id").toPandas()
+    return {"uf": np.round(np.stack(uf["features"].map(lambda v: np.asarray(v.toArray() if hasattr(v, "toArray")
+                                                                            else v))), 7).reshape(-1).tolist()}
+
+
+SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault, "trees": scenario_trees,
+             "trees_uneven": scenario_trees_uneven, "cv": scenario_cv, "als": scenario_als}
 
 
 def run(name):

@@ -707,6 +707,25 @@ def test_compact_records_histogram(dev):
     a = K.seg_hist(bins, d, B, p0, None, v1p, wp, sb, S, 5, sc, bins_rm=rm)
     b = K.seg_hist(bins, d, B, r1, None, None, None, sb, S, 5, sc, bins_rm=rm, rec=True)
     assert torch.equal(a, b)
+    # the CPU emulation (gloo ranks) produces the same int64 fixed-point histograms from the same codes
+    bins_c, v1_c = bins.cpu(), v1.cpu()
+    r_c, _, _, _, sg_c = K.codes_compact(codes.cpu(), tfirst, slot_of, S, None, v1_c, rec_scale=sc[1])
+    np.testing.assert_array_equal(sg, sg_c)
+    raw_g = K.seg_hist(bins, d, B, r1, None, None, None, sb, S, 5, sc, bins_rm=rm, rec=True, raw=True).cpu()
+    raw_c = K.seg_hist(bins_c, d, B, r_c, None, None, None, sb, S, 5, sc, rec=True, raw=True)
+    assert raw_g.dtype == raw_c.dtype == torch.int64 and torch.equal(raw_g, raw_c)
+    # non-record segment paths too (packed and two-statistic), raw int64
+    pc, _, v1pc, wpc, _ = K.codes_compact(codes.cpu(), tfirst, slot_of, S, None, v1_c)
+    ga = K.seg_hist(bins, d, B, p0, None, v1p, wp, sb, S, 5, sc, bins_rm=rm, raw=True).cpu()
+    ca = K.seg_hist(bins_c, d, B, pc, None, v1pc, wpc, sb, S, 5, sc, raw=True)
+    assert torch.equal(ga, ca)
+    v0 = (torch.rand(n, generator=g) + 0.1).to(dev)
+    sc2 = K.seg_scales(v0, v1, 5, n)
+    p2, v0p, v1p2, wp2, _ = K.codes_compact(codes, tfirst, slot_of, S, v0, v1)
+    p2c, v0pc, v1p2c, wp2c, _ = K.codes_compact(codes.cpu(), tfirst, slot_of, S, v0.cpu(), v1_c)
+    gb = K.seg_hist(bins, d, B, p2, v0p, v1p2, wp2, sb, S, 5, sc2, bins_rm=rm, raw=True).cpu()
+    cb = K.seg_hist(bins_c, d, B, p2c, v0pc, v1p2c, wp2c, sb, S, 5, sc2, raw=True)
+    assert torch.equal(gb, cb)
 
 
 def test_binize_lut_matches_reference(dev, monkeypatch):
@@ -818,9 +837,10 @@ def test_grad_hess_kernel(dev, obj, weighted):
     torch.testing.assert_close(hd.cpu(), h, rtol=2e-6, atol=2e-6)
 
 
-@pytest.mark.parametrize("raw", [True, False])
+@pytest.mark.parametrize("raw", [True, "pair", False])
 def test_hist_assemble(dev, raw):
-    """Level histogram assembly kernel == the torch sequence (fixed-point scale, parent - sibling)."""
+    """Level histogram assembly kernel == the torch sequence (fixed-point scale(s), parent - sibling), and ==
+    the CPU path of the same function (gloo ranks take it)."""
     g = torch.Generator().manual_seed(11)
     d, B, Kc = 7, 40, 2
     # 6 active nodes: siblings 0/1 (0 built), siblings 2/3 (3 built), 4 and 5 built without a sibling
@@ -829,9 +849,11 @@ def test_hist_assemble(dev, raw):
     sib = np.array([1, 0, 3, 2, -1, -1], dtype=np.int64)
     if raw:
         Hb = torch.randint(-2 ** 40, 2 ** 40, (4, d, B, Kc), generator=g, dtype=torch.int64)
-        scale = 2.0 ** 17
+        scale = 2.0 ** 17 if raw is True else (2.0 ** 9, 2.0 ** 21)
+        s0, s1 = K.raw_scales(scale)
         Hf = Hb.double()
-        Hf[..., 1] /= scale
+        Hf[..., 0] /= s0
+        Hf[..., 1] /= s1
     else:
         Hb = torch.randn(4, d, B, Kc, generator=g, dtype=torch.float64)
         scale, Hf = None, Hb
@@ -842,4 +864,22 @@ def test_hist_assemble(dev, raw):
     for a in np.nonzero(slot < 0)[0]:
         ref[a] = prev[parent[a]] - ref[sib[a]]
     out = K.hist_assemble(Hb.to(dev), scale, prev.to(dev), slot, parent, sib).cpu()
+    assert torch.equal(out, ref)
+    assert torch.equal(K.hist_assemble(Hb, scale, prev, slot, parent, sib), ref)
+
+
+def test_hist_assemble_many_nodes(dev):
+    """more than 65535 active nodes in one level (deep levels of many trees) -- the kernel strides
+    nodes over the grid instead of rejecting the launch."""
+    A = 70001
+    g = torch.Generator().manual_seed(3)
+    Hb = torch.randint(-2 ** 30, 2 ** 30, (A // 2 + 1, 1, 2, 2), generator=g, dtype=torch.int64)
+    prev = torch.randn(A, 1, 2, 2, generator=g, dtype=torch.float64)
+    slot = np.full(A, -1, dtype=np.int64)
+    slot[0::2] = np.arange(len(slot[0::2]))
+    sib = np.arange(A) + np.where(np.arange(A) % 2 == 0, 1, -1)
+    sib[-1] = -1
+    parent = np.arange(A) // 2
+    ref = K.hist_assemble(Hb, 2.0 ** 5, prev, slot, parent, sib)
+    out = K.hist_assemble(Hb.to(dev), 2.0 ** 5, prev.to(dev), slot, parent, sib).cpu()
     assert torch.equal(out, ref)

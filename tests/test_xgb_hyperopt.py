@@ -208,3 +208,26 @@ def test_boosting_checkpoint_resume_is_exact(spark, tmp_path, monkeypatch, kind)
     resumed = resumed_model.transform(df).select("prediction").toPandas().prediction.values
     np.testing.assert_array_equal(full, resumed)
     spark.conf.unset("cdnaml.checkpoint.dir")
+
+
+@pytest.mark.parametrize("kind", ["xgb", "gbt"])
+def test_checkpoint_never_resumes_foreign_data(spark, tmp_path, kind):
+    """two same-shape datasets fit in a row under one checkpoint dir give different models (the
+    checkpoint key carries a data fingerprint), and a completed fit leaves no checkpoint behind."""
+    import os
+    from cdnaml.ml.regression import GBTRegressor
+    spark.sparkContext.setCheckpointDir(str(tmp_path / "ck"))
+
+    def make():
+        if kind == "xgb":
+            return XgboostRegressor(n_estimators=6, max_depth=3, random_state=7, checkpoint_interval=2)
+        return GBTRegressor(maxIter=6, maxDepth=3, seed=7, checkpointInterval=2)
+
+    df1, _, _ = _reg(spark, n=800, seed=1)
+    df2, _, _ = _reg(spark, n=800, seed=2)
+    p1 = make().fit(df1).transform(df2).select("prediction").toPandas().prediction.values
+    left = [f for _, _, fs in os.walk(tmp_path / "ck") for f in fs]
+    assert left == []
+    p2 = make().fit(df2).transform(df2).select("prediction").toPandas().prediction.values
+    assert not np.array_equal(p1, p2)
+    spark.conf.unset("cdnaml.checkpoint.dir")
