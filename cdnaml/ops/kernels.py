@@ -1512,6 +1512,71 @@ def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1, re
     return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
 
 
+# --------------------------------------------------------------- K5m (MFMA)
+# forest levels where every tree builds few nodes: the level histogram as one int8 MFMA GEMM over the rows
+# (hist_mfma.hip), bit-identical to the LDS-atomic segment histograms (seg_hist raw)
+MFMA_HIST = __import__("os").environ.get("CDNAML_MFMA_HIST", "0") != "0"  # opt-in: measured slower (profiles/r2/mfma_hist_ab.md)
+_MFMA_BT = (2, 3, 4)          # cell tiles of 16 (B <= 64)
+_MFMA_NT = (2, 4, 6, 7, 8)    # column tiles of 16 (5 columns per slot, <= 25 slots per pass)
+MFMA_FPB = 8  # features (waves) per block: the block's B tile (row records -> digits) is built once for 8
+MFMA_STAGE = 512  # rows per LDS stage of hist_mfma.hip (chunks and the planar row stride are multiples)
+MFMA_BLOCKS = int(__import__("os").environ.get("CDNAML_MFMA_BLOCKS", "1024"))  # target blocks per launch
+
+
+def _mfma_tiles(B: int, ns: int):
+    bt = next((b for b in _MFMA_BT if 16 * b >= B), None)
+    nt = next((t for t in _MFMA_NT if 16 * t >= 5 * ns), None)
+    return bt, nt
+
+
+def mfma_hist_ok(dev, B: int, wmax: int) -> bool:
+    return MFMA_HIST and dev.type == "cuda" and B <= 16 * _MFMA_BT[-1] and wmax <= 127
+
+
+def planar_bins(bins: torch.Tensor):
+    """[G, n, 8] bins -> planar [d_pad = 8G, ldp] uint8 (feature-major rows, ldp = n rounded up to the MFMA
+    kernel's stage length)."""
+    G, n, _ = bins.shape
+    ldp = max(MFMA_STAGE, -(-n // MFMA_STAGE) * MFMA_STAGE)
+    out = torch.empty((G * 8, ldp), dtype=torch.uint8, device=bins.device)
+    if n:
+        _lib.check(_lib.lib().cdna_planar_bins(_ptr(bins), n, G * 8, ldp, _ptr(out), _stream(bins.device)),
+                   "cdna_planar_bins")
+    return out, ldp
+
+
+def hist_mfma(bp: torch.Tensor, ldp: int, n: int, d: int, B: int, codes: torch.Tensor, tfirst: np.ndarray,
+              build_slot: np.ndarray, S: int, v1: torch.Tensor, qs1: float) -> torch.Tensor:
+    """Exact int64 fixed-point histograms [S, d, B, 2] (count, sum w*q) of every built slot, one int8 MFMA GEMM
+    per pass of <= 25 slots (GPU).  Same integers as ``codes_compact(rec_scale=qs1)`` + ``seg_hist(raw=True)``."""
+    dev = codes.device
+    out = torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev)
+    bs = np.asarray(build_slot, dtype=np.int64)
+    tf = np.asarray(tfirst, dtype=np.int64)
+    act = np.nonzero(bs >= 0)[0]
+    if S == 0 or len(act) == 0:
+        return out
+    order = act[np.argsort(bs[act], kind="stable")]
+    tree = np.searchsorted(tf, order, side="right") - 1
+    loc = order - tf[tree]
+    slots = bs[order]
+    v1c = v1.float().contiguous()
+    nfg = -(-d // MFMA_FPB)
+    nchunks = max(1, MFMA_BLOCKS // nfg)
+    per = -(-max(n, 1) // nchunks)
+    chunk = min(1 << 24, max(MFMA_STAGE, -(-per // MFMA_STAGE) * MFMA_STAGE))
+    for p0 in range(0, len(order), 25):
+        sl = slice(p0, p0 + 25)
+        ns = len(order[sl])
+        bt, nt = _mfma_tiles(B, ns)
+        acc = torch.zeros((d, bt * 16, nt * 16), dtype=torch.int64, device=dev)
+        meta = torch.from_numpy(np.stack([tree[sl], loc[sl], slots[sl]]).astype(np.int32)).to(dev)
+        _lib.check(_lib.lib().cdna_hist_mfma(_ptr(bp), ldp, n, d, B, bt, nt, _ptr(codes), _ptr(meta[0]),
+                                             _ptr(meta[1]), _ptr(meta[2]), ns, _ptr(v1c), float(qs1), chunk,
+                                             MFMA_FPB, _ptr(acc), _ptr(out), _stream(dev)), "cdna_hist_mfma")
+    return out
+
+
 BINS_RM_PAD = __import__("os").environ.get("CDNAML_BINS_RM_PAD", "1") != "0"
 
 
