@@ -2,11 +2,17 @@
 
 ``CrossValidator`` assigns folds from a Philox uniform keyed by (seed, GLOBAL
 row id) — the same folds on 1 or 8 GPUs — materialises the fold-tagged data
-once in HBM (``cache``), and evaluates folds × param maps.  ``parallelism``
-> 1 runs param maps concurrently on separate HIP streams of the same GPU
-(single-process jobs); in multi-GPU SPMD jobs each fit is itself data-parallel
-over all ranks and maps run in lock-step order.  Reference: ML 07 - Random
-Forests and Hyperparameter Tuning.py:72-158 ("4 maps × 3 folds + 1 refit").
+once in HBM (``cache``), and evaluates folds × param maps.
+
+For the engine's DecisionTree / RandomForest estimators the folds × maps run
+through ``tree/fused.py``: the dataset is binned ONCE, a fold is a weight mask,
+and every map of a (numTrees, maxDepth) grid is a prefix of one forest per fold
+("4 maps × 3 folds + 1 refit" = 3 forest fits + 1 refit on shared bins).
+Other estimators take the generic path: ``parallelism`` > 1 runs param maps
+concurrently on separate HIP streams of the same GPU (single-process jobs); in
+multi-GPU SPMD jobs each fit is itself data-parallel over all ranks and maps
+run in lock-step order.  Reference: ML 07 - Random Forests and Hyperparameter
+Tuning.py:72-158.
 """
 from __future__ import annotations
 
@@ -20,6 +26,7 @@ import torch
 from ..sql import functions as F
 from .base import Estimator, Model
 from .param import NO_DEFAULT, Param, TypeConverters as TC, keyword_init
+from .tree.fused import FusedTreeTuner
 
 
 class ParamGridBuilder:
@@ -106,10 +113,21 @@ class CrossValidator(Estimator):
                 "__fold", F.floor(F.col("__u") * k).cast("int")).drop("__u").cache()
         metrics = np.zeros((len(maps), k))
         subs = [[None] * len(maps) for _ in range(k)]
+        fused = FusedTreeTuner(est, maps, dataset) if (not fold_col and FusedTreeTuner.supported(est, maps)) \
+            else None
         for f in range(k):
-            train = tagged.filter(F.col("__fold") != f).drop("__fold")
             valid = tagged.filter(F.col("__fold") == f).drop("__fold")
-            res = _run_maps(est, maps, train, valid, ev, self.getParallelism(), session)
+            if fused is not None:
+                valid = valid.cache()  # evaluated once per map: compact the fold's rows once
+                # one binned dataset, the fold as a weight mask, one forest per map group (tree/fused.py)
+                folds = fused.fold_ids(seed, k)
+                models = fused.fit_split(folds != f)
+                res = [(m, ev.evaluate(m.transform(valid))) for m in models]
+            else:
+                train = tagged.filter(F.col("__fold") != f).drop("__fold")
+                res = _run_maps(est, maps, train, valid, ev, self.getParallelism(), session)
+            if fused is not None:
+                valid.unpersist()
             for j, (m, met) in enumerate(res):
                 metrics[j, f] = met
                 if self.getCollectSubModels():
@@ -117,7 +135,7 @@ class CrossValidator(Estimator):
         avg = metrics.mean(1)
         std = metrics.std(1)
         best = int(np.argmax(avg) if ev.isLargerBetter() else np.argmin(avg))
-        best_model = est.fit(dataset, maps[best])
+        best_model = fused.refit(best) if fused is not None else est.fit(dataset, maps[best])
         tagged.unpersist()
         cvm = CrossValidatorModel(best_model, avg.tolist(), subs if self.getCollectSubModels() else None,
                                   std.tolist())
@@ -227,10 +245,17 @@ class TrainValidationSplit(Estimator):
         tr = self.getTrainRatio()
         train, valid = dataset.randomSplit([tr, 1 - tr], seed)
         train, valid = train.cache(), valid.cache()
-        res = _run_maps(est, maps, train, valid, ev, self.getParallelism(), dataset._session)
+        if FusedTreeTuner.supported(est, maps):
+            fused = FusedTreeTuner(est, maps, dataset)
+            # randomSplit's own draw (sql/dataframe.py): the row is in `train` iff its uniform < tr
+            models = fused.fit_split(fused.row_uniform(seed) < tr)
+            res = [(m, ev.evaluate(m.transform(valid))) for m in models]
+        else:
+            fused = None
+            res = _run_maps(est, maps, train, valid, ev, self.getParallelism(), dataset._session)
         metrics = [m for _, m in res]
         best = int(np.argmax(metrics) if ev.isLargerBetter() else np.argmin(metrics))
-        bm = est.fit(dataset, maps[best])
+        bm = fused.refit(best) if fused is not None else est.fit(dataset, maps[best])
         tvm = TrainValidationSplitModel(bm, metrics, [m for m, _ in res] if self.getCollectSubModels() else None)
         tvm._post_fit(self)
         return tvm

@@ -62,17 +62,29 @@ def regression_shard(n_total: int, d: int, seed: int, rank: int, world: int, dev
 
 
 def forest_digest(forest) -> str:
-    """Stable hash of a fitted forest's structure and leaf values (cross-world-size identity checks)."""
+    """Stable hash of a fitted forest's trees (splits, thresholds, leaf values), node-numbering independent:
+    each tree is walked breadth-first from its root (cross-world-size / fused-vs-alone identity checks)."""
     import hashlib
+    from collections import deque
 
     import numpy as np
 
     h = hashlib.sha256()
-    for name in ("feat", "bin", "left", "right", "roots"):
-        h.update(np.asarray(getattr(forest, name), dtype=np.int64).tobytes())
-    h.update(np.asarray(forest.thr, dtype=np.float64).tobytes())
-    h.update(np.concatenate([np.asarray(v, np.float64).reshape(-1) for v in forest.value]).tobytes()
-             if forest.value else b"")
+    for r in forest.roots:
+        q = deque([r])
+        while q:
+            i = q.popleft()
+            f = int(forest.feat[i])
+            h.update(np.asarray([f, int(forest.bin[i]) if f >= 0 else 0, int(bool(forest.is_cat[i]))],
+                                dtype=np.int64).tobytes())
+            if f >= 0:
+                h.update(np.asarray([forest.thr[i]], dtype=np.float64).tobytes())
+                if forest.is_cat[i]:
+                    h.update(np.asarray(forest.catmask[i], dtype=np.uint32).tobytes())
+                q.append(forest.left[i])
+                q.append(forest.right[i])
+            else:
+                h.update(np.asarray(forest.value[i], dtype=np.float64).reshape(-1).tobytes())
     return h.hexdigest()[:16]
 
 
