@@ -4,7 +4,7 @@
     python bench_configs.py lr        # 2: LinearRegression normal equations, bf16 MFMA Gram, 1e7 x 100
     python bench_configs.py cv        # 3: RandomForestRegressor + CrossValidator grid, 1e8 x 100
     python bench_configs.py gbdt      # 4: XGBoost-style GBDT, depth 8, 1e8 x 100 (rounds/s; --trees)
-    python bench_configs.py infer     # 5: batch inference of a trained RF over 1e9 rows (graph-captured)
+    python bench_configs.py infer     # 5: batch inference of a trained RF over 1e9 streamed rows (transform)
     python bench_configs.py airbnb    # 1: ML 02 LinearRegression on the Airbnb-SF schema (CPU plumbing)
 
 Each prints one JSON line (same fields as bench.py).  Multi-GPU: launch under
@@ -136,65 +136,67 @@ def bench_gbdt(spark, args):
 
 
 def bench_infer(spark, args):
-    """Stream synthetic chunks through a trained 20-tree RF; the per-chunk launch sequence is
-    captured once in a HIP graph and replayed (1e9 rows do not fit in HBM as 100 float32 features)."""
+    """Config 5 through the product path: ``model.transform`` over a STREAMED DataFrame of 1e9 rows x 100
+    fp32 features (400 GB: larger than HBM), consumed chunk by chunk with ``foreachBatch``.
+
+    --mode host (default): chunks come from pinned host memory through ``createDataFrameFromChunks``
+    (pinned double buffers, H2D on a copy stream overlapping the predict; the H2D of all 400 GB is in the
+    timed region).  The host pool holds --pool distinct chunks, cycled (host RAM cannot hold 400 GB).
+    --mode device: chunks are two device-resident buffers cycled through ``device_chunks`` (predict-bound).
+    In both modes the forest is uploaded once and each staging buffer's predict is a replayed HIP graph."""
+    from cdnaml.models.inference import device_chunks
     from cdnaml.models.regression import RandomForestRegressor
     dev = spark.device
     comm = spark.comm
     train, _ = _data(spark, int(2e6), 100)
     model = RandomForestRegressor(numTrees=20, maxDepth=5, maxBins=40, seed=42).fit(train)
-    forest = model._forest
     n_total = int(args.rows or 1e9)
     chunk = int(args.chunk)
     per_rank = n_total // comm.world_size
     n_chunks = max(1, per_rank // chunk)
-    tw = model._tree_w
+    rows = n_chunks * chunk * comm.world_size
     g = torch.Generator(device=dev).manual_seed(7 + comm.rank)
-    # two resident chunk buffers scored alternately (each 20 GB at the default chunk, far
-    # beyond L2/MALL, so every replay streams its features from HBM)
-    bufs = [torch.randn((chunk, 100), generator=g, dtype=torch.float32, device=dev) for _ in range(2)]
-    outs = [None, None]
+    if args.mode == "host" and dev.type == "cuda":
+        pool = []
+        for _ in range(int(args.pool)):
+            h = torch.empty((chunk, 100), dtype=torch.float32, pin_memory=True)
+            h.copy_(torch.randn((chunk, 100), generator=g, dtype=torch.float32, device=dev).cpu())
+            pool.append(h)
 
-    from cdnaml.ops import kernels as K
-    nodes, roots, vals, masks = forest.device_arrays(dev, "value")
-    tw_d = torch.tensor(np.asarray(tw, np.float32), device=dev)
-    masks = masks.int().contiguous() if masks.numel() else torch.zeros(8, dtype=torch.int32, device=dev)
+        def chunks():
+            for i in range(n_chunks):
+                yield {"features": pool[i % len(pool)]}
+        df = spark.createDataFrameFromChunks(chunks, chunk)
+    else:
+        filled = [False, False]
 
-    heap = forest.heap_arrays(dev, "value") if dev.type == "cuda" else None
+        def make(r0, n, bufs):
+            slot = (r0 // chunk) & 1
+            if not filled[slot]:
+                bufs["features"][:n].copy_(torch.randn((n, 100), generator=g, dtype=torch.float32, device=dev))
+                filled[slot] = True
+        df = device_chunks(spark, n_chunks * chunk, chunk, make, {"features": ((100,), torch.float32)})
+    pred = model.transform(df)
+    acc = torch.zeros((), dtype=torch.float64, device=dev)
 
-    def run_chunk(j):
-        # device-resident forest arrays, no host->device traffic: capturable in a HIP graph
-        out = K.tree_predict_heap(bufs[j], heap[0], heap[1], tw_d, heap[2]) if heap is not None else None
-        outs[j] = out if out is not None else K.tree_predict(bufs[j], nodes, roots, tw_d, vals, masks, forest.K, None)
-    graphs = None
-    if dev.type == "cuda" and not args.no_graph:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            run_chunk(0)
-            run_chunk(1)
-        torch.cuda.current_stream().wait_stream(s)
-        graphs = []
-        for j in range(2):
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr):
-                run_chunk(j)
-            graphs.append(gr)
+    def consume(b):
+        acc.add_(b.columns["prediction"].values.sum())
 
     def step():
-        for i in range(n_chunks):
-            if graphs is not None:
-                graphs[i & 1].replay()
-            else:
-                run_chunk(i & 1)
-        return outs[(n_chunks - 1) & 1]
-    ms, p = _timed(spark, step, args.steps, args.warmup)
-    rows = n_chunks * chunk * comm.world_size
-    _log(f"inference {rows:.3e} rows in {ms:.1f} ms; graph={graphs is not None}")
-    _emit(spark, "rows/sec batch inference, trained RandomForest (20 trees, depth 5), 1e9 rows",
-          rows / (ms / 1e3), "rows/s", args.steps, args.warmup, ms, True, "weak" if comm.world_size > 1 else "strong",
-          "fp32", "RandomForestRegressionModel(numTrees=20,maxDepth=5) predict, hipGraph-captured", rows,
-          f"dp{comm.world_size}")
+        acc.zero_()
+        pred.foreachBatch(consume)
+        return acc
+    ms, tot = _timed(spark, step, args.steps, args.warmup)
+    from cdnaml.models.inference import predictor_for
+    pr = predictor_for(model, "value", [0.0])
+    _log(f"inference {rows:.3e} rows in {ms:.1f} ms (mode={args.mode}); graph captures={pr.captures} "
+         f"replays={pr.replays}; mean prediction {float(tot) / (n_chunks * chunk):.4f}")
+    src = "pinned host chunks, H2D in the timed region" if args.mode == "host" else "device-resident chunks"
+    _emit(spark, f"rows/sec batch inference via DataFrame transform, RandomForest (20 trees, depth 5), 1e9 rows "
+                 f"({src})", rows / (ms / 1e3), "rows/s", args.steps, args.warmup, ms, True,
+          "weak" if comm.world_size > 1 else "strong", "fp32",
+          "RandomForestRegressionModel(numTrees=20,maxDepth=5).transform, streamed, hipGraph-replayed predict",
+          rows, f"dp{comm.world_size}")
 
 
 def bench_airbnb(spark, args):
@@ -224,8 +226,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--trees", type=int, default=None)
-    ap.add_argument("--chunk", type=float, default=2.5e7)
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--chunk", type=float, default=1e7)
+    ap.add_argument("--mode", choices=["host", "device"], default="host")
+    ap.add_argument("--pool", type=int, default=6, help="distinct pinned host chunks (--mode host)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--trace", default="", help="run one traced (untimed) step first; Chrome trace path")
     args = ap.parse_args()

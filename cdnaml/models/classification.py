@@ -348,13 +348,15 @@ class _TreeClassifierModel(_TreeModelBase):
         forest, tw = self._forest, self._tree_w
         kind = "counts" if self._counts_raw else "value"
         thresholds = self.getThresholds()
+        from .inference import predictor_for
+        predictor = predictor_for(self, kind)
 
         def fn(b, ctx):
             X = b.columns[fc].values
             if X.shape[0] == 0:
                 z = torch.zeros((0, forest.K), dtype=torch.float64, device=X.device)
                 return _append_cls_outputs(b, z, z, z[:, 0], names)
-            raw = forest.predict(X, tw, None, kind).double()
+            raw = predictor(X).double()
             s = raw.sum(1, keepdim=True)
             prob = raw / torch.where(s > 0, s, torch.ones_like(s))
             pred = _argmax_with_thresholds(prob, thresholds)

@@ -531,9 +531,12 @@ class _TreeRegressorModel(_TreeModelBase):
         require_vector(dataset, fc)
         forest, tw, base = self._forest, self._tree_w, self._base
 
+        from .inference import predictor_for
+        predictor = predictor_for(self, "value", [base])  # forest uploaded once; recurring buffers graph-replayed
+
         def fn(b, ctx):
             X = b.columns[fc].values
-            p = forest.predict(X, tw, [base])[:, 0].double() if X.shape[0] else \
+            p = predictor(X)[:, 0].double() if X.shape[0] else \
                 torch.zeros(0, dtype=torch.float64, device=X.device)
             out = {pc: ColumnData(p, T.DoubleType())}
             self._leaf_col(b, out)

@@ -298,6 +298,17 @@ class SparkSession:
         sch = b.schema()
         return self._from_local_batches("DeviceTensorScan", lambda: [b], sch)
 
+    def createDataFrameFromChunks(self, chunks, max_rows: int, schema=None) -> DataFrame:
+        """A DataFrame STREAMED from host chunks (inputs larger than HBM).
+
+        ``chunks``: a callable returning an iterator of ``{column: numpy array | cpu tensor}`` of at most
+        ``max_rows`` rows each (this rank's rows, in order).  Chunks pass through pinned double buffers and a
+        copy stream, so the H2D copy of chunk i + 1 overlaps the compute on chunk i.  Narrow pipelines
+        (``model.transform``, ``select``, ``withColumn``) then run chunk by chunk; consume them with
+        ``foreachBatch`` / ``count`` (batches are transient views of the staging buffers)."""
+        from .models.inference import chunked_dataframe
+        return chunked_dataframe(self, chunks, max_rows, schema)
+
     def table(self, name) -> DataFrame:
         return self.catalog._lookup(name)
 

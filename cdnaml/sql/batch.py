@@ -43,6 +43,10 @@ class ColumnData:
     def with_meta(self, meta):
         return ColumnData(self.values, self.dtype, self.valid, self.dictionary, meta)
 
+    def clone(self) -> "ColumnData":
+        return ColumnData(self.values.clone(), self.dtype, None if self.valid is None else self.valid.clone(),
+                          self.dictionary, self.meta)
+
     def valid_mask(self) -> torch.Tensor:
         if self.valid is None:
             return torch.ones(len(self), dtype=torch.bool, device=self.device)
@@ -211,6 +215,10 @@ class Batch:
 
     def schema(self) -> T.StructType:
         return T.StructType([T.StructField(k, c.dtype, True, c.meta) for k, c in self.columns.items()])
+
+    def clone(self) -> "Batch":
+        """Deep copy of the device tensors (a streamed batch aliases a reused staging buffer)."""
+        return Batch({k: c.clone() for k, c in self.columns.items()}, self.n, self.device)
 
     def select(self, names: Sequence[str]) -> "Batch":
         return Batch({k: self.columns[k] for k in names}, self.n, self.device)

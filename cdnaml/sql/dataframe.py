@@ -12,7 +12,7 @@ from __future__ import annotations
 import math
 
 import itertools
-from typing import Callable, Dict, List, Optional, Sequence, Union
+from typing import Iterator, Callable, Dict, List, Optional, Sequence, Union
 
 import numpy as np
 import pandas as pd
@@ -46,6 +46,23 @@ class Plan:
             self._result = res
         return res
 
+    @property
+    def streamable(self) -> bool:
+        """True when partitions can be produced one at a time (out-of-core narrow pipelines)."""
+        return False
+
+    def iter_execute(self) -> Iterator[Batch]:
+        """This rank's partitions one at a time.  Streamed sources (``SparkSession.createDataFrameFromChunks``)
+        produce them lazily, so a narrow pipeline over data larger than HBM never holds more than its
+        staging buffers; other plans yield their materialised partitions."""
+        if self._result is not None or not self.streamable:
+            yield from self.execute()
+        else:
+            yield from self._iter_execute()
+
+    def _iter_execute(self) -> Iterator[Batch]:  # pragma: no cover
+        yield from self._execute()
+
     def _execute(self) -> List[Batch]:  # pragma: no cover
         raise NotImplementedError
 
@@ -69,13 +86,27 @@ class Plan:
 
 
 class SourcePlan(Plan):
-    def __init__(self, session, name, fn: Callable[[], List[Batch]], schema: T.StructType):
+    """Leaf.  ``iter_fn`` (optional) yields the partitions lazily; each yielded batch may alias a staging
+    buffer that is reused once the consumer asks for the next one, so materialising such a source clones."""
+
+    def __init__(self, session, name, fn: Optional[Callable[[], List[Batch]]], schema: T.StructType,
+                 iter_fn: Optional[Callable[[], Iterator[Batch]]] = None):
         super().__init__(session, name)
         self.fn = fn
+        self.iter_fn = iter_fn
         self._schema = schema
 
+    @property
+    def streamable(self) -> bool:
+        return self.iter_fn is not None
+
     def _execute(self):
+        if self.fn is None:
+            return [b.clone() for b in self.iter_fn()]
         return self.fn()
+
+    def _iter_execute(self):
+        yield from self.iter_fn()
 
     def _compute_schema(self):
         return self._schema
@@ -94,6 +125,15 @@ class MapPlan(Plan):
         for i, b in enumerate(self.children[0].execute()):
             out.append(self.fn(b, EvalContext(self.session, rank * _PART_STRIDE + i, 0)))
         return out
+
+    @property
+    def streamable(self) -> bool:
+        return self.children[0].streamable
+
+    def _iter_execute(self):
+        rank = self.session.comm.rank
+        for i, b in enumerate(self.children[0].iter_execute()):
+            yield self.fn(b, EvalContext(self.session, rank * _PART_STRIDE + i, 0))
 
     def _compute_schema(self):
         b = self.fn(self.children[0].prototype(), EvalContext(self.session, 0, 0))
@@ -483,8 +523,17 @@ class DataFrame:
         return concat_batches(parts)
 
     def count(self) -> int:
-        n = sum(b.n for b in self._local())
+        if self._plan.streamable:
+            n = sum(b.n for b in self._plan.iter_execute())
+        else:
+            n = sum(b.n for b in self._local())
         return int(self._session.comm.all_reduce_scalar(float(n)))
+
+    def foreachBatch(self, fn) -> None:
+        """Call ``fn(batch)`` on each of this rank's device partitions, one at a time (streamed sources are
+        never materialised: out-of-core batch inference writes or reduces each batch here)."""
+        for b in self._plan.iter_execute():
+            fn(b)
 
     def isEmpty(self) -> bool:
         return self.count() == 0
