@@ -77,6 +77,8 @@ class TreeParams:
     min_child_weight: float = 1.0
     min_weight_fraction: float = 0.0
     subset_scope: str = "node"          # "node" (Spark / colsample_bynode) or "tree" (colsample_bytree)
+    tree_ids: Optional[np.ndarray] = None  # logical id of each forest tree for feature-subset hashing
+                                           # (batched many-model fits: tree t of every group hashes as t)
 
 
 # ============================================================ binning (K3/K4)
@@ -891,7 +893,8 @@ class ForestTrainer:
             slot_tree = a_tree[build_ids]
             masks_np = None
             if need_masks:
-                masks_np = self._feature_masks(a_tree.astype(np.uint64), a_key)
+                tid = a_tree if p.tree_ids is None else np.asarray(p.tree_ids, dtype=np.int64)[a_tree]
+                masks_np = self._feature_masks(tid.astype(np.uint64), a_key)
             fm_build = None
             if masked:
                 fm_build = torch.from_numpy(np.ascontiguousarray(masks_np[build_ids]).view(np.int32)).to(dev)

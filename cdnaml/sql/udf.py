@@ -159,6 +159,23 @@ def map_in_pandas(df, func, schema):
 
 
 # -------------------------------------------------------- applyInPandas
+def _apply_parallelism(session, ngroups: int) -> int:
+    """Threads for applyInPandas groups: ``cdnaml.applyInPandas.parallelism`` (default: one per group, at most
+    the process's CPU share, capped at 16)."""
+    import os
+    try:
+        v = int(session.conf.get("cdnaml.applyInPandas.parallelism"))
+    except Exception:
+        v = 0
+    if v <= 0:
+        try:
+            cpus = len(os.sched_getaffinity(0))
+        except AttributeError:
+            cpus = os.cpu_count() or 1
+        v = min(16, cpus)
+    return max(1, min(v, ngroups))
+
+
 def apply_in_pandas(grouped, func, schema):
     from .dataframe import DataFrame, PartitionsPlan, _shuffle
     schema = T.to_schema(schema)
@@ -175,16 +192,24 @@ def apply_in_pandas(grouped, func, schema):
         if b.n == 0:
             return [empty_batch(schema, session.device)]
         pdf = b.to_pandas()
-        outs = []
-        for key, g in pdf.groupby(keys, sort=True, dropna=False):
-            g = g.reset_index(drop=True)
+        groups = [(key, g.reset_index(drop=True)) for key, g in pdf.groupby(keys, sort=True, dropna=False)]
+
+        def one(item):
+            key, g = item
             if nparams == 2:
-                kt = key if isinstance(key, tuple) else (key,)
-                o = func(kt, g)
-            else:
-                o = func(g)
-            if o is not None and len(o):
-                outs.append(o)
+                return func(key if isinstance(key, tuple) else (key,), g)
+            return func(g)
+        # groups are independent: a thread pool runs them concurrently (numpy / scikit-learn / this engine's
+        # kernels release the GIL; the tracking store is thread-safe, with thread-local active runs), and
+        # the results are concatenated in group order, as the serial loop would
+        par = _apply_parallelism(session, len(groups))
+        if par > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(max_workers=par) as ex:
+                results = list(ex.map(one, groups))
+        else:
+            results = [one(it) for it in groups]
+        outs = [o for o in results if o is not None and len(o)]
         if not outs:
             return [empty_batch(schema, session.device)]
         res = pd.concat(outs, ignore_index=True)
