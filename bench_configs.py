@@ -6,6 +6,7 @@
     python bench_configs.py gbdt      # 4: XGBoost-style GBDT, depth 8, 1e8 x 100 (rounds/s; --trees)
     python bench_configs.py infer     # 5: batch inference of a trained RF over 1e9 streamed rows (transform)
     python bench_configs.py airbnb    # 1: ML 02 LinearRegression on the Airbnb-SF schema (CPU plumbing)
+    python bench_configs.py relational  # groupBy-count / groupBy-avg / join / dropDuplicates on 1e8 rows
 
 Each prints one JSON line (same fields as bench.py).  Multi-GPU: launch under
 ``torch.distributed.run`` exactly like bench.py; rows are split across ranks.
@@ -199,6 +200,39 @@ def bench_infer(spark, args):
           rows, f"dp{comm.world_size}")
 
 
+def bench_relational(spark, args):
+    """groupBy-count, a fact x dimension join and dropDuplicates on 1e8 rows (K16 hash tables, K19 compaction;
+    Labs/ML 00L - Dedup Lab.py:79-107, ML 01 - Data Cleansing.py:93,157-160, MLE 01:332-374)."""
+    from cdnaml.sql import functions as F
+    dev = spark.device
+    comm = spark.comm
+    n_total = int(args.rows or 1e8)
+    a, b = n_total * comm.rank // comm.world_size, n_total * (comm.rank + 1) // comm.world_size
+    n = b - a
+    g = torch.Generator(device=dev).manual_seed(11 + comm.rank)
+    k = torch.randint(0, 1_000_000, (n,), generator=g, device=dev)
+    k2 = torch.randint(0, 50, (n,), generator=g, device=dev)
+    v = torch.randn(n, generator=g, device=dev, dtype=torch.float64)
+    fact = spark.createDataFrameFromLocalTensors({"k": k, "k2": k2, "v": v})
+    dk = torch.arange(0, 1_000_000, 4, device=dev)
+    dim = spark.createDataFrameFromLocalTensors({"k": dk, "w": dk.double() * 0.5}) if comm.rank == 0 else \
+        spark.createDataFrameFromLocalTensors({"k": dk[:0], "w": dk[:0].double()})
+    ops = {
+        "groupBy(k).count": lambda: fact.groupBy("k").count().count(),
+        "groupBy(k2).avg": lambda: fact.groupBy("k2").agg(F.avg("v")).count(),
+        "join(dim on k)": lambda: fact.join(dim, on="k").count(),
+        "dropDuplicates(k, k2)": lambda: fact.dropDuplicates(["k", "k2"]).count(),
+    }
+    total = 0.0
+    for name, fn in ops.items():
+        ms, cnt = _timed(spark, fn, args.steps, args.warmup)
+        total += ms
+        _log(f"{name}: {ms:.1f} ms -> {cnt} rows")
+    _emit(spark, "rows/sec relational suite (groupBy-count, groupBy-avg, join, dropDuplicates) on 1e8 rows",
+          4 * n_total / (total / 1e3), "rows/s", args.steps, args.warmup, total, True, "strong", "fp64",
+          "groupBy/join/dropDuplicates on K16 device hash tables", n_total, f"dp{comm.world_size}")
+
+
 def bench_airbnb(spark, args):
     from cdnaml.ml.evaluation import RegressionEvaluator
     from cdnaml.ml.feature import VectorAssembler
@@ -221,7 +255,7 @@ def bench_airbnb(spark, args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("config", choices=["lr", "cv", "gbdt", "infer", "airbnb"])
+    ap.add_argument("config", choices=["lr", "cv", "gbdt", "infer", "airbnb", "relational"])
     ap.add_argument("--rows", type=float, default=None)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
@@ -236,7 +270,8 @@ def main():
     TRACE = args.trace or None
     import cdnaml
     spark = cdnaml.SparkSession.builder.appName("bench_configs").getOrCreate()
-    {"lr": bench_lr, "cv": bench_cv, "gbdt": bench_gbdt, "infer": bench_infer, "airbnb": bench_airbnb}[
+    {"lr": bench_lr, "cv": bench_cv, "gbdt": bench_gbdt, "infer": bench_infer, "airbnb": bench_airbnb,
+     "relational": bench_relational}[
         args.config](spark, args)
 
 

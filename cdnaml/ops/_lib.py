@@ -138,6 +138,11 @@ _SIGS = {
                               c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_float, c_void_p, c_void_p], c_int),
     "cdna_wave_scan": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
+    "cdna_hash_insert": ([c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p], c_int),
+    "cdna_hash_lookup": ([c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_void_p], c_int),
+    "cdna_dict_encode": ([c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_void_p,
+                          c_void_p], c_int),
+    "cdna_grouped_reduce": ([c_int, c_void_p, c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p], c_int),
     "cdna_planar_bins": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p], c_int),
     "cdna_hist_mfma": ([c_void_p, c_int64, c_int64, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                         c_void_p, c_int, c_void_p, c_float, c_int64, c_int, c_void_p, c_void_p, c_void_p], c_int),

@@ -322,6 +322,9 @@ def concat_batches(batches: List[Batch]) -> Batch:
 
 
 # ------------------------------------------------------------ conversions
+DICT_ENCODE_MIN_ROWS = 50_000
+
+
 def column_from_numpy(arr, dt: Optional[T.DataType], device) -> ColumnData:
     """Build a device column from host values (numpy / pandas / list)."""
     if isinstance(arr, pd.Series):
@@ -334,6 +337,17 @@ def column_from_numpy(arr, dt: Optional[T.DataType], device) -> ColumnData:
         dt = _infer_numpy_type(arr)
     if isinstance(dt, T.StringType):
         vals = np.asarray(arr, dtype=object)
+        if n >= DICT_ENCODE_MIN_ROWS and torch.device(device).type == "cuda":
+            # K17: Arrow strings -> device hash dictionary encode (no per-row Python, no object sort)
+            try:
+                import pyarrow as pa
+                pa_arr = pa.array(vals, type=pa.string(), from_pandas=True)
+            except (pa.ArrowInvalid, pa.ArrowTypeError):
+                pa_arr = None
+            if pa_arr is not None:
+                from ..ops import kernels as K
+                codes, valid, uni = K.dict_encode(pa_arr, device)
+                return ColumnData(codes, dt, valid, uni)
         isnull = np.array([v is None or (isinstance(v, float) and np.isnan(v)) for v in vals], dtype=bool) \
             if vals.dtype == object else np.zeros(n, bool)
         sv = np.where(isnull, "", vals.astype(str) if vals.dtype != object else vals).astype(object)

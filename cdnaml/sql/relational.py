@@ -13,6 +13,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 import torch
 
+from ..ops import kernels as K
 from . import types as T
 from .batch import Batch, ColumnData, column_from_numpy, concat_columns, unify_dictionaries
 
@@ -26,13 +27,13 @@ def column_codes(c: ColumnData) -> Tuple[torch.Tensor, int]:
     elif isinstance(c.dtype, T.StringType):
         codes = v.long() + 1
         if codes.numel():
-            uniq, inv = torch.unique(codes, return_inverse=True)
+            inv, _ = K.dense_ids(codes)  # K16 hash table on the GPU (sorted-rank ids, like torch.unique)
             codes = inv + 1
     else:
         x = v
         if x.dtype.is_floating_point:
             x = torch.where(x == 0, torch.zeros_like(x), x)  # -0.0 == 0.0
-        _, inv = torch.unique(x, return_inverse=True)
+        inv, _ = K.dense_ids(x)
         codes = inv + 1
     if c.valid is not None:
         codes = torch.where(c.valid, codes, torch.zeros_like(codes))
@@ -53,16 +54,12 @@ def combine_codes(cols: List[ColumnData], n: int, device) -> Tuple[torch.Tensor,
             combined = combined * k + codes
             if combined.numel() and int(combined.max()) > 2 ** 60 // max(k, 1):
                 _, combined = torch.unique(combined, return_inverse=True)
-    uniq, gid = torch.unique(combined, return_inverse=True)
-    return gid, int(uniq.numel())
+    gid, G = K.dense_ids(combined)
+    return gid, G
 
 
 def first_index_per_group(gid: torch.Tensor, ngroups: int) -> torch.Tensor:
-    n = gid.numel()
-    idx = torch.arange(n, device=gid.device)
-    first = torch.full((ngroups,), n, dtype=torch.int64, device=gid.device)
-    first.scatter_reduce_(0, gid, idx, reduce="amin", include_self=True)
-    return first
+    return K.group_first(gid, ngroups)
 
 
 # ----------------------------------------------------------------- aggregation
@@ -90,6 +87,8 @@ def aggregate(batch: Batch, keys: List[str], aggs: List[Tuple[str, object]]) -> 
 
 
 def _seg_sum(vals, gid, G, dtype=torch.float64):
+    if dtype == torch.float64 and vals.dim() == 1:
+        return K.group_sum(vals, gid, G)  # LDS-privatised for few groups (no contended global fp64 atomics)
     s = torch.zeros(G, dtype=dtype, device=vals.device)
     s.index_add_(0, gid, vals.to(dtype))
     return s
@@ -151,8 +150,7 @@ def _agg_one(batch: Batch, agg, gid, G, first, ctx) -> ColumnData:
                           None if bool(ok.all()) else ok, c.dictionary)
     x = c.values.to(torch.float64) if c.values.dim() == 1 else c.values.to(torch.float64)
     xz = torch.where(valid, x, torch.zeros_like(x))
-    cnt = torch.zeros(G, dtype=torch.float64, device=dev)
-    cnt.index_add_(0, gid, valid.to(torch.float64))
+    cnt = K.group_sum(None if c.valid is None else valid.to(torch.float64), gid, G)
     nonempty = cnt > 0
     vnull = None if bool(nonempty.all()) else nonempty
     if kind == "sum":

@@ -927,3 +927,66 @@ def test_planar_bins(dev):
     ref = K.bins_to_matrix(bins.cpu(), 21).t()
     assert ldp % K.MFMA_STAGE == 0 and ldp >= 4099
     assert torch.equal(bp[:21, :4099].cpu(), ref.to(torch.uint8))
+
+
+@pytest.mark.parametrize("dtype,card", [(torch.int64, 7), (torch.int64, 300000), (torch.float64, 1000),
+                                        (torch.float32, 5000), (torch.int32, 64)])
+def test_hash_dense_ids_match_torch_unique(dev, dtype, card):
+    """K16: hash-table dense ids == torch.unique's sorted inverse (incl. -0.0 == 0.0, INT64_MIN keys, and the
+    overflow retry when the first table is too small)."""
+    g = torch.Generator().manual_seed(card)
+    x = torch.randint(-card, card, (400000,), generator=g).to(dtype)
+    if dtype.is_floating_point:
+        x = x / 7.0
+        x[:5] = -0.0
+    if dtype == torch.int64:
+        x[7] = -(1 << 63)
+    ids, G, vals = K.hash_dense_ids(x.to(dev))
+    xr = torch.where(x == 0, torch.zeros_like(x), x) if dtype.is_floating_point else x
+    uniq, inv = torch.unique(xr, return_inverse=True)
+    assert G == uniq.numel()
+    assert torch.equal(ids.cpu(), inv)
+    assert torch.equal(vals.cpu(), uniq)
+
+
+def test_dict_encode_matches_numpy(dev):
+    """K17: device string dictionary encode == np.unique codes (nulls -> -1, empty strings, unicode)."""
+    import pyarrow as pa
+    rng = np.random.default_rng(0)
+    words = np.array(["a", "", "bé", "zz", "Mark", "mark", "x" * 40] + [f"w{i}" for i in range(3000)], dtype=object)
+    vals = words[rng.integers(0, len(words), 200000)]
+    vals[::97] = None
+    arr = pa.array(vals.tolist(), type=pa.string())
+    codes, valid, dic = K.dict_encode(arr, dev)
+    ok = np.array([v is not None for v in vals])
+    uni, inv = np.unique(vals[ok].astype(str), return_inverse=True)
+    assert dic.tolist() == uni.tolist()
+    c = codes.cpu().numpy()
+    assert (c[~ok] == -1).all() and np.array_equal(c[ok], inv)
+    assert np.array_equal(valid.cpu().numpy(), ok)
+
+
+def test_relational_on_hash_kernels_match_pandas(dev):
+    """groupBy-count, avg, join and dropDuplicates through the K16/K17 device path == pandas."""
+    import pandas as pd
+    import cdnaml
+    from cdnaml.sql import functions as F
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    rng = np.random.default_rng(3)
+    n = 120000
+    pdf = pd.DataFrame({"k": rng.integers(0, 5000, n), "s": rng.choice(["ann", "bob", "cé", None], n),
+                        "v": rng.normal(size=n)})
+    df = spark.createDataFrame(pdf)
+    got = df.groupBy("k").count().orderBy("k").toPandas()
+    ref = pdf.groupby("k").size().reset_index(name="count")
+    assert got["k"].tolist() == ref["k"].tolist() and got["count"].tolist() == ref["count"].tolist()
+    g2 = df.groupBy("s").agg(F.avg("v").alias("m")).toPandas().set_index("s")["m"]
+    r2 = pdf.groupby("s", dropna=False)["v"].mean()
+    for key, val in r2.items():
+        k2 = None if (isinstance(key, float) and np.isnan(key)) else key
+        assert g2.loc[g2.index.isna()].iloc[0] == pytest.approx(val) if k2 is None else \
+            g2.loc[k2] == pytest.approx(val)
+    dim = pd.DataFrame({"k": np.arange(0, 5000, 2), "name": [f"n{i}" for i in range(2500)]})
+    j = df.join(spark.createDataFrame(dim), on="k").count()
+    assert j == len(pdf.merge(dim, on="k"))
+    assert df.dropDuplicates(["k", "s"]).count() == len(pdf.drop_duplicates(["k", "s"]))
