@@ -200,28 +200,38 @@ __global__ __launch_bounds__(256) void gram_bf16s_kernel(const float* __restrict
                                                          PairTable tab, int npairs, int Dpad,
                                                          float* __restrict__ partial, int64_t rows_per_block) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int kCS = 72;  // column stride in bf16 elements (64 rows + 8 pad)
+  // 64-row tiles, 4 waves: the next tile's 8 rows x 4 columns per thread are in flight under the current
+  // tile's MFMAs.  Measured alternatives (profiles/r2/gram_ab.md): 128-row tiles with 512 threads 1.75 ms,
+  // 128-row tiles with 256 threads at one wave per SIMD no faster; this shape 1.54 ms.
+  constexpr int kRows = 64;
+  constexpr int kCS = kRows + 8;  // column stride in bf16 elements: 36-dword stride, conflict-free fragment reads
+  constexpr int kTh = 256;
   uint16_t* buf = reinterpret_cast<uint16_t*>(smem);
   const int tsz = Dpad * kCS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, half = lane >> 5;
   const int d4 = d >> 2;
-  const int items = 64 * d4;
-  // zero both buffers once: padding columns d+2..Dpad-1 stay zero forever
-  for (int i = tid; i < 2 * tsz / 2; i += 256) reinterpret_cast<uint32_t*>(buf)[i] = 0u;
-  int goff[NI], loff[NI], rr[NI];
+  // work item = (row octet r8, column quad c4), r8 fastest: a thread loads 8 rows x 4 columns and stores each
+  // column's 8 rows as ONE 16-byte ds_write_b128 (a column quad's 8 lanes fill 128 contiguous bytes:
+  // conflict-free; 2-byte column-major stores from row-major items were 80 % of the LDS cycles in conflicts)
+  constexpr int kOct = kRows / 8;
+  const int items = kOct * d4;
+  int goff[NI], loff[NI], r8s[NI];
   float4 sh[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int e = tid + 256 * i;
-    const int r = e < items ? e / d4 : 0, c4 = e < items ? e - (e / d4) * d4 : 0;
-    goff[i] = e < items ? (int)(r * ldx) + 4 * c4 : -1;
-    loff[i] = 4 * c4 * kCS + r;
-    rr[i] = r;
+    const int e = tid + kTh * i;
+    const bool ok = e < items;
+    const int r8 = ok ? (e % kOct) : 0, c4 = ok ? (e / kOct) : 0;
+    goff[i] = ok ? (int)(8 * r8 * ldx) + 4 * c4 : -1;
+    loff[i] = 4 * c4 * kCS + 8 * r8;
+    r8s[i] = r8;
     sh[i] = shift ? *reinterpret_cast<const float4*>(shift + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // zero both buffers once: padding columns d+2..Dpad-1 stay zero forever
+  for (int i = tid; i < 2 * tsz / 2; i += kTh) reinterpret_cast<uint32_t*>(buf)[i] = 0u;
   int pr[PW];
 #pragma unroll
-  for (int j = 0; j < PW; ++j) pr[j] = wid + 4 * j;
+  for (int j = 0; j < PW; ++j) pr[j] = wid + (kTh / 64) * j;
   f32x16 acc[PW];
 #pragma unroll
   for (int j = 0; j < PW; ++j)
@@ -231,34 +241,46 @@ __global__ __launch_bounds__(256) void gram_bf16s_kernel(const float* __restrict
   const int64_t rb0 = (int64_t)blockIdx.x * rows_per_block;
   int64_t rb1 = rb0 + rows_per_block;
   if (rb1 > n) rb1 = n;
-  float4 v[NI];
+  float4 v[NI][8];
   float yv = 0.f;
 // next tile's rows -> registers (rows past rb1 load the shift, i.e. become 0)
-#define GRAM_LOAD(T0)                                                                      \
-  {                                                                                        \
-    const int64_t lim_ = rb1 - (T0);                                                       \
-    _Pragma("unroll") for (int i = 0; i < NI; ++i) {                                       \
-      const bool ok_ = goff[i] >= 0 && rr[i] < lim_;                                       \
-      v[i] = ok_ ? *reinterpret_cast<const float4*>(X + (T0) * ldx + goff[i]) : sh[i];     \
-    }                                                                                      \
-    if (tid < 64) yv = (y != nullptr && tid < lim_) ? y[(T0) + tid] - yshift : 0.f;        \
+#define GRAM_LOAD(T0)                                                                            \
+  {                                                                                              \
+    const int64_t lim_ = rb1 - (T0);                                                             \
+    _Pragma("unroll") for (int i = 0; i < NI; ++i) {                                             \
+      _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                            \
+        const bool ok_ = goff[i] >= 0 && 8 * r8s[i] + q < lim_;                                  \
+        v[i][q] = ok_ ? *reinterpret_cast<const float4*>(X + (T0) * ldx + goff[i] + q * ldx) : sh[i]; \
+      }                                                                                          \
+    }                                                                                            \
+    if (tid < kRows) yv = (y != nullptr && tid < lim_) ? y[(T0) + tid] - yshift : 0.f;           \
   }
-// registers -> bf16 column-major LDS tile
-#define GRAM_STORE(TB, T0)                                                                 \
-  {                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < NI; ++i) {                                       \
-      if (goff[i] >= 0) {                                                                  \
-        uint16_t* p_ = (TB) + loff[i];                                                     \
-        p_[0] = __builtin_bit_cast(uint16_t, (__bf16)(v[i].x - sh[i].x));                  \
-        p_[kCS] = __builtin_bit_cast(uint16_t, (__bf16)(v[i].y - sh[i].y));                \
-        p_[2 * kCS] = __builtin_bit_cast(uint16_t, (__bf16)(v[i].z - sh[i].z));            \
-        p_[3 * kCS] = __builtin_bit_cast(uint16_t, (__bf16)(v[i].w - sh[i].w));            \
-      }                                                                                    \
-    }                                                                                      \
-    if (tid < 64) {                                                                        \
+// 8 rows of one column component -> one 16-byte store
+#define GRAM_COL(i_, comp_, dst_)                                                                \
+  {                                                                                              \
+    uint32_t w_[4];                                                                              \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                              \
+      const uint32_t lo_ = __builtin_bit_cast(uint16_t, (__bf16)(v[i_][2 * q].comp_ - sh[i_].comp_));     \
+      const uint32_t hi_ = __builtin_bit_cast(uint16_t, (__bf16)(v[i_][2 * q + 1].comp_ - sh[i_].comp_)); \
+      w_[q] = lo_ | (hi_ << 16);                                                                 \
+    }                                                                                            \
+    *reinterpret_cast<uint4*>(dst_) = uint4{w_[0], w_[1], w_[2], w_[3]};                          \
+  }
+#define GRAM_STORE(TB, T0)                                                                       \
+  {                                                                                              \
+    _Pragma("unroll") for (int i = 0; i < NI; ++i) {                                             \
+      if (goff[i] >= 0) {                                                                        \
+        uint16_t* p_ = (TB) + loff[i];                                                           \
+        GRAM_COL(i, x, p_);                                                                      \
+        GRAM_COL(i, y, p_ + kCS);                                                                \
+        GRAM_COL(i, z, p_ + 2 * kCS);                                                            \
+        GRAM_COL(i, w, p_ + 3 * kCS);                                                            \
+      }                                                                                          \
+    }                                                                                            \
+    if (tid < kRows) {                                                                           \
       (TB)[d * kCS + tid] = __builtin_bit_cast(uint16_t, (__bf16)((T0) + tid < rb1 ? 1.f : 0.f)); \
-      (TB)[(d + 1) * kCS + tid] = __builtin_bit_cast(uint16_t, (__bf16)yv);                \
-    }                                                                                      \
+      (TB)[(d + 1) * kCS + tid] = __builtin_bit_cast(uint16_t, (__bf16)yv);                      \
+    }                                                                                            \
   }
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
   __syncthreads();
@@ -267,13 +289,13 @@ __global__ __launch_bounds__(256) void gram_bf16s_kernel(const float* __restrict
     GRAM_LOAD(rb0);
     GRAM_STORE(buf, rb0);
   }
-  for (int64_t t0 = rb0; t0 < rb1; t0 += 64) {
-    const bool more = t0 + 64 < rb1;
-    if (more) GRAM_LOAD(t0 + 64);
+  for (int64_t t0 = rb0; t0 < rb1; t0 += kRows) {
+    const bool more = t0 + kRows < rb1;
+    if (more) GRAM_LOAD(t0 + kRows);
     __syncthreads();
     const uint16_t* tc = buf + cur * tsz;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 0; ks < kRows / 16; ++ks) {
       const int kr = ks * 16 + 8 * half;
 #pragma unroll
       for (int j = 0; j < PW; ++j) {
@@ -284,7 +306,7 @@ __global__ __launch_bounds__(256) void gram_bf16s_kernel(const float* __restrict
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[j], 0, 0, 0);
       }
     }
-    if (more) GRAM_STORE(buf + (cur ^ 1) * tsz, t0 + 64);
+    if (more) GRAM_STORE(buf + (cur ^ 1) * tsz, t0 + kRows);
     cur ^= 1;
   }
   const int col = lane & 31;
@@ -298,18 +320,32 @@ __global__ __launch_bounds__(256) void gram_bf16s_kernel(const float* __restrict
 }
 #undef GRAM_LOAD
 #undef GRAM_STORE
+#undef GRAM_COL
 
-__global__ void gram_reduce_kernel(const float* __restrict__ partial, int nblk, int npairs, PairTable tab, int D,
-                                   double* __restrict__ out) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)npairs * 1024) return;
-  const int gp = (int)(idx >> 10), e = (int)(idx & 1023);
+// partial [nblk][npairs][1024] -> out (symmetric fill).  16 threads per element each sum a fixed stride of
+// blocks, then a fixed-order LDS tree: deterministic, and 16x the parallelism of one thread per element
+// (the serial 1024-block loop took 0.35 ms of a 3.6 ms fit).
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ partial, int nblk, int npairs,
+                                                          PairTable tab, int D, double* __restrict__ out) {
+  __shared__ double red[16][16];
+  const int el = threadIdx.x & 15, part = threadIdx.x >> 4;
+  const int64_t idx = (int64_t)blockIdx.x * 16 + el;
+  const bool ok = idx < (int64_t)npairs * 1024;
+  const int gp = ok ? (int)(idx >> 10) : 0, e = ok ? (int)(idx & 1023) : 0;
   double s = 0.0;
-  for (int b = 0; b < nblk; ++b) s += (double)partial[((int64_t)b * npairs + gp) * 1024 + e];
-  const int i = tab.I[gp] * 32 + (e >> 5), j = tab.J[gp] * 32 + (e & 31);
-  if (i < D && j < D) {
-    out[(int64_t)i * D + j] = s;
-    out[(int64_t)j * D + i] = s;
+  if (ok)
+    for (int b = part; b < nblk; b += 16) s += (double)partial[((int64_t)b * npairs + gp) * 1024 + e];
+  red[part][el] = s;
+  __syncthreads();
+  if (part == 0 && ok) {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][el];
+    const int i = tab.I[gp] * 32 + (e >> 5), j = tab.J[gp] * 32 + (e & 31);
+    if (i < D && j < D) {
+      out[(int64_t)i * D + j] = t;
+      out[(int64_t)j * D + i] = t;
+    }
   }
 }
 
@@ -375,7 +411,7 @@ template <int PW, int NI>
 void launch_stream(const GramPlan& pl, const float* X, int64_t n, int d, int64_t ldx, const float* y,
                    const float* shift, float yshift, float* ws, hipStream_t st) {
   const int Dpad = ((pl.D + 31) / 32) * 32;
-  const size_t lds = (size_t)2 * Dpad * 72 * 2;
+  const size_t lds = (size_t)2 * Dpad * (64 + 8) * 2;
   hipLaunchKernelGGL((gram_bf16s_kernel<PW, NI>), dim3(pl.nblk), dim3(256), lds, st, X, n, d, ldx, y, shift, yshift,
                      pl.tab, pl.npairs, Dpad, ws, pl.rows_per_unit);
 }
@@ -383,10 +419,9 @@ void launch_stream(const GramPlan& pl, const float* X, int64_t n, int d, int64_t
 template <int PW>
 void launch_stream_ni(const GramPlan& pl, const float* X, int64_t n, int d, int64_t ldx, const float* y,
                       const float* shift, float yshift, float* ws, hipStream_t st) {
-  const int ni = (64 * (d / 4) + 255) / 256;
-  if (ni <= 4) launch_stream<PW, 4>(pl, X, n, d, ldx, y, shift, yshift, ws, st);
-  else if (ni <= 7) launch_stream<PW, 7>(pl, X, n, d, ldx, y, shift, yshift, ws, st);
-  else launch_stream<PW, 10>(pl, X, n, d, ldx, y, shift, yshift, ws, st);
+  const int ni = (8 * (d / 4) + 255) / 256;
+  if (ni <= 1) launch_stream<PW, 1>(pl, X, n, d, ldx, y, shift, yshift, ws, st);
+  else launch_stream<PW, 2>(pl, X, n, d, ldx, y, shift, yshift, ws, st);
 }
 
 template <int P>
@@ -427,7 +462,7 @@ CDNA_API int cdna_gram(const float* X, int64_t n, int d, int64_t ldx, const floa
   if (pl.npairs > kMaxPairs) return (int)hipErrorInvalidValue;
   if (bf16 && stream_ok(X, d, ldx, shift)) {
     pl = make_stream_plan(n, d);
-    const int pw = (pl.npairs + 3) / 4;
+    const int pw = (pl.npairs + 3) / 4;  // 4 waves share the tile pairs
     switch (pw) {
       case 1: launch_stream_ni<1>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
       case 2: launch_stream_ni<2>(pl, X, n, d, ldx, y, shift, yshift, ws, st); break;
@@ -456,7 +491,7 @@ CDNA_API int cdna_gram(const float* X, int64_t n, int d, int64_t ldx, const floa
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t tot = (int64_t)pl.npairs * 1024;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ws, pl.nblk,
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((tot + 15) / 16)), dim3(256), 0, st, ws, pl.nblk,
                      pl.npairs, pl.tab, pl.D, out);
   return (int)hipGetLastError();
 }
