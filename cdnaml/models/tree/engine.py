@@ -397,24 +397,33 @@ class Forest:
             return self._dev[key]
         N = self.num_nodes
         nodes = np.zeros((N, 4), dtype=np.int32)
-        vals = []
-        masks = []
-        for i in range(N):
-            if self.feat[i] < 0:
-                off = len(vals)
-                v = self.value[i] if values_kind == "value" else self.value[i] * self.weight[i]
-                vals.extend(v.tolist())
-                nodes[i] = (-1, off, 0, 0)
-            elif self.is_cat[i]:
-                nodes[i] = (-(self.feat[i] + 2), len(masks), self.left[i], self.right[i])
-                masks.append(self.catmask[i].view(np.int32))
-            else:
-                nodes[i] = (self.feat[i], np.array([self.thr[i]], dtype=np.float32).view(np.int32)[0],
-                            self.left[i], self.right[i])
-        out = (torch.from_numpy(nodes).to(device),
-               torch.tensor(self.roots, dtype=torch.int32, device=device),
-               torch.tensor(vals if vals else [0.0], dtype=torch.float32, device=device),
-               torch.from_numpy(np.concatenate(masks) if masks else np.zeros(8, np.int32)).to(device))
+        feat = np.asarray(self.feat, dtype=np.int32)
+        leaf = feat < 0
+        isc = np.asarray(self.is_cat, dtype=bool) & ~leaf
+        num = ~leaf & ~isc
+        left = np.asarray(self.left, dtype=np.int32)
+        right = np.asarray(self.right, dtype=np.int32)
+        lid = np.nonzero(leaf)[0]
+        V = (np.stack([self.value[i] for i in lid.tolist()]).astype(np.float64) if len(lid)
+             else np.zeros((0, self.K)))
+        if values_kind != "value" and len(lid):
+            V = V * np.asarray(self.weight, dtype=np.float64)[lid][:, None]
+        kv = V.shape[1] if V.ndim == 2 else 1
+        nodes[lid, 0] = -1
+        nodes[lid, 1] = np.arange(len(lid), dtype=np.int32) * kv
+        cid = np.nonzero(isc)[0]
+        nodes[cid, 0] = -(feat[cid] + 2)
+        nodes[cid, 1] = np.arange(len(cid), dtype=np.int32)
+        nid = np.nonzero(num)[0]
+        nodes[nid, 0] = feat[nid]
+        nodes[nid, 1] = np.asarray(self.thr, dtype=np.float64)[nid].astype(np.float32).view(np.int32)
+        inner = ~leaf
+        nodes[inner, 2] = left[inner]
+        nodes[inner, 3] = right[inner]
+        vals = V.reshape(-1).astype(np.float32) if V.size else np.zeros(1, np.float32)
+        masks = (np.stack([self.catmask[i] for i in cid.tolist()]).view(np.int32).reshape(-1) if len(cid)
+                 else np.zeros(8, np.int32))
+        out = tuple(K.upload(device, nodes, np.asarray(self.roots, dtype=np.int32), vals, masks))
         self._dev[key] = out
         return out
 
@@ -436,8 +445,8 @@ class Forest:
                 masks.append(self.catmask[g].view(np.int32))
             else:
                 nodes[j] = (self.feat[g], self.bin[g], pos[self.left[g]], pos[self.right[g]])
-        out = (torch.from_numpy(nodes).to(device), torch.tensor(vals, dtype=torch.float32, device=device),
-               torch.from_numpy(np.concatenate(masks) if masks else np.zeros(8, np.int32)).to(device))
+        out = tuple(K.upload(device, nodes, np.asarray(vals, dtype=np.float32).reshape(-1),
+                             np.concatenate(masks) if masks else np.zeros(8, np.int32)))
         self._dev[key] = out
         return out
 
@@ -474,13 +483,13 @@ class Forest:
             masks = [self.catmask[i].view(np.int32) for i in cat_ids.tolist()]
             heap[lt[isc], ls[isc], 0] = -(fl[isc] + 2)
             heap[lt[isc], ls[isc], 1] = np.arange(len(cat_ids), dtype=np.int32)
-            res = (torch.from_numpy(heap).to(device), D,
-                   torch.from_numpy(np.concatenate(masks) if masks else np.zeros(8, np.int32)).to(device))
+            h_t, m_t = K.upload(device, heap, np.concatenate(masks) if masks else np.zeros(8, np.int32))
+            res = (h_t, D, m_t)
         self._dev[key] = res
         return res
 
     def predict(self, X: torch.Tensor, tree_w: np.ndarray, base=None, values_kind="value") -> torch.Tensor:
-        tw = torch.tensor(np.asarray(tree_w, np.float32), device=X.device)
+        tw, = K.upload(X.device, np.asarray(tree_w, np.float32).reshape(-1))
         if self.K == 1 and X.device.type == "cuda" and HEAP_PREDICT:
             ha = self.heap_arrays(X.device, values_kind)
             if ha is not None:
@@ -489,7 +498,7 @@ class Forest:
                 if out is not None:
                     return out
         nodes, roots, vals, masks = self.device_arrays(X.device, values_kind)
-        b = None if base is None else torch.tensor(np.asarray(base, np.float32).reshape(-1), device=X.device)
+        b = None if base is None else K.upload(X.device, np.asarray(base, np.float32).reshape(-1))[0]
         return K.tree_predict(X, nodes, roots, tw, vals, masks, self.K, b)
 
     def predict_leaf_index(self, X: torch.Tensor) -> torch.Tensor:
@@ -897,8 +906,7 @@ class ForestTrainer:
                 masks_np = self._feature_masks(tid.astype(np.uint64), a_key)
             fm_build = None
             if masked:
-                fm_build = torch.from_numpy(np.ascontiguousarray(masks_np[build_ids]).view(np.int32)).to(dev)
-            build_slot = torch.from_numpy(slot_of).to(dev)
+                fm_build, = K.upload(dev, np.ascontiguousarray(masks_np[build_ids]).view(np.int32))
             id_tree = a_tree
             tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
             hist_raw_scale = None
@@ -938,13 +946,14 @@ class ForestTrainer:
                 elif use_codes:
                     Hb = K.hist_codes(1 if self.classification else 0, data.bins, d, codes, tfirst,
                                       stats_rows.get("v0"), stats_rows.get("v1"), stats_rows.get("label"), self.C,
-                                      build_slot, slot_tree, id_tree, fm_build, B, wmax=wmax)
+                                      K.upload(dev, slot_of)[0], slot_tree, id_tree, fm_build, B, wmax=wmax)
                 elif self.classification:
-                    Hb = K.hist_classes(data.bins, d, node, weights, stats_rows["label"], self.C, build_slot,
+                    Hb = K.hist_classes(data.bins, d, node, weights, stats_rows["label"], self.C,
+                                        K.upload(dev, slot_of)[0],
                                         slot_tree, fm_build, B, id_tree=id_tree)
                 else:
                     Hb = K.hist_moments(data.bins, d, node, weights, stats_rows.get("v0"), stats_rows["v1"],
-                                        build_slot, slot_tree, fm_build, B, id_tree=id_tree)
+                                        K.upload(dev, slot_of)[0], slot_tree, fm_build, B, id_tree=id_tree)
             with _tr.span("tree.allreduce", cat="comm", bytes=Hb.numel() * 8):
                 self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
             _split_span = _tr.span("tree.split", depth=depth)
@@ -958,7 +967,7 @@ class ForestTrainer:
                                     slot_of, a_parent, a_sib)
             else:
                 H = Hb
-            masks_t = torch.from_numpy(masks_np.view(np.int32)).to(dev) if masks_np is not None else None
+            masks_t = K.upload(dev, masks_np.view(np.int32))[0] if masks_np is not None else None
             if self._native_split(dev):
                 # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
                 mb = p.impurity == "xgb" and self.data.missing_bin
@@ -1049,9 +1058,9 @@ class ForestTrainer:
             # children in (node, side) order: ids base + 2j (left), base + 2j + 1 (right)
             k_st = lst_h.shape[1]
             ch_st = np.stack([lst_h[sp], rst_h[sp]], 1).reshape(-1, k_st)
-            ch_ids = forest.add_many(self._leaf_values_v(ch_st), self._weights_v(ch_st), depth + 1,
-                                     self._impurities_v(ch_st))
-            forest.set_splits(fid_sp, f_sp, gain_h[sp], b_sp, thr_sp, num, ch_ids[0::2], ch_ids[1::2])
+            # forest ids of the children (appended after the partition launch: the forest bookkeeping then
+            # runs on the host while the GPU partitions the rows)
+            ch_ids = np.arange(forest.num_nodes, forest.num_nodes + 2 * len(sp), dtype=np.int64)
             cw = self._weights_v(ch_st)
             leaf = (cw < 2 * p.min_instances) | (depth + 1 >= p.max_depth)
             if self.classification:
@@ -1086,13 +1095,15 @@ class ForestTrainer:
                             np.searchsorted(n_tree, np.arange(T), side="left").astype(np.int32))
                         K.partition_codes(data.bins, codes, tfirst, tfirst_next, torch.from_numpy(split_feat),
                                           torch.from_numpy(split_bin), torch.from_numpy(cat_off),
-                                          torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child),
+                                          torch.from_numpy(cm.reshape(-1)), torch.from_numpy(child),
                                           bins_rm=data.row_major_bins() if (PARTITION_RM and dev.type == "cuda")
                                           else None)
                     else:
-                        K.partition(data.bins, node, torch.from_numpy(split_feat).to(dev),
-                                    torch.from_numpy(split_bin).to(dev), torch.from_numpy(cat_off).to(dev),
-                                    torch.from_numpy(cm.reshape(-1)).to(dev), torch.from_numpy(child).to(dev))
+                        K.partition(data.bins, node, *K.upload(dev, split_feat, split_bin, cat_off,
+                                                               cm.reshape(-1), child))
+            got = forest.add_many(self._leaf_values_v(ch_st), cw, depth + 1, self._impurities_v(ch_st))
+            assert len(got) == len(ch_ids) and (not len(got) or got[0] == ch_ids[0])
+            forest.set_splits(fid_sp, f_sp, gain_h[sp], b_sp, thr_sp, num, ch_ids[0::2], ch_ids[1::2])
             prev_hist = H if subtract else None
             a_tree, a_fid, a_key, a_stats, a_sib, a_parent = n_tree, n_fid, n_key, n_stats, n_sib, n_parent
         forest.roots.extend(root_ids)

@@ -33,6 +33,41 @@ def _native(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+_TORCH_DT = {}
+
+
+def upload(dev, *arrays):
+    """Host numpy arrays -> device tensors through ONE pinned staging block and one async copy.
+
+    A pageable ``torch.from_numpy(x).to(dev)`` synchronises the stream (the copy must finish before the host
+    buffer may change), so every small per-level table used to drain the GPU queue and expose the host work
+    that followed as idle time (up to 0.5 ms per copy at the 8-GPU shard shape).  The staging block comes from
+    PyTorch's caching pinned-host allocator, which keeps it until the copy's stream event has passed.
+    On the CPU the arrays are wrapped as they are (no copy)."""
+    dev = torch.device(dev)
+    arrs = [np.ascontiguousarray(a) for a in arrays]
+    if dev.type != "cuda":
+        return [torch.from_numpy(a) for a in arrs]
+    offs, o = [], 0
+    for a in arrs:
+        o = -(-o // 16) * 16
+        offs.append(o)
+        o += a.nbytes
+    host = torch.empty(max(o, 16), dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
+    for a, off in zip(arrs, offs):
+        if a.nbytes:
+            hv[off:off + a.nbytes] = a.reshape(-1).view(np.uint8)
+    dbuf = host.to(dev, non_blocking=True)
+    out = []
+    for a, off in zip(arrs, offs):
+        tdt = _TORCH_DT.get(a.dtype)
+        if tdt is None:
+            tdt = _TORCH_DT[a.dtype] = torch.from_numpy(np.empty(0, dtype=a.dtype)).dtype
+        out.append(dbuf[off:off + a.nbytes].view(tdt).reshape(a.shape))
+    return out
+
+
 # --------------------------------------------------------------------- K1
 def gram(X: torch.Tensor, y: Optional[torch.Tensor] = None, shift: Optional[torch.Tensor] = None,
          yshift: float = 0.0, bf16: bool = False) -> torch.Tensor:
@@ -118,7 +153,7 @@ def hist_assemble(Hb: torch.Tensor, raw_scale, prev: Optional[torch.Tensor], slo
             H[der] = prev[par] - src[sl[sib_]]
         return H
     H = torch.empty((A, d, B, Kc), dtype=torch.float64, device=dev)
-    m = torch.from_numpy(np.stack([slot, parent, sib], 1).astype(np.int32).reshape(-1)).to(dev)
+    m, = upload(dev, np.stack([slot, parent, sib], 1).astype(np.int32).reshape(-1))
     src = Hb.contiguous() if raw else Hb.double().contiguous()
     if raw:
         assert Hb.dtype == torch.int64
@@ -648,7 +683,7 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
         i1 = int(np.searchsorted(id_tree, t1, side="right"))
         rows.append((a, t0, t1, i0, i1))
         a = b
-    grp = torch.tensor(rows, dtype=torch.int32, device=bins.device).reshape(-1)
+    grp, = upload(bins.device, np.asarray(rows, dtype=np.int32).reshape(-1))
     ng = len(rows)
     # the tree cap can leave groups smaller than the LDS budget allows: size LDS to the largest group
     SB = max(min(SB, (rows[i + 1][0] if i + 1 < ng else S) - rows[i][0]) for i in range(ng))
@@ -677,7 +712,8 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
     qs1 = _packed_scale(v1) if packed else _fixed_scale(v1, n, wmax, qmax_bits=30)
     iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
     assert codes.dtype == torch.int16 and codes.is_contiguous() and codes.shape[1] == n
-    tf = tfirst.to(device=bins.device, dtype=torch.int32).contiguous()
+    tf = (upload(bins.device, tfirst.numpy().astype(np.int32))[0] if not tfirst.is_cuda else
+          tfirst.to(dtype=torch.int32).contiguous())
     bs = build_slot.int().contiguous()
     _lib.check(lib.cdna_hist5(kbits, _ptr(bins), n, d, T, _ptr(codes), _ptr(tf), _ptr(v0), _ptr(v1), _ptr(label),
                               int(C), _ptr(bs), _ptr(fm), mw, S, B, SB, _ptr(grp), ng, nchunk, max_nt, qs0, qs1,
@@ -713,18 +749,16 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
     if n == 0 or T == 0:
         return
     if _native(bins):
-        cm = cat_mask.int().contiguous() if cat_mask.numel() else torch.zeros(8, dtype=torch.int32,
-                                                                                 device=bins.device)
-        srcs = (tfirst, tfirst_next, split_feat, split_bin, cat_off, child)
+        if not cat_mask.numel():
+            cat_mask = torch.zeros(8, dtype=torch.int32)
+        srcs = (tfirst, tfirst_next, split_feat, split_bin, cat_off, child, cat_mask)
         if all(not t.is_cuda for t in srcs):
-            # one host->device copy for the six small tables (six copies were ~0.13 ms of launch gaps per level)
-            flat = torch.cat([t.reshape(-1).to(torch.int32) for t in srcs]).to(bins.device)
-            args, o = [], 0
-            for t in srcs:
-                args.append(flat[o:o + t.numel()])
-                o += t.numel()
+            # one async host->device copy for the seven small tables (seven synchronous copies were ~0.13 ms
+            # of launch gaps per level)
+            args = upload(bins.device, *[t.numpy().astype(np.int32).reshape(-1) for t in srcs])
         else:
             args = [t.to(device=bins.device, dtype=torch.int32).contiguous() for t in srcs]
+        cm = args[6]
         A = int(split_feat.numel())
         # partition7 streams every bins word of every row once per level (10 GB at 1e8 x 100): it pays when
         # many trees share that pass; for few trees partition5's per-(row, tree) byte gathers move less (GBDT,
@@ -1148,7 +1182,7 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
             k = (sg[:, 1] + chunk - 1) // chunk
             j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
             work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
-        wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
+        wt, = upload(bins.device, work.reshape(-1))
         iout = torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
         assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
         _lib.check(_lib.lib().cdna_seg_hist(1 | 4 | 16, _ptr(bins_rm), n, d, B, _ptr(rec), None, None, None,
@@ -1202,9 +1236,9 @@ def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optio
             k = (sg[:, 1] + chunk - 1) // chunk
             j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
             work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
-        wt = torch.from_numpy(work.reshape(-1)).to(bins.device)
+        wt, = upload(bins.device, work.reshape(-1))
         iout = torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
-        mode = (1 if packed else 0) | (2 if wp is not None else 0) | (4 if bins_rm is not None else 0)
+        mode =(1 if packed else 0) | (2 if wp is not None else 0) | (4 if bins_rm is not None else 0)
         if bins_rm is not None:
             assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
         src = bins if bins_rm is None else bins_rm
@@ -1256,8 +1290,7 @@ def seg_hist_subset(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v1p:
         bins_rm = bins_row_major(bins)
     assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
     dev = bins.device
-    wt = torch.from_numpy(work.reshape(-1)).to(dev)
-    ft = torch.from_numpy(feats.reshape(-1)).to(dev)
+    wt, ft = upload(dev, work.reshape(-1), feats.reshape(-1))
     iout = torch.zeros(out.shape, dtype=torch.int64, device=dev)
     _lib.check(_lib.lib().cdna_seg_hist_subset(_ptr(bins_rm), n, bins_rm.shape[1] * 8, d, B, _ptr(perm), _ptr(v1p), _ptr(wp),
                                                _ptr(wt), len(work), float(qs1), _ptr(ft), m, _ptr(iout),
@@ -1328,12 +1361,10 @@ def seg_partition(bins: torch.Tensor, perm: Optional[torch.Tensor], v0p: Optiona
     work = _seg_work(np.concatenate([segs, tags[:, None]], 1), SEG_PART_CHUNK)
     nw = len(work)
     L = _lib.lib()
-    sf_t = torch.from_numpy(sf).to(dev)
-    sb_t = torch.from_numpy(np.asarray(split_bin, dtype=np.int32)).to(dev)
-    co_t = torch.from_numpy(np.asarray(cat_off, dtype=np.int32)).to(dev)
     cm = np.asarray(cat_mask, dtype=np.int32).reshape(-1)
-    cm_t = torch.from_numpy(cm if cm.size else np.zeros(8, np.int32)).to(dev)
-    wt = torch.from_numpy(work.reshape(-1)).to(dev)
+    sf_t, sb_t, co_t, cm_t, wt = upload(dev, sf, np.asarray(split_bin, dtype=np.int32),
+                                        np.asarray(cat_off, dtype=np.int32), cm if cm.size else np.zeros(8, np.int32),
+                                        work.reshape(-1))
     lrc = torch.zeros((2, max(nw, 1)), dtype=torch.int32, device=dev)
     impl_n = n if implicit else 0
     if nw:
@@ -1368,8 +1399,7 @@ def seg_partition(bins: torch.Tensor, perm: Optional[torch.Tensor], v0p: Optiona
     v0_o = None if v0p is None else torch.empty(total, dtype=torch.float32, device=dev)
     w_o = None if wp is None else torch.empty(total, dtype=torch.uint8, device=dev)
     if nw and total:
-        lb_t = torch.from_numpy(lb.astype(np.int32)).to(dev)
-        rb_t = torch.from_numpy(rb.astype(np.int32)).to(dev)
+        lb_t, rb_t = upload(dev, lb.astype(np.int32), rb.astype(np.int32))
         _lib.check(L.cdna_seg_partition(2, _ptr(bins), n, _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp), _ptr(wt), nw,
                                         _ptr(sf_t), _ptr(sb_t), _ptr(co_t), _ptr(cm_t), _ptr(lb_t), _ptr(rb_t),
                                         None, _ptr(perm_o), _ptr(v0_o), _ptr(v1_o), _ptr(w_o), impl_n, None,
@@ -1415,7 +1445,6 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
                 wts.to(torch.uint8), np.stack([starts, lens], 1))
     L = _lib.lib()
     assert tfirst.numel() == T
-    tf = tfirst.to(device=dev, dtype=torch.int32)
     # built nodes per tree -> wave-owned kernel when few (stable, no atomics)
     tf_h = tfirst.cpu().numpy().astype(np.int64)
     tree_of = np.searchsorted(tf_h, np.arange(A), side="right") - 1
@@ -1423,9 +1452,9 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
     nb_t = np.bincount(tree_of[built], minlength=T) if A else np.zeros(T, np.int64)
     kb_need = int(nb_t.max()) if T else 0
     if 0 < kb_need <= 16 and COMPACT_W:
-        return _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1,
+        return _codes_compact_w(codes, tf_h.astype(np.int32), bs, tree_of, built, nb_t, kb_need, S, v0, v1,
                                 rec_scale if (v0 is None and n < 2 ** 31) else None)
-    bs_t = torch.from_numpy(bs).to(dev)
+    tf, bs_t = upload(dev, tf_h.astype(np.int32), bs)
     v1c = v1.float().contiguous()
     v0c = None if v0 is None else v0.float().contiguous()
     cnt = torch.zeros(max(S, 1), dtype=torch.int32, device=dev)
@@ -1445,7 +1474,7 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
         v0p = None if v0 is None else torch.empty(total, dtype=torch.float32, device=dev)
         wp = torch.empty(total, dtype=torch.uint8, device=dev)
     if total:
-        cur = torch.from_numpy(np.concatenate([starts, [0]]).astype(np.int32)).to(dev)
+        cur, = upload(dev, np.concatenate([starts, [0]]).astype(np.int32))
         _lib.check(L.cdna_codes_compact(2, _ptr(codes), n, T, A, _ptr(tf), _ptr(bs_t), _ptr(v0c), _ptr(v1c),
                                         _ptr(cur), None if rec else _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp),
                                         _ptr(perm) if rec else None, float(rec_scale) if rec else 0.0,
@@ -1456,7 +1485,7 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
 COMPACT_W = __import__("os").environ.get("CDNAML_COMPACT_W", "1") != "0"
 
 
-def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1, rec_scale=None):
+def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, rec_scale=None):
     T, n = codes.shape
     dev = codes.device
     A = len(bs)
@@ -1472,7 +1501,7 @@ def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1, re
     per_wave = max(256, -(-n // (2048 * 256)) * 256)
     Wv = -(-n // per_wave)
     L = _lib.lib()
-    kmap_t = torch.from_numpy(kmap).to(dev)
+    tf, kmap_t = upload(dev, tf_h, kmap)
     v1c = v1.float().contiguous()
     v0c = None if v0 is None else v0.float().contiguous()
     wcnt = torch.empty((T, Wv, KB), dtype=torch.int32, device=dev)
@@ -1502,7 +1531,7 @@ def _codes_compact_w(codes, tf, bs, tree_of, built, nb_t, kb_need, S, v0, v1, re
     if total:
         kstart = np.zeros((T, KB), dtype=np.int64)
         kstart[valid] = starts[sl[valid]]
-        kstart_t = torch.from_numpy(kstart).to(dev)
+        kstart_t, = upload(dev, kstart)
         # wcnt now holds the per-wave exclusive offsets; the scatter pass adds each node's segment start
         _lib.check(L.cdna_codes_compact_w(2, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
                                           per_wave, Wv, None, _ptr(wcnt), None if rec else _ptr(perm), _ptr(v0p),
@@ -1570,7 +1599,7 @@ def hist_mfma(bp: torch.Tensor, ldp: int, n: int, d: int, B: int, codes: torch.T
         ns = len(order[sl])
         bt, nt = _mfma_tiles(B, ns)
         acc = torch.zeros((d, bt * 16, nt * 16), dtype=torch.int64, device=dev)
-        meta = torch.from_numpy(np.stack([tree[sl], loc[sl], slots[sl]]).astype(np.int32)).to(dev)
+        meta, = upload(dev, np.stack([tree[sl], loc[sl], slots[sl]]).astype(np.int32))
         _lib.check(_lib.lib().cdna_hist_mfma(_ptr(bp), ldp, n, d, B, bt, nt, _ptr(codes), _ptr(meta[0]),
                                              _ptr(meta[1]), _ptr(meta[2]), ns, _ptr(v1c), float(qs1), chunk,
                                              MFMA_FPB, _ptr(acc), _ptr(out), _stream(dev)), "cdna_hist_mfma")

@@ -52,7 +52,9 @@ run_step() {
         (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$s" -o p \
             -- python3 "$R/bench.py" --rows $rows --steps 2 --warmup 1 ${BENCH_ARGS} > "$O/$s/bench.log" 2>&1)
         local rc=$?; [ $rc -ne 0 ] && { tail -5 "$O/$s/bench.log"; return $rc; }
-        kstats "$O/$s" ;;
+        kstats "$O/$s"
+        python scripts/gaps.py "$(find "$O/$s" -name "*kernel_trace.csv" | sort | sed -n 1p)" > "$O/$s/gaps.txt"
+        cat "$O/$s/gaps.txt" ;;
     pmc:*)
         rm -rf "$O/pmc"; mkdir -p "$O/pmc"
         (cd /tmp && timeout -s KILL 300 rocprofv3 -i "$R/scripts/pmc_hist.txt" --kernel-include-regex "${s#pmc:}" \
