@@ -1077,6 +1077,10 @@ def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_glob
 
 
 SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "1024"))
+# record histograms through the lane-feature kernel (seg_hist_lane_kernel: lanes own features, bin-major
+# conflict-free LDS planes, one v_perm per cell address); B <= 80 (planes <= 80 KB of LDS)
+SEG_LANE = __import__("os").environ.get("CDNAML_SEG_LANE", "1") != "0"
+SEG_LANE_MAX_B = 80
 
 
 def _fill_chunk(segs: np.ndarray, chunk: int) -> int:
@@ -1185,7 +1189,8 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         wt, = upload(bins.device, work.reshape(-1))
         iout = torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
         assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
-        _lib.check(_lib.lib().cdna_seg_hist(1 | 4 | 16, _ptr(bins_rm), n, d, B, _ptr(rec), None, None, None,
+        mode = 1 | 4 | 16 | (128 if (SEG_LANE and B <= SEG_LANE_MAX_B) else 0)
+        _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(bins_rm), n, d, B, _ptr(rec), None, None, None,
                                             _ptr(wt), len(work), 1.0, qs1, _ptr(iout), bins_rm.shape[1],
                                             _stream(bins.device)), "cdna_seg_hist(rec)")
     if raw:

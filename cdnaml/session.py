@@ -37,6 +37,9 @@ _DEFAULT_CONF = {
 }
 
 
+_UNSET = object()
+
+
 class RuntimeConfig:
     def __init__(self, initial=None):
         self._d = dict(_DEFAULT_CONF)
@@ -49,10 +52,11 @@ class RuntimeConfig:
     def set(self, key, value):
         self._d[key] = str(value).lower() if isinstance(value, bool) else str(value)
 
-    def get(self, key, default=None):
+    def get(self, key, default=_UNSET):
+        """Like ``spark.conf.get``: an unset key raises unless a default (``None`` included) is given."""
         if key in self._d:
             return self._d[key]
-        if default is not None:
+        if default is not _UNSET:
             return default
         raise KeyError(f"conf {key} is not set")
 

@@ -56,6 +56,56 @@ class Classroom:
 
     validateYourAnswer = validate_your_answer
 
+    def validate_your_schema(self, what: str, df, exp_column_name: str, exp_column_type: Optional[str] = None) -> bool:
+        """Check that ``df`` has column ``exp_column_name`` (of type name ``exp_column_type`` when given, e.g.
+        "double", "string", "vector"); records the outcome under "<what> contains <col>:<type>" (UTIL:175-194)."""
+        key = f"{what} contains {exp_column_name}:{exp_column_type}"
+        try:
+            actual = df.schema[exp_column_name].dataType.typeName()
+        except (KeyError, IndexError, AttributeError):
+            self.test_results[what] = {"passed": False, "answer": "-not found-"}
+            print(f"{key}: NOT found")
+            return False
+        ok = exp_column_type is None or actual == exp_column_type
+        answer = "validated" if ok else f"{exp_column_name}:{actual}"
+        self.test_results[key] = {"passed": ok, "answer": answer}
+        print(f"{key}: validated" if ok else f"{key}: NOT matching ({answer})")
+        return ok
+
+    validateYourSchema = validate_your_schema
+
+    def all_done(self, advertisements: Dict[str, tuple]) -> str:
+        """Advertise the functions ("f"), variables ("v") and databases ("d") a setup cell defined (UTIL:297-351).
+
+        ``advertisements[name] = (kind, signature_or_value, description)``; a name is hidden when the conf
+        ``com.databricks.training.suppress.<name>`` is "true".  Returns the HTML (also sent to displayHTML)."""
+        from html import escape
+
+        from .dbutils import displayHTML
+        shown = {k: v for k, v in advertisements.items()
+                 if self.spark.conf.get(f"com.databricks.training.suppress.{k}", None) != "true"}
+        parts = []
+        for kind, title in (("f", "functions were defined"), ("v", "variables were defined"),
+                            ("d", "database were created")):
+            items = [(k, v) for k, v in shown.items() if v[0] == kind]
+            if not items:
+                continue
+            lis = []
+            for k, v in items:
+                if kind == "f":
+                    body = f"<b>{escape(k)}</b>(<i>{escape(str(v[1]))}</i>)"
+                elif kind == "v":
+                    body = f"<b>{escape(k)}</b>: <i>{escape(str(v[1]))}</i>"
+                else:
+                    body = f"Now using the database identified by <b>{escape(k)}</b>: <i>{escape(str(v[1]))}</i>"
+                lis.append(f"<li>{body}<div>{escape(str(v[2]))}</div></li>")
+            parts.append(f"The following {title} for you:<ul>{''.join(lis)}</ul>")
+        html = "".join(parts) + "All done!"
+        displayHTML(html)
+        return html
+
+    allDone = all_done
+
     def summarize_your_results(self) -> str:
         rows = [f"<tr><th>{k}</th><td>{'passed' if v['passed'] else 'FAILED'}</td></tr>"
                 for k, v in self.test_results.items()]

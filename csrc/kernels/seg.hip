@@ -347,6 +347,85 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
   }
 }
 
+// Lane-feature variant (packed item records, row-major bins).  The flat
+// kernel above gives each lane a (row, 8-feature group) pair: its cells are
+// (feature, bin) = random bank pairs (rocprofv3: 67 % of LDS cycles bank
+// conflicts) and every atomic costs ~12 VALU ops of cell arithmetic (VALU ~72 %
+// busy).  Here each 32-lane HALF of a wave takes one item and lane l' of the
+// half owns the 4 features of row dword l' (features f0 + 4l' + j):
+//   * one dword load per lane brings the item's 4 bins;
+//   * the LDS histogram is 4 byte-position planes [j][bin][32] u64, so the
+//     cell of (l', j, bin) is j * PLANE + bin * 32 + l': the 32 lanes of a half
+//     always hit 32 distinct bank pairs whatever the bins -- conflict-free;
+//   * the cell byte address (bin << 8 | l' * 8) is ONE v_perm_b32 of the bins
+//     dword and the lane offset, the plane offset j * PLANE * 8 an immediate.
+// ~5.5 VALU and 2 ds_add_u64 per item (flat kernel: ~17 and 1.45 with 3x the
+// LDS cycles per instruction).  Items past the chunk end load record 0 (weight
+// 0: their adds are 0).  Dwords past d carry zero / in-range bins of slots the
+// flush skips.
+template <int BP>
+__global__ __launch_bounds__(512) void seg_hist_lane_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins8,
+                                                            int row_bytes) {
+  constexpr int TH = 512, NW = TH / 64, U = 8;
+  constexpr int PLANE = BP * 32;
+  // static: the planes sit at a link-time-known LDS offset, so the cell address needs no base add
+  __shared__ __attribute__((aligned(16))) unsigned long long h[4 * PLANE];  // [4][BP][32]
+  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
+  const int f0 = blockIdx.y * 128;
+  for (int i = threadIdx.x; i < 4 * PLANE; i += TH) h[i] = 0ull;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, half = lane >> 5, lq = lane & 31;
+  const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  int dw = (f0 >> 2) + lq;
+  const int dmax = (row_bytes >> 2) - 1;
+  dw = dw < dmax ? dw : dmax;
+  const uint8_t* lbase = bins8 + 4 * dw;
+  const uint32_t loff = (uint32_t)lq * 8u;
+  const uint64_t* __restrict__ rec = a.rec + start;
+  for (int i0 = wid * 2 * U; i0 < len; i0 += NW * 2 * U) {
+    const bool full = i0 + 2 * U <= len;  // wave-uniform
+    uint64_t rc[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const int idx = i0 + 2 * p + half;
+      rc[p] = (full || idx < len) ? rec[idx] : 0ull;
+    }
+    uint32_t x[U];
+    unsigned long long add[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t lo = (uint32_t)rc[p], hi = (uint32_t)(rc[p] >> 32);
+      const uint32_t row = lo & 0x7FFFFFFFu;
+      x[p] = *reinterpret_cast<const uint32_t*>(lbase + (uint64_t)row * (uint64_t)row_bytes);
+      const uint32_t w = __builtin_amdgcn_alignbit(hi, lo, 31) & 0xFFu;
+      const uint32_t qb = hi >> 7;  // q1 + 2^23
+      add[p] = ((unsigned long long)(w << (kPackShift - 32)) << 32) + (unsigned long long)w * qb;
+    }
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t off = __builtin_amdgcn_perm(loff, x[p], 0x0C0C0004u | ((uint32_t)j << 8));  // bin<<8 | l'*8
+        atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h) + off) + j * PLANE, add[p]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 4 * PLANE; c += TH) {
+    const int j = c / PLANE, rem = c - j * PLANE;
+    const int bn = rem >> 5, l = rem & 31;
+    const int f = f0 + 4 * l + j;
+    if (bn >= a.B || f >= a.d) continue;
+    const unsigned long long v = h[c];
+    if (!v) continue;
+    const unsigned long long cnt = v >> kPackShift;
+    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+    atomicAdd(o, cnt);
+    atomicAdd(o + 1, (unsigned long long)sum);
+  }
+}
+
 // Feature-subset variant (RandomForest featureSubsetStrategy): a node's split
 // only considers its m sampled features (ML 07 / Spark "onethird" = 34 of 100),
 // so only those are accumulated.  Lanes take consecutive (row, sampled feature)
@@ -936,6 +1015,21 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
   SegHistArgs a{bins, n, d, B, perm, v0p, v1p, wp, work, qs0, qs1, out};
   a.rs = rm_stride;
   const bool packed = (mode & 1) != 0, has_w = (mode & 2) != 0;
+  if ((mode & 128) && (mode & 16) && (mode & 4) && packed) {
+    // lane-feature kernel: 128 features per block (4 byte planes of BP >= B bins x 32 lanes, BP KB of LDS)
+    if (B > 80) return (int)hipErrorInvalidValue;
+    const int G = (d + 7) / 8;
+    a.rec = reinterpret_cast<const uint64_t*>(perm);
+    const int row_bytes = (rm_stride ? rm_stride : G) * 8;
+    const dim3 grid((unsigned)nwork, (unsigned)((d + 127) / 128));
+    const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bins);
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(512), 0, st, a, b8, row_bytes); };
+    if (B <= 32) launch(seg_hist_lane_kernel<32>);
+    else if (B <= 40) launch(seg_hist_lane_kernel<40>);
+    else if (B <= 64) launch(seg_hist_lane_kernel<64>);
+    else launch(seg_hist_lane_kernel<80>);
+    return (int)hipGetLastError();
+  }
   if ((mode & 16) && (mode & 32) && (mode & 4) && packed && B <= 64) {
     // bank-private planes: one 8-feature group per block, 16 interleaved copies
     const int G = (d + 7) / 8;

@@ -990,3 +990,37 @@ def test_relational_on_hash_kernels_match_pandas(dev):
     j = df.join(spark.createDataFrame(dim), on="k").count()
     assert j == len(pdf.merge(dim, on="k"))
     assert df.dropDuplicates(["k", "s"]).count() == len(pdf.drop_duplicates(["k", "s"]))
+
+
+@pytest.mark.parametrize("d,B", [(21, 40), (100, 40), (130, 64), (100, 80), (64, 32), (257, 17)])
+def test_seg_hist_lane_matches_flat(dev, d, B, monkeypatch):
+    """K5 lane-feature kernel (lanes own features, bin-major LDS plane) gives exactly the int64 fixed-point
+    sums of the flat (row, group)-pair kernel: partial 64-lane feature halves, two feature blocks (d > 128),
+    B = 80, several chunks per segment and zero-weight records."""
+    T, n = 6, 150000
+    rng = np.random.default_rng(d * 7 + B)
+    loc = rng.integers(0, 3, (T, n))
+    w = rng.poisson(1.0, (T, n)).clip(0, 12)
+    loc = np.where(w == 0, 0xFF, loc)
+    codes = torch.from_numpy(((w << 8) | loc).astype(np.uint16).view(np.int16)).to(dev)
+    tfirst = torch.from_numpy(np.arange(T, dtype=np.int32) * 3)
+    slot_of = np.array([(t * 3 + k) if k < 2 else -1 for t in range(T) for k in range(3)], dtype=np.int32)
+    slot_of[slot_of >= 0] = np.arange(int((slot_of >= 0).sum()))
+    S = int((slot_of >= 0).sum())
+    g = torch.Generator().manual_seed(d)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    bins, rm = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), want_rm=True)
+    if rm is None:
+        rm = K.bins_row_major(bins)
+    v1 = (torch.randn(n, generator=g) * 5).to(dev)
+    sc = K.seg_scales(None, v1, 12, n)
+    rec, _, _, _, sg = K.codes_compact(codes, tfirst, slot_of, S, None, v1, rec_scale=sc[1])
+    sb = np.concatenate([sg, np.arange(S)[:, None]], 1)
+    monkeypatch.setattr(K, "SEG_HIST_CHUNK", 20000)
+    monkeypatch.setattr(K, "SEG_LANE", False)
+    ref = K.seg_hist(bins, d, B, rec, None, None, None, sb, S, 12, sc, bins_rm=rm, rec=True, raw=True)
+    monkeypatch.setattr(K, "SEG_LANE", True)
+    got = K.seg_hist(bins, d, B, rec, None, None, None, sb, S, 12, sc, bins_rm=rm, rec=True, raw=True)
+    assert got.dtype == torch.int64 and int(ref[..., 0].sum()) > 0
+    assert torch.equal(got.cpu(), ref.cpu())

@@ -132,3 +132,23 @@ def test_dedup_lab_with_classroom(spark, tmp_path, monkeypatch):
     final_count = spark.read.parquet(dest.replace("dbfs:/", str(tmp_path) + "/")).count()
     assert cr.validate_your_answer("01 Parquet File Exists", 1276280174, part_files)
     assert cr.validate_your_answer("02 Expected 100000 Records", 972882115, final_count)
+
+
+def test_validate_schema_and_all_done(spark, tmp_path, monkeypatch):
+    """H3 validateYourSchema (UTIL:175-194) and H7 allDone (UTIL:297-351)."""
+    monkeypatch.setenv("CDNAML_DBFS_ROOT", str(tmp_path))
+    cr = Classroom(spark, lesson="ML 01", install=False)
+    df = spark.createDataFrame([(1.0, "a")], ["price", "city"])
+    assert cr.validateYourSchema("01 schema", df, "price", "double")
+    assert cr.validateYourSchema("02 schema", df, "city")
+    assert not cr.validateYourSchema("03 schema", df, "city", "double")
+    assert not cr.validateYourSchema("04 schema", df, "missing", "double")
+    assert cr.test_results["03 schema contains city:double"] == {"passed": False, "answer": "city:string"}
+    assert cr.test_results["04 schema"]["answer"] == "-not found-"
+    spark.conf.set("com.databricks.training.suppress.hidden_fn", "true")
+    html = cr.allDone({"username": ("v", cr.username, "your user name"),
+                       "validateYourAnswer": ("f", "what, expectedHash, answer", "checks an answer"),
+                       "hidden_fn": ("f", "x", "not shown"),
+                       cr.database: ("d", cr.database, "your database")})
+    assert "validateYourAnswer" in html and "username" in html and cr.database in html
+    assert "hidden_fn" not in html and html.endswith("All done!")
