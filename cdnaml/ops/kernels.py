@@ -1081,6 +1081,8 @@ SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "1024
 # conflict-free LDS planes, one v_perm per cell address); B <= 80 (planes <= 80 KB of LDS)
 SEG_LANE = __import__("os").environ.get("CDNAML_SEG_LANE", "1") != "0"
 SEG_LANE_MAX_B = 80
+# records buffers carry REC_PAD readable entries past their end: the lane kernel's record loads are unconditional
+REC_PAD = 64
 
 
 def _fill_chunk(segs: np.ndarray, chunk: int) -> int:
@@ -1102,6 +1104,16 @@ def _seg_work(segs: np.ndarray, chunk: int) -> np.ndarray:
     st = segs[rep, 0] + j * chunk
     ln = np.minimum(chunk, segs[rep, 1] - j * chunk)
     return np.stack([st, ln, segs[rep, 2]], 1).astype(np.int32)
+
+
+def _interleave(work: np.ndarray, segs: np.ndarray, chunk: int) -> np.ndarray:
+    """Interleave segment chunks by relative position (chunk j of every segment covers about the same fraction of
+    the row ids), so concurrently running blocks gather nearby rows.  Tried on top: placing each round of
+    len(segs) chunks on one XCD (block b -> XCD b % 8) for L2 sharing -- measured 194 vs 190 ms, dropped."""
+    sg = segs[segs[:, 1] > 0]
+    k = (sg[:, 1] + chunk - 1) // chunk
+    j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
+    return work[np.argsort(j / np.repeat(k, k), kind="stable")]
 
 
 def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
@@ -1182,10 +1194,7 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         if len(work) == 0:
             return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
         if interleave and len(segs) > 1:
-            sg = segs[segs[:, 1] > 0]
-            k = (sg[:, 1] + chunk - 1) // chunk
-            j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
-            work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
+            work = _interleave(work, segs, chunk)
         wt, = upload(bins.device, work.reshape(-1))
         iout = torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
         assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
@@ -1471,7 +1480,7 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
     assert total < 2 ** 31
     rec = rec_scale is not None and v0 is None and n < 2 ** 31
     if rec:
-        perm = torch.empty(total, dtype=torch.int64, device=dev)
+        perm = torch.empty(total + REC_PAD, dtype=torch.int64, device=dev)[:total]  # readable tail
         v1p = v0p = wp = None
     else:
         perm = torch.empty(total, dtype=torch.int32, device=dev)
@@ -1526,7 +1535,7 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
     assert total < 2 ** 31
     rec = rec_scale is not None
     if rec:
-        perm = torch.empty(total, dtype=torch.int64, device=dev)
+        perm = torch.empty(total + REC_PAD, dtype=torch.int64, device=dev)[:total]  # readable tail
         v1p = v0p = wp = None
     else:
         perm = torch.empty(total, dtype=torch.int32, device=dev)

@@ -381,14 +381,23 @@ __global__ __launch_bounds__(512) void seg_hist_lane_kernel(const SegHistArgs a,
   dw = dw < dmax ? dw : dmax;
   const uint8_t* lbase = bins8 + 4 * dw;
   const uint32_t loff = (uint32_t)lq * 8u;
-  const uint64_t* __restrict__ rec = a.rec + start;
-  for (int i0 = wid * 2 * U; i0 < len; i0 += NW * 2 * U) {
-    const bool full = i0 + 2 * U <= len;  // wave-uniform
-    uint64_t rc[U];
+  // software-pipelined: the next trip's records are in flight while this trip's bins arrive and its atomics
+  // run.  Record loads are unconditional (lane base + immediate offsets): the record buffer carries >= 2U
+  // readable records past its end (codes_compact pads it), and a trip past the chunk end zeroes the
+  // out-of-range records (row 0, weight 0) before they are used.
+  const uint64_t* __restrict__ recp = a.rec + start + half;
+  uint64_t rc[U];
+  int i0 = wid * 2 * U;
+  auto load_recs = [&](int i) {
 #pragma unroll
-    for (int p = 0; p < U; ++p) {
-      const int idx = i0 + 2 * p + half;
-      rc[p] = (full || idx < len) ? rec[idx] : 0ull;
+    for (int p = 0; p < U; ++p) rc[p] = recp[i + 2 * p];
+  };
+  if (i0 < len) load_recs(i0);
+  for (; i0 < len; i0 += NW * 2 * U) {
+    if (i0 + 2 * U > len) {  // wave-uniform: the chunk's last trip
+#pragma unroll
+      for (int p = 0; p < U; ++p)
+        if (i0 + 2 * p + half >= len) rc[p] = 0ull;
     }
     uint32_t x[U];
     unsigned long long add[U];
@@ -401,6 +410,7 @@ __global__ __launch_bounds__(512) void seg_hist_lane_kernel(const SegHistArgs a,
       const uint32_t qb = hi >> 7;  // q1 + 2^23
       add[p] = ((unsigned long long)(w << (kPackShift - 32)) << 32) + (unsigned long long)w * qb;
     }
+    if (i0 + NW * 2 * U < len) load_recs(i0 + NW * 2 * U);
 #pragma unroll
     for (int p = 0; p < U; ++p) {
 #pragma unroll

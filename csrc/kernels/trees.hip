@@ -222,6 +222,130 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// binize v4 (d <= 128, d % 4 == 0, 16-byte aligned rows).  v2 spent ~72 VALU
+// lane-ops per value (rocprofv3: VALU-bound with half the wave time waiting on
+// memory): every value went HBM -> registers -> LDS tile -> registers, and each
+// search step carried a bound test.  v4:
+//   * thread task = (row, quad q): one float4 straight from HBM (a row's quads
+//     are 25 consecutive lanes), 4 searches in lockstep, one dword of bins;
+//   * thresholds in LDS padded with +inf to 2^steps entries per feature and a
+//     feature stride of 2^steps + 1 words (the first step's 32 lanes of a row
+//     read 32 different banks), so a step is add / read / compare / select;
+//   * the 32 x 32-dword bins tile goes through 4 KB of LDS once, then leaves as
+//     16-byte row-major stores (128-byte padded rows, padding zeroed) and
+//     256-byte column-major runs of 32 rows per 8-feature group;
+//   * the next tile's float4s are loaded before this tile's searches.
+// ---------------------------------------------------------------------------
+template <int STEPS>
+__global__ __launch_bounds__(256) void binize4_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                      const float* __restrict__ thr, const int* __restrict__ nthr,
+                                                      int tmax, int miss_on, float miss_val,
+                                                      uint64_t* __restrict__ out, uint64_t* __restrict__ rm, int Gs) {
+  extern __shared__ __attribute__((aligned(16))) float smf4[];
+  constexpr int R = 32;  // rows per tile
+  constexpr int P = 1 << STEPS, TS = P + 1;
+  float* sthr = smf4;                                                      // [d][TS]
+  int* snt = reinterpret_cast<int*>(sthr + (size_t)d * TS);                // [d]
+  uint32_t* tile = reinterpret_cast<uint32_t*>(snt + ((d + 3) & ~3));      // [R][32]
+  for (int i = threadIdx.x; i < d * TS; i += 256) {
+    const int f = i / TS, c = i - f * TS;
+    sthr[i] = (c < nthr[f] && c < tmax) ? thr[(size_t)f * tmax + c] : __builtin_inff();
+  }
+  for (int i = threadIdx.x; i < d; i += 256) snt[i] = nthr[i];
+  __syncthreads();
+  const int G = (d + 7) / 8;
+  const int Q = d >> 2;
+  const int q = threadIdx.x & 31, rsub = threadIdx.x >> 5;  // task k: row k * 8 + rsub, quad q
+  const bool qok = q < Q;
+  // per-quad constants: feature table offsets (entry cand - 1 of feature 4q + j), counts
+  int toff[4], nt[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int f = qok ? 4 * q + j : 0;
+    toff[j] = f * TS - 1;
+    nt[j] = snt[f];
+  }
+  const int64_t stride = (int64_t)gridDim.x * R;
+  float4 pre[4];
+  // unconditional float4 loads in float4 units (alignment known): rows past n re-read row n - 1, quads past
+  // Q re-read quad Q - 1 (their bins are masked / their rows not stored)
+  const float4* __restrict__ X4 = reinterpret_cast<const float4*>(X);
+  const int64_t ldx4 = ldx >> 2;
+  const int qc = qok ? q : Q - 1;
+  auto fetch = [&](int64_t r0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int64_t r = r0 + k * 8 + rsub;
+      r = r < n ? r : n - 1;
+      pre[k] = X4[r * ldx4 + qc];
+    }
+  };
+  if ((int64_t)blockIdx.x * R < n) fetch((int64_t)blockIdx.x * R);
+  for (int64_t r0 = (int64_t)blockIdx.x * R; r0 < n; r0 += stride) {
+    float x[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[k][0] = pre[k].x; x[k][1] = pre[k].y; x[k][2] = pre[k].z; x[k][3] = pre[k].w;
+    }
+    if (r0 + stride < n) fetch(r0 + stride);
+    int lo[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // XGBoost missing values (NaN or == missing) -> -inf -> bin 0 (thresholds start at -FLT_MAX)
+        if (miss_on && (x[k][j] != x[k][j] || x[k][j] == miss_val)) x[k][j] = -__builtin_inff();
+        lo[k][j] = 0;
+      }
+#pragma unroll
+    for (int s = STEPS - 1; s >= 0; --s) {
+      const int step = 1 << s;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cand = lo[k][j] + step;
+          lo[k][j] = sthr[toff[j] + cand] < x[k][j] ? cand : lo[k][j];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t b;
+        if (nt[j] < 0) {
+          const int c = (int)x[k][j];
+          b = (uint32_t)(c < 0 ? 0 : (c > 255 ? 255 : c));
+        } else {
+          b = (x[k][j] != x[k][j]) ? (uint32_t)nt[j] : (uint32_t)lo[k][j];
+        }
+        word |= b << (8 * j);
+      }
+      tile[(k * 8 + rsub) * 32 + q] = qok ? word : 0u;
+    }
+    __syncthreads();
+    const int rows = (int)((n - r0) < R ? (n - r0) : R);
+    if (rm) {
+      // row-major: 8 x 16 bytes per 128-byte padded row (Gs == 16)
+      const int row = threadIdx.x >> 3, c4 = threadIdx.x & 7;
+      if (row < rows) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&tile[row * 32 + 4 * c4]);
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(rm + (r0 + row) * Gs) + 4 * c4) = v;
+      }
+    }
+    for (int p = threadIdx.x; p < G * R; p += 256) {
+      const int g = p >> 5, row = p & 31;
+      if (row < rows) {
+        const uint64_t v = (uint64_t)tile[row * 32 + 2 * g] | ((uint64_t)tile[row * 32 + 2 * g + 1] << 32);
+        out[(int64_t)g * n + r0 + row] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // binize v3: LUT-narrowed search.  Per continuous feature the host tabulates,
 // over C uniform cells of [t_0, t_last], how many thresholds lie in earlier
 // cells (`lut[f][c]`, computed with the same f32 cell function as here, which
@@ -791,6 +915,35 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
                          int miss_on, float miss_val, uint64_t* out, uint64_t* rm, int Gs, hipStream_t st) {
   if (rm && Gs < (d + 7) / 8) return (int)hipErrorInvalidValue;
   if (n <= 0) return 0;
+  static const bool v4_on = [] {
+    const char* e = getenv("CDNAML_BINIZE_V4");
+    return !e || atoi(e) != 0;
+  }();
+  if (v4_on && d <= 128 && (d % 4) == 0 && (ldx % 4) == 0 && (reinterpret_cast<uintptr_t>(X) % 16) == 0 &&
+      (!rm || Gs == 16)) {
+    // v4: float4 tasks straight from HBM, padded +inf tables with a bank-skewed stride, 4 KB bins tile
+    int steps = 0;
+    while ((1 << steps) <= tmax) ++steps;
+    if (steps < 4) steps = 4;
+    const size_t lds = (size_t)d * ((1 << steps) + 1) * 4 + (size_t)((d + 3) & ~3) * 4 + 32 * 32 * 4;
+    if (steps <= 8 && lds <= 150 * 1024) {
+      auto launch = [&](auto kern) {
+        if (lds > 64 * 1024)
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds);
+        hipLaunchKernelGGL(kern, dim3(grid_for(n, 32, 2048)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
+                           tmax > 0 ? tmax : 1, miss_on, miss_val, out, rm, Gs);
+      };
+      switch (steps) {
+        case 4: launch(binize4_kernel<4>); break;
+        case 5: launch(binize4_kernel<5>); break;
+        case 6: launch(binize4_kernel<6>); break;
+        case 7: launch(binize4_kernel<7>); break;
+        default: launch(binize4_kernel<8>); break;
+      }
+      return (int)hipGetLastError();
+    }
+  }
   {
     // v2: tile of rows in LDS next to the thresholds (<= 64 KB per block)
     // CDNAML_BINIZE_PAD=1: +inf-padded power-of-two threshold tables (branch-free search steps).  Opt-in:

@@ -2,7 +2,7 @@
 
     python scripts/gaps.py gpurun_out/run/prof8/p_kernel_trace.csv [first_kernel] [last_kernel]
 
-The step is the span from the last launch of ``first_kernel`` (default binize2: the fit's first kernel) to
+The step is the span from the last launch of ``first_kernel`` (default binize: the fit's first kernel) to
 the following launch of ``last_kernel`` (default predict_heap: the transform).  Prints the span, the idle time
 between kernels (the host-bound part), the largest gaps and the per-kernel busy time.
 """
@@ -13,7 +13,7 @@ import sys
 
 def main():
     path = sys.argv[1]
-    first = sys.argv[2] if len(sys.argv) > 2 else "binize2"
+    first = sys.argv[2] if len(sys.argv) > 2 else "binize"
     last = sys.argv[3] if len(sys.argv) > 3 else "predict_heap"
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     s = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]][-1]

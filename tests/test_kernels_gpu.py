@@ -1,4 +1,5 @@
 """Numerics of every native HIP kernel vs its plain-PyTorch CPU reference."""
+import math
 import numpy as np
 import pytest
 import torch
@@ -1024,3 +1025,29 @@ def test_seg_hist_lane_matches_flat(dev, d, B, monkeypatch):
     got = K.seg_hist(bins, d, B, rec, None, None, None, sb, S, 12, sc, bins_rm=rm, rec=True, raw=True)
     assert got.dtype == torch.int64 and int(ref[..., 0].sum()) > 0
     assert torch.equal(got.cpu(), ref.cpu())
+
+
+@pytest.mark.parametrize("d,maxb,n,missing", [(100, 40, 100003, None), (64, 256, 5001, None), (8, 2, 77, None),
+                                              (128, 32, 4099, None), (100, 40, 3001, -999.0),
+                                              (100, 40, 3001, float("nan"))])
+def test_binize_v4_matches_reference(dev, d, maxb, n, missing):
+    """K4 binize v4 (float4 tasks, +inf-padded skewed tables, 32-row bins tile): column-major and padded row-major
+    bins equal the CPU searchsorted reference -- categorical columns, NaN / +-inf, ragged last tile, 4-8 search
+    steps, XGBoost missing values."""
+    g = torch.Generator().manual_seed(d + maxb)
+    X = torch.randn(n, d, generator=g) * 3
+    X[:, 1] = torch.randint(0, 9, (n,), generator=g).float()
+    thr, nthr = _thresholds(X, maxb)
+    nthr[1] = -1
+    X[5, 0] = float("nan")
+    X[7, 2 % d] = float("inf")
+    X[9, 3 % d] = -float("inf")
+    if missing is not None and not math.isnan(missing):
+        X[11:40, 4 % d] = missing
+    ref = K.binize(X, thr, nthr, missing=missing)
+    bins, rm = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), missing=missing, want_rm=True)
+    assert torch.equal(bins.cpu(), ref)
+    G = (d + 7) // 8
+    rmc = rm.cpu()
+    assert rm is not None and torch.equal(rmc[:, :G], K.bins_row_major(ref)) and not rmc[:, G:].any()
+    assert torch.equal(rm, K.bins_row_major(bins))
