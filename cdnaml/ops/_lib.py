@@ -100,9 +100,6 @@ _SIGS = {
     "cdna_hist_classes": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                            c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p], c_int),
-    "cdna_hist2": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                    c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p,
-                    c_void_p], c_int),
     "cdna_hist4": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,
                     c_void_p, c_void_p], c_int),
@@ -119,11 +116,7 @@ _SIGS = {
     "cdna_codes_compact": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p], c_int),
     "cdna_bins_row_major": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p], c_int),
-    "cdna_partition6": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_partition7": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p, c_void_p, c_void_p, c_void_p], c_int),
-    "cdna_partition8": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double,
                          c_double, c_double, c_void_p, c_void_p, c_void_p], c_int),
@@ -158,8 +151,6 @@ _SIGS = {
                         c_void_p], c_int),
     "cdna_tree_predict": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p,
                            c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p], c_int),
-    "cdna_binize_lut": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
-                         c_void_p, c_void_p], c_int),
     "cdna_tree_predict_heap": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                                 c_float, c_void_p, c_void_p], c_int),
     "cdna_predict_binned_add": ([c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p,

@@ -218,50 +218,6 @@ def quantile_thresholds(samp: torch.Tensor, max_bins: int):
 
 
 # --------------------------------------------------------------------- K4
-# binize v3 (LUT-narrowed search).  Opt-in: measured 38.8 ms vs 27.4 ms for the plain lockstep search at
-# 1e8 x 100 x 40 bins -- binize2 is not bound by its threshold reads (rocprofv3: 36 % of its LDS cycles are
-# bank conflicts of the tile stores, half of wave time waits on memory)
-BINIZE_LUT = __import__("os").environ.get("CDNAML_BINIZE_LUT", "0") != "0"
-
-
-def _binize_lut(thr: torch.Tensor, nthr: torch.Tensor):
-    """Cell tables for binize v3: per continuous feature, C uniform f32 cells over [t_0, t_last] and the
-    number of thresholds in earlier cells (the same f32 cell function as the kernel).  Picks the C in
-    (64, 128, 256) with the fewest in-cell search steps (ceil(log2(fullest cell + 1))), the smallest on ties;
-    None when that still needs more than 5 steps (the plain search is then as good)."""
-    T = thr.detach().float().cpu().numpy().reshape(len(nthr), -1) if thr.numel() else np.zeros((len(nthr), 1),
-                                                                                                np.float32)
-    nt = nthr.detach().cpu().numpy().astype(np.int64)
-    d = len(nt)
-    best = None
-    for C in (64, 128, 256):
-        lut = np.zeros((d, C + 1), dtype=np.uint8)
-        lo = np.zeros(d, dtype=np.float32)
-        sc = np.zeros(d, dtype=np.float32)
-        M = 0
-        for f in range(d):
-            k = int(nt[f])
-            if k <= 0:
-                continue
-            t = T[f, :k].astype(np.float32)
-            lo[f] = t[0]
-            span = np.float32(t[-1]) - np.float32(t[0])
-            sc[f] = np.float32(C) / span if span > 0 else np.float32(0.0)
-            with np.errstate(invalid="ignore", over="ignore"):
-                cf = (t - lo[f]) * sc[f]
-            cf = np.minimum(np.maximum(np.nan_to_num(cf, nan=0.0), np.float32(0.0)), np.float32(C - 1))
-            cells = cf.astype(np.int64)
-            lut[f] = np.searchsorted(cells, np.arange(C + 1), side="left")
-            M = max(M, int(np.diff(lut[f].astype(np.int64)).max()))
-        steps = int(M).bit_length()
-        if best is None or steps < best[3]:
-            best = (lut, np.concatenate([lo, sc]), C, steps)
-    if best is None or best[3] > 5:
-        return None
-    dev = thr.device
-    return (torch.from_numpy(best[0]).to(dev), torch.from_numpy(best[1]).to(dev), best[2], best[3])
-
-
 def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Optional[float] = None,
            want_rm: bool = False):
     """Raw features -> uint8 bins in feature-group-major layout [G, n, 8].
@@ -288,15 +244,6 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Opti
         miss_on = missing is not None
         miss_val = float("nan") if (missing is None or math.isnan(missing)) else float(missing)
         if n:
-            lut = _binize_lut(thr, nthr) if (BINIZE_LUT and not miss_on) else None
-            if lut is not None:
-                lut_t, losc_t, C, M = lut
-                rc = _lib.lib().cdna_binize_lut(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax,
-                                                _ptr(lut_t), _ptr(losc_t), C, M, _ptr(out), _stream(X.device))
-                if rc == 0:
-                    return (out, None) if want_rm else out
-                if rc != 1:  # 1 = hipErrorInvalidValue: LDS budget, use the search kernel
-                    _lib.check(rc, "cdna_binize_lut")
             rc = _lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, int(miss_on),
                                         miss_val, _ptr(out), _ptr(rm) if rm is not None else None, Gs,
                                         _stream(X.device))
@@ -402,12 +349,12 @@ def _packed_scale(v: torch.Tensor) -> float:
 
 def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_tree, id_tree, feat_mask, B,
            lds_budget, out):
-    """Launch the LDS histogram kernel: v4 integer (hist4.hip, default) or v2/v3 float (hist2.hip)."""
+    """Launch the LDS integer histogram kernel (hist4.hip)."""
     S = len(slot_tree)
     G, n, _ = bins.shape
     T = node.shape[0]
     Kst = 2 if mode == 0 else C
-    v4 = HIST_VERSION >= 4
+    v4 = True  # the v2 / v3 float-atomic kernels (hist2.hip) were removed in round 2 (measured slower)
     packed = v4 and HIST_PACKED and mode == 0 and v0 is None and HIST_MAP != 5
     if v4:
         kbits = mode | (4 if (mode == 0 and v0 is not None) else 0) | (16 if packed else 0)
@@ -448,12 +395,6 @@ def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_
     vmode = 2 if HIST_VERSION == 3 or HIST_MAP == 3 else (8 if HIST_MAP == 4 and HIST_VERSION >= 4 else 0)
     if HIST_MAP == 5 and v4 and v0 is None and id_span_max >= span:
         vmode = 32  # fast rotated kernel (LDS slot table must hold the whole id span)
-    if not v4:
-        _lib.check(_lib.lib().cdna_hist2(mode | vmode, _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0),
-                                         _ptr(v1), _ptr(label), int(C), _ptr(build_slot), _ptr(fm), mw, S, B, SB,
-                                         _ptr(grp), ng, nchunk, id_span_max, _ptr(out), _stream(bins.device)),
-                   "cdna_hist2")
-        return out
     wmax = 255 if weight is not None else 1
     qs0 = _fixed_scale(v0, n, wmax)
     qs1 = _packed_scale(v1) if packed else _fixed_scale(v1, n, wmax, qmax_bits=30 if vmode == 32 else 62)
@@ -486,7 +427,7 @@ def hist_moments(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optiona
     out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
     if S == 0 or n == 0:
         return out
-    if _native(bins) and id_tree is not None and HIST_VERSION >= 2:
+    if _native(bins) and id_tree is not None and HIST_VERSION >= 4:
         return _hist2(0, bins, d, node, weight, v0, v1, None, 0, build_slot, slot_tree, id_tree, feat_mask, B,
                       lds_budget or HIST_LDS_BUDGET, out)
     if _native(bins):
@@ -548,7 +489,7 @@ def hist_classes(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optiona
     out = torch.zeros((S, d, B, C), dtype=torch.float64, device=bins.device)
     if S == 0 or n == 0:
         return out
-    if _native(bins) and id_tree is not None and HIST_VERSION >= 2:
+    if _native(bins) and id_tree is not None and HIST_VERSION >= 4:
         return _hist2(1, bins, d, node, weight, None, None, label, C, build_slot, slot_tree, id_tree, feat_mask, B,
                       lds_budget or HIST_LDS_BUDGET, out)
     if _native(bins):
@@ -726,16 +667,10 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
     return out
 
 
-# all trees per row chunk over an LDS copy of the chunk's bins (partition6) instead of one tree per grid row.
-# Opt-in: measured 7.8 ms per level at 1e8 x 20 trees at every depth, the same as partition5 (both move
-# 8 GB of row records plus the bins at ~2.4 TB/s), so the bins re-reads were not the bound
-PARTITION6 = __import__("os").environ.get("CDNAML_PARTITION6", "0") != "0"
 # persistent partition (tables staged once per block, coalesced bins words, all trees' codes in flight)
 PARTITION7 = __import__("os").environ.get("CDNAML_PARTITION7", "1") != "0"
 PARTITION7_MIN_T = int(__import__("os").environ.get("CDNAML_PARTITION7_MIN_T", "16"))
-# ... two adjacent rows per lane (even n): half the memory instructions.  Opt-in: measured equal to partition7
-# (5.09 vs 5.00 ms per level at 1e8 x 20 trees; both stream ~18 GB per level: bins once, codes read + write)
-PARTITION8 = __import__("os").environ.get("CDNAML_PARTITION8", "0") != "0"
+
 
 
 def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tensor, tfirst_next: torch.Tensor,
@@ -763,22 +698,10 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
         # partition7 streams every bins word of every row once per level (10 GB at 1e8 x 100): it pays when
         # many trees share that pass; for few trees partition5's per-(row, tree) byte gathers move less (GBDT,
         # T = 1: 57.9 vs 40.6 ms per boosting round with partition7; CV grid with 5 / 10 trees: 2.18 vs 1.34 s)
-        if PARTITION7 and not PARTITION6 and T >= PARTITION7_MIN_T and G <= 16 and A <= 1024 and T <= 64 and \
-                bins_rm is None:
-            if PARTITION8 and n % 2 == 0 and codes.is_contiguous() and bins.data_ptr() % 16 == 0:
-                _lib.check(_lib.lib().cdna_partition8(_ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]),
-                                                      _ptr(args[1]), _ptr(args[2]), _ptr(args[3]), _ptr(args[4]),
-                                                      _ptr(cm), _ptr(args[5]), _stream(bins.device)),
-                           "cdna_partition8")
-                return
+        if PARTITION7 and T >= PARTITION7_MIN_T and G <= 16 and A <= 1024 and T <= 64 and bins_rm is None:
             _lib.check(_lib.lib().cdna_partition7(_ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]),
                                                   _ptr(args[1]), _ptr(args[2]), _ptr(args[3]), _ptr(args[4]),
                                                   _ptr(cm), _ptr(args[5]), _stream(bins.device)), "cdna_partition7")
-            return
-        if PARTITION6 and G <= 32 and A <= 1024 and T <= 64 and bins_rm is None:
-            _lib.check(_lib.lib().cdna_partition6(_ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]),
-                                                  _ptr(args[1]), _ptr(args[2]), _ptr(args[3]), _ptr(args[4]),
-                                                  _ptr(cm), _ptr(args[5]), _stream(bins.device)), "cdna_partition6")
             return
         src, rm_bytes = bins, 0
         if bins_rm is not None:

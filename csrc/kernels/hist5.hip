@@ -810,80 +810,6 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
   }
 }
 
-// Row-record partition, all trees per row chunk (partition6).  partition5 runs
-// one tree per grid.y and re-gathers, for every (row, tree), one byte from the
-// [G][n] bins: with up to 2^depth split features per tree, 20 trees re-read
-// the whole bins matrix from L2/HBM per level (5-10 ms at 1e8 x 100).  Here a
-// block stages its 256-row slice of ALL feature groups in LDS once (26 KB at
-// d = 100) and walks every tree over it: the bins cross HBM once per level,
-// and each tree's split table is staged in LDS per tree.
-constexpr int kP6Rows = 256;
-constexpr int kP6MaxA = 1024;  // active nodes of the level (all trees) staged in LDS
-constexpr int kP6MaxT = 64;
-__global__ __launch_bounds__(256) void partition6_kernel(const uint64_t* __restrict__ bins, int64_t n, int G, int T,
-                                                         int A, uint16_t* __restrict__ codes,
-                                                         const int* __restrict__ tfirst,
-                                                         const int* __restrict__ tfirst_next,
-                                                         const int* __restrict__ split_feat,
-                                                         const int* __restrict__ split_bin,
-                                                         const int* __restrict__ cat_off,
-                                                         const uint32_t* __restrict__ cat_mask,
-                                                         const int* __restrict__ child) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t tile[];  // [G][kP6Rows]
-  __shared__ int s_f[kP6MaxA], s_b[kP6MaxA], s_co[kP6MaxA];
-  __shared__ uint8_t s_ch[2 * kP6MaxA];
-  __shared__ int s_tf[kP6MaxT];
-  const int64_t r0 = (int64_t)blockIdx.x * kP6Rows;
-  const int rows = n - r0 < kP6Rows ? (int)(n - r0) : kP6Rows;
-  for (int i = threadIdx.x; i < G * kP6Rows; i += 256) {
-    const int g = i / kP6Rows, r = i - g * kP6Rows;
-    tile[i] = r < rows ? bins[(int64_t)g * n + r0 + r] : 0ull;
-  }
-  for (int i = threadIdx.x; i < T; i += 256) s_tf[i] = tfirst[i];
-  for (int i = threadIdx.x; i < A; i += 256) {
-    s_f[i] = split_feat[i];
-    s_b[i] = split_bin[i];
-    s_co[i] = cat_off[i];
-    // the tree of active node i: largest t with tfirst[t] <= i (tfirst is non-decreasing)
-    int lo = 0, hi = T - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (tfirst[mid] <= i) lo = mid; else hi = mid - 1;
-    }
-    const int tfn = tfirst_next[lo];
-    const int c0 = child[i * 2], c1 = child[i * 2 + 1];
-    s_ch[2 * i] = (uint8_t)(c0 >= 0 ? c0 - tfn : 0xFF);
-    s_ch[2 * i + 1] = (uint8_t)(c1 >= 0 ? c1 - tfn : 0xFF);
-  }
-  __syncthreads();
-  const uint8_t* tb = reinterpret_cast<const uint8_t*>(tile);
-  const int r = threadIdx.x;
-  if (r >= rows) return;
-  uint16_t* rec = codes + r0 + r;
-  // 8 trees' records in flight per thread, then their moves (one dependent load per tree was latency-bound)
-  constexpr int TB = 8;
-  for (int t0 = 0; t0 < T; t0 += TB) {
-    uint32_t c[TB];
-#pragma unroll
-    for (int u = 0; u < TB; ++u) c[u] = t0 + u < T ? (uint32_t)rec[(int64_t)(t0 + u) * n] : 0xFFu;
-#pragma unroll
-    for (int u = 0; u < TB; ++u) {
-      const uint32_t loc = c[u] & 0xFFu;
-      if (loc == 0xFFu) continue;
-      const int id = s_tf[t0 + u] + (int)loc;
-      const int f = s_f[id];
-      uint32_t nl = 0xFFu;
-      if (f >= 0) {
-        const int bin = tb[((f >> 3) * kP6Rows + r) * 8 + (f & 7)];
-        const int co = s_co[id];
-        const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u : bin <= s_b[id];
-        nl = s_ch[2 * id + (left ? 0 : 1)];
-      }
-      rec[(int64_t)(t0 + u) * n] = (uint16_t)((c[u] & 0xFF00u) | nl);
-    }
-  }
-}
-
 // Row-record partition, persistent (partition7).  partition5 (grid.y = tree)
 // re-gathers one byte per (row, tree) from the [G][n] planes, so 20 trees pull
 // the bins planes through HBM up to 20 times per level (4.7 -> 9.5 ms per level
@@ -899,7 +825,7 @@ constexpr int kP7MaxA = 1024;
 constexpr int kP7MaxT = 64;
 constexpr int kP7MaxG = 16;  // MAXG template: 8 / 13 / 16 words per row (registers sized to the row)
 constexpr int kP7TB = 24;
-template <int MAXG, bool LADDER>
+template <int MAXG>
 __global__ __launch_bounds__(256) void partition7_kernel(const uint64_t* __restrict__ bins, int64_t n, int G, int T,
                                                          int A, uint16_t* __restrict__ codes,
                                                          const int* __restrict__ tfirst,
@@ -937,11 +863,9 @@ __global__ __launch_bounds__(256) void partition7_kernel(const uint64_t* __restr
     uint32_t c[kP7TB];
 #pragma unroll
     for (int u = 0; u < kP7TB; ++u) c[u] = (cc[u] >> (16 * half)) & 0xFFFFu;
-    if (!LADDER) {
 #pragma unroll
-      for (int g = 0; g < MAXG; ++g)
-        if (g < G) tile7[g * 256 + lr] = w[g];
-    }
+    for (int g = 0; g < MAXG; ++g)
+      if (g < G) tile7[g * 256 + lr] = w[g];
     for (int t0 = 0; t0 < T; t0 += kP7TB) {
       if (t0 > 0) {
 #pragma unroll
@@ -956,21 +880,7 @@ __global__ __launch_bounds__(256) void partition7_kernel(const uint64_t* __restr
         const int f = fb & 0xFFFF;
         uint32_t nl = 0xFFu;
         if (f != 0xFFFF) {
-          int bin;
-          if (LADDER) {
-            // LADDER (opt-in CDNAML_PARTITION7_LADDER): the bin byte is selected from the row's registers (no LDS
-            // tile: 7 instead of 4 resident waves per SIMD); measured slower, 26.9 vs 19.9 ms per step at 1e8
-            const int wi = f >> 2;
-            uint32_t word = (uint32_t)w[0];
-#pragma unroll
-            for (int jj = 1; jj < 2 * MAXG; ++jj) {
-              const uint32_t v = (jj & 1) ? (uint32_t)(w[jj >> 1] >> 32) : (uint32_t)w[jj >> 1];
-              word = wi == jj ? v : word;
-            }
-            bin = (int)((word >> ((f & 3) * 8)) & 0xFFu);
-          } else {
-            bin = tb[((f >> 3) * 256 + lr) * 8 + (f & 7)];
-          }
+          const int bin = tb[((f >> 3) * 256 + lr) * 8 + (f & 7)];
           const int co = s_co[id];
           const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u : bin <= (fb >> 16);
           nl = s_ch[2 * id + (left ? 0 : 1)];
@@ -988,99 +898,6 @@ __global__ __launch_bounds__(256) void partition7_kernel(const uint64_t* __restr
 #pragma unroll
     for (int u = 0; u < kP7TB; ++u) cc[u] = u < T ? (uint32_t)codes[(int64_t)u * n + r] : 0xFFu;
     move_row(r, w, cc, 0);
-  }
-}
-
-// partition8: partition7 with two adjacent rows per lane (n even): one 16-byte
-// load per bins group and one 4-byte load / store per tree cover both rows
-// (half the memory instructions of partition7, whose 2-byte code accesses
-// bounded it), and the split bin is picked from the row's registers by a
-// select ladder instead of an LDS tile (tables only in LDS: more resident
-// blocks).
-template <int MAXG>
-__global__ __launch_bounds__(256) void partition8_kernel(const uint64_t* __restrict__ bins, int64_t n, int G, int T,
-                                                         int A, uint16_t* __restrict__ codes,
-                                                         const int* __restrict__ tfirst,
-                                                         const int* __restrict__ tfirst_next,
-                                                         const int* __restrict__ split_feat,
-                                                         const int* __restrict__ split_bin,
-                                                         const int* __restrict__ cat_off,
-                                                         const uint32_t* __restrict__ cat_mask,
-                                                         const int* __restrict__ child) {
-  __shared__ int s_fb[kP7MaxA], s_co[kP7MaxA];  // feature (0xFFFF: leaf) | bin << 16
-  __shared__ uint8_t s_ch[2 * kP7MaxA];
-  __shared__ int s_tf[kP7MaxT];
-  for (int i = threadIdx.x; i < T; i += 256) s_tf[i] = tfirst[i];
-  for (int i = threadIdx.x; i < A; i += 256) {
-    const int f = split_feat[i];
-    s_fb[i] = (f >= 0 ? f : 0xFFFF) | (split_bin[i] << 16);
-    s_co[i] = cat_off[i];
-    int lo = 0, hi = T - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (tfirst[mid] <= i) lo = mid; else hi = mid - 1;
-    }
-    const int tfn = tfirst_next[lo];
-    const int c0 = child[i * 2], c1 = child[i * 2 + 1];
-    s_ch[2 * i] = (uint8_t)(c0 >= 0 ? c0 - tfn : 0xFF);
-    s_ch[2 * i + 1] = (uint8_t)(c1 >= 0 ? c1 - tfn : 0xFF);
-  }
-  __syncthreads();
-  const int64_t np = n >> 1;
-  const uint32_t* codes2 = reinterpret_cast<const uint32_t*>(codes);
-  uint32_t* codes2w = reinterpret_cast<uint32_t*>(codes);
-  const int64_t n2 = n >> 1;  // row pairs per tree plane
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < np; q += (int64_t)gridDim.x * 256) {
-    // words[k][2g + h]: 32-bit half h of group g of row 2q + k
-    uint32_t wd[2][2 * MAXG];
-#pragma unroll
-    for (int g = 0; g < MAXG; ++g) {
-      if (g < G) {
-        const uint4 v = *reinterpret_cast<const uint4*>(bins + (int64_t)g * n + 2 * q);
-        wd[0][2 * g] = v.x;
-        wd[0][2 * g + 1] = v.y;
-        wd[1][2 * g] = v.z;
-        wd[1][2 * g + 1] = v.w;
-      } else {
-        wd[0][2 * g] = wd[0][2 * g + 1] = wd[1][2 * g] = wd[1][2 * g + 1] = 0u;
-      }
-    }
-    for (int t0 = 0; t0 < T; t0 += kP7TB) {
-      uint32_t cc[kP7TB];
-#pragma unroll
-      for (int u = 0; u < kP7TB; ++u) cc[u] = t0 + u < T ? codes2[(int64_t)(t0 + u) * n2 + q] : 0x00FF00FFu;
-#pragma unroll
-      for (int u = 0; u < kP7TB; ++u) {
-        if (t0 + u >= T || (cc[u] & 0x00FF00FFu) == 0x00FF00FFu) continue;  // both rows done in this tree
-        uint32_t o = 0;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const uint32_t c = (cc[u] >> (16 * k)) & 0xFFFFu;
-          const uint32_t loc = c & 0xFFu;
-          uint32_t res = c;
-          if (loc != 0xFFu) {
-            const int id = s_tf[t0 + u] + (int)loc;
-            const int fb = s_fb[id];
-            const int f = fb & 0xFFFF;
-            uint32_t nl = 0xFFu;
-            if (f != 0xFFFF) {
-              const int wi = f >> 2;
-              uint32_t word = wd[k][0];
-#pragma unroll
-              for (int j = 1; j < 2 * MAXG; ++j) word = wi == j ? wd[k][j] : word;
-              const int bin = (int)((word >> ((f & 3) * 8)) & 0xFFu);
-              const int co = s_co[id];
-              const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u
-                                        : bin <= (fb >> 16);
-              nl = s_ch[2 * id + (left ? 0 : 1)];
-            }
-            res = (c & 0xFF00u) | nl;
-          }
-          o |= res << (16 * k);
-        }
-        codes2w[(int64_t)(t0 + u) * n2 + q] = o;
-      }
-    }
   }
 }
 
@@ -1234,21 +1051,6 @@ CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T,
   return (int)hipGetLastError();
 }
 
-// all trees per 256-row chunk with the chunk's bins in LDS (G * 2 KB; G <= 32, A <= 1024, T <= 64)
-CDNA_API int cdna_partition6(const uint64_t* bins, int64_t n, int G, int T, int A, uint16_t* codes,
-                             const int* tfirst, const int* tfirst_next, const int* split_feat, const int* split_bin,
-                             const int* cat_off, const uint32_t* cat_mask, const int* child, hipStream_t st) {
-  if (n <= 0 || T <= 0) return 0;
-  if (G <= 0 || G > 32 || A > kP6MaxA || T > kP6MaxT) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)G * kP6Rows * 8;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(partition6_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(partition6_kernel, dim3((unsigned)((n + kP6Rows - 1) / kP6Rows)), dim3(256), lds, st, bins, n,
-                     G, T, A, codes, tfirst, tfirst_next, split_feat, split_bin, cat_off, cat_mask, child);
-  return (int)hipGetLastError();
-}
-
 CDNA_API int cdna_partition7(const uint64_t* bins, int64_t n, int G, int T, int A, uint16_t* codes,
                              const int* tfirst, const int* tfirst_next, const int* split_feat, const int* split_bin,
                              const int* cat_off, const uint32_t* cat_mask, const int* child, hipStream_t st) {
@@ -1266,42 +1068,9 @@ CDNA_API int cdna_partition7(const uint64_t* bins, int64_t n, int G, int T, int 
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, bins, n, G, T, A, codes, tfirst, tfirst_next, split_feat,
                        split_bin, cat_off, cat_mask, child);
   };
-  static const bool ladder = [] {
-    const char* e = getenv("CDNAML_PARTITION7_LADDER");
-    return e && atoi(e) != 0;
-  }();
-  if (ladder) {
-    const size_t lds0 = lds;
-    lds = 0;
-    if (G <= 8) launch(partition7_kernel<8, true>);
-    else if (G <= 13) launch(partition7_kernel<13, true>);
-    else launch(partition7_kernel<16, true>);
-    lds = lds0;
-  } else if (G <= 8) launch(partition7_kernel<8, false>);
-  else if (G <= 13) launch(partition7_kernel<13, false>);
-  else launch(partition7_kernel<16, false>);
-  return (int)hipGetLastError();
-}
-
-CDNA_API int cdna_partition8(const uint64_t* bins, int64_t n, int G, int T, int A, uint16_t* codes,
-                             const int* tfirst, const int* tfirst_next, const int* split_feat, const int* split_bin,
-                             const int* cat_off, const uint32_t* cat_mask, const int* child, hipStream_t st) {
-  if (n <= 0 || T <= 0) return 0;
-  if ((n & 1) || G <= 0 || G > kP7MaxG || A > kP7MaxA || T > kP7MaxT) return (int)hipErrorInvalidValue;
-  if ((reinterpret_cast<uintptr_t>(bins) & 15) || (reinterpret_cast<uintptr_t>(codes) & 3))
-    return (int)hipErrorInvalidValue;
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  auto launch = [&](auto kern) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 2;
-    const dim3 grid(grid_for(n / 2, 256, (unsigned)(per_cu * ncu)));
-    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, bins, n, G, T, A, codes, tfirst, tfirst_next, split_feat,
-                       split_bin, cat_off, cat_mask, child);
-  };
-  if (G <= 8) launch(partition8_kernel<8>);
-  else if (G <= 13) launch(partition8_kernel<13>);
-  else launch(partition8_kernel<16>);
+  if (G <= 8) launch(partition7_kernel<8>);
+  else if (G <= 13) launch(partition7_kernel<13>);
+  else launch(partition7_kernel<16>);
   return (int)hipGetLastError();
 }
 

@@ -253,7 +253,7 @@ __global__ __launch_bounds__(1024) void seg_hist_rm_kernel(const SegHistArgs a, 
 // ds_add wave instruction).  A lane's 8 cells are updated in a rotated order;
 // the partial last group (d % 8 != 0) masks its missing features per j, so the
 // wave issues exactly 8 atomic instructions per pair round.
-template <bool HAS_W, bool REC = false, int NC = 1>
+template <bool HAS_W, bool REC = false>
 __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a, const uint64_t* __restrict__ bins_rm,
                                                              int G, int ngb) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long h[];
@@ -264,11 +264,8 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
   const int ng = G - g0 < ngb ? G - g0 : ngb;
   const int plane_g = 8 * a.B;
   const int plane = ng * plane_g;
-  // NC > 1: NC interleaved copies of every cell (cell k, copy c at k * NC + c), lane l adding into copy
-  // l % NC, which splits a 16-lane atomic group's random bins over NC disjoint bank-pair sets
-  for (int i = threadIdx.x; i < plane * NC; i += TH) h[i] = 0ull;
+  for (int i = threadIdx.x; i < plane; i += TH) h[i] = 0ull;
   const int rot = threadIdx.x & 7;
-  const int copy = NC > 1 ? (int)(threadIdx.x % NC) : 0;
   __syncthreads();
   const uint32_t total = (uint32_t)len * (uint32_t)ng;
   const uint32_t Gu = (uint32_t)ng;
@@ -321,7 +318,7 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
       for (int j = 0; j < 8; ++j) {
         const int jj = (j + rot) & 7;
         const int cell = gbase + jj * a.B + (int)__builtin_amdgcn_ubfe(jj >= 4 ? hi : lo, (uint32_t)((jj & 3) * 8), 8u);
-        if ((frot >> j) & 1u) atomicAdd(h + cell * NC + copy, add);
+        if ((frot >> j) & 1u) atomicAdd(h + cell, add);
       }
     }
   }
@@ -331,15 +328,9 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
     const int jj = rem / a.B, bn = rem - jj * a.B;
     const int f = (g0 + gq) * 8 + jj;
     if (f >= a.d) continue;
-    unsigned long long cnt = 0;
-    long long sum = 0;
-#pragma unroll
-    for (int q = 0; q < NC; ++q) {
-      const unsigned long long v = h[c * NC + q];
-      const unsigned long long ck = v >> kPackShift;
-      cnt += ck;
-      sum += (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)ck;
-    }
+    const unsigned long long v = h[c];
+    const unsigned long long cnt = v >> kPackShift;
+    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
     if (!cnt) continue;
     unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
     atomicAdd(o, cnt);
@@ -496,80 +487,6 @@ __global__ __launch_bounds__(1024) void seg_hist_subset_kernel(const SegHistArgs
     unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
     const unsigned long long cnt = v >> kPackShift;
     const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
-    atomicAdd(o, cnt);
-    atomicAdd(o + 1, (unsigned long long)sum);
-  }
-}
-
-// Bank-private variant (packed item records, B <= 64): a block owns ONE
-// 8-feature group of one work chunk and keeps 16 copies of its 8 x B plane,
-// interleaved so copy c of cell k sits at u64 index k * 16 + c: lane l adds
-// into copy (l & 15), so the 16 lanes of a ds_add_u64 lane group always hit 16
-// different bank pairs whatever their bins.  rocprofv3 on the flat kernel:
-// 67 % of its LDS cycles were bank conflicts (random bins, ~3 lanes on the
-// busiest bank pair of a group).  Copies are unpacked and summed at the flush;
-// each copy sees 1/16 of the rows, so the packed count field has 16x headroom.
-// Blocks are numbered group-fastest so the G blocks of a chunk run together
-// and share the chunk's records and rows through L2.
-template <int NCOPY>
-__global__ __launch_bounds__(256) void seg_hist_priv_kernel(const SegHistArgs a, const uint64_t* __restrict__ bins_rm,
-                                                            int G) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long h[];  // [8 * B][NCOPY]
-  constexpr int TH = 256;
-  const int g = blockIdx.x % G, wi = blockIdx.x / G;
-  const int start = a.work[3 * wi], len = a.work[3 * wi + 1], slot = a.work[3 * wi + 2];
-  const int cells = 8 * a.B;
-  for (int i = threadIdx.x; i < cells * NCOPY; i += TH) h[i] = 0ull;
-  const int copy = threadIdx.x & (NCOPY - 1);
-  const int rot = (threadIdx.x >> 4) & 7;  // lane groups of 16 start on different features
-  const int valid_f = a.d - g * 8;
-  const uint32_t fvalid = valid_f >= 8 ? 0xFFu : ((1u << (valid_f > 0 ? valid_f : 0)) - 1u);
-  __syncthreads();
-  constexpr int U = 4;
-  for (int i0 = threadIdx.x; i0 < len; i0 += TH * U) {
-    uint64_t b8[U];
-    uint32_t w[U], qb[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * TH;
-      const bool ok = i < len;
-      const uint64_t rc = ok ? a.rec[start + i] : 0ull;
-      const int row = (int)(rc & 0x7FFFFFFFull);
-      b8[u] = ok ? bins_rm[(int64_t)row * (a.rs ? a.rs : G) + g] : 0ull;
-      w[u] = (uint32_t)(rc >> 31) & 0xFFu;
-      qb[u] = (uint32_t)(rc >> 39);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t fm = w[u] ? fvalid : 0u;
-      const uint32_t frot = ((fm >> rot) | (fm << (8 - rot))) & 0xFFu;
-      const uint32_t lo = (uint32_t)b8[u], hi = (uint32_t)(b8[u] >> 32);
-      const unsigned long long add =
-          ((unsigned long long)w[u] << kPackShift) + (unsigned long long)w[u] * (unsigned long long)qb[u];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int jj = (j + rot) & 7;
-        const int cell = jj * a.B + (int)__builtin_amdgcn_ubfe(jj >= 4 ? hi : lo, (uint32_t)((jj & 3) * 8), 8u);
-        if ((frot >> j) & 1u) atomicAdd(h + cell * NCOPY + copy, add);
-      }
-    }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < cells; c += TH) {
-    const int jj = c / a.B, bn = c - jj * a.B;
-    const int f = g * 8 + jj;
-    if (f >= a.d) continue;
-    unsigned long long cnt = 0;
-    long long sum = 0;
-#pragma unroll
-    for (int k = 0; k < NCOPY; ++k) {
-      const unsigned long long v = h[c * NCOPY + ((k + c) & (NCOPY - 1))];
-      const unsigned long long ck = v >> kPackShift;
-      cnt += ck;
-      sum += (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)ck;
-    }
-    if (!cnt) continue;
-    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
     atomicAdd(o, cnt);
     atomicAdd(o + 1, (unsigned long long)sum);
   }
@@ -1013,7 +930,7 @@ __global__ __launch_bounds__(256) void bins_row_major_kernel(const uint64_t* __r
 
 // mode bit0: packed (no v0; count | sum in one atomic); bit1: per-row weights wp present;
 // bit4: `perm` holds packed 8-byte item records (row | w << 31 | (q1 + 2^23) << 39; flat kernel only).
-// bit5 (with bit4, B <= 64): bank-private planes (seg_hist_priv_kernel); work chunks may be 16x longer.
+// bit7 (with bit4 and bit2, B <= 80): lane-feature kernel (seg_hist_lane_kernel).
 // bit2: bins are row-major [n][G] words (seg_hist_flat_kernel when packed and all groups fit 128 KB of LDS,
 // else seg_hist_rm_kernel); bit3: force seg_hist_rm_kernel.
 // work: [nwork][3] {start, len, slot}; grid = nwork x ceil(d / 8).
@@ -1040,15 +957,6 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
     else launch(seg_hist_lane_kernel<80>);
     return (int)hipGetLastError();
   }
-  if ((mode & 16) && (mode & 32) && (mode & 4) && packed && B <= 64) {
-    // bank-private planes: one 8-feature group per block, 16 interleaved copies
-    const int G = (d + 7) / 8;
-    a.rec = reinterpret_cast<const uint64_t*>(perm);
-    const size_t lds = (size_t)8 * B * 16 * 8;
-    hipLaunchKernelGGL(seg_hist_priv_kernel<16>, dim3((unsigned)((int64_t)nwork * G)), dim3(256), lds, st, a, bins,
-                       G);
-    return (int)hipGetLastError();
-  }
   if ((mode & 16) && !((mode & 4) && packed && (size_t)8 * B * 8 <= 128 * 1024 && !(mode & 8)))
     return (int)hipErrorInvalidValue;
   if ((mode & 4) && packed && (size_t)8 * B * 8 <= 128 * 1024 && !(mode & 8)) {
@@ -1065,14 +973,7 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
                                   (int)lds);
       hipLaunchKernelGGL(kern, dim3((unsigned)nwork, (unsigned)nblk_g), dim3(1024), lds, st, a, bins, G, ngb);
     };
-    if ((mode & 16) && (mode & 64) && (size_t)ngb * 8 * B * 8 * 4 <= 160 * 1024) {  // 4 bank-split copies
-      a.rec = reinterpret_cast<const uint64_t*>(perm);
-      const size_t lds4 = (size_t)ngb * 8 * B * 8 * 4;
-      auto k4 = seg_hist_flat_kernel<true, true, 4>;
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k4), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds4);
-      hipLaunchKernelGGL(k4, dim3((unsigned)nwork, (unsigned)nblk_g), dim3(1024), lds4, st, a, bins, G, ngb);
-    } else if (mode & 16) {  // perm holds packed item records
+    if (mode & 16) {  // perm holds packed item records
       a.rec = reinterpret_cast<const uint64_t*>(perm);
       launch(seg_hist_flat_kernel<true, true>);
     } else if (has_w) {

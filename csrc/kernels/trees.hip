@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
                                                       const float* __restrict__ thr, const int* __restrict__ nthr,
                                                       int tmax, int rows_per_tile, int steps, int miss_on,
                                                       float miss_val, uint64_t* __restrict__ out,
-                                                      uint64_t* __restrict__ rm, int Gs, int tpad) {
+                                                      uint64_t* __restrict__ rm, int Gs) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int G = (d + 7) / 8;
   // [rows_per_tile][dp]: an odd row stride keeps the per-task x reads (lanes = rows) conflict-free; with
@@ -97,18 +97,9 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
   const int dp = d | 1;
   float* sx = smf;                                  // [rows_per_tile][dp]
   float* sthr = smf + (size_t)rows_per_tile * dp;   // [d][tmax]
-  int* snt = reinterpret_cast<int*>(sthr + (size_t)d * (tpad > 0 ? tpad : tmax));
-  // tpad > 0: each feature's table padded with +inf to tpad = 2^steps entries, so the search reads
-  // sthr[f * tpad + cand - 1] unconditionally (no per-step bound test / select)
-  const int tst = tpad > 0 ? tpad : tmax;
-  if (tpad > 0) {
-    for (int i = threadIdx.x; i < d * tpad; i += 256) {
-      const int f = i / tpad, c = i - f * tpad;
-      sthr[i] = c < nthr[f] ? thr[f * tmax + c] : __builtin_inff();
-    }
-  } else {
-    for (int i = threadIdx.x; i < d * tmax; i += 256) sthr[i] = thr[i];
-  }
+  int* snt = reinterpret_cast<int*>(sthr + (size_t)d * tmax);
+  const int tst = tmax;
+  for (int i = threadIdx.x; i < d * tmax; i += 256) sthr[i] = thr[i];
   for (int i = threadIdx.x; i < d; i += 256) snt[i] = nthr[i];
   const bool contiguous = ldx == d && (d % 4) == 0;
   // register double buffer: the next tile's float4s are in flight while the
@@ -191,7 +182,7 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int cand = lo[j] + step;
-          const float tv = tpad > 0 ? sthr[toff[j] + cand] : (cand <= nt[j] ? sthr[toff[j] + cand] : __builtin_inff());
+          const float tv = cand <= nt[j] ? sthr[toff[j] + cand] : __builtin_inff();
           lo[j] = tv < x[j] ? cand : lo[j];
         }
       }
@@ -342,118 +333,6 @@ __global__ __launch_bounds__(256) void binize4_kernel(const float* __restrict__ 
       }
     }
     __syncthreads();
-  }
-}
-
-// ---------------------------------------------------------------------------
-// binize v3: LUT-narrowed search.  Per continuous feature the host tabulates,
-// over C uniform cells of [t_0, t_last], how many thresholds lie in earlier
-// cells (`lut[f][c]`, computed with the same f32 cell function as here, which
-// is monotone in x, so #{t < x} = lut[cell(x)] + #{t in cell(x) : t < x}).
-// A value then costs 2 LUT bytes + a lower-bound search of M = ceil(log2(fullest
-// cell + 1)) steps over that cell only, instead of a ceil(log2 B)-step search
-// over all thresholds: at 40 quantile bins of continuous data M = 2 (6 before).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void binize3_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
-                                                      const float* __restrict__ thr, const int* __restrict__ nthr,
-                                                      int tmax, const uint8_t* __restrict__ lut,
-                                                      const float* __restrict__ lo_sc, int C, int M,
-                                                      int rows_per_tile, uint64_t* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float smf[];
-  const int G = (d + 7) / 8;
-  const int dp = d | 1;
-  float* sx = smf;                                  // [rows_per_tile][dp]
-  float* sthr = smf + (size_t)rows_per_tile * dp;   // [d][tmax]
-  float* slo = sthr + (size_t)d * tmax;             // [d] lower edge, [d] cell scale
-  float* ssc = slo + d;
-  int* snt = reinterpret_cast<int*>(ssc + d);
-  uint8_t* slut = reinterpret_cast<uint8_t*>(snt + d);  // [d][C + 1]
-  for (int i = threadIdx.x; i < d * tmax; i += 256) sthr[i] = thr[i];
-  for (int i = threadIdx.x; i < d; i += 256) {
-    snt[i] = nthr[i];
-    slo[i] = lo_sc[i];
-    ssc[i] = lo_sc[d + i];
-  }
-  for (int i = threadIdx.x; i < d * (C + 1); i += 256) slut[i] = lut[i];
-  const float cmax = (float)(C - 1);
-  const bool contiguous = ldx == d && (d % 4) == 0;
-  constexpr int kPre = 8;
-  float4 pre[kPre];
-  const int64_t stride = (int64_t)gridDim.x * rows_per_tile;
-  auto fetch = [&](int64_t r0) {
-    if (!contiguous || r0 >= n) return;
-    const int rows = (int)((n - r0) < rows_per_tile ? (n - r0) : rows_per_tile);
-    const float4* src = reinterpret_cast<const float4*>(X + r0 * ldx);
-    const int nv = rows * d / 4;
-#pragma unroll
-    for (int k = 0; k < kPre; ++k) {
-      const int i = threadIdx.x + k * 256;
-      if (i < nv) pre[k] = src[i];
-    }
-  };
-  const bool use_pre = contiguous && rows_per_tile * d / 4 <= kPre * 256;
-  if (use_pre) fetch((int64_t)blockIdx.x * rows_per_tile);
-  for (int64_t r0 = (int64_t)blockIdx.x * rows_per_tile; r0 < n; r0 += stride) {
-    const int rows = (int)((n - r0) < rows_per_tile ? (n - r0) : rows_per_tile);
-    __syncthreads();
-    if (use_pre) {
-      const int nv = rows * d / 4;
-#pragma unroll
-      for (int k = 0; k < kPre; ++k) {
-        const int i = threadIdx.x + k * 256;
-        if (i < nv) {
-          const int e = i * 4, r = e / d, f = e - r * d;
-          float* dst = sx + r * dp + f;
-          dst[0] = pre[k].x;
-          dst[1] = pre[k].y;
-          dst[2] = pre[k].z;
-          dst[3] = pre[k].w;
-        }
-      }
-    } else {
-      for (int i = threadIdx.x; i < rows * d; i += 256) {
-        const int r = i / d, f = i - r * d;
-        sx[r * dp + f] = X[(r0 + r) * ldx + f];
-      }
-    }
-    __syncthreads();
-    if (use_pre) fetch(r0 + stride);
-    for (int task = threadIdx.x; task < rows * G; task += 256) {
-      const int g = task / rows, r = task - g * rows;
-      uint64_t word = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int f = g * 8 + j;
-        if (f >= d) break;
-        const float x = sx[r * dp + f];
-        const int nt = snt[f];
-        uint32_t b;
-        if (nt < 0) {
-          const int c = (int)x;
-          b = (uint32_t)(c < 0 ? 0 : (c > 255 ? 255 : c));
-        } else if (x != x) {
-          b = (uint32_t)nt;
-        } else {
-          float cf = __fmul_rn(__fsub_rn(x, slo[f]), ssc[f]);
-          cf = fminf(fmaxf(cf, 0.f), cmax);
-          const int c = (int)cf;
-          const uint8_t* lf = slut + f * (C + 1);
-          // lower bound inside the cell's threshold range [lf[c], lf[c+1]): M = ceil(log2(fullest cell + 1))
-          // fixed steps (1-2 at quantile bins of continuous data)
-          int base = lf[c], len = (int)lf[c + 1] - base;
-          const float* tf = sthr + f * tmax;
-          for (int k = 0; k < M; ++k) {
-            const int half = len >> 1;
-            const bool go = len > 0 && tf[base + half] < x;
-            base = go ? base + half + 1 : base;
-            len = go ? len - half - 1 : half;
-          }
-          b = (uint32_t)base;
-        }
-        word |= (uint64_t)b << (8 * j);
-      }
-      out[(int64_t)g * n + r0 + r] = word;
-    }
   }
 }
 
@@ -946,16 +825,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
   }
   {
     // v2: tile of rows in LDS next to the thresholds (<= 64 KB per block)
-    // CDNAML_BINIZE_PAD=1: +inf-padded power-of-two threshold tables (branch-free search steps).  Opt-in:
-    // measured equal (28.5 ms either way at 1e8 x 100 x 40 bins), so the per-step bound test is not the limit
-    static const bool pad_on = [] {
-      const char* e = getenv("CDNAML_BINIZE_PAD");
-      return e && atoi(e) != 0;
-    }();
-    int steps0 = 0;
-    while ((1 << steps0) <= tmax) ++steps0;
-    const int tpad = (pad_on && tmax > 0) ? (1 << steps0) : 0;
-    const size_t tb = (size_t)d * (tpad > 0 ? tpad : (tmax > 0 ? tmax : 1)) * 4 + (size_t)d * 4;
+    const size_t tb = (size_t)d * (tmax > 0 ? tmax : 1) * 4 + (size_t)d * 4;
     const size_t dp = (size_t)(d | 1);
     // up to 64 KB per block (2+ blocks per CU); large threshold tables (maxBins 256 at d = 100: 100 KB)
     // opt in to 150 KB rather than falling back to v1 (253 ms at 1e8 x 100 x 256 bins)
@@ -977,7 +847,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(binize2_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(binize2_kernel, dim3(grid_for(n, rpt, 8192)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
-                         tmax > 0 ? tmax : 1, rpt, steps, miss_on, miss_val, out, rm, Gs, tpad);
+                         tmax > 0 ? tmax : 1, rpt, steps, miss_on, miss_val, out, rm, Gs);
       return (int)hipGetLastError();
     }
   }
@@ -1076,18 +946,3 @@ CDNA_API int cdna_tree_predict_heap(const float* X, int64_t n, int d, int64_t ld
 
 // binize v3 (LUT-narrowed search): lut [d][C+1] uint8, lo_sc [2][d] (cell lower edge, cell scale);
 // M = search steps inside a cell = ceil(log2(largest threshold count of any cell + 1)) (<= 8).  Returns hipErrorInvalidValue when LDS does not fit.
-CDNA_API int cdna_binize_lut(const float* X, int64_t n, int d, int64_t ldx, const float* thr, const int* nthr,
-                             int tmax, const uint8_t* lut, const float* lo_sc, int C, int M, uint64_t* out,
-                             hipStream_t st) {
-  if (n <= 0) return 0;
-  if (M < 0 || M > 8 || C < 2 || C > 1024) return (int)hipErrorInvalidValue;
-  const size_t dp = (size_t)(d | 1);
-  const size_t tb = (size_t)d * (tmax > 0 ? tmax : 1) * 4 + (size_t)d * 12 + (((size_t)d * (C + 1) + 15) & ~15);
-  int rpt = 64;
-  while (rpt > 4 && ((size_t)rpt * dp * 4 + tb > 64 * 1024 || (size_t)rpt * d > 8192)) rpt /= 2;
-  const size_t lds = (size_t)rpt * dp * 4 + tb;
-  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(binize3_kernel, dim3(grid_for(n, rpt, 8192)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
-                     tmax > 0 ? tmax : 1, lut, lo_sc, C, M, rpt, out);
-  return (int)hipGetLastError();
-}

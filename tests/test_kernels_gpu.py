@@ -147,15 +147,15 @@ def _tree_state(n, T, A, seed):
 
 
 def _set_hist_version(monkeypatch, ver):
-    """ver: 1..4 kernel generation; 43 / 44 = v4 integer kernel with the v3 / rotated lane mapping;
-    45 = packed single-atomic regression kernel; 46 = fast rotated kernel (hist4f)."""
-    monkeypatch.setattr(K, "HIST_VERSION", 4 if ver in (43, 44, 45, 46) else max(ver, 2))
+    """ver: 1 = node-id kernel (trees.hip), 4 = v4 integer kernel; 43 / 44 = v4 with the v3 / rotated lane
+    mapping; 45 = packed single-atomic regression kernel; 46 = fast rotated kernel (hist4f)."""
+    monkeypatch.setattr(K, "HIST_VERSION", 4 if ver in (4, 43, 44, 45, 46) else 1)
     monkeypatch.setattr(K, "HIST_MAP", {43: 3, 44: 4, 45: 4, 46: 5}.get(ver, 2))
     monkeypatch.setattr(K, "HIST_PACKED", ver == 45)
 
 
 @pytest.mark.parametrize("B", [40, 256])
-@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43, 44, 45, 46])
+@pytest.mark.parametrize("ver", [1, 4, 43, 44, 45, 46])
 def test_hist_moments(dev, B, ver, monkeypatch):
     n, d, T, A = 20000, 19, 3, 12
     g = torch.Generator().manual_seed(B)
@@ -176,7 +176,7 @@ def test_hist_moments(dev, B, ver, monkeypatch):
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("ver", [1, 2, 3, 4, 43, 44, 46])
+@pytest.mark.parametrize("ver", [1, 4, 43, 44, 46])
 def test_hist_classes(dev, ver, monkeypatch):
     n, d, T, A, C, B = 10000, 10, 2, 8, 3, 32
     g = torch.Generator().manual_seed(11)
@@ -194,7 +194,7 @@ def test_hist_classes(dev, ver, monkeypatch):
     assert torch.allclose(out, ref)
 
 
-@pytest.mark.parametrize("ver", [2, 4, 44])
+@pytest.mark.parametrize("ver", [1, 4, 44])
 def test_hist_moments_v0(dev, ver, monkeypatch):
     """Moments with a real-valued v0 plane (XGBoost hessians) and no bootstrap weights."""
     n, d, T, A, B = 30000, 13, 2, 6, 64
@@ -386,13 +386,10 @@ def test_hist_codes(dev, kind, monkeypatch):
     assert torch.allclose(out, ref, rtol=1e-6, atol=1e-3)
 
 
-@pytest.mark.parametrize("variant,n,T,d", [("p6", 20000, 6, 12), ("p5", 20000, 6, 12), ("p6", 20001, 6, 12),
-                                           ("p7", 20001, 6, 12), ("p7", 70001, 30, 100), ("p8", 70000, 30, 100),
-                                           ("p8", 20000, 6, 12), ("p8", 4000, 3, 130)])
+@pytest.mark.parametrize("variant,n,T,d", [("p5", 20000, 6, 12), ("p5", 4000, 3, 130), ("p7", 20001, 6, 12),
+                                           ("p7", 70001, 30, 100), ("p7", 20000, 6, 12)])
 def test_partition_codes(dev, monkeypatch, variant, n, T, d):
-    monkeypatch.setattr(K, "PARTITION6", variant == "p6")
-    monkeypatch.setattr(K, "PARTITION7", variant in ("p7", "p8"))
-    monkeypatch.setattr(K, "PARTITION8", variant == "p8")
+    monkeypatch.setattr(K, "PARTITION7", variant == "p7")
     monkeypatch.setattr(K, "PARTITION7_MIN_T", 1)
     per = 4
     g = torch.Generator().manual_seed(5)
@@ -727,26 +724,6 @@ def test_compact_records_histogram(dev):
     gb = K.seg_hist(bins, d, B, p2, v0p, v1p2, wp2, sb, S, 5, sc2, bins_rm=rm, raw=True).cpu()
     cb = K.seg_hist(bins_c, d, B, p2c, v0pc, v1p2c, wp2c, sb, S, 5, sc2, raw=True)
     assert torch.equal(gb, cb)
-
-
-def test_binize_lut_matches_reference(dev, monkeypatch):
-    """binize v3 (LUT-narrowed search) == torch.searchsorted reference, incl. +-inf, NaN, ties at thresholds."""
-    from cdnaml.models.tree.engine import find_thresholds
-    g = torch.Generator().manual_seed(4)
-    n, d = 50000, 24
-    X = torch.randn(n, d, generator=g, dtype=torch.float64) * 3
-    X[:, 5] = torch.round(X[:, 5])
-    X[:, 6] = X[:, 6] ** 3
-    X[7, 1], X[8, 1], X[9, 2] = float("inf"), float("-inf"), float("nan")
-    thr, nthr = find_thresholds(X[:5000].numpy(), d, 40, {})
-    X[:100, 0] = torch.from_numpy(thr[0, :100 if thr.shape[1] > 100 else thr.shape[1]]).repeat(3)[:100]
-    thr_t = torch.from_numpy(thr.astype(np.float32))
-    nthr_t = torch.from_numpy(nthr)
-    monkeypatch.setattr(K, "BINIZE_LUT", True)
-    assert K._binize_lut(thr_t, nthr_t) is not None
-    ref = K.binize(X.float(), thr_t, nthr_t)
-    out = K.binize(X.float().to(dev), thr_t.to(dev), nthr_t.to(dev)).cpu()
-    assert torch.equal(out, ref)
 
 
 def test_native_split_scan_matches_torch(dev, monkeypatch):
