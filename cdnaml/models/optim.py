@@ -98,6 +98,9 @@ def minimize(fg: Callable[[np.ndarray], Tuple[float, np.ndarray]], x0: np.ndarra
         rel = abs(f - fn) / max(abs(fn), abs(f), 1e-12)
         x, f, g = xn, fn, gn
         hist.append(f)
-        if rel < tol:
+        # the first step is a scaled steepest-descent probe (1 / |g|): a tiny relative change there says
+        # nothing about convergence (it stopped LR on unscaled one-hot + count features after one step with
+        # ~1e-7 coefficients), so the relative-change test only applies once curvature pairs exist
+        if rel < tol and it > 1 and len(S) > 0:
             break
     return x, hist, it

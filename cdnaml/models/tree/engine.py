@@ -311,6 +311,8 @@ class Forest:
     def add_many(self, values: np.ndarray, weights: np.ndarray, depth: int, impurity: np.ndarray) -> np.ndarray:
         """Append N leaf nodes at once (values [N, k]); returns their ids."""
         i0, N = len(self.feat), len(weights)
+        if N == 0:  # a level whose splits all failed produces no children
+            return np.zeros(0, dtype=np.int64)
         values = np.asarray(values, dtype=np.float64).reshape(N, -1)
         self.feat.extend([-1] * N)
         self.thr.extend([0.0] * N)

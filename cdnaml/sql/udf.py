@@ -56,6 +56,10 @@ class UserDefinedFunction:
         return column_from_numpy(arr, rt, device)
 
     def _run(self, b, ctx, args):
+        if b.n == 0:
+            # Spark never hands a UDF an empty batch (schema inference here runs plans on 0 rows): models such
+            # as sklearn estimators raise on 0 samples
+            return column_from_numpy(np.array([], dtype=object), self.returnType, b.device)
         session = ctx.session
         bs = _max_records(session) if session is not None else 10000
         if self.evalType == "row":
@@ -63,7 +67,7 @@ class UserDefinedFunction:
             out = [self.func(*vals) for vals in zip(*hosts)] if hosts else [self.func() for _ in range(b.n)]
             return column_from_numpy(np.array(out, dtype=object), self.returnType, b.device)
         series = [pd.Series(a.to_numpy()) for a in args]
-        chunks = [(s0, min(b.n, s0 + bs)) for s0 in range(0, b.n, bs)] or [(0, 0)]
+        chunks = [(s0, min(b.n, s0 + bs)) for s0 in range(0, b.n, bs)]
         if self.evalType == "scalar":
             outs = [self.func(*[s.iloc[a:z].reset_index(drop=True) for s in series]) for a, z in chunks]
         elif self.evalType == "scalar_iter":

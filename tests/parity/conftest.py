@@ -1,0 +1,28 @@
+"""Notebook-parity suite: one flow per reference notebook, written with the
+reference's own imports (pyspark / mlflow / hyperopt / delta / koalas / databricks.*) through
+``cdnaml.compat.install()``, on the synthetic course datasets (``cdnaml.utils.datasets``), asserting
+the invariants each notebook states or implies."""
+import os
+
+import pytest
+
+
+@pytest.fixture(scope="module")
+def nb(tmp_path_factory):
+    """(spark, datasets_root, workdir) with the compat aliases installed for the module."""
+    import cdnaml
+    import cdnaml.compat as compat
+    from cdnaml.utils import datasets as D
+
+    root = tmp_path_factory.mktemp("parity")
+    os.environ["CDNAML_DBFS_ROOT"] = str(root / "dbfs")
+    os.environ["CDNAML_TRACKING_URI"] = str(root / "mlruns")
+    spark = cdnaml.SparkSession.builder.config("cdnaml.warehouse.dir", str(root / "warehouse")).getOrCreate()
+    installed = compat.install()
+    ds = D.install_datasets(str(root / "datasets"), spark, scale=0.03)
+    try:
+        yield spark, ds, str(root / "work")
+    finally:
+        compat.uninstall()
+        spark.stop()
+        del installed
