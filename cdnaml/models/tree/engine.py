@@ -58,6 +58,8 @@ PARTITION_RM = __import__("os").environ.get("CDNAML_PARTITION_RM", "0") != "0"
 # 5-8x slower (profiles/pmc_seg_hist_subset.txt): both children must be built, and every row gather of the
 # row-major bins (one or two 64 B lines) then feeds 34 atomics instead of 104
 MSEG_SUBSET = __import__("os").environ.get("CDNAML_MSEG_SUBSET", "0") != "0"
+# multi-rank record histograms: slot chunks whose all-reduces overlap the next chunk's histogram kernel
+HIST_OVERLAP = int(__import__("os").environ.get("CDNAML_HIST_OVERLAP", "4"))
 
 
 @dataclass
@@ -818,6 +820,33 @@ class ForestTrainer:
         return bgain, bf, bb, lstats, rstats, order, cat_feats, None
 
     # ------------------------------------------------------------ training
+    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev):
+        """Record histograms of a level's S slots in HIST_OVERLAP slot chunks; chunk c's all-reduce runs on the
+        collective stream while chunk c + 1 is built (one per-level RCCL all-reduce of 1-50 MB otherwise
+        serialises with the compute stream).  The sums are exact integers, so the result is identical to one
+        fused all-reduce."""
+        Hb = torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev)
+        k = min(HIST_OVERLAP, S)
+        bounds = np.linspace(0, S, k + 1).round().astype(np.int64)
+        rm = data.row_major_bins() if dev.type == "cuda" else None
+        pend = []
+        for c in range(k):
+            s0, s1 = int(bounds[c]), int(bounds[c + 1])
+            if s1 <= s0:
+                continue
+            sel = (sb[:, 2] >= s0) & (sb[:, 2] < s1)
+            sbc = sb[sel].copy()
+            sbc[:, 2] -= s0
+            with _tr.span("tree.hist_chunk", slots=s1 - s0):
+                K.seg_hist(data.bins, d, B, rec, None, None, None, sbc, s1 - s0, wmax, scales, bins_rm=rm,
+                           interleave=True, rec=True, raw=True, out=Hb[s0:s1])
+            with _tr.span("tree.allreduce_async", cat="comm", bytes=(s1 - s0) * d * B * 16):
+                pend.append(self.comm.all_reduce_async(Hb[s0:s1]))
+        with _tr.span("tree.allreduce_wait", cat="comm"):
+            for h in pend:
+                h.wait()
+        return Hb
+
     def train(self, num_trees: int, stats_rows: Dict[str, torch.Tensor], weights: Optional[torch.Tensor],
               forest: Optional[Forest] = None) -> Forest:
         """Grow ``num_trees`` trees. stats_rows: {'v0','v1'} (moments) or {'label'} (classes)."""
@@ -912,6 +941,7 @@ class ForestTrainer:
             id_tree = a_tree
             tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
             hist_raw_scale = None
+            reduced = False
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
                 if use_mseg and (depth >= 1 or MSEG_L0):
                     # gather the rows of the built nodes into slot segments, then segment histograms
@@ -930,6 +960,12 @@ class ForestTrainer:
                         Hb = K.seg_hist_subset(data.bins, d, B, perm, v1p, wp, sb, len(build_ids), wmax, feats,
                                                mseg_scales, bins_rm=data.row_major_bins() if dev.type == "cuda"
                                                else None, interleave=True)
+                    elif is_rec and self.comm.distributed and HIST_OVERLAP > 1 and len(build_ids) >= 2:
+                        # comm/compute overlap: the level's slots are built in chunks, each chunk's int64
+                        # histogram all-reduced (async, RCCL stream) while the next chunk is built
+                        Hb = self._hist_overlapped(data, d, B, perm, sb, len(build_ids), wmax, mseg_scales, dev)
+                        hist_raw_scale = mseg_raw
+                        reduced = True
                     else:
                         Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax,
                                         mseg_scales, bins_rm=data.row_major_bins() if dev.type == "cuda" else None,
@@ -956,8 +992,9 @@ class ForestTrainer:
                 else:
                     Hb = K.hist_moments(data.bins, d, node, weights, stats_rows.get("v0"), stats_rows["v1"],
                                         K.upload(dev, slot_of)[0], slot_tree, fm_build, B, id_tree=id_tree)
-            with _tr.span("tree.allreduce", cat="comm", bytes=Hb.numel() * 8):
-                self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
+            if not reduced:
+                with _tr.span("tree.allreduce", cat="comm", bytes=Hb.numel() * 8):
+                    self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
             _split_span = _tr.span("tree.split", depth=depth)
             _split_span.__enter__()
             # ---- assemble every active node's histogram

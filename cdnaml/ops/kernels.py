@@ -1042,16 +1042,21 @@ def _interleave(work: np.ndarray, segs: np.ndarray, chunk: int) -> np.ndarray:
 def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
              v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
              scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False,
-             rec: bool = False, raw: bool = False) -> torch.Tensor:
+             rec: bool = False, raw: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
+
+    out (rec + raw): a zeroed int64 [S, d, B, 2] tensor (e.g. a slot-range slice of a level's buffer) the sums
+    are accumulated into and returned -- lets the engine all-reduce one slot chunk while the next is built.
 
     rec: ``perm`` holds packed int64 item records from ``codes_compact(rec_scale=scales[1])`` (v1p/wp unused;
     GPU with ``bins_rm`` only).  raw (with rec): return the exact int64 fixed-point sums (count, sum * scales[1])
     instead of fp64 moments, so ranks can all-reduce integers (also without rec: (sum w*q0 | count, sum w*q1)).
     CPU: the same fixed-point integers as the HIP kernels (fp32 quantisation, int64 sums), so CPU ranks
     traverse the exact arithmetic of the GPU path."""
+    if out is not None:
+        assert rec and raw and out.dtype == torch.int64 and out.is_contiguous()
     if rec:
-        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw)
+        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw, out)
     return _seg_hist(bins, d, B, perm, v0p, v1p, wp, segs, S, wmax, scales, bins_rm, interleave, raw)
 
 
@@ -1099,27 +1104,33 @@ def rec_encode(rows: torch.Tensor, w: torch.Tensor, q: torch.Tensor) -> torch.Te
     return rows.to(torch.int64) | (w.to(torch.int64) << 31) | ((q.to(torch.int64) + (1 << 23)) << 39)
 
 
-def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False):
+def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False, out=None):
     G, n, _ = bins.shape
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
     if S == 0 or len(segs) == 0:
+        if out is not None:
+            return out
         return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
     qs1 = float(scales[1])
     if not _native(bins):
         pos, slot = _seg_items(segs)
         rows, w, q = rec_decode(rec[pos])
         iout = _int_hist_cpu(bins, d, B, S, rows, slot, w, w * q)
+        if out is not None:
+            iout = out.copy_(iout)
     else:
         assert bins_rm is not None and rec.dtype == torch.int64
         wm = int(max(1, min(255, wmax)))
         chunk = _fill_chunk(segs, min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1)))
         work = _seg_work(segs, chunk)
         if len(work) == 0:
+            if out is not None:
+                return out
             return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
         if interleave and len(segs) > 1:
             work = _interleave(work, segs, chunk)
         wt, = upload(bins.device, work.reshape(-1))
-        iout = torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
+        iout = out if out is not None else torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
         assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
         mode = 1 | 4 | 16 | (128 if (SEG_LANE and B <= SEG_LANE_MAX_B) else 0)
         _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(bins_rm), n, d, B, _ptr(rec), None, None, None,

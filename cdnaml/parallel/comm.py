@@ -79,6 +79,22 @@ class _Guard:
         return False
 
 
+class _Pending:
+    """An in-flight all-reduce (Comm.all_reduce_async)."""
+
+    def __init__(self, work, w: torch.Tensor, t: torch.Tensor, comm: Optional["Comm"] = None):
+        self.work, self.w, self.t, self.comm = work, w, t, comm
+
+    def wait(self) -> torch.Tensor:
+        if self.work is not None:
+            with self.comm._guard("all_reduce_wait"):
+                self.work.wait()
+            self.work = None
+            if self.w.data_ptr() != self.t.data_ptr():
+                self.t.copy_(self.w)
+        return self.t
+
+
 class Comm:
     """Communicator bound to this process's device."""
 
@@ -132,6 +148,24 @@ class Comm:
         if w.data_ptr() != t.data_ptr():
             t.copy_(w)
         return t
+
+    def all_reduce_async(self, t: torch.Tensor, op: str = "sum") -> "_Pending":
+        """Start an in-place all-reduce and return a handle whose ``wait()`` completes it.
+
+        RCCL: the collective is enqueued on the process group's stream after the work already queued on the
+        current stream, so kernels launched after this call overlap with it; ``wait()`` makes the current
+        stream wait for it.  gloo: the host copy is reduced on gloo's thread and copied back on ``wait()``."""
+        if not self.distributed:
+            return _Pending(None, t, t)
+        self.calls += 1
+        self.bytes_reduced += t.numel() * t.element_size()
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        w = self._dev_tensor(t)
+        if not w.is_contiguous():
+            w = w.contiguous()
+        with self._guard("all_reduce"):
+            work = dist.all_reduce(w, op=rop, async_op=True)
+        return _Pending(work, w, t, self)
 
     def all_reduce_many(self, tensors: Sequence[torch.Tensor], op: str = "sum") -> List[torch.Tensor]:
         """Fuse several same-dtype tensors into one bucket -> one collective."""
