@@ -1,14 +1,18 @@
 """Alternating least squares.
 
-Ratings are row-sharded across ranks; user/item factor tables (small) are
-replicated.  Each half-iteration every rank accumulates, for the ratings it
-holds, the per-entity normal equations Σ v vᵀ and Σ r v with one batched
-outer-product scatter on device; the partial systems are summed with one
-RCCL all-reduce and solved as a BATCH on the GPU — Cholesky for the default
-path, batched coordinate-descent NNLS when ``nonnegative=True``
-(MLE 01 - Collaborative Filtering Lab.py:136-202).  Regularisation follows
-MLlib's ALS-WR scaling (λ · n_u).  ``coldStartStrategy="drop"`` removes
-rows with unknown users/items from ``transform`` output.
+One process: each half-iteration accumulates, for every rating, the per-entity normal equations Σ v vᵀ and
+Σ r v on device (K12 als.hip, no [nnz, r, r] temporary) and solves them as a BATCH on the GPU -- Cholesky by
+default, coordinate-descent NNLS when ``nonnegative=True`` (MLE 01 - Collaborative Filtering Lab.py:136-202).
+Regularisation follows MLlib's ALS-WR scaling (λ · n_u).  ``coldStartStrategy="drop"`` removes rows with
+unknown users/items from ``transform`` output.
+
+Several ranks (block ALS, MLlib's in/out-block design re-done for one process per GPU): users and items are
+hash-partitioned over the ranks by dense id (owner = id % W) and the ratings are shuffled twice with
+``all_to_all_v`` -- one copy grouped by user owner, one by item owner.  A user half-step on rank p needs the
+item factors its users rated: every rank sends each peer exactly the rows of its own items that peer needs
+(an ``all_to_all_v`` of [m, rank] factor blocks, routing lists built once), and p then solves only its own
+users.  No rank holds or all-reduces the dense [n_entities, rank, rank] systems; the result equals the
+one-rank fit up to the fp64 summation order.  Factors are all-gathered once at the end for the model.
 """
 from __future__ import annotations
 
@@ -26,6 +30,21 @@ from .util import local_batch
 
 # K12 HIP path (als.hip) for ranks <= 32 on the GPU; the torch path is the reference
 ALS_NATIVE = True
+# several ranks: block-partitioned users / items with all-to-all factor exchange (else replicated + all-reduce)
+ALS_BLOCK = __import__("os").environ.get("CDNAML_ALS_BLOCK", "1") != "0"
+
+
+class _LocalComm:
+    """No-op reducer: block ALS half-steps solve rank-local systems."""
+    distributed = False
+
+    @staticmethod
+    def all_reduce_many(tensors, op="sum"):
+        return list(tensors)
+
+    @staticmethod
+    def all_reduce(t, op="sum"):
+        return t
 
 class ALS(Estimator):
     _params = {
@@ -83,7 +102,8 @@ class ALS(Estimator):
         off[1:] = torch.cumsum(counts, 0)
         return order, off
 
-    def _half_step_native(self, comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha, csr):
+    def _half_step_native(self, comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha, csr,
+                          gram=None):
         """K12 on the GPU (als.hip): per-destination Gram accumulation without an [nnz, r, r]
         temporary, one fused all-reduce, then batched in-LDS Cholesky / NNLS solves."""
         from ..ops import _lib
@@ -110,7 +130,7 @@ class ALS(Estimator):
             return out
         Ah, bh = A[hi].contiguous(), bvec[hi].contiguous()
         diag = (lam * cnt[hi].clamp_min(1)) if implicit else (lam * cnt[hi])
-        G = (Fd.T @ Fd).contiguous() if implicit else None
+        G = (gram.double() if gram is not None else Fd.T @ Fd).contiguous() if implicit else None
         x = torch.empty((E, rank), dtype=torch.float64, device=dev)
         info = torch.empty(E, dtype=torch.int32, device=dev)
         _lib.check(L.cdna_als_solve(E, rank, _ptr(Ah), _ptr(bh), _ptr(diag.contiguous()), _ptr(G), int(nonneg), 40,
@@ -123,11 +143,14 @@ class ALS(Estimator):
         out[hi] = x
         return out
 
-    def _half_step(self, comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha, csr=None):
+    def _half_step(self, comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha, csr=None,
+                   gram=None):
+        """gram: the implicit-feedback Y^T Y over ALL source factors (block ALS passes the all-reduced one)."""
         rank = F_src.shape[1]
         dev = F_src.device
         if csr is not None:
-            return self._half_step_native(comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha, csr)
+            return self._half_step_native(comm, src_idx, dst_idx, r, F_src, n_dst, lam, nonneg, implicit, alpha, csr,
+                                          gram)
         A = torch.zeros((n_dst, rank, rank), dtype=torch.float64, device=dev)
         bvec = torch.zeros((n_dst, rank), dtype=torch.float64, device=dev)
         cnt = torch.zeros(n_dst, dtype=torch.float64, device=dev)
@@ -147,7 +170,7 @@ class ALS(Estimator):
         comm.all_reduce_many([A.view(-1), bvec.view(-1), cnt])
         eye = torch.eye(rank, dtype=torch.float64, device=dev)
         if implicit:
-            YtY = F_src.T @ F_src
+            YtY = gram if gram is not None else F_src.T @ F_src
             A = A + YtY[None]
             A = A + lam * cnt.clamp_min(1)[:, None, None] * eye
         else:
@@ -191,11 +214,84 @@ class ALS(Estimator):
         native = ALS_NATIVE and u.device.type == "cuda" and k <= 32
         csr_u = self._csr(ui, uid.numel()) if native else None
         csr_i = self._csr(ii, iid.numel()) if native else None
-        for _ in range(self.getMaxIter()):
-            U = self._half_step(comm, ii, ui, r, V, uid.numel(), lam, nonneg, implicit, alpha, csr_u)
-            V = self._half_step(comm, ui, ii, r, U, iid.numel(), lam, nonneg, implicit, alpha, csr_i)
+        if comm.distributed and ALS_BLOCK:
+            U, V = self._fit_blocks(comm, ui, ii, r, U, V, lam, nonneg, implicit, alpha, k)
+        else:
+            for _ in range(self.getMaxIter()):
+                U = self._half_step(comm, ii, ui, r, V, uid.numel(), lam, nonneg, implicit, alpha, csr_u)
+                V = self._half_step(comm, ui, ii, r, U, iid.numel(), lam, nonneg, implicit, alpha, csr_i)
         model = ALSModel(uid.cpu().numpy(), U.float().cpu().numpy(), iid.cpu().numpy(), V.float().cpu().numpy())
         return model
+
+    # ------------------------------------------------------------------ block ALS (W > 1)
+    @staticmethod
+    def _shuffle(comm, owner, cols):
+        """Route rating rows to their owner rank: returns the received columns (concatenated)."""
+        W = comm.world_size
+        order = torch.argsort(owner, stable=True)
+        counts = torch.bincount(owner, minlength=W).tolist()
+        out = []
+        for c in cols:
+            parts = list(torch.split(c[order], counts))
+            out.append(torch.cat(comm.all_to_all_v(parts)))
+        return out
+
+    @staticmethod
+    def _routes(comm, need_ids):
+        """need_ids: sorted global ids of remote-owned (or own) entities this rank's ratings reference.
+        Returns (send_lists, need_sorted): send_lists[q] = global ids this rank owns that rank q needs (in q's
+        request order); need_sorted = this rank's needs ordered by (owner, id), the order replies arrive in."""
+        W = comm.world_size
+        own = need_ids % W
+        order = torch.argsort(own * (need_ids.max() + 1 if need_ids.numel() else 1) + need_ids)
+        need_sorted = need_ids[order]
+        counts = torch.bincount(own, minlength=W).tolist()
+        send_lists = comm.all_to_all_v(list(torch.split(need_sorted, counts)))
+        return send_lists, need_sorted
+
+    def _fit_blocks(self, comm, ui, ii, r, U0, V0, lam, nonneg, implicit, alpha, k):
+        W, me = comm.world_size, comm.rank
+        dev = ui.device
+        nu, ni = U0.shape[0], V0.shape[0]
+        # the ratings twice: grouped by user owner and by item owner
+        bu_u, bu_i, bu_r = self._shuffle(comm, ui % W, [ui, ii, r])
+        bi_u, bi_i, bi_r = self._shuffle(comm, ii % W, [ui, ii, r])
+        my_u = torch.arange(me, nu, W, device=dev)          # owned users (global ids), local index = id // W
+        my_i = torch.arange(me, ni, W, device=dev)
+        U = U0[my_u].clone()
+        V = V0[my_i].clone()
+        # routing: which item factors each rank needs for its user step (and users for the item step)
+        need_i = torch.unique(bu_i)
+        send_i, need_i_sorted = self._routes(comm, need_i)
+        need_u = torch.unique(bi_u)
+        send_u, need_u_sorted = self._routes(comm, need_u)
+        # rating -> row of the received factor block (replies arrive in (owner, id) order)
+        pos_i = torch.argsort(need_i_sorted)
+        src_in_u = pos_i[torch.searchsorted(need_i_sorted[pos_i], bu_i)]
+        pos_u = torch.argsort(need_u_sorted)
+        src_in_i = pos_u[torch.searchsorted(need_u_sorted[pos_u], bi_u)]
+        dst_u, dst_i = bu_u // W, bi_i // W
+        native = ALS_NATIVE and dev.type == "cuda" and k <= 32
+        csr_u = self._csr(dst_u, my_u.numel()) if native else None
+        csr_i = self._csr(dst_i, my_i.numel()) if native else None
+        local = _LocalComm()
+        for _ in range(self.getMaxIter()):
+            Vneed = torch.cat(comm.all_to_all_v([V[s // W] for s in send_i]))
+            gV = comm.all_reduce(V.T @ V) if implicit else None   # implicit Y^T Y spans every rank's items
+            U = self._half_step(local, src_in_u, dst_u, bu_r, Vneed, my_u.numel(), lam, nonneg, implicit, alpha,
+                                csr_u, gV)
+            Uneed = torch.cat(comm.all_to_all_v([U[s // W] for s in send_u]))
+            gU = comm.all_reduce(U.T @ U) if implicit else None
+            V = self._half_step(local, src_in_i, dst_i, bi_r, Uneed, my_i.numel(), lam, nonneg, implicit, alpha,
+                                csr_i, gU)
+        # assemble the replicated factors for the model (one gather each)
+        Uf = torch.zeros((nu, k), dtype=torch.float64, device=dev)
+        Vf = torch.zeros((ni, k), dtype=torch.float64, device=dev)
+        for ids, F in zip(comm.all_gather_varlen(my_u), comm.all_gather_varlen(U)):
+            Uf[ids.to(dev)] = F.to(dev)
+        for ids, F in zip(comm.all_gather_varlen(my_i), comm.all_gather_varlen(V)):
+            Vf[ids.to(dev)] = F.to(dev)
+        return Uf, Vf
 
 
 class ALSModel(Model):

@@ -116,6 +116,8 @@ _SIGS = {
     "cdna_codes_compact": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p], c_int),
     "cdna_bins_row_major": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p], c_int),
+    "cdna_expr_eval": ([c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int,
+                        c_void_p, c_void_p], c_int),
     "cdna_partition7": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double,

@@ -494,6 +494,7 @@ class Func(Expr):
         self.fname, self.fn, self.args = fname, fn, list(args)
         self.children = list(args)
         self.display = display
+        self.fuse = None  # K18 opcode tag when the function has a fused-kernel equivalent (sql/fused.py)
 
     def eval(self, b, ctx):
         return self.fn(b, ctx, [a.eval(b, ctx) for a in self.args])

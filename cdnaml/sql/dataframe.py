@@ -22,6 +22,7 @@ from . import relational as R
 from . import types as T
 from .batch import Batch, ColumnData, concat_batches, empty_batch
 from .column import (Alias, AnalysisException, ColRef, Column, EvalContext, Expr, Lit, SortOrder, Star, _to_expr)
+from . import fused as _fused
 
 _PART_STRIDE = 1 << 20
 
@@ -178,7 +179,7 @@ def _project(b: Batch, exprs: List[Expr], ctx) -> Batch:
                 cols[k] = c
             continue
         name = e.name()
-        c = e.eval(b, ctx)
+        c = _fused.evaluate(e, b, ctx)
         if len(c) != b.n and b.n and len(c) == 1:
             c = c.take(torch.zeros(b.n, dtype=torch.long, device=b.device))
         cols[name] = c
@@ -373,7 +374,7 @@ class DataFrame:
             raise AnalysisException("aggregate expressions are not allowed in withColumn")
 
         def fn(b, ctx):
-            c = e.eval(b, ctx)
+            c = _fused.evaluate(e, b, ctx)
             return b.with_column(name, c)
         return self._map(f"Project [*, {e.name()} AS {name}]", fn)
 
@@ -423,7 +424,7 @@ class DataFrame:
         e = cond._expr
 
         def fn(b, ctx):
-            c = e.eval(b, ctx)
+            c = _fused.evaluate(e, b, ctx)
             m = c.values.bool() & c.valid_mask() if c.valid is not None else c.values.bool()
             return b.filter(m)
         return self._map(f"Filter {e}", fn)

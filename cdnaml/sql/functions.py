@@ -92,7 +92,9 @@ def _math(fname, fn, out_t=None):
                 if bool(bad.any()):
                     valid = ~bad if valid is None else valid & ~bad
             return ColumnData(r if out_t is None else r.to(out_t.torch_dtype), out_t or T.DoubleType(), valid)
-        return Column(Func(fname, ev, [_ce(c)]))
+        fn_ = Func(fname, ev, [_ce(c)])
+        fn_.fuse = fname if (out_t is None and not extra) else None  # K18 opcode tag (sql/fused.py)
+        return Column(fn_)
     return f
 
 
@@ -129,6 +131,8 @@ def _rename(self, n):
     e = self._expr
     if isinstance(e, Func):
         e.fname = n
+        if getattr(e, "fuse", None) is not None:
+            e.fuse = n
     return self
 
 
@@ -139,7 +143,9 @@ def abs(c) -> Column:  # noqa: A001
     def ev(b, ctx, args):
         a = args[0]
         return ColumnData(torch.abs(a.values), a.dtype, a.valid)
-    return Column(Func("abs", ev, [_ce(c)]))
+    f = Func("abs", ev, [_ce(c)])
+    f.fuse = "abs"
+    return Column(f)
 
 
 def pow(a, b) -> Column:  # noqa: A001
@@ -156,7 +162,9 @@ def round(c, scale: int = 0) -> Column:  # noqa: A001
         m = 10.0 ** scale
         r = torch.sign(v) * torch.floor(torch.abs(v) * m + 0.5) / m  # HALF_UP like Spark
         return ColumnData(r, T.DoubleType() if not isinstance(a.dtype, T.FloatType) else T.FloatType(), a.valid)
-    return Column(Func("round", ev, [_ce(c)], display=f"round({_ce(c).name()}, {scale})"))
+    f = Func("round", ev, [_ce(c)], display=f"round({_ce(c).name()}, {scale})")
+    f.fuse = ("round", int(scale))
+    return Column(f)
 
 
 def bround(c, scale: int = 0) -> Column:
@@ -171,14 +179,18 @@ def floor(c) -> Column:
     def ev(b, ctx, args):
         a = args[0]
         return ColumnData(torch.floor(a.values.to(torch.float64)).to(torch.int64), T.LongType(), a.valid)
-    return Column(Func("FLOOR", ev, [_ce(c)]))
+    f = Func("FLOOR", ev, [_ce(c)])
+    f.fuse = "floor"
+    return Column(f)
 
 
 def ceil(c) -> Column:
     def ev(b, ctx, args):
         a = args[0]
         return ColumnData(torch.ceil(a.values.to(torch.float64)).to(torch.int64), T.LongType(), a.valid)
-    return Column(Func("CEIL", ev, [_ce(c)]))
+    f = Func("CEIL", ev, [_ce(c)])
+    f.fuse = "ceil"
+    return Column(f)
 
 
 def greatest(*cols) -> Column:

@@ -167,11 +167,18 @@ def scenario_als(spark):
     u, i = pairs // ni, pairs % ni
     pdf = pd.DataFrame({"userId": u, "movieId": i, "rating": (U[u] * V[i]).sum(1) + 3.0})
     df = spark.createDataFrame(pdf)
-    m = ALS(rank=3, maxIter=5, regParam=0.05, seed=42, userCol="userId", itemCol="movieId",
-            ratingCol="rating").fit(df)
-    uf = m.userFactors.orderBy("id").toPandas()
-    return {"uf": np.round(np.stack(uf["features"].map(lambda v: np.asarray(v.toArray() if hasattr(v, "toArray")
-                                                                            else v))), 7).reshape(-1).tolist()}
+    comm = spark.comm
+    a2a0 = comm.op_calls.get("all_to_all", 0)
+    out = {}
+    for name, kw in (("uf", {}), ("uf_implicit", {"implicitPrefs": True, "alpha": 2.0}),
+                     ("uf_nonneg", {"nonnegative": True})):
+        m = ALS(rank=3, maxIter=5, regParam=0.05, seed=42, userCol="userId", itemCol="movieId",
+                ratingCol="rating", **kw).fit(df)
+        out[name] = np.asarray(m._U, dtype=np.float64).reshape(-1).tolist()
+        out[name.replace("uf", "vf")] = np.asarray(m._V, dtype=np.float64).reshape(-1).tolist()
+    # block ALS (W > 1): factor blocks travel by all-to-all, no dense [n, r, r] all-reduce
+    out["block"] = comm.world_size == 1 or comm.op_calls.get("all_to_all", 0) > a2a0
+    return out
 
 
 SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault, "trees": scenario_trees,
