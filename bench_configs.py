@@ -233,6 +233,43 @@ def bench_relational(spark, args):
           "groupBy/join/dropDuplicates on K16 device hash tables", n_total, f"dp{comm.world_size}")
 
 
+def bench_expr(spark, args):
+    """K18: feature-engineering expressions of the course (ML 01 price cast / filters, L03 log-price and exp back,
+    MLE 03 when-label, ML 02 ratios) over 1e8 rows, one fused kernel each vs the operator-at-a-time path."""
+    from cdnaml.sql import functions as F
+    from cdnaml.sql import fused
+    dev = spark.device
+    comm = spark.comm
+    n_total = int(args.rows or 1e8)
+    n = n_total * (comm.rank + 1) // comm.world_size - n_total * comm.rank // comm.world_size
+    g = torch.Generator(device=dev).manual_seed(5 + comm.rank)
+    price = torch.exp(torch.randn(n, generator=g, device=dev, dtype=torch.float64) + 4.5)
+    beds = torch.randint(0, 6, (n,), generator=g, device=dev, dtype=torch.int32)
+    acc = torch.randint(1, 12, (n,), generator=g, device=dev, dtype=torch.int32)
+    df = spark.createDataFrameFromLocalTensors({"price": price, "bedrooms": beds, "accommodates": acc})
+    p, b, a = F.col("price"), F.col("bedrooms"), F.col("accommodates")
+    exprs = {
+        "log_price -> exp": F.exp(F.log(p) * 0.5 + 1.0) - 1.0,
+        "price per bed": F.when(b > 0, p / b).otherwise(p),
+        "priceClass label": F.when((p >= 150) & (a > 2), 1.0).otherwise(0.0),
+        "ratio + round": F.round(p / (a * 1.0) * 100.0, 2) + F.sqrt(b * 1.0),
+    }
+    total = {True: 0.0, False: 0.0}
+    for name, e in exprs.items():
+        res = {}
+        for on in (False, True):
+            fused.FUSE = on
+            ms, _ = _timed(spark, lambda: df.select(e.alias("r"))._plan.execute(), args.steps, args.warmup)
+            res[on] = ms
+            total[on] += ms
+        _log(f"{name}: operator path {res[False]:.2f} ms, fused {res[True]:.2f} ms ({res[False] / res[True]:.1f}x)")
+    fused.FUSE = True
+    _log(f"total: operator path {total[False]:.2f} ms, fused {total[True]:.2f} ms")
+    _emit(spark, "rows/sec fused column expressions (4 course feature expressions) on 1e8 rows",
+          4 * n_total / (total[True] / 1e3), "rows/s", args.steps, args.warmup, total[True], True, "strong", "fp64",
+          "K18 expr.hip fused elementwise", n_total, f"dp{comm.world_size}")
+
+
 def bench_airbnb(spark, args):
     from cdnaml.ml.evaluation import RegressionEvaluator
     from cdnaml.ml.feature import VectorAssembler
@@ -255,7 +292,7 @@ def bench_airbnb(spark, args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("config", choices=["lr", "cv", "gbdt", "infer", "airbnb", "relational"])
+    ap.add_argument("config", choices=["lr", "cv", "gbdt", "infer", "airbnb", "relational", "expr"])
     ap.add_argument("--rows", type=float, default=None)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
@@ -271,7 +308,7 @@ def main():
     import cdnaml
     spark = cdnaml.SparkSession.builder.appName("bench_configs").getOrCreate()
     {"lr": bench_lr, "cv": bench_cv, "gbdt": bench_gbdt, "infer": bench_infer, "airbnb": bench_airbnb,
-     "relational": bench_relational}[
+     "relational": bench_relational, "expr": bench_expr}[
         args.config](spark, args)
 
 
