@@ -444,7 +444,7 @@ def register_model(model_uri: str, name: str, await_registration_for: int = 300,
 
 
 # ---------------------------------------------------------------- autolog
-def _autolog_fit(est, model, log_models: bool):
+def _autolog_fit(est, model, log_models: bool, metrics=None):
     created = False
     if active_run() is None:
         start_run()
@@ -465,6 +465,8 @@ def _autolog_fit(est, model, log_models: bool):
                 log_param(k, v)
         set_tag("estimator_name", type(est).__name__)
         set_tag("estimator_class", f"{type(est).__module__}.{type(est).__name__}")
+        for k, v in (metrics or {}).items():
+            log_metric(k.replace("/", "_"), float(v))
         if log_models:
             from . import spark as _spark
             from ..models.pipeline import PipelineModel

@@ -27,6 +27,34 @@ import torch
 _state = {"enabled": os.environ.get("CDNAML_TRACE", "0") not in ("0", "", "false"), "events": [],
           "lock": threading.Lock(), "t0": time.perf_counter()}
 
+# roctx ranges: every span is also pushed as a ROCTx range, so `rocprofv3 --marker-trace` lines
+# the engine's phases (tree.hist, tree.allreduce, ...) up with the kernels.  CDNAML_ROCTX=1 turns ranges on
+# even when span timing is off; libroctx64 is loaded lazily (absent library: ranges are a no-op).
+_roctx = {"lib": None, "tried": False, "on": os.environ.get("CDNAML_ROCTX", "0") not in ("0", "", "false")}
+
+
+def _roctx_lib():
+    if not _roctx["tried"]:
+        _roctx["tried"] = True
+        import ctypes
+        for path in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+            try:
+                lib = ctypes.CDLL(path)
+                lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                lib.roctxRangePushA.restype = ctypes.c_int
+                lib.roctxRangePop.restype = ctypes.c_int
+                _roctx["lib"] = lib
+                break
+            except OSError:
+                continue
+    return _roctx["lib"]
+
+
+def enable_roctx(on: bool = True) -> bool:
+    """Emit ROCTx ranges for spans; returns whether libroctx64 is available."""
+    _roctx["on"] = on
+    return _roctx_lib() is not None
+
 
 def enable(on: bool = True):
     _state["enabled"] = on
@@ -68,8 +96,15 @@ class _Span:
 @contextlib.contextmanager
 def span(name: str, cat: str = "op", device: Optional[torch.device] = None, **args):
     """Time a region.  On a GPU the region is bracketed by HIP events on the current stream."""
+    rx = _roctx_lib() if _roctx["on"] else None
+    if rx is not None:
+        rx.roctxRangePushA(name.encode())
     if not _state["enabled"]:
-        yield
+        try:
+            yield
+        finally:
+            if rx is not None:
+                rx.roctxRangePop()
         return
     s = _Span()
     s.name, s.cat, s.args = name, cat, args
@@ -88,6 +123,8 @@ def span(name: str, cat: str = "op", device: Optional[torch.device] = None, **ar
         if use_cuda:
             s.ev1.record()
         s.t_host1 = time.perf_counter()
+        if rx is not None:
+            rx.roctxRangePop()
         with _state["lock"]:
             _state["events"].append(s)
 
@@ -108,24 +145,31 @@ def traced(name: Optional[str] = None, cat: str = "op"):
 
 
 def stats() -> Dict[str, Dict[str, float]]:
-    out: Dict[str, Dict[str, float]] = defaultdict(lambda: {"calls": 0, "total_ms": 0.0, "max_ms": 0.0})
+    out: Dict[str, Dict[str, float]] = defaultdict(lambda: {"calls": 0, "total_ms": 0.0, "max_ms": 0.0,
+                                                             "bytes": 0.0})
     for s in list(_state["events"]):
         d = s.duration_ms()
         o = out[s.name]
         o["calls"] += 1
         o["total_ms"] += d
         o["max_ms"] = max(o["max_ms"], d)
+        if s.cat == "comm" and "bytes" in s.args:
+            o["bytes"] += float(s.args["bytes"])
     for o in out.values():
         o["mean_ms"] = o["total_ms"] / max(o["calls"], 1)
+        # collectives: achieved bus-agnostic rate (payload bytes / span time)
+        o["GB_s"] = o["bytes"] / (o["total_ms"] * 1e6) if o["bytes"] and o["total_ms"] > 0 else 0.0
     return dict(out)
 
 
 def summary(sort: str = "total_ms") -> str:
     st = stats()
     rows = sorted(st.items(), key=lambda kv: -kv[1][sort])
-    lines = [f"{'op':40s} {'calls':>7s} {'total ms':>11s} {'mean ms':>10s} {'max ms':>10s}"]
+    lines = [f"{'op':40s} {'calls':>7s} {'total ms':>11s} {'mean ms':>10s} {'max ms':>10s} {'GB/s':>8s}"]
     for k, v in rows:
-        lines.append(f"{k[:40]:40s} {v['calls']:7d} {v['total_ms']:11.2f} {v['mean_ms']:10.3f} {v['max_ms']:10.3f}")
+        gbs = f"{v['GB_s']:8.1f}" if v.get("GB_s") else f"{'':8s}"
+        lines.append(f"{k[:40]:40s} {v['calls']:7d} {v['total_ms']:11.2f} {v['mean_ms']:10.3f} {v['max_ms']:10.3f} "
+                     f"{gbs}")
     try:
         from ..session import SparkSession
         s = SparkSession.getActiveSession()

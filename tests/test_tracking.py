@@ -177,5 +177,29 @@ def test_autolog_logs_fits(tracking, spark):
                 VectorAssembler(inputCols=["x"], outputCol="features").transform(df))
         r = mlflow.get_run(run.info.run_id)
         assert r.data.params.get("regParam") == "0.1"
+        # engine metrics of the fit
+        assert r.data.metrics["engine.fit_ms"] > 0 and "engine.collective_calls" in r.data.metrics
     finally:
         mlflow.pyspark.ml.autolog(disable=True)
+
+
+def test_tracing_spans_comm_rate_and_roctx(spark):
+    """spans carry collective byte counts -> GB/s in the summary; roctx ranges push/pop cleanly
+    (a no-op when libroctx64 is absent)."""
+    import time as _t
+    from cdnaml.utils import tracing
+    tracing.reset()
+    tracing.enable()
+    tracing.enable_roctx(True)
+    try:
+        with tracing.span("tree.allreduce", cat="comm", bytes=4_000_000):
+            _t.sleep(0.002)
+        with tracing.span("tree.hist"):
+            pass
+        st = tracing.stats()
+        assert st["tree.allreduce"]["bytes"] == 4e6 and 0 < st["tree.allreduce"]["GB_s"] < 2.1
+        assert "GB/s" in tracing.summary()
+    finally:
+        tracing.enable_roctx(False)
+        tracing.disable()
+        tracing.reset()
