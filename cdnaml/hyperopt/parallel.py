@@ -1,15 +1,23 @@
 """Concurrent trials: ``SparkTrials(parallelism=2)`` (Labs/ML 08L:89-112) and
 ``GPUTrials``.
 
-Each worker thread owns a HIP stream (and a device, round-robin over the
-visible GPUs when ``devices`` is not given), so independent single-node fits —
-sklearn on the host or this engine's kernels on the GPU — overlap.  Proposals
-are made on the driver thread from the trials completed so far, exactly like
-hyperopt's asynchronous SparkTrials loop.  Failed trials are recorded (status
-``fail``) instead of aborting the search.  Trials are auto-logged as nested
-tracking runs under the active run (Databricks SparkTrials behaviour, L08:89).
+Placement follows the engine's one-process-per-GPU design:
+
+* one process: worker threads share this process's GPU (the session's device), each with its own HIP
+  stream, so independent single-node fits -- sklearn on the host or this engine's kernels -- overlap.
+  Proposals are made on the driver thread from the trials completed so far, exactly like hyperopt's
+  asynchronous SparkTrials loop.
+* SPMD (torchrun, W ranks): trials are spread over the ranks -- every rank draws the same batch of W x
+  parallelism proposals (same history, same ``rstate``), evaluates the ones assigned to it on ITS GPU with a
+  rank-local communicator (a trial is a single-node fit, like a SparkTrials task on one worker), and the
+  results are all-gathered so every rank's ``Trials`` and TPE state stay identical.
+
+Failed trials are recorded (status ``fail``) instead of aborting the search.  Trials are auto-logged as nested
+tracking runs under the active run (Databricks SparkTrials behaviour, L08:89), by rank 0 only.
 """
 from __future__ import annotations
+
+import contextlib
 
 import concurrent.futures as cf
 import threading
@@ -25,13 +33,86 @@ class GPUTrials(Trials):
     def __init__(self, parallelism: Optional[int] = None, timeout: Optional[float] = None,
                  devices: Optional[List[int]] = None, spark_session=None, autolog: bool = True):
         super().__init__()
-        ngpu = torch.cuda.device_count() if torch.cuda.is_available() else 0
-        self.devices = list(devices) if devices is not None else list(range(ngpu))
-        default_par = max(1, len(self.devices)) if self.devices else 4
-        self.parallelism = int(parallelism) if parallelism else default_par
+        self.spark = spark_session
+        if devices is not None:
+            self.devices = list(devices)
+        else:
+            dev = self._session_device()
+            # this process's GPU only: the other visible GPUs belong to the other ranks of an SPMD job
+            self.devices = [dev.index if dev.index is not None else torch.cuda.current_device()] \
+                if dev is not None and dev.type == "cuda" else []
+        self.parallelism = int(parallelism) if parallelism else 4
         self.timeout = timeout
         self._autolog = autolog
         self._local = threading.local()
+
+    def _session(self):
+        if self.spark is not None:
+            return self.spark
+        try:
+            from ..session import SparkSession
+            return SparkSession.getActiveSession()
+        except Exception:  # noqa: BLE001
+            return None
+
+    def _session_device(self):
+        s = self._session()
+        if s is not None:
+            return s.device
+        return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
+
+    @contextlib.contextmanager
+    def _rank_local(self, session):
+        """Run a trial on this rank alone: engine fits inside use a one-rank communicator."""
+        if session is None or not session.comm.distributed:
+            yield
+            return
+        from ..parallel.comm import Comm
+        saved = session.comm
+        local = Comm(saved.device)
+        local.initialized, local.rank, local.world_size, local.backend = False, 0, 1, "local"
+        session.comm = local
+        try:
+            yield
+        finally:
+            session.comm = saved
+
+    def _run_spmd(self, comm, session, fn, space, next_assignment, should_stop, max_evals):
+        from .fmin import _TrialLogger, evaluate_trial
+        log = _TrialLogger(self) if comm.rank == 0 else None
+        W, me = comm.world_size, comm.rank
+        t0 = time.time()
+        per = max(1, self.parallelism)
+        while True:
+            timed_out = comm.broadcast_object(self.timeout is not None and time.time() - t0 >= self.timeout)
+            k = min(W * per, max_evals - len(self))
+            if timed_out or should_stop() or k <= 0:
+                break
+            assigns = [next_assignment() for _ in range(k)]        # identical on every rank
+            trials = [self.new_trial(a, space) for a in assigns]
+            mine = [i for i in range(k) if i % W == me]
+
+            def run(i):
+                evaluate_trial(fn, space, trials[i], True)
+                return i
+            # one rank-local communicator for the whole local batch (swapped once: the worker threads share it)
+            with self._rank_local(session):
+                if len(mine) > 1:
+                    with cf.ThreadPoolExecutor(max_workers=per, thread_name_prefix="cdnaml-trial") as ex:
+                        list(ex.map(run, mine))
+                else:
+                    for i in mine:
+                        run(i)
+            keys = ("state", "result", "book_time", "refresh_time")
+            done = comm.all_gather_object({i: {kk: trials[i][kk] for kk in keys} for i in mine})
+            for part in done:
+                for i, fields in part.items():
+                    trials[i].update(fields)
+            if log is not None:
+                for tr, a in zip(trials, assigns):
+                    log.log(tr, a)
+        if log is not None:
+            log.close()
 
     def _worker_ctx(self, slot: int):
         if not self.devices:
@@ -41,6 +122,9 @@ class GPUTrials(Trials):
 
     def _run_parallel(self, fn, space, next_assignment, should_stop, max_evals, catch):
         from .fmin import _TrialLogger, evaluate_trial
+        session = self._session()
+        if session is not None and session.comm.distributed:
+            return self._run_spmd(session.comm, session, fn, space, next_assignment, should_stop, max_evals)
         log = _TrialLogger(self)
         t0 = time.time()
         slots = list(range(self.parallelism))

@@ -181,8 +181,34 @@ def scenario_als(spark):
     return out
 
 
+def scenario_hyperopt(spark):
+    """GPUTrials in SPMD: trials spread over ranks (each a rank-local engine fit), results all-gathered; the
+    search history must equal the one-process search."""
+    from cdnaml.hyperopt import GPUTrials, fmin, hp, tpe
+    from cdnaml.ml.evaluation import RegressionEvaluator
+    from cdnaml.ml.feature import VectorAssembler
+    from cdnaml.ml.regression import LinearRegression
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(400, 3))
+    pdf = pd.DataFrame(X, columns=["a", "b", "c"])
+    pdf["label"] = X @ np.array([1.0, -2.0, 0.5]) + 0.3 * rng.normal(size=400)
+
+    def objective(p):
+        df = spark.createDataFrame(pdf)                       # rank-local inside a trial: the full table
+        va = VectorAssembler(inputCols=["a", "b", "c"], outputCol="features")
+        m = LinearRegression(regParam=p["reg"], elasticNetParam=p["en"]).fit(va.transform(df))
+        return round(RegressionEvaluator().evaluate(m.transform(va.transform(df))), 9)
+
+    trials = GPUTrials(parallelism=2)
+    best = fmin(objective, {"reg": hp.loguniform("reg", -6, 0), "en": hp.choice("en", [0.0, 0.5])},
+                algo=tpe.suggest, max_evals=8, trials=trials, rstate=np.random.default_rng(7))
+    return {"losses": [round(float(x), 9) for x in trials.losses()], "best_en": int(best["en"]),
+            "best_reg": round(float(best["reg"]), 12), "n": len(trials.trials)}
+
+
 SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault, "trees": scenario_trees,
-             "trees_uneven": scenario_trees_uneven, "cv": scenario_cv, "als": scenario_als}
+             "trees_uneven": scenario_trees_uneven, "cv": scenario_cv, "als": scenario_als,
+             "hyperopt": scenario_hyperopt}
 
 
 def run(name):
