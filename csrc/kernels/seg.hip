@@ -766,13 +766,21 @@ __device__ __forceinline__ bool v_aligned(const float* p) { return (reinterpret_
 template <int KB, bool SCATTER>
 __global__ __launch_bounds__(256) void codes_compact_w_kernel(const CompactWArgs a) {
   __shared__ int s_k[256];
-  const int t = blockIdx.y;
+  // XCD-aware block -> (row chunk, tree) map: block b runs on XCD b % 8, and the T blocks of one row chunk are
+  // consecutive slots of ONE XCD, so they run together and share that XCD's L2 copy of the chunk's labels
+  // (v1 is the same for every tree: with tree-major grids it crossed HBM once per tree, ~8 GB per level
+  // at 1e8 rows x 20 trees)
+  const int nch = (a.Wv + 3) / 4;
+  const int xcd = (int)(blockIdx.x & 7u), slot = (int)(blockIdx.x >> 3);
+  const int qc = slot / a.T, t = slot - qc * a.T;
+  const int chunk = qc * 8 + xcd;
+  if (chunk >= nch) return;  // block-uniform
   const int tf = a.tfirst[t];
   const int nloc = (t + 1 < a.T ? a.tfirst[t + 1] : a.A) - tf;
   for (int i = threadIdx.x; i < 256; i += 256) s_k[i] = (i < nloc && i < 255) ? a.kmap[tf + i] : -1;
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int w = chunk * 4 + (threadIdx.x >> 6);
   if (w >= a.Wv) return;
   const int64_t r_begin = (int64_t)w * a.per_wave;
   const int64_t r_end = r_begin + a.per_wave < a.n ? r_begin + a.per_wave : a.n;
@@ -1076,7 +1084,8 @@ CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64
   if (rec_out && (n >= (int64_t)1 << 31 || v0)) return (int)hipErrorInvalidValue;
   CompactWArgs a{codes, n, T, A, tfirst, kmap, v0, v1, per_wave, Wv, wcnt, woff, perm_out, v0_out, v1_out, w_out,
                  rec_out, qs1, kstart};
-  const dim3 grid((unsigned)((Wv + 3) / 4), (unsigned)T);
+  const int64_t nch = (Wv + 3) / 4;
+  const dim3 grid((unsigned)(((nch + 7) / 8) * 8 * T));  // (chunk, tree) pairs, XCD-aware order (kernel)
   auto go = [&](auto k1, auto k2) {
     if (pass == 1) hipLaunchKernelGGL(k1, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k2, grid, dim3(256), 0, st, a);
