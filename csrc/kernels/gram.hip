@@ -21,6 +21,7 @@
 // streaming form (gram_bf16s_kernel) reads X once with all tile pairs per
 // block; gram_bf16_kernel remains for unaligned / wide inputs.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -322,6 +323,175 @@ __global__ __launch_bounds__(256) void gram_bf16s_kernel(const float* __restrict
 #undef GRAM_STORE
 #undef GRAM_COL
 
+// ---------------------------------------------------------------------------
+// Streaming Gram with direct-to-LDS staging (gram_bf16d_kernel; ldx == d, d % 4 == 0, d + 2 <= 128).
+// gram_bf16s_kernel above stages the next tile in VGPRs (128 B per thread): 124 VGPRs + 48 accumulators cap
+// it at 2 waves per SIMD and ~51 KB of loads in flight per CU -- rocprofv3: 81 % of wave time waiting on
+// HBM, 2.6 TB/s.  Here the fp32 rows go HBM -> LDS with global_load_lds_dwordx4 (no VGPRs), NSTAGE = 5
+// tiles deep: four 25.6 KB tiles (~100 KB) are in flight per CU while the current tile is converted to the
+// transposed bf16 tile and multiplied on MFMA.  Every wave issues exactly kCPW DMA instructions per tile
+// (padding chunks re-read a valid address into the stage's spare slots), so the in-order vmcnt wait
+// "tile t has landed" is the compile-time count kCPW * (NSTAGE - 1).
+// Stage layout: chunks of 1 KB (one wave instruction each): 25 chunks of the tile's 64 x d fp32 rows (d =
+// 100: 25 600 B), one chunk whose first 16 lanes carry the 64 labels, spare chunks.
+// ---------------------------------------------------------------------------
+constexpr int kDRows = 64;
+constexpr int kDStages = 5;
+constexpr int kDWaves = 4;
+
+// HBM -> LDS DMA issued through inline asm: the compiler's wait-count pass would otherwise treat every LDS read
+// of the staging ring as aliasing the in-flight DMA and drain ALL of it (vmcnt(0)) before the conversion,
+// serialising the 5-deep pipeline.  The waits are explicit (vmcnt_imm below).  M0 holds the wave's LDS base;
+// lane i writes base + i * size.
+__device__ __forceinline__ void dma_dwordx4(const void* g, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(g),
+               "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory", "m0");
+}
+__device__ __forceinline__ void dma_dword(const void* g, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" : : "v"(g),
+               "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory", "m0");
+}
+
+__device__ __forceinline__ constexpr int vmcnt_imm(int n) {
+  return (n & 0xF) | (((n >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8);  // wait vmcnt <= n only
+}
+
+template <int PW, int CPW>
+__global__ __launch_bounds__(256) void gram_bf16d_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                         const float* __restrict__ y,
+                                                         const float* __restrict__ shift, float yshift,
+                                                         PairTable tab, int npairs, int Dpad,
+                                                         float* __restrict__ partial, int64_t rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int kCS = kDRows + 8;                 // bf16 column stride (conflict-free fragment reads)
+  constexpr int kStageBytes = CPW * kDWaves * 1024;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  char* stage0 = smem;                                                   // [kDStages][kStageBytes]
+  uint16_t* tb = reinterpret_cast<uint16_t*>(smem + kDStages * kStageBytes);  // [Dpad][kCS] bf16
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, half = lane >> 5;
+  const int d4 = d >> 2;
+  const int xchunks = d >> 2;                      // 64 rows x d floats = d / 4 chunks of 1 KB (d % 4 == 0)
+  const int64_t rb0 = (int64_t)blockIdx.x * rows_per_block;
+  int64_t rb1 = rb0 + rows_per_block;
+  if (rb1 > n) rb1 = n;
+  const int ntiles = rb0 < rb1 ? (int)((rb1 - rb0 + kDRows - 1) / kDRows) : 0;
+  const char* xend = reinterpret_cast<const char*>(X + n * d);
+  // one DMA round: this wave's kCPW chunks of tile `ti` into stage `ti % kDStages` (always kCPW instructions)
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  auto issue = [&](int ti) __attribute__((always_inline)) {
+    char* st = stage0 + (ti % kDStages) * kStageBytes;
+    const int64_t t0 = rb0 + (int64_t)ti * kDRows;
+    const char* xt = reinterpret_cast<const char*>(X + t0 * d);
+#pragma unroll
+    for (int k = 0; k < CPW; ++k) {
+      const int c = wid_u + kDWaves * k;           // chunk index (wave-uniform)
+      const char* g = reinterpret_cast<const char*>(X);  // spare: any valid address
+      const uint32_t la = (uint32_t)(uintptr_t)(lds_ptr)(st + c * 1024);
+      if (c == xchunks) {                          // labels: one dword per lane (64 rows)
+        if (ti < ntiles && y != nullptr && t0 + lane < n) g = reinterpret_cast<const char*>(y + t0 + lane);
+        dma_dword(g, la);
+        continue;
+      }
+      if (ti < ntiles && c < xchunks) {
+        const char* p = xt + (int64_t)c * 1024 + lane * 16;
+        g = p + 16 <= xend ? p : g;
+      }
+      dma_dwordx4(g, la);
+    }
+  };
+  // conversion item: (row octet r8, column quad c4); 8 x 25 = 200 items for d = 100, one per thread
+  constexpr int kOct = kDRows / 8;
+  const int items = kOct * d4;
+  const int e = tid;
+  const bool cv = e < items;
+  const int r8 = cv ? e % kOct : 0, c4 = cv ? e / kOct : 0;
+  const float4 sh = (cv && shift) ? *reinterpret_cast<const float4*>(shift + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  // zero the bf16 tile once: padding columns d + 2 .. Dpad - 1 stay zero
+  for (int i = tid; i < Dpad * kCS / 2; i += 256) reinterpret_cast<uint32_t*>(tb)[i] = 0u;
+  int pr[PW], TI[PW], TJ[PW];  // tile-pair ids resolved once (indexing the kernarg table in the loop was a
+#pragma unroll                // global load per MFMA, and its vmcnt wait drained the DMA)
+  for (int j = 0; j < PW; ++j) {
+    pr[j] = wid + kDWaves * j;
+    TI[j] = pr[j] < npairs ? tab.I[pr[j]] : 0;
+    TJ[j] = pr[j] < npairs ? tab.J[pr[j]] : 0;
+  }
+  f32x16 acc[PW];
+#pragma unroll
+  for (int j = 0; j < PW; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  // prologue: tiles 0 .. NSTAGE-2 in flight
+#pragma unroll
+  for (int s = 0; s < kDStages - 1; ++s) issue(s);
+  for (int ti = 0; ti < ntiles; ++ti) {
+    issue(ti + kDStages - 1);                      // keeps exactly kCPW * (NSTAGE - 1) newer loads per wave
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(CPW * (kDStages - 1)));  // this wave's chunks of tile ti landed
+    __builtin_amdgcn_s_barrier();                  // ... and every other wave's; MFMA(ti - 1) done with tb
+    // stage reads through address-space-3 pointers (ds_read, lgkmcnt): generic pointers became flat loads
+    // that also count in vmcnt, and every wait for them drained the in-flight DMA
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const f4v* lf4p;
+    typedef __attribute__((address_space(3))) const float* lfp;
+    const uint32_t sta = (uint32_t)(uintptr_t)(lds_ptr)(stage0 + (ti % kDStages) * kStageBytes);
+    const int64_t t0 = rb0 + (int64_t)ti * kDRows;
+    const int64_t lim = rb1 - t0;
+    if (cv) {
+      uint16_t* dst = tb + (4 * c4) * kCS + 8 * r8;
+      float4 v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = 8 * r8 + q;
+        const f4v lv = *(lf4p)(uintptr_t)(sta + (uint32_t)((r * d + 4 * c4) * 4));
+        v[q] = r < lim ? make_float4(lv.x, lv.y, lv.z, lv.w) : sh;
+      }
+#define GRAM_D_COL(comp_, off_)                                                                      \
+  {                                                                                                  \
+    uint32_t w_[4];                                                                                  \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                                  \
+      const uint32_t lo_ = __builtin_bit_cast(uint16_t, (__bf16)(v[2 * q].comp_ - sh.comp_));        \
+      const uint32_t hi_ = __builtin_bit_cast(uint16_t, (__bf16)(v[2 * q + 1].comp_ - sh.comp_));    \
+      w_[q] = lo_ | (hi_ << 16);                                                                     \
+    }                                                                                                \
+    *reinterpret_cast<uint4*>(dst + (off_)) = uint4{w_[0], w_[1], w_[2], w_[3]};                     \
+  }
+      GRAM_D_COL(x, 0);
+      GRAM_D_COL(y, kCS);
+      GRAM_D_COL(z, 2 * kCS);
+      GRAM_D_COL(w, 3 * kCS);
+#undef GRAM_D_COL
+    }
+    if (tid < kDRows) {
+      const float ly = *(lfp)(uintptr_t)(sta + (uint32_t)(xchunks * 1024 + 4 * tid));
+      const float yv = (y != nullptr && tid < lim) ? ly - yshift : 0.f;
+      tb[d * kCS + tid] = __builtin_bit_cast(uint16_t, (__bf16)(tid < lim ? 1.f : 0.f));
+      tb[(d + 1) * kCS + tid] = __builtin_bit_cast(uint16_t, (__bf16)yv);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0): this wave's tile stores are in LDS
+    __builtin_amdgcn_s_barrier();                  // transposed bf16 tile complete
+#pragma unroll
+    for (int ks = 0; ks < kDRows / 16; ++ks) {
+      const int kr = ks * 16 + 8 * half;
+#pragma unroll
+      for (int j = 0; j < PW; ++j) {
+        if (pr[j] >= npairs) continue;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&tb[(TI[j] * 32 + (lane & 31)) * kCS + kr]);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&tb[(TJ[j] * 32 + (lane & 31)) * kCS + kr]);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[j], 0, 0, 0);
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));        // drain the spare DMA rounds before the block exits
+  const int col = lane & 31;
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    if (pr[j] >= npairs) continue;
+    float* dst = partial + ((int64_t)blockIdx.x * npairs + pr[j]) * 1024;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dst[((q & 3) + 8 * (q >> 2) + 4 * half) * 32 + col] = acc[j][q];
+  }
+}
+
 // partial [nblk][npairs][1024] -> out (symmetric fill).  16 threads per element each sum a fixed stride of
 // blocks, then a fixed-order LDS tree: deterministic, and 16x the parallelism of one thread per element
 // (the serial 1024-block loop took 0.35 ms of a 3.6 ms fit).
@@ -424,6 +594,52 @@ void launch_stream_ni(const GramPlan& pl, const float* X, int64_t n, int d, int6
   else launch_stream<PW, 2>(pl, X, n, d, ldx, y, shift, yshift, ws, st);
 }
 
+template <int PW, int CPW>
+void launch_direct(const GramPlan& pl, const float* X, int64_t n, int d, const float* y, const float* shift,
+                   float yshift, float* ws, hipStream_t st) {
+  const int Dpad = ((pl.D + 31) / 32) * 32;
+  const size_t lds = (size_t)kDStages * CPW * kDWaves * 1024 + (size_t)Dpad * (kDRows + 8) * 2;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gram_bf16d_kernel<PW, CPW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((gram_bf16d_kernel<PW, CPW>), dim3(pl.nblk), dim3(256), lds, st, X, n, d, y, shift, yshift,
+                     pl.tab, pl.npairs, Dpad, ws, pl.rows_per_unit);
+}
+
+// direct-to-LDS streaming plan: one resident block per CU, contiguous rows (ldx == d), d % 4 == 0, and the
+// staging ring + bf16 tile within 160 KB (d <= 108: 7 chunk rounds per wave)
+bool direct_ok(const float* X, int d, int64_t ldx, const float* shift) {
+  return ldx == d && d % 4 == 0 && d + 2 <= 128 && (d / 4 + 1 + kDWaves - 1) / kDWaves <= 7 &&
+         (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (reinterpret_cast<uintptr_t>(shift) & 15) == 0;
+}
+
+GramPlan make_direct_plan(int64_t n, int d) {
+  GramPlan pl = make_plan(n, d, true);
+  pl.ngroups = 1;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  int64_t nb = (n + 4095) / 4096;
+  if (nb > ncu) nb = ncu;
+  if (nb < 1) nb = 1;
+  pl.nblk = (int)nb;
+  const int64_t rpb = (n + nb - 1) / nb;
+  pl.rows_per_unit = (rpb + kDRows - 1) / kDRows * kDRows;
+  return pl;
+}
+
+template <int PW>
+void launch_direct_cpw(const GramPlan& pl, const float* X, int64_t n, int d, const float* y, const float* shift,
+                       float yshift, float* ws, hipStream_t st) {
+  switch ((d / 4 + 1 + kDWaves - 1) / kDWaves) {
+    case 1:
+    case 2: launch_direct<PW, 2>(pl, X, n, d, y, shift, yshift, ws, st); break;
+    case 3: launch_direct<PW, 3>(pl, X, n, d, y, shift, yshift, ws, st); break;
+    case 4: launch_direct<PW, 4>(pl, X, n, d, y, shift, yshift, ws, st); break;
+    case 5: launch_direct<PW, 5>(pl, X, n, d, y, shift, yshift, ws, st); break;
+    case 6: launch_direct<PW, 6>(pl, X, n, d, y, shift, yshift, ws, st); break;
+    default: launch_direct<PW, 7>(pl, X, n, d, y, shift, yshift, ws, st); break;
+  }
+}
+
 template <int P>
 void launch_f32(const GramPlan& pl, const float* X, int64_t n, int d, int64_t ldx, const float* y, const float* shift,
                 float yshift, float* ws, hipStream_t st) {
@@ -460,7 +676,19 @@ CDNA_API int cdna_gram(const float* X, int64_t n, int d, int64_t ldx, const floa
   if (d + 2 > 32 * 17) return (int)hipErrorInvalidValue;
   GramPlan pl = make_plan(n, d, bf16 != 0);
   if (pl.npairs > kMaxPairs) return (int)hipErrorInvalidValue;
-  if (bf16 && stream_ok(X, d, ldx, shift)) {
+  static const bool direct_on = [] {
+    const char* e = getenv("CDNAML_GRAM_DIRECT");
+    return !e || atoi(e) != 0;
+  }();
+  if (bf16 && direct_on && direct_ok(X, d, ldx, shift)) {
+    pl = make_direct_plan(n, d);
+    switch ((pl.npairs + kDWaves - 1) / kDWaves) {
+      case 1: launch_direct_cpw<1>(pl, X, n, d, y, shift, yshift, ws, st); break;
+      case 2: launch_direct_cpw<2>(pl, X, n, d, y, shift, yshift, ws, st); break;
+      case 3: launch_direct_cpw<3>(pl, X, n, d, y, shift, yshift, ws, st); break;
+      default: launch_direct_cpw<4>(pl, X, n, d, y, shift, yshift, ws, st); break;
+    }
+  } else if (bf16 && stream_ok(X, d, ldx, shift)) {
     pl = make_stream_plan(n, d);
     const int pw = (pl.npairs + 3) / 4;  // 4 waves share the tile pairs
     switch (pw) {

@@ -357,7 +357,7 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
 template <int BP>
 __global__ __launch_bounds__(512) void seg_hist_lane_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins8,
                                                             int row_bytes) {
-  constexpr int TH = 512, NW = TH / 64, U = 8;
+  constexpr int TH = 512, NW = TH / 64, U = 16;
   constexpr int PLANE = BP * 32;
   // static: the planes sit at a link-time-known LDS offset, so the cell address needs no base add
   __shared__ __attribute__((aligned(16))) unsigned long long h[4 * PLANE];  // [4][BP][32]
@@ -372,19 +372,16 @@ __global__ __launch_bounds__(512) void seg_hist_lane_kernel(const SegHistArgs a,
   dw = dw < dmax ? dw : dmax;
   const uint8_t* lbase = bins8 + 4 * dw;
   const uint32_t loff = (uint32_t)lq * 8u;
-  // software-pipelined: the next trip's records are in flight while this trip's bins arrive and its atomics
-  // run.  Record loads are unconditional (lane base + immediate offsets): the record buffer carries >= 2U
-  // readable records past its end (codes_compact pads it), and a trip past the chunk end zeroes the
-  // out-of-range records (row 0, weight 0) before they are used.
+  // Record loads are unconditional (lane base + immediate offsets): the record buffer carries >= 2U readable
+  // records past its end (codes_compact pads it), and a trip past the chunk end zeroes the out-of-range records
+  // (row 0, weight 0) before they are used.  U = 16 item pairs per trip: the kernel is bound by the random
+  // row-line gathers, so bytes in flight per CU set its speed (U = 8 with the next trip's records prefetched
+  // was measured equal).
   const uint64_t* __restrict__ recp = a.rec + start + half;
-  uint64_t rc[U];
-  int i0 = wid * 2 * U;
-  auto load_recs = [&](int i) {
+  for (int i0 = wid * 2 * U; i0 < len; i0 += NW * 2 * U) {
+    uint64_t rc[U];
 #pragma unroll
-    for (int p = 0; p < U; ++p) rc[p] = recp[i + 2 * p];
-  };
-  if (i0 < len) load_recs(i0);
-  for (; i0 < len; i0 += NW * 2 * U) {
+    for (int p = 0; p < U; ++p) rc[p] = recp[i0 + 2 * p];
     if (i0 + 2 * U > len) {  // wave-uniform: the chunk's last trip
 #pragma unroll
       for (int p = 0; p < U; ++p)
@@ -401,7 +398,6 @@ __global__ __launch_bounds__(512) void seg_hist_lane_kernel(const SegHistArgs a,
       const uint32_t qb = hi >> 7;  // q1 + 2^23
       add[p] = ((unsigned long long)(w << (kPackShift - 32)) << 32) + (unsigned long long)w * qb;
     }
-    if (i0 + NW * 2 * U < len) load_recs(i0 + NW * 2 * U);
 #pragma unroll
     for (int p = 0; p < U; ++p) {
 #pragma unroll
