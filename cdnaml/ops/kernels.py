@@ -1001,9 +1001,10 @@ def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_glob
 
 SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "1024"))
 # record histograms through the lane-feature kernel (seg_hist_lane_kernel: lanes own features, bin-major
-# conflict-free LDS planes, one v_perm per cell address); B <= 80 (planes <= 80 KB of LDS)
+# conflict-free LDS planes, one v_perm per cell address); B <= 80 (4 planes <= 80 KB of LDS), 80 < B <= 256:
+# seg_hist_lane4_kernel (64 features per block, a quarter-wave per item; CDNAML_SEG_WIDE=0 keeps the flat kernel)
 SEG_LANE = __import__("os").environ.get("CDNAML_SEG_LANE", "1") != "0"
-SEG_LANE_MAX_B = 80
+SEG_LANE_MAX_B = 256 if __import__("os").environ.get("CDNAML_SEG_WIDE", "1") != "0" else 80
 # records buffers carry REC_PAD readable entries past their end: the lane kernel's record loads are unconditional
 REC_PAD = 64
 

@@ -16,9 +16,11 @@
 //     that became leaves are dropped, so perm shrinks level by level.
 // Counts/sums are the same fixed-point integers as hist5 (bit-reproducible).
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
+typedef const __attribute__((address_space(4))) uint64_t cu64;  // constant address space: s_load when uniform
 constexpr int kSegThreads = 256;
 constexpr int kPackShift = 44;
 constexpr int kPackQ = 1 << 23;
@@ -377,11 +379,17 @@ __global__ __launch_bounds__(512) void seg_hist_lane_kernel(const SegHistArgs a,
   // (row 0, weight 0) before they are used.  U = 16 item pairs per trip: the kernel is bound by the random
   // row-line gathers, so bytes in flight per CU set its speed (U = 8 with the next trip's records prefetched
   // was measured equal).
-  const uint64_t* __restrict__ recp = a.rec + start + half;
+  // The wave's records are read through the scalar cache (constant address space, wave-uniform addresses:
+  // s_load) and each half selects its item -- rocprofv3 had the texture-address unit ~80 % busy with one
+  // 64-lane record load per item pair next to the gather; this leaves it the gathers alone (185.2 -> 181.0 ms).
+  cu64* crec = (cu64*)(uintptr_t)(a.rec + start);
   for (int i0 = wid * 2 * U; i0 < len; i0 += NW * 2 * U) {
     uint64_t rc[U];
 #pragma unroll
-    for (int p = 0; p < U; ++p) rc[p] = recp[i0 + 2 * p];
+    for (int p = 0; p < U; ++p) {
+      const uint64_t ra = crec[i0 + 2 * p], rb = crec[i0 + 2 * p + 1];
+      rc[p] = half ? rb : ra;
+    }
     if (i0 + 2 * U > len) {  // wave-uniform: the chunk's last trip
 #pragma unroll
       for (int p = 0; p < U; ++p)
@@ -414,6 +422,174 @@ __global__ __launch_bounds__(512) void seg_hist_lane_kernel(const SegHistArgs a,
     const int f = f0 + 4 * l + j;
     if (bn >= a.B || f >= a.d) continue;
     const unsigned long long v = h[c];
+    if (!v) continue;
+    const unsigned long long cnt = v >> kPackShift;
+    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+    atomicAdd(o, cnt);
+    atomicAdd(o + 1, (unsigned long long)sum);
+  }
+}
+
+// Quarter-wave record histogram for B <= 64 (the forest levels).  rocprofv3 on
+// seg_hist_lane_kernel at the headline: texture-address unit ~79 % busy, LDS
+// ~44 %, HBM ~2.8 TB/s -- the 64-lane address work of one dword gather per
+// item PAIR binds it (moving the record loads to the scalar cache gained only
+// 2.7 %).  Here a 16-lane quarter takes one item and lane l' gathers the 8-byte
+// word l' of the row (features f0 + 8 l' + j): one dwordx2 gather serves FOUR
+// items, half the address work per item.  The two items of a half-wave would
+// collide on bank pairs (same l', same bin parity), so each keeps its own copy
+// of the cells, interleaved per bin: [8 planes j][BP][2 copies][16 lanes] u64,
+// cell byte address bin << 8 | copy << 7 | l' << 3 -- one v_perm_b32 as in the
+// lane kernel, and the 32 lanes of a half always hit 32 distinct bank pairs.
+// The flush adds the copies.  LDS = BP * 2 KB (80 KB at 40 bins: two
+// 1024-thread blocks per CU).
+template <int BP>
+__global__ __launch_bounds__(1024, 2) void seg_hist_lane8_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins8,
+                                                                 int row_bytes) {
+  constexpr int TH = 1024, NW = TH / 64, U = 8;
+  constexpr int PLANE = BP * 32;  // u64 cells per feature plane j
+  __shared__ __attribute__((aligned(16))) unsigned long long h[8 * PLANE];  // [8][BP][2][16]
+  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
+  const int f0 = blockIdx.y * 128;
+  for (int i = threadIdx.x; i < 8 * PLANE; i += TH) h[i] = 0ull;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, qt = lane >> 4, lq = lane & 15;
+  const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  int qw = (f0 >> 3) + lq;  // the lane's 8-byte word of the row
+  const int qmax = (row_bytes >> 3) - 1;
+  qw = qw < qmax ? qw : qmax;
+  const uint8_t* lbase = bins8 + 8 * qw;
+  const uint32_t loff = (uint32_t)(qt & 1) * 128u + (uint32_t)lq * 8u;  // copy << 7 | l' << 3
+  static_assert(4 * U <= 64, "record over-read must stay within REC_PAD");
+  // per-quarter vector record loads (scalar-cache records with a 4-way select: 174.6 vs 170.8 ms headline)
+  const uint64_t* __restrict__ recp = a.rec + start + qt;
+  for (int i0 = wid * 4 * U; i0 < len; i0 += NW * 4 * U) {
+    uint64_t rc[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) rc[p] = recp[i0 + 4 * p];
+    if (i0 + 4 * U > len) {
+#pragma unroll
+      for (int p = 0; p < U; ++p)
+        if (i0 + 4 * p + qt >= len) rc[p] = 0ull;
+    }
+    uint2 x[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t row = (uint32_t)rc[p] & 0x7FFFFFFFu;
+      x[p] = *reinterpret_cast<const uint2*>(lbase + (uint64_t)row * (uint64_t)row_bytes);
+    }
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t lo = (uint32_t)rc[p], hi = (uint32_t)(rc[p] >> 32);
+      const uint32_t w = __builtin_amdgcn_alignbit(hi, lo, 31) & 0xFFu;
+      const unsigned long long add = ((unsigned long long)(w << (kPackShift - 32)) << 32) +
+                                     (unsigned long long)w * (hi >> 7);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t off = __builtin_amdgcn_perm(loff, j < 4 ? x[p].x : x[p].y, 0x0C0C0004u | ((uint32_t)(j & 3) << 8));
+        atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h) + off) + j * PLANE, add);
+      }
+    }
+  }
+  __syncthreads();
+  // flush: thread -> (plane j, bin, lane l'), both copies summed
+  for (int c = threadIdx.x; c < 8 * BP * 16; c += TH) {
+    const int l = c & 15, rest = c >> 4;
+    const int bn = rest % BP, j = rest / BP;
+    const int f = f0 + 8 * l + j;
+    if (bn >= a.B || f >= a.d) continue;
+    const unsigned long long* cell = h + j * PLANE + bn * 32 + l;
+    const unsigned long long v0 = cell[0], v1 = cell[16];
+    const unsigned long long cnt = (v0 >> kPackShift) + (v1 >> kPackShift);
+    if (!cnt) continue;
+    const unsigned long long m = (1ull << kPackShift) - 1ull;
+    const long long sum = (long long)((v0 & m) + (v1 & m)) - (long long)kPackQ * (long long)cnt;
+    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+    atomicAdd(o, cnt);
+    atomicAdd(o + 1, (unsigned long long)sum);
+  }
+}
+
+// Wide-bin lane variant (80 < B <= 256: XGBoost-style 256-bin boosting).  Four
+// [BP][32] u64 planes of 256 bins would need 256 KB of LDS, so a block covers
+// 64 features: each 16-lane QUARTER of a wave takes one item and lane l' owns
+// the 4 features of row dword l' (one dword gather), so one record load + one
+// gather serve four items.  A first version (one item per 32-lane half, two
+// features per lane, conflict-free [2][BP][32] planes) had rocprofv3 show the
+// texture-address unit ~80 % busy (one record load + one u16 gather per PAIR
+// of items) with LDS ~20 % busy; this one halves the address work and costs
+// 784.5 -> 670.8 ms per 20 GBDT trees.  Planes [4][BP][16] u64 (128 KB at
+// BP = 256, one 1024-thread block per CU); the two items of a half-wave collide
+// on a bank pair when their bins at the same l' share parity, so an atomic
+// costs ~2 passes -- LDS has the headroom.  The cell byte offset
+// bin << 7 | l' << 3 (+ plane) is a bfe and an lshl_or.
+// XCD-aware 1-D grid: block b runs on XCD b % 8, and the ny feature blocks of
+// chunk c are slots k = (c / 8) * ny + y of XCD c % 8 -- dispatched back to
+// back, so the second half of each gathered 128-byte row line hits the L2 the
+// first half filled (the x-major 2-D order re-fetched every line: 867 -> 789 ms
+// per 20 trees when fixed).
+template <int BP, int U>
+__global__ __launch_bounds__(1024) void seg_hist_lane4_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins8,
+                                                              int row_bytes, int nwork, int ny) {
+  constexpr int TH = 1024, NW = TH / 64;
+  constexpr int PLANE = BP * 16;
+  static_assert(BP == 128 || BP == 256, "four planes of 128 or 256 bins");
+  __shared__ __attribute__((aligned(16))) unsigned long long h[4 * PLANE];  // [4][BP][16]
+  const int b = blockIdx.x, k = b >> 3;
+  const int c = (k / ny) * 8 + (b & 7), fy = k - (k / ny) * ny;
+  if (c >= nwork) return;
+  const int start = a.work[3 * c], len = a.work[3 * c + 1], slot = a.work[3 * c + 2];
+  const int f0 = fy * 64;
+  for (int i = threadIdx.x; i < 4 * PLANE; i += TH) h[i] = 0ull;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, qt = lane >> 4, lq = lane & 15;
+  const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  int dw = (f0 >> 2) + lq;
+  const int dmax = (row_bytes >> 2) - 1;
+  dw = dw < dmax ? dw : dmax;
+  const uint8_t* lbase = bins8 + 4 * dw;
+  const uint32_t loff = (uint32_t)lq * 8u;
+  // unconditional record loads reach 4U - 1 records past the chunk end: REC_PAD (64) covers U <= 16
+  static_assert(4 * U <= 64, "record over-read must stay within REC_PAD");
+  // per-quarter vector record loads (scalar-cache records with a 4-way select measured 743.6 vs 671.1 ms per 20
+  // GBDT trees: four selects per item and the lgkmcnt drain of the atomics before every trip)
+  const uint64_t* __restrict__ recp = a.rec + start + qt;
+  for (int i0 = wid * 4 * U; i0 < len; i0 += NW * 4 * U) {
+    uint64_t rc[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) rc[p] = recp[i0 + 4 * p];
+    if (i0 + 4 * U > len) {
+#pragma unroll
+      for (int p = 0; p < U; ++p)
+        if (i0 + 4 * p + qt >= len) rc[p] = 0ull;
+    }
+    uint32_t x[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t row = (uint32_t)rc[p] & 0x7FFFFFFFu;
+      x[p] = *reinterpret_cast<const uint32_t*>(lbase + (uint64_t)row * (uint64_t)row_bytes);
+    }
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t lo = (uint32_t)rc[p], hi = (uint32_t)(rc[p] >> 32);
+      const uint32_t w = __builtin_amdgcn_alignbit(hi, lo, 31) & 0xFFu;
+      const unsigned long long add = ((unsigned long long)(w << (kPackShift - 32)) << 32) +
+                                     (unsigned long long)w * (hi >> 7);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t off = (__builtin_amdgcn_ubfe(x[p], 8u * j, 8u) << 7) | loff;  // bin << 7 | l' << 3
+        atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h) + off) + j * PLANE, add);
+      }
+    }
+  }
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < 4 * PLANE; cc += TH) {
+    const int b_lo = cc & 7, l = (cc >> 3) & 15, j = (cc >> 7) & 3, b_hi = cc >> 9;
+    const int bn = b_hi * 8 + b_lo;
+    const int f = f0 + 4 * l + j;
+    if (bn >= a.B || f >= a.d) continue;
+    const unsigned long long v = h[j * PLANE + bn * 16 + l];
     if (!v) continue;
     const unsigned long long cnt = v >> kPackShift;
     const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
@@ -934,7 +1110,7 @@ __global__ __launch_bounds__(256) void bins_row_major_kernel(const uint64_t* __r
 
 // mode bit0: packed (no v0; count | sum in one atomic); bit1: per-row weights wp present;
 // bit4: `perm` holds packed 8-byte item records (row | w << 31 | (q1 + 2^23) << 39; flat kernel only).
-// bit7 (with bit4 and bit2, B <= 80): lane-feature kernel (seg_hist_lane_kernel).
+// bit7 (with bit4 and bit2, B <= 256): lane-feature kernels (seg_hist_lane_kernel, B > 80: seg_hist_lane4_kernel).
 // bit2: bins are row-major [n][G] words (seg_hist_flat_kernel when packed and all groups fit 128 KB of LDS,
 // else seg_hist_rm_kernel); bit3: force seg_hist_rm_kernel.
 // work: [nwork][3] {start, len, slot}; grid = nwork x ceil(d / 8).
@@ -947,14 +1123,33 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
   a.rs = rm_stride;
   const bool packed = (mode & 1) != 0, has_w = (mode & 2) != 0;
   if ((mode & 128) && (mode & 16) && (mode & 4) && packed) {
-    // lane-feature kernel: 128 features per block (4 byte planes of BP >= B bins x 32 lanes, BP KB of LDS)
-    if (B > 80) return (int)hipErrorInvalidValue;
+    // lane-feature kernel: 128 features per block (4 byte planes of BP >= B bins x 32 lanes, BP KB of LDS);
+    // 80 < B <= 256: 64 features per block, a quarter-wave per item (seg_hist_lane4_kernel)
+    if (B > 256) return (int)hipErrorInvalidValue;
     const int G = (d + 7) / 8;
     a.rec = reinterpret_cast<const uint64_t*>(perm);
     const int row_bytes = (rm_stride ? rm_stride : G) * 8;
-    const dim3 grid((unsigned)nwork, (unsigned)((d + 127) / 128));
     const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bins);
+    if (B > 80) {
+      const int ny = (d + 63) / 64;
+      const dim3 grid2((unsigned)(((nwork + 7) / 8) * 8 * ny));
+      auto launch2 = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid2, dim3(1024), 0, st, a, b8, row_bytes, nwork, ny);
+      };
+      if (B <= 128) launch2(seg_hist_lane4_kernel<128, 16>);
+      else launch2(seg_hist_lane4_kernel<256, 16>);
+      return (int)hipGetLastError();
+    }
+    const dim3 grid((unsigned)nwork, (unsigned)((d + 127) / 128));
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(512), 0, st, a, b8, row_bytes); };
+    static const bool lane8 = [] { const char* e = getenv("CDNAML_SEG_LANE8"); return !(e && atoi(e) == 0); }();
+    if (lane8 && B <= 64) {
+      auto launch8 = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(1024), 0, st, a, b8, row_bytes); };
+      if (B <= 32) launch8(seg_hist_lane8_kernel<32>);
+      else if (B <= 40) launch8(seg_hist_lane8_kernel<40>);
+      else launch8(seg_hist_lane8_kernel<64>);
+      return (int)hipGetLastError();
+    }
     if (B <= 32) launch(seg_hist_lane_kernel<32>);
     else if (B <= 40) launch(seg_hist_lane_kernel<40>);
     else if (B <= 64) launch(seg_hist_lane_kernel<64>);

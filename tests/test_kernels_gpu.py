@@ -972,11 +972,13 @@ def test_relational_on_hash_kernels_match_pandas(dev):
     assert df.dropDuplicates(["k", "s"]).count() == len(pdf.drop_duplicates(["k", "s"]))
 
 
-@pytest.mark.parametrize("d,B", [(21, 40), (100, 40), (130, 64), (100, 80), (64, 32), (257, 17)])
+@pytest.mark.parametrize("d,B", [(21, 40), (100, 40), (130, 64), (100, 80), (64, 32), (257, 17),
+                                 (100, 100), (100, 256), (130, 200), (37, 256), (64, 128)])
 def test_seg_hist_lane_matches_flat(dev, d, B, monkeypatch):
-    """K5 lane-feature kernel (lanes own features, bin-major LDS plane) gives exactly the int64 fixed-point
+    """K5 lane-feature kernels (lanes own features, bin-major LDS plane) give exactly the int64 fixed-point
     sums of the flat (row, group)-pair kernel: partial 64-lane feature halves, two feature blocks (d > 128),
-    B = 80, several chunks per segment and zero-weight records."""
+    B = 80, several chunks per segment and zero-weight records; 80 < B <= 256 runs the 64-feature
+    quarter-wave variant (seg_hist_lane4_kernel, BP = 128 / 256)."""
     T, n = 6, 150000
     rng = np.random.default_rng(d * 7 + B)
     loc = rng.integers(0, 3, (T, n))
