@@ -1432,6 +1432,9 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
 
 
 COMPACT_W = __import__("os").environ.get("CDNAML_COMPACT_W", "1") != "0"
+# record compaction without a host round trip before the scatter (device segment starts, totals copied back
+# behind the scatter kernel)
+COMPACT_DEFER = __import__("os").environ.get("CDNAML_COMPACT_DEFER", "1") != "0"
 
 
 def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, rec_scale=None):
@@ -1460,15 +1463,40 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
     # per-(tree, node) exclusive scan over the waves in place + node totals, one launch
     tot = torch.empty((T, KB), dtype=torch.int64, device=dev)
     _lib.check(L.cdna_wave_scan(_ptr(wcnt), T, Wv, KB, _ptr(tot), _stream(dev)), "cdna_wave_scan")
-    tot_h = tot.cpu().numpy()
-    lens = np.zeros(S, dtype=np.int64)
     sl = (first_slot[:, None] + np.arange(KB)[None, :])        # slot of (t, k)
     valid = np.arange(KB)[None, :] < nb_t[:, None]
+    rec = rec_scale is not None
+    if rec and COMPACT_DEFER and n * T < 2 ** 31:
+        # No host round trip before the scatter: slots are numbered tree-major with k inside the tree and
+        # (t, k) pairs that are not built count 0, so the segment starts are the exclusive prefix of the
+        # [T][KB] totals in place -- computed on the device.  The records buffer is sized by the n * T bound
+        # (one item per (row, tree)); the totals come back through pinned memory while the scatter runs, and the
+        # host builds the segment table (and the caller its histogram work list) behind it instead of idling
+        # the GPU for the D2H copy + host work + H2D copy of every level.
+        flat = tot.view(-1)
+        kstart_t = torch.cumsum(flat, 0) - flat
+        tot_p = torch.empty((T, KB), dtype=torch.int64, pin_memory=True)
+        tot_p.copy_(tot, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        perm = torch.empty(n * T + REC_PAD, dtype=torch.int64, device=dev)
+        _lib.check(L.cdna_codes_compact_w(2, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
+                                          per_wave, Wv, None, _ptr(wcnt), None, None, None, None, _ptr(perm),
+                                          float(rec_scale), _ptr(kstart_t), _stream(dev)),
+                   "cdna_codes_compact_w(scatter)")
+        ev.synchronize()
+        tot_h = tot_p.numpy()
+        lens = np.zeros(S, dtype=np.int64)
+        lens[sl[valid]] = tot_h[valid]
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if S else np.zeros(0, np.int64)
+        total = int(lens.sum())
+        return perm[:total], None, None, None, np.stack([starts, lens], 1)
+    tot_h = tot.cpu().numpy()
+    lens = np.zeros(S, dtype=np.int64)
     lens[sl[valid]] = tot_h[valid]
     starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if S else np.zeros(0, np.int64)
     total = int(lens.sum())
     assert total < 2 ** 31
-    rec = rec_scale is not None
     if rec:
         perm = torch.empty(total + REC_PAD, dtype=torch.int64, device=dev)[:total]  # readable tail
         v1p = v0p = wp = None

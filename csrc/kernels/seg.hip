@@ -906,10 +906,10 @@ __global__ __launch_bounds__(256) void codes_compact_kernel(const CompactArgs a)
 // peeling kernel: ~80 wave instructions per 64 records and 71 % of wave time
 // waiting (3.8 + 10.3 ms per level at 1e8 x 20 trees).  Here each wave owns a
 // fixed contiguous row range and counts its records per built node in
-// registers (pass 1 writes [T][waves][KB] counts, no atomics); the host scans
-// the counts into per-wave output offsets; pass 2 re-reads the range and
-// ranks a lane's (up to 4) records per node with 3 ballots (the count 0..4 in
-// binary).  Output order is the row order: stable and deterministic.
+// registers (pass 1 writes [T][waves][KB] counts, no atomics); a device scan
+// turns the counts into per-wave output offsets; pass 2 re-reads the range and
+// ranks the lanes' records per node with ballots.  Output order is the row
+// order: stable and deterministic.
 struct CompactWArgs {
   const uint16_t* codes;
   int64_t n;
@@ -933,15 +933,13 @@ struct CompactWArgs {
   const int64_t* kstart;  // pass 2, optional: [T][KB] segment start added to the per-wave offsets
 };
 
-__device__ __forceinline__ bool v_aligned(const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
-template <int KB, bool SCATTER>
-__global__ __launch_bounds__(256) void codes_compact_w_kernel(const CompactWArgs a) {
+// Pass 1: per-(tree, wave, built node) record counts.
+template <int KB>
+__global__ __launch_bounds__(256) void codes_count_w_kernel(const CompactWArgs a) {
   __shared__ int s_k[256];
   // XCD-aware block -> (row chunk, tree) map: block b runs on XCD b % 8, and the T blocks of one row chunk are
-  // consecutive slots of ONE XCD, so they run together and share that XCD's L2 copy of the chunk's labels
-  // (v1 is the same for every tree: with tree-major grids it crossed HBM once per tree, ~8 GB per level
-  // at 1e8 rows x 20 trees)
+  // consecutive slots of ONE XCD (the same map as the scatter pass, whose blocks share that XCD's L2 copy of
+  // the chunk's labels: v1 is the same for every tree)
   const int nch = (a.Wv + 3) / 4;
   const int xcd = (int)(blockIdx.x & 7u), slot = (int)(blockIdx.x >> 3);
   const int qc = slot / a.T, t = slot - qc * a.T;
@@ -949,7 +947,7 @@ __global__ __launch_bounds__(256) void codes_compact_w_kernel(const CompactWArgs
   if (chunk >= nch) return;  // block-uniform
   const int tf = a.tfirst[t];
   const int nloc = (t + 1 < a.T ? a.tfirst[t + 1] : a.A) - tf;
-  for (int i = threadIdx.x; i < 256; i += 256) s_k[i] = (i < nloc && i < 255) ? a.kmap[tf + i] : -1;
+  s_k[threadIdx.x] = (threadIdx.x < nloc && threadIdx.x < 255) ? a.kmap[tf + threadIdx.x] : -1;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int w = chunk * 4 + (threadIdx.x >> 6);
@@ -960,15 +958,12 @@ __global__ __launch_bounds__(256) void codes_compact_w_kernel(const CompactWArgs
   const int64_t cb = ((int64_t)t * a.Wv + w) * KB;
   int acc[KB];
 #pragma unroll
-  for (int k = 0; k < KB; ++k)
-    acc[k] = SCATTER ? a.woff[cb + k] + (a.kstart ? (int)a.kstart[(int64_t)t * KB + k] : 0) : 0;
-  // 2 x 4 records per lane per trip, codes (and, in pass 2, the statistics) loaded up front as vectors:
-  // the one-group loop waited on each trip's dependent load chain (codes -> LDS map -> v1 -> store)
-  const bool vec = (a.n & 3) == 0 && (reinterpret_cast<uintptr_t>(a.codes) & 7u) == 0 && v_aligned(a.v1) && (a.v0 == nullptr || v_aligned(a.v0));
+  for (int k = 0; k < KB; ++k) acc[k] = 0;
+  // 2 x 4 codes per lane per trip, loaded up front as 8-byte vectors
+  const bool vec = (a.n & 3) == 0 && (reinterpret_cast<uintptr_t>(a.codes) & 7u) == 0;
   constexpr int NG = 2;
   for (int64_t rb = r_begin; rb < r_end; rb += 256 * NG) {
     uint32_t cc[NG][4];
-    float x1[NG][4], x0[NG][4];
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
       const int64_t r = rb + q * 256 + lane * 4;
@@ -978,79 +973,94 @@ __global__ __launch_bounds__(256) void codes_compact_w_kernel(const CompactWArgs
         cc[q][1] = c4.x >> 16;
         cc[q][2] = c4.y & 0xFFFFu;
         cc[q][3] = c4.y >> 16;
-        if (SCATTER) {
-          const float4 f = *reinterpret_cast<const float4*>(a.v1 + r);
-          x1[q][0] = f.x, x1[q][1] = f.y, x1[q][2] = f.z, x1[q][3] = f.w;
-          if (a.v0) {
-            const float4 g = *reinterpret_cast<const float4*>(a.v0 + r);
-            x0[q][0] = g.x, x0[q][1] = g.y, x0[q][2] = g.z, x0[q][3] = g.w;
-          }
-        }
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool ok = r + j < r_end;
-          cc[q][j] = ok ? (uint32_t)rec[r + j] : 0xFFu;
-          if (SCATTER) {
-            x1[q][j] = ok ? a.v1[r + j] : 0.f;
-            if (a.v0) x0[q][j] = ok ? a.v0[r + j] : 0.f;
-          }
-        }
+        for (int j = 0; j < 4; ++j) cc[q][j] = r + j < r_end ? (uint32_t)rec[r + j] : 0xFFu;
       }
     }
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
-    const int64_t r = rb + q * 256 + lane * 4;
-    int kk[4];
+      int kk[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) kk[j] = s_k[cc[q][j] & 0xFFu];
-    if (!SCATTER) {
+      for (int j = 0; j < 4; ++j) kk[j] = s_k[cc[q][j] & 0xFFu];
 #pragma unroll
-      for (int k = 0; k < KB; ++k)
-        acc[k] += (kk[0] == k) + (kk[1] == k) + (kk[2] == k) + (kk[3] == k);
-    } else {
-      int pos[4] = {-1, -1, -1, -1};
-#pragma unroll
-      for (int k = 0; k < KB; ++k) {
-        const int c = (kk[0] == k) + (kk[1] == k) + (kk[2] == k) + (kk[3] == k);
-        const uint64_t b0 = __builtin_amdgcn_ballot_w64((c & 1) != 0);
-        const uint64_t b1 = __builtin_amdgcn_ballot_w64((c & 2) != 0);
-        const uint64_t b2 = __builtin_amdgcn_ballot_w64((c & 4) != 0);
-        if ((b0 | b1 | b2) == 0ull) continue;  // wave-uniform
-        auto below = [&](uint64_t m) {
-          return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        };
-        int p = acc[k] + below(b0) + 2 * below(b1) + 4 * below(b2);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (kk[j] == k) pos[j] = p++;
-        acc[k] += __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (pos[j] < 0) continue;
-        if (a.rec_out) {
-          int q1 = (int)rintf(x1[q][j] * a.qs1);
-          q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
-          a.rec_out[pos[j]] = (uint64_t)(r + j) | ((uint64_t)(cc[q][j] >> 8) << 31) |
-                              ((uint64_t)(uint32_t)(q1 + kPackQ) << 39);
-          continue;
-        }
-        a.perm_out[pos[j]] = (int)(r + j);
-        a.v1_out[pos[j]] = x1[q][j];
-        if (a.v0) a.v0_out[pos[j]] = x0[q][j];
-        a.w_out[pos[j]] = (uint8_t)(cc[q][j] >> 8);
-      }
-    }
+      for (int k = 0; k < KB; ++k) acc[k] += (kk[0] == k) + (kk[1] == k) + (kk[2] == k) + (kk[3] == k);
     }
   }
-  if (!SCATTER) {
 #pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      int v = acc[k];
+  for (int k = 0; k < KB; ++k) {
+    int v = acc[k];
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      if (lane == 0) a.wcnt[cb + k] = v;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) a.wcnt[cb + k] = v;
+  }
+}
+
+// Pass 2 with lane-strided rows.  The first version gave each lane 4
+// consecutive rows (ranked with 3 ballots per node), so the lanes' output
+// positions were ~4 records apart and every 8-byte store instruction spread
+// over ~16 partially written 128-byte lines (level-0 scatter: 14 GB in 5.4 ms
+// = 2.7 TB/s; all levels 20.5 ms per headline step).  Here trip row j of lane
+// l is rb + 64 j + l: one ballot per (j, node) ranks the lanes, so each store
+// instruction writes one contiguous run per node (14.6 ms per step).
+template <int KB>
+__global__ __launch_bounds__(256) void codes_scatter_w_kernel(const CompactWArgs a) {
+  __shared__ int s_k[256];
+  const int nch = (a.Wv + 3) / 4;
+  const int xcd = (int)(blockIdx.x & 7u), slot = (int)(blockIdx.x >> 3);
+  const int qc = slot / a.T, t = slot - qc * a.T;
+  const int chunk = qc * 8 + xcd;
+  if (chunk >= nch) return;  // block-uniform
+  const int tf = a.tfirst[t];
+  const int nloc = (t + 1 < a.T ? a.tfirst[t + 1] : a.A) - tf;
+  s_k[threadIdx.x] = (threadIdx.x < nloc && threadIdx.x < 255) ? a.kmap[tf + threadIdx.x] : -1;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int w = chunk * 4 + (threadIdx.x >> 6);
+  if (w >= a.Wv) return;
+  const int64_t r_begin = (int64_t)w * a.per_wave;
+  const int64_t r_end = r_begin + a.per_wave < a.n ? r_begin + a.per_wave : a.n;
+  const uint16_t* rec = a.codes + (int64_t)t * a.n;
+  const int64_t cb = ((int64_t)t * a.Wv + w) * KB;
+  int acc[KB];
+#pragma unroll
+  for (int k = 0; k < KB; ++k) acc[k] = a.woff[cb + k] + (a.kstart ? (int)a.kstart[(int64_t)t * KB + k] : 0);
+  constexpr int NJ = 8;
+  for (int64_t rb = r_begin; rb < r_end; rb += 64 * NJ) {
+    uint32_t cc[NJ];
+    float x1[NJ], x0[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t r = rb + j * 64 + lane;
+      const bool ok = r < r_end;
+      cc[j] = ok ? (uint32_t)rec[r] : 0xFFu;
+      x1[j] = ok ? a.v1[r] : 0.f;
+      x0[j] = (ok && a.v0) ? a.v0[r] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int kk = s_k[cc[j] & 0xFFu];
+      int pos = -1;
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(kk == k);
+        if (m == 0ull) continue;  // wave-uniform
+        if (kk == k)
+          pos = acc[k] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        acc[k] += __builtin_popcountll(m);
+      }
+      if (pos < 0) continue;
+      const int64_t r = rb + j * 64 + lane;
+      if (a.rec_out) {
+        int q1 = (int)rintf(x1[j] * a.qs1);
+        q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+        a.rec_out[pos] = (uint64_t)r | ((uint64_t)(cc[j] >> 8) << 31) | ((uint64_t)(uint32_t)(q1 + kPackQ) << 39);
+      } else {
+        a.perm_out[pos] = (int)r;
+        a.v1_out[pos] = x1[j];
+        if (a.v0) a.v0_out[pos] = x0[j];
+        a.w_out[pos] = (uint8_t)(cc[j] >> 8);
+      }
     }
   }
 }
@@ -1282,11 +1292,11 @@ CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64
     else hipLaunchKernelGGL(k2, grid, dim3(256), 0, st, a);
   };
   switch (KB) {
-    case 1: go(codes_compact_w_kernel<1, false>, codes_compact_w_kernel<1, true>); break;
-    case 2: go(codes_compact_w_kernel<2, false>, codes_compact_w_kernel<2, true>); break;
-    case 4: go(codes_compact_w_kernel<4, false>, codes_compact_w_kernel<4, true>); break;
-    case 8: go(codes_compact_w_kernel<8, false>, codes_compact_w_kernel<8, true>); break;
-    case 16: go(codes_compact_w_kernel<16, false>, codes_compact_w_kernel<16, true>); break;
+    case 1: go(codes_count_w_kernel<1>, codes_scatter_w_kernel<1>); break;
+    case 2: go(codes_count_w_kernel<2>, codes_scatter_w_kernel<2>); break;
+    case 4: go(codes_count_w_kernel<4>, codes_scatter_w_kernel<4>); break;
+    case 8: go(codes_count_w_kernel<8>, codes_scatter_w_kernel<8>); break;
+    case 16: go(codes_count_w_kernel<16>, codes_scatter_w_kernel<16>); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();

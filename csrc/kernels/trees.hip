@@ -213,127 +213,169 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// binize v4 (d <= 128, d % 4 == 0, 16-byte aligned rows).  v2 spent ~72 VALU
-// lane-ops per value (rocprofv3: VALU-bound with half the wave time waiting on
-// memory): every value went HBM -> registers -> LDS tile -> registers, and each
-// search step carried a bound test.  v4:
-//   * thread task = (row, quad q): one float4 straight from HBM (a row's quads
-//     are 25 consecutive lanes), 4 searches in lockstep, one dword of bins;
-//   * thresholds in LDS padded with +inf to 2^steps entries per feature and a
-//     feature stride of 2^steps + 1 words (the first step's 32 lanes of a row
-//     read 32 different banks), so a step is add / read / compare / select;
-//   * the 32 x 32-dword bins tile goes through 4 KB of LDS once, then leaves as
-//     16-byte row-major stores (128-byte padded rows, padding zeroed) and
-//     256-byte column-major runs of 32 rows per 8-feature group;
-//   * the next tile's float4s are loaded before this tile's searches.
+// binize v5 (d <= 128, d % 4 == 0, 16-byte aligned rows).  v4 (git history:
+// float4 tasks, skewed +inf-padded tables, 32-row bins tile; 23.8 ms at the
+// headline vs 20.9 ms for v5) put the 32 quads
+// of one row on the 32 lanes of a ds_read group, so every search step read 32
+// different feature tables: the first step was a 4-way bank conflict (feature
+// stride 65 = 1 mod 32 banks, 4 features per quad) and the later steps random
+// ones.  v5 turns the task around:
+//   * a wave owns (tile of 64 rows, group g of 8 features): lane = row, so all
+//     lanes of a ds_read group search the SAME 8 tables.  Step s reads at most
+//     2^(STEPS-1-s) distinct entries of a table (broadcast), at most 2-way
+//     conflicts, and the table offsets are wave-uniform (scalar registers);
+//   * the row's two float4s of the group come straight from HBM (the G waves of
+//     a block read the same 64 rows together, so the 128-byte lines are shared
+//     in L1/L2), the next tile's float4s are loaded before this tile's search;
+//   * the column-major word out[g][r] leaves from registers (512-byte runs);
+//     the row-major copy goes through a [64][17] u64 LDS tile (odd pitch:
+//     conflict-free 8-byte writes) and leaves as 16-byte stores of whole
+//     128-byte rows, padding words zeroed once.
+// Block = G waves (one per 8-feature group), persistent over row tiles.
 // ---------------------------------------------------------------------------
-template <int STEPS>
-__global__ __launch_bounds__(256) void binize4_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
-                                                      const float* __restrict__ thr, const int* __restrict__ nthr,
-                                                      int tmax, int miss_on, float miss_val,
-                                                      uint64_t* __restrict__ out, uint64_t* __restrict__ rm, int Gs) {
-  extern __shared__ __attribute__((aligned(16))) float smf4[];
-  constexpr int R = 32;  // rows per tile
-  constexpr int P = 1 << STEPS, TS = P + 1;
-  float* sthr = smf4;                                                      // [d][TS]
-  int* snt = reinterpret_cast<int*>(sthr + (size_t)d * TS);                // [d]
-  uint32_t* tile = reinterpret_cast<uint32_t*>(snt + ((d + 3) & ~3));      // [R][32]
-  for (int i = threadIdx.x; i < d * TS; i += 256) {
-    const int f = i / TS, c = i - f * TS;
+template <int STEPS, bool STAGE>
+__global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                       const float* __restrict__ thr, const int* __restrict__ nthr,
+                                                       int tmax, int miss_on, float miss_val,
+                                                       uint64_t* __restrict__ out, uint64_t* __restrict__ rm, int Gs) {
+  extern __shared__ __attribute__((aligned(16))) float smf5[];
+  constexpr int P = 1 << STEPS, RT = 64, TP = 17;
+  float* sthr = smf5;                                                          // [d][P]
+  uint64_t* tile = reinterpret_cast<uint64_t*>(sthr + (size_t)((d * P + 3) & ~3));  // [RT][TP]
+  // STAGE: the X tile [RT][dp] goes HBM -> registers (coalesced float4s of whole rows) -> LDS; a lane then reads
+  // its row's 8 features as two ds_read_b128 (dp / 4 odd: 16 rows of a lane group hit 16 distinct bank quads)
+  const int dp = ((d >> 2) & 1) ? d : d + 4;
+  float* xt = reinterpret_cast<float*>(tile + RT * TP);
+  for (int i = threadIdx.x; i < d * P; i += blockDim.x) {
+    const int f = i >> STEPS, c = i & (P - 1);
     sthr[i] = (c < nthr[f] && c < tmax) ? thr[(size_t)f * tmax + c] : __builtin_inff();
   }
-  for (int i = threadIdx.x; i < d; i += 256) snt[i] = nthr[i];
-  __syncthreads();
-  const int G = (d + 7) / 8;
+  if (rm)
+    for (int i = threadIdx.x; i < RT * TP; i += blockDim.x) tile[i] = 0ull;  // words g >= G stay 0 (row padding)
+  const int G = (d + 7) >> 3;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int Q = d >> 2;
-  const int q = threadIdx.x & 31, rsub = threadIdx.x >> 5;  // task k: row k * 8 + rsub, quad q
-  const bool qok = q < Q;
-  // per-quad constants: feature table offsets (entry cand - 1 of feature 4q + j), counts
-  int toff[4], nt[4];
+  const bool hi_ok = 2 * g + 1 < Q;  // the group's second quad exists
+  int nt[8], fb[8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int f = qok ? 4 * q + j : 0;
-    toff[j] = f * TS - 1;
-    nt[j] = snt[f];
+  for (int j = 0; j < 8; ++j) {
+    const int f = 8 * g + j < d ? 8 * g + j : d - 1;
+    nt[j] = __builtin_amdgcn_readfirstlane(nthr[f]);
+    fb[j] = f * P - 1;  // entry cand - 1 of feature f
   }
-  const int64_t stride = (int64_t)gridDim.x * R;
-  float4 pre[4];
-  // unconditional float4 loads in float4 units (alignment known): rows past n re-read row n - 1, quads past
-  // Q re-read quad Q - 1 (their bins are masked / their rows not stored)
+  __syncthreads();
   const float4* __restrict__ X4 = reinterpret_cast<const float4*>(X);
   const int64_t ldx4 = ldx >> 2;
-  const int qc = qok ? q : Q - 1;
-  auto fetch = [&](int64_t r0) {
+  const int64_t ntiles = (n + RT - 1) / RT;
+  auto search = [&](float (&x)[8]) -> uint64_t {
+    int lo[8];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      int64_t r = r0 + k * 8 + rsub;
-      r = r < n ? r : n - 1;
-      pre[k] = X4[r * ldx4 + qc];
+    for (int j = 0; j < 8; ++j) {
+      // XGBoost missing values (NaN or == missing) -> -inf -> bin 0 (thresholds start at -FLT_MAX)
+      if (miss_on && (x[j] != x[j] || x[j] == miss_val)) x[j] = -__builtin_inff();
+      lo[j] = 0;
     }
-  };
-  if ((int64_t)blockIdx.x * R < n) fetch((int64_t)blockIdx.x * R);
-  for (int64_t r0 = (int64_t)blockIdx.x * R; r0 < n; r0 += stride) {
-    float x[4][4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      x[k][0] = pre[k].x; x[k][1] = pre[k].y; x[k][2] = pre[k].z; x[k][3] = pre[k].w;
-    }
-    if (r0 + stride < n) fetch(r0 + stride);
-    int lo[4][4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        // XGBoost missing values (NaN or == missing) -> -inf -> bin 0 (thresholds start at -FLT_MAX)
-        if (miss_on && (x[k][j] != x[k][j] || x[k][j] == miss_val)) x[k][j] = -__builtin_inff();
-        lo[k][j] = 0;
-      }
 #pragma unroll
     for (int s = STEPS - 1; s >= 0; --s) {
       const int step = 1 << s;
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int cand = lo[k][j] + step;
-          lo[k][j] = sthr[toff[j] + cand] < x[k][j] ? cand : lo[k][j];
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint32_t word = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t b;
-        if (nt[j] < 0) {
-          const int c = (int)x[k][j];
-          b = (uint32_t)(c < 0 ? 0 : (c > 255 ? 255 : c));
-        } else {
-          b = (x[k][j] != x[k][j]) ? (uint32_t)nt[j] : (uint32_t)lo[k][j];
-        }
-        word |= b << (8 * j);
+      for (int j = 0; j < 8; ++j) {
+        const int cand = lo[j] + step;
+        lo[j] = sthr[fb[j] + cand] < x[j] ? cand : lo[j];
       }
-      tile[(k * 8 + rsub) * 32 + q] = qok ? word : 0u;
     }
-    __syncthreads();
-    const int rows = (int)((n - r0) < R ? (n - r0) : R);
-    if (rm) {
-      // row-major: 8 x 16 bytes per 128-byte padded row (Gs == 16)
-      const int row = threadIdx.x >> 3, c4 = threadIdx.x & 7;
+    uint64_t word = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint32_t b;
+      if (nt[j] < 0) {
+        const int c = (int)x[j];
+        b = (uint32_t)(c < 0 ? 0 : (c > 255 ? 255 : c));
+      } else {
+        b = (x[j] != x[j]) ? (uint32_t)nt[j] : (uint32_t)lo[j];
+      }
+      if (8 * g + j >= d) b = 0;
+      word |= (uint64_t)b << (8 * j);
+    }
+    return word;
+  };
+  auto store_rm = [&](int64_t tl) {
+    const int rows = (int)((n - tl * RT) < RT ? (n - tl * RT) : RT);
+    for (int i = threadIdx.x; i < RT * 8; i += blockDim.x) {
+      const int row = i >> 3, c = i & 7;
       if (row < rows) {
-        const uint4 v = *reinterpret_cast<const uint4*>(&tile[row * 32 + 4 * c4]);
-        *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(rm + (r0 + row) * Gs) + 4 * c4) = v;
+        const uint64_t* tr = tile + row * TP + 2 * c;
+        uint4 v;
+        v.x = (uint32_t)tr[0]; v.y = (uint32_t)(tr[0] >> 32);
+        v.z = (uint32_t)tr[1]; v.w = (uint32_t)(tr[1] >> 32);
+        *reinterpret_cast<uint4*>(rm + (tl * RT + row) * Gs + 2 * c) = v;
       }
     }
-    for (int p = threadIdx.x; p < G * R; p += 256) {
-      const int g = p >> 5, row = p & 31;
-      if (row < rows) {
-        const uint64_t v = (uint64_t)tile[row * 32 + 2 * g] | ((uint64_t)tile[row * 32 + 2 * g + 1] << 32);
-        out[(int64_t)g * n + r0 + row] = v;
+  };
+  if (STAGE) {
+    const int nth = (int)blockDim.x, per = RT * Q;
+    float4 sp[2];  // this thread's float4s of the next tile (per <= 2 * nth: Q <= 2 G)
+    auto sfetch = [&](int64_t tl) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int i = (int)threadIdx.x + k * nth;
+        if (i < per) {
+          const int row = i / Q, qq = i - row * Q;
+          int64_t r = tl * RT + row;
+          r = r < n ? r : n - 1;
+          sp[k] = X4[r * ldx4 + qq];
+        }
+      }
+    };
+    if ((int64_t)blockIdx.x < ntiles) sfetch(blockIdx.x);
+    for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+      __syncthreads();  // the previous tile's readers of xt (and of the rm tile) are done
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int i = (int)threadIdx.x + k * nth;
+        if (i < per) {
+          const int row = i / Q, qq = i - row * Q;
+          *reinterpret_cast<float4*>(xt + row * dp + 4 * qq) = sp[k];
+        }
+      }
+      if (tl + gridDim.x < ntiles) sfetch(tl + gridDim.x);
+      __syncthreads();
+      const float4 a0 = *reinterpret_cast<const float4*>(xt + lane * dp + 8 * g);
+      const float4 a1 = hi_ok ? *reinterpret_cast<const float4*>(xt + lane * dp + 8 * g + 4) : a0;
+      float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const uint64_t word = search(x);
+      const int64_t r = tl * RT + lane;
+      if (r < n) out[(int64_t)g * n + r] = word;
+      if (rm) {
+        tile[lane * TP + g] = word;
+        __syncthreads();
+        store_rm(tl);
       }
     }
-    __syncthreads();
+    return;
   }
+  float4 pre0, pre1;
+  auto fetch = [&](int64_t tl) {
+    int64_t r = tl * RT + lane;
+    r = r < n ? r : n - 1;
+    pre0 = X4[r * ldx4 + 2 * g];
+    pre1 = hi_ok ? X4[r * ldx4 + 2 * g + 1] : pre0;
+  };
+  if ((int64_t)blockIdx.x < ntiles) fetch(blockIdx.x);
+  for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+    float x[8] = {pre0.x, pre0.y, pre0.z, pre0.w, pre1.x, pre1.y, pre1.z, pre1.w};
+    if (tl + gridDim.x < ntiles) fetch(tl + gridDim.x);
+    const uint64_t word = search(x);
+    const int64_t r = tl * RT + lane;
+    if (r < n) out[(int64_t)g * n + r] = word;
+    if (rm) {
+      tile[lane * TP + g] = word;
+      __syncthreads();
+      store_rm(tl);
+      __syncthreads();
+    }
+  }
+  (void)G;
 }
 
 // ---------------------------------------------------------------------------
@@ -794,31 +836,37 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
                          int miss_on, float miss_val, uint64_t* out, uint64_t* rm, int Gs, hipStream_t st) {
   if (rm && Gs < (d + 7) / 8) return (int)hipErrorInvalidValue;
   if (n <= 0) return 0;
-  static const bool v4_on = [] {
-    const char* e = getenv("CDNAML_BINIZE_V4");
+  static const bool v5_on = [] {
+    const char* e = getenv("CDNAML_BINIZE_V5");
     return !e || atoi(e) != 0;
   }();
-  if (v4_on && d <= 128 && (d % 4) == 0 && (ldx % 4) == 0 && (reinterpret_cast<uintptr_t>(X) % 16) == 0 &&
+  if (v5_on && d <= 128 && (d % 4) == 0 && (ldx % 4) == 0 && (reinterpret_cast<uintptr_t>(X) % 16) == 0 &&
       (!rm || Gs == 16)) {
-    // v4: float4 tasks straight from HBM, padded +inf tables with a bank-skewed stride, 4 KB bins tile
+    // v5: wave = (64-row tile, 8-feature group), lanes search the same tables (broadcast LDS reads)
     int steps = 0;
     while ((1 << steps) <= tmax) ++steps;
     if (steps < 4) steps = 4;
-    const size_t lds = (size_t)d * ((1 << steps) + 1) * 4 + (size_t)((d + 3) & ~3) * 4 + 32 * 32 * 4;
+    const int G = (d + 7) / 8;
+    static const bool stage = [] {
+      const char* e = getenv("CDNAML_BINIZE_STAGE");
+      return e && atoi(e) != 0;
+    }();
+    const int dp = ((d >> 2) & 1) ? d : d + 4;
+    const size_t lds = (size_t)((d * (1 << steps) + 3) & ~3) * 4 + 64 * 17 * 8 + (stage ? (size_t)64 * dp * 4 : 0);
     if (steps <= 8 && lds <= 150 * 1024) {
       auto launch = [&](auto kern) {
         if (lds > 64 * 1024)
           (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds);
-        hipLaunchKernelGGL(kern, dim3(grid_for(n, 32, 2048)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
+        hipLaunchKernelGGL(kern, dim3(grid_for(n, 64, 1024)), dim3(64 * G), lds, st, X, n, d, ldx, thr, nthr,
                            tmax > 0 ? tmax : 1, miss_on, miss_val, out, rm, Gs);
       };
       switch (steps) {
-        case 4: launch(binize4_kernel<4>); break;
-        case 5: launch(binize4_kernel<5>); break;
-        case 6: launch(binize4_kernel<6>); break;
-        case 7: launch(binize4_kernel<7>); break;
-        default: launch(binize4_kernel<8>); break;
+        case 4: stage ? launch(binize5_kernel<4, true>) : launch(binize5_kernel<4, false>); break;
+        case 5: stage ? launch(binize5_kernel<5, true>) : launch(binize5_kernel<5, false>); break;
+        case 6: stage ? launch(binize5_kernel<6, true>) : launch(binize5_kernel<6, false>); break;
+        case 7: stage ? launch(binize5_kernel<7, true>) : launch(binize5_kernel<7, false>); break;
+        default: stage ? launch(binize5_kernel<8, true>) : launch(binize5_kernel<8, false>); break;
       }
       return (int)hipGetLastError();
     }

@@ -1011,10 +1011,10 @@ def test_seg_hist_lane_matches_flat(dev, d, B, monkeypatch):
 @pytest.mark.parametrize("d,maxb,n,missing", [(100, 40, 100003, None), (64, 256, 5001, None), (8, 2, 77, None),
                                               (128, 32, 4099, None), (100, 40, 3001, -999.0),
                                               (100, 40, 3001, float("nan"))])
-def test_binize_v4_matches_reference(dev, d, maxb, n, missing):
-    """K4 binize v4 (float4 tasks, +inf-padded skewed tables, 32-row bins tile): column-major and padded row-major
-    bins equal the CPU searchsorted reference -- categorical columns, NaN / +-inf, ragged last tile, 4-8 search
-    steps, XGBoost missing values."""
+def test_binize_v5_matches_reference(dev, d, maxb, n, missing):
+    """K4 binize v5 (wave = 64-row tile x 8-feature group, broadcast table reads, [64][17] row-major tile):
+    column-major and padded row-major bins equal the CPU searchsorted reference -- categorical columns, NaN / +-inf, ragged last tile, 1..16 waves per block, 4-8 search steps, XGBoost
+    missing values."""
     g = torch.Generator().manual_seed(d + maxb)
     X = torch.randn(n, d, generator=g) * 3
     X[:, 1] = torch.randint(0, 9, (n,), generator=g).float()
