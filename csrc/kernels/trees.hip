@@ -226,14 +226,16 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
 //     conflicts, and the table offsets are wave-uniform (scalar registers);
 //   * the row's two float4s of the group come straight from HBM (the G waves of
 //     a block read the same 64 rows together, so the 128-byte lines are shared
-//     in L1/L2), the next tile's float4s are loaded before this tile's search;
+//     in L1/L2), the next tile's float4s are loaded before this tile's search
+//     (staging the tile through LDS with coalesced loads instead: 29.5 vs
+//     19.1 ms, three block barriers per tile);
 //   * the column-major word out[g][r] leaves from registers (512-byte runs);
 //     the row-major copy goes through a [64][17] u64 LDS tile (odd pitch:
 //     conflict-free 8-byte writes) and leaves as 16-byte stores of whole
 //     128-byte rows, padding words zeroed once.
 // Block = G waves (one per 8-feature group), persistent over row tiles.
 // ---------------------------------------------------------------------------
-template <int STEPS, bool STAGE>
+template <int STEPS>
 __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                        const float* __restrict__ thr, const int* __restrict__ nthr,
                                                        int tmax, int miss_on, float miss_val,
@@ -242,10 +244,6 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
   constexpr int P = 1 << STEPS, RT = 64, TP = 17;
   float* sthr = smf5;                                                          // [d][P]
   uint64_t* tile = reinterpret_cast<uint64_t*>(sthr + (size_t)((d * P + 3) & ~3));  // [RT][TP]
-  // STAGE: the X tile [RT][dp] goes HBM -> registers (coalesced float4s of whole rows) -> LDS; a lane then reads
-  // its row's 8 features as two ds_read_b128 (dp / 4 odd: 16 rows of a lane group hit 16 distinct bank quads)
-  const int dp = ((d >> 2) & 1) ? d : d + 4;
-  float* xt = reinterpret_cast<float*>(tile + RT * TP);
   for (int i = threadIdx.x; i < d * P; i += blockDim.x) {
     const int f = i >> STEPS, c = i & (P - 1);
     sthr[i] = (c < nthr[f] && c < tmax) ? thr[(size_t)f * tmax + c] : __builtin_inff();
@@ -312,48 +310,6 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
       }
     }
   };
-  if (STAGE) {
-    const int nth = (int)blockDim.x, per = RT * Q;
-    float4 sp[2];  // this thread's float4s of the next tile (per <= 2 * nth: Q <= 2 G)
-    auto sfetch = [&](int64_t tl) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int i = (int)threadIdx.x + k * nth;
-        if (i < per) {
-          const int row = i / Q, qq = i - row * Q;
-          int64_t r = tl * RT + row;
-          r = r < n ? r : n - 1;
-          sp[k] = X4[r * ldx4 + qq];
-        }
-      }
-    };
-    if ((int64_t)blockIdx.x < ntiles) sfetch(blockIdx.x);
-    for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
-      __syncthreads();  // the previous tile's readers of xt (and of the rm tile) are done
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int i = (int)threadIdx.x + k * nth;
-        if (i < per) {
-          const int row = i / Q, qq = i - row * Q;
-          *reinterpret_cast<float4*>(xt + row * dp + 4 * qq) = sp[k];
-        }
-      }
-      if (tl + gridDim.x < ntiles) sfetch(tl + gridDim.x);
-      __syncthreads();
-      const float4 a0 = *reinterpret_cast<const float4*>(xt + lane * dp + 8 * g);
-      const float4 a1 = hi_ok ? *reinterpret_cast<const float4*>(xt + lane * dp + 8 * g + 4) : a0;
-      float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const uint64_t word = search(x);
-      const int64_t r = tl * RT + lane;
-      if (r < n) out[(int64_t)g * n + r] = word;
-      if (rm) {
-        tile[lane * TP + g] = word;
-        __syncthreads();
-        store_rm(tl);
-      }
-    }
-    return;
-  }
   float4 pre0, pre1;
   auto fetch = [&](int64_t tl) {
     int64_t r = tl * RT + lane;
@@ -847,12 +803,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
     while ((1 << steps) <= tmax) ++steps;
     if (steps < 4) steps = 4;
     const int G = (d + 7) / 8;
-    static const bool stage = [] {
-      const char* e = getenv("CDNAML_BINIZE_STAGE");
-      return e && atoi(e) != 0;
-    }();
-    const int dp = ((d >> 2) & 1) ? d : d + 4;
-    const size_t lds = (size_t)((d * (1 << steps) + 3) & ~3) * 4 + 64 * 17 * 8 + (stage ? (size_t)64 * dp * 4 : 0);
+    const size_t lds = (size_t)((d * (1 << steps) + 3) & ~3) * 4 + 64 * 17 * 8;
     if (steps <= 8 && lds <= 150 * 1024) {
       auto launch = [&](auto kern) {
         if (lds > 64 * 1024)
@@ -862,11 +813,11 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
                            tmax > 0 ? tmax : 1, miss_on, miss_val, out, rm, Gs);
       };
       switch (steps) {
-        case 4: stage ? launch(binize5_kernel<4, true>) : launch(binize5_kernel<4, false>); break;
-        case 5: stage ? launch(binize5_kernel<5, true>) : launch(binize5_kernel<5, false>); break;
-        case 6: stage ? launch(binize5_kernel<6, true>) : launch(binize5_kernel<6, false>); break;
-        case 7: stage ? launch(binize5_kernel<7, true>) : launch(binize5_kernel<7, false>); break;
-        default: stage ? launch(binize5_kernel<8, true>) : launch(binize5_kernel<8, false>); break;
+        case 4: launch(binize5_kernel<4>); break;
+        case 5: launch(binize5_kernel<5>); break;
+        case 6: launch(binize5_kernel<6>); break;
+        case 7: launch(binize5_kernel<7>); break;
+        default: launch(binize5_kernel<8>); break;
       }
       return (int)hipGetLastError();
     }
