@@ -235,22 +235,40 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
 //     128-byte rows, padding words zeroed once.
 // Block = G waves (one per 8-feature group), persistent over row tiles.
 // ---------------------------------------------------------------------------
-template <int STEPS>
+// Block barrier for LDS only: waits for this wave's LDS ops (lgkmcnt 0), not for its global loads in flight.
+// __syncthreads() also drains vmcnt, which emptied binize5's register prefetch at every tile.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int STEPS, int RPL>
 __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                        const float* __restrict__ thr, const int* __restrict__ nthr,
                                                        int tmax, int miss_on, float miss_val,
                                                        uint64_t* __restrict__ out, uint64_t* __restrict__ rm, int Gs) {
   extern __shared__ __attribute__((aligned(16))) float smf5[];
-  constexpr int P = 1 << STEPS, RT = 64, TP = 17;
+  constexpr int P = 1 << STEPS, RT = 64 * RPL, TP = 17;  // RPL rows per lane
   float* sthr = smf5;                                                          // [d][P]
   uint64_t* tile = reinterpret_cast<uint64_t*>(sthr + (size_t)((d * P + 3) & ~3));  // [RT][TP]
+  // Table layout by search step: step s (step 2^s) only ever probes cand = (2k + 1) 2^s, so entry cand - 1 is
+  // stored at q = P - 2^(STEPS - s) + k -- each step's candidates are consecutive words, and the 32 lanes of a
+  // read group hit distinct banks (the plain layout put cand and cand + 32 on one bank: 43 % of the LDS
+  // cycles were conflicts).  The last word (cand = P) is never probed.
   for (int i = threadIdx.x; i < d * P; i += blockDim.x) {
-    const int f = i >> STEPS, c = i & (P - 1);
-    sthr[i] = (c < nthr[f] && c < tmax) ? thr[(size_t)f * tmax + c] : __builtin_inff();
+    const int f = i >> STEPS, q = i & (P - 1);
+    int sg = 0;
+    while (sg < STEPS - 1 && q >= P - (P >> (sg + 1))) ++sg;
+    const int k = q - (P - (P >> sg));
+    const int c = ((2 * k + 1) << sg) - 1;  // threshold index held at q
+    sthr[i] = (q < P - 1 && c < nthr[f] && c < tmax) ? thr[(size_t)f * tmax + c] : __builtin_inff();
   }
   if (rm)
     for (int i = threadIdx.x; i < RT * TP; i += blockDim.x) tile[i] = 0ull;  // words g >= G stay 0 (row padding)
   const int G = (d + 7) >> 3;
+  const int nth = 64 * G;  // == blockDim.x (not re-read from the dispatch packet inside the tile loop)
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int Q = d >> 2;
   const bool hi_ok = 2 * g + 1 < Q;  // the group's second quad exists
@@ -259,7 +277,7 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
   for (int j = 0; j < 8; ++j) {
     const int f = 8 * g + j < d ? 8 * g + j : d - 1;
     nt[j] = __builtin_amdgcn_readfirstlane(nthr[f]);
-    fb[j] = f * P - 1;  // entry cand - 1 of feature f
+    fb[j] = f * P;  // feature f's table
   }
   __syncthreads();
   const float4* __restrict__ X4 = reinterpret_cast<const float4*>(X);
@@ -275,11 +293,11 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
     }
 #pragma unroll
     for (int s = STEPS - 1; s >= 0; --s) {
-      const int step = 1 << s;
+      const int step = 1 << s, base = P - (P >> s);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int cand = lo[j] + step;
-        lo[j] = sthr[fb[j] + cand] < x[j] ? cand : lo[j];
+        const int cand = lo[j] + step;  // lo is a multiple of 2^(s+1)
+        lo[j] = sthr[fb[j] + base + (lo[j] >> (s + 1))] < x[j] ? cand : lo[j];
       }
     }
     uint64_t word = 0;
@@ -299,7 +317,7 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
   };
   auto store_rm = [&](int64_t tl) {
     const int rows = (int)((n - tl * RT) < RT ? (n - tl * RT) : RT);
-    for (int i = threadIdx.x; i < RT * 8; i += blockDim.x) {
+    for (int i = threadIdx.x; i < RT * 8; i += nth) {
       const int row = i >> 3, c = i & 7;
       if (row < rows) {
         const uint64_t* tr = tile + row * TP + 2 * c;
@@ -310,26 +328,46 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
       }
     }
   };
-  float4 pre0, pre1;
-  auto fetch = [&](int64_t tl) {
-    int64_t r = tl * RT + lane;
-    r = r < n ? r : n - 1;
-    pre0 = X4[r * ldx4 + 2 * g];
-    pre1 = hi_ok ? X4[r * ldx4 + 2 * g + 1] : pre0;
-  };
-  if ((int64_t)blockIdx.x < ntiles) fetch(blockIdx.x);
-  for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
-    float x[8] = {pre0.x, pre0.y, pre0.z, pre0.w, pre1.x, pre1.y, pre1.z, pre1.w};
-    if (tl + gridDim.x < ntiles) fetch(tl + gridDim.x);
-    const uint64_t word = search(x);
-    const int64_t r = tl * RT + lane;
-    if (r < n) out[(int64_t)g * n + r] = word;
-    if (rm) {
-      tile[lane * TP + g] = word;
-      __syncthreads();
-      store_rm(tl);
-      __syncthreads();
+  // Two register sets of RPL rows per lane, each searched and THEN refilled (two tiles ahead): while one set
+  // is searched the other's loads are in flight, and no loaded register is copied (a copy of a fresh load --
+  // the single-set loop's phi at the back-edge -- costs a vmcnt(0) drain per tile).  Fetches past the last
+  // tile re-read the last tile (never stored), so every fetch is unconditional and counted exactly.
+  // Before: one set, __syncthreads() (another vmcnt(0) drain) -- 19.1 ms = 3.3 TB/s.
+  const int q1 = hi_ok ? 2 * g + 1 : 2 * g;  // no data dependence between the two loads of a row
+  const int64_t S = gridDim.x, last = ntiles - 1;
+  auto fetch = [&](int64_t tl, float4 (&p0)[RPL], float4 (&p1)[RPL]) {
+    tl = tl < last ? tl : last;
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      int64_t r = tl * RT + k * 64 + lane;
+      r = r < n ? r : n - 1;
+      p0[k] = X4[r * ldx4 + 2 * g];
+      p1[k] = X4[r * ldx4 + q1];
     }
+  };
+  auto body = [&](int64_t tl, const float4 (&p0)[RPL], const float4 (&p1)[RPL]) {
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      float x[8] = {p0[k].x, p0[k].y, p0[k].z, p0[k].w, p1[k].x, p1[k].y, p1[k].z, p1[k].w};
+      const uint64_t word = search(x);
+      const int64_t r = tl * RT + k * 64 + lane;
+      if (r < n) out[(int64_t)g * n + r] = word;
+      if (rm) tile[(k * 64 + lane) * TP + g] = word;
+    }
+    if (rm) {
+      lds_barrier();
+      store_rm(tl);
+      lds_barrier();
+    }
+  };
+  float4 a0[RPL], a1[RPL], b0[RPL], b1[RPL];
+  fetch(blockIdx.x, a0, a1);
+  fetch(blockIdx.x + S, b0, b1);
+  for (int64_t tl = blockIdx.x; tl < ntiles; tl += 2 * S) {
+    body(tl, a0, a1);
+    fetch(tl + 2 * S, a0, a1);
+    if (tl + S < ntiles) body(tl + S, b0, b1);  // block-uniform
+    fetch(tl + 3 * S, b0, b1);
   }
   (void)G;
 }
@@ -803,21 +841,25 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
     while ((1 << steps) <= tmax) ++steps;
     if (steps < 4) steps = 4;
     const int G = (d + 7) / 8;
-    const size_t lds = (size_t)((d * (1 << steps) + 3) & ~3) * 4 + 64 * 17 * 8;
+    static const int rpl = [] {
+      const char* e = getenv("CDNAML_BINIZE_RPL");
+      return e && atoi(e) == 2 ? 2 : 1;
+    }();
+    const size_t lds = (size_t)((d * (1 << steps) + 3) & ~3) * 4 + (size_t)64 * rpl * 17 * 8;
     if (steps <= 8 && lds <= 150 * 1024) {
       auto launch = [&](auto kern) {
         if (lds > 64 * 1024)
           (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds);
-        hipLaunchKernelGGL(kern, dim3(grid_for(n, 64, 1024)), dim3(64 * G), lds, st, X, n, d, ldx, thr, nthr,
+        hipLaunchKernelGGL(kern, dim3(grid_for(n, 64 * rpl, 1024)), dim3(64 * G), lds, st, X, n, d, ldx, thr, nthr,
                            tmax > 0 ? tmax : 1, miss_on, miss_val, out, rm, Gs);
       };
       switch (steps) {
-        case 4: launch(binize5_kernel<4>); break;
-        case 5: launch(binize5_kernel<5>); break;
-        case 6: launch(binize5_kernel<6>); break;
-        case 7: launch(binize5_kernel<7>); break;
-        default: launch(binize5_kernel<8>); break;
+        case 4: rpl == 1 ? launch(binize5_kernel<4, 1>) : launch(binize5_kernel<4, 2>); break;
+        case 5: rpl == 1 ? launch(binize5_kernel<5, 1>) : launch(binize5_kernel<5, 2>); break;
+        case 6: rpl == 1 ? launch(binize5_kernel<6, 1>) : launch(binize5_kernel<6, 2>); break;
+        case 7: rpl == 1 ? launch(binize5_kernel<7, 1>) : launch(binize5_kernel<7, 2>); break;
+        default: rpl == 1 ? launch(binize5_kernel<8, 1>) : launch(binize5_kernel<8, 2>); break;
       }
       return (int)hipGetLastError();
     }
