@@ -1040,6 +1040,21 @@ def _interleave(work: np.ndarray, segs: np.ndarray, chunk: int) -> np.ndarray:
     return work[np.argsort(j / np.repeat(k, k), kind="stable")]
 
 
+SEG_XCD = __import__("os").environ.get("CDNAML_SEG_XCD", "0") != "0"
+
+
+def _xcd_stripe(work: np.ndarray) -> np.ndarray:
+    """Position-ordered work items -> block order in which XCD x (block b runs on XCD b % 8) walks the x-th
+    eighth of the list: the blocks an XCD runs together cover the same relative row range of every segment,
+    so the gathered row lines are shared in that XCD's L2.  Padded with empty items (len 0)."""
+    m = len(work)
+    m8 = -(-m // 8)
+    i = np.arange(m)
+    out = np.zeros((m8 * 8, 3), dtype=work.dtype)
+    out[(i % m8) * 8 + i // m8] = work
+    return out
+
+
 def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
              v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
              scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False,
@@ -1130,6 +1145,8 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
             return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
         if interleave and len(segs) > 1:
             work = _interleave(work, segs, chunk)
+            if SEG_XCD:
+                work = _xcd_stripe(work)
         wt, = upload(bins.device, work.reshape(-1))
         iout = out if out is not None else torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
         assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()

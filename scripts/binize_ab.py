@@ -10,7 +10,6 @@ import sys
 VARIANTS = {
     "v2": {"CDNAML_BINIZE_V5": "0"},
     "v5": {},
-    "v5-rpl2": {"CDNAML_BINIZE_RPL": "2"},
 }
 
 
