@@ -1033,26 +1033,13 @@ def _seg_work(segs: np.ndarray, chunk: int) -> np.ndarray:
 def _interleave(work: np.ndarray, segs: np.ndarray, chunk: int) -> np.ndarray:
     """Interleave segment chunks by relative position (chunk j of every segment covers about the same fraction of
     the row ids), so concurrently running blocks gather nearby rows.  Tried on top: placing each round of
-    len(segs) chunks on one XCD (block b -> XCD b % 8) for L2 sharing -- measured 194 vs 190 ms, dropped."""
+    len(segs) chunks on one XCD (block b -> XCD b % 8) for L2 sharing -- measured 194 vs 190 ms with the
+    half-wave kernel; with the quarter-wave kernel XCD x walking the x-th eighth of this order measured 87.4 vs
+    87.0 ms of histograms per step (also with level-0/1 only) -- dropped both."""
     sg = segs[segs[:, 1] > 0]
     k = (sg[:, 1] + chunk - 1) // chunk
     j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
     return work[np.argsort(j / np.repeat(k, k), kind="stable")]
-
-
-SEG_XCD = __import__("os").environ.get("CDNAML_SEG_XCD", "0") != "0"
-
-
-def _xcd_stripe(work: np.ndarray) -> np.ndarray:
-    """Position-ordered work items -> block order in which XCD x (block b runs on XCD b % 8) walks the x-th
-    eighth of the list: the blocks an XCD runs together cover the same relative row range of every segment,
-    so the gathered row lines are shared in that XCD's L2.  Padded with empty items (len 0)."""
-    m = len(work)
-    m8 = -(-m // 8)
-    i = np.arange(m)
-    out = np.zeros((m8 * 8, 3), dtype=work.dtype)
-    out[(i % m8) * 8 + i // m8] = work
-    return out
 
 
 def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
@@ -1145,8 +1132,6 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
             return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
         if interleave and len(segs) > 1:
             work = _interleave(work, segs, chunk)
-            if SEG_XCD:
-                work = _xcd_stripe(work)
         wt, = upload(bins.device, work.reshape(-1))
         iout = out if out is not None else torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
         assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()

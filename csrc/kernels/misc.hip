@@ -24,16 +24,20 @@ __global__ void uniform_kernel(double* __restrict__ out, int64_t n, uint64_t see
 // bit-identical to the loop): the kernel does compares only, no exp / divide.
 constexpr int kCdf = 32;
 struct PoissonCdf {
-  double F[kCdf];
+  // u > F_k  <=>  w > floor(F_k 2^32) for the 32-bit uniform w = u 2^32 (exact: F_k 2^32 is exact in double
+  // and w is an integer), so the draws compare integers; saturated at 2^32 - 1 (never exceeded)
+  uint32_t T[kCdf];
 };
 
 // One Philox4x32-10 call yields the 32-bit uniforms of 4 consecutive global
 // elements (quad q = index >> 2, word = index & 3): 4x fewer Philox rounds
 // than one 53-bit double per draw (this kernel shares the GPU with the binning
 // kernel it overlaps, so its VALU time is not free).  Bit-identical to
-// cdnaml/ops/philox.py:uniform32.
+// cdnaml/ops/philox.py:uniform32.  A draw is 8 unrolled integer compares
+// against the tabulated CDF (a data-dependent double loop before: k > 7 has
+// probability ~1e-5 at rate 1) and an interior quad leaves as one dword store.
 __global__ __launch_bounds__(256) void poisson_kernel(uint8_t* __restrict__ out, int T, int64_t n, uint64_t seed,
-                                                      uint64_t offset, double rate, PoissonCdf cdf) {
+                                                      uint64_t offset, double rate, PoissonCdf cdf, int packed) {
   const int t = blockIdx.y;
   const uint64_t q0 = offset >> 2, q1 = (offset + (uint64_t)n - 1) >> 2;
   uint8_t* o = out + (int64_t)t * n;
@@ -43,15 +47,28 @@ __global__ __launch_bounds__(256) void poisson_kernel(uint8_t* __restrict__ out,
                                                           0xB00Fu},
                                               (uint32_t)seed, (uint32_t)(seed >> 32));
     const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    uint32_t k[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint64_t gi = q * 4 + j;
+      uint32_t kk = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) kk += w[j] > cdf.T[i] ? 1u : 0u;
+      if (kk == 8u) {
+        while (kk < (uint32_t)kCdf && w[j] > cdf.T[kk]) ++kk;
+        if (kk == (uint32_t)kCdf) kk = cdna::poisson_from_uniform((double)w[j] * (1.0 / 4294967296.0), rate);
+      }
+      k[j] = kk;
+    }
+    const uint64_t g0 = q * 4;
+    if (packed && g0 >= offset && g0 + 3 < offset + (uint64_t)n) {
+      *reinterpret_cast<uint32_t*>(o + (g0 - offset)) = k[0] | (k[1] << 8) | (k[2] << 16) | (k[3] << 24);
+      continue;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t gi = g0 + j;
       if (gi < offset || gi >= offset + (uint64_t)n) continue;
-      const double u = (double)w[j] * (1.0 / 4294967296.0);
-      uint32_t k = 0;
-      while (k < kCdf && u > cdf.F[k]) ++k;
-      if (k == kCdf) k = cdna::poisson_from_uniform(u, rate);  // tail beyond the table: exact loop
-      o[gi - offset] = (uint8_t)k;
+      o[gi - offset] = (uint8_t)k[j];
     }
   }
 }
@@ -325,15 +342,19 @@ CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_
   if (n <= 0 || T <= 0) return 0;
   PoissonCdf cdf;
   {
+    // same double operations in the same order as poisson_from_uniform's recurrence
     double p = exp(-rate), F = p;
     for (int k = 0; k < kCdf; ++k) {
-      cdf.F[k] = F;  // F after k loop iterations
+      const double x = F * 4294967296.0;  // F after k loop iterations, scaled exactly
+      cdf.T[k] = x >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)floor(x);
       p *= rate / (double)(k + 1);
       F += p;
     }
   }
+  // interior quads as dword stores when every tree row starts 4-byte aligned
+  const int packed = (offset % 4 == 0) && (n % 4 == 0) && (reinterpret_cast<uintptr_t>(out) % 4 == 0);
   hipLaunchKernelGGL(poisson_kernel, dim3(grid_for(n / 4 + 2, 256, 1024), T), dim3(256), 0, st, out, T, n, seed, offset,
-                     rate, cdf);
+                     rate, cdf, packed);
   return (int)hipGetLastError();
 }
 

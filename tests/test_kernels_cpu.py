@@ -200,19 +200,3 @@ def test_col_moments_reference_semantics():
     full = K.col_moments(X)
     assert torch.allclose(merged[0], full[0])
 
-
-def test_xcd_stripe_places_each_eighth_on_one_xcd():
-    """Histogram work in position order -> block order: XCD x (block b % 8) runs the x-th eighth of the list, in
-    order, and the padding items are empty."""
-    import numpy as np
-    from cdnaml.ops import kernels as K
-    for m in (1, 7, 8, 45, 1000):
-        work = np.stack([np.arange(m), np.ones(m), np.arange(m) % 5], 1).astype(np.int32)
-        out = K._xcd_stripe(work)
-        m8 = -(-m // 8)
-        assert out.shape == (m8 * 8, 3)
-        real = out[:, 1] > 0
-        assert real.sum() == m and sorted(out[real, 0].tolist()) == list(range(m))
-        for b in np.nonzero(real)[0]:
-            i = int(out[b, 0])
-            assert b % 8 == i // m8 and b // 8 == i % m8

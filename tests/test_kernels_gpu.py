@@ -62,10 +62,13 @@ def test_uniform_bit_identical(dev):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("rate", [1.0, 0.63, 2.5])
-def test_poisson_matches(dev, rate):
-    a = K.poisson_weights(4, 50000, 7, 1000, rate)
-    b = K.poisson_weights(4, 50000, 7, 1000, rate, device=dev).cpu()
+@pytest.mark.parametrize("rate,n,offset", [(1.0, 50000, 1000), (0.63, 50000, 1000), (2.5, 50000, 1000),
+                                           (1.0, 50003, 1001), (7.5, 4099, 6)])
+def test_poisson_matches(dev, rate, n, offset):
+    """Integer-threshold draws (8 unrolled compares, CDF loop past 7, exact tail) with dword stores of interior
+    quads (aligned) or byte stores (unaligned offsets / row lengths) equal the host Philox reference."""
+    a = K.poisson_weights(4, n, 7, offset, rate)
+    b = K.poisson_weights(4, n, 7, offset, rate, device=dev).cpu()
     assert (a != b).sum().item() <= 2  # libm exp() may differ in the last ulp
 
 
