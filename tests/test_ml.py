@@ -326,3 +326,25 @@ def test_standard_scaler(spark):
     S = np.stack([r.s.toArray() for r in out.select("s").collect()])
     np.testing.assert_allclose(S.mean(0), 0, atol=1e-6)
     np.testing.assert_allclose(S.std(0, ddof=1), 1, atol=1e-5)
+
+
+def test_linear_regression_standard_errors_ols(spark):
+    """coefficientStandardErrors / tValues (computed on first access) equal the textbook OLS values
+    sqrt(diag(sigma^2 (A^T A)^-1)) for [X | 1]."""
+    import numpy as np
+    import torch
+    from cdnaml.models.regression import LinearRegression
+    rng = np.random.default_rng(0)
+    n, d = 500, 3
+    X = rng.standard_normal((n, d))
+    y = X @ np.array([1.5, -2.0, 0.5]) + 3.0 + rng.standard_normal(n) * 0.3
+    df = spark.createDataFrameFromLocalTensors({"features": torch.from_numpy(X).float(),
+                                                "label": torch.from_numpy(y)})
+    m = LinearRegression(gramPrecision="fp32").fit(df)
+    Xf = X.astype(np.float32).astype(np.float64)
+    A = np.hstack([Xf, np.ones((n, 1))])
+    beta, *_ = np.linalg.lstsq(A, y, rcond=None)
+    sigma2 = ((y - A @ beta) ** 2).sum() / (n - d - 1)
+    se = np.sqrt(np.diag(np.linalg.inv(A.T @ A)) * sigma2)
+    np.testing.assert_allclose(m.summary.coefficientStandardErrors, se, rtol=1e-3)
+    np.testing.assert_allclose(m.summary.tValues, beta / se, rtol=1e-3)
