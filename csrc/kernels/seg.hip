@@ -1002,7 +1002,9 @@ __global__ __launch_bounds__(256) void codes_count_w_kernel(const CompactWArgs a
 // over ~16 partially written 128-byte lines (level-0 scatter: 14 GB in 5.4 ms
 // = 2.7 TB/s; all levels 20.5 ms per headline step).  Here trip row j of lane
 // l is rb + 64 j + l: one ballot per (j, node) ranks the lanes, so each store
-// instruction writes one contiguous run per node (14.6 ms per step).
+// instruction writes one contiguous run per node (14.6 ms per step).  Ranking
+// by the node id's bits (LK + 1 ballots, cursors one per lane read by
+// bpermute) instead of one ballot per node measured equal at KB = 4 / 8.
 template <int KB>
 __global__ __launch_bounds__(256) void codes_scatter_w_kernel(const CompactWArgs a) {
   __shared__ int s_k[256];
@@ -1025,15 +1027,6 @@ __global__ __launch_bounds__(256) void codes_scatter_w_kernel(const CompactWArgs
   int acc[KB];
 #pragma unroll
   for (int k = 0; k < KB; ++k) acc[k] = a.woff[cb + k] + (a.kstart ? (int)a.kstart[(int64_t)t * KB + k] : 0);
-  // KB >= 4: rank by the node id's bits instead of one ballot per node -- LK + 1 ballots, the lane's same-node
-  // mask from them, and the node cursors held one per lane (lane k: node k) and read with one bpermute
-  constexpr int LK = KB >= 16 ? 4 : (KB >= 8 ? 3 : (KB >= 4 ? 2 : 0));
-  int accv = 0;
-  if constexpr (LK > 0) {
-#pragma unroll
-    for (int k = 0; k < KB; ++k)
-      if (lane == k) accv = acc[k];
-  }
   constexpr int NJ = 8;
   for (int64_t rb = r_begin; rb < r_end; rb += 64 * NJ) {
     uint32_t cc[NJ];
@@ -1050,33 +1043,13 @@ __global__ __launch_bounds__(256) void codes_scatter_w_kernel(const CompactWArgs
     for (int j = 0; j < NJ; ++j) {
       const int kk = s_k[cc[j] & 0xFFu];
       int pos = -1;
-      if constexpr (LK > 0) {
-        const uint64_t vm = __builtin_amdgcn_ballot_w64(kk >= 0);
-        if (vm == 0ull) continue;  // wave-uniform
-        uint64_t bm[LK];
 #pragma unroll
-        for (int i = 0; i < LK; ++i) bm[i] = __builtin_amdgcn_ballot_w64(((kk >> i) & 1) != 0);
-        uint64_t same = vm, mine = vm;  // lanes on this lane's node / on node `lane` (the cursor it holds)
-#pragma unroll
-        for (int i = 0; i < LK; ++i) {
-          same &= ((kk >> i) & 1) ? bm[i] : ~bm[i];
-          mine &= ((lane >> i) & 1) ? bm[i] : ~bm[i];
-        }
-        const int base = __shfl(accv, kk < 0 ? 0 : kk);
-        if (kk >= 0)
-          pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
-        if (lane < KB) accv += __builtin_popcountll(mine);
-      } else {
-#pragma unroll
-        for (int k = 0; k < KB; ++k) {
-          const uint64_t m = __builtin_amdgcn_ballot_w64(kk == k);
-          if (m == 0ull) continue;  // wave-uniform
-          if (kk == k)
-            pos = acc[k] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          acc[k] += __builtin_popcountll(m);
-        }
+      for (int k = 0; k < KB; ++k) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(kk == k);
+        if (m == 0ull) continue;  // wave-uniform
+        if (kk == k)
+          pos = acc[k] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        acc[k] += __builtin_popcountll(m);
       }
       if (pos < 0) continue;
       const int64_t r = rb + j * 64 + lane;
