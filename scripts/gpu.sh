@@ -14,6 +14,7 @@
 #   pmc:<regex>      PMC pass (counters from scripts/pmc_hist.txt) over kernels matching <regex>
 #   configs          BASELINE configs 2-5 (bench_configs.py lr/cv/infer/gbdt)
 #   cfg:<name>       one bench_configs.py config
+#   profcfg:<name>   rocprofv3 --kernel-trace --stats of one bench_configs.py config (CFG_ARGS passed on)
 #   py:<file>        python <file> (a scratch experiment)
 # Extra environment for bench/prof steps: BENCH_ARGS="--steps 3 ..."
 set -o pipefail
@@ -55,6 +56,13 @@ run_step() {
         kstats "$O/$s"
         python scripts/gaps.py "$(find "$O/$s" -name "*kernel_trace.csv" | sort | sed -n 1p)" > "$O/$s/gaps.txt"
         cat "$O/$s/gaps.txt" ;;
+    profcfg:*)
+        local c=${s#profcfg:}
+        rm -rf "$O/profcfg"; mkdir -p "$O/profcfg"
+        (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profcfg" -o p \
+            -- python3 "$R/bench_configs.py" $c ${CFG_ARGS} > "$O/profcfg/run.log" 2>&1)
+        local rc=$?; [ $rc -ne 0 ] && { tail -5 "$O/profcfg/run.log"; return $rc; }
+        kstats "$O/profcfg" ;;
     pmc:*)
         rm -rf "$O/pmc"; mkdir -p "$O/pmc"
         (cd /tmp && timeout -s KILL 300 rocprofv3 -i "$R/scripts/pmc_hist.txt" --kernel-include-regex "${s#pmc:}" \
