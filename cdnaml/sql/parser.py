@@ -532,7 +532,8 @@ def _resolve(name: str, columns: List[str]) -> str:
 
 
 def _from_source(p: Parser, session):
-    """Parse a table reference; returns (DataFrame, alias)."""
+    """Parse a table reference; returns (DataFrame, alias, table name or None)."""
+    tname = None
     if p.accept_op("("):
         df = _select(p, session)
         p.expect_op(")")
@@ -550,18 +551,43 @@ def _from_source(p: Parser, session):
                 p.next()
                 name += "." + p.ident()
             df = session.table(name)
+            tname = name.split(".")[-1]
     alias = None
     if p.accept_kw("as"):
         alias = p.ident()
     elif p.peek().kind in ("id", "qid") and p.peek().val.lower() not in _KEYWORDS:
         alias = p.next().val
-    return df, alias
+    return df, alias, tname
+
+
+def _map_expr(e: Expr, fn) -> Expr:
+    """Rebuild ``e`` bottom-up; ``fn(node)`` may return a replacement for a node (else None = recurse)."""
+    import copy
+    r = fn(e)
+    if r is not None:
+        return r
+    e2 = copy.copy(e)
+    kids = None
+    for attr in ("l", "r", "x", "otherwise"):
+        if isinstance(getattr(e2, attr, None), Expr):
+            setattr(e2, attr, _map_expr(getattr(e2, attr), fn))
+    if hasattr(e2, "args"):
+        e2.args = [_map_expr(a, fn) for a in e2.args]
+        kids = list(e2.args)
+    elif hasattr(e2, "branches"):
+        e2.branches = [(_map_expr(c, fn), _map_expr(v, fn)) for c, v in e2.branches]
+        kids = [k for br in e2.branches for k in br] + ([e2.otherwise] if e2.otherwise is not None else [])
+    else:
+        kids = [getattr(e2, a) for a in ("l", "r", "x") if isinstance(getattr(e2, a, None), Expr)]
+    e2.children = kids
+    return e2
 
 
 def _collect_aggs(e: Expr, out: list):
     from .functions import AggExpr
     if isinstance(e, AggExpr):
-        out.append(e)
+        if all(a is not e for a in out):
+            out.append(e)
         return
     for c in e.children:
         if c is not None:
@@ -569,28 +595,93 @@ def _collect_aggs(e: Expr, out: list):
 
 
 def _replace_aggs(e: Expr, mapping: dict) -> Expr:
-    from .functions import AggExpr
-    import copy
-    if isinstance(e, AggExpr):
-        return ColRef(mapping[id(e)])
-    e2 = copy.copy(e)
-    for attr in ("l", "r", "x", "otherwise"):
-        if hasattr(e2, attr) and isinstance(getattr(e2, attr), Expr):
-            setattr(e2, attr, _replace_aggs(getattr(e2, attr), mapping))
-    if hasattr(e2, "args"):
-        e2.args = [_replace_aggs(a, mapping) for a in e2.args]
-    if hasattr(e2, "branches"):
-        e2.branches = [(_replace_aggs(c, mapping), _replace_aggs(v, mapping)) for c, v in e2.branches]
-    kids = []
-    for attr in ("l", "r", "x"):
-        if hasattr(e2, attr) and isinstance(getattr(e2, attr), Expr):
-            kids.append(getattr(e2, attr))
-    if hasattr(e2, "args"):
-        kids = list(e2.args)
-    if hasattr(e2, "branches"):
-        kids = [k for br in e2.branches for k in br] + ([e2.otherwise] if e2.otherwise is not None else [])
-    e2.children = kids
-    return e2
+    return _map_expr(e, lambda x: ColRef(mapping[id(x)]) if id(x) in mapping else None)
+
+
+def _display(e: Expr) -> str:
+    """Spark's output name of an un-aliased select item: column references lose their qualifier."""
+    return _map_expr(e, lambda x: ColRef(x.col_name.split(".")[-1]) if isinstance(x, ColRef) else None).name()
+
+
+class _Scope:
+    """Name resolution over the FROM clause (Spark's analyzer, the part SQL queries over joins need).
+
+    Every source's columns are renamed to unique internal names (``__s<i>_<col>``), so both sides of
+    a join stay addressable: ``alias.col`` resolves to that source's column, a bare name must match
+    exactly one source column (else ``AnalysisException: Reference 'x' is ambiguous``, as in Spark),
+    and ``JOIN … USING (k)`` merges the key into one column visible under both qualifiers.
+    """
+
+    def __init__(self):
+        self.entries: List[Tuple[Optional[str], str, str]] = []  # (qualifier lower, column, internal name)
+        self.nsrc = 0
+
+    def add(self, df, alias, tname):
+        i = self.nsrc
+        self.nsrc += 1
+        qual = (alias or tname)
+        qual = qual.lower() if qual else None
+        internal = [f"__s{i}_{c}" for c in df.columns]
+        for c, n in zip(df.columns, internal):
+            self.entries.append((qual, c, n))
+        return df.toDF(*internal), qual
+
+    def columns(self, qual=None):
+        seen, out = set(), []
+        for q, c, n in self.entries:
+            if (qual is None or q == qual) and n not in seen:
+                seen.add(n)
+                out.append((c, n))
+        return out
+
+    def lookup(self, name: str) -> Optional[str]:
+        parts = name.split(".")
+        if len(parts) >= 2:
+            q, c = parts[-2].lower(), parts[-1].lower()
+            hits = {n for qq, cc, n in self.entries if qq == q and cc.lower() == c}
+            if len(hits) == 1:
+                return hits.pop()
+        c = name.lower()
+        hits = {n for _, cc, n in self.entries if cc.lower() == c}
+        if not hits and len(parts) >= 2:
+            c = parts[-1].lower()
+            hits = {n for _, cc, n in self.entries if cc.lower() == c}
+        if len(hits) > 1:
+            raise AnalysisException(f"Reference '{name}' is ambiguous, could be: "
+                                    f"{sorted(q + '.' + cc if q else cc for q, cc, n in self.entries if n in hits)}")
+        return hits.pop() if hits else None
+
+    def bind(self, e: Expr, extra: Optional[dict] = None) -> Expr:
+        def fn(x):
+            if isinstance(x, ColRef):
+                if extra is not None and "." not in x.col_name and x.col_name.lower() in extra:
+                    return extra[x.col_name.lower()]
+                n = self.lookup(x.col_name)
+                if n is None:
+                    raise AnalysisException(f"cannot resolve column '{x.col_name}' given input columns "
+                                            f"{[c for c, _ in self.columns()]}")
+                return ColRef(n)
+            return None
+        return _map_expr(e, fn)
+
+
+def _join_keys(cond: Expr, scope: _Scope, left_names: set, lk, rk):
+    """Equi-join conditions (AND of col = col) bound to internal names, left side first."""
+    if isinstance(cond, BinOp) and cond.op == "and":
+        _join_keys(cond.l, scope, left_names, lk, rk)
+        _join_keys(cond.r, scope, left_names, lk, rk)
+        return
+    if isinstance(cond, BinOp) and cond.op == "==" and isinstance(cond.l, ColRef) and isinstance(cond.r, ColRef):
+        a, b = scope.bind(cond.l).col_name, scope.bind(cond.r).col_name
+        if a in left_names and b not in left_names:
+            lk.append(a)
+            rk.append(b)
+            return
+        if b in left_names and a not in left_names:
+            lk.append(b)
+            rk.append(a)
+            return
+    raise AnalysisException("only equality join conditions between the two sides (combined with AND) are supported")
 
 
 def _select(p: Parser, session):
@@ -603,9 +694,9 @@ def _select(p: Parser, session):
     items = [p.select_item()]
     while p.accept_op(","):
         items.append(p.select_item())
-    df = None
+    scope = _Scope()
     if p.accept_kw("from"):
-        df, _ = _from_source(p, session)
+        df, _ = scope.add(*_from_source(p, session))
         while True:
             how = None
             if p.is_kw("join"):
@@ -619,7 +710,9 @@ def _select(p: Parser, session):
             else:
                 break
             p.expect_kw("join")
-            other, _ = _from_source(p, session)
+            left_names = set(df.columns)
+            n_before = len(scope.entries)
+            other, oq = scope.add(*_from_source(p, session))
             if how == "cross":
                 df = df.crossJoin(other)
                 continue
@@ -629,34 +722,33 @@ def _select(p: Parser, session):
                 while p.accept_op(","):
                     keys.append(p.ident())
                 p.expect_op(")")
-                df = df.join(other, on=keys, how=how)
+                ren = {}
+                for k in keys:
+                    ln = [n for q, c, n in scope.entries[:n_before] if c.lower() == k.lower()]
+                    rn = [n for q, c, n in scope.entries[n_before:] if c.lower() == k.lower()]
+                    if len(set(ln)) != 1 or len(rn) != 1:
+                        raise AnalysisException(f"USING column '{k}' cannot be resolved on both sides of the join")
+                    ren[rn[0]] = ln[0]
+                # the right key becomes the left key column: one merged column under both qualifiers
+                other = other.toDF(*[ren.get(c, c) for c in other.columns])
+                scope.entries[n_before:] = [(q, c, ren.get(n, n)) for q, c, n in scope.entries[n_before:]]
+                df = df.join(other, on=[ren[r] for r in ren], how=how)
                 continue
             p.expect_kw("on")
             cond = p.expression()
             lk, rk = [], []
-            _equi_keys(cond, df.columns, other.columns, lk, rk)
-            if all(a.lower() == b.lower() for a, b in zip(lk, rk)) and lk:
-                if lk != rk:
-                    other = other.toDF(*[(lk[rk.index(c)] if c in rk else c) for c in other.columns])
-                df = df.join(other, on=lk, how=how)
-            else:
-                df = df.join(other, on=[Column(BinOp("==", ColRef(a), ColRef(b))) for a, b in zip(lk, rk)],
-                             how=how)
+            _join_keys(cond, scope, left_names, lk, rk)
+            df = df.join(other, on=[Column(BinOp("==", ColRef(a), ColRef(b))) for a, b in zip(lk, rk)], how=how)
     else:
-        df = session.range(1).select()
-        df = session.createDataFrame([(1,)], ["__dummy"])
-    if p.accept_kw("where"):
-        cond = p.expression()
-        df = df.filter(Column(cond))
+        df, _ = scope.add(session.createDataFrame([(1,)], ["__dummy"]), None, None)
+    where = p.expression() if p.accept_kw("where") else None
     group_keys = None
     if p.accept_kw("group"):
         p.expect_kw("by")
         group_keys = [p.expression()]
         while p.accept_op(","):
             group_keys.append(p.expression())
-    having = None
-    if p.accept_kw("having"):
-        having = p.expression()
+    having = p.expression() if p.accept_kw("having") else None
     order = None
     if p.accept_kw("order"):
         p.expect_kw("by")
@@ -667,78 +759,99 @@ def _select(p: Parser, session):
     if p.accept_kw("limit"):
         limit = int(p.next().val)
 
-    aggs: list = []
+    # ---- bind every expression to the FROM scope; output names are Spark's (unqualified) display names
+    from .column import Alias
+    out_exprs: List[Expr] = []
+    names: List[str] = []
     for it in items:
-        _collect_aggs(it, aggs)
-    if having is not None:
-        _collect_aggs(having, aggs)
-    if order:
-        for o in order:
-            _collect_aggs(o, aggs)
+        if isinstance(it, Star):
+            qual = it.table.lower() if it.table else None
+            cols = scope.columns(qual)
+            if qual is not None and not cols:
+                raise AnalysisException(f"cannot resolve '{it.table}.*'")
+            for c, n in cols:
+                if n == "__s0___dummy":
+                    continue
+                out_exprs.append(ColRef(n))
+                names.append(c)
+            continue
+        if isinstance(it, Alias):
+            out_exprs.append(scope.bind(it.x))
+            names.append(it.alias)
+        else:
+            out_exprs.append(scope.bind(it))
+            names.append(_display(it))
+    # duplicate output names (SELECT * over a join) stay addressable with a suffix
+    seen = {}
+    for i, nm in enumerate(names):
+        k = nm.lower()
+        if k in seen:
+            seen[k] += 1
+            names[i] = f"{nm}_{seen[k]}"
+        else:
+            seen[k] = 0
+    alias_map = {nm.lower(): e for nm, e in zip(names, out_exprs)}
+    if where is not None:
+        df = df.filter(Column(scope.bind(where)))
+    having_b = scope.bind(having, alias_map) if having is not None else None
+    order_b = [scope.bind(o, alias_map) for o in order] if order else None
+
+    aggs: list = []
+    for e in out_exprs:
+        _collect_aggs(e, aggs)
+    if having_b is not None:
+        _collect_aggs(having_b, aggs)
+    for o in order_b or []:
+        _collect_aggs(o, aggs)
     if group_keys is not None or aggs:
         keys = []
         for k in group_keys or []:
-            if isinstance(k, ColRef):
-                keys.append(_resolve(k.col_name, df.columns))
+            kb = scope.bind(k, alias_map) if not isinstance(k, Lit) else k
+            if isinstance(kb, ColRef):
+                keys.append(kb.col_name)
+            elif isinstance(kb, Lit) and isinstance(kb.value, int) and 1 <= kb.value <= len(out_exprs):
+                keys.append(Column(out_exprs[kb.value - 1]))  # GROUP BY <ordinal>
             else:
-                keys.append(Column(k))
+                keys.append(Column(kb))
         mapping = {id(a): f"__agg{i}" for i, a in enumerate(aggs)}
-        agg_cols = []
-        for a in aggs:
-            a2 = a
-            if a.x is not None and isinstance(a.x, ColRef):
-                import copy
-                a2 = copy.copy(a)
-                a2.x = ColRef(_resolve(a.x.col_name, df.columns))
-                a2.children = [a2.x]
-            agg_cols.append(Column(a2).alias(mapping[id(a)]))
+        agg_cols = [Column(a).alias(mapping[id(a)]) for a in aggs]
         df = df.groupBy(*keys).agg(*agg_cols) if agg_cols else df.groupBy(*keys).agg(
             F.count("*").alias("__cnt"))
-        items = [_replace_aggs(it, mapping) for it in items]
-        if having is not None:
-            df = df.filter(Column(_replace_aggs(having, mapping)))
-        if order:
-            order = [_replace_aggs(o, mapping) for o in order]
-    # projection
-    proj = []
-    for it in items:
-        proj.append(_strip_qualifiers(it, df.columns))
-    out = df.select(*[Column(e) for e in proj])
+        # non-column group keys come out under their display name: refer to them by it
+        kmap = {}
+        for k in keys:
+            if isinstance(k, Column) and not isinstance(k._expr, ColRef):
+                kmap[str(k._expr)] = k._expr.name()
+
+        def fix(e):
+            e = _replace_aggs(e, mapping)
+            if kmap:
+                e = _map_expr(e, lambda x: ColRef(kmap[str(x)]) if (not isinstance(x, (ColRef, Lit)) and
+                                                                    str(x) in kmap) else None)
+            return e
+        out_exprs = [fix(e) for e in out_exprs]
+        if having_b is not None:
+            df = df.filter(Column(fix(having_b)))
+        if order_b:
+            order_b = [fix(o) for o in order_b]
+    elif having_b is not None:
+        df = df.filter(Column(having_b))
+    proj = [Column(e).alias(nm) for e, nm in zip(out_exprs, names)]
     if distinct:
-        out = out.distinct()
-    if order:
-        cols_after = out.columns
-        fixed = [_strip_qualifiers(o, cols_after + df.columns) for o in order]
-        refs = [r for o in fixed for r in o.references()]
-        if all(any(r.lower() == c.lower() for c in cols_after) for r in refs):
-            out = out.orderBy(*[Column(_strip_qualifiers(o, cols_after)) for o in order])
-        else:
-            out = df.orderBy(*[Column(o) for o in fixed]).select(*[Column(e) for e in proj])
+        out = df.select(*proj).distinct()
+        if order_b:
+            # after DISTINCT only output columns can be ordered on
+            rev = {str(e): nm for e, nm in zip(out_exprs, names)}
+            fixed = [_map_expr(o, lambda x: ColRef(rev[str(x)]) if str(x) in rev and not isinstance(x, SortOrder)
+                               else None) for o in order_b]
+            out = out.orderBy(*[Column(o) for o in fixed])
+    else:
+        if order_b:
+            df = df.orderBy(*[Column(o) for o in order_b])
+        out = df.select(*proj)
     if limit is not None:
         out = out.limit(limit)
     return out
-
-
-def _strip_qualifiers(e: Expr, columns: List[str]) -> Expr:
-    import copy
-    if isinstance(e, ColRef):
-        try:
-            return ColRef(_resolve(e.col_name, columns))
-        except AnalysisException:
-            return e
-    e2 = copy.copy(e)
-    for attr in ("l", "r", "x", "otherwise"):
-        if hasattr(e2, attr) and isinstance(getattr(e2, attr), Expr):
-            setattr(e2, attr, _strip_qualifiers(getattr(e2, attr), columns))
-    if hasattr(e2, "args"):
-        e2.args = [_strip_qualifiers(a, columns) for a in e2.args]
-        e2.children = list(e2.args)
-    elif hasattr(e2, "branches"):
-        e2.branches = [(_strip_qualifiers(c, columns), _strip_qualifiers(v, columns)) for c, v in e2.branches]
-        e2.children = [k for br in e2.branches for k in br] + ([e2.otherwise] if e2.otherwise is not None else [])
-    else:
-        e2.children = [getattr(e2, a) for a in ("l", "r", "x") if hasattr(e2, a) and isinstance(getattr(e2, a), Expr)]
-    return e2
 
 
 def _order_item(p: Parser) -> Expr:
@@ -754,24 +867,3 @@ def _order_item(p: Parser) -> Expr:
         if not nulls_first:
             p.expect_kw("last")
     return SortOrder(e, asc, nulls_first)
-
-
-def _equi_keys(cond: Expr, lcols, rcols, lk, rk):
-    if isinstance(cond, BinOp) and cond.op == "and":
-        _equi_keys(cond.l, lcols, rcols, lk, rk)
-        _equi_keys(cond.r, lcols, rcols, lk, rk)
-        return
-    if isinstance(cond, BinOp) and cond.op == "==" and isinstance(cond.l, ColRef) and isinstance(cond.r, ColRef):
-        a, b = cond.l.col_name, cond.r.col_name
-        try:
-            la, rb = _resolve(a, lcols), _resolve(b, rcols)
-            lk.append(la)
-            rk.append(rb)
-            return
-        except AnalysisException:
-            pass
-        lb, ra = _resolve(b, lcols), _resolve(a, rcols)
-        lk.append(lb)
-        rk.append(ra)
-        return
-    raise AnalysisException("only equality join conditions (combined with AND) are supported")

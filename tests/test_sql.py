@@ -201,3 +201,78 @@ def test_to_pandas_vector_column(spark):
     v = VectorAssembler(inputCols=["a", "b"], outputCol="f").transform(df)
     rows = v.collect()
     assert rows[1].f.toArray().tolist() == [2.0, 4.0]
+
+
+def _mle01_tables(spark, seed=0):
+    rng = np.random.default_rng(seed)
+    n_movies, n_users = 400, 300
+    movies = pd.DataFrame({"ID": np.arange(n_movies), "title": [f"movie {i}" for i in range(n_movies)]})
+    # popular movies get many ratings, so both HAVING thresholds select a proper subset
+    mid = np.minimum(rng.zipf(1.3, 60000) - 1, n_movies - 1)
+    ratings = pd.DataFrame({"userId": rng.integers(1, n_users, 60000), "movieId": mid,
+                            "rating": rng.integers(1, 6, 60000).astype(np.float64)})
+    pred = movies.rename(columns={"ID": "movieId"}).assign(userId=0)
+    pred["prediction"] = np.round(rng.random(n_movies) * 5, 3)
+    return movies, ratings, pred
+
+
+def test_sql_join_aliases_mle01_verbatim(spark):
+    """Both MLE 01 queries verbatim (S/ML Electives/MLE 01 - Collaborative Filtering Lab.py:246-252,366-374)
+    on tables that share userId / movieId / rating, checked against pandas."""
+    movies, ratings, pred = _mle01_tables(spark)
+    spark.createDataFrame(movies).createOrReplaceTempView("movies")
+    spark.createDataFrame(ratings).createOrReplaceTempView("ratings")
+    spark.createDataFrame(pred).createOrReplaceTempView("predictions")
+    q1 = spark.sql("""
+        SELECT movieId, title, AVG(rating) AS avg_rating, COUNT(*) AS num_ratings
+        FROM ratings r JOIN movies m ON (r.movieID = m.ID)
+        GROUP BY r.movieId, m.title
+        HAVING COUNT(*) > 500
+        ORDER BY avg_rating DESC
+        LIMIT 100""").toPandas()
+    m = ratings.merge(movies, left_on="movieId", right_on="ID")
+    e1 = (m.groupby(["movieId", "title"]).agg(avg_rating=("rating", "mean"), num_ratings=("rating", "size"))
+          .reset_index())
+    e1 = e1[e1.num_ratings > 500].sort_values("avg_rating", ascending=False).head(100)
+    assert list(q1.columns) == ["movieId", "title", "avg_rating", "num_ratings"]
+    assert 0 < len(q1) == len(e1)
+    np.testing.assert_allclose(q1.avg_rating.values, e1.avg_rating.values)
+    assert sorted(q1.movieId.tolist()) == sorted(e1.movieId.tolist())
+
+    q2 = spark.sql("""
+        SELECT p.title, p.prediction AS your_predicted_rating
+        FROM ratings r INNER JOIN predictions p
+        ON (r.movieID = p.movieID)
+        WHERE p.userId = 0
+        GROUP BY p.title, p.prediction
+        HAVING COUNT(*) > 75
+        ORDER BY p.prediction DESC
+        LIMIT 25""").toPandas()
+    j = ratings.merge(pred, on="movieId", suffixes=("_r", "_p"))
+    j = j[j.userId_p == 0]
+    e2 = j.groupby(["title", "prediction"]).size().reset_index(name="n")
+    e2 = e2[e2.n > 75].sort_values("prediction", ascending=False).head(25)
+    assert list(q2.columns) == ["title", "your_predicted_rating"]
+    assert 0 < len(q2) == len(e2)
+    np.testing.assert_allclose(q2.your_predicted_rating.values, e2.prediction.values)
+
+
+def test_sql_qualified_and_ambiguous_names(spark):
+    from cdnaml.sql.column import AnalysisException
+    spark.createDataFrame(pd.DataFrame({"k": [1, 2, 3], "v": [10.0, 20.0, 30.0]})).createOrReplaceTempView("ta")
+    spark.createDataFrame(pd.DataFrame({"k": [1, 2, 4], "v": [-1.0, -2.0, -4.0]})).createOrReplaceTempView("tb")
+    out = spark.sql("SELECT b.v FROM ta a JOIN tb b ON (a.k = b.k) ORDER BY b.v").toPandas()
+    assert out.v.tolist() == [-2.0, -1.0]
+    out = spark.sql("SELECT a.v AS av, b.v AS bv FROM ta a JOIN tb b ON a.k = b.k ORDER BY a.k").toPandas()
+    assert out.av.tolist() == [10.0, 20.0] and out.bv.tolist() == [-1.0, -2.0]
+    # the table name qualifies when there is no alias
+    out = spark.sql("SELECT tb.v FROM ta JOIN tb ON ta.k = tb.k WHERE ta.v > 15").toPandas()
+    assert out.v.tolist() == [-2.0]
+    with pytest.raises(AnalysisException, match="ambiguous"):
+        spark.sql("SELECT v FROM ta a JOIN tb b ON (a.k = b.k)").toPandas()
+    # USING merges the key: a bare key is not ambiguous, and both qualifiers reach it
+    out = spark.sql("SELECT k, a.k AS ak, b.v FROM ta a JOIN tb b USING (k) ORDER BY k").toPandas()
+    assert out.k.tolist() == [1, 2] and out.ak.tolist() == [1, 2] and out.v.tolist() == [-1.0, -2.0]
+    out = spark.sql("SELECT a.*, b.v AS w FROM ta a LEFT JOIN tb b ON a.k = b.k ORDER BY a.k").toPandas()
+    assert list(out.columns) == ["k", "v", "w"]
+    assert out.w.isna().tolist() == [False, False, True]
