@@ -29,6 +29,68 @@ import torch
 from .base import Trials
 
 
+def _captured_frames(fn) -> list:
+    """DataFrames an objective reaches without creating them: closure cells, default arguments, the module
+    globals its code names, ``functools.partial`` arguments -- one level deep plus nested helper functions
+    (in a fixed order, so every rank replicates the same frames in the same collective order)."""
+    import functools
+    import types
+
+    from ..sql.dataframe import DataFrame
+    out, seen_fn, seen_df = [], set(), set()
+
+    def visit_value(v, depth):
+        if isinstance(v, DataFrame):
+            if id(v) not in seen_df:
+                seen_df.add(id(v))
+                out.append(v)
+        elif isinstance(v, (list, tuple)):
+            for x in v:
+                visit_value(x, depth)
+        elif isinstance(v, dict):
+            for x in v.values():
+                visit_value(x, depth)
+        elif isinstance(v, functools.partial):
+            visit_value(v.func, depth)
+            visit_value(v.args, depth)
+            visit_value(v.keywords, depth)
+        elif isinstance(v, (types.FunctionType, types.MethodType)) and depth < 3:
+            visit_fn(v, depth + 1)
+
+    def visit_fn(f, depth):
+        f = getattr(f, "__func__", f)
+        if id(f) in seen_fn or not hasattr(f, "__code__"):
+            return
+        seen_fn.add(id(f))
+        for cell in f.__closure__ or ():
+            try:
+                visit_value(cell.cell_contents, depth)
+            except ValueError:  # empty cell
+                pass
+        visit_value(f.__defaults__ or (), depth)
+        g = getattr(f, "__globals__", {})
+        for name in f.__code__.co_names:
+            if name in g:
+                visit_value(g[name], depth)
+    visit_value(fn, 0)
+    return out
+
+
+def _replicate_captured_frames(fn, session, rank_local) -> list:
+    """Swap the plan of every captured (rank-sharded) DataFrame for a replicated copy of the whole table;
+    returns [(frame, original plan)] to restore after the search."""
+    frames = _captured_frames(fn)
+    restore = []
+    for df in frames:
+        pdf = df.toPandas()                     # collective: every rank gets every row, in global order
+        schema = df.schema
+        with rank_local(session):
+            rep = session.createDataFrame(pdf, schema)
+        restore.append((df, df._plan))
+        df._plan = rep._plan
+    return restore
+
+
 class GPUTrials(Trials):
     def __init__(self, parallelism: Optional[int] = None, timeout: Optional[float] = None,
                  devices: Optional[List[int]] = None, spark_session=None, autolog: bool = True):
@@ -78,6 +140,17 @@ class GPUTrials(Trials):
             session.comm = saved
 
     def _run_spmd(self, comm, session, fn, space, next_assignment, should_stop, max_evals):
+        # DataFrames the objective closes over were sharded under the GLOBAL communicator (1/W of the rows
+        # on each rank); a rank-local trial must see the whole table, as a SparkTrials task does, so they
+        # are replicated on every rank for the duration of the search
+        restore = _replicate_captured_frames(fn, session, self._rank_local)
+        try:
+            return self._run_spmd_loop(comm, session, fn, space, next_assignment, should_stop, max_evals)
+        finally:
+            for df, plan in restore:
+                df._plan = plan
+
+    def _run_spmd_loop(self, comm, session, fn, space, next_assignment, should_stop, max_evals):
         from .fmin import _TrialLogger, evaluate_trial
         log = _TrialLogger(self) if comm.rank == 0 else None
         W, me = comm.world_size, comm.rank

@@ -24,6 +24,7 @@ Three pieces, used by ``Model.transform``, ``tracking.pyfunc.spark_udf`` and the
 from __future__ import annotations
 
 import os
+import threading
 from collections import OrderedDict
 from typing import Callable, Dict, Iterable, Iterator, Optional
 
@@ -45,6 +46,7 @@ class ForestPredictor:
         self.base = base
         self._dev: Dict[str, tuple] = {}
         self._graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
+        self._lock = threading.Lock()
         self._seen: Dict[tuple, int] = {}
         self.replays = 0
         self.captures = 0
@@ -74,7 +76,15 @@ class ForestPredictor:
         """[n, d] features -> [n, K] float32 predictions (a fresh tensor the caller owns)."""
         if not (GRAPH_PREDICT and X.is_cuda and X.shape[0] >= GRAPH_MIN_ROWS and X.is_contiguous()):
             return self._launch(X)
+        if threading.current_thread() is not threading.main_thread():
+            # worker threads (applyInPandas pools, GPUTrials, GroupedModel) may allocate or synchronise while
+            # another thread captures: graphs are captured and replayed from the main thread only
+            return self._launch(X)
         key = (X.data_ptr(), tuple(X.shape), X.dtype, X.device.index)
+        with self._lock:
+            return self._graph_call(X, key)
+
+    def _graph_call(self, X: torch.Tensor, key) -> torch.Tensor:
         g = self._graphs.get(key)
         if g is None:
             # capture on the second sighting of a buffer: staging buffers recur, one-off tensors do not
@@ -88,7 +98,7 @@ class ForestPredictor:
                 self._launch(X)  # warm-up outside capture (allocator, LDS attributes)
             torch.cuda.current_stream(X.device).wait_stream(s)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 out = self._launch(X)
             g = (graph, out)
             self._graphs[key] = g

@@ -244,14 +244,16 @@ class TrainValidationSplit(Estimator):
         seed = self.getSeed() if self.getSeed() is not None else 0x5EED
         tr = self.getTrainRatio()
         train, valid = dataset.randomSplit([tr, 1 - tr], seed)
-        train, valid = train.cache(), valid.cache()
         if FusedTreeTuner.supported(est, maps):
+            # the fused fits read the binned dataset through a weight mask: only the validation split is kept
+            valid = valid.cache()
             fused = FusedTreeTuner(est, maps, dataset)
             # randomSplit's own draw (sql/dataframe.py): the row is in `train` iff its uniform < tr
             models = fused.fit_split(fused.row_uniform(seed) < tr)
             res = [(m, ev.evaluate(m.transform(valid))) for m in models]
         else:
             fused = None
+            train, valid = train.cache(), valid.cache()
             res = _run_maps(est, maps, train, valid, ev, self.getParallelism(), dataset._session)
         metrics = [m for _, m in res]
         best = int(np.argmax(metrics) if ev.isLargerBetter() else np.argmin(metrics))

@@ -42,7 +42,19 @@ _MAX_STACK = 16
 _DT_CODE = {torch.float64: 0, torch.float32: 1, torch.int32: 2, torch.int64: 3, torch.bool: 4}
 _OUT_T = {T.DoubleType: torch.float64, T.FloatType: torch.float32, T.IntegerType: torch.int32,
           T.LongType: torch.int64, T.BooleanType: torch.bool}
-_NUM_IN = (T.DoubleType, T.FloatType, T.IntegerType, T.LongType, T.BooleanType)
+
+
+class _LongIn(T.LongType):
+    """Static type of a 64-bit integer INPUT (a LongType column, or a long literal of magnitude >= 2^53).
+
+    The kernel's operand stack is fp64, so such a value is exact only below 2^53 (monotonically_increasing_id
+    on rank >= 1 is far above it).  Flowing into double arithmetic / math functions / a cast to double is what
+    Spark itself does (long -> double promotion), so that fuses; anything that must keep the value as a long --
+    the result, a CASE value, a cast to int/long, abs/round, an ordering or equality test against another long
+    -- stays on the int64 operator path."""
+
+
+_NUM_IN = (T.DoubleType, T.FloatType, T.IntegerType, T.LongType, T.BooleanType, _LongIn)
 
 
 class _Unfusable(Exception):
@@ -85,7 +97,7 @@ def _compile(e: Expr, b, p: _Prog) -> T.DataType:
             p.inputs.append(name)
         p.nullable |= c.valid is not None
         p.emit("LOAD", p.inputs.index(name))
-        return c.dtype
+        return _LongIn() if _is(c.dtype, T.LongType) else c.dtype
     if isinstance(e, Lit):
         v = e.value
         if v is None:
@@ -97,6 +109,8 @@ def _compile(e: Expr, b, p: _Prog) -> T.DataType:
                 raise _Unfusable("literal type")
             p.consts.append(float(v))
             p.emit("CONST", len(p.consts) - 1)
+            if isinstance(v, int) and not isinstance(v, bool) and abs(v) >= 2 ** 53:
+                return _LongIn()
             return e.dtype
         raise _Unfusable("literal")
     if isinstance(e, BinOp):
@@ -113,6 +127,9 @@ def _compile(e: Expr, b, p: _Prog) -> T.DataType:
             p.emit(_BIN[op], pops=2)
             return T.BooleanType()
         if op in ("==", "!=", "<", "<=", ">", ">=", "<=>"):
+            if isinstance(lt, _LongIn) and _is(rt, T.LongType, _LongIn) or \
+                    isinstance(rt, _LongIn) and _is(lt, T.LongType, _LongIn):
+                raise _Unfusable("long comparison")   # two 64-bit values: fp64 rounding can merge them
             p.emit(_BIN[op], pops=2)
             return T.BooleanType()
         if op in ("&", "|", "^"):
@@ -155,6 +172,8 @@ def _compile(e: Expr, b, p: _Prog) -> T.DataType:
         dt = e.dt
         if not (_is(t, *_NUM_IN) or isinstance(t, T.NullType)):
             raise _Unfusable("cast source")
+        if isinstance(t, _LongIn) and not _is(dt, T.DoubleType, T.FloatType, T.BooleanType):
+            raise _Unfusable("long cast")
         if _is(dt, T.DoubleType):
             return dt
         if _is(dt, T.FloatType):
@@ -199,6 +218,8 @@ def _compile(e: Expr, b, p: _Prog) -> T.DataType:
             vts.append(_compile(val, b, p))
             p.emit("CASE", pops=3)
         dts = [t for t in vts if not isinstance(t, T.NullType)]
+        if any(isinstance(t, _LongIn) for t in dts):
+            raise _Unfusable("long case value")
         if not dts or any(not _is(t, *_NUM_IN) for t in dts):
             raise _Unfusable("case value type")
         dt = dts[0]
@@ -218,6 +239,8 @@ def _compile(e: Expr, b, p: _Prog) -> T.DataType:
         if not _is(t, *_NUM_IN):
             raise _Unfusable("function arg")
         name, extra = tag if isinstance(tag, tuple) else (tag, None)
+        if isinstance(t, _LongIn) and name in ("abs", "round"):
+            raise _Unfusable("long abs/round")
         if name in _MATH:
             if name in ("ln", "log10", "log2", "log1p", "sqrt"):
                 p.nullable = True
@@ -264,7 +287,7 @@ def _program(e: Expr, b):
     try:
         p = _Prog()
         rt = _compile(e, b, p)
-        if _op_count(p) < 2 or not _is(rt, *_NUM_IN):
+        if _op_count(p) < 2 or not _is(rt, *_NUM_IN) or isinstance(rt, _LongIn):
             res = None                     # a single torch op is already one kernel
         else:
             res = (p, rt)

@@ -206,9 +206,38 @@ def scenario_hyperopt(spark):
             "best_reg": round(float(best["reg"]), 12), "n": len(trials.trials)}
 
 
+def scenario_hyperopt_captured(spark):
+    """the objective closes over DataFrames created BEFORE fmin (the course pattern, ML 08:91-104):
+    each rank-local trial must still fit on the whole table, so the losses equal the one-process search."""
+    from cdnaml.hyperopt import GPUTrials, fmin, hp, tpe
+    from cdnaml.ml.evaluation import RegressionEvaluator
+    from cdnaml.ml.feature import VectorAssembler
+    from cdnaml.ml.regression import LinearRegression
+    rng = np.random.default_rng(2)
+    X = rng.normal(size=(500, 3))
+    pdf = pd.DataFrame(X, columns=["a", "b", "c"])
+    pdf["label"] = X @ np.array([0.5, 1.0, -1.5]) + 0.2 * rng.normal(size=500)
+    train_df = spark.createDataFrame(pdf)                     # sharded: 1/W of the rows on each rank
+    va = VectorAssembler(inputCols=["a", "b", "c"], outputCol="features")
+    assembled = va.transform(train_df)                        # a vector column, captured too
+
+    def objective(p):
+        m = LinearRegression(regParam=p["reg"]).fit(assembled)
+        n = train_df.count()
+        return round(RegressionEvaluator().evaluate(m.transform(va.transform(train_df))), 9) + 1000.0 * (n != 500)
+
+    trials = GPUTrials(parallelism=2)
+    fmin(objective, {"reg": hp.loguniform("reg", -6, 0)}, algo=tpe.suggest, max_evals=6, trials=trials,
+         rstate=np.random.default_rng(3))
+    # after the search the captured frame is sharded again
+    return {"losses": [round(float(x), 9) for x in trials.losses()], "n_after": train_df.count(),
+            "restored": sum(b.n for b in train_df._local()) == 500 // spark.comm.world_size}
+
+
 SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault, "trees": scenario_trees,
              "trees_uneven": scenario_trees_uneven, "cv": scenario_cv, "als": scenario_als,
-             "hyperopt": scenario_hyperopt}
+             "hyperopt": scenario_hyperopt,
+             "hyperopt_captured": scenario_hyperopt_captured}
 
 
 def run(name):

@@ -124,7 +124,8 @@ def test_bench_trains_identical_forest_on_1_2_4_8_ranks(tmp_path):
 
 
 @pytest.mark.parametrize("scenario,worlds", [("trees", (2, 4)), ("trees_uneven", (2, 4)), ("cv", (2,)),
-                                             ("als", (2, 4)), ("hyperopt", (2,))])
+                                             ("als", (2, 4)), ("hyperopt", (2,)),
+                                             ("hyperopt_captured", (2,))])
 def test_models_identical_across_world_sizes(scenario, worlds, tmp_path):
     """RF (T=20), DecisionTree, GBT, XGBoost regressor (packed unit-hessian path) and classifier (hessian
     path), RF classifier, CrossValidator and ALS at W ranks equal the 1-rank fit (tree models bit-identical;

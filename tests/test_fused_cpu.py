@@ -67,3 +67,40 @@ def test_fused_programs_match_operator_path_on_host(spark):
         gv, rv = got.values.double().numpy()[gm], ref.values.double().numpy()[rm]
         # libm transcendentals may differ in the last ulp; everything else is exact
         assert np.allclose(gv, rv, rtol=1e-12, atol=1e-300, equal_nan=True), str(e._expr)
+
+
+def test_fused_long_inputs_above_2p53(spark):
+    """64-bit integers above 2^53 (monotonically_increasing_id on rank >= 1) must not pass through the
+    fp64 operand stack where the result keeps them as longs; where they do fuse (double arithmetic, the same
+    long -> double promotion Spark applies) the host reference of the kernel equals the operator path."""
+    from cdnaml.models.util import local_batch
+    from cdnaml.sql import fused
+    from cdnaml.sql import functions as F
+    from cdnaml.sql.column import EvalContext
+    base = (1 << 33) * 3 + (1 << 53)
+    ids = base + np.arange(5000, dtype=np.int64)            # odd ids are not representable in fp64
+    pdf = pd.DataFrame({"id": ids, "x": np.linspace(-2, 2, 5000), "k": np.arange(5000).astype(np.int32)})
+    df = spark.createDataFrame(pdf)
+    b = local_batch(df, ["id", "x", "k"])
+    i_, x_, k_ = F.col("id"), F.col("x"), F.col("k")
+    refused = [F.when(x_ > 0, i_).otherwise(-1),            # a CASE value keeps the long
+               F.when(x_ > 0, i_ * 1.0).otherwise(i_),
+               (i_ * 1.0 > 0) & (i_ == i_ + 0),            # long == long
+               ((x_ > 0) & (i_ == int(base + 1))),          # long == a literal above 2^53
+               (i_ % 7 + x_).cast("int"),                   # hmm: long % int is long arithmetic
+               (i_ * 1.0).cast("long") + 0,
+               i_.cast("int") + x_,                         # long -> int cast through fp64
+               F.abs(i_) + x_]
+    for e in refused:
+        assert fused._program(e._expr, b) is None, str(e._expr)
+    ok = [i_ / 1000.0 + x_, (i_ * 1.0 > 1e3) & (x_ > 0), F.log(i_ * 1.0) + x_, i_.cast("double") * 2.0 - x_,
+          (k_ < 100) | (i_ * 1.0 > x_)]
+    for e in ok:
+        prog = fused._program(e._expr, b)
+        assert prog is not None, str(e._expr)
+        got = fused.interpret(prog[0], prog[1], b)
+        ref = e._expr.eval(b, EvalContext(spark))
+        assert np.array_equal(got.values.double().numpy(), ref.values.double().numpy()), str(e._expr)
+    # end to end: the operator path keeps odd ids exact
+    out = df.select(F.when(x_ > 0, i_).otherwise(-1).alias("v")).toPandas().v.to_numpy()
+    np.testing.assert_array_equal(out, np.where(pdf.x > 0, ids, -1))
