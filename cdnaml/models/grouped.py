@@ -90,7 +90,7 @@ def _fit_groups(tuner, e, T_: int, gid: torch.Tensor, groups: List[int]):
     from .classification import _num_classes
     from .regression import _bag_weights, _combine_weights, resolve_subset
     from .tree.engine import ForestTrainer, TreeParams
-    session, data, y, w, seed, meta = tuner.prep(e)
+    session, data, y, w, seed, meta = tuner.prep(e)[:6]
     if tuner.kind == "rf":
         strategy, bootstrap, rate = e.getFeatureSubsetStrategy(), e.getBootstrap(), e.getSubsamplingRate()
     else:

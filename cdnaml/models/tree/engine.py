@@ -60,6 +60,13 @@ PARTITION_RM = __import__("os").environ.get("CDNAML_PARTITION_RM", "0") != "0"
 MSEG_SUBSET = __import__("os").environ.get("CDNAML_MSEG_SUBSET", "0") != "0"
 # multi-rank record histograms: slot chunks whose all-reduces overlap the next chunk's histogram kernel
 HIST_OVERLAP = int(__import__("os").environ.get("CDNAML_HIST_OVERLAP", "4"))
+# feature-subset regression forests (RandomForestRegressor, featureSubsetStrategy auto / onethird / sqrt ...):
+# every node of a level built over its m sampled features only, items generated from the row codes on the fly
+# (subhist.hip) -- no record compaction, no sibling subtraction, 34 instead of 100 lane-ops per item.  Exact
+# (same forest), but opt-in: at the headline it measured 227 ms (v1) / 375 ms (v2) of histograms per step
+# against 87 + 19 ms for records + subtraction, because building BOTH children doubles the gathered row lines
+# at every level below the root (profiles/r3/subhist_ab.md)
+SUB_HIST = __import__("os").environ.get("CDNAML_SUB_HIST", "0") != "0"
 
 
 @dataclass
@@ -820,6 +827,46 @@ class ForestTrainer:
         return bgain, bf, bb, lstats, rstats, order, cat_feats, None
 
     # ------------------------------------------------------------ training
+    def _sub_hist_ok(self, mseg_ok: bool, need_masks: bool, stats_rows) -> bool:
+        """Subset histograms (subhist.hip) for this fit: packed regression statistics, a per-node feature subset
+        of at most half the features, <= 256 bins, and on the GPU a 128-byte row-major bins copy."""
+        p, data = self.p, self.data
+        if not (SUB_HIST and mseg_ok and need_masks and stats_rows.get("v0") is None and not self.classification):
+            return False
+        m = p.feature_subset
+        if m is None or m > K.SUB_HIST_MAX_M or 2 * m > data.d or data.B > 256 or data.categorical:
+            return False
+        if self.device.type == "cuda":
+            rm = data.row_major_bins()
+            if rm is None or rm.shape[1] * rm.shape[2] != 128 or K.sub_hist_ns_max(data.B, m) < 1:
+                return False
+        return True
+
+    def _sub_hist(self, data, codes, v1, qs1, tfirst_h, slot_tree, feats, B, wmax, dev):
+        """A level's subset histograms; on several ranks in HIST_OVERLAP slot chunks, each chunk's int64 sums
+        all-reduced on the collective stream while the next chunk is built (exact: the same sums as one
+        all-reduce)."""
+        S, m = feats.shape
+        rm = data.row_major_bins() if dev.type == "cuda" else None
+        Hc = torch.zeros((S, m, B, 2), dtype=torch.int64, device=dev)
+        k = min(HIST_OVERLAP, S) if self.comm.distributed else 1
+        bounds = np.linspace(0, S, max(k, 1) + 1).round().astype(np.int64)
+        pend = []
+        for c in range(max(k, 1)):
+            s0, s1 = int(bounds[c]), int(bounds[c + 1])
+            if s1 <= s0:
+                continue
+            with _tr.span("tree.sub_hist", slots=s1 - s0):
+                K.sub_hist(codes, v1, qs1, data.bins, rm, tfirst_h, slot_tree, feats, B, wmax, s0, s1, out=Hc[s0:s1])
+            if self.comm.distributed:
+                with _tr.span("tree.allreduce_async", cat="comm", bytes=(s1 - s0) * m * B * 16):
+                    pend.append(self.comm.all_reduce_async(Hc[s0:s1]))
+        if pend:
+            with _tr.span("tree.allreduce_wait", cat="comm"):
+                for h in pend:
+                    h.wait()
+        return Hc
+
     def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev):
         """Record histograms of a level's S slots in HIST_OVERLAP slot chunks; chunk c's all-reduce runs on the
         collective stream while chunk c + 1 is built (one per-level RCCL all-reduce of 1-50 MB otherwise
@@ -867,7 +914,8 @@ class ForestTrainer:
         # ... and with per-node feature subsets (RandomForest) only each node's sampled features are
         # accumulated (packed statistics only: no v0)
         subset_seg = mseg_ok and need_masks and MSEG_SUBSET and stats_rows.get("v0") is None
-        masked = need_masks and (HIST_MODE == "masked" or subset_seg)
+        use_sub = self._sub_hist_ok(mseg_ok, need_masks, stats_rows) and not subset_seg
+        masked = need_masks and (HIST_MODE == "masked" or subset_seg or use_sub)
         subtract = not masked
         # one regression tree: rows grouped by node in a permutation (segment mode)
         use_mseg = mseg_ok and (not masked or subset_seg)
@@ -892,7 +940,7 @@ class ForestTrainer:
         elif use_codes:
             codes, wmax = K.codes_init_max(weights, T, n, dev)
             node = None
-            if use_mseg:
+            if use_mseg or use_sub:
                 # one quantisation scale for every rank: the int64 level histograms then all-reduce to
                 # the same sums on 1 or N GPUs (the forest does not depend on the GPU count)
                 v0s = stats_rows.get("v0")
@@ -942,8 +990,16 @@ class ForestTrainer:
             tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
             hist_raw_scale = None
             reduced = False
+            sub_feats = None
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
-                if use_mseg and (depth >= 1 or MSEG_L0):
+                if use_sub:
+                    # every active node over its sampled features; exact int64 (count, sum w q) [A, m, B, 2]
+                    sub_feats = _mask_feature_lists(masks_np, d)
+                    Hb = self._sub_hist(data, codes, stats_rows["v1"], mseg_scales[1], tfirst.numpy(), a_tree,
+                                        sub_feats, B, wmax, dev)
+                    hist_raw_scale = mseg_raw
+                    reduced = True
+                elif use_mseg and (depth >= 1 or MSEG_L0):
                     # gather the rows of the built nodes into slot segments, then segment histograms
                     # packed item records on every device (the CPU emulates the HIP compaction + flat histogram
                     # exactly, so gloo ranks traverse the integer path RCCL ranks take)
@@ -1000,7 +1056,9 @@ class ForestTrainer:
             # ---- assemble every active node's histogram
             derived = np.nonzero(~build)[0]
             is_raw = Hb.dtype == torch.int64
-            if is_raw or len(derived):
+            if sub_feats is not None:
+                H = Hb if dev.type == "cuda" else K.sub_hist_expand(Hb, sub_feats, d, mseg_raw)
+            elif is_raw or len(derived):
                 # one kernel (CPU: the same arithmetic in torch): fixed-point -> fp64 and parent - sibling
                 H = K.hist_assemble(Hb, hist_raw_scale if is_raw else None, prev_hist if len(derived) else None,
                                     slot_of, a_parent, a_sib)
@@ -1010,8 +1068,12 @@ class ForestTrainer:
             if self._native_split(dev):
                 # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
                 mb = p.impurity == "xgb" and self.data.missing_bin
-                so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
-                                       p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight, missing_bin=mb)
+                if sub_feats is not None:
+                    so, tot = K.split_scan_sub(H, sub_feats, self._nthr_dev(dev), mseg_raw, p.min_instances)
+                else:
+                    so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
+                                           p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight,
+                                           missing_bin=mb)
                 # so [A, 8] = gain, feature, bin, left (2), right (2), missing-goes-right: copied to the host as is
                 # (plus the node totals at level 0), no per-column device ops
                 sw = so.shape[1]

@@ -1,27 +1,30 @@
-"""Fused tree-ensemble tuning: CrossValidator / TrainValidationSplit over ONE binned dataset
-(ML 07 - Random Forests and Hyperparameter Tuning.py:72-158,
-Labs/ML 07L - Hyperparameter Tuning Lab.py:105-141).
+"""Fused tree-ensemble tuning: CrossValidator / TrainValidationSplit over a tree estimator, or over a
+``Pipeline`` ending in one, fit once per data split instead of once per param map
+(ML 07 - Random Forests and Hyperparameter Tuning.py:72-158 -- the CV of
+``Pipeline([StringIndexer, VectorAssembler, rf])`` at ML 07:107 --, Labs/ML 07L - Hyperparameter Tuning
+Lab.py:105-141).
 
 The generic tuner fits every (fold, param map) pair from scratch: the course's 2 x 2 grid with 3 folds is
-12 fits + 1 refit, each re-sampling quantiles, re-binning 1e8 x 100 features and re-drawing bootstraps.
-For the engine's tree ensembles three facts make most of that work shared:
+12 fits + 1 refit, each re-fitting the pipeline's prefix stages, re-sampling quantiles, re-binning and
+re-drawing bootstraps.  Two facts make most of that work shared WITHOUT changing any result:
 
-* The binned matrix depends on the features, ``maxBins`` and ``seed`` only.  It is built once per
-  (maxBins, seed), from the global quantile sample of the whole dataset, and kept in HBM for every fold,
-  map and the refit.  The generic path bins each training fold's own sample instead; this is a deliberate
-  divergence from Spark: the split candidates see the validation rows' features, never their labels.
-* A fold is a weight mask.  Rows whose Philox fold id (the same draw as the generic path's ``__fold``
-  column) equals f get weight 0, multiplied into the Poisson bootstrap weights.  No fold is copied out.
+* Everything up to the tree estimator's histograms depends on the split's training rows, the prefix
+  stages and (maxBins, seed) only -- not on ``numTrees`` / ``maxDepth``.  Per split, the prefix stages are
+  fitted once, the training rows transformed once, and the binned matrix built once, exactly as one
+  generic fit on that split builds them (the same filtered DataFrame, the same global row ids, the same
+  quantile sample and Poisson streams).
 * Tree t of a forest sees bootstrap stream (seed, t) and feature subsets hashed from (seed, t, node), and
   its level-d histograms are exact integers.  So among maps that differ only in ``numTrees`` and
   ``maxDepth``, every model is a prefix of the largest one: the first ``numTrees`` trees, cut at
-  ``maxDepth`` (a node at depth D keeps its stored leaf value).  One forest per fold, with the largest
-  numTrees and maxDepth of the group, gives the whole grid, bit-identically to fitting each map
-  (``tests/test_tuning_fused.py``).  The 2 x 2 x 3 grid becomes 3 fits of 10 trees at depth 5.
+  ``maxDepth`` (a node at depth D keeps its stored leaf value).  One forest per split, with the largest
+  numTrees and maxDepth of the group, gives the whole grid.
 
-Maps are grouped by everything else (including the resolved feature-subset size, and numTrees == 1, which
-switches off bagging).  Regression groups also split at maxDepth 8, because deeper trees take a different
-histogram path.  Estimators other than the engine's DecisionTree / RandomForest use the generic path.
+Hence the fused CV's ``avgMetrics``, ``bestModel`` and sub-models are bit-identical to the generic path's
+(``tests/test_tuning_fused.py`` pins it for bare estimators and pipelines): the 2 x 2 x 3 grid becomes 3
+forest fits + 1 refit.  Maps are grouped by everything else (including the resolved feature-subset size,
+and numTrees == 1, which switches off bagging); regression groups also split at maxDepth 8 (a different
+histogram path).  A Pipeline qualifies when its last stage is one of the engine's DecisionTree /
+RandomForest estimators and every param map touches that stage only.
 """
 from __future__ import annotations
 
@@ -80,18 +83,34 @@ def truncate_forest(forest: Forest, num_trees: int, max_depth: int) -> Forest:
 
 
 class FusedTreeTuner:
-    """Fits all param maps of a tree estimator fold by fold on shared binned data (see module doc)."""
+    """Fits all param maps of a tree estimator (or of a Pipeline ending in one) per data split (module doc)."""
 
-    def __init__(self, est, maps: List[dict], dataset):
-        self.est = est
-        self.kind, self.cls = estimator_kind(est)
+    def __init__(self, est, maps: List[dict], dataset=None):
+        from ..pipeline import Pipeline
+        self.pipeline = est if isinstance(est, Pipeline) else None
+        self.prefix = est.getStages()[:-1] if self.pipeline is not None else []
+        self.tree = est.getStages()[-1] if self.pipeline is not None else est
+        self.kind, self.cls = estimator_kind(self.tree)
+        self.maps = list(maps) or [{}]
+        self.ests = [self.tree.copy(pm) if pm else self.tree for pm in self.maps]
         self.dataset = dataset
-        self.ests = [est.copy(pm) if pm else est for pm in maps]
-        self._preps: Dict[tuple, tuple] = {}
-        self.groups = self._group()
+
+    @staticmethod
+    def supported(est, maps) -> bool:
+        from ..pipeline import Pipeline
+        if not FUSED_TUNING:
+            return False
+        if isinstance(est, Pipeline):
+            stages = est.getStages()
+            if not stages or estimator_kind(stages[-1]) is None:
+                return False
+            uid = stages[-1].uid
+            # every map must touch the tree stage only: the prefix is then the same for all maps
+            return all(getattr(p, "parent", None) == uid for pm in (maps or []) for p in pm)
+        return estimator_kind(est) is not None
 
     # ------------------------------------------------------------------ planning
-    def _key(self, e) -> tuple:
+    def _key(self, e, d: int) -> tuple:
         from ..regression import resolve_subset
         vals = []
         for p, v in sorted(e.extractParamMap().items(), key=lambda kv: kv[0].name):
@@ -101,44 +120,31 @@ class FusedTreeTuner:
         T = e.getNumTrees() if self.kind == "rf" else 1
         D = e.getMaxDepth()
         strategy = e.getFeatureSubsetStrategy() if self.kind == "rf" else "all"
-        d = self.prep(e)[1].d
         sub = resolve_subset(strategy, d, T, self.cls)
         return tuple(vals) + (("subset", sub), ("bagged", T > 1), ("deep", (not self.cls) and D > 8))
 
-    def _group(self) -> List[List[int]]:
+    def groups(self, d: int) -> List[List[int]]:
         groups: Dict[tuple, List[int]] = {}
         for j, e in enumerate(self.ests):
-            groups.setdefault(self._key(e), []).append(j)
+            groups.setdefault(self._key(e, d), []).append(j)
         return list(groups.values())
 
-    @staticmethod
-    def supported(est, maps) -> bool:
-        return FUSED_TUNING and estimator_kind(est) is not None
-
     # ------------------------------------------------------------------ training
-    def prep(self, e):
-        """Binned data of the whole dataset for (maxBins, seed, columns): built once, shared by folds + refit."""
-        from ..regression import _default_seed, tree_fit_prepare
-        seed = e.getOrDefault("seed")
-        seed = _default_seed(type(e)) if seed is None else seed
-        key = (e.getMaxBins(), seed, e.getFeaturesCol(), e.getLabelCol(), e.getWeightCol())
-        if key not in self._preps:
-            self._preps[key] = tree_fit_prepare(e, self.dataset, classification=self.cls)
-        return self._preps[key]
+    def prefix_fit(self, train):
+        """The pipeline's prefix stages fitted on ``train`` (once per split) -> (PipelineModel | None, train
+        transformed)."""
+        if self.pipeline is None:
+            return None, train
+        from ..pipeline import Pipeline
+        pm = Pipeline(stages=self.prefix).fit(train)
+        return pm, pm.transform(train)
 
-    def row_uniform(self, seed: int) -> torch.Tensor:
-        """Per local row: the Philox uniform(seed, global row, stream 11) of ``DataFrame._with_global_uniform``
-        (the generic tuner's fold draw and ``randomSplit``'s draw)."""
-        data = self.prep(self.ests[0])[1]
-        return K.uniform(data.n_local, seed, data.row_offset, 11, device=data.bins.device)
-
-    def fold_ids(self, seed: int, k: int) -> torch.Tensor:
-        return torch.floor(self.row_uniform(seed) * k).to(torch.int32)
-
-    def fit_forest(self, e, T: int, D: int, mask: Optional[torch.Tensor]) -> Tuple[Forest, int]:
+    def fit_forest(self, prep, e, T: int, D: int, mask: Optional[torch.Tensor] = None) -> Tuple[Forest, int]:
+        """One forest of ``e``'s params with T trees of depth D on prepared (binned) training data -- what
+        ``e.fit`` does after its own ``tree_fit_prepare``."""
         from ..classification import _num_classes
         from ..regression import _bag_weights, _combine_weights, resolve_subset
-        session, data, y, w, seed, meta = self.prep(e)
+        session, data, y, w, seed, meta, train = prep
         if self.kind == "rf":
             strategy, bootstrap, rate = e.getFeatureSubsetStrategy(), e.getBootstrap(), e.getSubsamplingRate()
         else:
@@ -146,7 +152,7 @@ class FusedTreeTuner:
         subset = resolve_subset(strategy, data.d, T, self.cls)
         C = 0
         if self.cls:
-            C = max(2, _num_classes(session, y, (self.dataset.schema[e.getLabelCol()].metadata or {}).get("ml_attr")))
+            C = max(2, _num_classes(session, y, (train.schema[e.getLabelCol()].metadata or {}).get("ml_attr")))
         p = TreeParams(max_depth=D, max_bins=e.getMaxBins(), min_instances=float(e.getMinInstancesPerNode()),
                        min_info_gain=e.getMinInfoGain(), impurity=e.getImpurity(), num_classes=C,
                        feature_subset=subset, bootstrap=bootstrap, subsampling_rate=rate, seed=seed)
@@ -158,6 +164,29 @@ class FusedTreeTuner:
             weights = m.expand(T, -1).contiguous() if weights is None else (weights * m).contiguous()
         stats = {"label": y.int()} if self.cls else {"v0": None, "v1": y.float()}
         return ForestTrainer(session, data, p).train(T, stats, weights), data.d
+
+    def prep(self, e):
+        """Binned data of the tuner's whole dataset (cached per (maxBins, seed, columns)): the shared input of the
+        batched per-group fits (models/grouped.py)."""
+        cache = self.__dict__.setdefault("_preps", {})
+        key = self._prep_key(e)
+        if key not in cache:
+            cache[key] = self.prepare(e, self.dataset)
+        return cache[key]
+
+    def fit_forest_mask(self, e, T: int, D: int, mask: Optional[torch.Tensor]) -> Tuple[Forest, int]:
+        """A forest on the whole dataset's bins with the rows outside ``mask`` weighted 0."""
+        return self.fit_forest(self.prep(e), e, T, D, mask)
+
+    def prepare(self, e, train):
+        """Binned training data for (maxBins, seed, columns) -- ``tree_fit_prepare`` of the generic fit."""
+        from ..regression import tree_fit_prepare
+        return tree_fit_prepare(e, train, classification=self.cls) + (train,)
+
+    @staticmethod
+    def _prep_key(e) -> tuple:
+        return (e.getMaxBins(), e.getOrDefault("seed"), e.getFeaturesCol(), e.getLabelCol(),
+                e.getWeightCol() if e.hasParam("weightCol") else None)
 
     def model(self, e, forest: Forest, d: int):
         """The estimator's own model class around a (truncated) forest."""
@@ -173,23 +202,44 @@ class FusedTreeTuner:
         m._post_fit(e)
         return m
 
-    def fit_split(self, mask: Optional[torch.Tensor]) -> List:
-        """Models of every map trained on the rows where ``mask`` is 1 (all rows when None)."""
-        models = [None] * len(self.ests)
-        for grp in self.groups:
+    def fit_split(self, train) -> Tuple[list, object]:
+        """Every map fitted on the DataFrame ``train`` -> (models, prefix model or None).  Models are the tree
+        models (wrapped in the map's PipelineModel for a Pipeline), each equal to ``est.fit(train, map)``."""
+        from ..pipeline import PipelineModel
+        pm, tt = self.prefix_fit(train)
+        models: list = [None] * len(self.ests)
+        preps: Dict[tuple, tuple] = {}   # binned data per (maxBins, seed, columns): shared by the groups
+        d = 0
+        for e in self.ests:
+            key = self._prep_key(e)
+            if key not in preps:
+                preps[key] = self.prepare(e, tt)
+            d = preps[key][1].d
+        for grp in self.groups(d):
             es = [self.ests[j] for j in grp]
+            e0 = es[0]
+            key = self._prep_key(e0)
             Tm = max((e.getNumTrees() if self.kind == "rf" else 1) for e in es)
             Dm = max(e.getMaxDepth() for e in es)
-            forest, d = self.fit_forest(es[0], Tm, Dm, mask)
+            forest, dd = self.fit_forest(preps[key], e0, Tm, Dm)
             for j, e in zip(grp, es):
                 T = e.getNumTrees() if self.kind == "rf" else 1
                 D = e.getMaxDepth()
                 sub = forest if (T == Tm and D == Dm) else truncate_forest(forest, T, D)
-                models[j] = self.model(e, sub, d)
-        return models
+                tm = self.model(e, sub, dd)
+                if pm is not None:
+                    full = PipelineModel(list(pm.stages) + [tm])
+                    full.uid = self.pipeline.uid
+                    tm = full
+                models[j] = tm
+        return models, pm
 
-    def refit(self, j: int):
-        """Map j on the full dataset (the binned data is shared; identical to ``est.fit(dataset, map_j)``)."""
-        e = self.ests[j]
-        forest, d = self.fit_forest(e, e.getNumTrees() if self.kind == "rf" else 1, e.getMaxDepth(), None)
-        return self.model(e, forest, d)
+    def evaluate(self, models, prefix_model, valid, evaluator) -> List[float]:
+        """Metric of every model on ``valid`` (a Pipeline's prefix transforms ``valid`` once for all maps)."""
+        if prefix_model is None:
+            return [evaluator.evaluate(m.transform(valid)) for m in models]
+        vt = prefix_model.transform(valid).cache()
+        try:
+            return [evaluator.evaluate(m.stages[-1].transform(vt)) for m in models]
+        finally:
+            vt.unpersist()

@@ -4,10 +4,11 @@
 row id) — the same folds on 1 or 8 GPUs — materialises the fold-tagged data
 once in HBM (``cache``), and evaluates folds × param maps.
 
-For the engine's DecisionTree / RandomForest estimators the folds × maps run
-through ``tree/fused.py``: the dataset is binned ONCE, a fold is a weight mask,
-and every map of a (numTrees, maxDepth) grid is a prefix of one forest per fold
-("4 maps × 3 folds + 1 refit" = 3 forest fits + 1 refit on shared bins).
+For the engine's DecisionTree / RandomForest estimators -- bare or as the last
+stage of a Pipeline -- the folds × maps run through ``tree/fused.py``: per fold
+the prefix stages are fitted and the training rows binned once, and every map
+of a (numTrees, maxDepth) grid is a prefix of one forest ("4 maps × 3 folds + 1
+refit" = 3 forest fits + 1 refit), bit-identical to fitting each map.
 Other estimators take the generic path: ``parallelism`` > 1 runs param maps
 concurrently on separate HIP streams of the same GPU (single-process jobs); in
 multi-GPU SPMD jobs each fit is itself data-parallel over all ranks and maps
@@ -113,21 +114,20 @@ class CrossValidator(Estimator):
                 "__fold", F.floor(F.col("__u") * k).cast("int")).drop("__u").cache()
         metrics = np.zeros((len(maps), k))
         subs = [[None] * len(maps) for _ in range(k)]
-        fused = FusedTreeTuner(est, maps, dataset) if (not fold_col and FusedTreeTuner.supported(est, maps)) \
-            else None
+        fused = FusedTreeTuner(est, maps, dataset) if FusedTreeTuner.supported(est, maps) else None
         for f in range(k):
             valid = tagged.filter(F.col("__fold") == f).drop("__fold")
+            train = tagged.filter(F.col("__fold") != f).drop("__fold")
             if fused is not None:
-                valid = valid.cache()  # evaluated once per map: compact the fold's rows once
-                # one binned dataset, the fold as a weight mask, one forest per map group (tree/fused.py)
-                folds = fused.fold_ids(seed, k)
-                models = fused.fit_split(folds != f)
-                res = [(m, ev.evaluate(m.transform(valid))) for m in models]
-            else:
-                train = tagged.filter(F.col("__fold") != f).drop("__fold")
-                res = _run_maps(est, maps, train, valid, ev, self.getParallelism(), session)
-            if fused is not None:
+                # one prefix fit + one binned training set + one forest per map group for the fold, every map
+                # a prefix of that forest: the generic path's models, bit for bit (tree/fused.py)
+                train, valid = train.cache(), valid.cache()
+                models, prefix = fused.fit_split(train)
+                res = list(zip(models, fused.evaluate(models, prefix, valid, ev)))
+                train.unpersist()
                 valid.unpersist()
+            else:
+                res = _run_maps(est, maps, train, valid, ev, self.getParallelism(), session)
             for j, (m, met) in enumerate(res):
                 metrics[j, f] = met
                 if self.getCollectSubModels():
@@ -135,7 +135,7 @@ class CrossValidator(Estimator):
         avg = metrics.mean(1)
         std = metrics.std(1)
         best = int(np.argmax(avg) if ev.isLargerBetter() else np.argmin(avg))
-        best_model = fused.refit(best) if fused is not None else est.fit(dataset, maps[best])
+        best_model = est.fit(dataset, maps[best])
         tagged.unpersist()
         cvm = CrossValidatorModel(best_model, avg.tolist(), subs if self.getCollectSubModels() else None,
                                   std.tolist())
@@ -244,20 +244,16 @@ class TrainValidationSplit(Estimator):
         seed = self.getSeed() if self.getSeed() is not None else 0x5EED
         tr = self.getTrainRatio()
         train, valid = dataset.randomSplit([tr, 1 - tr], seed)
+        train, valid = train.cache(), valid.cache()
         if FusedTreeTuner.supported(est, maps):
-            # the fused fits read the binned dataset through a weight mask: only the validation split is kept
-            valid = valid.cache()
             fused = FusedTreeTuner(est, maps, dataset)
-            # randomSplit's own draw (sql/dataframe.py): the row is in `train` iff its uniform < tr
-            models = fused.fit_split(fused.row_uniform(seed) < tr)
-            res = [(m, ev.evaluate(m.transform(valid))) for m in models]
+            models, prefix = fused.fit_split(train)
+            res = list(zip(models, fused.evaluate(models, prefix, valid, ev)))
         else:
-            fused = None
-            train, valid = train.cache(), valid.cache()
             res = _run_maps(est, maps, train, valid, ev, self.getParallelism(), dataset._session)
         metrics = [m for _, m in res]
         best = int(np.argmax(metrics) if ev.isLargerBetter() else np.argmin(metrics))
-        bm = fused.refit(best) if fused is not None else est.fit(dataset, maps[best])
+        bm = est.fit(dataset, maps[best])
         tvm = TrainValidationSplitModel(bm, metrics, [m for m, _ in res] if self.getCollectSubModels() else None)
         tvm._post_fit(self)
         return tvm

@@ -120,6 +120,12 @@ _SIGS = {
                         c_void_p, c_void_p], c_int),
     "cdna_partition7": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_sub_hist": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
+                       c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p], c_int),
+    "cdna_sub_hist_slot_bytes": ([c_int, c_int], c_int),
+    "cdna_sub_hist_lds_budget": ([], c_int),
+    "cdna_split_scan_sub": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_double, c_double, c_void_p, c_void_p,
+                             c_void_p], c_int),
     "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double,
                          c_double, c_double, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_compact_mask": ([c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p], c_int),

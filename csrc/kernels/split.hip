@@ -220,3 +220,108 @@ CDNA_API int cdna_hist_assemble(const void* Hb, int raw, double scale0, double s
                      scale1, prev, map, A, cells, K, H);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// K6 over compact feature-subset histograms (subhist.hip): H [A][m][B][2] exact
+// int64 (count, sum w q * s1) of each node's m sampled features feats [A][m]
+// (ascending).  Same variance gain, legality and tie order (lowest f * B + b)
+// as split_scan_kernel on the full [A][d][B][2] fp64 histogram: the fp64
+// values are the same exact integers over a power-of-two scale, so every sum
+// below is exact and the decisions and child statistics are bit-identical.
+// Node totals: the first sampled feature (every feature's bins hold the same
+// total weight).  No hist_assemble pass: the int64 sums are read directly.
+// ---------------------------------------------------------------------------
+namespace {
+struct SplitSubArgs {
+  const long long* H;
+  const uint8_t* feats;
+  const int* nthr;
+  int A, m, B;
+  double scale1;
+  double min_inst;
+  double* out;
+  double* tot_out;
+};
+
+__global__ __launch_bounds__(kThreads) void split_scan_sub_kernel(const SplitSubArgs a) {
+  __shared__ double s_g[kThreads];
+  __shared__ int s_k[kThreads];
+  const int node = blockIdx.x;
+  const long long* Hn = a.H + (int64_t)node * a.m * a.B * 2;
+  const uint8_t* fl = a.feats + (int64_t)node * a.m;
+  double t0 = 0.0, t1 = 0.0;
+  for (int b = 0; b < a.B; ++b) {  // every thread: the node totals from sampled feature 0
+    t0 += (double)Hn[2 * b];
+    t1 += (double)Hn[2 * b + 1] / a.scale1;
+  }
+  double best = -__builtin_inf();
+  int bk = 0x7FFFFFFF;
+  SplitArgs g{};
+  g.kind = 0;
+  g.min_inst = a.min_inst;
+  for (int k = threadIdx.x; k < a.m; k += kThreads) {
+    const int f = fl[k];
+    const int lim = a.nthr[f] < 0 ? 0 : a.nthr[f];
+    const long long* hf = Hn + (int64_t)k * a.B * 2;
+    double l0 = 0.0, l1 = 0.0;
+    for (int b = 0; b < a.B && b < lim; ++b) {
+      l0 += (double)hf[2 * b];
+      l1 += (double)hf[2 * b + 1] / a.scale1;
+      bool ok;
+      const double gn = gain_of(g, l0, l1, t0 - l0, t1 - l1, t0, t1, &ok);
+      if (ok && gn == gn && gn != __builtin_inf() && gn != -__builtin_inf() && gn > best) {
+        best = gn;
+        bk = f * a.B + b;
+      }
+    }
+  }
+  s_g[threadIdx.x] = best;
+  s_k[threadIdx.x] = bk;
+  __syncthreads();
+  for (int o = kThreads / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const int j = threadIdx.x + o;
+      if (s_g[j] > s_g[threadIdx.x] || (s_g[j] == s_g[threadIdx.x] && s_k[j] < s_k[threadIdx.x])) {
+        s_g[threadIdx.x] = s_g[j];
+        s_k[threadIdx.x] = s_k[j];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double* o = a.out + (int64_t)node * 8;
+    const int k0 = s_k[0];
+    const bool found = k0 != 0x7FFFFFFF;
+    const int f = found ? k0 / a.B : 0, b = found ? k0 - f * a.B : 0;
+    double l0 = 0.0, l1 = 0.0;
+    if (found) {
+      int kk = 0;
+      while (kk < a.m && fl[kk] != f) ++kk;
+      const long long* hf = Hn + (int64_t)kk * a.B * 2;
+      for (int q = 0; q <= b; ++q) {
+        l0 += (double)hf[2 * q];
+        l1 += (double)hf[2 * q + 1] / a.scale1;
+      }
+    }
+    o[0] = found ? s_g[0] : -__builtin_inf();
+    o[1] = f;
+    o[2] = b;
+    o[3] = l0;
+    o[4] = l1;
+    o[5] = t0 - l0;
+    o[6] = t1 - l1;
+    o[7] = 0.0;
+    a.tot_out[node * 2] = t0;
+    a.tot_out[node * 2 + 1] = t1;
+  }
+}
+}  // namespace
+
+CDNA_API int cdna_split_scan_sub(const long long* H, const uint8_t* feats, const int* nthr, int A, int m, int B,
+                                 double scale1, double min_inst, double* out, double* tot_out, hipStream_t st) {
+  if (A <= 0) return 0;
+  if (m <= 0 || B <= 0 || m > 255 || !(scale1 > 0.0)) return (int)hipErrorInvalidValue;
+  SplitSubArgs a{H, feats, nthr, A, m, B, scale1, min_inst, out, tot_out};
+  hipLaunchKernelGGL(split_scan_sub_kernel, dim3((unsigned)A), dim3(kThreads), 0, st, a);
+  return (int)hipGetLastError();
+}

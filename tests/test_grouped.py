@@ -42,7 +42,7 @@ def test_grouped_estimator_equals_per_group_fits(spark, kind):
     for g in range(6):
         mask = torch.from_numpy(keys == g).to(dev)
         T = est.getNumTrees() if kind != "dt" else 1
-        alone, _ = tuner.fit_forest(tuner.ests[0], T, est.getMaxDepth(), mask)
+        alone, _ = tuner.fit_forest_mask(tuner.ests[0], T, est.getMaxDepth(), mask)
         assert forest_digest(gm.models[g]._forest) == forest_digest(alone), g
     # each row is scored by its own group's model
     pred = gm.transform(df).select("device_id", "features", "prediction").toPandas()

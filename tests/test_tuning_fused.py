@@ -29,55 +29,88 @@ def _est(kind, **kw):
 
 @pytest.mark.parametrize("kind", ["rf", "rfc", "dt", "dtc"])
 def test_grid_prefix_models_equal_separate_fits(spark, kind):
-    """Every map's model cut from the group's largest forest == that map fitted alone (same fold mask)."""
+    """Every map's model cut from the group's largest forest == that map fitted alone on the same split."""
     from cdnaml.ml.tuning import ParamGridBuilder
     from cdnaml.models.tree.fused import FusedTreeTuner
     df = _df(spark, cls=kind in ("rfc", "dtc"))
+    train = df.randomSplit([0.7, 0.3], seed=7)[0].cache()
     est = _est(kind)
     gb = ParamGridBuilder().addGrid(est.maxDepth, [2, 4, 5])
     if kind in ("rf", "rfc"):
         gb = gb.addGrid(est.numTrees, [3, 7])
     maps = gb.build()
     tuner = FusedTreeTuner(est, maps, df)
-    assert len(tuner.groups) == 1
-    mask = tuner.fold_ids(7, 3) != 1
-    fused = tuner.fit_split(mask)
+    assert len(tuner.groups(8)) == 1
+    fused, prefix = tuner.fit_split(train)
+    assert prefix is None
     for j, pm in enumerate(maps):
-        e = est.copy(pm)
-        T = e.getNumTrees() if kind in ("rf", "rfc") else 1
-        alone, _ = tuner.fit_forest(e, T, e.getMaxDepth(), mask)
-        assert forest_digest(fused[j]._forest) == forest_digest(alone), pm
+        alone = est.fit(train, pm)
+        assert forest_digest(fused[j]._forest) == forest_digest(alone._forest), pm
 
 
-def test_cross_validator_fused_matches_per_map_fits_and_refit(spark):
-    """CrossValidator through the fused path: avgMetrics equal evaluating each map fitted alone on each fold
-    mask, and bestModel equals a plain fit of the best map on the whole dataset."""
+def _cv_both_ways(monkeypatch, make_cv, df):
+    """(fused, generic) CrossValidatorModels of the same CV, plus the number of forests each trained."""
+    from cdnaml.models.tree import engine, fused as fz
+    calls = []
+    orig = engine.ForestTrainer.train
+
+    def counting(self, *a, **k):
+        calls.append(1)
+        return orig(self, *a, **k)
+    monkeypatch.setattr(engine.ForestTrainer, "train", counting)
+    out = []
+    for flag in (True, False):
+        monkeypatch.setattr(fz, "FUSED_TUNING", flag)
+        calls.clear()
+        out.append((make_cv().fit(df), len(calls)))
+    return out
+
+
+def test_cross_validator_fused_is_the_generic_cv(spark, monkeypatch):
+    """ML 07:81-130: CrossValidator(rf, 2 x 2 grid, 3 folds) through the fused path equals the generic path --
+    avgMetrics, bestModel -- bit for bit, with 3 forest fits + 1 refit instead of 12 + 1."""
     from cdnaml.ml.evaluation import RegressionEvaluator
     from cdnaml.ml.regression import RandomForestRegressor
     from cdnaml.ml.tuning import CrossValidator, ParamGridBuilder
-    from cdnaml.models.tree.fused import FusedTreeTuner
     df = _df(spark, n=2500)
     rf = RandomForestRegressor(maxBins=40, seed=42)
     grid = ParamGridBuilder().addGrid(rf.maxDepth, [2, 5]).addGrid(rf.numTrees, [5, 10]).build()
-    ev = RegressionEvaluator()
-    cvm = CrossValidator(estimator=rf, estimatorParamMaps=grid, evaluator=ev, numFolds=3, seed=42).fit(df)
-    tuner = FusedTreeTuner(rf, grid, df)
-    tagged = df._with_global_uniform(42, "__u")
-    from cdnaml.sql import functions as F
-    tagged = tagged.withColumn("__fold", F.floor(F.col("__u") * 3).cast("int")).drop("__u")
-    folds = tuner.fold_ids(42, 3)
-    expect = np.zeros((4, 3))
-    for f in range(3):
-        valid = tagged.filter(F.col("__fold") == f).drop("__fold")
-        for j, pm in enumerate(grid):
-            e = rf.copy(pm)
-            forest, d = tuner.fit_forest(e, e.getNumTrees(), e.getMaxDepth(), folds != f)
-            expect[j, f] = ev.evaluate(tuner.model(e, forest, d).transform(valid))
-    assert cvm.avgMetrics == pytest.approx(expect.mean(1).tolist(), rel=0, abs=0)
-    best = int(np.argmin(expect.mean(1)))
-    plain = rf.copy(grid[best]).fit(df)
-    assert forest_digest(cvm.bestModel._forest) == forest_digest(plain._forest)
-    assert cvm.bestModel.getMaxDepth() == grid[best][rf.maxDepth]
+    (fz, n_f), (gen, n_g) = _cv_both_ways(monkeypatch, lambda: CrossValidator(
+        estimator=rf, estimatorParamMaps=grid, evaluator=RegressionEvaluator(), numFolds=3, seed=42), df)
+    assert (n_f, n_g) == (3 + 1, 12 + 1)
+    assert fz.avgMetrics == gen.avgMetrics
+    assert forest_digest(fz.bestModel._forest) == forest_digest(gen.bestModel._forest)
+
+
+def test_cross_validator_fused_pipeline_ml07(spark, monkeypatch):
+    """ML 07:107 -- CrossValidator(estimator=Pipeline([StringIndexer, VectorAssembler, rf])): the prefix is fitted
+    per fold as Spark does, the grid shares one forest per fold, and the result equals the generic path's."""
+    from cdnaml.ml import Pipeline
+    from cdnaml.ml.evaluation import RegressionEvaluator
+    from cdnaml.ml.feature import StringIndexer, VectorAssembler
+    from cdnaml.ml.regression import RandomForestRegressor
+    from cdnaml.ml.tuning import CrossValidator, ParamGridBuilder
+    rng = np.random.default_rng(4)
+    n = 2400
+    pdf = pd.DataFrame({"room": rng.choice(["entire", "private", "shared", "hotel"], n, p=[.5, .3, .15, .05]),
+                        "hood": rng.choice([f"h{i}" for i in range(37)], n),
+                        "beds": rng.integers(1, 6, n).astype(float), "lat": rng.normal(size=n)})
+    pdf["price"] = 50 * pdf.beds + (pdf.room == "entire") * 80 + 5 * pdf.lat + rng.normal(size=n) * 10
+    df = spark.createDataFrame(pdf)
+    si = StringIndexer(inputCols=["room", "hood"], outputCols=["roomIndex", "hoodIndex"], handleInvalid="skip")
+    va = VectorAssembler(inputCols=["roomIndex", "hoodIndex", "beds", "lat"], outputCol="features")
+    rf = RandomForestRegressor(labelCol="price", maxBins=40, seed=42)
+    pipe = Pipeline(stages=[si, va, rf])
+    grid = ParamGridBuilder().addGrid(rf.maxDepth, [2, 5]).addGrid(rf.numTrees, [5, 10]).build()
+    (fz, n_f), (gen, n_g) = _cv_both_ways(monkeypatch, lambda: CrossValidator(
+        estimator=pipe, estimatorParamMaps=grid, evaluator=RegressionEvaluator(labelCol="price"), numFolds=3,
+        seed=42), df)
+    assert (n_f, n_g) == (3 + 1, 12 + 1)
+    assert fz.avgMetrics == gen.avgMetrics
+    assert forest_digest(fz.bestModel.stages[-1]._forest) == forest_digest(gen.bestModel.stages[-1]._forest)
+    # a map touching a prefix stage keeps the generic path
+    from cdnaml.models.tree.fused import FusedTreeTuner
+    assert not FusedTreeTuner.supported(pipe, [{si.handleInvalid: "keep", rf.maxDepth: 2}])
 
 
 def test_fused_groups_split_on_non_grid_params(spark):
@@ -90,7 +123,7 @@ def test_fused_groups_split_on_non_grid_params(spark):
     rf = RandomForestRegressor(maxBins=32, seed=1)
     maps = ParamGridBuilder().addGrid(rf.numTrees, [1, 4]).addGrid(rf.minInstancesPerNode, [1, 20]).build()
     tuner = FusedTreeTuner(rf, maps, df)
-    assert len(tuner.groups) == 4
+    assert len(tuner.groups(8)) == 4
 
 
 def test_train_validation_split_fused(spark):
