@@ -113,17 +113,21 @@ def fmin(fn: Callable, space, algo=None, max_evals: Optional[int] = None, timeou
                 return True
         return False
 
+    from ..models.tree import bincache
     runner = getattr(trials, "_run_parallel", None)
-    if runner is not None and getattr(trials, "parallelism", 1) > 1:
-        runner(fn, space, next_assignment, should_stop, max_evals, catch_eval_exceptions)
-    else:
-        log = _TrialLogger(trials)
-        while not should_stop():
-            a = next_assignment()
-            tr = trials.new_trial(a, space)
-            evaluate_trial(fn, space, tr, catch_eval_exceptions)
-            log.log(tr, a)
-        log.close()
+    # the trials of this search share binned training data (the same features re-binned per trial otherwise);
+    # the cache lives only until fmin returns
+    with bincache.scope():
+        if runner is not None and getattr(trials, "parallelism", 1) > 1:
+            runner(fn, space, next_assignment, should_stop, max_evals, catch_eval_exceptions)
+        else:
+            log = _TrialLogger(trials)
+            while not should_stop():
+                a = next_assignment()
+                tr = trials.new_trial(a, space)
+                evaluate_trial(fn, space, tr, catch_eval_exceptions)
+                log.log(tr, a)
+            log.close()
     if not return_argmin:
         return trials
     return trials.argmin

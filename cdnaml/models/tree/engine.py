@@ -67,6 +67,12 @@ HIST_OVERLAP = int(__import__("os").environ.get("CDNAML_HIST_OVERLAP", "4"))
 # against 87 + 19 ms for records + subtraction, because building BOTH children doubles the gathered row lines
 # at every level below the root (profiles/r3/subhist_ab.md)
 SUB_HIST = __import__("os").environ.get("CDNAML_SUB_HIST", "0") != "0"
+# Level histograms of at least this many bytes (int64, distributed, regression / XGBoost statistics, no
+# categorical features) are reduce-scattered by feature instead of all-reduced: every rank receives the sums of
+# d / W features (1/W of an all-reduce's bytes per GPU), runs K6 on its slice, and the per-node winners are
+# all-gathered (a few hundred bytes).  Once a fit switches a tree pass over, its later levels stay
+# reduce-scattered (sibling subtraction needs the parent's slice).  GBDT at max_bin=256, d=100: levels >= 5.
+RS_MIN_BYTES = int(__import__("os").environ.get("CDNAML_RS_MIN_BYTES", str(4 << 20)))
 
 
 @dataclass
@@ -234,6 +240,17 @@ def _global_sample(session, X: torch.Tensor, max_bins: int, seed: int, row_offse
 
 def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins: int, seed: int,
                 row_offset: int, n_global: int, missing: Optional[float] = None) -> BinnedData:
+    """:func:`_make_binned`, reused across the trials of one hyperparameter search (bincache.scope(), entered by
+    fmin; never outside one)."""
+    from . import bincache
+    return bincache.cached(
+        lambda: (bincache.fingerprint(X), tuple(sorted(categorical.items())), int(max_bins), int(seed),
+                 int(row_offset), int(n_global), None if missing is None else float(missing), str(X.device)),
+        lambda: _make_binned(session, X, categorical, max_bins, seed, row_offset, n_global, missing))
+
+
+def _make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins: int, seed: int,
+                 row_offset: int, n_global: int, missing: Optional[float] = None) -> BinnedData:
     """Global-sample quantile thresholds + device binning.
 
     ``missing`` (XGBoost semantics, ML 11:67 ``missing=0``): NaN and values equal
@@ -588,12 +605,15 @@ class Forest:
 
 # ============================================================ trainer
 def _impurity_from_counts(c: torch.Tensor, kind: str) -> torch.Tensor:
+    # classes are summed left to right with every product rounded first (no FMA), the order K6's impurity_c
+    # (split.hip) uses, so tied category centroids order the same way on both paths
     W = c.sum(-1)
     p = c / W.clamp_min(1e-300).unsqueeze(-1)
-    if kind == "gini":
-        return 1.0 - (p * p).sum(-1)
-    lp = torch.where(p > 0, torch.log2(p.clamp_min(1e-300)), torch.zeros_like(p))
-    return -(p * lp).sum(-1)
+    q = p if kind == "gini" else torch.where(p > 0, torch.log2(p.clamp_min(1e-300)), torch.zeros_like(p))
+    s = p[..., 0] * q[..., 0]
+    for i in range(1, c.shape[-1]):
+        s = s + p[..., i] * q[..., i]
+    return 1.0 - s if kind == "gini" else -s
 
 
 def _splitmix64(x: np.ndarray) -> np.ndarray:
@@ -715,17 +735,25 @@ class ForestTrainer:
         return (NATIVE_SPLIT and dev.type == "cuda" and not self.classification and not self.data.categorical and
                 self.stats_k == 2)
 
+    def _native_split_ex(self, dev) -> bool:
+        """K6 kernel for classification impurities (<= 32 classes) and categorical features (split_scan_ex)."""
+        if not (NATIVE_SPLIT and dev.type == "cuda" and self.data.B <= 256):
+            return False
+        if self.classification:
+            return self.p.impurity in ("gini", "entropy") and 1 <= self.C <= 32
+        return self.p.impurity == "variance" and self.stats_k == 2
+
     def _nthr_dev(self, dev):
         t = getattr(self, "_nthr_t", None)
         if t is None:
             t = self._nthr_t = torch.from_numpy(np.asarray(self.data.nthr, dtype=np.int32)).to(dev)
         return t
 
-    def _best_splits(self, H: torch.Tensor, tot: torch.Tensor, masks: torch.Tensor):
+    def _best_splits(self, H: torch.Tensor, tot: torch.Tensor, masks: torch.Tensor, nthr_np=None):
         """H [A, d, B, k] (f64) -> per node (gain, feat, bin, left stats, right stats, cat order)."""
         A, d, B, k = H.shape
         p = self.p
-        nthr = torch.from_numpy(self.data.nthr).to(H.device)
+        nthr = torch.from_numpy(self.data.nthr if nthr_np is None else nthr_np).to(H.device)
         cat_feats = sorted(self.data.categorical)
         Hs = H
         order = None
@@ -825,6 +853,69 @@ class ForestTrainer:
         lstats = left[ar, bf, bb]
         rstats = right[ar, bf, bb]
         return bgain, bf, bb, lstats, rstats, order, cat_feats, None
+
+    # ------------------------------------------------------------ reduce-scatter by feature
+    def _rs_want(self, Hb: torch.Tensor, rs_on: bool, sub_feats) -> bool:
+        if not self.comm.distributed or Hb.dtype != torch.int64 or sub_feats is not None:
+            return False
+        if self.data.categorical or self.classification or self.stats_k != 2:
+            return False
+        return rs_on or Hb.numel() * 8 >= RS_MIN_BYTES
+
+    def _reduce_scatter_features(self, Hb: torch.Tensor, d: int):
+        """Exact int64 level histograms [S, d, B, k] summed over ranks, this rank keeping features [f0, f1)
+        (d / W of them; RCCL reduce_scatter of the feature-major copy)."""
+        W, r = self.comm.world_size, self.comm.rank
+        dc = -(-d // W)
+        S, _, B, k = Hb.shape
+        Hp = torch.zeros((W * dc, S, B, k), dtype=Hb.dtype, device=Hb.device)
+        Hp[:d] = Hb.permute(1, 0, 2, 3)
+        with _tr.span("tree.reduce_scatter", cat="comm", bytes=Hp.numel() * 8 // W):
+            mine = self.comm.reduce_scatter(Hp.view(W, -1)).view(dc, S, B, k)
+        f0 = min(d, r * dc)
+        f1 = min(d, f0 + dc)
+        return (f0, f1), mine[: f1 - f0].permute(1, 0, 2, 3).contiguous()
+
+    def _rs_split(self, H: torch.Tensor, rs, masks_np, d: int, dev):
+        """K6 over this rank's feature slice, then the per-node winners of all ranks all-gathered and merged:
+        the largest gain, ties to the lowest global candidate key (missing-right * d * B + f * B + b), the
+        order one K6 over all features uses -- so the forest is the all-reduce forest bit for bit."""
+        p = self.p
+        f0, f1 = rs
+        A, dl, B = H.shape[0], f1 - f0, H.shape[2]
+        if dl > 0:
+            mk = None
+            if masks_np is not None:
+                f = np.arange(f0, f1)
+                bits = ((masks_np[:, f >> 5] >> (f & 31).astype(np.uint32)) & 1).astype(np.uint32)
+                words = np.zeros((A, -(-dl // 32)), dtype=np.uint32)
+                for j in range(dl):
+                    words[:, j >> 5] |= bits[:, j] << np.uint32(j & 31)
+                mk, = K.upload(dev, words.view(np.int32))
+            if self._native_split(dev):
+                so, tot = K.split_scan(H, self._nthr_dev(dev)[f0:f1].contiguous(), mk,
+                                       1 if p.impurity == "xgb" else 0, p.min_instances, p.reg_lambda, p.gamma,
+                                       p.min_child_weight, missing_bin=p.impurity == "xgb" and self.data.missing_bin)
+            else:
+                tot = self._node_stats(H, None)
+                gain, bf, bb, lst, rst, _, _, mr = self._best_splits(H, tot, mk, self.data.nthr[f0:f1])
+                mr = torch.zeros_like(gain) if mr is None else mr.double()
+                so = torch.cat([gain[:, None], bf[:, None].double(), bb[:, None].double(), lst, rst, mr[:, None]], 1)
+            so = so.clone()
+            found = torch.isfinite(so[:, 0])
+            so[:, 1] += f0
+            key = torch.where(found, so[:, 7] * (d * B) + so[:, 1] * B + so[:, 2],
+                              torch.full_like(so[:, 0], float("inf")))
+        else:
+            so = torch.zeros((A, 8), dtype=torch.float64, device=H.device)
+            so[:, 0] = float("-inf")
+            tot = torch.zeros((A, 2), dtype=torch.float64, device=H.device)
+            key = torch.full((A,), float("inf"), dtype=torch.float64, device=H.device)
+        allp = self.comm.all_gather_tensor(torch.cat([so, key[:, None], tot], 1))  # [W, A, 11]
+        g, kk = allp[:, :, 0], allp[:, :, 8]
+        kk = torch.where(g == g.max(0).values[None], kk, torch.full_like(kk, float("inf")))
+        sel = allp[kk.argmin(0), torch.arange(A, device=allp.device)]
+        return sel[:, :8].contiguous(), sel[:, 9:11].contiguous()
 
     # ------------------------------------------------------------ training
     def _sub_hist_ok(self, mseg_ok: bool, need_masks: bool, stats_rows) -> bool:
@@ -961,6 +1052,7 @@ class ForestTrainer:
         a_sib = np.full(T, -1, dtype=np.int64)
         a_parent = np.full(T, -1, dtype=np.int64)
         prev_hist = None  # [A_prev, d, B, k] histograms of last level's split nodes
+        rs_on = False     # this pass reduce-scatters its level histograms by feature (RS_MIN_BYTES)
         root_ids = [None] * T
         for depth in range(p.max_depth + 1):
             A = len(a_tree)
@@ -1048,7 +1140,13 @@ class ForestTrainer:
                 else:
                     Hb = K.hist_moments(data.bins, d, node, weights, stats_rows.get("v0"), stats_rows["v1"],
                                         K.upload(dev, slot_of)[0], slot_tree, fm_build, B, id_tree=id_tree)
-            if not reduced:
+            rs_slice = None
+            if not reduced and self._rs_want(Hb, rs_on, sub_feats):
+                rs_on = True
+                rs_slice, Hb = self._reduce_scatter_features(Hb, d)
+                if prev_hist is not None and prev_hist.shape[1] == d:
+                    prev_hist = prev_hist[:, rs_slice[0]:rs_slice[1]].contiguous()
+            elif not reduced:
                 with _tr.span("tree.allreduce", cat="comm", bytes=Hb.numel() * 8):
                     self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
             _split_span = _tr.span("tree.split", depth=depth)
@@ -1065,10 +1163,13 @@ class ForestTrainer:
             else:
                 H = Hb
             masks_t = K.upload(dev, masks_np.view(np.int32))[0] if masks_np is not None else None
-            if self._native_split(dev):
+            catm_h = None  # left-category bit masks of the native categorical scan
+            if rs_slice is not None or self._native_split(dev):
                 # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
                 mb = p.impurity == "xgb" and self.data.missing_bin
-                if sub_feats is not None:
+                if rs_slice is not None:
+                    so, tot = self._rs_split(H, rs_slice, masks_np, d, dev)
+                elif sub_feats is not None:
                     so, tot = K.split_scan_sub(H, sub_feats, self._nthr_dev(dev), mseg_raw, p.min_instances)
                 else:
                     so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
@@ -1083,6 +1184,19 @@ class ForestTrainer:
                 mr_h = host[:, 7] > 0.5 if mb else None
                 if depth == 0:
                     a_stats = host[:, sw:sw + tot.shape[1]].copy()
+                order, cat_feats = None, []
+            elif self._native_split_ex(dev):
+                # classification / categorical K6 in one kernel (centroid-ordered categories, Gini / entropy)
+                so, tot, cm = K.split_scan_ex(H, self._nthr_dev(dev), masks_t, p.impurity, p.min_instances)
+                kk = tot.shape[1]
+                host = torch.cat([so, cm.double()] + ([tot] if depth == 0 else []), 1).cpu().numpy()
+                gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
+                lst_h, rst_h = host[:, 4:4 + kk], host[:, 4 + kk:4 + 2 * kk]
+                c0 = 4 + 2 * kk
+                catm_h = (host[:, c0:c0 + 8].astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)
+                mr_h = None
+                if depth == 0:
+                    a_stats = host[:, c0 + 8:c0 + 8 + kk].copy()
                 order, cat_feats = None, []
             else:
                 tot = self._node_stats(H, None)
@@ -1131,10 +1245,13 @@ class ForestTrainer:
                 for j, a in enumerate(sp.tolist()):
                     f, b = int(f_sp[j]), int(b_sp[j])
                     if f in self.data.categorical:
-                        ci = cat_feats.index(f)
-                        m = np.zeros(8, dtype=np.uint32)
-                        for c in order_h[a, ci, : b + 1]:
-                            m[int(c) >> 5] |= np.uint32(1) << np.uint32(int(c) & 31)
+                        if catm_h is not None:
+                            m = catm_h[a].copy()
+                        else:
+                            ci = cat_feats.index(f)
+                            m = np.zeros(8, dtype=np.uint32)
+                            for c in order_h[a, ci, : b + 1]:
+                                m[int(c) >> 5] |= np.uint32(1) << np.uint32(int(c) & 31)
                     elif mr_h is not None and mr_h[a]:
                         # missing (bin 0) goes right: left = bins 1..b, expressed as a bin-set split
                         m = np.zeros(8, dtype=np.uint32)

@@ -23,8 +23,12 @@ from ctypes import c_double, c_float, c_int, c_int64, c_uint32, c_uint64, c_void
 _ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 _SRC_DIR = os.path.join(_ROOT, "csrc", "kernels")
 _OUT_DIR = os.path.join(_ROOT, "cdnaml", "_native")
-LIB_PATH = os.path.join(_OUT_DIR, "libcdnaml_hip.so")
+# CDNAML_HIP_DEBUG=1: the checked build (-O1 -g -DCDNA_DEBUG: device bounds checks in the record histogram,
+# partition and predict kernels, read back after every call) in its own file next to the release library
+DEBUG = os.environ.get("CDNAML_HIP_DEBUG", "0") not in ("", "0")
+LIB_PATH = os.path.join(_OUT_DIR, "libcdnaml_hip_debug.so" if DEBUG else "libcdnaml_hip.so")
 ARCH = os.environ.get("CDNAML_OFFLOAD_ARCH", "gfx950")
+_DEBUG_UNITS = ("seg", "hist5", "trees", "hashagg")
 
 _lock = threading.Lock()
 _lib = None
@@ -35,24 +39,30 @@ def _sources():
     return sorted(glob.glob(os.path.join(_SRC_DIR, "*.hip")) + glob.glob(os.path.join(_SRC_DIR, "*.h")))
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB_PATH):
+def _path(debug: bool) -> str:
+    return os.path.join(_OUT_DIR, "libcdnaml_hip_debug.so" if debug else "libcdnaml_hip.so")
+
+
+def _stale(path: str = LIB_PATH) -> bool:
+    if not os.path.exists(path):
         return True
-    t = os.path.getmtime(LIB_PATH)
+    t = os.path.getmtime(path)
     return any(os.path.getmtime(s) > t for s in _sources())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile the HIP kernel library for gfx950 (in-tree)."""
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, debug: bool = DEBUG) -> str:
+    """Compile the HIP kernel library for gfx950 (in-tree); ``debug``: the checked build."""
+    LIB_PATH = _path(debug)
+    if not force and not _stale(LIB_PATH):
         return LIB_PATH
     os.makedirs(_OUT_DIR, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     srcs = sorted(glob.glob(os.path.join(_SRC_DIR, "*.hip")))
     tmp = LIB_PATH + f".tmp{os.getpid()}"
-    objdir = os.path.join(_OUT_DIR, f".obj{os.getpid()}")
+    objdir = os.path.join(_OUT_DIR, f".obj{os.getpid()}{'d' if debug else ''}")
     os.makedirs(objdir, exist_ok=True)
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"]
+    flags = [f"--offload-arch={ARCH}", "-O1" if debug else "-O3", "-std=c++17", "-fPIC"] + \
+        (["-g", "-DCDNA_DEBUG"] if debug else [])
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
@@ -126,6 +136,8 @@ _SIGS = {
     "cdna_sub_hist_lds_budget": ([], c_int),
     "cdna_split_scan_sub": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_double, c_double, c_void_p, c_void_p,
                              c_void_p], c_int),
+    "cdna_split_scan_ex": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_void_p,
+                            c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double,
                          c_double, c_double, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_compact_mask": ([c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
@@ -143,6 +155,19 @@ _SIGS = {
     "cdna_hash_lookup": ([c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_void_p], c_int),
     "cdna_dict_encode": ([c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_void_p,
                           c_void_p], c_int),
+    "cdna_pack_keys": ([c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p], c_int),
+    "cdna_hp_hist": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p], c_int),
+    "cdna_hp_scatter": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_hp_agg_lds_bytes": ([c_int, c_int], c_int),
+    "cdna_hp_agg_lds_budget": ([], c_int),
+    "cdna_hp_agg": ([c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                     c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_void_p], c_int),
+    "cdna_join_build": ([c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],
+                        c_int),
+    "cdna_join_probe": ([c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p], c_int),
     "cdna_grouped_reduce": ([c_int, c_void_p, c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p], c_int),
     "cdna_planar_bins": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p], c_int),
     "cdna_hist_mfma": ([c_void_p, c_int64, c_int64, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
@@ -165,7 +190,7 @@ _SIGS = {
                                  c_void_p], c_int),
     "cdna_uniform": ([c_void_p, c_int64, c_uint64, c_uint64, c_uint32, c_void_p], c_int),
     "cdna_poisson": ([c_void_p, c_int, c_int64, c_uint64, c_uint64, c_double, c_void_p], c_int),
-    "cdna_reg_metrics": ([c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p], c_int),
+    "cdna_reg_metrics": ([c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_score_hist": ([c_void_p, c_void_p, c_int64, c_double, c_double, c_int, c_void_p, c_void_p], c_int),
     "cdna_kmeans_step": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_void_p], c_int),
@@ -192,6 +217,8 @@ def lib():
                 fn = getattr(L, name)
                 fn.argtypes = args
                 fn.restype = res
+            for u in _DEBUG_UNITS:
+                getattr(L, f"cdna_debug_status_{u}").restype = c_uint32
             _lib = L
         except Exception as e:  # pragma: no cover - exercised on GPU boxes
             _load_error = e
@@ -210,3 +237,9 @@ def available() -> bool:
 def check(code: int, name: str):
     if code != 0:
         raise RuntimeError(f"native kernel {name} failed with hipError {code}")
+    if DEBUG:
+        for u in _DEBUG_UNITS:
+            v = int(getattr(_lib, f"cdna_debug_status_{u}")())
+            if v:
+                raise RuntimeError(f"checked build: device bounds check 0x{v:04X} failed in {u}.hip "
+                                   f"(after {name})")

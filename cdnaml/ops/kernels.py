@@ -892,8 +892,9 @@ def reg_metrics(y: torch.Tensor, p: torch.Tensor, w: Optional[torch.Tensor] = No
     w = None if w is None else w.double().contiguous()
     if _native(y):
         acc = torch.zeros(8, dtype=torch.float64, device=y.device)
-        _lib.check(_lib.lib().cdna_reg_metrics(_ptr(y), _ptr(p), _ptr(w), y.numel(), _ptr(acc), _stream(y.device)),
-                   "cdna_reg_metrics")
+        part = torch.empty(8 * 1024, dtype=torch.float64, device=y.device)  # per-block partials (fixed-order sum)
+        _lib.check(_lib.lib().cdna_reg_metrics(_ptr(y), _ptr(p), _ptr(w), y.numel(), _ptr(part), _ptr(acc),
+                                               _stream(y.device)), "cdna_reg_metrics")
         return acc
     ww = torch.ones_like(y) if w is None else w
     e = y - p
@@ -1709,6 +1710,27 @@ def split_scan(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor
     return out, tot
 
 
+def split_scan_ex(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor], kind: str, min_inst: float):
+    """K6 for classification impurities and categorical features (split.hip split_scan_ex_kernel).
+
+    H [A, d, B, K] fp64; nthr [d] (< 0: categorical); kind 'variance' (K = 2) / 'gini' / 'entropy'.
+    Returns (out [A, 4 + 2K] = gain, feature, position, 0, left[K], right[K]; tot [A, K]; catmask [A, 8] int32 =
+    the left categories of a categorical winner)."""
+    A, d, B, Kc = H.shape
+    assert H.dtype == torch.float64 and _native(H)
+    out = torch.empty((A, 4 + 2 * Kc), dtype=torch.float64, device=H.device)
+    tot = torch.empty((A, Kc), dtype=torch.float64, device=H.device)
+    cm = torch.empty((A, 8), dtype=torch.int32, device=H.device)
+    nt = nthr.to(device=H.device, dtype=torch.int32).contiguous()
+    m = None if masks is None else masks.to(device=H.device, dtype=torch.int32).contiguous()
+    mw = 0 if m is None else m.shape[1]
+    kd = {"variance": 0, "gini": 2, "entropy": 3}[kind]
+    _lib.check(_lib.lib().cdna_split_scan_ex(_ptr(H.contiguous()), _ptr(nt), _ptr(m), mw, A, d, B, Kc, kd,
+                                             float(min_inst), _ptr(out), _ptr(tot), _ptr(cm), _stream(H.device)),
+               "cdna_split_scan_ex")
+    return out, tot, cm
+
+
 def compact_mask(mask: torch.Tensor) -> torch.Tensor:
     """K19: int64 indices of the True entries of a 1-D mask, in order (== torch.nonzero(mask).flatten())."""
     n = mask.numel()
@@ -1846,6 +1868,152 @@ def dict_encode(arr, device):
     codes = torch.where(rep >= 0, lut[rep.clamp_min(0).long()], torch.full_like(rep, -1))
     valid = None if valid_np is None else torch.from_numpy(valid_np).to(dev)
     return codes, valid, strs[order]
+
+
+# ----------------------------------------------------------- K16 partitioned hash operators (hashagg.hip)
+HP_MAX_ACC = 4
+HP_OPS = {"sum": 0, "min": 1, "max": 2, "count": 3, "last": 4}
+_PACK_DT = {torch.uint8: 0, torch.bool: 0, torch.int16: 1, torch.int32: 2, torch.int64: 3, torch.int8: 4}
+_VAL_DT = {torch.float64: 0, torch.float32: 1, torch.int64: 2, torch.int32: 3, torch.uint8: 4, torch.bool: 4,
+           torch.int16: 5, torch.int8: 6}
+
+
+def _ptr_array(ts):
+    import ctypes
+    arr = (ctypes.c_void_p * max(1, len(ts)))(*[_ptr(t) for t in ts])
+    return arr
+
+
+def pack_keys(cols, n: int, dev) -> torch.Tensor:
+    """K16 key words: cols = [(values 1-D integer tensor, valid bool tensor or None, lo, radix)] -> int64 [n] with
+    word = sum_j code_j * prod_{l > j} radix_l, code = value - lo + 1 (null 0): equality is tuple equality and the
+    signed order is the lexicographic tuple order with nulls first.  The caller checks prod(radix) < 2^62."""
+    import ctypes
+    vals = [v.contiguous() if v.dtype != torch.bool else v.contiguous().view(torch.uint8) for v, _, _, _ in cols]
+    valids = [None if m is None else m.contiguous().view(torch.uint8) for _, m, _, _ in cols]
+    k = len(cols)
+    lo = (ctypes.c_longlong * k)(*[int(c[2]) for c in cols])
+    rdx = (ctypes.c_longlong * k)(*[int(c[3]) for c in cols])
+    dts = (ctypes.c_int * k)(*[_PACK_DT[v.dtype] for v in vals])
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    _lib.check(_lib.lib().cdna_pack_keys(k, _ptr_array(vals), _ptr_array(valids), lo, rdx, dts, n, _ptr(out),
+                                         _stream(torch.device(dev))), "cdna_pack_keys")
+    return out
+
+
+def _hp_shape(n: int, na: int):
+    L = _lib.lib()
+    S = min(65535, L.cdna_hp_agg_lds_budget() // (16 + 8 * na) - 1)
+    cap = S * 7 // 8
+    # partitions: ~70 % of the table's capacity in rows per partition (so even all-distinct keys fit), <= 2^14
+    pbits = 0
+    while pbits < 14 and n > (cap * 7 // 10) << pbits:
+        pbits += 1
+    return S, cap, pbits
+
+
+def hash_groups(key: torch.Tensor, values=(), accs=(), mode: int = 0, pout: int = 1):
+    """K16 partitioned LDS hash aggregation / dedup over int64 key words [n] (hashagg.hip).
+
+    values: [(tensor 1-D, valid or None)] scattered with the keys (<= 4); accs: [(op name, value index)] with op in
+    sum / min / max / count (non-null count) / last (value index ignored).  mode 0: aggregate; 2: aggregate and
+    also return every row's group; 1: dedup.
+
+    mode 0 / 2 -> dict(G, pos (sparse positions of the groups, partition order), key, cnt, first, acc [na][n]
+    sparse arrays, gpos (mode 2: every row's sparse group position)); mode 1 -> keep uint8 [n] (1 + output
+    partition at the first row of every key, 0 elsewhere).  None when a partition overflowed its table."""
+    n = key.numel()
+    dev = key.device
+    L = _lib.lib()
+    st = _stream(dev)
+    na = len(accs)
+    assert na <= HP_MAX_ACC and len(values) <= HP_MAX_ACC and n < (1 << 31)
+    S, cap, pbits = _hp_shape(n, na)
+    P = 1 << pbits
+    rpb = max(4096, -(-n // 512))
+    nblk = -(-n // rpb)
+    key = key.contiguous()
+    counts = torch.empty((P, nblk), dtype=torch.int32, device=dev)
+    _lib.check(L.cdna_hp_hist(_ptr(key), n, pbits, rpb, _ptr(counts), st), "cdna_hp_hist")
+    flat = counts.view(-1).long()
+    offs = (torch.cumsum(flat, 0) - flat).contiguous()
+    kout = torch.empty(n, dtype=torch.int64, device=dev)
+    rout = torch.empty(n, dtype=torch.int32, device=dev)
+    nv = len(values)
+    vout = torch.empty((max(nv, 1), n), dtype=torch.int64, device=dev) if nv else None
+    vals = [v.contiguous() if v.dtype != torch.bool else v.contiguous().view(torch.uint8) for v, _ in values]
+    vvalid = [None if m is None else m.contiguous().view(torch.uint8) for _, m in values]
+    import ctypes
+    vdt = (ctypes.c_int * max(1, nv))(*[_VAL_DT[v.dtype] for v in vals])
+    _lib.check(L.cdna_hp_scatter(_ptr(key), n, pbits, rpb, _ptr(offs), nv, _ptr_array(vals), _ptr_array(vvalid),
+                                 vdt, _ptr(kout), _ptr(rout), _ptr(vout), st), "cdna_hp_scatter")
+    ops = (ctypes.c_int * max(1, na))(*[HP_OPS[o] for o, _ in accs])
+    vcols = (ctypes.c_int * max(1, na))(*[int(j) for _, j in accs])
+    ngroups = torch.empty(P, dtype=torch.int32, device=dev)
+    if mode == 1:
+        keep = torch.zeros(n, dtype=torch.uint8, device=dev)
+        _lib.check(L.cdna_hp_agg(_ptr(kout), _ptr(rout), _ptr(vout), n, _ptr(offs), pbits, nblk, S, cap, 0, ops, vcols,
+                                 1, int(pout), None, None, None, None, _ptr(ngroups), _ptr(keep), None, st),
+                   "cdna_hp_agg(dedup)")
+        if bool((ngroups < 0).any()):
+            return None
+        return keep
+    gkey = torch.empty(n, dtype=torch.int64, device=dev)
+    gcnt = torch.empty(n, dtype=torch.int32, device=dev)
+    gfirst = torch.empty(n, dtype=torch.int32, device=dev)
+    gacc = torch.empty((max(na, 1), n), dtype=torch.int64, device=dev)
+    gpos = torch.empty(n, dtype=torch.int32, device=dev) if mode == 2 else None
+    _lib.check(L.cdna_hp_agg(_ptr(kout), _ptr(rout), _ptr(vout), n, _ptr(offs), pbits, nblk, S, cap, na, ops, vcols,
+                             int(mode), 1, _ptr(gkey), _ptr(gcnt), _ptr(gfirst), _ptr(gacc), _ptr(ngroups), None,
+                             _ptr(gpos), st), "cdna_hp_agg")
+    ng = ngroups.long()
+    csum = torch.cumsum(ng, 0)
+    ovf, G = torch.stack([(ng < 0).any().long(), csum[-1]]).cpu().tolist()
+    if ovf:
+        return None
+    starts = offs.view(P, nblk)[:, 0]
+    pos = torch.repeat_interleave(starts - (csum - ng), ng, output_size=G) + torch.arange(G, device=dev)
+    return {"G": G, "pos": pos, "key": gkey, "cnt": gcnt, "first": gfirst, "acc": gacc, "gpos": gpos}
+
+
+def ordered_to_double(u: torch.Tensor) -> torch.Tensor:
+    """Inverse of hashagg.hip's ord_of (order-preserving u64 image of an fp64)."""
+    neg = u >= 0                      # top bit clear (as int64: non-negative) <- a negative double
+    bits = torch.where(neg, ~u, u & 0x7FFFFFFFFFFFFFFF)
+    return bits.view(torch.float64)
+
+
+def join_table(keys: torch.Tensor, valid: Optional[torch.Tensor]):
+    """K16 join build side: global open-addressing table (2x the rows, >= 1024 slots) of int64 key words.
+    Returns (table, mask, first build row per slot, build rows per slot) or None on overflow."""
+    n = keys.numel()
+    dev = keys.device
+    P = 1 << max(10, (2 * max(n, 1) - 1).bit_length())
+    table = torch.full((P + 1,), _EMPTY64, dtype=torch.int64, device=dev)
+    brow = torch.full((P + 1,), (1 << 63) - 1, dtype=torch.int64, device=dev)
+    bcnt = torch.zeros(P + 1, dtype=torch.int32, device=dev)
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    v8 = None if valid is None else valid.contiguous().view(torch.uint8)
+    _lib.check(_lib.lib().cdna_join_build(_ptr(keys.contiguous()), _ptr(v8), n, _ptr(table), P - 1, _ptr(brow),
+                                          _ptr(bcnt), _ptr(ovf), _stream(dev)), "cdna_join_build")
+    return table, P - 1, brow, bcnt, ovf
+
+
+def join_probe(keys: torch.Tensor, valid: Optional[torch.Tensor], tab, want_cnt: bool = False,
+               want_slot: bool = False):
+    """K16 join probe: per probe row the first matching build row (-1: none), optionally the number of build rows
+    with its key and its table slot."""
+    table, mask, brow, bcnt, _ = tab
+    n = keys.numel()
+    dev = keys.device
+    ri = torch.empty(n, dtype=torch.int64, device=dev)
+    cnt = torch.empty(n, dtype=torch.int32, device=dev) if want_cnt else None
+    slot = torch.empty(n, dtype=torch.int64, device=dev) if want_slot else None
+    v8 = None if valid is None else valid.contiguous().view(torch.uint8)
+    _lib.check(_lib.lib().cdna_join_probe(_ptr(keys.contiguous()), _ptr(v8), n, _ptr(table), mask, _ptr(brow),
+                                          _ptr(bcnt), _ptr(ri), _ptr(cnt), _ptr(slot), _stream(dev)),
+               "cdna_join_probe")
+    return ri, cnt, slot
 
 
 GROUPED_MAX = 8192  # groups an LDS-privatised reduction holds (64 KB of fp64)

@@ -225,6 +225,44 @@ class Comm:
             dist.all_gather(bufs, pad_w)
         return [b[:s].to(t.device) for b, s in zip(bufs, sizes)]
 
+    def reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
+        """t [W, ...] (the same shape on every rank) -> this rank's slice of the element-wise sum, t.sum over
+        ranks [rank].  RCCL: one reduce_scatter (each rank receives 1/W of the bytes an all-reduce moves);
+        gloo has no reduce-scatter, so it all-reduces and slices (the same integer sums)."""
+        if not self.distributed:
+            return t[0]
+        W = self.world_size
+        assert t.shape[0] == W
+        self.calls += 1
+        self.bytes_reduced += t.numel() * t.element_size() // W
+        if self.backend == "nccl":
+            w = self._dev_tensor(t).contiguous()
+            out = torch.empty(w.shape[1:], dtype=w.dtype, device=w.device)
+            with self._guard("reduce_scatter"):
+                dist.reduce_scatter_tensor(out, w)
+            return out.to(t.device)
+        w = self._dev_tensor(t).contiguous().clone()
+        with self._guard("reduce_scatter"):
+            dist.all_reduce(w)
+        return w[self.rank].to(t.device)
+
+    def all_gather_tensor(self, t: torch.Tensor) -> torch.Tensor:
+        """Same-shape tensors of every rank stacked: [W, *t.shape]."""
+        if not self.distributed:
+            return t[None]
+        w = self._dev_tensor(t).contiguous()
+        self.calls += 1
+        if self.backend == "nccl":
+            out = torch.empty((self.world_size,) + tuple(w.shape), dtype=w.dtype, device=w.device)
+            with self._guard("all_gather"):
+                dist.all_gather_into_tensor(out, w)
+        else:
+            bufs = [torch.empty_like(w) for _ in range(self.world_size)]
+            with self._guard("all_gather"):
+                dist.all_gather(bufs, w)
+            out = torch.stack(bufs)
+        return out.to(t.device)
+
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if not self.distributed:
             return t

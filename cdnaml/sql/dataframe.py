@@ -832,11 +832,19 @@ class DataFrame:
         def fn(parts):
             keys = subset or (parts[0].names if parts else self.columns)
             P = int(session.conf.get("spark.sql.shuffle.partitions"))
-            shuffled = _shuffle(session, parts, P, keys)
-            out = []
-            for p in shuffled:
-                out.append(p.take(R.dedup_indices(p, keys)))
-            return out
+            if session.device.type == "cuda" and parts:
+                # K16: route rows as _shuffle does, then keep every key's first row in the device hash table
+                comm = session.comm
+                b = _route(session, concat_batches(parts), P, keys)
+                nloc = len([p for p in range(P) if p % comm.world_size == comm.rank])
+                out = R.dedup_partitions(b, keys, nloc)
+                if out is not None:
+                    return out
+                from ..parallel.shuffle import hash_keys
+                shuffled = _split_local(session, b, hash_keys(b, keys) % P, P)
+            else:
+                shuffled = _shuffle(session, parts, P, keys)
+            return [p.take(R.dedup_indices(p, keys)) for p in shuffled]
         return self._new(PartitionsPlan(session, f"HashAggregate(dedup {subset})", [self._plan], fn, lambda s: s))
 
     drop_duplicates = dropDuplicates
@@ -1130,6 +1138,28 @@ def _num_str(v):
 
 
 # ==================================================================== shuffles
+def _route(session, b: Batch, P: int, keys: List[str]) -> Batch:
+    """Send every row to the rank that owns its hash partition (partition p lives on rank p % W)."""
+    comm = session.comm
+    if not comm.distributed:
+        return b
+    from ..parallel.shuffle import exchange, hash_keys, unify_global_dictionaries
+    b = unify_global_dictionaries(comm, b)
+    return exchange(comm, b, (hash_keys(b, keys) % P) % comm.world_size)
+
+
+def _split_local(session, b: Batch, pid: torch.Tensor, P: int) -> List[Batch]:
+    """This rank's partitions (p % W == rank) of rows already routed here, rows in order within a partition."""
+    comm = session.comm
+    W, rank = comm.world_size, comm.rank
+    order = torch.argsort(pid, stable=True)
+    b = b.take(order)
+    pid = pid[order]
+    mine = [p for p in range(P) if p % W == rank]
+    bounds = torch.searchsorted(pid, torch.tensor(mine + [P], device=pid.device).clamp(max=P)).cpu().tolist()
+    return [b.slice(bounds[i], bounds[i + 1]) for i in range(len(mine))]
+
+
 def _shuffle(session, parts: List[Batch], P: int, keys: Optional[List[str]]) -> List[Batch]:
     """Redistribute rows into P global partitions (partition p lives on rank p % W)."""
     comm = session.comm
@@ -1139,6 +1169,8 @@ def _shuffle(session, parts: List[Batch], P: int, keys: Optional[List[str]]) -> 
     b = concat_batches(parts) if parts else None
     if b is None:
         return []
+    if P == 1 and not comm.distributed:
+        return [b]
     if keys:
         from ..parallel.shuffle import hash_keys, unify_global_dictionaries
         if comm.distributed:

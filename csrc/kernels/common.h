@@ -13,6 +13,33 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// ---------------------------------------------------------------------------
+// Checked builds (CDNAML_HIP_DEBUG=1 builds libcdnaml_hip_debug.so with -O1 -g -DCDNA_DEBUG):
+// CDNA_DCHECK(cond, code) records the first failed bounds check of a translation unit in a device word and
+// evaluates to false, so the caller skips the access instead of faulting the GPU; the host reads and clears the
+// word after every call (cdna_debug_status_<unit>, ops/_lib.py) and raises.  Release builds compile it out.
+// ---------------------------------------------------------------------------
+#ifdef CDNA_DEBUG
+static __device__ unsigned int g_cdna_dbg = 0u;
+__device__ __forceinline__ bool cdna_dbg_fail(unsigned int code) {
+  atomicCAS(&g_cdna_dbg, 0u, code);
+  return false;
+}
+#define CDNA_DCHECK(cond, code) (__builtin_expect(!!(cond), 1) ? true : cdna_dbg_fail(code))
+#define CDNA_DEBUG_EXPORT(unit)                                                          \
+  CDNA_API unsigned int cdna_debug_status_##unit() {                                     \
+    unsigned int v = 0u, z = 0u;                                                         \
+    (void)hipDeviceSynchronize();                                                        \
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_cdna_dbg), sizeof(v), 0, hipMemcpyDeviceToHost); \
+    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_cdna_dbg), &z, sizeof(z), 0, hipMemcpyHostToDevice); \
+    return v;                                                                            \
+  }
+#else
+#define CDNA_DCHECK(cond, code) true
+#define CDNA_DEBUG_EXPORT(unit) \
+  CDNA_API unsigned int cdna_debug_status_##unit() { return 0u; }
+#endif
+
 namespace cdna {
 
 constexpr int kWave = 64;

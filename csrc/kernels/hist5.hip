@@ -876,10 +876,11 @@ __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __re
         const uint32_t loc = c[u] & 0xFFu;
         if (t0 + u >= T || loc == 0xFFu) continue;
         const int id = s_tf[t0 + u] + (int)loc;
+        if (!CDNA_DCHECK(id >= 0 && id < A, 0x9701u)) continue;  // code's local node outside the level
         const int fb = s_fb[id];
         const int f = fb & 0xFFFF;
         uint32_t nl = 0xFFu;
-        if (f != 0xFFFF) {
+        if (f != 0xFFFF && CDNA_DCHECK((f >> 3) < G, 0x9702u)) {
           const int bin = tb[((f >> 3) * 256 + lr) * 8 + (f & 7)];
           const int co = s_co[id];
           const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u : bin <= (fb >> 16);
@@ -1098,3 +1099,5 @@ CDNA_API int cdna_partition5(const uint64_t* bins, int64_t n, int T, int A, uint
                      tfirst_next, split_feat, split_bin, cat_off, cat_mask, child, rm_row_bytes);
   return (int)hipGetLastError();
 }
+
+CDNA_DEBUG_EXPORT(hist5)

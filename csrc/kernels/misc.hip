@@ -153,9 +153,18 @@ __global__ __launch_bounds__(256) void reg_metrics_kernel(const double* __restri
     if (lane == 0) red[wid][k] = v;
   }
   __syncthreads();
+  // per-block partials, summed in block order by reg_metrics_final: deterministic (fp64 atomics made the RMSE of
+  // one evaluation differ from the next in the last ulp)
+  if (threadIdx.x < 8)
+    acc[blockIdx.x * 8 + threadIdx.x] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                        red[3][threadIdx.x];
+}
+
+__global__ void reg_metrics_final(const double* __restrict__ part, int nblk, double* __restrict__ acc) {
   if (threadIdx.x < 8) {
-    const double v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(&acc[threadIdx.x], v);
+    double s = 0.0;
+    for (int b = 0; b < nblk; ++b) s += part[b * 8 + threadIdx.x];
+    acc[threadIdx.x] = s;
   }
 }
 
@@ -358,10 +367,12 @@ CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_
   return (int)hipGetLastError();
 }
 
-CDNA_API int cdna_reg_metrics(const double* y, const double* p, const double* w, int64_t n, double* acc,
-                              hipStream_t st) {
+CDNA_API int cdna_reg_metrics(const double* y, const double* p, const double* w, int64_t n, double* part,
+                              double* acc, hipStream_t st) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(reg_metrics_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, y, p, w, n, acc);
+  const unsigned nblk = grid_for(n, 256, 1024);  // part: >= 8 * 1024 doubles of workspace
+  hipLaunchKernelGGL(reg_metrics_kernel, dim3(nblk), dim3(256), 0, st, y, p, w, n, part);
+  hipLaunchKernelGGL(reg_metrics_final, dim3(1), dim3(64), 0, st, part, (int)nblk, acc);
   return (int)hipGetLastError();
 }
 

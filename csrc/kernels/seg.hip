@@ -452,6 +452,7 @@ __global__ __launch_bounds__(1024, 2) void seg_hist_lane8_kernel(const SegHistAr
   __shared__ __attribute__((aligned(16))) unsigned long long h[8 * PLANE];  // [8][BP][2][16]
   const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
   const int f0 = blockIdx.y * 128;
+  if (!CDNA_DCHECK(start >= 0 && len >= 0 && slot >= 0, 0x5E82u)) return;  // corrupt work item
   for (int i = threadIdx.x; i < 8 * PLANE; i += TH) h[i] = 0ull;
   __syncthreads();
   const int lane = threadIdx.x & 63, qt = lane >> 4, lq = lane & 15;
@@ -476,7 +477,8 @@ __global__ __launch_bounds__(1024, 2) void seg_hist_lane8_kernel(const SegHistAr
     uint2 x[U];
 #pragma unroll
     for (int p = 0; p < U; ++p) {
-      const uint32_t row = (uint32_t)rc[p] & 0x7FFFFFFFu;
+      uint32_t row = (uint32_t)rc[p] & 0x7FFFFFFFu;
+      if (!CDNA_DCHECK((int64_t)row < a.n, 0x5E81u)) row = 0u;  // record row outside the bins
       x[p] = *reinterpret_cast<const uint2*>(lbase + (uint64_t)row * (uint64_t)row_bytes);
     }
 #pragma unroll
@@ -1331,3 +1333,5 @@ CDNA_API int cdna_wave_scan(int* wcnt, int T, int Wv, int KB, int64_t* tot, hipS
   hipLaunchKernelGGL(wave_scan_kernel, dim3((unsigned)(T * KB)), dim3(256), 0, st, wcnt, Wv, KB, tot);
   return (int)hipGetLastError();
 }
+
+CDNA_DEBUG_EXPORT(seg)

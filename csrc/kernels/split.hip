@@ -325,3 +325,278 @@ CDNA_API int cdna_split_scan_sub(const long long* H, const uint8_t* feats, const
   hipLaunchKernelGGL(split_scan_sub_kernel, dim3((unsigned)A), dim3(kThreads), 0, st, a);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// K6 for classification (Gini / entropy on class counts) and for categorical
+// features (regression or classification), one block per node -- the torch
+// formulation these replace (cdnaml/models/tree/engine.py _best_splits) ran a
+// ~15-op chain per level (ML 06 - Decision Trees.py:79-118: StringIndexer'd
+// categoricals; Labs/ML 07L:105-141: RandomForestClassifier grid).
+//
+// Same decisions as that chain: node totals = the feature with the largest
+// weight (first on ties); numeric feature f: thresholds b < nthr[f];
+// categorical feature f (nthr[f] < 0): its bins ordered by centroid (mean label
+// for regression, P(class 1) for binary, the bin's impurity for multiclass;
+// empty bins last, stable), split positions j < (#non-empty bins) - 1, the left
+// set = the first j + 1 categories of that order (returned as a 256-bit mask);
+// argmax over the flat (feature, position) order.  All sums are exact (counts
+// and power-of-two fixed-point moments), so the split statistics match.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kExMaxK = 32;   // classes
+constexpr int kExMaxB = 256;
+
+struct SplitExArgs {
+  const double* H;       // [A][d][B][K]
+  const int* nthr;       // [d] (< 0: categorical)
+  const uint32_t* mask;  // [A][mw] or null
+  int mw;
+  int A, d, B, K;
+  int kind;              // 0 variance (K == 2), 2 gini, 3 entropy
+  double min_inst;
+  double* out;           // [A][4 + 2K]: gain, f, b, 0, left[K], right[K]
+  double* tot_out;       // [A][K]
+  uint32_t* cat_out;     // [A][8] left-category bits (categorical winners)
+};
+
+// No FMA contraction in the impurity / gain arithmetic: every product is rounded before it is added, as in the
+// torch path (engine.py _impurity_from_counts), so centroid ties and gains agree bit for bit.
+__device__ __forceinline__ double impurity_c(const double* c, int K, int kind) {
+#pragma clang fp contract(off)
+  double W = 0.0;
+  for (int i = 0; i < K; ++i) W += c[i];
+  const double Wc = W > 1e-300 ? W : 1e-300;
+  double s = 0.0;
+  if (kind == 2) {
+    for (int i = 0; i < K; ++i) {
+      const double p = c[i] / Wc;
+      s += p * p;
+    }
+    return 1.0 - s;
+  }
+  for (int i = 0; i < K; ++i) {
+    const double p = c[i] / Wc;
+    const double lp = p > 0.0 ? log2(p > 1e-300 ? p : 1e-300) : 0.0;
+    s += p * lp;
+  }
+  return -s;
+}
+
+// gain of a (left, right) partition; *ok = both sides carry enough weight
+__device__ __forceinline__ double gain_ex(const SplitExArgs& a, const double* l, const double* t, double imp_t,
+                                          bool* ok) {
+#pragma clang fp contract(off)
+  double r[kExMaxK];
+  for (int i = 0; i < a.K; ++i) r[i] = t[i] - l[i];
+  const double lo = a.min_inst > 1e-12 ? a.min_inst : 1e-12;
+  if (a.kind == 0) {
+    *ok = l[0] >= lo && r[0] >= lo;
+    const double wl = l[0] > 1e-300 ? l[0] : 1e-300, wr = r[0] > 1e-300 ? r[0] : 1e-300;
+    const double wt = t[0] > 1e-300 ? t[0] : 1e-300;
+    return (l[1] * l[1] / wl + r[1] * r[1] / wr - t[1] * t[1] / wt) / wt;
+  }
+  double WL = 0.0, WR = 0.0, Wt = 0.0;
+  for (int i = 0; i < a.K; ++i) {
+    WL += l[i];
+    WR += r[i];
+    Wt += t[i];
+  }
+  *ok = WL >= lo && WR >= lo;
+  return imp_t - WL / Wt * impurity_c(l, a.K, a.kind) - WR / Wt * impurity_c(r, a.K, a.kind);
+}
+
+__device__ __forceinline__ bool better(double g, int k, double bg, int bk) {
+  return g > bg || (g == bg && k < bk);
+}
+
+__global__ __launch_bounds__(128) void split_scan_ex_kernel(const SplitExArgs a) {
+  constexpr int TH = 128;
+  __shared__ double s_w[TH];
+  __shared__ int s_f[TH];
+  __shared__ double s_t[kExMaxK];
+  __shared__ double s_g[TH];
+  __shared__ int s_k[TH];
+  __shared__ double s_cent[kExMaxB];
+  __shared__ int s_ord[kExMaxB];
+  __shared__ double s_bg;
+  __shared__ int s_bk;
+  const int node = blockIdx.x;
+  const int K = a.K, B = a.B;
+  const double* Hn = a.H + (int64_t)node * a.d * B * K;
+  // ---- node totals: the first feature with the largest weight
+  double bw = -1.0;
+  int bf = 0x7FFFFFFF;
+  for (int f = threadIdx.x; f < a.d; f += TH) {
+    const double* hf = Hn + (int64_t)f * B * K;
+    double w = 0.0;
+    if (a.kind == 0) {
+      for (int b = 0; b < B; ++b) w += hf[b * K];
+    } else {
+      for (int b = 0; b < B; ++b) {
+        double wb = 0.0;
+        for (int i = 0; i < K; ++i) wb += hf[b * K + i];
+        w += wb;
+      }
+    }
+    if (w > bw) {
+      bw = w;
+      bf = f;
+    }
+  }
+  s_w[threadIdx.x] = bw;
+  s_f[threadIdx.x] = bf;
+  __syncthreads();
+  for (int o = TH / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const int j = threadIdx.x + o;
+      if (s_w[j] > s_w[threadIdx.x] || (s_w[j] == s_w[threadIdx.x] && s_f[j] < s_f[threadIdx.x])) {
+        s_w[threadIdx.x] = s_w[j];
+        s_f[threadIdx.x] = s_f[j];
+      }
+    }
+    __syncthreads();
+  }
+  const int tf = s_f[0];
+  if (threadIdx.x < K) {
+    double v = 0.0;
+    const double* hf = Hn + (int64_t)tf * B * K;
+    for (int b = 0; b < B; ++b) v += hf[b * K + threadIdx.x];
+    s_t[threadIdx.x] = v;
+  }
+  __syncthreads();
+  double t[kExMaxK];
+  for (int i = 0; i < K; ++i) t[i] = s_t[i];
+  const double imp_t = a.kind == 0 ? 0.0 : impurity_c(t, K, a.kind);
+  auto in_mask = [&](int f) {
+    return !a.mask || ((a.mask[(int64_t)node * a.mw + (f >> 5)] >> (f & 31)) & 1u) != 0u;
+  };
+  // ---- numeric features: a thread per feature
+  double best = -__builtin_inf();
+  int bk = 0x7FFFFFFF;
+  for (int f = threadIdx.x; f < a.d; f += TH) {
+    if (a.nthr[f] < 0 || !in_mask(f)) continue;
+    const int lim = a.nthr[f];
+    const double* hf = Hn + (int64_t)f * B * K;
+    double l[kExMaxK];
+    for (int i = 0; i < K; ++i) l[i] = 0.0;
+    for (int b = 0; b < B && b < lim; ++b) {
+      for (int i = 0; i < K; ++i) l[i] += hf[b * K + i];
+      bool ok;
+      const double g = gain_ex(a, l, t, imp_t, &ok);
+      if (ok && g == g && g != __builtin_inf() && g != -__builtin_inf() && g > best) {
+        best = g;
+        bk = f * B + b;
+      }
+    }
+  }
+  s_g[threadIdx.x] = best;
+  s_k[threadIdx.x] = bk;
+  __syncthreads();
+  for (int o = TH / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o && better(s_g[threadIdx.x + o], s_k[threadIdx.x + o], s_g[threadIdx.x], s_k[threadIdx.x])) {
+      s_g[threadIdx.x] = s_g[threadIdx.x + o];
+      s_k[threadIdx.x] = s_k[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    s_bg = s_g[0];
+    s_bk = s_k[0];
+  }
+  __syncthreads();
+  // ---- categorical features: the block orders one feature's bins by centroid, then thread 0 scans them
+  auto order_bins = [&](int f) {
+    const double* hf = Hn + (int64_t)f * B * K;
+    for (int b = threadIdx.x; b < B; b += TH) {
+      double c = __builtin_inf(), W = 0.0;
+      if (a.kind == 0) {
+        W = hf[b * K];
+        c = hf[b * K + 1] / (W > 1e-300 ? W : 1e-300);
+      } else {
+        for (int i = 0; i < K; ++i) W += hf[b * K + i];
+        c = K == 2 ? hf[b * K + 1] / (W > 1e-300 ? W : 1e-300) : impurity_c(hf + b * K, K, a.kind);
+      }
+      s_cent[b] = W > 0.0 ? c : __builtin_inf();
+    }
+    __syncthreads();
+    // stable rank sort: position of bin b = #{c < cent[b]} + #{c == cent[b], index < b}
+    for (int b = threadIdx.x; b < B; b += TH) {
+      const double cb = s_cent[b];
+      int r = 0;
+      for (int j = 0; j < B; ++j) {
+        const double cj = s_cent[j];
+        r += (cj < cb || (cj == cb && j < b)) ? 1 : 0;
+      }
+      s_ord[r] = b;
+    }
+    __syncthreads();
+  };
+  for (int f = 0; f < a.d; ++f) {
+    if (a.nthr[f] >= 0 || !in_mask(f)) continue;  // block-uniform
+    order_bins(f);
+    if (threadIdx.x == 0) {
+      const double* hf = Hn + (int64_t)f * B * K;
+      int ncnt = 0;
+      for (int b = 0; b < B; ++b) ncnt += s_cent[b] != __builtin_inf() ? 1 : 0;
+      double l[kExMaxK];
+      for (int i = 0; i < K; ++i) l[i] = 0.0;
+      for (int j = 0; j < B && j < ncnt - 1; ++j) {
+        const int b = s_ord[j];
+        for (int i = 0; i < K; ++i) l[i] += hf[b * K + i];
+        bool ok;
+        const double g = gain_ex(a, l, t, imp_t, &ok);
+        const int key = f * B + j;
+        if (ok && g == g && g != __builtin_inf() && g != -__builtin_inf() && better(g, key, s_bg, s_bk)) {
+          s_bg = g;
+          s_bk = key;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- the winner's statistics (and category set)
+  const int k0 = s_bk;
+  const bool found = k0 != 0x7FFFFFFF;
+  const int f = found ? k0 / B : 0, pos = found ? k0 - f * B : 0;
+  const bool cat = found && a.nthr[f] < 0;
+  if (cat) order_bins(f);
+  if (threadIdx.x == 0) {
+    double* o = a.out + (int64_t)node * (4 + 2 * K);
+    double l[kExMaxK];
+    for (int i = 0; i < K; ++i) l[i] = 0.0;
+    uint32_t bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (found) {
+      const double* hf = Hn + (int64_t)f * B * K;
+      for (int j = 0; j <= pos; ++j) {
+        const int b = cat ? s_ord[j] : j;
+        for (int i = 0; i < K; ++i) l[i] += hf[b * K + i];
+        if (cat) bits[b >> 5] |= 1u << (b & 31);
+      }
+    }
+    o[0] = found ? s_bg : -__builtin_inf();
+    o[1] = f;
+    o[2] = pos;
+    o[3] = 0.0;
+    for (int i = 0; i < K; ++i) {
+      o[4 + i] = l[i];
+      o[4 + K + i] = t[i] - l[i];
+      a.tot_out[(int64_t)node * K + i] = t[i];
+    }
+    for (int w = 0; w < 8; ++w) a.cat_out[(int64_t)node * 8 + w] = bits[w];
+  }
+}
+}  // namespace
+
+// kind: 0 variance (K = 2), 2 gini, 3 entropy.  out [A][4 + 2K], tot_out [A][K], cat_out [A][8].
+CDNA_API int cdna_split_scan_ex(const double* H, const int* nthr, const uint32_t* mask, int mw, int A, int d, int B,
+                                int K, int kind, double min_inst, double* out, double* tot_out, uint32_t* cat_out,
+                                hipStream_t st) {
+  if (A <= 0) return 0;
+  if (d <= 0 || B <= 0 || B > kExMaxB || K < 1 || K > kExMaxK || (kind == 0 && K != 2) ||
+      (kind != 0 && kind != 2 && kind != 3))
+    return (int)hipErrorInvalidValue;
+  if ((int64_t)d * B >= 0x7FFFFFFF) return (int)hipErrorInvalidValue;
+  SplitExArgs a{H, nthr, mask, mw, A, d, B, K, kind, min_inst, out, tot_out, cat_out};
+  hipLaunchKernelGGL(split_scan_ex_kernel, dim3((unsigned)A), dim3(128), 0, st, a);
+  return (int)hipGetLastError();
+}

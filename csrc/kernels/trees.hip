@@ -762,7 +762,9 @@ __global__ __launch_bounds__(256) void predict_heap_kernel(const float* __restri
           for (int u = 0; u < W; ++u) {
             const int t = tb + 4 * u;
             if (t >= T) continue;
+            if (!CDNA_DCHECK(idx[u] < S, 0x7E01u)) idx[u] = 0;  // walk left the heap
             const int2 nd = sheap[t * S + idx[u]];
+            if (nd.x >= 0 && !CDNA_DCHECK(nd.x < d, 0x7E02u)) continue;  // split feature outside the row
             if (nd.x >= 0) {
               idx[u] = 2 * idx[u] + (xr[nd.x] <= __int_as_float(nd.y) ? 1 : 2);
             } else if (nd.x < -1) {
@@ -985,3 +987,5 @@ CDNA_API int cdna_tree_predict_heap(const float* X, int64_t n, int d, int64_t ld
 
 // binize v3 (LUT-narrowed search): lut [d][C+1] uint8, lo_sc [2][d] (cell lower edge, cell scale);
 // M = search steps inside a cell = ceil(log2(largest threshold count of any cell + 1)) (<= 8).  Returns hipErrorInvalidValue when LDS does not fit.
+
+CDNA_DEBUG_EXPORT(trees)

@@ -144,6 +144,25 @@ def scenario_trees_uneven(spark):
     return _tree_digests(_tree_df(spark, uneven=0.3))
 
 
+def scenario_trees_rs(spark):
+    """Every level histogram reduce-scattered by feature (RS_MIN_BYTES = 0; RF without the chunked all-reduce
+    overlap, so its feature-subset masks are sliced too): 13 features give uneven slices and, at W = 8, ranks
+    without features.  The forests must equal the 1-rank (all-reduce-free) fits bit for bit."""
+    from cdnaml.models.tree import engine
+    engine.RS_MIN_BYTES = 0
+    engine.HIST_OVERLAP = 1
+    seen = {"rs": 0}
+    orig = engine.ForestTrainer._reduce_scatter_features
+
+    def counted(self, Hb, d):
+        seen["rs"] += 1
+        return orig(self, Hb, d)
+    engine.ForestTrainer._reduce_scatter_features = counted
+    out = _tree_digests(_tree_df(spark, d=13))
+    out["rs_levels"] = seen["rs"]
+    return out
+
+
 def scenario_cv(spark):
     from cdnaml.ml.evaluation import RegressionEvaluator
     from cdnaml.ml.regression import RandomForestRegressor
@@ -235,7 +254,7 @@ def scenario_hyperopt_captured(spark):
 
 
 SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault, "trees": scenario_trees,
-             "trees_uneven": scenario_trees_uneven, "cv": scenario_cv, "als": scenario_als,
+             "trees_uneven": scenario_trees_uneven, "trees_rs": scenario_trees_rs, "cv": scenario_cv, "als": scenario_als,
              "hyperopt": scenario_hyperopt,
              "hyperopt_captured": scenario_hyperopt_captured}
 

@@ -140,3 +140,14 @@ def test_models_identical_across_world_sizes(scenario, worlds, tmp_path):
                 assert got[key] == pytest.approx(one[key], abs=1e-6), (w, key)
         else:
             assert got == one, (w, got, one)
+
+
+def test_reduce_scatter_by_feature_forests_identical(tmp_path):
+    """Verdict r2 item 9: level histograms reduce-scattered by feature (K6 on each rank's slice, winners
+    all-gathered) give the 1-rank forests bit for bit at W = 2, 4 and 8."""
+    one = _run("trees_rs", tmp_path, 1)
+    assert one.pop("rs_levels") == 0
+    for w in (2, 4, 8):
+        got = _run("trees_rs", tmp_path, w)
+        assert got.pop("rs_levels") > 0, w
+        assert got == one, w

@@ -155,6 +155,48 @@ def test_forest_precision_heavy_tailed_label(sessions):
         r = f.roots[t]
         ours = float(gain[f.feat[r], f.bin[r]])
         assert f.feat[r] >= 0 and ours >= best * (1 - 1e-9), (t, f.feat[r], f.bin[r], ours, best)
+    # every level below the root too (levels 1-4 of the quantised path were never checked against
+    # fp64): route the rows through each tree by the bins, then every internal node's split must be the
+    # fp64-optimal split of its own rows and weights
+    feat = torch.tensor(f.feat, device=dev)
+    binv = torch.tensor(f.bin, device=dev)
+    left = torch.tensor(f.left, device=dev)
+    right = torch.tensor(f.right, device=dev)
+    checked = 0
+    for t in range(T):
+        wt = w[t].double()
+        node = torch.full((n,), f.roots[t], dtype=torch.int64, device=dev)
+        for depth in range(5):
+            nodes = torch.unique(node)
+            inner = nodes[feat[nodes] >= 0]
+            if inner.numel() == 0:
+                break
+            slot = torch.full((len(f.feat),), -1, dtype=torch.int64, device=dev)
+            slot[inner] = torch.arange(inner.numel(), device=dev)
+            rs = slot[node]
+            live = (rs >= 0) & (wt > 0)
+            rows = torch.nonzero(live).flatten()
+            S_ = inner.numel()
+            cnt = torch.zeros((S_, d, B), dtype=torch.float64, device=dev)
+            sm = torch.zeros((S_, d, B), dtype=torch.float64, device=dev)
+            idx = (rs[rows, None] * d + torch.arange(d, device=dev)[None, :]) * B + bm[rows]
+            cnt.view(-1).index_add_(0, idx.reshape(-1), wt[rows, None].expand(-1, d).reshape(-1))
+            sm.view(-1).index_add_(0, idx.reshape(-1), (wt * yd)[rows, None].expand(-1, d).reshape(-1))
+            cl, sl = cnt.cumsum(2)[:, :, :-1], sm.cumsum(2)[:, :, :-1]
+            N, S = cnt.sum(2, keepdim=True), sm.sum(2, keepdim=True)
+            cr, sr = N - cl, S - sl
+            ok = (cl > 0) & (cr > 0)
+            gain = torch.where(ok, sl * sl / cl.clamp(min=1) + sr * sr / cr.clamp(min=1) - S * S / N,
+                               torch.full_like(cl, -float("inf")))
+            best = gain.reshape(S_, -1).max(1).values
+            ours = gain[torch.arange(S_, device=dev), feat[inner], binv[inner]]
+            bad = ours < best - 1e-9 * best.abs()
+            assert not bool(bad.any()), (t, depth, inner[bad][:4].tolist(), ours[bad][:4].tolist(),
+                                         best[bad][:4].tolist())
+            checked += S_
+            go_left = bm.gather(1, feat[node].clamp(min=0)[:, None])[:, 0] <= binv[node]
+            node = torch.where(feat[node] >= 0, torch.where(go_left, left[node], right[node]), node)
+    assert checked >= T * 15  # the five levels of every tree were checked
     # quality vs sklearn on a subsample (matched depth, trees, feature fraction 1/3)
     from cdnaml.ml.evaluation import RegressionEvaluator
     from cdnaml.ml.feature import VectorAssembler  # noqa: F401  (API parity import)

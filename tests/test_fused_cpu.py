@@ -1,6 +1,7 @@
 """K18 expression compiler (CPU side): which trees become one fused kernel and which stay on the operator path
 (the kernel itself is checked against the operator path in tests/test_kernels_gpu.py)."""
 import numpy as np
+import pytest
 import pandas as pd
 
 
@@ -104,3 +105,15 @@ def test_fused_long_inputs_above_2p53(spark):
     # end to end: the operator path keeps odd ids exact
     out = df.select(F.when(x_ > 0, i_).otherwise(-1).alias("v")).toPandas().v.to_numpy()
     np.testing.assert_array_equal(out, np.where(pdf.x > 0, ids, -1))
+
+
+@pytest.fixture
+def spark(tmp_path):
+    """Host-reference tests of the expression compiler: a CPU session only (the kernel itself runs in
+    tests/test_kernels_gpu.py)."""
+    import cdnaml
+    from tests.conftest import session_device
+    with session_device("cpu"):
+        s = cdnaml.SparkSession.builder.config("cdnaml.warehouse.dir", str(tmp_path / "warehouse")).getOrCreate()
+        yield s
+        s.stop()

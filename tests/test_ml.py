@@ -111,7 +111,9 @@ def test_rformula(spark):
     rf = RFormula(formula="price ~ .", featuresCol="features", labelCol="label", handleInvalid="skip")
     out = rf.fit(df).transform(df)
     m = LinearRegression().fit(out)
-    assert RegressionEvaluator().evaluate(m.transform(out)) < 1e-6
+    # an exact linear law: fp64 feature vectors on the host; on the GPU features are fp32 vectors (7 digits)
+    tol = 1e-6 if spark.device.type == "cpu" else 2e-5
+    assert RegressionEvaluator().evaluate(m.transform(out)) < tol
     out2 = RFormula(formula="log_price ~ . - price").fit(df.withColumn("log_price", F.log(F.abs("price") + 1)))
     assert out2 is not None
 

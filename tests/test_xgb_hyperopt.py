@@ -162,6 +162,43 @@ def test_hyperopt_over_distributed_mllib(spark):
     assert 2 <= best["max_depth"] <= 5 and 10 <= best["num_trees"] <= 30
 
 
+def test_fmin_trials_share_binned_data_only_inside_the_search(spark):
+    """Verdict r2 item 6: fmin's trials reuse one binning of the training features (tuner-scoped cache keyed by
+    the features' content, so the per-trial StringIndexer / VectorAssembler refit still hits); the losses equal
+    fits outside fmin bit for bit, and after fmin returns a fit bins its data again (no global cache)."""
+    from cdnaml.models.tree import bincache
+    rng = np.random.default_rng(5)
+    n = 2000
+    X = rng.normal(size=(n, 3))
+    pdf = pd.DataFrame(X, columns=list("abc"))
+    pdf["room"] = rng.choice(["entire", "private", "shared"], n)
+    pdf["price"] = np.sin(2 * X[:, 0]) * 3 + X[:, 1] + (pdf["room"] == "entire") * 2.0
+    df = spark.createDataFrame(pdf)
+    train, val = df.randomSplit([0.8, 0.2], seed=42)
+    si = StringIndexer(inputCols=["room"], outputCols=["roomIdx"], handleInvalid="skip")
+    va = VectorAssembler(inputCols=["roomIdx", "a", "b", "c"], outputCol="features")
+    rf = RandomForestRegressor(labelCol="price", maxBins=40, seed=42)
+    pipeline = Pipeline(stages=[si, va, rf])
+    ev = RegressionEvaluator(labelCol="price")
+    seen = []
+
+    def objective(params):
+        seen.append((int(params["max_depth"]), int(params["num_trees"])))
+        est = pipeline.copy({rf.maxDepth: seen[-1][0], rf.numTrees: seen[-1][1]})
+        return ev.evaluate(est.fit(train).transform(val))
+
+    space = {"max_depth": hp.quniform("max_depth", 2, 5, 1), "num_trees": hp.quniform("num_trees", 10, 30, 1)}
+    b0, h0 = bincache.stats["builds"], bincache.stats["hits"]
+    trials = Trials()
+    fmin(objective, space, algo=tpe.suggest, max_evals=4, trials=trials, rstate=np.random.default_rng(1))
+    assert bincache.stats["builds"] - b0 == 1 and bincache.stats["hits"] - h0 == 3
+    assert not bincache.active()
+    for (dpt, nt), loss in zip(seen, trials.losses()):
+        est = pipeline.copy({rf.maxDepth: dpt, rf.numTrees: nt})
+        assert ev.evaluate(est.fit(train).transform(val)) == loss
+    assert bincache.stats["builds"] - b0 == 1 + len(seen)
+
+
 class _Crash(Exception):
     pass
 
