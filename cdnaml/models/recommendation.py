@@ -230,10 +230,11 @@ class ALS(Estimator):
         W = comm.world_size
         order = torch.argsort(owner, stable=True)
         counts = torch.bincount(owner, minlength=W).tolist()
+        recv = comm.all_to_all_counts(counts)  # one count exchange for all columns
         out = []
         for c in cols:
             parts = list(torch.split(c[order], counts))
-            out.append(torch.cat(comm.all_to_all_v(parts)))
+            out.append(torch.cat(comm.all_to_all_v(parts, recv)))
         return out
 
     @staticmethod
@@ -275,12 +276,15 @@ class ALS(Estimator):
         csr_u = self._csr(dst_u, my_u.numel()) if native else None
         csr_i = self._csr(dst_i, my_i.numel()) if native else None
         local = _LocalComm()
+        # every iteration's factor replies follow the same routing: rank q sends what this rank asked it for
+        recv_i = torch.bincount(need_i_sorted % W, minlength=W).tolist()
+        recv_u = torch.bincount(need_u_sorted % W, minlength=W).tolist()
         for _ in range(self.getMaxIter()):
-            Vneed = torch.cat(comm.all_to_all_v([V[s // W] for s in send_i]))
+            Vneed = torch.cat(comm.all_to_all_v([V[s // W] for s in send_i], recv_i))
             gV = comm.all_reduce(V.T @ V) if implicit else None   # implicit Y^T Y spans every rank's items
             U = self._half_step(local, src_in_u, dst_u, bu_r, Vneed, my_u.numel(), lam, nonneg, implicit, alpha,
                                 csr_u, gV)
-            Uneed = torch.cat(comm.all_to_all_v([U[s // W] for s in send_u]))
+            Uneed = torch.cat(comm.all_to_all_v([U[s // W] for s in send_u], recv_u))
             gU = comm.all_reduce(U.T @ U) if implicit else None
             V = self._half_step(local, src_in_i, dst_i, bi_r, Uneed, my_i.numel(), lam, nonneg, implicit, alpha,
                                 csr_i, gU)

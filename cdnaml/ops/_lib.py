@@ -157,13 +157,19 @@ _SIGS = {
                           c_void_p], c_int),
     "cdna_pack_keys": ([c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "cdna_hp_hist": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p], c_int),
-    "cdna_hp_scatter": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_hp_part": ([c_int, c_int64, c_int, c_int, c_int64, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                      c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                      c_void_p], c_int),
     "cdna_hp_agg_lds_bytes": ([c_int, c_int], c_int),
     "cdna_hp_agg_lds_budget": ([], c_int),
     "cdna_hp_agg": ([c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                      c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p], c_int),
+    "cdna_la_groups": ([c_void_p, c_int64, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                        c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_bucket_compact": ([c_int, c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_gather": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_join_build": ([c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],
                         c_int),
     "cdna_join_probe": ([c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,

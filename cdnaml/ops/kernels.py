@@ -1754,6 +1754,51 @@ def compact_mask(mask: torch.Tensor) -> torch.Tensor:
     return idx
 
 
+GATHER_MIN = int(__import__("os").environ.get("CDNAML_GATHER_MIN", "65536"))
+
+
+def gather_cols(tensors, idx: torch.Tensor):
+    """K19 gather: [t[idx] for t in tensors] for 1-D contiguous device tensors of 1/2/4/8-byte elements, up to 8 per
+    launch (relational.hip gather_kernel); entries that do not qualify come back as None."""
+    import ctypes
+    out = [None] * len(tensors)
+    ok = [i for i, t in enumerate(tensors) if t is not None and t.is_cuda and t.dim() == 1 and t.is_contiguous()
+          and t.element_size() in (1, 2, 4, 8)]
+    m = idx.numel()
+    ix = idx.to(torch.int64).contiguous()
+    for c0 in range(0, len(ok), 8):
+        grp = ok[c0:c0 + 8]
+        src = [tensors[i] for i in grp]
+        dst = [torch.empty(m, dtype=t.dtype, device=t.device) for t in src]
+        eb = (ctypes.c_int * len(grp))(*[t.element_size() for t in src])
+        _lib.check(_lib.lib().cdna_gather(_ptr(ix), m, len(grp), _ptr_array(src), _ptr_array(dst), eb,
+                                          _stream(ix.device)), "cdna_gather")
+        for i, d in zip(grp, dst):
+            out[i] = d
+    return out
+
+
+def bucket_compact(keep: torch.Tensor, nb: int):
+    """Rows with keep = 1 + bucket (uint8, 0 = dropped) grouped by bucket, in row order within a bucket:
+    (idx int64, counts per bucket int64 on the device)."""
+    n = keep.numel()
+    dev = keep.device
+    L = _lib.lib()
+    rpb = max(4096, -(-n // 1024))
+    nblk = -(-n // rpb)
+    counts = torch.empty((nb, nblk), dtype=torch.int32, device=dev)
+    _lib.check(L.cdna_bucket_compact(1, _ptr(keep), n, nb, rpb, _ptr(counts), None, None, _stream(dev)),
+               "cdna_bucket_compact(count)")
+    flat = counts.view(-1).long()
+    csum = torch.cumsum(flat, 0)
+    total = int(csum[-1].item())
+    idx = torch.empty(total, dtype=torch.int64, device=dev)
+    if total:
+        _lib.check(L.cdna_bucket_compact(2, _ptr(keep), n, nb, rpb, None, _ptr((csum - flat).contiguous()), _ptr(idx),
+                                         _stream(dev)), "cdna_bucket_compact(scatter)")
+    return idx, counts.long().sum(1)
+
+
 # ------------------------------------------------------------------- K16 / K17
 _EMPTY64 = -(1 << 63)
 
@@ -1901,6 +1946,14 @@ def pack_keys(cols, n: int, dev) -> torch.Tensor:
     return out
 
 
+def _excl_scan_n(c: torch.Tensor, n: int) -> torch.Tensor:
+    """Exclusive int64 prefix sums of c followed by the total n."""
+    out = torch.empty(c.numel() + 1, dtype=torch.int64, device=c.device)
+    torch.cumsum(c, 0, out=out[1:])
+    out[0] = 0
+    return out
+
+
 def _hp_shape(n: int, na: int):
     L = _lib.lib()
     S = min(65535, L.cdna_hp_agg_lds_budget() // (16 + 8 * na) - 1)
@@ -1928,6 +1981,10 @@ def hash_groups(key: torch.Tensor, values=(), accs=(), mode: int = 0, pout: int 
     st = _stream(dev)
     na = len(accs)
     assert na <= HP_MAX_ACC and len(values) <= HP_MAX_ACC and n < (1 << 31)
+    if LOCAL_FIRST:
+        r = _la_groups(key, values, accs, mode, pout)
+        if r is not None:
+            return r
     S, cap, pbits = _hp_shape(n, na)
     P = 1 << pbits
     rpb = max(4096, -(-n // 512))
@@ -1935,18 +1992,33 @@ def hash_groups(key: torch.Tensor, values=(), accs=(), mode: int = 0, pout: int 
     key = key.contiguous()
     counts = torch.empty((P, nblk), dtype=torch.int32, device=dev)
     _lib.check(L.cdna_hp_hist(_ptr(key), n, pbits, rpb, _ptr(counts), st), "cdna_hp_hist")
-    flat = counts.view(-1).long()
-    offs = (torch.cumsum(flat, 0) - flat).contiguous()
-    kout = torch.empty(n, dtype=torch.int64, device=dev)
-    rout = torch.empty(n, dtype=torch.int32, device=dev)
+    offs = _excl_scan_n(counts.view(-1), n)
     nv = len(values)
-    vout = torch.empty((max(nv, 1), n), dtype=torch.int64, device=dev) if nv else None
     vals = [v.contiguous() if v.dtype != torch.bool else v.contiguous().view(torch.uint8) for v, _ in values]
     vvalid = [None if m is None else m.contiguous().view(torch.uint8) for _, m in values]
     import ctypes
     vdt = (ctypes.c_int * max(1, nv))(*[_VAL_DT[v.dtype] for v in vals])
-    _lib.check(L.cdna_hp_scatter(_ptr(key), n, pbits, rpb, _ptr(offs), nv, _ptr_array(vals), _ptr_array(vvalid),
-                                 vdt, _ptr(kout), _ptr(rout), _ptr(vout), st), "cdna_hp_scatter")
+
+    def bufs():
+        return (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+                torch.empty((nv, n), dtype=torch.int64, device=dev) if nv else None)
+    kout, rout, vout = bufs()
+    if pbits <= 7:
+        _lib.check(L.cdna_hp_part(0, n, P, 64 - pbits, rpb, nblk, 1, 1, 1, _ptr(offs), None, _ptr(key), nv,
+                                  _ptr_array(vals), _ptr_array(vvalid), vdt, None, None, None, _ptr(kout), _ptr(rout),
+                                  _ptr(vout), st), "cdna_hp_part")
+    else:
+        hi = pbits - 7
+        offs_a = _excl_scan_n(counts.view(1 << hi, 128, nblk).sum(1, dtype=torch.int64).view(-1), n)
+        k1, r1, v1 = bufs()
+        _lib.check(L.cdna_hp_part(0, n, 1 << hi, 64 - hi, rpb, nblk, 1, 1, 1, _ptr(offs_a), None, _ptr(key), nv,
+                                  _ptr_array(vals), _ptr_array(vvalid), vdt, None, None, None, _ptr(k1), _ptr(r1),
+                                  _ptr(v1), st), "cdna_hp_part(0)")
+        gs = 16
+        _lib.check(L.cdna_hp_part(1, n, 128, 64 - pbits, rpb, nblk, gs, -(-nblk // gs), 1 << hi, _ptr(offs),
+                                  _ptr(offs_a), None, nv, None, None, None, _ptr(k1), _ptr(r1), _ptr(v1), _ptr(kout),
+                                  _ptr(rout), _ptr(vout), st), "cdna_hp_part(1)")
+        del k1, r1, v1
     ops = (ctypes.c_int * max(1, na))(*[HP_OPS[o] for o, _ in accs])
     vcols = (ctypes.c_int * max(1, na))(*[int(j) for _, j in accs])
     ngroups = torch.empty(P, dtype=torch.int32, device=dev)
@@ -1971,9 +2043,60 @@ def hash_groups(key: torch.Tensor, values=(), accs=(), mode: int = 0, pout: int 
     ovf, G = torch.stack([(ng < 0).any().long(), csum[-1]]).cpu().tolist()
     if ovf:
         return None
-    starts = offs.view(P, nblk)[:, 0]
+    starts = offs[:-1].view(P, nblk)[:, 0]
     pos = torch.repeat_interleave(starts - (csum - ng), ng, output_size=G) + torch.arange(G, device=dev)
     return {"G": G, "pos": pos, "key": gkey, "cnt": gcnt, "first": gfirst, "acc": gacc, "gpos": gpos}
+
+
+# try the low-cardinality path (per-block LDS tables over row chunks + one merge) before partitioning
+LOCAL_FIRST = __import__("os").environ.get("CDNAML_HASH_LOCAL", "1") != "0"
+
+
+def _la_groups(key: torch.Tensor, values, accs, mode: int, pout: int):
+    """hashagg.hip la_agg + la_merge: the same results as the partitioned path (dense group arrays, pos =
+    0..G-1) when every row chunk and the merged table hold at most one table of distinct keys; else None."""
+    import ctypes
+    n = key.numel()
+    dev = key.device
+    L = _lib.lib()
+    na, nv = len(accs), len(values)
+    S, cap, _ = _hp_shape(n, na)
+    nblk = max(1, min(1024, n // 16384))
+    rpb = -(-n // nblk)
+    nblk = -(-n // rpb)
+    pcap = nblk * (cap + 2)
+    pkey = torch.empty(pcap, dtype=torch.int64, device=dev)
+    pcnt = torch.empty(pcap, dtype=torch.int32, device=dev)
+    pfirst = torch.empty(pcap, dtype=torch.int32, device=dev)
+    pacc = torch.empty((max(na, 1), pcap), dtype=torch.int64, device=dev)
+    ctr = torch.zeros(2, dtype=torch.int32, device=dev)
+    gkey = torch.empty(S + 1, dtype=torch.int64, device=dev)
+    gcnt = torch.empty(S + 1, dtype=torch.int32, device=dev)
+    gfirst = torch.empty(S + 1, dtype=torch.int32, device=dev)
+    gacc = torch.empty((max(na, 1), S + 1), dtype=torch.int64, device=dev)
+    ng = torch.empty(1, dtype=torch.int32, device=dev)
+    keep = torch.zeros(n, dtype=torch.uint8, device=dev) if mode == 1 else None
+    vals = [v.contiguous() if v.dtype != torch.bool else v.contiguous().view(torch.uint8) for v, _ in values]
+    vvalid = [None if m is None else m.contiguous().view(torch.uint8) for _, m in values]
+    vdt = (ctypes.c_int * max(1, nv))(*[_VAL_DT[v.dtype] for v in vals])
+    ops = (ctypes.c_int * max(1, na))(*[HP_OPS[o] for o, _ in accs])
+    vcols = (ctypes.c_int * max(1, na))(*[int(j) for _, j in accs])
+    _lib.check(L.cdna_la_groups(_ptr(key.contiguous()), n, rpb, S, cap, na, ops, vcols, nv, _ptr_array(vals),
+                                _ptr_array(vvalid), vdt, 1 if mode == 1 else 0, int(pout), _ptr(pkey), _ptr(pcnt),
+                                _ptr(pfirst), _ptr(pacc), pcap, _ptr(ctr[0:1]), _ptr(ctr[1:2]), _ptr(gkey),
+                                _ptr(gcnt), _ptr(gfirst), _ptr(gacc), _ptr(ng), _ptr(keep), _stream(dev)),
+               "cdna_la_groups")
+    G = int(ng.item())
+    if G < 0:
+        return None
+    if mode == 1:
+        return keep
+    gpos = None
+    if mode == 2:
+        ri, _, _ = join_probe(key, None, join_table(gkey[:G], None))
+        gpos = ri.to(torch.int32)
+    return {"G": G, "pos": torch.arange(G, device=dev), "key": gkey, "cnt": gcnt, "first": gfirst, "acc": gacc,
+            "gpos": gpos}
 
 
 def ordered_to_double(u: torch.Tensor) -> torch.Tensor:

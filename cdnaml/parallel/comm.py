@@ -274,11 +274,28 @@ class Comm:
         return t
 
     # ------------------------------------------------------------ all-to-all
-    def all_to_all_v(self, chunks: List[torch.Tensor]) -> List[torch.Tensor]:
+    def all_to_all_counts(self, send_counts: Sequence[int]) -> List[int]:
+        """Rows each rank will send here, given the rows this rank sends to each (one tiny all-to-all; the only
+        host round trip of a shuffle -- pass its result to every all_to_all_v with the same routing)."""
+        if not self.distributed:
+            return [int(send_counts[0])]
+        W = self.world_size
+        send_n = torch.tensor([int(c) for c in send_counts], dtype=torch.int64)
+        recv_n = torch.empty(W, dtype=torch.int64)
+        s_w, r_w = self._dev_tensor(send_n), self._dev_tensor(recv_n)
+        with self._guard("all_to_all"):
+            dist.all_to_all_single(r_w, s_w)
+        self.calls += 1
+        return [int(x) for x in r_w.cpu().tolist()]
+
+    def all_to_all_v(self, chunks: List[torch.Tensor], recv_counts: Optional[Sequence[int]] = None
+                     ) -> List[torch.Tensor]:
         """chunks[j] goes to rank j; returns the list received from every rank.
 
-        Counts are exchanged first (one tiny all-to-all), then the payload in a
-        single all_to_all_single over xGMI (every link carries its own pair).
+        Without ``recv_counts`` the counts are exchanged first (one tiny all-to-all and a host read), then the
+        payload in a single all_to_all_single over xGMI (every link carries its own pair).  Exchanges whose
+        routing is known (the block-ALS factor replies of every iteration, the columns of one shuffle) pass the
+        counts and skip that round trip.
         """
         if not self.distributed:
             return [chunks[0]]
@@ -289,12 +306,10 @@ class Comm:
         inner = 1
         for s in tail:
             inner *= s
-        send_n = torch.tensor([c.shape[0] for c in chunks], dtype=torch.int64)
-        recv_n = torch.empty(W, dtype=torch.int64)
-        s_w, r_w = self._dev_tensor(send_n), self._dev_tensor(recv_n)
-        with self._guard("all_to_all"):
-            dist.all_to_all_single(r_w, s_w)
-        recv_counts = [int(x) for x in r_w.cpu().tolist()]
+        if recv_counts is None:
+            recv_counts = self.all_to_all_counts([c.shape[0] for c in chunks])
+            self.calls -= 1
+        recv_counts = [int(x) for x in recv_counts]
         flat = torch.cat([c.reshape(-1) for c in chunks]) if any(c.numel() for c in chunks) else \
             torch.empty(0, dtype=ref.dtype, device=ref.device)
         dtype = flat.dtype

@@ -38,23 +38,27 @@ def exchange(comm, batch: Batch, dest: torch.Tensor) -> Batch:
     """Send row i of ``batch`` to rank ``dest[i]``; return the rows received.
 
     All columns travel together: each row's column bytes (and a validity byte for every column that has nulls
-    on any rank) are packed into one [n, R] byte matrix, so a shuffle costs one flag all-reduce, one counts
-    all-to-all and ONE payload all-to-all whatever the column count (it used to be two all-to-alls plus an
-    all-reduce per column)."""
+    on any rank) are packed into one [n, R] byte matrix, and every rank's send counts and null flags travel in
+    one small all-gather, so a shuffle is that all-gather (the only host read) plus ONE payload all-to-all
+    whatever the column count."""
     if not comm.distributed:
         return batch
     W = comm.world_size
     batch = unify_global_dictionaries(comm, batch)
     from ..ops import kernels as K
     order, counts = K.partition_dest(dest, W)  # K16 stable counting sort (HIP on the GPU)
-    counts = counts.cpu().tolist()
     sorted_b = batch.take(order)
     names = list(sorted_b.columns)
     cols = [sorted_b.columns[k] for k in names]
     n = sorted_b.n
-    flags = torch.tensor([1.0 if c.valid is not None else 0.0 for c in cols] + [0.0], device=comm.device)
-    comm.all_reduce(flags, "max")                        # one agreement for every column's validity
-    nullable = [f > 0 for f in flags.cpu().tolist()[:-1]]
+    # ONE all-gather (and one host read) carries every rank's send counts and column null flags: each rank
+    # reads its receive counts (column `rank` of the count matrix) and the max of the flags from it
+    flags = torch.tensor([1 if c.valid is not None else 0 for c in cols], dtype=torch.int64)
+    info = torch.cat([counts.to(torch.int64).to(comm.device), flags.to(comm.device)])
+    allinfo = comm.all_gather_tensor(info).cpu()
+    counts = counts.cpu().tolist() if counts.is_cuda else counts.tolist()
+    recv_counts = allinfo[:, comm.rank].tolist()
+    nullable = [bool(f) for f in allinfo[:, W:].amax(0).tolist()] if cols else []
     parts, layout = [], []
     for c, nb in zip(cols, nullable):
         v = c.values.contiguous()
@@ -67,7 +71,7 @@ def exchange(comm, batch: Batch, dest: torch.Tensor) -> Batch:
         if nb:
             parts.append(c.valid_mask().to(torch.uint8).reshape(n, 1))
     packed = torch.cat(parts, 1) if parts else torch.zeros((n, 0), dtype=torch.uint8, device=batch.device)
-    got = comm.all_to_all_v(list(torch.split(packed, counts)))
+    got = comm.all_to_all_v(list(torch.split(packed, counts)), recv_counts)
     recv = torch.cat(got) if got else packed[:0]
     m = recv.shape[0]
     out_cols, o = {}, 0

@@ -21,6 +21,11 @@ from . import types as T
 _EPOCH = _dt.date(1970, 1, 1)
 
 
+def _gather_min() -> int:
+    from ..ops import kernels as K
+    return K.GATHER_MIN
+
+
 class ColumnData:
     __slots__ = ("values", "valid", "dtype", "dictionary", "meta")
 
@@ -229,8 +234,32 @@ class Batch:
         return Batch(cols, self.n, self.device)
 
     def take(self, idx: torch.Tensor) -> "Batch":
+        if idx.dtype != torch.bool and idx.is_cuda and idx.numel() >= _gather_min():
+            return self._take_native(idx)
         return Batch({k: c.take(idx) for k, c in self.columns.items()}, int(idx.shape[0]) if idx.dtype != torch.bool
                      else int(idx.sum()), self.device)
+
+    def _take_native(self, idx: torch.Tensor) -> "Batch":
+        """Every 1-D column (values and null masks) gathered by K19 gather kernels, 8 arrays per launch."""
+        from ..ops import kernels as K
+        names = list(self.columns)
+        arrs = []
+        for k in names:
+            c = self.columns[k]
+            arrs.append(c.values)
+            arrs.append(None if c.valid is None else c.valid.view(torch.uint8) if c.valid.dtype == torch.bool
+                        else c.valid)
+        got = K.gather_cols(arrs, idx)
+        cols = {}
+        for j, k in enumerate(names):
+            c = self.columns[k]
+            v = got[2 * j] if got[2 * j] is not None else c.values[idx]
+            m = None
+            if c.valid is not None:
+                m = got[2 * j + 1]
+                m = c.valid[idx] if m is None else (m.view(torch.bool) if c.valid.dtype == torch.bool else m)
+            cols[k] = ColumnData(v, c.dtype, m, c.dictionary, c.meta)
+        return Batch(cols, int(idx.shape[0]), self.device)
 
     def filter(self, mask: torch.Tensor) -> "Batch":
         from ..ops import kernels as K

@@ -699,11 +699,7 @@ def dedup_partitions(batch: Batch, keys: List[str], nparts: int) -> Optional[Lis
     keep = K.hash_groups(words, mode=1, pout=nparts)
     if keep is None:
         return None
-    idx = K.compact_mask(keep)
-    if nparts == 1:
-        return [batch.take(idx)]
-    pid = keep[idx].to(torch.int32) - 1
-    perm, counts = K.partition_dest(pid, nparts)
-    b = batch.take(idx[perm])
+    idx, counts = K.bucket_compact(keep, nparts)
+    b = batch.take(idx)
     bounds = [0] + torch.cumsum(counts, 0).cpu().tolist()
     return [b.slice(bounds[i], bounds[i + 1]) for i in range(nparts)]

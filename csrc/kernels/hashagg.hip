@@ -7,7 +7,7 @@
 // pack_keys_kernel).  Aggregation and dedup are radix-partitioned so that every partition's table lives in LDS:
 //
 //   hp_hist     pass 1: rows per (partition, block); partition = top bits of mix64(key)       (LDS counters)
-//   hp_scatter  pass 2: keys, row ids and value columns copied partition-contiguous            (LDS cursors)
+//   hp_part     keys, row ids and value columns radix-partitioned (1-2 passes of <= 128 buckets, LDS tile sort)
 //   hp_agg      one 1024-thread block per partition: open-addressing table in LDS holding the key, row count,
 //               first row (atomicMin) and up to four accumulators (fp64 sum, ordered-u64 min / max, non-null
 //               count, last row) per slot; then the occupied slots are written out as groups.  Dedup mode marks
@@ -89,7 +89,8 @@ __global__ __launch_bounds__(256) void pack_keys_kernel(const PackArgs a) {
   }
 }
 
-// ------------------------------------------------------------------------------------------- hp_hist / scatter
+// ------------------------------------------------------------------------------------------- hp_hist / part
+// Four keys in flight per thread (the LDS increment of one waits on nothing but its own load).
 __global__ __launch_bounds__(kHistThreads) void hp_hist_kernel(const unsigned long long* __restrict__ keys, int64_t n,
                                                                int pbits, int64_t rpb, int* __restrict__ counts) {
   extern __shared__ int s_cnt[];
@@ -98,27 +99,55 @@ __global__ __launch_bounds__(kHistThreads) void hp_hist_kernel(const unsigned lo
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = r0 + rpb < n ? r0 + rpb : n;
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += kHistThreads) atomicAdd(&s_cnt[part_of(mix64(keys[r]), pbits)], 1);
+  int64_t r = r0 + threadIdx.x;
+  for (; r + 3 * kHistThreads < r1; r += 4 * kHistThreads) {
+    unsigned long long k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = keys[r + u * kHistThreads];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) atomicAdd(&s_cnt[part_of(mix64(k[u]), pbits)], 1);
+  }
+  for (; r < r1; r += kHistThreads) atomicAdd(&s_cnt[part_of(mix64(keys[r]), pbits)], 1);
   __syncthreads();
   for (int i = threadIdx.x; i < P; i += kHistThreads) counts[(int64_t)i * gridDim.x + blockIdx.x] = s_cnt[i];
 }
 
-struct ScatterArgs {
-  const unsigned long long* keys;
+// Radix partition of (key, row, values) in one or two passes of <= 128 buckets (partition id = top pbits of the
+// key hash; pass 0 buckets by its top pbits - 7 bits when pbits > 7, pass 1 by the low 7).  A scattered 8-byte
+// store per row into 16384 partitions measured 6.9 ms per 1e8 rows (every store a partial line), so each block
+// sorts a tile of rows by bucket in LDS first and writes every bucket's run as consecutive stores; a bucket's
+// runs of successive tiles continue at the next address, so the partial lines at run ends complete in L2.
+//
+// Pass 0 block b reads rows [b * rpb, ...) of the input and writes bucket q's run at cur[q * nblk + b] onward.
+// Pass 1 block (p1, g) reads the pass-0 rows of bucket p1 that came from source blocks [g * gs, g * gs + gs) --
+// contiguous, since pass 0 stores bucket p1's rows by source block -- and writes partition (p1, p2) at
+// offs[(p1 * 128 + p2) * nblk + g * gs] onward, exactly where hp_agg expects that partition's rows.
+struct PartArgs {
+  int pass;                         // 0: from the original columns, 1: from pass-0 output
   int64_t n;
-  int pbits;
-  int64_t rpb;
-  const int64_t* offs;  // [P][nblk] exclusive scan of hp_hist's counts
-  int nv;
+  int nb;                           // buckets (power of two <= 128)
+  int shift;                        // bucket = (mix64(key) >> shift) & (nb - 1); shift 64: one bucket
+  int64_t rpb;                      // pass 0: rows per block
+  int nblk;                         // blocks of hp_hist
+  int gs, groups;                   // pass 1: source blocks per block, blocks per bucket
+  const int64_t* cur;               // pass 0: [nb][nblk] output starts; pass 1: offs [P][nblk]
+  const int64_t* src;               // pass 1: [P1][nblk] + 1 pass-0 output starts (last entry n)
+  const unsigned long long* keys;   // pass 0
   const void* val[kMaxAcc];
   const uint8_t* valid[kMaxAcc];
-  int vdtype[kMaxAcc];  // 0 f64, 1 f32, 2 i64, 3 i32, 4 u8/bool, 5 i16, 6 i8
+  int vdtype[kMaxAcc];              // 0 f64, 1 f32, 2 i64, 3 i32, 4 u8/bool, 5 i16, 6 i8
+  const unsigned long long* kin;    // pass 1
+  const uint32_t* rin;
+  const unsigned long long* vin;    // [nv][n]
+  int nv;
+  int tile;
   unsigned long long* kout;
   uint32_t* rout;
-  unsigned long long* vout;  // [nv][n] fp64 bits, kNullVal for nulls
+  unsigned long long* vout;         // [nv][n] fp64 bits, kNullVal for nulls
 };
 
-__device__ __forceinline__ unsigned long long value_bits(const ScatterArgs& a, int j, int64_t r) {
+template <class A>
+__device__ __forceinline__ unsigned long long value_bits(const A& a, int j, int64_t r) {
   if (a.valid[j] && !a.valid[j][r]) return kNullVal;
   double v;
   switch (a.vdtype[j]) {
@@ -133,20 +162,91 @@ __device__ __forceinline__ unsigned long long value_bits(const ScatterArgs& a, i
   return v != v ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(v);
 }
 
-__global__ __launch_bounds__(kHistThreads) void hp_scatter_kernel(const ScatterArgs a) {
-  extern __shared__ uint32_t s_cur[];
-  const int P = 1 << a.pbits;
-  for (int i = threadIdx.x; i < P; i += kHistThreads) s_cur[i] = (uint32_t)a.offs[(int64_t)i * gridDim.x + blockIdx.x];
-  __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * a.rpb;
-  const int64_t r1 = r0 + a.rpb < a.n ? r0 + a.rpb : a.n;
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += kHistThreads) {
-    const unsigned long long k = a.keys[r];
-    const uint32_t pos = atomicAdd(&s_cur[part_of(mix64(k), a.pbits)], 1u);
-    if (!CDNA_DCHECK(pos < (uint64_t)a.n, 0xA501)) continue;
-    a.kout[pos] = k;
-    a.rout[pos] = (uint32_t)r;
-    for (int j = 0; j < a.nv; ++j) a.vout[(int64_t)j * a.n + pos] = value_bits(a, j, r);
+constexpr int kPartThreads = 512;
+
+__global__ __launch_bounds__(kPartThreads) void hp_part_kernel(const PartArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int TILE = a.tile;
+  unsigned long long* s_key = reinterpret_cast<unsigned long long*>(smem);        // [TILE]
+  unsigned long long* s_val = s_key + TILE;                                        // [nv][TILE]
+  uint32_t* s_row = reinterpret_cast<uint32_t*>(s_val + (int64_t)a.nv * TILE);     // [TILE]
+  uint8_t* s_bk = reinterpret_cast<uint8_t*>(s_row + TILE);                        // [TILE]
+  __shared__ int s_cnt[128], s_start[128];
+  __shared__ int64_t s_cur[128];
+  int64_t r0, r1;
+  if (a.pass == 0) {
+    r0 = (int64_t)blockIdx.x * a.rpb;
+    r1 = r0 + a.rpb < a.n ? r0 + a.rpb : a.n;
+    for (int q = threadIdx.x; q < a.nb; q += kPartThreads) s_cur[q] = a.cur[(int64_t)q * a.nblk + blockIdx.x];
+  } else {
+    const int p1 = blockIdx.x / a.groups, g = blockIdx.x - p1 * a.groups;
+    const int b0 = g * a.gs, b1 = b0 + a.gs < a.nblk ? b0 + a.gs : a.nblk;
+    r0 = a.src[(int64_t)p1 * a.nblk + b0];
+    r1 = a.src[(int64_t)p1 * a.nblk + b1];
+    for (int q = threadIdx.x; q < a.nb; q += kPartThreads)
+      s_cur[q] = a.cur[((int64_t)p1 * a.nb + q) * a.nblk + b0];
+  }
+  constexpr int kPer = 8;  // rows per thread per tile (TILE <= 8 * 512)
+  for (int64_t t0 = r0; t0 < r1; t0 += TILE) {
+    const int m = (int)(r1 - t0 < TILE ? r1 - t0 : TILE);
+    for (int q = threadIdx.x; q < a.nb; q += kPartThreads) s_cnt[q] = 0;
+    __syncthreads();
+    unsigned long long k[kPer];
+    int bk[kPer], rk[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kPartThreads;
+      k[u] = 0;
+      bk[u] = -1;
+      if (i < m) k[u] = a.pass == 0 ? a.keys[t0 + i] : a.kin[t0 + i];
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kPartThreads;
+      if (i < m) {
+        bk[u] = a.shift >= 64 ? 0 : (int)((mix64(k[u]) >> a.shift) & (unsigned long long)(a.nb - 1));
+        rk[u] = atomicAdd(&s_cnt[bk[u]], 1);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of <= 128 counts by one wave (two per lane)
+      const int l = threadIdx.x;
+      const int c0 = 2 * l < a.nb ? s_cnt[2 * l] : 0, c1 = 2 * l + 1 < a.nb ? s_cnt[2 * l + 1] : 0;
+      int v = c0 + c1;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o);
+        if (l >= o) v += y;
+      }
+      const int ex = v - c0 - c1;
+      if (2 * l < a.nb) s_start[2 * l] = ex;
+      if (2 * l + 1 < a.nb) s_start[2 * l + 1] = ex + c0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kPartThreads;
+      if (i < m) {
+        const int pos = s_start[bk[u]] + rk[u];
+        const int64_t r = t0 + i;
+        s_key[pos] = k[u];
+        s_row[pos] = a.pass == 0 ? (uint32_t)r : a.rin[r];
+        s_bk[pos] = (uint8_t)bk[u];
+        for (int j = 0; j < a.nv; ++j)
+          s_val[(int64_t)j * TILE + pos] = a.pass == 0 ? value_bits(a, j, r) : a.vin[(int64_t)j * a.n + r];
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += kPartThreads) {
+      const int q = s_bk[i];
+      const int64_t dst = s_cur[q] + (i - s_start[q]);
+      if (!CDNA_DCHECK(dst >= 0 && dst < a.n, 0xA501)) continue;
+      a.kout[dst] = s_key[i];
+      a.rout[dst] = s_row[i];
+      for (int j = 0; j < a.nv; ++j) a.vout[(int64_t)j * a.n + dst] = s_val[(int64_t)j * TILE + i];
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < a.nb; q += kPartThreads) s_cur[q] += s_cnt[q];
   }
 }
 
@@ -290,6 +390,250 @@ __global__ __launch_bounds__(kAggThreads) void hp_agg_kernel(const AggArgs a) {
   }
 }
 
+// --------------------------------------------------------------------------------- low-cardinality path
+// Few distinct keys (groupBy over 50 values, a handful of categories): partitioning would put all rows of a key
+// into one partition and one block.  Instead every block aggregates a contiguous row chunk of the original
+// columns into its own LDS table (la_agg) and appends its partial groups to one list; a single block then merges
+// the partials (la_merge: counts and sums add, first rows and mins take the min, maxes and last rows the max).
+// A chunk with more distinct keys than its table holds stops early and raises the overflow flag; the host then
+// runs the partitioned path.
+__device__ __forceinline__ int lds_slot(unsigned long long* tk, int S, unsigned long long k, int cap, int* s_nd,
+                                        int* s_ovf) {
+  if (k == kEmpty) return S;
+  int pos = pos_of(mix64(k), S);
+  for (int t = 0; t < S; ++t) {
+    const unsigned long long cur = __hip_atomic_load(tk + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == k) return pos;
+    if (cur == kEmpty) {
+      const unsigned long long prev = atomicCAS(tk + pos, kEmpty, k);
+      if (prev == kEmpty) {
+        if (atomicAdd(s_nd, 1) >= cap) *s_ovf = 1;
+        return pos;
+      }
+      if (prev == k) return pos;
+    }
+    pos = pos + 1 == S ? 0 : pos + 1;
+  }
+  *s_ovf = 1;
+  return -1;
+}
+
+struct LocalArgs {
+  const unsigned long long* keys;
+  int64_t n;
+  int64_t rpb;
+  int S, cap, na;
+  int op[kMaxAcc];
+  int vcol[kMaxAcc];
+  const void* val[kMaxAcc];
+  const uint8_t* valid[kMaxAcc];
+  int vdtype[kMaxAcc];
+  int mode;                  // 0 aggregate, 1 dedup
+  int pout;
+  unsigned long long* pkey;  // partial groups [pcap]
+  uint32_t* pcnt;
+  uint32_t* pfirst;
+  unsigned long long* pacc;  // [na][pcap]
+  int64_t pcap;
+  int* total;                // partial groups appended so far
+  int* ovf;
+  unsigned long long* gkey;  // la_merge output [S + 1]
+  uint32_t* gcnt;
+  uint32_t* gfirst;
+  unsigned long long* gacc;  // [na][S + 1]
+  int* ngroups;              // la_merge: groups, -1 = overflow
+  uint8_t* keep;
+};
+
+struct LdsTable {
+  unsigned long long *tk, *ta;
+  uint32_t *tc, *tf;
+};
+
+__device__ __forceinline__ LdsTable lds_table(unsigned char* smem, int S, int na) {
+  LdsTable t;
+  t.tk = reinterpret_cast<unsigned long long*>(smem);
+  t.ta = t.tk + (S + 1);
+  t.tc = reinterpret_cast<uint32_t*>(t.ta + (int64_t)na * (S + 1));
+  t.tf = t.tc + (S + 1);
+  return t;
+}
+
+__device__ __forceinline__ void lds_table_init(const LdsTable& t, int S, int na, const int* op) {
+  for (int s = threadIdx.x; s <= S; s += kAggThreads) {
+    t.tk[s] = kEmpty;
+    t.tc[s] = 0u;
+    t.tf[s] = 0xFFFFFFFFu;
+    for (int j = 0; j < na; ++j) t.ta[(int64_t)j * (S + 1) + s] = acc_init(op[j]);
+  }
+}
+
+__global__ __launch_bounds__(kAggThreads) void la_agg_kernel(const LocalArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int S = a.S;
+  const LdsTable t = lds_table(smem, S, a.na);
+  __shared__ int s_nd, s_ovf, s_out, s_base;
+  lds_table_init(t, S, a.na, a.op);
+  if (threadIdx.x == 0) {
+    s_nd = 0;
+    s_ovf = 0;
+    s_out = 0;
+  }
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * a.rpb;
+  const int64_t r1 = r0 + a.rpb < a.n ? r0 + a.rpb : a.n;
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += kAggThreads) {
+    if (s_ovf) break;
+    const int s = lds_slot(t.tk, S, a.keys[r], a.cap, &s_nd, &s_ovf);
+    if (s < 0) break;
+    atomicMin(t.tf + s, (uint32_t)r);
+    if (a.mode == 1) continue;
+    atomicAdd(t.tc + s, 1u);
+    for (int j = 0; j < a.na; ++j) {
+      unsigned long long* slot = t.ta + (int64_t)j * (S + 1) + s;
+      const int op = a.op[j];
+      if (op == 4) {
+        atomicMax(slot, (unsigned long long)r);
+        continue;
+      }
+      const unsigned long long v = value_bits(a, a.vcol[j], r);
+      if (v == kNullVal) continue;
+      if (op == 0) atomicAdd(reinterpret_cast<double*>(slot), __longlong_as_double((long long)v));
+      else if (op == 1) atomicMin(slot, ord_of(v));
+      else if (op == 2) atomicMax(slot, ord_of(v));
+      else atomicAdd(slot, 1ull);
+    }
+  }
+  __syncthreads();
+  if (s_ovf) {
+    if (threadIdx.x == 0) atomicOr(a.ovf, 1);
+    return;
+  }
+  if (threadIdx.x == 0) s_base = atomicAdd(a.total, s_nd + (t.tf[S] != 0xFFFFFFFFu ? 1 : 0));
+  __syncthreads();
+  for (int s = threadIdx.x; s <= S; s += kAggThreads) {
+    const bool occ = s < S ? t.tk[s] != kEmpty : t.tf[s] != 0xFFFFFFFFu;
+    if (!occ) continue;
+    const int64_t o = (int64_t)s_base + atomicAdd(&s_out, 1);
+    if (!CDNA_DCHECK(o < a.pcap, 0xA502)) continue;
+    a.pkey[o] = s < S ? t.tk[s] : kEmpty;
+    a.pcnt[o] = t.tc[s];
+    a.pfirst[o] = t.tf[s];
+    for (int j = 0; j < a.na; ++j) a.pacc[(int64_t)j * a.pcap + o] = t.ta[(int64_t)j * (S + 1) + s];
+  }
+}
+
+__global__ __launch_bounds__(kAggThreads) void la_merge_kernel(const LocalArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int S = a.S;
+  const LdsTable t = lds_table(smem, S, a.na);
+  __shared__ int s_nd, s_ovf, s_out;
+  if (__hip_atomic_load(a.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    if (threadIdx.x == 0) a.ngroups[0] = -1;
+    return;
+  }
+  lds_table_init(t, S, a.na, a.op);
+  if (threadIdx.x == 0) {
+    s_nd = 0;
+    s_ovf = 0;
+    s_out = 0;
+  }
+  __syncthreads();
+  const int64_t total = *a.total;
+  for (int64_t e = threadIdx.x; e < total; e += kAggThreads) {
+    const int s = lds_slot(t.tk, S, a.pkey[e], S - 1, &s_nd, &s_ovf);
+    if (s < 0) break;
+    atomicMin(t.tf + s, a.pfirst[e]);
+    if (a.mode == 1) continue;
+    atomicAdd(t.tc + s, a.pcnt[e]);
+    for (int j = 0; j < a.na; ++j) {
+      unsigned long long* slot = t.ta + (int64_t)j * (S + 1) + s;
+      const unsigned long long v = a.pacc[(int64_t)j * a.pcap + e];
+      const int op = a.op[j];
+      if (op == 0) atomicAdd(reinterpret_cast<double*>(slot), __longlong_as_double((long long)v));
+      else if (op == 1) atomicMin(slot, v);
+      else if (op == 2 || op == 4) atomicMax(slot, v);
+      else atomicAdd(slot, v);
+    }
+  }
+  __syncthreads();
+  if (s_ovf) {
+    if (threadIdx.x == 0) a.ngroups[0] = -1;
+    return;
+  }
+  for (int s = threadIdx.x; s <= S; s += kAggThreads) {
+    const bool occ = s < S ? t.tk[s] != kEmpty : t.tf[s] != 0xFFFFFFFFu;
+    if (!occ) continue;
+    const unsigned long long k = s < S ? t.tk[s] : kEmpty;
+    const int gi = atomicAdd(&s_out, 1);
+    if (a.mode == 1) {
+      a.keep[t.tf[s]] = (uint8_t)(1 + (int)((uint32_t)(mix64(k) >> 16) % (uint32_t)a.pout));
+      continue;
+    }
+    a.gkey[gi] = k;
+    a.gcnt[gi] = t.tc[s];
+    a.gfirst[gi] = t.tf[s];
+    for (int j = 0; j < a.na; ++j) a.gacc[(int64_t)j * (S + 1) + gi] = t.ta[(int64_t)j * (S + 1) + s];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) a.ngroups[0] = s_out;
+}
+
+// ------------------------------------------------------------------------------------------ bucket_compact
+// dropDuplicates output: the rows whose keep byte is non-zero (1 + output partition), grouped by partition and
+// in row order within a partition, in two passes (counts per (bucket, block); a stable ballot-ranked scatter).
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void bucket_compact_kernel(const uint8_t* __restrict__ keep, int64_t n, int nb,
+                                                             int64_t rpb, int* __restrict__ counts,
+                                                             const int64_t* __restrict__ offs,
+                                                             int64_t* __restrict__ idx) {
+  __shared__ int s_cnt[256];
+  const int nblk = gridDim.x;
+  for (int i = threadIdx.x; i < nb; i += 256) s_cnt[i] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < n ? r0 + rpb : n;
+  if (!SCATTER) {
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+      const int b = keep[r];
+      if (b) atomicAdd(&s_cnt[b - 1], 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb; i += 256) counts[(int64_t)i * nblk + blockIdx.x] = s_cnt[i];
+    return;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t rb = r0; rb < r1; rb += 256) {
+    const int64_t r = rb + threadIdx.x;
+    const int b = r < r1 ? (int)keep[r] - 1 : -1;
+    for (int w = 0; w < 4; ++w) {  // waves take turns so earlier rows get lower positions
+      if (wid == w) {
+        bool want = b >= 0;
+        while (true) {
+          const uint64_t act = __builtin_amdgcn_ballot_w64(want);
+          if (!act) break;
+          const int leader = __builtin_ctzll(act);
+          const int lb = __shfl(b, leader);
+          const uint64_t msk = __builtin_amdgcn_ballot_w64(want && b == lb);
+          int base = 0;
+          if (lane == leader) {
+            base = s_cnt[lb];
+            s_cnt[lb] = base + __builtin_popcountll(msk);
+          }
+          base = __shfl(base, leader);
+          if (want && b == lb) {
+            const int below =
+                (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+            idx[offs[(int64_t)lb * nblk + blockIdx.x] + base + below] = r;
+            want = false;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------------- join
 __global__ __launch_bounds__(256) void join_build_kernel(const unsigned long long* __restrict__ keys,
                                                          const uint8_t* __restrict__ valid, int64_t n,
@@ -329,46 +673,78 @@ __global__ __launch_bounds__(256) void join_build_kernel(const unsigned long lon
   }
 }
 
+// Four rows per thread in flight: key loads, first table probes and the build-row loads of four rows are issued
+// back to back (one row's dependent chain at a time left the probe at 1.75 ms per 1e8 rows).
 __global__ __launch_bounds__(256) void join_probe_kernel(const unsigned long long* __restrict__ keys,
                                                          const uint8_t* __restrict__ valid, int64_t n,
                                                          const unsigned long long* __restrict__ table, int64_t mask,
                                                          const long long* __restrict__ brow,
                                                          const int* __restrict__ bcnt, long long* __restrict__ ri,
                                                          int* __restrict__ cnt, long long* __restrict__ slot) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    int64_t found = -1;
-    if (!valid || valid[i]) {
-      const unsigned long long k = keys[i];
-      if (k == kEmpty) {
-        found = bcnt[mask + 1] > 0 ? mask + 1 : -1;
-      } else {
-        int64_t h = (int64_t)(mix64(k) & (unsigned long long)mask);
-        for (int64_t t = 0; t <= mask; ++t) {
-          const unsigned long long cur = table[h];
-          if (cur == k) {
-            found = h;
-            break;
-          }
-          if (cur == kEmpty) break;
-          h = (h + 1) & mask;
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += stride * U) {
+    unsigned long long k[U], cur[U];
+    int64_t h[U], found[U];
+    bool live[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      live[u] = i < n && (!valid || valid[i]);
+      k[u] = live[u] ? keys[i] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      found[u] = -1;
+      h[u] = 0;
+      cur[u] = kEmpty;
+      if (live[u]) {
+        if (k[u] == kEmpty) {
+          found[u] = bcnt[mask + 1] > 0 ? mask + 1 : -1;
+          live[u] = false;
+        } else {
+          h[u] = (int64_t)(mix64(k[u]) & (unsigned long long)mask);
+          cur[u] = table[h[u]];
         }
       }
     }
-    ri[i] = found >= 0 ? brow[found] : -1;
-    if (cnt) cnt[i] = found >= 0 ? bcnt[found] : 0;
-    if (slot) slot[i] = found;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!live[u]) continue;
+      for (int64_t t = 0; t <= mask; ++t) {
+        if (cur[u] == k[u]) {
+          found[u] = h[u];
+          break;
+        }
+        if (cur[u] == kEmpty) break;
+        h[u] = (h[u] + 1) & mask;
+        cur[u] = table[h[u]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n) continue;
+      ri[i] = found[u] >= 0 ? brow[found[u]] : -1;
+      if (cnt) cnt[i] = found[u] >= 0 ? bcnt[found[u]] : 0;
+      if (slot) slot[i] = found[u];
+    }
   }
 }
 
-// dynamic LDS above 64 KB needs the attribute once per kernel (hp_agg's table takes up to 160 KB)
+// dynamic LDS above 64 KB needs the attribute once per kernel (the LDS tables take up to 160 KB)
 void set_lds_limit() {
   static bool done = false;
   if (done) return;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hp_hist_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                             65536);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hp_scatter_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hp_part_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            163840 - 2048);
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hp_agg_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            163840 - 64);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&la_agg_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            163840 - 64);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&la_merge_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                             163840 - 64);
   done = true;
 }
@@ -412,30 +788,44 @@ CDNA_API int cdna_hp_hist(const void* keys, int64_t n, int pbits, int64_t rpb, i
   return (int)hipGetLastError();
 }
 
-CDNA_API int cdna_hp_scatter(const void* keys, int64_t n, int pbits, int64_t rpb, const int64_t* offs, int nv,
-                             const void* const* vals, const uint8_t* const* valids, const int* vdtypes, void* kout,
-                             uint32_t* rout, void* vout, hipStream_t st) {
+// pass 0 / pass 1 (np1 pass-0 buckets x groups blocks): see PartArgs.  vals / valids / vdtypes: the value columns (pass 0 only).
+CDNA_API int cdna_hp_part(int pass, int64_t n, int nb, int shift, int64_t rpb, int nblk, int gs, int groups, int np1,
+                          const int64_t* cur, const int64_t* src, const void* keys, int nv, const void* const* vals,
+                          const uint8_t* const* valids, const int* vdtypes, const void* kin, const uint32_t* rin,
+                          const void* vin, void* kout, uint32_t* rout, void* vout, hipStream_t st) {
   if (n <= 0) return 0;
-  if (pbits < 0 || pbits > 14 || rpb <= 0 || nv < 0 || nv > kMaxAcc || n >= (1ll << 31))
+  if (nb < 1 || nb > 128 || (nb & (nb - 1)) || nv < 0 || nv > kMaxAcc || n >= (1ll << 31) || nblk <= 0 ||
+      (pass == 0 && rpb <= 0) || (pass == 1 && (gs <= 0 || groups <= 0 || np1 <= 0)))
     return (int)hipErrorInvalidValue;
-  ScatterArgs a{};
-  a.keys = reinterpret_cast<const unsigned long long*>(keys);
+  PartArgs a{};
+  a.pass = pass;
   a.n = n;
-  a.pbits = pbits;
+  a.nb = nb;
+  a.shift = shift;
   a.rpb = rpb;
-  a.offs = offs;
-  a.nv = nv;
+  a.nblk = nblk;
+  a.gs = gs;
+  a.groups = groups;
+  a.cur = cur;
+  a.src = src;
+  a.keys = reinterpret_cast<const unsigned long long*>(keys);
   for (int j = 0; j < nv; ++j) {
-    a.val[j] = vals[j];
-    a.valid[j] = valids[j];
-    a.vdtype[j] = vdtypes[j];
+    a.val[j] = pass == 0 ? vals[j] : nullptr;
+    a.valid[j] = pass == 0 ? valids[j] : nullptr;
+    a.vdtype[j] = pass == 0 ? vdtypes[j] : 0;
   }
+  a.kin = reinterpret_cast<const unsigned long long*>(kin);
+  a.rin = rin;
+  a.vin = reinterpret_cast<const unsigned long long*>(vin);
+  a.nv = nv;
+  a.tile = nv <= 1 ? 4096 : 2048;
   a.kout = reinterpret_cast<unsigned long long*>(kout);
   a.rout = rout;
   a.vout = reinterpret_cast<unsigned long long*>(vout);
-  const unsigned nblk = (unsigned)((n + rpb - 1) / rpb);
+  const size_t lds = (size_t)a.tile * (8 + 8 * nv + 4 + 1);
   set_lds_limit();
-  hipLaunchKernelGGL(hp_scatter_kernel, dim3(nblk), dim3(kHistThreads), (size_t)4 << pbits, st, a);
+  const unsigned nblocks = pass == 0 ? (unsigned)nblk : (unsigned)groups * (unsigned)np1;
+  hipLaunchKernelGGL(hp_part_kernel, dim3(nblocks), dim3(kPartThreads), lds, st, a);
   return (int)hipGetLastError();
 }
 
@@ -499,5 +889,70 @@ CDNA_API int cdna_join_probe(const void* keys, const uint8_t* valid, int64_t n, 
   hipLaunchKernelGGL(join_probe_kernel, dim3(grid_of(n)), dim3(256), 0, st,
                      reinterpret_cast<const unsigned long long*>(keys), valid, n,
                      reinterpret_cast<const unsigned long long*>(table), mask, brow, bcnt, ri, cnt, slot);
+  return (int)hipGetLastError();
+}
+
+// Low-cardinality aggregation / dedup: la_agg over nblk = ceil(n / rpb) blocks, then la_merge; ngroups[0] = groups
+// (-1: a chunk or the merged table overflowed -> the partitioned path).  total / ovf: two zeroed ints.
+CDNA_API int cdna_la_groups(const void* keys, int64_t n, int64_t rpb, int S, int cap, int na, const int* ops,
+                            const int* vcols, int nv, const void* const* vals, const uint8_t* const* valids,
+                            const int* vdtypes, int mode, int pout, void* pkey, uint32_t* pcnt, uint32_t* pfirst,
+                            void* pacc, int64_t pcap, int* total, int* ovf, void* gkey, uint32_t* gcnt,
+                            uint32_t* gfirst, void* gacc, int* ngroups, uint8_t* keep, hipStream_t st) {
+  if (n <= 0) return 0;
+  const int lds = cdna_hp_agg_lds_bytes(S, na);
+  if (rpb <= 0 || S < 64 || S > 65536 || cap >= S || na < 0 || na > kMaxAcc || nv < 0 || nv > kMaxAcc ||
+      lds > cdna_hp_agg_lds_budget() || mode < 0 || mode > 1 || (mode == 1 && (pout < 1 || pout > 255)) ||
+      n >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  const int64_t nblk = (n + rpb - 1) / rpb;
+  if (pcap < nblk * (int64_t)(cap + 2)) return (int)hipErrorInvalidValue;
+  LocalArgs a{};
+  a.keys = reinterpret_cast<const unsigned long long*>(keys);
+  a.n = n;
+  a.rpb = rpb;
+  a.S = S;
+  a.cap = cap;
+  a.na = na;
+  for (int j = 0; j < na; ++j) {
+    a.op[j] = ops[j];
+    a.vcol[j] = vcols[j];
+  }
+  for (int j = 0; j < nv; ++j) {
+    a.val[j] = vals[j];
+    a.valid[j] = valids[j];
+    a.vdtype[j] = vdtypes[j];
+  }
+  a.mode = mode;
+  a.pout = pout;
+  a.pkey = reinterpret_cast<unsigned long long*>(pkey);
+  a.pcnt = pcnt;
+  a.pfirst = pfirst;
+  a.pacc = reinterpret_cast<unsigned long long*>(pacc);
+  a.pcap = pcap;
+  a.total = total;
+  a.ovf = ovf;
+  a.gkey = reinterpret_cast<unsigned long long*>(gkey);
+  a.gcnt = gcnt;
+  a.gfirst = gfirst;
+  a.gacc = reinterpret_cast<unsigned long long*>(gacc);
+  a.ngroups = ngroups;
+  a.keep = keep;
+  set_lds_limit();
+  hipLaunchKernelGGL(la_agg_kernel, dim3((unsigned)nblk), dim3(kAggThreads), (size_t)lds, st, a);
+  hipLaunchKernelGGL(la_merge_kernel, dim3(1), dim3(kAggThreads), (size_t)lds, st, a);
+  return (int)hipGetLastError();
+}
+
+// pass 1: counts [nb][nblk] of the rows with keep = 1 + bucket; pass 2: idx from offs (exclusive scan of counts).
+CDNA_API int cdna_bucket_compact(int pass, const uint8_t* keep, int64_t n, int nb, int64_t rpb, int* counts,
+                                 const int64_t* offs, int64_t* idx, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (nb < 1 || nb > 255 || rpb <= 0) return (int)hipErrorInvalidValue;
+  const unsigned nblk = (unsigned)((n + rpb - 1) / rpb);
+  if (pass == 1)
+    hipLaunchKernelGGL(bucket_compact_kernel<false>, dim3(nblk), dim3(256), 0, st, keep, n, nb, rpb, counts, offs, idx);
+  else
+    hipLaunchKernelGGL(bucket_compact_kernel<true>, dim3(nblk), dim3(256), 0, st, keep, n, nb, rpb, counts, offs, idx);
   return (int)hipGetLastError();
 }

@@ -177,6 +177,53 @@ __global__ __launch_bounds__(kThreads) void compact_mask_kernel(const uint8_t* _
   if (!WRITE && threadIdx.x == 0) counts[blockIdx.x] = total;
 }
 
+// K19 gather: out_c[i] = src_c[idx[i]] for up to 8 one-dimensional columns of 1/2/4/8-byte elements in one launch
+// (Batch.take behind filter / join / dropDuplicates / groupBy keys).  Two rows per thread in flight; the
+// index loads and the output stores are coalesced, the source loads follow idx.
+constexpr int kMaxGather = 8;
+struct GatherArgs {
+  const int64_t* idx;
+  int64_t m;
+  int nc;
+  const void* src[kMaxGather];
+  void* dst[kMaxGather];
+  int eb[kMaxGather];
+};
+
+template <typename E>
+__device__ __forceinline__ void gcopy(const void* s, void* d, int64_t j, int64_t i) {
+  reinterpret_cast<E*>(d)[i] = reinterpret_cast<const E*>(s)[j];
+}
+
+__global__ __launch_bounds__(kThreads) void gather_kernel(const GatherArgs a) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x; i0 < a.m; i0 += 2 * stride) {
+    const int64_t i1 = i0 + stride;
+    const int64_t j0 = a.idx[i0];
+    const int64_t j1 = i1 < a.m ? a.idx[i1] : 0;
+    for (int c = 0; c < a.nc; ++c) {
+      switch (a.eb[c]) {
+        case 1:
+          gcopy<uint8_t>(a.src[c], a.dst[c], j0, i0);
+          if (i1 < a.m) gcopy<uint8_t>(a.src[c], a.dst[c], j1, i1);
+          break;
+        case 2:
+          gcopy<uint16_t>(a.src[c], a.dst[c], j0, i0);
+          if (i1 < a.m) gcopy<uint16_t>(a.src[c], a.dst[c], j1, i1);
+          break;
+        case 4:
+          gcopy<uint32_t>(a.src[c], a.dst[c], j0, i0);
+          if (i1 < a.m) gcopy<uint32_t>(a.src[c], a.dst[c], j1, i1);
+          break;
+        default:
+          gcopy<uint64_t>(a.src[c], a.dst[c], j0, i0);
+          if (i1 < a.m) gcopy<uint64_t>(a.src[c], a.dst[c], j1, i1);
+          break;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // dtype: 0 = f32, 1 = f64.  part: [nblk][d][5] (count, mean, M2, min, max); nblk = ceil(n / rows_per_block).
@@ -222,5 +269,25 @@ CDNA_API int cdna_compact_mask(int pass, const uint8_t* mask, int64_t n, int64_t
   else
     hipLaunchKernelGGL(compact_mask_kernel<true>, dim3(nblk), dim3(kThreads), 0, st, mask, n, rows_per_block, counts,
                        offsets, idx);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_gather(const int64_t* idx, int64_t m, int nc, const void* const* src, void* const* dst,
+                         const int* eb, hipStream_t st) {
+  if (m <= 0 || nc <= 0) return 0;
+  if (nc > kMaxGather) return (int)hipErrorInvalidValue;
+  GatherArgs a{};
+  a.idx = idx;
+  a.m = m;
+  a.nc = nc;
+  for (int c = 0; c < nc; ++c) {
+    if (eb[c] != 1 && eb[c] != 2 && eb[c] != 4 && eb[c] != 8) return (int)hipErrorInvalidValue;
+    a.src[c] = src[c];
+    a.dst[c] = dst[c];
+    a.eb[c] = eb[c];
+  }
+  int64_t g = (m + 2 * kThreads - 1) / (2 * kThreads);
+  g = g < 8192 ? (g > 0 ? g : 1) : 8192;
+  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)g), dim3(kThreads), 0, st, a);
   return (int)hipGetLastError();
 }

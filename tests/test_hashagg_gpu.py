@@ -39,6 +39,13 @@ def calls(monkeypatch):
     return seen
 
 
+@pytest.fixture(params=["local", "partitioned"])
+def path(request, monkeypatch):
+    """Both K16 aggregation paths: per-chunk LDS tables + merge (few keys), and the radix-partitioned tables."""
+    monkeypatch.setattr(K, "LOCAL_FIRST", request.param == "local")
+    return request.param
+
+
 def _frame(n, seed, nkeys=5000):
     rng = np.random.default_rng(seed)
     v = rng.normal(size=n)
@@ -48,7 +55,7 @@ def _frame(n, seed, nkeys=5000):
                          "i": rng.integers(-1000, 1000, n), "id": np.arange(n)})
 
 
-def test_groupby_int_key_all_table_aggregates(spark, calls):
+def test_groupby_int_key_all_table_aggregates(spark, calls, path):
     from cdnaml.sql import functions as F
     pdf = _frame(300_000, 1)
     df = spark.createDataFrame(pdf)
@@ -68,7 +75,7 @@ def test_groupby_int_key_all_table_aggregates(spark, calls):
         np.testing.assert_allclose(got[c].to_numpy(float), ref[c].to_numpy(float), rtol=1e-12, atol=1e-12)
 
 
-def test_groupby_generic_aggregates_use_table_group_ids(spark, calls):
+def test_groupby_generic_aggregates_use_table_group_ids(spark, calls, path):
     from cdnaml.sql import functions as F
     pdf = _frame(200_000, 2, nkeys=300)
     df = spark.createDataFrame(pdf)
@@ -81,7 +88,7 @@ def test_groupby_generic_aggregates_use_table_group_ids(spark, calls):
     np.testing.assert_allclose(got["m"].to_numpy(float), g["i"].mean().to_numpy(), rtol=1e-12)
 
 
-def test_groupby_multi_column_and_string_keys_with_nulls(spark, calls):
+def test_groupby_multi_column_and_string_keys_with_nulls(spark, calls, path):
     from cdnaml.sql import functions as F
     pdf = _frame(250_000, 3)
     df = spark.createDataFrame(pdf)
@@ -99,7 +106,7 @@ def test_groupby_multi_column_and_string_keys_with_nulls(spark, calls):
     assert sorted(got1["count"].tolist()) == sorted(pdf.groupby("s", dropna=False).size().tolist())
 
 
-def test_groupby_float_key_nan_negzero_null(spark, calls):
+def test_groupby_float_key_nan_negzero_null(spark, calls, path):
     """Float keys: -0.0 and 0.0 are one group, NaN is one group sorted last, null is one group sorted first."""
     from cdnaml.sql import functions as F
     rng = np.random.default_rng(4)
@@ -123,7 +130,7 @@ def test_groupby_float_key_nan_negzero_null(spark, calls):
     assert gx[1:5] == [-7.0, 0.0, 0.5, 2.25] and gx[5] != gx[5]
 
 
-def test_dropduplicates_first_rows_in_order(spark, calls):
+def test_dropduplicates_first_rows_in_order(spark, calls, path):
     pdf = _frame(400_000, 5, nkeys=20_000)
     df = spark.createDataFrame(pdf)
     out = df.dropDuplicates(["k", "k2"])
@@ -211,3 +218,26 @@ def test_hash_groups_all_distinct_keys(spark):
     k, c, f = r["key"][pos], r["cnt"][pos], r["first"][pos].long()
     assert torch.equal(keys[f], k)
     assert int(c.sum()) == keys.numel() and int((c == 2).sum()) == 1000
+
+
+def test_gather_cols_and_bucket_compact(spark):
+    """K19 multi-column gather == torch indexing for every element width (and Batch.take's null masks);
+    bucket compaction == a stable numpy grouping of the kept rows by bucket."""
+    g = torch.Generator(device="cuda").manual_seed(1)
+    n, m = 300_000, 200_000
+    cols = [torch.randint(0, 255, (n,), generator=g, device="cuda", dtype=torch.int64).to(dt)
+            for dt in (torch.uint8, torch.int16, torch.int32, torch.int64, torch.float32, torch.float64)]
+    cols += [torch.rand(n, generator=g, device="cuda") > 0.5] * 4
+    idx = torch.randint(0, n, (m,), generator=g, device="cuda")
+    got = K.gather_cols(cols + [torch.zeros((n, 3), device="cuda")], idx)
+    assert got[-1] is None
+    for c, o in zip(cols, got[:-1]):
+        assert torch.equal(c[idx] if c.dtype != torch.bool else c[idx].view(torch.uint8), o.view(c.dtype).view(
+            torch.uint8) if c.dtype == torch.bool else o)
+    keep = torch.randint(0, 6, (n,), generator=g, device="cuda").to(torch.uint8)
+    keep[keep == 5] = 0
+    ix, counts = K.bucket_compact(keep, 4)
+    k = keep.cpu().numpy()
+    ref = np.concatenate([np.nonzero(k == b + 1)[0] for b in range(4)])
+    assert np.array_equal(ix.cpu().numpy(), ref)
+    assert counts.cpu().tolist() == [int((k == b + 1).sum()) for b in range(4)]
