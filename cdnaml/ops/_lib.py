@@ -170,6 +170,10 @@ _SIGS = {
                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_bucket_compact": ([c_int, c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_gather": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_join_build_dense": ([c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],
+                              c_int),
+    "cdna_join_probe_dense": ([c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p], c_int),
     "cdna_join_build": ([c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],
                         c_int),
     "cdna_join_probe": ([c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,

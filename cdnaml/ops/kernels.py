@@ -1784,9 +1784,10 @@ def bucket_compact(keep: torch.Tensor, nb: int):
     n = keep.numel()
     dev = keep.device
     L = _lib.lib()
-    rpb = max(4096, -(-n // 1024))
-    nblk = -(-n // rpb)
-    counts = torch.empty((nb, nblk), dtype=torch.int32, device=dev)
+    rpb = max(1024, -(-n // 16384) + 63) // 64 * 64      # rows per wave
+    nw = -(-n // rpb)
+    nblk = 4 * (-(-nw // 4))
+    counts = torch.zeros((nb, nblk), dtype=torch.int32, device=dev)
     _lib.check(L.cdna_bucket_compact(1, _ptr(keep), n, nb, rpb, _ptr(counts), None, None, _stream(dev)),
                "cdna_bucket_compact(count)")
     flat = counts.view(-1).long()
@@ -2106,36 +2107,67 @@ def ordered_to_double(u: torch.Tensor) -> torch.Tensor:
     return bits.view(torch.float64)
 
 
-def join_table(keys: torch.Tensor, valid: Optional[torch.Tensor]):
-    """K16 join build side: global open-addressing table (2x the rows, >= 1024 slots) of int64 key words.
-    Returns (table, mask, first build row per slot, build rows per slot) or None on overflow."""
+class JoinTable:
+    """K16 join build side.  kind 'dense': direct-addressed arrays over the key range [lo, lo + R) plus a presence
+    bitmap; kind 'hash': open-addressing table of 2x the rows.  brow / bcnt: first build row and build rows per
+    slot; nslots: slot count (slot ids of probes are < nslots); ovf: device overflow flag (hash only)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+DENSE_JOIN_MAX = 1 << 26
+
+
+def join_table(keys: torch.Tensor, valid: Optional[torch.Tensor]) -> JoinTable:
+    """Build side of a K16 join over int64 key words (hashagg.hip join_build / join_build_dense)."""
     n = keys.numel()
     dev = keys.device
+    L = _lib.lib()
+    v8 = None if valid is None else valid.contiguous().view(torch.uint8)
+    keys = keys.contiguous()
+    if n:
+        kv = keys if valid is None else keys[valid]
+        if kv.numel():
+            lo, hi = (int(x) for x in torch.stack(list(torch.aminmax(kv))).cpu().tolist())
+            R = hi - lo + 1
+            if R <= max(1 << 22, 8 * n) and R <= DENSE_JOIN_MAX:
+                brow = torch.full((R,), (1 << 63) - 1, dtype=torch.int64, device=dev)
+                bcnt = torch.zeros(R, dtype=torch.int32, device=dev)
+                bits = torch.zeros((R + 31) // 32, dtype=torch.int32, device=dev)
+                _lib.check(L.cdna_join_build_dense(_ptr(keys), _ptr(v8), n, lo, R, _ptr(brow), _ptr(bcnt), _ptr(bits),
+                                                   _stream(dev)), "cdna_join_build_dense")
+                return JoinTable(kind="dense", lo=lo, R=R, brow=brow, bcnt=bcnt, bits=bits, nslots=R,
+                                 ovf=torch.zeros(1, dtype=torch.int32, device=dev))
     P = 1 << max(10, (2 * max(n, 1) - 1).bit_length())
     table = torch.full((P + 1,), _EMPTY64, dtype=torch.int64, device=dev)
     brow = torch.full((P + 1,), (1 << 63) - 1, dtype=torch.int64, device=dev)
     bcnt = torch.zeros(P + 1, dtype=torch.int32, device=dev)
     ovf = torch.zeros(1, dtype=torch.int32, device=dev)
-    v8 = None if valid is None else valid.contiguous().view(torch.uint8)
-    _lib.check(_lib.lib().cdna_join_build(_ptr(keys.contiguous()), _ptr(v8), n, _ptr(table), P - 1, _ptr(brow),
-                                          _ptr(bcnt), _ptr(ovf), _stream(dev)), "cdna_join_build")
-    return table, P - 1, brow, bcnt, ovf
+    _lib.check(L.cdna_join_build(_ptr(keys), _ptr(v8), n, _ptr(table), P - 1, _ptr(brow), _ptr(bcnt), _ptr(ovf),
+                                 _stream(dev)), "cdna_join_build")
+    return JoinTable(kind="hash", table=table, mask=P - 1, brow=brow, bcnt=bcnt, nslots=P + 1, ovf=ovf)
 
 
-def join_probe(keys: torch.Tensor, valid: Optional[torch.Tensor], tab, want_cnt: bool = False,
+def join_probe(keys: torch.Tensor, valid: Optional[torch.Tensor], tab: JoinTable, want_cnt: bool = False,
                want_slot: bool = False):
     """K16 join probe: per probe row the first matching build row (-1: none), optionally the number of build rows
     with its key and its table slot."""
-    table, mask, brow, bcnt, _ = tab
     n = keys.numel()
     dev = keys.device
     ri = torch.empty(n, dtype=torch.int64, device=dev)
     cnt = torch.empty(n, dtype=torch.int32, device=dev) if want_cnt else None
     slot = torch.empty(n, dtype=torch.int64, device=dev) if want_slot else None
     v8 = None if valid is None else valid.contiguous().view(torch.uint8)
-    _lib.check(_lib.lib().cdna_join_probe(_ptr(keys.contiguous()), _ptr(v8), n, _ptr(table), mask, _ptr(brow),
-                                          _ptr(bcnt), _ptr(ri), _ptr(cnt), _ptr(slot), _stream(dev)),
-               "cdna_join_probe")
+    L = _lib.lib()
+    if tab.kind == "dense":
+        _lib.check(L.cdna_join_probe_dense(_ptr(keys.contiguous()), _ptr(v8), n, tab.lo, tab.R, _ptr(tab.brow),
+                                           _ptr(tab.bcnt), _ptr(tab.bits), _ptr(ri), _ptr(cnt), _ptr(slot),
+                                           _stream(dev)), "cdna_join_probe_dense")
+    else:
+        _lib.check(L.cdna_join_probe(_ptr(keys.contiguous()), _ptr(v8), n, _ptr(tab.table), tab.mask, _ptr(tab.brow),
+                                     _ptr(tab.bcnt), _ptr(ri), _ptr(cnt), _ptr(slot), _stream(dev)),
+                   "cdna_join_probe")
     return ri, cnt, slot
 
 

@@ -580,7 +580,7 @@ def _join_native(left: Batch, right: Batch, lkeys, rkeys, how: str, drop_right_k
     (lw, rw), _ = kw
     lvalid, rvalid = _all_valid(lcols), _all_valid(rcols)
     tab = K.join_table(rw, rvalid)
-    ovf, maxc = torch.stack([tab[4][0].long(), tab[3].max().long()]).cpu().tolist()
+    ovf, maxc = torch.stack([tab.ovf[0].long(), tab.bcnt.max().long()]).cpu().tolist()
     if ovf:
         return None
     ri_all, cnt_l, slot_l = K.join_probe(lw, lvalid, tab, want_cnt=maxc > 1, want_slot=maxc > 1)
@@ -598,10 +598,9 @@ def _join_native(left: Batch, right: Batch, lkeys, rkeys, how: str, drop_right_k
         li = torch.repeat_interleave(torch.arange(nl, device=dev), cnt, output_size=total)
         # build rows grouped by table slot, in row order within a slot (CSR over the slots)
         _, _, rslot = K.join_probe(rw, rvalid, tab, want_slot=True)
-        P1 = tab[0].numel()
-        rslot = torch.where(rslot < 0, torch.full_like(rslot, P1), rslot)
+        rslot = torch.where(rslot < 0, torch.full_like(rslot, tab.nslots), rslot)
         order_r = torch.argsort(rslot, stable=True)
-        bc = tab[3].long()
+        bc = tab.bcnt.long()
         start = torch.cumsum(bc, 0) - bc
         within = torch.arange(total, device=dev) - torch.repeat_interleave(torch.cumsum(cnt, 0) - cnt, cnt,
                                                                            output_size=total)
@@ -626,16 +625,12 @@ def _assemble(left, right, li, ri, lmiss, rmiss, keypairs, drop_right_keys, how=
     nrm = 0 if rmiss is None else rmiss.numel()
     total = nmatch + nlm + nrm
     rkeys = {b: a for a, b in keypairs} if drop_right_keys else {}
-
-    def gather(c: ColumnData, idx, present_mask_len, side_present):
-        parts_v, parts_m = [], []
-        taken = c.take(idx)
-        parts_v.append(taken.values)
-        parts_m.append(taken.valid_mask())
-        return taken
+    # the matched rows of each side in one multi-column gather (K19 on the GPU)
+    lt = left.take(li)
+    rt = Batch({k: c for k, c in right.columns.items() if k not in rkeys}, right.n, right.device).take(ri)
 
     for name, c in left.columns.items():
-        pieces = [c.take(li)]
+        pieces = [lt.columns[name]]
         if nlm:
             pieces.append(c.take(lmiss))
         if nrm:
@@ -661,7 +656,7 @@ def _assemble(left, right, li, ri, lmiss, rmiss, keypairs, drop_right_keys, how=
             while outname in cols:
                 outname = f"{name}_{k}"
                 k += 1
-        pieces = [c.take(ri)]
+        pieces = [rt.columns[name]]
         if nlm:
             pieces.append(_null_like(c, nlm))
         if nrm:

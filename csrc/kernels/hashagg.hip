@@ -397,11 +397,18 @@ __global__ __launch_bounds__(kAggThreads) void hp_agg_kernel(const AggArgs a) {
 // the partials (la_merge: counts and sums add, first rows and mins take the min, maxes and last rows the max).
 // A chunk with more distinct keys than its table holds stops early and raises the overflow flag; the host then
 // runs the partitioned path.
+// Once the table has overflowed (cap distinct keys) a probe gives up within 32 steps: without that, every row after
+// the overflow walked the whole nearly-full table (4.4 ms per 1e8 high-cardinality rows before the fallback).
+__device__ __forceinline__ bool flagged(int* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+}
+
 __device__ __forceinline__ int lds_slot(unsigned long long* tk, int S, unsigned long long k, int cap, int* s_nd,
                                         int* s_ovf) {
   if (k == kEmpty) return S;
   int pos = pos_of(mix64(k), S);
   for (int t = 0; t < S; ++t) {
+    if ((t & 31) == 31 && flagged(s_ovf)) return -1;
     const unsigned long long cur = __hip_atomic_load(tk + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (cur == k) return pos;
     if (cur == kEmpty) {
@@ -470,6 +477,7 @@ __device__ __forceinline__ void lds_table_init(const LdsTable& t, int S, int na,
 
 __global__ __launch_bounds__(kAggThreads) void la_agg_kernel(const LocalArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (__hip_atomic_load(a.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // another chunk overflowed
   const int S = a.S;
   const LdsTable t = lds_table(smem, S, a.na);
   __shared__ int s_nd, s_ovf, s_out, s_base;
@@ -483,7 +491,7 @@ __global__ __launch_bounds__(kAggThreads) void la_agg_kernel(const LocalArgs a) 
   const int64_t r0 = (int64_t)blockIdx.x * a.rpb;
   const int64_t r1 = r0 + a.rpb < a.n ? r0 + a.rpb : a.n;
   for (int64_t r = r0 + threadIdx.x; r < r1; r += kAggThreads) {
-    if (s_ovf) break;
+    if (flagged(&s_ovf)) break;
     const int s = lds_slot(t.tk, S, a.keys[r], a.cap, &s_nd, &s_ovf);
     if (s < 0) break;
     atomicMin(t.tf + s, (uint32_t)r);
@@ -541,6 +549,7 @@ __global__ __launch_bounds__(kAggThreads) void la_merge_kernel(const LocalArgs a
   __syncthreads();
   const int64_t total = *a.total;
   for (int64_t e = threadIdx.x; e < total; e += kAggThreads) {
+    if (flagged(&s_ovf)) break;
     const int s = lds_slot(t.tk, S, a.pkey[e], S - 1, &s_nd, &s_ovf);
     if (s < 0) break;
     atomicMin(t.tf + s, a.pfirst[e]);
@@ -581,57 +590,61 @@ __global__ __launch_bounds__(kAggThreads) void la_merge_kernel(const LocalArgs a
 
 // ------------------------------------------------------------------------------------------ bucket_compact
 // dropDuplicates output: the rows whose keep byte is non-zero (1 + output partition), grouped by partition and
-// in row order within a partition, in two passes (counts per (bucket, block); a stable ballot-ranked scatter).
+// in row order within a partition.  Every wave owns a contiguous row range (no block barriers): pass 1 counts
+// its rows per bucket with one ballot per bucket and 64 rows, pass 2 writes each kept row at its bucket's
+// running offset + its rank among the wave's lanes (mbcnt).  Up to 16 buckets keep their counters in scalar
+// registers; more buckets elect one bucket per step from the active lanes.
 template <bool SCATTER>
 __global__ __launch_bounds__(256) void bucket_compact_kernel(const uint8_t* __restrict__ keep, int64_t n, int nb,
-                                                             int64_t rpb, int* __restrict__ counts,
+                                                             int64_t rpw, int* __restrict__ counts,
                                                              const int64_t* __restrict__ offs,
                                                              int64_t* __restrict__ idx) {
-  __shared__ int s_cnt[256];
-  const int nblk = gridDim.x;
-  for (int i = threadIdx.x; i < nb; i += 256) s_cnt[i] = 0;
-  __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * rpb;
-  const int64_t r1 = r0 + rpb < n ? r0 + rpb : n;
-  if (!SCATTER) {
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
-      const int b = keep[r];
-      if (b) atomicAdd(&s_cnt[b - 1], 1);
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t r0 = w * rpw;
+  const int64_t r1 = r0 + rpw < n ? r0 + rpw : n;
+  if (nb <= 16) {
+    int64_t c[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) c[q] = SCATTER && q < nb ? offs[(int64_t)q * nw + w] : 0;
+    for (int64_t rb = r0; rb < r1; rb += 64) {
+      const int64_t r = rb + lane;
+      const int b = r < r1 ? (int)keep[r] - 1 : -1;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (q >= nb) break;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(b == q);
+        if (SCATTER && b == q)
+          idx[c[q] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = r;
+        c[q] += __builtin_popcountll(m);
+      }
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nb; i += 256) counts[(int64_t)i * nblk + blockIdx.x] = s_cnt[i];
+    if (!SCATTER && lane == 0)
+      for (int q = 0; q < nb; ++q) counts[(int64_t)q * nw + w] = (int)c[q];
     return;
   }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int64_t rb = r0; rb < r1; rb += 256) {
-    const int64_t r = rb + threadIdx.x;
+  __shared__ int64_t s_c[4][256];
+  int64_t* c = s_c[threadIdx.x >> 6];
+  for (int q = lane; q < nb; q += 64) c[q] = SCATTER ? offs[(int64_t)q * nw + w] : 0;
+  for (int64_t rb = r0; rb < r1; rb += 64) {
+    const int64_t r = rb + lane;
     const int b = r < r1 ? (int)keep[r] - 1 : -1;
-    for (int w = 0; w < 4; ++w) {  // waves take turns so earlier rows get lower positions
-      if (wid == w) {
-        bool want = b >= 0;
-        while (true) {
-          const uint64_t act = __builtin_amdgcn_ballot_w64(want);
-          if (!act) break;
-          const int leader = __builtin_ctzll(act);
-          const int lb = __shfl(b, leader);
-          const uint64_t msk = __builtin_amdgcn_ballot_w64(want && b == lb);
-          int base = 0;
-          if (lane == leader) {
-            base = s_cnt[lb];
-            s_cnt[lb] = base + __builtin_popcountll(msk);
-          }
-          base = __shfl(base, leader);
-          if (want && b == lb) {
-            const int below =
-                (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
-            idx[offs[(int64_t)lb * nblk + blockIdx.x] + base + below] = r;
-            want = false;
-          }
-        }
-      }
-      __syncthreads();
+    bool want = b >= 0;
+    while (true) {
+      const uint64_t act = __builtin_amdgcn_ballot_w64(want);
+      if (!act) break;
+      const int lb = __shfl(b, __builtin_ctzll(act));
+      const uint64_t m = __builtin_amdgcn_ballot_w64(want && b == lb);
+      const int64_t base = c[lb];
+      if (SCATTER && want && b == lb)
+        idx[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = r;
+      if (want && b == lb) want = false;
+      if (lane == 0) c[lb] = base + __builtin_popcountll(m);
     }
   }
+  if (!SCATTER)
+    for (int q = lane; q < nb; q += 64) counts[(int64_t)q * nw + w] = (int)c[q];
 }
 
 // ---------------------------------------------------------------------------------------------------- join
@@ -728,6 +741,56 @@ __global__ __launch_bounds__(256) void join_probe_kernel(const unsigned long lon
       ri[i] = found[u] >= 0 ? brow[found[u]] : -1;
       if (cnt) cnt[i] = found[u] >= 0 ? bcnt[found[u]] : 0;
       if (slot) slot[i] = found[u];
+    }
+  }
+}
+
+// Dense join tables: when the build keys span a small range [lo, lo + R) (the course's integer ids, packed
+// (user, movie) pairs), the table is direct-addressed -- no hashing, no probing -- and a presence bitmap of
+// R bits (125 KB for 1e6 keys: L2-resident) answers the misses without touching the row array.
+__global__ __launch_bounds__(256) void join_build_dense_kernel(const long long* __restrict__ keys,
+                                                               const uint8_t* __restrict__ valid, int64_t n,
+                                                               long long lo, int64_t R, long long* __restrict__ brow,
+                                                               int* __restrict__ bcnt, uint32_t* __restrict__ bits) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (valid && !valid[i]) continue;
+    const long long f = keys[i] - lo;
+    if (!CDNA_DCHECK(f >= 0 && f < R, 0xA503)) continue;
+    atomicMin(brow + f, (long long)i);
+    atomicAdd(bcnt + f, 1);
+    atomicOr(bits + (f >> 5), 1u << (f & 31));
+  }
+}
+
+__global__ __launch_bounds__(256) void join_probe_dense_kernel(const long long* __restrict__ keys,
+                                                               const uint8_t* __restrict__ valid, int64_t n,
+                                                               long long lo, int64_t R,
+                                                               const long long* __restrict__ brow,
+                                                               const int* __restrict__ bcnt,
+                                                               const uint32_t* __restrict__ bits,
+                                                               long long* __restrict__ ri, int* __restrict__ cnt,
+                                                               long long* __restrict__ slot) {
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += stride * U) {
+    long long f[U];
+    bool hit[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      f[u] = -1;
+      if (i < n && (!valid || valid[i])) f[u] = keys[i] - lo;
+      if (f[u] >= R) f[u] = -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) hit[u] = f[u] >= 0 && ((bits[f[u] >> 5] >> (f[u] & 31)) & 1u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n) continue;
+      ri[i] = hit[u] ? brow[f[u]] : -1;
+      if (cnt) cnt[i] = hit[u] ? bcnt[f[u]] : 0;
+      if (slot) slot[i] = hit[u] ? f[u] : -1;
     }
   }
 }
@@ -944,15 +1007,37 @@ CDNA_API int cdna_la_groups(const void* keys, int64_t n, int64_t rpb, int S, int
   return (int)hipGetLastError();
 }
 
-// pass 1: counts [nb][nblk] of the rows with keep = 1 + bucket; pass 2: idx from offs (exclusive scan of counts).
-CDNA_API int cdna_bucket_compact(int pass, const uint8_t* keep, int64_t n, int nb, int64_t rpb, int* counts,
+// pass 1: counts [nb][nwaves] of the rows with keep = 1 + bucket (nwaves = 4 * ceil(n / (4 * rpw))); pass 2: idx
+// from offs (exclusive scan of counts).
+CDNA_API int cdna_bucket_compact(int pass, const uint8_t* keep, int64_t n, int nb, int64_t rpw, int* counts,
                                  const int64_t* offs, int64_t* idx, hipStream_t st) {
   if (n <= 0) return 0;
-  if (nb < 1 || nb > 255 || rpb <= 0) return (int)hipErrorInvalidValue;
-  const unsigned nblk = (unsigned)((n + rpb - 1) / rpb);
+  if (nb < 1 || nb > 255 || rpw <= 0 || (rpw & 63)) return (int)hipErrorInvalidValue;
+  const int64_t nw = (n + rpw - 1) / rpw;
+  const unsigned nblk = (unsigned)((nw + 3) / 4);
   if (pass == 1)
-    hipLaunchKernelGGL(bucket_compact_kernel<false>, dim3(nblk), dim3(256), 0, st, keep, n, nb, rpb, counts, offs, idx);
+    hipLaunchKernelGGL(bucket_compact_kernel<false>, dim3(nblk), dim3(256), 0, st, keep, n, nb, rpw, counts, offs, idx);
   else
-    hipLaunchKernelGGL(bucket_compact_kernel<true>, dim3(nblk), dim3(256), 0, st, keep, n, nb, rpb, counts, offs, idx);
+    hipLaunchKernelGGL(bucket_compact_kernel<true>, dim3(nblk), dim3(256), 0, st, keep, n, nb, rpw, counts, offs, idx);
+  return (int)hipGetLastError();
+}
+
+// brow [R] = INT64_MAX, bcnt [R] = 0, bits [(R + 31) / 32] = 0 on entry.
+CDNA_API int cdna_join_build_dense(const long long* keys, const uint8_t* valid, int64_t n, long long lo, int64_t R,
+                                   long long* brow, int* bcnt, uint32_t* bits, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (R <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(join_build_dense_kernel, dim3(grid_of(n)), dim3(256), 0, st, keys, valid, n, lo, R, brow, bcnt,
+                     bits);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_join_probe_dense(const long long* keys, const uint8_t* valid, int64_t n, long long lo, int64_t R,
+                                   const long long* brow, const int* bcnt, const uint32_t* bits, long long* ri,
+                                   int* cnt, long long* slot, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (R <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(join_probe_dense_kernel, dim3(grid_of(n)), dim3(256), 0, st, keys, valid, n, lo, R, brow, bcnt,
+                     bits, ri, cnt, slot);
   return (int)hipGetLastError();
 }

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kThreads) void compact_mask_kernel(const uint8_t* _
 }
 
 // K19 gather: out_c[i] = src_c[idx[i]] for up to 8 one-dimensional columns of 1/2/4/8-byte elements in one launch
-// (Batch.take behind filter / join / dropDuplicates / groupBy keys).  Two rows per thread in flight; the
+// (Batch.take behind filter / join / dropDuplicates / groupBy keys).  Eight rows per thread in flight; the
 // index loads and the output stores are coalesced, the source loads follow idx.
 constexpr int kMaxGather = 8;
 struct GatherArgs {
@@ -190,35 +190,31 @@ struct GatherArgs {
   int eb[kMaxGather];
 };
 
-template <typename E>
-__device__ __forceinline__ void gcopy(const void* s, void* d, int64_t j, int64_t i) {
-  reinterpret_cast<E*>(d)[i] = reinterpret_cast<const E*>(s)[j];
+// eight rows per thread: their index loads, then per column their eight source loads, are issued back to back
+template <typename E, int U>
+__device__ __forceinline__ void gcols(const void* s, void* d, const int64_t* j, int64_t i0, int64_t stride,
+                                      int64_t m) {
+  E v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = j[u] >= 0 ? reinterpret_cast<const E*>(s)[j[u]] : E(0);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (i0 + u * stride < m) reinterpret_cast<E*>(d)[i0 + u * stride] = v[u];
 }
 
 __global__ __launch_bounds__(kThreads) void gather_kernel(const GatherArgs a) {
+  constexpr int U = 8;
   const int64_t stride = (int64_t)gridDim.x * kThreads;
-  for (int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x; i0 < a.m; i0 += 2 * stride) {
-    const int64_t i1 = i0 + stride;
-    const int64_t j0 = a.idx[i0];
-    const int64_t j1 = i1 < a.m ? a.idx[i1] : 0;
+  for (int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x; i0 < a.m; i0 += stride * U) {
+    int64_t j[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) j[u] = i0 + u * stride < a.m ? a.idx[i0 + u * stride] : -1;
     for (int c = 0; c < a.nc; ++c) {
       switch (a.eb[c]) {
-        case 1:
-          gcopy<uint8_t>(a.src[c], a.dst[c], j0, i0);
-          if (i1 < a.m) gcopy<uint8_t>(a.src[c], a.dst[c], j1, i1);
-          break;
-        case 2:
-          gcopy<uint16_t>(a.src[c], a.dst[c], j0, i0);
-          if (i1 < a.m) gcopy<uint16_t>(a.src[c], a.dst[c], j1, i1);
-          break;
-        case 4:
-          gcopy<uint32_t>(a.src[c], a.dst[c], j0, i0);
-          if (i1 < a.m) gcopy<uint32_t>(a.src[c], a.dst[c], j1, i1);
-          break;
-        default:
-          gcopy<uint64_t>(a.src[c], a.dst[c], j0, i0);
-          if (i1 < a.m) gcopy<uint64_t>(a.src[c], a.dst[c], j1, i1);
-          break;
+        case 1: gcols<uint8_t, U>(a.src[c], a.dst[c], j, i0, stride, a.m); break;
+        case 2: gcols<uint16_t, U>(a.src[c], a.dst[c], j, i0, stride, a.m); break;
+        case 4: gcols<uint32_t, U>(a.src[c], a.dst[c], j, i0, stride, a.m); break;
+        default: gcols<uint64_t, U>(a.src[c], a.dst[c], j, i0, stride, a.m); break;
       }
     }
   }
@@ -286,7 +282,7 @@ CDNA_API int cdna_gather(const int64_t* idx, int64_t m, int nc, const void* cons
     a.dst[c] = dst[c];
     a.eb[c] = eb[c];
   }
-  int64_t g = (m + 2 * kThreads - 1) / (2 * kThreads);
+  int64_t g = (m + 8 * kThreads - 1) / (8 * kThreads);
   g = g < 8192 ? (g > 0 ? g : 1) : 8192;
   hipLaunchKernelGGL(gather_kernel, dim3((unsigned)g), dim3(kThreads), 0, st, a);
   return (int)hipGetLastError();
