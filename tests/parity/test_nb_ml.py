@@ -142,6 +142,7 @@ def test_ml07_random_forest_cross_validation(nb, tmp_path):
     assert ev.evaluate(model.transform(test)) > 0
 
 
+@pytest.mark.slow
 def test_ml11_xgboost(nb):
     """ML 11:36-103 -- log label, StringIndexer + VectorAssembler + XgboostRegressor pipeline, exp back,
     RMSE / R^2."""

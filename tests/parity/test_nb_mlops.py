@@ -1,3 +1,4 @@
+import pytest
 """Parity flows for the MLOps / bridge notebooks: ML 04 MLflow Tracking, ML 05 Registry, ML 08 Hyperopt,
 ML 09 AutoML, ML 10 Feature Store, ML 12 Pandas UDFs, ML 14 Koalas, MLE 00 Deployment (SURVEY Appendix A)."""
 import os
@@ -139,6 +140,7 @@ def test_ml08_hyperopt(nb):
     assert best2["depth"] in (0, 1)                                      # hp.choice returns the index
 
 
+@pytest.mark.slow
 def test_ml09_automl(nb):
     """ML 09:29-90 -- automl.regress, best trial's run id, pyfunc.spark_udf predictions, RMSE."""
     spark, df = _airbnb(nb)

@@ -1,3 +1,4 @@
+import pytest
 """AutoML (SURVEY §2.6 T5; ML 09 - AutoML.py:35-90)."""
 import numpy as np
 import pandas as pd
@@ -7,6 +8,7 @@ from cdnaml import tracking as mlflow
 from cdnaml.ml.evaluation import RegressionEvaluator
 
 
+@pytest.mark.slow
 def test_automl_regress_and_serve(spark, tmp_path):
     mlflow.set_tracking_uri(str(tmp_path / "mlruns"))
     try:

@@ -8,6 +8,10 @@ import sys
 
 import pytest
 
+# every test here launches torchrun process groups (about 4 of the CPU suite's 5 minutes): the tight iteration loop
+# is `pytest tests -m "not gpu and not slow"`
+pytestmark = pytest.mark.slow
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
