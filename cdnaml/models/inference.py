@@ -54,10 +54,12 @@ class ForestPredictor:
     def _arrays(self, dev):
         key = str(dev)
         if key not in self._dev:
-            tw = torch.tensor(self.tw_host, device=dev)
+            from ..ops import kernels as K
+            # async pinned uploads: a pageable torch.tensor(..., device=) copy waits for the queue to drain
+            tw, bb = K.upload(dev, self.tw_host.reshape(-1), np.asarray(0.0 if self.base is None else self.base,
+                                                                          np.float32).reshape(-1))
             heap = self.forest.heap_arrays(dev, self.kind) if (dev.type == "cuda" and self.forest.K == 1) else None
-            b = None if self.base is None else torch.tensor(np.asarray(self.base, np.float32).reshape(-1),
-                                                            device=dev)
+            b = None if self.base is None else bb
             self._dev[key] = (tw, heap, b)
         return self._dev[key]
 

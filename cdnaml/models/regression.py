@@ -405,8 +405,11 @@ def resolve_subset(strategy: str, d: int, num_trees: int, classification: bool) 
     raise IllegalArgumentException(f"invalid featureSubsetStrategy {strategy}")
 
 
-def tree_fit_prepare(est, dataset, classification: bool):
-    """Common: device features/labels, categorical info, global row offset, binned data."""
+def tree_fit_prepare(est, dataset, classification: bool, pre=None):
+    """Common: device features/labels, categorical info, global row offset, binned data.
+
+    pre(n_local, row_offset, seed, device, y): launched before the quantile sample and binning are queued (the
+    forest's bootstrap draws and label maximum, which depend on neither, then overlap them on a side stream)."""
     fc, lc = est.getFeaturesCol(), est.getLabelCol()
     wc = est.getWeightCol() if est.hasParam("weightCol") else None
     require_vector(dataset, fc)
@@ -426,6 +429,8 @@ def tree_fit_prepare(est, dataset, classification: bool):
     seed = est.getOrDefault("seed")
     if seed is None:
         seed = _default_seed(type(est))
+    if pre is not None:
+        pre(n, off, seed, X.device, y)
     data = make_binned(session, X, cat, est.getMaxBins(), seed, off, n_global)
     return session, data, y, w, seed, fcol.meta
 
@@ -561,18 +566,47 @@ class _TreeRegressorModel(_TreeModelBase):
                                   self._numFeatures)
 
 
+def _early_side_work(num_trees, bootstrap, rate, want_label_max=True):
+    """(pre, early): ``pre`` for tree_fit_prepare queues the Poisson bootstrap draws and the maxima the fit needs
+    on the host (largest weight, max |label|) on the side stream before the quantile sample / threshold / binning
+    kernels: they overlap the sort of the sample (100 of 256 CUs busy) instead of competing with the
+    memory-bound binning, and the first level reads the maxima without draining the queue.  ``early`` then holds
+    "w" (weights) and "yf" (fp32 label); call _join_early once the binning is queued."""
+    early = {}
+
+    def pre(n, off, seed_, dev, y_):
+        if dev.type != "cuda":
+            return
+        side = _side_stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        if want_label_max:
+            with torch.cuda.stream(side):
+                early["yf"] = y_.float()
+            K.prefetch_max(early["yf"], absval=True, stream=side)
+        if bootstrap and num_trees > 1:
+            early["w"] = _poisson_side(num_trees, n, seed_, off, rate, dev, join=False)
+            K.prefetch_max(early["w"], stream=side)
+    return pre, early
+
+
+def _join_early(early, dev):
+    for k in ("yf", "w"):
+        if k in early:
+            _join_side(early[k], dev)  # binning is queued: the trainer's first kernel waits for the side stream
+
+
 def _train_forest_regression(est, dataset, num_trees, subset, bootstrap, rate, impurity="variance"):
-    session, data, y, w, seed, meta = tree_fit_prepare(est, dataset, classification=False)
-    if w is not None and bootstrap:
-        pass
+    pre, early = _early_side_work(num_trees, bootstrap, rate)
+    session, data, y, w, seed, meta = tree_fit_prepare(est, dataset, classification=False, pre=pre)
+    _join_early(early, data.bins.device)
     p = TreeParams(max_depth=est.getMaxDepth(), max_bins=est.getMaxBins(),
                    min_instances=float(est.getMinInstancesPerNode()), min_info_gain=est.getMinInfoGain(),
                    impurity=impurity, feature_subset=subset, bootstrap=bootstrap, subsampling_rate=rate, seed=seed)
-    weights = _bag_weights(data, num_trees, bootstrap, rate, seed)
+    weights = early["w"] if "w" in early else _bag_weights(data, num_trees, bootstrap, rate, seed)
     if w is not None:
         weights = _combine_weights(weights, w, num_trees)
     trainer = ForestTrainer(session, data, p)
-    forest = trainer.train(num_trees, {"v0": None, "v1": y.float()}, weights)
+    forest = trainer.train(num_trees, {"v0": None, "v1": early.get("yf", y.float())}, weights)
     return forest, data.d
 
 
@@ -586,20 +620,29 @@ def _side_stream(dev):
     return s
 
 
+def _poisson_side(T_, n, seed, row_offset, rate, dev, join: bool = True):
+    """Compute-bound Philox Poisson draws on a side stream (they depend on nothing queued on the current one).
+    join: the current stream waits for them before its next kernel (else call _join_side before using them)."""
+    side = _side_stream(dev)
+    with torch.cuda.stream(side):
+        wts = K.poisson_weights(T_, n, seed, row_offset, rate, device=dev)
+    if join:
+        _join_side(wts, dev)
+    return wts
+
+
+def _join_side(wts, dev):
+    main = torch.cuda.current_stream(dev)
+    main.wait_stream(_side_stream(dev))
+    wts.record_stream(main)
+
+
 def _bag_weights(data, T_, bootstrap, rate, seed):
     n = data.n_local
     dev = data.bins.device
     if bootstrap and T_ > 1:
         if dev.type == "cuda":
-            # compute-bound Philox draws on a side stream, overlapping the memory-bound binning kernel that
-            # make_binned has just queued on the current stream (the draws depend on nothing queued there)
-            main = torch.cuda.current_stream(dev)
-            side = _side_stream(dev)
-            with torch.cuda.stream(side):
-                wts = K.poisson_weights(T_, n, seed, data.row_offset, rate, device=dev)
-            main.wait_stream(side)
-            wts.record_stream(main)
-            return wts
+            return _poisson_side(T_, n, seed, data.row_offset, rate, dev)
         return K.poisson_weights(T_, n, seed, data.row_offset, rate, device=dev)
     if rate < 1.0:
         u = torch.stack([K.uniform(n, seed, data.row_offset, 0x200 + t, device=dev) for t in range(T_)])
@@ -653,16 +696,19 @@ class RandomForestRegressor(Estimator):
 
 
 def _train_rf_reg(est, dataset, T_):
-    session, data, y, w, seed, meta = tree_fit_prepare(est, dataset, classification=False)
+    pre, early = _early_side_work(T_, est.getBootstrap(), est.getSubsamplingRate())
+    session, data, y, w, seed, meta = tree_fit_prepare(est, dataset, classification=False, pre=pre)
+    _join_early(early, data.bins.device)
     subset = resolve_subset(est.getFeatureSubsetStrategy(), data.d, T_, False)
     p = TreeParams(max_depth=est.getMaxDepth(), max_bins=est.getMaxBins(),
                    min_instances=float(est.getMinInstancesPerNode()), min_info_gain=est.getMinInfoGain(),
                    impurity="variance", feature_subset=subset, bootstrap=est.getBootstrap(),
                    subsampling_rate=est.getSubsamplingRate(), seed=seed)
-    weights = _bag_weights(data, T_, est.getBootstrap(), est.getSubsamplingRate(), seed)
+    weights = early["w"] if "w" in early else \
+        _bag_weights(data, T_, est.getBootstrap(), est.getSubsamplingRate(), seed)
     if w is not None:
         weights = _combine_weights(weights, w, T_)
-    forest = ForestTrainer(session, data, p).train(T_, {"v0": None, "v1": y.float()}, weights)
+    forest = ForestTrainer(session, data, p).train(T_, {"v0": None, "v1": early.get("yf", y.float())}, weights)
     return forest, data.d
 
 

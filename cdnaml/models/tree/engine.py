@@ -73,6 +73,9 @@ SUB_HIST = __import__("os").environ.get("CDNAML_SUB_HIST", "0") != "0"
 # all-gathered (a few hundred bytes).  Once a fit switches a tree pass over, its later levels stay
 # reduce-scattered (sibling subtraction needs the parent's slice).  GBDT at max_bin=256, d=100: levels >= 5.
 RS_MIN_BYTES = int(__import__("os").environ.get("CDNAML_RS_MIN_BYTES", str(4 << 20)))
+# numeric regression levels on row records: decode the split decisions into partition tables on the device and
+# queue the partition before the decisions reach the host (no idle device -> host -> device round trip per level)
+DEVICE_DECODE = __import__("os").environ.get("CDNAML_DEVICE_DECODE", "1") != "0"
 
 
 @dataclass
@@ -746,7 +749,8 @@ class ForestTrainer:
     def _nthr_dev(self, dev):
         t = getattr(self, "_nthr_t", None)
         if t is None:
-            t = self._nthr_t = torch.from_numpy(np.asarray(self.data.nthr, dtype=np.int32)).to(dev)
+            t, = K.upload(dev, np.asarray(self.data.nthr, dtype=np.int32))  # async (a pageable copy drains the queue)
+            self._nthr_t = t
         return t
 
     def _best_splits(self, H: torch.Tensor, tot: torch.Tensor, masks: torch.Tensor, nthr_np=None):
@@ -853,6 +857,26 @@ class ForestTrainer:
         lstats = left[ar, bf, bb]
         rstats = right[ar, bf, bb]
         return bgain, bf, bb, lstats, rstats, order, cat_feats, None
+
+    # ------------------------------------------------------------ device-side split decode
+    def _device_decode_ok(self, dev, use_codes: bool, missing_right: bool) -> bool:
+        return (DEVICE_DECODE and dev.type == "cuda" and use_codes and not self.data.categorical and
+                not self.classification and self.stats_k == 2)
+
+    @staticmethod
+    def _check_decode(dec, split_feat, split_bin, cat_off, cat_masks, child, n_tree, T):
+        """Checked build: the device decode equals the host decode the forest was built from (bin sets compared
+        by content: the host numbers them densely, the device by node)."""
+        tfn = np.searchsorted(n_tree, np.arange(T), side="left").astype(np.int32)
+        got = {k: v.cpu().numpy() for k, v in dec.items()}
+        sp = split_feat >= 0
+        ok = (np.array_equal(got["split_feat"], split_feat) and np.array_equal(got["split_bin"][sp], split_bin[sp])
+              and np.array_equal(got["child"], child) and np.array_equal(got["tfirst_next"], tfn)
+              and np.array_equal(got["cat_off"] >= 0, cat_off >= 0))
+        for a in np.nonzero(cat_off >= 0)[0]:
+            ok = ok and np.array_equal(got["masks"][a].view(np.uint32), np.asarray(cat_masks[cat_off[a]], np.uint32))
+        if not ok:
+            raise RuntimeError("device split decode differs from the host decode")
 
     # ------------------------------------------------------------ reduce-scatter by feature
     def _rs_want(self, Hb: torch.Tensor, rs_on: bool, sub_feats) -> bool:
@@ -1164,6 +1188,7 @@ class ForestTrainer:
                 H = Hb
             masks_t = K.upload(dev, masks_np.view(np.int32))[0] if masks_np is not None else None
             catm_h = None  # left-category bit masks of the native categorical scan
+            dec = None     # device-decoded partition tables (partition already queued)
             if rs_slice is not None or self._native_split(dev):
                 # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
                 mb = p.impurity == "xgb" and self.data.missing_bin
@@ -1175,10 +1200,33 @@ class ForestTrainer:
                     so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
                                            p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight,
                                            missing_bin=mb)
+                dec = None
+                host_p = None
+                if self._device_decode_ok(dev, use_codes, mb) and depth + 1 < p.max_depth:
+                    # the decisions leave for the host first (pinned, async): they arrive while the partition runs
+                    src = torch.cat([so, tot], 1) if depth == 0 else so
+                    host_p = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+                    host_p.copy_(src, non_blocking=True)
+                    host_ev = torch.cuda.Event()
+                    host_ev.record(torch.cuda.current_stream(dev))
+                    # the partition tables decoded on the device and the row partition queued right behind K6:
+                    # the GPU partitions while the decisions travel to the host and the host builds the forest
+                    # and the next level's layout (the same decode on the host, checked in the checked build)
+                    a_tree_d, tf_d = K.upload(dev, a_tree.astype(np.int32), tfirst.numpy().astype(np.int32))
+                    dec = K.split_decode(so, tot, a_tree_d, T, p.min_instances, p.min_info_gain,
+                                         depth < p.max_depth, depth + 1 >= p.max_depth, missing_bin=mb)
+                    with _tr.span("tree.partition", depth=depth):
+                        K.partition_codes(data.bins, codes, tf_d, dec["tfirst_next"], dec["split_feat"],
+                                          dec["split_bin"], dec["cat_off"], dec["masks"].reshape(-1), dec["child"],
+                                          bins_rm=data.row_major_bins() if PARTITION_RM else None)
                 # so [A, 8] = gain, feature, bin, left (2), right (2), missing-goes-right: copied to the host as is
                 # (plus the node totals at level 0), no per-column device ops
                 sw = so.shape[1]
-                host = (torch.cat([so, tot], 1) if depth == 0 else so).cpu().numpy()
+                if host_p is not None:
+                    host_ev.synchronize()
+                    host = host_p.numpy()
+                else:
+                    host = (torch.cat([so, tot], 1) if depth == 0 else so).cpu().numpy()
                 gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
                 lst_h, rst_h = host[:, 3:5], host[:, 5:7]
                 mr_h = host[:, 7] > 0.5 if mb else None
@@ -1308,6 +1356,9 @@ class ForestTrainer:
                         perm, v0p, v1p, wp, segs = K.seg_partition(data.bins, perm, v0p, v1p, wp, segs, split_feat,
                                                                     split_bin, cat_off, cm.reshape(-1), child,
                                                                     len(nl))
+                    elif use_codes and dec is not None:
+                        if K._lib.DEBUG:
+                            self._check_decode(dec, split_feat, split_bin, cat_off, cat_masks, child, n_tree, T)
                     elif use_codes:
                         tfirst_next = torch.from_numpy(
                             np.searchsorted(n_tree, np.arange(T), side="left").astype(np.int32))

@@ -136,6 +136,9 @@ _SIGS = {
     "cdna_sub_hist_lds_budget": ([], c_int),
     "cdna_split_scan_sub": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_double, c_double, c_void_p, c_void_p,
                              c_void_p], c_int),
+    "cdna_split_decode": ([c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_double, c_int, c_int,
+                           c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+                          c_int),
     "cdna_split_scan_ex": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_void_p,
                             c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double,
@@ -248,6 +251,9 @@ def check(code: int, name: str):
     if code != 0:
         raise RuntimeError(f"native kernel {name} failed with hipError {code}")
     if DEBUG:
+        import torch
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return  # the status read synchronises the device: not allowed inside a HIP graph capture
         for u in _DEBUG_UNITS:
             v = int(getattr(_lib, f"cdna_debug_status_{u}")())
             if v:

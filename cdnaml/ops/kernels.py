@@ -323,10 +323,44 @@ def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int, qmax_bits: int = 
     return float(2.0 ** max(-120, min(100, e)))
 
 
+# Maxima the host needs before a fit's first level (the label's max |v| for the fixed-point scale, the largest
+# bootstrap weight) are reduced on a side stream right after their inputs exist and copied to pinned memory;
+# the fit reads them later without draining the device queue (each .item() there idled the GPU ~0.1 ms).
+class _PendingScalar:
+    def __init__(self, t: torch.Tensor, stream):
+        self.host = torch.empty(1, dtype=t.dtype, pin_memory=True)
+        self.host.copy_(t.reshape(1), non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record(stream)
+
+    def get(self) -> float:
+        self.ev.synchronize()
+        return float(self.host[0])
+
+
+def prefetch_max(t: torch.Tensor, absval: bool = False, stream=None) -> None:
+    """Queue max(t) (max |t|) on ``stream`` (default: current) and attach it to the tensor object itself (never
+    keyed by address: a recycled allocation must not inherit a stale value) for packed_scale_global /
+    codes_init_max, which then read it instead of syncing."""
+    if not t.is_cuda or t.numel() == 0:
+        return
+    st = stream if stream is not None else torch.cuda.current_stream(t.device)
+    with torch.cuda.stream(st):
+        m = (t.abs() if absval else t).max()
+        setattr(t, "_cdna_absmax" if absval else "_cdna_max", _PendingScalar(m, st))
+
+
+def _prefetched(t: torch.Tensor, absval: bool) -> Optional[float]:
+    p = getattr(t, "_cdna_absmax" if absval else "_cdna_max", None)
+    return None if p is None else p.get()
+
+
 def packed_scale_global(v: torch.Tensor, comm) -> float:
     """``_packed_scale`` from the max |v| over all ranks: every rank quantises identically, so integer
     histograms all-reduce to the same sums whatever the number of GPUs."""
-    m = float(v.abs().max().item()) if v.numel() else 0.0
+    m = _prefetched(v, True) if v.numel() else 0.0
+    if m is None:
+        m = float(v.abs().max().item())
     m = comm.all_reduce_scalar(m, "max") if comm is not None else m
     if not math.isfinite(m):
         raise ValueError("histogram statistic contains NaN/Inf")
@@ -553,9 +587,10 @@ def codes_init_max(weights: Optional[torch.Tensor], T: int, n: int, device):
             and weights.data_ptr() % 16 == 0:
         codes = torch.empty((T, n), dtype=torch.int16, device=weights.device)
         wm = torch.zeros(1, dtype=torch.int32, device=weights.device)
+        pre = _prefetched(weights, False)
         _lib.check(_lib.lib().cdna_codes_init(_ptr(weights), T * n, _ptr(codes), _ptr(wm), _stream(weights.device)),
                    "cdna_codes_init")
-        return codes, max(1, int(wm.item()))
+        return codes, max(1, int(pre if pre is not None else wm.item()))
     if weights is None:
         # every row in every tree with weight 1 at the root (local node 0): one fill, no elementwise chain
         return torch.full((T, n), 1 << 8, dtype=torch.int16, device=device), 1
@@ -1708,6 +1743,27 @@ def split_scan(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor
                                           float(reg_lambda), float(gamma), float(min_child_weight), _ptr(out),
                                           _ptr(tot), _stream(H.device)), "cdna_split_scan")
     return out, tot
+
+
+def split_decode(so: torch.Tensor, tot: torch.Tensor, a_tree: torch.Tensor, T: int, min_inst: float,
+                 min_gain: float, can_level: bool, leaf_children: bool, missing_bin: bool = False):
+    """K6 decisions [A, >= 7] + node totals -> partition tables on the device (split.hip split_decode_kernel):
+    split_feat / split_bin / cat_off [A], masks [A, 8] (bin sets of missing-right splits, cat_off[a] = a),
+    child [2A], tfirst_next [T] (int32), the host decode's exact twin."""
+    A = so.shape[0]
+    dev = so.device
+    out = torch.empty(15 * A + T, dtype=torch.int32, device=dev)
+    sf, sb, co = out[:A], out[A:2 * A], out[2 * A:3 * A]
+    child, pref, tfn = out[3 * A:5 * A], out[5 * A:7 * A], out[7 * A:7 * A + T]
+    masks = out[7 * A + T:15 * A + T]
+    sc, tc = so.contiguous(), tot.contiguous()
+    _lib.check(_lib.lib().cdna_split_decode(_ptr(sc), sc.shape[1], _ptr(tc), tc.shape[1], _ptr(a_tree), A, T,
+                                            float(min_inst), float(min_gain), int(bool(can_level)),
+                                            int(bool(leaf_children)), int(bool(missing_bin)), _ptr(sf), _ptr(sb),
+                                            _ptr(co), _ptr(masks), _ptr(child), _ptr(pref), _ptr(tfn), _stream(dev)),
+               "cdna_split_decode")
+    return {"split_feat": sf, "split_bin": sb, "cat_off": co, "masks": masks.view(A, 8), "child": child,
+            "tfirst_next": tfn}
 
 
 def split_scan_ex(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor], kind: str, min_inst: float):

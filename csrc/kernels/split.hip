@@ -600,3 +600,107 @@ CDNA_API int cdna_split_scan_ex(const double* H, const int* nthr, const uint32_t
   hipLaunchKernelGGL(split_scan_ex_kernel, dim3((unsigned)A), dim3(128), 0, st, a);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------- split_decode
+// The level's split decisions turned into the partition tables on the device, so the row partition can be
+// launched right behind K6 while the decisions travel to the host (the host's copy of the same decode builds the
+// forest and the next level's layout in the meantime, instead of the GPU idling through a device -> host ->
+// device round trip at every level).  Numeric splits only (no categorical sets, no missing-value direction).
+//   can[a]        = gain finite, > 0, >= min_gain, node weight >= 2 min_inst, and the level may split
+//   split_feat[a] = can ? feature : -1;  split_bin[a] = can ? bin : 0;  cat_off[a] = -1
+//   child[2a + s] = index among the active children (in (node, side) order) or -1 (leaf / no split), a child
+//                   being active when its weight >= 2 min_inst and the next level is not the last
+//   tfirst_next[t]= active children of the trees before t (nodes are ordered by tree)
+namespace {
+
+__global__ __launch_bounds__(1024) void split_decode_kernel(const double* __restrict__ so, int sw,
+                                                            const double* __restrict__ tot, int tw,
+                                                            const int* __restrict__ a_tree, int A, int T,
+                                                            double min_inst, double min_gain, int can_level,
+                                                            int leaf_children, int missing_bin,
+                                                            int* __restrict__ split_feat,
+                                                            int* __restrict__ split_bin, int* __restrict__ cat_off,
+                                                            uint32_t* __restrict__ masks,
+                                                            int* __restrict__ child, int* __restrict__ pref,
+                                                            int* __restrict__ tfirst_next) {
+  __shared__ int s_wave[16];
+  __shared__ int s_carry;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (int base = 0; base < 2 * A; base += 1024) {
+    const int e = base + threadIdx.x;
+    int flag = 0;
+    if (e < 2 * A) {
+      const int a = e >> 1, s = e & 1;
+      const double g = so[(int64_t)a * sw];
+      const double W = tot[(int64_t)a * tw];
+      const bool can = can_level && g == g && g != __builtin_inf() && g > 0.0 && g >= min_gain && W >= 2.0 * min_inst;
+      if (s == 0) {
+        const int b = (int)so[(int64_t)a * sw + 2];
+        // XGBoost's missing-right splits (bin 0 = missing goes right): the left side is the bin set 1..b
+        const bool mr = can && missing_bin && sw >= 8 && so[(int64_t)a * sw + 7] > 0.5;
+        split_feat[a] = can ? (int)so[(int64_t)a * sw + 1] : -1;
+        split_bin[a] = can && !mr ? b : 0;
+        cat_off[a] = mr ? a : -1;
+        if (mr)
+          for (int w = 0; w < 8; ++w) {
+            uint32_t m = 0u;
+            for (int j = 0; j < 32; ++j) {
+              const int c = 32 * w + j;
+              if (c >= 1 && c <= b) m |= 1u << j;
+            }
+            masks[(int64_t)a * 8 + w] = m;
+          }
+      }
+      const double cw = so[(int64_t)a * sw + (s == 0 ? 3 : 5)];
+      flag = (can && !(cw < 2.0 * min_inst) && !leaf_children) ? 1 : 0;
+    }
+    // block exclusive scan of the flags
+    const uint64_t m = __builtin_amdgcn_ballot_w64(flag != 0);
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) s_wave[wid] = __builtin_popcountll(m);
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int w = 0; w < 16; ++w) {
+      before += w < wid ? s_wave[w] : 0;
+      total += s_wave[w];
+    }
+    const int ex = s_carry + before + below;
+    if (e < 2 * A) {
+      child[e] = flag ? ex : -1;
+      pref[e] = ex;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += total;
+    __syncthreads();
+  }
+  // the first active node of tree t starts its children at pref[2 * a]; trees without active nodes start where the
+  // next tree does
+  const int total_children = s_carry;
+  for (int t = threadIdx.x; t < T; t += 1024) {
+    int lo = 0, hi = A;  // first a with a_tree[a] >= t
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (a_tree[mid] < t) lo = mid + 1;
+      else hi = mid;
+    }
+    tfirst_next[t] = lo < A ? pref[2 * lo] : total_children;
+  }
+}
+
+}  // namespace
+
+// so [A][sw] (gain, feature, bin, left0, left1, right0, right1, ...), tot [A][tw]; pref: [2A] int scratch.
+// masks: [A][8] bin sets of missing-right splits (cat_off[a] = a), written only for those nodes.
+CDNA_API int cdna_split_decode(const double* so, int sw, const double* tot, int tw, const int* a_tree, int A, int T,
+                               double min_inst, double min_gain, int can_level, int leaf_children, int missing_bin,
+                               int* split_feat, int* split_bin, int* cat_off, uint32_t* masks, int* child, int* pref,
+                               int* tfirst_next, hipStream_t st) {
+  if (A <= 0 || T <= 0) return 0;
+  if (sw < 7 || tw < 1 || (missing_bin && sw < 8)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(split_decode_kernel, dim3(1), dim3(1024), 0, st, so, sw, tot, tw, a_tree, A, T, min_inst,
+                     min_gain, can_level, leaf_children, missing_bin, split_feat, split_bin, cat_off, masks, child,
+                     pref, tfirst_next);
+  return (int)hipGetLastError();
+}
