@@ -165,30 +165,36 @@ class LinearRegression(Estimator):
         comm = dataset._session.comm
         d = X.shape[1]
         fit_int = self.getFitIntercept()
-        # common shift (global mean of per-rank leading samples) keeps the f32 Gram well conditioned
+        # common shift (global mean of per-rank leading samples) keeps the f32 Gram well conditioned; it stays on
+        # the device (the label shift is applied to y there), so the fit reads the host once, for the Gram
+        bf16 = self.getGramPrecision() == "bf16"
+        sh = None
         if fit_int:
             k = min(X.shape[0], 4096)
-            sh = torch.cat([X[:k].double().mean(0) if k else torch.zeros(d, dtype=torch.float64, device=X.device),
-                            torch.tensor([y[:k].mean().item() if k else 0.0], dtype=torch.float64,
-                                         device=X.device)])
-            cnt = torch.tensor([1.0 if k else 0.0], dtype=torch.float64, device=X.device)
+            sh = torch.cat([X[:k].double().mean(0), y[:k].double().mean().reshape(1)]) if k else \
+                torch.zeros(d + 1, dtype=torch.float64, device=X.device)
+            cnt = torch.full((1,), 1.0 if k else 0.0, dtype=torch.float64, device=X.device)
             comm.all_reduce_many([sh, cnt])
-            sh = sh / max(float(cnt), 1.0)
-            shift, yshift = sh[:d].float(), float(sh[d])
+            sh = sh / cnt.clamp_min(1.0)
+            shift, yc = sh[:d].float(), y - sh[d]
         else:
-            shift, yshift = None, 0.0
+            shift, yc = None, y
         if w is None:
-            G = K.gram(X, y, shift, yshift, bf16=self.getGramPrecision() == "bf16") if X.shape[0] else \
+            G = K.gram(X, yc, shift, 0.0, bf16=bf16) if X.shape[0] else \
                 torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
         else:
-            A = torch.empty((X.shape[0], d + 2), dtype=torch.float64, device=X.device)
-            A[:, :d] = X.double() - (shift.double() if shift is not None else 0)
-            A[:, d] = 1.0
-            A[:, d + 1] = y - yshift
-            A = A * torch.sqrt(w)[:, None]
-            G = A.T @ A
+            # weighted Gram on K1 too: rows scaled by sqrt(w), with sqrt(w) itself as an extra feature column,
+            # so [X' | sqrt(w) | 1 | y']^T [...] holds sum w x x^T, sum w x, sum w and the y blocks
+            sw = torch.sqrt(w).float()[:, None]
+            Xw = torch.cat([(X.float() - (shift if shift is not None else 0.0)) * sw, sw], 1)
+            G3 = K.gram(Xw, (yc.float() * sw[:, 0]), None, 0.0, bf16=bf16) if X.shape[0] else \
+                torch.zeros((d + 3, d + 3), dtype=torch.float64, device=X.device)
+            keep = torch.tensor(list(range(d + 1)) + [d + 2], device=X.device)
+            G = G3[keep][:, keep].contiguous()
         comm.all_reduce(G)
-        G = G.cpu().numpy()
+        host = torch.cat([G.reshape(-1), sh if sh is not None else G.new_zeros(d + 1)]).cpu().numpy()
+        G = host[:(d + 2) * (d + 2)].reshape(d + 2, d + 2)
+        yshift = float(host[-1]) if fit_int else 0.0
         coef, intercept, hist, iters, stderr = self._solve(G, d, shift, yshift)
         model = LinearRegressionModel(coef, intercept)
         model._post_fit(self)

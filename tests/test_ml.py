@@ -43,6 +43,22 @@ def test_linear_regression_matches_sklearn(spark):
     assert rmse < 0.12 and r2 > 0.999
 
 
+def test_weighted_linear_regression_matches_sklearn(spark):
+    """weightCol: the weighted normal equations (K1 Gram over sqrt(w)-scaled rows with sqrt(w) as an extra
+    column on the GPU) equal sklearn's sample_weight fit."""
+    from sklearn.linear_model import LinearRegression as SkLR
+    df, X, y = _reg_frame(spark, n=4000, seed=3, noise=0.5)
+    wts = np.random.default_rng(4).integers(1, 6, len(y)).astype(float)
+    pdf = df.toPandas()
+    pdf["w"] = wts
+    va = VectorAssembler(inputCols=[f"x{i}" for i in range(5)], outputCol="features")
+    m = LinearRegression(featuresCol="features", labelCol="label", weightCol="w").fit(
+        va.transform(spark.createDataFrame(pdf)))
+    sk = SkLR().fit(X, y, sample_weight=wts)
+    np.testing.assert_allclose(m.coefficients.toArray(), sk.coef_, rtol=2e-5, atol=2e-6)
+    assert abs(m.intercept - sk.intercept_) < 2e-5
+
+
 def test_lr_on_non_vector_column_fails(spark):
     """ML 02:80-89: estimators need a vector features column."""
     df, _, _ = _reg_frame(spark, n=100)

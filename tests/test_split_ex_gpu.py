@@ -116,3 +116,28 @@ def test_forests_native_ex_equal_torch_path(dev, flow, monkeypatch):
         m = est.fit(df)
         digests.append(forest_digest(m._forest))
     assert digests[0] == digests[1]
+
+
+@pytest.mark.parametrize("model", ["rf", "gbt", "xgb_missing"])
+def test_device_split_decode_forests_identical(dev, model, monkeypatch):
+    """The partition tables decoded on the device (split.hip split_decode_kernel, partition queued before the
+    decisions reach the host) give the forests of the host decode bit for bit: numeric RF / GBT splits and
+    XGBoost's missing-right bin sets."""
+    import cdnaml
+    from cdnaml.models.tree import engine
+    from cdnaml.utils.synthetic import forest_digest, regression_shard
+    from cdnaml.ml.regression import GBTRegressor, RandomForestRegressor
+    from cdnaml.ml.xgboost import XgboostRegressor
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    X, y, _ = regression_shard(200_000, 30, 7, 0, 1, dev)
+    if model == "xgb_missing":
+        X = torch.where(X > 1.2, torch.zeros_like(X), X)     # zeros = missing values
+    df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
+    est = {"rf": RandomForestRegressor(numTrees=16, maxDepth=6, maxBins=32, seed=3),
+           "gbt": GBTRegressor(maxIter=4, maxDepth=5, seed=1),
+           "xgb_missing": XgboostRegressor(n_estimators=4, max_depth=6, missing=0.0, random_state=2)}[model]
+    digests = []
+    for flag in (True, False):
+        monkeypatch.setattr(engine, "DEVICE_DECODE", flag)
+        digests.append(forest_digest(est.fit(df)._forest))
+    assert digests[0] == digests[1]
