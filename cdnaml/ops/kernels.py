@@ -1035,7 +1035,7 @@ def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_glob
     return (_fixed_scale(m[0:1], n_global, w, qmax_bits=30), _fixed_scale(m[1:2], n_global, w, qmax_bits=30))
 
 
-SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "1024"))
+SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "2048"))
 # record histograms through the lane-feature kernel (seg_hist_lane_kernel: lanes own features, bin-major
 # conflict-free LDS planes, one v_perm per cell address); B <= 80 (4 planes <= 80 KB of LDS), 80 < B <= 256:
 # seg_hist_lane4_kernel (64 features per block, a quarter-wave per item; CDNAML_SEG_WIDE=0 keeps the flat kernel)
@@ -1045,11 +1045,14 @@ SEG_LANE_MAX_B = 256 if __import__("os").environ.get("CDNAML_SEG_WIDE", "1") != 
 REC_PAD = 64
 
 
-def _fill_chunk(segs: np.ndarray, chunk: int) -> int:
+def _fill_chunk(segs: np.ndarray, chunk: int, B: int = 0) -> int:
     """Shrink the rows-per-block chunk so a level with few rows still launches ~SEG_MIN_BLOCKS blocks
-    (at 1.25e7 rows per GPU a level's 95K-row chunks made only ~100 blocks for 256 CUs)."""
+    (at 1.25e7 rows per GPU a level's 95K-row chunks made only ~100 blocks for 256 CUs).  With 2048 instead of
+    1024 the per-rank shape of the 8-GPU point ran 22.6 -> 21.2 ms (the last round of blocks no longer idles
+    half the chip); wide-bin levels (B > 64: 128 KB LDS planes to clear and flush per block) keep 1024."""
     total = int(np.asarray(segs, dtype=np.int64).reshape(-1, 3)[:, 1].clip(min=0).sum())
-    return int(min(chunk, max(8192, -(-total // max(1, SEG_MIN_BLOCKS)))))
+    mb = SEG_MIN_BLOCKS if B <= 64 else min(SEG_MIN_BLOCKS, 1024)
+    return int(min(chunk, max(8192, -(-total // max(1, mb)))))
 
 
 def _seg_work(segs: np.ndarray, chunk: int) -> np.ndarray:
@@ -1160,7 +1163,7 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
     else:
         assert bins_rm is not None and rec.dtype == torch.int64
         wm = int(max(1, min(255, wmax)))
-        chunk = _fill_chunk(segs, min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1)))
+        chunk = _fill_chunk(segs, min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1)), B)
         work = _seg_work(segs, chunk)
         if len(work) == 0:
             if out is not None:
@@ -1214,7 +1217,7 @@ def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optio
         iout = _int_hist_cpu(bins, d, B, S, rows, slot, a0, a1)
     else:
         chunk = SEG_HIST_CHUNK if not packed else min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1))
-        chunk = _fill_chunk(segs, chunk)
+        chunk = _fill_chunk(segs, chunk, B)
         work = _seg_work(segs, chunk)
         if len(work) == 0:
             return zero()
