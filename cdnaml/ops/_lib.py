@@ -28,7 +28,7 @@ _OUT_DIR = os.path.join(_ROOT, "cdnaml", "_native")
 DEBUG = os.environ.get("CDNAML_HIP_DEBUG", "0") not in ("", "0")
 LIB_PATH = os.path.join(_OUT_DIR, "libcdnaml_hip_debug.so" if DEBUG else "libcdnaml_hip.so")
 ARCH = os.environ.get("CDNAML_OFFLOAD_ARCH", "gfx950")
-_DEBUG_UNITS = ("seg", "hist5", "trees", "hashagg")
+_DEBUG_UNITS = ("seg", "hist5", "trees", "hashagg", "relational")
 
 _lock = threading.Lock()
 _lib = None
@@ -172,7 +172,7 @@ _SIGS = {
                         c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_bucket_compact": ([c_int, c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
-    "cdna_gather": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_gather": ([c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_join_build_dense": ([c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],
                               c_int),
     "cdna_join_probe_dense": ([c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,

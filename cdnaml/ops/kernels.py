@@ -1830,8 +1830,8 @@ def gather_cols(tensors, idx: torch.Tensor):
         src = [tensors[i] for i in grp]
         dst = [torch.empty(m, dtype=t.dtype, device=t.device) for t in src]
         eb = (ctypes.c_int * len(grp))(*[t.element_size() for t in src])
-        _lib.check(_lib.lib().cdna_gather(_ptr(ix), m, len(grp), _ptr_array(src), _ptr_array(dst), eb,
-                                          _stream(ix.device)), "cdna_gather")
+        _lib.check(_lib.lib().cdna_gather(_ptr(ix), m, min(int(t.shape[0]) for t in src), len(grp), _ptr_array(src),
+                                          _ptr_array(dst), eb, _stream(ix.device)), "cdna_gather")
         for i, d in zip(grp, dst):
             out[i] = d
     return out

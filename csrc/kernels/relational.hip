@@ -184,6 +184,7 @@ constexpr int kMaxGather = 8;
 struct GatherArgs {
   const int64_t* idx;
   int64_t m;
+  int64_t nsrc;  // source rows: an index outside [0, nsrc) reads nothing and writes 0 (never a wild load)
   int nc;
   const void* src[kMaxGather];
   void* dst[kMaxGather];
@@ -208,7 +209,13 @@ __global__ __launch_bounds__(kThreads) void gather_kernel(const GatherArgs a) {
   for (int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x; i0 < a.m; i0 += stride * U) {
     int64_t j[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) j[u] = i0 + u * stride < a.m ? a.idx[i0 + u * stride] : -1;
+    for (int u = 0; u < U; ++u) {
+      j[u] = i0 + u * stride < a.m ? a.idx[i0 + u * stride] : -1;
+      if (j[u] >= a.nsrc) {  // always clamped; the checked build also reports it
+        (void)CDNA_DCHECK(false, 0xC019u);
+        j[u] = -1;
+      }
+    }
     for (int c = 0; c < a.nc; ++c) {
       switch (a.eb[c]) {
         case 1: gcols<uint8_t, U>(a.src[c], a.dst[c], j, i0, stride, a.m); break;
@@ -221,6 +228,8 @@ __global__ __launch_bounds__(kThreads) void gather_kernel(const GatherArgs a) {
 }
 
 }  // namespace
+
+CDNA_DEBUG_EXPORT(relational)
 
 // dtype: 0 = f32, 1 = f64.  part: [nblk][d][5] (count, mean, M2, min, max); nblk = ceil(n / rows_per_block).
 CDNA_API int cdna_col_moments(int dtype, const void* X, int64_t n, int d, int64_t ldx, const uint8_t* valid,
@@ -268,13 +277,14 @@ CDNA_API int cdna_compact_mask(int pass, const uint8_t* mask, int64_t n, int64_t
   return (int)hipGetLastError();
 }
 
-CDNA_API int cdna_gather(const int64_t* idx, int64_t m, int nc, const void* const* src, void* const* dst,
-                         const int* eb, hipStream_t st) {
+CDNA_API int cdna_gather(const int64_t* idx, int64_t m, int64_t nsrc, int nc, const void* const* src,
+                         void* const* dst, const int* eb, hipStream_t st) {
   if (m <= 0 || nc <= 0) return 0;
   if (nc > kMaxGather) return (int)hipErrorInvalidValue;
   GatherArgs a{};
   a.idx = idx;
   a.m = m;
+  a.nsrc = nsrc;
   a.nc = nc;
   for (int c = 0; c < nc; ++c) {
     if (eb[c] != 1 && eb[c] != 2 && eb[c] != 4 && eb[c] != 8) return (int)hipErrorInvalidValue;
