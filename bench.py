@@ -137,6 +137,7 @@ def main():
                        "global_batch": n_total, "seq_len": None, "num_features": d,
                        "parallelism": f"dp{W}"},
         }), flush=True)
+    comm.shutdown()
 
 
 if __name__ == "__main__":

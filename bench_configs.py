@@ -143,7 +143,9 @@ def bench_infer(spark, args):
     --mode host (default): chunks come from pinned host memory through ``createDataFrameFromChunks``
     (pinned double buffers, H2D on a copy stream overlapping the predict; the H2D of all 400 GB is in the
     timed region).  The host pool holds --pool distinct chunks, cycled (host RAM cannot hold 400 GB).
-    --mode device: chunks are two device-resident buffers cycled through ``device_chunks`` (predict-bound).
+    --mode device: every chunk is generated on the device (``K.normal32_``: Philox normals keyed by global row
+    id, one HBM write per element) into two staging buffers of ``device_chunks``: 1e9 distinct rows, with
+    their generation inside the timed region.
     In both modes the forest is uploaded once and each staging buffer's predict is a replayed HIP graph."""
     from cdnaml.models.inference import device_chunks
     from cdnaml.models.regression import RandomForestRegressor
@@ -169,13 +171,13 @@ def bench_infer(spark, args):
                 yield {"features": pool[i % len(pool)]}
         df = spark.createDataFrameFromChunks(chunks, chunk)
     else:
-        filled = [False, False]
+        from cdnaml.ops import kernels as K
+        row_base = comm.rank * n_chunks * chunk
 
         def make(r0, n, bufs):
-            slot = (r0 // chunk) & 1
-            if not filled[slot]:
-                bufs["features"][:n].copy_(torch.randn((n, 100), generator=g, dtype=torch.float32, device=dev))
-                filled[slot] = True
+            # every chunk is new data: rows keyed by global row id (Philox normals written straight into the
+            # staging buffer on the compute stream), so the 1e9 rows are distinct and their generation is timed
+            K.normal32_(bufs["features"][:n], 7, (row_base + r0) * 100, 0x10)
         df = device_chunks(spark, n_chunks * chunk, chunk, make, {"features": ((100,), torch.float32)})
     pred = model.transform(df)
     acc = torch.zeros((), dtype=torch.float64, device=dev)
@@ -188,11 +190,17 @@ def bench_infer(spark, args):
         pred.foreachBatch(consume)
         return acc
     ms, tot = _timed(spark, step, args.steps, args.warmup)
+    if args.mode == "device" and dev.type == "cuda":
+        scratch = {"features": torch.empty((chunk, 100), dtype=torch.float32, device=dev)}
+        gen_ms, _ = _timed(spark, lambda: [make(i * chunk, chunk, scratch) for i in range(n_chunks)], 2, 1)
+        del scratch
+        _log(f"generation alone: {gen_ms:.1f} ms ({n_chunks * chunk * 400 / gen_ms / 1e9:.2f} TB/s written)")
     from cdnaml.models.inference import predictor_for
     pr = predictor_for(model, "value", [0.0])
     _log(f"inference {rows:.3e} rows in {ms:.1f} ms (mode={args.mode}); graph captures={pr.captures} "
          f"replays={pr.replays}; mean prediction {float(tot) / (n_chunks * chunk):.4f}")
-    src = "pinned host chunks, H2D in the timed region" if args.mode == "host" else "device-resident chunks"
+    src = "pinned host chunks, H2D in the timed region" if args.mode == "host" else \
+        "distinct rows generated on device per chunk, generation in the timed region"
     _emit(spark, f"rows/sec batch inference via DataFrame transform, RandomForest (20 trees, depth 5), 1e9 rows "
                  f"({src})", rows / (ms / 1e3), "rows/s", args.steps, args.warmup, ms, True,
           "weak" if comm.world_size > 1 else "strong", "fp32",
@@ -310,6 +318,7 @@ def main():
     {"lr": bench_lr, "cv": bench_cv, "gbdt": bench_gbdt, "infer": bench_infer, "airbnb": bench_airbnb,
      "relational": bench_relational, "expr": bench_expr}[
         args.config](spark, args)
+    spark.comm.shutdown()
 
 
 if __name__ == "__main__":

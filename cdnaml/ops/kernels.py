@@ -112,6 +112,20 @@ def uniform(n: int, seed: int, offset: int = 0, stream: int = 0, device=None) ->
     return torch.from_numpy(_philox.uniform(n, seed, int(offset), int(stream)))
 
 
+def normal32_(out: torch.Tensor, seed: int, offset: int = 0, stream: int = 0) -> torch.Tensor:
+    """Fill the contiguous fp32 tensor ``out`` with standard normals for global elements offset..offset+numel-1
+    (Philox quads, Box-Muller; ``normal_f32_kernel``).  CPU: the numpy oracle ``philox.normal32``."""
+    if out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("normal32_ needs a contiguous float32 tensor")
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    if out.is_cuda:
+        _lib.check(_lib.lib().cdna_normal_f32(_ptr(out), out.numel(), seed, int(offset), int(stream) & 0xFFFFFFFF,
+                                              _stream(out.device)), "cdna_normal_f32")
+        return out
+    out.view(-1).copy_(torch.from_numpy(_philox.normal32(out.numel(), seed, int(offset), int(stream))))
+    return out
+
+
 def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=None) -> torch.Tensor:
     """uint8 [T, n] Poisson(rate) bootstrap multiplicities, tree t on stream 0x100+t."""
     device = torch.device(device) if device is not None else torch.device("cpu")

@@ -84,6 +84,28 @@ def uniform32(n: int, seed: int, offset: int = 0, stream: int = 0) -> np.ndarray
     return words.astype(np.float64) * (1.0 / 4294967296.0)
 
 
+def normal32(n: int, seed: int, offset: int = 0, stream: int = 0) -> np.ndarray:
+    """fp32 standard normals for elements offset..offset+n-1, the layout of ``normal_f32_kernel`` (misc.hip):
+    quad q = index >> 2, words (0, 1) and (2, 3) are Box-Muller pairs (r cos, r sin), u = (w + 1/2) 2^-32.
+    Computed in float64 here; the kernel's hardware log/sin/cos agree to ~1e-6 relative."""
+    seed &= 0xFFFFFFFFFFFFFFFF
+    if n <= 0:
+        return np.zeros(0, dtype=np.float32)
+    q0, q1 = offset >> 2, (offset + n - 1) >> 2
+    q = np.arange(q0, q1 + 1, dtype=np.uint64)
+    lo = (q & _MASK32).astype(np.uint32)
+    hi = (q >> np.uint64(32)).astype(np.uint32)
+    w = [(x.astype(np.float64) + 0.5) * (1.0 / 4294967296.0)
+         for x in philox4x32_10(lo, hi, np.uint32(stream & 0xFFFFFFFF), np.uint32(0x4E0A), seed & 0xFFFFFFFF,
+                                seed >> 32)]
+    z = np.empty((len(q), 4))
+    for p in range(2):
+        rad = np.sqrt(-2.0 * np.log(w[2 * p]))
+        th = 2.0 * np.pi * w[2 * p + 1]
+        z[:, 2 * p], z[:, 2 * p + 1] = rad * np.cos(th), rad * np.sin(th)
+    return z.reshape(-1)[offset - 4 * q0: offset - 4 * q0 + n].astype(np.float32)
+
+
 def poisson(T: int, n: int, seed: int, offset: int, rate: float) -> np.ndarray:
     out = np.empty((T, n), dtype=np.uint8)
     for t in range(T):

@@ -121,6 +121,18 @@ class Comm:
                 pass
             self.initialized = False
 
+    def shutdown(self) -> None:
+        """Orderly end of a distributed job: every rank reaches a barrier, then tears its process group down.
+
+        Left to interpreter exit, the group's destructors run in whatever order the ranks happen to exit; a
+        gloo rank whose peers already closed their sockets can then abort (SIGABRT) after the job's work is
+        done, which turns a finished run into a failed launch."""
+        if self.initialized and dist.is_initialized():
+            if self.world_size > 1:
+                self.barrier()
+            dist.destroy_process_group()
+            self.initialized = False
+
     # ----------------------------------------------------------------- info
     @property
     def distributed(self) -> bool:

@@ -17,6 +17,43 @@ __global__ void uniform_kernel(double* __restrict__ out, int64_t n, uint64_t see
     out[i] = cdna::philox_uniform(seed, offset + (uint64_t)i, stream);
 }
 
+// fp32 standard normals for elements offset..offset+n-1 (global element index
+// e = row * d + feature, so a table is the same however it is chunked or
+// sharded).  One Philox4x32-10 call per quad q = e >> 2 gives two Box-Muller
+// pairs: words (0, 1) -> elements 4q, 4q+1 (r cos, r sin), words (2, 3) ->
+// 4q+2, 4q+3.  u = (w + 1/2) 2^-32 is never 0 or 1.  Hardware log / sin / cos
+// (v_log_f32, v_sin_f32, v_cos_f32): HBM-write bound, ~4 B per element, with
+// float4 stores when the quad is interior and the output is 16-byte aligned.
+// Oracle: cdnaml/ops/philox.py:normal32.
+__global__ __launch_bounds__(256) void normal_f32_kernel(float* __restrict__ out, int64_t n, uint64_t seed,
+                                                         uint64_t offset, uint32_t stream, int vec) {
+  const uint64_t q0 = offset >> 2, q1 = (offset + (uint64_t)n - 1) >> 2;
+  constexpr float k2pi = 6.28318530717958647692f, kln2 = 0.69314718055994530942f, s32 = 2.3283064365386963e-10f;
+  for (uint64_t q = q0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= q1;
+       q += (uint64_t)gridDim.x * blockDim.x) {
+    const cdna::u32x4 r = cdna::philox4x32_10(cdna::u32x4{(uint32_t)q, (uint32_t)(q >> 32), stream, 0x4E0Au},
+                                              (uint32_t)seed, (uint32_t)(seed >> 32));
+    float z[4];
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const float u1 = ((float)w[2 * p] + 0.5f) * s32, u2 = ((float)w[2 * p + 1] + 0.5f) * s32;
+      const float rad = __fsqrt_rn(-2.f * kln2 * __builtin_amdgcn_logf(u1));
+      const float th = k2pi * u2;
+      z[2 * p] = rad * __cosf(th);
+      z[2 * p + 1] = rad * __sinf(th);
+    }
+    const int64_t i0 = (int64_t)(4 * q) - (int64_t)offset;  // output index of the quad's first element
+    if (vec && i0 >= 0 && i0 + 4 <= n) {
+      *reinterpret_cast<float4*>(out + i0) = float4{z[0], z[1], z[2], z[3]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (i0 + j >= 0 && i0 + j < n) out[i0 + j] = z[j];
+    }
+  }
+}
+
 // Poisson(rate) bootstrap multiplicities for T trees: out[t][i], stream = t + 1
 // (rate >= 1 with no bootstrap is handled on the host as all-ones).
 // The CDF F_0..F_{kCdf-1} of poisson_from_uniform's recurrence is tabulated on
@@ -296,6 +333,16 @@ __global__ __launch_bounds__(256) void logistic_kernel(const float* __restrict__
 CDNA_API int cdna_uniform(double* out, int64_t n, uint64_t seed, uint64_t offset, uint32_t stream, hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(uniform_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, out, n, seed, offset, stream);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_normal_f32(float* out, int64_t n, uint64_t seed, uint64_t offset, uint32_t stream,
+                             hipStream_t st) {
+  if (n <= 0) return 0;
+  const int64_t quads = (int64_t)(((offset + (uint64_t)n - 1) >> 2) - (offset >> 2)) + 1;
+  const int vec = ((uintptr_t)out % 16 == 0) && (offset % 4 == 0);
+  hipLaunchKernelGGL(normal_f32_kernel, dim3(grid_for(quads, 256, 8192)), dim3(256), 0, st, out, n, seed, offset,
+                     stream, vec);
   return (int)hipGetLastError();
 }
 

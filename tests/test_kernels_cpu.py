@@ -30,6 +30,19 @@ def test_uniform_offsets_are_consistent():
     np.testing.assert_array_equal(t.numpy(), a)
 
 
+def test_normal32_is_keyed_by_global_element():
+    """Box-Muller normals from Philox quads: any chunking of the element range gives the same values (the
+    inference bench generates its 1e9 rows chunk by chunk), and the moments are those of N(0, 1)."""
+    a = philox.normal32(200003, seed=5, offset=0, stream=0x10)
+    for off, m in ((0, 7), (1, 10), (3, 4097), (1000, 99003), (200000, 3)):
+        np.testing.assert_array_equal(philox.normal32(m, 5, off, 0x10), a[off:off + m])
+    assert a.dtype == np.float32
+    assert abs(a.mean()) < 0.01 and abs(a.std() - 1.0) < 0.01
+    assert abs((np.abs(a) < 1.0).mean() - 0.6827) < 0.005
+    t = K.normal32_(torch.empty(100, 3), 5, 6, 0x10)
+    np.testing.assert_array_equal(t.reshape(-1).numpy(), a[6:306])
+
+
 def test_poisson_weights_mean():
     w = K.poisson_weights(4, 20000, seed=3, offset=0, rate=1.0)
     assert w.shape == (4, 20000) and w.dtype == torch.uint8

@@ -62,6 +62,18 @@ def test_uniform_bit_identical(dev):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("n,offset,shift", [(100000, 0, 0), (100003, 5, 0), (4097, 2, 1), (3, 7, 0), (1, 0, 3)])
+def test_normal32_matches_host_oracle(dev, n, offset, shift):
+    """float4 stores (aligned output, offset % 4 == 0) and per-element stores (unaligned offset or output
+    pointer) against the float64 host oracle; only the kernel's fp32 u and hardware log/sin/cos differ."""
+    ref = torch.from_numpy(__import__("cdnaml.ops.philox", fromlist=["normal32"]).normal32(n, 9, offset, 0x10))
+    buf = torch.full((n + shift + 1,), 7.0, device=dev)
+    out = K.normal32_(buf[shift:shift + n], 9, offset, 0x10).cpu()
+    assert torch.allclose(out, ref, rtol=2e-4, atol=2e-4)
+    tail = buf.cpu()
+    assert tail[n + shift].item() == 7.0 and (shift == 0 or tail[shift - 1].item() == 7.0)
+
+
 @pytest.mark.parametrize("rate,n,offset", [(1.0, 50000, 1000), (0.63, 50000, 1000), (2.5, 50000, 1000),
                                            (1.0, 50003, 1001), (7.5, 4099, 6)])
 def test_poisson_matches(dev, rate, n, offset):
