@@ -50,6 +50,8 @@ MSEG_T1 = __import__("os").environ.get("CDNAML_MSEG_T1", "1") != "0"
 NATIVE_SPLIT = __import__("os").environ.get("CDNAML_NATIVE_SPLIT", "1") != "0"
 # segment-mode forests carry one packed 8-byte record per gathered row (row | weight | quantised label)
 MSEG_REC = __import__("os").environ.get("CDNAML_MSEG_REC", "1") != "0"
+# level 0 on seg10 rows: root records compacted inside the histogram kernel (no codes_compact pass)
+ROOT_HIST = __import__("os").environ.get("CDNAML_ROOT_HIST", "1") != "0"
 # single-output forests of depth <= 8 predict from a heap layout (8-byte nodes, fixed-step walks)
 HEAP_PREDICT = __import__("os").environ.get("CDNAML_HEAP_PREDICT", "1") != "0"
 # row-record partition gathers split bins from the row-major copy (one line per row) instead of [G][n]
@@ -114,11 +116,23 @@ class BinnedData:
     B: int
     missing_bin: bool = False         # bin 0 holds missing values (XGBoost sparsity-aware splits)
     bins_rm: Optional[torch.Tensor] = None  # lazily built row-major copy [n, G, 8] (segment-mode histograms)
+    bins_s10: Optional[torch.Tensor] = None  # seg10 row layout [n, 16, 8] written by binize (K.bins_seg10)
 
     def row_major_bins(self) -> torch.Tensor:
         if self.bins_rm is None:
             self.bins_rm = K.bins_row_major(self.bins)
         return self.bins_rm
+
+    def record_rows(self):
+        """(rows, is_seg10) for the record histograms: the seg10 copy when binize wrote one, else the standard
+        row-major copy."""
+        if self.bins_s10 is not None:
+            return self.bins_s10, True
+        return self.row_major_bins(), False
+
+
+def _seg10_ok(X: torch.Tensor, d: int, max_bins: int) -> bool:
+    return K.SEG10 and X.is_cuda and 80 < d <= 100 and d % 4 == 0 and max_bins <= 40
 
 
 def find_thresholds(sample: np.ndarray, d: int, max_bins: int, categorical: Dict[int, int]):
@@ -296,7 +310,11 @@ def _make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins
     nthr_t = torch.from_numpy(nthr).to(X.device)
     with _tr.span("tree.binize"):
         # the row-major copy (segment histograms' row gathers) comes out of the same kernel
-        bins, rm = K.binize(X, thr_t, nthr_t, want_rm=True)
+        s10 = _seg10_ok(X, d, max_bins)
+        bins, rm = K.binize(X, thr_t, nthr_t, want_rm=True, rm_layout="s10" if s10 else "std")
+    if s10:
+        return BinnedData(X, bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins, False,
+                          None, rm)
     return BinnedData(X, bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins, False, rm)
 
 
@@ -982,7 +1000,7 @@ class ForestTrainer:
                     h.wait()
         return Hc
 
-    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev):
+    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev, root=None):
         """Record histograms of a level's S slots in HIST_OVERLAP slot chunks; chunk c's all-reduce runs on the
         collective stream while chunk c + 1 is built (one per-level RCCL all-reduce of 1-50 MB otherwise
         serialises with the compute stream).  The sums are exact integers, so the result is identical to one
@@ -990,18 +1008,21 @@ class ForestTrainer:
         Hb = torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev)
         k = min(HIST_OVERLAP, S)
         bounds = np.linspace(0, S, k + 1).round().astype(np.int64)
-        rm = data.row_major_bins() if dev.type == "cuda" else None
+        rm, s10 = data.record_rows() if dev.type == "cuda" else (None, False)
         pend = []
         for c in range(k):
             s0, s1 = int(bounds[c]), int(bounds[c + 1])
             if s1 <= s0:
                 continue
-            sel = (sb[:, 2] >= s0) & (sb[:, 2] < s1)
-            sbc = sb[sel].copy()
-            sbc[:, 2] -= s0
             with _tr.span("tree.hist_chunk", slots=s1 - s0):
-                K.seg_hist(data.bins, d, B, rec, None, None, None, sbc, s1 - s0, wmax, scales, bins_rm=rm,
-                           interleave=True, rec=True, raw=True, out=Hb[s0:s1])
+                if root is not None:  # level 0: slot t = tree t, records compacted in the kernel
+                    K.seg_hist_root(data.bins_s10, d, B, root[0], root[1], scales[1], wmax, s0, s1, Hb[s0:s1])
+                else:
+                    sel = (sb[:, 2] >= s0) & (sb[:, 2] < s1)
+                    sbc = sb[sel].copy()
+                    sbc[:, 2] -= s0
+                    K.seg_hist(data.bins, d, B, rec, None, None, None, sbc, s1 - s0, wmax, scales, bins_rm=rm,
+                               interleave=True, rec=True, raw=True, out=Hb[s0:s1], rm_s10=s10)
             with _tr.span("tree.allreduce_async", cat="comm", bytes=(s1 - s0) * d * B * 16):
                 pend.append(self.comm.all_reduce_async(Hb[s0:s1]))
         with _tr.span("tree.allreduce_wait", cat="comm"):
@@ -1107,6 +1128,9 @@ class ForestTrainer:
             hist_raw_scale = None
             reduced = False
             sub_feats = None
+            rec_ok = (MSEG_REC and stats_rows.get("v0") is None and not subset_seg and 8 * B * 8 <= 128 * 1024)
+            root_ok = (ROOT_HIST and MSEG_L0 and use_mseg and not use_sub and depth == 0 and rec_ok and dev.type == "cuda" and
+                       data.bins_s10 is not None and len(build_ids) == T and d <= 100 and B <= 40)
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
                 if use_sub:
                     # every active node over its sampled features; exact int64 (count, sum w q) [A, m, B, 2]
@@ -1115,12 +1139,20 @@ class ForestTrainer:
                                         sub_feats, B, wmax, dev)
                     hist_raw_scale = mseg_raw
                     reduced = True
+                elif root_ok:
+                    # level 0 on seg10 rows: the roots' item records are compacted inside the histogram kernel
+                    if self.comm.distributed and HIST_OVERLAP > 1 and T >= 2:
+                        Hb = self._hist_overlapped(data, d, B, None, None, T, wmax, mseg_scales, dev,
+                                                   root=(codes, stats_rows["v1"]))
+                        reduced = True
+                    else:
+                        Hb = K.seg_hist_root(data.bins_s10, d, B, codes, stats_rows["v1"], mseg_scales[1], wmax, 0,
+                                             T, torch.zeros((T, d, B, 2), dtype=torch.int64, device=dev))
+                    hist_raw_scale = mseg_raw
                 elif use_mseg and (depth >= 1 or MSEG_L0):
                     # gather the rows of the built nodes into slot segments, then segment histograms
                     # packed item records on every device (the CPU emulates the HIP compaction + flat histogram
                     # exactly, so gloo ranks traverse the integer path RCCL ranks take)
-                    rec_ok = (MSEG_REC and stats_rows.get("v0") is None and not subset_seg and
-                              8 * B * 8 <= 128 * 1024)
                     perm, v0p, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, len(build_ids),
                                                              stats_rows.get("v0"), stats_rows["v1"],
                                                              rec_scale=mseg_scales[1] if rec_ok else None)
@@ -1139,9 +1171,10 @@ class ForestTrainer:
                         hist_raw_scale = mseg_raw
                         reduced = True
                     else:
+                        rm, s10 = (data.record_rows() if is_rec else (data.row_major_bins(), False)) \
+                            if dev.type == "cuda" else (None, False)
                         Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax,
-                                        mseg_scales, bins_rm=data.row_major_bins() if dev.type == "cuda" else None,
-                                        interleave=True, rec=is_rec, raw=True)
+                                        mseg_scales, bins_rm=rm, interleave=True, rec=is_rec, raw=True, rm_s10=s10)
                         hist_raw_scale = mseg_raw
                     del perm, v0p, v1p, wp
                 elif use_seg:

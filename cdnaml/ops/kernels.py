@@ -233,11 +233,13 @@ def quantile_thresholds(samp: torch.Tensor, max_bins: int):
 
 # --------------------------------------------------------------------- K4
 def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Optional[float] = None,
-           want_rm: bool = False):
+           want_rm: bool = False, rm_layout: str = "std"):
     """Raw features -> uint8 bins in feature-group-major layout [G, n, 8].
 
     want_rm: return ``(bins, rm)`` where ``rm`` is the row-major copy of ``bins_row_major`` written by the
     same kernel (GPU search kernel only; otherwise None and the caller transposes lazily).
+    rm_layout "s10" (d <= 100): ``rm`` [n, 16, 8] is in the seg10 layout of :func:`bins_seg10` instead (the
+    six-items-per-wave record histogram's rows); None when the kernel that ran cannot write it.
 
     Continuous feature f: bin = #{thr[f, :nthr[f]] < x}; NaN -> nthr[f].
     Categorical feature (nthr[f] < 0): bin = clamp(int(x), 0, 255).
@@ -253,14 +255,17 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Opti
         thr = thr.float().contiguous()
         nthr = nthr.int().contiguous()
         out = torch.empty((G, n, 8), dtype=torch.uint8, device=X.device)
-        Gs = 16 if (BINS_RM_PAD and G <= 16) else G
+        s10 = want_rm and rm_layout == "s10"
+        if s10 and d > 100:
+            raise ValueError("seg10 rows hold at most 100 features")
+        Gs = 16 if (s10 or (BINS_RM_PAD and G <= 16)) else G
         rm = torch.empty((n, Gs, 8), dtype=torch.uint8, device=X.device) if want_rm else None
         miss_on = missing is not None
         miss_val = float("nan") if (missing is None or math.isnan(missing)) else float(missing)
         if n:
             rc = _lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, int(miss_on),
-                                        miss_val, _ptr(out), _ptr(rm) if rm is not None else None, Gs,
-                                        _stream(X.device))
+                                        miss_val, _ptr(out), _ptr(rm) if rm is not None else None,
+                                        -10 if s10 else Gs, _stream(X.device))
             if rc == 2:  # the fallback kernel ran: no row-major copy
                 rm = None
             else:
@@ -281,6 +286,19 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Opti
             b = torch.where(torch.isnan(x), torch.full_like(b, nt), b)
         out[f // 8, :, f % 8] = b.to(torch.uint8)
     return (out, None) if want_rm else out
+
+
+def bins_seg10(bins: torch.Tensor, d: int) -> torch.Tensor:
+    """[G, n, 8] bins -> the seg10 row layout [n, 16, 8] (torch; reference of binize's ``rm_layout="s10"``):
+    byte 12 s + p of a row holds feature 10 s + p (s < 10, p < 10), every other byte is 0."""
+    G, n, _ = bins.shape
+    if d > 100:
+        raise ValueError("seg10 rows hold at most 100 features")
+    flat = bins.permute(1, 0, 2).reshape(n, G * 8)[:, :d]
+    out = torch.zeros((n, 128), dtype=torch.uint8, device=bins.device)
+    f = torch.arange(d, device=bins.device)
+    out[:, 12 * (f // 10) + f % 10] = flat
+    return out.view(n, 16, 8)
 
 
 def bins_to_matrix(bins: torch.Tensor, d: int) -> torch.Tensor:
@@ -1054,9 +1072,11 @@ SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "2048
 # conflict-free LDS planes, one v_perm per cell address); B <= 80 (4 planes <= 80 KB of LDS), 80 < B <= 256:
 # seg_hist_lane4_kernel (64 features per block, a quarter-wave per item; CDNAML_SEG_WIDE=0 keeps the flat kernel)
 SEG_LANE = __import__("os").environ.get("CDNAML_SEG_LANE", "1") != "0"
+# seg10 rows + the six-items-per-wave record histogram for 80 < d <= 100, B <= 40 (CDNAML_SEG10=0: lane8 rows)
+SEG10 = __import__("os").environ.get("CDNAML_SEG10", "1") != "0"
 SEG_LANE_MAX_B = 256 if __import__("os").environ.get("CDNAML_SEG_WIDE", "1") != "0" else 80
 # records buffers carry REC_PAD readable entries past their end: the lane kernel's record loads are unconditional
-REC_PAD = 64
+REC_PAD = 128
 
 
 def _fill_chunk(segs: np.ndarray, chunk: int, B: int = 0) -> int:
@@ -1098,8 +1118,11 @@ def _interleave(work: np.ndarray, segs: np.ndarray, chunk: int) -> np.ndarray:
 def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
              v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
              scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False,
-             rec: bool = False, raw: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+             rec: bool = False, raw: bool = False, out: Optional[torch.Tensor] = None,
+             rm_s10: bool = False) -> torch.Tensor:
     """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
+
+    rm_s10 (rec): ``bins_rm`` is in the seg10 layout (:func:`bins_seg10`): the six-items-per-wave kernel.
 
     out (rec + raw): a zeroed int64 [S, d, B, 2] tensor (e.g. a slot-range slice of a level's buffer) the sums
     are accumulated into and returned -- lets the engine all-reduce one slot chunk while the next is built.
@@ -1112,7 +1135,8 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
     if out is not None:
         assert rec and raw and out.dtype == torch.int64 and out.is_contiguous()
     if rec:
-        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw, out)
+        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw, out, rm_s10)
+    assert not rm_s10
     return _seg_hist(bins, d, B, perm, v0p, v1p, wp, segs, S, wmax, scales, bins_rm, interleave, raw)
 
 
@@ -1160,7 +1184,7 @@ def rec_encode(rows: torch.Tensor, w: torch.Tensor, q: torch.Tensor) -> torch.Te
     return rows.to(torch.int64) | (w.to(torch.int64) << 31) | ((q.to(torch.int64) + (1 << 23)) << 39)
 
 
-def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False, out=None):
+def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False, out=None, rm_s10=False):
     G, n, _ = bins.shape
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
     if S == 0 or len(segs) == 0:
@@ -1189,6 +1213,9 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         iout = out if out is not None else torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
         assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
         mode = 1 | 4 | 16 | (128 if (SEG_LANE and B <= SEG_LANE_MAX_B) else 0)
+        if rm_s10:
+            assert d <= 100 and B <= 40 and bins_rm.shape[1] == 16
+            mode |= 128 | 256
         _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(bins_rm), n, d, B, _ptr(rec), None, None, None,
                                             _ptr(wt), len(work), 1.0, qs1, _ptr(iout), bins_rm.shape[1],
                                             _stream(bins.device)), "cdna_seg_hist(rec)")
@@ -1196,6 +1223,39 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         return iout
     out = iout.double()
     out[..., 1] /= qs1
+    return out
+
+
+def seg_hist_root(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, v1: torch.Tensor, qs1: float,
+                  wmax: int, t0: int, t1: int, out: torch.Tensor) -> torch.Tensor:
+    """Level-0 record histograms of trees [t0, t1) straight from the row codes (GPU, seg10 rows): every row of
+    non-zero weight is an item of its tree's root.  Adds the exact int64 sums (count, sum w * q) into ``out``
+    [t1 - t0, d, B, 2] (zeroed by the caller) -- the same integers as ``codes_compact(rec_scale=qs1)`` +
+    ``seg_hist(rec=True, raw=True)``, without materialising the level's 8-byte records."""
+    T, n = codes.shape
+    assert _native(codes) and d <= 100 and B <= 40 and bins_s10.shape == (n, 16, 8)
+    assert out.dtype == torch.int64 and out.is_contiguous() and out.shape == (t1 - t0, d, B, 2)
+    if n == 0 or t1 <= t0:
+        return out
+    wm = int(max(1, min(255, wmax)))
+    # each LDS cell copy takes every third item of a wave's stream: rows x wmax / 3 (+ a partial trip per
+    # wave) stays below the 20-bit count field
+    rows = max(64, min(n, 3 * ((1 << 20) // (wm + 1)) - 16 * 64))
+    C = (n + rows - 1) // rows
+    # XCD-aware order: block b runs on XCD b % 8; the trees of row chunk c are consecutive blocks of XCD c % 8,
+    # so their row-line gathers and label reads share that XCD's L2
+    work = []
+    for cq in range((C + 7) // 8):
+        for t in range(t0, t1):
+            for x in range(8):
+                c = cq * 8 + x
+                if c < C:
+                    r0 = c * rows
+                    work.append((r0, min(rows, n - r0), t))
+    wt, = upload(codes.device, np.asarray(work, dtype=np.int32).reshape(-1))
+    v1c = v1.float().contiguous()
+    _lib.check(_lib.lib().cdna_seg_hist_root(_ptr(bins_s10), n, d, B, _ptr(codes), _ptr(v1c), float(qs1), _ptr(wt),
+                                             len(work), t0, _ptr(out), _stream(codes.device)), "cdna_seg_hist_root")
     return out
 
 

@@ -513,6 +513,209 @@ __global__ __launch_bounds__(1024, 2) void seg_hist_lane8_kernel(const SegHistAr
   }
 }
 
+// Six items per wave for 80 < d <= 100, B <= 40 (the headline forest levels).
+// The cost of seg_hist_lane8 is its ds_add_u64 wave instructions (~6 LDS
+// cycles each: the address and 8-byte data VGPRs move to the LDS at 2 cycles
+// per dword, active lanes or not), and at d = 100 its 4 items x 16 lanes x 8
+// features offer 512 lane slots for 400 updates (78 %).  Here the bins rows
+// are in the "seg10" layout (binize v5, Gs = -10: ten 12-byte chunks of 10
+// features per 128-byte row) and each 32-lane half takes THREE items: lane
+// l' = 10 c + s (c = item of the half, s = chunk) gathers its item's chunk s
+// with one dwordx3 load and makes 10 updates; lanes 30 / 31 of each half add 0.
+// 6 items x 100 updates per 10 wave instructions (94 %): 1.67 instead of 2.0
+// atomics per item, and one gather instruction per 6 items instead of 4.
+// Cells: [10 planes j][BP][32 columns] u64 with column = l' (item c's copy of
+// chunk s), so the 32 lanes of a half hit 32 distinct bank pairs whatever the
+// bins (cell byte address bin << 8 | l' << 3: one v_perm_b32, as in lane8);
+// the flush adds the three copies.  LDS = BP * 2.5 KB (100 KB at 40 bins:
+// one 1024-thread block per CU).
+template <int BP, int U>
+__global__ __launch_bounds__(1024) void seg_hist_lane10_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins8) {
+  constexpr int TH = 1024, NW = TH / 64, IPW = 6;
+  constexpr int PLANE = BP * 32;  // u64 cells per feature plane j
+  __shared__ __attribute__((aligned(16))) unsigned long long h[10 * PLANE];  // [10][BP][32]
+  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
+  if (!CDNA_DCHECK(start >= 0 && len >= 0 && slot >= 0, 0x5E83u)) return;  // corrupt work item
+  for (int i = threadIdx.x; i < 10 * PLANE; i += TH) h[i] = 0ull;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int c = l32 / 10, s = l32 - 10 * c;  // c = 3: lanes 30 / 31 (no item)
+  const bool on = c < 3;
+  const int item = half * 3 + (on ? c : 0);
+  const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint8_t* lbase = bins8 + 12 * (on ? s : 0);
+  const uint32_t loff = (uint32_t)l32 * 8u;  // column << 3
+  static_assert(IPW * U <= 128, "record over-read must stay within REC_PAD");
+  const uint64_t* __restrict__ recp = a.rec + start + item;
+  // U = 16 items per lane per trip (160 atomics): the trip's record load and gather latencies are exposed
+  // once per trip, so the other 15 waves of the CU need ~15 x 160 ds_add_u64 of work to cover them (U = 8:
+  // 13.7 ms per level; a two-set software pipeline did not survive the compiler's loop rotation)
+  for (int i0 = wid * IPW * U; i0 < len; i0 += NW * IPW * U) {
+    uint64_t rc[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) rc[p] = recp[i0 + IPW * p];
+    if (!on) {
+#pragma unroll
+      for (int p = 0; p < U; ++p) rc[p] = 0ull;
+    } else if (i0 + IPW * U > len) {
+#pragma unroll
+      for (int p = 0; p < U; ++p)
+        if (i0 + IPW * p + item >= len) rc[p] = 0ull;
+    }
+    uint32_t x0[U], x1[U], x2[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      uint32_t row = (uint32_t)rc[p] & 0x7FFFFFFFu;
+      if (!CDNA_DCHECK((int64_t)row < a.n, 0x5E84u)) row = 0u;  // record row outside the bins
+      const uint3 v = *reinterpret_cast<const uint3*>(lbase + (uint64_t)row * 128u);
+      x0[p] = v.x; x1[p] = v.y; x2[p] = v.z;
+    }
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t lo = (uint32_t)rc[p], hi = (uint32_t)(rc[p] >> 32);
+      const uint32_t w = __builtin_amdgcn_alignbit(hi, lo, 31) & 0xFFu;
+      const unsigned long long add = ((unsigned long long)(w << (kPackShift - 32)) << 32) +
+                                     (unsigned long long)w * (hi >> 7);
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const uint32_t src = j < 4 ? x0[p] : (j < 8 ? x1[p] : x2[p]);
+        const uint32_t off = __builtin_amdgcn_perm(loff, src, 0x0C0C0004u | ((uint32_t)(j & 3) << 8));
+        atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h) + off) + j * PLANE, add);
+      }
+    }
+  }
+  __syncthreads();
+  // flush: thread -> (plane j, bin, chunk s), the three item copies summed
+  for (int e = threadIdx.x; e < 10 * BP * 10; e += TH) {
+    const int sc = e % 10, rest = e / 10;
+    const int bn = rest % BP, j = rest / BP;
+    const int f = 10 * sc + j;
+    if (bn >= a.B || f >= a.d) continue;
+    const unsigned long long* cell = h + j * PLANE + bn * 32 + sc;
+    const unsigned long long v0 = cell[0], v1 = cell[10], v2 = cell[20];
+    const unsigned long long cnt = (v0 >> kPackShift) + (v1 >> kPackShift) + (v2 >> kPackShift);
+    if (!cnt) continue;
+    const unsigned long long m = (1ull << kPackShift) - 1ull;
+    const long long sum = (long long)((v0 & m) + (v1 & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt;
+    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+    atomicAdd(o, cnt);
+    atomicAdd(o + 1, (unsigned long long)sum);
+  }
+}
+
+// Level 0 of a forest without item records: every root holds every row of
+// non-zero weight, so the level-0 records (row, weight, quantised label) are
+// the row-order compaction of each tree's codes -- 1.26e9 records at the
+// headline, written and read back once (count + scatter: ~4.3 ms per step).
+// Here a work item is (tree, row range) and each wave compacts its own rows'
+// records on the fly into a 256-entry LDS ring: one coalesced 64-row load of
+// the tree's codes and labels (the next window's already in flight), a ballot
+// and mbcnt rank, one ds_write_b64 per item; then the lane10 trip consumes 96
+// ring entries.  The gathers of a wave walk consecutive rows (each line is read
+// by ~0.63 x 20 trees: the XCD-aware work order puts the trees of one row chunk
+// on one XCD back to back, so the L2 serves most of them).  Same int64 sums as
+// the record path (the sums do not depend on the item order).
+template <int BP>
+__global__ __launch_bounds__(1024) void seg_hist_lane10_root_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins8,
+                                                                    const uint16_t* __restrict__ codes,
+                                                                    const float* __restrict__ v1, float qs1, int slot0) {
+  constexpr int TH = 1024, NW = TH / 64, U = 16, IPW = 6, NI = IPW * U, RING = 256;  // NI - 1 + 64 < RING
+  constexpr int PLANE = BP * 32;
+  __shared__ __attribute__((aligned(16))) unsigned long long h[10 * PLANE];  // [10][BP][32]
+  __shared__ __attribute__((aligned(16))) uint64_t ring[NW][RING];
+  const int r0 = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], tree = a.work[3 * blockIdx.x + 2];
+  if (!CDNA_DCHECK(r0 >= 0 && len >= 0 && tree >= 0 && (int64_t)r0 + len <= a.n, 0x5E85u)) return;
+  for (int i = threadIdx.x; i < 10 * PLANE; i += TH) h[i] = 0ull;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int c = l32 / 10, s = l32 - 10 * c;
+  const bool on = c < 3;
+  const int item = half * 3 + (on ? c : 0);
+  const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint8_t* lbase = bins8 + 12 * (on ? s : 0);
+  const uint32_t loff = (uint32_t)l32 * 8u;
+  const uint16_t* ct = codes + (int64_t)tree * a.n;
+  uint64_t* rg = ring[wid];
+  // the wave's rows: a contiguous 64-aligned share of the block's range
+  const int per = ((len + NW - 1) / NW + 63) & ~63;
+  int64_t wr = (int64_t)r0 + (int64_t)wid * per;
+  const int64_t wend = (int64_t)r0 + len < wr + per ? (int64_t)r0 + len : wr + per;
+  uint32_t head = 0u, tail = 0u;  // wave-uniform ring cursors
+  uint32_t ncw = 0xFFu;
+  float ny = 0.f;
+  auto fetch = [&](int64_t r) {
+    ncw = r < wend ? (uint32_t)ct[r] : 0xFFu;
+    ny = r < wend ? v1[r] : 0.f;
+  };
+  fetch(wr + lane);
+  for (;;) {
+    while (tail - head < (uint32_t)NI && wr < wend) {  // wave-uniform refill, one 64-row window per round
+      const uint32_t cw = ncw;
+      const float y = ny;
+      const int64_t r = wr + lane;
+      wr += 64;
+      fetch(wr + lane);
+      const bool has = (cw & 0xFFu) != 0xFFu && (cw >> 8) != 0u;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(has);
+      if (has) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        int q1 = (int)rintf(y * qs1);
+        q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+        rg[(tail + rank) & (RING - 1)] =
+            (uint64_t)r | ((uint64_t)(cw >> 8) << 31) | ((uint64_t)(uint32_t)(q1 + kPackQ) << 39);
+      }
+      tail += (uint32_t)__builtin_popcountll(m);
+    }
+    const uint32_t avail = tail - head;
+    if (avail == 0u) break;  // wave-uniform: rows exhausted and ring drained
+    asm volatile("" ::: "memory");  // the ring writes above are issued before the reads below (LDS: in order)
+    uint64_t rc[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t k = (uint32_t)(IPW * p + item);
+      rc[p] = (on && k < avail) ? rg[(head + k) & (RING - 1)] : 0ull;
+    }
+    head += avail < (uint32_t)NI ? avail : (uint32_t)NI;
+    uint32_t x0[U], x1[U], x2[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t row = (uint32_t)rc[p] & 0x7FFFFFFFu;
+      const uint3 v = *reinterpret_cast<const uint3*>(lbase + (uint64_t)row * 128u);
+      x0[p] = v.x; x1[p] = v.y; x2[p] = v.z;
+    }
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t lo = (uint32_t)rc[p], hi = (uint32_t)(rc[p] >> 32);
+      const uint32_t w = __builtin_amdgcn_alignbit(hi, lo, 31) & 0xFFu;
+      const unsigned long long add = ((unsigned long long)(w << (kPackShift - 32)) << 32) +
+                                     (unsigned long long)w * (hi >> 7);
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const uint32_t src = j < 4 ? x0[p] : (j < 8 ? x1[p] : x2[p]);
+        const uint32_t off = __builtin_amdgcn_perm(loff, src, 0x0C0C0004u | ((uint32_t)(j & 3) << 8));
+        atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h) + off) + j * PLANE, add);
+      }
+    }
+    asm volatile("" ::: "memory");  // this trip's ring reads are issued before the next refill overwrites
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 10 * BP * 10; e += TH) {
+    const int sc = e % 10, rest = e / 10;
+    const int bn = rest % BP, j = rest / BP;
+    const int f = 10 * sc + j;
+    if (bn >= a.B || f >= a.d) continue;
+    const unsigned long long* cell = h + j * PLANE + bn * 32 + sc;
+    const unsigned long long v0 = cell[0], v1c = cell[10], v2 = cell[20];
+    const unsigned long long cnt = (v0 >> kPackShift) + (v1c >> kPackShift) + (v2 >> kPackShift);
+    if (!cnt) continue;
+    const unsigned long long m = (1ull << kPackShift) - 1ull;
+    const long long sum = (long long)((v0 & m) + (v1c & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt;
+    unsigned long long* o = &a.out[(((int64_t)(tree - slot0) * a.d + f) * a.B + bn) * 2];
+    atomicAdd(o, cnt);
+    atomicAdd(o + 1, (unsigned long long)sum);
+  }
+}
+
 // Wide-bin lane variant (80 < B <= 256: XGBoost-style 256-bin boosting).  Four
 // [BP][32] u64 planes of 256 bins would need 256 KB of LDS, so a block covers
 // 64 features: each 16-lane QUARTER of a wave takes one item and lane l' owns
@@ -1122,6 +1325,23 @@ __global__ __launch_bounds__(256) void bins_row_major_kernel(const uint64_t* __r
 
 }  // namespace
 
+// Level-0 record histograms straight from the codes (seg_hist_lane10_root_kernel): bins in the seg10 row layout,
+// work [nwork][3] {row start, row count, tree}; tree t's sums go to out slot t - slot0 (a slot-range slice).
+// Row counts per work item must keep count x max weight below 2^20 (the packed LDS cells).
+CDNA_API int cdna_seg_hist_root(const uint8_t* bins_s10, int64_t n, int d, int B, const uint16_t* codes,
+                                const float* v1, float qs1, const int* work, int nwork, int slot0,
+                                unsigned long long* out, hipStream_t st) {
+  if (nwork <= 0) return 0;
+  if (d > 100 || B > 40 || B < 1) return (int)hipErrorInvalidValue;
+  SegHistArgs a{nullptr, n, d, B, nullptr, nullptr, v1, nullptr, work, 1.f, qs1, out};
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), 0, st, a, bins_s10, codes, v1, qs1, slot0);
+  };
+  if (B <= 32) launch(seg_hist_lane10_root_kernel<32>);
+  else launch(seg_hist_lane10_root_kernel<40>);
+  return (int)hipGetLastError();
+}
+
 // mode bit0: packed (no v0; count | sum in one atomic); bit1: per-row weights wp present;
 // bit4: `perm` holds packed 8-byte item records (row | w << 31 | (q1 + 2^23) << 39; flat kernel only).
 // bit7 (with bit4 and bit2, B <= 256): lane-feature kernels (seg_hist_lane_kernel, B > 80: seg_hist_lane4_kernel).
@@ -1144,6 +1364,20 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
     a.rec = reinterpret_cast<const uint64_t*>(perm);
     const int row_bytes = (rm_stride ? rm_stride : G) * 8;
     const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bins);
+    if (mode & 256) {
+      // bins rows in the seg10 layout (binize v5 with Gs = -10): six items per wave
+      if (d > 100 || B > 40 || row_bytes != 128) return (int)hipErrorInvalidValue;
+      auto launch10 = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), 0, st, a, b8); };
+      static const int u10 = [] { const char* e = getenv("CDNAML_LANE10_U"); return e ? atoi(e) : 16; }();
+      if (u10 == 8) {
+        if (B <= 32) launch10(seg_hist_lane10_kernel<32, 8>);
+        else launch10(seg_hist_lane10_kernel<40, 8>);
+      } else {
+        if (B <= 32) launch10(seg_hist_lane10_kernel<32, 16>);
+        else launch10(seg_hist_lane10_kernel<40, 16>);
+      }
+      return (int)hipGetLastError();
+    }
     if (B > 80) {
       const int ny = (d + 63) / 64;
       const dim3 grid2((unsigned)(((nwork + 7) / 8) * 8 * ny));

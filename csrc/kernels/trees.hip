@@ -315,6 +315,10 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
     }
     return word;
   };
+  // Gs == -10: the "seg10" row layout of seg_hist_lane10_kernel -- ten 12-byte chunks per 128-byte row, chunk s
+  // holding features 10 s .. 10 s + 9 in its first 10 bytes (2 zero bytes, 8 zero bytes after chunk 9), so one
+  // aligned dwordx3 gather brings a lane its 10 features.  Output dword k of a row = row bytes
+  // [10 s + p, 10 s + p + 4) with s = 4k / 12, p = 4k % 12 (an alignbyte of two tile dwords; p = 8 keeps 2 bytes).
   auto store_rm = [&](int64_t tl) {
     const int rows = (int)((n - tl * RT) < RT ? (n - tl * RT) : RT);
     for (int i = threadIdx.x; i < RT * 8; i += nth) {
@@ -322,9 +326,28 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
       if (row < rows) {
         const uint64_t* tr = tile + row * TP + 2 * c;
         uint4 v;
-        v.x = (uint32_t)tr[0]; v.y = (uint32_t)(tr[0] >> 32);
-        v.z = (uint32_t)tr[1]; v.w = (uint32_t)(tr[1] >> 32);
-        *reinterpret_cast<uint4*>(rm + (tl * RT + row) * Gs + 2 * c) = v;
+        if (Gs == -10) {
+          const uint32_t* td = reinterpret_cast<const uint32_t*>(tile + row * TP);
+          uint32_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = 4 * c + e, s = (4 * k) / 12, p = (4 * k) - 12 * s;
+            const int f0 = 10 * s + p;  // even: the dword pair (f0 >> 2, +1) shifted by 0 or 2 bytes
+            uint32_t wv = 0u;
+            if (s < 10) {
+              const uint32_t lo = td[f0 >> 2], hi = td[(f0 >> 2) + 1];
+              wv = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(f0 & 3));
+              if (p == 8) wv &= 0xFFFFu;
+            }
+            o[e] = wv;
+          }
+          v.x = o[0]; v.y = o[1]; v.z = o[2]; v.w = o[3];
+          *reinterpret_cast<uint4*>(rm + (tl * RT + row) * 16 + 2 * c) = v;
+        } else {
+          v.x = (uint32_t)tr[0]; v.y = (uint32_t)(tr[0] >> 32);
+          v.z = (uint32_t)tr[1]; v.w = (uint32_t)(tr[1] >> 32);
+          *reinterpret_cast<uint4*>(rm + (tl * RT + row) * Gs + 2 * c) = v;
+        }
       }
     }
   };
@@ -831,14 +854,17 @@ inline unsigned grid_for(int64_t n, int per, unsigned cap) {
 // ran instead (rm not written).
 CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const float* thr, const int* nthr, int tmax,
                          int miss_on, float miss_val, uint64_t* out, uint64_t* rm, int Gs, hipStream_t st) {
-  if (rm && Gs < (d + 7) / 8) return (int)hipErrorInvalidValue;
+  // Gs == -10: rm gets the seg10 row layout (d <= 100, 128-byte rows; binize v5 only, see store_rm)
+  const bool s10 = rm && Gs == -10;
+  if (s10 && d > 100) return (int)hipErrorInvalidValue;
+  if (rm && !s10 && Gs < (d + 7) / 8) return (int)hipErrorInvalidValue;
   if (n <= 0) return 0;
   static const bool v5_on = [] {
     const char* e = getenv("CDNAML_BINIZE_V5");
     return !e || atoi(e) != 0;
   }();
   if (v5_on && d <= 128 && (d % 4) == 0 && (ldx % 4) == 0 && (reinterpret_cast<uintptr_t>(X) % 16) == 0 &&
-      (!rm || Gs == 16)) {
+      (!rm || Gs == 16 || s10)) {
     // v5: wave = (64-row tile, 8-feature group), lanes search the same tables (broadcast LDS reads)
     int steps = 0;
     while ((1 << steps) <= tmax) ++steps;
@@ -864,6 +890,8 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
       return (int)hipGetLastError();
     }
   }
+  const bool rm_wanted = rm != nullptr;
+  if (s10) rm = nullptr;  // the fallbacks write the standard layout only: report "rm not written" (2)
   {
     // v2: tile of rows in LDS next to the thresholds (<= 64 KB per block)
     const size_t tb = (size_t)d * (tmax > 0 ? tmax : 1) * 4 + (size_t)d * 4;
@@ -889,7 +917,8 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(binize2_kernel, dim3(grid_for(n, rpt, 8192)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
                          tmax > 0 ? tmax : 1, rpt, steps, miss_on, miss_val, out, rm, Gs);
-      return (int)hipGetLastError();
+      const int e = (int)hipGetLastError();
+      return e != 0 ? e : (s10 ? 2 : 0);
     }
   }
   const int G = (d + 7) / 8;
@@ -901,7 +930,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
   hipLaunchKernelGGL(binize_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
                      tmax, use_lds, miss_on, miss_val, out);
   const int e = (int)hipGetLastError();
-  return e != 0 ? e : (rm ? 2 : 0);
+  return e != 0 ? e : (rm_wanted ? 2 : 0);
 }
 
 // ngroups slot groups of SB slots (host-planned); out must be zeroed.

@@ -65,7 +65,7 @@ run_step() {
         kstats "$O/profcfg" ;;
     pmc:*)
         rm -rf "$O/pmc"; mkdir -p "$O/pmc"
-        (cd /tmp && timeout -s KILL 300 rocprofv3 -i "$R/scripts/pmc_hist.txt" --kernel-include-regex "${s#pmc:}" \
+        (cd /tmp && timeout -s KILL 300 rocprofv3 -i "$R/scripts/${PMC_FILE:-pmc_hist.txt}" --kernel-include-regex "${s#pmc:}" \
             --output-format csv -d "$O/pmc" -o p -- python3 "$R/bench.py" --steps 1 --warmup 0 ${BENCH_ARGS} \
             > "$O/pmc/run.log" 2>&1)
         local rc=$?; find "$O/pmc" -name "*counter_collection.csv"; return $rc ;;

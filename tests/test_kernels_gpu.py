@@ -1023,6 +1023,53 @@ def test_seg_hist_lane_matches_flat(dev, d, B, monkeypatch):
     assert torch.equal(got.cpu(), ref.cpu())
 
 
+@pytest.mark.parametrize("d,B", [(100, 40), (100, 32), (84, 40), (92, 17), (96, 2)])
+def test_seg10_rows_and_lane10_histogram(dev, d, B, monkeypatch):
+    """seg10 rows (binize v5, rm_layout="s10") equal the torch layout reference K.bins_seg10, and the
+    six-items-per-wave record histogram on them gives exactly the int64 sums of the flat (row, group)-pair
+    kernel on the standard rows: ragged last trips, several chunks per segment, zero-weight records, d < 100
+    (zero chunk bytes past d), B = 32 / 40 planes."""
+    T, n = 6, 150011
+    rng = np.random.default_rng(d * 11 + B)
+    loc = rng.integers(0, 3, (T, n))
+    w = rng.poisson(1.0, (T, n)).clip(0, 12)
+    loc = np.where(w == 0, 0xFF, loc)
+    codes = torch.from_numpy(((w << 8) | loc).astype(np.uint16).view(np.int16)).to(dev)
+    tfirst = torch.from_numpy(np.arange(T, dtype=np.int32) * 3)
+    slot_of = np.array([(t * 3 + k) if k < 2 else -1 for t in range(T) for k in range(3)], dtype=np.int32)
+    slot_of[slot_of >= 0] = np.arange(int((slot_of >= 0).sum()))
+    S = int((slot_of >= 0).sum())
+    g = torch.Generator().manual_seed(d)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    bins, s10 = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), want_rm=True, rm_layout="s10")
+    assert s10 is not None and s10.shape == (n, 16, 8)
+    assert torch.equal(s10, K.bins_seg10(bins, d))
+    rm = K.bins_row_major(bins)
+    v1 = (torch.randn(n, generator=g) * 5).to(dev)
+    sc = K.seg_scales(None, v1, 12, n)
+    rec, _, _, _, sg = K.codes_compact(codes, tfirst, slot_of, S, None, v1, rec_scale=sc[1])
+    sb = np.concatenate([sg, np.arange(S)[:, None]], 1)
+    monkeypatch.setattr(K, "SEG_HIST_CHUNK", 20000)
+    monkeypatch.setattr(K, "SEG_LANE", False)
+    ref = K.seg_hist(bins, d, B, rec, None, None, None, sb, S, 12, sc, bins_rm=rm, rec=True, raw=True)
+    monkeypatch.setattr(K, "SEG_LANE", True)
+    got = K.seg_hist(bins, d, B, rec, None, None, None, sb, S, 12, sc, bins_rm=s10, rec=True, raw=True, rm_s10=True)
+    assert got.dtype == torch.int64 and int(ref[..., 0].sum()) > 0
+    assert torch.equal(got.cpu(), ref.cpu())
+    # level 0 without records: every row of non-zero weight is an item of its tree's root
+    rcodes = torch.from_numpy(((w << 8) | np.where(w == 0, 0xFF, 0)).astype(np.uint16).view(np.int16)).to(dev)
+    rrec, _, _, _, rsg = K.codes_compact(rcodes, torch.arange(T, dtype=torch.int32), np.arange(T, dtype=np.int32),
+                                         T, None, v1, rec_scale=sc[1])
+    rsb = np.concatenate([rsg, np.arange(T)[:, None]], 1)
+    rref = K.seg_hist(bins, d, B, rrec, None, None, None, rsb, T, 12, sc, bins_rm=s10, rec=True, raw=True,
+                      rm_s10=True)
+    for t0, t1 in [(0, T), (2, 5)]:
+        rgot = K.seg_hist_root(s10, d, B, rcodes, v1, sc[1], 12, t0, t1,
+                               torch.zeros((t1 - t0, d, B, 2), dtype=torch.int64, device=dev))
+        assert torch.equal(rgot.cpu(), rref[t0:t1].cpu())
+
+
 @pytest.mark.parametrize("d,maxb,n,missing", [(100, 40, 100003, None), (64, 256, 5001, None), (8, 2, 77, None),
                                               (128, 32, 4099, None), (100, 40, 3001, -999.0),
                                               (100, 40, 3001, float("nan"))])
