@@ -1015,8 +1015,9 @@ class ForestTrainer:
             if s1 <= s0:
                 continue
             with _tr.span("tree.hist_chunk", slots=s1 - s0):
-                if root is not None:  # level 0: slot t = tree t, records compacted in the kernel
-                    K.seg_hist_root(data.bins_s10, d, B, root[0], root[1], scales[1], wmax, s0, s1, Hb[s0:s1])
+                if root is not None:  # <= 1 built node per tree: records compacted in the kernel
+                    K.seg_hist_codes(data.bins_s10, d, B, root[0], root[1], scales[1], wmax, root[2], root[3], s0,
+                                     s1, Hb[s0:s1])
                 else:
                     sel = (sb[:, 2] >= s0) & (sb[:, 2] < s1)
                     sbc = sb[sel].copy()
@@ -1129,8 +1130,11 @@ class ForestTrainer:
             reduced = False
             sub_feats = None
             rec_ok = (MSEG_REC and stats_rows.get("v0") is None and not subset_seg and 8 * B * 8 <= 128 * 1024)
-            root_ok = (ROOT_HIST and MSEG_L0 and use_mseg and not use_sub and depth == 0 and rec_ok and dev.type == "cuda" and
-                       data.bins_s10 is not None and len(build_ids) == T and d <= 100 and B <= 40)
+            # levels with <= 1 built node per tree (0: the roots, 1: the smaller children) on seg10 rows: the
+            # records are compacted inside the histogram kernel (no codes_compact pass)
+            root_ok = (ROOT_HIST and use_mseg and not use_sub and (depth >= 1 or MSEG_L0) and rec_ok and
+                       dev.type == "cuda" and data.bins_s10 is not None and d <= 100 and B <= 40 and
+                       len(build_ids) > 0 and np.bincount(slot_tree, minlength=T).max() <= 1)
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
                 if use_sub:
                     # every active node over its sampled features; exact int64 (count, sum w q) [A, m, B, 2]
@@ -1140,14 +1144,16 @@ class ForestTrainer:
                     hist_raw_scale = mseg_raw
                     reduced = True
                 elif root_ok:
-                    # level 0 on seg10 rows: the roots' item records are compacted inside the histogram kernel
-                    if self.comm.distributed and HIST_OVERLAP > 1 and T >= 2:
-                        Hb = self._hist_overlapped(data, d, B, None, None, T, wmax, mseg_scales, dev,
-                                                   root=(codes, stats_rows["v1"]))
+                    S_b = len(build_ids)
+                    sl_node = build_ids - tfirst.numpy()[slot_tree]  # the slot's local node in its tree's codes
+                    root = (codes, stats_rows["v1"], slot_tree, sl_node)
+                    if self.comm.distributed and HIST_OVERLAP > 1 and S_b >= 2:
+                        Hb = self._hist_overlapped(data, d, B, None, None, S_b, wmax, mseg_scales, dev, root=root)
                         reduced = True
                     else:
-                        Hb = K.seg_hist_root(data.bins_s10, d, B, codes, stats_rows["v1"], mseg_scales[1], wmax, 0,
-                                             T, torch.zeros((T, d, B, 2), dtype=torch.int64, device=dev))
+                        Hb = K.seg_hist_codes(data.bins_s10, d, B, codes, stats_rows["v1"], mseg_scales[1], wmax,
+                                              slot_tree, sl_node, 0, S_b,
+                                              torch.zeros((S_b, d, B, 2), dtype=torch.int64, device=dev))
                     hist_raw_scale = mseg_raw
                 elif use_mseg and (depth >= 1 or MSEG_L0):
                     # gather the rows of the built nodes into slot segments, then segment histograms

@@ -1226,37 +1226,52 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
     return out
 
 
-def seg_hist_root(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, v1: torch.Tensor, qs1: float,
-                  wmax: int, t0: int, t1: int, out: torch.Tensor) -> torch.Tensor:
-    """Level-0 record histograms of trees [t0, t1) straight from the row codes (GPU, seg10 rows): every row of
-    non-zero weight is an item of its tree's root.  Adds the exact int64 sums (count, sum w * q) into ``out``
-    [t1 - t0, d, B, 2] (zeroed by the caller) -- the same integers as ``codes_compact(rec_scale=qs1)`` +
-    ``seg_hist(rec=True, raw=True)``, without materialising the level's 8-byte records."""
+def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, v1: torch.Tensor, qs1: float,
+                   wmax: int, slot_tree: np.ndarray, slot_node: np.ndarray, s0: int, s1: int,
+                   out: torch.Tensor) -> torch.Tensor:
+    """Record histograms of slots [s0, s1) straight from the row codes (GPU, seg10 rows), for levels with at most
+    one built node per tree: slot s is local node ``slot_node[s]`` of tree ``slot_tree[s]`` (level 0: every root,
+    node 0).  Adds the exact int64 sums (count, sum w * q) into ``out`` [s1 - s0, d, B, 2] (zeroed by the caller)
+    -- the same integers as ``codes_compact(rec_scale=qs1)`` + ``seg_hist(rec=True, raw=True)``, without
+    materialising the level's 8-byte records."""
     T, n = codes.shape
     assert _native(codes) and d <= 100 and B <= 40 and bins_s10.shape == (n, 16, 8)
-    assert out.dtype == torch.int64 and out.is_contiguous() and out.shape == (t1 - t0, d, B, 2)
-    if n == 0 or t1 <= t0:
+    assert out.dtype == torch.int64 and out.is_contiguous() and out.shape == (s1 - s0, d, B, 2)
+    st = np.asarray(slot_tree, dtype=np.int64)
+    sn = np.asarray(slot_node, dtype=np.int64)
+    assert len(st) == len(sn) and np.all((st >= 0) & (st < T)) and np.all((sn >= 0) & (sn < 0xFF))
+    assert len(np.unique(st[s0:s1])) == s1 - s0  # one built node per tree
+    if n == 0 or s1 <= s0:
         return out
     wm = int(max(1, min(255, wmax)))
     # each LDS cell copy takes every third item of a wave's stream: rows x wmax / 3 (+ a partial trip per
     # wave) stays below the 20-bit count field
     rows = max(64, min(n, 3 * ((1 << 20) // (wm + 1)) - 16 * 64))
     C = (n + rows - 1) // rows
-    # XCD-aware order: block b runs on XCD b % 8; the trees of row chunk c are consecutive blocks of XCD c % 8,
-    # so their row-line gathers and label reads share that XCD's L2
+    # XCD-aware order: block b runs on XCD b % 8; the slots (trees) of row chunk c are consecutive blocks of
+    # XCD c % 8, so their row-line gathers and label reads share that XCD's L2
     work = []
     for cq in range((C + 7) // 8):
-        for t in range(t0, t1):
+        for sl in range(s0, s1):
             for x in range(8):
                 c = cq * 8 + x
                 if c < C:
                     r0 = c * rows
-                    work.append((r0, min(rows, n - r0), t))
-    wt, = upload(codes.device, np.asarray(work, dtype=np.int32).reshape(-1))
+                    work.append((r0, min(rows, n - r0), sl))
+    sinfo = np.stack([st, sn], 1).astype(np.int32).reshape(-1)
+    wt, si = upload(codes.device, np.asarray(work, dtype=np.int32).reshape(-1), sinfo)
     v1c = v1.float().contiguous()
     _lib.check(_lib.lib().cdna_seg_hist_root(_ptr(bins_s10), n, d, B, _ptr(codes), _ptr(v1c), float(qs1), _ptr(wt),
-                                             len(work), t0, _ptr(out), _stream(codes.device)), "cdna_seg_hist_root")
+                                             len(work), _ptr(si), s0, _ptr(out), _stream(codes.device)),
+               "cdna_seg_hist_root")
     return out
+
+
+def seg_hist_root(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, v1: torch.Tensor, qs1: float,
+                  wmax: int, t0: int, t1: int, out: torch.Tensor) -> torch.Tensor:
+    """Level 0: :func:`seg_hist_codes` with slot t = the root (local node 0) of tree t, slots [t0, t1)."""
+    T = codes.shape[0]
+    return seg_hist_codes(bins_s10, d, B, codes, v1, qs1, wmax, np.arange(T), np.zeros(T, np.int64), t0, t1, out)
 
 
 def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],

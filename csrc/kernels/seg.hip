@@ -603,12 +603,13 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_kernel(const SegHistArgs
   }
 }
 
-// Level 0 of a forest without item records: every root holds every row of
-// non-zero weight, so the level-0 records (row, weight, quantised label) are
-// the row-order compaction of each tree's codes -- 1.26e9 records at the
-// headline, written and read back once (count + scatter: ~4.3 ms per step).
-// Here a work item is (tree, row range) and each wave compacts its own rows'
-// records on the fly into a 256-entry LDS ring: one coalesced 64-row load of
+// Levels with at most one built node per tree (level 0: the roots; level 1:
+// the smaller child) without item records: the level's records (row, weight,
+// quantised label) are the row-order compaction of each tree's codes for that
+// node -- 1.26e9 records at level 0 of the headline, written and read back
+// once (count + scatter: ~4.3 ms per step at level 0, ~3 ms at level 1).
+// Here a work item is (slot, row range), sinfo[slot] = (tree, local node), and
+// each wave compacts its own rows' records on the fly into a 256-entry LDS ring: one coalesced 64-row load of
 // the tree's codes and labels (the next window's already in flight), a ballot
 // and mbcnt rank, one ds_write_b64 per item; then the lane10 trip consumes 96
 // ring entries.  The gathers of a wave walk consecutive rows (each line is read
@@ -618,13 +619,17 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_kernel(const SegHistArgs
 template <int BP>
 __global__ __launch_bounds__(1024) void seg_hist_lane10_root_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins8,
                                                                     const uint16_t* __restrict__ codes,
-                                                                    const float* __restrict__ v1, float qs1, int slot0) {
+                                                                    const float* __restrict__ v1, float qs1,
+                                                                    const int* __restrict__ sinfo, int slot0) {
   constexpr int TH = 1024, NW = TH / 64, U = 16, IPW = 6, NI = IPW * U, RING = 256;  // NI - 1 + 64 < RING
   constexpr int PLANE = BP * 32;
   __shared__ __attribute__((aligned(16))) unsigned long long h[10 * PLANE];  // [10][BP][32]
   __shared__ __attribute__((aligned(16))) uint64_t ring[NW][RING];
-  const int r0 = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], tree = a.work[3 * blockIdx.x + 2];
-  if (!CDNA_DCHECK(r0 >= 0 && len >= 0 && tree >= 0 && (int64_t)r0 + len <= a.n, 0x5E85u)) return;
+  const int r0 = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
+  const int tree = sinfo[2 * slot];
+  const uint32_t node = (uint32_t)sinfo[2 * slot + 1];
+  if (!CDNA_DCHECK(r0 >= 0 && len >= 0 && slot >= slot0 && tree >= 0 && node < 0xFFu && (int64_t)r0 + len <= a.n,
+                   0x5E85u)) return;
   for (int i = threadIdx.x; i < 10 * PLANE; i += TH) h[i] = 0ull;
   __syncthreads();
   const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
@@ -655,7 +660,7 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_root_kernel(const SegHis
       const int64_t r = wr + lane;
       wr += 64;
       fetch(wr + lane);
-      const bool has = (cw & 0xFFu) != 0xFFu && (cw >> 8) != 0u;
+      const bool has = (cw & 0xFFu) == node && (cw >> 8) != 0u;
       const uint64_t m = __builtin_amdgcn_ballot_w64(has);
       if (has) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -710,7 +715,7 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_root_kernel(const SegHis
     if (!cnt) continue;
     const unsigned long long m = (1ull << kPackShift) - 1ull;
     const long long sum = (long long)((v0 & m) + (v1c & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt;
-    unsigned long long* o = &a.out[(((int64_t)(tree - slot0) * a.d + f) * a.B + bn) * 2];
+    unsigned long long* o = &a.out[(((int64_t)(slot - slot0) * a.d + f) * a.B + bn) * 2];
     atomicAdd(o, cnt);
     atomicAdd(o + 1, (unsigned long long)sum);
   }
@@ -1325,17 +1330,18 @@ __global__ __launch_bounds__(256) void bins_row_major_kernel(const uint64_t* __r
 
 }  // namespace
 
-// Level-0 record histograms straight from the codes (seg_hist_lane10_root_kernel): bins in the seg10 row layout,
-// work [nwork][3] {row start, row count, tree}; tree t's sums go to out slot t - slot0 (a slot-range slice).
-// Row counts per work item must keep count x max weight below 2^20 (the packed LDS cells).
+// Record histograms straight from the codes (seg_hist_lane10_root_kernel) for levels with <= 1 built node per
+// tree: bins in the seg10 row layout, work [nwork][3] {row start, row count, slot}, sinfo [S][2] {tree, local
+// node of the slot}; slot s's sums go to out slot s - slot0 (a slot-range slice).  Row counts per work item
+// must keep count x max weight / 3 below 2^20 (the packed LDS cells).
 CDNA_API int cdna_seg_hist_root(const uint8_t* bins_s10, int64_t n, int d, int B, const uint16_t* codes,
-                                const float* v1, float qs1, const int* work, int nwork, int slot0,
+                                const float* v1, float qs1, const int* work, int nwork, const int* sinfo, int slot0,
                                 unsigned long long* out, hipStream_t st) {
   if (nwork <= 0) return 0;
   if (d > 100 || B > 40 || B < 1) return (int)hipErrorInvalidValue;
   SegHistArgs a{nullptr, n, d, B, nullptr, nullptr, v1, nullptr, work, 1.f, qs1, out};
   auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), 0, st, a, bins_s10, codes, v1, qs1, slot0);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), 0, st, a, bins_s10, codes, v1, qs1, sinfo, slot0);
   };
   if (B <= 32) launch(seg_hist_lane10_root_kernel<32>);
   else launch(seg_hist_lane10_root_kernel<40>);

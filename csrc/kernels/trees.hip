@@ -319,6 +319,21 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
   // holding features 10 s .. 10 s + 9 in its first 10 bytes (2 zero bytes, 8 zero bytes after chunk 9), so one
   // aligned dwordx3 gather brings a lane its 10 features.  Output dword k of a row = row bytes
   // [10 s + p, 10 s + p + 4) with s = 4k / 12, p = 4k % 12 (an alignbyte of two tile dwords; p = 8 keeps 2 bytes).
+  // seg10: a thread's 16-byte chunk c = i & 7 is the same on every trip (the block size 64 G is a multiple of
+  // 8), so its four source dword pairs, byte shifts and masks are fixed before the tile loop
+  int s10_src[4];
+  uint32_t s10_sh[4], s10_mask[4];
+  {
+    const int c = threadIdx.x & 7;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * c + e, sg = (4 * k) / 12, p = (4 * k) - 12 * sg;
+      const int f0 = 10 * sg + p;  // even: the dword pair (f0 >> 2, +1) shifted by 0 or 2 bytes
+      s10_src[e] = sg < 10 ? (f0 >> 2) : 0;
+      s10_sh[e] = (uint32_t)(f0 & 3);
+      s10_mask[e] = sg < 10 ? (p == 8 ? 0xFFFFu : 0xFFFFFFFFu) : 0u;
+    }
+  }
   auto store_rm = [&](int64_t tl) {
     const int rows = (int)((n - tl * RT) < RT ? (n - tl * RT) : RT);
     for (int i = threadIdx.x; i < RT * 8; i += nth) {
@@ -330,17 +345,8 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
           const uint32_t* td = reinterpret_cast<const uint32_t*>(tile + row * TP);
           uint32_t o[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int k = 4 * c + e, s = (4 * k) / 12, p = (4 * k) - 12 * s;
-            const int f0 = 10 * s + p;  // even: the dword pair (f0 >> 2, +1) shifted by 0 or 2 bytes
-            uint32_t wv = 0u;
-            if (s < 10) {
-              const uint32_t lo = td[f0 >> 2], hi = td[(f0 >> 2) + 1];
-              wv = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(f0 & 3));
-              if (p == 8) wv &= 0xFFFFu;
-            }
-            o[e] = wv;
-          }
+          for (int e = 0; e < 4; ++e)
+            o[e] = __builtin_amdgcn_alignbyte(td[s10_src[e] + 1], td[s10_src[e]], s10_sh[e]) & s10_mask[e];
           v.x = o[0]; v.y = o[1]; v.z = o[2]; v.w = o[3];
           *reinterpret_cast<uint4*>(rm + (tl * RT + row) * 16 + 2 * c) = v;
         } else {

@@ -1068,6 +1068,10 @@ def test_seg10_rows_and_lane10_histogram(dev, d, B, monkeypatch):
         rgot = K.seg_hist_root(s10, d, B, rcodes, v1, sc[1], 12, t0, t1,
                                torch.zeros((t1 - t0, d, B, 2), dtype=torch.int64, device=dev))
         assert torch.equal(rgot.cpu(), rref[t0:t1].cpu())
+    # one built node per tree below the root: local node 1 of every tree is slot 2 t + 1 of the record path
+    cgot = K.seg_hist_codes(s10, d, B, codes, v1, sc[1], 12, np.arange(T), np.ones(T, np.int64), 0, T,
+                            torch.zeros((T, d, B, 2), dtype=torch.int64, device=dev))
+    assert torch.equal(cgot.cpu(), ref[1::2].cpu())
 
 
 @pytest.mark.parametrize("d,maxb,n,missing", [(100, 40, 100003, None), (64, 256, 5001, None), (8, 2, 77, None),
