@@ -1068,6 +1068,9 @@ def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_glob
 
 
 SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "2048"))
+# three-times-larger record chunks for the six-items-per-wave kernel (its count field is spread over three cell
+# copies): measured 145.1 vs 139.8 ms per headline step (fewer, longer blocks) and neutral at 1.25e7 rows -- off
+LANE10_CHUNK3 = __import__("os").environ.get("CDNAML_LANE10_CHUNK3", "0") != "0"
 # record histograms through the lane-feature kernel (seg_hist_lane_kernel: lanes own features, bin-major
 # conflict-free LDS planes, one v_perm per cell address); B <= 80 (4 planes <= 80 KB of LDS), 80 < B <= 256:
 # seg_hist_lane4_kernel (64 features per block, a quarter-wave per item; CDNAML_SEG_WIDE=0 keeps the flat kernel)
@@ -1201,7 +1204,12 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
     else:
         assert bins_rm is not None and rec.dtype == torch.int64
         wm = int(max(1, min(255, wmax)))
-        chunk = _fill_chunk(segs, min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1)), B)
+        cap = (1 << 20) // (wm + 1)
+        if rm_s10 and LANE10_CHUNK3:
+            # the six-items-per-wave kernel spreads a block's items over three copies of every cell (item i of the
+            # chunk -> copy i % 3): each copy's 20-bit count holds a third of the chunk
+            cap = 3 * cap - 1024
+        chunk = _fill_chunk(segs, min(SEG_HIST_CHUNK * (3 if rm_s10 and LANE10_CHUNK3 else 1), cap), B)
         work = _seg_work(segs, chunk)
         if len(work) == 0:
             if out is not None:
@@ -1226,6 +1234,9 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
     return out
 
 
+CODES_HIST_BLOCKS = int(__import__("os").environ.get("CDNAML_CODES_HIST_BLOCKS", "0"))
+
+
 def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, v1: torch.Tensor, qs1: float,
                    wmax: int, slot_tree: np.ndarray, slot_node: np.ndarray, s0: int, s1: int,
                    out: torch.Tensor) -> torch.Tensor:
@@ -1247,6 +1258,13 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
     # each LDS cell copy takes every third item of a wave's stream: rows x wmax / 3 (+ a partial trip per
     # wave) stays below the 20-bit count field
     rows = max(64, min(n, 3 * ((1 << 20) // (wm + 1)) - 16 * 64))
+    # CDNAML_CODES_HIST_BLOCKS > 0: shrink the row chunks toward that many blocks (>= 16k rows each).  Off by
+    # default: at the per-rank 1.25e7 shape 4096 blocks ran 21.0-21.3 ms per step vs 20.0-20.1 ms with the
+    # largest chunks (the per-block LDS clear + flush of 100 KB outweighs the emptier last round)
+    S_l = max(1, s1 - s0)
+    if CODES_HIST_BLOCKS > 0:
+        rows = max(min(rows, 16384), min(rows, -(-(n * S_l) // CODES_HIST_BLOCKS)))
+    rows = (rows + 63) // 64 * 64
     C = (n + rows - 1) // rows
     # XCD-aware order: block b runs on XCD b % 8; the slots (trees) of row chunk c are consecutive blocks of
     # XCD c % 8, so their row-line gathers and label reads share that XCD's L2

@@ -10,6 +10,16 @@ import sys
 VARIANTS = {
     "v2": {"CDNAML_BINIZE_V5": "0"},
     "v5": {},
+    "v5_seg10": {"AB_S10": "1"},
+}
+# round 3 A/B (1x MI355X, 1e8 x 100 fp32, 40 bins): v5 16.02 ms, v5 + seg10 rows 16.72 ms; a third register set
+# (two tiles of loads in flight) 16.33 / 17.04 ms; non-temporal X loads 31.2 ms (2x slower) -- both dropped,
+    "v5_3sets": {"CDNAML_BINIZE_VAR": "1"},
+    "v5_nt": {"CDNAML_BINIZE_VAR": "2"},
+    "v5_3sets_nt": {"CDNAML_BINIZE_VAR": "3"},
+    "v5_seg10": {"AB_S10": "1"},
+    "v5_seg10_3sets": {"AB_S10": "1", "CDNAML_BINIZE_VAR": "1"},
+    "v5_seg10_nt": {"AB_S10": "1", "CDNAML_BINIZE_VAR": "2"},
 }
 
 
@@ -26,12 +36,12 @@ def child() -> None:
     nthr = torch.full((d,), nb - 1, dtype=torch.int32, device=dev)
     ref = None
     for _ in range(2):
-        b, rm = K.binize(X, thr, nthr, want_rm=True)
+        b, rm = K.binize(X, thr, nthr, want_rm=True, rm_layout="s10" if os.environ.get("AB_S10") else "std")
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(5):
-        b, rm = K.binize(X, thr, nthr, want_rm=True)
+        b, rm = K.binize(X, thr, nthr, want_rm=True, rm_layout="s10" if os.environ.get("AB_S10") else "std")
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / 5
