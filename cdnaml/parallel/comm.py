@@ -368,11 +368,13 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: Optional[float] 
         return
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
-    backend = "nccl" if device_type == "cuda" else "gloo"
+    # CDNAML_COMM_BACKEND=gloo on GPUs: host-staged collectives, so several ranks can share one GPU (a 1-GPU box
+    # rehearses the multi-rank GPU code path: ranks map to cuda:(LOCAL_RANK % device_count))
+    backend = os.environ.get("CDNAML_COMM_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     kwargs = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
     if backend == "nccl":
-        lr = int(os.environ.get("LOCAL_RANK", "0"))
+        lr = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(lr)
         kwargs["device_id"] = torch.device("cuda", lr)
     dist.init_process_group(**kwargs)
