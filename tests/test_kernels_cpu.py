@@ -68,6 +68,25 @@ def test_binize_matches_searchsorted():
         assert torch.equal(bm[:, f].long(), ref)
 
 
+@pytest.mark.parametrize("d", [100, 84, 7])
+def test_bins_seg10_layout(d):
+    """seg10 rows (the six-items-per-wave histogram's layout, binize rm_layout="s10"): 128 bytes per row, byte
+    12 s + p holds feature 10 s + p, the two bytes after each 10-feature chunk and the last 8 bytes are zero."""
+    X, thr, nthr, bins = _bins(n=257, d=d, B=40)
+    s10 = K.bins_seg10(bins, d)
+    assert s10.shape == (257, 16, 8) and s10.dtype == torch.uint8
+    flat = s10.reshape(257, 128).long()
+    bm = K.bins_to_matrix(bins, d).long()
+    used = torch.zeros(128, dtype=torch.bool)
+    for f in range(d):
+        pos = 12 * (f // 10) + f % 10
+        assert torch.equal(flat[:, pos], bm[:, f])
+        used[pos] = True
+    assert not flat[:, ~used].any()
+    with pytest.raises(ValueError):
+        K.bins_seg10(torch.zeros((13, 4, 8), dtype=torch.uint8), 101)
+
+
 def test_hist_moments_bruteforce():
     X, thr, nthr, bins = _bins(n=300, d=5, B=8)
     n, d, B = 300, 5, 8
