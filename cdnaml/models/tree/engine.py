@@ -61,7 +61,14 @@ PARTITION_RM = __import__("os").environ.get("CDNAML_PARTITION_RM", "0") != "0"
 # row-major bins (one or two 64 B lines) then feeds 34 atomics instead of 104
 MSEG_SUBSET = __import__("os").environ.get("CDNAML_MSEG_SUBSET", "0") != "0"
 # multi-rank record histograms: slot chunks whose all-reduces overlap the next chunk's histogram kernel
-HIST_OVERLAP = int(__import__("os").environ.get("CDNAML_HIST_OVERLAP", "4"))
+HIST_OVERLAP = int(__import__("os").environ.get("CDNAML_HIST_OVERLAP", "2"))
+# ... only for level histograms of at least this many bytes: at the 8-GPU point's per-rank shape (1.25e7 rows)
+# building a level in 4 / 2 slot chunks cost 22.2 / 20.6 ms per step vs 19.9 ms in one launch (each chunk's
+# launch ends in a partly idle round of blocks), while a <= 10 MB RCCL all-reduce over xGMI takes ~0.1-0.2 ms
+HIST_OVERLAP_MIN_BYTES = int(__import__("os").environ.get("CDNAML_HIST_OVERLAP_MIN_BYTES", str(64 << 20)))
+# take the slot-chunked (overlapped all-reduce) histogram path on one rank too: measures its launch cost at a
+# per-rank shape on a 1-GPU box
+HIST_OVERLAP_FORCE = __import__("os").environ.get("CDNAML_HIST_OVERLAP_FORCE", "0") != "0"
 # feature-subset regression forests (RandomForestRegressor, featureSubsetStrategy auto / onethird / sqrt ...):
 # every node of a level built over its m sampled features only, items generated from the row codes on the fly
 # (subhist.hip) -- no record compaction, no sibling subtraction, 34 instead of 100 lane-ops per item.  Exact
@@ -1000,7 +1007,7 @@ class ForestTrainer:
                     h.wait()
         return Hc
 
-    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev, root=None):
+    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev):
         """Record histograms of a level's S slots in HIST_OVERLAP slot chunks; chunk c's all-reduce runs on the
         collective stream while chunk c + 1 is built (one per-level RCCL all-reduce of 1-50 MB otherwise
         serialises with the compute stream).  The sums are exact integers, so the result is identical to one
@@ -1015,15 +1022,11 @@ class ForestTrainer:
             if s1 <= s0:
                 continue
             with _tr.span("tree.hist_chunk", slots=s1 - s0):
-                if root is not None:  # <= 1 built node per tree: records compacted in the kernel
-                    K.seg_hist_codes(data.bins_s10, d, B, root[0], root[1], scales[1], wmax, root[2], root[3], s0,
-                                     s1, Hb[s0:s1])
-                else:
-                    sel = (sb[:, 2] >= s0) & (sb[:, 2] < s1)
-                    sbc = sb[sel].copy()
-                    sbc[:, 2] -= s0
-                    K.seg_hist(data.bins, d, B, rec, None, None, None, sbc, s1 - s0, wmax, scales, bins_rm=rm,
-                               interleave=True, rec=True, raw=True, out=Hb[s0:s1], rm_s10=s10)
+                sel = (sb[:, 2] >= s0) & (sb[:, 2] < s1)
+                sbc = sb[sel].copy()
+                sbc[:, 2] -= s0
+                K.seg_hist(data.bins, d, B, rec, None, None, None, sbc, s1 - s0, wmax, scales, bins_rm=rm,
+                           interleave=True, rec=True, raw=True, out=Hb[s0:s1], rm_s10=s10)
             with _tr.span("tree.allreduce_async", cat="comm", bytes=(s1 - s0) * d * B * 16):
                 pend.append(self.comm.all_reduce_async(Hb[s0:s1]))
         with _tr.span("tree.allreduce_wait", cat="comm"):
@@ -1146,14 +1149,12 @@ class ForestTrainer:
                 elif root_ok:
                     S_b = len(build_ids)
                     sl_node = build_ids - tfirst.numpy()[slot_tree]  # the slot's local node in its tree's codes
-                    root = (codes, stats_rows["v1"], slot_tree, sl_node)
-                    if self.comm.distributed and HIST_OVERLAP > 1 and S_b >= 2:
-                        Hb = self._hist_overlapped(data, d, B, None, None, S_b, wmax, mseg_scales, dev, root=root)
-                        reduced = True
-                    else:
-                        Hb = K.seg_hist_codes(data.bins_s10, d, B, codes, stats_rows["v1"], mseg_scales[1], wmax,
-                                              slot_tree, sl_node, 0, S_b,
-                                              torch.zeros((S_b, d, B, 2), dtype=torch.int64, device=dev))
+                    # one launch for every slot, then the level's one all-reduce: these levels hold one node per
+                    # tree (20 x 100 x 40 cells = 1.3 MB at the headline), too little to overlap, and slot chunks
+                    # of a 1.25e7-row shard would launch ~1 round of blocks each (half of it idle)
+                    Hb = K.seg_hist_codes(data.bins_s10, d, B, codes, stats_rows["v1"], mseg_scales[1], wmax,
+                                          slot_tree, sl_node, 0, S_b,
+                                          torch.zeros((S_b, d, B, 2), dtype=torch.int64, device=dev))
                     hist_raw_scale = mseg_raw
                 elif use_mseg and (depth >= 1 or MSEG_L0):
                     # gather the rows of the built nodes into slot segments, then segment histograms
@@ -1170,7 +1171,9 @@ class ForestTrainer:
                         Hb = K.seg_hist_subset(data.bins, d, B, perm, v1p, wp, sb, len(build_ids), wmax, feats,
                                                mseg_scales, bins_rm=data.row_major_bins() if dev.type == "cuda"
                                                else None, interleave=True)
-                    elif is_rec and self.comm.distributed and HIST_OVERLAP > 1 and len(build_ids) >= 2:
+                    elif is_rec and (self.comm.distributed or HIST_OVERLAP_FORCE) and HIST_OVERLAP > 1 and \
+                            len(build_ids) >= 2 and \
+                            len(build_ids) * d * B * 16 >= HIST_OVERLAP_MIN_BYTES:
                         # comm/compute overlap: the level's slots are built in chunks, each chunk's int64
                         # histogram all-reduced (async, RCCL stream) while the next chunk is built
                         Hb = self._hist_overlapped(data, d, B, perm, sb, len(build_ids), wmax, mseg_scales, dev)

@@ -91,8 +91,8 @@ def test_fault_spec_parsing():
         _parse_fault("3-barrier")
 
 
-def _bench(tmp_path, nproc, rows="3e4", extra=()):
-    env = dict(os.environ, CDNAML_DEVICE="cpu", OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+def _bench(tmp_path, nproc, rows="3e4", extra=(), env_extra=None):
+    env = dict(os.environ, CDNAML_DEVICE="cpu", OMP_NUM_THREADS="1", PYTHONPATH=ROOT, **(env_extra or {}))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     args = [os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--rows", rows, "--steps", "1", "--warmup", "0",
@@ -121,7 +121,10 @@ def test_bench_trains_identical_forest_on_1_2_4_8_ranks(tmp_path):
     world size must print the same node count and forest digest."""
     ref = None
     for w in (1, 2, 4, 8):
-        res, tag = _bench(tmp_path, w)
+        # W = 2 and 8 build every level in slot chunks whose all-reduces overlap the next chunk
+        # (_hist_overlapped; by default only for level histograms of >= 64 MiB)
+        ov = {"CDNAML_HIST_OVERLAP_MIN_BYTES": "0"} if w in (2, 8) else None
+        res, tag = _bench(tmp_path, w, env_extra=ov)
         if ref is None:
             ref = tag
         assert tag == ref, (w, tag, ref)

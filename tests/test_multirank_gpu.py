@@ -1,9 +1,9 @@
 """Multi-rank GPU code path rehearsed on one GPU.
 
 The driver's 8-GPU scaling runs take the RCCL path of the tree engine: level histograms built in slot chunks
-whose all-reduces overlap the next chunk (``ForestTrainer._hist_overlapped``, incl. the record-free level-0/1
-kernel), device-side split decode, per-rank row shards.  A 1-GPU box cannot start RCCL with two ranks on one
-device, so here 2 and 3 ranks share cuda:0 over ``gloo`` (CDNAML_COMM_BACKEND=gloo: host-staged collectives,
+whose all-reduces overlap the next chunk (``ForestTrainer._hist_overlapped``), the record-free level-0/1
+kernel on each rank's shard, device-side split decode, per-rank row shards.  A 1-GPU box cannot start RCCL with
+two ranks on one device, so here 2 and 3 ranks share cuda:0 over ``gloo`` (CDNAML_COMM_BACKEND=gloo: host-staged collectives,
 the same int64 sums) and must grow the forest the single-rank run grows: bench.py's digest is a function of the
 global table only (rows keyed by global row id), whatever the GPU count.
 """
