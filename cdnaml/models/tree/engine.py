@@ -52,6 +52,8 @@ NATIVE_SPLIT = __import__("os").environ.get("CDNAML_NATIVE_SPLIT", "1") != "0"
 MSEG_REC = __import__("os").environ.get("CDNAML_MSEG_REC", "1") != "0"
 # level 0 on seg10 rows: root records compacted inside the histogram kernel (no codes_compact pass)
 ROOT_HIST = __import__("os").environ.get("CDNAML_ROOT_HIST", "1") != "0"
+# binning queued on the quantile kernel's device thresholds, checked on the host behind it
+SPEC_THRESHOLDS = __import__("os").environ.get("CDNAML_SPEC_THRESHOLDS", "1") != "0"
 # single-output forests of depth <= 8 predict from a heap layout (8-byte nodes, fixed-step walks)
 HEAP_PREDICT = __import__("os").environ.get("CDNAML_HEAP_PREDICT", "1") != "0"
 # row-record partition gathers split bins from the row-major copy (one line per row) instead of [G][n]
@@ -311,13 +313,30 @@ def _make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins
         raise IllegalArgumentException("maxBins must be <= 256 on this engine (uint8 bins)")
     n = X.shape[0]
     samp = _global_sample(session, X, max_bins, seed, row_offset, n_global)
+    s10 = _seg10_ok(X, d, max_bins)
+    if SPEC_THRESHOLDS and not categorical and X.is_cuda:
+        # the binning queued straight on the K3 kernel's device thresholds; the host checks behind it that every
+        # feature had more than max_bins distinct sample values (then the thresholds are exactly the host path's)
+        # -- no device -> host -> device round trip between the quantile kernel and the binning
+        with _tr.span("tree.find_thresholds"):
+            q = K.quantile_thresholds_dev(samp, max_bins)
+        if q is not None:
+            thr_d, nthr_d, pend = q
+            with _tr.span("tree.binize"):
+                bins, rm = K.binize(X, thr_d.float(), nthr_d, want_rm=True, rm_layout="s10" if s10 else "std")
+            thr, ints = pend.get()
+            if bool((ints[1] > max_bins).all()):
+                thr, nthr = thr.copy(), ints[0].copy()
+                if s10:
+                    return BinnedData(X, bins, thr, nthr, {}, n, n_global, row_offset, d, max_bins, False, None, rm)
+                return BinnedData(X, bins, thr, nthr, {}, n, n_global, row_offset, d, max_bins, False, rm)
+            del bins, rm  # a feature with few distinct values: the host path below, then bin again
     with _tr.span("tree.find_thresholds"):
         thr, nthr = find_thresholds_t(samp.double(), max_bins, categorical)
     thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
     nthr_t = torch.from_numpy(nthr).to(X.device)
     with _tr.span("tree.binize"):
         # the row-major copy (segment histograms' row gathers) comes out of the same kernel
-        s10 = _seg10_ok(X, d, max_bins)
         bins, rm = K.binize(X, thr_t, nthr_t, want_rm=True, rm_layout="s10" if s10 else "std")
     if s10:
         return BinnedData(X, bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins, False,

@@ -231,6 +231,40 @@ def quantile_thresholds(samp: torch.Tensor, max_bins: int):
     return thr.cpu().numpy(), ih[0].copy(), ih[1].copy(), sorted_
 
 
+class _HostCopies:
+    """Device tensors copied to pinned host buffers behind the work already queued; ``get()`` waits for them."""
+
+    def __init__(self, *ts: torch.Tensor):
+        self.h = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in ts]
+        for hb, t in zip(self.h, ts):
+            hb.copy_(t, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record(torch.cuda.current_stream(ts[0].device))
+
+    def get(self):
+        self.ev.synchronize()
+        return [hb.numpy() for hb in self.h]
+
+
+def quantile_thresholds_dev(samp: torch.Tensor, max_bins: int):
+    """K3 without a host round trip: (thr [d, max_bins-1] fp64, nthr [d] int32 -- both device tensors --, pending
+    host copies of (thr, nthr, kdist)), or None where :func:`quantile_thresholds` does not apply.  The binning can be
+    queued on the device thresholds at once; they equal the host path's only where every feature has more than
+    ``max_bins`` distinct values (kdist), which the caller checks on the host copy once it has queued the binning."""
+    s, d = samp.shape
+    if not _native(samp) or s == 0 or s > QUANTILE_MAX_S or not (2 <= max_bins <= 257):
+        return None
+    samp = samp.double().contiguous()
+    dev = samp.device
+    sorted_ = torch.empty((d, s), dtype=torch.float64, device=dev)
+    thr = torch.empty((d, max_bins - 1), dtype=torch.float64, device=dev)
+    ints = torch.empty((2, d), dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().cdna_quantile_thresholds(_ptr(samp), s, d, max_bins, _ptr(sorted_), _ptr(thr),
+                                                   _ptr(ints[0]), _ptr(ints[1]), _stream(dev)),
+               "cdna_quantile_thresholds")
+    return thr, ints[0], _HostCopies(thr, ints)
+
+
 # --------------------------------------------------------------------- K4
 def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Optional[float] = None,
            want_rm: bool = False, rm_layout: str = "std"):
@@ -1268,16 +1302,15 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
     C = (n + rows - 1) // rows
     # XCD-aware order: block b runs on XCD b % 8; the slots (trees) of row chunk c are consecutive blocks of
     # XCD c % 8, so their row-line gathers and label reads share that XCD's L2
-    work = []
-    for cq in range((C + 7) // 8):
-        for sl in range(s0, s1):
-            for x in range(8):
-                c = cq * 8 + x
-                if c < C:
-                    r0 = c * rows
-                    work.append((r0, min(rows, n - r0), sl))
+    nq = (C + 7) // 8
+    cq, sl, x = np.meshgrid(np.arange(nq), np.arange(s0, s1), np.arange(8), indexing="ij")  # (cq, slot, x) order
+    c = (cq * 8 + x).reshape(-1)
+    keep = c < C
+    c, sl = c[keep], sl.reshape(-1)[keep]
+    r0 = c * rows
+    work = np.stack([r0, np.minimum(rows, n - r0), sl], 1).astype(np.int32)
     sinfo = np.stack([st, sn], 1).astype(np.int32).reshape(-1)
-    wt, si = upload(codes.device, np.asarray(work, dtype=np.int32).reshape(-1), sinfo)
+    wt, si = upload(codes.device, work.reshape(-1), sinfo)
     v1c = v1.float().contiguous()
     _lib.check(_lib.lib().cdna_seg_hist_root(_ptr(bins_s10), n, d, B, _ptr(codes), _ptr(v1c), float(qs1), _ptr(wt),
                                              len(work), _ptr(si), s0, _ptr(out), _stream(codes.device)),
