@@ -77,6 +77,30 @@ def test_forest_gpu_equals_cpu(sessions):
     np.testing.assert_allclose(out[0][2], out[1][2], rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("few_distinct", [False, True])
+def test_binning_on_device_thresholds_equals_host_path(sessions, monkeypatch, few_distinct):
+    """make_binned queues the binning on the quantile kernel's device thresholds and checks the distinct-value
+    condition behind it; with a low-cardinality continuous column (3 values) the check fails and the host path
+    re-bins.  Either way the thresholds, bins and seg10 rows equal the host-threshold path's."""
+    from cdnaml.models.tree import engine
+    rng = np.random.default_rng(5)
+    n, d = 40000, 96
+    X = rng.normal(size=(n, d)).astype(np.float32)
+    if few_distinct:
+        X[:, 3] = rng.integers(0, 3, n).astype(np.float32)
+    Xd = torch.from_numpy(X).cuda()
+    got = []
+    for spec in (True, False):
+        monkeypatch.setattr(engine, "SPEC_THRESHOLDS", spec)
+        b = engine._make_binned(sessions, Xd, {}, 40, 7, 0, n)
+        got.append((b.thresholds, b.nthr, b.bins.cpu(), b.record_rows()[0].cpu()))
+    np.testing.assert_array_equal(got[0][1], got[1][1])
+    for f in range(d):
+        k = int(got[1][1][f])
+        np.testing.assert_array_equal(got[0][0][f, :k], got[1][0][f, :k])
+    assert torch.equal(got[0][2], got[1][2]) and torch.equal(got[0][3], got[1][3])
+
+
 def test_classifiers_gpu(sessions):
     from cdnaml.ml.classification import GBTClassifier, LogisticRegression, RandomForestClassifier
     from cdnaml.ml.evaluation import BinaryClassificationEvaluator
