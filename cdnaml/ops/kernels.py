@@ -1269,6 +1269,14 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
 
 
 CODES_HIST_BLOCKS = int(__import__("os").environ.get("CDNAML_CODES_HIST_BLOCKS", "0"))
+CODES_ROUND_FILL = __import__("os").environ.get("CDNAML_CODES_ROUND_FILL", "1") != "0"
+_NCU = {}
+
+
+def _num_cus(dev) -> int:
+    if dev.index not in _NCU:
+        _NCU[dev.index] = int(torch.cuda.get_device_properties(dev).multi_processor_count)
+    return _NCU[dev.index]
 
 
 def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, v1: torch.Tensor, qs1: float,
@@ -1300,6 +1308,17 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
         rows = max(min(rows, 16384), min(rows, -(-(n * S_l) // CODES_HIST_BLOCKS)))
     rows = (rows + 63) // 64 * 64
     C = (n + rows - 1) // rows
+    if CODES_ROUND_FILL and C * S_l < 64 * _num_cus(codes.device):
+        # one block per CU: grow the chunk count to the next whole round of blocks (at most +25 %), so the last
+        # round is not a handful of blocks on an otherwise idle chip (1.25e7 rows x 20 trees: 1040 -> 1280)
+        ncu = _num_cus(codes.device)
+        C2 = C
+        while (C2 * S_l) % ncu and C2 < C * 5 // 4:
+            C2 += 1
+        if (C2 * S_l) % ncu == 0:
+            C = C2
+            rows = (-(-n // C) + 63) // 64 * 64
+            C = (n + rows - 1) // rows
     # XCD-aware order: block b runs on XCD b % 8; the slots (trees) of row chunk c are consecutive blocks of
     # XCD c % 8, so their row-line gathers and label reads share that XCD's L2
     nq = (C + 7) // 8
