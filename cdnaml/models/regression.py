@@ -195,7 +195,10 @@ class LinearRegression(Estimator):
         host = torch.cat([G.reshape(-1), sh if sh is not None else G.new_zeros(d + 1)]).cpu().numpy()
         G = host[:(d + 2) * (d + 2)].reshape(d + 2, d + 2)
         yshift = float(host[-1]) if fit_int else 0.0
-        coef, intercept, hist, iters, stderr = self._solve(G, d, shift, yshift)
+        # the f32 shift the Gram kernel subtracted, from the same host copy (no second device read)
+        shift_h = host[(d + 2) * (d + 2):(d + 2) * (d + 2) + d].astype(np.float32).astype(np.float64) \
+            if shift is not None else None
+        coef, intercept, hist, iters, stderr = self._solve(G, d, shift_h, yshift)
         model = LinearRegressionModel(coef, intercept)
         model._post_fit(self)
         preds = model.transform(dataset)
@@ -210,7 +213,7 @@ class LinearRegression(Estimator):
         sx, sy = G[:d, d], G[d + 1, d]
         Sxx, Sxy, Syy = G[:d, :d], G[:d, d + 1], G[d + 1, d + 1]
         fit_int = self.getFitIntercept()
-        s = shift.double().cpu().numpy() if shift is not None else np.zeros(d)
+        s = np.asarray(shift, dtype=np.float64) if shift is not None else np.zeros(d)
         mx = s + sx / n
         my = yshift + sy / n
         Cxx = Sxx - np.outer(sx, sx) / n
