@@ -3,6 +3,7 @@
 
     python bench_configs.py lr        # 2: LinearRegression normal equations, bf16 MFMA Gram, 1e7 x 100
     python bench_configs.py cv        # 3: RandomForestRegressor + CrossValidator grid, 1e8 x 100
+    python bench_configs.py clf       # L07 at scale: RandomForestClassifier + CrossValidator grid, 1e7 x 100
     python bench_configs.py gbdt      # 4: XGBoost-style GBDT, depth 8, 1e8 x 100 (rounds/s; --trees)
     python bench_configs.py infer     # 5: batch inference of a trained RF over 1e9 streamed rows (transform)
     python bench_configs.py airbnb    # 1: ML 02 LinearRegression on the Airbnb-SF schema (CPU plumbing)
@@ -101,6 +102,27 @@ def bench_lr(spark, args):
     _emit(spark, "rows/sec LinearRegression.fit (normal equations, bf16 MFMA Gram)", n_total / (ms / 1e3),
           "rows/s", args.steps, args.warmup, ms, True, "strong", "bf16", "LinearRegression(d=100)", n_total,
           f"dp{spark.comm.world_size}")
+
+
+def bench_clf(spark, args):
+    """Labs/ML 07L:105-141 at scale: RandomForestClassifier (Gini) over a 2x2 grid of maxDepth x numTrees with
+    3-fold CrossValidator and a BinaryClassificationEvaluator, 1e7 x 100 binary labels.  The classification level
+    loop runs the class-count histograms and the native K6 (split_scan_ex: Gini on class counts)."""
+    from cdnaml.ml.classification import RandomForestClassifier
+    from cdnaml.ml.evaluation import BinaryClassificationEvaluator
+    from cdnaml.ml.tuning import CrossValidator, ParamGridBuilder
+    n_total = int(args.rows or 1e7)
+    df, n = _data(spark, n_total, 100, cls=True)
+    rf = RandomForestClassifier(maxBins=40, seed=42)
+    grid = ParamGridBuilder().addGrid(rf.maxDepth, [2, 5]).addGrid(rf.numTrees, [5, 10]).build()
+    cv = CrossValidator(estimator=rf, estimatorParamMaps=grid, evaluator=BinaryClassificationEvaluator(),
+                        numFolds=3, seed=42)
+    ms, model = _timed(spark, lambda: cv.fit(df), args.steps, args.warmup)
+    _log(f"RF classifier CV {ms:.1f} ms for {len(grid) * 3 + 1} fits, best maxDepth={model.bestModel.getMaxDepth()}, "
+         f"AUC {max(model.avgMetrics):.4f}")
+    _emit(spark, "rows/sec CrossValidator(RandomForestClassifier grid 2x2, 3 folds) fit", n_total / (ms / 1e3),
+          "rows/s", args.steps, args.warmup, ms, True, "strong", "fp32", "RandomForestClassifier(maxBins=40) CV 2x2x3",
+          n_total, f"dp{spark.comm.world_size}")
 
 
 def bench_cv(spark, args):
@@ -300,7 +322,7 @@ def bench_airbnb(spark, args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("config", choices=["lr", "cv", "gbdt", "infer", "airbnb", "relational", "expr"])
+    ap.add_argument("config", choices=["lr", "cv", "clf", "gbdt", "infer", "airbnb", "relational", "expr"])
     ap.add_argument("--rows", type=float, default=None)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
@@ -315,7 +337,7 @@ def main():
     TRACE = args.trace or None
     import cdnaml
     spark = cdnaml.SparkSession.builder.appName("bench_configs").getOrCreate()
-    {"lr": bench_lr, "cv": bench_cv, "gbdt": bench_gbdt, "infer": bench_infer, "airbnb": bench_airbnb,
+    {"lr": bench_lr, "cv": bench_cv, "clf": bench_clf, "gbdt": bench_gbdt, "infer": bench_infer, "airbnb": bench_airbnb,
      "relational": bench_relational, "expr": bench_expr}[
         args.config](spark, args)
     spark.comm.shutdown()

@@ -94,6 +94,26 @@ def _roc_pr_exact(score: np.ndarray, label: np.ndarray, weight: np.ndarray):
     return tp, fp
 
 
+def _roc_pr_exact_device(score: torch.Tensor, label: torch.Tensor, weight: torch.Tensor):
+    """``_roc_pr_exact`` on the GPU: one device sort of the scores (descending) and fp64 cumulative sums; only the
+    counts at the distinct-score boundaries come to the host.  The host version's np.argsort of a 3.3e6-row
+    validation fold took 250 ms of a 20 ms RandomForestClassifier fit (the CrossValidator's evaluate dominated
+    the L07 grid: 4.6 s for 13 fits at 1e7 rows).  With 0/1 labels and unit weights the sums are exact integers,
+    so the counts equal the host path's."""
+    n = score.numel()
+    if n == 0:
+        return np.zeros(0), np.zeros(0)
+    s, order = torch.sort(score, descending=True, stable=True)
+    lw = (weight * label)[order]
+    tp = torch.cumsum(lw, 0)
+    fp = torch.cumsum((weight * (1 - label))[order], 0)
+    last = torch.ones(n, dtype=torch.bool, device=score.device)
+    last[:-1] = s[1:] != s[:-1]
+    idx = K.compact_mask(last)
+    out = torch.stack([tp[idx], fp[idx]]).cpu().numpy()
+    return out[0], out[1]
+
+
 def _auc_from_counts(tp, fp, metric):
     P = tp[-1] if len(tp) else 0.0
     N = fp[-1] if len(fp) else 0.0
@@ -137,7 +157,10 @@ class BinaryClassificationEvaluator(Evaluator):
         comm = dataset._session.comm
         metric = self.getMetricName()
         if not comm.distributed:
-            tp, fp = _roc_pr_exact(score.cpu().numpy(), label.cpu().numpy(), w.cpu().numpy())
+            if score.is_cuda and not bool(torch.isnan(score).any()):
+                tp, fp = _roc_pr_exact_device(score.double(), label, w)
+            else:
+                tp, fp = _roc_pr_exact(score.cpu().numpy(), label.cpu().numpy(), w.cpu().numpy())
             return _auc_from_counts(tp, fp, metric)
         lo = torch.tensor([float(score.min()) if score.numel() else float("inf")], device=comm.device)
         hi = torch.tensor([float(score.max()) if score.numel() else float("-inf")], device=comm.device)

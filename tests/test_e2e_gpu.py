@@ -101,6 +101,21 @@ def test_binning_on_device_thresholds_equals_host_path(sessions, monkeypatch, fe
     assert torch.equal(got[0][2], got[1][2]) and torch.equal(got[0][3], got[1][3])
 
 
+def test_binary_evaluator_device_counts_equal_host(sessions):
+    """BinaryClassificationEvaluator's exact ROC / PR counts from the device sort equal the host argsort path:
+    tied scores (every tie group is one curve point), unit and integer weights."""
+    from cdnaml.models.evaluation import _roc_pr_exact, _roc_pr_exact_device
+    rng = np.random.default_rng(11)
+    n = 200003
+    score = np.round(rng.random(n), 3)  # ~1000 distinct values: ties
+    label = (rng.random(n) < score).astype(np.float64)
+    for w in (np.ones(n), rng.integers(1, 4, n).astype(np.float64)):
+        tp_h, fp_h = _roc_pr_exact(score, label, w)
+        tp_d, fp_d = _roc_pr_exact_device(*(torch.from_numpy(a).cuda() for a in (score, label, w)))
+        np.testing.assert_array_equal(tp_d, tp_h)
+        np.testing.assert_array_equal(fp_d, fp_h)
+
+
 def test_classifiers_gpu(sessions):
     from cdnaml.ml.classification import GBTClassifier, LogisticRegression, RandomForestClassifier
     from cdnaml.ml.evaluation import BinaryClassificationEvaluator
