@@ -273,3 +273,8 @@ if __name__ == "__main__":
     elif rank == 0:
         with open(sys.argv[2], "w") as f:
             json.dump(res, f)
+    if sys.argv[1] != "fault":
+        # orderly teardown (barrier, then destroy the group): left to interpreter exit, a gloo rank whose peer
+        # already closed its sockets can abort ("terminate called without an active exception", SIGABRT)
+        import cdnaml
+        cdnaml.SparkSession.getActiveSession().comm.shutdown()
