@@ -114,6 +114,22 @@ def _roc_pr_exact_device(score: torch.Tensor, label: torch.Tensor, weight: torch
     return out[0], out[1]
 
 
+def _downsample(tp, fp, num_bins: int):
+    """Spark's curve down-sampling (BinaryClassificationMetrics(numBins)): with more than 2 * numBins distinct
+    scores, consecutive score points are grouped ``countsSize / numBins`` at a time (one partition: the grouping
+    runs over the whole descending order) and the curve keeps the cumulative counts at each group's end."""
+    k = len(tp)
+    if num_bins <= 0 or k == 0:
+        return tp, fp
+    grouping = k // num_bins
+    if grouping < 2:
+        return tp, fp
+    ends = np.arange(grouping - 1, k, grouping)
+    if ends[-1] != k - 1:
+        ends = np.r_[ends, k - 1]
+    return tp[ends], fp[ends]
+
+
 def _auc_from_counts(tp, fp, metric):
     P = tp[-1] if len(tp) else 0.0
     N = fp[-1] if len(fp) else 0.0
@@ -161,7 +177,7 @@ class BinaryClassificationEvaluator(Evaluator):
                 tp, fp = _roc_pr_exact_device(score.double(), label, w)
             else:
                 tp, fp = _roc_pr_exact(score.cpu().numpy(), label.cpu().numpy(), w.cpu().numpy())
-            return _auc_from_counts(tp, fp, metric)
+            return _auc_from_counts(*_downsample(tp, fp, self.getNumBins()), metric)
         lo = torch.tensor([float(score.min()) if score.numel() else float("inf")], device=comm.device)
         hi = torch.tensor([float(score.max()) if score.numel() else float("-inf")], device=comm.device)
         comm.all_reduce(lo, "min")
@@ -173,7 +189,7 @@ class BinaryClassificationEvaluator(Evaluator):
         nz = (h.sum(1) > 0)
         tp = np.cumsum(h[:, 1])[nz]
         fp = np.cumsum(h[:, 0])[nz]
-        return _auc_from_counts(tp, fp, metric)
+        return _auc_from_counts(*_downsample(tp, fp, self.getNumBins()), metric)
 
     def isLargerBetter(self):
         return True

@@ -232,6 +232,28 @@ def test_logistic_regression_matches_sklearn(spark):
     assert abs(c[2]) < 1e-6 and abs(c[3]) < 1e-6 and abs(c[0]) > 0.1
 
 
+def test_binary_evaluator_num_bins_downsampling(spark):
+    """numBins (Spark's BinaryClassificationMetrics down-sampling): numBins=0 is the exact curve (== sklearn's
+    roc_auc_score); the default 1000 with 5000 distinct scores keeps every 5th cumulative point of the descending
+    order (Spark groups countsSize / numBins consecutive score points); fewer than 2 * numBins distinct scores
+    stay exact."""
+    from sklearn.metrics import roc_auc_score
+    rng = np.random.default_rng(4)
+    n = 5000
+    s = rng.normal(size=n)
+    yb = (rng.random(n) < 1 / (1 + np.exp(-2 * s))).astype(np.float64)
+    df = spark.createDataFrame(pd.DataFrame({"rawPrediction": s, "label": yb}))
+    exact = BinaryClassificationEvaluator(numBins=0).evaluate(df)
+    assert abs(exact - roc_auc_score(yb, s)) < 1e-12
+    order = np.argsort(-s)
+    tp, fp = np.cumsum(yb[order]), np.cumsum(1 - yb[order])
+    ends = np.arange(4, n, 5)
+    tpr = np.r_[0.0, tp[ends] / tp[-1], 1.0]
+    fpr = np.r_[0.0, fp[ends] / fp[-1], 1.0]
+    assert abs(BinaryClassificationEvaluator().evaluate(df) - np.trapezoid(tpr, fpr)) < 1e-12
+    assert BinaryClassificationEvaluator(numBins=5000).evaluate(df) == exact
+
+
 def test_tree_classifiers_and_aupr(spark):
     df, X, y = _cls_frame(spark, n=2000)
     for est in (DecisionTreeClassifier(maxDepth=4), RandomForestClassifier(numTrees=10, seed=42),
