@@ -1154,8 +1154,13 @@ class ForestTrainer:
             rec_ok = (MSEG_REC and stats_rows.get("v0") is None and not subset_seg and 8 * B * 8 <= 128 * 1024)
             # levels with <= 1 built node per tree (0: the roots, 1: the smaller children) on seg10 rows: the
             # records are compacted inside the histogram kernel (no codes_compact pass)
-            root_ok = (ROOT_HIST and use_mseg and not use_sub and (depth >= 1 or MSEG_L0) and rec_ok and
-                       dev.type == "cuda" and data.bins_s10 is not None and d <= 100 and B <= 40 and
+            root_rows = None  # seg10 rows (B <= 40) or standard row-major rows (boosting, 80 < B <= 256)
+            if dev.type == "cuda" and ROOT_HIST:
+                if data.bins_s10 is not None and d <= 100 and B <= 40:
+                    root_rows = data.bins_s10
+                elif 80 < B <= 256 and data.bins_rm is not None:
+                    root_rows = data.bins_rm
+            root_ok = (root_rows is not None and use_mseg and not use_sub and (depth >= 1 or MSEG_L0) and rec_ok and
                        len(build_ids) > 0 and np.bincount(slot_tree, minlength=T).max() <= 1)
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
                 if use_sub:
@@ -1171,7 +1176,7 @@ class ForestTrainer:
                     # one launch for every slot, then the level's one all-reduce: these levels hold one node per
                     # tree (20 x 100 x 40 cells = 1.3 MB at the headline), too little to overlap, and slot chunks
                     # of a 1.25e7-row shard would launch ~1 round of blocks each (half of it idle)
-                    Hb = K.seg_hist_codes(data.bins_s10, d, B, codes, stats_rows["v1"], mseg_scales[1], wmax,
+                    Hb = K.seg_hist_codes(root_rows, d, B, codes, stats_rows["v1"], mseg_scales[1], wmax,
                                           slot_tree, sl_node, 0, S_b,
                                           torch.zeros((S_b, d, B, 2), dtype=torch.int64, device=dev))
                     hist_raw_scale = mseg_raw

@@ -120,6 +120,8 @@ _SIGS = {
     "cdna_hist5_max_trees": ([], c_int),
     "cdna_seg_hist": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_int, c_float, c_float, c_void_p, c_int, c_void_p], c_int),
+    "cdna_seg_hist_root_wide": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int,
+                                 c_void_p, c_int, c_void_p, c_void_p], c_int),
     "cdna_seg_hist_root": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int, c_void_p,
                             c_int, c_void_p, c_void_p], c_int),
     "cdna_seg_partition": ([c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,

@@ -1288,7 +1288,11 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
     -- the same integers as ``codes_compact(rec_scale=qs1)`` + ``seg_hist(rec=True, raw=True)``, without
     materialising the level's 8-byte records."""
     T, n = codes.shape
-    assert _native(codes) and d <= 100 and B <= 40 and bins_s10.shape == (n, 16, 8)
+    wide = 80 < B <= 256
+    # B <= 40: seg10 rows, six-items-per-wave kernel; 80 < B <= 256 (boosting): standard row-major rows, lane4
+    assert _native(codes) and ((d <= 100 and B <= 40 and bins_s10.shape == (n, 16, 8)) or
+                               (wide and bins_s10.shape[0] == n and bins_s10.shape[1] * 8 >= d and
+                                bins_s10.is_contiguous()))
     assert out.dtype == torch.int64 and out.is_contiguous() and out.shape == (s1 - s0, d, B, 2)
     st = np.asarray(slot_tree, dtype=np.int64)
     sn = np.asarray(slot_node, dtype=np.int64)
@@ -1298,8 +1302,8 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
         return out
     wm = int(max(1, min(255, wmax)))
     # each LDS cell copy takes every third item of a wave's stream: rows x wmax / 3 (+ a partial trip per
-    # wave) stays below the 20-bit count field
-    rows = max(64, min(n, 3 * ((1 << 20) // (wm + 1)) - 16 * 64))
+    # wave) stays below the 20-bit count field (the wide kernel has one copy: rows x wmax)
+    rows = max(64, min(n, (1 << 20) // (wm + 1) - 64 if wide else 3 * ((1 << 20) // (wm + 1)) - 16 * 64))
     # CDNAML_CODES_HIST_BLOCKS > 0: shrink the row chunks toward that many blocks (>= 16k rows each).  Off by
     # default: at the per-rank 1.25e7 shape 4096 blocks ran 21.0-21.3 ms per step vs 20.0-20.1 ms with the
     # largest chunks (the per-block LDS clear + flush of 100 KB outweighs the emptier last round)
@@ -1308,14 +1312,25 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
         rows = max(min(rows, 16384), min(rows, -(-(n * S_l) // CODES_HIST_BLOCKS)))
     rows = (rows + 63) // 64 * 64
     C = (n + rows - 1) // rows
-    if CODES_ROUND_FILL and C * S_l < 64 * _num_cus(codes.device):
-        # one block per CU: grow the chunk count to the next whole round of blocks (at most +25 %), so the last
-        # round is not a handful of blocks on an otherwise idle chip (1.25e7 rows x 20 trees: 1040 -> 1280)
+    bpc = S_l * (-(-d // 64) if wide else 1)  # blocks per row chunk (the wide kernel: one per 64 features)
+    if codes.is_cuda:
+        # at least two rounds of blocks (one block per CU) while blocks keep >= 4096 rows: a boosting level of
+        # 1.25e7 rows in 524k-row chunks would run 48 blocks on 256 CUs
+        C_min = min(-(-2 * _num_cus(codes.device) // bpc), max(1, n // 4096))
+        if C < C_min:
+            C = C_min
+            rows = (-(-n // C) + 63) // 64 * 64
+            C = (n + rows - 1) // rows
+    if CODES_ROUND_FILL and C * bpc < 64 * _num_cus(codes.device):
+        # one block per CU: grow the chunk count to the next whole round of blocks (at most +25 %, +100 % for the
+        # few big blocks of a boosting level), so the last round is not a handful of blocks on an otherwise idle
+        # chip (1.25e7 rows x 20 trees: 1040 -> 1280 blocks; GBDT 1e8 rows: 382 -> 512)
         ncu = _num_cus(codes.device)
         C2 = C
-        while (C2 * S_l) % ncu and C2 < C * 5 // 4:
+        cap = C * 2 if wide else C * 5 // 4
+        while (C2 * bpc) % ncu and C2 < cap:
             C2 += 1
-        if (C2 * S_l) % ncu == 0:
+        if (C2 * bpc) % ncu == 0:
             C = C2
             rows = (-(-n // C) + 63) // 64 * 64
             C = (n + rows - 1) // rows
@@ -1329,8 +1344,16 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
     r0 = c * rows
     work = np.stack([r0, np.minimum(rows, n - r0), sl], 1).astype(np.int32)
     sinfo = np.stack([st, sn], 1).astype(np.int32).reshape(-1)
-    wt, si = upload(codes.device, work.reshape(-1), sinfo)
     v1c = v1.float().contiguous()
+    if wide:
+        # the kernel pairs the feature blocks of each item on one XCD itself: items in (chunk, slot) order
+        work = work[np.lexsort((work[:, 2], work[:, 0]))]
+        wt, si = upload(codes.device, work.reshape(-1), sinfo)
+        _lib.check(_lib.lib().cdna_seg_hist_root_wide(_ptr(bins_s10), n, d, B, bins_s10.shape[1] * 8, _ptr(codes),
+                                                      _ptr(v1c), float(qs1), _ptr(wt), len(work), _ptr(si), s0,
+                                                      _ptr(out), _stream(codes.device)), "cdna_seg_hist_root_wide")
+        return out
+    wt, si = upload(codes.device, work.reshape(-1), sinfo)
     _lib.check(_lib.lib().cdna_seg_hist_root(_ptr(bins_s10), n, d, B, _ptr(codes), _ptr(v1c), float(qs1), _ptr(wt),
                                              len(work), _ptr(si), s0, _ptr(out), _stream(codes.device)),
                "cdna_seg_hist_root")

@@ -1330,10 +1330,141 @@ __global__ __launch_bounds__(256) void bins_row_major_kernel(const uint64_t* __r
 
 }  // namespace
 
+namespace {
+// Wide-bin (80 < B <= 256) twin of seg_hist_lane10_root_kernel for boosting (GBDT, one tree per round: every
+// level-0 / level-1 histogram has one built node per tree): the quarter-wave lane4 histogram (64 features per
+// block, XCD-paired feature blocks) fed by per-wave LDS rings of records compacted from the row codes instead
+// of a codes_count_w + codes_scatter_w pass.  [4][BP][16] u64 planes (128 KB at 256 bins) + 16 x 128 ring
+// entries (16 KB).  All four quarters of a wave add into the same cells: a block's rows x max weight must stay
+// below 2^20.
+template <int BP, int U>
+__global__ __launch_bounds__(1024) void seg_hist_lane4_root_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins8,
+                                                                   int row_bytes, int nwork, int ny,
+                                                                   const uint16_t* __restrict__ codes,
+                                                                   const float* __restrict__ v1, float qs1,
+                                                                   const int* __restrict__ sinfo, int slot0) {
+  constexpr int TH = 1024, NW = TH / 64, NI = 4 * U, RING = 128;  // NI - 1 + 64 < RING
+  constexpr int PLANE = BP * 16;
+  static_assert(BP == 128 || BP == 256, "four planes of 128 or 256 bins");
+  __shared__ __attribute__((aligned(16))) unsigned long long h[4 * PLANE];  // [4][BP][16]
+  __shared__ __attribute__((aligned(16))) uint64_t ring[NW][RING];
+  const int b = blockIdx.x, k = b >> 3;
+  const int c = (k / ny) * 8 + (b & 7), fy = k - (k / ny) * ny;
+  if (c >= nwork) return;
+  const int r0 = a.work[3 * c], len = a.work[3 * c + 1], slot = a.work[3 * c + 2];
+  const int tree = sinfo[2 * slot];
+  const uint32_t node = (uint32_t)sinfo[2 * slot + 1];
+  if (!CDNA_DCHECK(r0 >= 0 && len >= 0 && slot >= slot0 && tree >= 0 && node < 0xFFu && (int64_t)r0 + len <= a.n,
+                   0x5E86u)) return;
+  const int f0 = fy * 64;
+  for (int i = threadIdx.x; i < 4 * PLANE; i += TH) h[i] = 0ull;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, qt = lane >> 4, lq = lane & 15;
+  const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  int dw = (f0 >> 2) + lq;
+  const int dmax = (row_bytes >> 2) - 1;
+  dw = dw < dmax ? dw : dmax;
+  const uint8_t* lbase = bins8 + 4 * dw;
+  const uint32_t loff = (uint32_t)lq * 8u;
+  const uint16_t* ct = codes + (int64_t)tree * a.n;
+  uint64_t* rg = ring[wid];
+  const int per = ((len + NW - 1) / NW + 63) & ~63;
+  int64_t wr = (int64_t)r0 + (int64_t)wid * per;
+  const int64_t wend = (int64_t)r0 + len < wr + per ? (int64_t)r0 + len : wr + per;
+  uint32_t head = 0u, tail = 0u;
+  uint32_t ncw = 0xFFu;
+  float ny_ = 0.f;
+  auto fetch = [&](int64_t r) {
+    ncw = r < wend ? (uint32_t)ct[r] : 0xFFu;
+    ny_ = r < wend ? v1[r] : 0.f;
+  };
+  fetch(wr + lane);
+  for (;;) {
+    while (tail - head < (uint32_t)NI && wr < wend) {
+      const uint32_t cw = ncw;
+      const float y = ny_;
+      const int64_t r = wr + lane;
+      wr += 64;
+      fetch(wr + lane);
+      const bool has = (cw & 0xFFu) == node && (cw >> 8) != 0u;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(has);
+      if (has) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        int q1 = (int)rintf(y * qs1);
+        q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+        rg[(tail + rank) & (RING - 1)] =
+            (uint64_t)r | ((uint64_t)(cw >> 8) << 31) | ((uint64_t)(uint32_t)(q1 + kPackQ) << 39);
+      }
+      tail += (uint32_t)__builtin_popcountll(m);
+    }
+    const uint32_t avail = tail - head;
+    if (avail == 0u) break;
+    asm volatile("" ::: "memory");
+    uint64_t rc[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t kk = (uint32_t)(4 * p + qt);
+      rc[p] = kk < avail ? rg[(head + kk) & (RING - 1)] : 0ull;
+    }
+    head += avail < (uint32_t)NI ? avail : (uint32_t)NI;
+    uint32_t x[U];
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t row = (uint32_t)rc[p] & 0x7FFFFFFFu;
+      x[p] = *reinterpret_cast<const uint32_t*>(lbase + (uint64_t)row * (uint64_t)row_bytes);
+    }
+#pragma unroll
+    for (int p = 0; p < U; ++p) {
+      const uint32_t lo = (uint32_t)rc[p], hi = (uint32_t)(rc[p] >> 32);
+      const uint32_t w = __builtin_amdgcn_alignbit(hi, lo, 31) & 0xFFu;
+      const unsigned long long add = ((unsigned long long)(w << (kPackShift - 32)) << 32) +
+                                     (unsigned long long)w * (hi >> 7);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t off = (__builtin_amdgcn_ubfe(x[p], 8u * j, 8u) << 7) | loff;  // bin << 7 | l' << 3
+        atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h) + off) + j * PLANE, add);
+      }
+    }
+    asm volatile("" ::: "memory");
+  }
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < 4 * PLANE; cc += TH) {
+    const int b_lo = cc & 7, l = (cc >> 3) & 15, j = (cc >> 7) & 3, b_hi = cc >> 9;
+    const int bn = b_hi * 8 + b_lo;
+    const int f = f0 + 4 * l + j;
+    if (bn >= a.B || f >= a.d) continue;
+    const unsigned long long v = h[j * PLANE + bn * 16 + l];
+    if (!v) continue;
+    const unsigned long long cnt = v >> kPackShift;
+    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    unsigned long long* o = &a.out[(((int64_t)(slot - slot0) * a.d + f) * a.B + bn) * 2];
+    atomicAdd(o, cnt);
+    atomicAdd(o + 1, (unsigned long long)sum);
+  }
+}
+}  // namespace
+
 // Record histograms straight from the codes (seg_hist_lane10_root_kernel) for levels with <= 1 built node per
 // tree: bins in the seg10 row layout, work [nwork][3] {row start, row count, slot}, sinfo [S][2] {tree, local
 // node of the slot}; slot s's sums go to out slot s - slot0 (a slot-range slice).  Row counts per work item
 // must keep count x max weight / 3 below 2^20 (the packed LDS cells).
+// Wide-bin twin (seg_hist_lane4_root_kernel): bins_rm standard row-major rows of row_bytes, 80 < B <= 256.
+CDNA_API int cdna_seg_hist_root_wide(const uint8_t* bins_rm, int64_t n, int d, int B, int row_bytes,
+                                     const uint16_t* codes, const float* v1, float qs1, const int* work, int nwork,
+                                     const int* sinfo, int slot0, unsigned long long* out, hipStream_t st) {
+  if (nwork <= 0) return 0;
+  if (B <= 80 || B > 256 || row_bytes < ((d + 7) / 8) * 8) return (int)hipErrorInvalidValue;
+  SegHistArgs a{nullptr, n, d, B, nullptr, nullptr, v1, nullptr, work, 1.f, qs1, out};
+  const int ny = (d + 63) / 64;
+  const dim3 grid((unsigned)(((nwork + 7) / 8) * 8 * ny));
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(1024), 0, st, a, bins_rm, row_bytes, nwork, ny, codes, v1, qs1, sinfo, slot0);
+  };
+  if (B <= 128) launch(seg_hist_lane4_root_kernel<128, 16>);
+  else launch(seg_hist_lane4_root_kernel<256, 16>);
+  return (int)hipGetLastError();
+}
+
 CDNA_API int cdna_seg_hist_root(const uint8_t* bins_s10, int64_t n, int d, int B, const uint16_t* codes,
                                 const float* v1, float qs1, const int* work, int nwork, const int* sinfo, int slot0,
                                 unsigned long long* out, hipStream_t st) {

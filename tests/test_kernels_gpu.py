@@ -1074,6 +1074,36 @@ def test_seg10_rows_and_lane10_histogram(dev, d, B, monkeypatch):
     assert torch.equal(cgot.cpu(), ref[1::2].cpu())
 
 
+@pytest.mark.parametrize("d,B", [(100, 256), (64, 256), (100, 100), (37, 129)])
+def test_wide_codes_histogram_equals_records(dev, d, B):
+    """Boosting levels with one built node per tree (80 < B <= 256) straight from the row codes
+    (seg_hist_lane4_root_kernel) give the int64 sums of codes_compact records + the lane4 record histogram:
+    bag weights 0/1/2, a non-root local node, slot-range slices."""
+    T, n = 3, 150011
+    rng = np.random.default_rng(d + B)
+    w = rng.integers(0, 3, (T, n))
+    loc = np.where(w == 0, 0xFF, rng.integers(0, 2, (T, n)))
+    codes = torch.from_numpy(((w << 8) | loc).astype(np.uint16).view(np.int16)).to(dev)
+    g = torch.Generator().manual_seed(d)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    bins, rm = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), want_rm=True)
+    if rm is None:
+        rm = K.bins_row_major(bins)
+    v1 = (torch.randn(n, generator=g) * 3).to(dev)
+    sc = K.seg_scales(None, v1, 2, n)
+    tfirst = torch.from_numpy(np.arange(T, dtype=np.int32) * 2)
+    slot_of = np.array([t if k == 1 else -1 for t in range(T) for k in range(2)], dtype=np.int32)  # node 1 built
+    rec, _, _, _, sg = K.codes_compact(codes, tfirst, slot_of, T, None, v1, rec_scale=sc[1])
+    sb = np.concatenate([sg, np.arange(T)[:, None]], 1)
+    ref = K.seg_hist(bins, d, B, rec, None, None, None, sb, T, 2, sc, bins_rm=rm, rec=True, raw=True)
+    for s0, s1 in [(0, T), (1, 3)]:
+        got = K.seg_hist_codes(rm, d, B, codes, v1, sc[1], 2, np.arange(T), np.ones(T, np.int64), s0, s1,
+                               torch.zeros((s1 - s0, d, B, 2), dtype=torch.int64, device=dev))
+        assert int(ref[s0:s1, ..., 0].sum()) > 0
+        assert torch.equal(got.cpu(), ref[s0:s1].cpu())
+
+
 @pytest.mark.parametrize("d,maxb,n,missing", [(100, 40, 100003, None), (64, 256, 5001, None), (8, 2, 77, None),
                                               (128, 32, 4099, None), (100, 40, 3001, -999.0),
                                               (100, 40, 3001, float("nan"))])
