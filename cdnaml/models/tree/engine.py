@@ -502,11 +502,42 @@ class Forest:
         self._dev[key] = out
         return out
 
+    def _binned_arrays_contiguous(self, tree: int):
+        """binned_arrays' tables with numpy when the tree's nodes are the contiguous id range [root, end) (a
+        boosting round grows its one tree there) and it has no categorical split; else None.  The per-node Python
+        loop cost ~0.45 ms per depth-8 tree, an idle GPU gap between every GBDT round's last split and its margin
+        update."""
+        r0 = self.roots[tree]
+        r1 = self.roots[tree + 1] if tree + 1 < len(self.roots) else len(self.feat)
+        if r1 - r0 < 1 or any(self.is_cat[r0:r1]):
+            return None
+        feat = np.asarray(self.feat[r0:r1], dtype=np.int64)
+        left = np.asarray(self.left[r0:r1], dtype=np.int64)
+        right = np.asarray(self.right[r0:r1], dtype=np.int64)
+        sp = feat >= 0
+        kids = np.concatenate([left[sp], right[sp]])
+        if len(kids) != r1 - r0 - 1 or not np.array_equal(np.sort(kids), np.arange(r0 + 1, r1)):
+            return None  # not exactly the nodes reachable from this root
+        leaf = ~sp
+        nodes = np.zeros((r1 - r0, 4), dtype=np.int32)
+        nodes[:, 0] = np.where(sp, feat, -1)
+        nodes[sp, 1] = np.asarray(self.bin[r0:r1], dtype=np.int64)[sp]
+        nodes[sp, 2] = left[sp] - r0
+        nodes[sp, 3] = right[sp] - r0
+        nodes[leaf, 1] = np.arange(int(leaf.sum()))
+        vals = np.array([self.value[r0 + j][0] for j in np.nonzero(leaf)[0].tolist()], dtype=np.float32)
+        return nodes, vals.reshape(-1), np.zeros(8, np.int32)
+
     def binned_arrays(self, device, tree: int):
         """Single tree with bin thresholds (GBDT training-set margin update)."""
         key = ("bin", str(device), tree)
         if key in self._dev:
             return self._dev[key]
+        fast = self._binned_arrays_contiguous(tree)
+        if fast is not None:
+            out = tuple(K.upload(device, *fast))
+            self._dev[key] = out
+            return out
         idx = self.tree_nodes(tree)
         pos = {g: j for j, g in enumerate(idx)}
         nodes = np.zeros((len(idx), 4), dtype=np.int32)
