@@ -428,7 +428,7 @@ class Forest:
                 stack.extend([self.right[i], self.left[i]])
         return out
 
-    def _layout(self):
+    def _layout(self, feat: Optional[np.ndarray] = None):
         """Per node: tree index (-1 if unreachable), heap slot (root 0, children 2i+1 / 2i+2) and, per tree,
         its depth -- one vectorised sweep per level instead of a Python walk per node."""
         N = len(self.feat)
@@ -438,7 +438,7 @@ class Forest:
         dep = np.zeros(T, dtype=np.int64)
         if T == 0:
             return tree_of, slot, dep
-        feat = np.asarray(self.feat, dtype=np.int64)
+        feat = np.asarray(self.feat, dtype=np.int64) if feat is None else feat
         left = np.asarray(self.left, dtype=np.int64)
         right = np.asarray(self.right, dtype=np.int64)
         fr = np.asarray(self.roots, dtype=np.int64)
@@ -564,18 +564,20 @@ class Forest:
         if key in self._dev:
             return self._dev[key]
         res = None
-        tree_of, slot, dep = self._layout()
+        feat = np.asarray(self.feat, dtype=np.int64)  # one list conversion shared with _layout (~1.3k nodes)
+        tree_of, slot, dep = self._layout(feat)
         D = int(dep.max()) if self.roots else 0
         if self.K == 1 and self.roots and D <= 8:
             S = 2 ** (D + 1) - 1
             heap = np.zeros((len(self.roots), S, 2), dtype=np.int32)
             heap[:, :, 0] = -1
-            feat = np.asarray(self.feat, dtype=np.int32)
             live = np.nonzero(tree_of >= 0)[0]
             lt, ls = tree_of[live], slot[live]
-            fl = feat[live]
+            fl = feat[live].astype(np.int32)
             leaf = fl < 0
-            v = np.array([self.value[i][0] for i in live[leaf].tolist()], dtype=np.float64)
+            vl = self.value
+            v = (np.concatenate([vl[i] for i in live[leaf].tolist()]) if leaf.any()
+                 else np.zeros(0)).astype(np.float64)
             if values_kind != "value":
                 v = v * np.asarray(self.weight, dtype=np.float64)[live[leaf]]
             heap[lt[leaf], ls[leaf], 1] = v.astype(np.float32).view(np.int32)

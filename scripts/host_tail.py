@@ -50,7 +50,7 @@ for i in range(8):
     t2 = time.perf_counter()
     out._plan.execute()
     t3 = time.perf_counter()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize() if torch.cuda.is_available() else None
     if i >= 3:
         tail.append((t1 - marks["train.end"], t2 - t1, t3 - t2))
 for a, b, c in tail:
@@ -58,9 +58,17 @@ for a, b, c in tail:
 import cProfile, pstats  # noqa: E401,E402
 pr = cProfile.Profile()
 m = rf.fit(df)
-torch.cuda.synchronize()
+torch.cuda.synchronize() if torch.cuda.is_available() else None
 pr.enable()
 out = m.transform(df)
 out._plan.execute()
 pr.disable()
 pstats.Stats(pr).sort_stats("cumtime").print_stats(25)
+# whole fit + transform, Python self time (what the host does while the GPU may idle)
+pr = cProfile.Profile()
+torch.cuda.synchronize() if torch.cuda.is_available() else None
+pr.enable()
+m = rf.fit(df)
+m.transform(df)._plan.execute()
+pr.disable()
+pstats.Stats(pr).sort_stats("tottime").print_stats(30)
