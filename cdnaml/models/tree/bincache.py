@@ -71,8 +71,12 @@ def fingerprint(X: torch.Tensor) -> tuple:
     return (n, d, v[0], v[1])
 
 
-def cached(key_fn: Callable[[], tuple], build: Callable[[], object]):
-    """build() outside a scope; inside, the value of an earlier build with the same key."""
+def cached(key_fn: Callable[[], tuple], build: Callable[[], object], comm=None):
+    """build() outside a scope; inside, the value of an earlier build with the same key.
+
+    ``comm`` (distributed): every rank keys the cache on its OWN shard, and a miss runs collectives (the quantile
+    sample's all-gather), so the ranks agree first -- a hit is used only when it is a hit on every rank, otherwise
+    all of them rebuild together (one rank hitting while another misses would issue mismatched collectives)."""
     if not _stack:
         stats["builds"] += 1
         return build()
@@ -80,11 +84,14 @@ def cached(key_fn: Callable[[], tuple], build: Callable[[], object]):
     cache = _stack[-1]
     with _lock:
         hit = cache.get(key)
+    if comm is not None and getattr(comm, "distributed", False):
+        if comm.all_reduce_scalar(0.0 if hit is None else 1.0, "min") < 1.0:
+            hit = None
     if hit is not None:
         stats["hits"] += 1
         return hit
     val = build()
     stats["builds"] += 1
     with _lock:
-        cache.setdefault(key, val)
+        cache[key] = val
     return val

@@ -272,7 +272,8 @@ def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins:
     return bincache.cached(
         lambda: (bincache.fingerprint(X), tuple(sorted(categorical.items())), int(max_bins), int(seed),
                  int(row_offset), int(n_global), None if missing is None else float(missing), str(X.device)),
-        lambda: _make_binned(session, X, categorical, max_bins, seed, row_offset, n_global, missing))
+        lambda: _make_binned(session, X, categorical, max_bins, seed, row_offset, n_global, missing),
+        comm=session.comm)
 
 
 def _make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins: int, seed: int,
@@ -957,11 +958,15 @@ class ForestTrainer:
 
     # ------------------------------------------------------------ reduce-scatter by feature
     def _rs_want(self, Hb: torch.Tensor, rs_on: bool, sub_feats) -> bool:
-        if not self.comm.distributed or Hb.dtype != torch.int64 or sub_feats is not None:
+        if Hb.dtype != torch.int64 or sub_feats is not None:
             return False
-        if self.data.categorical or self.classification or self.stats_k != 2:
+        return self._rs_level(Hb.numel() * 8, rs_on)
+
+    def _rs_level(self, nbytes: int, rs_on: bool) -> bool:
+        """An int64 level histogram of ``nbytes`` is reduce-scattered by feature (not all-reduced)."""
+        if not self.comm.distributed or self.data.categorical or self.classification or self.stats_k != 2:
             return False
-        return rs_on or Hb.numel() * 8 >= RS_MIN_BYTES
+        return rs_on or nbytes >= RS_MIN_BYTES
 
     def _reduce_scatter_features(self, Hb: torch.Tensor, d: int):
         """Exact int64 level histograms [S, d, B, k] summed over ranks, this rank keeping features [f0, f1)
@@ -1230,7 +1235,10 @@ class ForestTrainer:
                                                else None, interleave=True)
                     elif is_rec and (self.comm.distributed or HIST_OVERLAP_FORCE) and HIST_OVERLAP > 1 and \
                             len(build_ids) >= 2 and \
-                            len(build_ids) * d * B * 16 >= HIST_OVERLAP_MIN_BYTES:
+                            len(build_ids) * d * B * 16 >= HIST_OVERLAP_MIN_BYTES and \
+                            not self._rs_level(len(build_ids) * d * B * 16, rs_on):
+                        # (never once the pass reduce-scatters: the overlapped chunks are all-reduced over all
+                        # features, while prev_hist then holds only this rank's feature slice)
                         # comm/compute overlap: the level's slots are built in chunks, each chunk's int64
                         # histogram all-reduced (async, RCCL stream) while the next chunk is built
                         Hb = self._hist_overlapped(data, d, B, perm, sb, len(build_ids), wmax, mseg_scales, dev)

@@ -86,8 +86,10 @@ def uniform32(n: int, seed: int, offset: int = 0, stream: int = 0) -> np.ndarray
 
 def normal32(n: int, seed: int, offset: int = 0, stream: int = 0) -> np.ndarray:
     """fp32 standard normals for elements offset..offset+n-1, the layout of ``normal_f32_kernel`` (misc.hip):
-    quad q = index >> 2, words (0, 1) and (2, 3) are Box-Muller pairs (r cos, r sin), u = (w + 1/2) 2^-32.
-    Computed in float64 here; the kernel's hardware log/sin/cos agree to ~1e-6 relative."""
+    quad q = index >> 2, words (0, 1) and (2, 3) are Box-Muller pairs (r cos, r sin), u = (w + 1/2) 2^-32 formed
+    in fp32 exactly as the kernel forms it (w rounds to 24 significant bits first, so for w >= 2^32 - 128 the
+    radius uniform is exactly 1.0 and the pair is (0, 0) on both sides); the log / sin / cos are float64 here,
+    the kernel's hardware ones agree to ~1e-6 relative."""
     seed &= 0xFFFFFFFFFFFFFFFF
     if n <= 0:
         return np.zeros(0, dtype=np.float32)
@@ -95,7 +97,7 @@ def normal32(n: int, seed: int, offset: int = 0, stream: int = 0) -> np.ndarray:
     q = np.arange(q0, q1 + 1, dtype=np.uint64)
     lo = (q & _MASK32).astype(np.uint32)
     hi = (q >> np.uint64(32)).astype(np.uint32)
-    w = [(x.astype(np.float64) + 0.5) * (1.0 / 4294967296.0)
+    w = [((x.astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 4294967296.0)).astype(np.float64)
          for x in philox4x32_10(lo, hi, np.uint32(stream & 0xFFFFFFFF), np.uint32(0x4E0A), seed & 0xFFFFFFFF,
                                 seed >> 32)]
     z = np.empty((len(q), 4))

@@ -353,6 +353,21 @@ class Comm:
                     dist.barrier()
 
 
+def rank_device_index(backend: Optional[str] = None) -> int:
+    """This process's GPU: LOCAL_RANK.  Several ranks may share a GPU only under the host-staged gloo backend
+    (LOCAL_RANK % device_count, the 1-GPU rehearsal); RCCL does not support two ranks on one device, so under
+    nccl a LOCAL_RANK beyond the visible GPUs is an error here rather than an obscure failure later."""
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(1, torch.cuda.device_count())
+    if backend is None:
+        ws = int(os.environ.get("WORLD_SIZE", "1"))
+        backend = os.environ.get("CDNAML_COMM_BACKEND") or ("nccl" if ws > 1 else "gloo")
+    if backend == "nccl" and lr >= ndev:
+        raise RuntimeError(f"LOCAL_RANK {lr} but only {ndev} GPU(s) visible: one RCCL rank per GPU "
+                           f"(set CDNAML_COMM_BACKEND=gloo to share a GPU between ranks)")
+    return lr % ndev
+
+
 def init_from_env(device_type: Optional[str] = None, timeout_s: Optional[float] = None) -> None:
     """Initialise torch.distributed from torchrun-style env vars (idempotent).
 
@@ -374,7 +389,7 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: Optional[float] 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     kwargs = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
     if backend == "nccl":
-        lr = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        lr = rank_device_index(backend)
         torch.cuda.set_device(lr)
         kwargs["device_id"] = torch.device("cuda", lr)
     dist.init_process_group(**kwargs)

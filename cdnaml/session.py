@@ -151,8 +151,8 @@ class SparkSession:
         use_gpu = torch.cuda.is_available() and os.environ.get("CDNAML_DEVICE", "") != "cpu"
         init_from_env("cuda" if use_gpu else "cpu")
         if use_gpu:
-            lr = int(os.environ.get("LOCAL_RANK", "0"))
-            self.device = torch.device("cuda", lr % max(1, torch.cuda.device_count()))
+            from .parallel.comm import rank_device_index
+            self.device = torch.device("cuda", rank_device_index())
             torch.cuda.set_device(self.device)
         else:
             self.device = torch.device("cpu")

@@ -60,13 +60,23 @@ class ColumnData:
     def has_nulls(self) -> bool:
         return self.valid is not None and not bool(self.valid.all())
 
+    def _py_meta(self, sel):
+        """meta with the host-object payload (``_py``: one Python value per row -- collect_list arrays, struct
+        rows) re-indexed like the rows."""
+        py = self.meta.get("_py")
+        if py is None:
+            return self.meta
+        return dict(self.meta, _py=[py[i] for i in sel])
+
     def take(self, idx: torch.Tensor) -> "ColumnData":
+        meta = self._py_meta(idx.reshape(-1).cpu().tolist()) if "_py" in self.meta else self.meta
         return ColumnData(self.values[idx], self.dtype, None if self.valid is None else self.valid[idx],
-                          self.dictionary, self.meta)
+                          self.dictionary, meta)
 
     def slice(self, a: int, b: int) -> "ColumnData":
+        meta = self._py_meta(range(len(self.meta["_py"]))[a:b]) if "_py" in self.meta else self.meta
         return ColumnData(self.values[a:b], self.dtype, None if self.valid is None else self.valid[a:b],
-                          self.dictionary, self.meta)
+                          self.dictionary, meta)
 
     def to(self, device) -> "ColumnData":
         return ColumnData(self.values.to(device), self.dtype, None if self.valid is None else self.valid.to(device),
@@ -79,6 +89,14 @@ class ColumnData:
         ``nulls_as_nan``: numeric nulls become NaN in a float64 array (what Spark's
         Arrow ``toPandas`` produces); otherwise they are ``None`` in an object array.
         """
+        py = self.meta.get("_py")
+        if py is not None:  # host objects (collect_list arrays, struct rows), one per row
+            out = np.empty(len(py), dtype=object)
+            for i, x in enumerate(py):
+                out[i] = x
+            if self.valid is not None:
+                out[~self.valid.cpu().numpy()] = None
+            return out
         v = self.values.detach().cpu()
         valid = None if self.valid is None else self.valid.cpu().numpy()
         dt = self.dtype

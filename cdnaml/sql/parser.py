@@ -644,6 +644,10 @@ class _Scope:
         c = name.lower()
         hits = {n for _, cc, n in self.entries if cc.lower() == c}
         if not hits and len(parts) >= 2:
+            if parts[-2].lower() in {qq for qq, _, _ in self.entries if qq}:
+                # a known source qualifier whose source has no such column: Spark cannot resolve it (no
+                # fallback to another source's column of that name)
+                return None
             c = parts[-1].lower()
             hits = {n for _, cc, n in self.entries if cc.lower() == c}
         if len(hits) > 1:

@@ -346,6 +346,10 @@ def _agg_one(batch: Batch, agg, gid, G, first, ctx) -> ColumnData:
                                                                                            device=dev)
         return ColumnData(cnt[:G], T.LongType())
     c = agg.x.eval(batch, ctx)
+    if kind == "summarizer":
+        from ..ml.stat import summarize_groups
+        w = None if agg.param.get("weight") is None else agg.param["weight"].eval(batch, ctx)
+        return summarize_groups(c, w, gid, G, agg.param)
     valid = c.valid_mask()
     if agg.distinct:
         # dedupe (gid, value) pairs first
@@ -379,7 +383,8 @@ def _agg_one(batch: Batch, agg, gid, G, first, ctx) -> ColumnData:
         vm = valid.cpu().numpy()
         for i in range(batch.n):
             if vm[i]:
-                lists[g[i]].append(vals[i])
+                v = vals[i]
+                lists[g[i]].append(v.item() if isinstance(v, np.generic) else v)
         if kind == "collect_set":
             lists = [list(dict.fromkeys(x)) for x in lists]
         return ColumnData(torch.zeros(G, device=dev), T.ArrayType(c.dtype), meta={"_py": lists})

@@ -21,7 +21,10 @@ __global__ void uniform_kernel(double* __restrict__ out, int64_t n, uint64_t see
 // e = row * d + feature, so a table is the same however it is chunked or
 // sharded).  One Philox4x32-10 call per quad q = e >> 2 gives two Box-Muller
 // pairs: words (0, 1) -> elements 4q, 4q+1 (r cos, r sin), words (2, 3) ->
-// 4q+2, 4q+3.  u = (w + 1/2) 2^-32 is never 0 or 1.  Hardware log / sin / cos
+// 4q+2, 4q+3.  u = (w + 1/2) 2^-32 in fp32: never 0, but w rounds to 24
+// significant bits first, so u1 is exactly 1.0 for w >= 2^32 - 128 (2^-25 of
+// the draws) and that pair is (0, 0) where exact arithmetic gives a radius of
+// at most 2.4e-4; the oracle forms u the same fp32 way.  Hardware log / sin / cos
 // (v_log_f32, v_sin_f32, v_cos_f32): HBM-write bound, ~4 B per element, with
 // float4 stores when the quad is interior and the output is 16-byte aligned.
 // Oracle: cdnaml/ops/philox.py:normal32.

@@ -163,6 +163,37 @@ def scenario_trees_rs(spark):
     return out
 
 
+def scenario_trees_rs_overlap(spark):
+    """Reduce-scatter by feature together with the chunked (overlapped) all-reduce, the overlap left enabled
+    (ADVICE r3): (a) overlap for the shallow levels, reduce-scatter from level 2 on; (b) reduce-scatter from
+    level 0 with an overlap threshold the deeper levels cross -- the overlapped branch must not run once a pass
+    reduce-scatters (its full-d sums would meet the rank's sliced parent histograms).  Both must give the 1-rank
+    forests bit for bit."""
+    from cdnaml.models.tree import engine
+    seen = {"rs": 0, "ov": 0}
+    o_rs, o_ov = engine.ForestTrainer._reduce_scatter_features, engine.ForestTrainer._hist_overlapped
+
+    def rs(self, *a):
+        seen["rs"] += 1
+        return o_rs(self, *a)
+
+    def ov(self, *a):
+        seen["ov"] += 1
+        return o_ov(self, *a)
+    engine.ForestTrainer._reduce_scatter_features = rs
+    engine.ForestTrainer._hist_overlapped = ov
+    engine.HIST_OVERLAP = 2
+    df = _tree_df(spark, d=13)
+    out = {}
+    for tag, rs_min, ov_min in (("a", 200000, 100000), ("b", 0, 300000)):
+        engine.RS_MIN_BYTES, engine.HIST_OVERLAP_MIN_BYTES = rs_min, ov_min
+        seen.update(rs=0, ov=0)
+        for k, v in _tree_digests(df).items():
+            out[f"{tag}_{k}"] = v
+        out[f"{tag}_levels"] = dict(seen)
+    return out
+
+
 def scenario_cv(spark):
     from cdnaml.ml.evaluation import RegressionEvaluator
     from cdnaml.ml.regression import RandomForestRegressor
@@ -254,7 +285,8 @@ def scenario_hyperopt_captured(spark):
 
 
 SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault, "trees": scenario_trees,
-             "trees_uneven": scenario_trees_uneven, "trees_rs": scenario_trees_rs, "cv": scenario_cv, "als": scenario_als,
+             "trees_uneven": scenario_trees_uneven, "trees_rs": scenario_trees_rs,
+             "trees_rs_overlap": scenario_trees_rs_overlap, "cv": scenario_cv, "als": scenario_als,
              "hyperopt": scenario_hyperopt,
              "hyperopt_captured": scenario_hyperopt_captured}
 

@@ -158,3 +158,17 @@ def test_reduce_scatter_by_feature_forests_identical(tmp_path):
         got = _run("trees_rs", tmp_path, w)
         assert got.pop("rs_levels") > 0, w
         assert got == one, w
+
+
+def test_reduce_scatter_with_overlap_enabled(tmp_path):
+    """with the chunked all-reduce overlap enabled and both thresholds crossed, the
+    reduce-scatter pass never meets full-d overlapped sums; forests equal the 1-rank fits at W = 2 and 4."""
+    one = _run("trees_rs_overlap", tmp_path, 1)
+    for tag in ("a", "b"):
+        assert one.pop(f"{tag}_levels") == {"rs": 0, "ov": 0}
+    for w in (2, 4):
+        got = _run("trees_rs_overlap", tmp_path, w)
+        la, lb = got.pop("a_levels"), got.pop("b_levels")
+        assert la["ov"] > 0 and la["rs"] > 0, (w, la)   # overlap at the shallow levels, RS below
+        assert lb["rs"] > 0 and lb["ov"] == 0, (w, lb)  # RS from level 0: the overlap branch stays off
+        assert got == one, w

@@ -65,7 +65,8 @@ def test_uniform_bit_identical(dev):
 @pytest.mark.parametrize("n,offset,shift", [(100000, 0, 0), (100003, 5, 0), (4097, 2, 1), (3, 7, 0), (1, 0, 3)])
 def test_normal32_matches_host_oracle(dev, n, offset, shift):
     """float4 stores (aligned output, offset % 4 == 0) and per-element stores (unaligned offset or output
-    pointer) against the float64 host oracle; only the kernel's fp32 u and hardware log/sin/cos differ."""
+    pointer) against the host oracle (the same fp32 uniforms, float64 log/sin/cos): only the kernel's hardware
+    log/sin/cos differ."""
     ref = torch.from_numpy(__import__("cdnaml.ops.philox", fromlist=["normal32"]).normal32(n, 9, offset, 0x10))
     buf = torch.full((n + shift + 1,), 7.0, device=dev)
     out = K.normal32_(buf[shift:shift + n], 9, offset, 0x10).cpu()

@@ -276,3 +276,8 @@ def test_sql_qualified_and_ambiguous_names(spark):
     out = spark.sql("SELECT a.*, b.v AS w FROM ta a LEFT JOIN tb b ON a.k = b.k ORDER BY a.k").toPandas()
     assert list(out.columns) == ["k", "v", "w"]
     assert out.w.isna().tolist() == [False, False, True]
+    # a known qualifier whose source lacks the column does not fall back to the other side
+    spark.createDataFrame(pd.DataFrame({"k": [1, 2], "x": [5.0, 6.0]})).createOrReplaceTempView("tc")
+    with pytest.raises(AnalysisException, match="cannot resolve"):
+        spark.sql("SELECT a.x FROM ta a JOIN tc c ON a.k = c.k").toPandas()
+    assert spark.sql("SELECT c.x FROM ta a JOIN tc c ON a.k = c.k ORDER BY c.x").toPandas().x.tolist() == [5.0, 6.0]
