@@ -46,6 +46,8 @@ USE_MSEG = __import__("os").environ.get("CDNAML_TREE_MSEG", "1") != "0"
 MSEG_L0 = __import__("os").environ.get("CDNAML_MSEG_L0", "1") != "0"  # level 0 through segments too
 # single-tree packed fits (boosting rounds with unit hessians, DecisionTree) through row records + compaction
 MSEG_T1 = __import__("os").environ.get("CDNAML_MSEG_T1", "1") != "0"
+# binary classification forests on the packed record / segment path (class counts from (W, W1) sums)
+MSEG_CLS = __import__("os").environ.get("CDNAML_MSEG_CLS", "1") != "0"
 # K6 split search in one HIP kernel (split.hip) where it applies; else the torch formulation
 NATIVE_SPLIT = __import__("os").environ.get("CDNAML_NATIVE_SPLIT", "1") != "0"
 # segment-mode forests carry one packed 8-byte record per gathered row (row | weight | quantised label)
@@ -715,6 +717,18 @@ def _mask_feature_lists(words: np.ndarray, d: int) -> Optional[np.ndarray]:
     return np.nonzero(bits)[1].reshape(len(cnt), int(cnt[0])).astype(np.int32)
 
 
+def _built_nodes(w: np.ndarray, a_sib: np.ndarray, a_parent: np.ndarray) -> np.ndarray:
+    """Subtraction levels: the active nodes whose histogram is built -- the smaller of two active siblings (ties:
+    the first one), the other derived as parent - sibling; a node without an active sibling is built.  The
+    device twin is split.hip emit_plan_kernel (K.emit_plan_host)."""
+    build = np.ones(len(w), dtype=bool)
+    has = np.nonzero((a_sib >= 0) & (a_parent >= 0))[0]
+    wa, ws = w[has], w[a_sib[has]]
+    lose = (wa > ws) | ((wa == ws) & (has > a_sib[has]))
+    build[has[lose]] = False
+    return build
+
+
 class ForestTrainer:
     """Trains T trees level-synchronously over one BinnedData shard per rank."""
 
@@ -956,6 +970,41 @@ class ForestTrainer:
         if not ok:
             raise RuntimeError("device split decode differs from the host decode")
 
+    # ------------------------------------------------------------ record emission by the partition
+    @staticmethod
+    def _check_emitted(em, st, cap, codes, tfirst, slot_of, S, v1, qs1):
+        """Checked build: the device plan equals the host plan, every slot's emitted segment stays inside its
+        capacity, and its non-padding records are exactly the compaction's records of the same codes."""
+        got = em.seg_start[:S].cpu().numpy()
+        if not np.array_equal(got, st):
+            raise RuntimeError("device record-emission plan differs from the host plan")
+        ends = em.cursor.view(-1, em.cs)[:S, 0].cpu().numpy().astype(np.int64)
+        if np.any(ends < st) or np.any(ends > st + cap):
+            raise RuntimeError("emitted records outside their segment capacity")
+        ref, _, _, _, sg = K.codes_compact(codes, tfirst, slot_of, S, None, v1, rec_scale=qs1)
+        ref = ref.cpu().numpy()
+        rec = em.rec.cpu().numpy() if S else None
+        for s in range(S):
+            r = rec[st[s]:ends[s]]
+            r = np.sort(r[((r >> 31) & 0xFF) != 0])
+            e = np.sort(ref[sg[s, 0]:sg[s, 0] + sg[s, 1]])
+            if not np.array_equal(r, e):
+                raise RuntimeError(f"emitted records of slot {s} differ from the compaction's")
+    def _record_emit(self, dev, n: int, A: int, v1: torch.Tensor, qs1: float, w_total: float, rec_buf):
+        """A K.RecordEmit for the partition of a level with A active nodes (the next level's records written by the
+        partition itself), or None when its capacity plan does not fit int32 positions.  Capacities come from the
+        all-reduced child weights, so on W ranks each rank's buffer is sized by the global weights."""
+        G = self.data.bins.shape[0]
+        waves = K.partition7_waves(n, G)
+        share = n / max(1, self.data.n_global)
+        ch = K.emit_chunk(0.5 * w_total * share, waves, A)
+        cap_total = int(w_total) + A * (waves * ch + ch) + K.REC_PAD
+        if waves <= 0 or cap_total >= 2 ** 31 - 1:
+            return None
+        rec = rec_buf if (rec_buf is not None and rec_buf.numel() >= cap_total) else \
+            torch.empty(cap_total, dtype=torch.int64, device=dev)
+        return K.RecordEmit(dev, n, A, rec, v1, qs1, ch, waves)
+
     # ------------------------------------------------------------ reduce-scatter by feature
     def _rs_want(self, Hb: torch.Tensor, rs_on: bool, sub_feats) -> bool:
         if Hb.dtype != torch.int64 or sub_feats is not None:
@@ -1064,7 +1113,7 @@ class ForestTrainer:
                     h.wait()
         return Hc
 
-    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev):
+    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev, seg_end=None):
         """Record histograms of a level's S slots in HIST_OVERLAP slot chunks; chunk c's all-reduce runs on the
         collective stream while chunk c + 1 is built (one per-level RCCL all-reduce of 1-50 MB otherwise
         serialises with the compute stream).  The sums are exact integers, so the result is identical to one
@@ -1082,8 +1131,11 @@ class ForestTrainer:
                 sel = (sb[:, 2] >= s0) & (sb[:, 2] < s1)
                 sbc = sb[sel].copy()
                 sbc[:, 2] -= s0
+                se = None
+                if seg_end is not None:  # slot-range slice of the record ends
+                    se = (seg_end[0][s0 * seg_end[1]:], seg_end[1])
                 K.seg_hist(data.bins, d, B, rec, None, None, None, sbc, s1 - s0, wmax, scales, bins_rm=rm,
-                           interleave=True, rec=True, raw=True, out=Hb[s0:s1], rm_s10=s10)
+                           interleave=True, rec=True, raw=True, out=Hb[s0:s1], rm_s10=s10, seg_end=se)
             with _tr.span("tree.allreduce_async", cat="comm", bytes=(s1 - s0) * d * B * 16):
                 pend.append(self.comm.all_reduce_async(Hb[s0:s1]))
         with _tr.span("tree.allreduce_wait", cat="comm"):
@@ -1106,8 +1158,17 @@ class ForestTrainer:
         # several regression trees: row records for every level (one dense pass partitions all trees); before
         # each level's histogram the rows of the nodes it builds are gathered into slot segments, so the
         # histogram touches only those rows
+        # binary classification rides the packed regression path: with label y in {0, 1} and scale 1 the packed
+        # sums (count, sum w * y) are (W, W1), turned into the class counts (W - W1, W1) in int64 before K6 --
+        # exactly the class histograms of the node-id / codes kernels, so the forest does not change.  Forests
+        # deeper than 8 levels (u16 codes hold <= 255 nodes per tree) switch to node ids at level 8
+        cls2 = self.classification and self.C == 2 and MSEG_CLS
+        deep_switch = cls2 and p.max_depth > 8
+        if cls2:
+            stats_rows = dict(stats_rows, v1=stats_rows["label"].float())
         mseg_ok = (USE_MSEG and USE_CODES and (T > 1 or (MSEG_T1 and stats_rows.get("v0") is None)) and
-                   not self.classification and p.max_depth <= 8 and T * self.n_max < 2 ** 31 and data.n_global > 0)
+                   (not self.classification or cls2) and (p.max_depth <= 8 or deep_switch) and
+                   T * self.n_max < 2 ** 31 and data.n_global > 0)
         # ... and with per-node feature subsets (RandomForest) only each node's sampled features are
         # accumulated (packed statistics only: no v0)
         subset_seg = mseg_ok and need_masks and MSEG_SUBSET and stats_rows.get("v0") is None
@@ -1118,7 +1179,7 @@ class ForestTrainer:
         use_mseg = mseg_ok and (not masked or subset_seg)
         use_seg = USE_SEG and T == 1 and not self.classification and not masked and not use_mseg
         # row records (uint16 weight<<8 | local node) when every level fits 255 nodes per tree
-        use_codes = USE_CODES and p.max_depth <= 8 and not use_seg
+        use_codes = USE_CODES and (p.max_depth <= 8 or (deep_switch and use_mseg)) and not use_seg
         if use_seg:
             w1 = None if weights is None else weights.reshape(-1)
             wmax = int(w1.max().item()) if (w1 is not None and w1.numel()) else 1
@@ -1141,8 +1202,9 @@ class ForestTrainer:
                 # one quantisation scale for every rank: the int64 level histograms then all-reduce to
                 # the same sums on 1 or N GPUs (the forest does not depend on the GPU count)
                 v0s = stats_rows.get("v0")
-                mseg_scales = K.seg_scales(None if v0s is None else v0s.float(), stats_rows["v1"].float(), wmax,
-                                           data.n_global, self.comm)
+                mseg_scales = (1.0, 1.0) if cls2 else \
+                    K.seg_scales(None if v0s is None else v0s.float(), stats_rows["v1"].float(), wmax,
+                                 data.n_global, self.comm)
                 mseg_raw = mseg_scales[1] if v0s is None else mseg_scales
         else:
             node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
@@ -1159,6 +1221,10 @@ class ForestTrainer:
         a_parent = np.full(T, -1, dtype=np.int64)
         prev_hist = None  # [A_prev, d, B, k] histograms of last level's split nodes
         rs_on = False     # this pass reduce-scatters its level histograms by feature (RS_MIN_BYTES)
+        emitted = None    # K.RecordEmit: this level's item records, written by the previous level's partition
+        emits = []        # every RecordEmit of the fit (overflow flags checked at the end)
+        w_total = None    # sum of the root weights (bounds every level's records)
+        rec_buf = None
         root_ids = [None] * T
         for depth in range(p.max_depth + 1):
             A = len(a_tree)
@@ -1167,12 +1233,7 @@ class ForestTrainer:
             # ---- decide which active nodes get a histogram built
             build = np.ones(A, dtype=bool)
             if subtract and depth > 0:
-                # build only the smaller of two active siblings (ties: the first one)
-                has = np.nonzero((a_sib >= 0) & (a_parent >= 0))[0]
-                w_all = self._weights_v(a_stats)
-                wa, ws = w_all[has], w_all[a_sib[has]]
-                lose = (wa > ws) | ((wa == ws) & (has > a_sib[has]))
-                build[has[lose]] = False
+                build = _built_nodes(self._weights_v(a_stats), a_sib, a_parent)
             build_ids = np.nonzero(build)[0]
             slot_of = np.full(A, -1, dtype=np.int32)
             slot_of[build_ids] = np.arange(len(build_ids), dtype=np.int32)
@@ -1199,7 +1260,7 @@ class ForestTrainer:
                 elif 80 < B <= 256 and data.bins_rm is not None:
                     root_rows = data.bins_rm
             root_ok = (root_rows is not None and use_mseg and not use_sub and (depth >= 1 or MSEG_L0) and rec_ok and
-                       len(build_ids) > 0 and np.bincount(slot_tree, minlength=T).max() <= 1)
+                       emitted is None and len(build_ids) > 0 and np.bincount(slot_tree, minlength=T).max() <= 1)
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
                 if use_sub:
                     # every active node over its sampled features; exact int64 (count, sum w q) [A, m, B, 2]
@@ -1219,12 +1280,25 @@ class ForestTrainer:
                                           torch.zeros((S_b, d, B, 2), dtype=torch.int64, device=dev))
                     hist_raw_scale = mseg_raw
                 elif use_mseg and (depth >= 1 or MSEG_L0):
-                    # gather the rows of the built nodes into slot segments, then segment histograms
-                    # packed item records on every device (the CPU emulates the HIP compaction + flat histogram
-                    # exactly, so gloo ranks traverse the integer path RCCL ranks take)
-                    perm, v0p, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, len(build_ids),
-                                                             stats_rows.get("v0"), stats_rows["v1"],
-                                                             rec_scale=mseg_scales[1] if rec_ok else None)
+                    seg_end = None
+                    if emitted is not None:
+                        # the previous level's partition wrote this level's records (partition7 EMIT): segments
+                        # are the plan's capacities, the device cursors their ends
+                        wb = self._weights_v(a_stats)[build_ids]
+                        cap = ((wb.astype(np.int64) + emitted.ch - 1) // emitted.ch) * emitted.ch + emitted.padb
+                        st = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.int64)
+                        perm, v0p, v1p, wp, sg = emitted.rec, None, None, None, np.stack([st, cap], 1)
+                        seg_end = emitted.seg_end()
+                        if K._lib.DEBUG:
+                            self._check_emitted(emitted, st, cap, codes, tfirst, slot_of, len(build_ids),
+                                                stats_rows["v1"], mseg_scales[1])
+                    else:
+                        # gather the rows of the built nodes into slot segments, then segment histograms
+                        # packed item records on every device (the CPU emulates the HIP compaction + flat
+                        # histogram exactly, so gloo ranks traverse the integer path RCCL ranks take)
+                        perm, v0p, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, len(build_ids),
+                                                                 stats_rows.get("v0"), stats_rows["v1"],
+                                                                 rec_scale=mseg_scales[1] if rec_ok else None)
                     is_rec = rec_ok and v1p is None
                     sb = np.concatenate([sg, np.arange(len(build_ids), dtype=np.int64)[:, None]], 1)
                     if subset_seg:
@@ -1241,14 +1315,16 @@ class ForestTrainer:
                         # features, while prev_hist then holds only this rank's feature slice)
                         # comm/compute overlap: the level's slots are built in chunks, each chunk's int64
                         # histogram all-reduced (async, RCCL stream) while the next chunk is built
-                        Hb = self._hist_overlapped(data, d, B, perm, sb, len(build_ids), wmax, mseg_scales, dev)
+                        Hb = self._hist_overlapped(data, d, B, perm, sb, len(build_ids), wmax, mseg_scales, dev,
+                                                   seg_end)
                         hist_raw_scale = mseg_raw
                         reduced = True
                     else:
                         rm, s10 = (data.record_rows() if is_rec else (data.row_major_bins(), False)) \
                             if dev.type == "cuda" else (None, False)
                         Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax,
-                                        mseg_scales, bins_rm=rm, interleave=True, rec=is_rec, raw=True, rm_s10=s10)
+                                        mseg_scales, bins_rm=rm, interleave=True, rec=is_rec, raw=True, rm_s10=s10,
+                                        seg_end=seg_end)
                         hist_raw_scale = mseg_raw
                     del perm, v0p, v1p, wp
                 elif use_seg:
@@ -1271,6 +1347,8 @@ class ForestTrainer:
                 else:
                     Hb = K.hist_moments(data.bins, d, node, weights, stats_rows.get("v0"), stats_rows["v1"],
                                         K.upload(dev, slot_of)[0], slot_tree, fm_build, B, id_tree=id_tree)
+            if cls2 and hist_raw_scale is not None:
+                Hb[..., 0] -= Hb[..., 1]  # packed (W, W1) -> class counts (W0, W1), exact int64
             rs_slice = None
             if not reduced and self._rs_want(Hb, rs_on, sub_feats):
                 rs_on = True
@@ -1296,6 +1374,7 @@ class ForestTrainer:
             masks_t = K.upload(dev, masks_np.view(np.int32))[0] if masks_np is not None else None
             catm_h = None  # left-category bit masks of the native categorical scan
             dec = None     # device-decoded partition tables (partition already queued)
+            em_next = None  # records of the next level written by this level's partition
             if rs_slice is not None or self._native_split(dev):
                 # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
                 mb = p.impurity == "xgb" and self.data.missing_bin
@@ -1322,10 +1401,20 @@ class ForestTrainer:
                     a_tree_d, tf_d = K.upload(dev, a_tree.astype(np.int32), tfirst.numpy().astype(np.int32))
                     dec = K.split_decode(so, tot, a_tree_d, T, p.min_instances, p.min_info_gain,
                                          depth < p.max_depth, depth + 1 >= p.max_depth, missing_bin=mb)
+                    em = None
+                    if (K.EMIT_RECORDS and use_mseg and rec_ok and subtract and not use_sub and w_total is not None
+                            and data.bins_s10 is not None and A <= K.P7_MAX_SLOTS and data.bins.shape[0] <= 16
+                            and T <= 64):
+                        em = self._record_emit(dev, n, A, stats_rows["v1"], mseg_scales[1], w_total, rec_buf)
+                        if em is not None:
+                            rec_buf = em.rec
+                            em.plan(so, dec["child"])
+                            emits.append(em)
+                            em_next = em
                     with _tr.span("tree.partition", depth=depth):
                         K.partition_codes(data.bins, codes, tf_d, dec["tfirst_next"], dec["split_feat"],
                                           dec["split_bin"], dec["cat_off"], dec["masks"].reshape(-1), dec["child"],
-                                          bins_rm=data.row_major_bins() if PARTITION_RM else None)
+                                          bins_rm=data.row_major_bins() if PARTITION_RM else None, emit=em)
                 # so [A, 8] = gain, feature, bin, left (2), right (2), missing-goes-right: copied to the host as is
                 # (plus the node totals at level 0), no per-column device ops
                 sw = so.shape[1]
@@ -1382,6 +1471,8 @@ class ForestTrainer:
                 for t_, fid_ in zip(a_tree.tolist(), a_fid.tolist()):
                     root_ids[t_] = fid_
             W_a = self._weights_v(a_stats)
+            if depth == 0:
+                w_total = float(W_a.sum())  # bounds the records of every later level (each weighs >= 1)
             with np.errstate(invalid="ignore"):
                 can = np.isfinite(gain_h) & (gain_h > 0) & (gain_h >= p.min_info_gain) & \
                     (W_a >= 2 * p.min_instances)
@@ -1456,6 +1547,13 @@ class ForestTrainer:
             n_sib[rp[both]] = lp[both]
             if subtract:
                 n_parent[n_sib < 0] = -1
+            if len(nl) and deep_switch and use_codes and depth + 1 >= 8:
+                # the next level can hold more than 255 nodes per tree: leave the u16 codes for node ids
+                # (active index of the node, -1 = done), partitioned and histogrammed by the node-id kernels
+                node, _ = K.decode_codes(codes, tfirst.to(codes.device))
+                node = node.contiguous()
+                use_codes = use_mseg = False
+                codes = None
             if len(nl):
                 cm = np.stack(cat_masks).view(np.int32) if cat_masks else np.zeros((0, 8), np.int32)
                 with _tr.span("tree.partition", depth=depth):
@@ -1481,7 +1579,10 @@ class ForestTrainer:
             assert len(got) == len(ch_ids) and (not len(got) or got[0] == ch_ids[0])
             forest.set_splits(fid_sp, f_sp, gain_h[sp], b_sp, thr_sp, num, ch_ids[0::2], ch_ids[1::2])
             prev_hist = H if subtract else None
+            emitted = em_next
             a_tree, a_fid, a_key, a_stats, a_sib, a_parent = n_tree, n_fid, n_key, n_stats, n_sib, n_parent
+        if emits and int(torch.stack([e.err for e in emits]).max().item()):
+            raise RuntimeError("partition record emission overflowed its capacity plan")
         forest.roots.extend(root_ids)
         forest._dev = {}
         return forest

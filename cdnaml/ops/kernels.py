@@ -774,12 +774,91 @@ PARTITION7_MIN_T = int(__import__("os").environ.get("CDNAML_PARTITION7_MIN_T", "
 
 
 
+# ------------------------------------------------------------------ K7e: record emission by the partition
+EMIT_RECORDS = __import__("os").environ.get("CDNAML_P7_EMIT", "1") != "0"
+EMIT_CS = 32  # ints between chunk cursors (one 128-byte line each)
+
+
+class RecordEmit:
+    """Device state of one level's record emission (partition7 EMIT, hist5.hip; plan: split.hip emit_plan).
+
+    The partition of level L writes the packed item records of level L + 1's BUILT nodes (smaller active sibling,
+    ties to the left child; a lone active child) into per-slot segments of ``rec``: slot s owns
+    [seg_start[s], seg_lim[s]) with seg_lim - seg_start = roundup(W_s, ch) + padb, and after the partition its
+    records (plus zero-weight padding) are [seg_start[s], cursor[s * cs]).  The host derives the same plan from
+    the decisions it receives (:func:`emit_plan_host`)."""
+
+    def __init__(self, dev, n: int, A: int, rec: torch.Tensor, v1: torch.Tensor, qs1: float, ch: int, waves: int):
+        self.dev, self.ch, self.cs = dev, int(ch), EMIT_CS
+        self.nslots_max = A  # one built child per split at most
+        self.waves = int(waves)
+        self.padb = self.waves * self.ch
+        self.rec, self.v1, self.qs1 = rec, v1.float().contiguous(), float(qs1)
+        ints = torch.empty(2 * A * 3 + 2 * A * self.cs + 2, dtype=torch.int32, device=dev)
+        self.cslot = ints[:2 * A]
+        self.seg_start = ints[2 * A:4 * A]
+        self.seg_lim = ints[4 * A:6 * A]
+        self.cursor = ints[6 * A:6 * A + 2 * A * self.cs]
+        self.nslots = ints[-2:-1]
+        self.err = ints[-1:]
+        self.err.zero_()
+
+    def plan(self, so: torch.Tensor, child: torch.Tensor):
+        A = so.shape[0]
+        sc = so.contiguous()
+        _lib.check(_lib.lib().cdna_emit_plan(_ptr(sc), sc.shape[1], _ptr(child), A, self.ch, int(self.padb),
+                                             _ptr(self.cslot), _ptr(self.seg_start), _ptr(self.seg_lim),
+                                             _ptr(self.cursor), self.cs, _ptr(self.nslots), _stream(self.dev)),
+                   "cdna_emit_plan")
+
+    def seg_end(self):
+        """(cursor tensor, stride): slot s's records end at cursor[s * stride] after the partition."""
+        return self.cursor, self.cs
+
+
+P7_MAX_SLOTS = 256  # kP7MaxS (hist5.hip)
+
+
+def partition7_waves(n: int, G: int) -> int:
+    """Waves of an emitting partition7 launch over n rows (its zero padding is bounded by one chunk per wave)."""
+    return int(_lib.lib().cdna_partition7_waves(int(n), int(G), 1))
+
+
+def emit_chunk(records_est: float, waves: int, slots_est: int) -> int:
+    """Chunk length: a power of two near 1/16 of a wave's expected records per slot (so the zero padding of
+    each wave's last chunk stays a few percent of the level), in [8, 128]."""
+    per = records_est / max(1, waves * max(1, slots_est))
+    ch = 8
+    while ch < 128 and ch * 32 <= per:
+        ch *= 2
+    return ch
+
+
+def emit_plan_host(w_left: np.ndarray, w_right: np.ndarray, child: np.ndarray, ch: int, padb: int):
+    """Host twin of emit_plan_kernel: (cslot [2A], seg_start [S], cap [S]) from the level's left / right child
+    weights and the active-children table ``child`` [2A] (-1: not active)."""
+    A = len(w_left)
+    c = np.asarray(child).reshape(A, 2)
+    wl, wr = np.asarray(w_left, np.float64), np.asarray(w_right, np.float64)
+    bl = (c[:, 0] >= 0) & ((c[:, 1] < 0) | (wl <= wr))
+    br = (c[:, 1] >= 0) & ((c[:, 0] < 0) | (wr < wl))
+    built = np.stack([bl, br], 1).reshape(-1)
+    w = np.stack([wl, wr], 1).reshape(-1)
+    cslot = np.full(2 * A, -1, dtype=np.int64)
+    cslot[built] = np.arange(int(built.sum()))
+    cap = ((w[built].astype(np.int64) + ch - 1) // ch) * ch + padb
+    start = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.int64) if len(cap) else np.zeros(0, np.int64)
+    return cslot, start, cap
+
+
 def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tensor, tfirst_next: torch.Tensor,
                     split_feat: torch.Tensor, split_bin: torch.Tensor, cat_off: torch.Tensor,
-                    cat_mask: torch.Tensor, child: torch.Tensor, bins_rm: Optional[torch.Tensor] = None) -> None:
+                    cat_mask: torch.Tensor, child: torch.Tensor, bins_rm: Optional[torch.Tensor] = None,
+                    emit: Optional["RecordEmit"] = None) -> None:
     """In place: every row's code moves to the chosen child's local index (255 = done).
 
-    bins_rm: optional row-major copy [n, G, 8] of the bins, read instead of ``bins`` when given."""
+    bins_rm: optional row-major copy [n, G, 8] of the bins, read instead of ``bins`` when given.
+    emit: (GPU, partition7) also write the next level's item records of the built children (:class:`RecordEmit`)."""
     G, n, _ = bins.shape
     T = codes.shape[0]
     if n == 0 or T == 0:
@@ -799,11 +878,20 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
         # partition7 streams every bins word of every row once per level (10 GB at 1e8 x 100): it pays when
         # many trees share that pass; for few trees partition5's per-(row, tree) byte gathers move less (GBDT,
         # T = 1: 57.9 vs 40.6 ms per boosting round with partition7; CV grid with 5 / 10 trees: 2.18 vs 1.34 s)
-        if PARTITION7 and T >= PARTITION7_MIN_T and G <= 16 and A <= 1024 and T <= 64 and bins_rm is None:
-            _lib.check(_lib.lib().cdna_partition7(_ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]),
-                                                  _ptr(args[1]), _ptr(args[2]), _ptr(args[3]), _ptr(args[4]),
-                                                  _ptr(cm), _ptr(args[5]), _stream(bins.device)), "cdna_partition7")
+        if emit is not None or (PARTITION7 and T >= PARTITION7_MIN_T and G <= 16 and A <= 1024 and T <= 64 and
+                                bins_rm is None):
+            e = emit
+            _lib.check(_lib.lib().cdna_partition7(
+                _ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]), _ptr(args[2]), _ptr(args[3]),
+                _ptr(args[4]), _ptr(cm), _ptr(args[5]),
+                None if e is None else _ptr(e.cslot), None if e is None else _ptr(e.v1),
+                0.0 if e is None else float(e.qs1), None if e is None else _ptr(e.rec),
+                None if e is None else _ptr(e.cursor), 1 if e is None else e.cs,
+                None if e is None else _ptr(e.seg_lim), 0 if e is None else e.nslots_max,
+                1 if e is None else e.ch, None if e is None else _ptr(e.err), _stream(bins.device)),
+                "cdna_partition7")
             return
+        assert emit is None
         src, rm_bytes = bins, 0
         if bins_rm is not None:
             assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
@@ -1156,8 +1244,11 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
              v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
              scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False,
              rec: bool = False, raw: bool = False, out: Optional[torch.Tensor] = None,
-             rm_s10: bool = False) -> torch.Tensor:
+             rm_s10: bool = False, seg_end=None) -> torch.Tensor:
     """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
+
+    seg_end (rec + rm_s10, GPU): (tensor, stride) -- records emitted by the partition (:class:`RecordEmit`): the
+    segments in ``segs`` are capacities and slot s's records end at tensor[s * stride] (work items clipped).
 
     rm_s10 (rec): ``bins_rm`` is in the seg10 layout (:func:`bins_seg10`): the six-items-per-wave kernel.
 
@@ -1172,8 +1263,9 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
     if out is not None:
         assert rec and raw and out.dtype == torch.int64 and out.is_contiguous()
     if rec:
-        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw, out, rm_s10)
-    assert not rm_s10
+        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw, out, rm_s10,
+                             seg_end)
+    assert not rm_s10 and seg_end is None
     return _seg_hist(bins, d, B, perm, v0p, v1p, wp, segs, S, wmax, scales, bins_rm, interleave, raw)
 
 
@@ -1221,7 +1313,8 @@ def rec_encode(rows: torch.Tensor, w: torch.Tensor, q: torch.Tensor) -> torch.Te
     return rows.to(torch.int64) | (w.to(torch.int64) << 31) | ((q.to(torch.int64) + (1 << 23)) << 39)
 
 
-def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False, out=None, rm_s10=False):
+def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False, out=None, rm_s10=False,
+                  seg_end=None):
     G, n, _ = bins.shape
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
     if S == 0 or len(segs) == 0:
@@ -1230,6 +1323,7 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
     qs1 = float(scales[1])
     if not _native(bins):
+        assert seg_end is None
         pos, slot = _seg_items(segs)
         rows, w, q = rec_decode(rec[pos])
         iout = _int_hist_cpu(bins, d, B, S, rows, slot, w, w * q)
@@ -1258,8 +1352,12 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         if rm_s10:
             assert d <= 100 and B <= 40 and bins_rm.shape[1] == 16
             mode |= 128 | 256
+        if seg_end is not None:
+            assert rm_s10, "emitted records (seg_end) need the seg10 record kernel"
         _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(bins_rm), n, d, B, _ptr(rec), None, None, None,
                                             _ptr(wt), len(work), 1.0, qs1, _ptr(iout), bins_rm.shape[1],
+                                            None if seg_end is None else _ptr(seg_end[0]),
+                                            0 if seg_end is None else int(seg_end[1]),
                                             _stream(bins.device)), "cdna_seg_hist(rec)")
     if raw:
         return iout
@@ -1416,7 +1514,8 @@ def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optio
         src = bins if bins_rm is None else bins_rm
         _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(src), n, d, B, _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp),
                                             _ptr(wt), len(work), float(qs0), float(qs1), _ptr(iout),
-                                            0 if bins_rm is None else bins_rm.shape[1], _stream(bins.device)),
+                                            0 if bins_rm is None else bins_rm.shape[1], None, 0,
+                                            _stream(bins.device)),
                    "cdna_seg_hist")
     if raw:
         return iout

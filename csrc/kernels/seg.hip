@@ -40,6 +40,10 @@ struct SegHistArgs {
   // optional packed item records (flat kernel, REC): row | weight << 31 | (q1 + 2^23) << 39 (see CompactWArgs)
   const uint64_t* rec = nullptr;
   int rs = 0;  // row stride of the row-major bins in 8-byte words (0: G); 16 = one 128-byte line per row
+  // optional per-slot record ends (records emitted by the partition, hist5.hip partition7 EMIT): a work item's
+  // length is clipped to seg_end[slot * seg_end_stride] - start (work lists are cut from segment capacities)
+  const int* seg_end = nullptr;
+  int seg_end_stride = 0;
 };
 
 // PACKED: one u64 atomic per update (count << 44 | sum of w * (q + 2^23)); the
@@ -534,8 +538,14 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_kernel(const SegHistArgs
   constexpr int TH = 1024, NW = TH / 64, IPW = 6;
   constexpr int PLANE = BP * 32;  // u64 cells per feature plane j
   __shared__ __attribute__((aligned(16))) unsigned long long h[10 * PLANE];  // [10][BP][32]
-  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
+  const int start = a.work[3 * blockIdx.x], slot = a.work[3 * blockIdx.x + 2];
+  int len = a.work[3 * blockIdx.x + 1];
   if (!CDNA_DCHECK(start >= 0 && len >= 0 && slot >= 0, 0x5E83u)) return;  // corrupt work item
+  if (a.seg_end) {  // block-uniform: past the slot's emitted records (capacity chunk) -> nothing to do
+    const int e = a.seg_end[(int64_t)slot * a.seg_end_stride] - start;
+    len = len < e ? len : e;
+    if (len <= 0) return;
+  }
   for (int i = threadIdx.x; i < 10 * PLANE; i += TH) h[i] = 0ull;
   __syncthreads();
   const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
@@ -1485,13 +1495,18 @@ CDNA_API int cdna_seg_hist_root(const uint8_t* bins_s10, int64_t n, int d, int B
 // bit2: bins are row-major [n][G] words (seg_hist_flat_kernel when packed and all groups fit 128 KB of LDS,
 // else seg_hist_rm_kernel); bit3: force seg_hist_rm_kernel.
 // work: [nwork][3] {start, len, slot}; grid = nwork x ceil(d / 8).
+// seg_end (optional, seg10 record histograms only): per-slot record ends [slot * seg_end_stride].
 CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int B, const int* perm, const float* v0p,
                            const float* v1p, const uint8_t* wp, const int* work, int nwork, float qs0, float qs1,
-                           unsigned long long* out, int rm_stride, hipStream_t st) {
+                           unsigned long long* out, int rm_stride, const int* seg_end, int seg_end_stride,
+                           hipStream_t st) {
   if (nwork <= 0) return 0;
   if (rm_stride != 0 && rm_stride < (d + 7) / 8) return (int)hipErrorInvalidValue;
+  if (seg_end && (!(mode & 256) || seg_end_stride < 1)) return (int)hipErrorInvalidValue;
   SegHistArgs a{bins, n, d, B, perm, v0p, v1p, wp, work, qs0, qs1, out};
   a.rs = rm_stride;
+  a.seg_end = seg_end;
+  a.seg_end_stride = seg_end_stride;
   const bool packed = (mode & 1) != 0, has_w = (mode & 2) != 0;
   if ((mode & 128) && (mode & 16) && (mode & 4) && packed) {
     // lane-feature kernel: 128 features per block (4 byte planes of BP >= B bins x 32 lanes, BP KB of LDS);

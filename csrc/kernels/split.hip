@@ -704,3 +704,91 @@ CDNA_API int cdna_split_decode(const double* so, int sw, const double* tot, int 
                      pref, tfirst_next);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------- emit_plan
+// The next level's histogram slots and record segments, on the device, right behind split_decode: the row
+// partition then writes each built child's item records itself (partition7 EMIT, hist5.hip) instead of a
+// codes_count_w + codes_scatter_w pass over the new codes.  The host derives the same plan from the same
+// decisions (engine.py: smaller active sibling built, ties to the left child; a lone active child built).
+//   built(2a + s) = child active && (sibling inactive || W_s < W_other || (W_s == W_other && s == 0))
+//   cslot[2a + s] = exclusive count of built children before it (-1: not built)
+//   seg_start[slot] = exclusive prefix of cap = roundup(W, CH) + padb (records <= W: every record weighs >= 1;
+//                     padb bounds the zero-padded tail chunks, one per partition wave)
+//   seg_lim[slot] = seg_start + cap;  cursor[slot * cs] = seg_start (atomic chunk cursors, one per 128-B line)
+namespace {
+
+__global__ __launch_bounds__(1024) void emit_plan_kernel(const double* __restrict__ so, int sw, const int* __restrict__ child,
+                                                         int A, int ch, int64_t padb, int* __restrict__ cslot,
+                                                         int* __restrict__ seg_start, int* __restrict__ seg_lim,
+                                                         int* __restrict__ cursor, int cs, int* __restrict__ nslots) {
+  __shared__ int s_wave[16];
+  __shared__ int64_t s_cap[1024];
+  __shared__ int s_carry;
+  __shared__ int64_t s_ccap;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    s_carry = 0;
+    s_ccap = 0;
+  }
+  __syncthreads();
+  for (int base = 0; base < 2 * A; base += 1024) {
+    const int e = base + threadIdx.x;
+    int flag = 0;
+    int64_t cap = 0;
+    if (e < 2 * A) {
+      const int a = e >> 1, s = e & 1;
+      const int me = child[e], other = child[e ^ 1];
+      const double wm = so[(int64_t)a * sw + (s == 0 ? 3 : 5)], wo = so[(int64_t)a * sw + (s == 0 ? 5 : 3)];
+      flag = me >= 0 && (other < 0 || wm < wo || (wm == wo && s == 0)) ? 1 : 0;
+      if (flag) cap = ((((int64_t)wm + ch - 1) / ch) * ch) + padb;
+    }
+    const uint64_t m = __builtin_amdgcn_ballot_w64(flag != 0);
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) s_wave[wid] = __builtin_popcountll(m);
+    // inclusive scan of the capacities (Hillis-Steele over the block)
+    s_cap[threadIdx.x] = cap;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int64_t v = threadIdx.x >= o ? s_cap[threadIdx.x - o] : 0;
+      __syncthreads();
+      s_cap[threadIdx.x] += v;
+      __syncthreads();
+    }
+    int before = 0, total = 0;
+    for (int w = 0; w < 16; ++w) {
+      before += w < wid ? s_wave[w] : 0;
+      total += s_wave[w];
+    }
+    if (e < 2 * A) {
+      const int slot = s_carry + before + below;
+      cslot[e] = flag ? slot : -1;
+      if (flag) {
+        const int64_t st = s_ccap + s_cap[threadIdx.x] - cap;
+        seg_start[slot] = (int)st;
+        seg_lim[slot] = (int)(st + cap);
+        cursor[(int64_t)slot * cs] = (int)st;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_carry += total;
+      s_ccap += s_cap[1023];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *nslots = s_carry;
+}
+
+}  // namespace
+
+// so [A][sw] K6 decisions (left / right weights at columns 3 / 5), child [2A] from split_decode; outputs sized
+// 2A (cslot) and 2A (seg_start, seg_lim; the first nslots used), cursor [2A * cs].  The host bounds the total
+// capacity below 2^31.
+CDNA_API int cdna_emit_plan(const double* so, int sw, const int* child, int A, int ch, int64_t padb, int* cslot,
+                            int* seg_start, int* seg_lim, int* cursor, int cs, int* nslots, hipStream_t st) {
+  if (A <= 0) return 0;
+  if (sw < 7 || ch < 1 || (ch & (ch - 1)) || cs < 1 || padb < 0 || padb % ch) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(emit_plan_kernel, dim3(1), dim3(1024), 0, st, so, sw, child, A, ch, padb, cslot, seg_start,
+                     seg_lim, cursor, cs, nslots);
+  return (int)hipGetLastError();
+}
