@@ -320,9 +320,52 @@ def bench_airbnb(spark, args):
           f"dp{spark.comm.world_size}")
 
 
+def bench_ooc(spark, args):
+    """Out-of-core fits over a STREAMED frame too large for resident fp32 X: 5e8 x 100 rows
+    (200 GB of fp32 features) generated chunk by chunk on the device (``device_chunks``; Philox normals keyed by
+    global row id, label = a nonlinear function of the chunk's features), so every pass over the data -- the
+    label pass, the quantile-sample pass, the binning pass (RF) or the Gram pass (LR) -- regenerates the rows and
+    the generation is inside the timed region.  Resident: uint8 bins (+ seg10 rows), labels, codes.
+    --model lr (default) | rf (RandomForestRegressor numTrees=--trees (4), maxDepth 5, maxBins 40)."""
+    from cdnaml.models.inference import device_chunks
+    from cdnaml.models.regression import LinearRegression, RandomForestRegressor
+    from cdnaml.ops import kernels as K
+    dev = spark.device
+    comm = spark.comm
+    n_total = int(args.rows or 5e8)
+    chunk = int(args.chunk)
+    per_rank = n_total // comm.world_size
+    n_chunks = max(1, per_rank // chunk)
+    rows = n_chunks * chunk * comm.world_size
+    row_base = comm.rank * n_chunks * chunk
+    wv = torch.randn(100, generator=torch.Generator(device=dev).manual_seed(3), device=dev)
+
+    def make(r0, n, bufs):
+        X = bufs["features"][:n]
+        K.normal32_(X, 11, (row_base + r0) * 100, 0x10)
+        torch.matmul(X, wv, out=bufs["label"][:n])
+        bufs["label"][:n].add_(torch.sin(2.0 * X[:, 0]))
+    df = device_chunks(spark, n_chunks * chunk, chunk, make,
+                       {"features": ((100,), torch.float32), "label": ((), torch.float32)})
+    if args.model == "rf":
+        T = int(args.trees or 4)
+        est = RandomForestRegressor(numTrees=T, maxDepth=5, maxBins=40, seed=42)
+        name = f"RandomForestRegressor(numTrees={T},maxDepth=5,maxBins=40) streamed"
+    else:
+        est = LinearRegression()
+        name = "LinearRegression(d=100) streamed"
+    ms, model = _timed(spark, lambda: est.fit(df), args.steps, args.warmup)
+    peak = torch.cuda.max_memory_allocated(dev) / 2 ** 30 if dev.type == "cuda" else 0.0
+    _log(f"ooc {args.model}: {ms:.1f} ms per fit, {rows / ms * 1e3:.3e} rows/s, peak allocated {peak:.1f} GiB "
+         f"(fp32 X would be {rows * 400 / 2 ** 30:.0f} GiB)")
+    _emit(spark, f"rows/sec out-of-core fit ({name})", rows / ms * 1e3, "rows/s", args.steps, args.warmup, ms, True,
+          "strong", "fp32", name, rows, f"dp{comm.world_size}")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("config", choices=["lr", "cv", "clf", "gbdt", "infer", "airbnb", "relational", "expr"])
+    ap.add_argument("config", choices=["lr", "cv", "clf", "gbdt", "infer", "airbnb", "relational", "expr", "ooc"])
+    ap.add_argument("--model", choices=["lr", "rf"], default="lr", help="ooc: the streamed estimator")
     ap.add_argument("--rows", type=float, default=None)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
@@ -338,6 +381,7 @@ def main():
     import cdnaml
     spark = cdnaml.SparkSession.builder.appName("bench_configs").getOrCreate()
     {"lr": bench_lr, "cv": bench_cv, "clf": bench_clf, "gbdt": bench_gbdt, "infer": bench_infer, "airbnb": bench_airbnb,
+     "ooc": bench_ooc,
      "relational": bench_relational, "expr": bench_expr}[
         args.config](spark, args)
     spark.comm.shutdown()

@@ -17,6 +17,7 @@ from typing import Optional
 
 import numpy as np
 import torch
+from scipy.linalg import cho_factor as _scipy_cho_factor, cho_solve as _scipy_cho_solve
 
 from ..ops import kernels as K
 from ..sql import types as T
@@ -27,7 +28,7 @@ from .linalg import DenseVector, SparseVector
 from .param import NO_DEFAULT, TypeConverters as TC, keyword_init
 from .tree.engine import Forest, ForestTrainer, TreeParams, make_binned
 from .util import (IllegalArgumentException, categorical_info, global_count, global_offset, local_batch,
-                   local_xyw, require_vector)
+                   local_xyw, require_vector, streamed_columns)
 
 _PRED = {
     "featuresCol": ("features column name", "features", TC.toString),
@@ -132,6 +133,30 @@ class LinearRegressionTrainingSummary(_RegressionSummary):
         return [float(2 * stats.t.sf(abs(t), dof)) for t in self.tValues]
 
 
+def _lr_shift(Xk: torch.Tensor, yk: torch.Tensor, comm, d: int) -> torch.Tensor:
+    """[d + 1] fp64 common shift of the features and the label: the mean of every rank's leading rows (averaged
+    over the ranks that have any).  It only conditions the f32 Gram; the solve un-shifts exactly with the host
+    copy of the same values."""
+    k = Xk.shape[0]
+    if comm.distributed:
+        sh = torch.cat([Xk.double().mean(0), yk.double().mean().reshape(1)]) if k else \
+            torch.zeros(d + 1, dtype=torch.float64, device=Xk.device)
+        cnt = torch.full((1,), 1.0 if k else 0.0, dtype=torch.float64, device=Xk.device)
+        comm.all_reduce_many([sh, cnt])
+        return sh / cnt.clamp_min(1.0)
+    # one rank: one reduction, no all-reduce bookkeeping
+    return torch.cat([Xk, yk[:, None].to(Xk.dtype)], 1).double().mean(0) if k else \
+        torch.zeros(d + 1, dtype=torch.float64, device=Xk.device)
+
+
+def _cho_factor(A):
+    return _scipy_cho_factor(A, lower=True, check_finite=False)
+
+
+def _cho_solve(cl, b):
+    return _scipy_cho_solve(cl, b, check_finite=False)
+
+
 # =========================================================== LinearRegression
 class LinearRegression(Estimator):
     _params = dict(_PRED, **{
@@ -161,6 +186,9 @@ class LinearRegression(Estimator):
         require_vector(dataset, fc)
         from .util import require_numeric
         require_numeric(dataset, lc)
+        src = streamed_columns(dataset, fc, [lc] + ([wc] if wc else []), head_rows=4096)
+        if src is not None:
+            return self._fit_streamed(dataset, src, lc, wc)
         X, y, w = local_xyw(dataset, fc, lc, wc)
         comm = dataset._session.comm
         d = X.shape[1]
@@ -170,12 +198,7 @@ class LinearRegression(Estimator):
         bf16 = self.getGramPrecision() == "bf16"
         sh = None
         if fit_int:
-            k = min(X.shape[0], 4096)
-            sh = torch.cat([X[:k].double().mean(0), y[:k].double().mean().reshape(1)]) if k else \
-                torch.zeros(d + 1, dtype=torch.float64, device=X.device)
-            cnt = torch.full((1,), 1.0 if k else 0.0, dtype=torch.float64, device=X.device)
-            comm.all_reduce_many([sh, cnt])
-            sh = sh / cnt.clamp_min(1.0)
+            sh = _lr_shift(X[:4096], y[:4096], comm, d)
             shift, yc = sh[:d].float(), y - sh[d]
         else:
             shift, yc = None, y
@@ -204,6 +227,51 @@ class LinearRegression(Estimator):
         preds = model.transform(dataset)
         model.summary = LinearRegressionTrainingSummary(preds, lc, self.getPredictionCol(), d, hist, iters,
                                                         stderr, coef, intercept)
+        return model
+
+    def _fit_streamed(self, dataset, src, lc, wc):
+        """Out-of-core fit: K1 Gram blocks accumulated chunk by chunk in fp64 (X never resident),
+        the shift taken from the first chunk's leading rows, then the same solve as the materialised fit."""
+        Xs, cd, _ = src
+        comm = dataset._session.comm
+        d = Xs.d
+        y = cd[lc].values.double()
+        w = cd[wc].values.double() if wc else None
+        fit_int = self.getFitIntercept()
+        bf16 = self.getGramPrecision() == "bf16"
+        dev = Xs.device
+        head = cd["__head__"]
+        sh = _lr_shift(head, y[:head.shape[0]], comm, d) if fit_int else \
+            torch.zeros(d + 1, dtype=torch.float64, device=dev)
+        shift = sh[:d].float() if fit_int else None
+        extra = 1 if w is not None else 0
+        G = torch.zeros((d + 2 + extra, d + 2 + extra), dtype=torch.float64, device=dev)
+        for r0, Xc in Xs:
+            m = Xc.shape[0]
+            yc_ = y[r0:r0 + m]
+            ycc = yc_ - sh[d] if fit_int else yc_
+            if m == 0:
+                continue
+            if w is None:
+                G += K.gram(Xc, ycc, shift, 0.0, bf16=bf16)
+            else:
+                sw = torch.sqrt(w[r0:r0 + m]).float()[:, None]
+                Xw = torch.cat([(Xc.float() - (shift if shift is not None else 0.0)) * sw, sw], 1)
+                G += K.gram(Xw, ycc.float() * sw[:, 0], None, 0.0, bf16=bf16)
+        if w is not None:
+            keep = torch.tensor(list(range(d + 1)) + [d + 2], device=dev)
+            G = G[keep][:, keep].contiguous()
+        comm.all_reduce(G)
+        host = torch.cat([G.reshape(-1), sh]).cpu().numpy()
+        Gh = host[:(d + 2) * (d + 2)].reshape(d + 2, d + 2)
+        yshift = float(host[-1]) if fit_int else 0.0
+        shift_h = host[(d + 2) * (d + 2):(d + 2) * (d + 2) + d].astype(np.float32).astype(np.float64) \
+            if fit_int else None
+        coef, intercept, hist, iters, stderr = self._solve(Gh, d, shift_h, yshift)
+        model = LinearRegressionModel(coef, intercept)
+        model._post_fit(self)
+        model.summary = LinearRegressionTrainingSummary(model.transform(dataset), lc, self.getPredictionCol(), d,
+                                                        hist, iters, stderr, coef, intercept)
         return model
 
     def _solve(self, G, d, shift, yshift):
@@ -256,8 +324,9 @@ class LinearRegression(Estimator):
             if lam == 0.0 or alpha == 0.0:
                 A = Ma + np.diag(l2)
                 try:
-                    L = np.linalg.cholesky(A)
-                    b = np.linalg.solve(L.T, np.linalg.solve(L, ca))
+                    # SPD: Cholesky (raises when not positive definite) + two triangular solves, in LAPACK
+                    c_, low = _cho_factor(A)
+                    b = _cho_solve((c_, low), ca)
                 except np.linalg.LinAlgError:
                     b = np.linalg.lstsq(A, ca, rcond=None)[0]
                 iters = 1
@@ -424,14 +493,22 @@ def tree_fit_prepare(est, dataset, classification: bool, pre=None):
     require_vector(dataset, fc)
     session = dataset._session
     cols = [fc, lc] + ([wc] if wc else [])
-    b = local_batch(dataset, cols)
-    fcol = b.columns[fc]
-    X = fcol.values.float()
-    X = X if X.is_contiguous() else X.contiguous()
-    y = b.columns[lc].values.double()
-    w = b.columns[wc].values.double() if wc else None
+    src = streamed_columns(dataset, fc, cols[1:])
+    if src is not None:
+        # out-of-core: X streamed chunk by chunk into the quantile sample and the bins, never resident
+        X, cd, fmeta = src
+        y = cd[lc].values.double()
+        w = cd[wc].values.double() if wc else None
+    else:
+        b = local_batch(dataset, cols)
+        fcol = b.columns[fc]
+        fmeta = fcol.meta
+        X = fcol.values.float()
+        X = X if X.is_contiguous() else X.contiguous()
+        y = b.columns[lc].values.double()
+        w = b.columns[wc].values.double() if wc else None
     d = X.shape[1]
-    cat = categorical_info(fcol.meta, d, fc)
+    cat = categorical_info(fmeta, d, fc)
     n = X.shape[0]
     n_global = global_count(session, n)
     off = global_offset(session, n)
@@ -441,7 +518,7 @@ def tree_fit_prepare(est, dataset, classification: bool, pre=None):
     if pre is not None:
         pre(n, off, seed, X.device, y)
     data = make_binned(session, X, cat, est.getMaxBins(), seed, off, n_global)
-    return session, data, y, w, seed, fcol.meta
+    return session, data, y, w, seed, fmeta
 
 
 def _num_classes(session, y: torch.Tensor, meta_label: Optional[dict]) -> int:

@@ -249,14 +249,39 @@ def find_thresholds_t(samp: torch.Tensor, max_bins: int, categorical: Dict[int, 
     return thr, nthr
 
 
-def _global_sample(session, X: torch.Tensor, max_bins: int, seed: int, row_offset: int, n_global: int):
+class ChunkedRows:
+    """This rank's feature rows as a re-iterable stream of ``(row0, X_chunk [m, d] f32)`` (out-of-core fits,
+    SURVEY §5.7): the quantile sample and the binning read the chunks one at a time, so fp32 X is never
+    resident -- only its uint8 bins are.  ``it_fn()`` starts a new pass; chunks are transient (the source may
+    reuse their buffers once the work queued on them has run)."""
+
+    def __init__(self, it_fn, n: int, d: int, device):
+        self.it_fn, self.n, self.d, self.device = it_fn, int(n), int(d), torch.device(device)
+        self.shape = (self.n, self.d)
+        self.is_cuda = self.device.type == "cuda"
+
+    def __iter__(self):
+        return iter(self.it_fn())
+
+
+def _global_sample(session, X, max_bins: int, seed: int, row_offset: int, n_global: int):
     """Rows sampled by Philox keyed on the GLOBAL row id (the same rows whatever the GPU count), gathered
-    from every rank: the split-candidate sample."""
+    from every rank: the split-candidate sample.  ``X`` may be a :class:`ChunkedRows` stream (the same rows,
+    sampled chunk by chunk)."""
     comm = session.comm
     n = X.shape[0]
     target = max(max_bins * max_bins, 10000)
     frac = min(1.0, target / max(n_global, 1))
-    if frac < 1.0:
+    if isinstance(X, ChunkedRows):
+        parts = []
+        for r0, Xc in X:
+            if frac < 1.0:
+                u = K.uniform(Xc.shape[0], seed ^ 0x5BD1E995, row_offset + r0, 3, device=Xc.device)
+                parts.append(Xc[K.compact_mask(u < frac)].float())
+            else:
+                parts.append(Xc.float().clone())
+        samp = torch.cat(parts) if parts else torch.zeros((0, X.d), dtype=torch.float32, device=X.device)
+    elif frac < 1.0:
         u = K.uniform(n, seed ^ 0x5BD1E995, row_offset, 3, device=X.device)
         samp = X[K.compact_mask(u < frac)]
     else:
@@ -271,6 +296,8 @@ def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins:
     """:func:`_make_binned`, reused across the trials of one hyperparameter search (bincache.scope(), entered by
     fmin; never outside one)."""
     from . import bincache
+    if isinstance(X, ChunkedRows):  # streamed: no content fingerprint (X is never resident)
+        return _make_binned(session, X, categorical, max_bins, seed, row_offset, n_global, missing)
     return bincache.cached(
         lambda: (bincache.fingerprint(X), tuple(sorted(categorical.items())), int(max_bins), int(seed),
                  int(row_offset), int(n_global), None if missing is None else float(missing), str(X.device)),
@@ -278,7 +305,29 @@ def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins:
         comm=session.comm)
 
 
-def _make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins: int, seed: int,
+def _binize_src(X, thr, nthr, missing=None, want_rm=False, rm_layout="std"):
+    """K.binize of a tensor, or of a ChunkedRows stream chunk by chunk into full-size bins (and row copy)."""
+    if not isinstance(X, ChunkedRows):
+        return K.binize(X, thr, nthr, missing=missing, want_rm=want_rm, rm_layout=rm_layout)
+    n, d = X.shape
+    G = (d + 7) // 8
+    bins = torch.empty((G, n, 8), dtype=torch.uint8, device=X.device)
+    rm = None
+    if want_rm and X.is_cuda:
+        s10 = rm_layout == "s10"
+        Gs = 16 if (s10 or (K.BINS_RM_PAD and G <= 16)) else G
+        rm = torch.empty((n, Gs, 8), dtype=torch.uint8, device=X.device)
+    rm_ok = rm is not None
+    for r0, Xc in X:
+        res = K.binize(Xc, thr, nthr, missing=missing, want_rm=rm_ok, rm_layout=rm_layout,
+                       out_full=(bins, rm), row0=r0)
+        rm_ok = rm_ok and res[1] is not None
+    if want_rm and not rm_ok:  # a chunk took a kernel without the row copy: rebuilt from the bins on demand
+        rm = None if rm_layout != "s10" or not X.is_cuda else K.bins_seg10(bins, d)
+    return bins, (rm if want_rm else None)
+
+
+def _make_binned(session, X, categorical: Dict[int, int], max_bins: int, seed: int,
                  row_offset: int, n_global: int, missing: Optional[float] = None) -> BinnedData:
     """Global-sample quantile thresholds + device binning.
 
@@ -302,9 +351,10 @@ def _make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins
         nthr = inthr + 1
         thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
         with _tr.span("tree.binize"):
-            bins, rm = K.binize(X, thr_t, torch.from_numpy(nthr).to(X.device), missing=float(missing),
-                                want_rm=True)
-        return BinnedData(X, bins, thr, nthr, {}, X.shape[0], n_global, row_offset, d, max_bins, True, rm)
+            bins, rm = _binize_src(X, thr_t, torch.from_numpy(nthr).to(X.device), missing=float(missing),
+                                   want_rm=True)
+        return BinnedData(_resident(X), bins, thr, nthr, {}, X.shape[0], n_global, row_offset, d, max_bins, True,
+                          rm)
     for f, k in categorical.items():
         if k > max_bins:
             raise IllegalArgumentException(
@@ -317,7 +367,7 @@ def _make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins
     n = X.shape[0]
     samp = _global_sample(session, X, max_bins, seed, row_offset, n_global)
     s10 = _seg10_ok(X, d, max_bins)
-    if SPEC_THRESHOLDS and not categorical and X.is_cuda:
+    if SPEC_THRESHOLDS and not categorical and X.is_cuda and not isinstance(X, ChunkedRows):
         # the binning queued straight on the K3 kernel's device thresholds; the host checks behind it that every
         # feature had more than max_bins distinct sample values (then the thresholds are exactly the host path's)
         # -- no device -> host -> device round trip between the quantile kernel and the binning
@@ -340,11 +390,17 @@ def _make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins
     nthr_t = torch.from_numpy(nthr).to(X.device)
     with _tr.span("tree.binize"):
         # the row-major copy (segment histograms' row gathers) comes out of the same kernel
-        bins, rm = K.binize(X, thr_t, nthr_t, want_rm=True, rm_layout="s10" if s10 else "std")
+        bins, rm = _binize_src(X, thr_t, nthr_t, want_rm=True, rm_layout="s10" if s10 else "std")
     if s10:
-        return BinnedData(X, bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins, False,
-                          None, rm)
-    return BinnedData(X, bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins, False, rm)
+        return BinnedData(_resident(X), bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins,
+                          False, None, rm)
+    return BinnedData(_resident(X), bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins,
+                      False, rm)
+
+
+def _resident(X):
+    """BinnedData.X: the feature matrix, or None for a streamed (out-of-core) source."""
+    return None if isinstance(X, ChunkedRows) else X
 
 
 # ============================================================ forest storage

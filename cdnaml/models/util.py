@@ -69,6 +69,55 @@ def local_xyw(df, features_col: str, label_col: Optional[str] = None, weight_col
     return X, y, w
 
 
+# out-of-core fits: a training frame over a streamed source (createDataFrameFromChunks /
+# device_chunks) is never materialised -- its label / weight columns are collected, its features read chunk by chunk
+OOC_FIT = __import__("os").environ.get("CDNAML_OOC_FIT", "1") != "0"
+
+
+def streamed_columns(df, features_col: str, cols: List[str], head_rows: int = 0):
+    """For a streamable training frame: ``(ChunkedRows over the features, {col: ColumnData}, feature metadata)``
+    after one pass that collects the other (small) columns and counts the rows; None when the frame is not
+    streamed (the caller materialises it) or a collected column has nulls.  ``head_rows``: the dict also holds
+    ``"__head__"``, a copy of the first rows' features (at most that many)."""
+    from .tree.engine import ChunkedRows
+    if not OOC_FIT:
+        return None
+    sel = df.select(features_col, *cols)
+    if not sel._plan.streamable:
+        return None
+    parts = {c: [] for c in cols}
+    n, d = 0, None
+    head = []
+    for b in sel._plan.iter_execute():
+        if n < head_rows:
+            head.append(b.columns[features_col].values[:head_rows - n].float().clone())
+        for c in cols:
+            cd = b.columns[c]
+            if cd.valid is not None and not bool(cd.valid.all()):
+                return None  # null labels / weights: the materialised path drops those rows
+            parts[c].append(cd.values.clone())  # the source reuses its chunk buffers
+        d = int(b.columns[features_col].values.shape[1])
+        n += b.n
+    if d is None:
+        return None
+    dev = df._session.device
+    out = {}
+    for c in cols:
+        f = sel.schema[c]
+        v = torch.cat(parts[c]) if parts[c] else torch.zeros(0, device=dev)
+        out[c] = ColumnData(v.to(dev), f.dataType)
+    if head_rows:
+        out["__head__"] = torch.cat(head).to(dev) if head else torch.zeros((0, d), device=dev)
+
+    def chunks():
+        r0 = 0
+        for b in sel._plan.iter_execute():
+            X = b.columns[features_col].values
+            yield r0, (X if X.dtype == torch.float32 else X.float())
+            r0 += b.n
+    return ChunkedRows(chunks, n, d, dev), out, sel.schema[features_col].metadata
+
+
 def vector_attrs(meta: dict, width: int, name: str) -> List[dict]:
     """Per-slot attributes of a vector column (names, nominal arity)."""
     ma = (meta or {}).get("ml_attr")

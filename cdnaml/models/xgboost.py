@@ -37,6 +37,7 @@ from .param import TypeConverters as TC, keyword_init
 from .regression import _default_seed
 from .tree.engine import Forest, ForestTrainer, TreeParams, make_binned
 from .util import IllegalArgumentException, categorical_info, global_count, global_offset, local_batch, \
+    streamed_columns, \
     require_vector
 
 _XGB = {
@@ -136,12 +137,17 @@ class _XgbEstimatorBase(Estimator):
         for c in (self.getWeightCol(), self.getBaseMarginCol(), self.getValidationIndicatorCol()):
             if c:
                 cols.append(c)
-        b = local_batch(dataset, cols)
-        X = b.columns[fc].values.float().contiguous()
-        y = b.columns[lc].values.double()
-        w = b.columns[self.getWeightCol()].values.double() if self.getWeightCol() else None
-        bm = b.columns[self.getBaseMarginCol()].values.double() if self.getBaseMarginCol() else None
-        val = b.columns[self.getValidationIndicatorCol()].values.bool() if self.getValidationIndicatorCol() \
+        src = streamed_columns(dataset, fc, cols[1:])
+        if src is not None:  # out-of-core: features streamed into the bins, never resident
+            X, b_cols, _ = src
+        else:
+            b = local_batch(dataset, cols)
+            X = b.columns[fc].values.float().contiguous()
+            b_cols = b.columns
+        y = b_cols[lc].values.double()
+        w = b_cols[self.getWeightCol()].values.double() if self.getWeightCol() else None
+        bm = b_cols[self.getBaseMarginCol()].values.double() if self.getBaseMarginCol() else None
+        val = b_cols[self.getValidationIndicatorCol()].values.bool() if self.getValidationIndicatorCol() \
             else None
         n = X.shape[0]
         mb = self.getMax_bin()

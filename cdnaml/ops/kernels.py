@@ -267,7 +267,7 @@ def quantile_thresholds_dev(samp: torch.Tensor, max_bins: int):
 
 # --------------------------------------------------------------------- K4
 def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Optional[float] = None,
-           want_rm: bool = False, rm_layout: str = "std"):
+           want_rm: bool = False, rm_layout: str = "std", out_full=None, row0: int = 0):
     """Raw features -> uint8 bins in feature-group-major layout [G, n, 8].
 
     want_rm: return ``(bins, rm)`` where ``rm`` is the row-major copy of ``bins_row_major`` written by the
@@ -279,6 +279,9 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Opti
     Categorical feature (nthr[f] < 0): bin = clamp(int(x), 0, 255).
     missing (XGBoost): values that are NaN or equal ``missing`` are binned as -inf (bin 0 when the
     thresholds start at -FLT_MAX), without materialising a masked copy of X.
+
+    out_full (streamed fits, chunk by chunk): ``(bins [G, N, 8], rm [N, Gs, 8] or None)`` of the whole table;
+    this chunk's rows are written to rows [row0, row0 + n) of both, and ``(bins, rm)`` views of them returned.
     """
     n, d = X.shape
     G = (d + 7) // 8
@@ -288,24 +291,37 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Opti
         X = X if X.stride(1) == 1 else X.contiguous()
         thr = thr.float().contiguous()
         nthr = nthr.int().contiguous()
-        out = torch.empty((G, n, 8), dtype=torch.uint8, device=X.device)
         s10 = want_rm and rm_layout == "s10"
         if s10 and d > 100:
             raise ValueError("seg10 rows hold at most 100 features")
         Gs = 16 if (s10 or (BINS_RM_PAD and G <= 16)) else G
-        rm = torch.empty((n, Gs, 8), dtype=torch.uint8, device=X.device) if want_rm else None
+        if out_full is not None:
+            full, rm_full = out_full
+            assert full.shape[0] == G and full.is_contiguous() and row0 + n <= full.shape[1]
+            out = full[:, row0:row0 + n]
+            ldo, optr = full.shape[1], full.data_ptr() + row0 * 8
+            rm = None
+            if want_rm:
+                assert rm_full is not None and rm_full.shape[1] == Gs and rm_full.is_contiguous()
+                rm = rm_full[row0:row0 + n]
+        else:
+            out = torch.empty((G, n, 8), dtype=torch.uint8, device=X.device)
+            ldo, optr = 0, _ptr(out)
+            rm = torch.empty((n, Gs, 8), dtype=torch.uint8, device=X.device) if want_rm else None
         miss_on = missing is not None
         miss_val = float("nan") if (missing is None or math.isnan(missing)) else float(missing)
         if n:
             rc = _lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, int(miss_on),
-                                        miss_val, _ptr(out), _ptr(rm) if rm is not None else None,
-                                        -10 if s10 else Gs, _stream(X.device))
+                                        miss_val, optr, _ptr(rm) if rm is not None else None,
+                                        -10 if s10 else Gs, ldo, _stream(X.device))
             if rc == 2:  # the fallback kernel ran: no row-major copy
                 rm = None
             else:
                 _lib.check(rc, "cdna_binize")
         return (out, rm) if want_rm else out
-    out = torch.zeros((G, n, 8), dtype=torch.uint8)
+    out = torch.zeros((G, n, 8), dtype=torch.uint8) if out_full is None else out_full[0][:, row0:row0 + n]
+    if out_full is not None:
+        out.zero_()
     Xf = X.float()
     if missing is not None:
         miss = torch.isnan(Xf) if math.isnan(missing) else (torch.isnan(Xf) | (Xf == float(missing)))

@@ -30,7 +30,7 @@ namespace {
 __global__ __launch_bounds__(256) void binize_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                      const float* __restrict__ thr, const int* __restrict__ nthr,
                                                      int tmax, int use_lds, int miss_on, float miss_val,
-                                                     uint64_t* __restrict__ out) {
+                                                     uint64_t* __restrict__ out, int64_t ldo) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int G = (d + 7) / 8;
   const int dp = G * 8;
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void binize_kernel(const float* __restrict__ X
     __syncthreads();
     for (int e = threadIdx.x; e < rows * G; e += 256) {
       const int g = e / rows, r = e - g * rows;
-      out[(int64_t)g * n + r0 + r] = *reinterpret_cast<const uint64_t*>(&tile[r * dp + g * 8]);
+      out[(int64_t)g * ldo + r0 + r] = *reinterpret_cast<const uint64_t*>(&tile[r * dp + g * 8]);
     }
     __syncthreads();
   }
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
                                                       const float* __restrict__ thr, const int* __restrict__ nthr,
                                                       int tmax, int rows_per_tile, int steps, int miss_on,
                                                       float miss_val, uint64_t* __restrict__ out,
-                                                      uint64_t* __restrict__ rm, int Gs) {
+                                                      uint64_t* __restrict__ rm, int Gs, int64_t ldo) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int G = (d + 7) / 8;
   // [rows_per_tile][dp]: an odd row stride keeps the per-task x reads (lanes = rows) conflict-free; with
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void binize2_kernel(const float* __restrict__ 
         if (g * 8 + j >= d) b = 0;
         word |= (uint64_t)b << (8 * j);
       }
-      out[(int64_t)g * n + r0 + r] = word;
+      out[(int64_t)g * ldo + r0 + r] = word;
       if (rm) {
         // row-major copy [n][Gs] written from the same registers (saves the separate transpose kernel's
         // re-read of the [G][n] bins); the row's padding words are zeroed by its last group's task
@@ -248,7 +248,8 @@ template <int STEPS, int RPL>
 __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                        const float* __restrict__ thr, const int* __restrict__ nthr,
                                                        int tmax, int miss_on, float miss_val,
-                                                       uint64_t* __restrict__ out, uint64_t* __restrict__ rm, int Gs) {
+                                                       uint64_t* __restrict__ out, uint64_t* __restrict__ rm, int Gs,
+                                                       int64_t ldo) {
   extern __shared__ __attribute__((aligned(16))) float smf5[];
   constexpr int P = 1 << STEPS, RT = 64 * RPL, TP = 17;  // RPL rows per lane
   float* sthr = smf5;                                                          // [d][P]
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
       float x[8] = {p0[k].x, p0[k].y, p0[k].z, p0[k].w, p1[k].x, p1[k].y, p1[k].z, p1[k].w};
       const uint64_t word = search(x);
       const int64_t r = tl * RT + k * 64 + lane;
-      if (r < n) out[(int64_t)g * n + r] = word;
+      if (r < n) out[(int64_t)g * ldo + r] = word;
       if (rm) tile[(k * 64 + lane) * TP + g] = word;
     }
     if (rm) {
@@ -858,8 +859,13 @@ inline unsigned grid_for(int64_t n, int per, unsigned cap) {
 // miss_on: values that are NaN or equal miss_val are binned as -inf (XGBoost missing-value bin 0).
 // rm (optional): also write the row-major copy [n][Gs] (Gs >= G words per row).  Returns 2 when the v1 kernel
 // ran instead (rm not written).
+// ldo: row stride of out's [G][ldo] word planes (0: n) -- chunks of a streamed fit bin into their row slice of
+// the full bins (out = base + row0, ldo = total rows; rm = row-major base + row0).
 CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const float* thr, const int* nthr, int tmax,
-                         int miss_on, float miss_val, uint64_t* out, uint64_t* rm, int Gs, hipStream_t st) {
+                         int miss_on, float miss_val, uint64_t* out, uint64_t* rm, int Gs, int64_t ldo,
+                         hipStream_t st) {
+  if (ldo <= 0) ldo = n;
+  if (ldo < n) return (int)hipErrorInvalidValue;
   // Gs == -10: rm gets the seg10 row layout (d <= 100, 128-byte rows; binize v5 only, see store_rm)
   const bool s10 = rm && Gs == -10;
   if (s10 && d > 100) return (int)hipErrorInvalidValue;
@@ -884,7 +890,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
           (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds);
         hipLaunchKernelGGL(kern, dim3(grid_for(n, 64 * rpl, 1024)), dim3(64 * G), lds, st, X, n, d, ldx, thr, nthr,
-                           tmax > 0 ? tmax : 1, miss_on, miss_val, out, rm, Gs);
+                           tmax > 0 ? tmax : 1, miss_on, miss_val, out, rm, Gs, ldo);
       };
       switch (steps) {
         case 4: launch(binize5_kernel<4, rpl>); break;
@@ -922,7 +928,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(binize2_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(binize2_kernel, dim3(grid_for(n, rpt, 8192)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
-                         tmax > 0 ? tmax : 1, rpt, steps, miss_on, miss_val, out, rm, Gs);
+                         tmax > 0 ? tmax : 1, rpt, steps, miss_on, miss_val, out, rm, Gs, ldo);
       const int e = (int)hipGetLastError();
       return e != 0 ? e : (s10 ? 2 : 0);
     }
@@ -934,7 +940,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
   const size_t lds = tile + (use_lds ? tbytes : 0);
   if (tile > 120 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(binize_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), lds, st, X, n, d, ldx, thr, nthr,
-                     tmax, use_lds, miss_on, miss_val, out);
+                     tmax, use_lds, miss_on, miss_val, out, ldo);
   const int e = (int)hipGetLastError();
   return e != 0 ? e : (rm_wanted ? 2 : 0);
 }
