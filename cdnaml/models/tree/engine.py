@@ -423,6 +423,7 @@ class Forest:
         self.depth: List[int] = []
         self.roots: List[int] = []
         self._dev = {}
+        self._heap_np = None  # (heap [T, 2^(D+1)-1, 2] int32, D) built by ForestTrainer.train, or None
 
     def add(self, value, weight, depth, impurity=float("nan")) -> int:
         i = len(self.feat)
@@ -461,18 +462,27 @@ class Forest:
         return np.arange(i0, i0 + N, dtype=np.int64)
 
     def set_splits(self, fids, feats, gains, bins, thrs, has_thr, lefts, rights) -> None:
-        """Turn leaves ``fids`` into split nodes (numeric ones, ``has_thr``, also get bin + threshold)."""
-        for fid, f, g, b, t, h, l_, r_ in zip(np.asarray(fids).tolist(), np.asarray(feats).tolist(),
-                                              np.asarray(gains).tolist(), np.asarray(bins).tolist(),
-                                              np.asarray(thrs).tolist(), np.asarray(has_thr).tolist(),
-                                              np.asarray(lefts).tolist(), np.asarray(rights).tolist()):
-            self.feat[fid] = f
-            self.gain[fid] = g
-            self.left[fid] = l_
-            self.right[fid] = r_
-            if h:
-                self.bin[fid] = b
-                self.thr[fid] = t
+        """Turn leaves ``fids`` into split nodes (numeric ones, ``has_thr``, also get bin + threshold).
+
+        A level's split nodes lie in one contiguous id range (its active nodes were appended together), so each
+        field is updated as one numpy slice of that range instead of a Python loop per node (the last level's
+        loop ran while the GPU idled before the transform)."""
+        fids = np.asarray(fids, dtype=np.int64)
+        if fids.size == 0:
+            return
+        lo, hi = int(fids.min()), int(fids.max()) + 1
+        rel = fids - lo
+        h = np.asarray(has_thr, dtype=bool)
+        for name, vals, sel in (("feat", feats, None), ("gain", gains, None), ("left", lefts, None),
+                                ("right", rights, None), ("bin", bins, h), ("thr", thrs, h)):
+            lst = getattr(self, name)
+            seg = np.array(lst[lo:hi], dtype=np.float64 if name in ("gain", "thr") else np.int64)
+            v = np.asarray(vals)
+            if sel is None:
+                seg[rel] = v
+            else:
+                seg[rel[sel]] = v[sel]
+            lst[lo:hi] = seg.tolist()
 
     @property
     def num_nodes(self):
@@ -622,6 +632,13 @@ class Forest:
         key = ("heap", str(device), values_kind)
         if key in self._dev:
             return self._dev[key]
+        pre = getattr(self, "_heap_np", None)
+        if values_kind == "value" and pre is not None and pre[0].shape[0] == len(self.roots):
+            # filled level by level by the trainer (the same table as below; tests/test_engine_heap.py)
+            h_t, m_t = K.upload(device, pre[0], np.zeros(8, np.int32))
+            res = (h_t, pre[1], m_t)
+            self._dev[key] = res
+            return res
         res = None
         feat = np.asarray(self.feat, dtype=np.int64)  # one list conversion shared with _layout (~1.3k nodes)
         tree_of, slot, dep = self._layout(feat)
@@ -1207,7 +1224,17 @@ class ForestTrainer:
         dev = self.device
         n, d, B = data.n_local, data.d, data.B
         T = num_trees
+        fresh = forest is None
         forest = forest or Forest(self.C if self.classification else 1)
+        forest._heap_np = None
+        # single-output forests of depth <= 8 with numeric splits: the predict heap table (Forest.heap_arrays) is
+        # filled level by level here, from the keys and values the levels already hold, instead of re-walking the
+        # finished forest in Python between the last split and the transform (the GPU idles through that)
+        heap = None
+        if fresh and not self.classification and p.max_depth <= 8 and not data.categorical and not data.missing_bin:
+            heap = np.zeros((T, 2 ** (p.max_depth + 1) - 1, 2), dtype=np.int32)
+            heap[:, :, 0] = -1
+        heap_depth = 0
         need_masks = p.feature_subset is not None and p.feature_subset < d
         # "masked": accumulate only each node's sampled features (fewer atomics, no subtraction);
         # "full": accumulate all features, derive larger siblings by subtraction, mask at split time.
@@ -1524,6 +1551,8 @@ class ForestTrainer:
             if depth == 0:
                 a_fid = forest.add_many(self._leaf_values_v(a_stats), self._weights_v(a_stats), depth,
                                         self._impurities_v(a_stats))
+                if heap is not None:
+                    heap[a_tree, 0, 1] = self._leaf_values_v(a_stats)[:, 0].astype(np.float32).view(np.int32)
                 for t_, fid_ in zip(a_tree.tolist(), a_fid.tolist()):
                     root_ids[t_] = fid_
             W_a = self._weights_v(a_stats)
@@ -1631,7 +1660,18 @@ class ForestTrainer:
                     else:
                         K.partition(data.bins, node, *K.upload(dev, split_feat, split_bin, cat_off,
                                                                cm.reshape(-1), child))
-            got = forest.add_many(self._leaf_values_v(ch_st), cw, depth + 1, self._impurities_v(ch_st))
+            ch_vals = self._leaf_values_v(ch_st)
+            got = forest.add_many(ch_vals, cw, depth + 1, self._impurities_v(ch_st))
+            if heap is not None and len(sp):
+                if not plain.all():
+                    heap = None  # bin-set splits: Forest.heap_arrays builds the table from the forest
+                else:
+                    tsp, ksp = a_tree[sp], a_key[sp].astype(np.int64)
+                    heap[tsp, ksp - 1, 0] = f_sp
+                    heap[tsp, ksp - 1, 1] = thr_sp.astype(np.float32).view(np.int32)
+                    ck = np.stack([2 * ksp, 2 * ksp + 1], 1).reshape(-1)
+                    heap[np.repeat(tsp, 2), ck - 1, 1] = ch_vals[:, 0].astype(np.float32).view(np.int32)
+                    heap_depth = depth + 1
             assert len(got) == len(ch_ids) and (not len(got) or got[0] == ch_ids[0])
             forest.set_splits(fid_sp, f_sp, gain_h[sp], b_sp, thr_sp, num, ch_ids[0::2], ch_ids[1::2])
             prev_hist = H if subtract else None
@@ -1641,4 +1681,6 @@ class ForestTrainer:
             raise RuntimeError("partition record emission overflowed its capacity plan")
         forest.roots.extend(root_ids)
         forest._dev = {}
+        if heap is not None:
+            forest._heap_np = (np.ascontiguousarray(heap[:, :2 ** (heap_depth + 1) - 1]), heap_depth)
         return forest

@@ -1,0 +1,42 @@
+"""The predict heap table filled by ForestTrainer.train level by level equals Forest.heap_arrays' table built from
+the finished forest (tree of every node, heap slot from the root path, leaf values and thresholds as fp32 bits);
+and the vectorised Forest.set_splits equals the per-node assignment."""
+import numpy as np
+import torch
+
+from cdnaml.models.tree.engine import Forest
+
+
+def test_trainer_heap_equals_forest_walk():
+    import cdnaml
+    from cdnaml.models.regression import RandomForestRegressor
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator().manual_seed(0)
+    for n, d, T, depth in ((3000, 6, 5, 4), (2000, 12, 7, 6), (500, 4, 3, 8)):
+        X = torch.randn(n, d, generator=g)
+        y = (X[:, 0] * 2 - X[:, 1] + torch.sin(X[:, 2])).double()
+        df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
+        f = RandomForestRegressor(numTrees=T, maxDepth=depth, maxBins=16, seed=1, minInstancesPerNode=3).fit(df)._forest
+        assert f._heap_np is not None
+        pre = f._heap_np
+        f._heap_np = None
+        ref = f.heap_arrays(torch.device("cpu"))
+        assert ref[1] == pre[1]
+        np.testing.assert_array_equal(ref[0].numpy(), pre[0])
+
+
+def test_set_splits_vectorised():
+    rng = np.random.default_rng(0)
+    f = Forest(1)
+    f.add_many(np.zeros((50, 1)), np.ones(50), 0, np.zeros(50))
+    fids = np.sort(rng.choice(np.arange(10, 40), 12, replace=False))
+    feats, gains = rng.integers(0, 9, 12), rng.random(12)
+    bins, thrs, has = rng.integers(0, 30, 12), rng.random(12), rng.random(12) < 0.7
+    lefts, rights = rng.integers(50, 99, 12), rng.integers(50, 99, 12)
+    f.set_splits(fids, feats, gains, bins, thrs, has, lefts, rights)
+    for j, a in enumerate(fids):
+        assert f.feat[a] == feats[j] and f.gain[a] == gains[j] and f.left[a] == lefts[j] and f.right[a] == rights[j]
+        assert f.bin[a] == (bins[j] if has[j] else 0) and f.thr[a] == (thrs[j] if has[j] else 0.0)
+        assert type(f.feat[a]) is int and type(f.thr[a]) is float
+    other = np.setdiff1d(np.arange(50), fids)
+    assert all(f.feat[a] == -1 and f.left[a] == -1 for a in other)
