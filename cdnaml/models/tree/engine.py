@@ -1043,6 +1043,29 @@ class ForestTrainer:
         if not ok:
             raise RuntimeError("device split decode differs from the host decode")
 
+    # ------------------------------------------------------------ device-queued partition
+    def _device_partition(self, so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n, v1, qs1, w_total,
+                          rec_buf):
+        """Partition tables decoded on the device from the level's K6 decisions and the row partition queued right
+        behind them (the GPU partitions while the decisions travel to the host; the host repeats the decode to
+        build the forest and the next level, checked against the device's in the checked build).  With
+        ``emit_ok`` the partition also writes the next level's item records.  -> (decode tables, RecordEmit|None)."""
+        p, data, dev = self.p, self.data, self.device
+        A = so.shape[0]
+        a_tree_d, tf_d = K.upload(dev, a_tree.astype(np.int32), tfirst.numpy().astype(np.int32))
+        dec = K.split_decode(so, tot, a_tree_d, T, p.min_instances, p.min_info_gain,
+                             depth < p.max_depth, depth + 1 >= p.max_depth, missing_bin=mb)
+        em = None
+        if emit_ok and A <= K.P7_MAX_SLOTS and data.bins.shape[0] <= 16 and T <= 64:
+            em = self._record_emit(dev, n, A, v1, qs1, w_total, rec_buf)
+            if em is not None:
+                em.plan(so, dec["child"])
+        with _tr.span("tree.partition", depth=depth):
+            K.partition_codes(data.bins, codes, tf_d, dec["tfirst_next"], dec["split_feat"],
+                              dec["split_bin"], dec["cat_off"], dec["masks"].reshape(-1), dec["child"],
+                              bins_rm=data.row_major_bins() if PARTITION_RM else None, emit=em)
+        return dec, em
+
     # ------------------------------------------------------------ record emission by the partition
     @staticmethod
     def _check_emitted(em, st, cap, codes, tfirst, slot_of, S, v1, qs1):
@@ -1481,23 +1504,15 @@ class ForestTrainer:
                     # the partition tables decoded on the device and the row partition queued right behind K6:
                     # the GPU partitions while the decisions travel to the host and the host builds the forest
                     # and the next level's layout (the same decode on the host, checked in the checked build)
-                    a_tree_d, tf_d = K.upload(dev, a_tree.astype(np.int32), tfirst.numpy().astype(np.int32))
-                    dec = K.split_decode(so, tot, a_tree_d, T, p.min_instances, p.min_info_gain,
-                                         depth < p.max_depth, depth + 1 >= p.max_depth, missing_bin=mb)
-                    em = None
-                    if (K.EMIT_RECORDS and use_mseg and rec_ok and subtract and not use_sub and w_total is not None
-                            and data.bins_s10 is not None and A <= K.P7_MAX_SLOTS and data.bins.shape[0] <= 16
-                            and T <= 64):
-                        em = self._record_emit(dev, n, A, stats_rows["v1"], mseg_scales[1], w_total, rec_buf)
-                        if em is not None:
-                            rec_buf = em.rec
-                            em.plan(so, dec["child"])
-                            emits.append(em)
-                            em_next = em
-                    with _tr.span("tree.partition", depth=depth):
-                        K.partition_codes(data.bins, codes, tf_d, dec["tfirst_next"], dec["split_feat"],
-                                          dec["split_bin"], dec["cat_off"], dec["masks"].reshape(-1), dec["child"],
-                                          bins_rm=data.row_major_bins() if PARTITION_RM else None, emit=em)
+                    emit_ok = (K.EMIT_RECORDS and use_mseg and rec_ok and subtract and not use_sub and
+                               w_total is not None and data.bins_s10 is not None)
+                    dec, em = self._device_partition(so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n,
+                                                     stats_rows["v1"], mseg_scales[1] if use_mseg else 1.0,
+                                                     w_total, rec_buf)
+                    if em is not None:
+                        rec_buf = em.rec
+                        emits.append(em)
+                        em_next = em
                 # so [A, 8] = gain, feature, bin, left (2), right (2), missing-goes-right: copied to the host as is
                 # (plus the node totals at level 0), no per-column device ops
                 sw = so.shape[1]
@@ -1516,7 +1531,35 @@ class ForestTrainer:
                 # classification / categorical K6 in one kernel (centroid-ordered categories, Gini / entropy)
                 so, tot, cm = K.split_scan_ex(H, self._nthr_dev(dev), masks_t, p.impurity, p.min_instances)
                 kk = tot.shape[1]
-                host = torch.cat([so, cm.double()] + ([tot] if depth == 0 else []), 1).cpu().numpy()
+                src = torch.cat([so, cm.double()] + ([tot] if depth == 0 else []), 1)
+                if cls2 and use_codes and DEVICE_DECODE and not self.data.categorical and depth + 1 < p.max_depth \
+                        and not (deep_switch and depth + 1 >= 8):
+                    # binary classification on the codes: the same device decode + partition (+ record emission)
+                    # as regression, queued behind K6 while the decisions travel to the host.  The decode reads
+                    # (gain, feature, bin, left weight, ., right weight, .); a pure child (one class) weighs 0 there,
+                    # so it is a leaf on the device exactly as on the host
+                    host_p = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+                    host_p.copy_(src, non_blocking=True)
+                    host_ev = torch.cuda.Event()
+                    host_ev.record(torch.cuda.current_stream(dev))
+                    l0, l1, r0, r1 = so[:, 4], so[:, 5], so[:, 6], so[:, 7]
+                    zero = torch.zeros_like(l0)
+                    so_d = torch.stack([so[:, 0], so[:, 1], so[:, 2],
+                                        torch.where((l0 > 0) & (l1 > 0), l0 + l1, zero), l1,
+                                        torch.where((r0 > 0) & (r1 > 0), r0 + r1, zero), r1], 1)
+                    emit_ok = (K.EMIT_RECORDS and use_mseg and rec_ok and subtract and w_total is not None and
+                               data.bins_s10 is not None)
+                    dec, em = self._device_partition(so_d, tot.sum(1, keepdim=True), a_tree, tfirst, T, depth,
+                                                     False, codes, emit_ok, n, stats_rows["v1"], 1.0, w_total,
+                                                     rec_buf)
+                    if em is not None:
+                        rec_buf = em.rec
+                        emits.append(em)
+                        em_next = em
+                    host_ev.synchronize()
+                    host = host_p.numpy()
+                else:
+                    host = src.cpu().numpy()
                 gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
                 lst_h, rst_h = host[:, 4:4 + kk], host[:, 4 + kk:4 + 2 * kk]
                 c0 = 4 + 2 * kk
