@@ -791,7 +791,7 @@ PARTITION7_MIN_T = int(__import__("os").environ.get("CDNAML_PARTITION7_MIN_T", "
 
 
 # ------------------------------------------------------------------ K7e: record emission by the partition
-EMIT_RECORDS = __import__("os").environ.get("CDNAML_P7_EMIT", "1") != "0"
+EMIT_RECORDS = __import__("os").environ.get("CDNAML_P7_EMIT", "0") != "0"
 EMIT_CS = 32  # ints between chunk cursors (one 128-byte line each)
 
 

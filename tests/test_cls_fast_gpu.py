@@ -32,20 +32,25 @@ def test_packed_classification_forest_equals_class_histograms(spark, n, d, T, de
     df = spark.createDataFrameFromLocalTensors({"features": X, "label": y.double()})
     est = RandomForestClassifier(numTrees=T, maxDepth=depth, maxBins=40, seed=7, impurity=imp)
     out, calls = [], []
-    orig = K.seg_hist_codes
+    orig_c, orig_s = K.seg_hist_codes, K.seg_hist
     for flag in (False, True):
         cnt = {"n": 0}
 
-        def counted(*a, **k):
+        def counted_c(*a, **k):
             cnt["n"] += 1
-            return orig(*a, **k)
+            return orig_c(*a, **k)
+
+        def counted_s(*a, **k):
+            cnt["n"] += 1
+            return orig_s(*a, **k)
         engine.MSEG_CLS = flag
-        K.seg_hist_codes = counted
+        K.seg_hist_codes, K.seg_hist = counted_c, counted_s
         try:
             out.append(forest_digest(est.fit(df)._forest))
         finally:
             engine.MSEG_CLS = True
-            K.seg_hist_codes = orig
+            K.seg_hist_codes, K.seg_hist = orig_c, orig_s
         calls.append(cnt["n"])
-    assert calls[0] == 0 and calls[1] >= 1, calls  # the packed path ran (root levels from the codes)
+    # the packed path ran (root levels from the codes at d = 100, record histograms below / at other widths)
+    assert calls[0] == 0 and calls[1] >= 1, calls
     assert out[0] == out[1]

@@ -77,5 +77,8 @@ def test_streamed_linear_regression(spark, streamed_calls):
     ref = LinearRegression().fit(mat)
     got = LinearRegression().fit(_chunked(spark, X, y, 1500))
     assert streamed_calls["streamed"] == 1
-    np.testing.assert_allclose(got.coefficients.toArray(), ref.coefficients.toArray(), rtol=1e-9, atol=1e-9)
-    assert got.intercept == pytest.approx(ref.intercept, rel=1e-9, abs=1e-9)
+    # cpu: fp64 Gram blocks (summation order only); cuda: K1 accumulates each block's rows in fp32 MFMA partial
+    # slabs, so chunk boundaries move fp32 roundings (~1e-7 relative in the coefficients)
+    tol = 1e-9 if spark.device.type == "cpu" else 2e-5
+    np.testing.assert_allclose(got.coefficients.toArray(), ref.coefficients.toArray(), rtol=tol, atol=tol)
+    assert got.intercept == pytest.approx(ref.intercept, rel=tol, abs=tol)
