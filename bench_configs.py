@@ -105,24 +105,30 @@ def bench_lr(spark, args):
 
 
 def bench_clf(spark, args):
-    """Labs/ML 07L:105-141 at scale: RandomForestClassifier (Gini) over a 2x2 grid of maxDepth x numTrees with
-    3-fold CrossValidator and a BinaryClassificationEvaluator, 1e7 x 100 binary labels.  The classification level
-    loop runs the class-count histograms and the native K6 (split_scan_ex: Gini on class counts)."""
+    """S/Labs/ML 07L - Hyperparameter Tuning Lab.py:82,105-108,140-155 at scale: RandomForestClassifier (Gini,
+    maxBins 40) over the lab's exact 3x3 grid maxDepth {2, 5, 10} x numTrees {10, 20, 100} with a 3-fold
+    CrossValidator and BinaryClassificationEvaluator (areaUnderROC), 1e7 x 100 binary labels (--grid small: the
+    round-3 2x2 grid {2, 5} x {5, 10}).  The fused tuner grows one forest per fold at the group's largest numTrees /
+    maxDepth (100 trees, depth 10): binary labels ride the packed record path (class counts from (W, W1) sums,
+    levels 0-7 on the row codes, node ids from level 8)."""
     from cdnaml.ml.classification import RandomForestClassifier
     from cdnaml.ml.evaluation import BinaryClassificationEvaluator
     from cdnaml.ml.tuning import CrossValidator, ParamGridBuilder
     n_total = int(args.rows or 1e7)
     df, n = _data(spark, n_total, 100, cls=True)
     rf = RandomForestClassifier(maxBins=40, seed=42)
-    grid = ParamGridBuilder().addGrid(rf.maxDepth, [2, 5]).addGrid(rf.numTrees, [5, 10]).build()
+    depths, trees = ([2, 5], [5, 10]) if args.grid == "small" else ([2, 5, 10], [10, 20, 100])
+    grid = ParamGridBuilder().addGrid(rf.maxDepth, depths).addGrid(rf.numTrees, trees).build()
     cv = CrossValidator(estimator=rf, estimatorParamMaps=grid, evaluator=BinaryClassificationEvaluator(),
                         numFolds=3, seed=42)
     ms, model = _timed(spark, lambda: cv.fit(df), args.steps, args.warmup)
-    _log(f"RF classifier CV {ms:.1f} ms for {len(grid) * 3 + 1} fits, best maxDepth={model.bestModel.getMaxDepth()}, "
-         f"AUC {max(model.avgMetrics):.4f}")
-    _emit(spark, "rows/sec CrossValidator(RandomForestClassifier grid 2x2, 3 folds) fit", n_total / (ms / 1e3),
-          "rows/s", args.steps, args.warmup, ms, True, "strong", "fp32", "RandomForestClassifier(maxBins=40) CV 2x2x3",
-          n_total, f"dp{spark.comm.world_size}")
+    _log(f"RF classifier CV {ms:.1f} ms for {len(grid) * 3 + 1} fits, best maxDepth={model.bestModel.getMaxDepth()} "
+         f"numTrees={model.bestModel.getNumTrees}, AUC {max(model.avgMetrics):.4f}")
+    gname = f"{len(depths)}x{len(trees)}"
+    _emit(spark, f"rows/sec CrossValidator(RandomForestClassifier grid {gname}, 3 folds) fit", n_total / (ms / 1e3),
+          "rows/s", args.steps, args.warmup, ms, True, "strong", "fp32",
+          f"RandomForestClassifier(maxBins=40) CV maxDepth {depths} x numTrees {trees} x 3 folds", n_total,
+          f"dp{spark.comm.world_size}")
 
 
 def bench_cv(spark, args):
@@ -366,6 +372,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("config", choices=["lr", "cv", "clf", "gbdt", "infer", "airbnb", "relational", "expr", "ooc"])
     ap.add_argument("--model", choices=["lr", "rf"], default="lr", help="ooc: the streamed estimator")
+    ap.add_argument("--grid", choices=["lab", "small"], default="lab", help="clf: the L07 3x3 grid or the 2x2 one")
     ap.add_argument("--rows", type=float, default=None)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)

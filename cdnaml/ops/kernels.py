@@ -1206,6 +1206,10 @@ def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_glob
 
 
 SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "2048"))
+# wide-bin (80 < B <= 256, boosting) record levels: work items per level (x ceil(d / 64) feature blocks).  Every block
+# clears and flushes 64 features x B bins of LDS cells into the level histogram with global atomics, so at deep
+# boosting levels (fewer rows, the same number of blocks) the flush -- not the rows -- sets the level time
+SEG_MIN_BLOCKS_WIDE = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS_WIDE", "1024"))
 # three-times-larger record chunks for the six-items-per-wave kernel (its count field is spread over three cell
 # copies): measured 145.1 vs 139.8 ms per headline step (fewer, longer blocks) and neutral at 1.25e7 rows -- off
 LANE10_CHUNK3 = __import__("os").environ.get("CDNAML_LANE10_CHUNK3", "0") != "0"
@@ -1226,7 +1230,7 @@ def _fill_chunk(segs: np.ndarray, chunk: int, B: int = 0) -> int:
     1024 the per-rank shape of the 8-GPU point ran 22.6 -> 21.2 ms (the last round of blocks no longer idles
     half the chip); wide-bin levels (B > 64: 128 KB LDS planes to clear and flush per block) keep 1024."""
     total = int(np.asarray(segs, dtype=np.int64).reshape(-1, 3)[:, 1].clip(min=0).sum())
-    mb = SEG_MIN_BLOCKS if B <= 64 else min(SEG_MIN_BLOCKS, 1024)
+    mb = SEG_MIN_BLOCKS if B <= 64 else min(SEG_MIN_BLOCKS, SEG_MIN_BLOCKS_WIDE)
     return int(min(chunk, max(8192, -(-total // max(1, mb)))))
 
 
