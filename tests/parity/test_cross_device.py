@@ -75,7 +75,12 @@ def flow_cleansing(spark, ds, work):
         pos = pos.withColumn(c + "_na", when(col(c).isNull(), 1.0).otherwise(0.0))
     imp = Imputer(strategy="median", inputCols=nums, outputCols=nums).fit(pos)
     out = imp.transform(pos)
-    return {"summary": {k: [str(v) for v in summ.loc[k].tolist()] for k in summ.index},
+    def num(v):  # summary() cells are strings; compare their values (fp64 reduction order differs by device)
+        try:
+            return float(v)
+        except (TypeError, ValueError):
+            return str(v)
+    return {"summary": {k: [num(v) for v in summ.loc[k].tolist()] for k in summ.index},
             "room_counts": list(zip(counts.room_type, counts["count"].astype(int))),
             "hood_counts": list(zip(hood.neighbourhood_cleansed, hood["count"].astype(int))),
             "medians": {c: float(v) for c, v in zip(nums, imp.surrogateDF.toPandas().iloc[0].tolist())},
