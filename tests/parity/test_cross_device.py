@@ -239,12 +239,12 @@ FLOWS = {"dedup": flow_dedup, "cleansing": flow_cleansing, "exploration": flow_e
          "logistic": flow_logistic}
 
 # native kernels each data flow must reach on the GPU (any one of each tuple)
-NATIVE = {"dedup": [("cdna_hp_part", "cdna_hp_agg", "cdna_hash_insert", "cdna_bucket_compact")],
-          "cleansing": [("cdna_hp_part", "cdna_hp_agg", "cdna_hash_insert"), ("cdna_expr_eval",),
-                        ("cdna_col_moments",)],
-          "exploration": [("cdna_hp_part", "cdna_hp_agg", "cdna_hash_insert"), ("cdna_reg_metrics",)],
-          "sql": [("cdna_join_build", "cdna_join_build_dense"), ("cdna_join_probe", "cdna_join_probe_dense"),
-                  ("cdna_hp_part", "cdna_hp_agg", "cdna_hash_insert")],
+HASH = ("cdna_hp_part", "cdna_hp_agg", "cdna_hp_hist", "cdna_la_groups", "cdna_hash_insert", "cdna_pack_keys",
+        "cdna_bucket_compact", "cdna_grouped_reduce")
+NATIVE = {"dedup": [HASH],
+          "cleansing": [HASH, ("cdna_expr_eval",), ("cdna_col_moments",), ("cdna_gather", "cdna_compact_mask")],
+          "exploration": [HASH, ("cdna_reg_metrics",)],
+          "sql": [("cdna_join_build", "cdna_join_build_dense"), ("cdna_join_probe", "cdna_join_probe_dense"), HASH],
           "lr": [("cdna_gram",)], "dt": [("cdna_binize",), ("cdna_split_scan", "cdna_split_scan_ex")],
           "rf_cv": [("cdna_binize",), ("cdna_tree_predict_heap", "cdna_tree_predict")],
           "rf_cls": [("cdna_binize",), ("cdna_split_scan_ex",), ("cdna_score_hist", "cdna_tree_predict")],
@@ -297,6 +297,11 @@ def results(tmp_path_factory):
         gpu, calls = _run_all("cuda", root)
     finally:
         K.HASH_MIN_ROWS, K.GATHER_MIN, fused.FUSE_MIN_ROWS = saved
+    out = os.environ.get("CDNAML_PARITY_CALLS")
+    if out:  # e.g. gpurun_out/parity_calls.json: which native kernels each flow reached on the GPU
+        import json
+        with open(out, "w") as f:
+            json.dump({k: dict(v) for k, v in calls.items()}, f, indent=1, sort_keys=True)
     return cpu, gpu, calls
 
 
@@ -316,8 +321,15 @@ def _close(a, b, rel, path=""):
 
 
 EXACT = ("dedup", "sql")
-TREES = ("dt", "rf_cv", "rf_cls")        # int64 histograms on both devices: identical models
-TOL = {"cleansing": 1e-9, "exploration": 1e-9, "lr": 1e-4, "kmeans": 1e-6, "logistic": 1e-4}
+# int64 histograms on both devices: identical models (digests compared exactly); their metrics come from fp32
+# predictions / probabilities summed over trees in a device-specific order (~1e-8 .. 1e-6 relative)
+TREES = ("dt", "rf_cv", "rf_cls")
+TREE_METRIC_TOL = 1e-5
+# fp64 reductions in a different order: 1e-9.  LR: the GPU Gram accumulates each block's rows in fp32 MFMA
+# partial slabs (the CPU in fp64), and the OHE design's condition number (~1e4) carries that into the
+# coefficients (~4e-4 relative measured).  Logistic regression: L-BFGS / OWL-QN stops at the same loss tolerance
+# from fp32 device gradients vs fp64 host ones; weakly identified coefficients then differ by ~1e-4 absolute
+TOL = {"cleansing": 1e-9, "exploration": 1e-9, "lr": 2e-3, "kmeans": 1e-6, "logistic": 2e-3}
 
 
 @pytest.mark.parametrize("flow", list(FLOWS))
@@ -328,7 +340,7 @@ def test_flow_matches_across_devices(results, flow):
         assert a == b
     elif flow in TREES:
         assert a["digest"] == b["digest"]
-        _close(a, b, 1e-9)
+        _close(a, b, TREE_METRIC_TOL)
     else:
         _close(a, b, TOL[flow])
     for group in NATIVE.get(flow, []):
