@@ -133,6 +133,19 @@ class LinearRegressionTrainingSummary(_RegressionSummary):
         return [float(2 * stats.t.sf(abs(t), dof)) for t in self.tValues]
 
 
+GRAM_FP64_MAX_WORK = float(__import__("os").environ.get("CDNAML_GRAM_FP64_MAX_WORK", "4e9"))
+
+
+def _gram_fp64(prec: str, n: int, d: int) -> bool:
+    """gramPrecision "auto": problems of at most GRAM_FP64_MAX_WORK multiply-adds (n (d + 2)^2; d = 100: ~4e5
+    rows) take an fp64 library GEMM of the augmented matrix -- Spark's normal-equation solver works in fp64 and
+    course-sized one-hot designs are ill-conditioned (condition ~1e4: the K1 kernel's fp32 block accumulation
+    moved coefficients by ~2e-3 relative); larger ones take K1 (fp32 MFMA, HBM-bound)."""
+    if prec == "fp64":
+        return True
+    return prec == "auto" and float(n) * (d + 2) ** 2 <= GRAM_FP64_MAX_WORK
+
+
 def _lr_shift(Xk: torch.Tensor, yk: torch.Tensor, comm, d: int) -> torch.Tensor:
     """[d + 1] fp64 common shift of the features and the label: the mean of every rank's leading rows (averaged
     over the ranks that have any).  It only conditions the f32 Gram; the solve un-shifts exactly with the host
@@ -172,7 +185,8 @@ class LinearRegression(Estimator):
         "aggregationDepth": ("suggested depth for treeAggregate (>= 2)", 2, TC.toInt),
         "loss": ("the loss function to be optimized: squaredError, huber", "squaredError", TC.toString),
         "epsilon": ("the shape parameter to control the amount of robustness (huber)", 1.35, TC.toFloat),
-        "gramPrecision": ("Gram kernel input precision: fp32 (exact f32 MFMA) or bf16", "fp32", TC.toString),
+        "gramPrecision": ("Gram precision: auto (fp64 library GEMM for small problems, else fp32), fp32 (K1 f32 MFMA "
+                          "with fp32 block accumulation), bf16 (K1 bf16 MFMA) or fp64", "auto", TC.toString),
     })
 
     def __init__(self, featuresCol=None, labelCol=None, predictionCol=None, maxIter=None, regParam=None,
@@ -196,6 +210,7 @@ class LinearRegression(Estimator):
         # common shift (global mean of per-rank leading samples) keeps the f32 Gram well conditioned; it stays on
         # the device (the label shift is applied to y there), so the fit reads the host once, for the Gram
         bf16 = self.getGramPrecision() == "bf16"
+        fp64 = _gram_fp64(self.getGramPrecision(), X.shape[0], d + (1 if w is not None else 0))
         sh = None
         if fit_int:
             sh = _lr_shift(X[:4096], y[:4096], comm, d)
@@ -203,14 +218,14 @@ class LinearRegression(Estimator):
         else:
             shift, yc = None, y
         if w is None:
-            G = K.gram(X, yc, shift, 0.0, bf16=bf16) if X.shape[0] else \
+            G = K.gram(X, yc, shift, 0.0, bf16=bf16, fp64=fp64) if X.shape[0] else \
                 torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
         else:
             # weighted Gram on K1 too: rows scaled by sqrt(w), with sqrt(w) itself as an extra feature column,
             # so [X' | sqrt(w) | 1 | y']^T [...] holds sum w x x^T, sum w x, sum w and the y blocks
             sw = torch.sqrt(w).float()[:, None]
             Xw = torch.cat([(X.float() - (shift if shift is not None else 0.0)) * sw, sw], 1)
-            G3 = K.gram(Xw, (yc.float() * sw[:, 0]), None, 0.0, bf16=bf16) if X.shape[0] else \
+            G3 = K.gram(Xw, (yc.float() * sw[:, 0]), None, 0.0, bf16=bf16, fp64=fp64) if X.shape[0] else \
                 torch.zeros((d + 3, d + 3), dtype=torch.float64, device=X.device)
             keep = torch.tensor(list(range(d + 1)) + [d + 2], device=X.device)
             G = G3[keep][:, keep].contiguous()
@@ -239,6 +254,7 @@ class LinearRegression(Estimator):
         w = cd[wc].values.double() if wc else None
         fit_int = self.getFitIntercept()
         bf16 = self.getGramPrecision() == "bf16"
+        fp64 = _gram_fp64(self.getGramPrecision(), Xs.n, d + (1 if w is not None else 0))
         dev = Xs.device
         head = cd["__head__"]
         sh = _lr_shift(head, y[:head.shape[0]], comm, d) if fit_int else \
@@ -253,11 +269,11 @@ class LinearRegression(Estimator):
             if m == 0:
                 continue
             if w is None:
-                G += K.gram(Xc, ycc, shift, 0.0, bf16=bf16)
+                G += K.gram(Xc, ycc, shift, 0.0, bf16=bf16, fp64=fp64)
             else:
                 sw = torch.sqrt(w[r0:r0 + m]).float()[:, None]
                 Xw = torch.cat([(Xc.float() - (shift if shift is not None else 0.0)) * sw, sw], 1)
-                G += K.gram(Xw, ycc.float() * sw[:, 0], None, 0.0, bf16=bf16)
+                G += K.gram(Xw, ycc.float() * sw[:, 0], None, 0.0, bf16=bf16, fp64=fp64)
         if w is not None:
             keep = torch.tensor(list(range(d + 1)) + [d + 2], device=dev)
             G = G[keep][:, keep].contiguous()

@@ -70,15 +70,17 @@ def upload(dev, *arrays):
 
 # --------------------------------------------------------------------- K1
 def gram(X: torch.Tensor, y: Optional[torch.Tensor] = None, shift: Optional[torch.Tensor] = None,
-         yshift: float = 0.0, bf16: bool = False) -> torch.Tensor:
+         yshift: float = 0.0, bf16: bool = False, fp64: bool = False) -> torch.Tensor:
     """Return A^T A (float64, (d+2)x(d+2)) for A = [X - shift | 1 | y - yshift].
 
     Column d is the intercept column of ones; column d+1 is y (zeros if None).
+    fp64: the fp32 augmented matrix multiplied in fp64 by the library GEMM (the CPU path's arithmetic) instead of
+    the K1 MFMA kernel.
     """
     n, d = X.shape
     if X.dtype != torch.float32:
         X = X.float()
-    if _native(X) and d + 2 <= 512:
+    if _native(X) and d + 2 <= 512 and not fp64:
         X = X if X.stride(1) == 1 else X.contiguous()
         y32 = None if y is None else y.float().contiguous()
         sh = None if shift is None else shift.float().contiguous()
