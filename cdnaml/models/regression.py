@@ -668,7 +668,7 @@ class _TreeRegressorModel(_TreeModelBase):
                                   self._numFeatures)
 
 
-def _early_side_work(num_trees, bootstrap, rate, want_label_max=True):
+def _early_side_work(num_trees, bootstrap, rate, want_label_max=True, codes_ok=False):
     """(pre, early): ``pre`` for tree_fit_prepare queues the Poisson bootstrap draws and the maxima the fit needs
     on the host (largest weight, max |label|) on the side stream before the quantile sample / threshold / binning
     kernels: they overlap the sort of the sample (100 of 256 CUs busy) instead of competing with the
@@ -686,8 +686,14 @@ def _early_side_work(num_trees, bootstrap, rate, want_label_max=True):
                 early["yf"] = y_.float()
             K.prefetch_max(early["yf"], absval=True, stream=side)
         if bootstrap and num_trees > 1:
-            early["w"] = _poisson_side(num_trees, n, seed_, off, rate, dev, join=False)
-            K.prefetch_max(early["w"], stream=side)
+            if codes_ok and K.POISSON_CODES:
+                # the draws written straight as the engine's row codes + their max (no uint8 weights, no
+                # codes_init pass, no separate max reduction over T x n bytes)
+                with torch.cuda.stream(side):
+                    early["codes"] = K.BootstrapCodes(num_trees, n, seed_, off, rate, dev)
+            else:
+                early["w"] = _poisson_side(num_trees, n, seed_, off, rate, dev, join=False)
+                K.prefetch_max(early["w"], stream=side)
     return pre, early
 
 
@@ -695,6 +701,8 @@ def _join_early(early, dev):
     for k in ("yf", "w"):
         if k in early:
             _join_side(early[k], dev)  # binning is queued: the trainer's first kernel waits for the side stream
+    if "codes" in early:
+        _join_side(early["codes"].codes, dev)
 
 
 def _train_forest_regression(est, dataset, num_trees, subset, bootstrap, rate, impurity="variance"):
@@ -798,7 +806,8 @@ class RandomForestRegressor(Estimator):
 
 
 def _train_rf_reg(est, dataset, T_):
-    pre, early = _early_side_work(T_, est.getBootstrap(), est.getSubsamplingRate())
+    pre, early = _early_side_work(T_, est.getBootstrap(), est.getSubsamplingRate(),
+                                  codes_ok=not (est.hasParam("weightCol") and est.getWeightCol()))
     session, data, y, w, seed, meta = tree_fit_prepare(est, dataset, classification=False, pre=pre)
     _join_early(early, data.bins.device)
     subset = resolve_subset(est.getFeatureSubsetStrategy(), data.d, T_, False)
@@ -806,11 +815,17 @@ def _train_rf_reg(est, dataset, T_):
                    min_instances=float(est.getMinInstancesPerNode()), min_info_gain=est.getMinInfoGain(),
                    impurity="variance", feature_subset=subset, bootstrap=est.getBootstrap(),
                    subsampling_rate=est.getSubsamplingRate(), seed=seed)
-    weights = early["w"] if "w" in early else \
-        _bag_weights(data, T_, est.getBootstrap(), est.getSubsamplingRate(), seed)
+    bc = early.get("codes")
+    if bc is not None:
+        weights = None
+    else:
+        weights = early["w"] if "w" in early else \
+            _bag_weights(data, T_, est.getBootstrap(), est.getSubsamplingRate(), seed)
     if w is not None:
-        weights = _combine_weights(weights, w, T_)
-    forest = ForestTrainer(session, data, p).train(T_, {"v0": None, "v1": early.get("yf", y.float())}, weights)
+        weights = _combine_weights(bc.weights() if bc is not None else weights, w, T_)
+        bc = None
+    forest = ForestTrainer(session, data, p).train(T_, {"v0": None, "v1": early.get("yf", y.float())}, weights,
+                                                   codes_pre=bc)
     return forest, data.d
 
 

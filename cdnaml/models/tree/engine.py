@@ -1240,8 +1240,11 @@ class ForestTrainer:
         return Hb
 
     def train(self, num_trees: int, stats_rows: Dict[str, torch.Tensor], weights: Optional[torch.Tensor],
-              forest: Optional[Forest] = None) -> Forest:
-        """Grow ``num_trees`` trees. stats_rows: {'v0','v1'} (moments) or {'label'} (classes)."""
+              forest: Optional[Forest] = None, codes_pre=None) -> Forest:
+        """Grow ``num_trees`` trees. stats_rows: {'v0','v1'} (moments) or {'label'} (classes).
+
+        codes_pre: a K.BootstrapCodes (the bootstrap draws already written as the row codes) instead of
+        ``weights``."""
         p = self.p
         data = self.data
         dev = self.device
@@ -1286,6 +1289,8 @@ class ForestTrainer:
         use_seg = USE_SEG and T == 1 and not self.classification and not masked and not use_mseg
         # row records (uint16 weight<<8 | local node) when every level fits 255 nodes per tree
         use_codes = USE_CODES and (p.max_depth <= 8 or (deep_switch and use_mseg)) and not use_seg
+        if codes_pre is not None and not use_codes:
+            weights = codes_pre.weights()  # a path that reads the multiplicities themselves
         if use_seg:
             w1 = None if weights is None else weights.reshape(-1)
             wmax = int(w1.max().item()) if (w1 is not None and w1.numel()) else 1
@@ -1301,6 +1306,8 @@ class ForestTrainer:
             seg_raw = seg_scales if v0p is not None else seg_scales[1]
             segs = np.array([[0, perm.numel()]], dtype=np.int64)
             node = None
+        elif use_codes and codes_pre is not None:
+            codes, wmax = codes_pre.codes, codes_pre.wmax()
         elif use_codes:
             codes, wmax = K.codes_init_max(weights, T, n, dev)
             node = None

@@ -134,10 +134,34 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
     seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     if device.type == "cuda":
         out = torch.empty((T, n), dtype=torch.uint8, device=device)
-        _lib.check(_lib.lib().cdna_poisson(_ptr(out), T, n, seed, int(offset), float(rate), _stream(device)),
-                   "cdna_poisson")
+        _lib.check(_lib.lib().cdna_poisson(_ptr(out), T, n, seed, int(offset), float(rate), None, None,
+                                           _stream(device)), "cdna_poisson")
         return out
     return torch.from_numpy(_philox.poisson(T, n, seed, int(offset), float(rate)))
+
+
+POISSON_CODES = __import__("os").environ.get("CDNAML_POISSON_CODES", "1") != "0"
+
+
+class BootstrapCodes:
+    """Poisson bootstrap draws written straight as the tree engine's row codes (GPU): ``codes`` [T, n] int16
+    (weight << 8 | 0, 0xFF for weight 0 -- codes_init's format) and the largest weight, copied to the host behind
+    the kernel (``wmax()`` waits for that copy only).  ``weights()`` derives the uint8 multiplicities for the
+    paths that need them (bit-identical to poisson_weights)."""
+
+    def __init__(self, T: int, n: int, seed: int, offset: int, rate: float, device):
+        dev = torch.device(device)
+        self.codes = torch.empty((T, n), dtype=torch.int16, device=dev)
+        wm = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(_lib.lib().cdna_poisson(None, T, n, int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset), float(rate),
+                                           _ptr(self.codes), _ptr(wm), _stream(dev)), "cdna_poisson(codes)")
+        self._wmax = _PendingScalar(wm, torch.cuda.current_stream(dev))
+
+    def wmax(self) -> int:
+        return max(1, int(self._wmax.get()))
+
+    def weights(self) -> torch.Tensor:
+        return ((self.codes.to(torch.int32) >> 8) & 0xFF).to(torch.uint8)
 
 
 # ------------------------------------------------------- level histogram assembly

@@ -77,10 +77,13 @@ struct PoissonCdf {
 // against the tabulated CDF (a data-dependent double loop before: k > 7 has
 // probability ~1e-5 at rate 1) and an interior quad leaves as one dword store.
 __global__ __launch_bounds__(256) void poisson_kernel(uint8_t* __restrict__ out, int T, int64_t n, uint64_t seed,
-                                                      uint64_t offset, double rate, PoissonCdf cdf, int packed) {
+                                                      uint64_t offset, double rate, PoissonCdf cdf, int packed,
+                                                      uint16_t* __restrict__ codes, unsigned* __restrict__ wmax) {
   const int t = blockIdx.y;
   const uint64_t q0 = offset >> 2, q1 = (offset + (uint64_t)n - 1) >> 2;
   uint8_t* o = out + (int64_t)t * n;
+  uint16_t* oc = codes + (int64_t)t * n;
+  unsigned m = 0u;
   for (uint64_t q = q0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= q1;
        q += (uint64_t)gridDim.x * blockDim.x) {
     const cdna::u32x4 r = cdna::philox4x32_10(cdna::u32x4{(uint32_t)q, (uint32_t)(q >> 32), 0x100u + (uint32_t)t,
@@ -97,9 +100,27 @@ __global__ __launch_bounds__(256) void poisson_kernel(uint8_t* __restrict__ out,
         while (kk < (uint32_t)kCdf && w[j] > cdf.T[kk]) ++kk;
         if (kk == (uint32_t)kCdf) kk = cdna::poisson_from_uniform((double)w[j] * (1.0 / 4294967296.0), rate);
       }
-      k[j] = kk;
+      k[j] = kk > 255u ? 255u : kk;
     }
     const uint64_t g0 = q * 4;
+    if (codes) {  // fused row codes (weight << 8 | local node 0, or 0xFF when the weight is 0) + largest weight
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m = k[j] > m ? k[j] : m;
+      uint32_t c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[j] = (k[j] << 8) | (k[j] ? 0u : 0xFFu);
+      if (packed && g0 >= offset && g0 + 3 < offset + (uint64_t)n) {
+        *reinterpret_cast<uint2*>(oc + (g0 - offset)) = uint2{c[0] | (c[1] << 16), c[2] | (c[3] << 16)};
+        continue;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t gi = g0 + j;
+        if (gi < offset || gi >= offset + (uint64_t)n) continue;
+        oc[gi - offset] = (uint16_t)c[j];
+      }
+      continue;
+    }
     if (packed && g0 >= offset && g0 + 3 < offset + (uint64_t)n) {
       *reinterpret_cast<uint32_t*>(o + (g0 - offset)) = k[0] | (k[1] << 8) | (k[2] << 16) | (k[3] << 24);
       continue;
@@ -110,6 +131,14 @@ __global__ __launch_bounds__(256) void poisson_kernel(uint8_t* __restrict__ out,
       if (gi < offset || gi >= offset + (uint64_t)n) continue;
       o[gi - offset] = (uint8_t)k[j];
     }
+  }
+  if (codes) {  // one atomic per wave
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned v = (unsigned)__shfl_xor((int)m, off);
+      m = v > m ? v : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(wmax, m);
   }
 }
 
@@ -396,9 +425,13 @@ CDNA_API int cdna_codes_init(const uint8_t* w, int64_t total, uint16_t* codes, u
   return (int)hipGetLastError();
 }
 
+// codes (optional, then out may be null): the row codes [T][n] u16 of the tree engine (codes_init_kernel's
+// format) written straight from the draws, and atomicMax of the weights into *wmax (zeroed by the caller) --
+// no uint8 weights array, no codes_init pass, no separate max reduction.
 CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_t offset, double rate,
-                          hipStream_t st) {
+                          uint16_t* codes, unsigned* wmax, hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
+  if (codes && !wmax) return (int)hipErrorInvalidValue;
   PoissonCdf cdf;
   {
     // same double operations in the same order as poisson_from_uniform's recurrence
@@ -411,9 +444,10 @@ CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_
     }
   }
   // interior quads as dword stores when every tree row starts 4-byte aligned
-  const int packed = (offset % 4 == 0) && (n % 4 == 0) && (reinterpret_cast<uintptr_t>(out) % 4 == 0);
+  const int packed = (offset % 4 == 0) && (n % 4 == 0) &&
+                     (codes ? reinterpret_cast<uintptr_t>(codes) % 8 == 0 : reinterpret_cast<uintptr_t>(out) % 4 == 0);
   hipLaunchKernelGGL(poisson_kernel, dim3(grid_for(n / 4 + 2, 256, 1024), T), dim3(256), 0, st, out, T, n, seed, offset,
-                     rate, cdf, packed);
+                     rate, cdf, packed, codes, wmax);
   return (int)hipGetLastError();
 }
 

@@ -1179,3 +1179,15 @@ def test_fused_expressions_match_operator_path(dev, monkeypatch):
         # device libm transcendentals may differ from torch's in the last ulp; arithmetic / masks are exact
         assert np.allclose(gv.astype(np.float64), rv.astype(np.float64), rtol=1e-12, atol=1e-300,
                            equal_nan=True), name
+
+
+@pytest.mark.parametrize("T,n,offset,rate", [(20, 100003, 12, 1.0), (3, 4096, 0, 1.0), (5, 999, 7, 2.5)])
+def test_bootstrap_codes_equal_codes_of_poisson_weights(dev, T, n, offset, rate):
+    """K15 fused: the Poisson draws written straight as the engine's row codes (+ their max) equal codes_init of
+    the uint8 multiplicities, and their weights() equal poisson_weights bit for bit."""
+    w = K.poisson_weights(T, n, 31, offset, rate, device=dev)
+    ref, wm = K.codes_init_max(w, T, n, dev)
+    bc = K.BootstrapCodes(T, n, 31, offset, rate, dev)
+    assert torch.equal(bc.codes, ref)
+    assert bc.wmax() == wm == int(w.max())
+    assert torch.equal(bc.weights(), w)
