@@ -1306,10 +1306,11 @@ class ForestTrainer:
             seg_raw = seg_scales if v0p is not None else seg_scales[1]
             segs = np.array([[0, perm.numel()]], dtype=np.int64)
             node = None
-        elif use_codes and codes_pre is not None:
-            codes, wmax = codes_pre.codes, codes_pre.wmax()
         elif use_codes:
-            codes, wmax = K.codes_init_max(weights, T, n, dev)
+            if codes_pre is not None:
+                codes, wmax = codes_pre.codes, codes_pre.wmax()
+            else:
+                codes, wmax = K.codes_init_max(weights, T, n, dev)
             node = None
             if use_mseg or use_sub:
                 # one quantisation scale for every rank: the int64 level histograms then all-reduce to
