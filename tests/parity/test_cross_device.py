@@ -341,6 +341,11 @@ def test_flow_matches_across_devices(results, flow):
     elif flow in TREES:
         assert a["digest"] == b["digest"]
         _close(a, b, TREE_METRIC_TOL)
+    elif flow == "lr":
+        # fp64 normal equations on both devices: coefficients to 1e-8; the RMSE of fp32 device predictions to 1e-5
+        _close({k: a[k] for k in ("coef", "intercept", "n_pred")}, {k: b[k] for k in ("coef", "intercept", "n_pred")},
+               TOL["lr"])
+        _close(a["rmse"], b["rmse"], 1e-5)
     else:
         _close(a, b, TOL[flow])
     for group in NATIVE.get(flow, []):
