@@ -229,7 +229,10 @@ def flow_logistic(spark, ds, work):
     model = Pipeline(stages=[RFormula(formula="priceClass ~ . - price", handleInvalid="skip"),
                              LogisticRegression(labelCol="priceClass", regParam=0.1)]).fit(train)
     pred = model.transform(test)
-    return {"coef": model.stages[-1].coefficients.toArray().tolist(),
+    lrm = model.stages[-1]
+    # the fitted objective, not the coefficients: L-BFGS stops at the loss tolerance, and weakly identified
+    # coefficients of this design move by up to 2x within it (fp32 device gradients vs fp64 host ones)
+    return {"loss": float(lrm.summary.objectiveHistory[-1]),
             "acc": MulticlassClassificationEvaluator(labelCol="priceClass", metricName="accuracy").evaluate(pred),
             "auc": BinaryClassificationEvaluator(labelCol="priceClass").evaluate(pred)}
 
@@ -328,7 +331,7 @@ TREE_METRIC_TOL = 1e-5
 # fp64 reductions in a different order: 1e-9 (LR: course-sized normal equations take the fp64 Gram on both
 # devices -- gramPrecision auto; the K1 fp32 MFMA Gram had moved these ill-conditioned OHE coefficients by
 # 2e-3 relative).  Logistic regression: L-BFGS / OWL-QN stops at the same loss tolerance
-# from fp32 device gradients vs fp64 host ones; weakly identified coefficients then differ by ~1e-4 absolute
+# from fp32 device gradients vs fp64 host ones: the fitted objectives and the accuracy / AUC compared
 TOL = {"cleansing": 1e-9, "exploration": 1e-9, "lr": 1e-8, "kmeans": 1e-6, "logistic": 2e-3}
 
 
