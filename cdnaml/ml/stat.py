@@ -14,12 +14,8 @@ class Correlation:
         X, _, _ = local_xyw(dataset, column)
         if method == "spearman":
             X = torch.argsort(torch.argsort(X, 0), 0).float()
-        d = X.shape[1]
-        G = K.gram(X) if X.shape[0] else torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
-        dataset._session.comm.all_reduce(G)
-        n = float(G[d, d])
-        s = G[:d, d]
-        C = (G[:d, :d] - torch.outer(s, s) / n)
+        from ..models.util import centered_gram
+        _, _, C = centered_gram(X, dataset._session.comm)
         sd = torch.sqrt(torch.diagonal(C).clamp_min(1e-300))
         R = (C / torch.outer(sd, sd)).cpu().numpy()
         return _MatrixFrame(R, method, column)

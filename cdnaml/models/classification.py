@@ -26,7 +26,7 @@ from .param import NO_DEFAULT, TypeConverters as TC, keyword_init
 from .regression import (_GBT, _PRED, _RF, _TREE, _TreeModelBase, _bag_weights, _combine_weights, _num_classes,
                          _subforest, resolve_subset, tree_fit_prepare)
 from .tree.engine import Forest, ForestTrainer, TreeParams
-from .util import IllegalArgumentException, local_batch, local_xyw, require_vector
+from .util import IllegalArgumentException, centered_gram, local_batch, local_xyw, require_vector
 
 _CLS = dict(_PRED, **{
     "probabilityCol": ("Column name for predicted class conditional probabilities.", "probability", TC.toString),
@@ -86,19 +86,16 @@ class LogisticRegression(Estimator):
             family = "binomial" if C <= 2 else "multinomial"
         if family == "binomial" and C > 2:
             raise IllegalArgumentException(f"Binomial family only supports 1 or 2 outcome classes but found {C}.")
-        # feature std (population) from the Gram kernel's diagonal
-        G = K.gram(X) if X.shape[0] else torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
-        comm.all_reduce(G)
-        Gh = G.cpu().numpy()
-        n = Gh[d, d]
+        # feature std from the centred Gram (a raw-moment std weighs narrow, far-from-zero features wrongly in the
+        # standardised L2 penalty)
+        n, _, Cg = centered_gram(X, comm)
+        var = np.clip(torch.diagonal(Cg).cpu().numpy(), 0, None) / max(n - 1, 1)
         if w is not None:
             wsum = torch.tensor([float(w.sum())], dtype=torch.float64, device=X.device)
             comm.all_reduce(wsum)
             n_eff = float(wsum)
         else:
             n_eff = n
-        mean = Gh[:d, d] / max(n, 1)
-        var = np.clip(np.diag(Gh)[:d] / max(n, 1) - mean * mean, 0, None) * (n / max(n - 1, 1))
         sd = np.sqrt(var)
         sdz = np.where(sd > 0, sd, 1.0)
         lam, alpha = self.getRegParam(), self.getElasticNetParam()

@@ -617,18 +617,10 @@ class StandardScaler(Estimator):
         keyword_init(self, dict(withMean=withMean, withStd=withStd, inputCol=inputCol, outputCol=outputCol))
 
     def _fit(self, dataset):
-        from ..ops import kernels as K
-        from .util import local_xyw
+        from .util import centered_gram, local_xyw
         X, _, _ = local_xyw(dataset, self.getInputCol())
-        comm = dataset._session.comm
-        d = X.shape[1]
-        G = K.gram(X) if X.shape[0] else torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
-        comm.all_reduce(G)
-        n = float(G[d, d])
-        s = G[:d, d]
-        ss = torch.diagonal(G)[:d]
-        mean = s / max(n, 1)
-        var = (ss - s * s / max(n, 1)) / max(n - 1, 1)
+        n, mean, C = centered_gram(X, dataset._session.comm)
+        var = torch.diagonal(C) / max(n - 1, 1)
         return StandardScalerModel(mean=mean.cpu().numpy(), std=torch.sqrt(var.clamp_min(0)).cpu().numpy())
 
 
@@ -848,15 +840,10 @@ class PCA(Estimator):
         keyword_init(self, dict(k=k, inputCol=inputCol, outputCol=outputCol))
 
     def _fit(self, dataset):
-        from ..ops import kernels as K
-        from .util import local_xyw
+        from .util import centered_gram, local_xyw
         X, _, _ = local_xyw(dataset, self.getInputCol())
-        d = X.shape[1]
-        G = K.gram(X) if X.shape[0] else torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
-        dataset._session.comm.all_reduce(G)
-        n = float(G[d, d])
-        s = G[:d, d]
-        cov = (G[:d, :d] - torch.outer(s, s) / n) / max(n - 1, 1)
+        n, _, C = centered_gram(X, dataset._session.comm)
+        cov = C / max(n - 1, 1)
         w, v = torch.linalg.eigh(cov.cpu())
         order = torch.argsort(w, descending=True)[: self.getK()]
         pc = v[:, order].numpy()

@@ -118,6 +118,30 @@ def streamed_columns(df, features_col: str, cols: List[str], head_rows: int = 0)
     return ChunkedRows(chunks, n, d, dev), out, sel.schema[features_col].metadata
 
 
+def centered_gram(X: torch.Tensor, comm, lead: int = 1024):
+    """(n, mean[d], C[d, d]) over all ranks, C = sum (x - mean)(x - mean)^T, all fp64.
+
+    The Gram kernel runs on features shifted by a common mean estimate (every rank's leading rows, averaged over
+    the ranks that have any), so the second moments are formed about a point near the mean: E[x^2] - mean^2 of
+    the raw fp32 columns cancels catastrophically for narrow, far-from-zero features (latitude: sd 0.02 about 37.8).
+    """
+    from ..ops import kernels as K
+    n_loc, d = X.shape
+    k = min(n_loc, lead)
+    sh = X[:k].double().mean(0) if k else torch.zeros(d, dtype=torch.float64, device=X.device)
+    if comm.distributed:
+        cnt = torch.full((1,), 1.0 if k else 0.0, dtype=torch.float64, device=X.device)
+        comm.all_reduce_many([sh, cnt])
+        sh = sh / cnt.clamp_min(1.0)
+    sh = sh.float()
+    G = K.gram(X, shift=sh) if n_loc else torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
+    comm.all_reduce(G)
+    n = float(G[d, d])
+    s = G[:d, d]
+    C = G[:d, :d] - torch.outer(s, s) / max(n, 1.0)
+    return n, sh.double() + s / max(n, 1.0), C
+
+
 def vector_attrs(meta: dict, width: int, name: str) -> List[dict]:
     """Per-slot attributes of a vector column (names, nominal arity)."""
     ma = (meta or {}).get("ml_attr")
