@@ -13,7 +13,8 @@
 #   prof8            same at 1.25e7 rows
 #   pmc:<regex>      PMC pass (counters from scripts/pmc_hist.txt) over kernels matching <regex>
 #   configs          BASELINE configs 2-5 (bench_configs.py lr/cv/infer/gbdt)
-#   cfg:<name>       one bench_configs.py config
+#   cfg:<name>       one bench_configs.py config ('cfg:ooc --model rf': arguments after the name; outputs
+#                    cfg_<name and arguments, non-alphanumerics as _>.json/.log)
 #   profcfg:<name>   rocprofv3 --kernel-trace --stats of one bench_configs.py config (CFG_ARGS passed on)
 #   py:<file>        python <file> (a scratch experiment)
 # Extra environment for bench/prof steps: BENCH_ARGS="--steps 3 ..."
@@ -72,9 +73,9 @@ run_step() {
     configs)
         run_step cfg:lr && run_step cfg:cv && run_step cfg:infer && run_step cfg:gbdt ;;
     cfg:*)
-        local c=${s#cfg:}
-        timeout -k 10 600 python bench_configs.py $c ${CFG_ARGS} > "$O/cfg_$c.json" 2> "$O/cfg_$c.log"
-        local rc=$?; tail -2 "$O/cfg_$c.log"; cat "$O/cfg_$c.json"; return $rc ;;
+        local c=${s#cfg:}; local nm; nm=$(echo "$c" | tr -c 'A-Za-z0-9_\n-' '_')
+        timeout -k 10 600 python bench_configs.py $c ${CFG_ARGS} > "$O/cfg_$nm.json" 2> "$O/cfg_$nm.log"
+        local rc=$?; tail -2 "$O/cfg_$nm.log"; cat "$O/cfg_$nm.json"; return $rc ;;
     py:*)
         timeout -k 10 600 python -u "${s#py:}" > "$O/py.log" 2>&1; local rc=$?; tail -30 "$O/py.log"; return $rc ;;
     *)

@@ -109,7 +109,7 @@ def test_emit_checked_build(tmp_path):
     compaction's records of the same codes."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = dict(os.environ, CDNAML_HIP_DEBUG="1")
+    env = dict(os.environ, CDNAML_HIP_DEBUG="1", CDNAML_P7_EMIT="1")
     r = subprocess.run([sys.executable, "-c", SCRIPT], env=env, cwd=ROOT, capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0 and "emit checked ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
