@@ -63,45 +63,46 @@ class ForestPredictor:
             self._dev[key] = (tw, heap, b)
         return self._dev[key]
 
-    def _launch(self, X: torch.Tensor) -> torch.Tensor:
+    def _launch(self, X: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
         from ..ops import kernels as K
         tw, heap, b = self._arrays(X.device)
         if heap is not None:
             b0 = 0.0 if self.base is None else float(np.asarray(self.base, np.float64).reshape(-1)[0])
-            out = K.tree_predict_heap(X, heap[0], heap[1], tw, heap[2], b0)
+            out = K.tree_predict_heap(X, heap[0], heap[1], tw, heap[2], b0, dtype=dtype)
             if out is not None:
                 return out
         nodes, roots, vals, masks = self.forest.device_arrays(X.device, self.kind)
-        return K.tree_predict(X, nodes, roots, tw, vals, masks, self.forest.K, b)
+        return K.tree_predict(X, nodes, roots, tw, vals, masks, self.forest.K, b).to(dtype)
 
-    def __call__(self, X: torch.Tensor) -> torch.Tensor:
-        """[n, d] features -> [n, K] float32 predictions (a fresh tensor the caller owns)."""
+    def __call__(self, X: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+        """[n, d] features -> [n, K] predictions (a fresh tensor the caller owns): float32 sums, stored as
+        ``dtype`` (float64: widened in the kernel's store, == ``.double()`` of the float32 result)."""
         if not (GRAPH_PREDICT and X.is_cuda and X.shape[0] >= GRAPH_MIN_ROWS and X.is_contiguous()):
-            return self._launch(X)
+            return self._launch(X, dtype)
         if threading.current_thread() is not threading.main_thread():
             # worker threads (applyInPandas pools, GPUTrials, GroupedModel) may allocate or synchronise while
             # another thread captures: graphs are captured and replayed from the main thread only
-            return self._launch(X)
-        key = (X.data_ptr(), tuple(X.shape), X.dtype, X.device.index)
+            return self._launch(X, dtype)
+        key = (X.data_ptr(), tuple(X.shape), X.dtype, X.device.index, dtype)
         with self._lock:
-            return self._graph_call(X, key)
+            return self._graph_call(X, key, dtype)
 
-    def _graph_call(self, X: torch.Tensor, key) -> torch.Tensor:
+    def _graph_call(self, X: torch.Tensor, key, dtype=torch.float32) -> torch.Tensor:
         g = self._graphs.get(key)
         if g is None:
             # capture on the second sighting of a buffer: staging buffers recur, one-off tensors do not
             self._seen[key] = self._seen.get(key, 0) + 1
             if self._seen[key] < 2:
-                return self._launch(X)
+                return self._launch(X, dtype)
             self._arrays(X.device)
             s = torch.cuda.Stream(device=X.device)
             s.wait_stream(torch.cuda.current_stream(X.device))
             with torch.cuda.stream(s):
-                self._launch(X)  # warm-up outside capture (allocator, LDS attributes)
+                self._launch(X, dtype)  # warm-up outside capture (allocator, LDS attributes)
             torch.cuda.current_stream(X.device).wait_stream(s)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-                out = self._launch(X)
+                out = self._launch(X, dtype)
             g = (graph, out)
             self._graphs[key] = g
             self.captures += 1

@@ -648,7 +648,7 @@ class _TreeRegressorModel(_TreeModelBase):
 
         def fn(b, ctx):
             X = b.columns[fc].values
-            p = predictor(X)[:, 0].double() if X.shape[0] else \
+            p = predictor(X, torch.float64)[:, 0] if X.shape[0] else \
                 torch.zeros(0, dtype=torch.float64, device=X.device)
             out = {pc: ColumnData(p, T.DoubleType())}
             self._leaf_col(b, out)
@@ -682,9 +682,7 @@ def _early_side_work(num_trees, bootstrap, rate, want_label_max=True, codes_ok=F
         side = _side_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         if want_label_max:
-            with torch.cuda.stream(side):
-                early["yf"] = y_.float()
-            K.prefetch_max(early["yf"], absval=True, stream=side)
+            early["yf"] = K.float_with_absmax(y_, stream=side)
         if bootstrap and num_trees > 1:
             if codes_ok and K.POISSON_CODES:
                 # the draws written straight as the engine's row codes + their max (no uint8 weights, no

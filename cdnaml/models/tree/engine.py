@@ -282,8 +282,11 @@ def _global_sample(session, X, max_bins: int, seed: int, row_offset: int, n_glob
                 parts.append(Xc.float().clone())
         samp = torch.cat(parts) if parts else torch.zeros((0, X.d), dtype=torch.float32, device=X.device)
     elif frac < 1.0:
-        u = K.uniform(n, seed ^ 0x5BD1E995, row_offset, 3, device=X.device)
-        samp = X[K.compact_mask(u < frac)]
+        idx = K.sample_rows(n, seed ^ 0x5BD1E995, row_offset, 3, frac, X.device) if X.is_cuda and n else None
+        if idx is None:
+            u = K.uniform(n, seed ^ 0x5BD1E995, row_offset, 3, device=X.device)
+            idx = K.compact_mask(u < frac)
+        samp = X[idx]
     else:
         samp = X
     if comm.distributed:

@@ -206,10 +206,13 @@ _SIGS = {
     "cdna_tree_predict": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p,
                            c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p], c_int),
     "cdna_tree_predict_heap": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
-                                c_float, c_void_p, c_void_p], c_int),
+                                c_float, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_predict_binned_add": ([c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p,
                                  c_void_p], c_int),
     "cdna_uniform": ([c_void_p, c_int64, c_uint64, c_uint64, c_uint32, c_void_p], c_int),
+    "cdna_sample_rows": ([c_int64, c_uint64, c_uint64, c_uint32, c_double, c_void_p, c_int64, c_void_p, c_void_p],
+                         c_int),
+    "cdna_cast_absmax": ([c_void_p, c_int64, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_normal_f32": ([c_void_p, c_int64, c_uint64, c_uint64, c_uint32, c_void_p], c_int),
     "cdna_poisson": ([c_void_p, c_int, c_int64, c_uint64, c_uint64, c_double, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_reg_metrics": ([c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p], c_int),

@@ -446,6 +446,45 @@ class _PendingScalar:
         return float(self.host[0])
 
 
+def float_with_absmax(t: torch.Tensor, stream=None) -> torch.Tensor:
+    """``t.float()`` of a contiguous fp64 device column with max |t| queued alongside (as prefetch_max(absval)
+    attaches it): one pass of misc.hip cast_absmax_kernel instead of cast + abs + max."""
+    st = stream if stream is not None else torch.cuda.current_stream(t.device)
+    if not (_native(t) and t.dtype == torch.float64 and t.dim() == 1 and t.is_contiguous() and t.numel()):
+        with torch.cuda.stream(st):
+            out = t.float()
+        prefetch_max(out, absval=True, stream=st)
+        return out
+    with torch.cuda.stream(st):
+        out = torch.empty(t.shape, dtype=torch.float32, device=t.device)
+        bits = torch.empty(1, dtype=torch.int32, device=t.device)
+        rc = _lib.lib().cdna_cast_absmax(_ptr(t), t.numel(), _ptr(out), _ptr(bits), st.cuda_stream)
+        if rc == 1:  # misaligned view: the torch passes
+            out = t.float()
+            prefetch_max(out, absval=True, stream=st)
+            return out
+        _lib.check(rc, "cdna_cast_absmax")
+        setattr(out, "_cdna_absmax", _PendingScalar(bits.view(torch.float32), st))
+    return out
+
+
+def sample_rows(n: int, seed: int, offset: int, stream: int, frac: float, device) -> Optional[torch.Tensor]:
+    """Sorted int64 ids of the rows r < n with ``uniform(n, seed, offset, stream)[r] < frac`` (one fused kernel;
+    == compact_mask(uniform(...) < frac)).  None when the count passes the capacity sized from the expected
+    count (the caller then takes the materialised path)."""
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    exp_ = n * frac
+    cap = int(exp_ + 12.0 * math.sqrt(exp_ + 1.0) + 1024)
+    idx = torch.empty(cap, dtype=torch.int64, device=device)
+    cnt = torch.empty(1, dtype=torch.int32, device=device)
+    _lib.check(_lib.lib().cdna_sample_rows(n, seed, int(offset), int(stream) & 0xFFFFFFFF, float(frac), _ptr(idx),
+                                           cap, _ptr(cnt), _stream(torch.device(device))), "cdna_sample_rows")
+    c = int(cnt.item())
+    if c > cap:
+        return None
+    return torch.sort(idx[:c]).values
+
+
 def prefetch_max(t: torch.Tensor, absval: bool = False, stream=None) -> None:
     """Queue max(t) (max |t|) on ``stream`` (default: current) and attach it to the tensor object itself (never
     keyed by address: a recycled allocation must not inherit a stale value) for packed_scale_global /
@@ -999,9 +1038,10 @@ def partition(bins: torch.Tensor, node: torch.Tensor, split_feat: torch.Tensor, 
 
 # --------------------------------------------------------------------- K8
 def tree_predict_heap(X: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: torch.Tensor,
-                      masks: torch.Tensor, base: float = 0.0) -> Optional[torch.Tensor]:
+                      masks: torch.Tensor, base: float = 0.0, dtype=torch.float32) -> Optional[torch.Tensor]:
     """Single-output ensemble prediction over a heap-laid-out forest (int32 [T, S, 2], S = 2^(depth+1)-1).
 
+    dtype float64: the fp32 sums stored widened by the kernel (== the float32 result's .double()).
     Returns None when the forest does not fit the kernel's LDS budget (use ``tree_predict``)."""
     n, d = X.shape
     T, S, _ = heap.shape
@@ -1009,12 +1049,14 @@ def tree_predict_heap(X: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: t
         return None
     X = X.float()
     X = X if X.stride(1) == 1 else X.contiguous()
-    out = torch.empty((n, 1), dtype=torch.float32, device=X.device)
+    out = torch.empty((n, 1), dtype=dtype, device=X.device)
     if n == 0:
         return out
     m = masks.int().contiguous() if masks.numel() else torch.zeros(8, dtype=torch.int32, device=X.device)
+    f64 = dtype == torch.float64
     rc = _lib.lib().cdna_tree_predict_heap(_ptr(X), n, d, X.stride(0), _ptr(heap), S, depth,
-                                           _ptr(tree_w.float().contiguous()), T, _ptr(m), float(base), _ptr(out),
+                                           _ptr(tree_w.float().contiguous()), T, _ptr(m), float(base),
+                                           None if f64 else _ptr(out), _ptr(out) if f64 else None,
                                            _stream(X.device))
     if rc == 1:  # hipErrorInvalidValue: over the LDS budget
         return None

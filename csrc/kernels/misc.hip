@@ -446,8 +446,85 @@ CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_
   // interior quads as dword stores when every tree row starts 4-byte aligned
   const int packed = (offset % 4 == 0) && (n % 4 == 0) &&
                      (codes ? reinterpret_cast<uintptr_t>(codes) % 8 == 0 : reinterpret_cast<uintptr_t>(out) % 4 == 0);
-  hipLaunchKernelGGL(poisson_kernel, dim3(grid_for(n / 4 + 2, 256, 1024), T), dim3(256), 0, st, out, T, n, seed, offset,
-                     rate, cdf, packed, codes, wmax);
+  // A bounded grid (default 512 blocks over all trees, 2 per CU): the draws run on the side stream next to the
+  // quantile sample's latency-bound kernels, and a grid of T x 1024 blocks kept every CU full, so the sample's
+  // sort (100 blocks of 1024 threads) waited for whole CUs to drain: 2.1 ms instead of 0.3 ms at 1e8 rows.
+  static const int max_blocks = [] {
+    const char* e = getenv("CDNAML_POISSON_BLOCKS");
+    const int v = e ? atoi(e) : 512;
+    return v > 0 ? v : 512;
+  }();
+  unsigned gx = grid_for(n / 4 + 2, 256, 1024);
+  const unsigned cap = (unsigned)((max_blocks + T - 1) / T);
+  gx = gx < cap ? gx : (cap > 0 ? cap : 1u);
+  hipLaunchKernelGGL(poisson_kernel, dim3(gx, T), dim3(256), 0, st, out, T, n, seed, offset, rate, cdf, packed, codes,
+                     wmax);
+  return (int)hipGetLastError();
+}
+
+// Row ids r < n whose Philox uniform (seed, offset + r, stream) is below frac -- K.uniform(...) < frac compacted,
+// without the n doubles, the mask bytes and the count / scan / write passes (the quantile sample of
+// engine._global_sample, ~1e-4 of the rows).  Waves with a kept row claim their slots with one atomicAdd, so
+// the ids land in arbitrary order (the caller sorts the <= cap of them); *count (zeroed here) may pass cap,
+// then only ids below cap are written and the caller falls back.
+__global__ __launch_bounds__(256) void sample_rows_kernel(int64_t n, uint64_t seed, uint64_t offset, uint32_t stream,
+                                                          double frac, int64_t* __restrict__ idx, int64_t cap,
+                                                          unsigned* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t rb = (int64_t)blockIdx.x * 256; rb < n; rb += (int64_t)gridDim.x * 256) {
+    const int64_t r = rb + threadIdx.x;
+    const bool keep = r < n && cdna::philox_uniform(seed, offset + (uint64_t)r, stream) < frac;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
+    if (m == 0) continue;
+    unsigned base = 0u;
+    if (lane == 0) base = atomicAdd(count, (unsigned)__builtin_popcountll(m));
+    base = (unsigned)__shfl((int)base, 0);
+    const unsigned below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (keep && (int64_t)base + below < cap) idx[(int64_t)base + below] = r;
+  }
+}
+
+CDNA_API int cdna_sample_rows(int64_t n, uint64_t seed, uint64_t offset, uint32_t stream, double frac, int64_t* idx,
+                              int64_t cap, unsigned* count, hipStream_t st) {
+  if (!count || (cap > 0 && !idx)) return (int)hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(unsigned), st);
+  if (e != hipSuccess || n <= 0) return (int)e;
+  hipLaunchKernelGGL(sample_rows_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, n, seed, offset, stream, frac,
+                     idx, cap, count);
+  return (int)hipGetLastError();
+}
+
+// fp32 copy of an fp64 column and max |x| as fp32 bits (atomicMax on the int bits: non-negative floats order
+// as their bit patterns, and a NaN's (0x7FC00000) beats +inf, so a NaN label surfaces as a NaN maximum).
+// One pass for the forest's label (y.float() + |y|.max() were three full passes).  *amax is zeroed here.
+__global__ __launch_bounds__(256) void cast_absmax_kernel(const double* __restrict__ x, int64_t n,
+                                                          float* __restrict__ out, int* __restrict__ amax) {
+  int m = 0;
+  const int64_t n2 = n / 2;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n2; q += (int64_t)gridDim.x * 256) {
+    const double2 v = reinterpret_cast<const double2*>(x)[q];
+    const float a = (float)v.x, b = (float)v.y;
+    reinterpret_cast<float2*>(out)[q] = float2{a, b};
+    const int ia = __float_as_int(a) & 0x7FFFFFFF, ib = __float_as_int(b) & 0x7FFFFFFF;
+    m = max(m, max(ia, ib));
+  }
+  for (int64_t i = 2 * n2 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float a = (float)x[i];
+    out[i] = a;
+    m = max(m, __float_as_int(a) & 0x7FFFFFFF);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0 && m > 0) atomicMax(amax, m);
+}
+
+CDNA_API int cdna_cast_absmax(const double* x, int64_t n, float* out, int* amax, hipStream_t st) {
+  if (!amax) return (int)hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(amax, 0, sizeof(int), st);
+  if (e != hipSuccess || n <= 0) return (int)e;
+  if (reinterpret_cast<uintptr_t>(x) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 8 != 0)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(cast_absmax_kernel, dim3(grid_for(n / 2 + 1, 256, 512)), dim3(256), 0, st, x, n, out, amax);
   return (int)hipGetLastError();
 }
 

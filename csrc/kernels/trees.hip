@@ -727,7 +727,7 @@ __global__ __launch_bounds__(256) void predict_heap_kernel(const float* __restri
                                                            const int2* __restrict__ heap, int S, int depth,
                                                            const float* __restrict__ tree_w, int T,
                                                            const uint32_t* __restrict__ masks, float base,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ out, double* __restrict__ out_d) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   int2* sheap = reinterpret_cast<int2*>(sm);
   float* stw = sm + (size_t)T * S * 2;
@@ -813,8 +813,14 @@ __global__ __launch_bounds__(256) void predict_heap_kernel(const float* __restri
     }
     part[tl * 64 + row] = acc;
     __syncthreads();
-    if (threadIdx.x < rows) out[r0 + threadIdx.x] = base + part[threadIdx.x] + part[64 + threadIdx.x] +
-                                                    part[128 + threadIdx.x] + part[192 + threadIdx.x];
+    if (threadIdx.x < rows) {
+      const float v = base + part[threadIdx.x] + part[64 + threadIdx.x] + part[128 + threadIdx.x] +
+                      part[192 + threadIdx.x];
+      if (out_d)
+        out_d[r0 + threadIdx.x] = (double)v;  // the DoubleType prediction column directly (no fp32 -> fp64 pass)
+      else
+        out[r0 + threadIdx.x] = v;
+    }
   }
 }
 
@@ -1017,12 +1023,12 @@ CDNA_API int cdna_predict_binned_add(const uint64_t* bins, int64_t n, const int4
 // does not fit the LDS budget (the caller then uses cdna_tree_predict).
 CDNA_API int cdna_tree_predict_heap(const float* X, int64_t n, int d, int64_t ldx, const int2* heap, int S, int depth,
                                     const float* tree_w, int T, const uint32_t* masks, float base, float* out,
-                                    hipStream_t st) {
+                                    double* out_d, hipStream_t st) {
   if (n <= 0) return 0;
   const size_t lds = (size_t)T * S * 8 + (size_t)((T + 3) & ~3) * 4 + ((size_t)64 * (d + 1) + 256) * 4;
   if (lds > 64 * 1024 || depth < 0 || depth > 12) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(predict_heap_kernel, dim3(grid_for(n, 64, 8192)), dim3(256), lds, st, X, n, d, ldx, heap, S,
-                     depth, tree_w, T, masks, base, out);
+                     depth, tree_w, T, masks, base, out, out_d);
   return (int)hipGetLastError();
 }
 

@@ -1191,3 +1191,44 @@ def test_bootstrap_codes_equal_codes_of_poisson_weights(dev, T, n, offset, rate)
     assert torch.equal(bc.codes, ref)
     assert bc.wmax() == wm == int(w.max())
     assert torch.equal(bc.weights(), w)
+
+
+@pytest.mark.parametrize("n,offset,frac", [(1_000_003, 17, 1e-3), (5000, 0, 0.3), (1, 5, 0.999), (4096, 3, 1e-9)])
+def test_sample_rows_equals_compacted_uniform(dev, n, offset, frac):
+    """misc.hip sample_rows_kernel (one fused pass, ids claimed per wave, sorted after) == the materialised
+    compact_mask(uniform(...) < frac) of the quantile sample."""
+    ids = K.sample_rows(n, 0x5BD1E995 ^ 7, offset, 3, frac, dev)
+    ref = K.compact_mask(K.uniform(n, 0x5BD1E995 ^ 7, offset, 3, device=dev) < frac)
+    assert ids is not None and torch.equal(ids, ref)
+
+
+def test_float_with_absmax(dev):
+    """misc.hip cast_absmax_kernel: the fp32 copy and max |x| of an fp64 column (odd length: the scalar tail;
+    a NaN surfaces as a NaN maximum, which packed_scale_global rejects)."""
+    g = torch.Generator(device=dev).manual_seed(5)
+    y = torch.randn(1_000_001, generator=g, device=dev, dtype=torch.float64) * 3
+    y[77] = -41.5
+    yf = K.float_with_absmax(y)
+    assert torch.equal(yf, y.float())
+    assert K._prefetched(yf, True) == float(y.float().abs().max()) == 41.5
+    y[5] = float("nan")
+    assert math.isnan(K._prefetched(K.float_with_absmax(y), True))
+    z = K.float_with_absmax(torch.zeros(3, dtype=torch.float64, device=dev))
+    assert K._prefetched(z, True) == 0.0
+
+
+def test_heap_predict_double_store(dev):
+    """predict_heap_kernel's fp64 store == .double() of its fp32 output (the DoubleType prediction column)."""
+    import cdnaml
+    from cdnaml.models.regression import RandomForestRegressor
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator(device=dev).manual_seed(2)
+    X = torch.randn((20000, 12), generator=g, device=dev)
+    y = (X[:, 0] - 2 * X[:, 3]).double()
+    m = RandomForestRegressor(numTrees=6, maxDepth=4, seed=1).fit(
+        spark.createDataFrameFromLocalTensors({"features": X, "label": y}))
+    ha = m._forest.heap_arrays(X.device, "value")
+    tw = torch.tensor(m._tree_w, dtype=torch.float32, device=dev)
+    a = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], 0.0)
+    b = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], 0.0, dtype=torch.float64)
+    assert b.dtype == torch.float64 and torch.equal(b, a.double())
