@@ -502,8 +502,9 @@ def resolve_subset(strategy: str, d: int, num_trees: int, classification: bool) 
 def tree_fit_prepare(est, dataset, classification: bool, pre=None):
     """Common: device features/labels, categorical info, global row offset, binned data.
 
-    pre(n_local, row_offset, seed, device, y): launched before the quantile sample and binning are queued (the
-    forest's bootstrap draws and label maximum, which depend on neither, then overlap them on a side stream)."""
+    pre(n_local, row_offset, seed, device, y): launched before the quantile sample is queued (the label's fp32
+    copy and maximum, on a side stream); it may return a callable, run right before the binning is queued (the
+    bootstrap draws: compute-bound, they overlap the memory-bound binning)."""
     fc, lc = est.getFeaturesCol(), est.getLabelCol()
     wc = est.getWeightCol() if est.hasParam("weightCol") else None
     require_vector(dataset, fc)
@@ -531,9 +532,8 @@ def tree_fit_prepare(est, dataset, classification: bool, pre=None):
     seed = est.getOrDefault("seed")
     if seed is None:
         seed = _default_seed(type(est))
-    if pre is not None:
-        pre(n, off, seed, X.device, y)
-    data = make_binned(session, X, cat, est.getMaxBins(), seed, off, n_global)
+    late = pre(n, off, seed, X.device, y) if pre is not None else None
+    data = make_binned(session, X, cat, est.getMaxBins(), seed, off, n_global, before_binize=late)
     return session, data, y, w, seed, fmeta
 
 
@@ -669,29 +669,35 @@ class _TreeRegressorModel(_TreeModelBase):
 
 
 def _early_side_work(num_trees, bootstrap, rate, want_label_max=True, codes_ok=False):
-    """(pre, early): ``pre`` for tree_fit_prepare queues the Poisson bootstrap draws and the maxima the fit needs
-    on the host (largest weight, max |label|) on the side stream before the quantile sample / threshold / binning
-    kernels: they overlap the sort of the sample (100 of 256 CUs busy) instead of competing with the
-    memory-bound binning, and the first level reads the maxima without draining the queue.  ``early`` then holds
-    "w" (weights) and "yf" (fp32 label); call _join_early once the binning is queued."""
+    """(pre, early): ``pre`` for tree_fit_prepare queues the label's fp32 copy and max |label| on the side stream
+    before the quantile sample, and returns the Poisson bootstrap draws (+ the largest weight) for
+    tree_fit_prepare to queue on the side stream right before the binning; the first level reads the maxima
+    without draining the queue.  ``early`` then holds "yf" (fp32 label) and "codes" (BootstrapCodes) or "w"
+    (weights); call _join_early once the binning is queued."""
     early = {}
 
     def pre(n, off, seed_, dev, y_):
         if dev.type != "cuda":
-            return
+            return None
         side = _side_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         if want_label_max:
             early["yf"] = K.float_with_absmax(y_, stream=side)
-        if bootstrap and num_trees > 1:
-            if codes_ok and K.POISSON_CODES:
-                # the draws written straight as the engine's row codes + their max (no uint8 weights, no
-                # codes_init pass, no separate max reduction over T x n bytes)
-                with torch.cuda.stream(side):
-                    early["codes"] = K.BootstrapCodes(num_trees, n, seed_, off, rate, dev)
-            else:
-                early["w"] = _poisson_side(num_trees, n, seed_, off, rate, dev, join=False)
-                K.prefetch_max(early["w"], stream=side)
+
+        def draws():
+            # queued right before the binning: the Poisson kernel (compute-bound) beside the memory-bound binning,
+            # not beside the quantile sample's sort, whose 1024-thread blocks it kept off the CUs (1.6 ms for a
+            # 0.3 ms kernel at 1e8 rows)
+            if bootstrap and num_trees > 1:
+                if codes_ok and K.POISSON_CODES:
+                    # the draws written straight as the engine's row codes + their max (no uint8 weights, no
+                    # codes_init pass, no separate max reduction over T x n bytes)
+                    with torch.cuda.stream(side):
+                        early["codes"] = K.BootstrapCodes(num_trees, n, seed_, off, rate, dev)
+                else:
+                    early["w"] = _poisson_side(num_trees, n, seed_, off, rate, dev, join=False)
+                    K.prefetch_max(early["w"], stream=side)
+        return draws
     return pre, early
 
 

@@ -294,18 +294,38 @@ def _global_sample(session, X, max_bins: int, seed: int, row_offset: int, n_glob
     return samp
 
 
+class _Once:
+    """A callable run at most once (None: nothing)."""
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __call__(self):
+        fn, self.fn = self.fn, None
+        if fn is not None:
+            fn()
+
+
 def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins: int, seed: int,
-                row_offset: int, n_global: int, missing: Optional[float] = None) -> BinnedData:
+                row_offset: int, n_global: int, missing: Optional[float] = None, before_binize=None) -> BinnedData:
     """:func:`_make_binned`, reused across the trials of one hyperparameter search (bincache.scope(), entered by
-    fmin; never outside one)."""
+    fmin; never outside one).
+
+    before_binize(): run once, right before the binning kernel is queued (after the quantile sample and the
+    thresholds), or after a cache hit -- the caller's side-stream work that should overlap the memory-bound
+    binning rather than the latency-bound sample / sort kernels (the bootstrap draws)."""
     from . import bincache
+    hook = _Once(before_binize)
     if isinstance(X, ChunkedRows):  # streamed: no content fingerprint (X is never resident)
-        return _make_binned(session, X, categorical, max_bins, seed, row_offset, n_global, missing)
-    return bincache.cached(
-        lambda: (bincache.fingerprint(X), tuple(sorted(categorical.items())), int(max_bins), int(seed),
-                 int(row_offset), int(n_global), None if missing is None else float(missing), str(X.device)),
-        lambda: _make_binned(session, X, categorical, max_bins, seed, row_offset, n_global, missing),
-        comm=session.comm)
+        data = _make_binned(session, X, categorical, max_bins, seed, row_offset, n_global, missing, hook)
+    else:
+        data = bincache.cached(
+            lambda: (bincache.fingerprint(X), tuple(sorted(categorical.items())), int(max_bins), int(seed),
+                     int(row_offset), int(n_global), None if missing is None else float(missing), str(X.device)),
+            lambda: _make_binned(session, X, categorical, max_bins, seed, row_offset, n_global, missing, hook),
+            comm=session.comm)
+    hook()
+    return data
 
 
 def _binize_src(X, thr, nthr, missing=None, want_rm=False, rm_layout="std"):
@@ -331,7 +351,7 @@ def _binize_src(X, thr, nthr, missing=None, want_rm=False, rm_layout="std"):
 
 
 def _make_binned(session, X, categorical: Dict[int, int], max_bins: int, seed: int,
-                 row_offset: int, n_global: int, missing: Optional[float] = None) -> BinnedData:
+                 row_offset: int, n_global: int, missing: Optional[float] = None, before_binize=None) -> BinnedData:
     """Global-sample quantile thresholds + device binning.
 
     ``missing`` (XGBoost semantics, ML 11:67 ``missing=0``): NaN and values equal
@@ -339,6 +359,7 @@ def _make_binned(session, X, categorical: Dict[int, int], max_bins: int, seed: i
     hold the observed values, so every split can route missing rows either way.
     """
     d = X.shape[1]
+    before_binize = before_binize if before_binize is not None else (lambda: None)
     if missing is not None:
         # thresholds of the observed values from the (missing -> NaN) global sample; the binning kernel maps
         # missing values to -inf -> bin 0 on the fly (no masked copies of the full matrix)
@@ -353,6 +374,7 @@ def _make_binned(session, X, categorical: Dict[int, int], max_bins: int, seed: i
         thr = np.concatenate([np.full((d, 1), -np.finfo(np.float32).max), ithr], 1)
         nthr = inthr + 1
         thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
+        before_binize()
         with _tr.span("tree.binize"):
             bins, rm = _binize_src(X, thr_t, torch.from_numpy(nthr).to(X.device), missing=float(missing),
                                    want_rm=True)
@@ -378,6 +400,7 @@ def _make_binned(session, X, categorical: Dict[int, int], max_bins: int, seed: i
             q = K.quantile_thresholds_dev(samp, max_bins)
         if q is not None:
             thr_d, nthr_d, pend = q
+            before_binize()
             with _tr.span("tree.binize"):
                 bins, rm = K.binize(X, thr_d.float(), nthr_d, want_rm=True, rm_layout="s10" if s10 else "std")
             thr, ints = pend.get()
@@ -391,6 +414,7 @@ def _make_binned(session, X, categorical: Dict[int, int], max_bins: int, seed: i
         thr, nthr = find_thresholds_t(samp.double(), max_bins, categorical)
     thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
     nthr_t = torch.from_numpy(nthr).to(X.device)
+    before_binize()
     with _tr.span("tree.binize"):
         # the row-major copy (segment histograms' row gathers) comes out of the same kernel
         bins, rm = _binize_src(X, thr_t, nthr_t, want_rm=True, rm_layout="s10" if s10 else "std")
