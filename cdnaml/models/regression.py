@@ -685,14 +685,16 @@ def _early_side_work(num_trees, bootstrap, rate, want_label_max=True, codes_ok=F
             early["yf"] = K.float_with_absmax(y_, stream=side)
 
         def draws():
-            # queued right before the binning: the Poisson kernel (compute-bound) beside the memory-bound binning,
-            # not beside the quantile sample's sort, whose 1024-thread blocks it kept off the CUs (1.6 ms for a
-            # 0.3 ms kernel at 1e8 rows)
+            # queued right behind the quantile kernel, before the binning, on the MAIN stream (CDNAML_POISSON_STREAM
+            # =side: the side stream).  Measured at 1e8 rows (profiles/r4/prologue_ab.md): beside the quantile sort
+            # the draws kept its 1024-thread blocks off the CUs (2.1 ms for a 0.3 ms kernel); beside the binning --
+            # itself ~60 % VALU-bound (6-step threshold search) -- they slowed it by more than their own 2.2 ms;
+            # in series they cost exactly their 2.2 ms
             if bootstrap and num_trees > 1:
                 if codes_ok and K.POISSON_CODES:
                     # the draws written straight as the engine's row codes + their max (no uint8 weights, no
                     # codes_init pass, no separate max reduction over T x n bytes)
-                    with torch.cuda.stream(side):
+                    with torch.cuda.stream(side if K.POISSON_STREAM == "side" else torch.cuda.current_stream(dev)):
                         early["codes"] = K.BootstrapCodes(num_trees, n, seed_, off, rate, dev)
                 else:
                     early["w"] = _poisson_side(num_trees, n, seed_, off, rate, dev, join=False)

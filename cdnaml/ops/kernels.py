@@ -143,6 +143,9 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
 POISSON_CODES = __import__("os").environ.get("CDNAML_POISSON_CODES", "1") != "0"
 
 
+POISSON_STREAM = __import__("os").environ.get("CDNAML_POISSON_STREAM", "main")
+
+
 class BootstrapCodes:
     """Poisson bootstrap draws written straight as the tree engine's row codes (GPU): ``codes`` [T, n] int16
     (weight << 8 | 0, 0xFF for weight 0 -- codes_init's format) and the largest weight, copied to the host behind

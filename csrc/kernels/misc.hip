@@ -446,17 +446,18 @@ CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_
   // interior quads as dword stores when every tree row starts 4-byte aligned
   const int packed = (offset % 4 == 0) && (n % 4 == 0) &&
                      (codes ? reinterpret_cast<uintptr_t>(codes) % 8 == 0 : reinterpret_cast<uintptr_t>(out) % 4 == 0);
-  // A bounded grid (default 512 blocks over all trees, 2 per CU): the draws run on the side stream next to the
-  // quantile sample's latency-bound kernels, and a grid of T x 1024 blocks kept every CU full, so the sample's
-  // sort (100 blocks of 1024 threads) waited for whole CUs to drain: 2.1 ms instead of 0.3 ms at 1e8 rows.
+  // CDNAML_POISSON_BLOCKS > 0 bounds the grid (blocks over all trees) for runs beside other kernels: a grid of
+  // T x 1024 blocks keeps every CU full, so a co-running kernel of 1024-thread blocks (the quantile sort) waits
+  // for whole CUs to drain.  Default: unbounded (the engine queues the draws in series, profiles/r4/prologue_ab.md).
   static const int max_blocks = [] {
     const char* e = getenv("CDNAML_POISSON_BLOCKS");
-    const int v = e ? atoi(e) : 512;
-    return v > 0 ? v : 512;
+    return e ? atoi(e) : 0;
   }();
   unsigned gx = grid_for(n / 4 + 2, 256, 1024);
-  const unsigned cap = (unsigned)((max_blocks + T - 1) / T);
-  gx = gx < cap ? gx : (cap > 0 ? cap : 1u);
+  if (max_blocks > 0) {
+    const unsigned cap = (unsigned)((max_blocks + T - 1) / T);
+    gx = gx < cap ? gx : (cap > 0 ? cap : 1u);
+  }
   hipLaunchKernelGGL(poisson_kernel, dim3(gx, T), dim3(256), 0, st, out, T, n, seed, offset, rate, cdf, packed, codes,
                      wmax);
   return (int)hipGetLastError();
