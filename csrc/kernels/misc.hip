@@ -138,7 +138,10 @@ __global__ __launch_bounds__(256) void poisson_kernel(uint8_t* __restrict__ out,
       const unsigned v = (unsigned)__shfl_xor((int)m, off);
       m = v > m ? v : m;
     }
-    if ((threadIdx.x & 63) == 0 && m) atomicMax(wmax, m);
+    // most waves find the maximum already there: the read skips their atomic (T x 1024 blocks' worth of
+    // same-address atomics serialised in L2 -- ~0.6 ms of the 0.95 ms kernel at 1.25e7 rows x 20 trees)
+    if ((threadIdx.x & 63) == 0 && m && m > __hip_atomic_load(wmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(wmax, m);
   }
 }
 
@@ -446,12 +449,13 @@ CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_
   // interior quads as dword stores when every tree row starts 4-byte aligned
   const int packed = (offset % 4 == 0) && (n % 4 == 0) &&
                      (codes ? reinterpret_cast<uintptr_t>(codes) % 8 == 0 : reinterpret_cast<uintptr_t>(out) % 4 == 0);
-  // CDNAML_POISSON_BLOCKS > 0 bounds the grid (blocks over all trees) for runs beside other kernels: a grid of
-  // T x 1024 blocks keeps every CU full, so a co-running kernel of 1024-thread blocks (the quantile sort) waits
-  // for whole CUs to drain.  Default: unbounded (the engine queues the draws in series, profiles/r4/prologue_ab.md).
+  // CDNAML_POISSON_BLOCKS bounds the grid (blocks over all trees; default 2048 = 8 per CU, full occupancy):
+  // T x 1024 blocks of a dozen quads per thread at 1.25e7 rows paid more in block launches and wave-end atomics
+  // than in draws, and beside other kernels a full-chip grid keeps a co-running kernel of 1024-thread blocks
+  // (the quantile sort) waiting for whole CUs to drain.  <= 0: unbounded.
   static const int max_blocks = [] {
     const char* e = getenv("CDNAML_POISSON_BLOCKS");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2048;
   }();
   unsigned gx = grid_for(n / 4 + 2, 256, 1024);
   if (max_blocks > 0) {
