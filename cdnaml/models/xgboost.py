@@ -210,9 +210,11 @@ class _XgbEstimatorBase(Estimator):
                 with _tr.span("xgb.update_margin", round=m):
                     self._apply_l1(forest, t)
                     nodes, vals, masks = forest.binned_arrays(dev, t)
-                    col = F[:, k].contiguous()
-                    K.predict_binned_add(data.bins, nodes, 0, vals, masks, eta, col)
-                    F[:, k] = col
+                    col = F[:, k] if F[:, k].is_contiguous() else F[:, k].contiguous()
+                    K.predict_binned_add(data.bins, nodes, 0, vals, masks, eta, col,
+                                         bins_rm=data.bins_rm if dev.type == "cuda" else None)
+                    if col.data_ptr() != F[:, k].data_ptr():
+                        F[:, k] = col
             if val_mask is not None and metric_fn is not None:
                 v = metric_fn(F, val_mask)
                 history.append(v)
@@ -342,15 +344,21 @@ class _XgbModelBase(Model):
             self._dev[key] = (thr, torch.from_numpy(self._nthr).to(dev))
         thr, nthr = self._dev[key]
         Xf = X.float()
-        bins = K.binize(Xf, thr, nthr, missing=float(self.getMissing()))  # missing -> bin 0 inside the kernel
+        # missing -> bin 0 inside the kernel; the row-major copy (GPU) for the LDS-staged tree walks
+        rm = None
+        if dev.type == "cuda":
+            bins, rm = K.binize(Xf, thr, nthr, missing=float(self.getMissing()), want_rm=True)
+        else:
+            bins = K.binize(Xf, thr, nthr, missing=float(self.getMissing()))
         eta = self.getLearning_rate()
         F = torch.full((n, self._n_out), self._base, dtype=torch.float32, device=dev)
         for t in range(len(self._forest.roots)):
             nodes, vals, masks = self._forest.binned_arrays(dev, t)
             k = t % self._n_out
-            col = F[:, k].contiguous()
-            K.predict_binned_add(bins, nodes, 0, vals, masks, eta, col)
-            F[:, k] = col
+            col = F[:, k] if F[:, k].is_contiguous() else F[:, k].contiguous()
+            K.predict_binned_add(bins, nodes, 0, vals, masks, eta, col, bins_rm=rm)
+            if col.data_ptr() != F[:, k].data_ptr():
+                F[:, k] = col
         return F
 
     def _save_state(self):

@@ -1232,3 +1232,29 @@ def test_heap_predict_double_store(dev):
     a = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], 0.0)
     b = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], 0.0, dtype=torch.float64)
     assert b.dtype == torch.float64 and torch.equal(b, a.double())
+
+
+def test_predict_binned_rm_matches_column_major(dev):
+    """trees.hip predict_binned_rm (row-major bins, nodes in LDS, four walks per thread) adds the same fp32 leaf
+    values as the column-major walk, for every tree of a boosted model (missing-value bins included)."""
+    import cdnaml
+    from cdnaml.models.xgboost import XgboostRegressor
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator(device=dev).manual_seed(4)
+    n = 30011
+    X = torch.randn((n, 20), generator=g, device=dev)
+    X[::7, 3] = float("nan")
+    y = (X[:, 0].nan_to_num() * 2 + X[:, 1] * X[:, 2]).double()
+    m = XgboostRegressor(n_estimators=6, max_depth=6, learning_rate=0.3).fit(
+        spark.createDataFrameFromLocalTensors({"features": X, "label": y}))
+    thr = torch.from_numpy(m._thr.astype(np.float32)).to(dev)
+    nthr = torch.from_numpy(m._nthr).to(dev)
+    bins, rm = K.binize(X, thr, nthr, missing=float(m.getMissing()), want_rm=True)
+    assert rm is not None
+    a = torch.zeros(n, dtype=torch.float32, device=dev)
+    b = torch.zeros(n, dtype=torch.float32, device=dev)
+    for t in range(len(m._forest.roots)):
+        nodes, vals, masks = m._forest.binned_arrays(dev, t)
+        K.predict_binned_add(bins, nodes, 0, vals, masks, 0.3, a)
+        K.predict_binned_add(bins, nodes, 0, vals, masks, 0.3, b, bins_rm=rm)
+    assert torch.equal(a, b)
