@@ -211,8 +211,7 @@ class _XgbEstimatorBase(Estimator):
                     self._apply_l1(forest, t)
                     nodes, vals, masks = forest.binned_arrays(dev, t)
                     col = F[:, k] if F[:, k].is_contiguous() else F[:, k].contiguous()
-                    K.predict_binned_add(data.bins, nodes, 0, vals, masks, eta, col,
-                                         bins_rm=data.bins_rm if dev.type == "cuda" else None)
+                    K.predict_binned_add(data.bins, nodes, 0, vals, masks, eta, col)
                     if col.data_ptr() != F[:, k].data_ptr():
                         F[:, k] = col
             if val_mask is not None and metric_fn is not None:
@@ -344,19 +343,14 @@ class _XgbModelBase(Model):
             self._dev[key] = (thr, torch.from_numpy(self._nthr).to(dev))
         thr, nthr = self._dev[key]
         Xf = X.float()
-        # missing -> bin 0 inside the kernel; the row-major copy (GPU) for the LDS-staged tree walks
-        rm = None
-        if dev.type == "cuda":
-            bins, rm = K.binize(Xf, thr, nthr, missing=float(self.getMissing()), want_rm=True)
-        else:
-            bins = K.binize(Xf, thr, nthr, missing=float(self.getMissing()))
+        bins = K.binize(Xf, thr, nthr, missing=float(self.getMissing()))  # missing -> bin 0 inside the kernel
         eta = self.getLearning_rate()
         F = torch.full((n, self._n_out), self._base, dtype=torch.float32, device=dev)
         for t in range(len(self._forest.roots)):
             nodes, vals, masks = self._forest.binned_arrays(dev, t)
             k = t % self._n_out
             col = F[:, k] if F[:, k].is_contiguous() else F[:, k].contiguous()
-            K.predict_binned_add(bins, nodes, 0, vals, masks, eta, col, bins_rm=rm)
+            K.predict_binned_add(bins, nodes, 0, vals, masks, eta, col)
             if col.data_ptr() != F[:, k].data_ptr():
                 F[:, k] = col
         return F

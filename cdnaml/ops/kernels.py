@@ -1125,15 +1125,13 @@ def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree
     return out
 
 
-PREDICT_BINNED_RM = __import__("os").environ.get("CDNAML_PREDICT_BINNED_RM", "1") != "0"
+PREDICT_BINNED_LDS = __import__("os").environ.get("CDNAML_PREDICT_BINNED_LDS", "1") != "0"
 
 
 def predict_binned_add(bins: torch.Tensor, nodes: torch.Tensor, root: int, values: torch.Tensor,
-                       masks: torch.Tensor, scale: float, out: torch.Tensor,
-                       bins_rm: Optional[torch.Tensor] = None) -> None:
-    """out[r] += scale * leaf value of a bin-threshold tree (GBDT margin update).
-
-    bins_rm: the row-major copy [n, Gs, 8] (GPU): walked with the nodes in LDS (trees.hip predict_binned_rm)."""
+                       masks: torch.Tensor, scale: float, out: torch.Tensor) -> None:
+    """out[r] += scale * leaf value of a bin-threshold tree (GBDT margin update); GPU: the tree staged in LDS,
+    four walks per thread (trees.hip predict_binned_lds_kernel)."""
     G, n, _ = bins.shape
     if n == 0:
         return
@@ -1142,12 +1140,10 @@ def predict_binned_add(bins: torch.Tensor, nodes: torch.Tensor, root: int, value
         nodes, values = nodes.int().contiguous(), values.float().contiguous()
         assert out.dtype == torch.float32 and out.is_contiguous()
         nn = int(nodes.shape[0])
-        if (PREDICT_BINNED_RM and bins_rm is not None and bins_rm.is_contiguous() and bins_rm.shape[0] == n and
-                bins_rm.shape[1] >= G and 0 < nn <= 8192):
-            rb = bins_rm.shape[1] * bins_rm.shape[2]
-            _lib.check(_lib.lib().cdna_predict_binned_add_rm(_ptr(bins_rm), rb, n, _ptr(nodes), nn, int(root),
-                                                             _ptr(values), _ptr(m), float(scale), _ptr(out),
-                                                             _stream(bins.device)), "cdna_predict_binned_add_rm")
+        if PREDICT_BINNED_LDS and 0 < nn <= 8192:
+            _lib.check(_lib.lib().cdna_predict_binned_add_lds(_ptr(bins), n, _ptr(nodes), nn, int(root),
+                                                              _ptr(values), _ptr(m), float(scale), _ptr(out),
+                                                              _stream(bins.device)), "cdna_predict_binned_add_lds")
             return
         _lib.check(_lib.lib().cdna_predict_binned_add(_ptr(bins), n, _ptr(nodes), int(root), _ptr(values), _ptr(m),
                                                       float(scale), _ptr(out), _stream(bins.device)),

@@ -853,19 +853,20 @@ __global__ __launch_bounds__(256) void predict_binned_kernel(const uint64_t* __r
   }
 }
 
-// predict_binned_kernel on the row-major bins copy [n][rb bytes] with the tree's nodes staged in LDS: a row's
-// bytes share one or two cache lines, so after the first split the walk reads from L1 / L2 instead of a new plane
-// of the column-major bins per level, the node table costs an LDS read instead of a dependent global load, and
-// four rows per thread keep four walks in flight (the column-major kernel: 16 dependent global loads per row at
-// depth 8, 2.37 ms per boosting round at 1e8 rows).  Same leaves, same fp32 update as predict_binned_kernel.
-__global__ __launch_bounds__(256) void predict_binned_rm_kernel(const uint8_t* __restrict__ rm, int64_t rb, int64_t n,
-                                                                const int4* __restrict__ nodes, int nn, int root,
-                                                                const float* __restrict__ values,
-                                                                const uint32_t* __restrict__ masks, float scale,
-                                                                float* __restrict__ out) {
+// predict_binned_kernel with the tree's nodes staged in LDS and four rows per thread: the node table costs an LDS
+// read instead of a dependent global load, and four walks are in flight per thread (the one-row kernel: 16
+// dependent global loads per row at depth 8, 2.37 ms per boosting round at 1e8 rows).  The bins stay
+// column-major: a wave's rows at one node read one plane contiguously (a row-major walk -- one cache line per
+// lane per level -- measured 14 ms).  Same leaves, same fp32 update as predict_binned_kernel.
+__global__ __launch_bounds__(256) void predict_binned_lds_kernel(const uint64_t* __restrict__ bins, int64_t n,
+                                                                 const int4* __restrict__ nodes, int nn, int root,
+                                                                 const float* __restrict__ values,
+                                                                 const uint32_t* __restrict__ masks, float scale,
+                                                                 float* __restrict__ out) {
   extern __shared__ int4 snd[];
   for (int i = threadIdx.x; i < nn; i += 256) snd[i] = nodes[i];
   __syncthreads();
+  const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bins);
   constexpr int R = 4;
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t r0 = (int64_t)blockIdx.x * 256 + threadIdx.x; r0 < n; r0 += stride * R) {
@@ -884,7 +885,7 @@ __global__ __launch_bounds__(256) void predict_binned_rm_kernel(const uint8_t* _
         bin[u] = 0;
         if (live[u] && nv[u].x != -1) {
           const int f = nv[u].x >= 0 ? nv[u].x : -nv[u].x - 2;
-          bin[u] = rm[(r0 + u * stride) * rb + f];
+          bin[u] = b8[((int64_t)(f >> 3) * n + r0 + u * stride) * 8 + (f & 7)];
           any = true;
         }
       }
@@ -1070,17 +1071,17 @@ CDNA_API int cdna_predict_binned_add(const uint64_t* bins, int64_t n, const int4
   return (int)hipGetLastError();
 }
 
-// rm: row-major bins [n][rb] bytes; nodes [nn] staged in LDS (nn <= 8192).
-CDNA_API int cdna_predict_binned_add_rm(const uint8_t* rm, int64_t rb, int64_t n, const int4* nodes, int nn, int root,
-                                        const float* values, const uint32_t* masks, float scale, float* out,
-                                        hipStream_t st) {
+// nodes [nn] staged in LDS (nn <= 8192).
+CDNA_API int cdna_predict_binned_add_lds(const uint64_t* bins, int64_t n, const int4* nodes, int nn, int root,
+                                         const float* values, const uint32_t* masks, float scale, float* out,
+                                         hipStream_t st) {
   if (n <= 0) return 0;
-  if (nn <= 0 || nn > 8192 || root < 0 || root >= nn || rb <= 0) return (int)hipErrorInvalidValue;
+  if (nn <= 0 || nn > 8192 || root < 0 || root >= nn) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)nn * sizeof(int4);
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(predict_binned_rm_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(predict_binned_lds_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(predict_binned_rm_kernel, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), lds, st, rm, rb, n,
+  hipLaunchKernelGGL(predict_binned_lds_kernel, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), lds, st, bins, n,
                      nodes, nn, root, values, masks, scale, out);
   return (int)hipGetLastError();
 }

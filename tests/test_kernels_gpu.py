@@ -1234,9 +1234,9 @@ def test_heap_predict_double_store(dev):
     assert b.dtype == torch.float64 and torch.equal(b, a.double())
 
 
-def test_predict_binned_rm_matches_column_major(dev):
-    """trees.hip predict_binned_rm (row-major bins, nodes in LDS, four walks per thread) adds the same fp32 leaf
-    values as the column-major walk, for every tree of a boosted model (missing-value bins included)."""
+def test_predict_binned_lds_matches_one_row_walk(dev, monkeypatch):
+    """trees.hip predict_binned_lds (nodes in LDS, four walks per thread) adds the same fp32 leaf values as the
+    one-row walk with global node loads, for every tree of a boosted model (missing-value bins included)."""
     import cdnaml
     from cdnaml.models.xgboost import XgboostRegressor
     spark = cdnaml.SparkSession.builder.getOrCreate()
@@ -1249,12 +1249,13 @@ def test_predict_binned_rm_matches_column_major(dev):
         spark.createDataFrameFromLocalTensors({"features": X, "label": y}))
     thr = torch.from_numpy(m._thr.astype(np.float32)).to(dev)
     nthr = torch.from_numpy(m._nthr).to(dev)
-    bins, rm = K.binize(X, thr, nthr, missing=float(m.getMissing()), want_rm=True)
-    assert rm is not None
+    bins = K.binize(X, thr, nthr, missing=float(m.getMissing()))
     a = torch.zeros(n, dtype=torch.float32, device=dev)
     b = torch.zeros(n, dtype=torch.float32, device=dev)
     for t in range(len(m._forest.roots)):
         nodes, vals, masks = m._forest.binned_arrays(dev, t)
+        monkeypatch.setattr(K, "PREDICT_BINNED_LDS", False)
         K.predict_binned_add(bins, nodes, 0, vals, masks, 0.3, a)
-        K.predict_binned_add(bins, nodes, 0, vals, masks, 0.3, b, bins_rm=rm)
+        monkeypatch.setattr(K, "PREDICT_BINNED_LDS", True)
+        K.predict_binned_add(bins, nodes, 0, vals, masks, 0.3, b)
     assert torch.equal(a, b)
