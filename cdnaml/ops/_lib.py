@@ -207,8 +207,6 @@ _SIGS = {
                            c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p], c_int),
     "cdna_tree_predict_heap": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                                 c_float, c_void_p, c_void_p, c_void_p], c_int),
-    "cdna_predict_binned_add_lds": ([c_void_p, c_int64, c_void_p, c_int, c_int, c_void_p, c_void_p, c_float,
-                                     c_void_p, c_void_p], c_int),
     "cdna_predict_binned_add": ([c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p,
                                  c_void_p], c_int),
     "cdna_uniform": ([c_void_p, c_int64, c_uint64, c_uint64, c_uint32, c_void_p], c_int),

@@ -1125,13 +1125,12 @@ def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree
     return out
 
 
-PREDICT_BINNED_LDS = __import__("os").environ.get("CDNAML_PREDICT_BINNED_LDS", "1") != "0"
-
-
 def predict_binned_add(bins: torch.Tensor, nodes: torch.Tensor, root: int, values: torch.Tensor,
                        masks: torch.Tensor, scale: float, out: torch.Tensor) -> None:
-    """out[r] += scale * leaf value of a bin-threshold tree (GBDT margin update); GPU: the tree staged in LDS,
-    four walks per thread (trees.hip predict_binned_lds_kernel)."""
+    """out[r] += scale * leaf value of a bin-threshold tree (GBDT margin update).
+
+    (A/B, profiles/r4/gbdt_predict_ab.md: the tree in LDS with four walks per thread measured 3.16 ms and a
+    row-major walk 14 ms against this kernel's 2.37 ms per round at 1e8 rows; both dropped.)"""
     G, n, _ = bins.shape
     if n == 0:
         return
@@ -1139,12 +1138,6 @@ def predict_binned_add(bins: torch.Tensor, nodes: torch.Tensor, root: int, value
         m = masks.int().contiguous() if masks.numel() else torch.zeros(8, dtype=torch.int32, device=bins.device)
         nodes, values = nodes.int().contiguous(), values.float().contiguous()
         assert out.dtype == torch.float32 and out.is_contiguous()
-        nn = int(nodes.shape[0])
-        if PREDICT_BINNED_LDS and 0 < nn <= 8192:
-            _lib.check(_lib.lib().cdna_predict_binned_add_lds(_ptr(bins), n, _ptr(nodes), nn, int(root),
-                                                              _ptr(values), _ptr(m), float(scale), _ptr(out),
-                                                              _stream(bins.device)), "cdna_predict_binned_add_lds")
-            return
         _lib.check(_lib.lib().cdna_predict_binned_add(_ptr(bins), n, _ptr(nodes), int(root), _ptr(values), _ptr(m),
                                                       float(scale), _ptr(out), _stream(bins.device)),
                    "cdna_predict_binned_add")

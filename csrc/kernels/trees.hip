@@ -853,58 +853,6 @@ __global__ __launch_bounds__(256) void predict_binned_kernel(const uint64_t* __r
   }
 }
 
-// predict_binned_kernel with the tree's nodes staged in LDS and four rows per thread: the node table costs an LDS
-// read instead of a dependent global load, and four walks are in flight per thread (the one-row kernel: 16
-// dependent global loads per row at depth 8, 2.37 ms per boosting round at 1e8 rows).  The bins stay
-// column-major: a wave's rows at one node read one plane contiguously (a row-major walk -- one cache line per
-// lane per level -- measured 14 ms).  Same leaves, same fp32 update as predict_binned_kernel.
-__global__ __launch_bounds__(256) void predict_binned_lds_kernel(const uint64_t* __restrict__ bins, int64_t n,
-                                                                 const int4* __restrict__ nodes, int nn, int root,
-                                                                 const float* __restrict__ values,
-                                                                 const uint32_t* __restrict__ masks, float scale,
-                                                                 float* __restrict__ out) {
-  extern __shared__ int4 snd[];
-  for (int i = threadIdx.x; i < nn; i += 256) snd[i] = nodes[i];
-  __syncthreads();
-  const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bins);
-  constexpr int R = 4;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t r0 = (int64_t)blockIdx.x * 256 + threadIdx.x; r0 < n; r0 += stride * R) {
-    int4 nv[R];
-    bool live[R];
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      live[u] = r0 + u * stride < n;
-      nv[u] = snd[root];
-    }
-    for (int step = 0; step < 64; ++step) {  // depth <= 63: every walk ends (leaf x == -1) well before
-      bool any = false;
-      int bin[R];
-#pragma unroll
-      for (int u = 0; u < R; ++u) {
-        bin[u] = 0;
-        if (live[u] && nv[u].x != -1) {
-          const int f = nv[u].x >= 0 ? nv[u].x : -nv[u].x - 2;
-          bin[u] = b8[((int64_t)(f >> 3) * n + r0 + u * stride) * 8 + (f & 7)];
-          any = true;
-        }
-      }
-      if (!any) break;
-#pragma unroll
-      for (int u = 0; u < R; ++u) {
-        if (!(live[u] && nv[u].x != -1)) continue;
-        const bool left = nv[u].x >= 0 ? bin[u] <= nv[u].y
-                                       : ((masks[nv[u].y * 8 + (bin[u] >> 5)] >> (bin[u] & 31)) & 1u) != 0u;
-        const int nd = left ? nv[u].z : nv[u].w;
-        nv[u] = snd[nd < 0 ? 0 : (nd >= nn ? nn - 1 : nd)];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < R; ++u)
-      if (live[u]) out[r0 + u * stride] += scale * values[nv[u].y];
-  }
-}
-
 inline unsigned grid_for(int64_t n, int per, unsigned cap) {
   int64_t g = (n + per - 1) / per;
   if (g < 1) g = 1;
@@ -1068,21 +1016,6 @@ CDNA_API int cdna_predict_binned_add(const uint64_t* bins, int64_t n, const int4
   if (n <= 0) return 0;
   hipLaunchKernelGGL(predict_binned_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, bins, n, nodes, root,
                      values, masks, scale, out);
-  return (int)hipGetLastError();
-}
-
-// nodes [nn] staged in LDS (nn <= 8192).
-CDNA_API int cdna_predict_binned_add_lds(const uint64_t* bins, int64_t n, const int4* nodes, int nn, int root,
-                                         const float* values, const uint32_t* masks, float scale, float* out,
-                                         hipStream_t st) {
-  if (n <= 0) return 0;
-  if (nn <= 0 || nn > 8192 || root < 0 || root >= nn) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)nn * sizeof(int4);
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(predict_binned_lds_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(predict_binned_lds_kernel, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), lds, st, bins, n,
-                     nodes, nn, root, values, masks, scale, out);
   return (int)hipGetLastError();
 }
 

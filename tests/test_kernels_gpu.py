@@ -1233,29 +1233,3 @@ def test_heap_predict_double_store(dev):
     b = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], 0.0, dtype=torch.float64)
     assert b.dtype == torch.float64 and torch.equal(b, a.double())
 
-
-def test_predict_binned_lds_matches_one_row_walk(dev, monkeypatch):
-    """trees.hip predict_binned_lds (nodes in LDS, four walks per thread) adds the same fp32 leaf values as the
-    one-row walk with global node loads, for every tree of a boosted model (missing-value bins included)."""
-    import cdnaml
-    from cdnaml.models.xgboost import XgboostRegressor
-    spark = cdnaml.SparkSession.builder.getOrCreate()
-    g = torch.Generator(device=dev).manual_seed(4)
-    n = 30011
-    X = torch.randn((n, 20), generator=g, device=dev)
-    X[::7, 3] = float("nan")
-    y = (X[:, 0].nan_to_num() * 2 + X[:, 1] * X[:, 2]).double()
-    m = XgboostRegressor(n_estimators=6, max_depth=6, learning_rate=0.3).fit(
-        spark.createDataFrameFromLocalTensors({"features": X, "label": y}))
-    thr = torch.from_numpy(m._thr.astype(np.float32)).to(dev)
-    nthr = torch.from_numpy(m._nthr).to(dev)
-    bins = K.binize(X, thr, nthr, missing=float(m.getMissing()))
-    a = torch.zeros(n, dtype=torch.float32, device=dev)
-    b = torch.zeros(n, dtype=torch.float32, device=dev)
-    for t in range(len(m._forest.roots)):
-        nodes, vals, masks = m._forest.binned_arrays(dev, t)
-        monkeypatch.setattr(K, "PREDICT_BINNED_LDS", False)
-        K.predict_binned_add(bins, nodes, 0, vals, masks, 0.3, a)
-        monkeypatch.setattr(K, "PREDICT_BINNED_LDS", True)
-        K.predict_binned_add(bins, nodes, 0, vals, masks, 0.3, b)
-    assert torch.equal(a, b)
