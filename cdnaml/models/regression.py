@@ -152,13 +152,13 @@ def _lr_shift(Xk: torch.Tensor, yk: torch.Tensor, comm, d: int) -> torch.Tensor:
     copy of the same values."""
     k = Xk.shape[0]
     if comm.distributed:
-        sh = torch.cat([Xk.double().mean(0), yk.double().mean().reshape(1)]) if k else \
+        sh = torch.cat([torch.mean(Xk, 0, dtype=torch.float64), yk.double().mean().reshape(1)]) if k else \
             torch.zeros(d + 1, dtype=torch.float64, device=Xk.device)
         cnt = torch.full((1,), 1.0 if k else 0.0, dtype=torch.float64, device=Xk.device)
         comm.all_reduce_many([sh, cnt])
         return sh / cnt.clamp_min(1.0)
-    # one rank: one reduction, no all-reduce bookkeeping
-    return torch.cat([Xk, yk[:, None].to(Xk.dtype)], 1).double().mean(0) if k else \
+    # one rank: fp64-accumulated column means of the fp32 rows (no fp64 copy of the block), no all-reduce
+    return torch.cat([torch.mean(Xk, 0, dtype=torch.float64), yk.double().mean().reshape(1)]) if k else \
         torch.zeros(d + 1, dtype=torch.float64, device=Xk.device)
 
 
@@ -211,12 +211,13 @@ class LinearRegression(Estimator):
         # the device (the label shift is applied to y there), so the fit reads the host once, for the Gram
         bf16 = self.getGramPrecision() == "bf16"
         fp64 = _gram_fp64(self.getGramPrecision(), X.shape[0], d + (1 if w is not None else 0))
-        sh = None
+        sh = shift = None
+        yc = y
         if fit_int:
             sh = _lr_shift(X[:4096], y[:4096], comm, d)
-            shift, yc = sh[:d].float(), y - sh[d]
-        else:
-            shift, yc = None, y
+            shift = sh[:d].float()
+            # y - mean in fp64, rounded to fp32, in one pass (the Gram reads the fp32 label)
+            yc = K.shifted_f32(y, sh[d:]) if y.is_cuda else y - sh[d]
         if w is None:
             G = K.gram(X, yc, shift, 0.0, bf16=bf16, fp64=fp64) if X.shape[0] else \
                 torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)

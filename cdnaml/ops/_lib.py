@@ -212,7 +212,7 @@ _SIGS = {
     "cdna_uniform": ([c_void_p, c_int64, c_uint64, c_uint64, c_uint32, c_void_p], c_int),
     "cdna_sample_rows": ([c_int64, c_uint64, c_uint64, c_uint32, c_double, c_void_p, c_int64, c_void_p, c_void_p],
                          c_int),
-    "cdna_cast_absmax": ([c_void_p, c_int64, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_cast_absmax": ([c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_normal_f32": ([c_void_p, c_int64, c_uint64, c_uint64, c_uint32, c_void_p], c_int),
     "cdna_poisson": ([c_void_p, c_int, c_int64, c_uint64, c_uint64, c_double, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_reg_metrics": ([c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p], c_int),

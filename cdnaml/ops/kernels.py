@@ -461,13 +461,27 @@ def float_with_absmax(t: torch.Tensor, stream=None) -> torch.Tensor:
     with torch.cuda.stream(st):
         out = torch.empty(t.shape, dtype=torch.float32, device=t.device)
         bits = torch.empty(1, dtype=torch.int32, device=t.device)
-        rc = _lib.lib().cdna_cast_absmax(_ptr(t), t.numel(), _ptr(out), _ptr(bits), st.cuda_stream)
+        rc = _lib.lib().cdna_cast_absmax(_ptr(t), t.numel(), _ptr(out), _ptr(bits), None, st.cuda_stream)
         if rc == 1:  # misaligned view: the torch passes
             out = t.float()
             prefetch_max(out, absval=True, stream=st)
             return out
         _lib.check(rc, "cdna_cast_absmax")
         setattr(out, "_cdna_absmax", _PendingScalar(bits.view(torch.float32), st))
+    return out
+
+
+def shifted_f32(t: torch.Tensor, shift: torch.Tensor) -> torch.Tensor:
+    """``(t - shift).float()`` of a contiguous fp64 device column, ``shift`` a one-element fp64 device tensor: one
+    pass (misc.hip cast_absmax_kernel with its shift operand), the subtraction in fp64 before the rounding."""
+    if not (_native(t) and t.dtype == torch.float64 and t.dim() == 1 and t.is_contiguous() and t.numel()):
+        return (t - shift.double()).float()
+    sd = shift.double().reshape(1).contiguous()
+    out = torch.empty(t.shape, dtype=torch.float32, device=t.device)
+    rc = _lib.lib().cdna_cast_absmax(_ptr(t), t.numel(), _ptr(out), None, _ptr(sd), _stream(t.device))
+    if rc == 1:  # misaligned view
+        return (t - sd).float()
+    _lib.check(rc, "cdna_cast_absmax(shift)")
     return out
 
 

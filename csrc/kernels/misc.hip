@@ -499,37 +499,46 @@ CDNA_API int cdna_sample_rows(int64_t n, uint64_t seed, uint64_t offset, uint32_
   return (int)hipGetLastError();
 }
 
-// fp32 copy of an fp64 column and max |x| as fp32 bits (atomicMax on the int bits: non-negative floats order
-// as their bit patterns, and a NaN's (0x7FC00000) beats +inf, so a NaN label surfaces as a NaN maximum).
-// One pass for the forest's label (y.float() + |y|.max() were three full passes).  *amax is zeroed here.
+// fp32 copy of an fp64 column (minus an optional fp64 device shift, subtracted before the rounding) and,
+// when amax is given, max |result| as fp32 bits (atomicMax on the int bits: non-negative floats order as their
+// bit patterns, and a NaN's (0x7FC00000) beats +inf, so a NaN label surfaces as a NaN maximum).  One pass for
+// the forest's label (y.float() + |y|.max() were three full passes) and for the linear fit's shifted label
+// (y - mean, then .float(): two).  *amax is zeroed here.
 __global__ __launch_bounds__(256) void cast_absmax_kernel(const double* __restrict__ x, int64_t n,
-                                                          float* __restrict__ out, int* __restrict__ amax) {
+                                                          float* __restrict__ out, int* __restrict__ amax,
+                                                          const double* __restrict__ shift) {
   int m = 0;
+  const double sh = shift ? shift[0] : 0.0;
   const int64_t n2 = n / 2;
   for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n2; q += (int64_t)gridDim.x * 256) {
     const double2 v = reinterpret_cast<const double2*>(x)[q];
-    const float a = (float)v.x, b = (float)v.y;
+    const float a = (float)(v.x - sh), b = (float)(v.y - sh);
     reinterpret_cast<float2*>(out)[q] = float2{a, b};
     const int ia = __float_as_int(a) & 0x7FFFFFFF, ib = __float_as_int(b) & 0x7FFFFFFF;
     m = max(m, max(ia, ib));
   }
   for (int64_t i = 2 * n2 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float a = (float)x[i];
+    const float a = (float)(x[i] - sh);
     out[i] = a;
     m = max(m, __float_as_int(a) & 0x7FFFFFFF);
   }
+  if (!amax) return;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0 && m > 0) atomicMax(amax, m);
 }
 
-CDNA_API int cdna_cast_absmax(const double* x, int64_t n, float* out, int* amax, hipStream_t st) {
-  if (!amax) return (int)hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(amax, 0, sizeof(int), st);
-  if (e != hipSuccess || n <= 0) return (int)e;
+CDNA_API int cdna_cast_absmax(const double* x, int64_t n, float* out, int* amax, const double* shift,
+                              hipStream_t st) {
+  if (amax) {
+    hipError_t e = hipMemsetAsync(amax, 0, sizeof(int), st);
+    if (e != hipSuccess) return (int)e;
+  }
+  if (n <= 0) return 0;
   if (reinterpret_cast<uintptr_t>(x) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 8 != 0)
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(cast_absmax_kernel, dim3(grid_for(n / 2 + 1, 256, 512)), dim3(256), 0, st, x, n, out, amax);
+  hipLaunchKernelGGL(cast_absmax_kernel, dim3(grid_for(n / 2 + 1, 256, 512)), dim3(256), 0, st, x, n, out, amax,
+                     shift);
   return (int)hipGetLastError();
 }
 

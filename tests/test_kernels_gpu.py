@@ -1233,3 +1233,12 @@ def test_heap_predict_double_store(dev):
     b = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], 0.0, dtype=torch.float64)
     assert b.dtype == torch.float64 and torch.equal(b, a.double())
 
+
+
+def test_shifted_f32(dev):
+    """misc.hip cast_absmax_kernel with a device shift: (y - s).float() with the subtraction in fp64 (odd length:
+    the scalar tail)."""
+    g = torch.Generator(device=dev).manual_seed(6)
+    y = 1e5 + torch.randn(100_001, generator=g, device=dev, dtype=torch.float64) * 3
+    s = y[:1024].mean().reshape(1)
+    assert torch.equal(K.shifted_f32(y, s), (y - s).float())
