@@ -266,8 +266,8 @@ class ChunkedRows:
 
 def _global_sample(session, X, max_bins: int, seed: int, row_offset: int, n_global: int):
     """Rows sampled by Philox keyed on the GLOBAL row id (the same rows whatever the GPU count), gathered
-    from every rank: the split-candidate sample.  ``X`` may be a :class:`ChunkedRows` stream (the same rows,
-    sampled chunk by chunk)."""
+    from every rank: the split-candidate sample (a row set: its order is not defined).  ``X`` may be a
+    :class:`ChunkedRows` stream (the same rows, sampled chunk by chunk)."""
     comm = session.comm
     n = X.shape[0]
     target = max(max_bins * max_bins, 10000)
@@ -282,7 +282,10 @@ def _global_sample(session, X, max_bins: int, seed: int, row_offset: int, n_glob
                 parts.append(Xc.float().clone())
         samp = torch.cat(parts) if parts else torch.zeros((0, X.d), dtype=torch.float32, device=X.device)
     elif frac < 1.0:
-        idx = K.sample_rows(n, seed ^ 0x5BD1E995, row_offset, 3, frac, X.device) if X.is_cuda and n else None
+        # the quantile thresholds depend on the sample's values only (each column is sorted): the rows are
+        # gathered in the kernel's arbitrary order, no sort of the ids
+        idx = K.sample_rows(n, seed ^ 0x5BD1E995, row_offset, 3, frac, X.device, ordered=False) \
+            if X.is_cuda and n else None
         if idx is None:
             u = K.uniform(n, seed ^ 0x5BD1E995, row_offset, 3, device=X.device)
             idx = K.compact_mask(u < frac)

@@ -485,10 +485,11 @@ def shifted_f32(t: torch.Tensor, shift: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def sample_rows(n: int, seed: int, offset: int, stream: int, frac: float, device) -> Optional[torch.Tensor]:
-    """Sorted int64 ids of the rows r < n with ``uniform(n, seed, offset, stream)[r] < frac`` (one fused kernel;
-    == compact_mask(uniform(...) < frac)).  None when the count passes the capacity sized from the expected
-    count (the caller then takes the materialised path)."""
+def sample_rows(n: int, seed: int, offset: int, stream: int, frac: float, device,
+                ordered: bool = True) -> Optional[torch.Tensor]:
+    """int64 ids of the rows r < n with ``uniform(n, seed, offset, stream)[r] < frac`` (one fused kernel; the set
+    of compact_mask(uniform(...) < frac), in arbitrary order unless ``ordered``).  None when the count passes the
+    capacity sized from the expected count (the caller then takes the materialised path)."""
     seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     exp_ = n * frac
     cap = int(exp_ + 12.0 * math.sqrt(exp_ + 1.0) + 1024)
@@ -499,7 +500,7 @@ def sample_rows(n: int, seed: int, offset: int, stream: int, frac: float, device
     c = int(cnt.item())
     if c > cap:
         return None
-    return torch.sort(idx[:c]).values
+    return torch.sort(idx[:c]).values if ordered else idx[:c]
 
 
 def prefetch_max(t: torch.Tensor, absval: bool = False, stream=None) -> None:

@@ -11,26 +11,71 @@
 // chain of ~20 small torch ops (each a launch, 1.4 ms of launch gaps per fit).
 // The sorted column is also written out so the host can run the categorical /
 // few-distinct-values path on the features that need it.
+//
+// Sort: when the column is exactly fp32 (the engine's samples are rows of the fp32 feature matrix) and holds at
+// most kQRadixS values, a rocPRIM block radix sort of 32-bit keys held 12 per thread in registers (4 passes of
+// 8 bits) replaces the 105-stage LDS bitonic network over fp64 (275 us -> see profiles/r4/prologue_ab.md at the
+// 1e4-row sample of the headline); otherwise the bitonic path.  Both give the same sorted values (-0.0 / +0.0
+// aside, which compare equal everywhere downstream).
 #include "common.h"
+#include <rocprim/block/block_radix_sort.hpp>
 
 namespace {
 
 constexpr int kQThreads = 1024;
 constexpr int kQMaxS = 16384;
+constexpr int kQItems = 12;
+constexpr int kQRadixS = kQThreads * kQItems;  // 12288
+using QRadixSort = rocprim::block_radix_sort<float, kQThreads, kQItems>;
 
 __device__ __forceinline__ double nan_to_inf(double v) { return v != v ? __builtin_inf() : v; }
 
+// RADIX: the caller checked s <= kQRadixS; a block whose column is not exactly fp32 still takes the bitonic path
+// (then the dynamic LDS must hold P doubles: the launcher sizes it for both).
+template <bool RADIX>
 __global__ __launch_bounds__(kQThreads) void quantile_kernel(const double* __restrict__ samp, int s, int d,
                                                              int max_bins, double* __restrict__ sorted,
                                                              double* __restrict__ thr, int* __restrict__ nthr,
                                                              int* __restrict__ kdist) {
-  extern __shared__ double sv[];  // [P]
+  extern __shared__ double sv[];  // [P] (radix: the sort's storage first, then [s] sorted values)
   __shared__ int red_nn[kQThreads / 64], red_k[kQThreads / 64];
   __shared__ double cand[256];
   const int f = blockIdx.x;
   int P = 1;
   while (P < s) P <<= 1;
   int nn_loc = 0;
+  bool sorted_ok = false;
+  if (RADIX) {
+    float key[kQItems];
+    int inexact = 0;
+#pragma unroll
+    for (int j = 0; j < kQItems; ++j) {
+      const int i = (int)threadIdx.x * kQItems + j;  // blocked: thread t holds values [12 t, 12 t + 12)
+      float v = __builtin_inff();
+      if (i < s) {
+        const double x = samp[(int64_t)i * d + f];
+        nn_loc += x == x;
+        const double xi = nan_to_inf(x);
+        v = (float)xi;
+        inexact |= (double)v != xi;
+      }
+      key[j] = v;
+    }
+    if (!__syncthreads_or(inexact)) {
+      QRadixSort().sort(key, *reinterpret_cast<typename QRadixSort::storage_type*>(sv));
+      __syncthreads();  // the storage is reused as sv below
+#pragma unroll
+      for (int j = 0; j < kQItems; ++j) {
+        const int i = (int)threadIdx.x * kQItems + j;
+        if (i < s) sv[i] = (double)key[j];
+      }
+      __syncthreads();
+      sorted_ok = true;
+    } else {
+      nn_loc = 0;  // recounted by the bitonic path's load
+    }
+  }
+  if (!sorted_ok) {
   for (int i = threadIdx.x; i < P; i += kQThreads) {
     double v = __builtin_inf();
     if (i < s) {
@@ -58,6 +103,7 @@ __global__ __launch_bounds__(kQThreads) void quantile_kernel(const double* __res
       __syncthreads();
     }
   }
+  }  // bitonic path
   // nn and the distinct count over the first nn (non-NaN) sorted values
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int v_nn = nn_loc;
@@ -133,11 +179,20 @@ CDNA_API int cdna_quantile_thresholds(const double* samp, int s, int d, int max_
   if (s > kQMaxS || max_bins < 2 || max_bins > 257) return (int)hipErrorInvalidValue;
   int P = 1;
   while (P < s) P <<= 1;
-  const size_t lds = (size_t)P * sizeof(double);
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(quantile_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(quantile_kernel, dim3(d), dim3(kQThreads), lds, st, samp, s, d, max_bins, sorted, thr, nthr,
-                     kdist);
+  static const bool radix_on = [] {
+    const char* e = getenv("CDNAML_QUANTILE_RADIX");
+    return !e || atoi(e) != 0;
+  }();
+  const bool radix = radix_on && s <= kQRadixS;
+  size_t lds = (size_t)P * sizeof(double);
+  if (radix && lds < sizeof(typename QRadixSort::storage_type)) lds = sizeof(typename QRadixSort::storage_type);
+  auto launch = [&](auto kern) {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+    hipLaunchKernelGGL(kern, dim3(d), dim3(kQThreads), lds, st, samp, s, d, max_bins, sorted, thr, nthr, kdist);
+  };
+  if (radix) launch(quantile_kernel<true>);
+  else launch(quantile_kernel<false>);
   return (int)hipGetLastError();
 }

@@ -108,12 +108,17 @@ def test_binize(dev):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("max_bins,s", [(40, 10000), (256, 16384), (2, 3000), (32, 777)])
-def test_quantile_thresholds_kernel(dev, max_bins, s):
-    """K3 quantile kernel == the host findSplits reference (NaNs, +-inf, few-distinct and categorical columns)."""
+@pytest.mark.parametrize("max_bins,s,f32", [(40, 10000, False), (256, 16384, False), (2, 3000, False),
+                                            (32, 777, False), (40, 10000, True), (40, 12288, True),
+                                            (40, 12289, True), (256, 5000, True)])
+def test_quantile_thresholds_kernel(dev, max_bins, s, f32):
+    """K3 quantile kernel == the host findSplits reference (NaNs, +-inf, few-distinct and categorical columns).
+    f32: every column exactly fp32 (the engine's samples), so s <= 12288 takes the radix-sorted path for all."""
     from cdnaml.models.tree.engine import find_thresholds, find_thresholds_t
-    g = torch.Generator().manual_seed(max_bins)
+    g = torch.Generator().manual_seed(max_bins + s)
     samp = torch.randn(s, 37, generator=g, dtype=torch.float64)
+    if f32:
+        samp = samp.float().double()
     samp[:, 3] = torch.randint(0, 6, (s,), generator=g).double()       # categorical
     samp[:, 4] = torch.round(samp[:, 4] * 3)                             # few distinct values
     samp[::5, 7] = float("nan")
