@@ -60,6 +60,8 @@ SPEC_THRESHOLDS = __import__("os").environ.get("CDNAML_SPEC_THRESHOLDS", "1") !=
 HEAP_PREDICT = __import__("os").environ.get("CDNAML_HEAP_PREDICT", "1") != "0"
 # row-record partition gathers split bins from the row-major copy (one line per row) instead of [G][n]
 PARTITION_RM = __import__("os").environ.get("CDNAML_PARTITION_RM", "0") != "0"
+# boosting margins updated by the level partitions (ForestTrainer.train(margin=...)) instead of a tree walk
+GBDT_MARGIN = __import__("os").environ.get("CDNAML_GBDT_MARGIN", "1") != "0"
 # feature-subset forests: accumulate only each node's sampled features in segment mode.  Opt-in: measured
 # 5-8x slower (profiles/pmc_seg_hist_subset.txt): both children must be built, and every row gather of the
 # row-major bins (one or two 64 B lines) then feeds 34 atomics instead of 104
@@ -1075,7 +1077,7 @@ class ForestTrainer:
 
     # ------------------------------------------------------------ device-queued partition
     def _device_partition(self, so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n, v1, qs1, w_total,
-                          rec_buf):
+                          rec_buf, margin=None):
         """Partition tables decoded on the device from the level's K6 decisions and the row partition queued right
         behind them (the GPU partitions while the decisions travel to the host; the host repeats the decode to
         build the forest and the next level, checked against the device's in the checked build).  With
@@ -1084,7 +1086,8 @@ class ForestTrainer:
         A = so.shape[0]
         a_tree_d, tf_d = K.upload(dev, a_tree.astype(np.int32), tfirst.numpy().astype(np.int32))
         dec = K.split_decode(so, tot, a_tree_d, T, p.min_instances, p.min_info_gain,
-                             depth < p.max_depth, depth + 1 >= p.max_depth, missing_bin=mb)
+                             depth < p.max_depth, depth + 1 >= p.max_depth, missing_bin=mb,
+                             leaf_values=(p.impurity, p.reg_lambda) if margin is not None else None)
         em = None
         if emit_ok and A <= K.P7_MAX_SLOTS and data.bins.shape[0] <= 16 and T <= 64:
             em = self._record_emit(dev, n, A, v1, qs1, w_total, rec_buf)
@@ -1093,7 +1096,8 @@ class ForestTrainer:
         with _tr.span("tree.partition", depth=depth):
             K.partition_codes(data.bins, codes, tf_d, dec["tfirst_next"], dec["split_feat"],
                               dec["split_bin"], dec["cat_off"], dec["masks"].reshape(-1), dec["child"],
-                              bins_rm=data.row_major_bins() if PARTITION_RM else None, emit=em)
+                              bins_rm=data.row_major_bins() if PARTITION_RM else None, emit=em,
+                              margin=(margin[0], dec["lv"], margin[1]) if margin is not None else None)
         return dec, em
 
     # ------------------------------------------------------------ record emission by the partition
@@ -1270,11 +1274,14 @@ class ForestTrainer:
         return Hb
 
     def train(self, num_trees: int, stats_rows: Dict[str, torch.Tensor], weights: Optional[torch.Tensor],
-              forest: Optional[Forest] = None, codes_pre=None) -> Forest:
+              forest: Optional[Forest] = None, codes_pre=None, margin=None) -> Forest:
         """Grow ``num_trees`` trees. stats_rows: {'v0','v1'} (moments) or {'label'} (classes).
 
         codes_pre: a K.BootstrapCodes (the bootstrap draws already written as the row codes) instead of
-        ``weights``."""
+        ``weights``.
+        margin: ``(F [n] fp32, eta)`` (boosting, one tree): when the level loop can, each level's row partition
+        also adds ``eta * leaf value`` to F for the rows that finish there (a last partition at the deepest
+        level), so the caller needs no tree walk; ``self.margin_applied`` says whether it did."""
         p = self.p
         data = self.data
         dev = self.device
@@ -1321,6 +1328,13 @@ class ForestTrainer:
         use_codes = USE_CODES and (p.max_depth <= 8 or (deep_switch and use_mseg)) and not use_seg
         if codes_pre is not None and not use_codes:
             weights = codes_pre.weights()  # a path that reads the multiplicities themselves
+        # margin updates by the partition need every level on the device decode + partition5 path, every row in
+        # the tree (no zero weights) and leaf values the device can form (no categorical / classification)
+        margin_ok = (margin is not None and GBDT_MARGIN and use_codes and not deep_switch and T == 1 and
+                     weights is None and codes_pre is None and dev.type == "cuda" and p.impurity == "xgb" and
+                     self._device_decode_ok(dev, True, False) and self._native_split(dev) and not use_sub and
+                     not data.categorical and p.max_depth <= 8)
+        self.margin_applied = margin_ok
         if use_seg:
             w1 = None if weights is None else weights.reshape(-1)
             wmax = int(w1.max().item()) if (w1 is not None and w1.numel()) else 1
@@ -1532,7 +1546,7 @@ class ForestTrainer:
                                            missing_bin=mb)
                 dec = None
                 host_p = None
-                if self._device_decode_ok(dev, use_codes, mb) and depth + 1 < p.max_depth:
+                if self._device_decode_ok(dev, use_codes, mb) and (depth + 1 < p.max_depth or margin_ok):
                     # the decisions leave for the host first (pinned, async): they arrive while the partition runs
                     src = torch.cat([so, tot], 1) if depth == 0 else so
                     host_p = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
@@ -1543,10 +1557,10 @@ class ForestTrainer:
                     # the GPU partitions while the decisions travel to the host and the host builds the forest
                     # and the next level's layout (the same decode on the host, checked in the checked build)
                     emit_ok = (K.EMIT_RECORDS and use_mseg and rec_ok and subtract and not use_sub and
-                               w_total is not None and data.bins_s10 is not None)
+                               w_total is not None and data.bins_s10 is not None and not margin_ok)
                     dec, em = self._device_partition(so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n,
                                                      stats_rows["v1"], mseg_scales[1] if use_mseg else 1.0,
-                                                     w_total, rec_buf)
+                                                     w_total, rec_buf, margin=margin if margin_ok else None)
                     if em is not None:
                         rec_buf = em.rec
                         emits.append(em)

@@ -204,16 +204,22 @@ class _XgbEstimatorBase(Estimator):
                 # unit hessians (squared error, unweighted): H = row count, so the histogram
                 # takes the single-statistic (packed count|sum) path
                 v0 = None if unit_hess else h[:, k].float().contiguous()
+                # the margins of the rows updated by the level partitions as each row reaches its leaf (no walk of
+                # the finished tree) when the trainer's level loop allows it (every row in the tree, reg_alpha 0:
+                # the leaf values are the trainer's own)
+                fk = F[:, k]
+                margin = (fk, eta) if (bag is None and fk.is_contiguous() and self.getReg_alpha() <= 0) else None
                 trainer.train(1, {"v0": v0, "v1": g[:, k].float().contiguous()},
-                              None if bag is None else bag[None, :].contiguous(), forest)
+                              None if bag is None else bag[None, :].contiguous(), forest, margin=margin)
                 t = len(forest.roots) - 1
                 with _tr.span("xgb.update_margin", round=m):
                     self._apply_l1(forest, t)
-                    nodes, vals, masks = forest.binned_arrays(dev, t)
-                    col = F[:, k] if F[:, k].is_contiguous() else F[:, k].contiguous()
-                    K.predict_binned_add(data.bins, nodes, 0, vals, masks, eta, col)
-                    if col.data_ptr() != F[:, k].data_ptr():
-                        F[:, k] = col
+                    if not (margin is not None and trainer.margin_applied):
+                        nodes, vals, masks = forest.binned_arrays(dev, t)
+                        col = fk if fk.is_contiguous() else fk.contiguous()
+                        K.predict_binned_add(data.bins, nodes, 0, vals, masks, eta, col)
+                        if col.data_ptr() != fk.data_ptr():
+                            F[:, k] = col
             if val_mask is not None and metric_fn is not None:
                 v = metric_fn(F, val_mask)
                 history.append(v)

@@ -145,8 +145,8 @@ _SIGS = {
     "cdna_split_scan_sub": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_double, c_double, c_void_p, c_void_p,
                              c_void_p], c_int),
     "cdna_split_decode": ([c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_double, c_int, c_int,
-                           c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
-                          c_int),
+                           c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_int, c_double, c_void_p], c_int),
     "cdna_split_scan_ex": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_void_p,
                             c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double,
@@ -200,7 +200,7 @@ _SIGS = {
                         c_void_p], c_int),
     "cdna_codes_init": ([c_void_p, c_int64, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_partition5": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
+                         c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_float, c_void_p, c_void_p], c_int),
     "cdna_partition": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p], c_int),
     "cdna_tree_predict": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p,

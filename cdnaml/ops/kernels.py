@@ -953,11 +953,13 @@ def emit_plan_host(w_left: np.ndarray, w_right: np.ndarray, child: np.ndarray, c
 def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tensor, tfirst_next: torch.Tensor,
                     split_feat: torch.Tensor, split_bin: torch.Tensor, cat_off: torch.Tensor,
                     cat_mask: torch.Tensor, child: torch.Tensor, bins_rm: Optional[torch.Tensor] = None,
-                    emit: Optional["RecordEmit"] = None) -> None:
+                    emit: Optional["RecordEmit"] = None, margin: Optional[tuple] = None) -> None:
     """In place: every row's code moves to the chosen child's local index (255 = done).
 
     bins_rm: optional row-major copy [n, G, 8] of the bins, read instead of ``bins`` when given.
-    emit: (GPU, partition7) also write the next level's item records of the built children (:class:`RecordEmit`)."""
+    emit: (GPU, partition7) also write the next level's item records of the built children (:class:`RecordEmit`).
+    margin (GPU, partition5): ``(F [n] fp32, lv [3A] fp32 from split_decode, eta)`` -- rows that finish at this
+    level add ``eta * leaf value`` to F (boosting margin update without a tree walk)."""
     G, n, _ = bins.shape
     T = codes.shape[0]
     if n == 0 or T == 0:
@@ -977,8 +979,8 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
         # partition7 streams every bins word of every row once per level (10 GB at 1e8 x 100): it pays when
         # many trees share that pass; for few trees partition5's per-(row, tree) byte gathers move less (GBDT,
         # T = 1: 57.9 vs 40.6 ms per boosting round with partition7; CV grid with 5 / 10 trees: 2.18 vs 1.34 s)
-        if emit is not None or (PARTITION7 and T >= PARTITION7_MIN_T and G <= 16 and A <= 1024 and T <= 64 and
-                                bins_rm is None):
+        if margin is None and (emit is not None or (PARTITION7 and T >= PARTITION7_MIN_T and G <= 16 and
+                                                     A <= 1024 and T <= 64 and bins_rm is None)):
             e = emit
             _lib.check(_lib.lib().cdna_partition7(
                 _ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]), _ptr(args[2]), _ptr(args[3]),
@@ -995,10 +997,15 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
         if bins_rm is not None:
             assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
             src, rm_bytes = bins_rm, bins_rm.shape[1] * 8
+        F, lv, eta = margin if margin is not None else (None, None, 0.0)
+        if margin is not None:
+            assert F.dtype == torch.float32 and F.is_contiguous() and F.numel() == n and lv.numel() == 3 * A
         _lib.check(_lib.lib().cdna_partition5(_ptr(src), n, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]),
                                               _ptr(args[2]), _ptr(args[3]), _ptr(args[4]), _ptr(cm),
-                                              _ptr(args[5]), rm_bytes, _stream(bins.device)), "cdna_partition5")
+                                              _ptr(args[5]), rm_bytes, _ptr(lv), float(eta), _ptr(F),
+                                              _stream(bins.device)), "cdna_partition5")
         return
+    assert margin is None, "margin updates run in the GPU partition only"
     node, w = decode_codes(codes, tfirst)
     live = node >= 0
     partition(bins, node, split_feat, split_bin, cat_off, cat_mask, child)
@@ -2139,10 +2146,14 @@ def split_scan(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor
 
 
 def split_decode(so: torch.Tensor, tot: torch.Tensor, a_tree: torch.Tensor, T: int, min_inst: float,
-                 min_gain: float, can_level: bool, leaf_children: bool, missing_bin: bool = False):
+                 min_gain: float, can_level: bool, leaf_children: bool, missing_bin: bool = False,
+                 leaf_values: Optional[tuple] = None):
     """K6 decisions [A, >= 7] + node totals -> partition tables on the device (split.hip split_decode_kernel):
     split_feat / split_bin / cat_off [A], masks [A, 8] (bin sets of missing-right splits, cat_off[a] = a),
-    child [2A], tfirst_next [T] (int32), the host decode's exact twin."""
+    child [2A], tfirst_next [T] (int32), the host decode's exact twin.
+
+    leaf_values ("xgb" | "variance", lambda): also "lv" [3A] fp32, the leaf values of the rows' destinations at
+    this level (children that are leaves, active nodes that do not split) for the partition's margin update."""
     A = so.shape[0]
     dev = so.device
     out = torch.empty(15 * A + T, dtype=torch.int32, device=dev)
@@ -2150,13 +2161,16 @@ def split_decode(so: torch.Tensor, tot: torch.Tensor, a_tree: torch.Tensor, T: i
     child, pref, tfn = out[3 * A:5 * A], out[5 * A:7 * A], out[7 * A:7 * A + T]
     masks = out[7 * A + T:15 * A + T]
     sc, tc = so.contiguous(), tot.contiguous()
+    lv = torch.empty(3 * A, dtype=torch.float32, device=dev) if leaf_values is not None else None
+    vk, lam = (1 if leaf_values[0] == "xgb" else 0, float(leaf_values[1])) if leaf_values is not None else (0, 0.0)
     _lib.check(_lib.lib().cdna_split_decode(_ptr(sc), sc.shape[1], _ptr(tc), tc.shape[1], _ptr(a_tree), A, T,
                                             float(min_inst), float(min_gain), int(bool(can_level)),
                                             int(bool(leaf_children)), int(bool(missing_bin)), _ptr(sf), _ptr(sb),
-                                            _ptr(co), _ptr(masks), _ptr(child), _ptr(pref), _ptr(tfn), _stream(dev)),
+                                            _ptr(co), _ptr(masks), _ptr(child), _ptr(pref), _ptr(tfn), _ptr(lv), vk,
+                                            lam, _stream(dev)),
                "cdna_split_decode")
     return {"split_feat": sf, "split_bin": sb, "cat_off": co, "masks": masks.view(A, 8), "child": child,
-            "tfirst_next": tfn}
+            "tfirst_next": tfn, "lv": lv}
 
 
 def split_scan_ex(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor], kind: str, min_inst: float):

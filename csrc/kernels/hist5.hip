@@ -709,7 +709,9 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
                                                          const int* __restrict__ split_bin,
                                                          const int* __restrict__ cat_off,
                                                          const uint32_t* __restrict__ cat_mask,
-                                                         const int* __restrict__ child, int rm_row_bytes) {
+                                                         const int* __restrict__ child, int rm_row_bytes,
+                                                         const float* __restrict__ lv, float eta,
+                                                         float* __restrict__ F) {
   __shared__ int s_f[256], s_b[256], s_co[256], s_ch[512];
   const int t = blockIdx.y;
   const int tf = tfirst[t];
@@ -736,6 +738,12 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
   };
   uint16_t* rec = codes + (int64_t)t * n;
   const int64_t n4 = n / 4;
+  // F (boosting margins, optional): a row whose node becomes a leaf here -- a child that is a leaf, or an active
+  // node that does not split -- adds eta * its leaf value (lv[2 a + side] / lv[2 A + a], split_decode's table):
+  // the same fp32 update, once per row and tree, as predict_binned_kernel's walk after the tree is built
+  auto leaf_add = [&](int64_t r, int e) {
+    if (F) F[r] += eta * lv[e];
+  };
   auto move = [&](int64_t r, uint32_t c) -> uint32_t {
     const uint32_t loc = c & 0xFFu;
     if (loc == 0xFFu) return c;
@@ -746,6 +754,9 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
       const int co = s_co[loc];
       const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u : bin <= s_b[loc];
       nl = (uint32_t)s_ch[2 * loc + (left ? 0 : 1)];
+      if (nl == 0xFFu) leaf_add(r, 2 * (tf + (int)loc) + (left ? 0 : 1));
+    } else {
+      leaf_add(r, 2 * A + tf + (int)loc);
     }
     return (c & 0xFF00u) | nl;
   };
@@ -787,6 +798,7 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
           uint32_t res = c;
           if (loc != 0xFFu) {
             const int f = s_f[loc];
+            const int64_t r = (q0 + u * stride) * 4 + k;
             uint32_t nl = 0xFFu;
             if (f >= 0) {
               const int bin = bins_[u][k];
@@ -794,6 +806,9 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
               const bool left = co >= 0 ? ((cat_mask[co * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u
                                         : bin <= s_b[loc];
               nl = (uint32_t)s_ch[2 * loc + (left ? 0 : 1)];
+              if (nl == 0xFFu) leaf_add(r, 2 * (tf + (int)loc) + (left ? 0 : 1));
+            } else {
+              leaf_add(r, 2 * A + tf + (int)loc);
             }
             res = (c & 0xFF00u) | nl;
           }
@@ -1231,13 +1246,16 @@ CDNA_API int cdna_partition7(const uint64_t* bins, int64_t n, int G, int T, int 
   return (int)hipGetLastError();
 }
 
+// lv / eta / F (optional, F null: off): boosting margins updated by the rows that finish at this level.
 CDNA_API int cdna_partition5(const uint64_t* bins, int64_t n, int T, int A, uint16_t* codes, const int* tfirst,
                              const int* tfirst_next, const int* split_feat, const int* split_bin, const int* cat_off,
-                             const uint32_t* cat_mask, const int* child, int rm_row_bytes, hipStream_t st) {
+                             const uint32_t* cat_mask, const int* child, int rm_row_bytes, const float* lv, float eta,
+                             float* F, hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
+  if (F && !lv) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(partition5_kernel, dim3(grid_for(n / 4 + 1, 256, 1024), T), dim3(256), 0, st, bins, n, T, A,
                      codes, tfirst,
-                     tfirst_next, split_feat, split_bin, cat_off, cat_mask, child, rm_row_bytes);
+                     tfirst_next, split_feat, split_bin, cat_off, cat_mask, child, rm_row_bytes, lv, eta, F);
   return (int)hipGetLastError();
 }
 

@@ -622,9 +622,17 @@ __global__ __launch_bounds__(1024) void split_decode_kernel(const double* __rest
                                                             int* __restrict__ split_bin, int* __restrict__ cat_off,
                                                             uint32_t* __restrict__ masks,
                                                             int* __restrict__ child, int* __restrict__ pref,
-                                                            int* __restrict__ tfirst_next) {
+                                                            int* __restrict__ tfirst_next, float* __restrict__ lv,
+                                                            int vkind, double lam) {
   __shared__ int s_wave[16];
   __shared__ int s_carry;
+  // lv (optional) [3A]: leaf values of the rows' destinations at this level, for the partition's margin update
+  // -- lv[2a + s] the value of child s of a splitting node when that child is a leaf, lv[2A + a] the value of an
+  // active node that does not split; the host forest's values of the same nodes (engine._leaf_values_v, fp64,
+  // then fp32): vkind 1 (xgb) -S / (W + lam), else S / W (0 when W = 0).  Entries no row reads are 0.
+  auto leafval = [&](double W, double S) -> float {
+    return vkind == 1 ? (float)(-S / (W + lam)) : (float)(W > 0.0 ? S / W : 0.0);
+  };
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_carry = 0;
   __syncthreads();
@@ -655,6 +663,10 @@ __global__ __launch_bounds__(1024) void split_decode_kernel(const double* __rest
       }
       const double cw = so[(int64_t)a * sw + (s == 0 ? 3 : 5)];
       flag = (can && !(cw < 2.0 * min_inst) && !leaf_children) ? 1 : 0;
+      if (lv) {
+        lv[e] = (can && !flag) ? leafval(cw, so[(int64_t)a * sw + (s == 0 ? 4 : 6)]) : 0.f;
+        if (s == 0) lv[2 * A + a] = can ? 0.f : leafval(W, tot[(int64_t)a * tw + 1]);
+      }
     }
     // block exclusive scan of the flags
     const uint64_t m = __builtin_amdgcn_ballot_w64(flag != 0);
@@ -696,12 +708,12 @@ __global__ __launch_bounds__(1024) void split_decode_kernel(const double* __rest
 CDNA_API int cdna_split_decode(const double* so, int sw, const double* tot, int tw, const int* a_tree, int A, int T,
                                double min_inst, double min_gain, int can_level, int leaf_children, int missing_bin,
                                int* split_feat, int* split_bin, int* cat_off, uint32_t* masks, int* child, int* pref,
-                               int* tfirst_next, hipStream_t st) {
+                               int* tfirst_next, float* lv, int vkind, double lam, hipStream_t st) {
   if (A <= 0 || T <= 0) return 0;
-  if (sw < 7 || tw < 1 || (missing_bin && sw < 8)) return (int)hipErrorInvalidValue;
+  if (sw < 7 || tw < 1 || (missing_bin && sw < 8) || (lv && tw < 2)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(split_decode_kernel, dim3(1), dim3(1024), 0, st, so, sw, tot, tw, a_tree, A, T, min_inst,
                      min_gain, can_level, leaf_children, missing_bin, split_feat, split_bin, cat_off, masks, child,
-                     pref, tfirst_next);
+                     pref, tfirst_next, lv, vkind, lam);
   return (int)hipGetLastError();
 }
 
