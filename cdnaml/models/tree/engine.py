@@ -1077,7 +1077,7 @@ class ForestTrainer:
 
     # ------------------------------------------------------------ device-queued partition
     def _device_partition(self, so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n, v1, qs1, w_total,
-                          rec_buf, margin=None):
+                          rec_buf, margin=None, catm=None):
         """Partition tables decoded on the device from the level's K6 decisions and the row partition queued right
         behind them (the GPU partitions while the decisions travel to the host; the host repeats the decode to
         build the forest and the next level, checked against the device's in the checked build).  With
@@ -1087,7 +1087,8 @@ class ForestTrainer:
         a_tree_d, tf_d = K.upload(dev, a_tree.astype(np.int32), tfirst.numpy().astype(np.int32))
         dec = K.split_decode(so, tot, a_tree_d, T, p.min_instances, p.min_info_gain,
                              depth < p.max_depth, depth + 1 >= p.max_depth, missing_bin=mb,
-                             leaf_values=(p.impurity, p.reg_lambda) if margin is not None else None)
+                             leaf_values=(p.impurity, p.reg_lambda) if margin is not None else None,
+                             catm=catm, nthr=self._nthr_dev(dev) if catm is not None else None)
         em = None
         if emit_ok and A <= K.P7_MAX_SLOTS and data.bins.shape[0] <= 16 and T <= 64:
             em = self._record_emit(dev, n, A, v1, qs1, w_total, rec_buf)
@@ -1584,26 +1585,35 @@ class ForestTrainer:
                 so, tot, cm = K.split_scan_ex(H, self._nthr_dev(dev), masks_t, p.impurity, p.min_instances)
                 kk = tot.shape[1]
                 src = torch.cat([so, cm.double()] + ([tot] if depth == 0 else []), 1)
-                if cls2 and use_codes and DEVICE_DECODE and not self.data.categorical and depth + 1 < p.max_depth \
+                reg_ex = not self.classification and kk == 2  # variance regression with categorical features
+                if (cls2 or reg_ex) and use_codes and DEVICE_DECODE and depth + 1 < p.max_depth \
                         and not (deep_switch and depth + 1 >= 8):
-                    # binary classification on the codes: the same device decode + partition (+ record emission)
-                    # as regression, queued behind K6 while the decisions travel to the host.  The decode reads
-                    # (gain, feature, bin, left weight, ., right weight, .); a pure child (one class) weighs 0 there,
-                    # so it is a leaf on the device exactly as on the host
+                    # binary classification / categorical regression on the codes: the same device decode +
+                    # partition (+ record emission) as numeric regression, queued behind K6 while the decisions
+                    # travel to the host; categorical winners split by K6's category bitmasks.  The decode reads
+                    # (gain, feature, bin, left weight, ., right weight, .); a pure child (one class) weighs 0
+                    # there, so it is a leaf on the device exactly as on the host
                     host_p = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
                     host_p.copy_(src, non_blocking=True)
                     host_ev = torch.cuda.Event()
                     host_ev.record(torch.cuda.current_stream(dev))
-                    l0, l1, r0, r1 = so[:, 4], so[:, 5], so[:, 6], so[:, 7]
-                    zero = torch.zeros_like(l0)
-                    so_d = torch.stack([so[:, 0], so[:, 1], so[:, 2],
-                                        torch.where((l0 > 0) & (l1 > 0), l0 + l1, zero), l1,
-                                        torch.where((r0 > 0) & (r1 > 0), r0 + r1, zero), r1], 1)
+                    if cls2:
+                        l0, l1, r0, r1 = so[:, 4], so[:, 5], so[:, 6], so[:, 7]
+                        zero = torch.zeros_like(l0)
+                        so_d = torch.stack([so[:, 0], so[:, 1], so[:, 2],
+                                            torch.where((l0 > 0) & (l1 > 0), l0 + l1, zero), l1,
+                                            torch.where((r0 > 0) & (r1 > 0), r0 + r1, zero), r1], 1)
+                        tot_d = tot.sum(1, keepdim=True)
+                    else:
+                        so_d = so[:, [0, 1, 2, 4, 5, 6, 7]]
+                        tot_d = tot
                     emit_ok = (K.EMIT_RECORDS and use_mseg and rec_ok and subtract and w_total is not None and
-                               data.bins_s10 is not None)
-                    dec, em = self._device_partition(so_d, tot.sum(1, keepdim=True), a_tree, tfirst, T, depth,
-                                                     False, codes, emit_ok, n, stats_rows["v1"], 1.0, w_total,
-                                                     rec_buf)
+                               data.bins_s10 is not None and not self.data.categorical)
+                    dec, em = self._device_partition(so_d, tot_d, a_tree, tfirst, T, depth,
+                                                     False, codes, emit_ok, n, stats_rows["v1"],
+                                                     1.0 if cls2 else (mseg_scales[1] if use_mseg else 1.0),
+                                                     w_total, rec_buf,
+                                                     catm=cm if self.data.categorical else None)
                     if em is not None:
                         rec_buf = em.rec
                         emits.append(em)

@@ -146,7 +146,7 @@ _SIGS = {
                              c_void_p], c_int),
     "cdna_split_decode": ([c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_double, c_int, c_int,
                            c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                           c_int, c_double, c_void_p], c_int),
+                           c_int, c_double, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_scan_ex": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_void_p,
                             c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_scan": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double,

@@ -2147,13 +2147,16 @@ def split_scan(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor
 
 def split_decode(so: torch.Tensor, tot: torch.Tensor, a_tree: torch.Tensor, T: int, min_inst: float,
                  min_gain: float, can_level: bool, leaf_children: bool, missing_bin: bool = False,
-                 leaf_values: Optional[tuple] = None):
+                 leaf_values: Optional[tuple] = None, catm: Optional[torch.Tensor] = None,
+                 nthr: Optional[torch.Tensor] = None):
     """K6 decisions [A, >= 7] + node totals -> partition tables on the device (split.hip split_decode_kernel):
     split_feat / split_bin / cat_off [A], masks [A, 8] (bin sets of missing-right splits, cat_off[a] = a),
     child [2A], tfirst_next [T] (int32), the host decode's exact twin.
 
     leaf_values ("xgb" | "variance", lambda): also "lv" [3A] fp32, the leaf values of the rows' destinations at
-    this level (children that are leaves, active nodes that do not split) for the partition's margin update."""
+    this level (children that are leaves, active nodes that do not split) for the partition's margin update.
+    catm [A, 8] int32 + nthr [d] int32 (split_scan_ex): winners on categorical features (nthr < 0) split by the
+    node's category bitmask (cat_off[a] = a)."""
     A = so.shape[0]
     dev = so.device
     out = torch.empty(15 * A + T, dtype=torch.int32, device=dev)
@@ -2167,7 +2170,8 @@ def split_decode(so: torch.Tensor, tot: torch.Tensor, a_tree: torch.Tensor, T: i
                                             float(min_inst), float(min_gain), int(bool(can_level)),
                                             int(bool(leaf_children)), int(bool(missing_bin)), _ptr(sf), _ptr(sb),
                                             _ptr(co), _ptr(masks), _ptr(child), _ptr(pref), _ptr(tfn), _ptr(lv), vk,
-                                            lam, _stream(dev)),
+                                            lam, _ptr(None if catm is None else catm.contiguous()),
+                                            _ptr(None if nthr is None else nthr.contiguous()), _stream(dev)),
                "cdna_split_decode")
     return {"split_feat": sf, "split_bin": sb, "cat_off": co, "masks": masks.view(A, 8), "child": child,
             "tfirst_next": tfn, "lv": lv}

@@ -623,7 +623,8 @@ __global__ __launch_bounds__(1024) void split_decode_kernel(const double* __rest
                                                             uint32_t* __restrict__ masks,
                                                             int* __restrict__ child, int* __restrict__ pref,
                                                             int* __restrict__ tfirst_next, float* __restrict__ lv,
-                                                            int vkind, double lam) {
+                                                            int vkind, double lam, const int* __restrict__ catm,
+                                                            const int* __restrict__ nthr) {
   __shared__ int s_wave[16];
   __shared__ int s_carry;
   // lv (optional) [3A]: leaf values of the rows' destinations at this level, for the partition's margin update
@@ -646,12 +647,17 @@ __global__ __launch_bounds__(1024) void split_decode_kernel(const double* __rest
       const bool can = can_level && g == g && g != __builtin_inf() && g > 0.0 && g >= min_gain && W >= 2.0 * min_inst;
       if (s == 0) {
         const int b = (int)so[(int64_t)a * sw + 2];
+        const int fs = (int)so[(int64_t)a * sw + 1];
+        // a categorical winner (nthr < 0): left = split_scan_ex's category bitmask of the node
+        const bool cat = can && catm != nullptr && nthr != nullptr && fs >= 0 && nthr[fs] < 0;
         // XGBoost's missing-right splits (bin 0 = missing goes right): the left side is the bin set 1..b
-        const bool mr = can && missing_bin && sw >= 8 && so[(int64_t)a * sw + 7] > 0.5;
-        split_feat[a] = can ? (int)so[(int64_t)a * sw + 1] : -1;
-        split_bin[a] = can && !mr ? b : 0;
-        cat_off[a] = mr ? a : -1;
-        if (mr)
+        const bool mr = !cat && can && missing_bin && sw >= 8 && so[(int64_t)a * sw + 7] > 0.5;
+        split_feat[a] = can ? fs : -1;
+        split_bin[a] = can && !mr && !cat ? b : 0;
+        cat_off[a] = (mr || cat) ? a : -1;
+        if (cat)
+          for (int w = 0; w < 8; ++w) masks[(int64_t)a * 8 + w] = (uint32_t)catm[(int64_t)a * 8 + w];
+        else if (mr)
           for (int w = 0; w < 8; ++w) {
             uint32_t m = 0u;
             for (int j = 0; j < 32; ++j) {
@@ -704,16 +710,19 @@ __global__ __launch_bounds__(1024) void split_decode_kernel(const double* __rest
 }  // namespace
 
 // so [A][sw] (gain, feature, bin, left0, left1, right0, right1, ...), tot [A][tw]; pref: [2A] int scratch.
-// masks: [A][8] bin sets of missing-right splits (cat_off[a] = a), written only for those nodes.
+// masks: [A][8] bin sets of missing-right splits and categorical winners (cat_off[a] = a), written only for those
+// nodes; catm [A][8] / nthr [d] (optional): split_scan_ex's category bitmasks and the features' threshold counts
+// (< 0: categorical).
 CDNA_API int cdna_split_decode(const double* so, int sw, const double* tot, int tw, const int* a_tree, int A, int T,
                                double min_inst, double min_gain, int can_level, int leaf_children, int missing_bin,
                                int* split_feat, int* split_bin, int* cat_off, uint32_t* masks, int* child, int* pref,
-                               int* tfirst_next, float* lv, int vkind, double lam, hipStream_t st) {
+                               int* tfirst_next, float* lv, int vkind, double lam, const int* catm, const int* nthr,
+                               hipStream_t st) {
   if (A <= 0 || T <= 0) return 0;
   if (sw < 7 || tw < 1 || (missing_bin && sw < 8) || (lv && tw < 2)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(split_decode_kernel, dim3(1), dim3(1024), 0, st, so, sw, tot, tw, a_tree, A, T, min_inst,
                      min_gain, can_level, leaf_children, missing_bin, split_feat, split_bin, cat_off, masks, child,
-                     pref, tfirst_next, lv, vkind, lam);
+                     pref, tfirst_next, lv, vkind, lam, catm, nthr);
   return (int)hipGetLastError();
 }
 

@@ -141,3 +141,45 @@ def test_device_split_decode_forests_identical(dev, model, monkeypatch):
         monkeypatch.setattr(engine, "DEVICE_DECODE", flag)
         digests.append(forest_digest(est.fit(df)._forest))
     assert digests[0] == digests[1]
+
+
+@pytest.mark.parametrize("flow", ["dt_reg", "rf_reg", "rf_binary"])
+def test_device_decode_categorical_forests_identical(dev, flow, monkeypatch):
+    """Categorical winners decoded on the device (split_decode with split_scan_ex's category bitmasks, partition
+    queued before the decisions reach the host) give the host decode's forests bit for bit: regression trees /
+    forests with StringIndexer'd categoricals (ML 06) and a binary classifier on the same features."""
+    import cdnaml
+    import pandas as pd
+    from cdnaml.models.tree import engine
+    from cdnaml.utils.synthetic import forest_digest
+    from cdnaml.ml.feature import StringIndexer, VectorAssembler
+    from cdnaml.ml.classification import RandomForestClassifier
+    from cdnaml.ml.regression import DecisionTreeRegressor, RandomForestRegressor
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    rng = np.random.default_rng(5)
+    n = 60_000
+    pdf = pd.DataFrame({"hood": [f"h{i}" for i in rng.integers(0, 37, n)],
+                        "room": rng.choice(["entire", "private", "shared", "hotel"], n),
+                        "beds": rng.integers(1, 6, n).astype(float), "lat": rng.normal(size=n)})
+    hood_num = pdf.hood.str[1:].astype(int)
+    price = 40 * pdf.beds + 15 * (hood_num % 5) + 60 * (pdf.room == "entire") + 10 * pdf.lat + rng.normal(size=n) * 5
+    pdf["label"] = (price > np.median(price)).astype(float) if flow == "rf_binary" else price
+    sdf = spark.createDataFrame(pdf)
+    sdf = StringIndexer(inputCols=["hood", "room"], outputCols=["hoodIdx", "roomIdx"]).fit(sdf).transform(sdf)
+    df = VectorAssembler(inputCols=["hoodIdx", "roomIdx", "beds", "lat"], outputCol="features").transform(sdf)
+    est = {"dt_reg": DecisionTreeRegressor(maxDepth=6, maxBins=40),
+           "rf_reg": RandomForestRegressor(numTrees=8, maxDepth=6, maxBins=40, seed=2),
+           "rf_binary": RandomForestClassifier(numTrees=8, maxDepth=6, maxBins=40, seed=2)}[flow]
+    decodes = {"n": 0}
+    orig = K.split_decode
+
+    def counted(*a, **k):
+        decodes["n"] += int(k.get("catm") is not None)
+        return orig(*a, **k)
+    monkeypatch.setattr(K, "split_decode", counted)
+    digests = []
+    for flag in (True, False):
+        monkeypatch.setattr(engine, "DEVICE_DECODE", flag)
+        digests.append(forest_digest(est.fit(df)._forest))
+    assert decodes["n"] > 0  # the categorical device decode ran
+    assert digests[0] == digests[1]
