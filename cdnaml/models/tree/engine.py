@@ -25,6 +25,7 @@ Two histogram strategies:
 """
 from __future__ import annotations
 
+import functools
 import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -834,6 +835,14 @@ def _built_nodes(w: np.ndarray, a_sib: np.ndarray, a_parent: np.ndarray) -> np.n
     return build
 
 
+def _forest_level_ops(forest, add_args, split_args, first_id, count):
+    """One level's forest bookkeeping (ForestTrainer.train defers it to the next level's decision sync): append
+    the children, then turn the split nodes into splits pointing at them."""
+    got = forest.add_many(*add_args)
+    assert len(got) == count and (not count or got[0] == first_id)
+    forest.set_splits(*split_args)
+
+
 class ForestTrainer:
     """Trains T trees level-synchronously over one BinnedData shard per rank."""
 
@@ -1385,6 +1394,12 @@ class ForestTrainer:
         w_total = None    # sum of the root weights (bounds every level's records)
         rec_buf = None
         root_ids = [None] * T
+        pending = []  # deferred forest bookkeeping of the previous level (see flush points)
+
+        def flush():
+            while pending:
+                pending.pop(0)()
+        node_count = forest.num_nodes
         for depth in range(p.max_depth + 1):
             A = len(a_tree)
             if A == 0:
@@ -1569,6 +1584,7 @@ class ForestTrainer:
                 # so [A, 8] = gain, feature, bin, left (2), right (2), missing-goes-right: copied to the host as is
                 # (plus the node totals at level 0), no per-column device ops
                 sw = so.shape[1]
+                flush()  # the previous level's forest bookkeeping, while the GPU runs this level's kernels
                 if host_p is not None:
                     host_ev.synchronize()
                     host = host_p.numpy()
@@ -1618,9 +1634,11 @@ class ForestTrainer:
                         rec_buf = em.rec
                         emits.append(em)
                         em_next = em
+                    flush()
                     host_ev.synchronize()
                     host = host_p.numpy()
                 else:
+                    flush()
                     host = src.cpu().numpy()
                 gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
                 lst_h, rst_h = host[:, 4:4 + kk], host[:, 4 + kk:4 + 2 * kk]
@@ -1640,6 +1658,7 @@ class ForestTrainer:
                     cols.append(miss_right[:, None].double())
                 if depth == 0:
                     cols.append(tot)
+                flush()
                 host = torch.cat(cols, 1).cpu().numpy()
                 gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
                 lst_h, rst_h = host[:, 3:3 + kk], host[:, 3 + kk:3 + 2 * kk]
@@ -1656,6 +1675,7 @@ class ForestTrainer:
             if depth == 0:
                 a_fid = forest.add_many(self._leaf_values_v(a_stats), self._weights_v(a_stats), depth,
                                         self._impurities_v(a_stats))
+                node_count = forest.num_nodes
                 if heap is not None:
                     heap[a_tree, 0, 1] = self._leaf_values_v(a_stats)[:, 0].astype(np.float32).view(np.int32)
                 for t_, fid_ in zip(a_tree.tolist(), a_fid.tolist()):
@@ -1678,6 +1698,7 @@ class ForestTrainer:
             thr_sp = np.zeros(len(sp))
             plain = np.ones(len(sp), dtype=bool)
             if self.data.categorical or mr_h is not None:
+                flush()  # the writes below address the nodes the previous level appended
                 for j, a in enumerate(sp.tolist()):
                     f, b = int(f_sp[j]), int(b_sp[j])
                     if f in self.data.categorical:
@@ -1714,7 +1735,8 @@ class ForestTrainer:
             ch_st = np.stack([lst_h[sp], rst_h[sp]], 1).reshape(-1, k_st)
             # forest ids of the children (appended after the partition launch: the forest bookkeeping then
             # runs on the host while the GPU partitions the rows)
-            ch_ids = np.arange(forest.num_nodes, forest.num_nodes + 2 * len(sp), dtype=np.int64)
+            ch_ids = np.arange(node_count, node_count + 2 * len(sp), dtype=np.int64)
+            node_count += 2 * len(sp)
             cw = self._weights_v(ch_st)
             leaf = (cw < 2 * p.min_instances) | (depth + 1 >= p.max_depth)
             if self.classification:
@@ -1766,7 +1788,13 @@ class ForestTrainer:
                         K.partition(data.bins, node, *K.upload(dev, split_feat, split_bin, cat_off,
                                                                cm.reshape(-1), child))
             ch_vals = self._leaf_values_v(ch_st)
-            got = forest.add_many(ch_vals, cw, depth + 1, self._impurities_v(ch_st))
+            # the forest's node lists for this level are appended and split at the next level's decision sync
+            # (flush), i.e. while the GPU runs that level's histogram / K6 / partition, not between this level's
+            # decisions and the next level's launches (~0.2-0.4 ms of numpy per level at the headline's widths)
+            pending.append(functools.partial(_forest_level_ops, forest, (ch_vals, cw, depth + 1,
+                                                                          self._impurities_v(ch_st)),
+                                             (fid_sp, f_sp, gain_h[sp], b_sp, thr_sp, num, ch_ids[0::2],
+                                              ch_ids[1::2]), ch_ids[0] if len(ch_ids) else None, len(ch_ids)))
             if heap is not None and len(sp):
                 if not plain.all():
                     heap = None  # bin-set splits: Forest.heap_arrays builds the table from the forest
@@ -1777,11 +1805,10 @@ class ForestTrainer:
                     ck = np.stack([2 * ksp, 2 * ksp + 1], 1).reshape(-1)
                     heap[np.repeat(tsp, 2), ck - 1, 1] = ch_vals[:, 0].astype(np.float32).view(np.int32)
                     heap_depth = depth + 1
-            assert len(got) == len(ch_ids) and (not len(got) or got[0] == ch_ids[0])
-            forest.set_splits(fid_sp, f_sp, gain_h[sp], b_sp, thr_sp, num, ch_ids[0::2], ch_ids[1::2])
             prev_hist = H if subtract else None
             emitted = em_next
             a_tree, a_fid, a_key, a_stats, a_sib, a_parent = n_tree, n_fid, n_key, n_stats, n_sib, n_parent
+        flush()
         if emits and int(torch.stack([e.err for e in emits]).max().item()):
             raise RuntimeError("partition record emission overflowed its capacity plan")
         forest.roots.extend(root_ids)
