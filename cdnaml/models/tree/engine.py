@@ -437,8 +437,15 @@ def _resident(X):
 
 
 # ============================================================ forest storage
+_ZERO_MASK = np.zeros(8, dtype=np.uint32)
+_ZERO_MASK.flags.writeable = False
+
+
 class Forest:
-    """Struct-of-arrays node store for an ensemble (host), + cached device arrays."""
+    """Struct-of-arrays node store for an ensemble (host), + cached device arrays.
+
+    ``value[i]``: the node's k outputs (a float sequence: numpy array or list); ``catmask[i]``: uint32[8] bitmask
+    (leaves share one read-only zero mask)."""
 
     def __init__(self, K_: int):
         self.K = K_
@@ -485,9 +492,12 @@ class Forest:
         self.bin.extend([0] * N)
         self.left.extend([-1] * N)
         self.right.extend([-1] * N)
-        self.catmask.extend(list(np.zeros((N, 8), dtype=np.uint32)))
+        # leaves share one read-only zero mask (a categorical split assigns its own) and take their values as
+        # float lists: N fresh numpy rows per field cost ~0.2 ms at the headline's last level (640 leaves) while
+        # the GPU waits for the predict launch
+        self.catmask.extend([_ZERO_MASK] * N)
         self.is_cat.extend([False] * N)
-        self.value.extend(list(values))
+        self.value.extend(values.tolist())
         self.weight.extend(np.asarray(weights, dtype=np.float64).tolist())
         self.gain.extend([0.0] * N)
         self.impurity.extend(np.asarray(impurity, dtype=np.float64).tolist())
