@@ -516,6 +516,13 @@ class Forest:
         lo, hi = int(fids.min()), int(fids.max()) + 1
         rel = fids - lo
         h = np.asarray(has_thr, dtype=bool)
+        if hi - lo == fids.size and bool(h.all()) and bool((rel[1:] > rel[:-1]).all()):
+            # every node of the range splits, in order, on a threshold: plain slice assignments
+            for name, vals in (("feat", feats), ("gain", gains), ("left", lefts), ("right", rights), ("bin", bins),
+                               ("thr", thrs)):
+                getattr(self, name)[lo:hi] = np.asarray(vals, dtype=np.float64 if name in ("gain", "thr")
+                                                        else np.int64).tolist()
+            return
         for name, vals, sel in (("feat", feats, None), ("gain", gains, None), ("left", lefts, None),
                                 ("right", rights, None), ("bin", bins, h), ("thr", thrs, h)):
             lst = getattr(self, name)
