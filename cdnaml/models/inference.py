@@ -70,6 +70,7 @@ class ForestPredictor:
             b0 = 0.0 if self.base is None else float(np.asarray(self.base, np.float64).reshape(-1)[0])
             out = K.tree_predict_heap(X, heap[0], heap[1], tw, heap[2], b0, dtype=dtype)
             if out is not None:
+                self.forest.settle()  # the trainer's deferred node lists, while the GPU predicts
                 return out
         nodes, roots, vals, masks = self.forest.device_arrays(X.device, self.kind)
         return K.tree_predict(X, nodes, roots, tw, vals, masks, self.forest.K, b).to(dtype)

@@ -448,6 +448,11 @@ class Forest:
     (leaves share one read-only zero mask)."""
 
     def __init__(self, K_: int):
+        # bookkeeping a trainer left to run later (settle()): the last level's node lists, appended while the
+        # GPU predicts instead of between the last split and the predict launch (the node-list fields below are
+        # properties that settle first, so every reader sees the complete forest)
+        self._pending: list = []
+        self._settling = False
         self.K = K_
         self.feat: List[int] = []
         self.thr: List[float] = []
@@ -464,6 +469,23 @@ class Forest:
         self.roots: List[int] = []
         self._dev = {}
         self._heap_np = None  # (heap [T, 2^(D+1)-1, 2] int32, D) built by ForestTrainer.train, or None
+
+    def settle(self) -> None:
+        """Run the deferred bookkeeping (idempotent; a no-op when nothing is pending)."""
+        if self._settling:
+            return
+        self._settling = True
+        try:
+            while self._pending:
+                self._pending.pop(0)()
+        finally:
+            self._settling = False
+
+    def __getstate__(self):
+        self.settle()
+        st = dict(self.__dict__)
+        st["_pending"] = []
+        return st
 
     def add(self, value, weight, depth, impurity=float("nan")) -> int:
         i = len(self.feat)
@@ -850,6 +872,25 @@ def _built_nodes(w: np.ndarray, a_sib: np.ndarray, a_parent: np.ndarray) -> np.n
     lose = (wa > ws) | ((wa == ws) & (has > a_sib[has]))
     build[has[lose]] = False
     return build
+
+
+def _settled_list(name: str):
+    key = "_" + name
+
+    def get(self):
+        if self._pending and not self._settling:
+            self.settle()
+        return self.__dict__[key]
+
+    def set_(self, v):
+        self.__dict__[key] = v
+    return property(get, set_)
+
+
+for _name in ("feat", "thr", "bin", "left", "right", "catmask", "is_cat", "value", "weight", "gain", "impurity",
+              "depth"):
+    setattr(Forest, _name, _settled_list(_name))
+del _name
 
 
 def _forest_level_ops(forest, add_args, split_args, first_id, count):
@@ -1825,7 +1866,10 @@ class ForestTrainer:
             prev_hist = H if subtract else None
             emitted = em_next
             a_tree, a_fid, a_key, a_stats, a_sib, a_parent = n_tree, n_fid, n_key, n_stats, n_sib, n_parent
-        flush()
+        # the last level's bookkeeping stays with the forest (settled by the predictor right after its launch, or
+        # by the first reader of the node lists)
+        forest._pending.extend(pending)
+        pending.clear()
         if emits and int(torch.stack([e.err for e in emits]).max().item()):
             raise RuntimeError("partition record emission overflowed its capacity plan")
         forest.roots.extend(root_ids)

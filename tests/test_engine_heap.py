@@ -40,3 +40,29 @@ def test_set_splits_vectorised():
         assert type(f.feat[a]) is int and type(f.thr[a]) is float
     other = np.setdiff1d(np.arange(50), fids)
     assert all(f.feat[a] == -1 and f.left[a] == -1 for a in other)
+
+
+def test_last_level_bookkeeping_settles_on_first_read():
+    """ForestTrainer.train leaves the last level's node-list bookkeeping with the forest (run by the predictor
+    right after its launch, or by the first reader): readers always see the complete forest, copies settle."""
+    import copy
+    import torch
+    import cdnaml
+    from cdnaml.models.regression import RandomForestRegressor
+    from cdnaml.utils.synthetic import forest_digest
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn((3000, 8), generator=g)
+    y = (X[:, 0] * 2 + X[:, 1]).double()
+    df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
+    m = RandomForestRegressor(numTrees=3, maxDepth=4, seed=1).fit(df)
+    f = m._forest
+    assert f._pending  # deferred past fit
+    c = copy.deepcopy(f)  # a copy settles the original first and carries no pending work
+    assert not f._pending and not c._pending
+    assert forest_digest(c) == forest_digest(f)
+    m2 = RandomForestRegressor(numTrees=3, maxDepth=4, seed=1).fit(df)
+    assert m2._forest._pending
+    n = len(m2._forest.feat)  # any node-list read settles
+    assert not m2._forest._pending and n == len(f.feat)
+    assert forest_digest(m2._forest) == forest_digest(f)
