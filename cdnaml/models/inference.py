@@ -55,10 +55,19 @@ class ForestPredictor:
         key = str(dev)
         if key not in self._dev:
             from ..ops import kernels as K
-            # async pinned uploads: a pageable torch.tensor(..., device=) copy waits for the queue to drain
-            tw, bb = K.upload(dev, self.tw_host.reshape(-1), np.asarray(0.0 if self.base is None else self.base,
-                                                                          np.float32).reshape(-1))
-            heap = self.forest.heap_arrays(dev, self.kind) if (dev.type == "cuda" and self.forest.K == 1) else None
+            f = self.forest
+            base_np = np.asarray(0.0 if self.base is None else self.base, np.float32).reshape(-1)
+            pre = getattr(f, "_heap_np", None)
+            hkey = ("heap", str(dev), self.kind)
+            if (dev.type == "cuda" and f.K == 1 and self.kind == "value" and pre is not None and hkey not in f._dev
+                    and pre[0].shape[0] == len(f.roots)):
+                # the trainer-built heap table rides the same pinned staging block and copy as the tree weights
+                tw, bb, h_t, m_t = K.upload(dev, self.tw_host.reshape(-1), base_np, pre[0], np.zeros(8, np.int32))
+                f._dev[hkey] = (h_t, pre[1], m_t)
+            else:
+                # async pinned uploads: a pageable torch.tensor(..., device=) copy waits for the queue to drain
+                tw, bb = K.upload(dev, self.tw_host.reshape(-1), base_np)
+            heap = f.heap_arrays(dev, self.kind) if (dev.type == "cuda" and f.K == 1) else None
             b = None if self.base is None else bb
             self._dev[key] = (tw, heap, b)
         return self._dev[key]
