@@ -1302,6 +1302,7 @@ def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_glob
 
 
 SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "2048"))
+SEG_ROUND_FIT = __import__("os").environ.get("CDNAML_SEG_ROUND_FIT", "1") != "0"
 # wide-bin (80 < B <= 256, boosting) record levels: work items per level (x ceil(d / 64) feature blocks).  Every block
 # clears and flushes 64 features x B bins of LDS cells into the level histogram with global atomics, so at deep
 # boosting levels (fewer rows, the same number of blocks) the flush -- not the rows -- sets the level time
@@ -1320,14 +1321,36 @@ SEG_LANE_MAX_B = 256 if __import__("os").environ.get("CDNAML_SEG_WIDE", "1") != 
 REC_PAD = 128
 
 
-def _fill_chunk(segs: np.ndarray, chunk: int, B: int = 0) -> int:
+def _fill_chunk(segs: np.ndarray, chunk: int, B: int = 0, ncu: int = 0) -> int:
     """Shrink the rows-per-block chunk so a level with few rows still launches ~SEG_MIN_BLOCKS blocks
     (at 1.25e7 rows per GPU a level's 95K-row chunks made only ~100 blocks for 256 CUs).  With 2048 instead of
     1024 the per-rank shape of the 8-GPU point ran 22.6 -> 21.2 ms (the last round of blocks no longer idles
-    half the chip); wide-bin levels (B > 64: 128 KB LDS planes to clear and flush per block) keep 1024."""
-    total = int(np.asarray(segs, dtype=np.int64).reshape(-1, 3)[:, 1].clip(min=0).sum())
+    half the chip); wide-bin levels (B > 64: 128 KB LDS planes to clear and flush per block) keep 1024.
+
+    ncu > 0 (one block per CU, B <= 64): when the per-segment rounding leaves a last round of blocks less than
+    half full (2048 target blocks + one partial chunk per segment = 8 rounds + a sliver), the chunk grows -- up to
+    ``chunk`` -- just enough for the blocks to fit the whole rounds before it."""
+    lens = np.asarray(segs, dtype=np.int64).reshape(-1, 3)[:, 1].clip(min=0)
+    total = int(lens.sum())
     mb = SEG_MIN_BLOCKS if B <= 64 else min(SEG_MIN_BLOCKS, SEG_MIN_BLOCKS_WIDE)
-    return int(min(chunk, max(8192, -(-total // max(1, mb)))))
+    c0 = int(min(chunk, max(8192, -(-total // max(1, mb)))))
+    if ncu <= 0 or B > 64 or c0 >= chunk:
+        return c0
+    lens = lens[lens > 0]
+    blocks = int(((lens + c0 - 1) // c0).sum())
+    R, rem = divmod(blocks, ncu)
+    if R < 1 or rem == 0 or rem > ncu // 2:
+        return c0
+    lo, hi = c0, int(chunk)
+    if int(((lens + hi - 1) // hi).sum()) > R * ncu:
+        return c0
+    while lo < hi:  # smallest chunk whose blocks fit R rounds
+        mid = (lo + hi) // 2
+        if int(((lens + mid - 1) // mid).sum()) <= R * ncu:
+            hi = mid
+        else:
+            lo = mid + 1
+    return lo
 
 
 def _seg_work(segs: np.ndarray, chunk: int) -> np.ndarray:
@@ -1453,7 +1476,8 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
             # the six-items-per-wave kernel spreads a block's items over three copies of every cell (item i of the
             # chunk -> copy i % 3): each copy's 20-bit count holds a third of the chunk
             cap = 3 * cap - 1024
-        chunk = _fill_chunk(segs, min(SEG_HIST_CHUNK * (3 if rm_s10 and LANE10_CHUNK3 else 1), cap), B)
+        chunk = _fill_chunk(segs, min(SEG_HIST_CHUNK * (3 if rm_s10 and LANE10_CHUNK3 else 1), cap), B,
+                            _num_cus(bins.device) if (SEG_ROUND_FIT and rm_s10 and bins.is_cuda) else 0)
         work = _seg_work(segs, chunk)
         if len(work) == 0:
             if out is not None:
@@ -1536,17 +1560,15 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
             rows = (-(-n // C) + 63) // 64 * 64
             C = (n + rows - 1) // rows
     if CODES_ROUND_FILL and C * bpc < 64 * _num_cus(codes.device):
-        # one block per CU: grow the chunk count to the next whole round of blocks (at most +25 %, +100 % for the
-        # few big blocks of a boosting level), so the last round is not a handful of blocks on an otherwise idle
-        # chip (1.25e7 rows x 20 trees: 1040 -> 1280 blocks; GBDT 1e8 rows: 382 -> 512)
+        # one block per CU: spread the rows over as many chunks as the rounds of blocks already needed can hold,
+        # so the last round is full instead of a fraction of the chip (1.25e7 rows x 20 trees: 640 blocks in 2.5
+        # rounds -> 760 in 2.97, 19.2 -> 18.9 ms per step; an exact multiple of the CUs, 1280 blocks in 5
+        # rounds, pays each block's 100 KB LDS clear + flush twice as often)
         ncu = _num_cus(codes.device)
-        C2 = C
-        cap = C * 2 if wide else C * 5 // 4
-        while (C2 * bpc) % ncu and C2 < cap:
-            C2 += 1
-        if (C2 * bpc) % ncu == 0:
-            C = C2
-            rows = (-(-n // C) + 63) // 64 * 64
+        rounds = -(-(C * bpc) // ncu)
+        C2 = max(C, (rounds * ncu) // bpc)
+        if C2 > C:
+            rows = (-(-n // C2) + 63) // 64 * 64
             C = (n + rows - 1) // rows
     # XCD-aware order: block b runs on XCD b % 8; the slots (trees) of row chunk c are consecutive blocks of
     # XCD c % 8, so their row-line gathers and label reads share that XCD's L2
