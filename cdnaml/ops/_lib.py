@@ -214,7 +214,8 @@ _SIGS = {
                          c_int),
     "cdna_cast_absmax": ([c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_normal_f32": ([c_void_p, c_int64, c_uint64, c_uint64, c_uint32, c_void_p], c_int),
-    "cdna_poisson": ([c_void_p, c_int, c_int64, c_uint64, c_uint64, c_double, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_poisson": ([c_void_p, c_int, c_int64, c_uint64, c_uint64, c_double, c_void_p, c_void_p, c_int, c_void_p],
+                     c_int),
     "cdna_reg_metrics": ([c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_score_hist": ([c_void_p, c_void_p, c_int64, c_double, c_double, c_int, c_void_p, c_void_p], c_int),
     "cdna_kmeans_step": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_void_p,

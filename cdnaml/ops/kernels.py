@@ -134,7 +134,7 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
     seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     if device.type == "cuda":
         out = torch.empty((T, n), dtype=torch.uint8, device=device)
-        _lib.check(_lib.lib().cdna_poisson(_ptr(out), T, n, seed, int(offset), float(rate), None, None,
+        _lib.check(_lib.lib().cdna_poisson(_ptr(out), T, n, seed, int(offset), float(rate), None, None, 0,
                                            _stream(device)), "cdna_poisson")
         return out
     return torch.from_numpy(_philox.poisson(T, n, seed, int(offset), float(rate)))
@@ -143,7 +143,13 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
 POISSON_CODES = __import__("os").environ.get("CDNAML_POISSON_CODES", "1") != "0"
 
 
-POISSON_STREAM = __import__("os").environ.get("CDNAML_POISSON_STREAM", "main")
+# where the forest's bootstrap draws run (profiles/r4/prologue_ab.md): "main" -- in series right before the
+# binning; "side" -- the side stream at the same point; "auto" -- draws of at most POISSON_EARLY_MAX (T x rows)
+# start on the side stream with the fit (grid bounded to POISSON_EARLY_BLOCKS: beside the quantile sample's
+# latency-bound kernels, without keeping its sort's 1024-thread blocks off the CUs), larger ones in series
+POISSON_STREAM = __import__("os").environ.get("CDNAML_POISSON_STREAM", "auto")
+POISSON_EARLY_MAX = float(__import__("os").environ.get("CDNAML_POISSON_EARLY_MAX", "5e8"))
+POISSON_EARLY_BLOCKS = int(__import__("os").environ.get("CDNAML_POISSON_EARLY_BLOCKS", "512"))
 
 
 class BootstrapCodes:
@@ -152,12 +158,13 @@ class BootstrapCodes:
     the kernel (``wmax()`` waits for that copy only).  ``weights()`` derives the uint8 multiplicities for the
     paths that need them (bit-identical to poisson_weights)."""
 
-    def __init__(self, T: int, n: int, seed: int, offset: int, rate: float, device):
+    def __init__(self, T: int, n: int, seed: int, offset: int, rate: float, device, grid_blocks: int = 0):
         dev = torch.device(device)
         self.codes = torch.empty((T, n), dtype=torch.int16, device=dev)
         wm = torch.zeros(1, dtype=torch.int32, device=dev)
         _lib.check(_lib.lib().cdna_poisson(None, T, n, int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset), float(rate),
-                                           _ptr(self.codes), _ptr(wm), _stream(dev)), "cdna_poisson(codes)")
+                                           _ptr(self.codes), _ptr(wm), int(grid_blocks), _stream(dev)),
+                   "cdna_poisson(codes)")
         self._wmax = _PendingScalar(wm, torch.cuda.current_stream(dev))
 
     def wmax(self) -> int:

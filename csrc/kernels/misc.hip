@@ -432,7 +432,7 @@ CDNA_API int cdna_codes_init(const uint8_t* w, int64_t total, uint16_t* codes, u
 // format) written straight from the draws, and atomicMax of the weights into *wmax (zeroed by the caller) --
 // no uint8 weights array, no codes_init pass, no separate max reduction.
 CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_t offset, double rate,
-                          uint16_t* codes, unsigned* wmax, hipStream_t st) {
+                          uint16_t* codes, unsigned* wmax, int grid_blocks, hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
   if (codes && !wmax) return (int)hipErrorInvalidValue;
   PoissonCdf cdf;
@@ -453,10 +453,12 @@ CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_
   // keeps a co-running kernel of 1024-thread blocks (the quantile sort) waiting for whole CUs to drain.
   // Default unbounded: the engine queues the draws in series, where T x 1024 blocks measured 2.24 ms vs 2.64 ms
   // for 2048 blocks at 1e8 rows x 20 trees (profiles/r4/prologue_ab.md).
-  static const int max_blocks = [] {
+  // grid_blocks > 0: the caller's bound (draws queued beside the fit's prologue on a side stream)
+  static const int env_blocks = [] {
     const char* e = getenv("CDNAML_POISSON_BLOCKS");
     return e ? atoi(e) : 0;
   }();
+  const int max_blocks = grid_blocks > 0 ? grid_blocks : env_blocks;
   unsigned gx = grid_for(n / 4 + 2, 256, 1024);
   if (max_blocks > 0) {
     const unsigned cap = (unsigned)((max_blocks + T - 1) / T);
