@@ -1132,7 +1132,7 @@ class ForestTrainer:
         """Checked build: the device decode equals the host decode the forest was built from (bin sets compared
         by content: the host numbers them densely, the device by node)."""
         tfn = np.searchsorted(n_tree, np.arange(T), side="left").astype(np.int32)
-        got = {k: v.cpu().numpy() for k, v in dec.items()}
+        got = {k: v.cpu().numpy() for k, v in dec.items() if v is not None}
         sp = split_feat >= 0
         ok = (np.array_equal(got["split_feat"], split_feat) and np.array_equal(got["split_bin"][sp], split_bin[sp])
               and np.array_equal(got["child"], child) and np.array_equal(got["tfirst_next"], tfn)
