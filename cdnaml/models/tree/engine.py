@@ -487,20 +487,31 @@ class Forest:
         st["_pending"] = []
         return st
 
+    def lists(self) -> dict:
+        """The node-list fields (settled) as a dict name -> list, for loops that touch many nodes (one settle check
+        instead of one property call per access)."""
+        if self._pending and not self._settling:
+            self.settle()
+        d = self.__dict__
+        return {n: d["_" + n] for n in _NODE_FIELDS}
+
     def add(self, value, weight, depth, impurity=float("nan")) -> int:
-        i = len(self.feat)
-        self.feat.append(-1)
-        self.thr.append(0.0)
-        self.bin.append(0)
-        self.left.append(-1)
-        self.right.append(-1)
-        self.catmask.append(np.zeros(8, dtype=np.uint32))
-        self.is_cat.append(False)
-        self.value.append(np.asarray(value, dtype=np.float64).reshape(-1))
-        self.weight.append(float(weight))
-        self.gain.append(0.0)
-        self.impurity.append(float(impurity))
-        self.depth.append(depth)
+        if self._pending and not self._settling:
+            self.settle()
+        d = self.__dict__
+        i = len(d["_feat"])
+        d["_feat"].append(-1)
+        d["_thr"].append(0.0)
+        d["_bin"].append(0)
+        d["_left"].append(-1)
+        d["_right"].append(-1)
+        d["_catmask"].append(np.zeros(8, dtype=np.uint32))
+        d["_is_cat"].append(False)
+        d["_value"].append(np.asarray(value, dtype=np.float64).reshape(-1))
+        d["_weight"].append(float(weight))
+        d["_gain"].append(0.0)
+        d["_impurity"].append(float(impurity))
+        d["_depth"].append(depth)
         return i
 
     def add_many(self, values: np.ndarray, weights: np.ndarray, depth: int, impurity: np.ndarray) -> np.ndarray:
@@ -561,12 +572,14 @@ class Forest:
         return len(self.feat)
 
     def tree_nodes(self, t: int) -> List[int]:
+        L = self.lists()
+        feat, left, right = L["feat"], L["left"], L["right"]
         out, stack = [], [self.roots[t]]
         while stack:
             i = stack.pop()
             out.append(i)
-            if self.feat[i] >= 0:
-                stack.extend([self.right[i], self.left[i]])
+            if feat[i] >= 0:
+                stack.extend([right[i], left[i]])
         return out
 
     def _layout(self, feat: Optional[np.ndarray] = None):
@@ -887,8 +900,9 @@ def _settled_list(name: str):
     return property(get, set_)
 
 
-for _name in ("feat", "thr", "bin", "left", "right", "catmask", "is_cat", "value", "weight", "gain", "impurity",
-              "depth"):
+_NODE_FIELDS = ("feat", "thr", "bin", "left", "right", "catmask", "is_cat", "value", "weight", "gain", "impurity",
+                "depth")
+for _name in _NODE_FIELDS:
     setattr(Forest, _name, _settled_list(_name))
 del _name
 

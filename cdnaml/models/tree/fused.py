@@ -59,26 +59,63 @@ def estimator_kind(est) -> Optional[Tuple[str, bool]]:
     return None
 
 
-def truncate_forest(forest: Forest, num_trees: int, max_depth: int) -> Forest:
+def forest_arrays(forest: Forest) -> dict:
+    """numpy copies of a finished forest's scalar node fields (+ the object lists), for several truncate_forest
+    calls on the same forest (the list -> array conversions are most of one cut's cost)."""
+    F = forest.lists()
+    A = {n: np.asarray(F[n], dtype=np.float64 if n in ("thr", "weight", "gain", "impurity") else np.int64)
+         for n in ("feat", "left", "right", "thr", "bin", "weight", "gain", "impurity", "depth")}
+    A.update(catmask=F["catmask"], is_cat=F["is_cat"], value=F["value"])
+    return A
+
+
+def truncate_forest(forest: Forest, num_trees: int, max_depth: int, arrays: Optional[dict] = None) -> Forest:
     """The first ``num_trees`` trees cut at depth ``max_depth`` (depth-D nodes become leaves with the value
-    they already store), renumbered compactly."""
+    they already store), renumbered compactly (per tree, by original id).
+
+    One level-synchronous numpy sweep over the kept nodes instead of a Python walk per node: the fused tuner cuts
+    every fold's 100-tree depth-10 forest for each of the grid's maps (L07's 3 x 3 grid: 27 cuts of up to 2e5
+    nodes, ~3.5 s of per-node attribute traffic before)."""
+    A = arrays if arrays is not None else forest_arrays(forest)
+    feat, left, right = A["feat"], A["left"], A["right"]
+    roots = np.asarray(forest.roots[:num_trees], dtype=np.int64)
+    nodes, trees, inner = [], [], []
+    fr, tr, level = roots, np.arange(len(roots), dtype=np.int64), 0
+    while len(fr):
+        inn = (feat[fr] >= 0) & (level < max_depth)
+        nodes.append(fr)
+        trees.append(tr)
+        inner.append(inn)
+        ii, ti = fr[inn], tr[inn]
+        fr, tr = np.concatenate([left[ii], right[ii]]), np.concatenate([ti, ti])
+        level += 1
     out = Forest(forest.K)
-    for t in range(num_trees):
-        r = forest.roots[t]
-        base = forest.depth[r]
-        keep = [i for i in forest.tree_nodes(t) if forest.depth[i] - base <= max_depth]
-        pos = {g: j + len(out.feat) for j, g in enumerate(keep)}
-        for g in keep:
-            j = out.add(forest.value[g], forest.weight[g], forest.depth[g], forest.impurity[g])
-            inner = forest.feat[g] >= 0 and forest.depth[g] - base < max_depth
-            if inner:
-                out.feat[j], out.thr[j], out.bin[j] = forest.feat[g], forest.thr[g], forest.bin[g]
-                out.is_cat[j], out.catmask[j], out.gain[j] = forest.is_cat[g], forest.catmask[g], forest.gain[g]
-        for g in keep:
-            j = pos[g]
-            if out.feat[j] >= 0:
-                out.left[j], out.right[j] = pos[forest.left[g]], pos[forest.right[g]]
-        out.roots.append(pos[r])
+    if not nodes:
+        return out
+    g, tt, inn = np.concatenate(nodes), np.concatenate(trees), np.concatenate(inner)
+    order = np.lexsort((g, tt))
+    g, inn = g[order], inn[order]
+    newid = np.full(len(feat), -1, dtype=np.int64)
+    newid[g] = np.arange(len(g), dtype=np.int64)
+    O = out.lists()
+    gl, il = g.tolist(), inn.tolist()
+    O["feat"].extend(np.where(inn, feat[g], -1).tolist())
+    O["thr"].extend(np.where(inn, A["thr"][g], 0.0).tolist())
+    O["bin"].extend(np.where(inn, A["bin"][g], 0).tolist())
+    O["left"].extend(np.where(inn, newid[np.where(inn, left[g], 0)], -1).tolist())
+    O["right"].extend(np.where(inn, newid[np.where(inn, right[g], 0)], -1).tolist())
+    zero = np.zeros(8, dtype=np.uint32)
+    zero.flags.writeable = False
+    cm, ic = A["catmask"], A["is_cat"]
+    O["catmask"].extend([cm[x] if i else zero for x, i in zip(gl, il)])
+    O["is_cat"].extend([bool(ic[x]) and i for x, i in zip(gl, il)])
+    val = A["value"]
+    O["value"].extend([val[x] for x in gl])
+    O["weight"].extend(A["weight"][g].tolist())
+    O["gain"].extend(np.where(inn, A["gain"][g], 0.0).tolist())
+    O["impurity"].extend(A["impurity"][g].tolist())
+    O["depth"].extend(A["depth"][g].tolist())
+    out.roots.extend(newid[roots].tolist())
     return out
 
 
@@ -222,10 +259,15 @@ class FusedTreeTuner:
             Tm = max((e.getNumTrees() if self.kind == "rf" else 1) for e in es)
             Dm = max(e.getMaxDepth() for e in es)
             forest, dd = self.fit_forest(preps[key], e0, Tm, Dm)
+            arrays = None
             for j, e in zip(grp, es):
                 T = e.getNumTrees() if self.kind == "rf" else 1
                 D = e.getMaxDepth()
-                sub = forest if (T == Tm and D == Dm) else truncate_forest(forest, T, D)
+                if T == Tm and D == Dm:
+                    sub = forest
+                else:
+                    arrays = arrays if arrays is not None else forest_arrays(forest)
+                    sub = truncate_forest(forest, T, D, arrays)
                 tm = self.model(e, sub, dd)
                 if pm is not None:
                     full = PipelineModel(list(pm.stages) + [tm])
