@@ -61,6 +61,8 @@ SPEC_THRESHOLDS = __import__("os").environ.get("CDNAML_SPEC_THRESHOLDS", "1") !=
 HEAP_PREDICT = __import__("os").environ.get("CDNAML_HEAP_PREDICT", "1") != "0"
 # row-record partition gathers split bins from the row-major copy (one line per row) instead of [G][n]
 PARTITION_RM = __import__("os").environ.get("CDNAML_PARTITION_RM", "0") != "0"
+# levels below the u16 codes (binary classification deeper than 8) keep the record histograms via node ids
+DEEP_REC = __import__("os").environ.get("CDNAML_DEEP_REC", "1") != "0"
 # boosting margins updated by the level partitions (ForestTrainer.train(margin=...)) instead of a tree walk
 GBDT_MARGIN = __import__("os").environ.get("CDNAML_GBDT_MARGIN", "1") != "0"
 # feature-subset forests: accumulate only each node's sampled features in segment mode.  Opt-in: measured
@@ -1466,6 +1468,8 @@ class ForestTrainer:
         w_total = None    # sum of the root weights (bounds every level's records)
         rec_buf = None
         root_ids = [None] * T
+        deep_rec = False  # set at the switch to node ids (deep_switch)
+        wdeep = None
         pending = []  # deferred forest bookkeeping of the previous level (see flush points)
 
         def flush():
@@ -1573,6 +1577,20 @@ class ForestTrainer:
                                         seg_end=seg_end)
                         hist_raw_scale = mseg_raw
                     del perm, v0p, v1p, wp
+                elif deep_rec and len(build_ids) and \
+                        np.bincount(a_tree, minlength=T).max() <= K.NODE_COMPACT_MAX_LOC:
+                    # levels below the u16 codes (binary classification deeper than 8): the built rows' packed
+                    # records from the node ids, then the same record histograms as the shallow levels (the
+                    # node-id kernel re-read every row once per LDS-sized slot group: ~290 ms per level at
+                    # 1e7 rows x 100 trees)
+                    perm, sg = K.node_compact(node, wdeep, tfirst.numpy(), slot_of, len(build_ids),
+                                              stats_rows["v1"], mseg_scales[1])
+                    sb = np.concatenate([sg, np.arange(len(build_ids), dtype=np.int64)[:, None]], 1)
+                    rm, s10 = data.record_rows() if dev.type == "cuda" else (None, False)
+                    Hb = K.seg_hist(data.bins, d, B, perm, None, None, None, sb, len(build_ids), wmax,
+                                    mseg_scales, bins_rm=rm, interleave=True, rec=True, raw=True, rm_s10=s10)
+                    hist_raw_scale = mseg_raw
+                    del perm
                 elif use_seg:
                     sb = np.stack([segs[build_ids, 0], segs[build_ids, 1], slot_of[build_ids].astype(np.int64)], 1)
                     Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax, seg_scales,
@@ -1834,8 +1852,10 @@ class ForestTrainer:
             if len(nl) and deep_switch and use_codes and depth + 1 >= 8:
                 # the next level can hold more than 255 nodes per tree: leave the u16 codes for node ids
                 # (active index of the node, -1 = done), partitioned and histogrammed by the node-id kernels
-                node, _ = K.decode_codes(codes, tfirst.to(codes.device))
+                node, wdeep = K.decode_codes(codes, tfirst.to(codes.device))
                 node = node.contiguous()
+                # below level 8 the record histograms continue from the node ids (K.node_compact)
+                deep_rec = DEEP_REC and use_mseg and rec_ok
                 use_codes = use_mseg = False
                 codes = None
             if len(nl):

@@ -1898,6 +1898,50 @@ def codes_compact(codes: torch.Tensor, tfirst: torch.Tensor, build_slot: np.ndar
     return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
 
 
+def node_compact(node: torch.Tensor, w: torch.Tensor, tfirst: np.ndarray, build_slot: np.ndarray, S: int,
+                 v1: torch.Tensor, rec_scale: float):
+    """The packed item records of the rows of a level's built nodes from node ids (the levels below the u16
+    codes: node [T, n] int32 global active index, -1 = done; w [T, n] uint8), one segment per slot ->
+    (rec int64, segs [S, 2] {start, len}) -- codes_compact(rec_scale=...)'s output for these rows (the order
+    inside a segment is unspecified; the fixed-point histograms do not depend on it)."""
+    T, n = node.shape
+    dev = node.device
+    A = len(build_slot)
+    bs = np.asarray(build_slot, dtype=np.int32)
+    tf_h = np.asarray(tfirst, dtype=np.int64)
+    if not _native(node):
+        slot_t = torch.from_numpy(np.concatenate([bs, [-1]]).astype(np.int64))
+        ids = torch.where(node >= 0, node.long(), torch.full_like(node, A, dtype=torch.int64)).clamp_max(A)
+        slot = slot_t[ids]
+        flat = slot.reshape(-1)
+        keep = torch.nonzero(flat >= 0).flatten()
+        order = keep[torch.argsort(flat[keep], stable=True)]
+        rows = order % n
+        lens = np.bincount(flat[keep].numpy(), minlength=S)[:S].astype(np.int64)
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if S else np.zeros(0, np.int64)
+        wts = w.reshape(-1)[order].to(torch.int64)
+        return rec_encode(rows, wts, _quant(v1[rows], rec_scale, True)), np.stack([starts, lens], 1)
+    L = _lib.lib()
+    nloc = np.diff(np.concatenate([tf_h, [A]])) if T else np.zeros(0, np.int64)
+    max_loc = int(nloc.max()) if T else 0
+    tf, bs_t = upload(dev, tf_h.astype(np.int32), bs)
+    v1c = v1.float().contiguous()
+    cnt = torch.zeros(max(S, 1), dtype=torch.int32, device=dev)
+    _lib.check(L.cdna_node_compact(1, _ptr(node), _ptr(w), n, T, A, _ptr(tf), _ptr(bs_t), _ptr(v1c), _ptr(cnt), None,
+                                   float(rec_scale), max_loc, _stream(dev)), "cdna_node_compact(count)")
+    lens = cnt.cpu().numpy()[:S].astype(np.int64)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if S else np.zeros(0, np.int64)
+    total = int(lens.sum())
+    assert total < 2 ** 31
+    rec = torch.empty(total + REC_PAD, dtype=torch.int64, device=dev)[:total]  # readable tail
+    if total:
+        cur, = upload(dev, np.concatenate([starts, [0]]).astype(np.int32))
+        _lib.check(L.cdna_node_compact(2, _ptr(node), _ptr(w), n, T, A, _ptr(tf), _ptr(bs_t), _ptr(v1c), _ptr(cur),
+                                       _ptr(rec), float(rec_scale), max_loc, _stream(dev)), "cdna_node_compact(scatter)")
+    return rec, np.stack([starts, lens], 1)
+
+
+NODE_COMPACT_MAX_LOC = 1024  # seg.hip kNodeCompactLoc
 COMPACT_W = __import__("os").environ.get("CDNAML_COMPACT_W", "1") != "0"
 # record compaction without a host round trip before the scatter (device segment starts, totals copied back
 # behind the scatter kernel)

@@ -1121,6 +1121,90 @@ __global__ __launch_bounds__(256) void codes_compact_kernel(const CompactArgs a)
   }
 }
 
+// Node-id twin of codes_compact_kernel for forest levels deeper than the u16 codes reach (binary classification
+// below level 8: up to 512 active nodes per tree): node ids int32 [T][n] (global active index, -1 = done) and
+// the bootstrap weights uint8 [T][n] in, the level's packed item records (row | w << 31 | (q + 2^23) << 39) out,
+// one segment per built slot -- so the deep levels take the same record histograms (seg_hist_lane10) as the
+// shallow ones instead of the node-id kernel, which re-read every row once per LDS-sized slot group.
+constexpr int kNodeCompactLoc = 1024;  // active nodes per tree
+struct NodeCompactArgs {
+  const int* node;
+  const uint8_t* w;
+  int64_t n;
+  int T, A;
+  const int* tfirst;
+  const int* build_slot;  // [A]
+  const float* v1;
+  int* cnt;               // pass 1: [S] totals; pass 2: [S] write cursors (segment starts)
+  uint64_t* rec_out;
+  float qs1;
+};
+
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void node_compact_kernel(const NodeCompactArgs a) {
+  __shared__ int s_slot[kNodeCompactLoc], s_cnt[kNodeCompactLoc], s_base[kNodeCompactLoc];
+  const int t = blockIdx.y;
+  const int tf = a.tfirst[t];
+  const int nloc = (t + 1 < a.T ? a.tfirst[t + 1] : a.A) - tf;  // <= kNodeCompactLoc (host-checked)
+  for (int i = threadIdx.x; i < kNodeCompactLoc; i += 256) {
+    s_slot[i] = i < nloc ? a.build_slot[tf + i] : -1;
+    s_cnt[i] = 0;
+  }
+  __syncthreads();
+  const int* nd = a.node + (int64_t)t * a.n;
+  const uint8_t* wt = a.w + (int64_t)t * a.n;
+  const int64_t per = ((a.n + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
+  const int64_t r0 = (int64_t)blockIdx.x * per;
+  const int64_t r1 = r0 + per < a.n ? r0 + per : a.n;
+  constexpr int U = 8;
+  auto local = [&](int id) -> int {  // the row's local node when it is in a built slot, else -1
+    const int l = id - tf;
+    return (id >= 0 && l >= 0 && l < nloc && s_slot[l] >= 0) ? l : -1;
+  };
+  for (int64_t rb = r0; rb < r1; rb += 256 * U) {
+    int id[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = rb + u * 256 + threadIdx.x;
+      id[u] = r < r1 ? nd[r] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int l = local(id[u]);
+      if (l >= 0) atomicAdd(&s_cnt[l], 1);
+    }
+  }
+  __syncthreads();
+  if (!SCATTER) {
+    for (int i = threadIdx.x; i < nloc; i += 256)
+      if (s_cnt[i]) atomicAdd(&a.cnt[s_slot[i]], s_cnt[i]);
+    return;
+  }
+  for (int i = threadIdx.x; i < nloc; i += 256) {
+    s_base[i] = s_cnt[i] ? atomicAdd(&a.cnt[s_slot[i]], s_cnt[i]) : 0;
+    s_cnt[i] = 0;
+  }
+  __syncthreads();
+  for (int64_t rb = r0; rb < r1; rb += 256 * U) {
+    int id[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = rb + u * 256 + threadIdx.x;
+      id[u] = r < r1 ? nd[r] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = rb + u * 256 + threadIdx.x;
+      const int l = local(id[u]);
+      if (l < 0) continue;
+      const int pos = s_base[l] + atomicAdd(&s_cnt[l], 1);
+      int q1 = (int)rintf(a.v1[r] * a.qs1);
+      q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+      a.rec_out[pos] = (uint64_t)r | ((uint64_t)wt[r] << 31) | ((uint64_t)(uint32_t)(q1 + kPackQ) << 39);
+    }
+  }
+}
+
 // Wave-owned variant for few built nodes per tree (KB <= 16, every RF level of
 // depth <= 5 and the shallow levels of deeper forests).  rocprofv3 on the
 // peeling kernel: ~80 wave instructions per 64 records and 71 % of wave time
@@ -1652,6 +1736,21 @@ CDNA_API int cdna_codes_compact(int pass, const uint16_t* codes, int64_t n, int 
   const dim3 grid((unsigned)per_tree, (unsigned)T);
   if (pass == 1) hipLaunchKernelGGL(codes_compact_kernel<false>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(codes_compact_kernel<true>, grid, dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// pass 1: counts into cnt [S]; pass 2: records from the cursors in cnt (segment starts).  Every tree holds at
+// most kNodeCompactLoc active nodes (host-checked, else hipErrorInvalidValue).
+CDNA_API int cdna_node_compact(int pass, const int* node, const uint8_t* w, int64_t n, int T, int A, const int* tfirst,
+                               const int* build_slot, const float* v1, int* cnt, uint64_t* rec_out, float qs1,
+                               int max_loc, hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  if (max_loc > kNodeCompactLoc || n >= (int64_t)1 << 31 || (pass == 2 && !rec_out)) return (int)hipErrorInvalidValue;
+  NodeCompactArgs a{node, w, n, T, A, tfirst, build_slot, v1, cnt, rec_out, qs1};
+  int64_t nb = (n + 4095) / 4096;
+  const dim3 grid((unsigned)(nb < 512 ? nb : 512), (unsigned)T);
+  if (pass == 1) hipLaunchKernelGGL(node_compact_kernel<false>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(node_compact_kernel<true>, grid, dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

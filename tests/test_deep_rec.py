@@ -1,0 +1,47 @@
+"""Binary classification forests deeper than the u16 row codes (levels >= 8 on node ids): the record histograms
+continue through K.node_compact (seg.hip node_compact_kernel) instead of the node-id histogram kernel; the forests
+must be bit-identical either way (class counts are exact integers on both paths)."""
+import numpy as np
+import pytest
+import torch
+
+
+def _devices():
+    return ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+@pytest.mark.parametrize("device", _devices())
+@pytest.mark.parametrize("depth,trees", [(10, 6), (11, 3)])
+def test_deep_record_histograms_equal_node_id_kernel(device, depth, trees, monkeypatch):
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import cdnaml
+    from cdnaml.models.tree import engine
+    from cdnaml.ml.classification import RandomForestClassifier
+    from cdnaml.utils.synthetic import forest_digest
+    from tests.conftest import session_device
+    with session_device(device):
+        spark = cdnaml.SparkSession.builder.getOrCreate()
+        g = torch.Generator().manual_seed(depth)
+        n = 60_000 if device == "cpu" else 400_000
+        X = torch.randn((n, 12), generator=g)
+        logit = X[:, 0] * 2 - X[:, 1] + torch.sin(3 * X[:, 2]) + 0.5 * X[:, 3] * X[:, 4]
+        y = (logit + 0.3 * torch.randn(n, generator=g) > 0).double()
+        df = spark.createDataFrameFromLocalTensors({"features": X.to(device), "label": y.to(device)})
+        est = RandomForestClassifier(numTrees=trees, maxDepth=depth, maxBins=32, seed=5)
+        calls = {"n": 0}
+        orig = engine.K.node_compact
+
+        def counted(*a, **k):
+            calls["n"] += 1
+            return orig(*a, **k)
+        monkeypatch.setattr(engine.K, "node_compact", counted)
+        digests = []
+        try:
+            for flag in (True, False):
+                monkeypatch.setattr(engine, "DEEP_REC", flag)
+                digests.append(forest_digest(est.fit(df)._forest))
+        finally:
+            spark.stop()
+        assert calls["n"] >= 1  # the deep levels took the record path
+        assert digests[0] == digests[1]
