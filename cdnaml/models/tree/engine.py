@@ -63,6 +63,11 @@ HEAP_PREDICT = __import__("os").environ.get("CDNAML_HEAP_PREDICT", "1") != "0"
 PARTITION_RM = __import__("os").environ.get("CDNAML_PARTITION_RM", "0") != "0"
 # levels below the u16 codes (binary classification deeper than 8) keep the record histograms via node ids
 DEEP_REC = __import__("os").environ.get("CDNAML_DEEP_REC", "1") != "0"
+# regression forests (T > 1) deeper than 8 levels: the packed record levels down to 8, then node ids (as binary
+# classification); 0 = the node-id histograms from the root (round 3).  RF 20 trees depth 10 at 1e7 x 100:
+# 376 -> 88 ms per fit.  One tree keeps the permutation segment path (seg.hip, any depth): 14 ms at depth 12
+# against 38 ms switched (profiles/r4/deep_reg_ab.md)
+DEEP_REG = __import__("os").environ.get("CDNAML_DEEP_REG", "1") != "0"
 # boosting margins updated by the level partitions (ForestTrainer.train(margin=...)) instead of a tree walk
 GBDT_MARGIN = __import__("os").environ.get("CDNAML_GBDT_MARGIN", "1") != "0"
 # feature-subset forests: accumulate only each node's sampled features in segment mode.  Opt-in: measured
@@ -1393,7 +1398,7 @@ class ForestTrainer:
         # exactly the class histograms of the node-id / codes kernels, so the forest does not change.  Forests
         # deeper than 8 levels (u16 codes hold <= 255 nodes per tree) switch to node ids at level 8
         cls2 = self.classification and self.C == 2 and MSEG_CLS
-        deep_switch = cls2 and p.max_depth > 8
+        deep_switch = (cls2 or (not self.classification and DEEP_REG and T > 1)) and p.max_depth > 8
         if cls2:
             stats_rows = dict(stats_rows, v1=stats_rows["label"].float())
         mseg_ok = (USE_MSEG and USE_CODES and (T > 1 or (MSEG_T1 and stats_rows.get("v0") is None)) and
@@ -1401,7 +1406,8 @@ class ForestTrainer:
                    T * self.n_max < 2 ** 31 and data.n_global > 0)
         # ... and with per-node feature subsets (RandomForest) only each node's sampled features are
         # accumulated (packed statistics only: no v0)
-        subset_seg = mseg_ok and need_masks and MSEG_SUBSET and stats_rows.get("v0") is None
+        # (regression only: its float histograms skip the binary classification (W, W1) -> class counts step)
+        subset_seg = mseg_ok and need_masks and MSEG_SUBSET and stats_rows.get("v0") is None and not cls2
         use_sub = self._sub_hist_ok(mseg_ok, need_masks, stats_rows) and not subset_seg
         masked = need_masks and (HIST_MODE == "masked" or subset_seg or use_sub)
         subtract = not masked
@@ -1652,7 +1658,8 @@ class ForestTrainer:
                                            missing_bin=mb)
                 dec = None
                 host_p = None
-                if self._device_decode_ok(dev, use_codes, mb) and (depth + 1 < p.max_depth or margin_ok):
+                if self._device_decode_ok(dev, use_codes, mb) and (depth + 1 < p.max_depth or margin_ok) \
+                        and not (deep_switch and depth + 1 >= 8):
                     # the decisions leave for the host first (pinned, async): they arrive while the partition runs
                     src = torch.cat([so, tot], 1) if depth == 0 else so
                     host_p = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)

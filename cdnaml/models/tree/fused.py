@@ -158,7 +158,10 @@ class FusedTreeTuner:
         D = e.getMaxDepth()
         strategy = e.getFeatureSubsetStrategy() if self.kind == "rf" else "all"
         sub = resolve_subset(strategy, d, T, self.cls)
-        return tuple(vals) + (("subset", sub), ("bagged", T > 1), ("deep", (not self.cls) and D > 8))
+        # regression deeper than 8 takes the record path down to level 8 (engine.DEEP_REG): the depth-8 prefix of a
+        # deep forest is then the depth-8 forest, as for classification
+        from .engine import DEEP_REG
+        return tuple(vals) + (("subset", sub), ("bagged", T > 1), ("deep", (not self.cls) and D > 8 and (T == 1 or not DEEP_REG)))
 
     def groups(self, d: int) -> List[List[int]]:
         groups: Dict[tuple, List[int]] = {}

@@ -1,4 +1,4 @@
-"""Timing probe: RandomForestRegressor depth 10 (and 8) at 1e7 x 100, 20 trees (fit only)."""
+"""Timing probe: regression trees deeper than 8 levels at 1e7 x 100 (fit only; A/B with CDNAML_DEEP_REG)."""
 import os
 import sys
 import time
@@ -7,18 +7,20 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import cdnaml  # noqa: E402
-from cdnaml.models.regression import RandomForestRegressor  # noqa: E402
+from cdnaml.models.regression import DecisionTreeRegressor, RandomForestRegressor  # noqa: E402
 from cdnaml.utils.synthetic import regression_shard  # noqa: E402
 
 spark = cdnaml.SparkSession.builder.getOrCreate()
 X, y, _ = regression_shard(int(1e7), 100, 42, 0, 1, spark.device)
 df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
-for depth in (8, 10):
-    rf = RandomForestRegressor(numTrees=20, maxDepth=depth, maxBins=40, seed=42)
-    rf.fit(df)
+tag = os.environ.get("CDNAML_DEEP_REG", "1")
+for name, est in [("rf20 depth 8", RandomForestRegressor(numTrees=20, maxDepth=8, maxBins=40, seed=42)),
+                  ("rf20 depth 10", RandomForestRegressor(numTrees=20, maxDepth=10, maxBins=40, seed=42)),
+                  ("dt depth 12", DecisionTreeRegressor(maxDepth=12, maxBins=40, seed=42))]:
+    est.fit(df)
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(2):
-        m = rf.fit(df)
+        m = est.fit(df)
     torch.cuda.synchronize()
-    print(f"depth {depth}: {(time.perf_counter() - t) / 2 * 1e3:.1f} ms per fit, nodes {m.totalNumNodes}", flush=True)
+    print(f"DEEP_REG={tag} {name}: {(time.perf_counter() - t) / 2 * 1e3:.1f} ms per fit", flush=True)

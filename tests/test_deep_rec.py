@@ -45,3 +45,52 @@ def test_deep_record_histograms_equal_node_id_kernel(device, depth, trees, monke
             spark.stop()
         assert calls["n"] >= 1  # the deep levels took the record path
         assert digests[0] == digests[1]
+
+
+@pytest.mark.parametrize("device", _devices())
+@pytest.mark.parametrize("est_kind,depth,trees", [("rf", 10, 4), ("rf", 11, 2)])
+def test_deep_regression_prefix_is_depth8_forest(device, est_kind, depth, trees, monkeypatch):
+    """Regression forests deeper than 8 (engine.DEEP_REG): the record levels down to 8, then node ids + record histograms.
+    The depth-8 prefix of the deep forest is bit-identical to the depth-8 forest, and the deep levels improve the
+    training fit."""
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import cdnaml
+    from cdnaml.models.tree import engine
+    from cdnaml.models.tree.fused import truncate_forest
+    from cdnaml.ml.regression import DecisionTreeRegressor, RandomForestRegressor
+    from cdnaml.utils.synthetic import forest_digest
+    from tests.conftest import session_device
+    with session_device(device):
+        spark = cdnaml.SparkSession.builder.getOrCreate()
+        g = torch.Generator().manual_seed(depth)
+        n = 50_000 if device == "cpu" else 300_000
+        X = torch.randn((n, 10), generator=g)
+        y = (3 * X[:, 0] - X[:, 1] + torch.sin(4 * X[:, 2]) + X[:, 3] * X[:, 4]
+             + 0.2 * torch.randn(n, generator=g)).double()
+        df = spark.createDataFrameFromLocalTensors({"features": X.to(device), "label": y.to(device)})
+        calls = {"n": 0}
+        orig = engine.K.node_compact
+
+        def counted(*a, **k):
+            calls["n"] += 1
+            return orig(*a, **k)
+        monkeypatch.setattr(engine.K, "node_compact", counted)
+
+        def est(D):
+            if est_kind == "rf":
+                return RandomForestRegressor(numTrees=trees, maxDepth=D, maxBins=32, seed=3)
+            return DecisionTreeRegressor(maxDepth=D, maxBins=32, seed=3)
+        try:
+            deep = est(depth).fit(df)
+            assert calls["n"] >= 1  # the levels below 8 built record histograms from node ids
+            shallow = est(8).fit(df)
+            cut = truncate_forest(deep._forest, trees, 8)
+            assert forest_digest(cut) == forest_digest(shallow._forest)
+
+            def mse(m):
+                p = m.transform(df).select("prediction").toPandas()["prediction"].to_numpy()
+                return float(((p - y.numpy()) ** 2).mean())
+            assert mse(deep) < mse(shallow)
+        finally:
+            spark.stop()
