@@ -17,6 +17,8 @@ tag = os.environ.get("CDNAML_DEEP_REG", "1")
 for name, est in [("rf20 depth 8", RandomForestRegressor(numTrees=20, maxDepth=8, maxBins=40, seed=42)),
                   ("rf20 depth 10", RandomForestRegressor(numTrees=20, maxDepth=10, maxBins=40, seed=42)),
                   ("dt depth 12", DecisionTreeRegressor(maxDepth=12, maxBins=40, seed=42))]:
+    if len(sys.argv) > 1 and sys.argv[1] not in name:
+        continue
     est.fit(df)
     torch.cuda.synchronize()
     t = time.perf_counter()
