@@ -1165,7 +1165,7 @@ class ForestTrainer:
 
     # ------------------------------------------------------------ device-queued partition
     def _device_partition(self, so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n, v1, qs1, w_total,
-                          rec_buf, margin=None, catm=None):
+                          rec_buf, margin=None, catm=None, node=None):
         """Partition tables decoded on the device from the level's K6 decisions and the row partition queued right
         behind them (the GPU partitions while the decisions travel to the host; the host repeats the decode to
         build the forest and the next level, checked against the device's in the checked build).  With
@@ -1183,6 +1183,12 @@ class ForestTrainer:
             if em is not None:
                 em.plan(so, dec["child"])
         with _tr.span("tree.partition", depth=depth):
+            if node is not None:
+                # levels below the u16 codes: the node-id partition from the same device tables (child = the
+                # next level's global active index, as the host decode's)
+                K.partition(data.bins, node, dec["split_feat"], dec["split_bin"], dec["cat_off"],
+                            dec["masks"].reshape(-1), dec["child"])
+                return dec, em
             K.partition_codes(data.bins, codes, tf_d, dec["tfirst_next"], dec["split_feat"],
                               dec["split_bin"], dec["cat_off"], dec["masks"].reshape(-1), dec["child"],
                               bins_rm=data.row_major_bins() if PARTITION_RM else None, emit=em,
@@ -1658,8 +1664,10 @@ class ForestTrainer:
                                            missing_bin=mb)
                 dec = None
                 host_p = None
-                if self._device_decode_ok(dev, use_codes, mb) and (depth + 1 < p.max_depth or margin_ok) \
-                        and not (deep_switch and depth + 1 >= 8):
+                # (deep forests: not at the level that leaves the codes for node ids; below it on the node ids)
+                deep_ids = deep_switch and node is not None
+                if self._device_decode_ok(dev, use_codes or deep_ids, mb) and \
+                        (depth + 1 < p.max_depth or margin_ok) and not (deep_switch and use_codes and depth + 1 >= 8):
                     # the decisions leave for the host first (pinned, async): they arrive while the partition runs
                     src = torch.cat([so, tot], 1) if depth == 0 else so
                     host_p = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
@@ -1673,7 +1681,8 @@ class ForestTrainer:
                                w_total is not None and data.bins_s10 is not None and not margin_ok)
                     dec, em = self._device_partition(so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n,
                                                      stats_rows["v1"], mseg_scales[1] if use_mseg else 1.0,
-                                                     w_total, rec_buf, margin=margin if margin_ok else None)
+                                                     w_total, rec_buf, margin=margin if margin_ok else None,
+                                                     node=node if deep_ids else None)
                     if em is not None:
                         rec_buf = em.rec
                         emits.append(em)
@@ -1699,8 +1708,9 @@ class ForestTrainer:
                 kk = tot.shape[1]
                 src = torch.cat([so, cm.double()] + ([tot] if depth == 0 else []), 1)
                 reg_ex = not self.classification and kk == 2  # variance regression with categorical features
-                if (cls2 or reg_ex) and use_codes and DEVICE_DECODE and depth + 1 < p.max_depth \
-                        and not (deep_switch and depth + 1 >= 8):
+                deep_ids = deep_switch and node is not None
+                if (cls2 or reg_ex) and (use_codes or deep_ids) and DEVICE_DECODE and depth + 1 < p.max_depth \
+                        and not (deep_switch and use_codes and depth + 1 >= 8):
                     # binary classification / categorical regression on the codes: the same device decode +
                     # partition (+ record emission) as numeric regression, queued behind K6 while the decisions
                     # travel to the host; categorical winners split by K6's category bitmasks.  The decode reads
@@ -1726,7 +1736,8 @@ class ForestTrainer:
                                                      False, codes, emit_ok, n, stats_rows["v1"],
                                                      1.0 if cls2 else (mseg_scales[1] if use_mseg else 1.0),
                                                      w_total, rec_buf,
-                                                     catm=cm if self.data.categorical else None)
+                                                     catm=cm if self.data.categorical else None,
+                                                     node=node if deep_ids else None)
                     if em is not None:
                         rec_buf = em.rec
                         emits.append(em)
@@ -1872,7 +1883,7 @@ class ForestTrainer:
                         perm, v0p, v1p, wp, segs = K.seg_partition(data.bins, perm, v0p, v1p, wp, segs, split_feat,
                                                                     split_bin, cat_off, cm.reshape(-1), child,
                                                                     len(nl))
-                    elif use_codes and dec is not None:
+                    elif dec is not None:  # partitioned on the device behind K6
                         if K._lib.DEBUG:
                             self._check_decode(dec, split_feat, split_bin, cat_off, cat_masks, child, n_tree, T)
                     elif use_codes:
