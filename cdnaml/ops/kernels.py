@@ -774,7 +774,17 @@ def codes_init_max(weights: Optional[torch.Tensor], T: int, n: int, device):
 
 
 def decode_codes(codes: torch.Tensor, tfirst: torch.Tensor):
-    """codes [T, n] -> (node ids int32 [T, n] with -1 = done, weights uint8 [T, n])."""
+    """codes [T, n] -> (node ids int32 [T, n] with -1 = done, weights uint8 [T, n]).  GPU: one pass
+    (seg.hip codes_to_nodes_kernel)."""
+    if _native(codes) and codes.dim() == 2 and codes.dtype in (torch.uint16, torch.int16):
+        T, n = codes.shape
+        c = codes.contiguous()
+        tf, = upload(codes.device, tfirst.cpu().numpy().astype(np.int32))
+        node = torch.empty((T, n), dtype=torch.int32, device=codes.device)
+        w = torch.empty((T, n), dtype=torch.uint8, device=codes.device)
+        _lib.check(_lib.lib().cdna_codes_to_nodes(_ptr(c), n, T, _ptr(tf), _ptr(node), _ptr(w), _stream(codes.device)),
+                   "cdna_codes_to_nodes")
+        return node, w
     c = codes.to(torch.int32) & 0xFFFF
     loc = c & 0xFF
     w = (c >> 8).to(torch.uint8)

@@ -1754,6 +1754,60 @@ CDNA_API int cdna_node_compact(int pass, const int* node, const uint8_t* w, int6
   return (int)hipGetLastError();
 }
 
+// u16 row codes [T, n] (weight << 8 | local node, 255 = done) -> node ids int32 [T, n] (tfirst[t] + local, -1 for
+// done or weight 0) and weights uint8 [T, n]: the switch of a deep forest to node ids at level 8, one pass (the
+// torch formulation took seven passes over the [T, n] arrays, ~2.3 ms at 20 trees x 1e7 rows).  blockIdx.y = tree;
+// four codes per thread (one 8-byte load) when n % 4 == 0.
+__global__ __launch_bounds__(256) void codes_to_nodes_kernel(const uint16_t* __restrict__ codes, int64_t n,
+                                                             const int* __restrict__ tfirst, int* __restrict__ node,
+                                                             uint8_t* __restrict__ w, int vec4) {
+  const int t = blockIdx.y;
+  const int tf = tfirst[t];
+  const uint16_t* c = codes + (int64_t)t * n;
+  int* nd = node + (int64_t)t * n;
+  uint8_t* wt = w + (int64_t)t * n;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  auto one = [&](unsigned v, int& id, unsigned& wv) {
+    const unsigned loc = v & 0xFFu;
+    wv = (v >> 8) & 0xFFu;
+    id = (loc == 0xFFu || wv == 0u) ? -1 : tf + (int)loc;
+  };
+  if (vec4) {
+    const int64_t n4 = n / 4;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += stride) {
+      const uint2 v = reinterpret_cast<const uint2*>(c)[q];
+      int i0, i1, i2, i3;
+      unsigned w0, w1, w2, w3;
+      one(v.x & 0xFFFFu, i0, w0);
+      one(v.x >> 16, i1, w1);
+      one(v.y & 0xFFFFu, i2, w2);
+      one(v.y >> 16, i3, w3);
+      reinterpret_cast<int4*>(nd)[q] = int4{i0, i1, i2, i3};
+      reinterpret_cast<unsigned*>(wt)[q] = w0 | (w1 << 8) | (w2 << 16) | (w3 << 24);
+    }
+    return;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    int id;
+    unsigned wv;
+    one(c[i], id, wv);
+    nd[i] = id;
+    wt[i] = (uint8_t)wv;
+  }
+}
+
+CDNA_API int cdna_codes_to_nodes(const uint16_t* codes, int64_t n, int T, const int* tfirst, int* node, uint8_t* w,
+                                 hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  if (!codes || !tfirst || !node || !w || T > 65535) return (int)hipErrorInvalidValue;
+  const int vec4 = (n % 4 == 0) && ((uintptr_t)codes % 8 == 0) && ((uintptr_t)node % 16 == 0) && ((uintptr_t)w % 4 == 0);
+  const int64_t work = vec4 ? n / 4 : n;
+  int64_t nb = (work + 255) / 256;
+  const dim3 grid((unsigned)(nb < 1024 ? nb : 1024), (unsigned)T);
+  hipLaunchKernelGGL(codes_to_nodes_kernel, grid, dim3(256), 0, st, codes, n, tfirst, node, w, vec4);
+  return (int)hipGetLastError();
+}
+
 CDNA_API int cdna_bins_row_major(const uint64_t* bins, int64_t n, int G, int Gs, uint64_t* out, hipStream_t st) {
   if (n <= 0) return 0;
   if (G <= 0 || G > 32 || Gs < G) return (int)hipErrorInvalidValue;

@@ -1247,3 +1247,21 @@ def test_shifted_f32(dev):
     y = 1e5 + torch.randn(100_001, generator=g, device=dev, dtype=torch.float64) * 3
     s = y[:1024].mean().reshape(1)
     assert torch.equal(K.shifted_f32(y, s), (y - s).float())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4096, 1001])
+def test_codes_to_nodes_matches_torch(n):
+    """seg.hip codes_to_nodes_kernel (vectorised when n % 4 == 0, scalar otherwise) == the torch decode."""
+    from cdnaml.ops import kernels as K
+    g = torch.Generator().manual_seed(n)
+    T = 5
+    loc = torch.randint(0, 256, (T, n), generator=g)
+    w = torch.randint(0, 4, (T, n), generator=g)
+    codes = ((w << 8) | loc).to(torch.int16)
+    tfirst = torch.tensor([0, 7, 300, 301, 900], dtype=torch.int32)
+    node, wd = K.decode_codes(codes.cuda(), tfirst)
+    ids = tfirst[:, None].long() + loc
+    ref = torch.where((loc == K.CODE_DONE) | (w == 0), torch.full_like(ids, -1), ids)
+    assert torch.equal(node.cpu().long(), ref)
+    assert torch.equal(wd.cpu().long(), w)
