@@ -68,6 +68,9 @@ DEEP_REC = __import__("os").environ.get("CDNAML_DEEP_REC", "1") != "0"
 # 376 -> 88 ms per fit.  One tree keeps the permutation segment path (seg.hip, any depth): 14 ms at depth 12
 # against 38 ms switched (profiles/r4/deep_reg_ab.md)
 DEEP_REG = __import__("os").environ.get("CDNAML_DEEP_REG", "1") != "0"
+# per-node feature subsets drawn on the GPU (misc.hip feature_masks_kernel) on levels whose masks have no host
+# consumer; 0 = numpy + upload every level
+MASKS_DEV = __import__("os").environ.get("CDNAML_MASKS_DEV", "1") != "0"
 # boosting margins updated by the level partitions (ForestTrainer.train(margin=...)) instead of a tree walk
 GBDT_MARGIN = __import__("os").environ.get("CDNAML_GBDT_MARGIN", "1") != "0"
 # feature-subset forests: accumulate only each node's sampled features in segment mode.  Opt-in: measured
@@ -940,6 +943,14 @@ class ForestTrainer:
             self.comm.all_reduce_scalar(float(data.n_local), "max"))
 
     # ------------------------------------------------------------ helpers
+    def _mask_base(self, trees: np.ndarray, node_keys: np.ndarray) -> np.ndarray:
+        """Per-node uint64 mix of (seed, tree, heap key) that the feature hashes of _feature_masks start from."""
+        keys = np.ones(len(trees), dtype=np.uint64) if self.p.subset_scope == "tree" else node_keys.astype(np.uint64)
+        with np.errstate(over="ignore"):
+            return (np.uint64(self.p.seed & 0xFFFFFFFFFFFF) * np.uint64(0x9E3779B97F4A7C15)
+                    + trees.astype(np.uint64) * np.uint64(0xBF58476D1CE4E5B9)
+                    + keys * np.uint64(0x94D049BB133111EB))
+
     def _feature_masks(self, trees: np.ndarray, node_keys: np.ndarray) -> np.ndarray:
         """Feature-subset bit words [A, ceil(d/32)] for a level's nodes (featureSubsetStrategy).
 
@@ -954,11 +965,8 @@ class ForestTrainer:
         words = np.zeros((A, (d + 31) // 32), dtype=np.uint32)
         if k is None or k >= d or A == 0:
             return words
-        keys = np.ones(A, dtype=np.uint64) if self.p.subset_scope == "tree" else node_keys.astype(np.uint64)
+        base = self._mask_base(trees, node_keys)
         with np.errstate(over="ignore"):
-            base = (np.uint64(self.p.seed & 0xFFFFFFFFFFFF) * np.uint64(0x9E3779B97F4A7C15)
-                    + trees.astype(np.uint64) * np.uint64(0xBF58476D1CE4E5B9)
-                    + keys * np.uint64(0x94D049BB133111EB))
             h = _splitmix64(base[:, None] + np.arange(d, dtype=np.uint64)[None, :] * np.uint64(0xD6E8FEB86659FD93))
         feats = np.argpartition(h, k - 1, axis=1)[:, :k]
         rows = np.repeat(np.arange(A), k)
@@ -1501,9 +1509,15 @@ class ForestTrainer:
             slot_of[build_ids] = np.arange(len(build_ids), dtype=np.int32)
             slot_tree = a_tree[build_ids]
             masks_np = None
+            masks_dev = None  # the same words drawn on the GPU (no host consumer this level)
             if need_masks:
                 tid = a_tree if p.tree_ids is None else np.asarray(p.tree_ids, dtype=np.int64)[a_tree]
-                masks_np = self._feature_masks(tid.astype(np.uint64), a_key)
+                if MASKS_DEV and dev.type == "cuda" and not (masked or use_sub or subset_seg) and \
+                        d <= K.FEATURE_MASKS_MAX_D and p.feature_subset is not None and 0 < p.feature_subset < d:
+                    masks_dev = K.feature_masks(self._mask_base(tid.astype(np.uint64), a_key), d, p.feature_subset,
+                                                dev)
+                else:
+                    masks_np = self._feature_masks(tid.astype(np.uint64), a_key)
             fm_build = None
             if masked:
                 fm_build, = K.upload(dev, np.ascontiguousarray(masks_np[build_ids]).view(np.int32))
@@ -1647,7 +1661,8 @@ class ForestTrainer:
                                     slot_of, a_parent, a_sib)
             else:
                 H = Hb
-            masks_t = K.upload(dev, masks_np.view(np.int32))[0] if masks_np is not None else None
+            masks_t = masks_dev if masks_dev is not None else \
+                (K.upload(dev, masks_np.view(np.int32))[0] if masks_np is not None else None)
             catm_h = None  # left-category bit masks of the native categorical scan
             dec = None     # device-decoded partition tables (partition already queued)
             em_next = None  # records of the next level written by this level's partition
@@ -1655,6 +1670,8 @@ class ForestTrainer:
                 # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
                 mb = p.impurity == "xgb" and self.data.missing_bin
                 if rs_slice is not None:
+                    if masks_dev is not None:
+                        masks_np = self._feature_masks(tid.astype(np.uint64), a_key)
                     so, tot = self._rs_split(H, rs_slice, masks_np, d, dev)
                 elif sub_feats is not None:
                     so, tot = K.split_scan_sub(H, sub_feats, self._nthr_dev(dev), mseg_raw, p.min_instances)

@@ -211,6 +211,7 @@ _SIGS = {
                                  c_void_p], c_int),
     "cdna_node_compact": ([c_int, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_float, c_int, c_void_p], c_int),
+    "cdna_feature_masks": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
     "cdna_codes_to_nodes": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_uniform": ([c_void_p, c_int64, c_uint64, c_uint64, c_uint32, c_void_p], c_int),
     "cdna_sample_rows": ([c_int64, c_uint64, c_uint64, c_uint32, c_double, c_void_p, c_int64, c_void_p, c_void_p],

@@ -773,6 +773,23 @@ def codes_init_max(weights: Optional[torch.Tensor], T: int, n: int, device):
     return c.to(torch.int16).contiguous(), max(1, wmax)
 
 
+FEATURE_MASKS_MAX_D = 2048
+
+
+def feature_masks(base: np.ndarray, d: int, k: int, device) -> torch.Tensor:
+    """Per-node feature-subset bit words int32 [A, ceil(d/32)] on the GPU (misc.hip feature_masks_kernel): node a
+    keeps the k features with the smallest splitmix64(base[a] + f * 0xD6E8FEB86659FD93) -- the words of
+    ForestTrainer._feature_masks for the same per-node base.  d <= FEATURE_MASKS_MAX_D."""
+    A = len(base)
+    W = (d + 31) // 32
+    out = torch.empty((A, W), dtype=torch.int32, device=device)
+    if A == 0:
+        return out
+    b, = upload(device, np.ascontiguousarray(base, dtype=np.uint64).view(np.int64))
+    _lib.check(_lib.lib().cdna_feature_masks(_ptr(b), A, d, k, _ptr(out), _stream(out.device)), "cdna_feature_masks")
+    return out
+
+
 def decode_codes(codes: torch.Tensor, tfirst: torch.Tensor):
     """codes [T, n] -> (node ids int32 [T, n] with -1 = done, weights uint8 [T, n]).  GPU: one pass
     (seg.hip codes_to_nodes_kernel)."""

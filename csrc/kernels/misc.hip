@@ -491,6 +491,57 @@ __global__ __launch_bounds__(256) void sample_rows_kernel(int64_t n, uint64_t se
   }
 }
 
+// Per-node feature subsets (featureSubsetStrategy) as bit words [A, W]: node a keeps the k features with the
+// smallest splitmix64(base[a] + f * 0xD6E8FEB86659FD93) -- the host formula of engine.ForestTrainer._feature_masks
+// (base[a] = its seed / tree / heap-key mix, computed on the host).  splitmix64 is a bijection and the inputs of a
+// node differ, so the k smallest hashes are one well-defined set: the words equal the host's argpartition result.
+// One wave per node, the node's d hashes in LDS, each feature's rank by counting smaller hashes (d <= 2048); the
+// host version spent up to ~6 ms per deep level on the [A, d] uint64 arrays while the GPU idled.
+__device__ __forceinline__ uint64_t splitmix64_mix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void feature_masks_kernel(const uint64_t* __restrict__ base, int A, int d, int k,
+                                                            int W, unsigned* __restrict__ words) {
+  extern __shared__ uint64_t fm_hash[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int a = blockIdx.x * 4 + wave;
+  uint64_t* h = fm_hash + (size_t)wave * d;
+  if (a < A) {
+    const uint64_t b = base[a];
+    for (int f = lane; f < d; f += 64) h[f] = splitmix64_mix(b + (uint64_t)f * 0xD6E8FEB86659FD93ull);
+  }
+  __syncthreads();
+  if (a >= A) return;
+  for (int j = 0; 2 * j < W; ++j) {
+    const int f = j * 64 + lane;
+    bool sel = false;
+    if (f < d) {
+      const uint64_t hf = h[f];
+      int r = 0;
+      for (int g = 0; g < d; ++g) r += h[g] < hf ? 1 : 0;
+      sel = r < k;
+    }
+    const uint64_t m = __ballot(sel);
+    if (lane == 0) {
+      words[(size_t)a * W + 2 * j] = (unsigned)m;
+      if (2 * j + 1 < W) words[(size_t)a * W + 2 * j + 1] = (unsigned)(m >> 32);
+    }
+  }
+}
+
+CDNA_API int cdna_feature_masks(const uint64_t* base, int A, int d, int k, unsigned* words, hipStream_t st) {
+  if (A <= 0) return 0;
+  if (!base || !words || d <= 0 || d > 2048 || k <= 0 || k > d) return (int)hipErrorInvalidValue;
+  const int W = (d + 31) / 32;
+  hipLaunchKernelGGL(feature_masks_kernel, dim3((unsigned)((A + 3) / 4)), dim3(256), (size_t)4 * d * 8, st, base, A, d,
+                     k, W, words);
+  return (int)hipGetLastError();
+}
+
 CDNA_API int cdna_sample_rows(int64_t n, uint64_t seed, uint64_t offset, uint32_t stream, double frac, int64_t* idx,
                               int64_t cap, unsigned* count, hipStream_t st) {
   if (!count || (cap > 0 && !idx)) return (int)hipErrorInvalidValue;

@@ -21,8 +21,12 @@ for name, est in [("rf20 depth 8", RandomForestRegressor(numTrees=20, maxDepth=8
         continue
     est.fit(df)
     torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(2):
+    ts = []
+    for _ in range(int(os.environ.get("REPS", "5"))):
+        t = time.perf_counter()
         m = est.fit(df)
-    torch.cuda.synchronize()
-    print(f"DEEP_REG={tag} {name}: {(time.perf_counter() - t) / 2 * 1e3:.1f} ms per fit", flush=True)
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t) * 1e3)
+        del m
+    print(f"DEEP_REG={tag} {name}: median {sorted(ts)[len(ts) // 2]:.1f} ms per fit "
+          f"({' '.join(f'{x:.1f}' for x in ts)})", flush=True)

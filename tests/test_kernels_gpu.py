@@ -1265,3 +1265,24 @@ def test_codes_to_nodes_matches_torch(n):
     ref = torch.where((loc == K.CODE_DONE) | (w == 0), torch.full_like(ids, -1), ids)
     assert torch.equal(node.cpu().long(), ref)
     assert torch.equal(wd.cpu().long(), w)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,k", [(100, 33), (7, 3), (300, 17), (64, 63), (1, 1)])
+def test_feature_masks_match_host(d, k):
+    """misc.hip feature_masks_kernel == the host draw of ForestTrainer._feature_masks (k smallest splitmix64 hashes
+    of base + f * C per node, as bit words)."""
+    import numpy as np
+    from cdnaml.models.tree.engine import _splitmix64
+    from cdnaml.ops import kernels as K
+    rng = np.random.default_rng(d * 1000 + k)
+    A = 777
+    base = rng.integers(0, 2 ** 63, size=A, dtype=np.int64).astype(np.uint64) * np.uint64(2) + np.uint64(1)
+    with np.errstate(over="ignore"):
+        h = _splitmix64(base[:, None] + np.arange(d, dtype=np.uint64)[None, :] * np.uint64(0xD6E8FEB86659FD93))
+    feats = np.argpartition(h, k - 1, axis=1)[:, :k]
+    words = np.zeros((A, (d + 31) // 32), dtype=np.uint32)
+    f = feats.reshape(-1)
+    np.bitwise_or.at(words, (np.repeat(np.arange(A), k), f >> 5), np.uint32(1) << (f & 31).astype(np.uint32))
+    got = K.feature_masks(base, d, k, torch.device("cuda")).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, words)
