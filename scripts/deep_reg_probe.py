@@ -10,6 +10,9 @@ import cdnaml  # noqa: E402
 from cdnaml.models.regression import DecisionTreeRegressor, RandomForestRegressor  # noqa: E402
 from cdnaml.utils.synthetic import regression_shard  # noqa: E402
 
+if os.environ.get("GC_OFF") == "1":
+    import gc
+    gc.disable()
 spark = cdnaml.SparkSession.builder.getOrCreate()
 X, y, _ = regression_shard(int(1e7), 100, 42, 0, 1, spark.device)
 df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
