@@ -1378,6 +1378,12 @@ def _fill_chunk(segs: np.ndarray, chunk: int, B: int = 0, ncu: int = 0) -> int:
     lo, hi = c0, int(chunk)
     if int(((lens + hi - 1) // hi).sum()) > R * ncu:
         return c0
+    # the answer c satisfies total / c <= sum ceil(len / c) <= R * ncu and sum ceil(len / c) <= total / c + k:
+    # it lies in [total / (R ncu), total / (R ncu - k)] (a few bisection steps, not ~17 over [c0, chunk])
+    cap = R * ncu
+    lo = max(lo, -(-total // cap))
+    if cap > len(lens):
+        hi = min(hi, -(-total // (cap - len(lens))))
     while lo < hi:  # smallest chunk whose blocks fit R rounds
         mid = (lo + hi) // 2
         if int(((lens + mid - 1) // mid).sum()) <= R * ncu:
@@ -1387,30 +1393,34 @@ def _fill_chunk(segs: np.ndarray, chunk: int, B: int = 0, ncu: int = 0) -> int:
     return lo
 
 
-def _seg_work(segs: np.ndarray, chunk: int) -> np.ndarray:
-    """segs [k, 3] {start, len, tag} -> work items [m, 3] of at most `chunk` rows each."""
+def _seg_work(segs: np.ndarray, chunk: int, interleave: bool = False) -> np.ndarray:
+    """segs [k, 3] {start, len, tag} -> work items [m, 3] of at most `chunk` rows each.
+
+    interleave: ordered by relative position inside the segment, so that concurrently running blocks gather nearby
+    rows (chunk j of every segment covers about the same fraction of the row ids; placing rounds of chunks on one
+    XCD for L2 sharing measured no better and was dropped), built in the same pass: the
+    position is bucketed to a uint16 key (chunk j of a k-chunk segment -> j * kmax // k), whose stable argsort is a
+    radix sort -- the float key's merge sort plus a second pass cost ~60-70 us of host time per level at the
+    per-rank shape, while the GPU waited.  Any order gives the same histograms (exact fixed-point sums)."""
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
     segs = segs[segs[:, 1] > 0]
     if len(segs) == 0:
         return np.zeros((0, 3), dtype=np.int32)
     k = (segs[:, 1] + chunk - 1) // chunk
     rep = np.repeat(np.arange(len(segs)), k)
-    j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
-    st = segs[rep, 0] + j * chunk
-    ln = np.minimum(chunk, segs[rep, 1] - j * chunk)
-    return np.stack([st, ln, segs[rep, 2]], 1).astype(np.int32)
-
-
-def _interleave(work: np.ndarray, segs: np.ndarray, chunk: int) -> np.ndarray:
-    """Interleave segment chunks by relative position (chunk j of every segment covers about the same fraction of
-    the row ids), so concurrently running blocks gather nearby rows.  Tried on top: placing each round of
-    len(segs) chunks on one XCD (block b -> XCD b % 8) for L2 sharing -- measured 194 vs 190 ms with the
-    half-wave kernel; with the quarter-wave kernel XCD x walking the x-th eighth of this order measured 87.4 vs
-    87.0 ms of histograms per step (also with level-0/1 only) -- dropped both."""
-    sg = segs[segs[:, 1] > 0]
-    k = (sg[:, 1] + chunk - 1) // chunk
-    j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
-    return work[np.argsort(j / np.repeat(k, k), kind="stable")]
+    j = np.arange(len(rep)) - (np.cumsum(k) - k)[rep]
+    if interleave and len(segs) > 1:
+        kmax = int(k.max())
+        key = j * kmax // k[rep]
+        if kmax < 1 << 16:
+            key = key.astype(np.uint16)
+        o = np.argsort(key, kind="stable")
+        rep, j = rep[o], j[o]
+    out = np.empty((len(rep), 3), dtype=np.int32)
+    out[:, 0] = segs[rep, 0] + j * chunk
+    out[:, 1] = np.minimum(chunk, segs[rep, 1] - j * chunk)
+    out[:, 2] = segs[rep, 2]
+    return out
 
 
 def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optional[torch.Tensor],
@@ -1512,13 +1522,11 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
             cap = 3 * cap - 1024
         chunk = _fill_chunk(segs, min(SEG_HIST_CHUNK * (3 if rm_s10 and LANE10_CHUNK3 else 1), cap), B,
                             _num_cus(bins.device) if (SEG_ROUND_FIT and rm_s10 and bins.is_cuda) else 0)
-        work = _seg_work(segs, chunk)
+        work = _seg_work(segs, chunk, interleave)
         if len(work) == 0:
             if out is not None:
                 return out
             return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
-        if interleave and len(segs) > 1:
-            work = _interleave(work, segs, chunk)
         wt, = upload(bins.device, work.reshape(-1))
         iout = out if out is not None else torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
         assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
@@ -1670,14 +1678,9 @@ def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optio
     else:
         chunk = SEG_HIST_CHUNK if not packed else min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1))
         chunk = _fill_chunk(segs, chunk, B)
-        work = _seg_work(segs, chunk)
+        work = _seg_work(segs, chunk, interleave)
         if len(work) == 0:
             return zero()
-        if interleave and len(segs) > 1:
-            sg = segs[segs[:, 1] > 0]
-            k = (sg[:, 1] + chunk - 1) // chunk
-            j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
-            work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
         wt, = upload(bins.device, work.reshape(-1))
         iout = torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
         mode =(1 if packed else 0) | (2 if wp is not None else 0) | (4 if bins_rm is not None else 0)
@@ -1720,14 +1723,9 @@ def seg_hist_subset(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v1p:
         return out
     wm = int(max(1, min(255, wmax)))
     chunk = min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1), ((1 << 24) - 1) // max(m, 1))  # pair index < 2^24
-    work = _seg_work(segs, chunk)
+    work = _seg_work(segs, chunk, interleave)
     if len(work) == 0:
         return out
-    if interleave and len(segs) > 1:
-        sg = segs[segs[:, 1] > 0]
-        k = (sg[:, 1] + chunk - 1) // chunk
-        j = np.arange(int(k.sum())) - np.repeat(np.cumsum(k) - k, k)
-        work = work[np.argsort(j / np.repeat(k, k), kind="stable")]
     qs1 = (scales if scales is not None else seg_scales(None, v1p, wm, n))[1]
     if bins_rm is None:
         bins_rm = bins_row_major(bins)
