@@ -194,6 +194,36 @@ def scenario_trees_rs_overlap(spark):
     return out
 
 
+def scenario_trees_deep(spark):
+    """Forests deeper than 8 levels (binary classification and regression forests switch from the u16 row codes
+    to node ids at level 8, then build node-id record histograms): bit-identical at any world size, also with
+    every level reduce-scattered by feature."""
+    from cdnaml.ml.classification import RandomForestClassifier
+    from cdnaml.ml.regression import RandomForestRegressor
+    from cdnaml.models.tree import engine
+    from cdnaml.utils.synthetic import forest_digest
+    df = _tree_df(spark, n=12000, d=13)
+    calls = {"n": 0}
+    orig = engine.K.node_compact
+
+    def counted(*a, **k):
+        calls["n"] += 1
+        return orig(*a, **k)
+    engine.K.node_compact = counted
+    out = {}
+    for tag, rs_min in (("ar", 1 << 62), ("rs", 0)):
+        engine.RS_MIN_BYTES = rs_min
+        engine.HIST_OVERLAP = 1
+        for k, est in (("rf_reg", RandomForestRegressor(numTrees=3, maxDepth=11, maxBins=32, seed=5)),
+                       ("rf_cls", RandomForestClassifier(numTrees=3, maxDepth=10, maxBins=32, seed=9,
+                                                         labelCol="cls"))):
+            m = est.fit(df)
+            out[f"{tag}_{k}"] = forest_digest(m._forest)
+            out[f"{tag}_{k}_nodes"] = int(sum(len(m._forest.tree_nodes(t)) for t in range(len(m._forest.roots))))
+    assert calls["n"] > 0, "the node-id record levels did not run"
+    return out
+
+
 def scenario_cv(spark):
     from cdnaml.ml.evaluation import RegressionEvaluator
     from cdnaml.ml.regression import RandomForestRegressor
@@ -286,7 +316,7 @@ def scenario_hyperopt_captured(spark):
 
 SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault, "trees": scenario_trees,
              "trees_uneven": scenario_trees_uneven, "trees_rs": scenario_trees_rs,
-             "trees_rs_overlap": scenario_trees_rs_overlap, "cv": scenario_cv, "als": scenario_als,
+             "trees_rs_overlap": scenario_trees_rs_overlap, "trees_deep": scenario_trees_deep, "cv": scenario_cv, "als": scenario_als,
              "hyperopt": scenario_hyperopt,
              "hyperopt_captured": scenario_hyperopt_captured}
 

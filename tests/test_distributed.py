@@ -130,7 +130,8 @@ def test_bench_trains_identical_forest_on_1_2_4_8_ranks(tmp_path):
         assert tag == ref, (w, tag, ref)
 
 
-@pytest.mark.parametrize("scenario,worlds", [("trees", (2, 4)), ("trees_uneven", (2, 4)), ("cv", (2,)),
+@pytest.mark.parametrize("scenario,worlds", [("trees", (2, 4)), ("trees_uneven", (2, 4)), ("trees_deep", (2, 3)),
+                                             ("cv", (2,)),
                                              ("als", (2, 4)), ("hyperopt", (2,)),
                                              ("hyperopt_captured", (2,))])
 def test_models_identical_across_world_sizes(scenario, worlds, tmp_path):
