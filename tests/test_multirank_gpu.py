@@ -42,3 +42,30 @@ def test_ranks_sharing_one_gpu_grow_the_single_rank_forest():
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args + ["--gpus", str(nproc)]
         assert _digest(cmd, env) == ref, f"{nproc} ranks on one GPU grew a different forest"
+
+
+def _worker(scenario, tmp_path, nproc, device):
+    import json
+    out = tmp_path / f"{scenario}_{device}_{nproc}.json"
+    env = {**os.environ, "CDNAML_COMM_BACKEND": "gloo", "OMP_NUM_THREADS": "2", "PYTHONPATH": ROOT,
+           "CDNAML_DEVICE": device, "CDNAML_CONF_CDNAML__WAREHOUSE__DIR": str(tmp_path / f"wh_{device}{nproc}")}
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    w = os.path.join(ROOT, "tests", "dist_worker.py")
+    cmd = [sys.executable, w, scenario, str(out)] if nproc == 1 else \
+        [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+         "--master-addr", "127.0.0.1", "--master-port", str(_port()), w, scenario, str(out)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    return json.loads(out.read_text())
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_deep_forests_gpu_ranks_match_cpu(tmp_path):
+    """Forests deeper than 8 levels on the GPU path (device split decode + node-id partition, GPU-drawn feature
+    subsets, node_compact record histograms), with and without reduce-scatter: 1 and 2 ranks on cuda:0 grow the
+    forests the CPU emulation grows, bit for bit."""
+    cpu = _worker("trees_deep", tmp_path, 1, "cpu")
+    for nproc in (1, 2):
+        assert _worker("trees_deep", tmp_path, nproc, "cuda") == cpu, nproc
