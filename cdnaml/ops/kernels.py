@@ -426,12 +426,20 @@ HIST5_PACKED_LDS = int(__import__("os").environ.get("CDNAML_HIST5_PACKED_LDS", s
 HIST5_COMPACT = int(__import__("os").environ.get("CDNAML_HIST5_COMPACT", "1"))
 
 
+def _absmax(v: torch.Tensor) -> float:
+    """max |v| (NaN if v holds one) in one reduction kernel: the inf-norm reduces |v| inside the reduction, where
+    ``v.abs().max()`` first wrote |v| in a full elementwise pass (0.14 ms of a 1e8-row boosting round)."""
+    if v.is_floating_point():
+        return float(torch.linalg.vector_norm(v.reshape(-1), float("inf")).item())
+    return float(v.abs().max().item())
+
+
 def _fixed_scale(v: Optional[torch.Tensor], n: int, wmax: int, qmax_bits: int = 62) -> float:
     """Power-of-two fixed-point scale so that sum_r w_r * |round(v_r * s)| < 2^62 over n rows
     (and |round(v_r * s)| < 2^qmax_bits for kernels that quantise in 32 bits)."""
     if v is None or v.numel() == 0:
         return 1.0
-    m = float(v.abs().max().item())
+    m = _absmax(v)
     if not math.isfinite(m):
         raise ValueError("histogram statistic contains NaN/Inf")
     if m == 0.0:
@@ -532,7 +540,7 @@ def packed_scale_global(v: torch.Tensor, comm) -> float:
     histograms all-reduce to the same sums whatever the number of GPUs."""
     m = _prefetched(v, True) if v.numel() else 0.0
     if m is None:
-        m = float(v.abs().max().item())
+        m = _absmax(v)
     m = comm.all_reduce_scalar(m, "max") if comm is not None else m
     if not math.isfinite(m):
         raise ValueError("histogram statistic contains NaN/Inf")
@@ -544,7 +552,7 @@ def packed_scale_global(v: torch.Tensor, comm) -> float:
 
 def _packed_scale(v: torch.Tensor) -> float:
     """Power-of-two scale with |round(v * s)| <= 2^23 (packed count|sum LDS words)."""
-    m = float(v.abs().max().item()) if v.numel() else 0.0
+    m = _absmax(v) if v.numel() else 0.0
     if not math.isfinite(m):
         raise ValueError("histogram statistic contains NaN/Inf")
     if m == 0.0:
@@ -1328,8 +1336,8 @@ def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_glob
         return 1.0, (packed_scale_global(v1p, comm) if comm is not None else _packed_scale(v1p))
     if comm is None or not comm.distributed:
         return (_fixed_scale(v0p, n_global, wmax, qmax_bits=30), _fixed_scale(v1p, n_global, wmax, qmax_bits=30))
-    m = torch.tensor([float(v0p.abs().max()) if v0p.numel() else 0.0,
-                      float(v1p.abs().max()) if v1p.numel() else 0.0, float(wmax)], dtype=torch.float64)
+    m = torch.tensor([_absmax(v0p) if v0p.numel() else 0.0,
+                      _absmax(v1p) if v1p.numel() else 0.0, float(wmax)], dtype=torch.float64)
     comm.all_reduce(m, "max")
     w = int(m[2])
     return (_fixed_scale(m[0:1], n_global, w, qmax_bits=30), _fixed_scale(m[1:2], n_global, w, qmax_bits=30))
