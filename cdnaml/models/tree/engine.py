@@ -1173,14 +1173,16 @@ class ForestTrainer:
 
     # ------------------------------------------------------------ device-queued partition
     def _device_partition(self, so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n, v1, qs1, w_total,
-                          rec_buf, margin=None, catm=None, node=None):
+                          rec_buf, margin=None, catm=None, node=None, pre=None):
         """Partition tables decoded on the device from the level's K6 decisions and the row partition queued right
         behind them (the GPU partitions while the decisions travel to the host; the host repeats the decode to
         build the forest and the next level, checked against the device's in the checked build).  With
         ``emit_ok`` the partition also writes the next level's item records.  -> (decode tables, RecordEmit|None)."""
         p, data, dev = self.p, self.data, self.device
         A = so.shape[0]
-        a_tree_d, tf_d = K.upload(dev, a_tree.astype(np.int32), tfirst.numpy().astype(np.int32))
+        # (``pre``: the two tables uploaded at the level start with the level's other small tables)
+        a_tree_d, tf_d = pre if pre is not None else \
+            K.upload(dev, a_tree.astype(np.int32), tfirst.numpy().astype(np.int32))
         dec = K.split_decode(so, tot, a_tree_d, T, p.min_instances, p.min_info_gain,
                              depth < p.max_depth, depth + 1 >= p.max_depth, missing_bin=mb,
                              leaf_values=(p.impurity, p.reg_lambda) if margin is not None else None,
@@ -1510,19 +1512,28 @@ class ForestTrainer:
             slot_tree = a_tree[build_ids]
             masks_np = None
             masks_dev = None  # the same words drawn on the GPU (no host consumer this level)
+            mask_base = None
             if need_masks:
                 tid = a_tree if p.tree_ids is None else np.asarray(p.tree_ids, dtype=np.int64)[a_tree]
                 if MASKS_DEV and dev.type == "cuda" and not (masked or use_sub or subset_seg) and \
                         d <= K.FEATURE_MASKS_MAX_D and p.feature_subset is not None and 0 < p.feature_subset < d:
-                    masks_dev = K.feature_masks(self._mask_base(tid.astype(np.uint64), a_key), d, p.feature_subset,
-                                                dev)
+                    mask_base = self._mask_base(tid.astype(np.uint64), a_key)
                 else:
                     masks_np = self._feature_masks(tid.astype(np.uint64), a_key)
+            id_tree = a_tree
+            tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
+            # the level's small device tables in ONE host->device copy (each separate copy was a blit kernel plus a
+            # launch gap): hist_assemble's (slot, parent, sibling), the decode's a_tree / tfirst, the mask bases
+            lvl = None
+            if dev.type == "cuda":
+                lvl = K.upload(dev, K.assemble_table(slot_of, a_parent, a_sib), a_tree.astype(np.int32),
+                               tfirst.numpy().astype(np.int32),
+                               *([mask_base.view(np.int64)] if mask_base is not None else []))
+                if mask_base is not None:
+                    masks_dev = K.feature_masks(mask_base, d, p.feature_subset, dev, base_dev=lvl[3])
             fm_build = None
             if masked:
                 fm_build, = K.upload(dev, np.ascontiguousarray(masks_np[build_ids]).view(np.int32))
-            id_tree = a_tree
-            tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
             hist_raw_scale = None
             reduced = False
             sub_feats = None
@@ -1658,7 +1669,7 @@ class ForestTrainer:
             elif is_raw or len(derived):
                 # one kernel (CPU: the same arithmetic in torch): fixed-point -> fp64 and parent - sibling
                 H = K.hist_assemble(Hb, hist_raw_scale if is_raw else None, prev_hist if len(derived) else None,
-                                    slot_of, a_parent, a_sib)
+                                    slot_of, a_parent, a_sib, table=lvl[0] if lvl is not None else None)
             else:
                 H = Hb
             masks_t = masks_dev if masks_dev is not None else \
@@ -1699,7 +1710,8 @@ class ForestTrainer:
                     dec, em = self._device_partition(so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n,
                                                      stats_rows["v1"], mseg_scales[1] if use_mseg else 1.0,
                                                      w_total, rec_buf, margin=margin if margin_ok else None,
-                                                     node=node if deep_ids else None)
+                                                     node=node if deep_ids else None,
+                                                     pre=(lvl[1], lvl[2]) if lvl is not None else None)
                     if em is not None:
                         rec_buf = em.rec
                         emits.append(em)
@@ -1754,7 +1766,8 @@ class ForestTrainer:
                                                      1.0 if cls2 else (mseg_scales[1] if use_mseg else 1.0),
                                                      w_total, rec_buf,
                                                      catm=cm if self.data.categorical else None,
-                                                     node=node if deep_ids else None)
+                                                     node=node if deep_ids else None,
+                                                     pre=(lvl[1], lvl[2]) if lvl is not None else None)
                     if em is not None:
                         rec_buf = em.rec
                         emits.append(em)

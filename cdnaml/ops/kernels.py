@@ -175,11 +175,17 @@ class BootstrapCodes:
 
 
 # ------------------------------------------------------- level histogram assembly
+def assemble_table(slot: np.ndarray, parent: np.ndarray, sib: np.ndarray) -> np.ndarray:
+    """hist_assemble's device table: int32 [A, 3] (slot, parent, sibling), flattened."""
+    return np.stack([slot, parent, sib], 1).astype(np.int32).reshape(-1)
+
+
 def hist_assemble(Hb: torch.Tensor, raw_scale, prev: Optional[torch.Tensor], slot: np.ndarray,
-                  parent: np.ndarray, sib: np.ndarray) -> torch.Tensor:
+                  parent: np.ndarray, sib: np.ndarray, table: Optional[torch.Tensor] = None) -> torch.Tensor:
     """fp64 histograms [A, d, B, K] of a level's active nodes in one launch (split.hip): built node a copies
     Hb[slot[a]] (int64 fixed point when ``raw_scale`` is given: a float divides stat 1, a pair (s0, s1)
-    divides stats 0 and 1); a derived node (slot -1) is prev[parent[a]] - (its sibling's built histogram)."""
+    divides stats 0 and 1); a derived node (slot -1) is prev[parent[a]] - (its sibling's built histogram).
+    ``table``: assemble_table(slot, parent, sib) already on the device (uploaded with the level's other tables)."""
     A = len(slot)
     nb, d, B, Kc = Hb.shape
     dev = Hb.device
@@ -203,7 +209,7 @@ def hist_assemble(Hb: torch.Tensor, raw_scale, prev: Optional[torch.Tensor], slo
             H[der] = prev[par] - src[sl[sib_]]
         return H
     H = torch.empty((A, d, B, Kc), dtype=torch.float64, device=dev)
-    m, = upload(dev, np.stack([slot, parent, sib], 1).astype(np.int32).reshape(-1))
+    m = table if table is not None else upload(dev, assemble_table(slot, parent, sib))[0]
     src = Hb.contiguous() if raw else Hb.double().contiguous()
     if raw:
         assert Hb.dtype == torch.int64
@@ -784,7 +790,7 @@ def codes_init_max(weights: Optional[torch.Tensor], T: int, n: int, device):
 FEATURE_MASKS_MAX_D = 2048
 
 
-def feature_masks(base: np.ndarray, d: int, k: int, device) -> torch.Tensor:
+def feature_masks(base: np.ndarray, d: int, k: int, device, base_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Per-node feature-subset bit words int32 [A, ceil(d/32)] on the GPU (misc.hip feature_masks_kernel): node a
     keeps the k features with the smallest splitmix64(base[a] + f * 0xD6E8FEB86659FD93) -- the words of
     ForestTrainer._feature_masks for the same per-node base.  d <= FEATURE_MASKS_MAX_D."""
@@ -793,7 +799,7 @@ def feature_masks(base: np.ndarray, d: int, k: int, device) -> torch.Tensor:
     out = torch.empty((A, W), dtype=torch.int32, device=device)
     if A == 0:
         return out
-    b, = upload(device, np.ascontiguousarray(base, dtype=np.uint64).view(np.int64))
+    b = base_dev if base_dev is not None else upload(device, np.ascontiguousarray(base, dtype=np.uint64).view(np.int64))[0]
     _lib.check(_lib.lib().cdna_feature_masks(_ptr(b), A, d, k, _ptr(out), _stream(out.device)), "cdna_feature_masks")
     return out
 
