@@ -1902,6 +1902,9 @@ class ForestTrainer:
                 # (active index of the node, -1 = done), partitioned and histogrammed by the node-id kernels
                 node, wdeep = K.decode_codes(codes, tfirst.to(codes.device))
                 node = node.contiguous()
+                # the node-id histogram kernels (levels past NODE_COMPACT_MAX_LOC nodes per tree) read the row weights
+                # from ``weights``: None when the bootstrap draws arrived as row codes (BootstrapCodes)
+                weights = wdeep
                 # below level 8 the record histograms continue from the node ids (K.node_compact)
                 deep_rec = DEEP_REC and use_mseg and rec_ok
                 use_codes = use_mseg = False

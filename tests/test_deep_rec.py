@@ -94,3 +94,35 @@ def test_deep_regression_prefix_is_depth8_forest(device, est_kind, depth, trees,
             assert mse(deep) < mse(shallow)
         finally:
             spark.stop()
+
+
+@pytest.mark.parametrize("device", _devices())
+def test_deep_fallback_node_histograms_use_bootstrap_weights(device, monkeypatch):
+    """Past NODE_COMPACT_MAX_LOC active nodes per tree the deep levels fall back to the node-id histogram kernel,
+    which reads the row weights: with the bootstrap draws written straight as row codes (GPU BootstrapCodes, no
+    weights tensor) they must come from the decoded codes -- the forest equals the one grown from the same draws
+    passed as a weights tensor (K.POISSON_CODES off)."""
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import cdnaml
+    from cdnaml.models.tree import engine
+    from cdnaml.ml.regression import RandomForestRegressor
+    from cdnaml.utils.synthetic import forest_digest
+    from tests.conftest import session_device
+    with session_device(device):
+        spark = cdnaml.SparkSession.builder.getOrCreate()
+        g = torch.Generator().manual_seed(17)
+        n = 40_000 if device == "cpu" else 200_000
+        X = torch.randn((n, 10), generator=g)
+        y = (2 * X[:, 0] + torch.sin(3 * X[:, 1]) + 0.3 * torch.randn(n, generator=g)).double()
+        df = spark.createDataFrameFromLocalTensors({"features": X.to(device), "label": y.to(device)})
+        est = RandomForestRegressor(numTrees=3, maxDepth=10, maxBins=32, seed=2)
+        monkeypatch.setattr(engine.K, "NODE_COMPACT_MAX_LOC", 1)
+        try:
+            got = {}
+            for codes in (True, False):
+                monkeypatch.setattr(engine.K, "POISSON_CODES", codes)
+                got[codes] = forest_digest(est.fit(df)._forest)
+        finally:
+            spark.stop()
+        assert got[True] == got[False]
