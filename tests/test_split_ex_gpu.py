@@ -143,11 +143,12 @@ def test_device_split_decode_forests_identical(dev, model, monkeypatch):
     assert digests[0] == digests[1]
 
 
-@pytest.mark.parametrize("flow", ["dt_reg", "rf_reg", "rf_binary"])
+@pytest.mark.parametrize("flow", ["dt_reg", "rf_reg", "rf_binary", "rf_reg_deep", "rf_binary_deep"])
 def test_device_decode_categorical_forests_identical(dev, flow, monkeypatch):
     """Categorical winners decoded on the device (split_decode with split_scan_ex's category bitmasks, partition
     queued before the decisions reach the host) give the host decode's forests bit for bit: regression trees /
-    forests with StringIndexer'd categoricals (ML 06) and a binary classifier on the same features."""
+    forests with StringIndexer'd categoricals (ML 06) and a binary classifier on the same features, also deeper
+    than 8 levels (node-id partition from the device tables)."""
     import cdnaml
     import pandas as pd
     from cdnaml.models.tree import engine
@@ -163,13 +164,16 @@ def test_device_decode_categorical_forests_identical(dev, flow, monkeypatch):
                         "beds": rng.integers(1, 6, n).astype(float), "lat": rng.normal(size=n)})
     hood_num = pdf.hood.str[1:].astype(int)
     price = 40 * pdf.beds + 15 * (hood_num % 5) + 60 * (pdf.room == "entire") + 10 * pdf.lat + rng.normal(size=n) * 5
-    pdf["label"] = (price > np.median(price)).astype(float) if flow == "rf_binary" else price
+    pdf["label"] = (price > np.median(price)).astype(float) if flow.startswith("rf_binary") else price
     sdf = spark.createDataFrame(pdf)
     sdf = StringIndexer(inputCols=["hood", "room"], outputCols=["hoodIdx", "roomIdx"]).fit(sdf).transform(sdf)
     df = VectorAssembler(inputCols=["hoodIdx", "roomIdx", "beds", "lat"], outputCol="features").transform(sdf)
     est = {"dt_reg": DecisionTreeRegressor(maxDepth=6, maxBins=40),
            "rf_reg": RandomForestRegressor(numTrees=8, maxDepth=6, maxBins=40, seed=2),
-           "rf_binary": RandomForestClassifier(numTrees=8, maxDepth=6, maxBins=40, seed=2)}[flow]
+           "rf_binary": RandomForestClassifier(numTrees=8, maxDepth=6, maxBins=40, seed=2),
+           # deeper than 8: the node-id levels decode on the device too (node-id partition behind K6)
+           "rf_reg_deep": RandomForestRegressor(numTrees=4, maxDepth=11, maxBins=40, seed=2),
+           "rf_binary_deep": RandomForestClassifier(numTrees=4, maxDepth=11, maxBins=40, seed=2)}[flow]
     decodes = {"n": 0}
     orig = K.split_decode
 
