@@ -1353,8 +1353,10 @@ SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "2048
 SEG_ROUND_FIT = __import__("os").environ.get("CDNAML_SEG_ROUND_FIT", "1") != "0"
 # wide-bin (80 < B <= 256, boosting) record levels: work items per level (x ceil(d / 64) feature blocks).  Every block
 # clears and flushes 64 features x B bins of LDS cells into the level histogram with global atomics, so at deep
-# boosting levels (fewer rows, the same number of blocks) the flush -- not the rows -- sets the level time
-SEG_MIN_BLOCKS_WIDE = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS_WIDE", "1024"))
+# boosting levels (fewer rows, the same number of blocks) the flush -- not the rows -- sets the level time.
+# bench_configs.py gbdt (1e8 x 100, 256 bins), 3 interleaved reps: 1024 -> 28.05-28.23, 768 -> 27.83-27.85,
+# 512 -> 27.78-27.83 ms per tree (profiles/r4/gbdt_min_blocks_ab.txt)
+SEG_MIN_BLOCKS_WIDE = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS_WIDE", "512"))
 # three-times-larger record chunks for the six-items-per-wave kernel (its count field is spread over three cell
 # copies): measured 145.1 vs 139.8 ms per headline step (fewer, longer blocks) and neutral at 1.25e7 rows -- off
 LANE10_CHUNK3 = __import__("os").environ.get("CDNAML_LANE10_CHUNK3", "0") != "0"
