@@ -71,6 +71,8 @@ DEEP_REG = __import__("os").environ.get("CDNAML_DEEP_REG", "1") != "0"
 # per-node feature subsets drawn on the GPU (misc.hip feature_masks_kernel) on levels whose masks have no host
 # consumer; 0 = numpy + upload every level
 MASKS_DEV = __import__("os").environ.get("CDNAML_MASKS_DEV", "1") != "0"
+# predictor tables of tuner-cut forests from the arrays truncate_forest computed (0: from the node lists)
+CUT_ARRAYS = __import__("os").environ.get("CDNAML_CUT_ARRAYS", "1") != "0"
 # boosting margins updated by the level partitions (ForestTrainer.train(margin=...)) instead of a tree walk
 GBDT_MARGIN = __import__("os").environ.get("CDNAML_GBDT_MARGIN", "1") != "0"
 # feature-subset forests: accumulate only each node's sampled features in segment mode.  Opt-in: measured
@@ -636,17 +638,25 @@ class Forest:
             return self._dev[key]
         N = self.num_nodes
         nodes = np.zeros((N, 4), dtype=np.int32)
-        feat = np.asarray(self.feat, dtype=np.int32)
+        # a forest cut by the fused tuner carries its node fields as arrays (truncate_forest): no list round trip
+        npa = self.__dict__.get("_np") if CUT_ARRAYS else None
+        if npa is not None and (len(npa["feat"]) != N or npa["is_cat"] is None or npa["value"] is None):
+            npa = None
+        feat = npa["feat"].astype(np.int32) if npa is not None else np.asarray(self.feat, dtype=np.int32)
         leaf = feat < 0
-        isc = np.asarray(self.is_cat, dtype=bool) & ~leaf
+        isc = (npa["is_cat"] if npa is not None else np.asarray(self.is_cat, dtype=bool)) & ~leaf
         num = ~leaf & ~isc
-        left = np.asarray(self.left, dtype=np.int32)
-        right = np.asarray(self.right, dtype=np.int32)
+        left = npa["left"].astype(np.int32) if npa is not None else np.asarray(self.left, dtype=np.int32)
+        right = npa["right"].astype(np.int32) if npa is not None else np.asarray(self.right, dtype=np.int32)
         lid = np.nonzero(leaf)[0]
-        V = (np.stack([self.value[i] for i in lid.tolist()]).astype(np.float64) if len(lid)
-             else np.zeros((0, self.K)))
+        if npa is not None:
+            V = npa["value"][lid] if len(lid) else np.zeros((0, self.K))
+        else:
+            V = (np.stack([self.value[i] for i in lid.tolist()]).astype(np.float64) if len(lid)
+                 else np.zeros((0, self.K)))
         if values_kind != "value" and len(lid):
-            V = V * np.asarray(self.weight, dtype=np.float64)[lid][:, None]
+            w_all = npa["weight"] if npa is not None else np.asarray(self.weight, dtype=np.float64)
+            V = V * w_all[lid][:, None]
         kv = V.shape[1] if V.ndim == 2 else 1
         nodes[lid, 0] = -1
         nodes[lid, 1] = np.arange(len(lid), dtype=np.int32) * kv
@@ -655,7 +665,8 @@ class Forest:
         nodes[cid, 1] = np.arange(len(cid), dtype=np.int32)
         nid = np.nonzero(num)[0]
         nodes[nid, 0] = feat[nid]
-        nodes[nid, 1] = np.asarray(self.thr, dtype=np.float64)[nid].astype(np.float32).view(np.int32)
+        thr = npa["thr"] if npa is not None else np.asarray(self.thr, dtype=np.float64)
+        nodes[nid, 1] = thr[nid].astype(np.float32).view(np.int32)
         inner = ~leaf
         nodes[inner, 2] = left[inner]
         nodes[inner, 3] = right[inner]

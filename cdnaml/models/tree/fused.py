@@ -66,6 +66,9 @@ def forest_arrays(forest: Forest) -> dict:
     A = {n: np.asarray(F[n], dtype=np.float64 if n in ("thr", "weight", "gain", "impurity") else np.int64)
          for n in ("feat", "left", "right", "thr", "bin", "weight", "gain", "impurity", "depth")}
     A.update(catmask=F["catmask"], is_cat=F["is_cat"], value=F["value"])
+    A["is_cat_arr"] = np.asarray(F["is_cat"], dtype=bool)
+    A["value_mat"] = np.asarray(F["value"], dtype=np.float64).reshape(len(F["value"]), -1) if len(F["value"]) \
+        else np.zeros((0, forest.K))
     return A
 
 
@@ -116,6 +119,13 @@ def truncate_forest(forest: Forest, num_trees: int, max_depth: int, arrays: Opti
     O["impurity"].extend(A["impurity"][g].tolist())
     O["depth"].extend(A["depth"][g].tolist())
     out.roots.extend(newid[roots].tolist())
+    # the cut's node fields as arrays too: Forest.device_arrays (the predictor of every grid model) reads them
+    # instead of converting the lists back (~0.3 s of a 27-model L07 grid evaluation)
+    lnew = np.where(inn, newid[np.where(inn, left[g], 0)], -1)
+    rnew = np.where(inn, newid[np.where(inn, right[g], 0)], -1)
+    out._np = {"feat": np.where(inn, feat[g], -1), "thr": np.where(inn, A["thr"][g], 0.0), "left": lnew,
+               "right": rnew, "is_cat": A["is_cat_arr"][g] & inn if "is_cat_arr" in A else None,
+               "value": A["value_mat"][g] if "value_mat" in A else None, "weight": A["weight"][g]}
     return out
 
 
