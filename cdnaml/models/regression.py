@@ -17,7 +17,6 @@ from typing import Optional
 
 import numpy as np
 import torch
-from scipy.linalg import cho_factor as _scipy_cho_factor, cho_solve as _scipy_cho_solve
 
 from ..ops import kernels as K
 from ..sql import types as T
@@ -163,11 +162,13 @@ def _lr_shift(Xk: torch.Tensor, yk: torch.Tensor, comm, d: int) -> torch.Tensor:
 
 
 def _cho_factor(A):
-    return _scipy_cho_factor(A, lower=True, check_finite=False)
+    from scipy.linalg import cho_factor  # lazily: tree / xgboost imports of this module need no scipy
+    return cho_factor(A, lower=True, check_finite=False)
 
 
 def _cho_solve(cl, b):
-    return _scipy_cho_solve(cl, b, check_finite=False)
+    from scipy.linalg import cho_solve
+    return cho_solve(cl, b, check_finite=False)
 
 
 # =========================================================== LinearRegression

@@ -918,7 +918,36 @@ def _settled_list(name: str):
 
     def set_(self, v):
         self.__dict__[key] = v
+        self.__dict__.pop("_np", None)  # a reassigned node list invalidates a cut's array snapshot
     return property(get, set_)
+
+
+class _FrozenList(list):
+    """A node list of a forest cut by the fused tuner (truncate_forest): its node fields are also held as an
+    array snapshot (``Forest._np``) that the predictor reads instead of the lists, so the lists must not change
+    after the cut.  Reads are plain list reads; every in-place mutation raises."""
+
+    def _frozen(self, *a, **k):
+        raise TypeError("the node lists of a cut forest are immutable (its array snapshot feeds the predictor); "
+                        "build a new Forest instead")
+
+    __setitem__ = __delitem__ = __iadd__ = __imul__ = append = extend = insert = pop = remove = clear = \
+        sort = reverse = _frozen
+
+    def __reduce__(self):  # pickle / deepcopy rebuild from a plain list (the default would extend())
+        return (_FrozenList, (list(self),))
+
+
+def freeze_cut(forest: "Forest", arrays: dict) -> None:
+    """Attach the cut's node arrays (read-only) to ``forest`` and freeze its node lists (see _FrozenList)."""
+    d = forest.__dict__
+    for n in _NODE_FIELDS:
+        d["_" + n] = _FrozenList(d["_" + n])
+    d["roots"] = _FrozenList(d["roots"])
+    for a in arrays.values():
+        if isinstance(a, np.ndarray):
+            a.flags.writeable = False
+    d["_np"] = arrays
 
 
 _NODE_FIELDS = ("feat", "thr", "bin", "left", "right", "catmask", "is_cat", "value", "weight", "gain", "impurity",
@@ -1911,7 +1940,7 @@ class ForestTrainer:
             if len(nl) and deep_switch and use_codes and depth + 1 >= 8:
                 # the next level can hold more than 255 nodes per tree: leave the u16 codes for node ids
                 # (active index of the node, -1 = done), partitioned and histogrammed by the node-id kernels
-                node, wdeep = K.decode_codes(codes, tfirst.to(codes.device))
+                node, wdeep = K.decode_codes(codes, tfirst)  # host tfirst: uploaded once, no D2H
                 node = node.contiguous()
                 # the node-id histogram kernels (levels past NODE_COMPACT_MAX_LOC nodes per tree) read the row weights
                 # from ``weights``: None when the bootstrap draws arrived as row codes (BootstrapCodes)

@@ -35,7 +35,7 @@ import numpy as np
 import torch
 
 from ...ops import kernels as K
-from .engine import Forest, ForestTrainer, TreeParams
+from .engine import Forest, ForestTrainer, TreeParams, freeze_cut
 
 FUSED_TUNING = os.environ.get("CDNAML_FUSED_TUNING", "1") != "0"
 
@@ -123,9 +123,9 @@ def truncate_forest(forest: Forest, num_trees: int, max_depth: int, arrays: Opti
     # instead of converting the lists back (~0.3 s of a 27-model L07 grid evaluation)
     lnew = np.where(inn, newid[np.where(inn, left[g], 0)], -1)
     rnew = np.where(inn, newid[np.where(inn, right[g], 0)], -1)
-    out._np = {"feat": np.where(inn, feat[g], -1), "thr": np.where(inn, A["thr"][g], 0.0), "left": lnew,
-               "right": rnew, "is_cat": A["is_cat_arr"][g] & inn if "is_cat_arr" in A else None,
-               "value": A["value_mat"][g] if "value_mat" in A else None, "weight": A["weight"][g]}
+    freeze_cut(out, {"feat": np.where(inn, feat[g], -1), "thr": np.where(inn, A["thr"][g], 0.0), "left": lnew,
+                     "right": rnew, "is_cat": A["is_cat_arr"][g] & inn if "is_cat_arr" in A else None,
+                     "value": A["value_mat"][g] if "value_mat" in A else None, "weight": A["weight"][g]})
     return out
 
 

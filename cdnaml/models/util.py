@@ -88,17 +88,29 @@ def streamed_columns(df, features_col: str, cols: List[str], head_rows: int = 0)
     parts = {c: [] for c in cols}
     n, d = 0, None
     head = []
+    ok = True
     for b in sel._plan.iter_execute():
         if n < head_rows:
             head.append(b.columns[features_col].values[:head_rows - n].float().clone())
         for c in cols:
             cd = b.columns[c]
             if cd.valid is not None and not bool(cd.valid.all()):
-                return None  # null labels / weights: the materialised path drops those rows
+                ok = False  # null labels / weights: the materialised path drops those rows
+                break
             parts[c].append(cd.values.clone())  # the source reuses its chunk buffers
+        if not ok:
+            break
         d = int(b.columns[features_col].values.shape[1])
         n += b.n
-    if d is None:
+    # the streamed and materialised paths issue different collectives, so every rank takes the same one: any
+    # rank with nulls sends all of them to the materialised path; a rank with no chunks streams an empty shard
+    # of the width the other ranks saw
+    comm = df._session.comm
+    if comm.distributed:
+        ok = comm.all_reduce_scalar(1.0 if ok else 0.0, "min") > 0.5
+        d = int(comm.all_reduce_scalar(float(-1 if d is None else d), "max"))
+        d = None if d < 0 else d
+    if not ok or d is None:
         return None
     dev = df._session.device
     out = {}

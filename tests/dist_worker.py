@@ -224,6 +224,49 @@ def scenario_trees_deep(spark):
     return out
 
 
+def scenario_ooc_uneven(spark):
+    """Out-of-core (streamed) fits with the last rank's shard EMPTY: every rank must take the same
+    streamed path (the choice is agreed over ranks) and the forests must equal the 1-rank streamed fit."""
+    import torch
+    from cdnaml.ml.regression import RandomForestRegressor
+    from cdnaml.ml.xgboost import XgboostRegressor
+    from cdnaml.models import util
+    from cdnaml.sql import types as T
+    from cdnaml.utils.synthetic import forest_digest
+    comm = spark.comm
+    W, r = comm.world_size, comm.rank
+    n, d = 3001, 8
+    rng = np.random.default_rng(5)
+    X = rng.normal(size=(n, d)).astype(np.float32)
+    y = (X[:, 0] * 2 - X[:, 1] + np.sin(2 * X[:, 2])).astype(np.float64)
+    owners = max(W - 1, 1)  # the last rank of a multi-rank job holds no rows
+    a, b = (n * r // owners, n * (r + 1) // owners) if r < owners else (n, n)
+
+    def chunks():
+        for r0 in range(a, b, 700):
+            yield {"features": X[r0:min(b, r0 + 700)], "label": y[r0:min(b, r0 + 700)]}
+    schema = T.StructType([T.StructField("features", T.VectorUDT(), True),
+                           T.StructField("label", T.DoubleType(), True)])
+    df = spark.createDataFrameFromChunks(chunks, max_rows=700, schema=schema)
+    seen = {"streamed": 0}
+    orig = util.streamed_columns
+
+    def counted(*args, **kw):
+        res = orig(*args, **kw)
+        seen["streamed"] += res is not None
+        return res
+    import cdnaml.models.regression as R
+    import cdnaml.models.xgboost as XG
+    R.streamed_columns = XG.streamed_columns = counted
+    out = {}
+    for k, est in {"rf": RandomForestRegressor(numTrees=6, maxDepth=4, maxBins=32, seed=2),
+                   "xgb": XgboostRegressor(n_estimators=3, max_depth=3, learning_rate=0.3, random_state=1,
+                                           missing=0.0)}.items():
+        out[k] = forest_digest(est.fit(df)._forest)
+    out["streamed"] = int(comm.all_reduce_scalar(float(seen["streamed"]), "min"))
+    return out
+
+
 def scenario_cv(spark):
     from cdnaml.ml.evaluation import RegressionEvaluator
     from cdnaml.ml.regression import RandomForestRegressor
@@ -318,6 +361,7 @@ SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault
              "trees_uneven": scenario_trees_uneven, "trees_rs": scenario_trees_rs,
              "trees_rs_overlap": scenario_trees_rs_overlap, "trees_deep": scenario_trees_deep, "cv": scenario_cv, "als": scenario_als,
              "hyperopt": scenario_hyperopt,
+             "ooc_uneven": scenario_ooc_uneven,
              "hyperopt_captured": scenario_hyperopt_captured}
 
 

@@ -126,3 +126,28 @@ def test_deep_fallback_node_histograms_use_bootstrap_weights(device, monkeypatch
         finally:
             spark.stop()
         assert got[True] == got[False]
+
+
+def test_cut_forest_lists_are_frozen(spark):
+    """the predictor of a forest cut by the fused tuner reads the cut's array snapshot, so the cut's
+    node lists must not change after the cut (mutation raises); pickling and reassigning still work (a
+    reassigned list drops the snapshot, so the predictor rebuilds from the lists)."""
+    import pickle
+    from cdnaml.ml.regression import RandomForestRegressor
+    from cdnaml.models.tree.fused import truncate_forest
+    from cdnaml.utils.synthetic import forest_digest
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn((3000, 6), generator=g)
+    y = (X[:, 0] - 2 * X[:, 1]).double()
+    df = spark.createDataFrameFromLocalTensors({"features": X.to(spark.device), "label": y.to(spark.device)})
+    m = RandomForestRegressor(numTrees=3, maxDepth=4, maxBins=16, seed=1).fit(df)
+    cut = truncate_forest(m._forest, 2, 3)
+    for op in (lambda: cut.thr.__setitem__(0, 1.0), lambda: cut.feat.append(-1), lambda: cut.value.pop(),
+               lambda: cut.roots.extend([0])):
+        with pytest.raises(TypeError):
+            op()
+    assert not cut._np["thr"].flags.writeable
+    back = pickle.loads(pickle.dumps(cut))
+    assert forest_digest(back) == forest_digest(cut)
+    cut.thr = [t + 0.0 for t in cut.thr]
+    assert "_np" not in cut.__dict__

@@ -173,3 +173,13 @@ def test_reduce_scatter_with_overlap_enabled(tmp_path):
         assert la["ov"] > 0 and la["rs"] > 0, (w, la)   # overlap at the shallow levels, RS below
         assert lb["rs"] > 0 and lb["ov"] == 0, (w, lb)  # RS from level 0: the overlap branch stays off
         assert got == one, w
+
+
+def test_ooc_fit_with_an_empty_shard(tmp_path):
+    """the streamed / materialised choice is agreed over ranks, and a rank without chunks streams an
+    empty shard -- no rank falls back alone (different collectives would hang the fit)."""
+    one = _run("ooc_uneven", tmp_path, 1)
+    assert one["streamed"] == 2
+    for w in (2, 3):
+        got = _run("ooc_uneven", tmp_path, w)
+        assert got == one, (w, got, one)
