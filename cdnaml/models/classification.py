@@ -2,7 +2,8 @@
 
 LogisticRegression (binomial): every L-BFGS / OWL-QN iteration is ONE pass of
 the fused K11 HIP kernel (margin, log-loss and gradient together) plus one
-RCCL all-reduce of d+2 doubles.  Multinomial uses device GEMMs.  Tree
+RCCL all-reduce of d+2 doubles; its margins are fp64 (Spark's Double).  Multinomial uses fp64 GEMMs at course
+sizes, fp32 device GEMMs above MULTINOMIAL_F64_MAX.  Tree
 classifiers (DT / RF / GBT) share the histogram engine with class-count
 statistics (gini / entropy).  Reference: MLE 03 - Logistic Regression
 Lab.py:99-158; Labs/ML 07L:42-209 (RandomForestClassifier + AUC).
@@ -27,6 +28,10 @@ from .regression import (_GBT, _PRED, _RF, _TREE, _TreeModelBase, _bag_weights, 
                          _subforest, resolve_subset, tree_fit_prepare)
 from .tree.engine import Forest, ForestTrainer, TreeParams
 from .util import IllegalArgumentException, centered_gram, local_batch, local_xyw, require_vector
+
+# multinomial logistic regression: fp64 logits / gradients up to this many n*d*C multiply-adds per pass (course
+# sizes; Spark's Double), the fp32 device GEMMs above
+MULTINOMIAL_F64_MAX = 4e9
 
 _CLS = dict(_PRED, **{
     "probabilityCol": ("Column name for predicted class conditional probabilities.", "probability", TC.toString),
@@ -137,11 +142,17 @@ class LogisticRegression(Estimator):
             sd_t = torch.tensor(sdz, dtype=torch.float32, device=X.device)
             wv = w if w is not None else None
 
+            # course-sized problems take fp64 logits and gradients (Spark's Double); large ones the fp32 GEMMs
+            f64 = X.shape[0] * d * C <= MULTINOMIAL_F64_MAX
+            if f64:
+                sd_t = sd_t.double()
+
             def fg(theta):
                 Wm = theta[: C * d].reshape(C, d)
                 b = theta[C * d:] if fit_int else np.zeros(C)
-                Wt = torch.tensor(Wm, dtype=torch.float32, device=X.device) / sd_t[None, :]
-                logits = (X @ Wt.T).double() + torch.tensor(b, dtype=torch.float64, device=X.device)
+                Wt = torch.tensor(Wm, dtype=sd_t.dtype, device=X.device) / sd_t[None, :]
+                logits = (_margins64(X, Wt) if f64 else (X @ Wt.T).double()) + \
+                    torch.tensor(b, dtype=torch.float64, device=X.device)
                 lse = torch.logsumexp(logits, 1)
                 ll = lse - (logits * Yoh).sum(1)
                 P = torch.softmax(logits, 1)
@@ -149,7 +160,7 @@ class LogisticRegression(Estimator):
                 if wv is not None:
                     ll = ll * wv
                     R = R * wv[:, None]
-                gW = (R.float().T @ X).double() / sd_t.double()[None, :]
+                gW = ((R.T @ X.double()) if f64 else (R.float().T @ X).double()) / sd_t.double()[None, :]
                 gb = R.sum(0)
                 acc = torch.cat([gW.reshape(-1), gb, ll.sum().reshape(1)])
                 comm.all_reduce(acc)
@@ -170,6 +181,16 @@ class LogisticRegression(Estimator):
         model._post_fit(self)
         model.summary = _LogRegTrainingSummary(model, dataset, hist, iters)
         return model
+
+
+def _margins64(X: torch.Tensor, W: torch.Tensor, chunk: int = 1 << 20) -> torch.Tensor:
+    """X [n, d] (fp32 features) @ W[C, d].T with fp64 products and sums (Spark's Double margins), in row chunks
+    so the fp64 copy of X stays small."""
+    W = W.to(X.device, torch.float64)
+    out = torch.empty((X.shape[0], W.shape[0]), dtype=torch.float64, device=X.device)
+    for r0 in range(0, X.shape[0], chunk):
+        out[r0:r0 + chunk] = X[r0:r0 + chunk].double() @ W.T
+    return out
 
 
 class LogisticRegressionModel(Model):
@@ -220,7 +241,7 @@ class LogisticRegressionModel(Model):
         fc = self.getFeaturesCol()
         require_vector(dataset, fc)
         names = (self.getRawPredictionCol(), self.getPredictionCol(), self.getProbabilityCol())
-        W = torch.tensor(self._W, dtype=torch.float32)
+        W = torch.tensor(self._W, dtype=torch.float64)
         bvec = torch.tensor(self._b, dtype=torch.float64)
         multi, thr = self._multi, self.getThreshold()
         thresholds = self.getThresholds()
@@ -232,13 +253,13 @@ class LogisticRegressionModel(Model):
                 z = torch.zeros((0, max(self._C, 2)), dtype=torch.float64, device=X.device)
                 return _append_cls_outputs(b, z, z, z[:, 0], (names[0], names[1], names[2]))
             if not multi:
-                m = (X @ Wd[0]).double() + bd[0]
+                m = _margins64(X, Wd[:1])[:, 0] + bd[0]
                 raw = torch.stack([-m, m], 1)
                 p1 = torch.sigmoid(m)
                 prob = torch.stack([1 - p1, p1], 1)
                 pred = (p1 > thr).double() if not thresholds else _argmax_with_thresholds(prob, thresholds)
             else:
-                raw = (X @ Wd.T).double() + bd
+                raw = _margins64(X, Wd) + bd
                 prob = torch.softmax(raw, 1)
                 pred = _argmax_with_thresholds(prob, thresholds)
             return _append_cls_outputs(b, raw, prob, pred, (names[0], names[1], names[2]))

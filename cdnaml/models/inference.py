@@ -42,7 +42,7 @@ class ForestPredictor:
         self.forest = forest
         self.kind = values_kind
         self.device = torch.device(device) if device is not None else None
-        self.tw_host = np.asarray(tree_w, np.float32)
+        self.tw_host = np.asarray(tree_w, np.float64)
         self.base = base
         self._dev: Dict[str, tuple] = {}
         self._graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
@@ -56,14 +56,15 @@ class ForestPredictor:
         if key not in self._dev:
             from ..ops import kernels as K
             f = self.forest
-            base_np = np.asarray(0.0 if self.base is None else self.base, np.float32).reshape(-1)
+            base_np = np.asarray(0.0 if self.base is None else self.base, np.float64).reshape(-1)
             pre = getattr(f, "_heap_np", None)
             hkey = ("heap", str(dev), self.kind)
             if (dev.type == "cuda" and f.K == 1 and self.kind == "value" and pre is not None and hkey not in f._dev
                     and pre[0].shape[0] == len(f.roots)):
                 # the trainer-built heap table rides the same pinned staging block and copy as the tree weights
-                tw, bb, h_t, m_t = K.upload(dev, self.tw_host.reshape(-1), base_np, pre[0], np.zeros(8, np.int32))
-                f._dev[hkey] = (h_t, pre[1], m_t)
+                tw, bb, h_t, m_t = K.upload(dev, self.tw_host.reshape(-1), base_np, K.pack_heap(*pre),
+                                            np.zeros(8, np.int32))
+                f._dev[hkey] = (h_t, pre[2], m_t)
             else:
                 # async pinned uploads: a pageable torch.tensor(..., device=) copy waits for the queue to drain
                 tw, bb = K.upload(dev, self.tw_host.reshape(-1), base_np)
@@ -72,7 +73,7 @@ class ForestPredictor:
             self._dev[key] = (tw, heap, b)
         return self._dev[key]
 
-    def _launch(self, X: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    def _launch(self, X: torch.Tensor, dtype=torch.float64) -> torch.Tensor:
         from ..ops import kernels as K
         tw, heap, b = self._arrays(X.device)
         if heap is not None:
@@ -84,9 +85,9 @@ class ForestPredictor:
         nodes, roots, vals, masks = self.forest.device_arrays(X.device, self.kind)
         return K.tree_predict(X, nodes, roots, tw, vals, masks, self.forest.K, b).to(dtype)
 
-    def __call__(self, X: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
-        """[n, d] features -> [n, K] predictions (a fresh tensor the caller owns): float32 sums, stored as
-        ``dtype`` (float64: widened in the kernel's store, == ``.double()`` of the float32 result)."""
+    def __call__(self, X: torch.Tensor, dtype=torch.float64) -> torch.Tensor:
+        """[n, d] features -> [n, K] predictions (a fresh tensor the caller owns): fp64 leaf values, weights and
+        sums in one fixed tree order (K.ordered_tree_sum), stored as ``dtype``."""
         if not (GRAPH_PREDICT and X.is_cuda and X.shape[0] >= GRAPH_MIN_ROWS and X.is_contiguous()):
             return self._launch(X, dtype)
         if threading.current_thread() is not threading.main_thread():
@@ -97,7 +98,7 @@ class ForestPredictor:
         with self._lock:
             return self._graph_call(X, key, dtype)
 
-    def _graph_call(self, X: torch.Tensor, key, dtype=torch.float32) -> torch.Tensor:
+    def _graph_call(self, X: torch.Tensor, key, dtype=torch.float64) -> torch.Tensor:
         g = self._graphs.get(key)
         if g is None:
             # capture on the second sighting of a buffer: staging buffers recur, one-off tensors do not

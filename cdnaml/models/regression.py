@@ -26,8 +26,8 @@ from .base import Estimator, Model
 from .linalg import DenseVector, SparseVector
 from .param import NO_DEFAULT, TypeConverters as TC, keyword_init
 from .tree.engine import Forest, ForestTrainer, TreeParams, make_binned
-from .util import (IllegalArgumentException, categorical_info, global_count, global_offset, local_batch,
-                   local_xyw, require_vector, streamed_columns)
+from .util import (IllegalArgumentException, categorical_info, global_count, global_offset, gram_fp64_auto,
+                   local_batch, local_xyw, require_vector, streamed_columns)
 
 _PRED = {
     "featuresCol": ("features column name", "features", TC.toString),
@@ -132,17 +132,14 @@ class LinearRegressionTrainingSummary(_RegressionSummary):
         return [float(2 * stats.t.sf(abs(t), dof)) for t in self.tValues]
 
 
-GRAM_FP64_MAX_WORK = float(__import__("os").environ.get("CDNAML_GRAM_FP64_MAX_WORK", "4e9"))
-
-
 def _gram_fp64(prec: str, n: int, d: int) -> bool:
-    """gramPrecision "auto": problems of at most GRAM_FP64_MAX_WORK multiply-adds (n (d + 2)^2; d = 100: ~4e5
-    rows) take an fp64 library GEMM of the augmented matrix -- Spark's normal-equation solver works in fp64 and
-    course-sized one-hot designs are ill-conditioned (condition ~1e4: the K1 kernel's fp32 block accumulation
-    moved coefficients by ~2e-3 relative); larger ones take K1 (fp32 MFMA, HBM-bound)."""
+    """gramPrecision "auto" (util.gram_fp64_auto): course-sized problems take an fp64 library GEMM of the
+    augmented matrix -- Spark's normal-equation solver works in fp64 and course-sized one-hot designs are
+    ill-conditioned (condition ~1e4: the K1 kernel's fp32 block accumulation moved coefficients by ~2e-3
+    relative); larger ones take K1 (fp32 MFMA, HBM-bound)."""
     if prec == "fp64":
         return True
-    return prec == "auto" and float(n) * (d + 2) ** 2 <= GRAM_FP64_MAX_WORK
+    return prec == "auto" and gram_fp64_auto(n, d)
 
 
 def _lr_shift(Xk: torch.Tensor, yk: torch.Tensor, comm, d: int) -> torch.Tensor:

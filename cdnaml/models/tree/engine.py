@@ -480,7 +480,8 @@ class Forest:
         self.depth: List[int] = []
         self.roots: List[int] = []
         self._dev = {}
-        self._heap_np = None  # (heap [T, 2^(D+1)-1, 2] int32, D) built by ForestTrainer.train, or None
+        self._heap_np = None  # (struct [T, 2^(D+1)-1, 2] int32, leaf values [T, 2^(D+1)-1] f64, D) built by
+        # ForestTrainer.train (Forest.heap_struct's arrays), or None
 
     def settle(self) -> None:
         """Run the deferred bookkeeping (idempotent; a no-op when nothing is pending)."""
@@ -670,7 +671,7 @@ class Forest:
         inner = ~leaf
         nodes[inner, 2] = left[inner]
         nodes[inner, 3] = right[inner]
-        vals = V.reshape(-1).astype(np.float32) if V.size else np.zeros(1, np.float32)
+        vals = V.reshape(-1).astype(np.float64) if V.size else np.zeros(1, np.float64)
         masks = (np.stack([self.catmask[i] for i in cid.tolist()]).view(np.int32).reshape(-1) if len(cid)
                  else np.zeros(8, np.int32))
         out = tuple(K.upload(device, nodes, np.asarray(self.roots, dtype=np.int32), vals, masks))
@@ -732,54 +733,67 @@ class Forest:
         return out
 
     def heap_arrays(self, device, values_kind: str = "value"):
-        """Single-output forests of depth <= 8: heap layout [T, 2^(D+1)-1, 2] int32 (children of slot i at
-        2i+1 / 2i+2; {feature | -1 leaf | -(f+2) categorical, threshold / leaf value / mask-offset bits})
-        plus the categorical masks, or None."""
+        """Single-output forests of depth <= 8: the packed predict heap (``K.pack_heap``: int32 [T, 2^(D+2)-2],
+        internal slots {feature | -1 pass-through | -(f+2) categorical, threshold / mask-offset bits} with the
+        children of slot i at 2i+1 / 2i+2, then the depth-D leaf values as fp64) plus the categorical masks, or
+        None."""
         key = ("heap", str(device), values_kind)
         if key in self._dev:
             return self._dev[key]
         pre = getattr(self, "_heap_np", None)
         if values_kind == "value" and pre is not None and pre[0].shape[0] == len(self.roots):
             # filled level by level by the trainer (the same table as below; tests/test_engine_heap.py)
-            h_t, m_t = K.upload(device, pre[0], np.zeros(8, np.int32))
-            res = (h_t, pre[1], m_t)
+            h_t, m_t = K.upload(device, K.pack_heap(pre[0], pre[1], pre[2]), np.zeros(8, np.int32))
+            res = (h_t, pre[2], m_t)
             self._dev[key] = res
             return res
         res = None
-        feat = np.asarray(self.feat, dtype=np.int64)  # one list conversion shared with _layout (~1.3k nodes)
-        tree_of, slot, dep = self._layout(feat)
-        D = int(dep.max()) if self.roots else 0
-        if self.K == 1 and self.roots and D <= 8:
-            S = 2 ** (D + 1) - 1
-            heap = np.zeros((len(self.roots), S, 2), dtype=np.int32)
-            heap[:, :, 0] = -1
-            live = np.nonzero(tree_of >= 0)[0]
-            lt, ls = tree_of[live], slot[live]
-            fl = feat[live].astype(np.int32)
-            leaf = fl < 0
-            vl = self.value
-            v = (np.concatenate([vl[i] for i in live[leaf].tolist()]) if leaf.any()
-                 else np.zeros(0)).astype(np.float64)
-            if values_kind != "value":
-                v = v * np.asarray(self.weight, dtype=np.float64)[live[leaf]]
-            heap[lt[leaf], ls[leaf], 1] = v.astype(np.float32).view(np.int32)
-            sp = ~leaf
-            isc = np.asarray(self.is_cat, dtype=bool)[live] & sp
-            num = sp & ~isc
-            heap[lt[num], ls[num], 0] = fl[num]
-            heap[lt[num], ls[num], 1] = np.asarray(self.thr, dtype=np.float64)[live[num]].astype(
-                np.float32).view(np.int32)
-            cat_ids = live[isc]
-            masks = [self.catmask[i].view(np.int32) for i in cat_ids.tolist()]
-            heap[lt[isc], ls[isc], 0] = -(fl[isc] + 2)
-            heap[lt[isc], ls[isc], 1] = np.arange(len(cat_ids), dtype=np.int32)
-            h_t, m_t = K.upload(device, heap, np.concatenate(masks) if masks else np.zeros(8, np.int32))
+        hs = self.heap_struct(values_kind)
+        if hs is not None:
+            struct, vals, D, masks = hs
+            h_t, m_t = K.upload(device, K.pack_heap(struct, vals, D), masks)
             res = (h_t, D, m_t)
         self._dev[key] = res
         return res
 
+    def heap_struct(self, values_kind: str = "value"):
+        """(struct int32 [T, 2^(D+1)-1, 2], leaf values f64 [T, 2^(D+1)-1], D, masks) of a single-output forest
+        of depth <= 8 (``K.pack_heap``'s input; the trainer fills the same arrays level by level), else None."""
+        feat = np.asarray(self.feat, dtype=np.int64)  # one list conversion shared with _layout (~1.3k nodes)
+        tree_of, slot, dep = self._layout(feat)
+        D = int(dep.max()) if self.roots else 0
+        if not (self.K == 1 and self.roots and D <= 8):
+            return None
+        S = 2 ** (D + 1) - 1
+        heap = np.zeros((len(self.roots), S, 2), dtype=np.int32)
+        heap[:, :, 0] = -1
+        hv = np.zeros((len(self.roots), S), dtype=np.float64)
+        live = np.nonzero(tree_of >= 0)[0]
+        lt, ls = tree_of[live], slot[live]
+        fl = feat[live].astype(np.int32)
+        leaf = fl < 0
+        vl = self.value
+        v = (np.concatenate([vl[i] for i in live[leaf].tolist()]) if leaf.any()
+             else np.zeros(0)).astype(np.float64)
+        if values_kind != "value":
+            v = v * np.asarray(self.weight, dtype=np.float64)[live[leaf]]
+        hv[lt[leaf], ls[leaf]] = v
+        sp = ~leaf
+        isc = np.asarray(self.is_cat, dtype=bool)[live] & sp
+        num = sp & ~isc
+        heap[lt[num], ls[num], 0] = fl[num]
+        heap[lt[num], ls[num], 1] = np.asarray(self.thr, dtype=np.float64)[live[num]].astype(
+            np.float32).view(np.int32)
+        cat_ids = live[isc]
+        masks = [self.catmask[i].view(np.int32) for i in cat_ids.tolist()]
+        heap[lt[isc], ls[isc], 0] = -(fl[isc] + 2)
+        heap[lt[isc], ls[isc], 1] = np.arange(len(cat_ids), dtype=np.int32)
+        return heap, hv, D, (np.concatenate(masks) if masks else np.zeros(8, np.int32))
+
     def predict(self, X: torch.Tensor, tree_w: np.ndarray, base=None, values_kind="value") -> torch.Tensor:
-        tw, = K.upload(X.device, np.asarray(tree_w, np.float32).reshape(-1))
+        """[n, K] float64 predictions: base + sum_t tree_w[t] * leaf value, all fp64 in one fixed tree order on
+        every device (K.ordered_tree_sum)."""
+        tw, = K.upload(X.device, np.asarray(tree_w, np.float64).reshape(-1))
         if self.K == 1 and X.device.type == "cuda" and HEAP_PREDICT:
             ha = self.heap_arrays(X.device, values_kind)
             if ha is not None:
@@ -788,7 +802,7 @@ class Forest:
                 if out is not None:
                     return out
         nodes, roots, vals, masks = self.device_arrays(X.device, values_kind)
-        b = None if base is None else K.upload(X.device, np.asarray(base, np.float32).reshape(-1))[0]
+        b = None if base is None else K.upload(X.device, np.asarray(base, np.float64).reshape(-1))[0]
         return K.tree_predict(X, nodes, roots, tw, vals, masks, self.K, b)
 
     def predict_leaf_index(self, X: torch.Tensor) -> torch.Tensor:
@@ -1438,10 +1452,11 @@ class ForestTrainer:
         # single-output forests of depth <= 8 with numeric splits: the predict heap table (Forest.heap_arrays) is
         # filled level by level here, from the keys and values the levels already hold, instead of re-walking the
         # finished forest in Python between the last split and the transform (the GPU idles through that)
-        heap = None
+        heap = heap_v = None
         if fresh and not self.classification and p.max_depth <= 8 and not data.categorical and not data.missing_bin:
             heap = np.zeros((T, 2 ** (p.max_depth + 1) - 1, 2), dtype=np.int32)
             heap[:, :, 0] = -1
+            heap_v = np.zeros((T, 2 ** (p.max_depth + 1) - 1), dtype=np.float64)  # leaf values per slot (fp64)
         heap_depth = 0
         need_masks = p.feature_subset is not None and p.feature_subset < d
         # "masked": accumulate only each node's sampled features (fewer atomics, no subtraction);
@@ -1855,7 +1870,7 @@ class ForestTrainer:
                                         self._impurities_v(a_stats))
                 node_count = forest.num_nodes
                 if heap is not None:
-                    heap[a_tree, 0, 1] = self._leaf_values_v(a_stats)[:, 0].astype(np.float32).view(np.int32)
+                    heap_v[a_tree, 0] = self._leaf_values_v(a_stats)[:, 0]
                 for t_, fid_ in zip(a_tree.tolist(), a_fid.tolist()):
                     root_ids[t_] = fid_
             W_a = self._weights_v(a_stats)
@@ -1986,7 +2001,7 @@ class ForestTrainer:
                     heap[tsp, ksp - 1, 0] = f_sp
                     heap[tsp, ksp - 1, 1] = thr_sp.astype(np.float32).view(np.int32)
                     ck = np.stack([2 * ksp, 2 * ksp + 1], 1).reshape(-1)
-                    heap[np.repeat(tsp, 2), ck - 1, 1] = ch_vals[:, 0].astype(np.float32).view(np.int32)
+                    heap_v[np.repeat(tsp, 2), ck - 1] = ch_vals[:, 0]
                     heap_depth = depth + 1
             prev_hist = H if subtract else None
             emitted = em_next
@@ -2000,5 +2015,6 @@ class ForestTrainer:
         forest.roots.extend(root_ids)
         forest._dev = {}
         if heap is not None:
-            forest._heap_np = (np.ascontiguousarray(heap[:, :2 ** (heap_depth + 1) - 1]), heap_depth)
+            S_ = 2 ** (heap_depth + 1) - 1
+            forest._heap_np = (np.ascontiguousarray(heap[:, :S_]), np.ascontiguousarray(heap_v[:, :S_]), heap_depth)
         return forest

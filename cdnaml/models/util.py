@@ -130,8 +130,19 @@ def streamed_columns(df, features_col: str, cols: List[str], head_rows: int = 0)
     return ChunkedRows(chunks, n, d, dev), out, sel.schema[features_col].metadata
 
 
+GRAM_FP64_MAX_WORK = float(__import__("os").environ.get("CDNAML_GRAM_FP64_MAX_WORK", "4e9"))
+
+
+def gram_fp64_auto(n: int, d: int) -> bool:
+    """Course-sized Gram matrices (at most GRAM_FP64_MAX_WORK multiply-adds, n (d + 2)^2; d = 100: ~4e5 rows) take
+    an fp64 library GEMM of the augmented fp32 rows -- Spark forms these statistics in Double and one-hot designs
+    are ill-conditioned -- larger ones the K1 kernel (fp32 MFMA, HBM-bound)."""
+    return float(n) * (d + 2) ** 2 <= GRAM_FP64_MAX_WORK
+
+
 def centered_gram(X: torch.Tensor, comm, lead: int = 1024):
-    """(n, mean[d], C[d, d]) over all ranks, C = sum (x - mean)(x - mean)^T, all fp64.
+    """(n, mean[d], C[d, d]) over all ranks, C = sum (x - mean)(x - mean)^T, all fp64 (the Gram in fp64 arithmetic
+    at course sizes: ``gram_fp64_auto``, so a feature standardisation equals the host's to rounding).
 
     The Gram kernel runs on features shifted by a common mean estimate (every rank's leading rows, averaged over
     the ranks that have any), so the second moments are formed about a point near the mean: E[x^2] - mean^2 of
@@ -146,7 +157,8 @@ def centered_gram(X: torch.Tensor, comm, lead: int = 1024):
         comm.all_reduce_many([sh, cnt])
         sh = sh / cnt.clamp_min(1.0)
     sh = sh.float()
-    G = K.gram(X, shift=sh) if n_loc else torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
+    G = K.gram(X, shift=sh, fp64=gram_fp64_auto(n_loc, d)) if n_loc else \
+        torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
     comm.all_reduce(G)
     n = float(G[d, d])
     s = G[:d, d]

@@ -1110,16 +1110,53 @@ def partition(bins: torch.Tensor, node: torch.Tensor, split_feat: torch.Tensor, 
 
 
 # --------------------------------------------------------------------- K8
-def tree_predict_heap(X: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: torch.Tensor,
-                      masks: torch.Tensor, base: float = 0.0, dtype=torch.float32) -> Optional[torch.Tensor]:
-    """Single-output ensemble prediction over a heap-laid-out forest (int32 [T, S, 2], S = 2^(depth+1)-1).
+def pack_heap(struct: np.ndarray, vals: np.ndarray, depth: int) -> np.ndarray:
+    """Predict-heap table (trees.hip predict_heap_kernel) from a per-slot forest layout.
 
-    dtype float64: the fp32 sums stored widened by the kernel (== the float32 result's .double()).
-    Returns None when the forest does not fit the kernel's LDS budget (use ``tree_predict``)."""
+    ``struct`` int32 [T, 2^(D+1)-1, 2]: per heap slot {feature | -1 leaf/unreachable | -(f+2) categorical,
+    threshold bits | mask offset}; ``vals`` float64 [T, 2^(D+1)-1]: the slot's leaf value.  Returns int32
+    [T, 2^(D+2)-2]: the 2^D-1 internal slots (leaf slots become pass-through-left), then the 2^D depth-D leaf
+    values as fp64, a shallower leaf's value at its leftmost depth-D descendant."""
+    T = struct.shape[0]
+    NI = (1 << depth) - 1
+    out = np.empty((T, 4 * NI + 2), dtype=np.int32)
+    out[:, :2 * NI] = struct[:, :NI].reshape(T, 2 * NI)
+    leaf = np.zeros((T, NI + 1), dtype=np.float64)
+    for k in range(depth, -1, -1):  # shallow last: a reachable leaf overwrites the unreachable slots below it
+        s0, s1 = (1 << k) - 1, (1 << (k + 1)) - 1
+        tt, ss = np.nonzero(struct[:, s0:s1, 0] == -1)
+        if len(tt):
+            leaf[tt, (s0 + ss + 1) * (1 << (depth - k)) - 1 - NI] = vals[tt, s0 + ss]
+    out[:, 2 * NI:] = leaf.view(np.int32)
+    return out
+
+
+def ordered_tree_sum(contribs, T: int, n: int, K: int, base=None) -> torch.Tensor:
+    """The fp64 ensemble sum in the device kernels' order (trees.hip predict_kernel): lane q = t % 4 adds
+    ``contribs(t)`` (tree_w[t] * leaf value, already a rounded product) for its trees in ascending order, then
+    base + lane 0 + lane 1 + lane 2 + lane 3.  The cpu predictions therefore equal the GPU's bit for bit."""
+    lanes = [torch.zeros((n, K), dtype=torch.float64) for _ in range(4)]
+    for t in range(T):
+        lanes[t & 3] += contribs(t)
+    out = torch.zeros((n, K), dtype=torch.float64)
+    if base is not None:
+        out += base.double().cpu()[None, :]
+    for q in range(4):
+        out += lanes[q]
+    return out
+
+
+def tree_predict_heap(X: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: torch.Tensor,
+                      masks: torch.Tensor, base: float = 0.0, dtype=torch.float64) -> Optional[torch.Tensor]:
+    """Single-output ensemble prediction over a packed heap forest (int32 [T, 2^(depth+2)-2], ``pack_heap``):
+    fp64 leaves, weights and sums (Spark's Double predictions), stored as ``dtype``.  Returns None when the forest
+    does not fit the kernel's LDS budget (use ``tree_predict``)."""
     n, d = X.shape
-    T, S, _ = heap.shape
+    T = heap.shape[0]
     if not _native(X):
         return None
+    assert heap.dtype == torch.int32 and heap.dim() == 2 and heap.shape[1] == (4 << depth) - 2, \
+        (tuple(heap.shape), depth)
     X = X.float()
     X = X if X.stride(1) == 1 else X.contiguous()
     out = torch.empty((n, 1), dtype=dtype, device=X.device)
@@ -1127,8 +1164,9 @@ def tree_predict_heap(X: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: t
         return out
     m = masks.int().contiguous() if masks.numel() else torch.zeros(8, dtype=torch.int32, device=X.device)
     f64 = dtype == torch.float64
-    rc = _lib.lib().cdna_tree_predict_heap(_ptr(X), n, d, X.stride(0), _ptr(heap), S, depth,
-                                           _ptr(tree_w.float().contiguous()), T, _ptr(m), float(base),
+    assert tree_w.numel() == T
+    rc = _lib.lib().cdna_tree_predict_heap(_ptr(X), n, d, X.stride(0), _ptr(heap.contiguous()), depth,
+                                           _ptr(tree_w.double().contiguous()), T, _ptr(m), float(base),
                                            None if f64 else _ptr(out), _ptr(out) if f64 else None,
                                            _stream(X.device))
     if rc == 1:  # hipErrorInvalidValue: over the LDS budget
@@ -1140,7 +1178,8 @@ def tree_predict_heap(X: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: t
 def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree_w: torch.Tensor,
                  values: torch.Tensor, masks: torch.Tensor, K: int, base: Optional[torch.Tensor] = None
                  ) -> torch.Tensor:
-    """Ensemble prediction on raw features -> float32 [n, K].
+    """Ensemble prediction on raw features -> float64 [n, K] (fp64 leaf values, weights and sums; the cpu path
+    sums in the kernel's order: ``ordered_tree_sum``).
 
     nodes: int32 [N, 4] packed as documented in trees.hip.
     """
@@ -1149,26 +1188,25 @@ def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree
     if _native(X):
         X = X.float()
         X = X if X.stride(1) == 1 else X.contiguous()
-        out = torch.empty((n, K), dtype=torch.float32, device=X.device)
+        out = torch.empty((n, K), dtype=torch.float64, device=X.device)
         if n:
             m = masks.int().contiguous() if masks.numel() else torch.zeros(8, dtype=torch.int32, device=X.device)
             nodes, roots = nodes.int().contiguous(), roots.int().contiguous()
-            tree_w, values = tree_w.float().contiguous(), values.float().contiguous()
-            base = None if base is None else base.float().contiguous()
+            tree_w, values = tree_w.double().contiguous(), values.double().contiguous()
+            base = None if base is None else base.double().contiguous()
             _lib.check(_lib.lib().cdna_tree_predict(_ptr(X), n, d, X.stride(0), _ptr(nodes), int(nodes.shape[0]),
                                                     _ptr(roots),
                                                     _ptr(tree_w), T, _ptr(values), _ptr(m), K, _ptr(base), _ptr(out),
                                                     int(values.numel()), _stream(X.device)), "cdna_tree_predict")
         return out
-    Xf = X.float()
-    out = torch.zeros((n, K), dtype=torch.float32)
-    if base is not None:
-        out += base.float()[None, :]
-    nd = nodes.long()
-    vals = values.float()
-    mk = masks.long() & 0xFFFFFFFF
+    Xf = X.float().cpu()
+    nd = nodes.long().cpu()
+    vals = values.double().cpu()
+    tw = tree_w.double().cpu()
+    mk = masks.long().cpu() & 0xFFFFFFFF
     rows = torch.arange(n)
-    for t in range(T):
+
+    def contrib(t):
         cur = torch.full((n,), int(roots[t]), dtype=torch.long)
         for _ in range(64):
             nv = nd[cur]
@@ -1191,8 +1229,8 @@ def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree
             cur = torch.where(internal, nxt, cur)
         off = nd[cur][:, 1]
         idx = off[:, None] + torch.arange(K)[None, :]
-        out += float(tree_w[t]) * vals[idx]
-    return out
+        return vals[idx] * tw[t]
+    return ordered_tree_sum(contrib, T, n, K, base).to(X.device)
 
 
 def predict_binned_add(bins: torch.Tensor, nodes: torch.Tensor, root: int, values: torch.Tensor,

@@ -312,6 +312,9 @@ __global__ __launch_bounds__(256) void kmeans_kernel(const float* __restrict__ X
 // One wave per row group; lanes span features (coalesced row reads), the dot
 // product is a wave butterfly, gradient accumulates lane-local then is folded
 // once per block (f64 global atomics).  grad has d+1 entries (+ intercept).
+// Everything past the fp32 feature load is fp64: w, the margin's products and its wave sum (Spark's Double
+// margins; the fp32 dot product moved the fitted objective by ~1e-3 relative against the host's fp64 one, and
+// L-BFGS at tol 1e-6 then stopped elsewhere).  The kernel stays HBM-bound on the fp32 rows.
 __global__ __launch_bounds__(256) void logistic_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                        const double* __restrict__ y, const double* __restrict__ wt,
                                                        const double* __restrict__ w, double b,
@@ -323,25 +326,25 @@ __global__ __launch_bounds__(256) void logistic_kernel(const float* __restrict__
   const int64_t gw = (int64_t)blockIdx.x * 4 + wid, nw = (int64_t)gridDim.x * 4;
   constexpr int FPL = 8;  // features per lane handled in registers (d <= 512)
   double gacc[FPL];
-  float wl[FPL];
+  double wl[FPL];
 #pragma unroll
   for (int q = 0; q < FPL; ++q) {
     gacc[q] = 0.0;
     const int f = lane + 64 * q;
-    wl[q] = f < d ? (float)w[f] : 0.f;
+    wl[q] = f < d ? w[f] : 0.0;
   }
   double gb = 0.0, ls = 0.0;
   for (int64_t r = gw; r < n; r += nw) {
     const float* x = X + r * ldx;
     float xv[FPL];
-    float dot = 0.f;
+    double dot = 0.0;
 #pragma unroll
     for (int q = 0; q < FPL; ++q) {
       const int f = lane + 64 * q;
       xv[q] = f < d ? x[f] : 0.f;
-      dot += xv[q] * wl[q];
+      dot += (double)xv[q] * wl[q];
     }
-    const double m = (double)cdna::wave_sum(dot) + b;
+    const double m = cdna::wave_sum(dot) + b;
     const double yy = y[r], ww = wt ? wt[r] : 1.0;
     const double p = 1.0 / (1.0 + exp(-m));
     const double res = ww * (p - yy);

@@ -567,31 +567,34 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint64_t* __restri
 //   continuous : {f, float_bits(thr), left, right}      left iff x <= thr
 //   categorical: {-(f+2), mask_off, left, right}        left iff bit (int)x
 //   leaf       : {-1, value_off, 0, 0}                  values[value_off .. +K]
-// out[r][k] = base[k] + sum_t tree_w[t] * leafval_t(r)[k]
-// Block = 256 threads = 64 rows x 4 tree lanes; the 64-row tile of X is
-// staged in LDS with coalesced loads, per-tree-lane partial sums folded in LDS.
+// out[r][k] = base[k] + sum_t tree_w[t] * leafval_t(r)[k], all in fp64 (Spark's Double predictions): the leaf
+// values, tree weights and sums are doubles, and the sum has ONE fixed order that the host reference
+// (kernels.tree_predict on cpu) repeats bit for bit: tree lane q = t % 4 adds its trees in ascending order
+// (product rounded, then added: no FMA contraction), then base + lane 0 + lane 1 + lane 2 + lane 3.
+// Block = 256 threads = 64 rows x 4 tree lanes; the 64-row tile of X is staged in LDS with coalesced loads.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void predict_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                       const int4* __restrict__ nodes, const int* __restrict__ roots,
-                                                      const float* __restrict__ tree_w, int T,
-                                                      const float* __restrict__ values, const uint32_t* __restrict__ masks,
-                                                      int K, const float* __restrict__ base, float* __restrict__ out,
+                                                      const double* __restrict__ tree_w, int T,
+                                                      const double* __restrict__ values,
+                                                      const uint32_t* __restrict__ masks, int K,
+                                                      const double* __restrict__ base, double* __restrict__ out,
                                                       int n_nodes_lds, int n_vals_lds) {
-  // LDS: [n_nodes_lds] int4 forest (when it fits), then X tile [64][d+1], then [4][64][K] partials.
+#pragma clang fp contract(off)
+  // LDS: [n_nodes_lds] int4 forest (when it fits), then (when n_vals_lds > 0) the leaf values and tree weights
+  // (doubles) and roots, then the X tile [64][d+1] floats, then [4][64][K] double partials.
   // rocprofv3 on the global-node version: 78 % of wave time waiting on the
   // dependent node loads of each root-to-leaf walk; walking an LDS copy of the
   // forest turns each step into a ~100-cycle ds_read_b128.
   extern __shared__ __attribute__((aligned(16))) float sx_all[];
-  // n_vals_lds > 0: the leaf values, roots and tree weights are staged next to the forest (rocprofv3: with
-  // them in global memory every tree's walk ended in three dependent global loads, 70 % of wave time waiting)
   int4* snodes = reinterpret_cast<int4*>(sx_all);
-  float* svals = sx_all + (size_t)n_nodes_lds * 4;
-  const int nv_pad = n_vals_lds > 0 ? ((n_vals_lds + 3) & ~3) + ((2 * T + 3) & ~3) : 0;
-  int* sroots = reinterpret_cast<int*>(svals + ((n_vals_lds + 3) & ~3));
-  float* stw = reinterpret_cast<float*>(sroots + T);
-  float* sx = svals + nv_pad;
+  double* svals = reinterpret_cast<double*>(sx_all + (size_t)n_nodes_lds * 4);
+  const int nv_pad = n_vals_lds > 0 ? ((n_vals_lds + 1) & ~1) + ((T + 1) & ~1) : 0;  // doubles
+  double* stw = svals + ((n_vals_lds + 1) & ~1);
+  int* sroots = reinterpret_cast<int*>(svals + nv_pad);
+  float* sx = reinterpret_cast<float*>(sroots) + (n_vals_lds > 0 ? ((T + 3) & ~3) : 0);
   const int dp = d + 1;
-  float* part = sx + 64 * dp;
+  double* part = reinterpret_cast<double*>(sx + 64 * dp);  // 64 * dp * 4 bytes: a multiple of 8
   const int4* nd_src = n_nodes_lds > 0 ? snodes : nodes;
   for (int i = threadIdx.x; i < n_nodes_lds; i += 256) snodes[i] = nodes[i];
   if (n_vals_lds > 0) {
@@ -659,12 +662,12 @@ __global__ __launch_bounds__(256) void predict_kernel(const float* __restrict__ 
         sx[r * dp + f] = X[(r0 + r) * ldx + f];
       }
     }
-    for (int e = threadIdx.x; e < 4 * 64 * K; e += 256) part[e] = 0.f;
+    for (int e = threadIdx.x; e < 4 * 64 * K; e += 256) part[e] = 0.0;
     __syncthreads();
     if (use_pre) fetch(r0 + stride);
     if (row < rows) {
       const float* xr = sx + row * dp;
-      float* pr = part + (tl * 64 + row) * K;
+      double* pr = part + (tl * 64 + row) * K;
       // up to 8 of this lane's trees walk in lockstep: independent node
       // reads per level instead of one dependent chain per tree
       constexpr int W = 8;
@@ -694,47 +697,56 @@ __global__ __launch_bounds__(256) void predict_kernel(const float* __restrict__ 
             any = true;
           }
         }
+        // ascending tree order within the lane (t = tb + 4u grows with u, then with tb)
 #pragma unroll
         for (int u = 0; u < W; ++u) {
           if (!live[u]) continue;
-          const float tw = tree_w[tb + 4 * u];
-          const float* v = values + nv[u].y;
-          for (int k = 0; k < K; ++k) pr[k] += tw * v[k];
+          const double tw = tree_w[tb + 4 * u];
+          const double* v = values + nv[u].y;
+          for (int k = 0; k < K; ++k) {
+            const double prod = tw * v[k];
+            pr[k] = pr[k] + prod;
+          }
         }
       }
     }
     __syncthreads();
     for (int e = threadIdx.x; e < rows * K; e += 256) {
       const int r = e / K, k = e - r * K;
-      float sacc = base ? base[k] : 0.f;
+      double sacc = base ? base[k] : 0.0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sacc += part[(q * 64 + r) * K + k];
+      for (int q = 0; q < 4; ++q) sacc = sacc + part[(q * 64 + r) * K + k];
       out[(r0 + r) * K + k] = sacc;
     }
   }
 }
 
-// K8 on a heap-laid-out forest (single output, every tree depth <= 8): node i
-// of a tree has children 2i+1 / 2i+2, so a node is 8 bytes {feature | -1 leaf
-// | -(f+2) categorical, threshold / leaf value / mask offset} and a walk is
-// exactly `depth` steps with no child loads or termination test (leaves stay
-// put).  The forest is ~2x smaller in LDS than the int4 form (20 trees of
-// depth 5: 10 KB), so 4 blocks fit a CU instead of 3; the walk is
-// branch-uniform.  Same semantics as predict_kernel: left iff x <= thr (NaN
-// goes right), categorical left iff the category's mask bit is set.  (Two register sets refilled two tiles
-// ahead with LDS-only barriers, as in binize5, measured 8.38 vs 7.78 ms at 1e8 x 100: kept one set.)
+// K8 on a heap-laid-out forest (single output, every tree depth <= 12).  Per tree, in int32 words
+// (stride 2^(D+2) - 2): the 2^D - 1 internal slots as int2 {feature | -1 pass-through | -(f+2) categorical,
+// threshold bits / mask offset} with the children of slot i at 2i+1 / 2i+2, then the 2^D leaf values of depth D
+// as doubles.  A leaf shallower than D is stored as pass-through slots (go left) down to its leftmost depth-D
+// descendant, which holds its value, so a walk is exactly D branch-uniform steps with no child loads or
+// termination test, and ends in the leaf table.  LDS per tree equals the previous int2-per-slot form with fp32
+// leaves (20 trees of depth 5: 10 KB), so 4 blocks still fit a CU at d = 100.  Same split semantics as
+// predict_kernel: left iff x <= thr (NaN goes right), categorical left iff the category's mask bit is set.
+// Sums in fp64 in predict_kernel's order (lane q = t % 4 ascending, then base + lanes 0..3, no contraction).
+// (Two register sets refilled two tiles ahead with LDS-only barriers, as in binize5, measured 8.38 vs 7.78 ms at
+// 1e8 x 100: kept one set.)
 __global__ __launch_bounds__(256) void predict_heap_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
-                                                           const int2* __restrict__ heap, int S, int depth,
-                                                           const float* __restrict__ tree_w, int T,
-                                                           const uint32_t* __restrict__ masks, float base,
+                                                           const int* __restrict__ heap, int depth,
+                                                           const double* __restrict__ tree_w, int T,
+                                                           const uint32_t* __restrict__ masks, double base,
                                                            float* __restrict__ out, double* __restrict__ out_d) {
+#pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  int2* sheap = reinterpret_cast<int2*>(sm);
-  float* stw = sm + (size_t)T * S * 2;
-  float* sx = stw + ((T + 3) & ~3);
+  const int NI = (1 << depth) - 1;     // internal slots per tree
+  const int Wt = 4 * NI + 2;           // int32 words per tree: 2 NI (int2 slots) + 2 (NI + 1) (double leaves)
+  int* sheap = reinterpret_cast<int*>(sm);
+  double* stw = reinterpret_cast<double*>(sm + (size_t)T * Wt);  // T * Wt is even: 8-byte aligned
+  float* sx = reinterpret_cast<float*>(stw + ((T + 1) & ~1));
   const int dp = d + 1;
-  float* part = sx + 64 * dp;
-  for (int i = threadIdx.x; i < T * S; i += 256) sheap[i] = heap[i];
+  double* part = reinterpret_cast<double*>(sx + 64 * dp);
+  for (int i = threadIdx.x; i < T * Wt; i += 256) sheap[i] = heap[i];
   for (int i = threadIdx.x; i < T; i += 256) stw[i] = tree_w[i];
   const int tl = threadIdx.x >> 6, row = threadIdx.x & 63;
   const bool vec = ldx == d && (d % 4) == 0;
@@ -779,7 +791,7 @@ __global__ __launch_bounds__(256) void predict_heap_kernel(const float* __restri
     }
     __syncthreads();
     if (use_pre) fetch(r0 + stride);
-    float acc = 0.f;
+    double acc = 0.0;
     if (row < rows) {
       const float* xr = sx + row * dp;
       constexpr int W = 8;
@@ -792,8 +804,8 @@ __global__ __launch_bounds__(256) void predict_heap_kernel(const float* __restri
           for (int u = 0; u < W; ++u) {
             const int t = tb + 4 * u;
             if (t >= T) continue;
-            if (!CDNA_DCHECK(idx[u] < S, 0x7E01u)) idx[u] = 0;  // walk left the heap
-            const int2 nd = sheap[t * S + idx[u]];
+            if (!CDNA_DCHECK(idx[u] < NI, 0x7E01u)) idx[u] = 0;  // walk left the internal slots
+            const int2 nd = *reinterpret_cast<const int2*>(sheap + t * Wt + 2 * idx[u]);
             if (nd.x >= 0 && !CDNA_DCHECK(nd.x < d, 0x7E02u)) continue;  // split feature outside the row
             if (nd.x >= 0) {
               idx[u] = 2 * idx[u] + (xr[nd.x] <= __int_as_float(nd.y) ? 1 : 2);
@@ -801,25 +813,34 @@ __global__ __launch_bounds__(256) void predict_heap_kernel(const float* __restri
               const int c = (int)xr[-nd.x - 2];
               const bool left = (c >= 0 && c < 256) ? ((masks[nd.y * 8 + (c >> 5)] >> (c & 31)) & 1u) : false;
               idx[u] = 2 * idx[u] + (left ? 1 : 2);
+            } else {
+              idx[u] = 2 * idx[u] + 1;  // pass-through slot of a shallower leaf
             }
           }
         }
 #pragma unroll
         for (int u = 0; u < W; ++u) {
           const int t = tb + 4 * u;
-          if (t < T) acc += stw[t] * __int_as_float(sheap[t * S + idx[u]].y);
+          if (t < T) {
+            const int j = idx[u] - NI;
+            if (!CDNA_DCHECK(j >= 0 && j <= NI, 0x7E03u)) continue;
+            const double v = *reinterpret_cast<const double*>(sheap + t * Wt + 2 * NI + 2 * j);
+            const double prod = stw[t] * v;
+            acc = acc + prod;
+          }
         }
       }
     }
     part[tl * 64 + row] = acc;
     __syncthreads();
     if (threadIdx.x < rows) {
-      const float v = base + part[threadIdx.x] + part[64 + threadIdx.x] + part[128 + threadIdx.x] +
-                      part[192 + threadIdx.x];
+      double v = base;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v = v + part[q * 64 + threadIdx.x];
       if (out_d)
-        out_d[r0 + threadIdx.x] = (double)v;  // the DoubleType prediction column directly (no fp32 -> fp64 pass)
+        out_d[r0 + threadIdx.x] = v;  // the DoubleType prediction column directly
       else
-        out[r0 + threadIdx.x] = v;
+        out[r0 + threadIdx.x] = (float)v;
     }
   }
 }
@@ -992,17 +1013,17 @@ CDNA_API int cdna_partition(const uint64_t* bins, int64_t n, int T, int* node, c
 }
 
 CDNA_API int cdna_tree_predict(const float* X, int64_t n, int d, int64_t ldx, const int4* nodes, int64_t n_nodes_total,
-                               const int* roots, const float* tree_w, int T, const float* values,
-                               const uint32_t* masks, int K, const float* base, float* out, int64_t n_values,
+                               const int* roots, const double* tree_w, int T, const double* values,
+                               const uint32_t* masks, int K, const double* base, double* out, int64_t n_values,
                                hipStream_t st) {
   if (n <= 0) return 0;
-  const size_t lds0 = ((size_t)64 * (d + 1) + (size_t)4 * 64 * K) * 4;
+  const size_t lds0 = (size_t)64 * (d + 1) * 4 + (size_t)4 * 64 * K * 8;
   if (lds0 > 160 * 1024) return (int)hipErrorInvalidValue;
   // forest copy in LDS when it fits next to the tile (<= 64 KB per block keeps 2 blocks / CU)
   int n_nodes = 0, n_vals = 0;
   const size_t room = lds0 < 64 * 1024 ? 64 * 1024 - lds0 : 0;
   n_nodes = n_nodes_total <= (int64_t)(room / 16) ? (int)n_nodes_total : 0;
-  const size_t vbytes = (size_t)(((n_values + 3) & ~3) + ((2 * T + 3) & ~3)) * 4;
+  const size_t vbytes = (size_t)(((n_values + 1) & ~1) + ((T + 1) & ~1)) * 8 + (size_t)((T + 3) & ~3) * 4;
   if (n_nodes > 0 && n_values > 0 && (size_t)n_nodes * 16 + vbytes <= room) n_vals = (int)n_values;
   const size_t lds = lds0 + (size_t)n_nodes * 16 + (n_vals > 0 ? vbytes : 0);
   hipLaunchKernelGGL(predict_kernel, dim3(grid_for(n, 64, 8192)), dim3(256), lds, st, X, n, d, ldx, nodes, roots,
@@ -1019,15 +1040,17 @@ CDNA_API int cdna_predict_binned_add(const uint64_t* bins, int64_t n, const int4
   return (int)hipGetLastError();
 }
 
-// heap forest [T][S] int2 (S = 2^(depth+1) - 1), single output; returns hipErrorInvalidValue when it
-// does not fit the LDS budget (the caller then uses cdna_tree_predict).
-CDNA_API int cdna_tree_predict_heap(const float* X, int64_t n, int d, int64_t ldx, const int2* heap, int S, int depth,
-                                    const float* tree_w, int T, const uint32_t* masks, float base, float* out,
+// heap forest [T][2^(depth+2) - 2] int32 words (predict_heap_kernel), single output; returns
+// hipErrorInvalidValue when it does not fit the LDS budget (the caller then uses cdna_tree_predict).
+CDNA_API int cdna_tree_predict_heap(const float* X, int64_t n, int d, int64_t ldx, const int* heap, int depth,
+                                    const double* tree_w, int T, const uint32_t* masks, double base, float* out,
                                     double* out_d, hipStream_t st) {
   if (n <= 0) return 0;
-  const size_t lds = (size_t)T * S * 8 + (size_t)((T + 3) & ~3) * 4 + ((size_t)64 * (d + 1) + 256) * 4;
-  if (lds > 64 * 1024 || depth < 0 || depth > 12) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(predict_heap_kernel, dim3(grid_for(n, 64, 8192)), dim3(256), lds, st, X, n, d, ldx, heap, S,
+  if (depth < 0 || depth > 12) return (int)hipErrorInvalidValue;
+  const size_t wt = ((size_t)4 << depth) - 2;
+  const size_t lds = (size_t)T * wt * 4 + (size_t)((T + 1) & ~1) * 8 + (size_t)64 * (d + 1) * 4 + 256 * 8;
+  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(predict_heap_kernel, dim3(grid_for(n, 64, 8192)), dim3(256), lds, st, X, n, d, ldx, heap,
                      depth, tree_w, T, masks, base, out, out_d);
   return (int)hipGetLastError();
 }

@@ -3,8 +3,11 @@ the GPU (cuda) in one test, with the GPU's native-kernel size thresholds set to 
 FUSE_MIN_ROWS) so the course-sized frames go through the HIP kernels, and the outputs are compared:
 
 * row counts, dedup results, group counts, SQL results, bests maps: exactly;
-* tree models (int64 fixed-point histograms on both devices): forest digests exactly, avgMetrics / RMSE / AUC
-  to 1e-9 relative (only the fp64 evaluation order differs);
+* tree models (int64 fixed-point histograms on both devices): forest digests exactly, predictions bit for bit
+  (fp64 leaves and sums in one tree order), avgMetrics / RMSE / AUC to 1e-12 (only the fp64 metric reductions'
+  order differs);
+* logistic regression (fp64 margins on both devices): the objective to 1e-7, coefficients to 1e-4, the MLE 03
+  regParam x elasticNet CV to the same best map;
 * models fitted through floating-point reductions whose order differs between the devices (the K1 Gram's fp32
   MFMA partial slabs, L-BFGS on fp64 device vectors, K-means sums): to the tolerance stated per flow.
 
@@ -230,16 +233,36 @@ def flow_logistic(spark, ds, work):
                              LogisticRegression(labelCol="priceClass", regParam=0.1)]).fit(train)
     pred = model.transform(test)
     lrm = model.stages[-1]
-    # the fitted objective, not the coefficients: L-BFGS stops at the loss tolerance, and weakly identified
-    # coefficients of this design move by up to 2x within it (fp32 device gradients vs fp64 host ones)
-    return {"loss": float(lrm.summary.objectiveHistory[-1]),
+    # fp64 margins and gradients on both devices (K11): the same L-BFGS path up to summation order
+    return {"loss": float(lrm.summary.objectiveHistory[-1]), "coef": list(lrm.coefficients.toArray()),
+            "intercept": float(lrm.intercept), "iters": int(lrm.summary.totalIterations),
             "acc": MulticlassClassificationEvaluator(labelCol="priceClass", metricName="accuracy").evaluate(pred),
             "auc": BinaryClassificationEvaluator(labelCol="priceClass").evaluate(pred)}
 
 
+def flow_logistic_cv(spark, ds, work):
+    """MLE 03's regParam x elasticNetParam grid in a 3-fold CrossValidator on AUC (S/ML Electives/MLE 03 -
+    Logistic Regression Lab.py:143-158): both devices must pick the same map with the same fold metrics."""
+    from pyspark.sql.functions import col, when
+    from pyspark.ml import Pipeline
+    from pyspark.ml.classification import LogisticRegression
+    from pyspark.ml.feature import RFormula
+    from pyspark.ml.evaluation import BinaryClassificationEvaluator
+    from pyspark.ml.tuning import CrossValidator, ParamGridBuilder
+    data = _airbnb(spark, ds).withColumn("priceClass", when(col("price") >= 150, 1.0).otherwise(0.0))
+    train, _ = data.randomSplit([0.8, 0.2], seed=42)
+    lr = LogisticRegression(labelCol="priceClass")
+    grid = ParamGridBuilder().addGrid(lr.regParam, [0.1, 0.2]).addGrid(lr.elasticNetParam, [0.0, 0.5, 1.0]).build()
+    cv = CrossValidator(estimator=lr, evaluator=BinaryClassificationEvaluator(labelCol="priceClass"),
+                        estimatorParamMaps=grid, numFolds=3, seed=42)
+    model = Pipeline(stages=[RFormula(formula="priceClass ~ . - price", handleInvalid="skip"), cv]).fit(train)
+    cvm = model.stages[-1]
+    return {"avg": list(cvm.avgMetrics), "best": int(np.argmax(cvm.avgMetrics))}
+
+
 FLOWS = {"dedup": flow_dedup, "cleansing": flow_cleansing, "exploration": flow_exploration, "sql": flow_sql,
          "lr": flow_lr, "dt": flow_dt, "rf_cv": flow_rf_cv, "rf_cls": flow_rf_cls, "kmeans": flow_kmeans,
-         "logistic": flow_logistic}
+         "logistic": flow_logistic, "logistic_cv": flow_logistic_cv}
 
 # native kernels each data flow must reach on the GPU (any one of each tuple)
 HASH = ("cdna_hp_part", "cdna_hp_agg", "cdna_hp_hist", "cdna_la_groups", "cdna_hash_insert", "cdna_pack_keys",
@@ -251,7 +274,8 @@ NATIVE = {"dedup": [HASH],
           "lr": [("cdna_reg_metrics",)], "dt": [("cdna_binize",), ("cdna_split_scan", "cdna_split_scan_ex")],
           "rf_cv": [("cdna_binize",), ("cdna_tree_predict_heap", "cdna_tree_predict")],
           "rf_cls": [("cdna_binize",), ("cdna_split_scan_ex",), ("cdna_score_hist", "cdna_tree_predict")],
-          "kmeans": [("cdna_kmeans_step",)], "logistic": [("cdna_logistic_grad",)]}
+          "kmeans": [("cdna_kmeans_step",)], "logistic": [("cdna_logistic_grad",)],
+          "logistic_cv": [("cdna_logistic_grad",)]}
 
 
 def _run_all(device, root, monkeypatch=None):
@@ -324,15 +348,16 @@ def _close(a, b, rel, path=""):
 
 
 EXACT = ("dedup", "sql")
-# int64 histograms on both devices: identical models (digests compared exactly); their metrics come from fp32
-# predictions / probabilities summed over trees in a device-specific order (~1e-8 .. 1e-6 relative)
+# int64 histograms on both devices: identical models (digests compared exactly); their predictions / probabilities
+# are fp64 sums over trees in ONE fixed order on both devices (K.ordered_tree_sum), bit-identical; the metrics
+# over them are fp64 reductions (the device's in another summation order: RMSE to ~1e-16, AUC from exact counts)
 TREES = ("dt", "rf_cv", "rf_cls")
-TREE_METRIC_TOL = 1e-5
+TREE_METRIC_TOL = 1e-12
 # fp64 reductions in a different order: 1e-9 (LR: course-sized normal equations take the fp64 Gram on both
 # devices -- gramPrecision auto; the K1 fp32 MFMA Gram had moved these ill-conditioned OHE coefficients by
 # 2e-3 relative).  Logistic regression: L-BFGS / OWL-QN stops at the same loss tolerance
 # from fp32 device gradients vs fp64 host ones: the fitted objectives and the accuracy / AUC compared
-TOL = {"cleansing": 1e-9, "exploration": 1e-9, "lr": 1e-8, "kmeans": 1e-6, "logistic": 2e-3}
+TOL = {"cleansing": 1e-9, "exploration": 1e-9, "lr": 1e-8, "kmeans": 1e-6, "logistic": 1e-7, "logistic_cv": 1e-7}
 
 
 @pytest.mark.parametrize("flow", list(FLOWS))
@@ -349,6 +374,11 @@ def test_flow_matches_across_devices(results, flow):
         _close({k: a[k] for k in ("coef", "intercept", "n_pred")}, {k: b[k] for k in ("coef", "intercept", "n_pred")},
                TOL["lr"])
         _close(a["rmse"], b["rmse"], 1e-5)
+    elif flow == "logistic":
+        # fp64 margins on both devices (K11): the fitted objective to 1e-7, the coefficients to 1e-4
+        _close(a["loss"], b["loss"], TOL["logistic"])
+        _close({k: a[k] for k in ("coef", "intercept")}, {k: b[k] for k in ("coef", "intercept")}, 1e-4)
+        _close({k: a[k] for k in ("acc", "auc")}, {k: b[k] for k in ("acc", "auc")}, 1e-9)
     else:
         _close(a, b, TOL[flow])
     for group in NATIVE.get(flow, []):

@@ -29,8 +29,8 @@ torch.cuda.synchronize()
 assert torch.isfinite(p).all()
 heap, D, masks = m._forest.heap_arrays(X.device)
 bad = heap.clone()
-bad[0, 0, 0] = 24 + 5                                   # root split on feature 29 of a 24-feature row
-tw = torch.full((heap.shape[0],), 1.0 / heap.shape[0], device="cuda")
+bad[0, 0] = 24 + 5                                      # root split on feature 29 of a 24-feature row
+tw = torch.full((heap.shape[0],), 1.0 / heap.shape[0], device="cuda", dtype=torch.float64)
 try:
     K.tree_predict_heap(X, bad, D, tw, masks, 0.0)
     torch.cuda.synchronize()

@@ -5,6 +5,7 @@ import numpy as np
 import torch
 
 from cdnaml.models.tree.engine import Forest
+from cdnaml.ops import kernels as K
 
 
 def test_trainer_heap_equals_forest_walk():
@@ -20,9 +21,11 @@ def test_trainer_heap_equals_forest_walk():
         assert f._heap_np is not None
         pre = f._heap_np
         f._heap_np = None
-        ref = f.heap_arrays(torch.device("cpu"))
-        assert ref[1] == pre[1]
-        np.testing.assert_array_equal(ref[0].numpy(), pre[0])
+        st, vals, D, _ = f.heap_struct()
+        assert D == pre[2]
+        np.testing.assert_array_equal(st, pre[0])
+        # the trainer's per-slot values hold every node's value (splits too); the packed table reads leaves only
+        np.testing.assert_array_equal(K.pack_heap(st, vals, D), K.pack_heap(pre[0], pre[1], pre[2]))
 
 
 def test_set_splits_vectorised():

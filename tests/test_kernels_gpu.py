@@ -294,7 +294,7 @@ def _random_forest_arrays(T, depth, d, K_, seed):
             nodes.append([-1, len(values), 0, 0])
             values.extend(torch.randn(K_, generator=g).tolist())
     return (torch.tensor(nodes, dtype=torch.int32), torch.tensor(roots, dtype=torch.int32),
-            torch.tensor(values, dtype=torch.float32), masks)
+            torch.tensor(values, dtype=torch.float64), masks)
 
 
 @pytest.mark.parametrize("K_", [1, 3])
@@ -307,12 +307,13 @@ def test_tree_predict(dev, K_):
     # categorical nodes use feature 3 only
     cat = nodes[:, 0] < -1
     nodes[cat, 0] = -(3 + 2)
-    tw = torch.rand(T, generator=g)
-    base = torch.randn(K_, generator=g)
+    tw = torch.rand(T, generator=g, dtype=torch.float64)
+    base = torch.randn(K_, generator=g, dtype=torch.float64)
     ref = K.tree_predict(X, nodes, roots, tw, values, masks, K_, base)
     out = K.tree_predict(X.to(dev), nodes.to(dev), roots.to(dev), tw.to(dev), values.to(dev), masks.to(dev), K_,
                          base.to(dev)).cpu()
-    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-5)
+    # fp64 leaves / weights / sums in one fixed tree order on both devices: bit-identical
+    assert out.dtype == torch.float64 and torch.equal(out, ref)
 
 
 def test_reg_metrics(dev):
@@ -1223,7 +1224,9 @@ def test_float_with_absmax(dev):
 
 
 def test_heap_predict_double_store(dev):
-    """predict_heap_kernel's fp64 store == .double() of its fp32 output (the DoubleType prediction column)."""
+    """predict_heap_kernel sums in fp64 (its fp32 store is the rounded fp64 result) and equals the int4-node
+    kernel and the cpu reference bit for bit (the same fixed tree order), including a forest with shallow leaves
+    (pass-through slots) and categorical splits."""
     import cdnaml
     from cdnaml.models.regression import RandomForestRegressor
     spark = cdnaml.SparkSession.builder.getOrCreate()
@@ -1233,10 +1236,59 @@ def test_heap_predict_double_store(dev):
     m = RandomForestRegressor(numTrees=6, maxDepth=4, seed=1).fit(
         spark.createDataFrameFromLocalTensors({"features": X, "label": y}))
     ha = m._forest.heap_arrays(X.device, "value")
-    tw = torch.tensor(m._tree_w, dtype=torch.float32, device=dev)
-    a = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], 0.0)
-    b = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], 0.0, dtype=torch.float64)
-    assert b.dtype == torch.float64 and torch.equal(b, a.double())
+    tw = torch.tensor(m._tree_w, dtype=torch.float64, device=dev)
+    a = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], 0.25, dtype=torch.float32)
+    b = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], 0.25, dtype=torch.float64)
+    assert b.dtype == torch.float64 and torch.equal(b.float(), a)
+    nodes, roots, vals, masks = m._forest.device_arrays(X.device, "value")
+    base = torch.tensor([0.25], dtype=torch.float64, device=dev)
+    c = K.tree_predict(X, nodes, roots, tw, vals, masks, 1, base)
+    assert torch.equal(b, c)
+    ref = K.tree_predict(X.cpu(), nodes.cpu(), roots.cpu(), tw.cpu(), vals.cpu(), masks.cpu(), 1, base.cpu())
+    assert torch.equal(b.cpu(), ref)
+    # categorical splits and leaves at several depths
+    nodes2, roots2, vals2, masks2 = _random_forest_arrays(9, 5, 12, 1, 3)
+    cat = nodes2[:, 0] < -1
+    nodes2[cat, 0] = -(3 + 2)
+    Xc = X.clone()
+    Xc[:, 3] = torch.randint(0, 40, (X.shape[0],), generator=g, device=dev).float()
+    f = _forest_from_arrays(nodes2, roots2, vals2, masks2)
+    hs = f.heap_struct()
+    assert hs is not None and hs[2] == 5
+    heap = torch.from_numpy(K.pack_heap(hs[0], hs[1], hs[2])).to(dev)
+    tw2 = torch.rand(9, dtype=torch.float64, generator=torch.Generator().manual_seed(4)).to(dev)
+    got = K.tree_predict_heap(Xc, heap, hs[2], tw2, torch.from_numpy(hs[3]).to(dev), 0.0)
+    n3, r3, v3, m3 = f.device_arrays(torch.device("cpu"))
+    want = K.tree_predict(Xc.cpu(), n3, r3, tw2.cpu(), v3, m3, 1, None)
+    assert torch.equal(got.cpu(), want)
+    assert torch.equal(K.tree_predict(Xc, n3.to(dev), r3.to(dev), tw2, v3.to(dev), m3.to(dev), 1, None).cpu(), want)
+
+
+def _forest_from_arrays(nodes, roots, vals, masks):
+    """A host Forest from _random_forest_arrays' int4 node table (K = 1), with some leaves cut shallow."""
+    from cdnaml.models.tree.engine import Forest
+    nd = nodes.numpy()
+    f = Forest(1)
+    L = f.lists()
+    mk = masks.numpy().view(np.uint32).reshape(-1, 8) if masks.numel() else np.zeros((0, 8), np.uint32)
+    v = vals.numpy()
+    for i, (a, b, l, r) in enumerate(nd.tolist()):
+        shallow = a != -1 and i % 7 == 3  # turn some internal nodes into leaves (unreachable subtrees)
+        leaf = a == -1 or shallow
+        L["feat"].append(-1 if leaf else (a if a >= 0 else -a - 2))
+        L["thr"].append(0.0 if leaf or a < 0 else float(np.array([b], np.int32).view(np.float32)[0]))
+        L["bin"].append(0)
+        L["left"].append(-1 if leaf else l)
+        L["right"].append(-1 if leaf else r)
+        L["catmask"].append(mk[b] if (not leaf and a < -1) else np.zeros(8, np.uint32))
+        L["is_cat"].append(bool(not leaf and a < -1))
+        L["value"].append(np.array([v[b] if a == -1 else 0.5 * i], np.float64))
+        L["weight"].append(1.0)
+        L["gain"].append(0.0)
+        L["impurity"].append(0.0)
+        L["depth"].append(0)
+    f.roots.extend(roots.tolist())
+    return f
 
 
 
