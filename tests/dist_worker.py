@@ -194,6 +194,41 @@ def scenario_trees_rs_overlap(spark):
     return out
 
 
+def scenario_trees_rs_nccl(spark):
+    """the RCCL branches of Comm (reduce_scatter_tensor, all_gather_into_tensor, device
+    barriers) driven through tests/fake_nccl.py's recording nccl-over-gloo proxy (installed before the session's
+    Comm is built, see run()): direct collective checks, then the trees_rs forests (every level histogram
+    reduce-scattered by feature, winners all-gathered) -- which must equal the 1-rank fits bit for bit."""
+    import torch
+    import fake_nccl
+    comm = spark.comm
+    W, r = comm.world_size, comm.rank
+    out = {"backend": comm.backend}
+    # reduce-scatter: [W, 3, 5] int64 -> this rank's [3, 5] slice of the sum, on the caller's device
+    t = (torch.arange(W * 15, dtype=torch.int64).reshape(W, 3, 5) + 100 * r)
+    got = comm.reduce_scatter(t)
+    want = (torch.arange(W * 15, dtype=torch.int64).reshape(W, 3, 5) * W + 100 * sum(range(W)))[r]
+    out["rs_ok"] = bool(got.shape == (3, 5) and got.device == t.device and torch.equal(got, want))
+    # non-contiguous input is made contiguous before RCCL sees it
+    tt = torch.arange(W * 10, dtype=torch.float64).reshape(10, W).T
+    out["rs_noncontig_ok"] = bool(torch.equal(comm.reduce_scatter(tt), tt[r] * W))
+    g = comm.all_gather_tensor(torch.full((2, 3), float(r)))
+    out["ag_ok"] = bool(g.shape == (W, 2, 3) and all(bool((g[k] == k).all()) for k in range(W)))
+    a = torch.ones(7, dtype=torch.float64) * (r + 1)
+    out["ar_async_ok"] = bool(torch.equal(comm.all_reduce_async(a).wait(), torch.full((7,), W * (W + 1) / 2.0,
+                                                                                   dtype=torch.float64)))
+    chunks = [torch.full((j + 1, 2), float(r * 10 + j)) for j in range(W)]
+    recv = comm.all_to_all_v(chunks)
+    out["a2a_ok"] = bool(all(x.shape == (r + 1, 2) and bool((x == k * 10 + r).all()) for k, x in enumerate(recv)))
+    comm.barrier()
+    res = scenario_trees_rs(spark)
+    out.update(res)
+    rec = comm.all_gather_object(dict(fake_nccl.RECORD))
+    out["record_min"] = {k: min(x.get(k, 0) for x in rec) for k in rec[0]}
+    out["violations"] = sorted(set(sum(comm.all_gather_object(list(fake_nccl.VIOLATIONS)), [])))
+    return out
+
+
 def scenario_trees_deep(spark):
     """Forests deeper than 8 levels (binary classification and regression forests switch from the u16 row codes
     to node ids at level 8, then build node-id record histograms): bit-identical at any world size, also with
@@ -362,10 +397,20 @@ SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault
              "trees_rs_overlap": scenario_trees_rs_overlap, "trees_deep": scenario_trees_deep, "cv": scenario_cv, "als": scenario_als,
              "hyperopt": scenario_hyperopt,
              "ooc_uneven": scenario_ooc_uneven,
+             "trees_rs_nccl": scenario_trees_rs_nccl,
              "hyperopt_captured": scenario_hyperopt_captured}
 
 
 def run(name):
+    if name.endswith("_nccl") and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # the recording nccl-over-gloo proxy must be in place before the session builds its Comm
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import torch.distributed as dist
+        import fake_nccl
+        from cdnaml.parallel import comm as comm_mod
+        comm_mod.init_from_env()
+        assert dist.get_backend() == "gloo"
+        fake_nccl.install(comm_mod)
     spark = _session()
     return SCENARIOS[name](spark)
 

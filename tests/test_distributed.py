@@ -183,3 +183,23 @@ def test_ooc_fit_with_an_empty_shard(tmp_path):
     for w in (2, 3):
         got = _run("ooc_uneven", tmp_path, w)
         assert got == one, (w, got, one)
+
+
+def test_rccl_branches_through_recording_fake(tmp_path):
+    """the RCCL branches of Comm (never run by gloo CI) through tests/fake_nccl.py -- a
+    recording nccl-over-gloo torch.distributed proxy that checks contiguity, dtypes, in/out sizes and split
+    sums of every call.  Direct collective checks, then the reduce-scatter-by-feature forests at W = 2 and 4,
+    which must equal the 1-rank (gloo) fits bit for bit."""
+    one = _run("trees_rs", tmp_path, 1)
+    assert one.pop("rs_levels") == 0
+    for w in (2, 4):
+        got = _run("trees_rs_nccl", tmp_path, w)
+        assert got.pop("backend") == "nccl"
+        assert got.pop("violations") == [], w
+        for k in ("rs_ok", "rs_noncontig_ok", "ag_ok", "ar_async_ok", "a2a_ok"):
+            assert got.pop(k) is True, (w, k)
+        rec = got.pop("record_min")
+        assert rec.get("reduce_scatter_tensor", 0) > 0 and rec.get("all_gather_into_tensor", 0) > 0, (w, rec)
+        assert rec.get("barrier", 0) > 0, (w, rec)
+        assert got.pop("rs_levels") > 0, w
+        assert got == one, w
