@@ -207,7 +207,20 @@ def bench_infer(spark, args):
             # staging buffer on the compute stream), so the 1e9 rows are distinct and their generation is timed
             K.normal32_(bufs["features"][:n], 7, (row_base + r0) * 100, 0x10)
         df = device_chunks(spark, n_chunks * chunk, chunk, make, {"features": ((100,), torch.float32)})
-    pred = model.transform(df)
+    udf = None
+    if args.api == "spark_udf":
+        # the reference's route (ML 09 - AutoML.py:78-82, Labs/ML 12L:78-96): log the model with the tracking
+        # flavour, load it as a Spark UDF from "runs:/<id>/model" and apply it column-wise to the streamed frame
+        import tempfile
+        from cdnaml import tracking as mlflow
+        from cdnaml.models.pipeline import PipelineModel
+        mlflow.set_tracking_uri(os.path.join(tempfile.mkdtemp(prefix="cfg_infer_"), "mlruns"))
+        with mlflow.start_run() as run:
+            mlflow.spark.log_model(PipelineModel([model]), "model")
+        udf = mlflow.pyfunc.spark_udf(spark, f"runs:/{run.info.run_id}/model")
+        pred = df.withColumn("prediction", udf("features"))
+    else:
+        pred = model.transform(df)
     acc = torch.zeros((), dtype=torch.float64, device=dev)
 
     def consume(b):
@@ -224,15 +237,17 @@ def bench_infer(spark, args):
         del scratch
         _log(f"generation alone: {gen_ms:.1f} ms ({n_chunks * chunk * 400 / gen_ms / 1e9:.2f} TB/s written)")
     from cdnaml.models.inference import predictor_for
-    pr = predictor_for(model, "value", [0.0])
-    _log(f"inference {rows:.3e} rows in {ms:.1f} ms (mode={args.mode}); graph captures={pr.captures} "
-         f"replays={pr.replays}; mean prediction {float(tot) / (n_chunks * chunk):.4f}")
+    pr = predictor_for(udf.pm.stages[-1] if udf is not None else model, "value", [0.0])
+    _log(f"inference {rows:.3e} rows in {ms:.1f} ms (mode={args.mode}, api={args.api}); graph captures="
+         f"{pr.captures} replays={pr.replays}; mean prediction {float(tot) / (n_chunks * chunk):.6f}"
+         + (f"; udf batches={udf.batches} plans built={udf.plans_built}" if udf is not None else ""))
     src = "pinned host chunks, H2D in the timed region" if args.mode == "host" else \
         "distinct rows generated on device per chunk, generation in the timed region"
-    _emit(spark, f"rows/sec batch inference via DataFrame transform, RandomForest (20 trees, depth 5), 1e9 rows "
+    via = "mlflow.pyfunc.spark_udf (runs:/ URI) in withColumn" if args.api == "spark_udf" else "DataFrame transform"
+    _emit(spark, f"rows/sec batch inference via {via}, RandomForest (20 trees, depth 5), 1e9 rows "
                  f"({src})", rows / (ms / 1e3), "rows/s", args.steps, args.warmup, ms, True,
           "weak" if comm.world_size > 1 else "strong", "fp32",
-          "RandomForestRegressionModel(numTrees=20,maxDepth=5).transform, streamed, hipGraph-replayed predict",
+          f"RandomForestRegressionModel(numTrees=20,maxDepth=5) via {via}, streamed, hipGraph-replayed predict",
           rows, f"dp{comm.world_size}")
 
 
@@ -351,8 +366,25 @@ def bench_ooc(spark, args):
         K.normal32_(X, 11, (row_base + r0) * 100, 0x10)
         torch.matmul(X, wv, out=bufs["label"][:n])
         bufs["label"][:n].add_(torch.sin(2.0 * X[:, 0]))
-    df = device_chunks(spark, n_chunks * chunk, chunk, make,
-                       {"features": ((100,), torch.float32), "label": ((), torch.float32)})
+    if args.source == "host" and dev.type == "cuda":
+        # pinned host chunks through createDataFrameFromChunks (pinned staging, H2D on the copy stream overlapping
+        # the compute): every pass over the frame moves all rows over PCIe inside the timed region.  The host pool
+        # holds --pool distinct chunks, cycled (host RAM cannot hold 320 GB of rows either).
+        pool = []
+        scratch = {"features": torch.empty((chunk, 100), dtype=torch.float32, device=dev),
+                   "label": torch.empty((chunk,), dtype=torch.float32, device=dev)}
+        for i in range(int(args.pool)):
+            make(i * chunk, chunk, scratch)
+            pool.append({k: v.cpu().pin_memory() for k, v in scratch.items()})
+        del scratch
+
+        def host_chunks():
+            for i in range(n_chunks):
+                yield pool[i % len(pool)]
+        df = spark.createDataFrameFromChunks(host_chunks, chunk)
+    else:
+        df = device_chunks(spark, n_chunks * chunk, chunk, make,
+                           {"features": ((100,), torch.float32), "label": ((), torch.float32)})
     if args.model == "rf":
         T = int(args.trees or 4)
         est = RandomForestRegressor(numTrees=T, maxDepth=5, maxBins=40, seed=42)
@@ -364,8 +396,10 @@ def bench_ooc(spark, args):
     peak = torch.cuda.max_memory_allocated(dev) / 2 ** 30 if dev.type == "cuda" else 0.0
     _log(f"ooc {args.model}: {ms:.1f} ms per fit, {rows / ms * 1e3:.3e} rows/s, peak allocated {peak:.1f} GiB "
          f"(fp32 X would be {rows * 400 / 2 ** 30:.0f} GiB)")
-    _emit(spark, f"rows/sec out-of-core fit ({name})", rows / ms * 1e3, "rows/s", args.steps, args.warmup, ms, True,
-          "strong", "fp32", name, rows, f"dp{comm.world_size}")
+    src = "pinned host chunks (cycled pool), H2D in the timed region" if args.source == "host" else \
+        "chunks generated on device, generation in the timed region"
+    _emit(spark, f"rows/sec out-of-core fit ({name}; {src})", rows / ms * 1e3, "rows/s", args.steps, args.warmup,
+          ms, True, "strong", "fp32", name, rows, f"dp{comm.world_size}")
 
 
 def main():
@@ -379,7 +413,10 @@ def main():
     ap.add_argument("--trees", type=int, default=None)
     ap.add_argument("--chunk", type=float, default=1e7)
     ap.add_argument("--mode", choices=["host", "device"], default="host")
-    ap.add_argument("--pool", type=int, default=6, help="distinct pinned host chunks (--mode host)")
+    ap.add_argument("--api", choices=["transform", "spark_udf"], default="transform",
+                    help="infer: model.transform, or the tracking flavour loaded with pyfunc.spark_udf")
+    ap.add_argument("--pool", type=int, default=6, help="distinct pinned host chunks (--mode host / --source host)")
+    ap.add_argument("--source", choices=["host", "device"], default="device", help="ooc: where the chunks come from")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--trace", default="", help="run one traced (untimed) step first; Chrome trace path")
     args = ap.parse_args()

@@ -17,11 +17,9 @@ needed.  Bins come from a global quantile sample (all-gathered), so they do
 not depend on the GPU count.  Bootstrap weights are Philox-Poisson keyed by
 the GLOBAL row id: a forest trained on 1 or 8 GPUs is the same forest.
 
-Two histogram strategies:
-  * masked  — per-node feature subsets (RF): only the node's sampled
-              features are accumulated, no sibling subtraction;
-  * subtract — all features (DT/GBDT): only the smaller child of each
-              split is built, its sibling is parent − child.
+Histograms accumulate every feature of the smaller child of each split; its
+sibling is parent − child (per-node feature subsets of random forests are
+applied at split time).
 """
 from __future__ import annotations
 
@@ -37,7 +35,6 @@ from ...ops import kernels as K
 from ...utils import tracing as _tr
 from ..util import IllegalArgumentException
 
-HIST_MODE = __import__("os").environ.get("CDNAML_RF_HIST", "full")
 # compact uint16 row records (hist5.hip) instead of int32 node ids + uint8 weights
 USE_CODES = __import__("os").environ.get("CDNAML_TREE_CODES", "1") != "0"
 # single-tree regression fits (boosting rounds, DecisionTree): rows kept grouped by node (seg.hip)
@@ -75,10 +72,6 @@ MASKS_DEV = __import__("os").environ.get("CDNAML_MASKS_DEV", "1") != "0"
 CUT_ARRAYS = __import__("os").environ.get("CDNAML_CUT_ARRAYS", "1") != "0"
 # boosting margins updated by the level partitions (ForestTrainer.train(margin=...)) instead of a tree walk
 GBDT_MARGIN = __import__("os").environ.get("CDNAML_GBDT_MARGIN", "1") != "0"
-# feature-subset forests: accumulate only each node's sampled features in segment mode.  Opt-in: measured
-# 5-8x slower (profiles/pmc_seg_hist_subset.txt): both children must be built, and every row gather of the
-# row-major bins (one or two 64 B lines) then feeds 34 atomics instead of 104
-MSEG_SUBSET = __import__("os").environ.get("CDNAML_MSEG_SUBSET", "0") != "0"
 # multi-rank record histograms: slot chunks whose all-reduces overlap the next chunk's histogram kernel
 HIST_OVERLAP = int(__import__("os").environ.get("CDNAML_HIST_OVERLAP", "2"))
 # ... only for level histograms of at least this many bytes: at the 8-GPU point's per-rank shape (1.25e7 rows)
@@ -88,13 +81,6 @@ HIST_OVERLAP_MIN_BYTES = int(__import__("os").environ.get("CDNAML_HIST_OVERLAP_M
 # take the slot-chunked (overlapped all-reduce) histogram path on one rank too: measures its launch cost at a
 # per-rank shape on a 1-GPU box
 HIST_OVERLAP_FORCE = __import__("os").environ.get("CDNAML_HIST_OVERLAP_FORCE", "0") != "0"
-# feature-subset regression forests (RandomForestRegressor, featureSubsetStrategy auto / onethird / sqrt ...):
-# every node of a level built over its m sampled features only, items generated from the row codes on the fly
-# (subhist.hip) -- no record compaction, no sibling subtraction, 34 instead of 100 lane-ops per item.  Exact
-# (same forest), but opt-in: at the headline it measured 227 ms (v1) / 375 ms (v2) of histograms per step
-# against 87 + 19 ms for records + subtraction, because building BOTH children doubles the gathered row lines
-# at every level below the root (profiles/r3/subhist_ab.md)
-SUB_HIST = __import__("os").environ.get("CDNAML_SUB_HIST", "0") != "0"
 # Level histograms of at least this many bytes (int64, distributed, regression / XGBoost statistics, no
 # categorical features) are reduce-scattered by feature instead of all-reduced: every rank receives the sums of
 # d / W features (1/W of an all-reduce's bytes per GPU), runs K6 on its slice, and the per-node winners are
@@ -900,16 +886,6 @@ def _splitmix64(x: np.ndarray) -> np.ndarray:
         return z ^ (z >> np.uint64(31))
 
 
-def _mask_feature_lists(words: np.ndarray, d: int) -> Optional[np.ndarray]:
-    """Feature-subset bit words [S, ceil(d/32)] -> feature ids [S, m] (None if m differs between nodes)."""
-    f = np.arange(d)
-    bits = ((words[:, f >> 5] >> (f & 31).astype(np.uint32)) & 1).astype(bool)
-    cnt = bits.sum(1)
-    if len(cnt) == 0 or cnt.min() != cnt.max() or cnt[0] == 0:
-        return None
-    return np.nonzero(bits)[1].reshape(len(cnt), int(cnt[0])).astype(np.int32)
-
-
 def _built_nodes(w: np.ndarray, a_sib: np.ndarray, a_parent: np.ndarray) -> np.ndarray:
     """Subtraction levels: the active nodes whose histogram is built -- the smaller of two active siblings (ties:
     the first one), the other derived as parent - sibling; a node without an active sibling is built.  The
@@ -1295,8 +1271,8 @@ class ForestTrainer:
         return K.RecordEmit(dev, n, A, rec, v1, qs1, ch, waves)
 
     # ------------------------------------------------------------ reduce-scatter by feature
-    def _rs_want(self, Hb: torch.Tensor, rs_on: bool, sub_feats) -> bool:
-        if Hb.dtype != torch.int64 or sub_feats is not None:
+    def _rs_want(self, Hb: torch.Tensor, rs_on: bool) -> bool:
+        if Hb.dtype != torch.int64:
             return False
         return self._rs_level(Hb.numel() * 8, rs_on)
 
@@ -1362,46 +1338,6 @@ class ForestTrainer:
         return sel[:, :8].contiguous(), sel[:, 9:11].contiguous()
 
     # ------------------------------------------------------------ training
-    def _sub_hist_ok(self, mseg_ok: bool, need_masks: bool, stats_rows) -> bool:
-        """Subset histograms (subhist.hip) for this fit: packed regression statistics, a per-node feature subset
-        of at most half the features, <= 256 bins, and on the GPU a 128-byte row-major bins copy."""
-        p, data = self.p, self.data
-        if not (SUB_HIST and mseg_ok and need_masks and stats_rows.get("v0") is None and not self.classification):
-            return False
-        m = p.feature_subset
-        if m is None or m > K.SUB_HIST_MAX_M or 2 * m > data.d or data.B > 256 or data.categorical:
-            return False
-        if self.device.type == "cuda":
-            rm = data.row_major_bins()
-            if rm is None or rm.shape[1] * rm.shape[2] != 128 or K.sub_hist_ns_max(data.B, m) < 1:
-                return False
-        return True
-
-    def _sub_hist(self, data, codes, v1, qs1, tfirst_h, slot_tree, feats, B, wmax, dev):
-        """A level's subset histograms; on several ranks in HIST_OVERLAP slot chunks, each chunk's int64 sums
-        all-reduced on the collective stream while the next chunk is built (exact: the same sums as one
-        all-reduce)."""
-        S, m = feats.shape
-        rm = data.row_major_bins() if dev.type == "cuda" else None
-        Hc = torch.zeros((S, m, B, 2), dtype=torch.int64, device=dev)
-        k = min(HIST_OVERLAP, S) if self.comm.distributed else 1
-        bounds = np.linspace(0, S, max(k, 1) + 1).round().astype(np.int64)
-        pend = []
-        for c in range(max(k, 1)):
-            s0, s1 = int(bounds[c]), int(bounds[c + 1])
-            if s1 <= s0:
-                continue
-            with _tr.span("tree.sub_hist", slots=s1 - s0):
-                K.sub_hist(codes, v1, qs1, data.bins, rm, tfirst_h, slot_tree, feats, B, wmax, s0, s1, out=Hc[s0:s1])
-            if self.comm.distributed:
-                with _tr.span("tree.allreduce_async", cat="comm", bytes=(s1 - s0) * m * B * 16):
-                    pend.append(self.comm.all_reduce_async(Hc[s0:s1]))
-        if pend:
-            with _tr.span("tree.allreduce_wait", cat="comm"):
-                for h in pend:
-                    h.wait()
-        return Hc
-
     def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev, seg_end=None):
         """Record histograms of a level's S slots in HIST_OVERLAP slot chunks; chunk c's all-reduce runs on the
         collective stream while chunk c + 1 is built (one per-level RCCL all-reduce of 1-50 MB otherwise
@@ -1459,8 +1395,6 @@ class ForestTrainer:
             heap_v = np.zeros((T, 2 ** (p.max_depth + 1) - 1), dtype=np.float64)  # leaf values per slot (fp64)
         heap_depth = 0
         need_masks = p.feature_subset is not None and p.feature_subset < d
-        # "masked": accumulate only each node's sampled features (fewer atomics, no subtraction);
-        # "full": accumulate all features, derive larger siblings by subtraction, mask at split time.
         # several regression trees: row records for every level (one dense pass partitions all trees); before
         # each level's histogram the rows of the nodes it builds are gathered into slot segments, so the
         # histogram touches only those rows
@@ -1475,16 +1409,12 @@ class ForestTrainer:
         mseg_ok = (USE_MSEG and USE_CODES and (T > 1 or (MSEG_T1 and stats_rows.get("v0") is None)) and
                    (not self.classification or cls2) and (p.max_depth <= 8 or deep_switch) and
                    T * self.n_max < 2 ** 31 and data.n_global > 0)
-        # ... and with per-node feature subsets (RandomForest) only each node's sampled features are
-        # accumulated (packed statistics only: no v0)
-        # (regression only: its float histograms skip the binary classification (W, W1) -> class counts step)
-        subset_seg = mseg_ok and need_masks and MSEG_SUBSET and stats_rows.get("v0") is None and not cls2
-        use_sub = self._sub_hist_ok(mseg_ok, need_masks, stats_rows) and not subset_seg
-        masked = need_masks and (HIST_MODE == "masked" or subset_seg or use_sub)
-        subtract = not masked
+        # every level builds all features of the smaller child of each split; its sibling is parent - child
+        # (feature subsets are applied at split time: the measured alternatives that accumulate only each node's
+        # sampled features lost 2-8x, profiles/r3/subhist_ab.md, profiles/pmc_seg_hist_subset.txt)
+        use_mseg = mseg_ok
         # one regression tree: rows grouped by node in a permutation (segment mode)
-        use_mseg = mseg_ok and (not masked or subset_seg)
-        use_seg = USE_SEG and T == 1 and not self.classification and not masked and not use_mseg
+        use_seg = USE_SEG and T == 1 and not self.classification and not use_mseg
         # row records (uint16 weight<<8 | local node) when every level fits 255 nodes per tree
         use_codes = USE_CODES and (p.max_depth <= 8 or (deep_switch and use_mseg)) and not use_seg
         if codes_pre is not None and not use_codes:
@@ -1493,7 +1423,7 @@ class ForestTrainer:
         # the tree (no zero weights) and leaf values the device can form (no categorical / classification)
         margin_ok = (margin is not None and GBDT_MARGIN and use_codes and not deep_switch and T == 1 and
                      weights is None and codes_pre is None and dev.type == "cuda" and p.impurity == "xgb" and
-                     self._device_decode_ok(dev, True, False) and self._native_split(dev) and not use_sub and
+                     self._device_decode_ok(dev, True, False) and self._native_split(dev) and
                      not data.categorical and p.max_depth <= 8)
         self.margin_applied = margin_ok
         if use_seg:
@@ -1517,7 +1447,7 @@ class ForestTrainer:
             else:
                 codes, wmax = K.codes_init_max(weights, T, n, dev)
             node = None
-            if use_mseg or use_sub:
+            if use_mseg:
                 # one quantisation scale for every rank: the int64 level histograms then all-reduce to
                 # the same sums on 1 or N GPUs (the forest does not depend on the GPU count)
                 v0s = stats_rows.get("v0")
@@ -1559,7 +1489,7 @@ class ForestTrainer:
                 break
             # ---- decide which active nodes get a histogram built
             build = np.ones(A, dtype=bool)
-            if subtract and depth > 0:
+            if depth > 0:
                 build = _built_nodes(self._weights_v(a_stats), a_sib, a_parent)
             build_ids = np.nonzero(build)[0]
             slot_of = np.full(A, -1, dtype=np.int32)
@@ -1570,7 +1500,7 @@ class ForestTrainer:
             mask_base = None
             if need_masks:
                 tid = a_tree if p.tree_ids is None else np.asarray(p.tree_ids, dtype=np.int64)[a_tree]
-                if MASKS_DEV and dev.type == "cuda" and not (masked or use_sub or subset_seg) and \
+                if MASKS_DEV and dev.type == "cuda" and \
                         d <= K.FEATURE_MASKS_MAX_D and p.feature_subset is not None and 0 < p.feature_subset < d:
                     mask_base = self._mask_base(tid.astype(np.uint64), a_key)
                 else:
@@ -1586,13 +1516,9 @@ class ForestTrainer:
                                *([mask_base.view(np.int64)] if mask_base is not None else []))
                 if mask_base is not None:
                     masks_dev = K.feature_masks(mask_base, d, p.feature_subset, dev, base_dev=lvl[3])
-            fm_build = None
-            if masked:
-                fm_build, = K.upload(dev, np.ascontiguousarray(masks_np[build_ids]).view(np.int32))
             hist_raw_scale = None
             reduced = False
-            sub_feats = None
-            rec_ok = (MSEG_REC and stats_rows.get("v0") is None and not subset_seg and 8 * B * 8 <= 128 * 1024)
+            rec_ok = (MSEG_REC and stats_rows.get("v0") is None and 8 * B * 8 <= 128 * 1024)
             # levels with <= 1 built node per tree (0: the roots, 1: the smaller children) on seg10 rows: the
             # records are compacted inside the histogram kernel (no codes_compact pass)
             root_rows = None  # seg10 rows (B <= 40) or standard row-major rows (boosting, 80 < B <= 256)
@@ -1601,17 +1527,10 @@ class ForestTrainer:
                     root_rows = data.bins_s10
                 elif 80 < B <= 256 and data.bins_rm is not None:
                     root_rows = data.bins_rm
-            root_ok = (root_rows is not None and use_mseg and not use_sub and (depth >= 1 or MSEG_L0) and rec_ok and
+            root_ok = (root_rows is not None and use_mseg and (depth >= 1 or MSEG_L0) and rec_ok and
                        emitted is None and len(build_ids) > 0 and np.bincount(slot_tree, minlength=T).max() <= 1)
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
-                if use_sub:
-                    # every active node over its sampled features; exact int64 (count, sum w q) [A, m, B, 2]
-                    sub_feats = _mask_feature_lists(masks_np, d)
-                    Hb = self._sub_hist(data, codes, stats_rows["v1"], mseg_scales[1], tfirst.numpy(), a_tree,
-                                        sub_feats, B, wmax, dev)
-                    hist_raw_scale = mseg_raw
-                    reduced = True
-                elif root_ok:
+                if root_ok:
                     S_b = len(build_ids)
                     sl_node = build_ids - tfirst.numpy()[slot_tree]  # the slot's local node in its tree's codes
                     # one launch for every slot, then the level's one all-reduce: these levels hold one node per
@@ -1643,13 +1562,7 @@ class ForestTrainer:
                                                                  rec_scale=mseg_scales[1] if rec_ok else None)
                     is_rec = rec_ok and v1p is None
                     sb = np.concatenate([sg, np.arange(len(build_ids), dtype=np.int64)[:, None]], 1)
-                    if subset_seg:
-                        feats = _mask_feature_lists(masks_np[build_ids], d)
-                    if subset_seg and feats is not None:
-                        Hb = K.seg_hist_subset(data.bins, d, B, perm, v1p, wp, sb, len(build_ids), wmax, feats,
-                                               mseg_scales, bins_rm=data.row_major_bins() if dev.type == "cuda"
-                                               else None, interleave=True)
-                    elif is_rec and (self.comm.distributed or HIST_OVERLAP_FORCE) and HIST_OVERLAP > 1 and \
+                    if is_rec and (self.comm.distributed or HIST_OVERLAP_FORCE) and HIST_OVERLAP > 1 and \
                             len(build_ids) >= 2 and \
                             len(build_ids) * d * B * 16 >= HIST_OVERLAP_MIN_BYTES and \
                             not self._rs_level(len(build_ids) * d * B * 16, rs_on):
@@ -1695,18 +1608,18 @@ class ForestTrainer:
                 elif use_codes:
                     Hb = K.hist_codes(1 if self.classification else 0, data.bins, d, codes, tfirst,
                                       stats_rows.get("v0"), stats_rows.get("v1"), stats_rows.get("label"), self.C,
-                                      K.upload(dev, slot_of)[0], slot_tree, id_tree, fm_build, B, wmax=wmax)
+                                      K.upload(dev, slot_of)[0], slot_tree, id_tree, None, B, wmax=wmax)
                 elif self.classification:
                     Hb = K.hist_classes(data.bins, d, node, weights, stats_rows["label"], self.C,
                                         K.upload(dev, slot_of)[0],
-                                        slot_tree, fm_build, B, id_tree=id_tree)
+                                        slot_tree, None, B, id_tree=id_tree)
                 else:
                     Hb = K.hist_moments(data.bins, d, node, weights, stats_rows.get("v0"), stats_rows["v1"],
-                                        K.upload(dev, slot_of)[0], slot_tree, fm_build, B, id_tree=id_tree)
+                                        K.upload(dev, slot_of)[0], slot_tree, None, B, id_tree=id_tree)
             if cls2 and hist_raw_scale is not None:
                 Hb[..., 0] -= Hb[..., 1]  # packed (W, W1) -> class counts (W0, W1), exact int64
             rs_slice = None
-            if not reduced and self._rs_want(Hb, rs_on, sub_feats):
+            if not reduced and self._rs_want(Hb, rs_on):
                 rs_on = True
                 rs_slice, Hb = self._reduce_scatter_features(Hb, d)
                 if prev_hist is not None and prev_hist.shape[1] == d:
@@ -1719,9 +1632,7 @@ class ForestTrainer:
             # ---- assemble every active node's histogram
             derived = np.nonzero(~build)[0]
             is_raw = Hb.dtype == torch.int64
-            if sub_feats is not None:
-                H = Hb if dev.type == "cuda" else K.sub_hist_expand(Hb, sub_feats, d, mseg_raw)
-            elif is_raw or len(derived):
+            if is_raw or len(derived):
                 # one kernel (CPU: the same arithmetic in torch): fixed-point -> fp64 and parent - sibling
                 H = K.hist_assemble(Hb, hist_raw_scale if is_raw else None, prev_hist if len(derived) else None,
                                     slot_of, a_parent, a_sib, table=lvl[0] if lvl is not None else None)
@@ -1739,8 +1650,6 @@ class ForestTrainer:
                     if masks_dev is not None:
                         masks_np = self._feature_masks(tid.astype(np.uint64), a_key)
                     so, tot = self._rs_split(H, rs_slice, masks_np, d, dev)
-                elif sub_feats is not None:
-                    so, tot = K.split_scan_sub(H, sub_feats, self._nthr_dev(dev), mseg_raw, p.min_instances)
                 else:
                     so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
                                            p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight,
@@ -1760,7 +1669,7 @@ class ForestTrainer:
                     # the partition tables decoded on the device and the row partition queued right behind K6:
                     # the GPU partitions while the decisions travel to the host and the host builds the forest
                     # and the next level's layout (the same decode on the host, checked in the checked build)
-                    emit_ok = (K.EMIT_RECORDS and use_mseg and rec_ok and subtract and not use_sub and
+                    emit_ok = (K.EMIT_RECORDS and use_mseg and rec_ok and
                                w_total is not None and data.bins_s10 is not None and not margin_ok)
                     dec, em = self._device_partition(so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n,
                                                      stats_rows["v1"], mseg_scales[1] if use_mseg else 1.0,
@@ -1814,7 +1723,7 @@ class ForestTrainer:
                     else:
                         so_d = so[:, [0, 1, 2, 4, 5, 6, 7]]
                         tot_d = tot
-                    emit_ok = (K.EMIT_RECORDS and use_mseg and rec_ok and subtract and w_total is not None and
+                    emit_ok = (K.EMIT_RECORDS and use_mseg and rec_ok and w_total is not None and
                                data.bins_s10 is not None and not self.data.categorical)
                     dec, em = self._device_partition(so_d, tot_d, a_tree, tfirst, T, depth,
                                                      False, codes, emit_ok, n, stats_rows["v1"],
@@ -1950,8 +1859,7 @@ class ForestTrainer:
             n_sib = np.full(len(nl), -1, dtype=np.int64)
             n_sib[lp[both]] = rp[both]
             n_sib[rp[both]] = lp[both]
-            if subtract:
-                n_parent[n_sib < 0] = -1
+            n_parent[n_sib < 0] = -1
             if len(nl) and deep_switch and use_codes and depth + 1 >= 8:
                 # the next level can hold more than 255 nodes per tree: leave the u16 codes for node ids
                 # (active index of the node, -1 = done), partitioned and histogrammed by the node-id kernels
@@ -2003,7 +1911,7 @@ class ForestTrainer:
                     ck = np.stack([2 * ksp, 2 * ksp + 1], 1).reshape(-1)
                     heap_v[np.repeat(tsp, 2), ck - 1] = ch_vals[:, 0]
                     heap_depth = depth + 1
-            prev_hist = H if subtract else None
+            prev_hist = H
             emitted = em_next
             a_tree, a_fid, a_key, a_stats, a_sib, a_parent = n_tree, n_fid, n_key, n_stats, n_sib, n_parent
         # the last level's bookkeeping stays with the forest (settled by the predictor right after its launch, or

@@ -138,12 +138,6 @@ _SIGS = {
     "cdna_partition7_waves": ([c_int64, c_int, c_int], c_int),
     "cdna_emit_plan": ([c_void_p, c_int, c_void_p, c_int, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_int, c_void_p, c_void_p], c_int),
-    "cdna_sub_hist": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
-                       c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p], c_int),
-    "cdna_sub_hist_slot_bytes": ([c_int, c_int], c_int),
-    "cdna_sub_hist_lds_budget": ([], c_int),
-    "cdna_split_scan_sub": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_double, c_double, c_void_p, c_void_p,
-                             c_void_p], c_int),
     "cdna_split_decode": ([c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_double, c_int, c_int,
                            c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_int, c_double, c_void_p, c_void_p, c_void_p], c_int),
@@ -156,8 +150,6 @@ _SIGS = {
                          c_int),
     "cdna_partition_dest": ([c_int, c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],
                             c_int),
-    "cdna_seg_hist_subset": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                              c_float, c_void_p, c_int, c_void_p, c_void_p], c_int),
     "cdna_codes_compact_w": ([c_int, c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_float, c_void_p, c_void_p], c_int),
@@ -190,9 +182,6 @@ _SIGS = {
     "cdna_join_probe": ([c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p], c_int),
     "cdna_grouped_reduce": ([c_int, c_void_p, c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p], c_int),
-    "cdna_planar_bins": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p], c_int),
-    "cdna_hist_mfma": ([c_void_p, c_int64, c_int64, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                        c_void_p, c_int, c_void_p, c_float, c_int64, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_als_max_rank": ([], c_int),
     "cdna_als_accumulate": ([c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p,
                              c_void_p, c_void_p, c_void_p], c_int),

@@ -1755,46 +1755,6 @@ def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optio
     return out
 
 
-def seg_hist_subset(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v1p: torch.Tensor,
-                    wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int, feats: np.ndarray,
-                    scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False) -> torch.Tensor:
-    """Packed segment histograms [S, d, B, 2] over each slot's sampled features only (others stay 0).
-
-    feats: [S, m] feature ids of slot s (RandomForest per-node feature subsets).
-    """
-    G, n, _ = bins.shape
-    feats = np.asarray(feats, dtype=np.int32).reshape(S, -1)
-    m = feats.shape[1]
-    if not _native(bins):
-        out = seg_hist(bins, d, B, perm, None, v1p, wp, segs, S, wmax, scales)
-        keep = torch.zeros((S, d), dtype=torch.bool)
-        if S:
-            keep[torch.arange(S)[:, None], torch.from_numpy(feats).long()] = True
-        return out * keep[:, :, None, None]
-    out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
-    segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
-    if S == 0 or len(segs) == 0:
-        return out
-    wm = int(max(1, min(255, wmax)))
-    chunk = min(SEG_HIST_CHUNK, (1 << 20) // (wm + 1), ((1 << 24) - 1) // max(m, 1))  # pair index < 2^24
-    work = _seg_work(segs, chunk, interleave)
-    if len(work) == 0:
-        return out
-    qs1 = (scales if scales is not None else seg_scales(None, v1p, wm, n))[1]
-    if bins_rm is None:
-        bins_rm = bins_row_major(bins)
-    assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
-    dev = bins.device
-    wt, ft = upload(dev, work.reshape(-1), feats.reshape(-1))
-    iout = torch.zeros(out.shape, dtype=torch.int64, device=dev)
-    _lib.check(_lib.lib().cdna_seg_hist_subset(_ptr(bins_rm), n, bins_rm.shape[1] * 8, d, B, _ptr(perm), _ptr(v1p), _ptr(wp),
-                                               _ptr(wt), len(work), float(qs1), _ptr(ft), m, _ptr(iout),
-                                               _stream(dev)), "cdna_seg_hist_subset")
-    out.copy_(iout)
-    out[..., 1] /= qs1
-    return out
-
-
 def seg_partition(bins: torch.Tensor, perm: Optional[torch.Tensor], v0p: Optional[torch.Tensor], v1p: torch.Tensor,
                   wp: Optional[torch.Tensor], segs: np.ndarray, split_feat: np.ndarray, split_bin: np.ndarray,
                   cat_off: np.ndarray, cat_mask: np.ndarray, child: np.ndarray, n_next: int):
@@ -2106,71 +2066,6 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
                                           float(rec_scale) if rec else 0.0, _ptr(kstart_t), _stream(dev)),
                    "cdna_codes_compact_w(scatter)")
     return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
-
-
-# --------------------------------------------------------------- K5m (MFMA)
-# forest levels where every tree builds few nodes: the level histogram as one int8 MFMA GEMM over the rows
-# (hist_mfma.hip), bit-identical to the LDS-atomic segment histograms (seg_hist raw)
-MFMA_HIST = __import__("os").environ.get("CDNAML_MFMA_HIST", "0") != "0"  # opt-in: measured slower (profiles/r2/mfma_hist_ab.md)
-_MFMA_BT = (2, 3, 4)          # cell tiles of 16 (B <= 64)
-_MFMA_NT = (2, 4, 6, 7, 8)    # column tiles of 16 (5 columns per slot, <= 25 slots per pass)
-MFMA_FPB = 8  # features (waves) per block: the block's B tile (row records -> digits) is built once for 8
-MFMA_STAGE = 512  # rows per LDS stage of hist_mfma.hip (chunks and the planar row stride are multiples)
-MFMA_BLOCKS = int(__import__("os").environ.get("CDNAML_MFMA_BLOCKS", "1024"))  # target blocks per launch
-
-
-def _mfma_tiles(B: int, ns: int):
-    bt = next((b for b in _MFMA_BT if 16 * b >= B), None)
-    nt = next((t for t in _MFMA_NT if 16 * t >= 5 * ns), None)
-    return bt, nt
-
-
-def mfma_hist_ok(dev, B: int, wmax: int) -> bool:
-    return MFMA_HIST and dev.type == "cuda" and B <= 16 * _MFMA_BT[-1] and wmax <= 127
-
-
-def planar_bins(bins: torch.Tensor):
-    """[G, n, 8] bins -> planar [d_pad = 8G, ldp] uint8 (feature-major rows, ldp = n rounded up to the MFMA
-    kernel's stage length)."""
-    G, n, _ = bins.shape
-    ldp = max(MFMA_STAGE, -(-n // MFMA_STAGE) * MFMA_STAGE)
-    out = torch.empty((G * 8, ldp), dtype=torch.uint8, device=bins.device)
-    if n:
-        _lib.check(_lib.lib().cdna_planar_bins(_ptr(bins), n, G * 8, ldp, _ptr(out), _stream(bins.device)),
-                   "cdna_planar_bins")
-    return out, ldp
-
-
-def hist_mfma(bp: torch.Tensor, ldp: int, n: int, d: int, B: int, codes: torch.Tensor, tfirst: np.ndarray,
-              build_slot: np.ndarray, S: int, v1: torch.Tensor, qs1: float) -> torch.Tensor:
-    """Exact int64 fixed-point histograms [S, d, B, 2] (count, sum w*q) of every built slot, one int8 MFMA GEMM
-    per pass of <= 25 slots (GPU).  Same integers as ``codes_compact(rec_scale=qs1)`` + ``seg_hist(raw=True)``."""
-    dev = codes.device
-    out = torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev)
-    bs = np.asarray(build_slot, dtype=np.int64)
-    tf = np.asarray(tfirst, dtype=np.int64)
-    act = np.nonzero(bs >= 0)[0]
-    if S == 0 or len(act) == 0:
-        return out
-    order = act[np.argsort(bs[act], kind="stable")]
-    tree = np.searchsorted(tf, order, side="right") - 1
-    loc = order - tf[tree]
-    slots = bs[order]
-    v1c = v1.float().contiguous()
-    nfg = -(-d // MFMA_FPB)
-    nchunks = max(1, MFMA_BLOCKS // nfg)
-    per = -(-max(n, 1) // nchunks)
-    chunk = min(1 << 24, max(MFMA_STAGE, -(-per // MFMA_STAGE) * MFMA_STAGE))
-    for p0 in range(0, len(order), 25):
-        sl = slice(p0, p0 + 25)
-        ns = len(order[sl])
-        bt, nt = _mfma_tiles(B, ns)
-        acc = torch.zeros((d, bt * 16, nt * 16), dtype=torch.int64, device=dev)
-        meta, = upload(dev, np.stack([tree[sl], loc[sl], slots[sl]]).astype(np.int32))
-        _lib.check(_lib.lib().cdna_hist_mfma(_ptr(bp), ldp, n, d, B, bt, nt, _ptr(codes), _ptr(meta[0]),
-                                             _ptr(meta[1]), _ptr(meta[2]), ns, _ptr(v1c), float(qs1), chunk,
-                                             MFMA_FPB, _ptr(acc), _ptr(out), _stream(dev)), "cdna_hist_mfma")
-    return out
 
 
 BINS_RM_PAD = __import__("os").environ.get("CDNAML_BINS_RM_PAD", "1") != "0"
@@ -2830,120 +2725,3 @@ def group_first(gid: torch.Tensor, G: int) -> torch.Tensor:
     return first
 
 
-# --------------------------------------------------------------------- K5s / K6s (subhist.hip, split.hip)
-SUB_HIST_MAX_M = 127
-
-
-def sub_hist_groups(slot_tree: np.ndarray, ns_max: int) -> np.ndarray:
-    """Slot groups of a level: [G, 4] (s0, s1, t0, t1) runs of <= ns_max consecutive slots (slot_tree is
-    nondecreasing: the level's active nodes in (tree, node) order)."""
-    S = len(slot_tree)
-    out = []
-    for s0 in range(0, S, ns_max):
-        s1 = min(S, s0 + ns_max)
-        out.append((s0, s1, int(slot_tree[s0]), int(slot_tree[s1 - 1]) + 1))
-    return np.asarray(out, dtype=np.int32).reshape(-1, 4)
-
-
-def sub_hist_ns_max(B: int, m: int) -> int:
-    """Slots whose LDS histograms fit one block of the subset-histogram kernel (0: the kernel does not apply)."""
-    L = _lib.lib()
-    per = int(L.cdna_sub_hist_slot_bytes(B, m))
-    return max(0, min(8, int(L.cdna_sub_hist_lds_budget()) // per))
-
-
-def sub_hist(codes: torch.Tensor, v1: torch.Tensor, qs1: float, bins: torch.Tensor, bins_rm: Optional[torch.Tensor],
-             tfirst: np.ndarray, slot_tree: np.ndarray, feats: np.ndarray, B: int, wmax: int,
-             s_lo: int = 0, s_hi: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Exact int64 level histograms [S, m, B, 2] = (sum w, sum w q) over each active node's m sampled features.
-
-    codes [T, n] row codes (weight << 8 | local node); slot a of tree t = tfirst[t] + local node; feats [S, m]
-    the sampled features of every slot (ascending).  q = clamp(rint(v1 * qs1), +-2^23) -- the quantisation of the
-    record histograms, so these are the integers the full-feature histogram holds for the same features.
-    s_lo / s_hi / out: build slots [s_lo, s_hi) only, into ``out`` ([s_hi - s_lo, m, B, 2], zeroed).
-    GPU: subhist.hip (items generated from the codes on the fly, no compaction); CPU: the same integers."""
-    T, n = codes.shape
-    S = len(slot_tree)
-    s_hi = S if s_hi is None else s_hi
-    m = feats.shape[1]
-    dev = codes.device
-    ns = s_hi - s_lo
-    if out is None:
-        out = torch.zeros((ns, m, B, 2), dtype=torch.int64, device=dev)
-    if ns <= 0 or n == 0:
-        return out
-    tf = np.asarray(tfirst, dtype=np.int64)
-    if not _native(codes):
-        c = codes.to(torch.int32) & 0xFFFF
-        loc = c & 0xFF
-        w = c >> 8
-        ids = torch.from_numpy(tf)[:, None] + loc.long()
-        ok = (loc != CODE_DONE) & (w > 0) & (ids >= s_lo) & (ids < s_hi)
-        tt, rr = torch.nonzero(ok, as_tuple=True)
-        if rr.numel():
-            slot = ids[tt, rr] - s_lo
-            ww = w[tt, rr].long()
-            q = _quant(v1[rr], qs1, True)
-            G_, _, _ = bins.shape
-            flat = bins.permute(1, 0, 2).reshape(n, G_ * 8).long()
-            fl = torch.from_numpy(np.ascontiguousarray(feats[s_lo:s_hi]).astype(np.int64))
-            fi = fl[slot]                                                   # [N, m]
-            bi = flat[rr[:, None], fi]                                      # [N, m]
-            cell = ((slot[:, None] * m + torch.arange(m)[None, :]) * B + bi) * 2
-            o = out.view(-1)
-            o.index_add_(0, cell.reshape(-1), ww[:, None].expand(-1, m).reshape(-1))
-            o.index_add_(0, cell.reshape(-1) + 1, (ww * q)[:, None].expand(-1, m).reshape(-1))
-        return out
-    assert bins_rm is not None and bins_rm.shape[0] == n and bins_rm.shape[1] * bins_rm.shape[2] == 128
-    assert codes.is_contiguous() and out.is_contiguous() and out.dtype == torch.int64
-    assert m <= SUB_HIST_MAX_M and B <= 256
-    ns_max = sub_hist_ns_max(B, m)
-    assert ns_max >= 1
-    st = np.asarray(slot_tree, dtype=np.int64)[s_lo:s_hi]
-    groups = sub_hist_groups(st, ns_max)
-    G = len(groups)
-    lim = max(32, (1 << 20) // (max(1, min(255, wmax)) + 1))
-    target = -(-n * G // 1024)                       # >= ~4 blocks per CU
-    chunk = int(min(lim, max(4096, target)))
-    chunk -= chunk % 32
-    v1f = v1 if (v1.dtype == torch.float32 and v1.is_contiguous()) else v1.float().contiguous()
-    f8 = np.ascontiguousarray(feats[s_lo:s_hi]).astype(np.uint8)
-    tf_l, g_t, f_t = upload(dev, (tf - s_lo).astype(np.int32), groups.reshape(-1), f8.reshape(-1))
-    _lib.check(_lib.lib().cdna_sub_hist(_ptr(codes), _ptr(v1f), _ptr(bins_rm), n, 128, T, B, m, float(qs1),
-                                        _ptr(tf_l), _ptr(g_t), G, _ptr(f_t), ns_max, chunk, _ptr(out), _stream(dev)),
-               "cdna_sub_hist")
-    return out
-
-
-def split_scan_sub(Hc: torch.Tensor, feats: np.ndarray, nthr: torch.Tensor, scale1: float, min_inst: float):
-    """Best split per node of compact subset histograms Hc [A, m, B, 2] int64 (sub_hist) -> (out [A, 8],
-    tot [A, 2]) in split_scan's format (variance gain; features are the actual ids)."""
-    A, m, B, _ = Hc.shape
-    dev = Hc.device
-    if not _native(Hc):
-        # the fp64 arithmetic of the kernel through the full-feature torch path: expand into [A, d, B, 2]
-        raise RuntimeError("split_scan_sub runs on the GPU; the CPU engine scans the expanded histogram")
-    out = torch.empty((A, 8), dtype=torch.float64, device=dev)
-    tot = torch.empty((A, 2), dtype=torch.float64, device=dev)
-    if A == 0:
-        return out, tot
-    f_t, = upload(dev, np.ascontiguousarray(feats).astype(np.uint8).reshape(-1))
-    nt = nthr.to(device=dev, dtype=torch.int32).contiguous()
-    _lib.check(_lib.lib().cdna_split_scan_sub(_ptr(Hc.contiguous()), _ptr(f_t), _ptr(nt), A, m, B, float(scale1),
-                                              float(min_inst), _ptr(out), _ptr(tot), _stream(dev)),
-               "cdna_split_scan_sub")
-    return out, tot
-
-
-def sub_hist_expand(Hc: torch.Tensor, feats: np.ndarray, d: int, scale1: float) -> torch.Tensor:
-    """Compact int64 subset histograms [A, m, B, 2] -> fp64 moments [A, d, B, 2] (unsampled features zero), the
-    input of the torch split path (CPU ranks)."""
-    A, m, B, _ = Hc.shape
-    H = torch.zeros((A, d, B, 2), dtype=torch.float64, device=Hc.device)
-    if A == 0:
-        return H
-    src = Hc.double()
-    src[..., 1] /= scale1
-    idx = torch.from_numpy(np.ascontiguousarray(feats).astype(np.int64)).to(Hc.device)
-    H.scatter_(1, idx[:, :, None, None].expand(-1, -1, B, 2), src)
-    return H

@@ -887,39 +887,6 @@ def test_hist_assemble_many_nodes(dev):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("T,d,B,nb,n", [(20, 100, 40, 1, 200003), (20, 100, 40, 2, 50000), (7, 13, 17, 1, 30001),
-                                        (30, 21, 64, 1, 40000), (20, 100, 40, 3, 20000)])
-def test_hist_mfma_matches_segment_histograms(dev, T, d, B, nb, n):
-    """K5m: the int8-MFMA level histogram (one-hot bins x limb-split weighted labels) gives exactly the int64
-    fixed-point sums of the LDS-atomic path (codes_compact records + seg_hist raw), for 1-3 built nodes per
-    tree, > 25 slots (several passes), partial feature groups and cell tiles."""
-    rng = np.random.default_rng(T * 1000 + d + nb)
-    nloc = nb + 1                                           # active nodes per tree: nb built + one derived
-    loc = rng.integers(0, nloc, (T, n))
-    w = rng.poisson(1.0, (T, n)).clip(0, 12)
-    loc = np.where(w == 0, 0xFF, loc)
-    codes = torch.from_numpy(((w << 8) | loc).astype(np.uint16).view(np.int16)).to(dev)
-    tfirst = np.arange(T, dtype=np.int32) * nloc
-    slot_of = np.full(T * nloc, -1, dtype=np.int32)
-    built = [t * nloc + k for t in range(T) for k in range(nloc) if k != (t % nloc)]
-    slot_of[built] = np.arange(len(built))
-    S = len(built)
-    g = torch.Generator().manual_seed(5)
-    X = torch.randn(n, d, generator=g)
-    thr, nthr = _thresholds(X, B)
-    bins, rm = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), want_rm=True)
-    if rm is None:
-        rm = K.bins_row_major(bins)
-    v1 = (torch.randn(n, generator=g) * 7).to(dev)
-    sc = K.seg_scales(None, v1, 12, n)
-    rec, _, _, _, sg = K.codes_compact(codes, torch.from_numpy(tfirst), slot_of, S, None, v1, rec_scale=sc[1])
-    sb = np.concatenate([sg, np.arange(S)[:, None]], 1)
-    ref = K.seg_hist(bins, d, B, rec, None, None, None, sb, S, 12, sc, bins_rm=rm, rec=True, raw=True)
-    bp, ldp = K.planar_bins(bins)
-    got = K.hist_mfma(bp, ldp, n, d, B, codes, tfirst, slot_of, S, v1, sc[1])
-    assert got.dtype == torch.int64 and torch.equal(got.cpu(), ref.cpu())
-
-
 def test_planar_bins(dev):
     g = torch.Generator().manual_seed(1)
     X = torch.randn(4099, 21, generator=g)
