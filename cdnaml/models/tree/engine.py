@@ -36,60 +36,56 @@ from ...utils import tracing as _tr
 from ..util import IllegalArgumentException
 
 # compact uint16 row records (hist5.hip) instead of int32 node ids + uint8 weights
-USE_CODES = __import__("os").environ.get("CDNAML_TREE_CODES", "1") != "0"
+USE_CODES = True
 # single-tree regression fits (boosting rounds, DecisionTree): rows kept grouped by node (seg.hip)
-USE_SEG = __import__("os").environ.get("CDNAML_TREE_SEG", "1") != "0"
+USE_SEG = True
 # multi-tree regression forests: level 0 on row records, then rows grouped by (tree, node) segments
-USE_MSEG = __import__("os").environ.get("CDNAML_TREE_MSEG", "1") != "0"
-MSEG_L0 = __import__("os").environ.get("CDNAML_MSEG_L0", "1") != "0"  # level 0 through segments too
+USE_MSEG = True
+MSEG_L0 = True  # level 0 through segments too
 # single-tree packed fits (boosting rounds with unit hessians, DecisionTree) through row records + compaction
-MSEG_T1 = __import__("os").environ.get("CDNAML_MSEG_T1", "1") != "0"
+MSEG_T1 = True
 # binary classification forests on the packed record / segment path (class counts from (W, W1) sums)
-MSEG_CLS = __import__("os").environ.get("CDNAML_MSEG_CLS", "1") != "0"
+MSEG_CLS = True
 # K6 split search in one HIP kernel (split.hip) where it applies; else the torch formulation
-NATIVE_SPLIT = __import__("os").environ.get("CDNAML_NATIVE_SPLIT", "1") != "0"
+NATIVE_SPLIT = True
 # segment-mode forests carry one packed 8-byte record per gathered row (row | weight | quantised label)
-MSEG_REC = __import__("os").environ.get("CDNAML_MSEG_REC", "1") != "0"
+MSEG_REC = True
 # level 0 on seg10 rows: root records compacted inside the histogram kernel (no codes_compact pass)
-ROOT_HIST = __import__("os").environ.get("CDNAML_ROOT_HIST", "1") != "0"
+ROOT_HIST = True
 # binning queued on the quantile kernel's device thresholds, checked on the host behind it
-SPEC_THRESHOLDS = __import__("os").environ.get("CDNAML_SPEC_THRESHOLDS", "1") != "0"
+SPEC_THRESHOLDS = True
 # single-output forests of depth <= 8 predict from a heap layout (8-byte nodes, fixed-step walks)
-HEAP_PREDICT = __import__("os").environ.get("CDNAML_HEAP_PREDICT", "1") != "0"
-# row-record partition gathers split bins from the row-major copy (one line per row) instead of [G][n]
-PARTITION_RM = __import__("os").environ.get("CDNAML_PARTITION_RM", "0") != "0"
-# levels below the u16 codes (binary classification deeper than 8) keep the record histograms via node ids
-DEEP_REC = __import__("os").environ.get("CDNAML_DEEP_REC", "1") != "0"
+HEAP_PREDICT = True
 # regression forests (T > 1) deeper than 8 levels: the packed record levels down to 8, then node ids (as binary
 # classification); 0 = the node-id histograms from the root (round 3).  RF 20 trees depth 10 at 1e7 x 100:
 # 376 -> 88 ms per fit.  One tree keeps the permutation segment path (seg.hip, any depth): 14 ms at depth 12
 # against 38 ms switched (profiles/r4/deep_reg_ab.md)
-DEEP_REG = __import__("os").environ.get("CDNAML_DEEP_REG", "1") != "0"
+DEEP_REG = True
 # per-node feature subsets drawn on the GPU (misc.hip feature_masks_kernel) on levels whose masks have no host
 # consumer; 0 = numpy + upload every level
-MASKS_DEV = __import__("os").environ.get("CDNAML_MASKS_DEV", "1") != "0"
+MASKS_DEV = True
 # predictor tables of tuner-cut forests from the arrays truncate_forest computed (0: from the node lists)
-CUT_ARRAYS = __import__("os").environ.get("CDNAML_CUT_ARRAYS", "1") != "0"
+CUT_ARRAYS = True
 # boosting margins updated by the level partitions (ForestTrainer.train(margin=...)) instead of a tree walk
-GBDT_MARGIN = __import__("os").environ.get("CDNAML_GBDT_MARGIN", "1") != "0"
+GBDT_MARGIN = True
 # multi-rank record histograms: slot chunks whose all-reduces overlap the next chunk's histogram kernel
-HIST_OVERLAP = int(__import__("os").environ.get("CDNAML_HIST_OVERLAP", "2"))
+HIST_OVERLAP = 2
 # ... only for level histograms of at least this many bytes: at the 8-GPU point's per-rank shape (1.25e7 rows)
 # building a level in 4 / 2 slot chunks cost 22.2 / 20.6 ms per step vs 19.9 ms in one launch (each chunk's
 # launch ends in a partly idle round of blocks), while a <= 10 MB RCCL all-reduce over xGMI takes ~0.1-0.2 ms
-HIST_OVERLAP_MIN_BYTES = int(__import__("os").environ.get("CDNAML_HIST_OVERLAP_MIN_BYTES", str(64 << 20)))
+HIST_OVERLAP_MIN_BYTES = 64 << 20
 # take the slot-chunked (overlapped all-reduce) histogram path on one rank too: measures its launch cost at a
 # per-rank shape on a 1-GPU box
-HIST_OVERLAP_FORCE = __import__("os").environ.get("CDNAML_HIST_OVERLAP_FORCE", "0") != "0"
+HIST_OVERLAP_FORCE = False
 # Level histograms of at least this many bytes (int64, distributed, regression / XGBoost statistics, no
 # categorical features) are reduce-scattered by feature instead of all-reduced: every rank receives the sums of
 # d / W features (1/W of an all-reduce's bytes per GPU), runs K6 on its slice, and the per-node winners are
 # all-gathered (a few hundred bytes).  Once a fit switches a tree pass over, its later levels stay
 # reduce-scattered (sibling subtraction needs the parent's slice).  GBDT at max_bin=256, d=100: levels >= 5.
-RS_MIN_BYTES = int(__import__("os").environ.get("CDNAML_RS_MIN_BYTES", str(4 << 20)))
+RS_MIN_BYTES = 4 << 20
 # numeric regression levels on row records: decode the split decisions into partition tables on the device and
 # queue the partition before the decisions reach the host (no idle device -> host -> device round trip per level)
-DEVICE_DECODE = __import__("os").environ.get("CDNAML_DEVICE_DECODE", "1") != "0"
+DEVICE_DECODE = True
 
 
 @dataclass
@@ -888,8 +884,7 @@ def _splitmix64(x: np.ndarray) -> np.ndarray:
 
 def _built_nodes(w: np.ndarray, a_sib: np.ndarray, a_parent: np.ndarray) -> np.ndarray:
     """Subtraction levels: the active nodes whose histogram is built -- the smaller of two active siblings (ties:
-    the first one), the other derived as parent - sibling; a node without an active sibling is built.  The
-    device twin is split.hip emit_plan_kernel (K.emit_plan_host)."""
+    the first one), the other derived as parent - sibling; a node without an active sibling is built."""
     build = np.ones(len(w), dtype=bool)
     has = np.nonzero((a_sib >= 0) & (a_parent >= 0))[0]
     wa, ws = w[has], w[a_sib[has]]
@@ -1202,14 +1197,13 @@ class ForestTrainer:
             raise RuntimeError("device split decode differs from the host decode")
 
     # ------------------------------------------------------------ device-queued partition
-    def _device_partition(self, so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n, v1, qs1, w_total,
-                          rec_buf, margin=None, catm=None, node=None, pre=None):
+    def _device_partition(self, so, tot, a_tree, tfirst, T, depth, mb, codes, margin=None, catm=None, node=None,
+                          pre=None):
         """Partition tables decoded on the device from the level's K6 decisions and the row partition queued right
         behind them (the GPU partitions while the decisions travel to the host; the host repeats the decode to
-        build the forest and the next level, checked against the device's in the checked build).  With
-        ``emit_ok`` the partition also writes the next level's item records.  -> (decode tables, RecordEmit|None)."""
+        build the forest and the next level, checked against the device's in the checked build).  -> the decode
+        tables."""
         p, data, dev = self.p, self.data, self.device
-        A = so.shape[0]
         # (``pre``: the two tables uploaded at the level start with the level's other small tables)
         a_tree_d, tf_d = pre if pre is not None else \
             K.upload(dev, a_tree.astype(np.int32), tfirst.numpy().astype(np.int32))
@@ -1217,58 +1211,17 @@ class ForestTrainer:
                              depth < p.max_depth, depth + 1 >= p.max_depth, missing_bin=mb,
                              leaf_values=(p.impurity, p.reg_lambda) if margin is not None else None,
                              catm=catm, nthr=self._nthr_dev(dev) if catm is not None else None)
-        em = None
-        if emit_ok and A <= K.P7_MAX_SLOTS and data.bins.shape[0] <= 16 and T <= 64:
-            em = self._record_emit(dev, n, A, v1, qs1, w_total, rec_buf)
-            if em is not None:
-                em.plan(so, dec["child"])
         with _tr.span("tree.partition", depth=depth):
             if node is not None:
                 # levels below the u16 codes: the node-id partition from the same device tables (child = the
                 # next level's global active index, as the host decode's)
                 K.partition(data.bins, node, dec["split_feat"], dec["split_bin"], dec["cat_off"],
                             dec["masks"].reshape(-1), dec["child"])
-                return dec, em
+                return dec
             K.partition_codes(data.bins, codes, tf_d, dec["tfirst_next"], dec["split_feat"],
                               dec["split_bin"], dec["cat_off"], dec["masks"].reshape(-1), dec["child"],
-                              bins_rm=data.row_major_bins() if PARTITION_RM else None, emit=em,
                               margin=(margin[0], dec["lv"], margin[1]) if margin is not None else None)
-        return dec, em
-
-    # ------------------------------------------------------------ record emission by the partition
-    @staticmethod
-    def _check_emitted(em, st, cap, codes, tfirst, slot_of, S, v1, qs1):
-        """Checked build: the device plan equals the host plan, every slot's emitted segment stays inside its
-        capacity, and its non-padding records are exactly the compaction's records of the same codes."""
-        got = em.seg_start[:S].cpu().numpy()
-        if not np.array_equal(got, st):
-            raise RuntimeError("device record-emission plan differs from the host plan")
-        ends = em.cursor.view(-1, em.cs)[:S, 0].cpu().numpy().astype(np.int64)
-        if np.any(ends < st) or np.any(ends > st + cap):
-            raise RuntimeError("emitted records outside their segment capacity")
-        ref, _, _, _, sg = K.codes_compact(codes, tfirst, slot_of, S, None, v1, rec_scale=qs1)
-        ref = ref.cpu().numpy()
-        rec = em.rec.cpu().numpy() if S else None
-        for s in range(S):
-            r = rec[st[s]:ends[s]]
-            r = np.sort(r[((r >> 31) & 0xFF) != 0])
-            e = np.sort(ref[sg[s, 0]:sg[s, 0] + sg[s, 1]])
-            if not np.array_equal(r, e):
-                raise RuntimeError(f"emitted records of slot {s} differ from the compaction's")
-    def _record_emit(self, dev, n: int, A: int, v1: torch.Tensor, qs1: float, w_total: float, rec_buf):
-        """A K.RecordEmit for the partition of a level with A active nodes (the next level's records written by the
-        partition itself), or None when its capacity plan does not fit int32 positions.  Capacities come from the
-        all-reduced child weights, so on W ranks each rank's buffer is sized by the global weights."""
-        G = self.data.bins.shape[0]
-        waves = K.partition7_waves(n, G)
-        share = n / max(1, self.data.n_global)
-        ch = K.emit_chunk(0.5 * w_total * share, waves, A)
-        cap_total = int(w_total) + A * (waves * ch + ch) + K.REC_PAD
-        if waves <= 0 or cap_total >= 2 ** 31 - 1:
-            return None
-        rec = rec_buf if (rec_buf is not None and rec_buf.numel() >= cap_total) else \
-            torch.empty(cap_total, dtype=torch.int64, device=dev)
-        return K.RecordEmit(dev, n, A, rec, v1, qs1, ch, waves)
+        return dec
 
     # ------------------------------------------------------------ reduce-scatter by feature
     def _rs_want(self, Hb: torch.Tensor, rs_on: bool) -> bool:
@@ -1338,7 +1291,7 @@ class ForestTrainer:
         return sel[:, :8].contiguous(), sel[:, 9:11].contiguous()
 
     # ------------------------------------------------------------ training
-    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev, seg_end=None):
+    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev):
         """Record histograms of a level's S slots in HIST_OVERLAP slot chunks; chunk c's all-reduce runs on the
         collective stream while chunk c + 1 is built (one per-level RCCL all-reduce of 1-50 MB otherwise
         serialises with the compute stream).  The sums are exact integers, so the result is identical to one
@@ -1356,11 +1309,8 @@ class ForestTrainer:
                 sel = (sb[:, 2] >= s0) & (sb[:, 2] < s1)
                 sbc = sb[sel].copy()
                 sbc[:, 2] -= s0
-                se = None
-                if seg_end is not None:  # slot-range slice of the record ends
-                    se = (seg_end[0][s0 * seg_end[1]:], seg_end[1])
                 K.seg_hist(data.bins, d, B, rec, None, None, None, sbc, s1 - s0, wmax, scales, bins_rm=rm,
-                           interleave=True, rec=True, raw=True, out=Hb[s0:s1], rm_s10=s10, seg_end=se)
+                           interleave=True, rec=True, raw=True, out=Hb[s0:s1], rm_s10=s10)
             with _tr.span("tree.allreduce_async", cat="comm", bytes=(s1 - s0) * d * B * 16):
                 pend.append(self.comm.all_reduce_async(Hb[s0:s1]))
         with _tr.span("tree.allreduce_wait", cat="comm"):
@@ -1470,10 +1420,6 @@ class ForestTrainer:
         a_parent = np.full(T, -1, dtype=np.int64)
         prev_hist = None  # [A_prev, d, B, k] histograms of last level's split nodes
         rs_on = False     # this pass reduce-scatters its level histograms by feature (RS_MIN_BYTES)
-        emitted = None    # K.RecordEmit: this level's item records, written by the previous level's partition
-        emits = []        # every RecordEmit of the fit (overflow flags checked at the end)
-        w_total = None    # sum of the root weights (bounds every level's records)
-        rec_buf = None
         root_ids = [None] * T
         deep_rec = False  # set at the switch to node ids (deep_switch)
         wdeep = None
@@ -1528,7 +1474,7 @@ class ForestTrainer:
                 elif 80 < B <= 256 and data.bins_rm is not None:
                     root_rows = data.bins_rm
             root_ok = (root_rows is not None and use_mseg and (depth >= 1 or MSEG_L0) and rec_ok and
-                       emitted is None and len(build_ids) > 0 and np.bincount(slot_tree, minlength=T).max() <= 1)
+                       len(build_ids) > 0 and np.bincount(slot_tree, minlength=T).max() <= 1)
             with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
                 if root_ok:
                     S_b = len(build_ids)
@@ -1541,25 +1487,12 @@ class ForestTrainer:
                                           torch.zeros((S_b, d, B, 2), dtype=torch.int64, device=dev))
                     hist_raw_scale = mseg_raw
                 elif use_mseg and (depth >= 1 or MSEG_L0):
-                    seg_end = None
-                    if emitted is not None:
-                        # the previous level's partition wrote this level's records (partition7 EMIT): segments
-                        # are the plan's capacities, the device cursors their ends
-                        wb = self._weights_v(a_stats)[build_ids]
-                        cap = ((wb.astype(np.int64) + emitted.ch - 1) // emitted.ch) * emitted.ch + emitted.padb
-                        st = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.int64)
-                        perm, v0p, v1p, wp, sg = emitted.rec, None, None, None, np.stack([st, cap], 1)
-                        seg_end = emitted.seg_end()
-                        if K._lib.DEBUG:
-                            self._check_emitted(emitted, st, cap, codes, tfirst, slot_of, len(build_ids),
-                                                stats_rows["v1"], mseg_scales[1])
-                    else:
-                        # gather the rows of the built nodes into slot segments, then segment histograms
-                        # packed item records on every device (the CPU emulates the HIP compaction + flat
-                        # histogram exactly, so gloo ranks traverse the integer path RCCL ranks take)
-                        perm, v0p, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, len(build_ids),
-                                                                 stats_rows.get("v0"), stats_rows["v1"],
-                                                                 rec_scale=mseg_scales[1] if rec_ok else None)
+                    # gather the rows of the built nodes into slot segments, then segment histograms of packed
+                    # item records on every device (the CPU emulates the HIP compaction + flat histogram
+                    # exactly, so gloo ranks traverse the integer path RCCL ranks take)
+                    perm, v0p, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, len(build_ids),
+                                                             stats_rows.get("v0"), stats_rows["v1"],
+                                                             rec_scale=mseg_scales[1] if rec_ok else None)
                     is_rec = rec_ok and v1p is None
                     sb = np.concatenate([sg, np.arange(len(build_ids), dtype=np.int64)[:, None]], 1)
                     if is_rec and (self.comm.distributed or HIST_OVERLAP_FORCE) and HIST_OVERLAP > 1 and \
@@ -1570,16 +1503,14 @@ class ForestTrainer:
                         # features, while prev_hist then holds only this rank's feature slice)
                         # comm/compute overlap: the level's slots are built in chunks, each chunk's int64
                         # histogram all-reduced (async, RCCL stream) while the next chunk is built
-                        Hb = self._hist_overlapped(data, d, B, perm, sb, len(build_ids), wmax, mseg_scales, dev,
-                                                   seg_end)
+                        Hb = self._hist_overlapped(data, d, B, perm, sb, len(build_ids), wmax, mseg_scales, dev)
                         hist_raw_scale = mseg_raw
                         reduced = True
                     else:
                         rm, s10 = (data.record_rows() if is_rec else (data.row_major_bins(), False)) \
                             if dev.type == "cuda" else (None, False)
                         Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax,
-                                        mseg_scales, bins_rm=rm, interleave=True, rec=is_rec, raw=True, rm_s10=s10,
-                                        seg_end=seg_end)
+                                        mseg_scales, bins_rm=rm, interleave=True, rec=is_rec, raw=True, rm_s10=s10)
                         hist_raw_scale = mseg_raw
                     del perm, v0p, v1p, wp
                 elif deep_rec and len(build_ids) and \
@@ -1642,7 +1573,6 @@ class ForestTrainer:
                 (K.upload(dev, masks_np.view(np.int32))[0] if masks_np is not None else None)
             catm_h = None  # left-category bit masks of the native categorical scan
             dec = None     # device-decoded partition tables (partition already queued)
-            em_next = None  # records of the next level written by this level's partition
             if rs_slice is not None or self._native_split(dev):
                 # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
                 mb = p.impurity == "xgb" and self.data.missing_bin
@@ -1669,17 +1599,10 @@ class ForestTrainer:
                     # the partition tables decoded on the device and the row partition queued right behind K6:
                     # the GPU partitions while the decisions travel to the host and the host builds the forest
                     # and the next level's layout (the same decode on the host, checked in the checked build)
-                    emit_ok = (K.EMIT_RECORDS and use_mseg and rec_ok and
-                               w_total is not None and data.bins_s10 is not None and not margin_ok)
-                    dec, em = self._device_partition(so, tot, a_tree, tfirst, T, depth, mb, codes, emit_ok, n,
-                                                     stats_rows["v1"], mseg_scales[1] if use_mseg else 1.0,
-                                                     w_total, rec_buf, margin=margin if margin_ok else None,
-                                                     node=node if deep_ids else None,
-                                                     pre=(lvl[1], lvl[2]) if lvl is not None else None)
-                    if em is not None:
-                        rec_buf = em.rec
-                        emits.append(em)
-                        em_next = em
+                    dec = self._device_partition(so, tot, a_tree, tfirst, T, depth, mb, codes,
+                                                 margin=margin if margin_ok else None,
+                                                 node=node if deep_ids else None,
+                                                 pre=(lvl[1], lvl[2]) if lvl is not None else None)
                 # so [A, 8] = gain, feature, bin, left (2), right (2), missing-goes-right: copied to the host as is
                 # (plus the node totals at level 0), no per-column device ops
                 sw = so.shape[1]
@@ -1723,19 +1646,10 @@ class ForestTrainer:
                     else:
                         so_d = so[:, [0, 1, 2, 4, 5, 6, 7]]
                         tot_d = tot
-                    emit_ok = (K.EMIT_RECORDS and use_mseg and rec_ok and w_total is not None and
-                               data.bins_s10 is not None and not self.data.categorical)
-                    dec, em = self._device_partition(so_d, tot_d, a_tree, tfirst, T, depth,
-                                                     False, codes, emit_ok, n, stats_rows["v1"],
-                                                     1.0 if cls2 else (mseg_scales[1] if use_mseg else 1.0),
-                                                     w_total, rec_buf,
-                                                     catm=cm if self.data.categorical else None,
-                                                     node=node if deep_ids else None,
-                                                     pre=(lvl[1], lvl[2]) if lvl is not None else None)
-                    if em is not None:
-                        rec_buf = em.rec
-                        emits.append(em)
-                        em_next = em
+                    dec = self._device_partition(so_d, tot_d, a_tree, tfirst, T, depth, False, codes,
+                                                 catm=cm if self.data.categorical else None,
+                                                 node=node if deep_ids else None,
+                                                 pre=(lvl[1], lvl[2]) if lvl is not None else None)
                     flush()
                     host_ev.synchronize()
                     host = host_p.numpy()
@@ -1783,8 +1697,6 @@ class ForestTrainer:
                 for t_, fid_ in zip(a_tree.tolist(), a_fid.tolist()):
                     root_ids[t_] = fid_
             W_a = self._weights_v(a_stats)
-            if depth == 0:
-                w_total = float(W_a.sum())  # bounds the records of every later level (each weighs >= 1)
             with np.errstate(invalid="ignore"):
                 can = np.isfinite(gain_h) & (gain_h > 0) & (gain_h >= p.min_info_gain) & \
                     (W_a >= 2 * p.min_instances)
@@ -1869,7 +1781,7 @@ class ForestTrainer:
                 # from ``weights``: None when the bootstrap draws arrived as row codes (BootstrapCodes)
                 weights = wdeep
                 # below level 8 the record histograms continue from the node ids (K.node_compact)
-                deep_rec = DEEP_REC and use_mseg and rec_ok
+                deep_rec = use_mseg and rec_ok
                 use_codes = use_mseg = False
                 codes = None
             if len(nl):
@@ -1887,9 +1799,7 @@ class ForestTrainer:
                             np.searchsorted(n_tree, np.arange(T), side="left").astype(np.int32))
                         K.partition_codes(data.bins, codes, tfirst, tfirst_next, torch.from_numpy(split_feat),
                                           torch.from_numpy(split_bin), torch.from_numpy(cat_off),
-                                          torch.from_numpy(cm.reshape(-1)), torch.from_numpy(child),
-                                          bins_rm=data.row_major_bins() if (PARTITION_RM and dev.type == "cuda")
-                                          else None)
+                                          torch.from_numpy(cm.reshape(-1)), torch.from_numpy(child))
                     else:
                         K.partition(data.bins, node, *K.upload(dev, split_feat, split_bin, cat_off,
                                                                cm.reshape(-1), child))
@@ -1912,17 +1822,19 @@ class ForestTrainer:
                     heap_v[np.repeat(tsp, 2), ck - 1] = ch_vals[:, 0]
                     heap_depth = depth + 1
             prev_hist = H
-            emitted = em_next
             a_tree, a_fid, a_key, a_stats, a_sib, a_parent = n_tree, n_fid, n_key, n_stats, n_sib, n_parent
         # the last level's bookkeeping stays with the forest (settled by the predictor right after its launch, or
         # by the first reader of the node lists)
         forest._pending.extend(pending)
         pending.clear()
-        if emits and int(torch.stack([e.err for e in emits]).max().item()):
-            raise RuntimeError("partition record emission overflowed its capacity plan")
         forest.roots.extend(root_ids)
         forest._dev = {}
         if heap is not None:
             S_ = 2 ** (heap_depth + 1) - 1
             forest._heap_np = (np.ascontiguousarray(heap[:, :S_]), np.ascontiguousarray(heap_v[:, :S_]), heap_depth)
         return forest
+
+
+from ...ops import tune as _tune  # noqa: E402  (CDNAML_TUNE overrides of the constants above)
+_tune.apply(__import__(__name__, fromlist=["_"]))
+_tune.check()

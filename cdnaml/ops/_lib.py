@@ -119,7 +119,7 @@ _SIGS = {
                     c_int, c_void_p, c_void_p], c_int),
     "cdna_hist5_max_trees": ([], c_int),
     "cdna_seg_hist": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                       c_int, c_float, c_float, c_void_p, c_int, c_void_p, c_int, c_void_p], c_int),
+                       c_int, c_float, c_float, c_void_p, c_int, c_void_p], c_int),
     "cdna_seg_hist_root_wide": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int,
                                  c_void_p, c_int, c_void_p, c_void_p], c_int),
     "cdna_seg_hist_root": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int, c_void_p,
@@ -133,11 +133,7 @@ _SIGS = {
     "cdna_expr_eval": ([c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int,
                         c_void_p, c_void_p], c_int),
     "cdna_partition7": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int,
-                         c_void_p, c_int, c_int, c_void_p, c_void_p], c_int),
-    "cdna_partition7_waves": ([c_int64, c_int, c_int], c_int),
-    "cdna_emit_plan": ([c_void_p, c_int, c_void_p, c_int, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
-                        c_int, c_void_p, c_void_p], c_int),
+                         c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_split_decode": ([c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_double, c_int, c_int,
                            c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_int, c_double, c_void_p, c_void_p, c_void_p], c_int),

@@ -140,16 +140,16 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
     return torch.from_numpy(_philox.poisson(T, n, seed, int(offset), float(rate)))
 
 
-POISSON_CODES = __import__("os").environ.get("CDNAML_POISSON_CODES", "1") != "0"
+POISSON_CODES = True
 
 
 # where the forest's bootstrap draws run (profiles/r4/prologue_ab.md): "main" -- in series right before the
 # binning; "side" -- the side stream at the same point; "auto" -- draws of at most POISSON_EARLY_MAX (T x rows)
 # start on the side stream with the fit (grid bounded to POISSON_EARLY_BLOCKS: beside the quantile sample's
 # latency-bound kernels, without keeping its sort's 1024-thread blocks off the CUs), larger ones in series
-POISSON_STREAM = __import__("os").environ.get("CDNAML_POISSON_STREAM", "auto")
-POISSON_EARLY_MAX = float(__import__("os").environ.get("CDNAML_POISSON_EARLY_MAX", "5e8"))
-POISSON_EARLY_BLOCKS = int(__import__("os").environ.get("CDNAML_POISSON_EARLY_BLOCKS", "512"))
+POISSON_STREAM = "auto"
+POISSON_EARLY_MAX = 500000000.0
+POISSON_EARLY_BLOCKS = 512
 
 
 class BootstrapCodes:
@@ -416,20 +416,20 @@ def _plan_chunks(n: int, G: int, ngroups: int, target_blocks: int = 2048) -> int
     return int(max(1, min(per, (n + 4095) // 4096)))
 
 
-HIST_LDS_BUDGET = int(__import__("os").environ.get("CDNAML_HIST_LDS", str(64 * 1024)))
-HIST_VERSION = int(__import__("os").environ.get("CDNAML_HIST_VERSION", "4"))
+HIST_LDS_BUDGET = 64 * 1024
+HIST_VERSION = 4
 # lane mapping: 2 = lane per row; 3 = lane = 8*row + feature; 4 = lane per row, rotated features + pipelined
 # loads; 5 = 4 with the per-update VALU work hoisted (hist4f_kernel)
-HIST_MAP = int(__import__("os").environ.get("CDNAML_HIST_MAP", "5"))
+HIST_MAP = 5
 # regression histograms: one packed (count | offset sum) ds_add_u64 per update (hist4.hip hist4p_kernel)
-HIST_PACKED = __import__("os").environ.get("CDNAML_HIST_PACKED", "0") != "0"
+HIST_PACKED = False
 # hist v5 (row records): packed single-atomic regression histograms, trees per block group when packed
-HIST5_PACKED = __import__("os").environ.get("CDNAML_HIST5_PACKED", "1") != "0"
-HIST5_PACKED_MAXT = int(__import__("os").environ.get("CDNAML_HIST5_PACKED_MAXT", "8"))
-HIST5_PACKED_LDS = int(__import__("os").environ.get("CDNAML_HIST5_PACKED_LDS", str(128 * 1024)))
+HIST5_PACKED = True
+HIST5_PACKED_MAXT = 8
+HIST5_PACKED_LDS = 128 * 1024
 # wave-compacted packed kernel (hist5q): full-wave LDS atomic rounds over sparse (row, tree) work
 # 0 off, 1 where it pays (deep levels), 2 always (tests)
-HIST5_COMPACT = int(__import__("os").environ.get("CDNAML_HIST5_COMPACT", "1"))
+HIST5_COMPACT = 1
 
 
 def _absmax(v: torch.Tensor) -> float:
@@ -916,96 +916,16 @@ def hist_codes(mode: int, bins: torch.Tensor, d: int, codes: torch.Tensor, tfirs
 
 
 # persistent partition (tables staged once per block, coalesced bins words, all trees' codes in flight)
-PARTITION7 = __import__("os").environ.get("CDNAML_PARTITION7", "1") != "0"
-PARTITION7_MIN_T = int(__import__("os").environ.get("CDNAML_PARTITION7_MIN_T", "16"))
+PARTITION7 = True
+PARTITION7_MIN_T = 16
 
-
-
-# ------------------------------------------------------------------ K7e: record emission by the partition
-EMIT_RECORDS = __import__("os").environ.get("CDNAML_P7_EMIT", "0") != "0"
-EMIT_CS = 32  # ints between chunk cursors (one 128-byte line each)
-
-
-class RecordEmit:
-    """Device state of one level's record emission (partition7 EMIT, hist5.hip; plan: split.hip emit_plan).
-
-    The partition of level L writes the packed item records of level L + 1's BUILT nodes (smaller active sibling,
-    ties to the left child; a lone active child) into per-slot segments of ``rec``: slot s owns
-    [seg_start[s], seg_lim[s]) with seg_lim - seg_start = roundup(W_s, ch) + padb, and after the partition its
-    records (plus zero-weight padding) are [seg_start[s], cursor[s * cs]).  The host derives the same plan from
-    the decisions it receives (:func:`emit_plan_host`)."""
-
-    def __init__(self, dev, n: int, A: int, rec: torch.Tensor, v1: torch.Tensor, qs1: float, ch: int, waves: int):
-        self.dev, self.ch, self.cs = dev, int(ch), EMIT_CS
-        self.nslots_max = A  # one built child per split at most
-        self.waves = int(waves)
-        self.padb = self.waves * self.ch
-        self.rec, self.v1, self.qs1 = rec, v1.float().contiguous(), float(qs1)
-        ints = torch.empty(2 * A * 3 + 2 * A * self.cs + 2, dtype=torch.int32, device=dev)
-        self.cslot = ints[:2 * A]
-        self.seg_start = ints[2 * A:4 * A]
-        self.seg_lim = ints[4 * A:6 * A]
-        self.cursor = ints[6 * A:6 * A + 2 * A * self.cs]
-        self.nslots = ints[-2:-1]
-        self.err = ints[-1:]
-        self.err.zero_()
-
-    def plan(self, so: torch.Tensor, child: torch.Tensor):
-        A = so.shape[0]
-        sc = so.contiguous()
-        _lib.check(_lib.lib().cdna_emit_plan(_ptr(sc), sc.shape[1], _ptr(child), A, self.ch, int(self.padb),
-                                             _ptr(self.cslot), _ptr(self.seg_start), _ptr(self.seg_lim),
-                                             _ptr(self.cursor), self.cs, _ptr(self.nslots), _stream(self.dev)),
-                   "cdna_emit_plan")
-
-    def seg_end(self):
-        """(cursor tensor, stride): slot s's records end at cursor[s * stride] after the partition."""
-        return self.cursor, self.cs
-
-
-P7_MAX_SLOTS = 256  # kP7MaxS (hist5.hip)
-
-
-def partition7_waves(n: int, G: int) -> int:
-    """Waves of an emitting partition7 launch over n rows (its zero padding is bounded by one chunk per wave)."""
-    return int(_lib.lib().cdna_partition7_waves(int(n), int(G), 1))
-
-
-def emit_chunk(records_est: float, waves: int, slots_est: int) -> int:
-    """Chunk length: a power of two near 1/16 of a wave's expected records per slot (so the zero padding of
-    each wave's last chunk stays a few percent of the level), in [8, 128]."""
-    per = records_est / max(1, waves * max(1, slots_est))
-    ch = 8
-    while ch < 128 and ch * 32 <= per:
-        ch *= 2
-    return ch
-
-
-def emit_plan_host(w_left: np.ndarray, w_right: np.ndarray, child: np.ndarray, ch: int, padb: int):
-    """Host twin of emit_plan_kernel: (cslot [2A], seg_start [S], cap [S]) from the level's left / right child
-    weights and the active-children table ``child`` [2A] (-1: not active)."""
-    A = len(w_left)
-    c = np.asarray(child).reshape(A, 2)
-    wl, wr = np.asarray(w_left, np.float64), np.asarray(w_right, np.float64)
-    bl = (c[:, 0] >= 0) & ((c[:, 1] < 0) | (wl <= wr))
-    br = (c[:, 1] >= 0) & ((c[:, 0] < 0) | (wr < wl))
-    built = np.stack([bl, br], 1).reshape(-1)
-    w = np.stack([wl, wr], 1).reshape(-1)
-    cslot = np.full(2 * A, -1, dtype=np.int64)
-    cslot[built] = np.arange(int(built.sum()))
-    cap = ((w[built].astype(np.int64) + ch - 1) // ch) * ch + padb
-    start = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.int64) if len(cap) else np.zeros(0, np.int64)
-    return cslot, start, cap
 
 
 def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tensor, tfirst_next: torch.Tensor,
                     split_feat: torch.Tensor, split_bin: torch.Tensor, cat_off: torch.Tensor,
-                    cat_mask: torch.Tensor, child: torch.Tensor, bins_rm: Optional[torch.Tensor] = None,
-                    emit: Optional["RecordEmit"] = None, margin: Optional[tuple] = None) -> None:
+                    cat_mask: torch.Tensor, child: torch.Tensor, margin: Optional[tuple] = None) -> None:
     """In place: every row's code moves to the chosen child's local index (255 = done).
 
-    bins_rm: optional row-major copy [n, G, 8] of the bins, read instead of ``bins`` when given.
-    emit: (GPU, partition7) also write the next level's item records of the built children (:class:`RecordEmit`).
     margin (GPU, partition5): ``(F [n] fp32, lv [3A] fp32 from split_decode, eta)`` -- rows that finish at this
     level add ``eta * leaf value`` to F (boosting margin update without a tree walk)."""
     G, n, _ = bins.shape
@@ -1027,30 +947,17 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
         # partition7 streams every bins word of every row once per level (10 GB at 1e8 x 100): it pays when
         # many trees share that pass; for few trees partition5's per-(row, tree) byte gathers move less (GBDT,
         # T = 1: 57.9 vs 40.6 ms per boosting round with partition7; CV grid with 5 / 10 trees: 2.18 vs 1.34 s)
-        if margin is None and (emit is not None or (PARTITION7 and T >= PARTITION7_MIN_T and G <= 16 and
-                                                     A <= 1024 and T <= 64 and bins_rm is None)):
-            e = emit
+        if margin is None and PARTITION7 and T >= PARTITION7_MIN_T and G <= 16 and A <= 1024 and T <= 64:
             _lib.check(_lib.lib().cdna_partition7(
                 _ptr(bins), n, G, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]), _ptr(args[2]), _ptr(args[3]),
-                _ptr(args[4]), _ptr(cm), _ptr(args[5]),
-                None if e is None else _ptr(e.cslot), None if e is None else _ptr(e.v1),
-                0.0 if e is None else float(e.qs1), None if e is None else _ptr(e.rec),
-                None if e is None else _ptr(e.cursor), 1 if e is None else e.cs,
-                None if e is None else _ptr(e.seg_lim), 0 if e is None else e.nslots_max,
-                1 if e is None else e.ch, None if e is None else _ptr(e.err), _stream(bins.device)),
-                "cdna_partition7")
+                _ptr(args[4]), _ptr(cm), _ptr(args[5]), _stream(bins.device)), "cdna_partition7")
             return
-        assert emit is None
-        src, rm_bytes = bins, 0
-        if bins_rm is not None:
-            assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
-            src, rm_bytes = bins_rm, bins_rm.shape[1] * 8
         F, lv, eta = margin if margin is not None else (None, None, 0.0)
         if margin is not None:
             assert F.dtype == torch.float32 and F.is_contiguous() and F.numel() == n and lv.numel() == 3 * A
-        _lib.check(_lib.lib().cdna_partition5(_ptr(src), n, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]),
+        _lib.check(_lib.lib().cdna_partition5(_ptr(bins), n, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]),
                                               _ptr(args[2]), _ptr(args[3]), _ptr(args[4]), _ptr(cm),
-                                              _ptr(args[5]), rm_bytes, _ptr(lv), float(eta), _ptr(F),
+                                              _ptr(args[5]), 0, _ptr(lv), float(eta), _ptr(F),
                                               _stream(bins.device)), "cdna_partition5")
         return
     assert margin is None, "margin updates run in the GPU partition only"
@@ -1365,9 +1272,9 @@ def logistic_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b: float,
 
 
 # ------------------------------------------------------------ segment mode (seg.hip)
-SEG_HIST_CHUNK = int(__import__("os").environ.get("CDNAML_SEG_HIST_CHUNK", "262144"))
+SEG_HIST_CHUNK = 262144
 # row-major bins copy for segment histograms (one cache line per row instead of one per 8-feature group)
-SEG_ROW_MAJOR = __import__("os").environ.get("CDNAML_SEG_ROW_MAJOR", "1") != "0"
+SEG_ROW_MAJOR = True
 SEG_PART_CHUNK = 8192
 
 
@@ -1387,24 +1294,24 @@ def seg_scales(v0p: Optional[torch.Tensor], v1p: torch.Tensor, wmax: int, n_glob
     return (_fixed_scale(m[0:1], n_global, w, qmax_bits=30), _fixed_scale(m[1:2], n_global, w, qmax_bits=30))
 
 
-SEG_MIN_BLOCKS = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS", "2048"))
-SEG_ROUND_FIT = __import__("os").environ.get("CDNAML_SEG_ROUND_FIT", "1") != "0"
+SEG_MIN_BLOCKS = 2048
+SEG_ROUND_FIT = True
 # wide-bin (80 < B <= 256, boosting) record levels: work items per level (x ceil(d / 64) feature blocks).  Every block
 # clears and flushes 64 features x B bins of LDS cells into the level histogram with global atomics, so at deep
 # boosting levels (fewer rows, the same number of blocks) the flush -- not the rows -- sets the level time.
 # bench_configs.py gbdt (1e8 x 100, 256 bins), 3 interleaved reps: 1024 -> 28.05-28.23, 768 -> 27.83-27.85,
 # 512 -> 27.78-27.83 ms per tree (profiles/r4/gbdt_min_blocks_ab.txt)
-SEG_MIN_BLOCKS_WIDE = int(__import__("os").environ.get("CDNAML_SEG_MIN_BLOCKS_WIDE", "512"))
+SEG_MIN_BLOCKS_WIDE = 512
 # three-times-larger record chunks for the six-items-per-wave kernel (its count field is spread over three cell
 # copies): measured 145.1 vs 139.8 ms per headline step (fewer, longer blocks) and neutral at 1.25e7 rows -- off
-LANE10_CHUNK3 = __import__("os").environ.get("CDNAML_LANE10_CHUNK3", "0") != "0"
+LANE10_CHUNK3 = False
 # record histograms through the lane-feature kernel (seg_hist_lane_kernel: lanes own features, bin-major
 # conflict-free LDS planes, one v_perm per cell address); B <= 80 (4 planes <= 80 KB of LDS), 80 < B <= 256:
 # seg_hist_lane4_kernel (64 features per block, a quarter-wave per item; CDNAML_SEG_WIDE=0 keeps the flat kernel)
-SEG_LANE = __import__("os").environ.get("CDNAML_SEG_LANE", "1") != "0"
+SEG_LANE = True
 # seg10 rows + the six-items-per-wave record histogram for 80 < d <= 100, B <= 40 (CDNAML_SEG10=0: lane8 rows)
-SEG10 = __import__("os").environ.get("CDNAML_SEG10", "1") != "0"
-SEG_LANE_MAX_B = 256 if __import__("os").environ.get("CDNAML_SEG_WIDE", "1") != "0" else 80
+SEG10 = True
+SEG_LANE_MAX_B = 256
 # records buffers carry REC_PAD readable entries past their end: the lane kernel's record loads are unconditional
 REC_PAD = 128
 
@@ -1481,11 +1388,8 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
              v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
              scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False,
              rec: bool = False, raw: bool = False, out: Optional[torch.Tensor] = None,
-             rm_s10: bool = False, seg_end=None) -> torch.Tensor:
+             rm_s10: bool = False) -> torch.Tensor:
     """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
-
-    seg_end (rec + rm_s10, GPU): (tensor, stride) -- records emitted by the partition (:class:`RecordEmit`): the
-    segments in ``segs`` are capacities and slot s's records end at tensor[s * stride] (work items clipped).
 
     rm_s10 (rec): ``bins_rm`` is in the seg10 layout (:func:`bins_seg10`): the six-items-per-wave kernel.
 
@@ -1500,9 +1404,8 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
     if out is not None:
         assert rec and raw and out.dtype == torch.int64 and out.is_contiguous()
     if rec:
-        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw, out, rm_s10,
-                             seg_end)
-    assert not rm_s10 and seg_end is None
+        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw, out, rm_s10)
+    assert not rm_s10
     return _seg_hist(bins, d, B, perm, v0p, v1p, wp, segs, S, wmax, scales, bins_rm, interleave, raw)
 
 
@@ -1550,8 +1453,7 @@ def rec_encode(rows: torch.Tensor, w: torch.Tensor, q: torch.Tensor) -> torch.Te
     return rows.to(torch.int64) | (w.to(torch.int64) << 31) | ((q.to(torch.int64) + (1 << 23)) << 39)
 
 
-def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False, out=None, rm_s10=False,
-                  seg_end=None):
+def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False, out=None, rm_s10=False):
     G, n, _ = bins.shape
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
     if S == 0 or len(segs) == 0:
@@ -1560,7 +1462,6 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
     qs1 = float(scales[1])
     if not _native(bins):
-        assert seg_end is None
         pos, slot = _seg_items(segs)
         rows, w, q = rec_decode(rec[pos])
         iout = _int_hist_cpu(bins, d, B, S, rows, slot, w, w * q)
@@ -1588,12 +1489,8 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         if rm_s10:
             assert d <= 100 and B <= 40 and bins_rm.shape[1] == 16
             mode |= 128 | 256
-        if seg_end is not None:
-            assert rm_s10, "emitted records (seg_end) need the seg10 record kernel"
         _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(bins_rm), n, d, B, _ptr(rec), None, None, None,
                                             _ptr(wt), len(work), 1.0, qs1, _ptr(iout), bins_rm.shape[1],
-                                            None if seg_end is None else _ptr(seg_end[0]),
-                                            0 if seg_end is None else int(seg_end[1]),
                                             _stream(bins.device)), "cdna_seg_hist(rec)")
     if raw:
         return iout
@@ -1602,8 +1499,8 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
     return out
 
 
-CODES_HIST_BLOCKS = int(__import__("os").environ.get("CDNAML_CODES_HIST_BLOCKS", "0"))
-CODES_ROUND_FILL = __import__("os").environ.get("CDNAML_CODES_ROUND_FILL", "1") != "0"
+CODES_HIST_BLOCKS = 0
+CODES_ROUND_FILL = True
 _NCU = {}
 
 
@@ -1743,8 +1640,7 @@ def _seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Optio
         src = bins if bins_rm is None else bins_rm
         _lib.check(_lib.lib().cdna_seg_hist(mode, _ptr(src), n, d, B, _ptr(perm), _ptr(v0p), _ptr(v1p), _ptr(wp),
                                             _ptr(wt), len(work), float(qs0), float(qs1), _ptr(iout),
-                                            0 if bins_rm is None else bins_rm.shape[1], None, 0,
-                                            _stream(bins.device)),
+                                            0 if bins_rm is None else bins_rm.shape[1], _stream(bins.device)),
                    "cdna_seg_hist")
     if raw:
         return iout
@@ -1981,10 +1877,10 @@ def node_compact(node: torch.Tensor, w: torch.Tensor, tfirst: np.ndarray, build_
 
 
 NODE_COMPACT_MAX_LOC = 1024  # seg.hip kNodeCompactLoc
-COMPACT_W = __import__("os").environ.get("CDNAML_COMPACT_W", "1") != "0"
+COMPACT_W = True
 # record compaction without a host round trip before the scatter (device segment starts, totals copied back
 # behind the scatter kernel)
-COMPACT_DEFER = __import__("os").environ.get("CDNAML_COMPACT_DEFER", "1") != "0"
+COMPACT_DEFER = True
 
 
 def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, rec_scale=None):
@@ -2068,7 +1964,7 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
     return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
 
 
-BINS_RM_PAD = __import__("os").environ.get("CDNAML_BINS_RM_PAD", "1") != "0"
+BINS_RM_PAD = True
 
 
 def bins_row_major(bins: torch.Tensor, pad: Optional[bool] = None) -> torch.Tensor:
@@ -2564,7 +2460,7 @@ def hash_groups(key: torch.Tensor, values=(), accs=(), mode: int = 0, pout: int 
 
 
 # try the low-cardinality path (per-block LDS tables over row chunks + one merge) before partitioning
-LOCAL_FIRST = __import__("os").environ.get("CDNAML_HASH_LOCAL", "1") != "0"
+LOCAL_FIRST = True
 
 
 def _la_groups(key: torch.Tensor, values, accs, mode: int, pout: int):
@@ -2725,3 +2621,5 @@ def group_first(gid: torch.Tensor, G: int) -> torch.Tensor:
     return first
 
 
+from . import tune as _tune  # noqa: E402  (CDNAML_TUNE overrides of the constants above)
+_tune.apply(__import__(__name__, fromlist=["_"]))

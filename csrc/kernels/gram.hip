@@ -676,11 +676,7 @@ CDNA_API int cdna_gram(const float* X, int64_t n, int d, int64_t ldx, const floa
   if (d + 2 > 32 * 17) return (int)hipErrorInvalidValue;
   GramPlan pl = make_plan(n, d, bf16 != 0);
   if (pl.npairs > kMaxPairs) return (int)hipErrorInvalidValue;
-  static const bool direct_on = [] {
-    const char* e = getenv("CDNAML_GRAM_DIRECT");
-    return !e || atoi(e) != 0;
-  }();
-  if (bf16 && direct_on && direct_ok(X, d, ldx, shift)) {
+  if (bf16 && direct_ok(X, d, ldx, shift)) {
     pl = make_direct_plan(n, d);
     switch ((pl.npairs + kDWaves - 1) / kDWaves) {
       case 1: launch_direct_cpw<1>(pl, X, n, d, y, shift, yshift, ws, st); break;

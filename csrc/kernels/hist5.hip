@@ -840,33 +840,10 @@ constexpr int kP7MaxA = 1024;
 constexpr int kP7MaxT = 64;
 constexpr int kP7MaxG = 16;  // MAXG template: 8 / 13 / 16 words per row (registers sized to the row)
 constexpr int kP7TB = 24;
-constexpr int kP7MaxS = 256;  // EMIT: next-level slots (4 lane-distributed VGPRs of chunk cursors per wave)
 
-// EMIT (numeric regression forests on item records): the partition also writes the next level's packed item
-// records (row | w << 31 | (q + 2^23) << 39, the codes_scatter_w format) of every row whose new node is a
-// BUILT slot, so the level's histogram needs no codes_count_w + codes_scatter_w pass over the new codes.  Each
-// wave owns one open chunk of `ch` records per slot (its cursor held lane-distributed in 4 VGPRs: slot s at lane
-// s & 63 of register s >> 6); a wave's records of one slot in one tree are ranked by ballot (one peel per distinct
-// slot) and written at the chunk cursor, a full chunk is replaced by a fresh one reserved with ONE atomic add on
-// the slot's device cursor (k chunks at once when the wave needs more).  Chunks are contiguous in the slot's
-// segment, the last one of each wave is padded with zero records (weight 0: they add nothing) when the wave
-// ends, so segment = [seg_start, cursor) holds every record once.  Segment order differs from the scatter's row
-// order; the histogram's int64 sums do not depend on it.  The capacity bound (emit_plan: roundup(W, ch) + one
-// chunk per wave) holds because every record weighs >= 1; a reservation past seg_lim sets *err and drops.
-struct P7Emit {
-  const int* cslot;       // [2A] next-level slot of (node, side), -1: not built
-  const float* v1;        // [n] labels
-  float qs1;
-  uint64_t* rec;          // records buffer (absolute positions)
-  int* cursor;            // [S * cs] chunk cursors (initialised to the segment starts)
-  int cs;
-  const int* seg_lim;     // [S] segment capacity ends
-  int nslots;             // S (host-side upper bound is fine: unused states stay 0)
-  int ch;                 // chunk length (power of two)
-  int* err;               // overflow flag
-};
-
-template <int MAXG, bool EMIT>
+// (A variant that also wrote the next level's item records from the partition -- "EMIT", record emission --
+// measured 172.7 vs 138.9 ms per headline step and was removed: profiles/r4/emission_ab.md.)
+template <int MAXG>
 __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __restrict__ bins, int64_t n, int G, int T,
                                                          int A, uint16_t* __restrict__ codes,
                                                          const int* __restrict__ tfirst,
@@ -875,13 +852,12 @@ __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __re
                                                          const int* __restrict__ split_bin,
                                                          const int* __restrict__ cat_off,
                                                          const uint32_t* __restrict__ cat_mask,
-                                                         const int* __restrict__ child, const P7Emit em) {
+                                                         const int* __restrict__ child) {
   extern __shared__ __attribute__((aligned(16))) uint64_t tile7[];  // [G][256]
   // numeric: feature (0xFFFF: leaf) | bin << 16; categorical / bin-set split: feature | cat_off << 16 | 1 << 31
   __shared__ int s_fb[kP7MaxA];
   __shared__ uint8_t s_ch[2 * kP7MaxA];
   __shared__ int s_tf[kP7MaxT];
-  __shared__ int16_t s_cs[EMIT ? 2 * kP7MaxA : 1];
   for (int i = threadIdx.x; i < T; i += 256) s_tf[i] = tfirst[i];
   for (int i = threadIdx.x; i < A; i += 256) {
     const int f = split_feat[i];
@@ -896,66 +872,14 @@ __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __re
     const int c0 = child[i * 2], c1 = child[i * 2 + 1];
     s_ch[2 * i] = (uint8_t)(c0 >= 0 ? c0 - tfn : 0xFF);
     s_ch[2 * i + 1] = (uint8_t)(c1 >= 0 ? c1 - tfn : 0xFF);
-    if (EMIT) {
-      s_cs[2 * i] = (int16_t)em.cslot[2 * i];
-      s_cs[2 * i + 1] = (int16_t)em.cslot[2 * i + 1];
-    }
   }
   __syncthreads();
   const uint8_t* tb = reinterpret_cast<const uint8_t*>(tile7);
   const int lr = threadIdx.x;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * 256;
-  int vst[EMIT ? 4 : 1];  // EMIT: this wave's open-chunk cursor of slot 64 j + lane in vst[j] (0: none)
-#pragma unroll
-  for (int j = 0; j < (EMIT ? 4 : 1); ++j) vst[j] = 0;
-  // one tree's records of this wave: ranked per slot, written at the wave's chunk cursors
-  auto emit = [&](int slot, uint64_t rc) {
-    uint64_t pend = __builtin_amdgcn_ballot_w64(slot >= 0);
-    while (pend) {
-      const int ld = __builtin_ctzll(pend);
-      const int s = __builtin_amdgcn_readlane(slot, ld);
-      const uint64_t m = __builtin_amdgcn_ballot_w64(slot == s);
-      const int cnt = __builtin_popcountll(m);
-      const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      const int j = s >> 6, sl = s & 63;
-      int p = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (k == j) p = __builtin_amdgcn_readlane(vst[k], sl);
-      const int off = p & (em.ch - 1);
-      const int room = off ? em.ch - off : 0;
-      int dst = p + rank;
-      if (cnt > room) {  // wave-uniform: reserve enough fresh chunks for the rest
-        const int need = ((cnt - room + em.ch - 1) / em.ch) * em.ch;
-        int nb = 0;
-        if (lane == ld) {
-          nb = atomicAdd(&em.cursor[(int64_t)s * em.cs], need);
-          if (nb + need > em.seg_lim[s]) {
-            *em.err = 1;  // capacity bound violated: drop (never expected)
-            nb = -1;
-          }
-        }
-        nb = __builtin_amdgcn_readlane(nb, ld);
-        if (nb < 0) {
-          dst = rank < room ? p + rank : -1;
-          p = room ? p + room : 0;
-        } else {
-          dst = rank < room ? p + rank : nb + (rank - room);
-          p = nb + (cnt - room);
-        }
-      } else {
-        p += cnt;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (k == j) vst[k] = lane == sl ? p : vst[k];
-      if (slot == s && dst >= 0) em.rec[dst] = rc;
-      pend &= ~m;
-    }
-  };
   // one row: park its bins words in this thread's LDS column (no barrier), move every tree's code
-  auto move_row = [&](int64_t r, const uint64_t (&w)[MAXG], const uint32_t (&cc)[kP7TB], float y, bool live) {
+  auto move_row = [&](int64_t r, const uint64_t (&w)[MAXG], const uint32_t (&cc)[kP7TB], bool live) {
     uint32_t c[kP7TB];
 #pragma unroll
     for (int u = 0; u < kP7TB; ++u) c[u] = cc[u] & 0xFFFFu;
@@ -963,12 +887,6 @@ __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __re
 #pragma unroll
       for (int g = 0; g < MAXG; ++g)
         if (g < G) tile7[g * 256 + lr] = w[g];
-    }
-    uint64_t rq = 0;
-    if (EMIT) {
-      int q1 = (int)rintf(y * em.qs1);
-      q1 = q1 > (1 << 23) ? (1 << 23) : (q1 < -(1 << 23) ? -(1 << 23) : q1);
-      rq = (uint64_t)r | ((uint64_t)(uint32_t)(q1 + (1 << 23)) << 39);
     }
     for (int t0 = 0; t0 < T; t0 += kP7TB) {
       if (t0 > 0 && live) {
@@ -979,7 +897,6 @@ __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __re
       for (int u = 0; u < kP7TB; ++u) {
         if (t0 + u >= T) break;  // uniform
         const uint32_t loc = c[u] & 0xFFu;
-        int slot = -1;
         if (live && loc != 0xFFu) {
           const int id = s_tf[t0 + u] + (int)loc;
           if (CDNA_DCHECK(id >= 0 && id < A, 0x9701u)) {  // code's local node outside the level
@@ -991,54 +908,38 @@ __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __re
               const bool left = fb < 0 ? ((cat_mask[((fb >> 16) & 0x7FFF) * 8 + (bin >> 5)] >> (bin & 31)) & 1u) != 0u
                                        : bin <= ((fb >> 16) & 0xFF);
               nl = s_ch[2 * id + (left ? 0 : 1)];
-              if (EMIT && nl != 0xFFu && (c[u] >> 8) != 0u) slot = s_cs[2 * id + (left ? 0 : 1)];
             }
             codes[(int64_t)(t0 + u) * n + r] = (uint16_t)((c[u] & 0xFF00u) | nl);
           }
         }
-        if (EMIT) emit(slot, rq | ((uint64_t)(c[u] >> 8) << 31));
       }
     }
   };
-  auto load_row = [&](int64_t r, uint64_t (&w)[MAXG], uint32_t (&cc)[kP7TB], float& y) {
+  auto load_row = [&](int64_t r, uint64_t (&w)[MAXG], uint32_t (&cc)[kP7TB]) {
 #pragma unroll
     for (int g = 0; g < MAXG; ++g)
       if (g < G) w[g] = bins[(int64_t)g * n + r];
 #pragma unroll
     for (int u = 0; u < kP7TB; ++u) cc[u] = u < T ? (uint32_t)codes[(int64_t)u * n + r] : 0xFFu;
-    if (EMIT) y = em.v1[r];
   };
   // software-pipelined: the next trip's bins words and codes are in flight while this row's codes move
   // (the one-stage loop waited on every trip's loads: 82 % of wave time on memory at ~3.8 TB/s, 19.6 ms per
-  // headline step; pipelined at 120 VGPRs / 4 waves per SIMD: 13.2 ms).  EMIT: the trip count is made
-  // wave-uniform (lanes past n run the trip with live = false), so every emit ballot sees the whole wave.
+  // headline step; pipelined at 120 VGPRs / 4 waves per SIMD: 13.2 ms).
   int64_t r = (int64_t)blockIdx.x * 256 + lr;
   uint64_t w[MAXG];
   uint32_t cc[kP7TB];
-  float y = 0.f;
-  if (r < n) load_row(r, w, cc, y);
+  if (r < n) load_row(r, w, cc);
   const int64_t rw = r - lane;  // the wave's first row this trip
   for (int64_t rb = rw; rb < n; rb += stride, r += stride) {
     uint64_t wn[MAXG];
     uint32_t cn[kP7TB];
-    float yn = 0.f;
     const int64_t rn = r + stride;
-    if (rn < n) load_row(rn, wn, cn, yn);
-    move_row(r, w, cc, y, r < n);
+    if (rn < n) load_row(rn, wn, cn);
+    move_row(r, w, cc, r < n);
 #pragma unroll
     for (int g = 0; g < MAXG; ++g) w[g] = wn[g];
 #pragma unroll
     for (int u = 0; u < kP7TB; ++u) cc[u] = cn[u];
-    y = yn;
-  }
-  if (EMIT) {  // pad this wave's open chunks (their unused tails) with zero records
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int p = vst[j];
-      const int off = p & (em.ch - 1);
-      if (64 * j + lane < em.nslots && off)
-        for (int k = off; k < em.ch; ++k) em.rec[p + (k - off)] = 0ull;
-    }
   }
 }
 
@@ -1192,57 +1093,35 @@ CDNA_API int cdna_hist5(int mode, const uint64_t* bins, int64_t n, int d, int T,
   return (int)hipGetLastError();
 }
 
-// Blocks of a partition7 launch over n rows (the EMIT pad bound is one chunk per wave of it).
-static unsigned p7_grid(int64_t n, int G, bool emit) {
+// Blocks of a partition7 launch over n rows.
+static unsigned p7_grid(int64_t n, int G) {
   size_t lds = (size_t)G * 256 * 8;
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   int per_cu = 0;
-  const void* k = emit ? (G <= 8 ? reinterpret_cast<const void*>(partition7_kernel<8, true>)
-                                 : G <= 13 ? reinterpret_cast<const void*>(partition7_kernel<13, true>)
-                                           : reinterpret_cast<const void*>(partition7_kernel<16, true>))
-                       : (G <= 8 ? reinterpret_cast<const void*>(partition7_kernel<8, false>)
-                                 : G <= 13 ? reinterpret_cast<const void*>(partition7_kernel<13, false>)
-                                           : reinterpret_cast<const void*>(partition7_kernel<16, false>));
+  const void* k = G <= 8 ? reinterpret_cast<const void*>(partition7_kernel<8>)
+                          : G <= 13 ? reinterpret_cast<const void*>(partition7_kernel<13>)
+                                    : reinterpret_cast<const void*>(partition7_kernel<16>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, lds) != hipSuccess || per_cu < 1) per_cu = 2;
   // exactly the resident blocks (one round): a 4-per-CU grid with only 3 resident per CU (LDS) ran a
   // second, quarter-full round
   return grid_for(n, 256, (unsigned)(per_cu * ncu));
 }
 
-CDNA_API int cdna_partition7_waves(int64_t n, int G, int emit) {
-  if (n <= 0 || G <= 0 || G > kP7MaxG) return 0;
-  return (int)p7_grid(n, G, emit != 0) * 4;
-}
-
-// emit: null, or {cslot, v1, rec, cursor, seg_lim, err} device pointers with qs1, cs, nslots, ch (see P7Emit).
 CDNA_API int cdna_partition7(const uint64_t* bins, int64_t n, int G, int T, int A, uint16_t* codes,
                              const int* tfirst, const int* tfirst_next, const int* split_feat, const int* split_bin,
-                             const int* cat_off, const uint32_t* cat_mask, const int* child, const int* cslot,
-                             const float* v1, float qs1, uint64_t* rec, int* cursor, int cs, const int* seg_lim,
-                             int nslots, int ch, int* err, hipStream_t st) {
+                             const int* cat_off, const uint32_t* cat_mask, const int* child, hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
   if (G <= 0 || G > kP7MaxG || A > kP7MaxA || T > kP7MaxT || G * 8 > 0xFFFF) return (int)hipErrorInvalidValue;
-  const bool emit = cslot != nullptr;
-  if (emit && (!v1 || !rec || !cursor || !seg_lim || !err || nslots > kP7MaxS || nslots > 0x7FFF || ch < 1 ||
-               (ch & (ch - 1)) || cs < 1 || n >= ((int64_t)1 << 31)))
-    return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)G * 256 * 8;
-  const P7Emit em{cslot, v1, qs1, rec, cursor, cs, seg_lim, nslots, ch, err};
-  const dim3 grid(p7_grid(n, G, emit));
+  const dim3 grid(p7_grid(n, G));
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, bins, n, G, T, A, codes, tfirst, tfirst_next, split_feat,
-                       split_bin, cat_off, cat_mask, child, em);
+                       split_bin, cat_off, cat_mask, child);
   };
-  if (emit) {
-    if (G <= 8) launch(partition7_kernel<8, true>);
-    else if (G <= 13) launch(partition7_kernel<13, true>);
-    else launch(partition7_kernel<16, true>);
-  } else {
-    if (G <= 8) launch(partition7_kernel<8, false>);
-    else if (G <= 13) launch(partition7_kernel<13, false>);
-    else launch(partition7_kernel<16, false>);
-  }
+  if (G <= 8) launch(partition7_kernel<8>);
+  else if (G <= 13) launch(partition7_kernel<13>);
+  else launch(partition7_kernel<16>);
   return (int)hipGetLastError();
 }
 

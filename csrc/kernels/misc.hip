@@ -452,16 +452,11 @@ CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_
   // interior quads as dword stores when every tree row starts 4-byte aligned
   const int packed = (offset % 4 == 0) && (n % 4 == 0) &&
                      (codes ? reinterpret_cast<uintptr_t>(codes) % 8 == 0 : reinterpret_cast<uintptr_t>(out) % 4 == 0);
-  // CDNAML_POISSON_BLOCKS > 0 bounds the grid (blocks over all trees): beside other kernels a full-chip grid
-  // keeps a co-running kernel of 1024-thread blocks (the quantile sort) waiting for whole CUs to drain.
-  // Default unbounded: the engine queues the draws in series, where T x 1024 blocks measured 2.24 ms vs 2.64 ms
+  // grid_blocks > 0 bounds the grid (blocks over all trees; the caller's bound for draws queued beside the fit's
+  // prologue on a side stream: a full-chip grid keeps a co-running kernel of 1024-thread blocks -- the quantile
+  // sort -- waiting for whole CUs to drain).  Unbounded in series: T x 1024 blocks measured 2.24 ms vs 2.64 ms
   // for 2048 blocks at 1e8 rows x 20 trees (profiles/r4/prologue_ab.md).
-  // grid_blocks > 0: the caller's bound (draws queued beside the fit's prologue on a side stream)
-  static const int env_blocks = [] {
-    const char* e = getenv("CDNAML_POISSON_BLOCKS");
-    return e ? atoi(e) : 0;
-  }();
-  const int max_blocks = grid_blocks > 0 ? grid_blocks : env_blocks;
+  const int max_blocks = grid_blocks;
   unsigned gx = grid_for(n / 4 + 2, 256, 1024);
   if (max_blocks > 0) {
     const unsigned cap = (unsigned)((max_blocks + T - 1) / T);

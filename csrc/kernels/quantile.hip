@@ -179,11 +179,7 @@ CDNA_API int cdna_quantile_thresholds(const double* samp, int s, int d, int max_
   if (s > kQMaxS || max_bins < 2 || max_bins > 257) return (int)hipErrorInvalidValue;
   int P = 1;
   while (P < s) P <<= 1;
-  static const bool radix_on = [] {
-    const char* e = getenv("CDNAML_QUANTILE_RADIX");
-    return !e || atoi(e) != 0;
-  }();
-  const bool radix = radix_on && s <= kQRadixS;
+  const bool radix = s <= kQRadixS;
   size_t lds = (size_t)P * sizeof(double);
   if (radix && lds < sizeof(typename QRadixSort::storage_type)) lds = sizeof(typename QRadixSort::storage_type);
   auto launch = [&](auto kern) {

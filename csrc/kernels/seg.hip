@@ -40,10 +40,6 @@ struct SegHistArgs {
   // optional packed item records (flat kernel, REC): row | weight << 31 | (q1 + 2^23) << 39 (see CompactWArgs)
   const uint64_t* rec = nullptr;
   int rs = 0;  // row stride of the row-major bins in 8-byte words (0: G); 16 = one 128-byte line per row
-  // optional per-slot record ends (records emitted by the partition, hist5.hip partition7 EMIT): a work item's
-  // length is clipped to seg_end[slot * seg_end_stride] - start (work lists are cut from segment capacities)
-  const int* seg_end = nullptr;
-  int seg_end_stride = 0;
 };
 
 // PACKED: one u64 atomic per update (count << 44 | sum of w * (q + 2^23)); the
@@ -539,13 +535,8 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_kernel(const SegHistArgs
   constexpr int PLANE = BP * 32;  // u64 cells per feature plane j
   __shared__ __attribute__((aligned(16))) unsigned long long h[10 * PLANE];  // [10][BP][32]
   const int start = a.work[3 * blockIdx.x], slot = a.work[3 * blockIdx.x + 2];
-  int len = a.work[3 * blockIdx.x + 1];
+  const int len = a.work[3 * blockIdx.x + 1];
   if (!CDNA_DCHECK(start >= 0 && len >= 0 && slot >= 0, 0x5E83u)) return;  // corrupt work item
-  if (a.seg_end) {  // block-uniform: past the slot's emitted records (capacity chunk) -> nothing to do
-    const int e = a.seg_end[(int64_t)slot * a.seg_end_stride] - start;
-    len = len < e ? len : e;
-    if (len <= 0) return;
-  }
   for (int i = threadIdx.x; i < 10 * PLANE; i += TH) h[i] = 0ull;
   __syncthreads();
   const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
@@ -814,71 +805,6 @@ __global__ __launch_bounds__(1024) void seg_hist_lane4_kernel(const SegHistArgs 
     const unsigned long long cnt = v >> kPackShift;
     const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
     unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
-    atomicAdd(o, cnt);
-    atomicAdd(o + 1, (unsigned long long)sum);
-  }
-}
-
-// Feature-subset variant (RandomForest featureSubsetStrategy): a node's split
-// only considers its m sampled features (ML 07 / Spark "onethird" = 34 of 100),
-// so only those are accumulated.  Lanes take consecutive (row, sampled feature)
-// PAIRS: one byte gather from the row-major bins and one packed atomic per
-// lane, every lane busy.  Both children of a split are built (no sibling
-// subtraction: the parent's histogram only holds the parent's features); at
-// m = 34 that is 2 x 34 = 68 atomics per parent row instead of 104 for the
-// smaller child alone, and 34 instead of 104 at the root.
-template <bool HAS_W>
-__global__ __launch_bounds__(1024) void seg_hist_subset_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins_rm,
-                                                               int row_bytes, const int* __restrict__ feats, int m) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long h[];  // [m][B]
-  constexpr int TH = 1024;
-  int* s_f = reinterpret_cast<int*>(h + (size_t)m * a.B);
-  const int start = a.work[3 * blockIdx.x], len = a.work[3 * blockIdx.x + 1], slot = a.work[3 * blockIdx.x + 2];
-  const int plane = m * a.B;
-  for (int i = threadIdx.x; i < plane; i += TH) h[i] = 0ull;
-  for (int i = threadIdx.x; i < m; i += TH) s_f[i] = feats[(int64_t)slot * m + i];
-  __syncthreads();
-  const uint32_t total = (uint32_t)len * (uint32_t)m;
-  const int mi = m;
-  const float inv_m = 1.0f / (float)m;
-  // 16 pairs in flight per lane: each pair is a dependent perm -> byte-gather chain, so a few pairs per
-  // trip left the waves waiting on memory (U = 4 ran 5x slower than the flat kernel)
-  constexpr int U = 16;
-  for (uint32_t q0 = threadIdx.x; q0 < total; q0 += TH * U) {
-    int cell[U];
-    unsigned long long add[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t q = q0 + u * TH;
-      const bool ok = q < total;
-      // q < 2^24 (host-bounded chunk x m): float quotient, one correction step
-      int i = (int)((float)q * inv_m);
-      int fi = (int)q - i * mi;
-      if (fi < 0) { --i; fi += mi; }
-      if (fi >= mi) { ++i; fi -= mi; }
-      if (!ok) { i = 0; fi = 0; }
-      const int row = ok ? a.perm[start + i] : 0;
-      const int f = s_f[fi];
-      const int bin = ok ? (int)bins_rm[(int64_t)row * row_bytes + f] : 0;
-      const uint32_t w = ok ? (HAS_W ? (uint32_t)a.wp[start + i] : 1u) : 0u;
-      int q1 = ok ? (int)rintf(a.v1p[start + i] * a.qs1) : 0;
-      q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
-      add[u] = ((unsigned long long)w << kPackShift) + (unsigned long long)w * (unsigned long long)(q1 + kPackQ);
-      cell[u] = fi * a.B + bin;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (add[u]) atomicAdd(h + cell[u], add[u]);
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < plane; c += TH) {
-    const int fi = c / a.B, bn = c - fi * a.B;
-    const unsigned long long v = h[c];
-    if (!v) continue;
-    const int f = s_f[fi];
-    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
-    const unsigned long long cnt = v >> kPackShift;
-    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
     atomicAdd(o, cnt);
     atomicAdd(o + 1, (unsigned long long)sum);
   }
@@ -1579,18 +1505,14 @@ CDNA_API int cdna_seg_hist_root(const uint8_t* bins_s10, int64_t n, int d, int B
 // bit2: bins are row-major [n][G] words (seg_hist_flat_kernel when packed and all groups fit 128 KB of LDS,
 // else seg_hist_rm_kernel); bit3: force seg_hist_rm_kernel.
 // work: [nwork][3] {start, len, slot}; grid = nwork x ceil(d / 8).
-// seg_end (optional, seg10 record histograms only): per-slot record ends [slot * seg_end_stride].
 CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int B, const int* perm, const float* v0p,
                            const float* v1p, const uint8_t* wp, const int* work, int nwork, float qs0, float qs1,
-                           unsigned long long* out, int rm_stride, const int* seg_end, int seg_end_stride,
+                           unsigned long long* out, int rm_stride,
                            hipStream_t st) {
   if (nwork <= 0) return 0;
   if (rm_stride != 0 && rm_stride < (d + 7) / 8) return (int)hipErrorInvalidValue;
-  if (seg_end && (!(mode & 256) || seg_end_stride < 1)) return (int)hipErrorInvalidValue;
   SegHistArgs a{bins, n, d, B, perm, v0p, v1p, wp, work, qs0, qs1, out};
   a.rs = rm_stride;
-  a.seg_end = seg_end;
-  a.seg_end_stride = seg_end_stride;
   const bool packed = (mode & 1) != 0, has_w = (mode & 2) != 0;
   if ((mode & 128) && (mode & 16) && (mode & 4) && packed) {
     // lane-feature kernel: 128 features per block (4 byte planes of BP >= B bins x 32 lanes, BP KB of LDS);
@@ -1604,14 +1526,8 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
       // bins rows in the seg10 layout (binize v5 with Gs = -10): six items per wave
       if (d > 100 || B > 40 || row_bytes != 128) return (int)hipErrorInvalidValue;
       auto launch10 = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), 0, st, a, b8); };
-      static const int u10 = [] { const char* e = getenv("CDNAML_LANE10_U"); return e ? atoi(e) : 16; }();
-      if (u10 == 8) {
-        if (B <= 32) launch10(seg_hist_lane10_kernel<32, 8>);
-        else launch10(seg_hist_lane10_kernel<40, 8>);
-      } else {
-        if (B <= 32) launch10(seg_hist_lane10_kernel<32, 16>);
-        else launch10(seg_hist_lane10_kernel<40, 16>);
-      }
+      if (B <= 32) launch10(seg_hist_lane10_kernel<32, 16>);
+      else launch10(seg_hist_lane10_kernel<40, 16>);
       return (int)hipGetLastError();
     }
     if (B > 80) {
@@ -1626,18 +1542,14 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
     }
     const dim3 grid((unsigned)nwork, (unsigned)((d + 127) / 128));
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(512), 0, st, a, b8, row_bytes); };
-    static const bool lane8 = [] { const char* e = getenv("CDNAML_SEG_LANE8"); return !(e && atoi(e) == 0); }();
-    if (lane8 && B <= 64) {
+    if (B <= 64) {
       auto launch8 = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(1024), 0, st, a, b8, row_bytes); };
       if (B <= 32) launch8(seg_hist_lane8_kernel<32>);
       else if (B <= 40) launch8(seg_hist_lane8_kernel<40>);
       else launch8(seg_hist_lane8_kernel<64>);
       return (int)hipGetLastError();
     }
-    if (B <= 32) launch(seg_hist_lane_kernel<32>);
-    else if (B <= 40) launch(seg_hist_lane_kernel<40>);
-    else if (B <= 64) launch(seg_hist_lane_kernel<64>);
-    else launch(seg_hist_lane_kernel<80>);
+    launch(seg_hist_lane_kernel<80>);  // 64 < B <= 80 (B <= 64: the quarter-wave lane8 kernel above)
     return (int)hipGetLastError();
   }
   if ((mode & 16) && !((mode & 4) && packed && (size_t)8 * B * 8 <= 128 * 1024 && !(mode & 8)))
@@ -1842,27 +1754,6 @@ CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64
     case 16: go(codes_count_w_kernel<16>, codes_scatter_w_kernel<16>); break;
     default: return (int)hipErrorInvalidValue;
   }
-  return (int)hipGetLastError();
-}
-
-// Packed (count | sum) segment histograms over each slot's m sampled features only.
-// feats [S][m] (slot-major feature ids); bins_rm row-major [n][row_bytes]; out [S][d][B][2] zeroed.
-CDNA_API int cdna_seg_hist_subset(const uint8_t* bins_rm, int64_t n, int row_bytes, int d, int B, const int* perm,
-                                  const float* v1p, const uint8_t* wp, const int* work, int nwork, float qs1,
-                                  const int* feats, int m, unsigned long long* out, hipStream_t st) {
-  if (nwork <= 0) return 0;
-  if (m <= 0 || m > d) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)m * B * 8 + (size_t)m * 4;
-  if (lds > 128 * 1024) return (int)hipErrorInvalidValue;
-  SegHistArgs a{nullptr, n, d, B, perm, nullptr, v1p, wp, work, 1.f, qs1, out};
-  auto launch = [&](auto kern) {
-    if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), lds, st, a, bins_rm, row_bytes, feats, m);
-  };
-  if (wp) launch(seg_hist_subset_kernel<true>);
-  else launch(seg_hist_subset_kernel<false>);
   return (int)hipGetLastError();
 }
 

@@ -222,111 +222,6 @@ CDNA_API int cdna_hist_assemble(const void* Hb, int raw, double scale0, double s
 }
 
 // ---------------------------------------------------------------------------
-// K6 over compact feature-subset histograms (subhist.hip): H [A][m][B][2] exact
-// int64 (count, sum w q * s1) of each node's m sampled features feats [A][m]
-// (ascending).  Same variance gain, legality and tie order (lowest f * B + b)
-// as split_scan_kernel on the full [A][d][B][2] fp64 histogram: the fp64
-// values are the same exact integers over a power-of-two scale, so every sum
-// below is exact and the decisions and child statistics are bit-identical.
-// Node totals: the first sampled feature (every feature's bins hold the same
-// total weight).  No hist_assemble pass: the int64 sums are read directly.
-// ---------------------------------------------------------------------------
-namespace {
-struct SplitSubArgs {
-  const long long* H;
-  const uint8_t* feats;
-  const int* nthr;
-  int A, m, B;
-  double scale1;
-  double min_inst;
-  double* out;
-  double* tot_out;
-};
-
-__global__ __launch_bounds__(kThreads) void split_scan_sub_kernel(const SplitSubArgs a) {
-  __shared__ double s_g[kThreads];
-  __shared__ int s_k[kThreads];
-  const int node = blockIdx.x;
-  const long long* Hn = a.H + (int64_t)node * a.m * a.B * 2;
-  const uint8_t* fl = a.feats + (int64_t)node * a.m;
-  double t0 = 0.0, t1 = 0.0;
-  for (int b = 0; b < a.B; ++b) {  // every thread: the node totals from sampled feature 0
-    t0 += (double)Hn[2 * b];
-    t1 += (double)Hn[2 * b + 1] / a.scale1;
-  }
-  double best = -__builtin_inf();
-  int bk = 0x7FFFFFFF;
-  SplitArgs g{};
-  g.kind = 0;
-  g.min_inst = a.min_inst;
-  for (int k = threadIdx.x; k < a.m; k += kThreads) {
-    const int f = fl[k];
-    const int lim = a.nthr[f] < 0 ? 0 : a.nthr[f];
-    const long long* hf = Hn + (int64_t)k * a.B * 2;
-    double l0 = 0.0, l1 = 0.0;
-    for (int b = 0; b < a.B && b < lim; ++b) {
-      l0 += (double)hf[2 * b];
-      l1 += (double)hf[2 * b + 1] / a.scale1;
-      bool ok;
-      const double gn = gain_of(g, l0, l1, t0 - l0, t1 - l1, t0, t1, &ok);
-      if (ok && gn == gn && gn != __builtin_inf() && gn != -__builtin_inf() && gn > best) {
-        best = gn;
-        bk = f * a.B + b;
-      }
-    }
-  }
-  s_g[threadIdx.x] = best;
-  s_k[threadIdx.x] = bk;
-  __syncthreads();
-  for (int o = kThreads / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      const int j = threadIdx.x + o;
-      if (s_g[j] > s_g[threadIdx.x] || (s_g[j] == s_g[threadIdx.x] && s_k[j] < s_k[threadIdx.x])) {
-        s_g[threadIdx.x] = s_g[j];
-        s_k[threadIdx.x] = s_k[j];
-      }
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    double* o = a.out + (int64_t)node * 8;
-    const int k0 = s_k[0];
-    const bool found = k0 != 0x7FFFFFFF;
-    const int f = found ? k0 / a.B : 0, b = found ? k0 - f * a.B : 0;
-    double l0 = 0.0, l1 = 0.0;
-    if (found) {
-      int kk = 0;
-      while (kk < a.m && fl[kk] != f) ++kk;
-      const long long* hf = Hn + (int64_t)kk * a.B * 2;
-      for (int q = 0; q <= b; ++q) {
-        l0 += (double)hf[2 * q];
-        l1 += (double)hf[2 * q + 1] / a.scale1;
-      }
-    }
-    o[0] = found ? s_g[0] : -__builtin_inf();
-    o[1] = f;
-    o[2] = b;
-    o[3] = l0;
-    o[4] = l1;
-    o[5] = t0 - l0;
-    o[6] = t1 - l1;
-    o[7] = 0.0;
-    a.tot_out[node * 2] = t0;
-    a.tot_out[node * 2 + 1] = t1;
-  }
-}
-}  // namespace
-
-CDNA_API int cdna_split_scan_sub(const long long* H, const uint8_t* feats, const int* nthr, int A, int m, int B,
-                                 double scale1, double min_inst, double* out, double* tot_out, hipStream_t st) {
-  if (A <= 0) return 0;
-  if (m <= 0 || B <= 0 || m > 255 || !(scale1 > 0.0)) return (int)hipErrorInvalidValue;
-  SplitSubArgs a{H, feats, nthr, A, m, B, scale1, min_inst, out, tot_out};
-  hipLaunchKernelGGL(split_scan_sub_kernel, dim3((unsigned)A), dim3(kThreads), 0, st, a);
-  return (int)hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // K6 for classification (Gini / entropy on class counts) and for categorical
 // features (regression or classification), one block per node -- the torch
 // formulation these replace (cdnaml/models/tree/engine.py _best_splits) ran a
@@ -723,93 +618,5 @@ CDNA_API int cdna_split_decode(const double* so, int sw, const double* tot, int 
   hipLaunchKernelGGL(split_decode_kernel, dim3(1), dim3(1024), 0, st, so, sw, tot, tw, a_tree, A, T, min_inst,
                      min_gain, can_level, leaf_children, missing_bin, split_feat, split_bin, cat_off, masks, child,
                      pref, tfirst_next, lv, vkind, lam, catm, nthr);
-  return (int)hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------------- emit_plan
-// The next level's histogram slots and record segments, on the device, right behind split_decode: the row
-// partition then writes each built child's item records itself (partition7 EMIT, hist5.hip) instead of a
-// codes_count_w + codes_scatter_w pass over the new codes.  The host derives the same plan from the same
-// decisions (engine.py: smaller active sibling built, ties to the left child; a lone active child built).
-//   built(2a + s) = child active && (sibling inactive || W_s < W_other || (W_s == W_other && s == 0))
-//   cslot[2a + s] = exclusive count of built children before it (-1: not built)
-//   seg_start[slot] = exclusive prefix of cap = roundup(W, CH) + padb (records <= W: every record weighs >= 1;
-//                     padb bounds the zero-padded tail chunks, one per partition wave)
-//   seg_lim[slot] = seg_start + cap;  cursor[slot * cs] = seg_start (atomic chunk cursors, one per 128-B line)
-namespace {
-
-__global__ __launch_bounds__(1024) void emit_plan_kernel(const double* __restrict__ so, int sw, const int* __restrict__ child,
-                                                         int A, int ch, int64_t padb, int* __restrict__ cslot,
-                                                         int* __restrict__ seg_start, int* __restrict__ seg_lim,
-                                                         int* __restrict__ cursor, int cs, int* __restrict__ nslots) {
-  __shared__ int s_wave[16];
-  __shared__ int64_t s_cap[1024];
-  __shared__ int s_carry;
-  __shared__ int64_t s_ccap;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) {
-    s_carry = 0;
-    s_ccap = 0;
-  }
-  __syncthreads();
-  for (int base = 0; base < 2 * A; base += 1024) {
-    const int e = base + threadIdx.x;
-    int flag = 0;
-    int64_t cap = 0;
-    if (e < 2 * A) {
-      const int a = e >> 1, s = e & 1;
-      const int me = child[e], other = child[e ^ 1];
-      const double wm = so[(int64_t)a * sw + (s == 0 ? 3 : 5)], wo = so[(int64_t)a * sw + (s == 0 ? 5 : 3)];
-      flag = me >= 0 && (other < 0 || wm < wo || (wm == wo && s == 0)) ? 1 : 0;
-      if (flag) cap = ((((int64_t)wm + ch - 1) / ch) * ch) + padb;
-    }
-    const uint64_t m = __builtin_amdgcn_ballot_w64(flag != 0);
-    const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (lane == 0) s_wave[wid] = __builtin_popcountll(m);
-    // inclusive scan of the capacities (Hillis-Steele over the block)
-    s_cap[threadIdx.x] = cap;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-      const int64_t v = threadIdx.x >= o ? s_cap[threadIdx.x - o] : 0;
-      __syncthreads();
-      s_cap[threadIdx.x] += v;
-      __syncthreads();
-    }
-    int before = 0, total = 0;
-    for (int w = 0; w < 16; ++w) {
-      before += w < wid ? s_wave[w] : 0;
-      total += s_wave[w];
-    }
-    if (e < 2 * A) {
-      const int slot = s_carry + before + below;
-      cslot[e] = flag ? slot : -1;
-      if (flag) {
-        const int64_t st = s_ccap + s_cap[threadIdx.x] - cap;
-        seg_start[slot] = (int)st;
-        seg_lim[slot] = (int)(st + cap);
-        cursor[(int64_t)slot * cs] = (int)st;
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      s_carry += total;
-      s_ccap += s_cap[1023];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *nslots = s_carry;
-}
-
-}  // namespace
-
-// so [A][sw] K6 decisions (left / right weights at columns 3 / 5), child [2A] from split_decode; outputs sized
-// 2A (cslot) and 2A (seg_start, seg_lim; the first nslots used), cursor [2A * cs].  The host bounds the total
-// capacity below 2^31.
-CDNA_API int cdna_emit_plan(const double* so, int sw, const int* child, int A, int ch, int64_t padb, int* cslot,
-                            int* seg_start, int* seg_lim, int* cursor, int cs, int* nslots, hipStream_t st) {
-  if (A <= 0) return 0;
-  if (sw < 7 || ch < 1 || (ch & (ch - 1)) || cs < 1 || padb < 0 || padb % ch) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(emit_plan_kernel, dim3(1), dim3(1024), 0, st, so, sw, child, A, ch, padb, cslot, seg_start,
-                     seg_lim, cursor, cs, nslots);
   return (int)hipGetLastError();
 }

@@ -898,11 +898,7 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
   if (s10 && d > 100) return (int)hipErrorInvalidValue;
   if (rm && !s10 && Gs < (d + 7) / 8) return (int)hipErrorInvalidValue;
   if (n <= 0) return 0;
-  static const bool v5_on = [] {
-    const char* e = getenv("CDNAML_BINIZE_V5");
-    return !e || atoi(e) != 0;
-  }();
-  if (v5_on && d <= 128 && (d % 4) == 0 && (ldx % 4) == 0 && (reinterpret_cast<uintptr_t>(X) % 16) == 0 &&
+  if (d <= 128 && (d % 4) == 0 && (ldx % 4) == 0 && (reinterpret_cast<uintptr_t>(X) % 16) == 0 &&
       (!rm || Gs == 16 || s10)) {
     // v5: wave = (64-row tile, 8-feature group), lanes search the same tables (broadcast LDS reads)
     int steps = 0;
@@ -939,13 +935,8 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
     // opt in to 150 KB rather than falling back to v1 (253 ms at 1e8 x 100 x 256 bins)
     const size_t budget = tb + 64 * dp * 4 <= 64 * 1024 ? 64 * 1024 : 150 * 1024;
     // 32-row tiles: 29 KB blocks, 5 per CU (measured 22.6 ms vs 25.1 ms for 64-row tiles at 1e8 x 100 x 40
-    // bins); CDNAML_BINIZE_RPT overrides
-    static const int rpt0 = [] {
-      const char* e = getenv("CDNAML_BINIZE_RPT");
-      const int v = e ? atoi(e) : 32;
-      return v >= 4 && v <= 64 ? v : 32;
-    }();
-    int rpt = rpt0;
+    // bins)
+    int rpt = 32;
     while (rpt > 4 && ((size_t)rpt * dp * 4 + tb > budget || (size_t)rpt * d > 8192)) rpt /= 2;
     if ((size_t)rpt * dp * 4 + tb <= budget) {
       int steps = 0;

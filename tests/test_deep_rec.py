@@ -38,8 +38,9 @@ def test_deep_record_histograms_equal_node_id_kernel(device, depth, trees, monke
         monkeypatch.setattr(engine.K, "node_compact", counted)
         digests = []
         try:
-            for flag in (True, False):
-                monkeypatch.setattr(engine, "DEEP_REC", flag)
+            for cap in (engine.K.NODE_COMPACT_MAX_LOC, 0):
+                # cap 0: every deep level takes the node-id histogram kernels instead of the node-id records
+                monkeypatch.setattr(engine.K, "NODE_COMPACT_MAX_LOC", cap)
                 digests.append(forest_digest(est.fit(df)._forest))
         finally:
             spark.stop()

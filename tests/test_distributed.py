@@ -123,7 +123,7 @@ def test_bench_trains_identical_forest_on_1_2_4_8_ranks(tmp_path):
     for w in (1, 2, 4, 8):
         # W = 2 and 8 build every level in slot chunks whose all-reduces overlap the next chunk
         # (_hist_overlapped; by default only for level histograms of >= 64 MiB)
-        ov = {"CDNAML_HIST_OVERLAP_MIN_BYTES": "0"} if w in (2, 8) else None
+        ov = {"CDNAML_TUNE": "HIST_OVERLAP_MIN_BYTES=0"} if w in (2, 8) else None
         res, tag = _bench(tmp_path, w, env_extra=ov)
         if ref is None:
             ref = tag

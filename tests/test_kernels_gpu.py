@@ -498,22 +498,6 @@ def test_seg_partition(dev, with_v0, weights):
         assert torch.equal(ref[3], out[3].cpu())
 
 
-@pytest.mark.parametrize("weights,B,d,m", [(True, 40, 100, 34), (False, 32, 21, 7), (True, 256, 60, 20)])
-def test_seg_hist_subset(dev, weights, B, d, m):
-    """Feature-subset segment histograms = full segment histograms restricted to each slot's features."""
-    bins, perm, v0, v1, wp, segs = _seg_state(30000, d, B, 6, 5, weights)
-    build = [0, 1, 3, 5]
-    sb = np.array([[segs[a, 0], segs[a, 1], i] for i, a in enumerate(build)])
-    rng = np.random.default_rng(4)
-    feats = np.stack([np.sort(rng.choice(d, m, replace=False)) for _ in build]).astype(np.int32)
-    ref = K.seg_hist_subset(bins, d, B, perm, v1, wp, sb, len(build), 3, feats)
-    bd = bins.to(dev)
-    out = K.seg_hist_subset(bd, d, B, perm.to(dev), v1.to(dev), None if wp is None else wp.to(dev), sb, len(build),
-                            3, feats, interleave=True).cpu()
-    assert torch.allclose(out, ref, rtol=1e-6, atol=1e-3)
-    assert float(out[0, np.setdiff1d(np.arange(d), feats[0])].abs().sum()) == 0.0
-
-
 def test_seg_partition_implicit_level0(dev):
     """Multi-tree entry: tree t's root segment is every row, weight-0 rows are dropped (stable)."""
     n, d, B, T = 30000, 12, 32, 5
