@@ -1326,25 +1326,48 @@ class ForestTrainer:
         ``weights``.
         margin: ``(F [n] fp32, eta)`` (boosting, one tree): when the level loop can, each level's row partition
         also adds ``eta * leaf value`` to F for the rows that finish there (a last partition at the deepest
-        level), so the caller needs no tree walk; ``self.margin_applied`` says whether it did."""
-        p = self.p
-        data = self.data
-        dev = self.device
-        n, d, B = data.n_local, data.d, data.B
-        T = num_trees
-        fresh = forest is None
-        forest = forest or Forest(self.C if self.classification else 1)
-        forest._heap_np = None
+        level), so the caller needs no tree walk; ``self.margin_applied`` says whether it did.
+
+        Per level (every tree of the forest at once): ``_level_tables`` (which nodes build a histogram, feature
+        masks, the level's small device tables), ``_level_histogram`` (HIP record / code / node-id histograms),
+        ``_level_reduce`` (one RCCL all-reduce or a reduce-scatter by feature), ``_level_decide`` (histogram
+        assembly + K6 split search; the device decode + partition queued behind it where it applies) and
+        ``_level_advance`` (the children, the host-side partition paths, the forest bookkeeping)."""
+        st = self._fit_paths(num_trees, stats_rows, weights, forest, codes_pre, margin)
+        self._fit_rows(st, codes_pre)
+        for depth in range(self.p.max_depth + 1):
+            if len(st.a_tree) == 0:
+                break
+            lv = self._level_tables(st, depth)
+            with _tr.span("tree.hist", depth=depth, slots=len(lv.build_ids)):
+                self._level_histogram(st, lv, depth)
+            self._level_reduce(st, lv)
+            with _tr.span("tree.split", depth=depth):
+                self._level_decide(st, lv, depth)
+            self._level_advance(st, lv, depth)
+        return self._fit_finish(st)
+
+    # ------------------------------------------------------------ fit: paths and row state
+    def _fit_paths(self, T: int, stats_rows, weights, forest, codes_pre, margin) -> "_FitState":
+        """Choose the fit's histogram / partition paths once (they hold for every level but a deep forest's switch
+        to node ids) and set up the per-fit state."""
+        p, data, dev = self.p, self.data, self.device
+        st = _FitState()
+        st.T = T
+        st.fresh = forest is None
+        st.forest = forest or Forest(self.C if self.classification else 1)
+        st.forest._heap_np = None
         # single-output forests of depth <= 8 with numeric splits: the predict heap table (Forest.heap_arrays) is
         # filled level by level here, from the keys and values the levels already hold, instead of re-walking the
         # finished forest in Python between the last split and the transform (the GPU idles through that)
-        heap = heap_v = None
-        if fresh and not self.classification and p.max_depth <= 8 and not data.categorical and not data.missing_bin:
-            heap = np.zeros((T, 2 ** (p.max_depth + 1) - 1, 2), dtype=np.int32)
-            heap[:, :, 0] = -1
-            heap_v = np.zeros((T, 2 ** (p.max_depth + 1) - 1), dtype=np.float64)  # leaf values per slot (fp64)
-        heap_depth = 0
-        need_masks = p.feature_subset is not None and p.feature_subset < d
+        st.heap = st.heap_v = None
+        if st.fresh and not self.classification and p.max_depth <= 8 and not data.categorical and \
+                not data.missing_bin:
+            st.heap = np.zeros((T, 2 ** (p.max_depth + 1) - 1, 2), dtype=np.int32)
+            st.heap[:, :, 0] = -1
+            st.heap_v = np.zeros((T, 2 ** (p.max_depth + 1) - 1), dtype=np.float64)  # leaf values per slot (fp64)
+        st.heap_depth = 0
+        st.need_masks = p.feature_subset is not None and p.feature_subset < data.d
         # several regression trees: row records for every level (one dense pass partitions all trees); before
         # each level's histogram the rows of the nodes it builds are gathered into slot segments, so the
         # histogram touches only those rows
@@ -1352,487 +1375,543 @@ class ForestTrainer:
         # sums (count, sum w * y) are (W, W1), turned into the class counts (W - W1, W1) in int64 before K6 --
         # exactly the class histograms of the node-id / codes kernels, so the forest does not change.  Forests
         # deeper than 8 levels (u16 codes hold <= 255 nodes per tree) switch to node ids at level 8
-        cls2 = self.classification and self.C == 2 and MSEG_CLS
-        deep_switch = (cls2 or (not self.classification and DEEP_REG and T > 1)) and p.max_depth > 8
-        if cls2:
+        st.cls2 = self.classification and self.C == 2 and MSEG_CLS
+        st.deep_switch = (st.cls2 or (not self.classification and DEEP_REG and T > 1)) and p.max_depth > 8
+        if st.cls2:
             stats_rows = dict(stats_rows, v1=stats_rows["label"].float())
-        mseg_ok = (USE_MSEG and USE_CODES and (T > 1 or (MSEG_T1 and stats_rows.get("v0") is None)) and
-                   (not self.classification or cls2) and (p.max_depth <= 8 or deep_switch) and
-                   T * self.n_max < 2 ** 31 and data.n_global > 0)
+        st.stats_rows = stats_rows
         # every level builds all features of the smaller child of each split; its sibling is parent - child
         # (feature subsets are applied at split time: the measured alternatives that accumulate only each node's
         # sampled features lost 2-8x, profiles/r3/subhist_ab.md, profiles/pmc_seg_hist_subset.txt)
-        use_mseg = mseg_ok
+        st.use_mseg = (USE_MSEG and USE_CODES and (T > 1 or (MSEG_T1 and stats_rows.get("v0") is None)) and
+                       (not self.classification or st.cls2) and (p.max_depth <= 8 or st.deep_switch) and
+                       T * self.n_max < 2 ** 31 and data.n_global > 0)
         # one regression tree: rows grouped by node in a permutation (segment mode)
-        use_seg = USE_SEG and T == 1 and not self.classification and not use_mseg
+        st.use_seg = USE_SEG and T == 1 and not self.classification and not st.use_mseg
         # row records (uint16 weight<<8 | local node) when every level fits 255 nodes per tree
-        use_codes = USE_CODES and (p.max_depth <= 8 or (deep_switch and use_mseg)) and not use_seg
-        if codes_pre is not None and not use_codes:
+        st.use_codes = USE_CODES and (p.max_depth <= 8 or (st.deep_switch and st.use_mseg)) and not st.use_seg
+        if codes_pre is not None and not st.use_codes:
             weights = codes_pre.weights()  # a path that reads the multiplicities themselves
+        st.weights = weights
         # margin updates by the partition need every level on the device decode + partition5 path, every row in
         # the tree (no zero weights) and leaf values the device can form (no categorical / classification)
-        margin_ok = (margin is not None and GBDT_MARGIN and use_codes and not deep_switch and T == 1 and
-                     weights is None and codes_pre is None and dev.type == "cuda" and p.impurity == "xgb" and
-                     self._device_decode_ok(dev, True, False) and self._native_split(dev) and
-                     not data.categorical and p.max_depth <= 8)
-        self.margin_applied = margin_ok
-        if use_seg:
-            w1 = None if weights is None else weights.reshape(-1)
-            wmax = int(w1.max().item()) if (w1 is not None and w1.numel()) else 1
-            perm = (torch.arange(n, dtype=torch.int32, device=dev) if w1 is None else
-                    torch.nonzero(w1 > 0).flatten().to(torch.int32))
-            pl = perm.long()
-            v1p = stats_rows["v1"].float()[pl].contiguous()
-            v0p = None if stats_rows.get("v0") is None else stats_rows["v0"].float()[pl].contiguous()
-            wp = None if (w1 is None or wmax <= 1) else w1[pl].to(torch.uint8).contiguous()
-            # scales agreed over all ranks (max |v|, max weight, global row count): the int64 fixed-point
-            # level histograms all-reduce exactly, so the tree does not depend on the GPU count
-            seg_scales = K.seg_scales(v0p, v1p, wmax, data.n_global, self.comm)
-            seg_raw = seg_scales if v0p is not None else seg_scales[1]
-            segs = np.array([[0, perm.numel()]], dtype=np.int64)
-            node = None
-        elif use_codes:
-            if codes_pre is not None:
-                codes, wmax = codes_pre.codes, codes_pre.wmax()
-            else:
-                codes, wmax = K.codes_init_max(weights, T, n, dev)
-            node = None
-            if use_mseg:
-                # one quantisation scale for every rank: the int64 level histograms then all-reduce to
-                # the same sums on 1 or N GPUs (the forest does not depend on the GPU count)
-                v0s = stats_rows.get("v0")
-                mseg_scales = (1.0, 1.0) if cls2 else \
-                    K.seg_scales(None if v0s is None else v0s.float(), stats_rows["v1"].float(), wmax,
-                                 data.n_global, self.comm)
-                mseg_raw = mseg_scales[1] if v0s is None else mseg_scales
-        else:
-            node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
-                torch.zeros((T, 0), dtype=torch.int32, device=dev)
+        st.margin = margin
+        st.margin_ok = (margin is not None and GBDT_MARGIN and st.use_codes and not st.deep_switch and T == 1 and
+                        weights is None and codes_pre is None and dev.type == "cuda" and p.impurity == "xgb" and
+                        self._device_decode_ok(dev, True, False) and self._native_split(dev) and
+                        not data.categorical and p.max_depth <= 8)
+        self.margin_applied = st.margin_ok
+        # packed 8-byte item records (row | weight | quantised label) for the segment histograms
+        st.rec_ok = MSEG_REC and stats_rows.get("v0") is None and 8 * data.B * 8 <= 128 * 1024
         # the level's active nodes as a struct of arrays (host): tree, forest id, heap key, stats [A, k],
         # sibling / parent positions (-1 = none).  The per-level host work between the split decisions'
         # device->host copy and the next level's launches is a few vectorised numpy ops, not a per-node
         # Python loop (that loop idled the GPU for 0.2-2.5 ms per level at 20 trees x 2^L nodes)
-        a_tree = np.arange(T, dtype=np.int32)
-        a_fid = np.full(T, -1, dtype=np.int64)
-        a_key = np.ones(T, dtype=np.uint64)
-        a_stats = np.zeros((T, 0))
-        a_sib = np.full(T, -1, dtype=np.int64)
-        a_parent = np.full(T, -1, dtype=np.int64)
-        prev_hist = None  # [A_prev, d, B, k] histograms of last level's split nodes
-        rs_on = False     # this pass reduce-scatters its level histograms by feature (RS_MIN_BYTES)
-        root_ids = [None] * T
-        deep_rec = False  # set at the switch to node ids (deep_switch)
-        wdeep = None
-        pending = []  # deferred forest bookkeeping of the previous level (see flush points)
+        st.a_tree = np.arange(T, dtype=np.int32)
+        st.a_fid = np.full(T, -1, dtype=np.int64)
+        st.a_key = np.ones(T, dtype=np.uint64)
+        st.a_stats = np.zeros((T, 0))
+        st.a_sib = np.full(T, -1, dtype=np.int64)
+        st.a_parent = np.full(T, -1, dtype=np.int64)
+        st.prev_hist = None  # [A_prev, d, B, k] histograms of last level's split nodes
+        st.rs_on = False     # this pass reduce-scatters its level histograms by feature (RS_MIN_BYTES)
+        st.root_ids = [None] * T
+        st.deep_rec = False  # set at the switch to node ids (deep_switch)
+        st.wdeep = None
+        st.node_count = st.forest.num_nodes
+        return st
 
-        def flush():
-            while pending:
-                pending.pop(0)()
-        node_count = forest.num_nodes
-        for depth in range(p.max_depth + 1):
-            A = len(a_tree)
-            if A == 0:
-                break
-            # ---- decide which active nodes get a histogram built
-            build = np.ones(A, dtype=bool)
-            if depth > 0:
-                build = _built_nodes(self._weights_v(a_stats), a_sib, a_parent)
-            build_ids = np.nonzero(build)[0]
-            slot_of = np.full(A, -1, dtype=np.int32)
-            slot_of[build_ids] = np.arange(len(build_ids), dtype=np.int32)
-            slot_tree = a_tree[build_ids]
-            masks_np = None
-            masks_dev = None  # the same words drawn on the GPU (no host consumer this level)
-            mask_base = None
-            if need_masks:
-                tid = a_tree if p.tree_ids is None else np.asarray(p.tree_ids, dtype=np.int64)[a_tree]
-                if MASKS_DEV and dev.type == "cuda" and \
-                        d <= K.FEATURE_MASKS_MAX_D and p.feature_subset is not None and 0 < p.feature_subset < d:
-                    mask_base = self._mask_base(tid.astype(np.uint64), a_key)
-                else:
-                    masks_np = self._feature_masks(tid.astype(np.uint64), a_key)
-            id_tree = a_tree
-            tfirst = torch.from_numpy(np.searchsorted(id_tree, np.arange(T), side="left").astype(np.int32))
-            # the level's small device tables in ONE host->device copy (each separate copy was a blit kernel plus a
-            # launch gap): hist_assemble's (slot, parent, sibling), the decode's a_tree / tfirst, the mask bases
-            lvl = None
-            if dev.type == "cuda":
-                lvl = K.upload(dev, K.assemble_table(slot_of, a_parent, a_sib), a_tree.astype(np.int32),
-                               tfirst.numpy().astype(np.int32),
-                               *([mask_base.view(np.int64)] if mask_base is not None else []))
-                if mask_base is not None:
-                    masks_dev = K.feature_masks(mask_base, d, p.feature_subset, dev, base_dev=lvl[3])
-            hist_raw_scale = None
-            reduced = False
-            rec_ok = (MSEG_REC and stats_rows.get("v0") is None and 8 * B * 8 <= 128 * 1024)
-            # levels with <= 1 built node per tree (0: the roots, 1: the smaller children) on seg10 rows: the
-            # records are compacted inside the histogram kernel (no codes_compact pass)
-            root_rows = None  # seg10 rows (B <= 40) or standard row-major rows (boosting, 80 < B <= 256)
-            if dev.type == "cuda" and ROOT_HIST:
-                if data.bins_s10 is not None and d <= 100 and B <= 40:
-                    root_rows = data.bins_s10
-                elif 80 < B <= 256 and data.bins_rm is not None:
-                    root_rows = data.bins_rm
-            root_ok = (root_rows is not None and use_mseg and (depth >= 1 or MSEG_L0) and rec_ok and
-                       len(build_ids) > 0 and np.bincount(slot_tree, minlength=T).max() <= 1)
-            with _tr.span("tree.hist", depth=depth, slots=len(build_ids)):
-                if root_ok:
-                    S_b = len(build_ids)
-                    sl_node = build_ids - tfirst.numpy()[slot_tree]  # the slot's local node in its tree's codes
-                    # one launch for every slot, then the level's one all-reduce: these levels hold one node per
-                    # tree (20 x 100 x 40 cells = 1.3 MB at the headline), too little to overlap, and slot chunks
-                    # of a 1.25e7-row shard would launch ~1 round of blocks each (half of it idle)
-                    Hb = K.seg_hist_codes(root_rows, d, B, codes, stats_rows["v1"], mseg_scales[1], wmax,
-                                          slot_tree, sl_node, 0, S_b,
-                                          torch.zeros((S_b, d, B, 2), dtype=torch.int64, device=dev))
-                    hist_raw_scale = mseg_raw
-                elif use_mseg and (depth >= 1 or MSEG_L0):
-                    # gather the rows of the built nodes into slot segments, then segment histograms of packed
-                    # item records on every device (the CPU emulates the HIP compaction + flat histogram
-                    # exactly, so gloo ranks traverse the integer path RCCL ranks take)
-                    perm, v0p, v1p, wp, sg = K.codes_compact(codes, tfirst, slot_of, len(build_ids),
-                                                             stats_rows.get("v0"), stats_rows["v1"],
-                                                             rec_scale=mseg_scales[1] if rec_ok else None)
-                    is_rec = rec_ok and v1p is None
-                    sb = np.concatenate([sg, np.arange(len(build_ids), dtype=np.int64)[:, None]], 1)
-                    if is_rec and (self.comm.distributed or HIST_OVERLAP_FORCE) and HIST_OVERLAP > 1 and \
-                            len(build_ids) >= 2 and \
-                            len(build_ids) * d * B * 16 >= HIST_OVERLAP_MIN_BYTES and \
-                            not self._rs_level(len(build_ids) * d * B * 16, rs_on):
-                        # (never once the pass reduce-scatters: the overlapped chunks are all-reduced over all
-                        # features, while prev_hist then holds only this rank's feature slice)
-                        # comm/compute overlap: the level's slots are built in chunks, each chunk's int64
-                        # histogram all-reduced (async, RCCL stream) while the next chunk is built
-                        Hb = self._hist_overlapped(data, d, B, perm, sb, len(build_ids), wmax, mseg_scales, dev)
-                        hist_raw_scale = mseg_raw
-                        reduced = True
-                    else:
-                        rm, s10 = (data.record_rows() if is_rec else (data.row_major_bins(), False)) \
-                            if dev.type == "cuda" else (None, False)
-                        Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax,
-                                        mseg_scales, bins_rm=rm, interleave=True, rec=is_rec, raw=True, rm_s10=s10)
-                        hist_raw_scale = mseg_raw
-                    del perm, v0p, v1p, wp
-                elif deep_rec and len(build_ids) and \
-                        np.bincount(a_tree, minlength=T).max() <= K.NODE_COMPACT_MAX_LOC:
-                    # levels below the u16 codes (binary classification deeper than 8): the built rows' packed
-                    # records from the node ids, then the same record histograms as the shallow levels (the
-                    # node-id kernel re-read every row once per LDS-sized slot group: ~290 ms per level at
-                    # 1e7 rows x 100 trees)
-                    perm, sg = K.node_compact(node, wdeep, tfirst.numpy(), slot_of, len(build_ids),
-                                              stats_rows["v1"], mseg_scales[1])
-                    sb = np.concatenate([sg, np.arange(len(build_ids), dtype=np.int64)[:, None]], 1)
-                    rm, s10 = data.record_rows() if dev.type == "cuda" else (None, False)
-                    Hb = K.seg_hist(data.bins, d, B, perm, None, None, None, sb, len(build_ids), wmax,
-                                    mseg_scales, bins_rm=rm, interleave=True, rec=True, raw=True, rm_s10=s10)
-                    hist_raw_scale = mseg_raw
-                    del perm
-                elif use_seg:
-                    sb = np.stack([segs[build_ids, 0], segs[build_ids, 1], slot_of[build_ids].astype(np.int64)], 1)
-                    Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, len(build_ids), wmax, seg_scales,
-                                    # sparse node segments (>= 4 built nodes) gather whole rows from the
-                                    # row-major copy; dense shallow levels stream the [G][n] layout
-                                    bins_rm=data.row_major_bins() if (K.SEG_ROW_MAJOR and dev.type == "cuda"
-                                                                      and len(build_ids) >= 4) else None,
-                                    interleave=use_mseg, raw=True)
-                    hist_raw_scale = seg_raw
-                elif use_codes:
-                    Hb = K.hist_codes(1 if self.classification else 0, data.bins, d, codes, tfirst,
-                                      stats_rows.get("v0"), stats_rows.get("v1"), stats_rows.get("label"), self.C,
-                                      K.upload(dev, slot_of)[0], slot_tree, id_tree, None, B, wmax=wmax)
-                elif self.classification:
-                    Hb = K.hist_classes(data.bins, d, node, weights, stats_rows["label"], self.C,
-                                        K.upload(dev, slot_of)[0],
-                                        slot_tree, None, B, id_tree=id_tree)
-                else:
-                    Hb = K.hist_moments(data.bins, d, node, weights, stats_rows.get("v0"), stats_rows["v1"],
-                                        K.upload(dev, slot_of)[0], slot_tree, None, B, id_tree=id_tree)
-            if cls2 and hist_raw_scale is not None:
-                Hb[..., 0] -= Hb[..., 1]  # packed (W, W1) -> class counts (W0, W1), exact int64
-            rs_slice = None
-            if not reduced and self._rs_want(Hb, rs_on):
-                rs_on = True
-                rs_slice, Hb = self._reduce_scatter_features(Hb, d)
-                if prev_hist is not None and prev_hist.shape[1] == d:
-                    prev_hist = prev_hist[:, rs_slice[0]:rs_slice[1]].contiguous()
-            elif not reduced:
-                with _tr.span("tree.allreduce", cat="comm", bytes=Hb.numel() * 8):
-                    self.comm.all_reduce(Hb)  # one fused RCCL all-reduce per level
-            _split_span = _tr.span("tree.split", depth=depth)
-            _split_span.__enter__()
-            # ---- assemble every active node's histogram
-            derived = np.nonzero(~build)[0]
-            is_raw = Hb.dtype == torch.int64
-            if is_raw or len(derived):
-                # one kernel (CPU: the same arithmetic in torch): fixed-point -> fp64 and parent - sibling
-                H = K.hist_assemble(Hb, hist_raw_scale if is_raw else None, prev_hist if len(derived) else None,
-                                    slot_of, a_parent, a_sib, table=lvl[0] if lvl is not None else None)
+    def _fit_rows(self, st: "_FitState", codes_pre) -> None:
+        """The fit's row state: a node permutation (one tree, segment mode), u16 row codes (+ the fixed-point
+        scales every rank agrees on), or int32 node ids."""
+        data, dev, n, T = self.data, self.device, self.data.n_local, st.T
+        stats_rows, weights = st.stats_rows, st.weights
+        st.codes = st.node = st.perm = None
+        st.wmax = 1
+        if st.use_seg:
+            w1 = None if weights is None else weights.reshape(-1)
+            st.wmax = int(w1.max().item()) if (w1 is not None and w1.numel()) else 1
+            perm = (torch.arange(n, dtype=torch.int32, device=dev) if w1 is None else
+                    torch.nonzero(w1 > 0).flatten().to(torch.int32))
+            pl = perm.long()
+            st.perm = perm
+            st.v1p = stats_rows["v1"].float()[pl].contiguous()
+            st.v0p = None if stats_rows.get("v0") is None else stats_rows["v0"].float()[pl].contiguous()
+            st.wp = None if (w1 is None or st.wmax <= 1) else w1[pl].to(torch.uint8).contiguous()
+            # scales agreed over all ranks (max |v|, max weight, global row count): the int64 fixed-point
+            # level histograms all-reduce exactly, so the tree does not depend on the GPU count
+            st.seg_scales = K.seg_scales(st.v0p, st.v1p, st.wmax, data.n_global, self.comm)
+            st.seg_raw = st.seg_scales if st.v0p is not None else st.seg_scales[1]
+            st.segs = np.array([[0, perm.numel()]], dtype=np.int64)
+        elif st.use_codes:
+            if codes_pre is not None:
+                st.codes, st.wmax = codes_pre.codes, codes_pre.wmax()
             else:
-                H = Hb
-            masks_t = masks_dev if masks_dev is not None else \
-                (K.upload(dev, masks_np.view(np.int32))[0] if masks_np is not None else None)
-            catm_h = None  # left-category bit masks of the native categorical scan
-            dec = None     # device-decoded partition tables (partition already queued)
-            if rs_slice is not None or self._native_split(dev):
-                # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
-                mb = p.impurity == "xgb" and self.data.missing_bin
-                if rs_slice is not None:
-                    if masks_dev is not None:
-                        masks_np = self._feature_masks(tid.astype(np.uint64), a_key)
-                    so, tot = self._rs_split(H, rs_slice, masks_np, d, dev)
-                else:
-                    so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
-                                           p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight,
-                                           missing_bin=mb)
-                dec = None
-                host_p = None
-                # (deep forests: not at the level that leaves the codes for node ids; below it on the node ids)
-                deep_ids = deep_switch and node is not None
-                if self._device_decode_ok(dev, use_codes or deep_ids, mb) and \
-                        (depth + 1 < p.max_depth or margin_ok) and not (deep_switch and use_codes and depth + 1 >= 8):
-                    # the decisions leave for the host first (pinned, async): they arrive while the partition runs
-                    src = torch.cat([so, tot], 1) if depth == 0 else so
-                    host_p = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
-                    host_p.copy_(src, non_blocking=True)
-                    host_ev = torch.cuda.Event()
-                    host_ev.record(torch.cuda.current_stream(dev))
-                    # the partition tables decoded on the device and the row partition queued right behind K6:
-                    # the GPU partitions while the decisions travel to the host and the host builds the forest
-                    # and the next level's layout (the same decode on the host, checked in the checked build)
-                    dec = self._device_partition(so, tot, a_tree, tfirst, T, depth, mb, codes,
-                                                 margin=margin if margin_ok else None,
-                                                 node=node if deep_ids else None,
-                                                 pre=(lvl[1], lvl[2]) if lvl is not None else None)
-                # so [A, 8] = gain, feature, bin, left (2), right (2), missing-goes-right: copied to the host as is
-                # (plus the node totals at level 0), no per-column device ops
-                sw = so.shape[1]
-                flush()  # the previous level's forest bookkeeping, while the GPU runs this level's kernels
-                if host_p is not None:
-                    host_ev.synchronize()
-                    host = host_p.numpy()
-                else:
-                    host = (torch.cat([so, tot], 1) if depth == 0 else so).cpu().numpy()
-                gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
-                lst_h, rst_h = host[:, 3:5], host[:, 5:7]
-                mr_h = host[:, 7] > 0.5 if mb else None
-                if depth == 0:
-                    a_stats = host[:, sw:sw + tot.shape[1]].copy()
-                order, cat_feats = None, []
-            elif self._native_split_ex(dev):
-                # classification / categorical K6 in one kernel (centroid-ordered categories, Gini / entropy)
-                so, tot, cm = K.split_scan_ex(H, self._nthr_dev(dev), masks_t, p.impurity, p.min_instances)
-                kk = tot.shape[1]
-                src = torch.cat([so, cm.double()] + ([tot] if depth == 0 else []), 1)
-                reg_ex = not self.classification and kk == 2  # variance regression with categorical features
-                deep_ids = deep_switch and node is not None
-                if (cls2 or reg_ex) and (use_codes or deep_ids) and DEVICE_DECODE and depth + 1 < p.max_depth \
-                        and not (deep_switch and use_codes and depth + 1 >= 8):
-                    # binary classification / categorical regression on the codes: the same device decode +
-                    # partition (+ record emission) as numeric regression, queued behind K6 while the decisions
-                    # travel to the host; categorical winners split by K6's category bitmasks.  The decode reads
-                    # (gain, feature, bin, left weight, ., right weight, .); a pure child (one class) weighs 0
-                    # there, so it is a leaf on the device exactly as on the host
-                    host_p = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
-                    host_p.copy_(src, non_blocking=True)
-                    host_ev = torch.cuda.Event()
-                    host_ev.record(torch.cuda.current_stream(dev))
-                    if cls2:
-                        l0, l1, r0, r1 = so[:, 4], so[:, 5], so[:, 6], so[:, 7]
-                        zero = torch.zeros_like(l0)
-                        so_d = torch.stack([so[:, 0], so[:, 1], so[:, 2],
-                                            torch.where((l0 > 0) & (l1 > 0), l0 + l1, zero), l1,
-                                            torch.where((r0 > 0) & (r1 > 0), r0 + r1, zero), r1], 1)
-                        tot_d = tot.sum(1, keepdim=True)
-                    else:
-                        so_d = so[:, [0, 1, 2, 4, 5, 6, 7]]
-                        tot_d = tot
-                    dec = self._device_partition(so_d, tot_d, a_tree, tfirst, T, depth, False, codes,
-                                                 catm=cm if self.data.categorical else None,
-                                                 node=node if deep_ids else None,
-                                                 pre=(lvl[1], lvl[2]) if lvl is not None else None)
-                    flush()
-                    host_ev.synchronize()
-                    host = host_p.numpy()
-                else:
-                    flush()
-                    host = src.cpu().numpy()
-                gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
-                lst_h, rst_h = host[:, 4:4 + kk], host[:, 4 + kk:4 + 2 * kk]
-                c0 = 4 + 2 * kk
-                catm_h = (host[:, c0:c0 + 8].astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)
-                mr_h = None
-                if depth == 0:
-                    a_stats = host[:, c0 + 8:c0 + 8 + kk].copy()
-                order, cat_feats = None, []
-            else:
-                tot = self._node_stats(H, None)
-                gain, bf, bb, lst, rst, order, cat_feats, miss_right = self._best_splits(H, tot, masks_t)
-                # one device->host transfer for the whole level's decisions (ids < 2^53 are exact in f64)
-                kk = lst.shape[1]
-                cols = [gain[:, None], bf[:, None].double(), bb[:, None].double(), lst, rst]
-                if miss_right is not None:
-                    cols.append(miss_right[:, None].double())
-                if depth == 0:
-                    cols.append(tot)
-                flush()
-                host = torch.cat(cols, 1).cpu().numpy()
-                gain_h, bf_h, bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
-                lst_h, rst_h = host[:, 3:3 + kk], host[:, 3 + kk:3 + 2 * kk]
-                c0 = 3 + 2 * kk
-                mr_h = None
-                if miss_right is not None:
-                    mr_h = host[:, c0] != 0
-                    c0 += 1
-                if depth == 0:
-                    a_stats = host[:, c0:c0 + tot.shape[1]].copy()
-            order_h = order.cpu().numpy() if order is not None else None
-            _split_span.__exit__(None, None, None)
-            # ---- create forest nodes for the active set, decide splits
-            if depth == 0:
-                a_fid = forest.add_many(self._leaf_values_v(a_stats), self._weights_v(a_stats), depth,
-                                        self._impurities_v(a_stats))
-                node_count = forest.num_nodes
-                if heap is not None:
-                    heap_v[a_tree, 0] = self._leaf_values_v(a_stats)[:, 0]
-                for t_, fid_ in zip(a_tree.tolist(), a_fid.tolist()):
-                    root_ids[t_] = fid_
-            W_a = self._weights_v(a_stats)
-            with np.errstate(invalid="ignore"):
-                can = np.isfinite(gain_h) & (gain_h > 0) & (gain_h >= p.min_info_gain) & \
-                    (W_a >= 2 * p.min_instances)
-            if depth >= p.max_depth:
-                can[:] = False
-            sp = np.nonzero(can)[0]
-            split_feat = np.full(A, -1, dtype=np.int32)
-            split_bin = np.zeros(A, dtype=np.int32)
-            cat_off = np.full(A, -1, dtype=np.int32)
-            cat_masks = []
-            child = np.full(2 * A, -1, dtype=np.int32)
-            f_sp, b_sp, fid_sp = bf_h[sp], bb_h[sp], a_fid[sp]
-            thr_sp = np.zeros(len(sp))
-            plain = np.ones(len(sp), dtype=bool)
-            if self.data.categorical or mr_h is not None:
-                flush()  # the writes below address the nodes the previous level appended
-                for j, a in enumerate(sp.tolist()):
-                    f, b = int(f_sp[j]), int(b_sp[j])
-                    if f in self.data.categorical:
-                        if catm_h is not None:
-                            m = catm_h[a].copy()
-                        else:
-                            ci = cat_feats.index(f)
-                            m = np.zeros(8, dtype=np.uint32)
-                            for c in order_h[a, ci, : b + 1]:
-                                m[int(c) >> 5] |= np.uint32(1) << np.uint32(int(c) & 31)
-                    elif mr_h is not None and mr_h[a]:
-                        # missing (bin 0) goes right: left = bins 1..b, expressed as a bin-set split
-                        m = np.zeros(8, dtype=np.uint32)
-                        for c in range(1, b + 1):
-                            m[c >> 5] |= np.uint32(1) << np.uint32(c & 31)
-                        forest.bin[int(fid_sp[j])] = b
-                        thr_sp[j] = float(self.data.thresholds[f, b])
-                    else:
-                        continue
-                    plain[j] = False
-                    forest.is_cat[int(fid_sp[j])] = True
-                    forest.catmask[int(fid_sp[j])] = m
-                    cat_off[a] = len(cat_masks)
-                    cat_masks.append(m)
-            cat_f = np.array([f in self.data.categorical for f in f_sp.tolist()], dtype=bool) if \
-                self.data.categorical else np.zeros(len(sp), dtype=bool)
-            num = ~cat_f  # numeric splits carry a bin threshold (missing-right ones too)
-            if num.any():
-                thr_sp[num] = self.data.thresholds[f_sp[num], b_sp[num]]
-            split_bin[sp[plain]] = b_sp[plain]
-            split_feat[sp] = f_sp
-            # children in (node, side) order: ids base + 2j (left), base + 2j + 1 (right)
-            k_st = lst_h.shape[1]
-            ch_st = np.stack([lst_h[sp], rst_h[sp]], 1).reshape(-1, k_st)
-            # forest ids of the children (appended after the partition launch: the forest bookkeeping then
-            # runs on the host while the GPU partitions the rows)
-            ch_ids = np.arange(node_count, node_count + 2 * len(sp), dtype=np.int64)
-            node_count += 2 * len(sp)
-            cw = self._weights_v(ch_st)
-            leaf = (cw < 2 * p.min_instances) | (depth + 1 >= p.max_depth)
-            if self.classification:
-                leaf |= (ch_st > 0).sum(1) <= 1  # pure node
-            nl = np.nonzero(~leaf)[0]
-            ch_par = np.repeat(sp, 2)
-            child[2 * ch_par[nl] + (nl & 1)] = np.arange(len(nl), dtype=np.int32)
-            n_tree = a_tree[ch_par[nl]]
-            n_fid = ch_ids[nl]
-            n_key = a_key[ch_par[nl]] * np.uint64(2) + (nl & 1).astype(np.uint64)
-            n_stats = ch_st[nl]
-            n_parent = ch_par[nl].astype(np.int64)
-            # siblings (both children active) for subtraction; a single active child is built directly
-            pos = np.full(2 * len(sp), -1, dtype=np.int64)
-            pos[nl] = np.arange(len(nl))
-            lp, rp = pos[0::2], pos[1::2]
-            both = (lp >= 0) & (rp >= 0)
-            n_sib = np.full(len(nl), -1, dtype=np.int64)
-            n_sib[lp[both]] = rp[both]
-            n_sib[rp[both]] = lp[both]
-            n_parent[n_sib < 0] = -1
-            if len(nl) and deep_switch and use_codes and depth + 1 >= 8:
-                # the next level can hold more than 255 nodes per tree: leave the u16 codes for node ids
-                # (active index of the node, -1 = done), partitioned and histogrammed by the node-id kernels
-                node, wdeep = K.decode_codes(codes, tfirst)  # host tfirst: uploaded once, no D2H
-                node = node.contiguous()
-                # the node-id histogram kernels (levels past NODE_COMPACT_MAX_LOC nodes per tree) read the row weights
-                # from ``weights``: None when the bootstrap draws arrived as row codes (BootstrapCodes)
-                weights = wdeep
-                # below level 8 the record histograms continue from the node ids (K.node_compact)
-                deep_rec = use_mseg and rec_ok
-                use_codes = use_mseg = False
-                codes = None
-            if len(nl):
-                cm = np.stack(cat_masks).view(np.int32) if cat_masks else np.zeros((0, 8), np.int32)
-                with _tr.span("tree.partition", depth=depth):
-                    if use_seg:
-                        perm, v0p, v1p, wp, segs = K.seg_partition(data.bins, perm, v0p, v1p, wp, segs, split_feat,
-                                                                    split_bin, cat_off, cm.reshape(-1), child,
-                                                                    len(nl))
-                    elif dec is not None:  # partitioned on the device behind K6
-                        if K._lib.DEBUG:
-                            self._check_decode(dec, split_feat, split_bin, cat_off, cat_masks, child, n_tree, T)
-                    elif use_codes:
-                        tfirst_next = torch.from_numpy(
-                            np.searchsorted(n_tree, np.arange(T), side="left").astype(np.int32))
-                        K.partition_codes(data.bins, codes, tfirst, tfirst_next, torch.from_numpy(split_feat),
-                                          torch.from_numpy(split_bin), torch.from_numpy(cat_off),
-                                          torch.from_numpy(cm.reshape(-1)), torch.from_numpy(child))
-                    else:
-                        K.partition(data.bins, node, *K.upload(dev, split_feat, split_bin, cat_off,
-                                                               cm.reshape(-1), child))
-            ch_vals = self._leaf_values_v(ch_st)
-            # the forest's node lists for this level are appended and split at the next level's decision sync
-            # (flush), i.e. while the GPU runs that level's histogram / K6 / partition, not between this level's
-            # decisions and the next level's launches (~0.2-0.4 ms of numpy per level at the headline's widths)
-            pending.append(functools.partial(_forest_level_ops, forest, (ch_vals, cw, depth + 1,
-                                                                          self._impurities_v(ch_st)),
-                                             (fid_sp, f_sp, gain_h[sp], b_sp, thr_sp, num, ch_ids[0::2],
-                                              ch_ids[1::2]), ch_ids[0] if len(ch_ids) else None, len(ch_ids)))
-            if heap is not None and len(sp):
-                if not plain.all():
-                    heap = None  # bin-set splits: Forest.heap_arrays builds the table from the forest
-                else:
-                    tsp, ksp = a_tree[sp], a_key[sp].astype(np.int64)
-                    heap[tsp, ksp - 1, 0] = f_sp
-                    heap[tsp, ksp - 1, 1] = thr_sp.astype(np.float32).view(np.int32)
-                    ck = np.stack([2 * ksp, 2 * ksp + 1], 1).reshape(-1)
-                    heap_v[np.repeat(tsp, 2), ck - 1] = ch_vals[:, 0]
-                    heap_depth = depth + 1
-            prev_hist = H
-            a_tree, a_fid, a_key, a_stats, a_sib, a_parent = n_tree, n_fid, n_key, n_stats, n_sib, n_parent
+                st.codes, st.wmax = K.codes_init_max(weights, T, n, dev)
+            if st.use_mseg:
+                # one quantisation scale for every rank: the int64 level histograms then all-reduce to
+                # the same sums on 1 or N GPUs (the forest does not depend on the GPU count)
+                v0s = stats_rows.get("v0")
+                st.mseg_scales = (1.0, 1.0) if st.cls2 else \
+                    K.seg_scales(None if v0s is None else v0s.float(), stats_rows["v1"].float(), st.wmax,
+                                 data.n_global, self.comm)
+                st.mseg_raw = st.mseg_scales[1] if v0s is None else st.mseg_scales
+        else:
+            st.node = torch.arange(T, dtype=torch.int32, device=dev)[:, None].expand(T, n).contiguous() if n else \
+                torch.zeros((T, 0), dtype=torch.int32, device=dev)
+
+    def _fit_finish(self, st: "_FitState") -> Forest:
+        forest = st.forest
         # the last level's bookkeeping stays with the forest (settled by the predictor right after its launch, or
         # by the first reader of the node lists)
-        forest._pending.extend(pending)
-        pending.clear()
-        forest.roots.extend(root_ids)
+        forest._pending.extend(st.pending)
+        st.pending.clear()
+        forest.roots.extend(st.root_ids)
         forest._dev = {}
-        if heap is not None:
-            S_ = 2 ** (heap_depth + 1) - 1
-            forest._heap_np = (np.ascontiguousarray(heap[:, :S_]), np.ascontiguousarray(heap_v[:, :S_]), heap_depth)
+        if st.heap is not None:
+            S_ = 2 ** (st.heap_depth + 1) - 1
+            forest._heap_np = (np.ascontiguousarray(st.heap[:, :S_]), np.ascontiguousarray(st.heap_v[:, :S_]),
+                               st.heap_depth)
         return forest
+
+    # ------------------------------------------------------------ level: tables
+    def _level_tables(self, st: "_FitState", depth: int) -> "_Level":
+        """Which active nodes build a histogram (the smaller of two siblings), the level's feature masks and its
+        small device tables (one host -> device copy)."""
+        p, data, dev, d, T = self.p, self.data, self.device, self.data.d, st.T
+        lv = _Level()
+        A = len(st.a_tree)
+        lv.A = A
+        lv.build = np.ones(A, dtype=bool)
+        if depth > 0:
+            lv.build = _built_nodes(self._weights_v(st.a_stats), st.a_sib, st.a_parent)
+        lv.build_ids = np.nonzero(lv.build)[0]
+        lv.slot_of = np.full(A, -1, dtype=np.int32)
+        lv.slot_of[lv.build_ids] = np.arange(len(lv.build_ids), dtype=np.int32)
+        lv.slot_tree = st.a_tree[lv.build_ids]
+        lv.masks_np = None
+        lv.masks_dev = None  # the same words drawn on the GPU (no host consumer this level)
+        mask_base = None
+        lv.tid = None
+        if st.need_masks:
+            lv.tid = st.a_tree if p.tree_ids is None else np.asarray(p.tree_ids, dtype=np.int64)[st.a_tree]
+            if MASKS_DEV and dev.type == "cuda" and \
+                    d <= K.FEATURE_MASKS_MAX_D and p.feature_subset is not None and 0 < p.feature_subset < d:
+                mask_base = self._mask_base(lv.tid.astype(np.uint64), st.a_key)
+            else:
+                lv.masks_np = self._feature_masks(lv.tid.astype(np.uint64), st.a_key)
+        lv.tfirst = torch.from_numpy(np.searchsorted(st.a_tree, np.arange(T), side="left").astype(np.int32))
+        # the level's small device tables in ONE host->device copy (each separate copy was a blit kernel plus a
+        # launch gap): hist_assemble's (slot, parent, sibling), the decode's a_tree / tfirst, the mask bases
+        lv.lvl = None
+        if dev.type == "cuda":
+            lv.lvl = K.upload(dev, K.assemble_table(lv.slot_of, st.a_parent, st.a_sib), st.a_tree.astype(np.int32),
+                              lv.tfirst.numpy().astype(np.int32),
+                              *([mask_base.view(np.int64)] if mask_base is not None else []))
+            if mask_base is not None:
+                lv.masks_dev = K.feature_masks(mask_base, d, p.feature_subset, dev, base_dev=lv.lvl[3])
+        return lv
+
+    # ------------------------------------------------------------ level: histograms
+    def _root_rows(self):
+        """Row-major bins for the histograms straight from the codes: seg10 rows (B <= 40) or standard rows
+        (boosting, 80 < B <= 256), else None."""
+        data = self.data
+        if self.device.type == "cuda" and ROOT_HIST:
+            if data.bins_s10 is not None and data.d <= 100 and data.B <= 40:
+                return data.bins_s10
+            if 80 < data.B <= 256 and data.bins_rm is not None:
+                return data.bins_rm
+        return None
+
+    def _level_histogram(self, st: "_FitState", lv: "_Level", depth: int) -> None:
+        """lv.Hb: the level's built-slot histograms (int64 fixed-point sums on the record / segment paths, their
+        scale in lv.hist_raw_scale; lv.reduced when they are already summed over ranks)."""
+        data, dev, d, B, T = self.data, self.device, self.data.d, self.data.B, st.T
+        stats_rows, wmax = st.stats_rows, st.wmax
+        build_ids, slot_of, slot_tree, tfirst = lv.build_ids, lv.slot_of, lv.slot_tree, lv.tfirst
+        S = len(build_ids)
+        lv.hist_raw_scale = None
+        lv.reduced = False
+        # levels with <= 1 built node per tree (0: the roots, 1: the smaller children): the records are compacted
+        # inside the histogram kernel (no codes_compact pass)
+        root_rows = self._root_rows()
+        root_ok = (root_rows is not None and st.use_mseg and (depth >= 1 or MSEG_L0) and st.rec_ok and
+                   S > 0 and np.bincount(slot_tree, minlength=T).max() <= 1)
+        if root_ok:
+            sl_node = build_ids - tfirst.numpy()[slot_tree]  # the slot's local node in its tree's codes
+            # one launch for every slot, then the level's one all-reduce: these levels hold one node per
+            # tree (20 x 100 x 40 cells = 1.3 MB at the headline), too little to overlap, and slot chunks
+            # of a 1.25e7-row shard would launch ~1 round of blocks each (half of it idle)
+            lv.Hb = K.seg_hist_codes(root_rows, d, B, st.codes, stats_rows["v1"], st.mseg_scales[1], wmax,
+                                     slot_tree, sl_node, 0, S,
+                                     torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev))
+            lv.hist_raw_scale = st.mseg_raw
+        elif st.use_mseg and (depth >= 1 or MSEG_L0):
+            # gather the rows of the built nodes into slot segments, then segment histograms of packed
+            # item records on every device (the CPU emulates the HIP compaction + flat histogram
+            # exactly, so gloo ranks traverse the integer path RCCL ranks take)
+            perm, v0p, v1p, wp, sg = K.codes_compact(st.codes, tfirst, slot_of, S, stats_rows.get("v0"),
+                                                     stats_rows["v1"],
+                                                     rec_scale=st.mseg_scales[1] if st.rec_ok else None)
+            is_rec = st.rec_ok and v1p is None
+            sb = np.concatenate([sg, np.arange(S, dtype=np.int64)[:, None]], 1)
+            if is_rec and (self.comm.distributed or HIST_OVERLAP_FORCE) and HIST_OVERLAP > 1 and S >= 2 and \
+                    S * d * B * 16 >= HIST_OVERLAP_MIN_BYTES and not self._rs_level(S * d * B * 16, st.rs_on):
+                # (never once the pass reduce-scatters: the overlapped chunks are all-reduced over all
+                # features, while prev_hist then holds only this rank's feature slice)
+                # comm/compute overlap: the level's slots are built in chunks, each chunk's int64
+                # histogram all-reduced (async, RCCL stream) while the next chunk is built
+                lv.Hb = self._hist_overlapped(data, d, B, perm, sb, S, wmax, st.mseg_scales, dev)
+                lv.reduced = True
+            else:
+                rm, s10 = (data.record_rows() if is_rec else (data.row_major_bins(), False)) \
+                    if dev.type == "cuda" else (None, False)
+                lv.Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, S, wmax, st.mseg_scales, bins_rm=rm,
+                                   interleave=True, rec=is_rec, raw=True, rm_s10=s10)
+            lv.hist_raw_scale = st.mseg_raw
+        elif st.deep_rec and S and np.bincount(st.a_tree, minlength=T).max() <= K.NODE_COMPACT_MAX_LOC:
+            # levels below the u16 codes (binary classification deeper than 8): the built rows' packed
+            # records from the node ids, then the same record histograms as the shallow levels (the
+            # node-id kernel re-read every row once per LDS-sized slot group: ~290 ms per level at
+            # 1e7 rows x 100 trees)
+            perm, sg = K.node_compact(st.node, st.wdeep, tfirst.numpy(), slot_of, S, stats_rows["v1"],
+                                      st.mseg_scales[1])
+            sb = np.concatenate([sg, np.arange(S, dtype=np.int64)[:, None]], 1)
+            rm, s10 = data.record_rows() if dev.type == "cuda" else (None, False)
+            lv.Hb = K.seg_hist(data.bins, d, B, perm, None, None, None, sb, S, wmax, st.mseg_scales, bins_rm=rm,
+                               interleave=True, rec=True, raw=True, rm_s10=s10)
+            lv.hist_raw_scale = st.mseg_raw
+        elif st.use_seg:
+            sb = np.stack([st.segs[build_ids, 0], st.segs[build_ids, 1], slot_of[build_ids].astype(np.int64)], 1)
+            lv.Hb = K.seg_hist(data.bins, d, B, st.perm, st.v0p, st.v1p, st.wp, sb, S, wmax, st.seg_scales,
+                               # sparse node segments (>= 4 built nodes) gather whole rows from the
+                               # row-major copy; dense shallow levels stream the [G][n] layout
+                               bins_rm=data.row_major_bins() if (K.SEG_ROW_MAJOR and dev.type == "cuda"
+                                                                 and S >= 4) else None,
+                               interleave=st.use_mseg, raw=True)
+            lv.hist_raw_scale = st.seg_raw
+        elif st.use_codes:
+            lv.Hb = K.hist_codes(1 if self.classification else 0, data.bins, d, st.codes, tfirst,
+                                 stats_rows.get("v0"), stats_rows.get("v1"), stats_rows.get("label"), self.C,
+                                 K.upload(dev, slot_of)[0], slot_tree, st.a_tree, None, B, wmax=wmax)
+        elif self.classification:
+            lv.Hb = K.hist_classes(data.bins, d, st.node, st.weights, stats_rows["label"], self.C,
+                                   K.upload(dev, slot_of)[0], slot_tree, None, B, id_tree=st.a_tree)
+        else:
+            lv.Hb = K.hist_moments(data.bins, d, st.node, st.weights, stats_rows.get("v0"), stats_rows["v1"],
+                                   K.upload(dev, slot_of)[0], slot_tree, None, B, id_tree=st.a_tree)
+        if st.cls2 and lv.hist_raw_scale is not None:
+            lv.Hb[..., 0] -= lv.Hb[..., 1]  # packed (W, W1) -> class counts (W0, W1), exact int64
+
+    def _level_reduce(self, st: "_FitState", lv: "_Level") -> None:
+        """The level histograms summed over ranks: one fused all-reduce, or (large int64 levels) a reduce-scatter
+        by feature -- lv.rs_slice is then this rank's feature range and prev_hist is cut to it."""
+        lv.rs_slice = None
+        if lv.reduced:
+            return
+        if self._rs_want(lv.Hb, st.rs_on):
+            st.rs_on = True
+            lv.rs_slice, lv.Hb = self._reduce_scatter_features(lv.Hb, self.data.d)
+            if st.prev_hist is not None and st.prev_hist.shape[1] == self.data.d:
+                st.prev_hist = st.prev_hist[:, lv.rs_slice[0]:lv.rs_slice[1]].contiguous()
+        else:
+            with _tr.span("tree.allreduce", cat="comm", bytes=lv.Hb.numel() * 8):
+                self.comm.all_reduce(lv.Hb)  # one fused RCCL all-reduce per level
+
+    # ------------------------------------------------------------ level: split decisions
+    def _level_decide(self, st: "_FitState", lv: "_Level", depth: int) -> None:
+        """Assemble every active node's histogram, find the best splits (K6 kernels on the GPU), queue the device
+        decode + partition behind them where it applies, and bring the decisions to the host (lv.gain_h,
+        lv.bf_h, lv.bb_h, lv.lst_h, lv.rst_h, lv.mr_h, lv.catm_h, lv.order_h, lv.cat_feats; level 0 also sets the
+        roots' stats)."""
+        p, dev, d, T = self.p, self.device, self.data.d, st.T
+        Hb = lv.Hb
+        derived = np.nonzero(~lv.build)[0]
+        is_raw = Hb.dtype == torch.int64
+        if is_raw or len(derived):
+            # one kernel (CPU: the same arithmetic in torch): fixed-point -> fp64 and parent - sibling
+            H = K.hist_assemble(Hb, lv.hist_raw_scale if is_raw else None, st.prev_hist if len(derived) else None,
+                                lv.slot_of, st.a_parent, st.a_sib, table=lv.lvl[0] if lv.lvl is not None else None)
+        else:
+            H = Hb
+        lv.H = H
+        masks_t = lv.masks_dev if lv.masks_dev is not None else \
+            (K.upload(dev, lv.masks_np.view(np.int32))[0] if lv.masks_np is not None else None)
+        lv.catm_h = None  # left-category bit masks of the native categorical scan
+        lv.dec = None     # device-decoded partition tables (partition already queued)
+        order = None
+        lv.cat_feats = []
+        pre = (lv.lvl[1], lv.lvl[2]) if lv.lvl is not None else None
+        # (deep forests: not at the level that leaves the codes for node ids; below it on the node ids)
+        deep_ids = st.deep_switch and st.node is not None
+        leaving_codes = st.deep_switch and st.use_codes and depth + 1 >= 8
+        if lv.rs_slice is not None or self._native_split(dev):
+            # K6 in one kernel: node totals, prefix scans, gains, masks, argmax
+            mb = p.impurity == "xgb" and self.data.missing_bin
+            if lv.rs_slice is not None:
+                masks_np = lv.masks_np
+                if lv.masks_dev is not None:
+                    masks_np = self._feature_masks(lv.tid.astype(np.uint64), st.a_key)
+                so, tot = self._rs_split(H, lv.rs_slice, masks_np, d, dev)
+            else:
+                so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
+                                       p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight, missing_bin=mb)
+            host_p = None
+            if self._device_decode_ok(dev, st.use_codes or deep_ids, mb) and \
+                    (depth + 1 < p.max_depth or st.margin_ok) and not leaving_codes:
+                # the decisions leave for the host first (pinned, async): they arrive while the partition runs
+                src = torch.cat([so, tot], 1) if depth == 0 else so
+                host_p = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+                host_p.copy_(src, non_blocking=True)
+                host_ev = torch.cuda.Event()
+                host_ev.record(torch.cuda.current_stream(dev))
+                # the partition tables decoded on the device and the row partition queued right behind K6:
+                # the GPU partitions while the decisions travel to the host and the host builds the forest
+                # and the next level's layout (the same decode on the host, checked in the checked build)
+                lv.dec = self._device_partition(so, tot, st.a_tree, lv.tfirst, T, depth, mb, st.codes,
+                                                margin=st.margin if st.margin_ok else None,
+                                                node=st.node if deep_ids else None, pre=pre)
+            # so [A, 8] = gain, feature, bin, left (2), right (2), missing-goes-right: copied to the host as is
+            # (plus the node totals at level 0), no per-column device ops
+            sw = so.shape[1]
+            st.flush()  # the previous level's forest bookkeeping, while the GPU runs this level's kernels
+            if host_p is not None:
+                host_ev.synchronize()
+                host = host_p.numpy()
+            else:
+                host = (torch.cat([so, tot], 1) if depth == 0 else so).cpu().numpy()
+            lv.lst_h, lv.rst_h = host[:, 3:5], host[:, 5:7]
+            lv.mr_h = host[:, 7] > 0.5 if mb else None
+            if depth == 0:
+                st.a_stats = host[:, sw:sw + tot.shape[1]].copy()
+        elif self._native_split_ex(dev):
+            # classification / categorical K6 in one kernel (centroid-ordered categories, Gini / entropy)
+            so, tot, cm = K.split_scan_ex(H, self._nthr_dev(dev), masks_t, p.impurity, p.min_instances)
+            kk = tot.shape[1]
+            src = torch.cat([so, cm.double()] + ([tot] if depth == 0 else []), 1)
+            reg_ex = not self.classification and kk == 2  # variance regression with categorical features
+            if (st.cls2 or reg_ex) and (st.use_codes or deep_ids) and DEVICE_DECODE and depth + 1 < p.max_depth \
+                    and not leaving_codes:
+                # binary classification / categorical regression on the codes: the same device decode +
+                # partition as numeric regression, queued behind K6 while the decisions travel to the host;
+                # categorical winners split by K6's category bitmasks.  The decode reads (gain, feature, bin,
+                # left weight, ., right weight, .); a pure child (one class) weighs 0 there, so it is a leaf on
+                # the device exactly as on the host
+                host_p = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+                host_p.copy_(src, non_blocking=True)
+                host_ev = torch.cuda.Event()
+                host_ev.record(torch.cuda.current_stream(dev))
+                if st.cls2:
+                    l0, l1, r0, r1 = so[:, 4], so[:, 5], so[:, 6], so[:, 7]
+                    zero = torch.zeros_like(l0)
+                    so_d = torch.stack([so[:, 0], so[:, 1], so[:, 2],
+                                        torch.where((l0 > 0) & (l1 > 0), l0 + l1, zero), l1,
+                                        torch.where((r0 > 0) & (r1 > 0), r0 + r1, zero), r1], 1)
+                    tot_d = tot.sum(1, keepdim=True)
+                else:
+                    so_d = so[:, [0, 1, 2, 4, 5, 6, 7]]
+                    tot_d = tot
+                lv.dec = self._device_partition(so_d, tot_d, st.a_tree, lv.tfirst, T, depth, False, st.codes,
+                                                catm=cm if self.data.categorical else None,
+                                                node=st.node if deep_ids else None, pre=pre)
+                st.flush()
+                host_ev.synchronize()
+                host = host_p.numpy()
+            else:
+                st.flush()
+                host = src.cpu().numpy()
+            lv.lst_h, lv.rst_h = host[:, 4:4 + kk], host[:, 4 + kk:4 + 2 * kk]
+            c0 = 4 + 2 * kk
+            lv.catm_h = (host[:, c0:c0 + 8].astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)
+            lv.mr_h = None
+            if depth == 0:
+                st.a_stats = host[:, c0 + 8:c0 + 8 + kk].copy()
+        else:
+            tot = self._node_stats(H, None)
+            gain, bf, bb, lst, rst, order, lv.cat_feats, miss_right = self._best_splits(H, tot, masks_t)
+            # one device->host transfer for the whole level's decisions (ids < 2^53 are exact in f64)
+            kk = lst.shape[1]
+            cols = [gain[:, None], bf[:, None].double(), bb[:, None].double(), lst, rst]
+            if miss_right is not None:
+                cols.append(miss_right[:, None].double())
+            if depth == 0:
+                cols.append(tot)
+            st.flush()
+            host = torch.cat(cols, 1).cpu().numpy()
+            lv.lst_h, lv.rst_h = host[:, 3:3 + kk], host[:, 3 + kk:3 + 2 * kk]
+            c0 = 3 + 2 * kk
+            lv.mr_h = None
+            if miss_right is not None:
+                lv.mr_h = host[:, c0] != 0
+                c0 += 1
+            if depth == 0:
+                st.a_stats = host[:, c0:c0 + tot.shape[1]].copy()
+        lv.gain_h, lv.bf_h, lv.bb_h = host[:, 0], host[:, 1].astype(np.int64), host[:, 2].astype(np.int64)
+        lv.order_h = order.cpu().numpy() if order is not None else None
+
+    # ------------------------------------------------------------ level: children and bookkeeping
+    def _level_advance(self, st: "_FitState", lv: "_Level", depth: int) -> None:
+        """The level's splits on the host: the children (the next active set), the row partition where the device
+        did not already queue it, and the forest / heap bookkeeping (deferred to the next level's sync)."""
+        p, data, dev, T, A = self.p, self.data, self.device, st.T, lv.A
+        forest = st.forest
+        a_tree, a_fid, a_key = st.a_tree, st.a_fid, st.a_key
+        if depth == 0:
+            a_fid = st.a_fid = forest.add_many(self._leaf_values_v(st.a_stats), self._weights_v(st.a_stats), depth,
+                                               self._impurities_v(st.a_stats))
+            st.node_count = forest.num_nodes
+            if st.heap is not None:
+                st.heap_v[a_tree, 0] = self._leaf_values_v(st.a_stats)[:, 0]
+            for t_, fid_ in zip(a_tree.tolist(), a_fid.tolist()):
+                st.root_ids[t_] = fid_
+        gain_h, bf_h, bb_h, mr_h, catm_h = lv.gain_h, lv.bf_h, lv.bb_h, lv.mr_h, lv.catm_h
+        W_a = self._weights_v(st.a_stats)
+        with np.errstate(invalid="ignore"):
+            can = np.isfinite(gain_h) & (gain_h > 0) & (gain_h >= p.min_info_gain) & (W_a >= 2 * p.min_instances)
+        if depth >= p.max_depth:
+            can[:] = False
+        sp = np.nonzero(can)[0]
+        split_feat = np.full(A, -1, dtype=np.int32)
+        split_bin = np.zeros(A, dtype=np.int32)
+        cat_off = np.full(A, -1, dtype=np.int32)
+        cat_masks = []
+        child = np.full(2 * A, -1, dtype=np.int32)
+        f_sp, b_sp, fid_sp = bf_h[sp], bb_h[sp], a_fid[sp]
+        thr_sp = np.zeros(len(sp))
+        plain = np.ones(len(sp), dtype=bool)
+        if data.categorical or mr_h is not None:
+            st.flush()  # the writes below address the nodes the previous level appended
+            for j, a in enumerate(sp.tolist()):
+                f, b = int(f_sp[j]), int(b_sp[j])
+                if f in data.categorical:
+                    if catm_h is not None:
+                        m = catm_h[a].copy()
+                    else:
+                        ci = lv.cat_feats.index(f)
+                        m = np.zeros(8, dtype=np.uint32)
+                        for c in lv.order_h[a, ci, : b + 1]:
+                            m[int(c) >> 5] |= np.uint32(1) << np.uint32(int(c) & 31)
+                elif mr_h is not None and mr_h[a]:
+                    # missing (bin 0) goes right: left = bins 1..b, expressed as a bin-set split
+                    m = np.zeros(8, dtype=np.uint32)
+                    for c in range(1, b + 1):
+                        m[c >> 5] |= np.uint32(1) << np.uint32(c & 31)
+                    forest.bin[int(fid_sp[j])] = b
+                    thr_sp[j] = float(data.thresholds[f, b])
+                else:
+                    continue
+                plain[j] = False
+                forest.is_cat[int(fid_sp[j])] = True
+                forest.catmask[int(fid_sp[j])] = m
+                cat_off[a] = len(cat_masks)
+                cat_masks.append(m)
+        cat_f = np.array([f in data.categorical for f in f_sp.tolist()], dtype=bool) if \
+            data.categorical else np.zeros(len(sp), dtype=bool)
+        num = ~cat_f  # numeric splits carry a bin threshold (missing-right ones too)
+        if num.any():
+            thr_sp[num] = data.thresholds[f_sp[num], b_sp[num]]
+        split_bin[sp[plain]] = b_sp[plain]
+        split_feat[sp] = f_sp
+        # children in (node, side) order: ids base + 2j (left), base + 2j + 1 (right)
+        k_st = lv.lst_h.shape[1]
+        ch_st = np.stack([lv.lst_h[sp], lv.rst_h[sp]], 1).reshape(-1, k_st)
+        # forest ids of the children (appended after the partition launch: the forest bookkeeping then
+        # runs on the host while the GPU partitions the rows)
+        ch_ids = np.arange(st.node_count, st.node_count + 2 * len(sp), dtype=np.int64)
+        st.node_count += 2 * len(sp)
+        cw = self._weights_v(ch_st)
+        leaf = (cw < 2 * p.min_instances) | (depth + 1 >= p.max_depth)
+        if self.classification:
+            leaf |= (ch_st > 0).sum(1) <= 1  # pure node
+        nl = np.nonzero(~leaf)[0]
+        ch_par = np.repeat(sp, 2)
+        child[2 * ch_par[nl] + (nl & 1)] = np.arange(len(nl), dtype=np.int32)
+        n_tree = a_tree[ch_par[nl]]
+        n_fid = ch_ids[nl]
+        n_key = a_key[ch_par[nl]] * np.uint64(2) + (nl & 1).astype(np.uint64)
+        n_stats = ch_st[nl]
+        n_parent = ch_par[nl].astype(np.int64)
+        # siblings (both children active) for subtraction; a single active child is built directly
+        pos = np.full(2 * len(sp), -1, dtype=np.int64)
+        pos[nl] = np.arange(len(nl))
+        lp, rp = pos[0::2], pos[1::2]
+        both = (lp >= 0) & (rp >= 0)
+        n_sib = np.full(len(nl), -1, dtype=np.int64)
+        n_sib[lp[both]] = rp[both]
+        n_sib[rp[both]] = lp[both]
+        n_parent[n_sib < 0] = -1
+        if len(nl) and st.deep_switch and st.use_codes and depth + 1 >= 8:
+            # the next level can hold more than 255 nodes per tree: leave the u16 codes for node ids
+            # (active index of the node, -1 = done), partitioned and histogrammed by the node-id kernels
+            node, st.wdeep = K.decode_codes(st.codes, lv.tfirst)  # host tfirst: uploaded once, no D2H
+            st.node = node.contiguous()
+            # the node-id histogram kernels (levels past NODE_COMPACT_MAX_LOC nodes per tree) read the row weights
+            # from ``weights``: None when the bootstrap draws arrived as row codes (BootstrapCodes)
+            st.weights = st.wdeep
+            # below level 8 the record histograms continue from the node ids (K.node_compact)
+            st.deep_rec = st.use_mseg and st.rec_ok
+            st.use_codes = st.use_mseg = False
+            st.codes = None
+        if len(nl):
+            cm = np.stack(cat_masks).view(np.int32) if cat_masks else np.zeros((0, 8), np.int32)
+            with _tr.span("tree.partition", depth=depth):
+                if st.use_seg:
+                    st.perm, st.v0p, st.v1p, st.wp, st.segs = K.seg_partition(
+                        data.bins, st.perm, st.v0p, st.v1p, st.wp, st.segs, split_feat, split_bin, cat_off,
+                        cm.reshape(-1), child, len(nl))
+                elif lv.dec is not None:  # partitioned on the device behind K6
+                    if K._lib.DEBUG:
+                        self._check_decode(lv.dec, split_feat, split_bin, cat_off, cat_masks, child, n_tree, T)
+                elif st.use_codes:
+                    tfirst_next = torch.from_numpy(np.searchsorted(n_tree, np.arange(T), side="left").astype(np.int32))
+                    K.partition_codes(data.bins, st.codes, lv.tfirst, tfirst_next, torch.from_numpy(split_feat),
+                                      torch.from_numpy(split_bin), torch.from_numpy(cat_off),
+                                      torch.from_numpy(cm.reshape(-1)), torch.from_numpy(child))
+                else:
+                    K.partition(data.bins, st.node, *K.upload(dev, split_feat, split_bin, cat_off, cm.reshape(-1),
+                                                              child))
+        ch_vals = self._leaf_values_v(ch_st)
+        # the forest's node lists for this level are appended and split at the next level's decision sync
+        # (flush), i.e. while the GPU runs that level's histogram / K6 / partition, not between this level's
+        # decisions and the next level's launches (~0.2-0.4 ms of numpy per level at the headline's widths)
+        st.pending.append(functools.partial(_forest_level_ops, forest, (ch_vals, cw, depth + 1,
+                                                                         self._impurities_v(ch_st)),
+                                            (fid_sp, f_sp, gain_h[sp], b_sp, thr_sp, num, ch_ids[0::2],
+                                             ch_ids[1::2]), ch_ids[0] if len(ch_ids) else None, len(ch_ids)))
+        if st.heap is not None and len(sp):
+            if not plain.all():
+                st.heap = None  # bin-set splits: Forest.heap_arrays builds the table from the forest
+            else:
+                tsp, ksp = a_tree[sp], a_key[sp].astype(np.int64)
+                st.heap[tsp, ksp - 1, 0] = f_sp
+                st.heap[tsp, ksp - 1, 1] = thr_sp.astype(np.float32).view(np.int32)
+                ck = np.stack([2 * ksp, 2 * ksp + 1], 1).reshape(-1)
+                st.heap_v[np.repeat(tsp, 2), ck - 1] = ch_vals[:, 0]
+                st.heap_depth = depth + 1
+        st.prev_hist = lv.H
+        st.a_tree, st.a_fid, st.a_key, st.a_stats, st.a_sib, st.a_parent = \
+            n_tree, n_fid, n_key, n_stats, n_sib, n_parent
+
+
+class _FitState:
+    """Per-fit state of ForestTrainer.train: the paths chosen once per fit (``_fit_paths``), the row state
+    (``_fit_rows``: codes / node ids / segment permutation and their fixed-point scales), the active node set as
+    host arrays (a_tree, a_fid, a_key, a_stats, a_sib, a_parent), the previous level's histograms, the forest and
+    its predict heap table, and the forest bookkeeping deferred to the next level's sync (``pending``)."""
+
+    def __init__(self):
+        self.pending = []
+
+    def flush(self) -> None:
+        """Run the deferred forest bookkeeping of the previous level (called while the GPU runs this level)."""
+        while self.pending:
+            self.pending.pop(0)()
+
+
+class _Level:
+    """One level's tables (``_level_tables``), histograms (``_level_histogram`` / ``_level_reduce``) and host-side
+    decisions (``_level_decide``)."""
 
 
 from ...ops import tune as _tune  # noqa: E402  (CDNAML_TUNE overrides of the constants above)
