@@ -180,11 +180,9 @@ def main():
             torch.cuda.empty_cache()
             continue
         bins, node, w, y, build, st, it, fm = make_state(n, d, T, L, B, masked)
-        K.HIST_VERSION = min(ver, 4)
-        K.HIST_PACKED = ver == 5
         K.HIST_MAP = lmap
         fn = lambda: K.hist_moments(bins, d, node, w if wts else None, None, y, build, st, fm, B,  # noqa: E731
-                                    lds_budget=lds, id_tree=it if ver >= 2 else None)
+                                    lds_budget=lds, id_tree=it)
         ms = timeit(fn, args.reps)
         frac_w = float((w > 0).float().mean()) if wts else 1.0
         feats = int(np.ceil(d / 3)) if masked else d

@@ -104,12 +104,6 @@ _SIGS = {
     "cdna_binize": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,
                      c_int, c_int64, c_void_p],
                     c_int),
-    "cdna_hist_moments": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                           c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
-                           c_void_p, c_void_p], c_int),
-    "cdna_hist_classes": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                           c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
-                           c_void_p, c_void_p], c_int),
     "cdna_hist4": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,
                     c_void_p, c_void_p], c_int),

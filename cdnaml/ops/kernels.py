@@ -400,29 +400,10 @@ def bins_to_matrix(bins: torch.Tensor, d: int) -> torch.Tensor:
 
 
 # --------------------------------------------------------------------- K5
-def _slot_groups(slot_tree: np.ndarray, SB: int):
-    S = len(slot_tree)
-    s0, t0, t1 = [], [], []
-    for a in range(0, S, SB):
-        b = min(S, a + SB)
-        s0.append(a)
-        t0.append(int(slot_tree[a]))
-        t1.append(int(slot_tree[b - 1]))
-    return np.array(s0, np.int32), np.array(t0, np.int32), np.array(t1, np.int32)
-
-
-def _plan_chunks(n: int, G: int, ngroups: int, target_blocks: int = 2048) -> int:
-    per = max(1, target_blocks // max(1, G * ngroups))
-    return int(max(1, min(per, (n + 4095) // 4096)))
-
-
 HIST_LDS_BUDGET = 64 * 1024
-HIST_VERSION = 4
-# lane mapping: 2 = lane per row; 3 = lane = 8*row + feature; 4 = lane per row, rotated features + pipelined
-# loads; 5 = 4 with the per-update VALU work hoisted (hist4f_kernel)
+# lane mapping: 2 = lane per row (hist4_kernel); 5 = rotated features with the per-update VALU work hoisted
+# (hist4f_kernel, when its LDS slot table holds the level's id span)
 HIST_MAP = 5
-# regression histograms: one packed (count | offset sum) ds_add_u64 per update (hist4.hip hist4p_kernel)
-HIST_PACKED = False
 # hist v5 (row records): packed single-atomic regression histograms, trees per block group when packed
 HIST5_PACKED = True
 HIST5_PACKED_MAXT = 8
@@ -573,16 +554,8 @@ def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_
     S = len(slot_tree)
     G, n, _ = bins.shape
     T = node.shape[0]
-    Kst = 2 if mode == 0 else C
-    v4 = True  # the v2 / v3 float-atomic kernels (hist2.hip) were removed in round 2 (measured slower)
-    packed = v4 and HIST_PACKED and mode == 0 and v0 is None and HIST_MAP != 5
-    if v4:
-        kbits = mode | (4 if (mode == 0 and v0 is not None) else 0) | (16 if packed else 0)
-        per_slot = 8 * B * int(_lib.lib().cdna_hist4_bytes_per_bin(kbits, int(C)))
-        if packed:
-            lds_budget = min(lds_budget, 8192 * 8)  # register drain holds <= 16 cells per thread
-    else:
-        per_slot = Kst * 8 * B * 4
+    kbits = mode | (4 if (mode == 0 and v0 is not None) else 0)
+    per_slot = 8 * B * int(_lib.lib().cdna_hist4_bytes_per_bin(kbits, int(C)))
     SB = max(1, min(S, lds_budget // per_slot))
     if per_slot > 150 * 1024:
         raise ValueError("histogram too large for LDS (classes x bins)")
@@ -612,14 +585,14 @@ def _hist2(mode: int, bins, d, node, weight, v0, v1, label, C, build_slot, slot_
     v1 = None if v1 is None else v1.float().contiguous()
     label = None if label is None else label.int().contiguous()
     build_slot = build_slot.int().contiguous()
-    vmode = 2 if HIST_VERSION == 3 or HIST_MAP == 3 else (8 if HIST_MAP == 4 and HIST_VERSION >= 4 else 0)
-    if HIST_MAP == 5 and v4 and v0 is None and id_span_max >= span:
+    vmode = 0
+    if HIST_MAP == 5 and v0 is None and id_span_max >= span:
         vmode = 32  # fast rotated kernel (LDS slot table must hold the whole id span)
     wmax = 255 if weight is not None else 1
     qs0 = _fixed_scale(v0, n, wmax)
-    qs1 = _packed_scale(v1) if packed else _fixed_scale(v1, n, wmax, qmax_bits=30 if vmode == 32 else 62)
+    qs1 = _fixed_scale(v1, n, wmax, qmax_bits=30 if vmode == 32 else 62)
     iout = torch.zeros(out.shape, dtype=torch.int64, device=bins.device)
-    _lib.check(_lib.lib().cdna_hist4(kbits | (vmode if not packed else 0), _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0),
+    _lib.check(_lib.lib().cdna_hist4(kbits | vmode, _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0),
                                      _ptr(v1), _ptr(label), int(C), _ptr(build_slot), _ptr(fm), mw, S, B, SB,
                                      _ptr(grp), ng, nchunk, id_span_max, qs0, qs1, _ptr(iout),
                                      _stream(bins.device)), "cdna_hist4")
@@ -647,28 +620,10 @@ def hist_moments(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optiona
     out = torch.zeros((S, d, B, 2), dtype=torch.float64, device=bins.device)
     if S == 0 or n == 0:
         return out
-    if _native(bins) and id_tree is not None and HIST_VERSION >= 4:
+    if _native(bins):
+        assert id_tree is not None, "the GPU node-id histograms need id_tree (the tree of every active node)"
         return _hist2(0, bins, d, node, weight, v0, v1, None, 0, build_slot, slot_tree, id_tree, feat_mask, B,
                       lds_budget or HIST_LDS_BUDGET, out)
-    if _native(bins):
-        lds_budget = lds_budget or 64 * 1024
-        SB = max(1, min(S, lds_budget // (8 * B * 2 * 4)))
-        s0, t0, t1 = _slot_groups(np.asarray(slot_tree), SB)
-        ng = len(s0)
-        grp = torch.from_numpy(np.concatenate([s0, t0, t1])).to(bins.device)
-        nchunk = _plan_chunks(n, G, ng)
-        mw = 0 if feat_mask is None else feat_mask.shape[1]
-        fm = None if feat_mask is None else feat_mask.int().contiguous()
-        node = node.int().contiguous()
-        weight = None if weight is None else weight.to(torch.uint8).contiguous()
-        v0 = None if v0 is None else v0.float().contiguous()
-        v1 = v1.float().contiguous()
-        build_slot = build_slot.int().contiguous()
-        _lib.check(_lib.lib().cdna_hist_moments(
-            _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(v0), _ptr(v1), _ptr(build_slot), _ptr(fm), mw, S,
-            B, SB, ng, _ptr(grp), _ptr(grp) + 4 * ng, _ptr(grp) + 8 * ng, nchunk, _ptr(out), _stream(bins.device)),
-            "cdna_hist_moments")
-        return out
     bm = bins_to_matrix(bins, d)
     a0 = torch.ones(n, dtype=torch.float64) if v0 is None else v0.double()
     a1 = v1.double()
@@ -709,29 +664,10 @@ def hist_classes(bins: torch.Tensor, d: int, node: torch.Tensor, weight: Optiona
     out = torch.zeros((S, d, B, C), dtype=torch.float64, device=bins.device)
     if S == 0 or n == 0:
         return out
-    if _native(bins) and id_tree is not None and HIST_VERSION >= 4:
+    if _native(bins):
+        assert id_tree is not None, "the GPU node-id histograms need id_tree (the tree of every active node)"
         return _hist2(1, bins, d, node, weight, None, None, label, C, build_slot, slot_tree, id_tree, feat_mask, B,
                       lds_budget or HIST_LDS_BUDGET, out)
-    if _native(bins):
-        lds_budget = lds_budget or 64 * 1024
-        SB = max(1, min(S, lds_budget // (8 * B * C * 4)))
-        if 8 * B * C * 4 > 160 * 1024:
-            raise ValueError("too many classes x bins for the LDS histogram")
-        s0, t0, t1 = _slot_groups(np.asarray(slot_tree), SB)
-        ng = len(s0)
-        grp = torch.from_numpy(np.concatenate([s0, t0, t1])).to(bins.device)
-        nchunk = _plan_chunks(n, G, ng)
-        mw = 0 if feat_mask is None else feat_mask.shape[1]
-        fm = None if feat_mask is None else feat_mask.int().contiguous()
-        lab = label.int().contiguous()
-        node = node.int().contiguous()
-        weight = None if weight is None else weight.to(torch.uint8).contiguous()
-        build_slot = build_slot.int().contiguous()
-        _lib.check(_lib.lib().cdna_hist_classes(
-            _ptr(bins), n, d, T, _ptr(node), _ptr(weight), _ptr(lab), C, _ptr(build_slot), _ptr(fm), mw, S, B, SB,
-            ng, _ptr(grp), _ptr(grp) + 4 * ng, _ptr(grp) + 8 * ng, nchunk, _ptr(out), _stream(bins.device)),
-            "cdna_hist_classes")
-        return out
     bm = bins_to_matrix(bins, d)
     lab = label.long()
     fr = torch.arange(d)

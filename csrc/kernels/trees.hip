@@ -403,133 +403,6 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// K5 hist_build (moments): hist[slot][f][bin][2] += w * (v0, v1)
-// grid: linear; decoded (after XCD remap) as g fastest, then row chunk, then
-// slot group.  Slot group k covers slots [grp_s0[k], grp_s0[k]+SB) which all
-// live in trees [grp_t0[k], grp_t1[k]].
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void hist_moments_kernel(
-    const uint64_t* __restrict__ bins, int64_t n, int d, int T, const int* __restrict__ node,
-    const uint8_t* __restrict__ weight, const float* __restrict__ v0, const float* __restrict__ v1,
-    const int* __restrict__ build_slot, const uint32_t* __restrict__ feat_mask, int mask_words, int S, int B,
-    int SB, const int* __restrict__ grp_s0, const int* __restrict__ grp_t0, const int* __restrict__ grp_t1,
-    int nchunk, int64_t rows_per_chunk, double* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float lh[];  // [SB][8][B][2]
-  const int G = (d + 7) / 8;
-  const uint32_t nblk = gridDim.x;
-  const uint32_t w = cdna::xcd_remap(blockIdx.x, nblk);
-  const int g = (int)(w % G);
-  const int chunk = (int)((w / G) % nchunk);
-  const int grp = (int)(w / ((uint32_t)G * nchunk));
-  const int s0 = grp_s0[grp], t0 = grp_t0[grp], t1 = grp_t1[grp];
-  const int hsz = SB * 8 * B * 2;
-  for (int i = threadIdx.x; i < hsz; i += 256) lh[i] = 0.f;
-  __syncthreads();
-  const int64_t rb = (int64_t)chunk * rows_per_chunk;
-  int64_t re = rb + rows_per_chunk;
-  if (re > n) re = n;
-  const int fbase = g * 8;
-  const int mword = fbase >> 5, mshift = fbase & 31;
-  for (int64_t r = rb + threadIdx.x; r < re; r += 256) {
-    const uint64_t b8 = bins[(int64_t)g * n + r];
-    const float a0 = v0 ? v0[r] : 1.f;
-    const float a1 = v1[r];
-    for (int t = t0; t <= t1; ++t) {
-      const int id = node[(int64_t)t * n + r];
-      if (id < 0) continue;
-      const int ls = build_slot[id] - s0;
-      if (ls < 0 || ls >= SB) continue;
-      const float wt = weight ? (float)weight[(int64_t)t * n + r] : 1.f;
-      if (wt == 0.f) continue;
-      uint32_t m = 0xFFu;
-      if (feat_mask) m = (feat_mask[(int64_t)(ls + s0) * mask_words + mword] >> mshift) & 0xFFu;
-      const float x0 = wt * a0, x1 = wt * a1;
-      float* base = lh + (int64_t)ls * 8 * B * 2;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if ((m >> j) & 1u) {
-          const int bin = (int)((b8 >> (8 * j)) & 0xFFu);
-          float* p = base + (j * B + bin) * 2;
-          atomicAdd(p, x0);
-          atomicAdd(p + 1, x1);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < hsz; i += 256) {
-    const float v = lh[i];
-    if (v == 0.f) continue;
-    const int k = i & 1;
-    const int bin = (i >> 1) % B;
-    const int j = ((i >> 1) / B) & 7;
-    const int ls = (i >> 1) / (B * 8);
-    const int f = fbase + j;
-    const int slot = s0 + ls;
-    if (f < d && slot < S) atomicAdd(&out[(((int64_t)slot * d + f) * B + bin) * 2 + k], (double)v);
-  }
-}
-
-// K5 (classification): hist[slot][f][bin][c] += w for label class c
-__global__ __launch_bounds__(256) void hist_classes_kernel(
-    const uint64_t* __restrict__ bins, int64_t n, int d, int T, const int* __restrict__ node,
-    const uint8_t* __restrict__ weight, const int* __restrict__ label, int C, const int* __restrict__ build_slot,
-    const uint32_t* __restrict__ feat_mask, int mask_words, int S, int B, int SB, const int* __restrict__ grp_s0,
-    const int* __restrict__ grp_t0, const int* __restrict__ grp_t1, int nchunk, int64_t rows_per_chunk,
-    double* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float lh[];  // [SB][8][B][C]
-  const int G = (d + 7) / 8;
-  const uint32_t w = cdna::xcd_remap(blockIdx.x, gridDim.x);
-  const int g = (int)(w % G);
-  const int chunk = (int)((w / G) % nchunk);
-  const int grp = (int)(w / ((uint32_t)G * nchunk));
-  const int s0 = grp_s0[grp], t0 = grp_t0[grp], t1 = grp_t1[grp];
-  const int hsz = SB * 8 * B * C;
-  for (int i = threadIdx.x; i < hsz; i += 256) lh[i] = 0.f;
-  __syncthreads();
-  const int64_t rb = (int64_t)chunk * rows_per_chunk;
-  int64_t re = rb + rows_per_chunk;
-  if (re > n) re = n;
-  const int fbase = g * 8;
-  const int mword = fbase >> 5, mshift = fbase & 31;
-  for (int64_t r = rb + threadIdx.x; r < re; r += 256) {
-    const uint64_t b8 = bins[(int64_t)g * n + r];
-    const int c = label[r];
-    if (c < 0 || c >= C) continue;
-    for (int t = t0; t <= t1; ++t) {
-      const int id = node[(int64_t)t * n + r];
-      if (id < 0) continue;
-      const int ls = build_slot[id] - s0;
-      if (ls < 0 || ls >= SB) continue;
-      const float wt = weight ? (float)weight[(int64_t)t * n + r] : 1.f;
-      if (wt == 0.f) continue;
-      uint32_t m = 0xFFu;
-      if (feat_mask) m = (feat_mask[(int64_t)(ls + s0) * mask_words + mword] >> mshift) & 0xFFu;
-      float* base = lh + (int64_t)ls * 8 * B * C;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if ((m >> j) & 1u) {
-          const int bin = (int)((b8 >> (8 * j)) & 0xFFu);
-          atomicAdd(base + (j * B + bin) * C + c, wt);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < hsz; i += 256) {
-    const float v = lh[i];
-    if (v == 0.f) continue;
-    const int c = i % C;
-    const int bin = (i / C) % B;
-    const int j = (i / (C * B)) & 7;
-    const int ls = i / (C * B * 8);
-    const int f = fbase + j;
-    const int slot = s0 + ls;
-    if (f < d && slot < S) atomicAdd(&out[(((int64_t)slot * d + f) * B + bin) * C + c], (double)v);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // K7 row_partition: move every row of every tree to its child for the level.
 // split_feat[id] : -1 -> node became a leaf (row leaves the active set)
 // split_bin[id]  : continuous: left iff bin <= split_bin
@@ -961,37 +834,6 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
                      tmax, use_lds, miss_on, miss_val, out, ldo);
   const int e = (int)hipGetLastError();
   return e != 0 ? e : (rm_wanted ? 2 : 0);
-}
-
-// ngroups slot groups of SB slots (host-planned); out must be zeroed.
-CDNA_API int cdna_hist_moments(const uint64_t* bins, int64_t n, int d, int T, const int* node, const uint8_t* weight,
-                               const float* v0, const float* v1, const int* build_slot, const uint32_t* feat_mask,
-                               int mask_words, int S, int B, int SB, int ngroups, const int* grp_s0,
-                               const int* grp_t0, const int* grp_t1, int nchunk, double* out, hipStream_t st) {
-  if (n <= 0 || S <= 0) return 0;
-  const int G = (d + 7) / 8;
-  const int64_t rpc = (n + nchunk - 1) / nchunk;
-  const size_t lds = (size_t)SB * 8 * B * 2 * 4;
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  const unsigned nblk = (unsigned)G * nchunk * ngroups;
-  hipLaunchKernelGGL(hist_moments_kernel, dim3(nblk), dim3(256), lds, st, bins, n, d, T, node, weight, v0, v1,
-                     build_slot, feat_mask, mask_words, S, B, SB, grp_s0, grp_t0, grp_t1, nchunk, rpc, out);
-  return (int)hipGetLastError();
-}
-
-CDNA_API int cdna_hist_classes(const uint64_t* bins, int64_t n, int d, int T, const int* node, const uint8_t* weight,
-                               const int* label, int C, const int* build_slot, const uint32_t* feat_mask,
-                               int mask_words, int S, int B, int SB, int ngroups, const int* grp_s0,
-                               const int* grp_t0, const int* grp_t1, int nchunk, double* out, hipStream_t st) {
-  if (n <= 0 || S <= 0) return 0;
-  const int G = (d + 7) / 8;
-  const int64_t rpc = (n + nchunk - 1) / nchunk;
-  const size_t lds = (size_t)SB * 8 * B * C * 4;
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  const unsigned nblk = (unsigned)G * nchunk * ngroups;
-  hipLaunchKernelGGL(hist_classes_kernel, dim3(nblk), dim3(256), lds, st, bins, n, d, T, node, weight, label, C,
-                     build_slot, feat_mask, mask_words, S, B, SB, grp_s0, grp_t0, grp_t1, nchunk, rpc, out);
-  return (int)hipGetLastError();
 }
 
 CDNA_API int cdna_partition(const uint64_t* bins, int64_t n, int T, int* node, const int* split_feat,

@@ -170,15 +170,13 @@ def _tree_state(n, T, A, seed):
 
 
 def _set_hist_version(monkeypatch, ver):
-    """ver: 1 = node-id kernel (trees.hip), 4 = v4 integer kernel; 43 / 44 = v4 with the v3 / rotated lane
-    mapping; 45 = packed single-atomic regression kernel; 46 = fast rotated kernel (hist4f)."""
-    monkeypatch.setattr(K, "HIST_VERSION", 4 if ver in (4, 43, 44, 45, 46) else 1)
-    monkeypatch.setattr(K, "HIST_MAP", {43: 3, 44: 4, 45: 4, 46: 5}.get(ver, 2))
-    monkeypatch.setattr(K, "HIST_PACKED", ver == 45)
+    """ver: 4 = the v4 integer kernel with the lane-per-row mapping (hist4_kernel); 46 = the fast rotated
+    kernel (hist4f_kernel)."""
+    monkeypatch.setattr(K, "HIST_MAP", 5 if ver == 46 else 2)
 
 
 @pytest.mark.parametrize("B", [40, 256])
-@pytest.mark.parametrize("ver", [1, 4, 43, 44, 45, 46])
+@pytest.mark.parametrize("ver", [4, 46])
 def test_hist_moments(dev, B, ver, monkeypatch):
     n, d, T, A = 20000, 19, 3, 12
     g = torch.Generator().manual_seed(B)
@@ -191,7 +189,7 @@ def test_hist_moments(dev, B, ver, monkeypatch):
     y = torch.randn(n, generator=g)
     mw = (d + 31) // 32
     fm = torch.randint(0, 2 ** 31 - 1, (S, mw), generator=g, dtype=torch.int64).to(torch.int32)
-    id_tree = np.arange(A) // (A // T) if ver >= 2 else None
+    id_tree = np.arange(A) // (A // T)
     _set_hist_version(monkeypatch, ver)
     ref = K.hist_moments(bins, d, node, w, None, y, build, slot_tree, fm, B)
     out = K.hist_moments(bins.to(dev), d, node.to(dev), w.to(dev), None, y.to(dev), build.to(dev), slot_tree,
@@ -199,7 +197,7 @@ def test_hist_moments(dev, B, ver, monkeypatch):
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("ver", [1, 4, 43, 44, 46])
+@pytest.mark.parametrize("ver", [4, 46])
 def test_hist_classes(dev, ver, monkeypatch):
     n, d, T, A, C, B = 10000, 10, 2, 8, 3, 32
     g = torch.Generator().manual_seed(11)
@@ -210,14 +208,14 @@ def test_hist_classes(dev, ver, monkeypatch):
     w = K.poisson_weights(T, n, 5, 0, 1.0)
     lab = torch.randint(0, C, (n,), generator=g, dtype=torch.int32)
     ref = K.hist_classes(bins, d, node, w, lab, C, build, slot_tree, None, B)
-    id_tree = np.arange(A) // (A // T) if ver >= 2 else None
+    id_tree = np.arange(A) // (A // T)
     _set_hist_version(monkeypatch, ver)
     out = K.hist_classes(bins.to(dev), d, node.to(dev), w.to(dev), lab.to(dev), C, build.to(dev), slot_tree, None,
                          B, id_tree=id_tree).cpu()
     assert torch.allclose(out, ref)
 
 
-@pytest.mark.parametrize("ver", [1, 4, 44])
+@pytest.mark.parametrize("ver", [4])
 def test_hist_moments_v0(dev, ver, monkeypatch):
     """Moments with a real-valued v0 plane (XGBoost hessians) and no bootstrap weights."""
     n, d, T, A, B = 30000, 13, 2, 6, 64
@@ -235,7 +233,7 @@ def test_hist_moments_v0(dev, ver, monkeypatch):
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("ver", [4, 45, 46])
+@pytest.mark.parametrize("ver", [4, 46])
 def test_hist_v4_deterministic(dev, ver, monkeypatch):
     """Integer histograms are bit-identical across launches with different chunkings."""
     n, d, T, A, B = 50000, 16, 2, 4, 32
@@ -869,17 +867,6 @@ def test_hist_assemble_many_nodes(dev):
     ref = K.hist_assemble(Hb, 2.0 ** 5, prev, slot, parent, sib)
     out = K.hist_assemble(Hb.to(dev), 2.0 ** 5, prev.to(dev), slot, parent, sib).cpu()
     assert torch.equal(out, ref)
-
-
-def test_planar_bins(dev):
-    g = torch.Generator().manual_seed(1)
-    X = torch.randn(4099, 21, generator=g)
-    thr, nthr = _thresholds(X, 40)
-    bins = K.binize(X.to(dev), thr.to(dev), nthr.to(dev))
-    bp, ldp = K.planar_bins(bins)
-    ref = K.bins_to_matrix(bins.cpu(), 21).t()
-    assert ldp % K.MFMA_STAGE == 0 and ldp >= 4099
-    assert torch.equal(bp[:21, :4099].cpu(), ref.to(torch.uint8))
 
 
 @pytest.mark.parametrize("dtype,card", [(torch.int64, 7), (torch.int64, 300000), (torch.float64, 1000),
