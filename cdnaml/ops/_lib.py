@@ -102,7 +102,7 @@ _SIGS = {
     "cdna_gram": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int,
                    c_void_p], c_int),
     "cdna_binize": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,
-                     c_int, c_int64, c_void_p],
+                     c_int, c_int64, c_int, c_void_p],
                     c_int),
     "cdna_hist4": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,

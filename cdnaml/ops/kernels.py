@@ -308,6 +308,11 @@ def quantile_thresholds_dev(samp: torch.Tensor, max_bins: int):
 
 
 # --------------------------------------------------------------------- K4
+# binize v6: the per-feature uniform-grid LUT narrows the threshold search to the few thresholds of the value's cell
+# (trees.hip binize5_kernel<LUT>); False: the 6-step LDS binary search of v5
+BINIZE_LUT = True
+
+
 def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Optional[float] = None,
            want_rm: bool = False, rm_layout: str = "std", out_full=None, row0: int = 0):
     """Raw features -> uint8 bins in feature-group-major layout [G, n, 8].
@@ -355,7 +360,7 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Opti
         if n:
             rc = _lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, int(miss_on),
                                         miss_val, optr, _ptr(rm) if rm is not None else None,
-                                        -10 if s10 else Gs, ldo, _stream(X.device))
+                                        -10 if s10 else Gs, ldo, int(BINIZE_LUT), _stream(X.device))
             if rc == 2:  # the fallback kernel ran: no row-major copy
                 rm = None
             else:

@@ -244,27 +244,81 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int STEPS, int RPL>
+// LUT (binize v6): the threshold search narrowed by a per-feature uniform grid of kLutCells cells over
+// [t_0, t_last].  cell(v) = int(clamp((v - t_0) * scale, 0, C - 1)) with the subtraction and the product rounded
+// separately (no contraction) is monotone in v, so for x in cell c every threshold of a lower cell is < x and
+// every threshold of a higher cell is > x: bin(x) = base[c] + #{thresholds of cell c that are < x}, where base[c] =
+// #{t_j : cell(t_j) < c} -- the same count as the binary search, exactly, whatever the rounding.  The grid is
+// built in LDS by every block from the device thresholds (no host round trip); the refinement walks the sorted
+// table kmax = max thresholds per cell steps (Gaussian-like columns at 40 bins: 1-2) instead of the 6 search
+// steps, and falls back to a binary search of the sorted table when kmax > kLutMaxK (heavy-tailed columns).
+constexpr int kLutCells = 64;
+constexpr int kLutMaxK = 6;
+
+template <int STEPS, int RPL, bool LUT>
 __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                        const float* __restrict__ thr, const int* __restrict__ nthr,
                                                        int tmax, int miss_on, float miss_val,
                                                        uint64_t* __restrict__ out, uint64_t* __restrict__ rm, int Gs,
                                                        int64_t ldo) {
+#pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float smf5[];
   constexpr int P = 1 << STEPS, RT = 64 * RPL, TP = 17;  // RPL rows per lane
+  constexpr int C = kLutCells;
   float* sthr = smf5;                                                          // [d][P]
-  uint64_t* tile = reinterpret_cast<uint64_t*>(sthr + (size_t)((d * P + 3) & ~3));  // [RT][TP]
-  // Table layout by search step: step s (step 2^s) only ever probes cand = (2k + 1) 2^s, so entry cand - 1 is
-  // stored at q = P - 2^(STEPS - s) + k -- each step's candidates are consecutive words, and the 32 lanes of a
-  // read group hit distinct banks (the plain layout put cand and cand + 32 on one bank: 43 % of the LDS
-  // cycles were conflicts).  The last word (cand = P) is never probed.
-  for (int i = threadIdx.x; i < d * P; i += blockDim.x) {
-    const int f = i >> STEPS, q = i & (P - 1);
-    int sg = 0;
-    while (sg < STEPS - 1 && q >= P - (P >> (sg + 1))) ++sg;
-    const int k = q - (P - (P >> sg));
-    const int c = ((2 * k + 1) << sg) - 1;  // threshold index held at q
-    sthr[i] = (q < P - 1 && c < nthr[f] && c < tmax) ? thr[(size_t)f * tmax + c] : __builtin_inff();
+  uint8_t* sbase = reinterpret_cast<uint8_t*>(sthr + (size_t)((d * P + 3) & ~3));  // LUT: [d][C]
+  float* sprm = reinterpret_cast<float*>(sbase + (LUT ? (size_t)d * C : 0));        // LUT: [d][2] lo, scale
+  uint64_t* tile = reinterpret_cast<uint64_t*>(sprm + (LUT ? (size_t)((2 * d + 3) & ~3) : 0));  // [RT][TP]
+  __shared__ int s_kf[LUT ? 128 : 1];  // LUT: largest threshold count of a cell, per feature (d <= 128)
+  if (LUT) {
+    // sorted thresholds, +inf padded: the refinement reads t[b] for b <= nthr < P
+    for (int f = threadIdx.x; f < d; f += blockDim.x) s_kf[f] = 0;
+    for (int i = threadIdx.x; i < d * P; i += blockDim.x) {
+      const int f = i >> STEPS, q = i & (P - 1);
+      sthr[i] = (q < nthr[f] && q < tmax) ? thr[(size_t)f * tmax + q] : __builtin_inff();
+    }
+    __syncthreads();
+    for (int f = threadIdx.x; f < d; f += blockDim.x) {
+      const int nt = nthr[f] < tmax ? nthr[f] : tmax;
+      float lo = 0.f, sc = 0.f;
+      if (nt >= 1) lo = sthr[f * P];
+      if (nt >= 3 && lo <= -3.0e38f) lo = sthr[f * P + 1];  // XGBoost's -FLT_MAX missing-value threshold: off-grid
+      if (nt >= 2) {
+        const float span = sthr[f * P + nt - 1] - lo;
+        sc = (float)C / span;
+        if (!(sc > 0.f) || !(sc < __builtin_inff())) sc = 0.f;  // one cell: the walk covers every threshold
+      }
+      sprm[2 * f] = lo;
+      sprm[2 * f + 1] = sc;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < d * C; e += blockDim.x) {
+      const int f = e / C, c = e - f * C;
+      const int nt = nthr[f] < tmax ? nthr[f] : tmax;
+      const float lo = sprm[2 * f], sc = sprm[2 * f + 1];
+      int below = 0, in = 0;
+      for (int j = 0; j < nt; ++j) {
+        const float v = fminf(fmaxf((sthr[f * P + j] - lo) * sc, 0.f), (float)(C - 1));
+        const int cj = (int)v;
+        below += cj < c;
+        in += cj == c;
+      }
+      sbase[e] = (uint8_t)below;
+      if (in) atomicMax(&s_kf[f], in);
+    }
+  } else {
+    // Table layout by search step: step s (step 2^s) only ever probes cand = (2k + 1) 2^s, so entry cand - 1 is
+    // stored at q = P - 2^(STEPS - s) + k -- each step's candidates are consecutive words, and the 32 lanes of a
+    // read group hit distinct banks (the plain layout put cand and cand + 32 on one bank: 43 % of the LDS
+    // cycles were conflicts).  The last word (cand = P) is never probed.
+    for (int i = threadIdx.x; i < d * P; i += blockDim.x) {
+      const int f = i >> STEPS, q = i & (P - 1);
+      int sg = 0;
+      while (sg < STEPS - 1 && q >= P - (P >> (sg + 1))) ++sg;
+      const int k = q - (P - (P >> sg));
+      const int c = ((2 * k + 1) << sg) - 1;  // threshold index held at q
+      sthr[i] = (q < P - 1 && c < nthr[f] && c < tmax) ? thr[(size_t)f * tmax + c] : __builtin_inff();
+    }
   }
   if (rm)
     for (int i = threadIdx.x; i < RT * TP; i += blockDim.x) tile[i] = 0ull;  // words g >= G stay 0 (row padding)
@@ -281,6 +335,22 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
     fb[j] = f * P;  // feature f's table
   }
   __syncthreads();
+  float llo[8], lsc[8];
+  int kmax = 0;
+  if (LUT) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 8 * g + j < d ? 8 * g + j : d - 1;
+      llo[j] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sprm[2 * f])));
+      lsc[j] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sprm[2 * f + 1])));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 8 * g + j < d ? 8 * g + j : d - 1;
+      kmax = kmax > s_kf[f] ? kmax : s_kf[f];
+    }
+    kmax = __builtin_amdgcn_readfirstlane(kmax);  // this wave's 8 features
+  }
   const float4* __restrict__ X4 = reinterpret_cast<const float4*>(X);
   const int64_t ldx4 = ldx >> 2;
   const int64_t ntiles = (n + RT - 1) / RT;
@@ -292,13 +362,31 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
       if (miss_on && (x[j] != x[j] || x[j] == miss_val)) x[j] = -__builtin_inff();
       lo[j] = 0;
     }
+    if (!LUT) {
 #pragma unroll
-    for (int s = STEPS - 1; s >= 0; --s) {
-      const int step = 1 << s, base = P - (P >> s);
+      for (int s = STEPS - 1; s >= 0; --s) {
+        const int step = 1 << s, base = P - (P >> s);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int cand = lo[j] + step;  // lo is a multiple of 2^(s+1)
+          lo[j] = sthr[fb[j] + base + (lo[j] >> (s + 1))] < x[j] ? cand : lo[j];
+        }
+      }
+    } else if (kmax <= kLutMaxK) {  // wave-uniform
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int cand = lo[j] + step;  // lo is a multiple of 2^(s+1)
-        lo[j] = sthr[fb[j] + base + (lo[j] >> (s + 1))] < x[j] ? cand : lo[j];
+        const float v = fminf(fmaxf((x[j] - llo[j]) * lsc[j], 0.f), (float)(C - 1));
+        lo[j] = sbase[(fb[j] >> STEPS) * C + (int)v];
+      }
+      for (int s = 0; s < kmax; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lo[j] += sthr[fb[j] + lo[j]] < x[j] ? 1 : 0;
+      }
+    } else {  // many thresholds in one cell: binary search of the sorted table
+#pragma unroll
+      for (int s = STEPS - 1; s >= 0; --s) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lo[j] += sthr[fb[j] + lo[j] + (1 << s) - 1] < x[j] ? (1 << s) : 0;
       }
     }
     uint64_t word = 0;
@@ -762,7 +850,7 @@ inline unsigned grid_for(int64_t n, int per, unsigned cap) {
 // ldo: row stride of out's [G][ldo] word planes (0: n) -- chunks of a streamed fit bin into their row slice of
 // the full bins (out = base + row0, ldo = total rows; rm = row-major base + row0).
 CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const float* thr, const int* nthr, int tmax,
-                         int miss_on, float miss_val, uint64_t* out, uint64_t* rm, int Gs, int64_t ldo,
+                         int miss_on, float miss_val, uint64_t* out, uint64_t* rm, int Gs, int64_t ldo, int lut,
                          hipStream_t st) {
   if (ldo <= 0) ldo = n;
   if (ldo < n) return (int)hipErrorInvalidValue;
@@ -779,8 +867,10 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
     if (steps < 4) steps = 4;
     const int G = (d + 7) / 8;
     constexpr int rpl = 1;  // 2 rows per lane (two tiles of registers, a 128-row LDS tile): 18.7 vs 15.4 ms
-    const size_t lds = (size_t)((d * (1 << steps) + 3) & ~3) * 4 + (size_t)64 * rpl * 17 * 8;
-    if (steps <= 8 && lds <= 150 * 1024) {
+    const bool use_lut = lut != 0;
+    const size_t lds = (size_t)((d * (1 << steps) + 3) & ~3) * 4 + (size_t)64 * rpl * 17 * 8 +
+                       (use_lut ? (size_t)d * kLutCells + (size_t)((2 * d + 3) & ~3) * 4 : 0);
+    if (steps <= 8 && lds <= 150 * 1024 && (!use_lut || d <= 128)) {
       auto launch = [&](auto kern) {
         if (lds > 64 * 1024)
           (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -788,12 +878,22 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
         hipLaunchKernelGGL(kern, dim3(grid_for(n, 64 * rpl, 1024)), dim3(64 * G), lds, st, X, n, d, ldx, thr, nthr,
                            tmax > 0 ? tmax : 1, miss_on, miss_val, out, rm, Gs, ldo);
       };
-      switch (steps) {
-        case 4: launch(binize5_kernel<4, rpl>); break;
-        case 5: launch(binize5_kernel<5, rpl>); break;
-        case 6: launch(binize5_kernel<6, rpl>); break;
-        case 7: launch(binize5_kernel<7, rpl>); break;
-        default: launch(binize5_kernel<8, rpl>); break;
+      if (use_lut) {
+        switch (steps) {
+          case 4: launch(binize5_kernel<4, rpl, true>); break;
+          case 5: launch(binize5_kernel<5, rpl, true>); break;
+          case 6: launch(binize5_kernel<6, rpl, true>); break;
+          case 7: launch(binize5_kernel<7, rpl, true>); break;
+          default: launch(binize5_kernel<8, rpl, true>); break;
+        }
+      } else {
+        switch (steps) {
+          case 4: launch(binize5_kernel<4, rpl, false>); break;
+          case 5: launch(binize5_kernel<5, rpl, false>); break;
+          case 6: launch(binize5_kernel<6, rpl, false>); break;
+          case 7: launch(binize5_kernel<7, rpl, false>); break;
+          default: launch(binize5_kernel<8, rpl, false>); break;
+        }
       }
       return (int)hipGetLastError();
     }

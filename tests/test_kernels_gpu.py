@@ -108,6 +108,33 @@ def test_binize(dev):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("lut", [True, False])
+def test_binize_lut_columns(dev, lut, monkeypatch):
+    """binize v6 (uniform-grid LUT + a short walk of the value's cell) equals the host count #{t < x} exactly on
+    columns the grid fits badly: heavy tails (lognormal, Cauchy: the wave falls back to the binary search),
+    a constant column (one threshold), two thresholds, a narrow far-from-zero column, +-inf / NaN values and
+    values equal to thresholds; the row-major seg10 copy too."""
+    monkeypatch.setattr(K, "BINIZE_LUT", lut)
+    g = torch.Generator().manual_seed(9)
+    n, d = 20003, 24
+    X = torch.randn(n, d, generator=g)
+    X[:, 1] = torch.exp(3 * X[:, 1])                          # lognormal
+    X[:, 2] = torch.tan(3.1 * (torch.rand(n, generator=g) - 0.5))  # Cauchy-like
+    X[:, 3] = 7.0                                             # constant
+    X[:, 4] = torch.randint(0, 3, (n,), generator=g).float()  # three values
+    X[:, 5] = 37.8 + 0.02 * X[:, 5]                           # latitude-like
+    X[:, 6] = torch.round(X[:, 6] * 4) / 4                    # ties with the thresholds
+    X[::97, 7] = float("inf")
+    X[::89, 7] = float("-inf")
+    X[::13, 8] = float("nan")
+    thr, nthr = _thresholds(X.nan_to_num(0.0, posinf=0.0, neginf=0.0), 40)
+    X[:50, 6] = thr[6, 0]                                     # exactly on a threshold
+    ref = K.binize(X, thr, nthr)
+    out, rm = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), want_rm=True, rm_layout="s10")
+    assert torch.equal(out.cpu(), ref)
+    assert torch.equal(rm.cpu(), K.bins_seg10(ref.to(dev), d).cpu())
+
+
 @pytest.mark.parametrize("max_bins,s,f32", [(40, 10000, False), (256, 16384, False), (2, 3000, False),
                                             (32, 777, False), (40, 10000, True), (40, 12288, True),
                                             (40, 12289, True), (256, 5000, True)])
