@@ -731,9 +731,11 @@ def _early_side_work(num_trees, bootstrap, rate, want_label_max=True, codes_ok=F
             if bootstrap and num_trees > 1:
                 if codes_ok and K.POISSON_CODES:
                     # the draws written straight as the engine's row codes + their max (no uint8 weights, no
-                    # codes_init pass, no separate max reduction over T x n bytes)
+                    # codes_init pass, no separate max reduction over T x n bytes); lazy: the trainer's level-0
+                    # root histogram draws them itself when it can (K.POISSON_FUSED), else they run here on demand
                     with torch.cuda.stream(side if K.POISSON_STREAM == "side" else torch.cuda.current_stream(dev)):
-                        early["codes"] = K.BootstrapCodes(num_trees, n, seed_, off, rate, dev)
+                        early["codes"] = K.BootstrapCodes(num_trees, n, seed_, off, rate, dev,
+                                                          lazy=K.POISSON_FUSED and K.POISSON_STREAM != "side")
                 else:
                     early["w"] = _poisson_side(num_trees, n, seed_, off, rate, dev, join=False)
                     K.prefetch_max(early["w"], stream=side)

@@ -1428,6 +1428,7 @@ class ForestTrainer:
         stats_rows, weights = st.stats_rows, st.weights
         st.codes = st.node = st.perm = None
         st.wmax = 1
+        st.lazy_codes = None  # a lazy K.BootstrapCodes: the level-0 root histogram draws the codes
         if st.use_seg:
             w1 = None if weights is None else weights.reshape(-1)
             st.wmax = int(w1.max().item()) if (w1 is not None and w1.numel()) else 1
@@ -1446,6 +1447,8 @@ class ForestTrainer:
         elif st.use_codes:
             if codes_pre is not None:
                 st.codes, st.wmax = codes_pre.codes, codes_pre.wmax()
+                if getattr(codes_pre, "pending", False):
+                    st.lazy_codes = codes_pre
             else:
                 st.codes, st.wmax = K.codes_init_max(weights, T, n, dev)
             if st.use_mseg:
@@ -1538,6 +1541,16 @@ class ForestTrainer:
         root_rows = self._root_rows()
         root_ok = (root_rows is not None and st.use_mseg and (depth >= 1 or MSEG_L0) and st.rec_ok and
                    S > 0 and np.bincount(slot_tree, minlength=T).max() <= 1)
+        draw = None
+        if st.lazy_codes is not None:
+            # the bootstrap draws are still pending: the level-0 root histogram (seg10 rows) draws and writes the
+            # codes itself, any other path materialises them first
+            if depth == 0 and root_ok and root_rows is data.bins_s10 and K.POISSON_FUSED and S == T:
+                draw = st.lazy_codes.draw_args()
+            else:
+                st.lazy_codes.materialize()
+            st.lazy_codes.mark_drawn()
+            st.lazy_codes = None
         if root_ok:
             sl_node = build_ids - tfirst.numpy()[slot_tree]  # the slot's local node in its tree's codes
             # one launch for every slot, then the level's one all-reduce: these levels hold one node per
@@ -1545,7 +1558,7 @@ class ForestTrainer:
             # of a 1.25e7-row shard would launch ~1 round of blocks each (half of it idle)
             lv.Hb = K.seg_hist_codes(root_rows, d, B, st.codes, stats_rows["v1"], st.mseg_scales[1], wmax,
                                      slot_tree, sl_node, 0, S,
-                                     torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev))
+                                     torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev), draw=draw)
             lv.hist_raw_scale = st.mseg_raw
         elif st.use_mseg and (depth >= 1 or MSEG_L0):
             # gather the rows of the built nodes into slot segments, then segment histograms of packed

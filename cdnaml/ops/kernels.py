@@ -152,25 +152,63 @@ POISSON_EARLY_MAX = 500000000.0
 POISSON_EARLY_BLOCKS = 512
 
 
+def poisson_max_draw(rate: float) -> int:
+    """The largest bootstrap weight the tabulated Poisson draws can produce at ``rate`` (-1: no static bound)."""
+    return int(_lib.lib().cdna_poisson_max_draw(float(rate)))
+
+
+# level 0 of a bootstrapped forest draws its Poisson weights inside the root histogram kernel (seg.hip RootDraw)
+# instead of a draws kernel in series ahead of it
+POISSON_FUSED = True
+
+
 class BootstrapCodes:
     """Poisson bootstrap draws written straight as the tree engine's row codes (GPU): ``codes`` [T, n] int16
     (weight << 8 | 0, 0xFF for weight 0 -- codes_init's format) and the largest weight, copied to the host behind
     the kernel (``wmax()`` waits for that copy only).  ``weights()`` derives the uint8 multiplicities for the
-    paths that need them (bit-identical to poisson_weights)."""
+    paths that need them (bit-identical to poisson_weights).
 
-    def __init__(self, T: int, n: int, seed: int, offset: int, rate: float, device, grid_blocks: int = 0):
+    lazy: nothing is launched yet when the draws have a static bound (``poisson_max_draw``): the trainer's level-0
+    root histogram draws and writes the codes itself (``draw_args`` / ``mark_drawn``), any other first reader calls
+    ``materialize`` (the draws kernel); ``wmax()`` is then the static bound."""
+
+    def __init__(self, T: int, n: int, seed: int, offset: int, rate: float, device, grid_blocks: int = 0,
+                 lazy: bool = False):
         dev = torch.device(device)
+        self.T, self.n, self.seed, self.offset, self.rate, self.dev = T, n, int(seed), int(offset), float(rate), dev
         self.codes = torch.empty((T, n), dtype=torch.int16, device=dev)
-        wm = torch.zeros(1, dtype=torch.int32, device=dev)
-        _lib.check(_lib.lib().cdna_poisson(None, T, n, int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset), float(rate),
-                                           _ptr(self.codes), _ptr(wm), int(grid_blocks), _stream(dev)),
-                   "cdna_poisson(codes)")
-        self._wmax = _PendingScalar(wm, torch.cuda.current_stream(dev))
+        self._bound = poisson_max_draw(rate) if lazy else -1
+        self.pending = self._bound >= 1
+        self._wmax = None
+        if not self.pending:
+            self._launch(grid_blocks)
+
+    def _launch(self, grid_blocks: int = 0) -> None:
+        wm = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        _lib.check(_lib.lib().cdna_poisson(None, self.T, self.n, self.seed & 0xFFFFFFFFFFFFFFFF, self.offset,
+                                           self.rate, _ptr(self.codes), _ptr(wm), int(grid_blocks),
+                                           _stream(self.dev)), "cdna_poisson(codes)")
+        self._wmax = _PendingScalar(wm, torch.cuda.current_stream(self.dev))
+
+    def draw_args(self):
+        """(seed, row offset, rate) for a kernel that draws the pending codes itself, else None."""
+        return (self.seed, self.offset, self.rate) if self.pending else None
+
+    def mark_drawn(self) -> None:
+        self.pending = False
+
+    def materialize(self) -> None:
+        if self.pending:
+            self._launch()
+            self.pending = False
 
     def wmax(self) -> int:
+        if self._bound >= 1:
+            return self._bound
         return max(1, int(self._wmax.get()))
 
     def weights(self) -> torch.Tensor:
+        self.materialize()
         return ((self.codes.to(torch.int32) >> 8) & 0xFF).to(torch.uint8)
 
 
@@ -1453,12 +1491,16 @@ def _num_cus(dev) -> int:
 
 def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, v1: torch.Tensor, qs1: float,
                    wmax: int, slot_tree: np.ndarray, slot_node: np.ndarray, s0: int, s1: int,
-                   out: torch.Tensor) -> torch.Tensor:
+                   out: torch.Tensor, draw: Optional[tuple] = None) -> torch.Tensor:
     """Record histograms of slots [s0, s1) straight from the row codes (GPU, seg10 rows), for levels with at most
     one built node per tree: slot s is local node ``slot_node[s]`` of tree ``slot_tree[s]`` (level 0: every root,
     node 0).  Adds the exact int64 sums (count, sum w * q) into ``out`` [s1 - s0, d, B, 2] (zeroed by the caller)
     -- the same integers as ``codes_compact(rec_scale=qs1)`` + ``seg_hist(rec=True, raw=True)``, without
-    materialising the level's 8-byte records."""
+    materialising the level's 8-byte records.
+
+    draw (level 0 of a bootstrapped forest, B <= 40): ``(seed, row offset, rate)`` -- the kernel draws every row's
+    Poisson weight itself and WRITES ``codes`` (the lazy :class:`BootstrapCodes`); ``wmax`` must then be the draws'
+    static bound (``poisson_max_draw``)."""
     T, n = codes.shape
     wide = 80 < B <= 256
     # B <= 40: seg10 rows, six-items-per-wave kernel; 80 < B <= 256 (boosting): standard row-major rows, lane4
@@ -1524,8 +1566,13 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
                                                       _ptr(out), _stream(codes.device)), "cdna_seg_hist_root_wide")
         return out
     wt, si = upload(codes.device, work.reshape(-1), sinfo)
+    if draw is not None:
+        assert np.array_equal(np.sort(st[s0:s1]), np.arange(T)) and not np.any(sn[s0:s1]), "draws need every root"
+    seed, off, rate = draw if draw is not None else (0, 0, 1.0)
     _lib.check(_lib.lib().cdna_seg_hist_root(_ptr(bins_s10), n, d, B, _ptr(codes), _ptr(v1c), float(qs1), _ptr(wt),
-                                             len(work), _ptr(si), s0, _ptr(out), _stream(codes.device)),
+                                             len(work), _ptr(si), s0, _ptr(out), int(draw is not None),
+                                             int(seed) & 0xFFFFFFFFFFFFFFFF, int(off), float(rate),
+                                             _stream(codes.device)),
                "cdna_seg_hist_root")
     return out
 

@@ -107,6 +107,48 @@ __host__ __device__ __forceinline__ uint32_t poisson_from_uniform(double u, doub
   return k;
 }
 
+// Tabulated CDF F_0..F_{kCdf-1} of poisson_from_uniform's recurrence (built on the host with the same double
+// operations in the same order, so every draw is bit-identical to the loop): u > F_k  <=>  w > floor(F_k 2^32)
+// for the 32-bit uniform w = u 2^32, saturated at 2^32 - 1 (never exceeded).
+constexpr int kCdf = 32;
+struct PoissonCdf {
+  uint32_t T[kCdf];
+};
+
+inline PoissonCdf poisson_cdf(double rate) {
+  PoissonCdf cdf;
+  double p = exp(-rate), F = p;
+  for (int k = 0; k < kCdf; ++k) {
+    const double x = F * 4294967296.0;  // F after k loop iterations, scaled exactly
+    cdf.T[k] = x >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)floor(x);
+    p *= rate / (double)(k + 1);
+    F += p;
+  }
+  return cdf;
+}
+
+// The draw of the 32-bit uniform w: #{k : w > T[k]} (8 unrolled compares, then the rare tail); when the table does
+// not saturate within kCdf entries the recurrence itself.
+__device__ __forceinline__ uint32_t poisson_draw(uint32_t w, const PoissonCdf& cdf, double rate) {
+  uint32_t kk = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) kk += w > cdf.T[i] ? 1u : 0u;
+  if (kk == 8u) {
+    while (kk < (uint32_t)kCdf && w > cdf.T[kk]) ++kk;
+    if (kk == (uint32_t)kCdf) kk = poisson_from_uniform((double)w * (1.0 / 4294967296.0), rate);
+  }
+  return kk > 255u ? 255u : kk;
+}
+
+// Philox stream / constant of the bootstrap draws of tree t (misc.hip poisson_kernel, cdnaml/ops/philox.py)
+__device__ __forceinline__ uint32_t bootstrap_uniform(uint64_t seed, uint64_t gi, int t) {
+  const uint64_t q = gi >> 2;
+  const u32x4 r = philox4x32_10(u32x4{(uint32_t)q, (uint32_t)(q >> 32), 0x100u + (uint32_t)t, 0xB00Fu},
+                                (uint32_t)seed, (uint32_t)(seed >> 32));
+  const uint32_t j = (uint32_t)(gi & 3u);
+  return j == 0 ? r.x : (j == 1 ? r.y : (j == 2 ? r.z : r.w));
+}
+
 // XCD-aware bijective block remap (blocks that share an XCD get contiguous work).
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblk) {
   const uint32_t nx = 8;

@@ -2,6 +2,9 @@
 // K14 auc score histogram.
 #include "common.h"
 
+using cdna::kCdf;
+using cdna::PoissonCdf;
+
 namespace {
 
 inline unsigned grid_for(int64_t n, int per, unsigned cap) {
@@ -59,16 +62,8 @@ __global__ __launch_bounds__(256) void normal_f32_kernel(float* __restrict__ out
 
 // Poisson(rate) bootstrap multiplicities for T trees: out[t][i], stream = t + 1
 // (rate >= 1 with no bootstrap is handled on the host as all-ones).
-// The CDF F_0..F_{kCdf-1} of poisson_from_uniform's recurrence is tabulated on
-// the host (same double operations in the same order, so every draw is
-// bit-identical to the loop): the kernel does compares only, no exp / divide.
-constexpr int kCdf = 32;
-struct PoissonCdf {
-  // u > F_k  <=>  w > floor(F_k 2^32) for the 32-bit uniform w = u 2^32 (exact: F_k 2^32 is exact in double
-  // and w is an integer), so the draws compare integers; saturated at 2^32 - 1 (never exceeded)
-  uint32_t T[kCdf];
-};
-
+// The CDF of poisson_from_uniform's recurrence is tabulated on the host (common.h poisson_cdf): the kernel does
+// compares only, no exp / divide.
 // One Philox4x32-10 call yields the 32-bit uniforms of 4 consecutive global
 // elements (quad q = index >> 2, word = index & 3): 4x fewer Philox rounds
 // than one 53-bit double per draw (this kernel shares the GPU with the binning
@@ -438,17 +433,7 @@ CDNA_API int cdna_poisson(uint8_t* out, int T, int64_t n, uint64_t seed, uint64_
                           uint16_t* codes, unsigned* wmax, int grid_blocks, hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
   if (codes && !wmax) return (int)hipErrorInvalidValue;
-  PoissonCdf cdf;
-  {
-    // same double operations in the same order as poisson_from_uniform's recurrence
-    double p = exp(-rate), F = p;
-    for (int k = 0; k < kCdf; ++k) {
-      const double x = F * 4294967296.0;  // F after k loop iterations, scaled exactly
-      cdf.T[k] = x >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)floor(x);
-      p *= rate / (double)(k + 1);
-      F += p;
-    }
-  }
+  const PoissonCdf cdf = cdna::poisson_cdf(rate);
   // interior quads as dword stores when every tree row starts 4-byte aligned
   const int packed = (offset % 4 == 0) && (n % 4 == 0) &&
                      (codes ? reinterpret_cast<uintptr_t>(codes) % 8 == 0 : reinterpret_cast<uintptr_t>(out) % 4 == 0);

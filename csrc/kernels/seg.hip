@@ -617,11 +617,23 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_kernel(const SegHistArgs
 // by ~0.63 x 20 trees: the XCD-aware work order puts the trees of one row chunk
 // on one XCD back to back, so the L2 serves most of them).  Same int64 sums as
 // the record path (the sums do not depend on the item order).
-template <int BP>
+// DRAW (level 0 of a bootstrapped forest): the rows' Poisson bootstrap weights are drawn here (the same Philox
+// uniforms and tabulated CDF as misc.hip poisson_kernel, keyed by global row id) instead of read from the codes,
+// and the level's codes (weight << 8 | 0, 0xFF for weight 0) are written for the partition -- no separate draws
+// kernel in series ahead of the histogram: the ~100 VALU instructions of a window's Philox calls run in the
+// shadow of its ~70 ds_add_u64 (the kernel is LDS-bound, its VALU mostly idle).
+struct RootDraw {
+  uint64_t seed, offset;  // Philox key, global row id of local row 0
+  double rate;
+  cdna::PoissonCdf cdf;
+};
+
+template <int BP, bool DRAW>
 __global__ __launch_bounds__(1024) void seg_hist_lane10_root_kernel(const SegHistArgs a, const uint8_t* __restrict__ bins8,
                                                                     const uint16_t* __restrict__ codes,
                                                                     const float* __restrict__ v1, float qs1,
-                                                                    const int* __restrict__ sinfo, int slot0) {
+                                                                    const int* __restrict__ sinfo, int slot0,
+                                                                    const RootDraw dr) {
   constexpr int TH = 1024, NW = TH / 64, U = 16, IPW = 6, NI = IPW * U, RING = 256;  // NI - 1 + 64 < RING
   constexpr int PLANE = BP * 32;
   __shared__ __attribute__((aligned(16))) unsigned long long h[10 * PLANE];  // [10][BP][32]
@@ -641,6 +653,7 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_root_kernel(const SegHis
   const uint8_t* lbase = bins8 + 12 * (on ? s : 0);
   const uint32_t loff = (uint32_t)l32 * 8u;
   const uint16_t* ct = codes + (int64_t)tree * a.n;
+  uint16_t* cw_out = DRAW ? const_cast<uint16_t*>(ct) : nullptr;
   uint64_t* rg = ring[wid];
   // the wave's rows: a contiguous 64-aligned share of the block's range
   const int per = ((len + NW - 1) / NW + 63) & ~63;
@@ -650,7 +663,15 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_root_kernel(const SegHis
   uint32_t ncw = 0xFFu;
   float ny = 0.f;
   auto fetch = [&](int64_t r) {
-    ncw = r < wend ? (uint32_t)ct[r] : 0xFFu;
+    if (DRAW) {
+      const uint32_t w = cdna::poisson_draw(cdna::bootstrap_uniform(dr.seed, dr.offset + (uint64_t)r, tree), dr.cdf,
+                                            dr.rate);
+      ncw = (w << 8) | (w ? 0u : 0xFFu);
+      if (r < wend) cw_out[r] = (uint16_t)ncw;
+      else ncw = 0xFFu;
+    } else {
+      ncw = r < wend ? (uint32_t)ct[r] : 0xFFu;
+    }
     ny = r < wend ? v1[r] : 0.f;
   };
   fetch(wr + lane);
@@ -1485,18 +1506,37 @@ CDNA_API int cdna_seg_hist_root_wide(const uint8_t* bins_rm, int64_t n, int d, i
   return (int)hipGetLastError();
 }
 
+// draw != 0 (level 0, every slot a tree's root): the bootstrap weights of tree sinfo[2 s] are drawn from Philox
+// (seed, global row offset + r, rate) and written to codes as the level's row codes (see RootDraw).
 CDNA_API int cdna_seg_hist_root(const uint8_t* bins_s10, int64_t n, int d, int B, const uint16_t* codes,
                                 const float* v1, float qs1, const int* work, int nwork, const int* sinfo, int slot0,
-                                unsigned long long* out, hipStream_t st) {
+                                unsigned long long* out, int draw, uint64_t seed, uint64_t offset, double rate,
+                                hipStream_t st) {
   if (nwork <= 0) return 0;
   if (d > 100 || B > 40 || B < 1) return (int)hipErrorInvalidValue;
   SegHistArgs a{nullptr, n, d, B, nullptr, nullptr, v1, nullptr, work, 1.f, qs1, out};
+  RootDraw dr{seed, offset, rate, cdna::poisson_cdf(draw ? rate : 1.0)};
   auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), 0, st, a, bins_s10, codes, v1, qs1, sinfo, slot0);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), 0, st, a, bins_s10, codes, v1, qs1, sinfo, slot0, dr);
   };
-  if (B <= 32) launch(seg_hist_lane10_root_kernel<32>);
-  else launch(seg_hist_lane10_root_kernel<40>);
+  if (draw) {
+    if (B <= 32) launch(seg_hist_lane10_root_kernel<32, true>);
+    else launch(seg_hist_lane10_root_kernel<40, true>);
+  } else {
+    if (B <= 32) launch(seg_hist_lane10_root_kernel<32, false>);
+    else launch(seg_hist_lane10_root_kernel<40, false>);
+  }
   return (int)hipGetLastError();
+}
+
+// Largest bootstrap weight the draws can produce at this rate (the saturated CDF table's length), -1 when the table
+// does not saturate within kCdf entries (no static bound: the caller draws ahead with the weights' max).
+CDNA_API int cdna_poisson_max_draw(double rate) {
+  const cdna::PoissonCdf cdf = cdna::poisson_cdf(rate);
+  if (cdf.T[cdna::kCdf - 1] != 0xFFFFFFFFu) return -1;
+  int k = 0;
+  while (k < cdna::kCdf && cdf.T[k] != 0xFFFFFFFFu) ++k;
+  return k;
 }
 
 // mode bit0: packed (no v0; count | sum in one atomic); bit1: per-row weights wp present;

@@ -1046,6 +1046,58 @@ def test_seg10_rows_and_lane10_histogram(dev, d, B, monkeypatch):
     assert torch.equal(cgot.cpu(), ref[1::2].cpu())
 
 
+@pytest.mark.parametrize("d,B,off", [(100, 40, 0), (92, 17, 12345), (100, 32, 3)])
+def test_root_histogram_draws_the_bootstrap(dev, d, B, off):
+    """Level 0 with the Poisson draws fused into the root histogram kernel (lazy K.BootstrapCodes): the codes it
+    writes equal the draws kernel's (misc.hip poisson_kernel, same Philox uniforms keyed by global row id + row
+    offset, same tabulated CDF) and its int64 sums equal the root histogram over those codes."""
+    T, n = 7, 100003
+    g = torch.Generator().manual_seed(d + B)
+    X = torch.randn(n, d, generator=g)
+    thr, nthr = _thresholds(X, B)
+    _, s10 = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), want_rm=True, rm_layout="s10")
+    v1 = (torch.randn(n, generator=g) * 3).to(dev)
+    bound = K.poisson_max_draw(1.0)
+    assert 8 <= bound <= 31
+    sc = K.seg_scales(None, v1, bound, n)
+    ref_codes = K.BootstrapCodes(T, n, 77, off, 1.0, dev)
+    assert ref_codes.wmax() <= bound
+    ref = K.seg_hist_root(s10, d, B, ref_codes.codes, v1, sc[1], bound, 0, T,
+                          torch.zeros((T, d, B, 2), dtype=torch.int64, device=dev))
+    lazy = K.BootstrapCodes(T, n, 77, off, 1.0, dev, lazy=True)
+    assert lazy.pending and lazy.wmax() == bound
+    got = K.seg_hist_codes(s10, d, B, lazy.codes, v1, sc[1], bound, np.arange(T), np.zeros(T, np.int64), 0, T,
+                           torch.zeros((T, d, B, 2), dtype=torch.int64, device=dev), draw=lazy.draw_args())
+    assert torch.equal(lazy.codes.cpu(), ref_codes.codes.cpu())
+    assert torch.equal(got.cpu(), ref.cpu())
+
+
+def test_fused_draws_grow_the_same_forest(dev, monkeypatch):
+    """RandomForestRegressor with the bootstrap draws fused into the level-0 histogram equals the draws-kernel
+    path bit for bit (forest digest)."""
+    import cdnaml
+    from cdnaml.ml.regression import RandomForestRegressor
+    from cdnaml.utils.synthetic import forest_digest
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator(device=dev).manual_seed(4)
+    X = torch.randn((300000, 100), generator=g, device=dev)
+    y = (X[:, 0] * 2 - X[:, 1] + torch.sin(3 * X[:, 2])).double()
+    df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
+    calls = {"n": 0}
+    orig = K.seg_hist_codes
+
+    def counted(*a, **k):
+        calls["n"] += k.get("draw") is not None
+        return orig(*a, **k)
+    monkeypatch.setattr(K, "seg_hist_codes", counted)
+    monkeypatch.setattr(K, "POISSON_EARLY_MAX", 0)  # the headline's placement: draws in series before the binning
+    digests = []
+    for fused in (True, False):
+        monkeypatch.setattr(K, "POISSON_FUSED", fused)
+        digests.append(forest_digest(RandomForestRegressor(numTrees=20, maxDepth=5, maxBins=40, seed=3).fit(df)._forest))
+    assert calls["n"] == 1 and digests[0] == digests[1]
+
+
 @pytest.mark.parametrize("d,B", [(100, 256), (64, 256), (100, 100), (37, 129)])
 def test_wide_codes_histogram_equals_records(dev, d, B):
     """Boosting levels with one built node per tree (80 < B <= 256) straight from the row codes
