@@ -37,12 +37,13 @@ def _sync(dev):
         torch.cuda.synchronize()
 
 
-def _emit(spark, metric, value, unit, steps, warmup, ms, hib, scaling, dtype, model, rows, par):
+def _emit(spark, metric, value, unit, steps, warmup, ms, hib, scaling, dtype, model, rows, par,
+          data="synthetic (generated in HBM)"):
     if spark.comm.rank == 0:
         print(json.dumps({"metric": metric, "value": value, "unit": unit, "n_gpus": spark.comm.world_size,
                           "steps": steps, "warmup": warmup, "ms_per_step": ms, "higher_is_better": hib,
                           "scaling": scaling, "vs_baseline": None, "dtype": dtype,
-                          "data": "synthetic (generated in HBM)",
+                          "data": data,
                           "config": {"model": model, "global_batch": rows, "seq_len": None, "parallelism": par}}),
               flush=True)
 
@@ -399,7 +400,9 @@ def bench_ooc(spark, args):
     src = "pinned host chunks (cycled pool), H2D in the timed region" if args.source == "host" else \
         "chunks generated on device, generation in the timed region"
     _emit(spark, f"rows/sec out-of-core fit ({name}; {src})", rows / ms * 1e3, "rows/s", args.steps, args.warmup,
-          ms, True, "strong", "fp32", name, rows, f"dp{comm.world_size}")
+          ms, True, "strong", "fp32", name, rows, f"dp{comm.world_size}",
+          data="synthetic (generated on the device, copied to pinned host chunks)" if args.source == "host"
+          else "synthetic (generated in HBM)")
 
 
 def main():

@@ -143,7 +143,7 @@ _SIGS = {
                             c_int),
     "cdna_codes_compact_w": ([c_int, c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                              c_float, c_void_p, c_void_p], c_int),
+                              c_float, c_void_p, c_int, c_void_p], c_int),
     "cdna_wave_scan": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
     "cdna_hash_insert": ([c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p], c_int),
     "cdna_hash_lookup": ([c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_void_p], c_int),

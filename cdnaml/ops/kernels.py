@@ -1871,6 +1871,16 @@ COMPACT_W = True
 COMPACT_DEFER = True
 
 
+# how codes_scatter_w ranks the lanes of one node (seg.hip codes_scatter_w_kernel): 0 = a ballot per node,
+# 1 = one DPP prefix scan per 4 nodes (from SCATTER_SCAN_MIN_KB built nodes per tree; KB = 8: 3.54 vs 3.85 ms)
+SCATTER_RANK = 1
+SCATTER_SCAN_MIN_KB = 4
+
+
+def _scatter_rank(KB: int) -> int:
+    return 0 if (SCATTER_RANK == 1 and KB < SCATTER_SCAN_MIN_KB) else SCATTER_RANK
+
+
 def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, rec_scale=None):
     T, n = codes.shape
     dev = codes.device
@@ -1892,7 +1902,7 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
     v0c = None if v0 is None else v0.float().contiguous()
     wcnt = torch.empty((T, Wv, KB), dtype=torch.int32, device=dev)
     _lib.check(L.cdna_codes_compact_w(1, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
-                                      per_wave, Wv, _ptr(wcnt), None, None, None, None, None, None, 0.0, None,
+                                      per_wave, Wv, _ptr(wcnt), None, None, None, None, None, None, 0.0, None, 0,
                                       _stream(dev)), "cdna_codes_compact_w(count)")
     # per-(tree, node) exclusive scan over the waves in place + node totals, one launch
     tot = torch.empty((T, KB), dtype=torch.int64, device=dev)
@@ -1916,7 +1926,7 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
         perm = torch.empty(n * T + REC_PAD, dtype=torch.int64, device=dev)
         _lib.check(L.cdna_codes_compact_w(2, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
                                           per_wave, Wv, None, _ptr(wcnt), None, None, None, None, _ptr(perm),
-                                          float(rec_scale), _ptr(kstart_t), _stream(dev)),
+                                          float(rec_scale), _ptr(kstart_t), _scatter_rank(KB), _stream(dev)),
                    "cdna_codes_compact_w(scatter)")
         ev.synchronize()
         tot_h = tot_p.numpy()
@@ -1947,7 +1957,8 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
         _lib.check(L.cdna_codes_compact_w(2, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
                                           per_wave, Wv, None, _ptr(wcnt), None if rec else _ptr(perm), _ptr(v0p),
                                           _ptr(v1p), _ptr(wp), _ptr(perm) if rec else None,
-                                          float(rec_scale) if rec else 0.0, _ptr(kstart_t), _stream(dev)),
+                                          float(rec_scale) if rec else 0.0, _ptr(kstart_t), _scatter_rank(KB),
+                                          _stream(dev)),
                    "cdna_codes_compact_w(scatter)")
     return perm, v0p, v1p, wp, np.stack([starts, lens], 1)
 

@@ -1184,10 +1184,15 @@ struct CompactWArgs {
   const int64_t* kstart;  // pass 2, optional: [T][KB] segment start added to the per-wave offsets
 };
 
-// Pass 1: per-(tree, wave, built node) record counts.
+// Pass 1: per-(tree, wave, built node) record counts.  rocprofv3 (PMC) on the first version, one compare-add per
+// (row, node): VALU-issue bound (KB = 8: 6.2e8 VALU instructions in 2.5e6 cycles, 4 cycles each per SIMD).  Here
+// the LDS table maps a local node to a one-hot increment of 8-bit fields packed four to a word, so a row costs
+// one table read and NW = KB / 4 adds whatever KB is; the fields are flushed into the per-node counts before they
+// can overflow (31 trips x 8 rows per lane <= 255).
 template <int KB>
 __global__ __launch_bounds__(256) void codes_count_w_kernel(const CompactWArgs a) {
-  __shared__ int s_k[256];
+  constexpr int NW = KB > 4 ? KB / 4 : 1;
+  __shared__ uint32_t s_oh[256 * NW];
   // XCD-aware block -> (row chunk, tree) map: block b runs on XCD b % 8, and the T blocks of one row chunk are
   // consecutive slots of ONE XCD (the same map as the scatter pass, whose blocks share that XCD's L2 copy of
   // the chunk's labels: v1 is the same for every tree)
@@ -1198,7 +1203,12 @@ __global__ __launch_bounds__(256) void codes_count_w_kernel(const CompactWArgs a
   if (chunk >= nch) return;  // block-uniform
   const int tf = a.tfirst[t];
   const int nloc = (t + 1 < a.T ? a.tfirst[t + 1] : a.A) - tf;
-  s_k[threadIdx.x] = (threadIdx.x < nloc && threadIdx.x < 255) ? a.kmap[tf + threadIdx.x] : -1;
+  {
+    const int kk = (threadIdx.x < nloc && threadIdx.x < 255) ? a.kmap[tf + threadIdx.x] : -1;
+#pragma unroll
+    for (int q = 0; q < NW; ++q)
+      s_oh[threadIdx.x * NW + q] = (kk >= 0 && (kk >> 2) == q) ? 1u << (8 * (kk & 3)) : 0u;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int w = chunk * 4 + (threadIdx.x >> 6);
@@ -1208,11 +1218,21 @@ __global__ __launch_bounds__(256) void codes_count_w_kernel(const CompactWArgs a
   const uint16_t* rec = a.codes + (int64_t)t * a.n;
   const int64_t cb = ((int64_t)t * a.Wv + w) * KB;
   int acc[KB];
+  uint32_t pk[NW];
 #pragma unroll
   for (int k = 0; k < KB; ++k) acc[k] = 0;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) pk[q] = 0;
+  auto flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < KB; ++k) acc[k] += (int)((pk[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+#pragma unroll
+    for (int q = 0; q < NW; ++q) pk[q] = 0;
+  };
   // 2 x 4 codes per lane per trip, loaded up front as 8-byte vectors
   const bool vec = (a.n & 3) == 0 && (reinterpret_cast<uintptr_t>(a.codes) & 7u) == 0;
   constexpr int NG = 2;
+  int trips = 0;
   for (int64_t rb = r_begin; rb < r_end; rb += 256 * NG) {
     uint32_t cc[NG][4];
 #pragma unroll
@@ -1230,14 +1250,17 @@ __global__ __launch_bounds__(256) void codes_count_w_kernel(const CompactWArgs a
       }
     }
 #pragma unroll
-    for (int q = 0; q < NG; ++q) {
-      int kk[4];
+    for (int q = 0; q < NG; ++q)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) kk[j] = s_k[cc[q][j] & 0xFFu];
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int k = 0; k < KB; ++k) acc[k] += (kk[0] == k) + (kk[1] == k) + (kk[2] == k) + (kk[3] == k);
+        for (int u = 0; u < NW; ++u) pk[u] += s_oh[(cc[q][j] & 0xFFu) * NW + u];
+    if (++trips == 31) {
+      flush();
+      trips = 0;
     }
   }
+  flush();
 #pragma unroll
   for (int k = 0; k < KB; ++k) {
     int v = acc[k];
@@ -1247,17 +1270,39 @@ __global__ __launch_bounds__(256) void codes_count_w_kernel(const CompactWArgs a
   }
 }
 
+// Inclusive wave-wide prefix sum in six DPP adds: row_shr 1 / 2 / 4 / 8 scan each 16-lane row, then
+// row_bcast:15 carries row 0's total into row 1 (and row 2's into row 3) and row_bcast:31 carries lane 31's
+// (rows 0-1) into rows 2-3.  Lanes whose DPP source is out of range or whose row is masked add the old value 0.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+  return v;
+}
+
 // Pass 2 with lane-strided rows.  The first version gave each lane 4
 // consecutive rows (ranked with 3 ballots per node), so the lanes' output
 // positions were ~4 records apart and every 8-byte store instruction spread
 // over ~16 partially written 128-byte lines (level-0 scatter: 14 GB in 5.4 ms
 // = 2.7 TB/s; all levels 20.5 ms per headline step).  Here trip row j of lane
-// l is rb + 64 j + l: one ballot per (j, node) ranks the lanes, so each store
-// instruction writes one contiguous run per node (14.6 ms per step).  Ranking
-// by the node id's bits (LK + 1 ballots, cursors one per lane read by
-// bpermute) instead of one ballot per node measured equal at KB = 4 / 8.
-template <int KB>
+// l is rb + 64 j + l, and the lanes of one node get consecutive positions, so
+// each store instruction writes one contiguous run per node.
+//
+// Ranking the lanes inside a node (RANK):
+//  0  one ballot + mbcnt per node: ~6 VALU instructions per (row slot, node).  PMC: VALU-issue bound at KB = 8
+//     (2.5e9 VALU instructions = the whole 3.8 ms of the level's scatter at 4 cycles per wave64 instruction).
+//  1  one DPP prefix scan of one-hot 8-bit fields packed four nodes to a word (NW = KB / 4 scans of 6 adds) gives
+//     each lane the count of same-node lanes below it; the node cursors live in lanes 0..KB-1 and are read with
+//     ds_bpermute.  Cost independent of KB per word; output order is still the row order.
+// A third method, per-wave LDS cursors bumped with a returning LDS atomic, measured the same headline step as both
+// (131.4 vs 131.1-131.5 ms) and was dropped; so was giving each lane 4 consecutive rows per trip loaded as 8- and
+// 16-byte vectors (scatter 9.8 vs 8.9 ms per step).
+template <int KB, int RANK>
 __global__ __launch_bounds__(256) void codes_scatter_w_kernel(const CompactWArgs a) {
+  constexpr int NW = KB > 4 ? KB / 4 : 1;
   __shared__ int s_k[256];
   const int nch = (a.Wv + 3) / 4;
   const int xcd = (int)(blockIdx.x & 7u), slot = (int)(blockIdx.x >> 3);
@@ -1267,17 +1312,24 @@ __global__ __launch_bounds__(256) void codes_scatter_w_kernel(const CompactWArgs
   const int tf = a.tfirst[t];
   const int nloc = (t + 1 < a.T ? a.tfirst[t + 1] : a.A) - tf;
   s_k[threadIdx.x] = (threadIdx.x < nloc && threadIdx.x < 255) ? a.kmap[tf + threadIdx.x] : -1;
-  __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int w = chunk * 4 + (threadIdx.x >> 6);
+  const int wib = threadIdx.x >> 6;
+  const int w = chunk * 4 + wib;
+  const int64_t cb = ((int64_t)t * a.Wv + w) * KB;
+  auto start = [&](int k) { return a.woff[cb + k] + (a.kstart ? (int)a.kstart[(int64_t)t * KB + k] : 0); };
+  __syncthreads();
   if (w >= a.Wv) return;
   const int64_t r_begin = (int64_t)w * a.per_wave;
   const int64_t r_end = r_begin + a.per_wave < a.n ? r_begin + a.per_wave : a.n;
   const uint16_t* rec = a.codes + (int64_t)t * a.n;
-  const int64_t cb = ((int64_t)t * a.Wv + w) * KB;
-  int acc[KB];
+  int acc[RANK == 0 ? KB : 1];
+  int cur = 0;  // RANK 1: lane k < KB holds node k's cursor
+  if (RANK == 0) {
 #pragma unroll
-  for (int k = 0; k < KB; ++k) acc[k] = a.woff[cb + k] + (a.kstart ? (int)a.kstart[(int64_t)t * KB + k] : 0);
+    for (int k = 0; k < KB; ++k) acc[k] = start(k);
+  } else {
+    cur = lane < KB ? start(lane) : 0;
+  }
   constexpr int NJ = 8;
   for (int64_t rb = r_begin; rb < r_end; rb += 64 * NJ) {
     uint32_t cc[NJ];
@@ -1294,13 +1346,31 @@ __global__ __launch_bounds__(256) void codes_scatter_w_kernel(const CompactWArgs
     for (int j = 0; j < NJ; ++j) {
       const int kk = s_k[cc[j] & 0xFFu];
       int pos = -1;
+      if (RANK == 0) {
 #pragma unroll
-      for (int k = 0; k < KB; ++k) {
-        const uint64_t m = __builtin_amdgcn_ballot_w64(kk == k);
-        if (m == 0ull) continue;  // wave-uniform
-        if (kk == k)
-          pos = acc[k] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        acc[k] += __builtin_popcountll(m);
+        for (int k = 0; k < KB; ++k) {
+          const uint64_t m = __builtin_amdgcn_ballot_w64(kk == k);
+          if (m == 0ull) continue;  // wave-uniform
+          if (kk == k)
+            pos = acc[k] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          acc[k] += __builtin_popcountll(m);
+        }
+      } else {
+        const int kc = kk < 0 ? 0 : kk;
+        const uint32_t one = kk < 0 ? 0u : 1u << (8 * (kc & 3));
+        uint32_t below = 0, tot_mine = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          const uint32_t x = (kc >> 2) == q ? one : 0u;
+          const uint32_t inc = wave_incl_scan(x);
+          if ((kc >> 2) == q) below = inc - x;
+          // node totals = lane 63's inclusive fields; lane k < KB takes the field of node k
+          const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+          if ((lane >> 2) == q) tot_mine = tot;
+        }
+        const int base = __builtin_amdgcn_ds_bpermute(kc << 2, cur);
+        if (kk >= 0) pos = base + (int)((below >> (8 * (kc & 3))) & 0xFFu);
+        cur += (int)((tot_mine >> (8 * (lane & 3))) & 0xFFu);
       }
       if (pos < 0) continue;
       const int64_t r = rb + j * 64 + lane;
@@ -1769,12 +1839,12 @@ CDNA_API int cdna_bins_row_major(const uint64_t* bins, int64_t n, int G, int Gs,
 }
 
 // Wave-owned compaction (KB = max built nodes per tree, <= 16).  pass 1 writes wcnt, pass 2 scatters
-// from woff.  per_wave must be a multiple of 256; Wv = ceil(n / per_wave).
+// from woff, ranking the lanes of a node with method `rank` (codes_scatter_w_kernel).  per_wave must be a multiple of 256; Wv = ceil(n / per_wave).
 CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64_t n, int T, int A,
                                   const int* tfirst, const int* kmap, const float* v0, const float* v1,
                                   int64_t per_wave, int Wv, int* wcnt, const int* woff, int* perm_out, float* v0_out,
                                   float* v1_out, uint8_t* w_out, uint64_t* rec_out, float qs1,
-                                  const int64_t* kstart, hipStream_t st) {
+                                  const int64_t* kstart, int rank, hipStream_t st) {
   if (n <= 0 || T <= 0) return 0;
   if (per_wave % 256 != 0 || (int64_t)Wv * per_wave < n) return (int)hipErrorInvalidValue;
   if (rec_out && (n >= (int64_t)1 << 31 || v0)) return (int)hipErrorInvalidValue;
@@ -1782,18 +1852,22 @@ CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64
                  rec_out, qs1, kstart};
   const int64_t nch = (Wv + 3) / 4;
   const dim3 grid((unsigned)(((nch + 7) / 8) * 8 * T));  // (chunk, tree) pairs, XCD-aware order (kernel)
-  auto go = [&](auto k1, auto k2) {
+  if (rank < 0 || rank > 1) return (int)hipErrorInvalidValue;
+  auto go = [&](auto k1, auto k2r0, auto k2r1) {
     if (pass == 1) hipLaunchKernelGGL(k1, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k2, grid, dim3(256), 0, st, a);
+    else if (rank == 0) hipLaunchKernelGGL(k2r0, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k2r1, grid, dim3(256), 0, st, a);
   };
+#define CDNA_CW(K) go(codes_count_w_kernel<K>, codes_scatter_w_kernel<K, 0>, codes_scatter_w_kernel<K, 1>)
   switch (KB) {
-    case 1: go(codes_count_w_kernel<1>, codes_scatter_w_kernel<1>); break;
-    case 2: go(codes_count_w_kernel<2>, codes_scatter_w_kernel<2>); break;
-    case 4: go(codes_count_w_kernel<4>, codes_scatter_w_kernel<4>); break;
-    case 8: go(codes_count_w_kernel<8>, codes_scatter_w_kernel<8>); break;
-    case 16: go(codes_count_w_kernel<16>, codes_scatter_w_kernel<16>); break;
+    case 1: CDNA_CW(1); break;
+    case 2: CDNA_CW(2); break;
+    case 4: CDNA_CW(4); break;
+    case 8: CDNA_CW(8); break;
+    case 16: CDNA_CW(16); break;
     default: return (int)hipErrorInvalidValue;
   }
+#undef CDNA_CW
   return (int)hipGetLastError();
 }
 

@@ -545,17 +545,23 @@ def test_seg_partition_implicit_level0(dev):
     assert int(ref[3].min()) > 0  # out-of-bag rows dropped
 
 
-@pytest.mark.parametrize("wave_owned", [True, False])
-def test_codes_compact(dev, monkeypatch, wave_owned):
-    """Rows of built nodes gathered into slot segments: same (row, v1, w) multiset per slot as the reference
-    (the wave-owned kernel is also stable: exactly the reference order)."""
-    monkeypatch.setattr(K, "COMPACT_W", wave_owned)
+@pytest.mark.parametrize("rank", [None, 0, 1])
+@pytest.mark.parametrize("max_loc", [9, 17])
+def test_codes_compact(dev, monkeypatch, rank, max_loc):
+    """Rows of built nodes gathered into slot segments: same (row, v1, w) multiset per slot as the reference.
+    rank None = the atomic (not wave-owned) kernel; else the wave-owned kernel ranking a node's lanes by ballots
+    (0) or a DPP prefix scan (1; from one built node up), both stable: exactly the reference order.  max_loc 17
+    reaches 16 built nodes per tree (KB = 16)."""
+    monkeypatch.setattr(K, "COMPACT_W", rank is not None)
+    if rank is not None:
+        monkeypatch.setattr(K, "SCATTER_RANK", rank)
+        monkeypatch.setattr(K, "SCATTER_SCAN_MIN_KB", 1)
     T, n = 6, 50000
-    rng = np.random.default_rng(2)
-    nloc = rng.integers(1, 9, T)
+    rng = np.random.default_rng(2 + max_loc)
+    nloc = rng.integers(1, max_loc, T)
     tfirst = torch.from_numpy(np.concatenate([[0], np.cumsum(nloc)[:-1]]).astype(np.int32))
     A = int(nloc.sum())
-    loc = rng.integers(0, 9, (T, n))
+    loc = rng.integers(0, max_loc, (T, n))
     loc = np.where(loc >= nloc[:, None], 0xFF, loc)
     w = rng.integers(1, 5, (T, n))
     codes = torch.from_numpy(((w << 8) | loc).astype(np.uint16).view(np.int16))
@@ -573,8 +579,14 @@ def test_codes_compact(dev, monkeypatch, wave_owned):
         assert key_r == key_o
         rows = out[0][st:st + ln].long().cpu()
         assert torch.equal(out[2][st:st + ln].cpu(), v1[rows])
-    if wave_owned:
+    if rank is not None:
         assert torch.equal(out[0].cpu(), ref[0]) and torch.equal(out[3].cpu(), ref[3])
+        # packed records through the same ranking
+        sc = 1024.0
+        rec, _, _, _, sg = K.codes_compact(codes.to(dev), tfirst, slot_of, S, None, v1.to(dev), rec_scale=sc)
+        rref, _, _, _, _ = K.codes_compact(codes, tfirst, slot_of, S, None, v1, rec_scale=sc)
+        np.testing.assert_array_equal(sg, ref[4])
+        assert torch.equal(rec.cpu(), rref)
 
 
 def test_bins_row_major(dev):
