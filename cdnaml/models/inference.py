@@ -178,9 +178,15 @@ class HostChunkStream:
             self._copy_stream = torch.cuda.Stream(device=self.dev)
 
     def __iter__(self) -> Iterator:
+        return self.iter_columns(None)
+
+    def iter_columns(self, columns=None) -> Iterator:
+        """A pass that copies only ``columns`` (None: all) to the device: a pass over the labels of a frame whose
+        features are hundreds of GB moves only the label bytes over PCIe."""
         from ..sql import types as T
         from ..sql.batch import Batch, ColumnData
         cuda = self.dev.type == "cuda"
+        want = None if columns is None else set(columns)
         freed = [None] * self.nbuf     # event: compute work on the slot's previous chunk is enqueued before it
         ready = [None] * self.nbuf     # event: the slot's H2D copy finished
         it = iter(self.chunks())
@@ -206,6 +212,8 @@ class HostChunkStream:
                         self._copy_stream.wait_event(freed[slot])
                     srcs = []
                     for k, a in ch.items():
+                        if want is not None and k not in want:
+                            continue
                         src = torch.as_tensor(a)
                         d = self._dbuf[slot][k]
                         if src.is_pinned() and src.dtype == d.dtype and src.is_contiguous():
@@ -221,7 +229,8 @@ class HostChunkStream:
                     ready[slot] = ev
             else:
                 for k, a in ch.items():
-                    self._dbuf[slot][k][:n].copy_(torch.as_tensor(a))
+                    if want is None or k in want:
+                        self._dbuf[slot][k][:n].copy_(torch.as_tensor(a))
             pending.append((slot, n))
             return True
 
@@ -234,6 +243,8 @@ class HostChunkStream:
                 torch.cuda.current_stream(self.dev).wait_event(ready[s])
             cols = {}
             for k, t in self._dbuf[s].items():
+                if want is not None and k not in want:
+                    continue
                 v = t[:n]
                 cols[k] = ColumnData(v, T.VectorUDT() if v.dim() == 2 else T.from_torch(v.dtype))
             yield Batch(cols, n, self.dev)
@@ -253,7 +264,12 @@ def chunked_dataframe(session, chunks: Callable[[], Iterable[dict]], max_rows: i
     if schema is None:
         first = next(iter(chunks()))
         schema = _schema_of(first)
-    return DataFrame(SourcePlan(session, "HostChunkScan", None, schema, iter_fn=lambda: iter(stream)), session)
+    plan = SourcePlan(session, "HostChunkScan", None, schema, iter_fn=lambda: iter(stream))
+    # column-projected passes and the host chunks themselves, for out-of-core fits (models.util.streamed_columns):
+    # a label pass copies only the labels, the quantile sample gathers its rows on the host
+    plan.iter_cols_fn = stream.iter_columns
+    plan.host_chunks_fn = chunks
+    return DataFrame(plan, session)
 
 
 def device_chunks(session, n_rows: int, chunk_rows: int, make: Callable[[int, int, dict], None], columns: dict,

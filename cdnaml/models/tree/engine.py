@@ -250,10 +250,12 @@ class ChunkedRows:
     """This rank's feature rows as a re-iterable stream of ``(row0, X_chunk [m, d] f32)`` (out-of-core fits,
     SURVEY §5.7): the quantile sample and the binning read the chunks one at a time, so fp32 X is never
     resident -- only its uint8 bins are.  ``it_fn()`` starts a new pass; chunks are transient (the source may
-    reuse their buffers once the work queued on them has run)."""
+    reuse their buffers once the work queued on them has run).  ``host_it_fn`` (optional) yields the same
+    ``(row0, X_chunk)`` from HOST memory, without any copy: the quantile sample gathers its few rows there."""
 
-    def __init__(self, it_fn, n: int, d: int, device):
+    def __init__(self, it_fn, n: int, d: int, device, host_it_fn=None):
         self.it_fn, self.n, self.d, self.device = it_fn, int(n), int(d), torch.device(device)
+        self.host_it_fn = host_it_fn
         self.shape = (self.n, self.d)
         self.is_cuda = self.device.type == "cuda"
 
@@ -269,7 +271,16 @@ def _global_sample(session, X, max_bins: int, seed: int, row_offset: int, n_glob
     n = X.shape[0]
     target = max(max_bins * max_bins, 10000)
     frac = min(1.0, target / max(n_global, 1))
-    if isinstance(X, ChunkedRows):
+    if isinstance(X, ChunkedRows) and X.host_it_fn is not None and frac < 1.0:
+        # the sampled rows (the same Philox draws on the device) gathered from the host chunks: a few thousand
+        # rows cross PCIe instead of the whole frame
+        parts = []
+        for r0, Xh in X.host_it_fn():
+            u = K.uniform(Xh.shape[0], seed ^ 0x5BD1E995, row_offset + r0, 3, device=X.device)
+            ih = K.compact_mask(u < frac).cpu()
+            parts.append(Xh.index_select(0, ih).float().to(X.device))
+        samp = torch.cat(parts) if parts else torch.zeros((0, X.d), dtype=torch.float32, device=X.device)
+    elif isinstance(X, ChunkedRows):
         parts = []
         for r0, Xc in X:
             if frac < 1.0:

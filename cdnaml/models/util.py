@@ -89,9 +89,28 @@ def streamed_columns(df, features_col: str, cols: List[str], head_rows: int = 0)
     n, d = 0, None
     head = []
     ok = True
-    for b in sel._plan.iter_execute():
-        if n < head_rows:
-            head.append(b.columns[features_col].values[:head_rows - n].float().clone())
+    # a host-chunk source read directly: the collection pass copies only the small columns, and the quantile
+    # sample gathers its rows from the host chunks (the features cross PCIe once, in the binning pass)
+    base = df._plan
+    host_fn = getattr(base, "host_chunks_fn", None)
+    if host_fn is not None and getattr(base, "iter_cols_fn", None) is not None:
+        got = 0
+        for ch in host_fn():  # the width (and the head rows) from the first host chunks
+            Xh = torch.as_tensor(ch[features_col])
+            d = int(Xh.shape[1])
+            if got >= head_rows:
+                break
+            head.append(Xh[:head_rows - got].float().to(df._session.device))
+            got += head[-1].shape[0]
+        it = base.iter_cols_fn(list(cols))
+        head_rows_left = 0
+    else:
+        host_fn = None
+        it = sel._plan.iter_execute()
+        head_rows_left = head_rows
+    for b in it:
+        if n < head_rows_left:
+            head.append(b.columns[features_col].values[:head_rows_left - n].float().clone())
         for c in cols:
             cd = b.columns[c]
             if cd.valid is not None and not bool(cd.valid.all()):
@@ -100,7 +119,8 @@ def streamed_columns(df, features_col: str, cols: List[str], head_rows: int = 0)
             parts[c].append(cd.values.clone())  # the source reuses its chunk buffers
         if not ok:
             break
-        d = int(b.columns[features_col].values.shape[1])
+        if host_fn is None:
+            d = int(b.columns[features_col].values.shape[1])
         n += b.n
     # the streamed and materialised paths issue different collectives, so every rank takes the same one: any
     # rank with nulls sends all of them to the materialised path; a rank with no chunks streams an empty shard
@@ -123,11 +143,19 @@ def streamed_columns(df, features_col: str, cols: List[str], head_rows: int = 0)
 
     def chunks():
         r0 = 0
-        for b in sel._plan.iter_execute():
+        for b in (sel._plan.iter_execute() if host_fn is None else base.iter_cols_fn([features_col])):
             X = b.columns[features_col].values
             yield r0, (X if X.dtype == torch.float32 else X.float())
             r0 += b.n
-    return ChunkedRows(chunks, n, d, dev), out, sel.schema[features_col].metadata
+
+    def host_chunks():
+        r0 = 0
+        for ch in host_fn():
+            X = torch.as_tensor(ch[features_col])
+            yield r0, X
+            r0 += X.shape[0]
+    return (ChunkedRows(chunks, n, d, dev, host_it_fn=host_chunks if host_fn is not None else None), out,
+            sel.schema[features_col].metadata)
 
 
 GRAM_FP64_MAX_WORK = float(__import__("os").environ.get("CDNAML_GRAM_FP64_MAX_WORK", "4e9"))

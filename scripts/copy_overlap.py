@@ -47,7 +47,7 @@ def main(d):
     kr = _rows(d, "kernel_trace.csv")
     cr = _rows(d, "memory_copy_trace.csv")
     kern = _union((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in kr)
-    dcol = next((c for c in cr[0] if "Direction" in c or c == "Kind"), None) if cr else None
+    dcol = next((c for c in cr[0] if "Direction" in c), None) if cr else None
     h2d = [r for r in cr if dcol is None or "HOST_TO_DEVICE" in r[dcol].upper() or "H2D" in r[dcol].upper()]
     bcol = next((c for c in (cr[0] if cr else {}) if "Bytes" in c or c == "Size"), None)
     civ = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in h2d]
@@ -61,6 +61,16 @@ def main(d):
     print(f"H2D copies: {len(h2d)}" + (f", {nbytes / 1e9:.1f} GB" if nbytes else "") +
           f", busy {cbusy / 1e9:.3f} s" + (f" ({nbytes / cbusy:.1f} GB/s while copying)" if nbytes else ""))
     print(f"H2D busy time with a kernel running: {ov / 1e9:.3f} s = {100.0 * ov / max(cbusy, 1):.1f} % of the copy time")
+    if cu:
+        # inside the streaming window (first copy start .. last copy end): how much of the kernel work ran while a
+        # copy was in flight (the per-chunk compute hidden under the PCIe stream)
+        win = [[cu[0][0], cu[-1][1]]]
+        kin = [[max(s, win[0][0]), min(e, win[0][1])] for s, e in kern if e > win[0][0] and s < win[0][1]]
+        kb = sum(e - s for s, e in kin)
+        print(f"streaming window {(win[0][1] - win[0][0]) / 1e9:.3f} s: copies busy {100.0 * cbusy / (win[0][1] - win[0][0]):.1f} %, "
+              f"kernels busy {kb / 1e9:.3f} s, of which {100.0 * _overlap(kin, cu) / max(kb, 1):.1f} % under a running copy")
+        after = sum(e - s for s, e in kern if s >= win[0][1])
+        print(f"after the stream: kernels busy {after / 1e9:.3f} s (the tree levels: they need every row's bins)")
     nb = 100
     w = (t1 - t0) / nb
     print("timeline (1 % bins): copy-busy % / kernel-busy %")

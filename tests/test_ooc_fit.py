@@ -82,3 +82,29 @@ def test_streamed_linear_regression(spark, streamed_calls):
     tol = 1e-9 if spark.device.type == "cpu" else 2e-5
     np.testing.assert_allclose(got.coefficients.toArray(), ref.coefficients.toArray(), rtol=tol, atol=tol)
     assert got.intercept == pytest.approx(ref.intercept, rel=tol, abs=tol)
+
+
+def test_streamed_fit_moves_the_features_once(spark, monkeypatch):
+    """A host-chunk frame: the label pass copies only the label column, the quantile sample (frac < 1 here:
+    40000 rows for a 10000-row target) gathers its rows from the host chunks, so only the binning pass streams
+    the features (and only them) -- and the forest still equals the materialised fit."""
+    import torch
+    from cdnaml.ml.regression import RandomForestRegressor
+    from cdnaml.models import inference
+    from cdnaml.utils.synthetic import forest_digest
+    passes = []
+    orig = inference.HostChunkStream.iter_columns
+
+    def rec(self, columns=None):
+        passes.append(None if columns is None else tuple(columns))
+        return orig(self, columns)
+    monkeypatch.setattr(inference.HostChunkStream, "iter_columns", rec)
+    n, d = 40000, 10
+    X, y = _data(n, d, seed=7)
+    mat = spark.createDataFrameFromLocalTensors({"features": torch.from_numpy(X).to(spark.device),
+                                                 "label": torch.from_numpy(y).to(spark.device)})
+    est = RandomForestRegressor(numTrees=4, maxDepth=4, maxBins=16, seed=9)
+    ref = forest_digest(est.fit(mat)._forest)
+    got = forest_digest(est.fit(_chunked(spark, X, y, 6000))._forest)
+    assert got == ref
+    assert passes == [("label",), ("features",)]
