@@ -185,6 +185,8 @@ _SIGS = {
                         c_void_p], c_int),
     "cdna_tree_predict": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p,
                            c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p], c_int),
+    "cdna_heap_last_level": ([c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double,
+                              c_double, c_void_p, c_int, c_int, c_void_p], c_int),
     "cdna_tree_predict_heap": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                 c_double, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_predict_binned_add": ([c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p,

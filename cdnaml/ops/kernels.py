@@ -1017,6 +1017,42 @@ def pack_heap(struct: np.ndarray, vals: np.ndarray, depth: int) -> np.ndarray:
     return out
 
 
+def heap_last_level(so: torch.Tensor, a_tree: torch.Tensor, a_key: torch.Tensor, a_w: torch.Tensor,
+                    thr: torch.Tensor, min_gain: float, min_w: float, heap: torch.Tensor, depth: int) -> None:
+    """Write a regression forest's last split level into its packed predict heap in place (``pack_heap`` layout
+    of depth ``depth``; trees.hip heap_last_level_kernel): for each active node a whose K6 row ``so[a]`` (gain,
+    feature, bin, left W, left S, right W, right S, ...) passes the host's split rule (finite gain > 0, >=
+    min_gain; node weight a_w[a] >= min_w), the internal slot a_key[a] - 1 gets (feature, fp32 threshold bits of
+    thr[feature, bin]) and its two depth-``depth`` leaves S / W (0 for an empty child).  a_tree / a_key int32,
+    a_w f64, thr f32 [d, Bt], heap int32 [T, 2^(depth+2)-2]."""
+    A = so.shape[0]
+    if A == 0:
+        return
+    T = heap.shape[0]
+    NI = (1 << depth) - 1
+    assert heap.shape[1] == 4 * NI + 2 and so.dtype == torch.float64
+    if _native(so):
+        d, Bt = thr.shape
+        _lib.check(_lib.lib().cdna_heap_last_level(_ptr(so), so.shape[1], A, _ptr(a_tree), _ptr(a_key), _ptr(a_w),
+                                                   _ptr(thr), Bt, d, float(min_gain), float(min_w), _ptr(heap),
+                                                   depth, T, _stream(so.device)), "cdna_heap_last_level")
+        return
+    gain = so[:, 0]
+    ok = torch.isfinite(gain) & (gain > 0) & (gain >= min_gain) & (a_w >= min_w)
+    idx = torch.nonzero(ok).flatten()
+    if not len(idx):
+        return
+    f, b = so[idx, 1].long(), so[idx, 2].long()
+    t, k = a_tree[idx].long(), a_key[idx].long()
+    heap[t, 2 * (k - 1)] = f.to(torch.int32)
+    heap[t, 2 * (k - 1) + 1] = thr[f, b].float().view(torch.int32)
+    leaf = heap[:, 2 * NI:].view(torch.float64)  # [T, 2^depth] (a view: writes land in heap)
+    for side in (0, 1):
+        W, S = so[idx, 3 + 2 * side], so[idx, 4 + 2 * side]
+        leaf[t, 2 * k + side - (1 << depth)] = torch.where(W > 0, S / torch.where(W > 0, W, torch.ones_like(W)),
+                                                           torch.zeros_like(W))
+
+
 def ordered_tree_sum(contribs, T: int, n: int, K: int, base=None) -> torch.Tensor:
     """The fp64 ensemble sum in the device kernels' order (trees.hip predict_kernel): lane q = t % 4 adds
     ``contribs(t)`` (tree_w[t] * leaf value, already a rounded product) for its trees in ascending order, then

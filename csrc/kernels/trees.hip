@@ -988,7 +988,46 @@ CDNA_API int cdna_tree_predict_heap(const float* X, int64_t n, int d, int64_t ld
   return (int)hipGetLastError();
 }
 
-// binize v3 (LUT-narrowed search): lut [d][C+1] uint8, lo_sc [2][d] (cell lower edge, cell scale);
-// M = search steps inside a cell = ceil(log2(largest threshold count of any cell + 1)) (<= 8).  Returns hipErrorInvalidValue when LDS does not fit.
+// The last split level of a regression forest written straight into its packed predict heap (depth D: the
+// level's nodes sit at depth D - 1, their children are depth-D leaves), so the predict can follow the split
+// scan on the GPU while the host turns the same decisions into the forest's node lists.  Per active node a
+// (K6 row so[a] = gain, feature, bin, left W, left S, right W, right S, ...): the host's rule -- gain finite,
+// > 0 and >= min_gain, node weight >= min_w -- splits it: internal slot key - 1 = (feature, fp32 threshold bits)
+// and the two leaf values S / W (0 for an empty child) at depth-D leaf indices 2 key - 2^D, 2 key + 1 - 2^D.
+// A node that does not split keeps the heap's pass-through slot and its own value, already in place.
+__global__ __launch_bounds__(256) void heap_last_level_kernel(const double* __restrict__ so, int sw, int A,
+                                                              const int* __restrict__ a_tree,
+                                                              const int* __restrict__ a_key,
+                                                              const double* __restrict__ a_w,
+                                                              const float* __restrict__ thr, int Bt, int d,
+                                                              double min_gain, double min_w, int* __restrict__ heap,
+                                                              int D, int T) {
+  const int a = blockIdx.x * 256 + threadIdx.x;
+  if (a >= A) return;
+  const double* s = so + (int64_t)a * sw;
+  const double gain = s[0];
+  if (!(isfinite(gain) && gain > 0.0 && gain >= min_gain && a_w[a] >= min_w)) return;
+  const int f = (int)s[1], b = (int)s[2], t = a_tree[a], k = a_key[a];
+  const int NI = (1 << D) - 1;
+  if (!CDNA_DCHECK(f >= 0 && f < d && b >= 0 && b < Bt && t >= 0 && t < T && k >= (1 << (D - 1)) && k <= NI,
+                   0x4EA1u))
+    return;  // a K6 row or heap key outside the tables
+  int* h = heap + (int64_t)t * (4 * NI + 2);
+  h[2 * (k - 1)] = f;
+  h[2 * (k - 1) + 1] = __float_as_int(thr[(int64_t)f * Bt + b]);
+  double* leaf = reinterpret_cast<double*>(h + 2 * NI);
+  leaf[2 * k - (1 << D)] = s[3] > 0.0 ? s[4] / s[3] : 0.0;
+  leaf[2 * k + 1 - (1 << D)] = s[5] > 0.0 ? s[6] / s[5] : 0.0;
+}
+
+CDNA_API int cdna_heap_last_level(const double* so, int sw, int A, const int* a_tree, const int* a_key,
+                                  const double* a_w, const float* thr, int Bt, int d, double min_gain, double min_w,
+                                  int* heap, int D, int T, hipStream_t st) {
+  if (A <= 0) return 0;
+  if (sw < 7 || D < 1 || D > 12 || T <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(heap_last_level_kernel, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, st, so, sw, A, a_tree,
+                     a_key, a_w, thr, Bt, d, min_gain, min_w, heap, D, T);
+  return (int)hipGetLastError();
+}
 
 CDNA_DEBUG_EXPORT(trees)

@@ -18,6 +18,7 @@ def test_trainer_heap_equals_forest_walk():
         y = (X[:, 0] * 2 - X[:, 1] + torch.sin(X[:, 2])).double()
         df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
         f = RandomForestRegressor(numTrees=T, maxDepth=depth, maxBins=16, seed=1, minInstancesPerNode=3).fit(df)._forest
+        f.settle()  # a deferred last level fills the host arrays when it runs (test_device_last_level_heap)
         assert f._heap_np is not None
         pre = f._heap_np
         f._heap_np = None
@@ -26,6 +27,41 @@ def test_trainer_heap_equals_forest_walk():
         np.testing.assert_array_equal(st, pre[0])
         # the trainer's per-slot values hold every node's value (splits too); the packed table reads leaves only
         np.testing.assert_array_equal(K.pack_heap(st, vals, D), K.pack_heap(pre[0], pre[1], pre[2]))
+
+
+def test_device_last_level_heap(spark):
+    """The last split level decided on the device (K.heap_last_level into a copy of the packed heap, the host side
+    left pending): the device table equals the host arrays' table once the pending work has run, the forest
+    (digest) equals the one grown with the deferral off, and so do the predictions (cpu and, marked gpu, cuda:
+    there the HIP kernel writes the table and the predictor reads it before the host has seen the level)."""
+    from cdnaml.models.regression import RandomForestRegressor
+    from cdnaml.models.tree import engine as E
+    from cdnaml.utils.synthetic import forest_digest
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(4000, 9, generator=g)
+    y = (X[:, 0] * 2 - X[:, 1] + torch.sin(X[:, 2]) + 0.2 * torch.randn(4000, generator=g)).double()
+    df = spark.createDataFrameFromLocalTensors({"features": X.to(spark.device), "label": y.to(spark.device)})
+    est = RandomForestRegressor(numTrees=6, maxDepth=5, maxBins=24, seed=2, minInstancesPerNode=2)
+    m = est.fit(df)
+    f = m._forest
+    key = ("heap", str(spark.device), "value")
+    assert key in f._dev and f._pending, "the last level was not deferred"
+    h_dev, D, _ = f._dev[key]
+    p1 = m.transform(df).select("prediction").toPandas()["prediction"].to_numpy()
+    assert not f._pending  # the predictor ran the pending level right after its launch
+    pre = f._heap_np
+    assert pre is not None and pre[2] == D == 5
+    np.testing.assert_array_equal(h_dev.cpu().numpy(), K.pack_heap(*pre))
+    old = E.HEAP_LAST_DEVICE
+    try:
+        E.HEAP_LAST_DEVICE = False
+        m2 = est.fit(df)
+    finally:
+        E.HEAP_LAST_DEVICE = old
+    f2 = m2._forest
+    assert key not in f2._dev and forest_digest(f2) == forest_digest(f)
+    p2 = m2.transform(df).select("prediction").toPandas()["prediction"].to_numpy()
+    np.testing.assert_array_equal(p1, p2)
 
 
 def test_set_splits_vectorised():
