@@ -347,8 +347,8 @@ def quantile_thresholds_dev(samp: torch.Tensor, max_bins: int):
 
 # --------------------------------------------------------------------- K4
 # binize v6: the per-feature uniform-grid LUT narrows the threshold search to the few thresholds of the value's cell
-# (trees.hip binize5_kernel<LUT>); False: the 6-step LDS binary search of v5
-BINIZE_LUT = True
+# (trees.hip binize5_kernel<C>): cells per feature, 64 or 256; 0 = the 6-step LDS binary search of v5
+BINIZE_LUT = 256
 
 
 def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Optional[float] = None,

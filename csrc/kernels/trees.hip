@@ -19,6 +19,7 @@
 // re-reads.
 #include "common.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -252,10 +253,12 @@ __device__ __forceinline__ void lds_barrier() {
 // built in LDS by every block from the device thresholds (no host round trip); the refinement walks the sorted
 // table kmax = max thresholds per cell steps (Gaussian-like columns at 40 bins: 1-2) instead of the 6 search
 // steps, and falls back to a binary search of the sorted table when kmax > kLutMaxK (heavy-tailed columns).
-constexpr int kLutCells = 64;
+// C = cells per feature (template; 0 = no LUT).  Gaussian columns at 40 bins: 64 cells (one cell ~ one threshold
+// spacing near the centre) leave 2 thresholds in the fullest cells, so every element walks 2 dependent steps;
+// 256 cells leave 1.
 constexpr int kLutMaxK = 6;
 
-template <int STEPS, int RPL, bool LUT>
+template <int STEPS, int RPL, int C>
 __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                        const float* __restrict__ thr, const int* __restrict__ nthr,
                                                        int tmax, int miss_on, float miss_val,
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float smf5[];
   constexpr int P = 1 << STEPS, RT = 64 * RPL, TP = 17;  // RPL rows per lane
-  constexpr int C = kLutCells;
+  constexpr bool LUT = C > 0;
   float* sthr = smf5;                                                          // [d][P]
   uint8_t* sbase = reinterpret_cast<uint8_t*>(sthr + (size_t)((d * P + 3) & ~3));  // LUT: [d][C]
   float* sprm = reinterpret_cast<float*>(sbase + (LUT ? (size_t)d * C : 0));        // LUT: [d][2] lo, scale
@@ -296,15 +299,21 @@ __global__ __launch_bounds__(1024) void binize5_kernel(const float* __restrict__
       const int f = e / C, c = e - f * C;
       const int nt = nthr[f] < tmax ? nthr[f] : tmax;
       const float lo = sprm[2 * f], sc = sprm[2 * f + 1];
-      int below = 0, in = 0;
-      for (int j = 0; j < nt; ++j) {
-        const float v = fminf(fmaxf((sthr[f * P + j] - lo) * sc, 0.f), (float)(C - 1));
-        const int cj = (int)v;
-        below += cj < c;
-        in += cj == c;
+      // the thresholds' cells are non-decreasing in j (sorted table, monotone cell map): base = #{cell_j < c} and
+      // the cell's count = #{cell_j <= c} - base, two binary searches
+      auto cell = [&](int j) { return (int)fminf(fmaxf((sthr[f * P + j] - lo) * sc, 0.f), (float)(C - 1)); };
+      int a0 = 0, a1 = nt;  // first j with cell_j >= c
+      while (a0 < a1) {
+        const int m = (a0 + a1) >> 1;
+        if (cell(m) < c) a0 = m + 1; else a1 = m;
       }
-      sbase[e] = (uint8_t)below;
-      if (in) atomicMax(&s_kf[f], in);
+      int b0 = a0, b1 = nt;  // first j with cell_j > c
+      while (b0 < b1) {
+        const int m = (b0 + b1) >> 1;
+        if (cell(m) <= c) b0 = m + 1; else b1 = m;
+      }
+      sbase[e] = (uint8_t)a0;
+      if (b0 > a0) atomicMax(&s_kf[f], b0 - a0);
     }
   } else {
     // Table layout by search step: step s (step 2^s) only ever probes cand = (2k + 1) 2^s, so entry cand - 1 is
@@ -867,9 +876,11 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
     if (steps < 4) steps = 4;
     const int G = (d + 7) / 8;
     constexpr int rpl = 1;  // 2 rows per lane (two tiles of registers, a 128-row LDS tile): 18.7 vs 15.4 ms
-    const bool use_lut = lut != 0;
+    // lut = cells per feature of the threshold grid (64 or 256), 0 = binary search only
+    const int lut_cells = lut >= 256 ? 256 : (lut > 0 ? 64 : 0);
+    const bool use_lut = lut_cells > 0;
     const size_t lds = (size_t)((d * (1 << steps) + 3) & ~3) * 4 + (size_t)64 * rpl * 17 * 8 +
-                       (use_lut ? (size_t)d * kLutCells + (size_t)((2 * d + 3) & ~3) * 4 : 0);
+                       (use_lut ? (size_t)d * lut_cells + (size_t)((2 * d + 3) & ~3) * 4 : 0);
     if (steps <= 8 && lds <= 150 * 1024 && (!use_lut || d <= 128)) {
       auto launch = [&](auto kern) {
         if (lds > 64 * 1024)
@@ -878,23 +889,19 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
         hipLaunchKernelGGL(kern, dim3(grid_for(n, 64 * rpl, 1024)), dim3(64 * G), lds, st, X, n, d, ldx, thr, nthr,
                            tmax > 0 ? tmax : 1, miss_on, miss_val, out, rm, Gs, ldo);
       };
-      if (use_lut) {
+      auto by_steps = [&](auto c_tag) {
+        constexpr int CC = decltype(c_tag)::value;
         switch (steps) {
-          case 4: launch(binize5_kernel<4, rpl, true>); break;
-          case 5: launch(binize5_kernel<5, rpl, true>); break;
-          case 6: launch(binize5_kernel<6, rpl, true>); break;
-          case 7: launch(binize5_kernel<7, rpl, true>); break;
-          default: launch(binize5_kernel<8, rpl, true>); break;
+          case 4: launch(binize5_kernel<4, rpl, CC>); break;
+          case 5: launch(binize5_kernel<5, rpl, CC>); break;
+          case 6: launch(binize5_kernel<6, rpl, CC>); break;
+          case 7: launch(binize5_kernel<7, rpl, CC>); break;
+          default: launch(binize5_kernel<8, rpl, CC>); break;
         }
-      } else {
-        switch (steps) {
-          case 4: launch(binize5_kernel<4, rpl, false>); break;
-          case 5: launch(binize5_kernel<5, rpl, false>); break;
-          case 6: launch(binize5_kernel<6, rpl, false>); break;
-          case 7: launch(binize5_kernel<7, rpl, false>); break;
-          default: launch(binize5_kernel<8, rpl, false>); break;
-        }
-      }
+      };
+      if (lut_cells == 256) by_steps(std::integral_constant<int, 256>{});
+      else if (lut_cells == 64) by_steps(std::integral_constant<int, 64>{});
+      else by_steps(std::integral_constant<int, 0>{});
       return (int)hipGetLastError();
     }
   }

@@ -108,7 +108,7 @@ def test_binize(dev):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("lut", [True, False])
+@pytest.mark.parametrize("lut", [256, 64, 0])
 def test_binize_lut_columns(dev, lut, monkeypatch):
     """binize v6 (uniform-grid LUT + a short walk of the value's cell) equals the host count #{t < x} exactly on
     columns the grid fits badly: heavy tails (lognormal, Cauchy: the wave falls back to the binary search),
