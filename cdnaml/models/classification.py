@@ -26,7 +26,8 @@ from .optim import minimize
 from .param import NO_DEFAULT, TypeConverters as TC, keyword_init
 from .regression import (_GBT, _PRED, _RF, _TREE, _TreeModelBase, _bag_weights, _combine_weights, _num_classes,
                          _subforest, resolve_subset, tree_fit_prepare)
-from .tree.engine import Forest, ForestTrainer, TreeParams
+from .tree.engine import ForestTrainer, TreeParams
+from .tree.forest import Forest
 from .util import IllegalArgumentException, centered_gram, local_batch, local_xyw, require_vector
 
 # multinomial logistic regression: fp64 logits / gradients up to this many n*d*C multiply-adds per pass (course

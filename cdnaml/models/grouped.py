@@ -121,7 +121,7 @@ def _fit_groups(tuner, e, T_: int, gid: torch.Tensor, groups: List[int]):
 
 def _slice_forest(forest, t0: int, t1: int):
     from .tree.fused import truncate_forest
-    from .tree.engine import Forest
+    from .tree.forest import Forest
     sub = Forest(forest.K)
     sub.roots = forest.roots[t0:t1]
     for name in ("feat", "thr", "bin", "left", "right", "catmask", "is_cat", "value", "weight", "gain",

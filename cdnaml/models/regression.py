@@ -25,7 +25,9 @@ from ..sql.dataframe import MapPlan
 from .base import Estimator, Model
 from .linalg import DenseVector, SparseVector
 from .param import NO_DEFAULT, TypeConverters as TC, keyword_init
-from .tree.engine import Forest, ForestTrainer, TreeParams, make_binned
+from .tree.binning import make_binned
+from .tree.engine import ForestTrainer, TreeParams
+from .tree.forest import Forest
 from .util import (IllegalArgumentException, categorical_info, global_count, global_offset, gram_fp64_auto,
                    local_batch, local_xyw, require_vector, streamed_columns)
 

@@ -1,2 +1,4 @@
 """Histogram tree learning engine shared by DT / RF / GBT / XGBoost-style models."""
-from .engine import BinnedData, Forest, ForestTrainer, TreeParams, make_binned  # noqa: F401
+from .binning import BinnedData, make_binned  # noqa: F401
+from .engine import ForestTrainer, TreeParams  # noqa: F401
+from .forest import Forest  # noqa: F401

@@ -30,7 +30,7 @@ from typing import Any, Dict, Optional, Tuple
 import numpy as np
 import torch
 
-from .engine import Forest
+from .forest import Forest
 
 
 def data_fingerprint(session, data, labels: Optional[torch.Tensor]) -> str:

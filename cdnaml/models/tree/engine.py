@@ -34,6 +34,9 @@ import torch
 from ...ops import kernels as K
 from ...utils import tracing as _tr
 from ..util import IllegalArgumentException
+from .binning import (BinnedData, ChunkedRows, _binize_src, _global_sample, _make_binned, _resident,  # noqa: F401
+                      _seg10_ok, find_thresholds, find_thresholds_t, make_binned)
+from .forest import (Forest, _FrozenList, _NODE_FIELDS, _forest_level_ops, _settled_list, freeze_cut)  # noqa: F401
 
 # compact uint16 row records (hist5.hip) instead of int32 node ids + uint8 weights
 USE_CODES = True
@@ -52,10 +55,6 @@ NATIVE_SPLIT = True
 MSEG_REC = True
 # level 0 on seg10 rows: root records compacted inside the histogram kernel (no codes_compact pass)
 ROOT_HIST = True
-# binning queued on the quantile kernel's device thresholds, checked on the host behind it
-SPEC_THRESHOLDS = True
-# single-output forests of depth <= 8 predict from a heap layout (8-byte nodes, fixed-step walks)
-HEAP_PREDICT = True
 # regression forests (T > 1) deeper than 8 levels: the packed record levels down to 8, then node ids (as binary
 # classification); 0 = the node-id histograms from the root (round 3).  RF 20 trees depth 10 at 1e7 x 100:
 # 376 -> 88 ms per fit.  One tree keeps the permutation segment path (seg.hip, any depth): 14 ms at depth 12
@@ -64,8 +63,6 @@ DEEP_REG = True
 # per-node feature subsets drawn on the GPU (misc.hip feature_masks_kernel) on levels whose masks have no host
 # consumer; 0 = numpy + upload every level
 MASKS_DEV = True
-# predictor tables of tuner-cut forests from the arrays truncate_forest computed (0: from the node lists)
-CUT_ARRAYS = True
 # boosting margins updated by the level partitions (ForestTrainer.train(margin=...)) instead of a tree walk
 GBDT_MARGIN = True
 # multi-rank record histograms: slot chunks whose all-reduces overlap the next chunk's histogram kernel
@@ -114,769 +111,6 @@ class TreeParams:
                                            # (batched many-model fits: tree t of every group hashes as t)
 
 
-# ============================================================ binning (K3/K4)
-@dataclass
-class BinnedData:
-    X: torch.Tensor
-    bins: torch.Tensor
-    thresholds: np.ndarray            # [d, B-1] float64 raw thresholds
-    nthr: np.ndarray                  # [d] int (-1 categorical)
-    categorical: Dict[int, int]
-    n_local: int
-    n_global: int
-    row_offset: int
-    d: int
-    B: int
-    missing_bin: bool = False         # bin 0 holds missing values (XGBoost sparsity-aware splits)
-    bins_rm: Optional[torch.Tensor] = None  # lazily built row-major copy [n, G, 8] (segment-mode histograms)
-    bins_s10: Optional[torch.Tensor] = None  # seg10 row layout [n, 16, 8] written by binize (K.bins_seg10)
-
-    def row_major_bins(self) -> torch.Tensor:
-        if self.bins_rm is None:
-            self.bins_rm = K.bins_row_major(self.bins)
-        return self.bins_rm
-
-    def record_rows(self):
-        """(rows, is_seg10) for the record histograms: the seg10 copy when binize wrote one, else the standard
-        row-major copy."""
-        if self.bins_s10 is not None:
-            return self.bins_s10, True
-        return self.row_major_bins(), False
-
-
-def _seg10_ok(X: torch.Tensor, d: int, max_bins: int) -> bool:
-    return K.SEG10 and X.is_cuda and 80 < d <= 100 and d % 4 == 0 and max_bins <= 40
-
-
-def find_thresholds(sample: np.ndarray, d: int, max_bins: int, categorical: Dict[int, int]):
-    """Per-feature split thresholds from a (global) sample (Spark findSplits semantics)."""
-    thr = np.zeros((d, max(max_bins - 1, 1)), dtype=np.float64)
-    nthr = np.zeros(d, dtype=np.int32)
-    for f in range(d):
-        if f in categorical:
-            nthr[f] = -1
-            continue
-        col = sample[:, f]
-        col = col[~np.isnan(col)]
-        if col.size == 0:
-            continue
-        vals, counts = np.unique(col, return_counts=True)
-        if len(vals) <= 1:
-            continue
-        if len(vals) <= max_bins:
-            cand = (vals[:-1] + vals[1:]) / 2.0
-        else:
-            cum = np.cumsum(counts)
-            total = cum[-1]
-            targets = total * np.arange(1, max_bins) / max_bins
-            idx = np.searchsorted(cum, targets, side="left")
-            idx = np.unique(np.clip(idx, 0, len(vals) - 2))
-            cand = (vals[idx] + vals[idx + 1]) / 2.0
-        cand = np.unique(cand)[: max_bins - 1]
-        thr[f, : len(cand)] = cand
-        nthr[f] = len(cand)
-    return thr, nthr
-
-
-def find_thresholds_t(samp: torch.Tensor, max_bins: int, categorical: Dict[int, int]):
-    """``find_thresholds`` on a [s, d] float64 tensor, vectorised over features (runs on the sample's device).
-
-    Features with more distinct values than ``max_bins`` (the common continuous case) take the batched
-    quantile path: one sort of the whole sample, the quantile positions, and a batched searchsorted for
-    the next distinct value.  Categorical / few-distinct / empty features fall back to the per-feature host
-    code on their (already sorted) column.  Bit-identical to ``find_thresholds``.
-    """
-    s, d = samp.shape
-    thr = np.zeros((d, max(max_bins - 1, 1)), dtype=np.float64)
-    nthr = np.zeros(d, dtype=np.int32)
-    if s == 0 or d == 0:
-        for f in categorical:
-            nthr[f] = -1
-        return thr, nthr
-    dev = samp.device
-    q = K.quantile_thresholds(samp, max_bins)
-    if q is not None:
-        # one K3 kernel (sort in LDS + candidates + de-dup per feature block) instead of ~20 torch launches
-        qthr, qn, kdist, S = q
-        fast = kdist > max_bins
-        for f in categorical:
-            fast[f] = False
-        thr[fast], nthr[fast] = qthr[fast], qn[fast]
-        slow = np.nonzero(~fast)[0].tolist()
-        if slow:
-            cols = S[slow].t().cpu().numpy()
-            t2, n2 = find_thresholds(cols, len(slow), max_bins,
-                                     {i: categorical[f] for i, f in enumerate(slow) if f in categorical})
-            thr[slow], nthr[slow] = t2, n2
-        return thr, nthr
-    S = torch.sort(samp.t().contiguous(), dim=1).values          # [d, s], NaN last
-    nn = (~torch.isnan(S)).sum(1)                                 # non-NaN count per feature
-    Sf = torch.where(torch.isnan(S), torch.full_like(S, float("inf")), S)
-    ar = torch.arange(s, device=dev)
-    valid = ar[None, :] < nn[:, None]
-    newv = torch.ones_like(valid)
-    newv[:, 1:] = Sf[:, 1:] != Sf[:, :-1]
-    k = (newv & valid).sum(1)                                     # distinct non-NaN values
-    cat = torch.zeros(d, dtype=torch.bool, device=dev)
-    if categorical:
-        cat[torch.tensor(sorted(categorical), device=dev)] = True
-    fast = (k > max_bins) & ~cat
-    if max_bins > 1 and bool(fast.any()):
-        j = torch.arange(1, max_bins, device=dev, dtype=torch.int64)
-        tgt = (nn[:, None] * j[None, :]).double() / max_bins      # same operations as the host code
-        pos = (torch.ceil(tgt).long() - 1).clamp_min(0)
-        pos = torch.minimum(pos, (nn - 1).clamp_min(0)[:, None])
-        v = Sf.gather(1, pos)
-        vmax = Sf.gather(1, (nn - 1).clamp_min(0)[:, None])
-        first_max = torch.searchsorted(Sf, vmax, right=False)
-        prev_max = Sf.gather(1, (first_max - 1).clamp_min(0))
-        v = torch.where(v == vmax, prev_max, v)                  # idx clipped to len(vals) - 2
-        nxt = Sf.gather(1, torch.searchsorted(Sf, v, right=True).clamp_max(s - 1))
-        cand = ((v + nxt) / 2.0).cpu().numpy()
-        # per feature np.unique of a nondecreasing row == drop repeats, for all features at once
-        fr = torch.nonzero(fast).flatten().cpu().numpy()
-        cf = cand[fr]
-        keep = np.ones(cf.shape, dtype=bool)
-        keep[:, 1:] = (cf[:, 1:] != cf[:, :-1]) & ~(np.isnan(cf[:, 1:]) & np.isnan(cf[:, :-1]))
-        col = np.cumsum(keep, 1) - 1
-        rows = np.broadcast_to(fr[:, None], cf.shape)
-        thr[rows[keep], col[keep]] = cf[keep]
-        nthr[fr] = keep.sum(1)
-    slow = torch.nonzero(~fast).flatten().tolist()
-    if slow:
-        cols = S[slow].t().cpu().numpy()
-        t2, n2 = find_thresholds(cols, len(slow), max_bins,
-                                 {i: categorical[f] for i, f in enumerate(slow) if f in categorical})
-        thr[slow], nthr[slow] = t2, n2
-    return thr, nthr
-
-
-class ChunkedRows:
-    """This rank's feature rows as a re-iterable stream of ``(row0, X_chunk [m, d] f32)`` (out-of-core fits,
-    SURVEY §5.7): the quantile sample and the binning read the chunks one at a time, so fp32 X is never
-    resident -- only its uint8 bins are.  ``it_fn()`` starts a new pass; chunks are transient (the source may
-    reuse their buffers once the work queued on them has run).  ``host_it_fn`` (optional) yields the same
-    ``(row0, X_chunk)`` from HOST memory, without any copy: the quantile sample gathers its few rows there."""
-
-    def __init__(self, it_fn, n: int, d: int, device, host_it_fn=None):
-        self.it_fn, self.n, self.d, self.device = it_fn, int(n), int(d), torch.device(device)
-        self.host_it_fn = host_it_fn
-        self.shape = (self.n, self.d)
-        self.is_cuda = self.device.type == "cuda"
-
-    def __iter__(self):
-        return iter(self.it_fn())
-
-
-def _global_sample(session, X, max_bins: int, seed: int, row_offset: int, n_global: int):
-    """Rows sampled by Philox keyed on the GLOBAL row id (the same rows whatever the GPU count), gathered
-    from every rank: the split-candidate sample (a row set: its order is not defined).  ``X`` may be a
-    :class:`ChunkedRows` stream (the same rows, sampled chunk by chunk)."""
-    comm = session.comm
-    n = X.shape[0]
-    target = max(max_bins * max_bins, 10000)
-    frac = min(1.0, target / max(n_global, 1))
-    if isinstance(X, ChunkedRows) and X.host_it_fn is not None and frac < 1.0:
-        # the sampled rows (the same Philox draws on the device) gathered from the host chunks: a few thousand
-        # rows cross PCIe instead of the whole frame
-        parts = []
-        for r0, Xh in X.host_it_fn():
-            u = K.uniform(Xh.shape[0], seed ^ 0x5BD1E995, row_offset + r0, 3, device=X.device)
-            ih = K.compact_mask(u < frac).cpu()
-            parts.append(Xh.index_select(0, ih).float().to(X.device))
-        samp = torch.cat(parts) if parts else torch.zeros((0, X.d), dtype=torch.float32, device=X.device)
-    elif isinstance(X, ChunkedRows):
-        parts = []
-        for r0, Xc in X:
-            if frac < 1.0:
-                u = K.uniform(Xc.shape[0], seed ^ 0x5BD1E995, row_offset + r0, 3, device=Xc.device)
-                parts.append(Xc[K.compact_mask(u < frac)].float())
-            else:
-                parts.append(Xc.float().clone())
-        samp = torch.cat(parts) if parts else torch.zeros((0, X.d), dtype=torch.float32, device=X.device)
-    elif frac < 1.0:
-        # the quantile thresholds depend on the sample's values only (each column is sorted): the rows are
-        # gathered in the kernel's arbitrary order, no sort of the ids
-        idx = K.sample_rows(n, seed ^ 0x5BD1E995, row_offset, 3, frac, X.device, ordered=False) \
-            if X.is_cuda and n else None
-        if idx is None:
-            u = K.uniform(n, seed ^ 0x5BD1E995, row_offset, 3, device=X.device)
-            idx = K.compact_mask(u < frac)
-        samp = X[idx]
-    else:
-        samp = X
-    if comm.distributed:
-        samp = torch.cat(comm.all_gather_varlen(samp.contiguous()))
-    return samp
-
-
-class _Once:
-    """A callable run at most once (None: nothing)."""
-
-    def __init__(self, fn):
-        self.fn = fn
-
-    def __call__(self):
-        fn, self.fn = self.fn, None
-        if fn is not None:
-            fn()
-
-
-def make_binned(session, X: torch.Tensor, categorical: Dict[int, int], max_bins: int, seed: int,
-                row_offset: int, n_global: int, missing: Optional[float] = None, before_binize=None) -> BinnedData:
-    """:func:`_make_binned`, reused across the trials of one hyperparameter search (bincache.scope(), entered by
-    fmin; never outside one).
-
-    before_binize(): run once, right before the binning kernel is queued (after the quantile sample and the
-    thresholds), or after a cache hit -- the caller's side-stream work that should overlap the memory-bound
-    binning rather than the latency-bound sample / sort kernels (the bootstrap draws)."""
-    from . import bincache
-    hook = _Once(before_binize)
-    if isinstance(X, ChunkedRows):  # streamed: no content fingerprint (X is never resident)
-        data = _make_binned(session, X, categorical, max_bins, seed, row_offset, n_global, missing, hook)
-    else:
-        data = bincache.cached(
-            lambda: (bincache.fingerprint(X), tuple(sorted(categorical.items())), int(max_bins), int(seed),
-                     int(row_offset), int(n_global), None if missing is None else float(missing), str(X.device)),
-            lambda: _make_binned(session, X, categorical, max_bins, seed, row_offset, n_global, missing, hook),
-            comm=session.comm)
-    hook()
-    return data
-
-
-def _binize_src(X, thr, nthr, missing=None, want_rm=False, rm_layout="std"):
-    """K.binize of a tensor, or of a ChunkedRows stream chunk by chunk into full-size bins (and row copy)."""
-    if not isinstance(X, ChunkedRows):
-        return K.binize(X, thr, nthr, missing=missing, want_rm=want_rm, rm_layout=rm_layout)
-    n, d = X.shape
-    G = (d + 7) // 8
-    bins = torch.empty((G, n, 8), dtype=torch.uint8, device=X.device)
-    rm = None
-    if want_rm and X.is_cuda:
-        s10 = rm_layout == "s10"
-        Gs = 16 if (s10 or (K.BINS_RM_PAD and G <= 16)) else G
-        rm = torch.empty((n, Gs, 8), dtype=torch.uint8, device=X.device)
-    rm_ok = rm is not None
-    for r0, Xc in X:
-        res = K.binize(Xc, thr, nthr, missing=missing, want_rm=rm_ok, rm_layout=rm_layout,
-                       out_full=(bins, rm), row0=r0)
-        rm_ok = rm_ok and res[1] is not None
-    if want_rm and not rm_ok:  # a chunk took a kernel without the row copy: rebuilt from the bins on demand
-        rm = None if rm_layout != "s10" or not X.is_cuda else K.bins_seg10(bins, d)
-    return bins, (rm if want_rm else None)
-
-
-def _make_binned(session, X, categorical: Dict[int, int], max_bins: int, seed: int,
-                 row_offset: int, n_global: int, missing: Optional[float] = None, before_binize=None) -> BinnedData:
-    """Global-sample quantile thresholds + device binning.
-
-    ``missing`` (XGBoost semantics, ML 11:67 ``missing=0``): NaN and values equal
-    to ``missing`` go to a dedicated bin 0; the remaining ``max_bins - 1`` bins
-    hold the observed values, so every split can route missing rows either way.
-    """
-    d = X.shape[1]
-    before_binize = before_binize if before_binize is not None else (lambda: None)
-    if missing is not None:
-        # thresholds of the observed values from the (missing -> NaN) global sample; the binning kernel maps
-        # missing values to -inf -> bin 0 on the fly (no masked copies of the full matrix)
-        samp = _global_sample(session, X, max_bins - 1, seed, row_offset, n_global)
-        sm = torch.isnan(samp) if math.isnan(missing) else (torch.isnan(samp) | (samp == float(missing)))
-        samp = torch.where(sm, torch.full_like(samp, float("nan")), samp)
-        if max_bins > 2:
-            with _tr.span("tree.find_thresholds"):
-                ithr, inthr = find_thresholds_t(samp.double(), max_bins - 1, {})
-        else:
-            ithr, inthr = np.zeros((d, 0)), np.zeros(d, dtype=np.int32)
-        thr = np.concatenate([np.full((d, 1), -np.finfo(np.float32).max), ithr], 1)
-        nthr = inthr + 1
-        thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
-        before_binize()
-        with _tr.span("tree.binize"):
-            bins, rm = _binize_src(X, thr_t, torch.from_numpy(nthr).to(X.device), missing=float(missing),
-                                   want_rm=True)
-        return BinnedData(_resident(X), bins, thr, nthr, {}, X.shape[0], n_global, row_offset, d, max_bins, True,
-                          rm)
-    for f, k in categorical.items():
-        if k > max_bins:
-            raise IllegalArgumentException(
-                f"requirement failed: DecisionTree requires maxBins (= {max_bins}) to be at least as large as the "
-                f"number of values in each categorical feature, but categorical feature {f} has {k} values. "
-                f"Consider removing this and other categorical features with a large number of values, or add "
-                f"more training examples.")
-    if max_bins > 256:
-        raise IllegalArgumentException("maxBins must be <= 256 on this engine (uint8 bins)")
-    n = X.shape[0]
-    samp = _global_sample(session, X, max_bins, seed, row_offset, n_global)
-    s10 = _seg10_ok(X, d, max_bins)
-    if SPEC_THRESHOLDS and not categorical and X.is_cuda and not isinstance(X, ChunkedRows):
-        # the binning queued straight on the K3 kernel's device thresholds; the host checks behind it that every
-        # feature had more than max_bins distinct sample values (then the thresholds are exactly the host path's)
-        # -- no device -> host -> device round trip between the quantile kernel and the binning
-        with _tr.span("tree.find_thresholds"):
-            q = K.quantile_thresholds_dev(samp, max_bins)
-        if q is not None:
-            thr_d, nthr_d, pend = q
-            before_binize()
-            with _tr.span("tree.binize"):
-                bins, rm = K.binize(X, thr_d.float(), nthr_d, want_rm=True, rm_layout="s10" if s10 else "std")
-            thr, ints = pend.get()
-            if bool((ints[1] > max_bins).all()):
-                thr, nthr = thr.copy(), ints[0].copy()
-                if s10:
-                    return BinnedData(X, bins, thr, nthr, {}, n, n_global, row_offset, d, max_bins, False, None, rm)
-                return BinnedData(X, bins, thr, nthr, {}, n, n_global, row_offset, d, max_bins, False, rm)
-            del bins, rm  # a feature with few distinct values: the host path below, then bin again
-    with _tr.span("tree.find_thresholds"):
-        thr, nthr = find_thresholds_t(samp.double(), max_bins, categorical)
-    thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)
-    nthr_t = torch.from_numpy(nthr).to(X.device)
-    before_binize()
-    with _tr.span("tree.binize"):
-        # the row-major copy (segment histograms' row gathers) comes out of the same kernel
-        bins, rm = _binize_src(X, thr_t, nthr_t, want_rm=True, rm_layout="s10" if s10 else "std")
-    if s10:
-        return BinnedData(_resident(X), bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins,
-                          False, None, rm)
-    return BinnedData(_resident(X), bins, thr, nthr, dict(categorical), n, n_global, row_offset, d, max_bins,
-                      False, rm)
-
-
-def _resident(X):
-    """BinnedData.X: the feature matrix, or None for a streamed (out-of-core) source."""
-    return None if isinstance(X, ChunkedRows) else X
-
-
-# ============================================================ forest storage
-_ZERO_MASK = np.zeros(8, dtype=np.uint32)
-_ZERO_MASK.flags.writeable = False
-
-
-class Forest:
-    """Struct-of-arrays node store for an ensemble (host), + cached device arrays.
-
-    ``value[i]``: the node's k outputs (a float sequence: numpy array or list); ``catmask[i]``: uint32[8] bitmask
-    (leaves share one read-only zero mask)."""
-
-    def __init__(self, K_: int):
-        # bookkeeping a trainer left to run later (settle()): the last level's node lists, appended while the
-        # GPU predicts instead of between the last split and the predict launch (the node-list fields below are
-        # properties that settle first, so every reader sees the complete forest)
-        self._pending: list = []
-        self._settling = False
-        self.K = K_
-        self.feat: List[int] = []
-        self.thr: List[float] = []
-        self.bin: List[int] = []
-        self.left: List[int] = []
-        self.right: List[int] = []
-        self.catmask: List[np.ndarray] = []
-        self.is_cat: List[bool] = []
-        self.value: List[np.ndarray] = []
-        self.weight: List[float] = []
-        self.gain: List[float] = []
-        self.impurity: List[float] = []
-        self.depth: List[int] = []
-        self.roots: List[int] = []
-        self._dev = {}
-        self._heap_np = None  # (struct [T, 2^(D+1)-1, 2] int32, leaf values [T, 2^(D+1)-1] f64, D) built by
-        # ForestTrainer.train (Forest.heap_struct's arrays), or None
-
-    def settle(self) -> None:
-        """Run the deferred bookkeeping (idempotent; a no-op when nothing is pending)."""
-        if self._settling:
-            return
-        self._settling = True
-        try:
-            while self._pending:
-                self._pending.pop(0)()
-        finally:
-            self._settling = False
-
-    def __getstate__(self):
-        self.settle()
-        st = dict(self.__dict__)
-        st["_pending"] = []
-        return st
-
-    def lists(self) -> dict:
-        """The node-list fields (settled) as a dict name -> list, for loops that touch many nodes (one settle check
-        instead of one property call per access)."""
-        if self._pending and not self._settling:
-            self.settle()
-        d = self.__dict__
-        return {n: d["_" + n] for n in _NODE_FIELDS}
-
-    def add(self, value, weight, depth, impurity=float("nan")) -> int:
-        if self._pending and not self._settling:
-            self.settle()
-        d = self.__dict__
-        i = len(d["_feat"])
-        d["_feat"].append(-1)
-        d["_thr"].append(0.0)
-        d["_bin"].append(0)
-        d["_left"].append(-1)
-        d["_right"].append(-1)
-        d["_catmask"].append(np.zeros(8, dtype=np.uint32))
-        d["_is_cat"].append(False)
-        d["_value"].append(np.asarray(value, dtype=np.float64).reshape(-1))
-        d["_weight"].append(float(weight))
-        d["_gain"].append(0.0)
-        d["_impurity"].append(float(impurity))
-        d["_depth"].append(depth)
-        return i
-
-    def add_many(self, values: np.ndarray, weights: np.ndarray, depth: int, impurity: np.ndarray) -> np.ndarray:
-        """Append N leaf nodes at once (values [N, k]); returns their ids."""
-        i0, N = len(self.feat), len(weights)
-        if N == 0:  # a level whose splits all failed produces no children
-            return np.zeros(0, dtype=np.int64)
-        values = np.asarray(values, dtype=np.float64).reshape(N, -1)
-        self.feat.extend([-1] * N)
-        self.thr.extend([0.0] * N)
-        self.bin.extend([0] * N)
-        self.left.extend([-1] * N)
-        self.right.extend([-1] * N)
-        # leaves share one read-only zero mask (a categorical split assigns its own) and take their values as
-        # float lists: N fresh numpy rows per field cost ~0.2 ms at the headline's last level (640 leaves) while
-        # the GPU waits for the predict launch
-        self.catmask.extend([_ZERO_MASK] * N)
-        self.is_cat.extend([False] * N)
-        self.value.extend(values.tolist())
-        self.weight.extend(np.asarray(weights, dtype=np.float64).tolist())
-        self.gain.extend([0.0] * N)
-        self.impurity.extend(np.asarray(impurity, dtype=np.float64).tolist())
-        self.depth.extend([depth] * N)
-        return np.arange(i0, i0 + N, dtype=np.int64)
-
-    def set_splits(self, fids, feats, gains, bins, thrs, has_thr, lefts, rights) -> None:
-        """Turn leaves ``fids`` into split nodes (numeric ones, ``has_thr``, also get bin + threshold).
-
-        A level's split nodes lie in one contiguous id range (its active nodes were appended together), so each
-        field is updated as one numpy slice of that range instead of a Python loop per node (the last level's
-        loop ran while the GPU idled before the transform)."""
-        fids = np.asarray(fids, dtype=np.int64)
-        if fids.size == 0:
-            return
-        lo, hi = int(fids.min()), int(fids.max()) + 1
-        rel = fids - lo
-        h = np.asarray(has_thr, dtype=bool)
-        if hi - lo == fids.size and bool(h.all()) and bool((rel[1:] > rel[:-1]).all()):
-            # every node of the range splits, in order, on a threshold: plain slice assignments
-            for name, vals in (("feat", feats), ("gain", gains), ("left", lefts), ("right", rights), ("bin", bins),
-                               ("thr", thrs)):
-                getattr(self, name)[lo:hi] = np.asarray(vals, dtype=np.float64 if name in ("gain", "thr")
-                                                        else np.int64).tolist()
-            return
-        for name, vals, sel in (("feat", feats, None), ("gain", gains, None), ("left", lefts, None),
-                                ("right", rights, None), ("bin", bins, h), ("thr", thrs, h)):
-            lst = getattr(self, name)
-            seg = np.array(lst[lo:hi], dtype=np.float64 if name in ("gain", "thr") else np.int64)
-            v = np.asarray(vals)
-            if sel is None:
-                seg[rel] = v
-            else:
-                seg[rel[sel]] = v[sel]
-            lst[lo:hi] = seg.tolist()
-
-    @property
-    def num_nodes(self):
-        return len(self.feat)
-
-    def tree_nodes(self, t: int) -> List[int]:
-        L = self.lists()
-        feat, left, right = L["feat"], L["left"], L["right"]
-        out, stack = [], [self.roots[t]]
-        while stack:
-            i = stack.pop()
-            out.append(i)
-            if feat[i] >= 0:
-                stack.extend([right[i], left[i]])
-        return out
-
-    def _layout(self, feat: Optional[np.ndarray] = None):
-        """Per node: tree index (-1 if unreachable), heap slot (root 0, children 2i+1 / 2i+2) and, per tree,
-        its depth -- one vectorised sweep per level instead of a Python walk per node."""
-        N = len(self.feat)
-        tree_of = np.full(N, -1, dtype=np.int64)
-        slot = np.zeros(N, dtype=np.int64)
-        T = len(self.roots)
-        dep = np.zeros(T, dtype=np.int64)
-        if T == 0:
-            return tree_of, slot, dep
-        feat = np.asarray(self.feat, dtype=np.int64) if feat is None else feat
-        left = np.asarray(self.left, dtype=np.int64)
-        right = np.asarray(self.right, dtype=np.int64)
-        fr = np.asarray(self.roots, dtype=np.int64)
-        tree_of[fr] = np.arange(T)
-        level = 0
-        while len(fr):
-            dep[tree_of[fr]] = level
-            inner = fr[feat[fr] >= 0]
-            if not len(inner):
-                break
-            lc, rc = left[inner], right[inner]
-            tree_of[lc] = tree_of[inner]
-            tree_of[rc] = tree_of[inner]
-            if level < 62:
-                slot[lc] = 2 * slot[inner] + 1
-                slot[rc] = 2 * slot[inner] + 2
-            fr = np.concatenate([lc, rc])
-            level += 1
-        return tree_of, slot, dep
-
-    def tree_depths(self) -> np.ndarray:
-        return self._layout()[2]
-
-    def tree_depth(self, t: int) -> int:
-        return max(self.depth[i] for i in self.tree_nodes(t)) - self.depth[self.roots[t]]
-
-    # ----------------------------------------------------------- device
-    def device_arrays(self, device, values_kind: str = "value"):
-        key = (str(device), values_kind)
-        if key in self._dev:
-            return self._dev[key]
-        N = self.num_nodes
-        nodes = np.zeros((N, 4), dtype=np.int32)
-        # a forest cut by the fused tuner carries its node fields as arrays (truncate_forest): no list round trip
-        npa = self.__dict__.get("_np") if CUT_ARRAYS else None
-        if npa is not None and (len(npa["feat"]) != N or npa["is_cat"] is None or npa["value"] is None):
-            npa = None
-        feat = npa["feat"].astype(np.int32) if npa is not None else np.asarray(self.feat, dtype=np.int32)
-        leaf = feat < 0
-        isc = (npa["is_cat"] if npa is not None else np.asarray(self.is_cat, dtype=bool)) & ~leaf
-        num = ~leaf & ~isc
-        left = npa["left"].astype(np.int32) if npa is not None else np.asarray(self.left, dtype=np.int32)
-        right = npa["right"].astype(np.int32) if npa is not None else np.asarray(self.right, dtype=np.int32)
-        lid = np.nonzero(leaf)[0]
-        if npa is not None:
-            V = npa["value"][lid] if len(lid) else np.zeros((0, self.K))
-        else:
-            V = (np.stack([self.value[i] for i in lid.tolist()]).astype(np.float64) if len(lid)
-                 else np.zeros((0, self.K)))
-        if values_kind != "value" and len(lid):
-            w_all = npa["weight"] if npa is not None else np.asarray(self.weight, dtype=np.float64)
-            V = V * w_all[lid][:, None]
-        kv = V.shape[1] if V.ndim == 2 else 1
-        nodes[lid, 0] = -1
-        nodes[lid, 1] = np.arange(len(lid), dtype=np.int32) * kv
-        cid = np.nonzero(isc)[0]
-        nodes[cid, 0] = -(feat[cid] + 2)
-        nodes[cid, 1] = np.arange(len(cid), dtype=np.int32)
-        nid = np.nonzero(num)[0]
-        nodes[nid, 0] = feat[nid]
-        thr = npa["thr"] if npa is not None else np.asarray(self.thr, dtype=np.float64)
-        nodes[nid, 1] = thr[nid].astype(np.float32).view(np.int32)
-        inner = ~leaf
-        nodes[inner, 2] = left[inner]
-        nodes[inner, 3] = right[inner]
-        vals = V.reshape(-1).astype(np.float64) if V.size else np.zeros(1, np.float64)
-        masks = (np.stack([self.catmask[i] for i in cid.tolist()]).view(np.int32).reshape(-1) if len(cid)
-                 else np.zeros(8, np.int32))
-        out = tuple(K.upload(device, nodes, np.asarray(self.roots, dtype=np.int32), vals, masks))
-        self._dev[key] = out
-        return out
-
-    def _binned_arrays_contiguous(self, tree: int):
-        """binned_arrays' tables with numpy when the tree's nodes are the contiguous id range [root, end) (a
-        boosting round grows its one tree there) and it has no categorical split; else None.  The per-node Python
-        loop cost ~0.45 ms per depth-8 tree, an idle GPU gap between every GBDT round's last split and its margin
-        update."""
-        r0 = self.roots[tree]
-        r1 = self.roots[tree + 1] if tree + 1 < len(self.roots) else len(self.feat)
-        if r1 - r0 < 1 or any(self.is_cat[r0:r1]):
-            return None
-        feat = np.asarray(self.feat[r0:r1], dtype=np.int64)
-        left = np.asarray(self.left[r0:r1], dtype=np.int64)
-        right = np.asarray(self.right[r0:r1], dtype=np.int64)
-        sp = feat >= 0
-        kids = np.concatenate([left[sp], right[sp]])
-        if len(kids) != r1 - r0 - 1 or not np.array_equal(np.sort(kids), np.arange(r0 + 1, r1)):
-            return None  # not exactly the nodes reachable from this root
-        leaf = ~sp
-        nodes = np.zeros((r1 - r0, 4), dtype=np.int32)
-        nodes[:, 0] = np.where(sp, feat, -1)
-        nodes[sp, 1] = np.asarray(self.bin[r0:r1], dtype=np.int64)[sp]
-        nodes[sp, 2] = left[sp] - r0
-        nodes[sp, 3] = right[sp] - r0
-        nodes[leaf, 1] = np.arange(int(leaf.sum()))
-        vals = np.array([self.value[r0 + j][0] for j in np.nonzero(leaf)[0].tolist()], dtype=np.float32)
-        return nodes, vals.reshape(-1), np.zeros(8, np.int32)
-
-    def binned_arrays(self, device, tree: int):
-        """Single tree with bin thresholds (GBDT training-set margin update)."""
-        key = ("bin", str(device), tree)
-        if key in self._dev:
-            return self._dev[key]
-        fast = self._binned_arrays_contiguous(tree)
-        if fast is not None:
-            out = tuple(K.upload(device, *fast))
-            self._dev[key] = out
-            return out
-        idx = self.tree_nodes(tree)
-        pos = {g: j for j, g in enumerate(idx)}
-        nodes = np.zeros((len(idx), 4), dtype=np.int32)
-        vals, masks = [], []
-        for j, g in enumerate(idx):
-            if self.feat[g] < 0:
-                nodes[j] = (-1, len(vals), 0, 0)
-                vals.append(float(self.value[g][0]))
-            elif self.is_cat[g]:
-                nodes[j] = (-(self.feat[g] + 2), len(masks), pos[self.left[g]], pos[self.right[g]])
-                masks.append(self.catmask[g].view(np.int32))
-            else:
-                nodes[j] = (self.feat[g], self.bin[g], pos[self.left[g]], pos[self.right[g]])
-        out = tuple(K.upload(device, nodes, np.asarray(vals, dtype=np.float32).reshape(-1),
-                             np.concatenate(masks) if masks else np.zeros(8, np.int32)))
-        self._dev[key] = out
-        return out
-
-    def heap_arrays(self, device, values_kind: str = "value"):
-        """Single-output forests of depth <= 8: the packed predict heap (``K.pack_heap``: int32 [T, 2^(D+2)-2],
-        internal slots {feature | -1 pass-through | -(f+2) categorical, threshold / mask-offset bits} with the
-        children of slot i at 2i+1 / 2i+2, then the depth-D leaf values as fp64) plus the categorical masks, or
-        None."""
-        key = ("heap", str(device), values_kind)
-        if key in self._dev:
-            return self._dev[key]
-        pre = getattr(self, "_heap_np", None)
-        if values_kind == "value" and pre is not None and pre[0].shape[0] == len(self.roots):
-            # filled level by level by the trainer (the same table as below; tests/test_engine_heap.py)
-            h_t, m_t = K.upload(device, K.pack_heap(pre[0], pre[1], pre[2]), np.zeros(8, np.int32))
-            res = (h_t, pre[2], m_t)
-            self._dev[key] = res
-            return res
-        res = None
-        hs = self.heap_struct(values_kind)
-        if hs is not None:
-            struct, vals, D, masks = hs
-            h_t, m_t = K.upload(device, K.pack_heap(struct, vals, D), masks)
-            res = (h_t, D, m_t)
-        self._dev[key] = res
-        return res
-
-    def heap_struct(self, values_kind: str = "value"):
-        """(struct int32 [T, 2^(D+1)-1, 2], leaf values f64 [T, 2^(D+1)-1], D, masks) of a single-output forest
-        of depth <= 8 (``K.pack_heap``'s input; the trainer fills the same arrays level by level), else None."""
-        feat = np.asarray(self.feat, dtype=np.int64)  # one list conversion shared with _layout (~1.3k nodes)
-        tree_of, slot, dep = self._layout(feat)
-        D = int(dep.max()) if self.roots else 0
-        if not (self.K == 1 and self.roots and D <= 8):
-            return None
-        S = 2 ** (D + 1) - 1
-        heap = np.zeros((len(self.roots), S, 2), dtype=np.int32)
-        heap[:, :, 0] = -1
-        hv = np.zeros((len(self.roots), S), dtype=np.float64)
-        live = np.nonzero(tree_of >= 0)[0]
-        lt, ls = tree_of[live], slot[live]
-        fl = feat[live].astype(np.int32)
-        leaf = fl < 0
-        vl = self.value
-        v = (np.concatenate([vl[i] for i in live[leaf].tolist()]) if leaf.any()
-             else np.zeros(0)).astype(np.float64)
-        if values_kind != "value":
-            v = v * np.asarray(self.weight, dtype=np.float64)[live[leaf]]
-        hv[lt[leaf], ls[leaf]] = v
-        sp = ~leaf
-        isc = np.asarray(self.is_cat, dtype=bool)[live] & sp
-        num = sp & ~isc
-        heap[lt[num], ls[num], 0] = fl[num]
-        heap[lt[num], ls[num], 1] = np.asarray(self.thr, dtype=np.float64)[live[num]].astype(
-            np.float32).view(np.int32)
-        cat_ids = live[isc]
-        masks = [self.catmask[i].view(np.int32) for i in cat_ids.tolist()]
-        heap[lt[isc], ls[isc], 0] = -(fl[isc] + 2)
-        heap[lt[isc], ls[isc], 1] = np.arange(len(cat_ids), dtype=np.int32)
-        return heap, hv, D, (np.concatenate(masks) if masks else np.zeros(8, np.int32))
-
-    def predict(self, X: torch.Tensor, tree_w: np.ndarray, base=None, values_kind="value") -> torch.Tensor:
-        """[n, K] float64 predictions: base + sum_t tree_w[t] * leaf value, all fp64 in one fixed tree order on
-        every device (K.ordered_tree_sum)."""
-        tw, = K.upload(X.device, np.asarray(tree_w, np.float64).reshape(-1))
-        if self.K == 1 and X.device.type == "cuda" and HEAP_PREDICT:
-            ha = self.heap_arrays(X.device, values_kind)
-            if ha is not None:
-                b0 = 0.0 if base is None else float(np.asarray(base, np.float64).reshape(-1)[0])
-                out = K.tree_predict_heap(X, ha[0], ha[1], tw, ha[2], b0)
-                if out is not None:
-                    return out
-        nodes, roots, vals, masks = self.device_arrays(X.device, values_kind)
-        b = None if base is None else K.upload(X.device, np.asarray(base, np.float64).reshape(-1))[0]
-        return K.tree_predict(X, nodes, roots, tw, vals, masks, self.K, b)
-
-    def predict_leaf_index(self, X: torch.Tensor) -> torch.Tensor:
-        """Host reference traversal returning leaf ids [n, T] (small inputs only)."""
-        Xn = X.double().cpu().numpy()
-        out = np.zeros((Xn.shape[0], len(self.roots)), dtype=np.int64)
-        for t, r in enumerate(self.roots):
-            for i in range(Xn.shape[0]):
-                j = r
-                while self.feat[j] >= 0:
-                    x = Xn[i, self.feat[j]]
-                    if self.is_cat[j]:
-                        c = int(x)
-                        go_left = 0 <= c < 256 and (int(self.catmask[j][c >> 5]) >> (c & 31)) & 1
-                    else:
-                        go_left = x <= self.thr[j]
-                    j = self.left[j] if go_left else self.right[j]
-                out[i, t] = j
-        return torch.from_numpy(out)
-
-    # ----------------------------------------------------------- persistence
-    def state(self, prefix="forest_"):
-        catm = np.stack(self.catmask) if self.catmask else np.zeros((0, 8), np.uint32)
-        vals = np.stack(self.value) if self.value else np.zeros((0, self.K))
-        return {
-            prefix + "feat": torch.tensor(self.feat, dtype=torch.int32),
-            prefix + "thr": torch.tensor(self.thr, dtype=torch.float64),
-            prefix + "bin": torch.tensor(self.bin, dtype=torch.int32),
-            prefix + "left": torch.tensor(self.left, dtype=torch.int32),
-            prefix + "right": torch.tensor(self.right, dtype=torch.int32),
-            prefix + "catmask": torch.from_numpy(catm.view(np.int32).copy()),
-            prefix + "is_cat": torch.tensor(self.is_cat, dtype=torch.bool),
-            prefix + "value": torch.from_numpy(vals),
-            prefix + "weight": torch.tensor(self.weight, dtype=torch.float64),
-            prefix + "gain": torch.tensor(self.gain, dtype=torch.float64),
-            prefix + "impurity": torch.tensor(self.impurity, dtype=torch.float64),
-            prefix + "depth": torch.tensor(self.depth, dtype=torch.int32),
-            prefix + "roots": torch.tensor(self.roots, dtype=torch.int32),
-        }
-
-    @classmethod
-    def from_state(cls, st, prefix="forest_"):
-        vals = st[prefix + "value"].numpy()
-        f = cls(vals.shape[1] if vals.ndim == 2 else 1)
-        f.feat = st[prefix + "feat"].tolist()
-        f.thr = st[prefix + "thr"].tolist()
-        f.bin = st[prefix + "bin"].tolist()
-        f.left = st[prefix + "left"].tolist()
-        f.right = st[prefix + "right"].tolist()
-        f.catmask = [r.view(np.uint32).copy() for r in st[prefix + "catmask"].numpy()]
-        f.is_cat = st[prefix + "is_cat"].tolist()
-        f.value = [v for v in vals]
-        f.weight = st[prefix + "weight"].tolist()
-        f.gain = st[prefix + "gain"].tolist()
-        f.impurity = st[prefix + "impurity"].tolist()
-        f.depth = st[prefix + "depth"].tolist()
-        f.roots = st[prefix + "roots"].tolist()
-        return f
-
-    def feature_importances(self, d: int, trees: Optional[List[int]] = None) -> np.ndarray:
-        """Spark semantics: per-tree gain×count, normalised per tree, averaged, normalised."""
-        total = np.zeros(d)
-        trees = range(len(self.roots)) if trees is None else trees
-        for t in trees:
-            imp = np.zeros(d)
-            for i in self.tree_nodes(t):
-                if self.feat[i] >= 0:
-                    imp[self.feat[i]] += self.gain[i] * self.weight[i]
-            s = imp.sum()
-            if s > 0:
-                imp /= s
-            total += imp
-        s = total.sum()
-        return total / s if s > 0 else total
-
-
 # ============================================================ trainer
 def _impurity_from_counts(c: torch.Tensor, kind: str) -> torch.Tensor:
     # classes are summed left to right with every product rounded first (no FMA), the order K6's impurity_c
@@ -907,63 +141,6 @@ def _built_nodes(w: np.ndarray, a_sib: np.ndarray, a_parent: np.ndarray) -> np.n
     lose = (wa > ws) | ((wa == ws) & (has > a_sib[has]))
     build[has[lose]] = False
     return build
-
-
-def _settled_list(name: str):
-    key = "_" + name
-
-    def get(self):
-        if self._pending and not self._settling:
-            self.settle()
-        return self.__dict__[key]
-
-    def set_(self, v):
-        self.__dict__[key] = v
-        self.__dict__.pop("_np", None)  # a reassigned node list invalidates a cut's array snapshot
-    return property(get, set_)
-
-
-class _FrozenList(list):
-    """A node list of a forest cut by the fused tuner (truncate_forest): its node fields are also held as an
-    array snapshot (``Forest._np``) that the predictor reads instead of the lists, so the lists must not change
-    after the cut.  Reads are plain list reads; every in-place mutation raises."""
-
-    def _frozen(self, *a, **k):
-        raise TypeError("the node lists of a cut forest are immutable (its array snapshot feeds the predictor); "
-                        "build a new Forest instead")
-
-    __setitem__ = __delitem__ = __iadd__ = __imul__ = append = extend = insert = pop = remove = clear = \
-        sort = reverse = _frozen
-
-    def __reduce__(self):  # pickle / deepcopy rebuild from a plain list (the default would extend())
-        return (_FrozenList, (list(self),))
-
-
-def freeze_cut(forest: "Forest", arrays: dict) -> None:
-    """Attach the cut's node arrays (read-only) to ``forest`` and freeze its node lists (see _FrozenList)."""
-    d = forest.__dict__
-    for n in _NODE_FIELDS:
-        d["_" + n] = _FrozenList(d["_" + n])
-    d["roots"] = _FrozenList(d["roots"])
-    for a in arrays.values():
-        if isinstance(a, np.ndarray):
-            a.flags.writeable = False
-    d["_np"] = arrays
-
-
-_NODE_FIELDS = ("feat", "thr", "bin", "left", "right", "catmask", "is_cat", "value", "weight", "gain", "impurity",
-                "depth")
-for _name in _NODE_FIELDS:
-    setattr(Forest, _name, _settled_list(_name))
-del _name
-
-
-def _forest_level_ops(forest, add_args, split_args, first_id, count):
-    """One level's forest bookkeeping (ForestTrainer.train defers it to the next level's decision sync): append
-    the children, then turn the split nodes into splits pointing at them."""
-    got = forest.add_many(*add_args)
-    assert len(got) == count and (not count or got[0] == first_id)
-    forest.set_splits(*split_args)
 
 
 class ForestTrainer:

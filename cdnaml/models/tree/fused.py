@@ -35,7 +35,8 @@ import numpy as np
 import torch
 
 from ...ops import kernels as K
-from .engine import Forest, ForestTrainer, TreeParams, freeze_cut
+from .engine import ForestTrainer, TreeParams
+from .forest import Forest, freeze_cut
 
 FUSED_TUNING = os.environ.get("CDNAML_FUSED_TUNING", "1") != "0"
 

@@ -79,7 +79,7 @@ def streamed_columns(df, features_col: str, cols: List[str], head_rows: int = 0)
     after one pass that collects the other (small) columns and counts the rows; None when the frame is not
     streamed (the caller materialises it) or a collected column has nulls.  ``head_rows``: the dict also holds
     ``"__head__"``, a copy of the first rows' features (at most that many)."""
-    from .tree.engine import ChunkedRows
+    from .tree.binning import ChunkedRows
     if not OOC_FIT:
         return None
     sel = df.select(features_col, *cols)

@@ -35,7 +35,9 @@ from .base import Estimator, Model
 from .linalg import SparseVector
 from .param import TypeConverters as TC, keyword_init
 from .regression import _default_seed
-from .tree.engine import Forest, ForestTrainer, TreeParams, make_binned
+from .tree.binning import make_binned
+from .tree.engine import ForestTrainer, TreeParams
+from .tree.forest import Forest
 from .util import IllegalArgumentException, categorical_info, global_count, global_offset, local_batch, \
     streamed_columns, \
     require_vector

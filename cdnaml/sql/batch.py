@@ -22,8 +22,8 @@ _EPOCH = _dt.date(1970, 1, 1)
 
 
 def _gather_min() -> int:
-    from ..ops import kernels as K
-    return K.GATHER_MIN
+    from ..ops import relops as R
+    return R.GATHER_MIN
 
 
 class ColumnData:

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from ..ops import kernels as K
+from ..ops import relops as R
 from . import types as T
 from .batch import Batch, ColumnData, column_from_numpy, concat_columns, unify_dictionaries
 
@@ -75,7 +76,7 @@ _INT_DT = (torch.int8, torch.uint8, torch.int16, torch.int32, torch.int64, torch
 
 
 def _native_rows(dev, *ns) -> bool:
-    return dev.type == "cuda" and sum(ns) >= K.HASH_MIN_ROWS and max(ns) < (1 << 31)
+    return dev.type == "cuda" and sum(ns) >= R.HASH_MIN_ROWS and max(ns) < (1 << 31)
 
 
 def _col_kind(c: ColumnData) -> Optional[str]:
@@ -222,14 +223,14 @@ def _aggregate_native(batch: Batch, keys: List[str], aggs) -> Optional[Batch]:
     def value(expr, c):
         k = str(expr)
         if k not in vidx:
-            if len(values) == K.HP_MAX_ACC:
+            if len(values) == R.HP_MAX_ACC:
                 return None
             vidx[k] = len(values)
             values.append((c.values, c.valid))
         return vidx[k]
 
     def acc(op, j):
-        if len(accs) == K.HP_MAX_ACC:
+        if len(accs) == R.HP_MAX_ACC:
             return None
         accs.append((op, j))
         return len(accs) - 1
@@ -239,7 +240,7 @@ def _aggregate_native(batch: Batch, keys: List[str], aggs) -> Optional[Batch]:
             plan.append((name, "count*", None, ()))
             continue
         c = agg.x.eval(batch, ctx)
-        simple = (not agg.distinct and c.values.dim() == 1 and c.values.dtype in K._VAL_DT and
+        simple = (not agg.distinct and c.values.dim() == 1 and c.values.dtype in R._VAL_DT and
                   not isinstance(c.dtype, T.StringType))
         step = None
         if agg.kind == "first" and not agg.distinct:

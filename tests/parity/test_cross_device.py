@@ -314,16 +314,16 @@ def results(tmp_path_factory):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from cdnaml.ops import kernels as K
+    from cdnaml.ops import kernels as K, relops as R
     from cdnaml.sql import fused
     root = tmp_path_factory.mktemp("xdev")
     cpu, _ = _run_all("cpu", root)
-    saved = (K.HASH_MIN_ROWS, K.GATHER_MIN, fused.FUSE_MIN_ROWS)
-    K.HASH_MIN_ROWS, K.GATHER_MIN, fused.FUSE_MIN_ROWS = 0, 0, 0
+    saved = (R.HASH_MIN_ROWS, R.GATHER_MIN, fused.FUSE_MIN_ROWS)
+    R.HASH_MIN_ROWS, R.GATHER_MIN, fused.FUSE_MIN_ROWS = 0, 0, 0
     try:
         gpu, calls = _run_all("cuda", root)
     finally:
-        K.HASH_MIN_ROWS, K.GATHER_MIN, fused.FUSE_MIN_ROWS = saved
+        R.HASH_MIN_ROWS, R.GATHER_MIN, fused.FUSE_MIN_ROWS = saved
     out = os.environ.get("CDNAML_PARITY_CALLS")
     if out:  # e.g. gpurun_out/parity_calls.json: which native kernels each flow reached on the GPU
         import json

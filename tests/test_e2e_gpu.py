@@ -82,7 +82,7 @@ def test_binning_on_device_thresholds_equals_host_path(sessions, monkeypatch, fe
     """make_binned queues the binning on the quantile kernel's device thresholds and checks the distinct-value
     condition behind it; with a low-cardinality continuous column (3 values) the check fails and the host path
     re-bins.  Either way the thresholds, bins and seg10 rows equal the host-threshold path's."""
-    from cdnaml.models.tree import engine
+    from cdnaml.models.tree import binning
     rng = np.random.default_rng(5)
     n, d = 40000, 96
     X = rng.normal(size=(n, d)).astype(np.float32)
@@ -91,8 +91,8 @@ def test_binning_on_device_thresholds_equals_host_path(sessions, monkeypatch, fe
     Xd = torch.from_numpy(X).cuda()
     got = []
     for spec in (True, False):
-        monkeypatch.setattr(engine, "SPEC_THRESHOLDS", spec)
-        b = engine._make_binned(sessions, Xd, {}, 40, 7, 0, n)
+        monkeypatch.setattr(binning, "SPEC_THRESHOLDS", spec)
+        b = binning._make_binned(sessions, Xd, {}, 40, 7, 0, n)
         got.append((b.thresholds, b.nthr, b.bins.cpu(), b.record_rows()[0].cpu()))
     np.testing.assert_array_equal(got[0][1], got[1][1])
     for f in range(d):

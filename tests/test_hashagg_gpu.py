@@ -8,7 +8,7 @@ import pandas as pd
 import pytest
 import torch
 
-from cdnaml.ops import _lib, kernels as K
+from cdnaml.ops import _lib, kernels as K, relops as R
 
 pytestmark = pytest.mark.gpu
 
@@ -42,7 +42,7 @@ def calls(monkeypatch):
 @pytest.fixture(params=["local", "partitioned"])
 def path(request, monkeypatch):
     """Both K16 aggregation paths: per-chunk LDS tables + merge (few keys), and the radix-partitioned tables."""
-    monkeypatch.setattr(K, "LOCAL_FIRST", request.param == "local")
+    monkeypatch.setattr(R, "LOCAL_FIRST", request.param == "local")
     return request.param
 
 
@@ -199,7 +199,7 @@ def test_partition_overflow_falls_back(spark, monkeypatch):
     pdf = _frame(150_000, 9, nkeys=100_000)
     df = spark.createDataFrame(pdf)
     ref = df.groupBy("k").agg(F.sum("i").alias("s")).toPandas()
-    monkeypatch.setattr(K, "_hp_shape", lambda n, na: (64, 56, 1))
+    monkeypatch.setattr(R, "_hp_shape", lambda n, na: (64, 56, 1))
     assert K.hash_groups(torch.arange(10_000, device="cuda")) is None
     got = df.groupBy("k").agg(F.sum("i").alias("s")).toPandas()
     assert got["k"].tolist() == ref["k"].tolist() and got["s"].tolist() == ref["s"].tolist()

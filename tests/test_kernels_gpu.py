@@ -700,7 +700,7 @@ def test_partition_dest(dev, W):
 def test_heap_predict_matches_node_predict(dev, monkeypatch):
     """K8 heap-layout walk == int4-node walk (categorical splits, NaN features, GBT weighted leaves)."""
     import cdnaml
-    from cdnaml.models.tree import engine as E
+    from cdnaml.models.tree import forest as F
     from cdnaml.ml.regression import RandomForestRegressor, GBTRegressor
     spark = cdnaml.SparkSession.builder.getOrCreate()
     g = torch.Generator(device=dev).manual_seed(3)
@@ -716,7 +716,7 @@ def test_heap_predict_matches_node_predict(dev, monkeypatch):
         tw = m._tree_w if hasattr(m, "_tree_w") and len(m._tree_w) else np.full(len(f.roots), 1.0 / len(f.roots))
         outs = []
         for heap in (True, False):
-            monkeypatch.setattr(E, "HEAP_PREDICT", heap)
+            monkeypatch.setattr(F, "HEAP_PREDICT", heap)
             outs.append(f.predict(Xq, tw).cpu())
         assert torch.allclose(outs[0], outs[1], rtol=1e-6, atol=1e-5)
 
