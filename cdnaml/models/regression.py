@@ -725,7 +725,7 @@ def _early_side_work(num_trees, bootstrap, rate, want_label_max=True, codes_ok=F
             return None
 
         def draws():
-            # queued right behind the quantile kernel, before the binning, on the MAIN stream (CDNAML_POISSON_STREAM
+            # queued right behind the quantile kernel, before the binning, on the MAIN stream (K.POISSON_STREAM
             # =side: the side stream).  Measured at 1e8 rows (profiles/r4/prologue_ab.md): beside the quantile sort
             # the draws kept its 1024-thread blocks off the CUs (2.1 ms for a 0.3 ms kernel); beside the binning --
             # itself ~60 % VALU-bound (6-step threshold search) -- they slowed it by more than their own 2.2 ms;

@@ -1278,9 +1278,9 @@ SEG_MIN_BLOCKS_WIDE = 512
 LANE10_CHUNK3 = False
 # record histograms through the lane-feature kernel (seg_hist_lane_kernel: lanes own features, bin-major
 # conflict-free LDS planes, one v_perm per cell address); B <= 80 (4 planes <= 80 KB of LDS), 80 < B <= 256:
-# seg_hist_lane4_kernel (64 features per block, a quarter-wave per item; CDNAML_SEG_WIDE=0 keeps the flat kernel)
+# seg_hist_lane4_kernel (64 features per block, a quarter-wave per item; SEG_LANE=False keeps the flat kernel)
 SEG_LANE = True
-# seg10 rows + the six-items-per-wave record histogram for 80 < d <= 100, B <= 40 (CDNAML_SEG10=0: lane8 rows)
+# seg10 rows + the six-items-per-wave record histogram for 80 < d <= 100, B <= 40 (SEG10=False: lane8 rows)
 SEG10 = True
 SEG_LANE_MAX_B = 256
 # records buffers carry REC_PAD readable entries past their end: the lane kernel's record loads are unconditional
@@ -1510,7 +1510,7 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
     # each LDS cell copy takes every third item of a wave's stream: rows x wmax / 3 (+ a partial trip per
     # wave) stays below the 20-bit count field (the wide kernel has one copy: rows x wmax)
     rows = max(64, min(n, (1 << 20) // (wm + 1) - 64 if wide else 3 * ((1 << 20) // (wm + 1)) - 16 * 64))
-    # CDNAML_CODES_HIST_BLOCKS > 0: shrink the row chunks toward that many blocks (>= 16k rows each).  Off by
+    # CODES_HIST_BLOCKS > 0: shrink the row chunks toward that many blocks (>= 16k rows each).  Off by
     # default: at the per-rank 1.25e7 shape 4096 blocks ran 21.0-21.3 ms per step vs 20.0-20.1 ms with the
     # largest chunks (the per-block LDS clear + flush of 100 KB outweighs the emptier last round)
     S_l = max(1, s1 - s0)
