@@ -858,9 +858,14 @@ __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __re
   __shared__ int s_fb[kP7MaxA];
   __shared__ uint8_t s_ch[2 * kP7MaxA];
   __shared__ int s_tf[kP7MaxT];
+  __shared__ uint32_t s_gmask;  // the bins words (8-feature groups) some split of the level reads
+  if (threadIdx.x == 0) s_gmask = 0u;
   for (int i = threadIdx.x; i < T; i += 256) s_tf[i] = tfirst[i];
+  __syncthreads();
+  uint32_t gm = 0u;
   for (int i = threadIdx.x; i < A; i += 256) {
     const int f = split_feat[i];
+    if (f >= 0 && (f >> 3) < G) gm |= 1u << (f >> 3);
     const int co = cat_off[i];
     s_fb[i] = f < 0 ? 0xFFFF : (co >= 0 ? (f | (co << 16) | (int)0x80000000) : (f | (split_bin[i] << 16)));
     int lo = 0, hi = T - 1;  // the tree of active node i: largest t with tfirst[t] <= i
@@ -873,7 +878,11 @@ __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __re
     s_ch[2 * i] = (uint8_t)(c0 >= 0 ? c0 - tfn : 0xFF);
     s_ch[2 * i + 1] = (uint8_t)(c1 >= 0 ? c1 - tfn : 0xFF);
   }
+  if (gm) atomicOr(&s_gmask, gm);
   __syncthreads();
+  // only the words some split reads are loaded and parked (shallow levels split on a few of the 13 groups:
+  // every skipped word is n x 8 bytes less HBM traffic per level); the mask is block-uniform
+  const uint32_t gmask = __builtin_amdgcn_readfirstlane(s_gmask);
   const uint8_t* tb = reinterpret_cast<const uint8_t*>(tile7);
   const int lr = threadIdx.x;
   const int lane = threadIdx.x & 63;
@@ -886,7 +895,7 @@ __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __re
     if (live) {
 #pragma unroll
       for (int g = 0; g < MAXG; ++g)
-        if (g < G) tile7[g * 256 + lr] = w[g];
+        if (g < G && ((gmask >> g) & 1u)) tile7[g * 256 + lr] = w[g];
     }
     for (int t0 = 0; t0 < T; t0 += kP7TB) {
       if (t0 > 0 && live) {
@@ -918,7 +927,7 @@ __global__ __launch_bounds__(256, 4) void partition7_kernel(const uint64_t* __re
   auto load_row = [&](int64_t r, uint64_t (&w)[MAXG], uint32_t (&cc)[kP7TB]) {
 #pragma unroll
     for (int g = 0; g < MAXG; ++g)
-      if (g < G) w[g] = bins[(int64_t)g * n + r];
+      if (g < G && ((gmask >> g) & 1u)) w[g] = bins[(int64_t)g * n + r];
 #pragma unroll
     for (int u = 0; u < kP7TB; ++u) cc[u] = u < T ? (uint32_t)codes[(int64_t)u * n + r] : 0xFFu;
   };
