@@ -714,15 +714,6 @@ def _early_side_work(num_trees, bootstrap, rate, want_label_max=True, codes_ok=F
         if want_label_max:
             early["yf"] = K.float_with_absmax(y_, stream=side)
 
-        early_draws = (bootstrap and num_trees > 1 and codes_ok and K.POISSON_CODES and K.POISSON_STREAM == "auto"
-                       and float(num_trees) * n <= K.POISSON_EARLY_MAX)
-        if early_draws:
-            # small shards (the 8-GPU point's 1.25e7 rows x 20 trees): the draws start now on the side stream with
-            # a bounded grid, beside the quantile sample's latency-bound kernels (off the critical path)
-            with torch.cuda.stream(side):
-                early["codes"] = K.BootstrapCodes(num_trees, n, seed_, off, rate, dev,
-                                                  grid_blocks=K.POISSON_EARLY_BLOCKS)
-            return None
 
         def draws():
             # queued right behind the quantile kernel, before the binning, on the MAIN stream (K.POISSON_STREAM

@@ -99,13 +99,11 @@ def poisson_weights(T: int, n: int, seed: int, offset: int, rate: float, device=
 POISSON_CODES = True
 
 
-# where the forest's bootstrap draws run (profiles/r4/prologue_ab.md): "main" -- in series right before the
-# binning; "side" -- the side stream at the same point; "auto" -- draws of at most POISSON_EARLY_MAX (T x rows)
-# start on the side stream with the fit (grid bounded to POISSON_EARLY_BLOCKS: beside the quantile sample's
-# latency-bound kernels, without keeping its sort's 1024-thread blocks off the CUs), larger ones in series
-POISSON_STREAM = "auto"
-POISSON_EARLY_MAX = 500000000.0
-POISSON_EARLY_BLOCKS = 512
+# where the forest's bootstrap draws run when the level-0 root histogram cannot draw them itself (POISSON_FUSED):
+# "main" -- in series before the binning, "side" -- on the side stream at the same point (profiles/r4/prologue_ab.md).
+# (An "auto" placement that started small shards' draws on the side stream with the fit measured 17.6 vs 17.5 ms at
+# the 8-GPU point's per-rank shape against the fused draws, and was removed.)
+POISSON_STREAM = "main"
 
 
 def poisson_max_draw(rate: float) -> int:

@@ -1102,7 +1102,6 @@ def test_fused_draws_grow_the_same_forest(dev, monkeypatch):
         calls["n"] += k.get("draw") is not None
         return orig(*a, **k)
     monkeypatch.setattr(K, "seg_hist_codes", counted)
-    monkeypatch.setattr(K, "POISSON_EARLY_MAX", 0)  # the headline's placement: draws in series before the binning
     digests = []
     for fused in (True, False):
         monkeypatch.setattr(K, "POISSON_FUSED", fused)
