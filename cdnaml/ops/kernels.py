@@ -1867,6 +1867,12 @@ SCATTER_RANK = 1
 SCATTER_SCAN_MIN_KB = 4
 
 
+# waves per tree of the wave-owned compaction (each owns a contiguous row range: per-wave counts, then offsets).
+# A/B (round 5): 512 / 1024 / 2048 -> 17.7 / 17.6 / 17.5-17.6 ms at the per-rank shape, 131.2-131.5 vs 129.7-129.8
+# ms at the headline for 512 vs 2048
+COMPACT_WAVES = 2048
+
+
 def _scatter_rank(KB: int) -> int:
     return 0 if (SCATTER_RANK == 1 and KB < SCATTER_SCAN_MIN_KB) else SCATTER_RANK
 
@@ -1884,7 +1890,7 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
     first_slot[1:] = np.cumsum(nb_t)[:-1]
     kmap[built] = bs[built] - first_slot[tree_of[built]]
     assert np.all(kmap[built] >= 0) and np.all(kmap[built] < KB)
-    per_wave = max(256, -(-n // (2048 * 256)) * 256)
+    per_wave = max(256, -(-n // (COMPACT_WAVES * 256)) * 256)
     Wv = -(-n // per_wave)
     L = _lib.lib()
     tf, kmap_t = upload(dev, tf_h, kmap)
