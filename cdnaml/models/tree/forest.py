@@ -12,20 +12,132 @@ from ...ops import kernels as K
 
 # single-output forests of depth <= 8 predict from a heap layout (8-byte nodes, fixed-step walks)
 HEAP_PREDICT = True
-# predictor tables of tuner-cut forests from the arrays truncate_forest computed (0: from the node lists)
-CUT_ARRAYS = True
 
 
 # ============================================================ forest storage
-_ZERO_MASK = np.zeros(8, dtype=np.uint32)
-_ZERO_MASK.flags.writeable = False
+class NodeField:
+    """One node field of a :class:`Forest`: list-like -- ``f[i]`` is a Python scalar (a read-only numpy row for the
+    [N, k] fields ``value`` / ``catmask``), slices are lists, ``append`` / ``extend`` / item and slice assignment,
+    iteration, ``==`` -- over a growable numpy array (``array()``: a view of the live nodes).  The trainer appends
+    whole levels and the predictors / tuners read the arrays: no list <-> array round trips (the L07 classifier
+    grid spent ~0.5 s per CrossValidator fit converting 100-tree depth-10 forests between the two)."""
+
+    def __init__(self, dtype, width: int = 0, data=None):
+        self._w = int(width)
+        self._a = np.zeros((16,) if self._w == 0 else (16, self._w), dtype=dtype)
+        self._n = 0
+        self.frozen = False
+        if data is not None:
+            self.extend(data)
+
+    def __len__(self) -> int:
+        return self._n
+
+    def array(self) -> np.ndarray:
+        """The live nodes' values (a view: read-only use)."""
+        return self._a[:self._n]
+
+    def __array__(self, dtype=None, copy=None):
+        a = self._a[:self._n]
+        return a.astype(dtype) if dtype is not None and a.dtype != dtype else a.copy()
+
+    def _check(self):
+        if self.frozen:
+            raise TypeError("the node lists of a cut forest are immutable; build a new Forest instead")
+
+    def _reserve(self, m: int) -> None:
+        if m > len(self._a):
+            b = np.zeros((max(m, 2 * len(self._a)),) + self._a.shape[1:], dtype=self._a.dtype)
+            b[:self._n] = self._a[:self._n]
+            self._a = b
+
+    def append(self, v) -> None:
+        self._check()
+        self._reserve(self._n + 1)
+        self._a[self._n] = v
+        self._n += 1
+
+    def extend(self, vals) -> None:
+        self._check()
+        if isinstance(vals, NodeField):
+            vals = vals.array()
+        arr = np.asarray(vals, dtype=self._a.dtype)
+        if self._w:
+            arr = arr.reshape(-1, self._w)
+        m = arr.shape[0] if arr.ndim else 0
+        self._reserve(self._n + m)
+        self._a[self._n:self._n + m] = arr
+        self._n += m
+
+    def _index(self, i) -> int:
+        i = int(i)
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError("node index out of range")
+        return i
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            sub = self._a[:self._n][i]
+            return sub.tolist() if self._w == 0 else [r.copy() for r in sub]
+        v = self._a[self._index(i)]
+        if self._w == 0:
+            return v.item()
+        v = v.view()
+        v.flags.writeable = False
+        return v
+
+    def pop(self):
+        self._check()
+        v = self[self._n - 1]
+        self._n -= 1
+        return v
+
+    def __setitem__(self, i, v) -> None:
+        self._check()
+        if isinstance(i, slice):
+            self._a[:self._n][i] = np.asarray(v, dtype=self._a.dtype)
+        else:
+            self._a[self._index(i)] = v
+
+    def __iter__(self):
+        a = self._a[:self._n]
+        return iter(a.tolist()) if self._w == 0 else iter([r.copy() for r in a])
+
+    def __eq__(self, other) -> bool:
+        o = other.array() if isinstance(other, NodeField) else np.asarray(other)
+        a = self._a[:self._n]
+        return a.shape == o.shape and bool(np.array_equal(a, o))
+
+    __hash__ = None
+
+    def __repr__(self) -> str:
+        return f"NodeField({self._a[:self._n]!r})"
+
+    def __reduce__(self):
+        return (_node_field, (self._a.dtype.str, self._w, self._a[:self._n].copy(), self.frozen))
+
+
+def _node_field(dtype, width, data, frozen=False):
+    f = NodeField(np.dtype(dtype), width, data)
+    f.frozen = frozen
+    return f
+
+
+def _fields(K_: int) -> dict:
+    return {"feat": NodeField(np.int64), "thr": NodeField(np.float64), "bin": NodeField(np.int64),
+            "left": NodeField(np.int64), "right": NodeField(np.int64), "catmask": NodeField(np.uint32, 8),
+            "is_cat": NodeField(np.bool_), "value": NodeField(np.float64, max(1, K_)),
+            "weight": NodeField(np.float64), "gain": NodeField(np.float64), "impurity": NodeField(np.float64),
+            "depth": NodeField(np.int64)}
 
 
 class Forest:
     """Struct-of-arrays node store for an ensemble (host), + cached device arrays.
 
-    ``value[i]``: the node's k outputs (a float sequence: numpy array or list); ``catmask[i]``: uint32[8] bitmask
-    (leaves share one read-only zero mask)."""
+    Every node field is a :class:`NodeField` (list-like over a growable numpy array): ``value[i]`` is the node's
+    k outputs, ``catmask[i]`` its uint32[8] category bitmask."""
 
     def __init__(self, K_: int):
         # bookkeeping a trainer left to run later (settle()): the last level's node lists, appended while the
@@ -34,18 +146,8 @@ class Forest:
         self._pending: list = []
         self._settling = False
         self.K = K_
-        self.feat: List[int] = []
-        self.thr: List[float] = []
-        self.bin: List[int] = []
-        self.left: List[int] = []
-        self.right: List[int] = []
-        self.catmask: List[np.ndarray] = []
-        self.is_cat: List[bool] = []
-        self.value: List[np.ndarray] = []
-        self.weight: List[float] = []
-        self.gain: List[float] = []
-        self.impurity: List[float] = []
-        self.depth: List[int] = []
+        for n_, f_ in _fields(K_).items():
+            self.__dict__["_" + n_] = f_
         self.roots: List[int] = []
         self._dev = {}
         self._heap_np = None  # (struct [T, 2^(D+1)-1, 2] int32, leaf values [T, 2^(D+1)-1] f64, D) built by
@@ -86,7 +188,7 @@ class Forest:
         d["_bin"].append(0)
         d["_left"].append(-1)
         d["_right"].append(-1)
-        d["_catmask"].append(np.zeros(8, dtype=np.uint32))
+        d["_catmask"].append(0)
         d["_is_cat"].append(False)
         d["_value"].append(np.asarray(value, dtype=np.float64).reshape(-1))
         d["_weight"].append(float(weight))
@@ -101,21 +203,18 @@ class Forest:
         if N == 0:  # a level whose splits all failed produces no children
             return np.zeros(0, dtype=np.int64)
         values = np.asarray(values, dtype=np.float64).reshape(N, -1)
-        self.feat.extend([-1] * N)
-        self.thr.extend([0.0] * N)
-        self.bin.extend([0] * N)
-        self.left.extend([-1] * N)
-        self.right.extend([-1] * N)
-        # leaves share one read-only zero mask (a categorical split assigns its own) and take their values as
-        # float lists: N fresh numpy rows per field cost ~0.2 ms at the headline's last level (640 leaves) while
-        # the GPU waits for the predict launch
-        self.catmask.extend([_ZERO_MASK] * N)
-        self.is_cat.extend([False] * N)
-        self.value.extend(values.tolist())
-        self.weight.extend(np.asarray(weights, dtype=np.float64).tolist())
-        self.gain.extend([0.0] * N)
-        self.impurity.extend(np.asarray(impurity, dtype=np.float64).tolist())
-        self.depth.extend([depth] * N)
+        self.feat.extend(np.full(N, -1, dtype=np.int64))
+        self.thr.extend(np.zeros(N))
+        self.bin.extend(np.zeros(N, dtype=np.int64))
+        self.left.extend(np.full(N, -1, dtype=np.int64))
+        self.right.extend(np.full(N, -1, dtype=np.int64))
+        self.catmask.extend(np.zeros((N, 8), dtype=np.uint32))
+        self.is_cat.extend(np.zeros(N, dtype=bool))
+        self.value.extend(values)
+        self.weight.extend(np.asarray(weights, dtype=np.float64))
+        self.gain.extend(np.zeros(N))
+        self.impurity.extend(np.asarray(impurity, dtype=np.float64))
+        self.depth.extend(np.full(N, depth, dtype=np.int64))
         return np.arange(i0, i0 + N, dtype=np.int64)
 
     def set_splits(self, fids, feats, gains, bins, thrs, has_thr, lefts, rights) -> None:
@@ -130,23 +229,16 @@ class Forest:
         lo, hi = int(fids.min()), int(fids.max()) + 1
         rel = fids - lo
         h = np.asarray(has_thr, dtype=bool)
-        if hi - lo == fids.size and bool(h.all()) and bool((rel[1:] > rel[:-1]).all()):
-            # every node of the range splits, in order, on a threshold: plain slice assignments
-            for name, vals in (("feat", feats), ("gain", gains), ("left", lefts), ("right", rights), ("bin", bins),
-                               ("thr", thrs)):
-                getattr(self, name)[lo:hi] = np.asarray(vals, dtype=np.float64 if name in ("gain", "thr")
-                                                        else np.int64).tolist()
-            return
         for name, vals, sel in (("feat", feats, None), ("gain", gains, None), ("left", lefts, None),
                                 ("right", rights, None), ("bin", bins, h), ("thr", thrs, h)):
-            lst = getattr(self, name)
-            seg = np.array(lst[lo:hi], dtype=np.float64 if name in ("gain", "thr") else np.int64)
+            a = getattr(self, name)
+            a._check()
+            seg = a.array()[lo:hi]  # a view: the assignments land in the field
             v = np.asarray(vals)
             if sel is None:
                 seg[rel] = v
             else:
                 seg[rel[sel]] = v[sel]
-            lst[lo:hi] = seg.tolist()
 
     @property
     def num_nodes(self):
@@ -154,13 +246,13 @@ class Forest:
 
     def tree_nodes(self, t: int) -> List[int]:
         L = self.lists()
-        feat, left, right = L["feat"], L["left"], L["right"]
-        out, stack = [], [self.roots[t]]
+        feat, left, right = L["feat"].array(), L["left"].array(), L["right"].array()
+        out, stack = [], [int(self.roots[t])]
         while stack:
             i = stack.pop()
             out.append(i)
             if feat[i] >= 0:
-                stack.extend([right[i], left[i]])
+                stack.extend([int(right[i]), int(left[i])])
         return out
 
     def _layout(self, feat: Optional[np.ndarray] = None):
@@ -207,25 +299,16 @@ class Forest:
             return self._dev[key]
         N = self.num_nodes
         nodes = np.zeros((N, 4), dtype=np.int32)
-        # a forest cut by the fused tuner carries its node fields as arrays (truncate_forest): no list round trip
-        npa = self.__dict__.get("_np") if CUT_ARRAYS else None
-        if npa is not None and (len(npa["feat"]) != N or npa["is_cat"] is None or npa["value"] is None):
-            npa = None
-        feat = npa["feat"].astype(np.int32) if npa is not None else np.asarray(self.feat, dtype=np.int32)
+        L = self.lists()
+        feat = L["feat"].array().astype(np.int32)
         leaf = feat < 0
-        isc = (npa["is_cat"] if npa is not None else np.asarray(self.is_cat, dtype=bool)) & ~leaf
+        isc = L["is_cat"].array() & ~leaf
         num = ~leaf & ~isc
-        left = npa["left"].astype(np.int32) if npa is not None else np.asarray(self.left, dtype=np.int32)
-        right = npa["right"].astype(np.int32) if npa is not None else np.asarray(self.right, dtype=np.int32)
+        left, right = L["left"].array(), L["right"].array()
         lid = np.nonzero(leaf)[0]
-        if npa is not None:
-            V = npa["value"][lid] if len(lid) else np.zeros((0, self.K))
-        else:
-            V = (np.stack([self.value[i] for i in lid.tolist()]).astype(np.float64) if len(lid)
-                 else np.zeros((0, self.K)))
+        V = L["value"].array()[lid] if len(lid) else np.zeros((0, self.K))
         if values_kind != "value" and len(lid):
-            w_all = npa["weight"] if npa is not None else np.asarray(self.weight, dtype=np.float64)
-            V = V * w_all[lid][:, None]
+            V = V * L["weight"].array()[lid][:, None]
         kv = V.shape[1] if V.ndim == 2 else 1
         nodes[lid, 0] = -1
         nodes[lid, 1] = np.arange(len(lid), dtype=np.int32) * kv
@@ -234,14 +317,13 @@ class Forest:
         nodes[cid, 1] = np.arange(len(cid), dtype=np.int32)
         nid = np.nonzero(num)[0]
         nodes[nid, 0] = feat[nid]
-        thr = npa["thr"] if npa is not None else np.asarray(self.thr, dtype=np.float64)
+        thr = L["thr"].array()
         nodes[nid, 1] = thr[nid].astype(np.float32).view(np.int32)
         inner = ~leaf
         nodes[inner, 2] = left[inner]
         nodes[inner, 3] = right[inner]
         vals = V.reshape(-1).astype(np.float64) if V.size else np.zeros(1, np.float64)
-        masks = (np.stack([self.catmask[i] for i in cid.tolist()]).view(np.int32).reshape(-1) if len(cid)
-                 else np.zeros(8, np.int32))
+        masks = (L["catmask"].array()[cid].view(np.int32).reshape(-1) if len(cid) else np.zeros(8, np.int32))
         out = tuple(K.upload(device, nodes, np.asarray(self.roots, dtype=np.int32), vals, masks))
         self._dev[key] = out
         return out
@@ -269,7 +351,7 @@ class Forest:
         nodes[sp, 2] = left[sp] - r0
         nodes[sp, 3] = right[sp] - r0
         nodes[leaf, 1] = np.arange(int(leaf.sum()))
-        vals = np.array([self.value[r0 + j][0] for j in np.nonzero(leaf)[0].tolist()], dtype=np.float32)
+        vals = self.value.array()[r0 + np.nonzero(leaf)[0], 0].astype(np.float32)
         return nodes, vals.reshape(-1), np.zeros(8, np.int32)
 
     def binned_arrays(self, device, tree: int):
@@ -327,7 +409,7 @@ class Forest:
     def heap_struct(self, values_kind: str = "value"):
         """(struct int32 [T, 2^(D+1)-1, 2], leaf values f64 [T, 2^(D+1)-1], D, masks) of a single-output forest
         of depth <= 8 (``K.pack_heap``'s input; the trainer fills the same arrays level by level), else None."""
-        feat = np.asarray(self.feat, dtype=np.int64)  # one list conversion shared with _layout (~1.3k nodes)
+        feat = self.feat.array()
         tree_of, slot, dep = self._layout(feat)
         D = int(dep.max()) if self.roots else 0
         if not (self.K == 1 and self.roots and D <= 8):
@@ -340,9 +422,7 @@ class Forest:
         lt, ls = tree_of[live], slot[live]
         fl = feat[live].astype(np.int32)
         leaf = fl < 0
-        vl = self.value
-        v = (np.concatenate([vl[i] for i in live[leaf].tolist()]) if leaf.any()
-             else np.zeros(0)).astype(np.float64)
+        v = self.value.array()[live[leaf], 0]
         if values_kind != "value":
             v = v * np.asarray(self.weight, dtype=np.float64)[live[leaf]]
         hv[lt[leaf], ls[leaf]] = v
@@ -353,10 +433,10 @@ class Forest:
         heap[lt[num], ls[num], 1] = np.asarray(self.thr, dtype=np.float64)[live[num]].astype(
             np.float32).view(np.int32)
         cat_ids = live[isc]
-        masks = [self.catmask[i].view(np.int32) for i in cat_ids.tolist()]
+        masks = self.catmask.array()[cat_ids].view(np.int32).reshape(-1)
         heap[lt[isc], ls[isc], 0] = -(fl[isc] + 2)
         heap[lt[isc], ls[isc], 1] = np.arange(len(cat_ids), dtype=np.int32)
-        return heap, hv, D, (np.concatenate(masks) if masks else np.zeros(8, np.int32))
+        return heap, hv, D, (masks if len(cat_ids) else np.zeros(8, np.int32))
 
     def predict(self, X: torch.Tensor, tree_w: np.ndarray, base=None, values_kind="value") -> torch.Tensor:
         """[n, K] float64 predictions: base + sum_t tree_w[t] * leaf value, all fp64 in one fixed tree order on
@@ -393,40 +473,21 @@ class Forest:
 
     # ----------------------------------------------------------- persistence
     def state(self, prefix="forest_"):
-        catm = np.stack(self.catmask) if self.catmask else np.zeros((0, 8), np.uint32)
-        vals = np.stack(self.value) if self.value else np.zeros((0, self.K))
-        return {
-            prefix + "feat": torch.tensor(self.feat, dtype=torch.int32),
-            prefix + "thr": torch.tensor(self.thr, dtype=torch.float64),
-            prefix + "bin": torch.tensor(self.bin, dtype=torch.int32),
-            prefix + "left": torch.tensor(self.left, dtype=torch.int32),
-            prefix + "right": torch.tensor(self.right, dtype=torch.int32),
-            prefix + "catmask": torch.from_numpy(catm.view(np.int32).copy()),
-            prefix + "is_cat": torch.tensor(self.is_cat, dtype=torch.bool),
-            prefix + "value": torch.from_numpy(vals),
-            prefix + "weight": torch.tensor(self.weight, dtype=torch.float64),
-            prefix + "gain": torch.tensor(self.gain, dtype=torch.float64),
-            prefix + "impurity": torch.tensor(self.impurity, dtype=torch.float64),
-            prefix + "depth": torch.tensor(self.depth, dtype=torch.int32),
-            prefix + "roots": torch.tensor(self.roots, dtype=torch.int32),
-        }
+        L = self.lists()
+        dt = {"feat": np.int32, "bin": np.int32, "left": np.int32, "right": np.int32, "depth": np.int32}
+        out = {prefix + n: torch.from_numpy(np.array(L[n].array(), dtype=dt.get(n, L[n].array().dtype)))
+               for n in _NODE_FIELDS}
+        out[prefix + "catmask"] = torch.from_numpy(L["catmask"].array().view(np.int32).copy())
+        out[prefix + "roots"] = torch.tensor(list(self.roots), dtype=torch.int32)
+        return out
 
     @classmethod
     def from_state(cls, st, prefix="forest_"):
         vals = st[prefix + "value"].numpy()
         f = cls(vals.shape[1] if vals.ndim == 2 else 1)
-        f.feat = st[prefix + "feat"].tolist()
-        f.thr = st[prefix + "thr"].tolist()
-        f.bin = st[prefix + "bin"].tolist()
-        f.left = st[prefix + "left"].tolist()
-        f.right = st[prefix + "right"].tolist()
-        f.catmask = [r.view(np.uint32).copy() for r in st[prefix + "catmask"].numpy()]
-        f.is_cat = st[prefix + "is_cat"].tolist()
-        f.value = [v for v in vals]
-        f.weight = st[prefix + "weight"].tolist()
-        f.gain = st[prefix + "gain"].tolist()
-        f.impurity = st[prefix + "impurity"].tolist()
-        f.depth = st[prefix + "depth"].tolist()
+        for n in _NODE_FIELDS:
+            a = st[prefix + n].numpy()
+            setattr(f, n, a.view(np.uint32) if n == "catmask" else a)
         f.roots = st[prefix + "roots"].tolist()
         return f
 
@@ -434,11 +495,13 @@ class Forest:
         """Spark semantics: per-tree gain×count, normalised per tree, averaged, normalised."""
         total = np.zeros(d)
         trees = range(len(self.roots)) if trees is None else trees
+        L = self.lists()
+        feat, gain, weight = L["feat"].array(), L["gain"].array(), L["weight"].array()
         for t in trees:
             imp = np.zeros(d)
             for i in self.tree_nodes(t):
-                if self.feat[i] >= 0:
-                    imp[self.feat[i]] += self.gain[i] * self.weight[i]
+                if feat[i] >= 0:
+                    imp[feat[i]] += gain[i] * weight[i]
             s = imp.sum()
             if s > 0:
                 imp /= s
@@ -456,19 +519,19 @@ def _settled_list(name: str):
         return self.__dict__[key]
 
     def set_(self, v):
-        self.__dict__[key] = v
-        self.__dict__.pop("_np", None)  # a reassigned node list invalidates a cut's array snapshot
+        cur = self.__dict__[key]
+        f = NodeField(cur._a.dtype, cur._w)
+        f.extend(v)
+        self.__dict__[key] = f
     return property(get, set_)
 
 
 class _FrozenList(list):
-    """A node list of a forest cut by the fused tuner (truncate_forest): its node fields are also held as an
-    array snapshot (``Forest._np``) that the predictor reads instead of the lists, so the lists must not change
-    after the cut.  Reads are plain list reads; every in-place mutation raises."""
+    """The root list of a forest cut by the fused tuner (truncate_forest): reads are plain list reads; every
+    in-place mutation raises (the cut shares its node layout with the models the tuner scores)."""
 
     def _frozen(self, *a, **k):
-        raise TypeError("the node lists of a cut forest are immutable (its array snapshot feeds the predictor); "
-                        "build a new Forest instead")
+        raise TypeError("the node lists of a cut forest are immutable; build a new Forest instead")
 
     __setitem__ = __delitem__ = __iadd__ = __imul__ = append = extend = insert = pop = remove = clear = \
         sort = reverse = _frozen
@@ -477,16 +540,12 @@ class _FrozenList(list):
         return (_FrozenList, (list(self),))
 
 
-def freeze_cut(forest: "Forest", arrays: dict) -> None:
-    """Attach the cut's node arrays (read-only) to ``forest`` and freeze its node lists (see _FrozenList)."""
+def freeze_cut(forest: "Forest") -> None:
+    """Freeze a cut forest's node fields and roots (in-place mutations raise; reassigning a field still works)."""
     d = forest.__dict__
     for n in _NODE_FIELDS:
-        d["_" + n] = _FrozenList(d["_" + n])
+        d["_" + n].frozen = True
     d["roots"] = _FrozenList(d["roots"])
-    for a in arrays.values():
-        if isinstance(a, np.ndarray):
-            a.flags.writeable = False
-    d["_np"] = arrays
 
 
 _NODE_FIELDS = ("feat", "thr", "bin", "left", "right", "catmask", "is_cat", "value", "weight", "gain", "impurity",

@@ -61,16 +61,9 @@ def estimator_kind(est) -> Optional[Tuple[str, bool]]:
 
 
 def forest_arrays(forest: Forest) -> dict:
-    """numpy copies of a finished forest's scalar node fields (+ the object lists), for several truncate_forest
-    calls on the same forest (the list -> array conversions are most of one cut's cost)."""
-    F = forest.lists()
-    A = {n: np.asarray(F[n], dtype=np.float64 if n in ("thr", "weight", "gain", "impurity") else np.int64)
-         for n in ("feat", "left", "right", "thr", "bin", "weight", "gain", "impurity", "depth")}
-    A.update(catmask=F["catmask"], is_cat=F["is_cat"], value=F["value"])
-    A["is_cat_arr"] = np.asarray(F["is_cat"], dtype=bool)
-    A["value_mat"] = np.asarray(F["value"], dtype=np.float64).reshape(len(F["value"]), -1) if len(F["value"]) \
-        else np.zeros((0, forest.K))
-    return A
+    """A finished forest's node fields as arrays (views of its NodeFields), for several truncate_forest calls on
+    the same forest."""
+    return {n: f.array() for n, f in forest.lists().items()}
 
 
 def truncate_forest(forest: Forest, num_trees: int, max_depth: int, arrays: Optional[dict] = None) -> Forest:
@@ -102,31 +95,22 @@ def truncate_forest(forest: Forest, num_trees: int, max_depth: int, arrays: Opti
     newid = np.full(len(feat), -1, dtype=np.int64)
     newid[g] = np.arange(len(g), dtype=np.int64)
     O = out.lists()
-    gl, il = g.tolist(), inn.tolist()
-    O["feat"].extend(np.where(inn, feat[g], -1).tolist())
-    O["thr"].extend(np.where(inn, A["thr"][g], 0.0).tolist())
-    O["bin"].extend(np.where(inn, A["bin"][g], 0).tolist())
-    O["left"].extend(np.where(inn, newid[np.where(inn, left[g], 0)], -1).tolist())
-    O["right"].extend(np.where(inn, newid[np.where(inn, right[g], 0)], -1).tolist())
-    zero = np.zeros(8, dtype=np.uint32)
-    zero.flags.writeable = False
-    cm, ic = A["catmask"], A["is_cat"]
-    O["catmask"].extend([cm[x] if i else zero for x, i in zip(gl, il)])
-    O["is_cat"].extend([bool(ic[x]) and i for x, i in zip(gl, il)])
-    val = A["value"]
-    O["value"].extend([val[x] for x in gl])
-    O["weight"].extend(A["weight"][g].tolist())
-    O["gain"].extend(np.where(inn, A["gain"][g], 0.0).tolist())
-    O["impurity"].extend(A["impurity"][g].tolist())
-    O["depth"].extend(A["depth"][g].tolist())
-    out.roots.extend(newid[roots].tolist())
-    # the cut's node fields as arrays too: Forest.device_arrays (the predictor of every grid model) reads them
-    # instead of converting the lists back (~0.3 s of a 27-model L07 grid evaluation)
     lnew = np.where(inn, newid[np.where(inn, left[g], 0)], -1)
     rnew = np.where(inn, newid[np.where(inn, right[g], 0)], -1)
-    freeze_cut(out, {"feat": np.where(inn, feat[g], -1), "thr": np.where(inn, A["thr"][g], 0.0), "left": lnew,
-                     "right": rnew, "is_cat": A["is_cat_arr"][g] & inn if "is_cat_arr" in A else None,
-                     "value": A["value_mat"][g] if "value_mat" in A else None, "weight": A["weight"][g]})
+    O["feat"].extend(np.where(inn, feat[g], -1))
+    O["thr"].extend(np.where(inn, A["thr"][g], 0.0))
+    O["bin"].extend(np.where(inn, A["bin"][g], 0))
+    O["left"].extend(lnew)
+    O["right"].extend(rnew)
+    O["catmask"].extend(np.where(inn[:, None], A["catmask"][g], 0))
+    O["is_cat"].extend(A["is_cat"][g] & inn)
+    O["value"].extend(A["value"][g])
+    O["weight"].extend(A["weight"][g])
+    O["gain"].extend(np.where(inn, A["gain"][g], 0.0))
+    O["impurity"].extend(A["impurity"][g])
+    O["depth"].extend(A["depth"][g])
+    out.roots.extend(newid[roots].tolist())
+    freeze_cut(out)
     return out
 
 

@@ -70,21 +70,24 @@ def forest_digest(forest) -> str:
     import numpy as np
 
     h = hashlib.sha256()
+    feat, bins, is_cat, thr, left, right = (np.asarray(getattr(forest, n)) for n in
+                                            ("feat", "bin", "is_cat", "thr", "left", "right"))
+    catmask, value = forest.catmask, forest.value
     for r in forest.roots:
         q = deque([r])
         while q:
             i = q.popleft()
-            f = int(forest.feat[i])
-            h.update(np.asarray([f, int(forest.bin[i]) if f >= 0 else 0, int(bool(forest.is_cat[i]))],
+            f = int(feat[i])
+            h.update(np.asarray([f, int(bins[i]) if f >= 0 else 0, int(bool(is_cat[i]))],
                                 dtype=np.int64).tobytes())
             if f >= 0:
-                h.update(np.asarray([forest.thr[i]], dtype=np.float64).tobytes())
-                if forest.is_cat[i]:
-                    h.update(np.asarray(forest.catmask[i], dtype=np.uint32).tobytes())
-                q.append(forest.left[i])
-                q.append(forest.right[i])
+                h.update(np.asarray([thr[i]], dtype=np.float64).tobytes())
+                if is_cat[i]:
+                    h.update(np.asarray(catmask[i], dtype=np.uint32).tobytes())
+                q.append(int(left[i]))
+                q.append(int(right[i]))
             else:
-                h.update(np.asarray(forest.value[i], dtype=np.float64).reshape(-1).tobytes())
+                h.update(np.asarray(value[i], dtype=np.float64).reshape(-1).tobytes())
     return h.hexdigest()[:16]
 
 

@@ -130,9 +130,8 @@ def test_deep_fallback_node_histograms_use_bootstrap_weights(device, monkeypatch
 
 
 def test_cut_forest_lists_are_frozen(spark):
-    """the predictor of a forest cut by the fused tuner reads the cut's array snapshot, so the cut's
-    node lists must not change after the cut (mutation raises); pickling and reassigning still work (a
-    reassigned list drops the snapshot, so the predictor rebuilds from the lists)."""
+    """a forest cut by the fused tuner is immutable after the cut (in-place mutation of its node fields
+    raises); pickling and reassigning a field still work."""
     import pickle
     from cdnaml.ml.regression import RandomForestRegressor
     from cdnaml.models.tree.fused import truncate_forest
@@ -147,8 +146,11 @@ def test_cut_forest_lists_are_frozen(spark):
                lambda: cut.roots.extend([0])):
         with pytest.raises(TypeError):
             op()
-    assert not cut._np["thr"].flags.writeable
     back = pickle.loads(pickle.dumps(cut))
     assert forest_digest(back) == forest_digest(cut)
+    with pytest.raises(TypeError):
+        back.thr[0] = 1.0
+    d0 = forest_digest(cut)
     cut.thr = [t + 0.0 for t in cut.thr]
-    assert "_np" not in cut.__dict__
+    cut.thr[0] = cut.thr[0]
+    assert forest_digest(cut) == d0
