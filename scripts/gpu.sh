@@ -12,6 +12,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of the headline step
 #   prof8            same at 1.25e7 rows
 #   pmc:<regex>      PMC pass (counters from scripts/pmc_hist.txt) over kernels matching <regex>
+#   pmccfg:<regex>   same over one bench_configs.py config (CFG_ARGS: the config and its arguments)
 #   configs          BASELINE configs 2-5 (bench_configs.py lr/cv/infer/gbdt)
 #   cfg:<name>       one bench_configs.py config ('cfg:ooc --model rf': arguments after the name; outputs
 #                    cfg_<name and arguments, non-alphanumerics as _>.json/.log)
@@ -70,6 +71,12 @@ run_step() {
             --output-format csv -d "$O/pmc" -o p -- python3 "$R/bench.py" --steps 1 --warmup 0 ${BENCH_ARGS} \
             > "$O/pmc/run.log" 2>&1)
         local rc=$?; find "$O/pmc" -name "*counter_collection.csv"; return $rc ;;
+    pmccfg:*)
+        rm -rf "$O/pmccfg"; mkdir -p "$O/pmccfg"
+        (cd /tmp && timeout -s KILL 300 rocprofv3 -i "$R/scripts/${PMC_FILE:-pmc_hist.txt}" --kernel-include-regex "${s#pmccfg:}" \
+            --output-format csv -d "$O/pmccfg" -o p -- python3 "$R/bench_configs.py" ${CFG_ARGS} \
+            > "$O/pmccfg/run.log" 2>&1)
+        local rc=$?; find "$O/pmccfg" -name "*counter_collection.csv"; return $rc ;;
     configs)
         run_step cfg:lr && run_step cfg:cv && run_step cfg:infer && run_step cfg:gbdt ;;
     cfg:*)
