@@ -47,7 +47,8 @@ USE_MSEG = True
 MSEG_L0 = True  # level 0 through segments too
 # single-tree packed fits (boosting rounds with unit hessians, DecisionTree) through row records + compaction
 MSEG_T1 = True
-# binary classification forests on the packed record / segment path (class counts from (W, W1) sums)
+# binary and 3-class classification forests on the packed record / segment path (class counts from (W, W1)
+# sums; 3 classes: (W, W1 + 2^32 W2), K.cls3_expand)
 MSEG_CLS = True
 # K6 split search in one HIP kernel (split.hip) where it applies; else the torch formulation
 NATIVE_SPLIT = True
@@ -484,7 +485,7 @@ class ForestTrainer:
         return sel[:, :8].contiguous(), sel[:, 9:11].contiguous()
 
     # ------------------------------------------------------------ training
-    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev):
+    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev, cls3=False):
         """Record histograms of a level's S slots in HIST_OVERLAP slot chunks; chunk c's all-reduce runs on the
         collective stream while chunk c + 1 is built (one per-level RCCL all-reduce of 1-50 MB otherwise
         serialises with the compute stream).  The sums are exact integers, so the result is identical to one
@@ -503,7 +504,7 @@ class ForestTrainer:
                 sbc = sb[sel].copy()
                 sbc[:, 2] -= s0
                 K.seg_hist(data.bins, d, B, rec, None, None, None, sbc, s1 - s0, wmax, scales, bins_rm=rm,
-                           interleave=True, rec=True, raw=True, out=Hb[s0:s1], rm_s10=s10)
+                           interleave=True, rec=True, raw=True, out=Hb[s0:s1], rm_s10=s10, cls3=cls3)
             with _tr.span("tree.allreduce_async", cat="comm", bytes=(s1 - s0) * d * B * 16):
                 pend.append(self.comm.all_reduce_async(Hb[s0:s1]))
         with _tr.span("tree.allreduce_wait", cat="comm"):
@@ -574,15 +575,24 @@ class ForestTrainer:
         # exactly the class histograms of the node-id / codes kernels, so the forest does not change.  Forests
         # deeper than 8 levels (u16 codes hold <= 255 nodes per tree) switch to node ids at level 8
         st.cls2 = self.classification and self.C == 2 and MSEG_CLS
+        # three classes: label codes 0 / 1 / 2^22 in the records' one quantised value; the histogram kernels
+        # re-space each block's sum to W1 + 2^32 W2, so the int64 totals must keep W1 < 2^32 (weights <= 255),
+        # and the codes hold <= 255 nodes per tree (no node-id switch below level 8)
+        st.cls3 = (self.classification and self.C == 3 and MSEG_CLS and p.max_depth <= 8 and
+                   data.n_global * 255 < 2 ** 32 and MSEG_REC and stats_rows.get("v0") is None and
+                   8 * data.B * 8 <= 128 * 1024)
         st.deep_switch = (st.cls2 or (not self.classification and DEEP_REG and T > 1)) and p.max_depth > 8
         if st.cls2:
             stats_rows = dict(stats_rows, v1=stats_rows["label"].float())
+        elif st.cls3:
+            lab = stats_rows["label"]
+            stats_rows = dict(stats_rows, v1=torch.where(lab == 2, torch.full_like(lab, K.CLS3_CODE), lab).float())
         st.stats_rows = stats_rows
         # every level builds all features of the smaller child of each split; its sibling is parent - child
         # (feature subsets are applied at split time: the measured alternatives that accumulate only each node's
         # sampled features lost 2-8x, profiles/r3/subhist_ab.md, profiles/pmc_seg_hist_subset.txt)
         st.use_mseg = (USE_MSEG and USE_CODES and (T > 1 or (MSEG_T1 and stats_rows.get("v0") is None)) and
-                       (not self.classification or st.cls2) and (p.max_depth <= 8 or st.deep_switch) and
+                       (not self.classification or st.cls2 or st.cls3) and (p.max_depth <= 8 or st.deep_switch) and
                        T * self.n_max < 2 ** 31 and data.n_global > 0)
         # one regression tree: rows grouped by node in a permutation (segment mode)
         st.use_seg = USE_SEG and T == 1 and not self.classification and not st.use_mseg
@@ -653,7 +663,7 @@ class ForestTrainer:
                 # one quantisation scale for every rank: the int64 level histograms then all-reduce to
                 # the same sums on 1 or N GPUs (the forest does not depend on the GPU count)
                 v0s = stats_rows.get("v0")
-                st.mseg_scales = (1.0, 1.0) if st.cls2 else \
+                st.mseg_scales = (1.0, 1.0) if (st.cls2 or st.cls3) else \
                     K.seg_scales(None if v0s is None else v0s.float(), stats_rows["v1"].float(), st.wmax,
                                  data.n_global, self.comm)
                 st.mseg_raw = st.mseg_scales[1] if v0s is None else st.mseg_scales
@@ -812,7 +822,8 @@ class ForestTrainer:
             # of a 1.25e7-row shard would launch ~1 round of blocks each (half of it idle)
             lv.Hb = K.seg_hist_codes(root_rows, d, B, st.codes, stats_rows["v1"], st.mseg_scales[1], wmax,
                                      slot_tree, sl_node, 0, S,
-                                     torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev), draw=draw)
+                                     torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev), draw=draw,
+                                     cls3=st.cls3)
             lv.hist_raw_scale = st.mseg_raw
         elif st.use_mseg and (depth >= 1 or MSEG_L0):
             # gather the rows of the built nodes into slot segments, then segment histograms of packed
@@ -829,13 +840,13 @@ class ForestTrainer:
                 # features, while prev_hist then holds only this rank's feature slice)
                 # comm/compute overlap: the level's slots are built in chunks, each chunk's int64
                 # histogram all-reduced (async, RCCL stream) while the next chunk is built
-                lv.Hb = self._hist_overlapped(data, d, B, perm, sb, S, wmax, st.mseg_scales, dev)
+                lv.Hb = self._hist_overlapped(data, d, B, perm, sb, S, wmax, st.mseg_scales, dev, cls3=st.cls3)
                 lv.reduced = True
             else:
                 rm, s10 = (data.record_rows() if is_rec else (data.row_major_bins(), False)) \
                     if dev.type == "cuda" else (None, False)
                 lv.Hb = K.seg_hist(data.bins, d, B, perm, v0p, v1p, wp, sb, S, wmax, st.mseg_scales, bins_rm=rm,
-                                   interleave=True, rec=is_rec, raw=True, rm_s10=s10)
+                                   interleave=True, rec=is_rec, raw=True, rm_s10=s10, cls3=st.cls3)
             lv.hist_raw_scale = st.mseg_raw
         elif st.deep_rec and S and np.bincount(st.a_tree, minlength=T).max() <= K.NODE_COMPACT_MAX_LOC:
             # levels below the u16 codes (binary classification deeper than 8): the built rows' packed
@@ -870,6 +881,8 @@ class ForestTrainer:
                                    K.upload(dev, slot_of)[0], slot_tree, None, B, id_tree=st.a_tree)
         if st.cls2 and lv.hist_raw_scale is not None:
             lv.Hb[..., 0] -= lv.Hb[..., 1]  # packed (W, W1) -> class counts (W0, W1), exact int64
+        elif st.cls3 and lv.hist_raw_scale is not None:
+            lv.Hb = K.cls3_expand(lv.Hb)  # packed (W, W1 + 2^32 W2) -> class counts (W0, W1, W2)
 
     def _level_reduce(self, st: "_FitState", lv: "_Level") -> None:
         """The level histograms summed over ranks: one fused all-reduce, or (large int64 levels) a reduce-scatter

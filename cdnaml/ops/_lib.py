@@ -115,9 +115,9 @@ _SIGS = {
     "cdna_seg_hist": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_int, c_float, c_float, c_void_p, c_int, c_void_p], c_int),
     "cdna_seg_hist_root_wide": ([c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int,
-                                 c_void_p, c_int, c_void_p, c_void_p], c_int),
+                                 c_void_p, c_int, c_void_p, c_int, c_void_p], c_int),
     "cdna_seg_hist_root": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int, c_void_p,
-                            c_int, c_void_p, c_int, c_uint64, c_uint64, c_double, c_void_p], c_int),
+                            c_int, c_void_p, c_int, c_uint64, c_uint64, c_double, c_int, c_void_p], c_int),
     "cdna_poisson_max_draw": ([c_double], c_int),
     "cdna_seg_partition": ([c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -1357,10 +1357,13 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
              v1p: torch.Tensor, wp: Optional[torch.Tensor], segs: np.ndarray, S: int, wmax: int,
              scales=None, bins_rm: Optional[torch.Tensor] = None, interleave: bool = False,
              rec: bool = False, raw: bool = False, out: Optional[torch.Tensor] = None,
-             rm_s10: bool = False) -> torch.Tensor:
+             rm_s10: bool = False, cls3: bool = False) -> torch.Tensor:
     """Moments [S, d, B, 2] of node segments of ``perm`` (row ids grouped by node).
 
     rm_s10 (rec): ``bins_rm`` is in the seg10 layout (:func:`bins_seg10`): the six-items-per-wave kernel.
+
+    cls3 (rec + raw): 3-class records (label codes 0 / 1 / ``CLS3_CODE``, scale 1): the sums are (W, W1 + 2^32 W2)
+    (:func:`cls3_expand` turns them into class counts).
 
     out (rec + raw): a zeroed int64 [S, d, B, 2] tensor (e.g. a slot-range slice of a level's buffer) the sums
     are accumulated into and returned -- lets the engine all-reduce one slot chunk while the next is built.
@@ -1373,7 +1376,7 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
     if out is not None:
         assert rec and raw and out.dtype == torch.int64 and out.is_contiguous()
     if rec:
-        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw, out, rm_s10)
+        return _seg_hist_rec(bins, d, B, perm, segs, S, wmax, scales, bins_rm, interleave, raw, out, rm_s10, cls3)
     assert not rm_s10
     return _seg_hist(bins, d, B, perm, v0p, v1p, wp, segs, S, wmax, scales, bins_rm, interleave, raw)
 
@@ -1412,6 +1415,24 @@ def _quant(v: torch.Tensor, scale: float, clamp: bool) -> torch.Tensor:
     return q.clamp(-(1 << 23), 1 << 23) if clamp else q
 
 
+# 3-class packed records (seg.hip kClsSplit): class c's label code is 0 / 1 / CLS3_CODE, so a histogram block's
+# sum w * q is W1 + 2^22 W2; the kernels re-space it to W1 + 2^32 W2 in their flush
+CLS3_CODE = 1 << 22
+
+
+def _cls3_respace(q: torch.Tensor) -> torch.Tensor:
+    """CPU twin of the kernels' flush re-spacing, per item (linear in w): q -> (q mod 2^22) + 2^32 (q >> 22)."""
+    return (q & (CLS3_CODE - 1)) + ((q >> 22) << 32)
+
+
+def cls3_expand(Hb: torch.Tensor) -> torch.Tensor:
+    """Packed 3-class sums [..., 2] (W, W1 + 2^32 W2) -> exact int64 class counts [..., 3] (W0, W1, W2)."""
+    W, P = Hb[..., 0], Hb[..., 1]
+    W1 = P & 0xFFFFFFFF
+    W2 = P >> 32
+    return torch.stack([W - W1 - W2, W1, W2], -1)
+
+
 def rec_decode(rec: torch.Tensor):
     """Packed item records -> (row, weight, quantised label) int64 tensors."""
     r = rec.to(torch.int64)
@@ -1422,7 +1443,8 @@ def rec_encode(rows: torch.Tensor, w: torch.Tensor, q: torch.Tensor) -> torch.Te
     return rows.to(torch.int64) | (w.to(torch.int64) << 31) | ((q.to(torch.int64) + (1 << 23)) << 39)
 
 
-def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False, out=None, rm_s10=False):
+def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, raw=False, out=None, rm_s10=False,
+                  cls3=False):
     G, n, _ = bins.shape
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
     if S == 0 or len(segs) == 0:
@@ -1433,7 +1455,7 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
     if not _native(bins):
         pos, slot = _seg_items(segs)
         rows, w, q = rec_decode(rec[pos])
-        iout = _int_hist_cpu(bins, d, B, S, rows, slot, w, w * q)
+        iout = _int_hist_cpu(bins, d, B, S, rows, slot, w, w * (_cls3_respace(q) if cls3 else q))
         if out is not None:
             iout = out.copy_(iout)
     else:
@@ -1454,7 +1476,7 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         wt, = upload(bins.device, work.reshape(-1))
         iout = out if out is not None else torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
         assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
-        mode = 1 | 4 | 16 | (128 if (SEG_LANE and B <= SEG_LANE_MAX_B) else 0)
+        mode = 1 | 4 | 16 | (128 if (SEG_LANE and B <= SEG_LANE_MAX_B) else 0) | (512 if cls3 else 0)
         if rm_s10:
             assert d <= 100 and B <= 40 and bins_rm.shape[1] == 16
             mode |= 128 | 256
@@ -1481,7 +1503,7 @@ def _num_cus(dev) -> int:
 
 def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, v1: torch.Tensor, qs1: float,
                    wmax: int, slot_tree: np.ndarray, slot_node: np.ndarray, s0: int, s1: int,
-                   out: torch.Tensor, draw: Optional[tuple] = None) -> torch.Tensor:
+                   out: torch.Tensor, draw: Optional[tuple] = None, cls3: bool = False) -> torch.Tensor:
     """Record histograms of slots [s0, s1) straight from the row codes (GPU, seg10 rows), for levels with at most
     one built node per tree: slot s is local node ``slot_node[s]`` of tree ``slot_tree[s]`` (level 0: every root,
     node 0).  Adds the exact int64 sums (count, sum w * q) into ``out`` [s1 - s0, d, B, 2] (zeroed by the caller)
@@ -1553,7 +1575,8 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
         wt, si = upload(codes.device, work.reshape(-1), sinfo)
         _lib.check(_lib.lib().cdna_seg_hist_root_wide(_ptr(bins_s10), n, d, B, bins_s10.shape[1] * 8, _ptr(codes),
                                                       _ptr(v1c), float(qs1), _ptr(wt), len(work), _ptr(si), s0,
-                                                      _ptr(out), _stream(codes.device)), "cdna_seg_hist_root_wide")
+                                                      _ptr(out), int(cls3), _stream(codes.device)),
+                   "cdna_seg_hist_root_wide")
         return out
     wt, si = upload(codes.device, work.reshape(-1), sinfo)
     if draw is not None:
@@ -1561,7 +1584,7 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
     seed, off, rate = draw if draw is not None else (0, 0, 1.0)
     _lib.check(_lib.lib().cdna_seg_hist_root(_ptr(bins_s10), n, d, B, _ptr(codes), _ptr(v1c), float(qs1), _ptr(wt),
                                              len(work), _ptr(si), s0, _ptr(out), int(draw is not None),
-                                             int(seed) & 0xFFFFFFFFFFFFFFFF, int(off), float(rate),
+                                             int(seed) & 0xFFFFFFFFFFFFFFFF, int(off), float(rate), int(cls3),
                                              _stream(codes.device)),
                "cdna_seg_hist_root")
     return out

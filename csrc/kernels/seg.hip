@@ -40,7 +40,18 @@ struct SegHistArgs {
   // optional packed item records (flat kernel, REC): row | weight << 31 | (q1 + 2^23) << 39 (see CompactWArgs)
   const uint64_t* rec = nullptr;
   int rs = 0;  // row stride of the row-major bins in 8-byte words (0: G); 16 = one 128-byte line per row
+  // 3-class records (kClsSplit): q = 1 (class 1) or 2^22 (class 2), so a block's sum w * q is W1 + 2^22 W2 with
+  // W1 < 3 * 2^20 (the cells' 20-bit counts); the flush re-spaces it to W1 + 2^32 W2 so the global int64 sums of
+  // many blocks (and ranks) keep the two fields apart
+  int cls_split = 0;
 };
+
+constexpr int kClsSplit = 22;
+
+__device__ __forceinline__ long long cls_respace(long long sum, int sp) {
+  if (!sp) return sum;
+  return (sum & ((1ll << sp) - 1ll)) | ((sum >> sp) << 32);
+}
 
 // PACKED: one u64 atomic per update (count << 44 | sum of w * (q + 2^23)); the
 // host bounds chunk length x max weight below 2^20 so neither field overflows.
@@ -128,7 +139,7 @@ __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const SegHistArgs
       const unsigned long long v = h[c];
       if (!v) continue;
       const unsigned long long cnt = v >> kPackShift;
-      const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+      const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
       atomicAdd(o, cnt);
       atomicAdd(o + 1, (unsigned long long)sum);
     } else {
@@ -237,7 +248,7 @@ __global__ __launch_bounds__(1024) void seg_hist_rm_kernel(const SegHistArgs a, 
       const unsigned long long v = h[c];
       if (!v) continue;
       const unsigned long long cnt = v >> kPackShift;
-      const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+      const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
       atomicAdd(o, cnt);
       atomicAdd(o + 1, (unsigned long long)sum);
     } else {
@@ -332,7 +343,7 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
     if (f >= a.d) continue;
     const unsigned long long v = h[c];
     const unsigned long long cnt = v >> kPackShift;
-    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
     if (!cnt) continue;
     unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
     atomicAdd(o, cnt);
@@ -424,7 +435,7 @@ __global__ __launch_bounds__(512) void seg_hist_lane_kernel(const SegHistArgs a,
     const unsigned long long v = h[c];
     if (!v) continue;
     const unsigned long long cnt = v >> kPackShift;
-    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
     unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
     atomicAdd(o, cnt);
     atomicAdd(o + 1, (unsigned long long)sum);
@@ -506,7 +517,7 @@ __global__ __launch_bounds__(1024, 2) void seg_hist_lane8_kernel(const SegHistAr
     const unsigned long long cnt = (v0 >> kPackShift) + (v1 >> kPackShift);
     if (!cnt) continue;
     const unsigned long long m = (1ull << kPackShift) - 1ull;
-    const long long sum = (long long)((v0 & m) + (v1 & m)) - (long long)kPackQ * (long long)cnt;
+    const long long sum = cls_respace((long long)((v0 & m) + (v1 & m)) - (long long)kPackQ * (long long)cnt, a.cls_split);
     unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
     atomicAdd(o, cnt);
     atomicAdd(o + 1, (unsigned long long)sum);
@@ -597,7 +608,8 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_kernel(const SegHistArgs
     const unsigned long long cnt = (v0 >> kPackShift) + (v1 >> kPackShift) + (v2 >> kPackShift);
     if (!cnt) continue;
     const unsigned long long m = (1ull << kPackShift) - 1ull;
-    const long long sum = (long long)((v0 & m) + (v1 & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt;
+    const long long sum = cls_respace((long long)((v0 & m) + (v1 & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt,
+                                        a.cls_split);
     unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
     atomicAdd(o, cnt);
     atomicAdd(o + 1, (unsigned long long)sum);
@@ -736,7 +748,8 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_root_kernel(const SegHis
     const unsigned long long cnt = (v0 >> kPackShift) + (v1c >> kPackShift) + (v2 >> kPackShift);
     if (!cnt) continue;
     const unsigned long long m = (1ull << kPackShift) - 1ull;
-    const long long sum = (long long)((v0 & m) + (v1c & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt;
+    const long long sum = cls_respace((long long)((v0 & m) + (v1c & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt,
+                                        a.cls_split);
     unsigned long long* o = &a.out[(((int64_t)(slot - slot0) * a.d + f) * a.B + bn) * 2];
     atomicAdd(o, cnt);
     atomicAdd(o + 1, (unsigned long long)sum);
@@ -824,7 +837,7 @@ __global__ __launch_bounds__(1024) void seg_hist_lane4_kernel(const SegHistArgs 
     const unsigned long long v = h[j * PLANE + bn * 16 + l];
     if (!v) continue;
     const unsigned long long cnt = v >> kPackShift;
-    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
     unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
     atomicAdd(o, cnt);
     atomicAdd(o + 1, (unsigned long long)sum);
@@ -1547,7 +1560,7 @@ __global__ __launch_bounds__(1024) void seg_hist_lane4_root_kernel(const SegHist
     const unsigned long long v = h[j * PLANE + bn * 16 + l];
     if (!v) continue;
     const unsigned long long cnt = v >> kPackShift;
-    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
     unsigned long long* o = &a.out[(((int64_t)(slot - slot0) * a.d + f) * a.B + bn) * 2];
     atomicAdd(o, cnt);
     atomicAdd(o + 1, (unsigned long long)sum);
@@ -1562,10 +1575,11 @@ __global__ __launch_bounds__(1024) void seg_hist_lane4_root_kernel(const SegHist
 // Wide-bin twin (seg_hist_lane4_root_kernel): bins_rm standard row-major rows of row_bytes, 80 < B <= 256.
 CDNA_API int cdna_seg_hist_root_wide(const uint8_t* bins_rm, int64_t n, int d, int B, int row_bytes,
                                      const uint16_t* codes, const float* v1, float qs1, const int* work, int nwork,
-                                     const int* sinfo, int slot0, unsigned long long* out, hipStream_t st) {
+                                     const int* sinfo, int slot0, unsigned long long* out, int cls3, hipStream_t st) {
   if (nwork <= 0) return 0;
   if (B <= 80 || B > 256 || row_bytes < ((d + 7) / 8) * 8) return (int)hipErrorInvalidValue;
   SegHistArgs a{nullptr, n, d, B, nullptr, nullptr, v1, nullptr, work, 1.f, qs1, out};
+  a.cls_split = cls3 ? kClsSplit : 0;
   const int ny = (d + 63) / 64;
   const dim3 grid((unsigned)(((nwork + 7) / 8) * 8 * ny));
   auto launch = [&](auto kern) {
@@ -1581,10 +1595,11 @@ CDNA_API int cdna_seg_hist_root_wide(const uint8_t* bins_rm, int64_t n, int d, i
 CDNA_API int cdna_seg_hist_root(const uint8_t* bins_s10, int64_t n, int d, int B, const uint16_t* codes,
                                 const float* v1, float qs1, const int* work, int nwork, const int* sinfo, int slot0,
                                 unsigned long long* out, int draw, uint64_t seed, uint64_t offset, double rate,
-                                hipStream_t st) {
+                                int cls3, hipStream_t st) {
   if (nwork <= 0) return 0;
   if (d > 100 || B > 40 || B < 1) return (int)hipErrorInvalidValue;
   SegHistArgs a{nullptr, n, d, B, nullptr, nullptr, v1, nullptr, work, 1.f, qs1, out};
+  a.cls_split = cls3 ? kClsSplit : 0;
   RootDraw dr{seed, offset, rate, cdna::poisson_cdf(draw ? rate : 1.0)};
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3((unsigned)nwork), dim3(1024), 0, st, a, bins_s10, codes, v1, qs1, sinfo, slot0, dr);
@@ -1612,6 +1627,7 @@ CDNA_API int cdna_poisson_max_draw(double rate) {
 // mode bit0: packed (no v0; count | sum in one atomic); bit1: per-row weights wp present;
 // bit4: `perm` holds packed 8-byte item records (row | w << 31 | (q1 + 2^23) << 39; flat kernel only).
 // bit7 (with bit4 and bit2, B <= 256): lane-feature kernels (seg_hist_lane_kernel, B > 80: seg_hist_lane4_kernel).
+// bit9 (packed): 3-class records, sums re-spaced to W1 + 2^32 W2 (SegHistArgs::cls_split).
 // bit2: bins are row-major [n][G] words (seg_hist_flat_kernel when packed and all groups fit 128 KB of LDS,
 // else seg_hist_rm_kernel); bit3: force seg_hist_rm_kernel.
 // work: [nwork][3] {start, len, slot}; grid = nwork x ceil(d / 8).
@@ -1623,6 +1639,7 @@ CDNA_API int cdna_seg_hist(int mode, const uint64_t* bins, int64_t n, int d, int
   if (rm_stride != 0 && rm_stride < (d + 7) / 8) return (int)hipErrorInvalidValue;
   SegHistArgs a{bins, n, d, B, perm, v0p, v1p, wp, work, qs0, qs1, out};
   a.rs = rm_stride;
+  a.cls_split = (mode & 512) ? kClsSplit : 0;
   const bool packed = (mode & 1) != 0, has_w = (mode & 2) != 0;
   if ((mode & 128) && (mode & 16) && (mode & 4) && packed) {
     // lane-feature kernel: 128 features per block (4 byte planes of BP >= B bins x 32 lanes, BP KB of LDS);

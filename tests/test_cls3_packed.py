@@ -1,0 +1,68 @@
+"""3-class forests on the packed record path (engine.MSEG_CLS with C = 3): label codes 0 / 1 / 2^22 ride the
+records' one quantised value, the histogram kernels re-space each block's sum to W1 + 2^32 W2 in their flush
+(seg.hip cls_respace) and K.cls3_expand turns (W, W1 + 2^32 W2) into exact class counts, so the forests must equal
+the class-histogram path's forests bit for bit (multiclass was off the fast path)."""
+import numpy as np
+import pytest
+import torch
+
+
+def _devices():
+    return ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def test_cls3_expand_and_respace_are_exact():
+    from cdnaml.ops import kernels as K
+    rng = np.random.default_rng(0)
+    w = torch.from_numpy(rng.integers(0, 5, 1000))
+    y = torch.from_numpy(rng.integers(0, 3, 1000))
+    q = torch.where(y == 2, torch.full_like(y, K.CLS3_CODE), y)
+    s = int((w * K._cls3_respace(q)).sum())
+    Hb = torch.tensor([[int(w.sum()), s]], dtype=torch.int64)
+    got = K.cls3_expand(Hb)[0].tolist()
+    assert got == [int(w[y == c].sum()) for c in range(3)]
+
+
+@pytest.mark.parametrize("device", _devices())
+@pytest.mark.parametrize("depth,trees,imp", [(5, 8, "gini"), (7, 3, "entropy")])
+def test_packed_3class_forest_equals_class_histograms(device, depth, trees, imp, monkeypatch):
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import cdnaml
+    from cdnaml.ml.classification import RandomForestClassifier
+    from cdnaml.models.tree import engine
+    from cdnaml.utils.synthetic import forest_digest
+    from tests.conftest import session_device
+    with session_device(device):
+        spark = cdnaml.SparkSession.builder.getOrCreate()
+        g = torch.Generator().manual_seed(depth + trees)
+        n = 40_000 if device == "cpu" else 300_000
+        d = 16 if device == "cpu" else 100
+        X = torch.randn((n, d), generator=g)
+        s = X[:, 0] * 2 - X[:, 1] + torch.sin(3 * X[:, 2]) + 0.4 * torch.randn(n, generator=g)
+        y = (s > -0.5).double() + (s > 0.8).double()  # classes 0 / 1 / 2
+        df = spark.createDataFrameFromLocalTensors({"features": X.to(device), "label": y.to(device)})
+        est = RandomForestClassifier(numTrees=trees, maxDepth=depth, maxBins=32, seed=3, impurity=imp)
+        calls = {"n": 0}
+        orig = engine.K.cls3_expand
+
+        def counted(*a, **k):
+            calls["n"] += 1
+            return orig(*a, **k)
+        monkeypatch.setattr(engine.K, "cls3_expand", counted)
+        digests, probs = [], []
+        try:
+            for flag in (False, True):
+                engine.MSEG_CLS = flag
+                calls["n"] = 0
+                m = est.fit(df)
+                digests.append(forest_digest(m._forest))
+                probs.append(m.transform(df).select("probability").toPandas()["probability"].head(50).tolist())
+                if flag:
+                    assert calls["n"] >= depth  # every level's histograms came through the packed path
+                else:
+                    assert calls["n"] == 0
+        finally:
+            engine.MSEG_CLS = True
+        assert digests[0] == digests[1]
+        assert probs[0] == probs[1]
