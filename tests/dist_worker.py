@@ -177,9 +177,9 @@ def scenario_trees_rs_overlap(spark):
         seen["rs"] += 1
         return o_rs(self, *a)
 
-    def ov(self, *a):
+    def ov(self, *a, **k):
         seen["ov"] += 1
-        return o_ov(self, *a)
+        return o_ov(self, *a, **k)
     engine.ForestTrainer._reduce_scatter_features = rs
     engine.ForestTrainer._hist_overlapped = ov
     engine.HIST_OVERLAP = 2
