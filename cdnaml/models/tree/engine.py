@@ -443,7 +443,13 @@ class ForestTrainer:
         f1 = min(d, f0 + dc)
         return (f0, f1), mine[: f1 - f0].permute(1, 0, 2, 3).contiguous()
 
-    def _rs_split(self, H: torch.Tensor, rs, masks_np, d: int, dev):
+    def _k6_exact(self, st: "_FitState", lv: "_Level") -> bool:
+        """The level histograms are exact in fp64: packed int64 sums (|q| <= 2^23 at a power-of-two scale, unit
+        count scale) whose totals stay below 2^53 ulps (total weight < 2^30), assembled by exact differences."""
+        sc = lv.hist_raw_scale
+        return sc is not None and not isinstance(sc, tuple) and self.data.n_global * max(1, st.wmax) < 2 ** 30
+
+    def _rs_split(self, H: torch.Tensor, rs, masks_np, d: int, dev, exact: bool = False):
         """K6 over this rank's feature slice, then the per-node winners of all ranks all-gathered and merged:
         the largest gain, ties to the lowest global candidate key (missing-right * d * B + f * B + b), the
         order one K6 over all features uses -- so the forest is the all-reduce forest bit for bit."""
@@ -462,7 +468,8 @@ class ForestTrainer:
             if self._native_split(dev):
                 so, tot = K.split_scan(H, self._nthr_dev(dev)[f0:f1].contiguous(), mk,
                                        1 if p.impurity == "xgb" else 0, p.min_instances, p.reg_lambda, p.gamma,
-                                       p.min_child_weight, missing_bin=p.impurity == "xgb" and self.data.missing_bin)
+                                       p.min_child_weight, missing_bin=p.impurity == "xgb" and self.data.missing_bin,
+                                       exact=exact)
             else:
                 tot = self._node_stats(H, None)
                 gain, bf, bb, lst, rst, _, _, mr = self._best_splits(H, tot, mk, self.data.nthr[f0:f1])
@@ -935,10 +942,11 @@ class ForestTrainer:
                 masks_np = lv.masks_np
                 if lv.masks_dev is not None:
                     masks_np = self._feature_masks(lv.tid.astype(np.uint64), st.a_key)
-                so, tot = self._rs_split(H, lv.rs_slice, masks_np, d, dev)
+                so, tot = self._rs_split(H, lv.rs_slice, masks_np, d, dev, exact=self._k6_exact(st, lv))
             else:
                 so, tot = K.split_scan(H, self._nthr_dev(dev), masks_t, 1 if p.impurity == "xgb" else 0,
-                                       p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight, missing_bin=mb)
+                                       p.min_instances, p.reg_lambda, p.gamma, p.min_child_weight, missing_bin=mb,
+                                       exact=self._k6_exact(st, lv))
             host_p = None
             if self._device_decode_ok(dev, st.use_codes or deep_ids, mb) and \
                     (depth + 1 < p.max_depth or st.margin_ok) and not leaving_codes:

@@ -3,6 +3,7 @@ tables the predictors read (node arrays, the packed predict heap), the pending b
 while the GPU predicts (``Forest.settle``) and the frozen node lists of a tuner-cut forest."""
 from __future__ import annotations
 
+import operator
 from typing import List, Optional
 
 import numpy as np
@@ -25,6 +26,7 @@ class NodeField:
     def __init__(self, dtype, width: int = 0, data=None):
         self._w = int(width)
         self._a = np.zeros((16,) if self._w == 0 else (16, self._w), dtype=dtype)
+        self._ro = self._read_only()
         self._n = 0
         self.frozen = False
         if data is not None:
@@ -45,11 +47,17 @@ class NodeField:
         if self.frozen:
             raise TypeError("the node lists of a cut forest are immutable; build a new Forest instead")
 
+    def _read_only(self) -> np.ndarray:
+        ro = self._a.view()
+        ro.flags.writeable = False  # rows handed out by [i] are read-only views
+        return ro
+
     def _reserve(self, m: int) -> None:
         if m > len(self._a):
             b = np.zeros((max(m, 2 * len(self._a)),) + self._a.shape[1:], dtype=self._a.dtype)
             b[:self._n] = self._a[:self._n]
             self._a = b
+            self._ro = self._read_only()
 
     def append(self, v) -> None:
         self._check()
@@ -70,7 +78,7 @@ class NodeField:
         self._n += m
 
     def _index(self, i) -> int:
-        i = int(i)
+        i = operator.index(i)
         if i < 0:
             i += self._n
         if not 0 <= i < self._n:
@@ -78,15 +86,13 @@ class NodeField:
         return i
 
     def __getitem__(self, i):
+        if i.__class__ is int and 0 <= i < self._n:  # the per-node loops' case: no index normalisation
+            return self._a.item(i) if self._w == 0 else self._ro[i]
         if isinstance(i, slice):
             sub = self._a[:self._n][i]
             return sub.tolist() if self._w == 0 else [r.copy() for r in sub]
-        v = self._a[self._index(i)]
-        if self._w == 0:
-            return v.item()
-        v = v.view()
-        v.flags.writeable = False
-        return v
+        i = self._index(i)
+        return self._a.item(i) if self._w == 0 else self._ro[i]
 
     def pop(self):
         self._check()

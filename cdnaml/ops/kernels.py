@@ -2002,13 +2002,20 @@ def bins_row_major(bins: torch.Tensor, pad: Optional[bool] = None) -> torch.Tens
 
 
 # ------------------------------------------------------------ K6 (split.hip)
+# K6 over exact histograms (split_scan(exact=True)) in the wave-parallel kernel: a wave per feature instead of a
+# thread walking every bin, the same winner bit for bit (split.hip split_scan_wave_kernel)
+SPLIT_WAVE = True
+
+
 def split_scan(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor], kind: int, min_inst: float,
                reg_lambda: float = 1.0, gamma: float = 0.0, min_child_weight: float = 1.0,
-               missing_bin: bool = False):
+               missing_bin: bool = False, exact: bool = False):
     """Best split per node of level histograms H [A, d, B, 2] (fp64) -> (out [A, 8], tot [A, 2]).
 
     out = (gain, feature, bin, left0, left1, right0, right1, missing-goes-right); gain -inf when no legal split.
-    kind 0: variance gain on (weight, sum); kind 1: XGBoost gain on (hess, grad)."""
+    kind 0: variance gain on (weight, sum); kind 1: XGBoost gain on (hess, grad).
+    exact: every prefix sum of H is exact in fp64 (int64 fixed point at power-of-two scales below 2^53), so the
+    wave-parallel kernel's summation order gives the serial kernel's bits (``SPLIT_WAVE``)."""
     A, d, B, k = H.shape
     assert k == 2 and H.dtype == torch.float64 and _native(H)
     Hc = H.contiguous()
@@ -2017,7 +2024,8 @@ def split_scan(H: torch.Tensor, nthr: torch.Tensor, masks: Optional[torch.Tensor
     nt = nthr.to(device=H.device, dtype=torch.int32).contiguous()
     m = None if masks is None else masks.to(device=H.device, dtype=torch.int32).contiguous()
     mw = 0 if m is None else m.shape[1]
-    _lib.check(_lib.lib().cdna_split_scan(_ptr(Hc), _ptr(nt), _ptr(m), mw, A, d, B, kind, int(missing_bin),
+    kw = kind | (0x100 if (exact and SPLIT_WAVE) else 0)
+    _lib.check(_lib.lib().cdna_split_scan(_ptr(Hc), _ptr(nt), _ptr(m), mw, A, d, B, kw, int(missing_bin),
                                           float(min_inst),
                                           float(reg_lambda), float(gamma), float(min_child_weight), _ptr(out),
                                           _ptr(tot), _stream(H.device)), "cdna_split_scan")

@@ -163,16 +163,221 @@ __global__ __launch_bounds__(kThreads) void split_scan_kernel(const SplitArgs a)
   }
 }
 
+// Wave-parallel K6 for EXACT histograms (int64 fixed-point sums at power-of-two scales, as every record /
+// codes path produces: each prefix sum is an exact dyadic number, so any summation order gives the same bits).
+// split_scan_kernel walks a feature's B bins serially in one thread, so a level costs one thread's 2 x B-bin walk
+// whatever A is (~155 us per level at B = 256: 1.25 ms of a 24 ms boosting round).  Here a wave owns a feature
+// (lane l: bins [R l, R l + R)), 16 waves per node: lane prefix + wave scan, the same gain_of per candidate, and
+// the same winner as split_scan_kernel including its tie order -- thread t of that kernel walks features
+// t, t + 128, ... in (feature, bin, left-then-right) order and keeps the FIRST candidate of its best gain, then the
+// block keeps the lowest key among equal gains; the per-feature first candidates kept here reproduce both steps.
+constexpr int kWaveMaxD = 4096;
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int R>
+__global__ __launch_bounds__(1024) void split_scan_wave_kernel(const SplitArgs a) {
+  __shared__ double s_fg[kWaveMaxD];  // per feature: best legal gain (-inf: none)
+  __shared__ int s_fc[kWaveMaxD];     // per feature: its first candidate of that gain, bin << 1 | missing-right
+  __shared__ double s_w[16], s_t0[16], s_t1[16], s_g[16];
+  __shared__ int s_f[16], s_k[16];
+  const int node = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const double* Hn = a.H + (int64_t)node * a.d * a.B * 2;
+  // pass 1: per-feature totals; node totals = those of the feature with the most weight (lowest feature on ties)
+  double bw = -1.0, b0 = 0.0, b1 = 0.0;
+  int bf = 0x7FFFFFFF;
+  for (int f = wid; f < a.d; f += 16) {
+    const double* hf = Hn + (int64_t)f * a.B * 2;
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int b = lane * R + r;
+      if (b < a.B) {
+        t0 += hf[2 * b];
+        t1 += hf[2 * b + 1];
+      }
+    }
+    t0 = wave_sum_d(t0);
+    t1 = wave_sum_d(t1);
+    if (t0 > bw) {
+      bw = t0;
+      b0 = t0;
+      b1 = t1;
+      bf = f;
+    }
+  }
+  if (lane == 0) {
+    s_w[wid] = bw;
+    s_t0[wid] = b0;
+    s_t1[wid] = b1;
+    s_f[wid] = bf;
+  }
+  __syncthreads();
+  double t0 = 0.0, t1 = 0.0;
+  {
+    double w = -2.0;
+    int ff = 0x7FFFFFFF;
+    for (int i = 0; i < 16; ++i)
+      if (s_w[i] > w || (s_w[i] == w && s_f[i] < ff)) {
+        w = s_w[i];
+        ff = s_f[i];
+        t0 = s_t0[i];
+        t1 = s_t1[i];
+      }
+  }
+  // pass 2: every legal threshold; per feature the best gain and its first candidate in the serial walk's order
+  for (int f = wid; f < a.d; f += 16) {
+    double best = -__builtin_inf();
+    int code = 0x7FFFFFFF;
+    const bool on = !(a.mask && !((a.mask[(int64_t)node * a.mw + (f >> 5)] >> (f & 31)) & 1u));
+    if (on) {
+      const int lim = a.nthr[f] < 0 ? 0 : a.nthr[f];
+      const double* hf = Hn + (int64_t)f * a.B * 2;
+      const double m0 = hf[0], m1 = hf[1];
+      double p0[R], p1[R];
+      double c0 = 0.0, c1 = 0.0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int b = lane * R + r;
+        c0 += b < a.B ? hf[2 * b] : 0.0;
+        c1 += b < a.B ? hf[2 * b + 1] : 0.0;
+        p0[r] = c0;
+        p1[r] = c1;
+      }
+      // exclusive wave scan of the lane totals
+      double e0 = c0, e1 = c1;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double u0 = __shfl_up(e0, o, 64), u1 = __shfl_up(e1, o, 64);
+        if (lane >= o) {
+          e0 += u0;
+          e1 += u1;
+        }
+      }
+      e0 -= c0;
+      e1 -= c1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int b = lane * R + r;
+        if (b < a.B && b < lim) {
+          const double l0 = e0 + p0[r], l1 = e1 + p1[r];
+          bool ok;
+          const double g = gain_of(a, l0, l1, t0 - l0, t1 - l1, t0, t1, &ok);
+          if (ok && g == g && g != __builtin_inf() && g != -__builtin_inf() && g > best) {
+            best = g;
+            code = b << 1;
+          }
+          if (a.missing_bin && b >= 1) {
+            const double q0 = l0 - m0, q1 = l1 - m1;
+            const double g2 = gain_of(a, q0, q1, t0 - q0, t1 - q1, t0, t1, &ok);
+            if (ok && g2 == g2 && g2 != __builtin_inf() && g2 != -__builtin_inf() && g2 > best) {
+              best = g2;
+              code = (b << 1) | 1;
+            }
+          }
+        }
+      }
+    }
+    // wave: the highest gain, the lowest code (the serial walk's first) among equal gains
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double og = __shfl_xor(best, o, 64);
+      const int oc = __shfl_xor(code, o, 64);
+      if (og > best || (og == best && oc < code)) {
+        best = og;
+        code = oc;
+      }
+    }
+    if (lane == 0) {
+      s_fg[f] = best;
+      s_fc[f] = code;
+    }
+  }
+  __syncthreads();
+  // the best gain over the node's features
+  double G = -__builtin_inf();
+  for (int f = lane; f < a.d; f += 64) G = s_fg[f] > G ? s_fg[f] : G;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(G, o, 64);
+    G = og > G ? og : G;
+  }
+  // split_scan_kernel's thread t (features t, t + 128, ...) keeps its first candidate of gain G; the block keeps the
+  // lowest key of those
+  const int off2 = a.d * a.B;
+  int key = 0x7FFFFFFF;
+  if (G != -__builtin_inf() && threadIdx.x < 128) {
+    for (int f = threadIdx.x; f < a.d; f += 128)
+      if (s_fg[f] == G) {
+        const int c = s_fc[f];
+        key = (c & 1) ? off2 + f * a.B + (c >> 1) : f * a.B + (c >> 1);
+        break;
+      }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int ok = __shfl_xor(key, o, 64);
+    key = ok < key ? ok : key;
+  }
+  if (lane == 0) s_k[wid] = key;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int k0 = s_k[0] < s_k[1] ? s_k[0] : s_k[1];
+    double* o = a.out + (int64_t)node * 8;
+    const bool found = k0 != 0x7FFFFFFF;
+    const bool mr = found && k0 >= off2;
+    const int k = mr ? k0 - off2 : k0;
+    const int f = found ? k / a.B : 0, b = found ? k - (k / a.B) * a.B : 0;
+    double l0 = 0.0, l1 = 0.0;
+    if (found) {
+      const double* hf = Hn + (int64_t)f * a.B * 2;
+      for (int q = 0; q <= b; ++q) {
+        l0 += hf[2 * q];
+        l1 += hf[2 * q + 1];
+      }
+      if (mr) {
+        l0 -= hf[0];
+        l1 -= hf[1];
+      }
+    }
+    o[0] = found ? G : -__builtin_inf();
+    o[1] = f;
+    o[2] = b;
+    o[3] = l0;
+    o[4] = l1;
+    o[5] = t0 - l0;
+    o[6] = t1 - l1;
+    o[7] = mr ? 1.0 : 0.0;
+    a.tot_out[node * 2] = t0;
+    a.tot_out[node * 2 + 1] = t1;
+  }
+}
+
 }  // namespace
 
-// kind: 0 = variance (regression trees), 1 = XGBoost gain.  out [A][8], tot_out [A][2] (fp64).
+// kind: 0 = variance (regression trees), 1 = XGBoost gain (| 0x100: exact histograms, split_scan_wave_kernel).
+// out [A][8], tot_out [A][2] (fp64).
 CDNA_API int cdna_split_scan(const double* H, const int* nthr, const uint32_t* mask, int mw, int A, int d, int B,
                              int kind, int missing_bin, double min_inst, double lambda, double gamma, double mcw,
                              double* out, double* tot_out, hipStream_t st) {
   if (A <= 0) return 0;
+  // kind bit 8: exact histograms (power-of-two fixed point) -> the wave-parallel kernel (B <= 256, d <= 4096)
+  const bool wave = (kind & 0x100) != 0;
+  kind &= 0xFF;
   if (d <= 0 || B <= 0 || (kind != 0 && kind != 1) || (missing_bin && kind != 1)) return (int)hipErrorInvalidValue;
   if ((int64_t)2 * d * B >= 0x7FFFFFFF) return (int)hipErrorInvalidValue;
   SplitArgs a{H, nthr, mask, mw, A, d, B, kind, missing_bin, min_inst, lambda, gamma, mcw, out, tot_out};
+  if (wave && B <= 256 && d <= kWaveMaxD) {
+    if (B <= 64) hipLaunchKernelGGL(split_scan_wave_kernel<1>, dim3((unsigned)A), dim3(1024), 0, st, a);
+    else if (B <= 128) hipLaunchKernelGGL(split_scan_wave_kernel<2>, dim3((unsigned)A), dim3(1024), 0, st, a);
+    else hipLaunchKernelGGL(split_scan_wave_kernel<4>, dim3((unsigned)A), dim3(1024), 0, st, a);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(split_scan_kernel, dim3((unsigned)A), dim3(kThreads), 0, st, a);
   return (int)hipGetLastError();
 }

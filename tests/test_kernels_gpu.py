@@ -792,6 +792,60 @@ def test_native_split_scan_matches_torch(dev, monkeypatch):
         assert np.abs(preds[0] - preds[1]).max() < 1e-4
 
 
+@pytest.mark.parametrize("A,d,B,kind,missing,masked", [(7, 100, 256, 1, False, False), (33, 37, 256, 1, True, False),
+                                                       (5, 100, 40, 0, False, True), (12, 300, 100, 0, False, False),
+                                                       (3, 64, 64, 1, True, True), (9, 13, 17, 0, False, False)])
+def test_split_scan_wave_bit_identical(dev, A, d, B, kind, missing, masked, monkeypatch):
+    """K6 over exact histograms: the wave-parallel kernel (a wave per feature, split_scan_wave_kernel) returns the
+    serial kernel's bits -- gains, winners (incl. the serial walk's tie order: empty bins make runs of equal gains,
+    and with no missing rows every missing-right candidate ties its left twin), left / right sums, node totals."""
+    g = torch.Generator().manual_seed(A * d + B)
+    cnt = torch.randint(0, 50, (A, d, B), generator=g).double()
+    cnt[torch.rand((A, d, B), generator=g) < 0.4] = 0.0  # empty bins: equal-gain runs
+    if missing:
+        cnt[: A // 2, :, 0] = 0.0  # half the nodes without missing rows: left / right twins tie
+    s = torch.randint(-(1 << 20), 1 << 20, (A, d, B), generator=g).double() * cnt.sign() * 2.0 ** -14
+    H = torch.stack([cnt, s], -1)
+    nthr = torch.randint(B // 2, B + 1, (d,), generator=g).int()
+    nthr[d // 3] = -1  # a feature with no legal threshold
+    masks = None
+    if masked:
+        bits = torch.rand((A, d), generator=g) < 0.5
+        words = torch.zeros((A, (d + 31) // 32), dtype=torch.int64)
+        for f in range(d):
+            words[:, f >> 5] |= bits[:, f].long() << (f & 31)
+        masks = words.to(torch.int32)
+    Hd = H.to(dev)
+    outs = []
+    for exact in (False, True):
+        monkeypatch.setattr(K, "SPLIT_WAVE", True)
+        so, tot = K.split_scan(Hd, nthr.to(dev), None if masks is None else masks.to(dev), kind, 1.0, 1.5, 0.0,
+                               1.0, missing_bin=missing, exact=exact)
+        outs.append((so.cpu(), tot.cpu()))
+    assert torch.equal(outs[0][1], outs[1][1])
+    a, b = outs[0][0], outs[1][0]
+    assert torch.equal(a[:, 1:], b[:, 1:]), (a[:, :3], b[:, :3])
+    assert torch.equal(a[:, 0], b[:, 0])
+
+
+def test_split_scan_wave_same_boosted_forest(dev, monkeypatch):
+    """The boosting rounds take the wave-parallel K6 (exact packed histograms): the forest is the serial kernel's."""
+    import cdnaml
+    from cdnaml.ml.xgboost import XgboostRegressor
+    from cdnaml.utils.synthetic import forest_digest
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator(device=dev).manual_seed(9)
+    X = torch.randn((200000, 40), generator=g, device=dev)
+    y = (X[:, 0] * 2 + torch.sin(X[:, 1] * 3) + (X[:, 2] > 0.5).float()).double()
+    df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
+    digests = []
+    for wave in (False, True):
+        monkeypatch.setattr(K, "SPLIT_WAVE", wave)
+        m = XgboostRegressor(n_estimators=4, max_depth=8, max_bin=256, learning_rate=0.3).fit(df)
+        digests.append(forest_digest(m._forest))
+    assert digests[0] == digests[1]
+
+
 @pytest.mark.parametrize("n,p", [(1000003, 0.3), (4097, 0.0), (50000, 1.0)])
 def test_compact_mask(dev, n, p):
     """K19 stream compaction == torch.nonzero order."""
