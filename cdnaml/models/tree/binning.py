@@ -36,11 +36,19 @@ class BinnedData:
     missing_bin: bool = False         # bin 0 holds missing values (XGBoost sparsity-aware splits)
     bins_rm: Optional[torch.Tensor] = None  # lazily built row-major copy [n, G, 8] (segment-mode histograms)
     bins_s10: Optional[torch.Tensor] = None  # seg10 row layout [n, 16, 8] written by binize (K.bins_seg10)
+    bins_fm: Optional[torch.Tensor] = None   # lazily built feature-major byte copy [G * 8, n] (boosting partitions)
 
     def row_major_bins(self) -> torch.Tensor:
         if self.bins_rm is None:
             self.bins_rm = K.bins_row_major(self.bins)
         return self.bins_rm
+
+    def feature_major_bins(self) -> torch.Tensor:
+        """[G * 8, n] uint8: byte f * n + r is row r's bin of feature f (built once, kept for the fit's rounds)."""
+        if self.bins_fm is None:
+            G, n, _ = self.bins.shape
+            self.bins_fm = self.bins.permute(0, 2, 1).reshape(G * 8, n).contiguous()
+        return self.bins_fm
 
     def record_rows(self):
         """(rows, is_seg10) for the record histograms: the seg10 copy when binize wrote one, else the standard

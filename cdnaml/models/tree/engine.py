@@ -412,9 +412,11 @@ class ForestTrainer:
                 K.partition(data.bins, node, dec["split_feat"], dec["split_bin"], dec["cat_off"],
                             dec["masks"].reshape(-1), dec["child"])
                 return dec
+            fm = data.feature_major_bins() if (margin is not None and K.PART_FEATURE_MAJOR) else None
             K.partition_codes(data.bins, codes, tf_d, dec["tfirst_next"], dec["split_feat"],
                               dec["split_bin"], dec["cat_off"], dec["masks"].reshape(-1), dec["child"],
-                              margin=(margin[0], dec["lv"], margin[1]) if margin is not None else None)
+                              margin=(margin[0], dec["lv"], margin[1]) if margin is not None else None,
+                              bins_fm=fm)
         return dec
 
     # ------------------------------------------------------------ reduce-scatter by feature

@@ -211,7 +211,10 @@ class _XgbEstimatorBase(Estimator):
                 # the leaf values are the trainer's own)
                 fk = F[:, k]
                 margin = (fk, eta) if (bag is None and fk.is_contiguous() and self.getReg_alpha() <= 0) else None
-                trainer.train(1, {"v0": v0, "v1": g[:, k].float().contiguous()},
+                v1 = g[:, k].float().contiguous()
+                if n_out == 1 and getattr(g, "_cdna_absmax", None) is not None:
+                    v1._cdna_absmax = g._cdna_absmax  # max |g| from the grad / hess pass (K.grad_hess)
+                trainer.train(1, {"v0": v0, "v1": v1},
                               None if bag is None else bag[None, :].contiguous(), forest, margin=margin)
                 t = len(forest.roots) - 1
                 with _tr.span("xgb.update_margin", round=m):

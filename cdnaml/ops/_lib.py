@@ -208,7 +208,8 @@ _SIGS = {
                           c_void_p, c_void_p], c_int),
     "cdna_hist_assemble": ([c_void_p, c_int, c_double, c_double, c_void_p, c_void_p, c_int, c_int64, c_int,
                             c_void_p, c_void_p], c_int),
-    "cdna_grad_hess": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p], c_int),
+    "cdna_grad_hess": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                        c_void_p], c_int),
     "cdna_logistic_grad": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_double, c_void_p,
                             c_void_p, c_void_p], c_int),
 }

@@ -228,15 +228,19 @@ GRAD_HESS_OBJ = {"reg:squarederror": 0, "reg:linear": 0, "reg:absoluteerror": 1,
 
 def grad_hess(F: torch.Tensor, y: torch.Tensor, w: Optional[torch.Tensor], obj: int):
     """K9: gradient and hessian [n, K] of objective code ``obj`` (GRAD_HESS_OBJ) at margin F [n, K] (GPU).
-    y: float labels (class index for softmax); w: optional float row weights."""
+    y: float labels (class index for softmax); w: optional float row weights.  max |g| is computed in the same
+    pass and attached to g as a pending scalar (``prefetch_max``'s attribute: packed_scale_global reads it)."""
     n, Kc = F.shape
     F = F.float().contiguous()
     y = y.float().contiguous()
     w = None if w is None else w.float().contiguous()
     g = torch.empty_like(F)
     h = torch.empty_like(F)
-    _lib.check(_lib.lib().cdna_grad_hess(_ptr(F), _ptr(y), _ptr(w), n, Kc, int(obj), _ptr(g), _ptr(h),
-                                         _stream(F.device)), "cdna_grad_hess")
+    bits = torch.empty(1, dtype=torch.int32, device=F.device)
+    st = torch.cuda.current_stream(F.device)
+    _lib.check(_lib.lib().cdna_grad_hess(_ptr(F), _ptr(y), _ptr(w), n, Kc, int(obj), _ptr(g), _ptr(h), _ptr(bits),
+                                         st.cuda_stream), "cdna_grad_hess")
+    setattr(g, "_cdna_absmax", _PendingScalar(bits.view(torch.float32), st))
     return g, h
 
 
@@ -854,13 +858,20 @@ PARTITION7_MIN_T = 16
 
 
 
+# boosting partitions (partition5 with margins) gather each row's split byte from a feature-major [d][n] byte copy
+# of the bins (BinnedData.feature_major_bins, built once per fit) instead of the [G][n] 8-feature words
+PART_FEATURE_MAJOR = True
+
+
 def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tensor, tfirst_next: torch.Tensor,
                     split_feat: torch.Tensor, split_bin: torch.Tensor, cat_off: torch.Tensor,
-                    cat_mask: torch.Tensor, child: torch.Tensor, margin: Optional[tuple] = None) -> None:
+                    cat_mask: torch.Tensor, child: torch.Tensor, margin: Optional[tuple] = None,
+                    bins_fm: Optional[torch.Tensor] = None) -> None:
     """In place: every row's code moves to the chosen child's local index (255 = done).
 
     margin (GPU, partition5): ``(F [n] fp32, lv [3A] fp32 from split_decode, eta)`` -- rows that finish at this
-    level add ``eta * leaf value`` to F (boosting margin update without a tree walk)."""
+    level add ``eta * leaf value`` to F (boosting margin update without a tree walk).
+    bins_fm (partition5): the feature-major byte copy [G * 8, n] of ``bins`` the row bytes are gathered from."""
     G, n, _ = bins.shape
     T = codes.shape[0]
     if n == 0 or T == 0:
@@ -888,9 +899,12 @@ def partition_codes(bins: torch.Tensor, codes: torch.Tensor, tfirst: torch.Tenso
         F, lv, eta = margin if margin is not None else (None, None, 0.0)
         if margin is not None:
             assert F.dtype == torch.float32 and F.is_contiguous() and F.numel() == n and lv.numel() == 3 * A
-        _lib.check(_lib.lib().cdna_partition5(_ptr(bins), n, T, A, _ptr(codes), _ptr(args[0]), _ptr(args[1]),
-                                              _ptr(args[2]), _ptr(args[3]), _ptr(args[4]), _ptr(cm),
-                                              _ptr(args[5]), 0, _ptr(lv), float(eta), _ptr(F),
+        fm = bins_fm is not None
+        if fm:
+            assert bins_fm.shape == (G * 8, n) and bins_fm.dtype == torch.uint8 and bins_fm.is_contiguous()
+        _lib.check(_lib.lib().cdna_partition5(_ptr(bins_fm if fm else bins), n, T, A, _ptr(codes), _ptr(args[0]),
+                                              _ptr(args[1]), _ptr(args[2]), _ptr(args[3]), _ptr(args[4]), _ptr(cm),
+                                              _ptr(args[5]), -1 if fm else 0, _ptr(lv), float(eta), _ptr(F),
                                               _stream(bins.device)), "cdna_partition5")
         return
     assert margin is None, "margin updates run in the GPU partition only"

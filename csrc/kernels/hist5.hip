@@ -732,9 +732,13 @@ __global__ __launch_bounds__(256) void partition5_kernel(const uint64_t* __restr
   __syncthreads();
   const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bins);
   // rm_row_bytes > 0: bins is the row-major copy [n][G*8] (a row's bytes share 1-2 cache lines, so the
-  // up-to-255 different split features of a tree's rows do not each pull a line of their own group)
+  // up-to-255 different split features of a tree's rows do not each pull a line of their own group);
+  // rm_row_bytes < 0: bins is the feature-major byte copy [G*8][n] -- a 64-byte sector serves 64 rows of ONE
+  // feature, so a level pulls only the sectors of the features its nodes split on (the [G][n] words pull the
+  // sector of a row's 8-feature group for 8 rows: a deep boosting level, every group in use, read ~half of all)
   auto bidx = [&](int64_t r, int f) -> int64_t {
-    return rm_row_bytes > 0 ? r * rm_row_bytes + f : ((int64_t)(f >> 3) * n + r) * 8 + (f & 7);
+    return rm_row_bytes > 0 ? r * rm_row_bytes + f
+                            : (rm_row_bytes < 0 ? (int64_t)f * n + r : ((int64_t)(f >> 3) * n + r) * 8 + (f & 7));
   };
   uint16_t* rec = codes + (int64_t)t * n;
   const int64_t n4 = n / 4;

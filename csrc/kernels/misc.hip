@@ -146,9 +146,13 @@ __global__ __launch_bounds__(256) void poisson_kernel(uint8_t* __restrict__ out,
 // 1 absolute error, 2 pseudo-Huber, 3 Poisson (hessian * exp(max_delta_step
 // 0.7), XGBoost), 4 binary logistic, 5 softmax over K classes (label = class
 // index).  Same f32 formulas as the torch path in cdnaml/models/xgboost.py.
+// gmax (optional, zeroed by the launcher): max |g| as float bits (atomicMax over non-negative float bit patterns;
+// a NaN beats +inf), the fixed-point scale's input -- no separate abs + max pass over g per boosting round.
 __global__ __launch_bounds__(256) void grad_hess_kernel(const float* __restrict__ F, const float* __restrict__ y,
                                                         const float* __restrict__ w, int64_t n, int K, int obj,
-                                                        float* __restrict__ g, float* __restrict__ h) {
+                                                        float* __restrict__ g, float* __restrict__ h,
+                                                        int* __restrict__ gmax) {
+  int gm = 0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float yy = y[i];
     const float ww = w ? w[i] : 1.0f;
@@ -161,8 +165,10 @@ __global__ __launch_bounds__(256) void grad_hess_kernel(const float* __restrict_
       const int c = (int)yy;
       for (int k = 0; k < K; ++k) {
         const float p = expf(f[k] - m) / z;
-        g[i * K + k] = (p - (k == c ? 1.0f : 0.0f)) * ww;
+        const float gk = (p - (k == c ? 1.0f : 0.0f)) * ww;
+        g[i * K + k] = gk;
         h[i * K + k] = fmaxf(2.0f * p * (1.0f - p), 1e-16f) * ww;
+        gm = max(gm, __float_as_int(gk) & 0x7FFFFFFF);
       }
       continue;
     }
@@ -189,9 +195,15 @@ __global__ __launch_bounds__(256) void grad_hess_kernel(const float* __restrict_
       gg = p - yy;
       hh = fmaxf(p * (1.0f - p), 1e-16f);
     }
-    g[i] = gg * ww;
+    const float gw = gg * ww;
+    g[i] = gw;
     h[i] = hh * ww;
+    gm = max(gm, __float_as_int(gw) & 0x7FFFFFFF);
   }
+  if (!gmax) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) gm = max(gm, __shfl_xor(gm, o));
+  if ((threadIdx.x & 63) == 0 && gm > 0) atomicMax(gmax, gm);
 }
 
 // ------------------------------------------------------- K13 reg metrics
@@ -616,9 +628,14 @@ CDNA_API int cdna_logistic_grad(const float* X, int64_t n, int d, int64_t ldx, c
 }
 
 CDNA_API int cdna_grad_hess(const float* F, const float* y, const float* w, int64_t n, int K, int obj, float* g,
-                            float* h, hipStream_t st) {
+                            float* h, int* gmax, hipStream_t st) {
+  if (gmax) {
+    const hipError_t e = hipMemsetAsync(gmax, 0, sizeof(int), st);
+    if (e != hipSuccess) return (int)e;
+  }
   if (n <= 0) return 0;
   if (obj < 0 || obj > 5 || K < 1 || (obj != 5 && K != 1)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(grad_hess_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, F, y, w, n, K, obj, g, h);
+  hipLaunchKernelGGL(grad_hess_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, F, y, w, n, K, obj, g, h,
+                     gmax);
   return (int)hipGetLastError();
 }

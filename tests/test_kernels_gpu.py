@@ -829,7 +829,8 @@ def test_split_scan_wave_bit_identical(dev, A, d, B, kind, missing, masked, monk
 
 
 def test_split_scan_wave_same_boosted_forest(dev, monkeypatch):
-    """The boosting rounds take the wave-parallel K6 (exact packed histograms): the forest is the serial kernel's."""
+    """The boosting rounds take the wave-parallel K6 (exact packed histograms) and partition from the feature-major
+    byte copy: the forest (and the margins the partitions update) are the serial kernel's / the [G][n] words'."""
     import cdnaml
     from cdnaml.ml.xgboost import XgboostRegressor
     from cdnaml.utils.synthetic import forest_digest
@@ -838,12 +839,15 @@ def test_split_scan_wave_same_boosted_forest(dev, monkeypatch):
     X = torch.randn((200000, 40), generator=g, device=dev)
     y = (X[:, 0] * 2 + torch.sin(X[:, 1] * 3) + (X[:, 2] > 0.5).float()).double()
     df = spark.createDataFrameFromLocalTensors({"features": X, "label": y})
-    digests = []
-    for wave in (False, True):
+    digests, preds = [], []
+    for wave, fm in ((False, False), (True, False), (True, True)):
         monkeypatch.setattr(K, "SPLIT_WAVE", wave)
+        monkeypatch.setattr(K, "PART_FEATURE_MAJOR", fm)  # partition5 from the feature-major byte copy
         m = XgboostRegressor(n_estimators=4, max_depth=8, max_bin=256, learning_rate=0.3).fit(df)
         digests.append(forest_digest(m._forest))
-    assert digests[0] == digests[1]
+        preds.append(m.transform(df).select("prediction").toPandas().prediction.values)
+    assert digests[0] == digests[1] == digests[2]
+    assert np.array_equal(preds[0], preds[1]) and np.array_equal(preds[0], preds[2])
 
 
 @pytest.mark.parametrize("n,p", [(1000003, 0.3), (4097, 0.0), (50000, 1.0)])
