@@ -99,7 +99,8 @@ def _tree_df(spark, n=4000, d=12, seed=3, uneven=None):
     rng = np.random.default_rng(seed)
     X = rng.normal(size=(n, d))
     y = X[:, 0] * 2.0 - X[:, 1] + np.sin(2 * X[:, 2]) + 0.1 * rng.normal(size=n)
-    pdf = pd.DataFrame({"idx": np.arange(n), "label": y, "cls": (y > 0).astype(float)})
+    pdf = pd.DataFrame({"idx": np.arange(n), "label": y, "cls": (y > 0).astype(float),
+                        "cls3": (y > -0.5).astype(float) + (y > 0.8).astype(float)})
     from cdnaml.ml.feature import VectorAssembler
     for i in range(d):
         pdf[f"x{i}"] = X[:, i]
@@ -124,6 +125,8 @@ def _tree_digests(df):
         "xgb_reg": XgboostRegressor(n_estimators=5, max_depth=4, learning_rate=0.3, random_state=42, missing=0.0),
         "xgb_cls": XgboostClassifier(n_estimators=4, max_depth=3, random_state=7, labelCol="cls"),
         "rf_cls": RandomForestClassifier(numTrees=5, maxDepth=4, seed=11, labelCol="cls"),
+        # three classes on the packed record path (sums W1 + 2^32 W2 all-reduced as int64)
+        "rf_cls3": RandomForestClassifier(numTrees=4, maxDepth=4, seed=13, labelCol="cls3"),
     }
     for k, est in fits.items():
         m = est.fit(df)
