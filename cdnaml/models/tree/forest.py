@@ -176,6 +176,17 @@ class Forest:
         st["_pending"] = []
         return st
 
+    def __setstate__(self, st):
+        # forests pickled before the node fields were NodeFields hold plain lists: convert them
+        K_ = int(st.get("K", 1))
+        for n_, f_ in _fields(K_).items():
+            v = st.get("_" + n_)
+            if v is not None and not isinstance(v, NodeField):
+                f_.extend(np.asarray(v, dtype=f_._a.dtype).reshape((-1,) + f_._a.shape[1:]) if len(v) else [])
+                st["_" + n_] = f_
+        st.pop("_np", None)
+        self.__dict__.update(st)
+
     def lists(self) -> dict:
         """The node-list fields (settled) as a dict name -> list, for loops that touch many nodes (one settle check
         instead of one property call per access)."""

@@ -69,3 +69,20 @@ def test_forest_fields_round_trip_and_cut_freeze():
     fo.thr = [t + 0.0 for t in fo.thr]  # reassigning a field still works (a fresh, unfrozen field)
     fo.thr[0] = 2.0
     assert fo.thr[0] == 2.0
+
+
+def test_forest_pickled_with_list_fields_still_loads():
+    """A forest pickled when the node fields were plain lists (before NodeField) unpickles into NodeFields."""
+    fo = Forest(1)
+    fo.add_many(np.array([[0.5], [1.5]]), np.array([2.0, 1.0]), 0, np.zeros(2))
+    fo.roots = [0]
+    st = fo.__getstate__()
+    old = dict(st)
+    for n in ("feat", "thr", "bin", "left", "right", "is_cat", "weight", "gain", "impurity", "depth"):
+        old["_" + n] = list(st["_" + n])
+    old["_value"] = [np.array([0.5]), np.array([1.5])]
+    old["_catmask"] = [np.zeros(8, np.uint32)] * 2
+    f2 = Forest.__new__(Forest)
+    f2.__setstate__(old)
+    assert isinstance(f2.value, NodeField) and f2.value[1].tolist() == [1.5] and f2.feat == [-1, -1]
+    assert f2.catmask.array().shape == (2, 8)
