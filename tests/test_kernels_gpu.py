@@ -793,11 +793,11 @@ def test_native_split_scan_matches_torch(dev, monkeypatch):
 
 
 @pytest.mark.parametrize("A,d,B,kind,missing,masked", [(7, 100, 256, 1, False, False), (33, 37, 256, 1, True, False),
-                                                       (5, 100, 40, 0, False, True), (12, 300, 100, 0, False, False),
-                                                       (3, 64, 64, 1, True, True), (9, 13, 17, 0, False, False)])
+                                                       (5, 100, 200, 0, False, True), (12, 300, 100, 0, False, False),
+                                                       (3, 64, 65, 1, True, True), (9, 13, 129, 0, False, False)])
 def test_split_scan_wave_bit_identical(dev, A, d, B, kind, missing, masked, monkeypatch):
-    """K6 over exact histograms: the wave-parallel kernel (a wave per feature, split_scan_wave_kernel) returns the
-    serial kernel's bits -- gains, winners (incl. the serial walk's tie order: empty bins make runs of equal gains,
+    """K6 over exact histograms (B > 64): the wave-parallel kernel (a wave per feature, split_scan_wave_kernel)
+    returns the serial kernel's bits -- gains, winners (incl. the serial walk's tie order: empty bins make runs of equal gains,
     and with no missing rows every missing-right candidate ties its left twin), left / right sums, node totals."""
     g = torch.Generator().manual_seed(A * d + B)
     cnt = torch.randint(0, 50, (A, d, B), generator=g).double()
