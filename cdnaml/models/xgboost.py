@@ -357,6 +357,10 @@ class _XgbModelBase(Model):
         bins = K.binize(Xf, thr, nthr, missing=float(self.getMissing()))  # missing -> bin 0 inside the kernel
         eta = self.getLearning_rate()
         F = torch.full((n, self._n_out), self._base, dtype=torch.float32, device=dev)
+        if dev.type == "cpu":
+            K.predict_binned_forest_host(bins, [self._forest.binned_arrays(dev, t)
+                                                for t in range(len(self._forest.roots))], eta, F)
+            return F
         for t in range(len(self._forest.roots)):
             nodes, vals, masks = self._forest.binned_arrays(dev, t)
             k = t % self._n_out

@@ -1161,6 +1161,57 @@ def predict_binned_add(bins: torch.Tensor, nodes: torch.Tensor, root: int, value
     out += scale * values.float()[nd[cur][:, 1]]
 
 
+def predict_binned_forest_host(bins: torch.Tensor, trees, scale: float, F: torch.Tensor) -> None:
+    """Host twin of ``predict_binned_add`` over a WHOLE forest: every tree walks at once (one [T*n] cursor),
+    so a 100-tree margin costs ~depth vector steps instead of 100 x depth.  ``trees[t] = (nodes, values,
+    masks)`` as ``Forest.binned_arrays``; tree t adds to column ``t % F.shape[1]``, summed tree by tree in
+    float32 like the per-tree path (identical results)."""
+    G, n, _ = bins.shape
+    T = len(trees)
+    if n == 0 or T == 0:
+        return
+    bm = bins_to_matrix(bins, G * 8)
+    nodes, vals, masks, roots = [], [], [], []
+    no = vo = mo = 0
+    for nd_t, v_t, m_t in trees:
+        nd_t = nd_t.long().clone()
+        leaf = nd_t[:, 0] == -1
+        cat = nd_t[:, 0] <= -2
+        nd_t[~leaf, 2:] += no
+        nd_t[leaf, 1] += vo
+        nd_t[cat, 1] += mo
+        roots.append(no)
+        nodes.append(nd_t)
+        vals.append(v_t.float().reshape(-1))
+        m_t = m_t.long().reshape(-1) & 0xFFFFFFFF
+        masks.append(m_t)
+        no += nd_t.shape[0]
+        vo += vals[-1].numel()
+        mo += m_t.numel() // 8
+    nd = torch.cat(nodes)
+    mk = torch.cat(masks)
+    vv = torch.cat(vals)
+    rows = torch.arange(n).repeat(T)
+    cur = torch.tensor(roots, dtype=torch.long).repeat_interleave(n)
+    for _ in range(64):
+        nv = nd[cur]
+        internal = nv[:, 0] != -1
+        if not internal.any():
+            break
+        f = nv[:, 0]
+        cont = f >= 0
+        fi = torch.where(cont, f, -f - 2).clamp(min=0)
+        b = bm[rows, fi]
+        moff = torch.where(f <= -2, nv[:, 1], torch.zeros_like(f)).clamp(min=0)
+        words = mk[(moff * 8 + (b >> 5))]
+        left = torch.where(cont, b <= nv[:, 1], ((words >> (b & 31)) & 1).bool())
+        cur = torch.where(internal, torch.where(left, nv[:, 2], nv[:, 3]), cur)
+    leafv = vv[nd[cur][:, 1]].view(T, n)
+    K = F.shape[1]
+    for t in range(T):
+        F[:, t % K] += scale * leafv[t]
+
+
 # -------------------------------------------------------------------- K13
 def reg_metrics(y: torch.Tensor, p: torch.Tensor, w: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[Σw, Σw e², Σw|e|, Σw y, Σw y², Σw p, Σw p², Σw y p] as float64[8] (local)."""

@@ -404,11 +404,11 @@ class DataFrameReader:
 
 
 def _strip_dbfs(p: str) -> str:
-    if p.startswith("dbfs:"):
-        p = p[5:]
-    if p.startswith("file:"):
-        p = p[5:]
-    return p
+    """Every ``spark.read`` / ``write`` / Delta / stream / catalog path goes through
+    the one DBFS resolver (``utils.dbutils.to_local``), so ``dbfs:/x``, ``/dbfs/x`` and
+    ``file:/dbfs/x`` name the same file as ``dbutils.fs`` and pandas see."""
+    from ..utils.dbutils import to_local
+    return to_local(p)
 
 
 def _table_df(session, tbl: pa.Table, schema: T.StructType, name: str) -> DataFrame:

@@ -171,7 +171,14 @@ class StructField:
         return f"{self.name}:{self.dataType.simpleString()}"
 
     def __eq__(self, other):
-        return (isinstance(other, StructField) and self.name == other.name and self.dataType == other.dataType)
+        """Spark's field equality: name, type, nullability and metadata all count (so
+        ``set(a.schema.fields) ^ set(b.schema.fields)`` of Labs/ML 05L:257 finds schema drift)."""
+        return (isinstance(other, StructField) and self.name == other.name and self.dataType == other.dataType
+                and bool(self.nullable) == bool(other.nullable) and self.metadata == other.metadata)
+
+    def __hash__(self):
+        return hash((self.name, self.dataType, bool(self.nullable),
+                     json.dumps(self.metadata, sort_keys=True, default=str)))
 
     def __repr__(self):
         return f"StructField('{self.name}', {self.dataType!r}, {self.nullable})"

@@ -37,8 +37,5 @@ def resolve(uri: str) -> str:
                 raise TrackingException(f"No versions of model {name} in stage {ver}")
             mv = cands[-1]
         return resolve(mv.source)
-    if uri.startswith("file://"):
-        return uri[len("file://"):]
-    if uri.startswith("dbfs:"):
-        return uri[len("dbfs:"):]
-    return uri
+    from ..utils.dbutils import to_local
+    return to_local(uri)

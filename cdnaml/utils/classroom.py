@@ -29,7 +29,8 @@ class Classroom:
         from ..session import SparkSession
         self.spark = spark or SparkSession.builder.getOrCreate()
         self.username = get_username(self.spark)
-        self.cleaned_username = re.sub(r"[^a-zA-Z0-9]", "_", self.username).lower()
+        # Classroom-Setup.py:13 -- the local part of the e-mail, lower-cased, non-alphanumerics -> "_"
+        self.cleaned_username = re.sub(r"[^a-zA-Z0-9]", "_", self.username.lower().split("@")[0])
         self.userhome = f"dbfs:/user/{self.username}/dbacademy"
         self.course_dir = f"{self.userhome}/{course}"
         self.datasets_dir = f"{self.course_dir}/datasets"
@@ -174,9 +175,14 @@ def to_hash(spark, value) -> int:
     return int(df.select(F.abs(F.hash(F.col("value"))).cast("int").alias("h")).first().h)
 
 
+def database_name(username: str, course: str) -> str:
+    """Per-user database name (UTIL:134-142)."""
+    return re.sub(r"[^a-zA-Z0-9]", "_", f"{username}_{course[:12]}").lower()
+
+
 def create_user_database(spark, username: str, course: str, lesson: str) -> str:
     """Per-user database (UTIL:134-150)."""
-    name = re.sub(r"[^a-zA-Z0-9]", "_", f"{username}_{course[:12]}").lower()
+    name = database_name(username, course)
     spark.sql(f"CREATE DATABASE IF NOT EXISTS {name}")
     spark.sql(f"USE {name}")
     return name

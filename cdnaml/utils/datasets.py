@@ -14,7 +14,7 @@ IoT table of ML 13:35-42 exactly as specified).
     airbnb/sf-listings/sf-listings-2019-03-06-clean.parquet/      4 partitions
     airbnb/sf-listings/sf-listings-2019-03-06-clean.delta/        same, versioned
     airbnb/sf-listings/sf-listings-2019-03-06-clean-100p.parquet/ 100 part files
-    airbnb/sf-listings/airbnb-cleaned-mlflow.csv                  all-numeric (ML 12:131)
+    airbnb/sf-listings/airbnb-cleaned-mlflow.csv                  all-numeric + zipcode (ML 12:34,131)
     airbnb/sf-listings/models/sf-listings-2019-03-06/pipeline_model
     dataframes/people-with-dups.txt                               ':'-separated
     movielens/ratings.parquet/, movielens/movies.parquet/
@@ -129,6 +129,9 @@ def airbnb_mlflow_csv(clean: Optional[pd.DataFrame] = None) -> pd.DataFrame:
     out = clean[cols].copy()
     for c in ("neighbourhood_cleansed", "property_type", "room_type", "bed_type"):
         out[c] = pd.Categorical(out[c]).codes.astype(np.int64)
+    # SF zip codes (941xx) keyed by neighbourhood; ML 12:34 / Labs/ML 08L:34 drop it, ML 05:69 and
+    # Labs/ML 12L:35 keep it as a feature (SURVEY §2.8 "zipcode dropped for some uses")
+    out.insert(4, "zipcode", (94102.0 + (out["neighbourhood_cleansed"] * 7) % 32).astype(float))
     return out
 
 
@@ -139,7 +142,7 @@ def people_with_dups(n_unique: int = 100000, n_dups: int = 3000, seed: int = 0) 
                       "William", "Elizabeth", "David", "Jennifer", "Richard", "Maria", "Joseph", "Susan", "Thomas"])
     last = np.array(["Smith", "Johnson", "Williams", "Brown", "Jones", "Garcia", "Miller", "Davis", "Rodriguez",
                      "Martinez", "Hernandez", "Lopez", "Gonzalez", "Wilson", "Anderson", "Thomas", "Taylor"])
-    ssn_num = rng.choice(np.arange(100000000, 999999999), n_unique, replace=False)
+    ssn_num = 100000000 + rng.choice(899999999, n_unique, replace=False)  # Floyd sampling, no 7 GB arange
     ssn = [f"{s // 1000000:03d}-{(s // 10000) % 100:02d}-{s % 10000:04d}" for s in ssn_num]
     gender = rng.choice(["F", "M"], n_unique)
     birth = [(datetime.date(1950, 1, 1) + datetime.timedelta(days=int(d))).isoformat() + "T05:00:00.000+0000"

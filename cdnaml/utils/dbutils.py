@@ -16,15 +16,41 @@ def dbfs_root() -> str:
     return os.path.abspath(os.environ.get("CDNAML_DBFS_ROOT", "dbfs"))
 
 
-def to_local(path: str) -> str:
-    """``dbfs:/x`` and ``/dbfs/x`` -> ``<dbfs_root>/x``; ``file:/x`` -> ``/x``."""
-    if path.startswith("dbfs:/"):
-        return os.path.join(dbfs_root(), path[len("dbfs:/"):].lstrip("/"))
-    if path.startswith("/dbfs/"):
-        return os.path.join(dbfs_root(), path[len("/dbfs/"):])
+def to_local(path) -> str:
+    """The ONE DBFS resolver used by every reader, writer, Delta table, stream,
+    catalog location, model path and ``dbutils.fs`` call.
+
+    ``dbfs:/x``, ``dbfs:x``, ``/dbfs/x``, ``file:/dbfs/x`` and ``file:///dbfs/x``
+    all resolve to ``<dbfs_root>/x`` (the FUSE mount of ``Includes/Reset.py:11`` and
+    the ``.replace("dbfs:/", "/dbfs/")`` idiom of ``ML 05:69`` / ``ML 12:34``);
+    ``file:/x`` / ``file:///x`` -> ``/x``; anything else is a host path.  A ``dbfs:``
+    URI never resolves outside the DBFS root: ``..`` components are rejected."""
+    if not isinstance(path, str):
+        path = os.fspath(path)
     if path.startswith("file:"):
-        return path[len("file:"):]
+        rest = path[len("file:"):]
+        local = "/" + rest.lstrip("/") if rest.startswith("/") else rest
+        if local == "/dbfs" or local.startswith("/dbfs/"):
+            return _under_root(local[len("/dbfs"):])
+        return local
+    if path.startswith("dbfs:"):
+        return _under_root(path[len("dbfs:"):])
+    if path == "/dbfs" or path.startswith("/dbfs/"):
+        return _under_root(path[len("/dbfs"):])
     return path
+
+
+def _under_root(rel: str) -> str:
+    root = dbfs_root()
+    rel = rel.lstrip("/")
+    if not rel:
+        return root
+    full = os.path.normpath(os.path.join(root, rel))
+    if full != root and not full.startswith(root + os.sep):
+        raise ValueError(f"DBFS path escapes the DBFS root: {rel!r}")
+    if rel.endswith("/"):
+        full += "/"
+    return full
 
 
 class FileInfo:

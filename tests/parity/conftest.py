@@ -15,7 +15,10 @@ def nb(request, tmp_path_factory):
     host (CPU suite) and on the GPU (the cuda variant is marked gpu)."""
     import cdnaml
     import cdnaml.compat as compat
+    from cdnaml.utils import Classroom
     from cdnaml.utils import datasets as D
+    from cdnaml.utils.dbutils import to_local
+    from cdnaml.utils.notebook import mount_dbfs_fuse, unmount_dbfs_fuse
 
     with session_device(request.param):
         root = tmp_path_factory.mktemp(f"parity_{request.param}")
@@ -24,10 +27,15 @@ def nb(request, tmp_path_factory):
         spark = cdnaml.SparkSession.builder.config("cdnaml.warehouse.dir", str(root / "warehouse")).getOrCreate()
         assert spark.device.type == request.param
         installed = compat.install()
-        ds = D.install_datasets(str(root / "datasets"), spark, scale=0.03)
+        # the notebooks' own path convention: f"{datasets_dir}/..." dbfs:/ URIs (Classroom-Setup.py:17-18) and
+        # .replace("dbfs:/", "/dbfs/") for pandas (ML 05:69) -- every read and write goes through the resolver
+        cr = Classroom(spark, lesson=f"parity {request.param}", install=False)
+        D.install_datasets(to_local(cr.datasets_dir), spark, scale=0.03)
+        mount_dbfs_fuse()
         try:
-            yield spark, ds, str(root / "work")
+            yield spark, cr.datasets_dir, cr.working_dir
         finally:
+            unmount_dbfs_fuse()
             compat.uninstall()
             spark.stop()
             del installed

@@ -4,6 +4,8 @@ import os
 
 import pytest
 
+from cdnaml.utils.dbutils import dbutils
+
 
 def _sf(ds, name):
     return os.path.join(ds, "airbnb", "sf-listings", name)
@@ -42,7 +44,8 @@ def test_ml00c_delta_review(nb):
        .partitionBy("neighbourhood_cleansed").save(path))
     df.filter(df.price > 100).write.format("delta").mode("overwrite").save(path)
     log = os.path.join(path, "_delta_log")
-    assert sorted(f for f in os.listdir(log) if f.endswith(".json"))[0] == "00000000000000000000.json"
+    assert path.startswith("dbfs:/")
+    assert sorted(f.name for f in dbutils.fs.ls(log) if f.name.endswith(".json"))[0] == "00000000000000000000.json"
     assert spark.read.json(os.path.join(log, "00000000000000000000.json")).count() >= 1
     dt = DeltaTable.forPath(spark, path)
     hist = dt.history()
@@ -94,9 +97,9 @@ def test_l00_dedup_lab(nb):
     from cdnaml.utils import datasets as D
 
     # full-size people file (the installed datasets are scaled down): 100,000 people + 3,000 re-cased duplicates
-    src = os.path.join(work, "people-with-dups.txt")
-    os.makedirs(work, exist_ok=True)
-    D.people_with_dups(n_unique=100000, n_dups=3000).to_csv(src, sep=":", index=False)
+    src = f"{work}/people-with-dups.txt"
+    dbutils.fs.mkdirs(work)
+    D.people_with_dups(n_unique=100000, n_dups=3000).to_csv(src.replace("dbfs:/", "/dbfs/"), sep=":", index=False)
     spark.conf.set("spark.sql.shuffle.partitions", 8)
     df = spark.read.csv(src, header=True, sep=":", inferSchema=True)
     assert df.count() == 103000
@@ -108,7 +111,7 @@ def test_l00_dedup_lab(nb):
              .drop("lcFirstName", "lcMiddleName", "lcLastName", "ssnNums"))
     dest = os.path.join(work, "people.parquet")
     dedup.write.mode("overwrite").parquet(dest)
-    parts = len([f for f in os.listdir(dest) if f.endswith(".parquet")])
+    parts = len([f for f in dbutils.fs.ls(dest) if f.name.endswith(".parquet")])  # L00:139
     final = spark.read.parquet(dest).count()
     cr = Classroom(spark, lesson="ML 00L", install=False)
     assert cr.validateYourAnswer("01 Parquet File Exists", 1276280174, parts)

@@ -71,7 +71,7 @@ def test_ml05_model_registry(nb):
     from mlflow.tracking import MlflowClient
     from sklearn.linear_model import LinearRegression as SkLR, Ridge
 
-    pdf = pd.read_csv(_sf(ds, "airbnb-cleaned-mlflow.csv"))
+    pdf = pd.read_csv(_sf(ds, "airbnb-cleaned-mlflow.csv").replace("dbfs:/", "/dbfs/"))  # ML 05:69
     X, y = pdf.drop(["price"], axis=1), pdf["price"]
     name = "parity_ml05"
     with mlflow.start_run(run_name="LR Model") as run:

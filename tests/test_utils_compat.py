@@ -66,7 +66,10 @@ def test_generators_have_course_schemas():
     assert clean.neighbourhood_cleansed.nunique() > 32  # forces maxBins=40 (ML 06:110)
     assert clean.price.max() <= 10000 and (clean.price > 0).all()
     m = D.airbnb_mlflow_csv(clean)
-    assert str(m.neighbourhood_cleansed.dtype) == "int64" and "zipcode" not in m.columns
+    assert str(m.neighbourhood_cleansed.dtype) == "int64" and "zipcode" in m.columns
+    # ML 12:131 is the schema after .drop(["zipcode"])
+    assert list(m.drop(["zipcode"], axis=1).columns[:4]) == ["host_total_listings_count", "neighbourhood_cleansed",
+                                                          "latitude", "longitude"]
     p = D.people_with_dups(n_unique=1000, n_dups=30)
     assert len(p) == 1030
     key = p.firstName.str.lower() + p.middleName.str.lower() + p.lastName.str.lower() + \
@@ -152,3 +155,84 @@ def test_validate_schema_and_all_done(spark, tmp_path, monkeypatch):
                        cr.database: ("d", cr.database, "your database")})
     assert "validateYourAnswer" in html and "username" in html and cr.database in html
     assert "hidden_fn" not in html and html.endswith("All done!")
+
+
+def test_one_dbfs_namespace(tmp_path, monkeypatch):
+    """dbfs:/x, /dbfs/x, file:/dbfs/x and file:///dbfs/x are one file for spark.read/write, Delta, dbutils and
+    pandas (Includes/Reset.py:11; ML 05:69); a dbfs: URI never lands on the host root."""
+    import pandas as pd
+
+    import cdnaml
+    from cdnaml.sql.readwriter import _strip_dbfs
+    from cdnaml.utils.dbutils import dbutils, to_local
+    from cdnaml.utils.notebook import mount_dbfs_fuse, unmount_dbfs_fuse
+
+    root = str(tmp_path / "dbfs")
+    monkeypatch.setenv("CDNAML_DBFS_ROOT", root)
+    for p in ("dbfs:/user/a/x.csv", "dbfs:user/a/x.csv", "/dbfs/user/a/x.csv", "file:/dbfs/user/a/x.csv",
+              "file:///dbfs/user/a/x.csv"):
+        assert to_local(p) == os.path.join(root, "user/a/x.csv"), p
+        assert _strip_dbfs(p) == to_local(p)
+    assert to_local("file:///tmp/q") == "/tmp/q" and to_local("/tmp/q") == "/tmp/q"
+    with pytest.raises(ValueError):
+        to_local("dbfs:/../../etc/passwd")
+    spark = cdnaml.SparkSession.builder.config("cdnaml.warehouse.dir", str(tmp_path / "wh")).getOrCreate()
+    df = spark.createDataFrame(pd.DataFrame({"a": [1.0, 2.0, 3.0]}))
+    df.write.mode("overwrite").parquet("dbfs:/user/a/t.parquet")
+    assert os.path.isdir(os.path.join(root, "user/a/t.parquet"))
+    assert spark.read.parquet("/dbfs/user/a/t.parquet").count() == 3
+    assert any(f.name.endswith(".parquet") for f in dbutils.fs.ls("dbfs:/user/a/t.parquet"))
+    df.write.format("delta").mode("overwrite").save("dbfs:/user/a/d")
+    assert spark.read.format("delta").load("file:/dbfs/user/a/d").count() == 3
+    assert mount_dbfs_fuse()
+    try:
+        pd.DataFrame({"b": [1, 2]}).to_csv("/dbfs/user/a/p.csv", index=False)
+        assert pd.read_csv("dbfs:/user/a/p.csv".replace("dbfs:/", "/dbfs/")).b.sum() == 3
+        assert spark.read.csv("dbfs:/user/a/p.csv", header=True).count() == 2
+    finally:
+        unmount_dbfs_fuse()
+    assert not hasattr(pd.read_csv, "__wrapped__")
+    spark.stop()
+
+
+def test_structfield_spark_equality_and_hash():
+    """Labs/ML 05L:257 takes set(a.schema.fields) ^ set(b.schema.fields); Spark compares nullable/metadata."""
+    from cdnaml.sql import types as T
+
+    a = T.StructType([T.StructField("x", T.DoubleType()), T.StructField("y", T.StringType())])
+    b = T.StructType([T.StructField("x", T.DoubleType()), T.StructField("z", T.LongType())])
+    assert {f.name for f in set(a.fields) ^ set(b.fields)} == {"y", "z"}
+    assert T.StructField("x", T.DoubleType(), True) != T.StructField("x", T.DoubleType(), False)
+    assert T.StructField("x", T.DoubleType(), metadata={"k": 1}) != T.StructField("x", T.DoubleType())
+    assert hash(T.StructField("x", T.DoubleType())) == hash(T.StructField("x", T.DoubleType()))
+
+
+def test_notebook_namespace_and_cells(tmp_path, monkeypatch):
+    """The Databricks globals + Classroom-Setup names (H1/H12) and the cell splitter/runner."""
+    import cdnaml
+    from cdnaml.utils import notebook as N
+
+    monkeypatch.setenv("CDNAML_DBFS_ROOT", str(tmp_path / "dbfs"))
+    spark = cdnaml.SparkSession.builder.config("cdnaml.warehouse.dir", str(tmp_path / "wh")).getOrCreate()
+    ns = N.notebook_namespace(spark, lesson="unit", install=False, quiet_display=True)
+    try:
+        for k in ("spark", "sc", "sql", "table", "display", "displayHTML", "dbutils", "username", "userhome",
+                  "datasets_dir", "working_dir", "validateYourAnswer", "toHash", "untilStreamIsReady", "FILL_IN"):
+            assert k in ns, k
+        assert ns["datasets_dir"].startswith("dbfs:/user/") and "@" not in ns["cleaned_username"]
+        src = ("# Databricks notebook source\n# MAGIC %md # title\n\n# COMMAND ----------\n\n"
+               "# MAGIC %run ./Includes/Classroom-Setup\n\n# COMMAND ----------\n\n"
+               "df = spark.range(5)\ndf.createOrReplaceTempView('v')\n\n# COMMAND ----------\n\n"
+               "# MAGIC %sql\n# MAGIC SELECT COUNT(*) AS c FROM v\n\n# COMMAND ----------\n\n"
+               "# just a comment\n\n# COMMAND ----------\n\nassert sql('SELECT * FROM v').count() == 5\n"
+               "x = 1 / 0\n")
+        cells = N.split_cells(src)
+        assert [c.kind for c in cells] == ["md", "run", "python", "sql", "python"]
+        p = tmp_path / "nb.py"
+        p.write_text(src)
+        r = N.run_notebook(str(p), ns)
+        assert [c.ok for c in r.cells] == [True, True, False]
+        assert r.cells[-1].error.startswith("ZeroDivisionError") and r.cells[-1].line > 1
+    finally:
+        N.unmount_dbfs_fuse()
+        spark.stop()
