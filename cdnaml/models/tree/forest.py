@@ -4,6 +4,7 @@ while the GPU predicts (``Forest.settle``) and the frozen node lists of a tuner-
 from __future__ import annotations
 
 import operator
+import threading
 from typing import List, Optional
 
 import numpy as np
@@ -150,7 +151,8 @@ class Forest:
         # GPU predicts instead of between the last split and the predict launch (the node-list fields below are
         # properties that settle first, so every reader sees the complete forest)
         self._pending: list = []
-        self._settling = False
+        self._settling = None            # ident of the thread running settle(), or None
+        self._settle_lock = threading.RLock()
         self.K = K_
         for n_, f_ in _fields(K_).items():
             self.__dict__["_" + n_] = f_
@@ -160,20 +162,27 @@ class Forest:
         # ForestTrainer.train (Forest.heap_struct's arrays), or None
 
     def settle(self) -> None:
-        """Run the deferred bookkeeping (idempotent; a no-op when nothing is pending)."""
-        if self._settling:
+        """Run the deferred bookkeeping (idempotent; a no-op when nothing is pending).
+
+        Re-entrant for the settling thread (the pending closures read node fields, which call back here);
+        any OTHER thread blocks on the lock until the forest is complete (ForestPredictor serves worker threads)."""
+        if not self._pending or self._settling == threading.get_ident():
             return
-        self._settling = True
-        try:
-            while self._pending:
-                self._pending.pop(0)()
-        finally:
-            self._settling = False
+        with self._settle_lock:
+            self._settling = threading.get_ident()
+            try:
+                while self._pending:
+                    self._pending[0]()      # dequeued only once done: other threads see work pending and wait
+                    self._pending.pop(0)
+            finally:
+                self._settling = None
 
     def __getstate__(self):
         self.settle()
         st = dict(self.__dict__)
         st["_pending"] = []
+        st["_settling"] = None
+        st.pop("_settle_lock", None)
         return st
 
     def __setstate__(self, st):
@@ -185,18 +194,24 @@ class Forest:
                 f_.extend(np.asarray(v, dtype=f_._a.dtype).reshape((-1,) + f_._a.shape[1:]) if len(v) else [])
                 st["_" + n_] = f_
         st.pop("_np", None)
+        pre = st.get("_heap_np")
+        if pre is not None and len(pre) != 3:
+            st["_heap_np"] = None   # an older (table, D) heap: rebuilt through heap_struct on demand
+        st["_settling"] = None
+        st.setdefault("_pending", [])
         self.__dict__.update(st)
+        self.__dict__["_settle_lock"] = threading.RLock()
 
     def lists(self) -> dict:
         """The node-list fields (settled) as a dict name -> list, for loops that touch many nodes (one settle check
         instead of one property call per access)."""
-        if self._pending and not self._settling:
+        if self._pending:
             self.settle()
         d = self.__dict__
         return {n: d["_" + n] for n in _NODE_FIELDS}
 
     def add(self, value, weight, depth, impurity=float("nan")) -> int:
-        if self._pending and not self._settling:
+        if self._pending:
             self.settle()
         d = self.__dict__
         i = len(d["_feat"])
@@ -531,7 +546,7 @@ def _settled_list(name: str):
     key = "_" + name
 
     def get(self):
-        if self._pending and not self._settling:
+        if self._pending:
             self.settle()
         return self.__dict__[key]
 

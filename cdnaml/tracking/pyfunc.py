@@ -83,26 +83,37 @@ class _NativeUDF:
     UDFs.py:73-143 loads the model once per executor for the same reason)."""
 
     def __init__(self, path, names, rt):
+        import threading
+        import weakref
+
         from ..models.pipeline import PipelineModel
         self.pm = PipelineModel.load(path)
         self.names = names
         self.rt = rt
-        self._cur = None
-        self._plan = None
-        self._plan_key = None
+        # the batch being evaluated is per THREAD: CrossValidator(parallelism=4) threads, threaded streaming sinks
+        # and applyInPandas pools may evaluate the same UDF concurrently through the one cached plan
+        self._tls = threading.local()
+        self._lock = threading.Lock()
+        # plans per session (weak: a new session can reuse a dead one's id()) and input schema
+        self._plans: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
         self.batches = 0
         self.plans_built = 0
+
+    def _current(self):
+        return [self._tls.cur]
 
     def _plan_for(self, sess, part):
         from ..sql.dataframe import DataFrame, SourcePlan
         schema = part.schema()
-        key = (id(sess), tuple((f.name, f.dataType.simpleString()) for f in schema.fields))
-        if key != self._plan_key:
-            src = DataFrame(SourcePlan(sess, "udf-batch", lambda: [self._cur], schema), sess)
-            self._plan = self.pm.transform(src)._plan
-            self._plan_key = key
-            self.plans_built += 1
-        return self._plan
+        key = tuple((f.name, f.dataType.simpleString()) for f in schema.fields)
+        with self._lock:
+            per = self._plans.setdefault(sess, {})
+            plan = per.get(key)
+            if plan is None:
+                src = DataFrame(SourcePlan(sess, "udf-batch", self._current, schema), sess)
+                plan = per[key] = self.pm.transform(src)._plan
+                self.plans_built += 1
+        return plan
 
     def __call__(self, *cols):
         from ..sql.column import Column, Func, _cast
@@ -113,12 +124,15 @@ class _NativeUDF:
 
         def ev(b, ctx, args):
             ns = names if names and len(names) == len(args) else [e.name() for e in exprs]
-            self._cur = Batch({n: a for n, a in zip(ns, args)}, b.n, b.device)
+            cur = Batch({n: a for n, a in zip(ns, args)}, b.n, b.device)
+            prev = getattr(self._tls, "cur", None)
+            self._tls.cur = cur
             try:
-                out = self._plan_for(ctx.session, self._cur).execute()
+                out = self._plan_for(ctx.session, cur).execute()
             finally:
-                self._cur = None
-            self.batches += 1
+                self._tls.cur = prev
+            with self._lock:
+                self.batches += 1
             c = out[0].columns["prediction"] if out else None
             if c is None or len(c) != b.n:
                 raise RuntimeError("model dropped rows inside spark_udf (use handleInvalid='keep')")

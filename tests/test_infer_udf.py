@@ -59,3 +59,44 @@ def test_spark_udf_streamed_forest(tracking, spark, monkeypatch):
     pr = predictor_for(udf.pm.stages[-1], "value", [0.0])
     if spark.device.type == "cuda":
         assert pr.replays > 0  # the staging buffers' predicts are replayed HIP graphs
+
+
+def test_spark_udf_reentrant_threads(tracking, spark):
+    """One ``spark_udf`` evaluated over two different frames from 4 threads at once gives the serial results bit
+    for bit (the current batch is per thread, not instance state: ADVICE r5; ML 12:73-143 under
+    CrossValidator(parallelism=4)-style thread pools)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from cdnaml.ml import Pipeline
+    from cdnaml.ml.regression import RandomForestRegressor
+    rng = np.random.default_rng(5)
+    d = 8
+    Xtr = rng.normal(size=(6000, d)).astype(np.float32)
+    ytr = Xtr[:, 0] * 2 - Xtr[:, 1] + np.sin(Xtr[:, 2])
+    train = spark.createDataFrameFromLocalTensors({"features": torch.from_numpy(Xtr).to(spark.device),
+                                                   "label": torch.from_numpy(ytr).double().to(spark.device)})
+    pm = Pipeline(stages=[RandomForestRegressor(numTrees=6, maxDepth=5, maxBins=32, seed=2)]).fit(train)
+    with mlflow.start_run() as run:
+        mlflow.spark.log_model(pm, "model")
+    udf = mlflow.pyfunc.spark_udf(spark, f"runs:/{run.info.run_id}/model")
+    frames = []
+    for seed, n in ((11, 3000), (12, 1700)):
+        X = np.random.default_rng(seed).normal(size=(n, d)).astype(np.float32)
+        frames.append(spark.createDataFrameFromLocalTensors({"features": torch.from_numpy(X).to(spark.device)}))
+
+    def run_one(i):
+        out = frames[i % 2].withColumn("prediction", udf("features")).select("prediction")._plan.execute()
+        return torch.cat([b.columns["prediction"].values.cpu() for b in out])
+    serial = [run_one(0), run_one(1)]
+    import time
+    orig = udf._plan_for
+
+    def slow_plan_for(sess, part):  # widen the window between "batch set" and "plan executes"
+        time.sleep(0.01)
+        return orig(sess, part)
+    udf._plan_for = slow_plan_for
+    with ThreadPoolExecutor(4) as ex:
+        got = list(ex.map(run_one, range(16)))
+    for i, g in enumerate(got):
+        assert torch.equal(g, serial[i % 2]), i
+    assert udf.plans_built == 1

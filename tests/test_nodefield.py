@@ -82,7 +82,37 @@ def test_forest_pickled_with_list_fields_still_loads():
         old["_" + n] = list(st["_" + n])
     old["_value"] = [np.array([0.5]), np.array([1.5])]
     old["_catmask"] = [np.zeros(8, np.uint32)] * 2
+    old["_heap_np"] = (np.zeros((1, 6), np.int32), 1)        # the pre-r5 (table, D) heap
+    old["_settling"] = False                                  # the pre-r6 bool flag, no lock
     f2 = Forest.__new__(Forest)
     f2.__setstate__(old)
     assert isinstance(f2.value, NodeField) and f2.value[1].tolist() == [1.5] and f2.feat == [-1, -1]
     assert f2.catmask.array().shape == (2, 8)
+    assert f2._heap_np is None and f2._settling is None
+    f2.settle()
+    import copy
+    f3 = copy.deepcopy(f2)
+    assert f3.feat == [-1, -1] and f3._settle_lock is not f2._settle_lock
+
+
+def test_forest_settle_blocks_other_threads():
+    """A reader on another thread waits for the settling thread instead of reading a half-built forest
+    (settle() was guarded by a flag, not a lock)."""
+    import threading
+    import time
+
+    fo = Forest(1)
+    fo.roots = [0]
+    started = threading.Event()
+
+    def slow_level():
+        started.set()
+        time.sleep(0.2)
+        fo.add(np.array([0.5]), 1.0, 0)
+    fo._pending.append(slow_level)
+    t = threading.Thread(target=fo.settle)
+    t.start()
+    started.wait()
+    n = len(fo.lists()["feat"])   # blocks until the settling thread finished
+    t.join()
+    assert n == 1
