@@ -11,7 +11,7 @@ class Correlation:
     @staticmethod
     def corr(dataset, column, method="pearson"):
         from ..models.util import local_xyw
-        X, _, _ = local_xyw(dataset, column)
+        X, _, _ = local_xyw(dataset, column, keep_f64=True)
         if method == "spearman":
             X = torch.argsort(torch.argsort(X, 0), 0).float()
         from ..models.util import centered_gram

@@ -28,7 +28,7 @@ from .regression import (_GBT, _PRED, _RF, _TREE, _TreeModelBase, _bag_weights, 
                          _subforest, resolve_subset, tree_fit_prepare)
 from .tree.engine import ForestTrainer, TreeParams
 from .tree.forest import Forest
-from .util import IllegalArgumentException, centered_gram, local_batch, local_xyw, require_vector
+from .util import VECTOR_F64_MAX, IllegalArgumentException, centered_gram, local_batch, local_xyw, require_vector
 
 # multinomial logistic regression: fp64 logits / gradients up to this many n*d*C multiply-adds per pass (course
 # sizes; Spark's Double), the fp32 device GEMMs above
@@ -45,10 +45,12 @@ _CLS = dict(_PRED, **{
 def _append_cls_outputs(b, raw, prob, pred, names):
     rc, pc, pr = names
     nb = b
+    # Spark's rawPrediction / probability are Double vectors: kept fp64 at course scale (util.VECTOR_F64_MAX)
+    vdt = torch.float64 if raw.numel() <= VECTOR_F64_MAX else torch.float32
     if rc:
-        nb = nb.with_column(rc, ColumnData(raw.float(), T.VectorUDT()))
+        nb = nb.with_column(rc, ColumnData(raw.to(vdt), T.VectorUDT()))
     if pr:
-        nb = nb.with_column(pr, ColumnData(prob.float(), T.VectorUDT()))
+        nb = nb.with_column(pr, ColumnData(prob.to(vdt), T.VectorUDT()))
     return nb.with_column(pc, ColumnData(pred.double(), T.DoubleType()))
 
 
@@ -81,7 +83,7 @@ class LogisticRegression(Estimator):
 
     def _fit(self, dataset):
         fc, lc, wc = self.getFeaturesCol(), self.getLabelCol(), self.getWeightCol()
-        X, y, w = local_xyw(dataset, fc, lc, wc)
+        X, y, w = local_xyw(dataset, fc, lc, wc, keep_f64=True)
         session = dataset._session
         comm = session.comm
         d = X.shape[1]
@@ -144,7 +146,7 @@ class LogisticRegression(Estimator):
             wv = w if w is not None else None
 
             # course-sized problems take fp64 logits and gradients (Spark's Double); large ones the fp32 GEMMs
-            f64 = X.shape[0] * d * C <= MULTINOMIAL_F64_MAX
+            f64 = X.dtype == torch.float64 or X.shape[0] * d * C <= MULTINOMIAL_F64_MAX
             if f64:
                 sd_t = sd_t.double()
 
@@ -248,7 +250,8 @@ class LogisticRegressionModel(Model):
         thresholds = self.getThresholds()
 
         def fn(b, ctx):
-            X = b.columns[fc].values.float()
+            X = b.columns[fc].values
+            X = X if X.dtype == torch.float64 else X.float()
             Wd, bd = W.to(X.device), bvec.to(X.device)
             if X.shape[0] == 0:
                 z = torch.zeros((0, max(self._C, 2)), dtype=torch.float64, device=X.device)

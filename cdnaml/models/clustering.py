@@ -72,7 +72,7 @@ class KMeans(Estimator):
 
     def _fit(self, dataset):
         fc = self.getFeaturesCol()
-        X, _, w = local_xyw(dataset, fc, None, self.getWeightCol())
+        X, _, w = local_xyw(dataset, fc, None, self.getWeightCol(), keep_f64=True)
         session = dataset._session
         comm = session.comm
         seed = self.getSeed() if self.getSeed() is not None else _default_seed(type(self))
@@ -84,7 +84,7 @@ class KMeans(Estimator):
         cost = float("nan")
         it = 0
         for it in range(self.getMaxIter()):
-            Ct = torch.tensor(C, dtype=torch.float32, device=X.device)
+            Ct = torch.tensor(C, dtype=X.dtype, device=X.device)
             _, sums, counts, c = K.kmeans_step(X, Ct)
             acc = torch.cat([sums.reshape(-1), counts, c.reshape(1)])
             comm.all_reduce(acc)
@@ -100,7 +100,7 @@ class KMeans(Estimator):
                 it += 1
                 break
         # final cost / sizes with the final centres
-        Ct = torch.tensor(C, dtype=torch.float32, device=X.device)
+        Ct = torch.tensor(C, dtype=X.dtype, device=X.device)
         assign, _, counts, c = K.kmeans_step(X, Ct)
         acc = torch.cat([counts, c.reshape(1)])
         comm.all_reduce(acc)
@@ -152,8 +152,8 @@ class KMeansModel(Model):
         return int(np.argmin(((self._C - x) ** 2).sum(1)))
 
     def computeCost(self, dataset):
-        X, _, _ = local_xyw(dataset, self.getFeaturesCol())
-        _, _, _, c = K.kmeans_step(X, torch.tensor(self._C, dtype=torch.float32, device=X.device), with_sums=False)
+        X, _, _ = local_xyw(dataset, self.getFeaturesCol(), keep_f64=True)
+        _, _, _, c = K.kmeans_step(X, torch.tensor(self._C, dtype=X.dtype, device=X.device), with_sums=False)
         t = torch.tensor([float(c)], dtype=torch.float64, device=dataset._session.comm.device)
         dataset._session.comm.all_reduce(t)
         return float(t)
@@ -161,17 +161,18 @@ class KMeansModel(Model):
     def _transform(self, dataset):
         fc, pc = self.getFeaturesCol(), self.getPredictionCol()
         require_vector(dataset, fc)
-        Cd = torch.tensor(self._C, dtype=torch.float32)
+        Cd = torch.tensor(self._C, dtype=torch.float64)
         cosine = self.getDistanceMeasure() == "cosine"
 
         def fn(b, ctx):
-            X = b.columns[fc].values.float()
+            X = b.columns[fc].values
+            X = X if X.dtype == torch.float64 else X.float()   # Double vectors: fp64 distances (kernel <double>)
             if cosine:
                 X = X / torch.linalg.vector_norm(X, dim=1, keepdim=True).clamp_min(1e-30)
             if X.shape[0] == 0:
                 a = torch.zeros(0, dtype=torch.int32, device=X.device)
             else:
-                a, _, _, _ = K.kmeans_step(X, Cd.to(X.device), with_sums=False)
+                a, _, _, _ = K.kmeans_step(X, Cd.to(X.device, X.dtype), with_sums=False)
             return b.with_column(pc, ColumnData(a.to(torch.int32), T.IntegerType()))
         return dataset._new(MapPlan(dataset._plan, "KMeansModel", fn))
 
@@ -189,7 +190,7 @@ class BisectingKMeans(KMeans):
 
     def _fit(self, dataset):
         fc = self.getFeaturesCol()
-        X, _, _ = local_xyw(dataset, fc)
+        X, _, _ = local_xyw(dataset, fc, keep_f64=True)
         session = dataset._session
         comm = session.comm
         seed = self.getSeed() if self.getSeed() is not None else _default_seed(type(self))
@@ -201,7 +202,7 @@ class BisectingKMeans(KMeans):
         rng = np.random.default_rng(seed)
         while len(centers) < self.getK():
             C = np.array(centers)
-            assign, _, counts, _ = K.kmeans_step(X, torch.tensor(C, dtype=torch.float32, device=X.device))
+            assign, _, counts, _ = K.kmeans_step(X, torch.tensor(C, dtype=X.dtype, device=X.device))
             comm.all_reduce(counts)
             big = int(torch.argmax(counts))
             sub = X[assign.long() == big]
@@ -209,7 +210,7 @@ class BisectingKMeans(KMeans):
             jitter = rng.normal(scale=1e-3, size=base.shape) * (np.abs(base) + 1)
             pair = np.stack([base + jitter, base - jitter])
             for _ in range(self.getMaxIter()):
-                _, s2, c2, _ = K.kmeans_step(sub, torch.tensor(pair, dtype=torch.float32, device=X.device))
+                _, s2, c2, _ = K.kmeans_step(sub, torch.tensor(pair, dtype=X.dtype, device=X.device))
                 acc = torch.cat([s2.reshape(-1), c2])
                 comm.all_reduce(acc)
                 a = acc.cpu().numpy()

@@ -20,7 +20,7 @@ from ..sql.column import _cast
 from ..sql.dataframe import MapPlan
 from .base import Estimator, Model, Transformer
 from .param import NO_DEFAULT, TypeConverters as TC, keyword_init
-from .util import IllegalArgumentException, local_batch, require_vector, scalar_attr, vector_attrs
+from .util import VECTOR_F64_MAX, IllegalArgumentException, local_batch, require_vector, scalar_attr, vector_attrs
 
 
 class SparkException(RuntimeError):
@@ -63,24 +63,46 @@ class VectorAssembler(Transformer):
                 raise IllegalArgumentException(
                     f"Data type string of column {c} is not supported.")
 
+        prec = str(dataset._session.conf.get("cdnaml.ml.vectorPrecision", "auto")).lower()
+
+        def out_dtype(b: Batch):
+            """Spark's VectorUDT is Double: "auto" assembles fp64 unless an input is an fp32 matrix of real values
+            (the benchmark's fp32 features, an fp32 stage's output: kept fp32, no 2x copy) or the batch exceeds
+            ``util.VECTOR_F64_MAX`` elements (HBM-bound fp32 kernels from there on).  One-hot (binary) fp32 vectors
+            are exact in either width.  conf ``cdnaml.ml.vectorPrecision``: auto | fp64 | fp32."""
+            if prec in ("fp32", "float", "float32"):
+                return torch.float32
+            if prec in ("fp64", "double", "float64"):
+                return torch.float64
+            width = 0
+            for c in ins:
+                v = b.columns[c].values
+                width += v.shape[1] if v.dim() == 2 else 1
+                if v.dim() == 2 and v.dtype != torch.float64:
+                    attrs_ = ((b.columns[c].meta or {}).get("ml_attr") or {}).get("attrs") or []
+                    if not attrs_ or any(a.get("type") != "binary" for a in attrs_):
+                        return torch.float32
+            return torch.float64 if b.n * max(width, 1) <= VECTOR_F64_MAX else torch.float32
+
         def fn(b: Batch, ctx):
             mats, attrs = [], []
             bad = torch.zeros(b.n, dtype=torch.bool, device=b.device)
+            vdt = out_dtype(b)
             for c in ins:
                 col = b.columns[c]
                 if col.values.dim() == 2:
-                    m = col.values.to(torch.float32)
+                    m = col.values.to(vdt)
                     w = m.shape[1]
                     ma = (col.meta or {}).get("ml_attr", {})
                     if w == 0 and ma.get("num_attrs"):
                         w = int(ma["num_attrs"])
-                        m = torch.zeros((b.n, w), dtype=torch.float32, device=b.device)
+                        m = torch.zeros((b.n, w), dtype=vdt, device=b.device)
                     for a in vector_attrs(col.meta, w, c):
                         a = dict(a)
                         a["name"] = f"{c}_{a['name']}" if not str(a.get("name", "")).startswith(c) else a["name"]
                         attrs.append(a)
                 else:
-                    m = col.values.to(torch.float32)[:, None]
+                    m = col.values.to(vdt)[:, None]
                     a = scalar_attr(col.meta, c)
                     a["name"] = c
                     attrs.append(a)
@@ -89,7 +111,7 @@ class VectorAssembler(Transformer):
                 if m.numel():
                     bad |= torch.isnan(m).any(1)
                 mats.append(m)
-            X = torch.cat(mats, 1) if mats else torch.zeros((b.n, 0), device=b.device)
+            X = torch.cat(mats, 1) if mats else torch.zeros((b.n, 0), dtype=vdt, device=b.device)
             for i, a in enumerate(attrs):
                 a["idx"] = i
             meta = {"ml_attr": {"attrs": attrs, "num_attrs": len(attrs)}}
@@ -618,7 +640,7 @@ class StandardScaler(Estimator):
 
     def _fit(self, dataset):
         from .util import centered_gram, local_xyw
-        X, _, _ = local_xyw(dataset, self.getInputCol())
+        X, _, _ = local_xyw(dataset, self.getInputCol(), keep_f64=True)
         n, mean, C = centered_gram(X, dataset._session.comm)
         var = torch.diagonal(C) / max(n - 1, 1)
         return StandardScalerModel(mean=mean.cpu().numpy(), std=torch.sqrt(var.clamp_min(0)).cpu().numpy())
@@ -645,19 +667,20 @@ class StandardScalerModel(Model):
     def _transform(self, dataset):
         ic, oc = self.getInputCol(), self.getOutputCol()
         wm, ws = self.getWithMean(), self.getWithStd()
-        mu = torch.tensor(self._mean, dtype=torch.float32)
-        sd = torch.tensor(np.where(self._std > 0, self._std, 1.0), dtype=torch.float32)
+        mu = torch.tensor(self._mean, dtype=torch.float64)
+        sd = torch.tensor(np.where(self._std > 0, self._std, 1.0), dtype=torch.float64)
         zero = torch.tensor(self._std == 0)
 
         def fn(b, ctx):
-            X = b.columns[ic].values.float()
+            X = b.columns[ic].values
+            X = X if X.dtype == torch.float64 else X.float()   # Double vectors stay Double
             if X.shape[0] == 0:
                 X = X.new_zeros((0, len(mu)))
             Y = X
             if wm:
-                Y = Y - mu.to(b.device)
+                Y = Y - mu.to(b.device, X.dtype)
             if ws:
-                Y = Y / sd.to(b.device)
+                Y = Y / sd.to(b.device, X.dtype)
                 Y = torch.where(zero.to(b.device)[None, :], torch.zeros_like(Y), Y)
             return b.with_column(oc, ColumnData(Y, T.VectorUDT(), b.columns[ic].valid, meta=b.columns[ic].meta))
         return dataset._new(MapPlan(dataset._plan, "StandardScalerModel", fn))
@@ -684,7 +707,7 @@ class MinMaxScaler(Estimator):
 
     def _fit(self, dataset):
         from .util import local_xyw
-        X, _, _ = local_xyw(dataset, self.getInputCol())
+        X, _, _ = local_xyw(dataset, self.getInputCol(), keep_f64=True)
         comm = dataset._session.comm
         lo = X.min(0).values.double() if X.shape[0] else torch.full((X.shape[1],), float("inf"), device=X.device,
                                                                     dtype=torch.float64)
@@ -716,13 +739,14 @@ class MinMaxScalerModel(Model):
     def _transform(self, dataset):
         ic, oc = self.getInputCol(), self.getOutputCol()
         a, z = self.getMin(), self.getMax()
-        lo = torch.tensor(self._lo, dtype=torch.float32)
-        rng = torch.tensor(self._hi - self._lo, dtype=torch.float32)
+        lo = torch.tensor(self._lo, dtype=torch.float64)
+        rng = torch.tensor(self._hi - self._lo, dtype=torch.float64)
 
         def fn(b, ctx):
-            X = b.columns[ic].values.float()
-            r = rng.to(b.device)
-            scaled = torch.where(r[None, :] != 0, (X - lo.to(b.device)) / torch.where(r != 0, r, torch.ones_like(r)),
+            X = b.columns[ic].values
+            X = X if X.dtype == torch.float64 else X.float()
+            r = rng.to(b.device, X.dtype)
+            scaled = torch.where(r[None, :] != 0, (X - lo.to(b.device, X.dtype)) / torch.where(r != 0, r, torch.ones_like(r)),
                                  torch.full_like(X, 0.5))
             return b.with_column(oc, ColumnData(scaled * (z - a) + a, T.VectorUDT()))
         return dataset._new(MapPlan(dataset._plan, "MinMaxScalerModel", fn))
@@ -841,7 +865,7 @@ class PCA(Estimator):
 
     def _fit(self, dataset):
         from .util import centered_gram, local_xyw
-        X, _, _ = local_xyw(dataset, self.getInputCol())
+        X, _, _ = local_xyw(dataset, self.getInputCol(), keep_f64=True)
         n, _, C = centered_gram(X, dataset._session.comm)
         cov = C / max(n - 1, 1)
         w, v = torch.linalg.eigh(cov.cpu())
@@ -871,10 +895,12 @@ class PCAModel(Model):
 
     def _transform(self, dataset):
         ic, oc = self.getInputCol(), self.getOutputCol()
-        P = torch.tensor(self._pc, dtype=torch.float32)
+        P = torch.tensor(self._pc, dtype=torch.float64)
 
         def fn(b, ctx):
-            return b.with_column(oc, ColumnData(b.columns[ic].values.float() @ P.to(b.device), T.VectorUDT()))
+            X = b.columns[ic].values
+            X = X if X.dtype == torch.float64 else X.float()
+            return b.with_column(oc, ColumnData(X @ P.to(b.device, X.dtype), T.VectorUDT()))
         return dataset._new(MapPlan(dataset._plan, "PCAModel", fn))
 
     def _save_state(self):

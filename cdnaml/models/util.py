@@ -1,6 +1,7 @@
 """Shared helpers for estimators: device matrices, ML attributes, errors."""
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -44,15 +45,30 @@ def local_batch(df, cols: List[str]) -> Batch:
     return concat_batches(parts)
 
 
+# Spark's VectorUDT holds Doubles.  A Double feature matrix of at most this many elements per rank (2^27: 1 GiB of
+# fp64; the course's Airbnb / iris / MovieLens designs are 1e3-1e6) is consumed in fp64 by the linear-algebra
+# estimators that opt in (linear / logistic regression, k-means, scalers, statistics); larger ones, and every fp32
+# matrix (the 1e8 x 100 benchmark shapes), take the fp32 HBM-bound kernels.  CDNAML_VECTOR_F64_MAX=0 disables.
+VECTOR_F64_MAX = int(os.environ.get("CDNAML_VECTOR_F64_MAX", str(1 << 27)))
+
+
+def feature_dtype(X: torch.Tensor) -> torch.dtype:
+    """The compute dtype of a feature matrix: fp64 for course-sized Double vectors, else fp32."""
+    return torch.float64 if X.dtype == torch.float64 and X.numel() <= VECTOR_F64_MAX else torch.float32
+
+
 def local_xyw(df, features_col: str, label_col: Optional[str] = None, weight_col: Optional[str] = None,
-              drop_null_label: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor], Optional[torch.Tensor]]:
-    """This rank's rows as device tensors: X f32 [n, d], y f64 [n], w f64 [n]."""
+              drop_null_label: bool = True, keep_f64: bool = False
+              ) -> Tuple[torch.Tensor, Optional[torch.Tensor], Optional[torch.Tensor]]:
+    """This rank's rows as device tensors: X [n, d] (f32, or f64 when ``keep_f64`` and the column holds a
+    course-sized Double matrix: ``feature_dtype``), y f64 [n], w f64 [n]."""
     require_vector(df, features_col)
     cols = [features_col] + ([label_col] if label_col else []) + ([weight_col] if weight_col else [])
     b = local_batch(df, cols)
     X = b.columns[features_col].values
-    if X.dtype != torch.float32:
-        X = X.float()
+    want = feature_dtype(X) if keep_f64 else torch.float32
+    if X.dtype != want:
+        X = X.to(want)
     y = w = None
     keep = None
     if label_col:
@@ -185,7 +201,7 @@ def centered_gram(X: torch.Tensor, comm, lead: int = 1024):
         comm.all_reduce_many([sh, cnt])
         sh = sh / cnt.clamp_min(1.0)
     sh = sh.float()
-    G = K.gram(X, shift=sh, fp64=gram_fp64_auto(n_loc, d)) if n_loc else \
+    G = K.gram(X, shift=sh, fp64=X.dtype == torch.float64 or gram_fp64_auto(n_loc, d)) if n_loc else \
         torch.zeros((d + 2, d + 2), dtype=torch.float64, device=X.device)
     comm.all_reduce(G)
     n = float(G[d, d])

@@ -205,13 +205,13 @@ _SIGS = {
     "cdna_reg_metrics": ([c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_score_hist": ([c_void_p, c_void_p, c_int64, c_double, c_double, c_int, c_void_p, c_void_p], c_int),
     "cdna_kmeans_step": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
-                          c_void_p, c_void_p], c_int),
+                          c_void_p, c_int, c_void_p], c_int),
     "cdna_hist_assemble": ([c_void_p, c_int, c_double, c_double, c_void_p, c_void_p, c_int, c_int64, c_int,
                             c_void_p, c_void_p], c_int),
     "cdna_grad_hess": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p,
                         c_void_p], c_int),
     "cdna_logistic_grad": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_double, c_void_p,
-                            c_void_p, c_void_p], c_int),
+                            c_void_p, c_int, c_void_p], c_int),
 }
 
 

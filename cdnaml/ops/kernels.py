@@ -34,6 +34,14 @@ def gram(X: torch.Tensor, y: Optional[torch.Tensor] = None, shift: Optional[torc
     the K1 MFMA kernel.
     """
     n, d = X.shape
+    if X.dtype == torch.float64:
+        # Spark's Double vectors (course scale): the augmented matrix is formed and multiplied in fp64 as is --
+        # no fp32 rounding of the features (the shift is the caller's fp32-rounded value, used exactly)
+        A = torch.empty((n, d + 2), dtype=torch.float64, device=X.device)
+        A[:, :d] = X if shift is None else X - shift.double()
+        A[:, d] = 1.0
+        A[:, d + 1] = 0.0 if y is None else (y.double() - yshift)
+        return A.T @ A
     if X.dtype != torch.float32:
         X = X.float()
     if _native(X) and d + 2 <= 512 and not fp64:
@@ -1252,10 +1260,11 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor, with_sums: bool = True):
     """Assign rows to nearest centre; return (assign, sums[k,d], counts[k], cost) (local)."""
     n, d = X.shape
     k = C.shape[0]
-    if _native(X) and (2 * k * d + k) * 4 <= 64 * 1024:
-        X = X.float()
+    f64 = X.dtype == torch.float64   # Spark's Double vectors at course scale: the fp64 kernel instantiation
+    if _native(X) and (2 * k * d + k) * (8 if f64 else 4) <= 64 * 1024:
+        X = X if f64 else X.float()
         X = X if X.stride(1) == 1 else X.contiguous()
-        Cf = C.float().contiguous()
+        Cf = C.to(X.dtype).contiguous()
         assign = torch.empty(n, dtype=torch.int32, device=X.device)
         sums = torch.zeros((k, d), dtype=torch.float64, device=X.device)
         counts = torch.zeros(k, dtype=torch.float64, device=X.device)
@@ -1263,11 +1272,11 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor, with_sums: bool = True):
         if n:
             _lib.check(_lib.lib().cdna_kmeans_step(_ptr(X), n, d, X.stride(0), _ptr(Cf), k, _ptr(assign),
                                                    _ptr(sums) if with_sums else None,
-                                                   _ptr(counts) if with_sums else None, _ptr(cost),
+                                                   _ptr(counts) if with_sums else None, _ptr(cost), int(f64),
                                                    _stream(X.device)), "cdna_kmeans_step")
         return assign, sums, counts, cost[0]
-    Xf = X.float()
-    dist = torch.cdist(Xf, C.float()) ** 2
+    Xf = X if f64 else X.float()
+    dist = ((Xf[:, None, :] - C.to(Xf.dtype)[None, :, :]) ** 2).sum(2) if f64 else torch.cdist(Xf, C.float()) ** 2
     best, assign = dist.min(dim=1)
     sums = torch.zeros((k, d), dtype=torch.float64, device=X.device)
     sums.index_add_(0, assign, Xf.double())
@@ -1283,14 +1292,15 @@ def logistic_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b: float,
     y = y.double().contiguous()
     wt = None if wt is None else wt.double().contiguous()
     if _native(X) and d <= 512:
-        X = X.float()
+        f64 = X.dtype == torch.float64   # Double vectors (course scale): the fp64 instantiation reads them as is
+        X = X if f64 else X.float()
         X = X if X.stride(1) == 1 else X.contiguous()
         wd = w.double().contiguous()
         grad = torch.zeros(d + 1, dtype=torch.float64, device=X.device)
         loss = torch.zeros(1, dtype=torch.float64, device=X.device)
         if n:
             _lib.check(_lib.lib().cdna_logistic_grad(_ptr(X), n, d, X.stride(0), _ptr(y), _ptr(wt), _ptr(wd),
-                                                     float(b), _ptr(grad), _ptr(loss), _stream(X.device)),
+                                                     float(b), _ptr(grad), _ptr(loss), int(f64), _stream(X.device)),
                        "cdna_logistic_grad")
         return grad, loss[0]
     Xd = X.double()

@@ -263,30 +263,34 @@ __global__ __launch_bounds__(256) void score_hist_kernel(const double* __restric
 
 // -------------------------------------------------------- K10 k-means step
 // assign each row to its nearest centre; accumulate per-centre sums/counts
-// (LDS-privatised, f64 flush).  centres/sums staged in LDS (k*d <= 8192).
-__global__ __launch_bounds__(256) void kmeans_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
-                                                     const float* __restrict__ C, int k, int* __restrict__ assign,
+// (LDS-privatised, f64 flush).  centres/sums staged in LDS.  T = float (the
+// HBM-bound large-data path; LDS k*d <= 8192) or double (Spark's Double
+// vectors at course scale: distances, LDS partial sums and flush all in fp64;
+// ds_add_f64 on gfx950; k*d <= 4096).
+template <typename T>
+__global__ __launch_bounds__(256) void kmeans_kernel(const T* __restrict__ X, int64_t n, int d, int64_t ldx,
+                                                     const T* __restrict__ C, int k, int* __restrict__ assign,
                                                      double* __restrict__ sums, double* __restrict__ counts,
                                                      double* __restrict__ cost) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* sc = sm;               // [k][d]
-  float* ss = sm + k * d;       // [k][d]
-  float* scnt = ss + k * d;     // [k]
+  extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+  T* sc = reinterpret_cast<T*>(smraw);  // [k][d]
+  T* ss = sc + k * d;                   // [k][d]
+  T* scnt = ss + k * d;                 // [k]
   for (int i = threadIdx.x; i < k * d; i += 256) {
     sc[i] = C[i];
-    ss[i] = 0.f;
+    ss[i] = T(0);
   }
-  for (int i = threadIdx.x; i < k; i += 256) scnt[i] = 0.f;
+  for (int i = threadIdx.x; i < k; i += 256) scnt[i] = T(0);
   __syncthreads();
   double mycost = 0.0;
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
-    const float* x = X + r * ldx;
-    float best = 3.4e38f;
+    const T* x = X + r * ldx;
+    T best = T(3.4e38);
     int bi = 0;
     for (int c = 0; c < k; ++c) {
-      float dist = 0.f;
+      T dist = T(0);
       for (int f = 0; f < d; ++f) {
-        const float df = x[f] - sc[c * d + f];
+        const T df = x[f] - sc[c * d + f];
         dist += df * df;
       }
       if (dist < best) {
@@ -295,18 +299,18 @@ __global__ __launch_bounds__(256) void kmeans_kernel(const float* __restrict__ X
       }
     }
     assign[r] = bi;
-    mycost += best;
+    mycost += (double)best;
     if (sums) {
       for (int f = 0; f < d; ++f) atomicAdd(&ss[bi * d + f], x[f]);
-      atomicAdd(&scnt[bi], 1.f);
+      atomicAdd(&scnt[bi], T(1));
     }
   }
   __syncthreads();
   if (sums) {
     for (int i = threadIdx.x; i < k * d; i += 256)
-      if (ss[i] != 0.f) atomicAdd(&sums[i], (double)ss[i]);
+      if (ss[i] != T(0)) atomicAdd(&sums[i], (double)ss[i]);
     for (int i = threadIdx.x; i < k; i += 256)
-      if (scnt[i] != 0.f) atomicAdd(&counts[i], (double)scnt[i]);
+      if (scnt[i] != T(0)) atomicAdd(&counts[i], (double)scnt[i]);
   }
   if (cost) {
     const double v = cdna::wave_sum(mycost);
@@ -322,7 +326,9 @@ __global__ __launch_bounds__(256) void kmeans_kernel(const float* __restrict__ X
 // Everything past the fp32 feature load is fp64: w, the margin's products and its wave sum (Spark's Double
 // margins; the fp32 dot product moved the fitted objective by ~1e-3 relative against the host's fp64 one, and
 // L-BFGS at tol 1e-6 then stopped elsewhere).  The kernel stays HBM-bound on the fp32 rows.
-__global__ __launch_bounds__(256) void logistic_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
+// T = double: Spark's Double feature vectors at course scale (the whole margin and gradient exact fp64).
+template <typename T>
+__global__ __launch_bounds__(256) void logistic_kernel(const T* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                        const double* __restrict__ y, const double* __restrict__ wt,
                                                        const double* __restrict__ w, double b,
                                                        double* __restrict__ grad, double* __restrict__ loss) {
@@ -342,13 +348,13 @@ __global__ __launch_bounds__(256) void logistic_kernel(const float* __restrict__
   }
   double gb = 0.0, ls = 0.0;
   for (int64_t r = gw; r < n; r += nw) {
-    const float* x = X + r * ldx;
-    float xv[FPL];
+    const T* x = X + r * ldx;
+    T xv[FPL];
     double dot = 0.0;
 #pragma unroll
     for (int q = 0; q < FPL; ++q) {
       const int f = lane + 64 * q;
-      xv[q] = f < d ? x[f] : 0.f;
+      xv[q] = f < d ? x[f] : T(0);
       dot += (double)xv[q] * wl[q];
     }
     const double m = cdna::wave_sum(dot) + b;
@@ -607,23 +613,32 @@ CDNA_API int cdna_score_hist(const double* score, const double* label, int64_t n
   return (int)hipGetLastError();
 }
 
-CDNA_API int cdna_kmeans_step(const float* X, int64_t n, int d, int64_t ldx, const float* C, int k, int* assign,
-                              double* sums, double* counts, double* cost, hipStream_t st) {
+// f64: X and C are double (else float)
+CDNA_API int cdna_kmeans_step(const void* X, int64_t n, int d, int64_t ldx, const void* C, int k, int* assign,
+                              double* sums, double* counts, double* cost, int f64, hipStream_t st) {
   if (n <= 0) return 0;
-  if ((size_t)(2 * k * d + k) * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)(2 * k * d + k) * 4;
-  hipLaunchKernelGGL(kmeans_kernel, dim3(grid_for(n, 256, 2048)), dim3(256), lds, st, X, n, d, ldx, C, k, assign,
-                     sums, counts, cost);
+  const size_t lds = (size_t)(2 * k * d + k) * (f64 ? 8 : 4);
+  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
+  if (f64)
+    hipLaunchKernelGGL(kmeans_kernel<double>, dim3(grid_for(n, 256, 2048)), dim3(256), lds, st,
+                       (const double*)X, n, d, ldx, (const double*)C, k, assign, sums, counts, cost);
+  else
+    hipLaunchKernelGGL(kmeans_kernel<float>, dim3(grid_for(n, 256, 2048)), dim3(256), lds, st,
+                       (const float*)X, n, d, ldx, (const float*)C, k, assign, sums, counts, cost);
   return (int)hipGetLastError();
 }
 
-CDNA_API int cdna_logistic_grad(const float* X, int64_t n, int d, int64_t ldx, const double* y, const double* wt,
-                                const double* w, double b, double* grad, double* loss, hipStream_t st) {
+CDNA_API int cdna_logistic_grad(const void* X, int64_t n, int d, int64_t ldx, const double* y, const double* wt,
+                                const double* w, double b, double* grad, double* loss, int f64, hipStream_t st) {
   if (n <= 0) return 0;
   if (d > 512) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)(d + 1) * 8;
-  hipLaunchKernelGGL(logistic_kernel, dim3(grid_for(n, 64, 1024)), dim3(256), lds, st, X, n, d, ldx, y, wt, w, b,
-                     grad, loss);
+  if (f64)
+    hipLaunchKernelGGL(logistic_kernel<double>, dim3(grid_for(n, 64, 1024)), dim3(256), lds, st,
+                       (const double*)X, n, d, ldx, y, wt, w, b, grad, loss);
+  else
+    hipLaunchKernelGGL(logistic_kernel<float>, dim3(grid_for(n, 64, 1024)), dim3(256), lds, st,
+                       (const float*)X, n, d, ldx, y, wt, w, b, grad, loss);
   return (int)hipGetLastError();
 }
 

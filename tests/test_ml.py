@@ -291,7 +291,7 @@ def test_kmeans_maxiter_zero_returns_init_centres(spark):
     m20 = KMeans(k=3, seed=221, maxIter=20).fit(df)
     c0 = np.array(m0.clusterCenters())
     np.testing.assert_array_equal(c0, np.array(KMeans(k=3, seed=221, maxIter=0).fit(df).clusterCenters()))
-    rows = {tuple(r) for r in X.astype(np.float32).astype(np.float64).tolist()}  # vectors are fp32
+    rows = {tuple(r) for r in X.tolist()}  # vectors are Double, as Spark's VectorUDT
     cr = KMeans(k=3, seed=221, maxIter=0, initMode="random").fit(df).clusterCenters()
     assert all(tuple(c) in rows for c in np.array(cr).tolist())  # random init picks data points
     assert m20.summary.trainingCost <= m0.summary.trainingCost

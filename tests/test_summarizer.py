@@ -15,8 +15,8 @@ def _frame(spark, n=5000, seed=3):
     pdf["w"] = w
     pdf["k"] = np.arange(n) % 3
     df = VectorAssembler(inputCols=list("abcd"), outputCol="features").transform(spark.createDataFrame(pdf))
-    # the engine's feature vectors are fp32 (statistics accumulate in fp64)
-    return df, X.astype(np.float32).astype(np.float64), w, pdf["k"].to_numpy()
+    # the assembled vectors are Double (Spark's VectorUDT) at this size: the statistics are exact fp64
+    return df, X, w, pdf["k"].to_numpy()
 
 
 def _expect(X, w):
