@@ -4,7 +4,7 @@ A ``Batch`` is one partition: an ordered set of ``ColumnData`` that all live
 on the rank's GPU (or CPU in CPU-only runs).  Numeric columns are torch
 tensors, strings are dictionary codes + a host dictionary (so string
 predicates, lower()/translate() and group keys run as integer ops on the
-GPU), vectors are dense float32 ``[n, d]`` matrices.  Nulls are a separate
+GPU), vectors are dense ``[n, d]`` matrices (fp64 = Spark's Double at course scale, fp32 for large ones).  Nulls are a separate
 validity mask (``None`` = no nulls).
 """
 from __future__ import annotations
@@ -185,7 +185,7 @@ def full_column(value, dt: T.DataType, n: int, device) -> ColumnData:
         return ColumnData(torch.zeros(n, dtype=torch.int32, device=device), dt,
                           dictionary=np.array([str(value)], dtype=object))
     if isinstance(dt, T.VectorUDT):
-        arr = torch.as_tensor(np.asarray(value.toArray() if hasattr(value, "toArray") else value, np.float32))
+        arr = torch.as_tensor(np.asarray(value.toArray() if hasattr(value, "toArray") else value, np.float64))
         return ColumnData(arr.to(device)[None, :].expand(n, -1).contiguous(), dt)
     if isinstance(dt, T.DateType) and isinstance(value, _dt.date):
         value = (value - _EPOCH).days
@@ -417,11 +417,13 @@ def column_from_numpy(arr, dt: Optional[T.DataType], device) -> ColumnData:
                 isnull[i] = True
                 rows.append(None)
                 continue
-            a = np.asarray(v.toArray() if hasattr(v, "toArray") else v, dtype=np.float32)
+            a = np.asarray(v.toArray() if hasattr(v, "toArray") else v, dtype=np.float64)
             width = len(a)
             rows.append(a)
         width = width or 0
-        mat = np.zeros((n, width), np.float32)
+        # Spark's vectors hold Doubles: kept fp64 at course scale (models.util.VECTOR_F64_MAX elements)
+        from ..models.util import VECTOR_F64_MAX
+        mat = np.zeros((n, width), np.float64 if n * width <= VECTOR_F64_MAX else np.float32)
         for i, r in enumerate(rows):
             if r is not None:
                 mat[i] = r

@@ -2,8 +2,9 @@
 
 Every type knows its device storage: scalar numerics are torch tensors of the
 matching width, strings are dictionary codes (int32) on device plus a host
-dictionary, vectors (``VectorUDT``) are dense float32 ``[n, d]`` matrices —
-the layout the MFMA/histogram kernels consume directly.
+dictionary, vectors (``VectorUDT``) are dense ``[n, d]`` matrices — fp64 (Spark's
+Double) at course scale, fp32 for the large shapes the MFMA/histogram kernels
+stream (``models.util.VECTOR_F64_MAX``).
 Reference usage: ``df.dtypes`` splits (ML 03:56,74), ``schema.fields`` /
 ``IntegerType()`` checks (ML 01:203), DDL strings (ML 12:131,142;
 ML 13:54-59).
@@ -131,7 +132,7 @@ class BinaryType(DataType):
 
 
 class VectorUDT(DataType):
-    """ML vector column: dense float32 [n, d] on device."""
+    """ML vector column: dense [n, d] on device (fp64 at course scale, fp32 for large matrices)."""
     _name = "vector"
     torch_dtype = torch.float32
 
