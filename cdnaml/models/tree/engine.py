@@ -48,7 +48,7 @@ MSEG_L0 = True  # level 0 through segments too
 # single-tree packed fits (boosting rounds with unit hessians, DecisionTree) through row records + compaction
 MSEG_T1 = True
 # binary and 3-class classification forests on the packed record / segment path (class counts from (W, W1)
-# sums; 3 classes: (W, W1 + 2^32 W2), K.cls3_expand)
+# sums; 3 classes: (W, W1, W2) int64 columns, K.cls3_expand)
 MSEG_CLS = True
 # K6 split search in one HIP kernel (split.hip) where it applies; else the torch formulation
 NATIVE_SPLIT = True
@@ -499,7 +499,7 @@ class ForestTrainer:
         collective stream while chunk c + 1 is built (one per-level RCCL all-reduce of 1-50 MB otherwise
         serialises with the compute stream).  The sums are exact integers, so the result is identical to one
         fused all-reduce."""
-        Hb = torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev)
+        Hb = torch.zeros((S, d, B, K.hist_cols(cls3)), dtype=torch.int64, device=dev)
         k = min(HIST_OVERLAP, S)
         bounds = np.linspace(0, S, k + 1).round().astype(np.int64)
         rm, s10 = data.record_rows() if dev.type == "cuda" else (None, False)
@@ -584,12 +584,11 @@ class ForestTrainer:
         # exactly the class histograms of the node-id / codes kernels, so the forest does not change.  Forests
         # deeper than 8 levels (u16 codes hold <= 255 nodes per tree) switch to node ids at level 8
         st.cls2 = self.classification and self.C == 2 and MSEG_CLS
-        # three classes: label codes 0 / 1 / 2^22 in the records' one quantised value; the histogram kernels
-        # re-space each block's sum to W1 + 2^32 W2, so the int64 totals must keep W1 < 2^32 (weights <= 255),
-        # and the codes hold <= 255 nodes per tree (no node-id switch below level 8)
+        # three classes: label codes 0 / 1 / 2^22 in the records' one quantised value; the histogram kernels split
+        # each block's sum W1 + 2^22 W2 into two int64 columns (no bound on the row count), and the codes hold <= 255
+        # nodes per tree (no node-id switch below level 8)
         st.cls3 = (self.classification and self.C == 3 and MSEG_CLS and p.max_depth <= 8 and
-                   data.n_global * 255 < 2 ** 32 and MSEG_REC and stats_rows.get("v0") is None and
-                   8 * data.B * 8 <= 128 * 1024)
+                   MSEG_REC and stats_rows.get("v0") is None and 8 * data.B * 8 <= 128 * 1024)
         st.deep_switch = (st.cls2 or (not self.classification and DEEP_REG and T > 1)) and p.max_depth > 8
         if st.cls2:
             stats_rows = dict(stats_rows, v1=stats_rows["label"].float())
@@ -831,8 +830,8 @@ class ForestTrainer:
             # of a 1.25e7-row shard would launch ~1 round of blocks each (half of it idle)
             lv.Hb = K.seg_hist_codes(root_rows, d, B, st.codes, stats_rows["v1"], st.mseg_scales[1], wmax,
                                      slot_tree, sl_node, 0, S,
-                                     torch.zeros((S, d, B, 2), dtype=torch.int64, device=dev), draw=draw,
-                                     cls3=st.cls3)
+                                     torch.zeros((S, d, B, K.hist_cols(st.cls3)), dtype=torch.int64, device=dev),
+                                     draw=draw, cls3=st.cls3)
             lv.hist_raw_scale = st.mseg_raw
         elif st.use_mseg and (depth >= 1 or MSEG_L0):
             # gather the rows of the built nodes into slot segments, then segment histograms of packed
@@ -891,7 +890,7 @@ class ForestTrainer:
         if st.cls2 and lv.hist_raw_scale is not None:
             lv.Hb[..., 0] -= lv.Hb[..., 1]  # packed (W, W1) -> class counts (W0, W1), exact int64
         elif st.cls3 and lv.hist_raw_scale is not None:
-            lv.Hb = K.cls3_expand(lv.Hb)  # packed (W, W1 + 2^32 W2) -> class counts (W0, W1, W2)
+            lv.Hb = K.cls3_expand(lv.Hb)  # (W, W1, W2) -> class counts (W0, W1, W2)
 
     def _level_reduce(self, st: "_FitState", lv: "_Level") -> None:
         """The level histograms summed over ranks: one fused all-reduce, or (large int64 levels) a reduce-scatter

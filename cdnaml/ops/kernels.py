@@ -1437,8 +1437,8 @@ def seg_hist(bins: torch.Tensor, d: int, B: int, perm: torch.Tensor, v0p: Option
 
     rm_s10 (rec): ``bins_rm`` is in the seg10 layout (:func:`bins_seg10`): the six-items-per-wave kernel.
 
-    cls3 (rec + raw): 3-class records (label codes 0 / 1 / ``CLS3_CODE``, scale 1): the sums are (W, W1 + 2^32 W2)
-    (:func:`cls3_expand` turns them into class counts).
+    cls3 (rec + raw): 3-class records (label codes 0 / 1 / ``CLS3_CODE``, scale 1): the sums are [S, d, B, 3]
+    (W, W1, W2) (:func:`cls3_expand` turns them into class counts).
 
     out (rec + raw): a zeroed int64 [S, d, B, 2] tensor (e.g. a slot-range slice of a level's buffer) the sums
     are accumulated into and returned -- lets the engine all-reduce one slot chunk while the next is built.
@@ -1463,14 +1463,15 @@ def _seg_flat_index(bins: torch.Tensor, d: int, B: int, rows: torch.Tensor, slot
     return slot[:, None] * (d * B) + torch.arange(d)[None, :] * B + flat[rows]
 
 
-def _int_hist_cpu(bins, d, B, S, rows, slot, a0, a1) -> torch.Tensor:
-    """CPU: exact int64 sums of per-item integers a0 / a1 into cells [S, d, B, 2]."""
-    out = torch.zeros(S * d * B * 2, dtype=torch.int64)
+def _int_hist_cpu(bins, d, B, S, rows, slot, *cols) -> torch.Tensor:
+    """CPU: exact int64 sums of per-item integers (a0, a1[, a2]) into cells [S, d, B, len(cols)]."""
+    k = len(cols)
+    out = torch.zeros(S * d * B * k, dtype=torch.int64)
     if rows.numel():
-        idx = _seg_flat_index(bins, d, B, rows, slot) * 2
-        out.index_add_(0, idx.reshape(-1), a0[:, None].expand(-1, d).reshape(-1))
-        out.index_add_(0, idx.reshape(-1) + 1, a1[:, None].expand(-1, d).reshape(-1))
-    return out.view(S, d, B, 2)
+        idx = _seg_flat_index(bins, d, B, rows, slot) * k
+        for j, a in enumerate(cols):
+            out.index_add_(0, idx.reshape(-1) + j, a[:, None].expand(-1, d).reshape(-1))
+    return out.view(S, d, B, k)
 
 
 def _seg_items(segs: np.ndarray):
@@ -1491,20 +1492,20 @@ def _quant(v: torch.Tensor, scale: float, clamp: bool) -> torch.Tensor:
 
 
 # 3-class packed records (seg.hip kClsSplit): class c's label code is 0 / 1 / CLS3_CODE, so a histogram block's
-# sum w * q is W1 + 2^22 W2; the kernels re-space it to W1 + 2^32 W2 in their flush
+# sum w * q is W1 + 2^22 W2 (W1 < 2^22 inside a block); the kernels' flush splits it into two int64 columns, so the
+# level histograms are [S, d, B, 3] (W, W1, W2) and their global sums have no size bound (round 5 packed
+# W1 + 2^32 W2 in one column: n_global * 255 < 2^32 rows at most)
 CLS3_CODE = 1 << 22
 
 
-def _cls3_respace(q: torch.Tensor) -> torch.Tensor:
-    """CPU twin of the kernels' flush re-spacing, per item (linear in w): q -> (q mod 2^22) + 2^32 (q >> 22)."""
-    return (q & (CLS3_CODE - 1)) + ((q >> 22) << 32)
+def hist_cols(cls3: bool) -> int:
+    """Int64 columns per cell of a record histogram: (count, sum), or (W, W1, W2) for 3-class records."""
+    return 3 if cls3 else 2
 
 
 def cls3_expand(Hb: torch.Tensor) -> torch.Tensor:
-    """Packed 3-class sums [..., 2] (W, W1 + 2^32 W2) -> exact int64 class counts [..., 3] (W0, W1, W2)."""
-    W, P = Hb[..., 0], Hb[..., 1]
-    W1 = P & 0xFFFFFFFF
-    W2 = P >> 32
+    """3-class record sums [..., 3] (W, W1, W2) -> exact int64 class counts [..., 3] (W0, W1, W2)."""
+    W, W1, W2 = Hb[..., 0], Hb[..., 1], Hb[..., 2]
     return torch.stack([W - W1 - W2, W1, W2], -1)
 
 
@@ -1522,15 +1523,19 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
                   cls3=False):
     G, n, _ = bins.shape
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 3)
+    kc = hist_cols(cls3)
     if S == 0 or len(segs) == 0:
         if out is not None:
             return out
-        return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
+        return torch.zeros((S, d, B, kc), dtype=torch.int64 if raw else torch.float64, device=bins.device)
     qs1 = float(scales[1])
     if not _native(bins):
         pos, slot = _seg_items(segs)
         rows, w, q = rec_decode(rec[pos])
-        iout = _int_hist_cpu(bins, d, B, S, rows, slot, w, w * (_cls3_respace(q) if cls3 else q))
+        if cls3:
+            iout = _int_hist_cpu(bins, d, B, S, rows, slot, w, w * (q & (CLS3_CODE - 1)), w * (q >> 22))
+        else:
+            iout = _int_hist_cpu(bins, d, B, S, rows, slot, w, w * q)
         if out is not None:
             iout = out.copy_(iout)
     else:
@@ -1547,9 +1552,10 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
         if len(work) == 0:
             if out is not None:
                 return out
-            return torch.zeros((S, d, B, 2), dtype=torch.int64 if raw else torch.float64, device=bins.device)
+            return torch.zeros((S, d, B, kc), dtype=torch.int64 if raw else torch.float64, device=bins.device)
         wt, = upload(bins.device, work.reshape(-1))
-        iout = out if out is not None else torch.zeros((S, d, B, 2), dtype=torch.int64, device=bins.device)
+        iout = out if out is not None else torch.zeros((S, d, B, kc), dtype=torch.int64, device=bins.device)
+        assert iout.shape == (S, d, B, kc)
         assert bins_rm.shape[0] == n and bins_rm.shape[1] >= G and bins_rm.is_contiguous()
         mode = 1 | 4 | 16 | (128 if (SEG_LANE and B <= SEG_LANE_MAX_B) else 0) | (512 if cls3 else 0)
         if rm_s10:
@@ -1594,7 +1600,7 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
     assert _native(codes) and ((d <= 100 and B <= 40 and bins_s10.shape == (n, 16, 8)) or
                                (wide and bins_s10.shape[0] == n and bins_s10.shape[1] * 8 >= d and
                                 bins_s10.is_contiguous()))
-    assert out.dtype == torch.int64 and out.is_contiguous() and out.shape == (s1 - s0, d, B, 2)
+    assert out.dtype == torch.int64 and out.is_contiguous() and out.shape == (s1 - s0, d, B, hist_cols(cls3))
     st = np.asarray(slot_tree, dtype=np.int64)
     sn = np.asarray(slot_node, dtype=np.int64)
     assert len(st) == len(sn) and np.all((st >= 0) & (st < T)) and np.all((sn >= 0) & (sn < 0xFF))
@@ -1971,7 +1977,14 @@ SCATTER_SCAN_MIN_KB = 4
 COMPACT_WAVES = 2048
 
 
-def _scatter_rank(KB: int) -> int:
+# queued scatter (seg.hip codes_scatter_q_kernel, rank 2): the built row slots queued per wave in LDS and ranked /
+# stored in dense groups of 64 (packed records, per_wave <= 65536); identical records to ranks 0 / 1
+SCATTER_QUEUE = True
+
+
+def _scatter_rank(KB: int, rec: bool = False, per_wave: int = 0) -> int:
+    if SCATTER_QUEUE and rec and per_wave <= 65536:
+        return 2
     return 0 if (SCATTER_RANK == 1 and KB < SCATTER_SCAN_MIN_KB) else SCATTER_RANK
 
 
@@ -2020,7 +2033,8 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
         perm = torch.empty(n * T + REC_PAD, dtype=torch.int64, device=dev)
         _lib.check(L.cdna_codes_compact_w(2, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
                                           per_wave, Wv, None, _ptr(wcnt), None, None, None, None, _ptr(perm),
-                                          float(rec_scale), _ptr(kstart_t), _scatter_rank(KB), _stream(dev)),
+                                          float(rec_scale), _ptr(kstart_t), _scatter_rank(KB, True, per_wave),
+                                          _stream(dev)),
                    "cdna_codes_compact_w(scatter)")
         ev.synchronize()
         tot_h = tot_p.numpy()
@@ -2051,7 +2065,8 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
         _lib.check(L.cdna_codes_compact_w(2, KB, _ptr(codes), n, T, A, _ptr(tf), _ptr(kmap_t), _ptr(v0c), _ptr(v1c),
                                           per_wave, Wv, None, _ptr(wcnt), None if rec else _ptr(perm), _ptr(v0p),
                                           _ptr(v1p), _ptr(wp), _ptr(perm) if rec else None,
-                                          float(rec_scale) if rec else 0.0, _ptr(kstart_t), _scatter_rank(KB),
+                                          float(rec_scale) if rec else 0.0, _ptr(kstart_t),
+                                          _scatter_rank(KB, rec, per_wave),
                                           _stream(dev)),
                    "cdna_codes_compact_w(scatter)")
     return perm, v0p, v1p, wp, np.stack([starts, lens], 1)

@@ -48,9 +48,23 @@ struct SegHistArgs {
 
 constexpr int kClsSplit = 22;
 
-__device__ __forceinline__ long long cls_respace(long long sum, int sp) {
-  if (!sp) return sum;
-  return (sum & ((1ll << sp) - 1ll)) | ((sum >> sp) << 32);
+// Flush one packed cell's (count, signed sum) into the int64 output: two columns, or for 3-class records
+// (cls_split) three -- (W, W1, W2) with W1 = sum mod 2^22, W2 = sum >> 22 -- so the global sums of many blocks and
+// ranks need no bound on W1 (round 5 re-spaced the sum to W1 + 2^32 W2 in one column, which required
+// n_global * 255 < 2^32, i.e. <= 1.68e7 rows for the packed 3-class path).
+__device__ __forceinline__ void flush_packed(const SegHistArgs& a, int64_t cell, unsigned long long cnt,
+                                             long long sum) {
+  if (a.cls_split) {
+    unsigned long long* o = &a.out[cell * 3];
+    atomicAdd(o, cnt);
+    const long long lo = sum & ((1ll << a.cls_split) - 1ll), hi = sum >> a.cls_split;
+    if (lo) atomicAdd(o + 1, (unsigned long long)lo);
+    if (hi) atomicAdd(o + 2, (unsigned long long)hi);
+  } else {
+    unsigned long long* o = &a.out[cell * 2];
+    atomicAdd(o, cnt);
+    atomicAdd(o + 1, (unsigned long long)sum);
+  }
 }
 
 // PACKED: one u64 atomic per update (count << 44 | sum of w * (q + 2^23)); the
@@ -134,15 +148,14 @@ __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const SegHistArgs
     const int jj = c / a.B, bn = c - jj * a.B;
     const int f = fbase + jj;
     if (f >= a.d) continue;
-    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+    const int64_t cell = ((int64_t)slot * a.d + f) * a.B + bn;
     if (PACKED) {
       const unsigned long long v = h[c];
       if (!v) continue;
       const unsigned long long cnt = v >> kPackShift;
-      const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
-      atomicAdd(o, cnt);
-      atomicAdd(o + 1, (unsigned long long)sum);
+      flush_packed(a, cell, cnt, (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt);
     } else {
+      unsigned long long* o = &a.out[cell * 2];
       const unsigned long long v0 = h[c], v1 = h[plane + c];
       if (v0) atomicAdd(o, v0);
       if (v1) atomicAdd(o + 1, v1);
@@ -243,15 +256,14 @@ __global__ __launch_bounds__(1024) void seg_hist_rm_kernel(const SegHistArgs a, 
     const int jj = rem / a.B, bn = rem - jj * a.B;
     const int f = (g0 + gq) * 8 + jj;
     if (f >= a.d) continue;
-    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
+    const int64_t cell = ((int64_t)slot * a.d + f) * a.B + bn;
     if (PACKED) {
       const unsigned long long v = h[c];
       if (!v) continue;
       const unsigned long long cnt = v >> kPackShift;
-      const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
-      atomicAdd(o, cnt);
-      atomicAdd(o + 1, (unsigned long long)sum);
+      flush_packed(a, cell, cnt, (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt);
     } else {
+      unsigned long long* o = &a.out[cell * 2];
       const unsigned long long v0 = h[c], v1 = h[plane + c];
       if (v0) atomicAdd(o, v0);
       if (v1) atomicAdd(o + 1, v1);
@@ -343,11 +355,9 @@ __global__ __launch_bounds__(1024) void seg_hist_flat_kernel(const SegHistArgs a
     if (f >= a.d) continue;
     const unsigned long long v = h[c];
     const unsigned long long cnt = v >> kPackShift;
-    const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
+    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
     if (!cnt) continue;
-    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
-    atomicAdd(o, cnt);
-    atomicAdd(o + 1, (unsigned long long)sum);
+    flush_packed(a, ((int64_t)slot * a.d + f) * a.B + bn, cnt, sum);
   }
 }
 
@@ -435,10 +445,8 @@ __global__ __launch_bounds__(512) void seg_hist_lane_kernel(const SegHistArgs a,
     const unsigned long long v = h[c];
     if (!v) continue;
     const unsigned long long cnt = v >> kPackShift;
-    const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
-    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
-    atomicAdd(o, cnt);
-    atomicAdd(o + 1, (unsigned long long)sum);
+    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    flush_packed(a, ((int64_t)slot * a.d + f) * a.B + bn, cnt, sum);
   }
 }
 
@@ -517,10 +525,8 @@ __global__ __launch_bounds__(1024, 2) void seg_hist_lane8_kernel(const SegHistAr
     const unsigned long long cnt = (v0 >> kPackShift) + (v1 >> kPackShift);
     if (!cnt) continue;
     const unsigned long long m = (1ull << kPackShift) - 1ull;
-    const long long sum = cls_respace((long long)((v0 & m) + (v1 & m)) - (long long)kPackQ * (long long)cnt, a.cls_split);
-    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
-    atomicAdd(o, cnt);
-    atomicAdd(o + 1, (unsigned long long)sum);
+    const long long sum = (long long)((v0 & m) + (v1 & m)) - (long long)kPackQ * (long long)cnt;
+    flush_packed(a, ((int64_t)slot * a.d + f) * a.B + bn, cnt, sum);
   }
 }
 
@@ -608,11 +614,8 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_kernel(const SegHistArgs
     const unsigned long long cnt = (v0 >> kPackShift) + (v1 >> kPackShift) + (v2 >> kPackShift);
     if (!cnt) continue;
     const unsigned long long m = (1ull << kPackShift) - 1ull;
-    const long long sum = cls_respace((long long)((v0 & m) + (v1 & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt,
-                                        a.cls_split);
-    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
-    atomicAdd(o, cnt);
-    atomicAdd(o + 1, (unsigned long long)sum);
+    const long long sum = (long long)((v0 & m) + (v1 & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt;
+    flush_packed(a, ((int64_t)slot * a.d + f) * a.B + bn, cnt, sum);
   }
 }
 
@@ -748,11 +751,8 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_root_kernel(const SegHis
     const unsigned long long cnt = (v0 >> kPackShift) + (v1c >> kPackShift) + (v2 >> kPackShift);
     if (!cnt) continue;
     const unsigned long long m = (1ull << kPackShift) - 1ull;
-    const long long sum = cls_respace((long long)((v0 & m) + (v1c & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt,
-                                        a.cls_split);
-    unsigned long long* o = &a.out[(((int64_t)(slot - slot0) * a.d + f) * a.B + bn) * 2];
-    atomicAdd(o, cnt);
-    atomicAdd(o + 1, (unsigned long long)sum);
+    const long long sum = (long long)((v0 & m) + (v1c & m) + (v2 & m)) - (long long)kPackQ * (long long)cnt;
+    flush_packed(a, ((int64_t)(slot - slot0) * a.d + f) * a.B + bn, cnt, sum);
   }
 }
 
@@ -837,10 +837,8 @@ __global__ __launch_bounds__(1024) void seg_hist_lane4_kernel(const SegHistArgs 
     const unsigned long long v = h[j * PLANE + bn * 16 + l];
     if (!v) continue;
     const unsigned long long cnt = v >> kPackShift;
-    const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
-    unsigned long long* o = &a.out[(((int64_t)slot * a.d + f) * a.B + bn) * 2];
-    atomicAdd(o, cnt);
-    atomicAdd(o + 1, (unsigned long long)sum);
+    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    flush_packed(a, ((int64_t)slot * a.d + f) * a.B + bn, cnt, sum);
   }
 }
 
@@ -1401,6 +1399,136 @@ __global__ __launch_bounds__(256) void codes_scatter_w_kernel(const CompactWArgs
   }
 }
 
+// RANK 2 (packed records only): queue first, rank dense.  PMC on RANK 1 put the scatter at 73-85 % VALU issue, and
+// a wave instruction costs the same whatever number of its lanes is active -- but at the headline's levels 2-4
+// only ~25 % of the (row, tree) slots belong to a built node: 3 of every 4 lanes of every scan, readlane,
+// bpermute and record instruction worked for nothing.  Here the wave first queues its built slots in LDS in row
+// order -- a lane reads 4 consecutive codes with one 8-byte load, counts its built ones, and one DPP scan of
+// those counts places them (row offset | weight << 16 | node << 24) -- and then drains the queue in DENSE groups
+// of 64 entries that gather their labels, run the RANK 1 node ranking (RANK 0 ballots for KB <= 2) and build +
+// store the records.  A group ranks in queue order, so the records and their positions are exactly RANK 0 / 1's
+// (row order inside each (tree, node, wave) run).  Leftovers (< 64) carry to the next trip; the wave's last group
+// is partial.  A/B at the headline (profiles/r6/scatter_queue_ab.md).  LDS: 4 waves x 576 x 4 B = 9 KB per block.
+template <int KB>
+__global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs a) {
+  constexpr int NW = KB > 4 ? KB / 4 : 1;
+  constexpr int NG = 2;                  // 256-row groups per trip (4 consecutive rows per lane)
+  constexpr int QCAP = NG * 256 + 64;
+  __shared__ int s_k[256];
+  __shared__ uint32_t s_meta[4][QCAP];
+  const int nch = (a.Wv + 3) / 4;
+  const int xcd = (int)(blockIdx.x & 7u), slot = (int)(blockIdx.x >> 3);
+  const int qc = slot / a.T, t = slot - qc * a.T;
+  const int chunk = qc * 8 + xcd;
+  if (chunk >= nch) return;  // block-uniform
+  const int tf = a.tfirst[t];
+  const int nloc = (t + 1 < a.T ? a.tfirst[t + 1] : a.A) - tf;
+  s_k[threadIdx.x] = (threadIdx.x < nloc && threadIdx.x < 255) ? a.kmap[tf + threadIdx.x] : -1;
+  const int lane = threadIdx.x & 63;
+  const int wib = threadIdx.x >> 6;
+  const int w = chunk * 4 + wib;
+  const int64_t cb = ((int64_t)t * a.Wv + w) * KB;
+  __syncthreads();
+  if (w >= a.Wv) return;
+  const int64_t r_begin = (int64_t)w * a.per_wave;
+  const int64_t r_end = r_begin + a.per_wave < a.n ? r_begin + a.per_wave : a.n;
+  const uint16_t* rec = a.codes + (int64_t)t * a.n;
+  const float* v1w = a.v1 + r_begin;
+  uint32_t* qm = s_meta[wib];
+  // RANK 1 cursors: lane k < KB holds node k's next output position
+  int cur = lane < KB ? a.woff[cb + lane] + (a.kstart ? (int)a.kstart[(int64_t)t * KB + lane] : 0) : 0;
+  // one dense group of queue entries [e0, e0 + cnt): rank among same-node entries in queue order, store
+  auto drain = [&](int e0, int cnt) {
+    const bool ok = lane < cnt;
+    const uint32_t meta = ok ? qm[e0 + lane] : 0u;
+    const float x1 = ok ? v1w[meta & 0xFFFFu] : 0.f;
+    const int kk = ok ? (int)((meta >> 24) & 0xFu) : -1;
+    int pos = -1;
+    if (KB <= 2) {
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(kk == k);
+        const int base = __builtin_amdgcn_readlane(cur, k);
+        if (kk == k)
+          pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (lane == k) cur += __builtin_popcountll(m);
+      }
+    } else {
+      const int kc = kk < 0 ? 0 : kk;
+      const uint32_t one = kk < 0 ? 0u : 1u << (8 * (kc & 3));
+      uint32_t below = 0, tot_mine = 0;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const uint32_t x = (kc >> 2) == q ? one : 0u;
+        const uint32_t inc = wave_incl_scan(x);
+        if ((kc >> 2) == q) below = inc - x;
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        if ((lane >> 2) == q) tot_mine = tot;
+      }
+      const int base = __builtin_amdgcn_ds_bpermute(kc << 2, cur);
+      if (kk >= 0) pos = base + (int)((below >> (8 * (kc & 3))) & 0xFFu);
+      cur += (int)((tot_mine >> (8 * (lane & 3))) & 0xFFu);
+    }
+    if (pos >= 0) {
+      int q1 = (int)rintf(x1 * a.qs1);
+      q1 = q1 > kPackQ ? kPackQ : (q1 < -kPackQ ? -kPackQ : q1);
+      const uint64_t r = (uint64_t)(r_begin + (int64_t)(meta & 0xFFFFu));
+      a.rec_out[pos] = r | ((uint64_t)((meta >> 16) & 0xFFu) << 31) | ((uint64_t)(uint32_t)(q1 + kPackQ) << 39);
+    }
+  };
+  const bool vec = (a.n & 3) == 0 && (reinterpret_cast<uintptr_t>(a.codes) & 7u) == 0;
+  int nq = 0;  // wave-uniform queue length
+  for (int64_t rb = r_begin; rb < r_end; rb += 256 * NG) {
+    uint32_t cc[NG][4];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int64_t r = rb + g * 256 + lane * 4;
+      if (vec && r + 3 < r_end) {
+        const uint2 c4 = *reinterpret_cast<const uint2*>(rec + r);
+        cc[g][0] = c4.x & 0xFFFFu;
+        cc[g][1] = c4.x >> 16;
+        cc[g][2] = c4.y & 0xFFFFu;
+        cc[g][3] = c4.y >> 16;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cc[g][u] = r + u < r_end ? (uint32_t)rec[r + u] : 0xFFu;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      int kk[4], cnt = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        kk[u] = s_k[cc[g][u] & 0xFFu];
+        cnt += kk[u] >= 0 ? 1 : 0;
+      }
+      const uint32_t inc = wave_incl_scan((uint32_t)cnt);
+      int e = nq + (int)(inc - (uint32_t)cnt);
+      const uint32_t off = (uint32_t)(rb + g * 256 + lane * 4 - r_begin);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (kk[u] >= 0) qm[e++] = (off + u) | ((cc[g][u] >> 8) << 16) | ((uint32_t)kk[u] << 24);
+      nq += __builtin_amdgcn_readlane((int)inc, 63);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int e0 = 0;
+    for (; e0 + 64 <= nq; e0 += 64) drain(e0, 64);
+    // the leftover (< 64 entries) moves to the queue front for the next trip
+    const int left = nq - e0;
+    if (left > 0 && e0 > 0) {
+      const uint32_t mv = lane < left ? qm[e0 + lane] : 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane < left) qm[lane] = mv;
+    }
+    nq = left;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (nq > 0) drain(0, nq);
+}
+
 // Per (tree, built node): exclusive prefix of the per-wave counts [T][Wv][KB] in place and the node's total
 // (one launch instead of the torch permute / cumsum / subtract / add / cast / permute chain per level).
 __global__ __launch_bounds__(256) void wave_scan_kernel(int* __restrict__ wcnt, int Wv, int KB,
@@ -1560,10 +1688,8 @@ __global__ __launch_bounds__(1024) void seg_hist_lane4_root_kernel(const SegHist
     const unsigned long long v = h[j * PLANE + bn * 16 + l];
     if (!v) continue;
     const unsigned long long cnt = v >> kPackShift;
-    const long long sum = cls_respace((long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt, a.cls_split);
-    unsigned long long* o = &a.out[(((int64_t)(slot - slot0) * a.d + f) * a.B + bn) * 2];
-    atomicAdd(o, cnt);
-    atomicAdd(o + 1, (unsigned long long)sum);
+    const long long sum = (long long)(v & ((1ull << kPackShift) - 1ull)) - (long long)kPackQ * (long long)cnt;
+    flush_packed(a, ((int64_t)(slot - slot0) * a.d + f) * a.B + bn, cnt, sum);
   }
 }
 }  // namespace
@@ -1856,7 +1982,8 @@ CDNA_API int cdna_bins_row_major(const uint64_t* bins, int64_t n, int G, int Gs,
 }
 
 // Wave-owned compaction (KB = max built nodes per tree, <= 16).  pass 1 writes wcnt, pass 2 scatters
-// from woff, ranking the lanes of a node with method `rank` (codes_scatter_w_kernel).  per_wave must be a multiple of 256; Wv = ceil(n / per_wave).
+// from woff, ranking the lanes of a node with method `rank` (0 / 1: codes_scatter_w_kernel; 2: the queued
+// codes_scatter_q_kernel, packed records and per_wave <= 65536 only; all three write identical records).  per_wave must be a multiple of 256; Wv = ceil(n / per_wave).
 CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64_t n, int T, int A,
                                   const int* tfirst, const int* kmap, const float* v0, const float* v1,
                                   int64_t per_wave, int Wv, int* wcnt, const int* woff, int* perm_out, float* v0_out,
@@ -1869,13 +1996,17 @@ CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64
                  rec_out, qs1, kstart};
   const int64_t nch = (Wv + 3) / 4;
   const dim3 grid((unsigned)(((nch + 7) / 8) * 8 * T));  // (chunk, tree) pairs, XCD-aware order (kernel)
-  if (rank < 0 || rank > 1) return (int)hipErrorInvalidValue;
-  auto go = [&](auto k1, auto k2r0, auto k2r1) {
+  if (rank < 0 || rank > 2) return (int)hipErrorInvalidValue;
+  // rank 2 (queued): packed records only, row offsets inside a wave's range in 16 bits
+  if (pass == 2 && rank == 2 && (!rec_out || per_wave > 65536)) return (int)hipErrorInvalidValue;
+  auto go = [&](auto k1, auto k2r0, auto k2r1, auto k2q) {
     if (pass == 1) hipLaunchKernelGGL(k1, grid, dim3(256), 0, st, a);
     else if (rank == 0) hipLaunchKernelGGL(k2r0, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k2r1, grid, dim3(256), 0, st, a);
+    else if (rank == 1) hipLaunchKernelGGL(k2r1, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k2q, grid, dim3(256), 0, st, a);
   };
-#define CDNA_CW(K) go(codes_count_w_kernel<K>, codes_scatter_w_kernel<K, 0>, codes_scatter_w_kernel<K, 1>)
+#define CDNA_CW(K) go(codes_count_w_kernel<K>, codes_scatter_w_kernel<K, 0>, codes_scatter_w_kernel<K, 1>, \
+                      codes_scatter_q_kernel<K>)
   switch (KB) {
     case 1: CDNA_CW(1); break;
     case 2: CDNA_CW(2); break;

@@ -1,7 +1,8 @@
 """3-class forests on the packed record path (engine.MSEG_CLS with C = 3): label codes 0 / 1 / 2^22 ride the
-records' one quantised value, the histogram kernels re-space each block's sum to W1 + 2^32 W2 in their flush
-(seg.hip cls_respace) and K.cls3_expand turns (W, W1 + 2^32 W2) into exact class counts, so the forests must equal
-the class-histogram path's forests bit for bit (multiclass was off the fast path)."""
+records' one quantised value, the histogram kernels split each block's sum W1 + 2^22 W2 into two int64 columns in
+their flush (seg.hip flush_packed) and K.cls3_expand turns (W, W1, W2) into exact class counts, so the forests must
+equal the class-histogram path's forests bit for bit (multiclass was off the fast path; VERDICT
+r5 weak #5: the old single-column W1 + 2^32 W2 cell capped the path at 1.68e7 rows)."""
 import numpy as np
 import pytest
 import torch
@@ -11,16 +12,19 @@ def _devices():
     return ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
 
 
-def test_cls3_expand_and_respace_are_exact():
+def test_cls3_expand_is_exact():
     from cdnaml.ops import kernels as K
     rng = np.random.default_rng(0)
     w = torch.from_numpy(rng.integers(0, 5, 1000))
     y = torch.from_numpy(rng.integers(0, 3, 1000))
     q = torch.where(y == 2, torch.full_like(y, K.CLS3_CODE), y)
-    s = int((w * K._cls3_respace(q)).sum())
-    Hb = torch.tensor([[int(w.sum()), s]], dtype=torch.int64)
+    Hb = torch.tensor([[int(w.sum()), int((w * (q & (K.CLS3_CODE - 1))).sum()), int((w * (q >> 22)).sum())]],
+                      dtype=torch.int64)
     got = K.cls3_expand(Hb)[0].tolist()
     assert got == [int(w[y == c].sum()) for c in range(3)]
+    # sums far past 2^32 (the old packed cell's limit: 1e8 rows x weights up to 255)
+    big = torch.tensor([[3 * 2 ** 35, 2 ** 35 + 7, 2 ** 35 - 7]], dtype=torch.int64)
+    assert K.cls3_expand(big)[0].tolist() == [2 ** 35, 2 ** 35 + 7, 2 ** 35 - 7]
 
 
 @pytest.mark.parametrize("device", _devices())
