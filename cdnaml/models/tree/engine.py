@@ -445,6 +445,13 @@ class ForestTrainer:
         f1 = min(d, f0 + dc)
         return (f0, f1), mine[: f1 - f0].permute(1, 0, 2, 3).contiguous()
 
+    def _rs_enter(self, st: "_FitState", rs_slice) -> None:
+        """A level was reduce-scattered by feature: the pass stays on this rank's feature slice, and the parents'
+        histograms (parent - sibling derivation) are cut to it."""
+        st.rs_on = True
+        if st.prev_hist is not None and st.prev_hist.shape[1] == self.data.d:
+            st.prev_hist = st.prev_hist[:, rs_slice[0]:rs_slice[1]].contiguous()
+
     def _k6_exact(self, st: "_FitState", lv: "_Level") -> bool:
         """The level histograms are exact in fp64: packed int64 sums (|q| <= 2^23 at a power-of-two scale, unit
         count scale) whose totals stay below 2^53 ulps (total weight < 2^30), assembled by exact differences."""
@@ -494,15 +501,22 @@ class ForestTrainer:
         return sel[:, :8].contiguous(), sel[:, 9:11].contiguous()
 
     # ------------------------------------------------------------ training
-    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev, cls3=False):
-        """Record histograms of a level's S slots in HIST_OVERLAP slot chunks; chunk c's all-reduce runs on the
-        collective stream while chunk c + 1 is built (one per-level RCCL all-reduce of 1-50 MB otherwise
+    def _hist_overlapped(self, data, d, B, rec, sb, S, wmax, scales, dev, cls3=False, rs=False):
+        """Record histograms of a level's S slots in HIST_OVERLAP slot chunks; chunk c's collective runs on the
+        collective stream while chunk c + 1 is built (one per-level RCCL collective of 1-50 MB otherwise
         serialises with the compute stream).  The sums are exact integers, so the result is identical to one
-        fused all-reduce."""
-        Hb = torch.zeros((S, d, B, K.hist_cols(cls3)), dtype=torch.int64, device=dev)
+        fused collective.
+
+        rs (reduce-scatter by feature, RS_MIN_BYTES levels): each chunk's feature-major copy is reduce-scattered
+        asynchronously instead of all-reduced, and the result is this rank's feature slice of all S slots --
+        ``(H [S, f1 - f0, B, k], (f0, f1))``, what ``_reduce_scatter_features`` returns for the whole level."""
+        kc = K.hist_cols(cls3)
+        Hb = torch.zeros((S, d, B, kc), dtype=torch.int64, device=dev)
         k = min(HIST_OVERLAP, S)
         bounds = np.linspace(0, S, k + 1).round().astype(np.int64)
         rm, s10 = data.record_rows() if dev.type == "cuda" else (None, False)
+        W, r = self.comm.world_size, self.comm.rank
+        dc = -(-d // W)
         pend = []
         for c in range(k):
             s0, s1 = int(bounds[c]), int(bounds[c + 1])
@@ -514,12 +528,30 @@ class ForestTrainer:
                 sbc[:, 2] -= s0
                 K.seg_hist(data.bins, d, B, rec, None, None, None, sbc, s1 - s0, wmax, scales, bins_rm=rm,
                            interleave=True, rec=True, raw=True, out=Hb[s0:s1], rm_s10=s10, cls3=cls3)
-            with _tr.span("tree.allreduce_async", cat="comm", bytes=(s1 - s0) * d * B * 16):
-                pend.append(self.comm.all_reduce_async(Hb[s0:s1]))
-        with _tr.span("tree.allreduce_wait", cat="comm"):
-            for h in pend:
-                h.wait()
-        return Hb
+            nbytes = (s1 - s0) * d * B * kc * 8
+            if rs:
+                Hp = torch.zeros((W * dc, s1 - s0, B, kc), dtype=torch.int64, device=dev)
+                Hp[:d] = Hb[s0:s1].permute(1, 0, 2, 3)
+                sp = _tr.begin("tree.reduce_scatter", cat="comm", bytes=nbytes // W, slots=s1 - s0)
+                pend.append((s0, s1, self.comm.reduce_scatter_async(Hp.view(W, -1)), sp))
+            else:
+                sp = _tr.begin("tree.allreduce_async", cat="comm", bytes=nbytes, slots=s1 - s0)
+                pend.append((s0, s1, self.comm.all_reduce_async(Hb[s0:s1]), sp))
+        if not rs:
+            with _tr.span("tree.allreduce_wait", cat="comm"):
+                for _, _, h, sp in pend:
+                    h.wait()
+                    _tr.end(sp)
+            return Hb
+        f0 = min(d, r * dc)
+        f1 = min(d, f0 + dc)
+        out = torch.empty((S, f1 - f0, B, kc), dtype=torch.int64, device=dev)
+        with _tr.span("tree.reduce_scatter_wait", cat="comm"):
+            for s0, s1, h, sp in pend:
+                mine = h.wait().view(dc, s1 - s0, B, kc)
+                _tr.end(sp)
+                out[s0:s1] = mine[: f1 - f0].permute(1, 0, 2, 3)
+        return out, (f0, f1)
 
     def train(self, num_trees: int, stats_rows: Dict[str, torch.Tensor], weights: Optional[torch.Tensor],
               forest: Optional[Forest] = None, codes_pre=None, margin=None) -> Forest:
@@ -842,13 +874,20 @@ class ForestTrainer:
                                                      rec_scale=st.mseg_scales[1] if st.rec_ok else None)
             is_rec = st.rec_ok and v1p is None
             sb = np.concatenate([sg, np.arange(S, dtype=np.int64)[:, None]], 1)
+            lv_bytes = S * d * B * K.hist_cols(st.cls3) * 8
             if is_rec and (self.comm.distributed or HIST_OVERLAP_FORCE) and HIST_OVERLAP > 1 and S >= 2 and \
-                    S * d * B * 16 >= HIST_OVERLAP_MIN_BYTES and not self._rs_level(S * d * B * 16, st.rs_on):
-                # (never once the pass reduce-scatters: the overlapped chunks are all-reduced over all
-                # features, while prev_hist then holds only this rank's feature slice)
-                # comm/compute overlap: the level's slots are built in chunks, each chunk's int64
-                # histogram all-reduced (async, RCCL stream) while the next chunk is built
-                lv.Hb = self._hist_overlapped(data, d, B, perm, sb, S, wmax, st.mseg_scales, dev, cls3=st.cls3)
+                    lv_bytes >= HIST_OVERLAP_MIN_BYTES:
+                # comm/compute overlap: the level's slots are built in chunks, each chunk's int64 histogram
+                # all-reduced -- or, on reduce-scatter levels, reduce-scattered by feature -- asynchronously on
+                # the RCCL stream while the next chunk is built
+                rs = self._rs_level(lv_bytes, st.rs_on)
+                res = self._hist_overlapped(data, d, B, perm, sb, S, wmax, st.mseg_scales, dev, cls3=st.cls3,
+                                            rs=rs)
+                if rs:
+                    lv.Hb, lv.rs_slice = res
+                    self._rs_enter(st, lv.rs_slice)
+                else:
+                    lv.Hb = res
                 lv.reduced = True
             else:
                 rm, s10 = (data.record_rows() if is_rec else (data.row_major_bins(), False)) \
@@ -895,14 +934,11 @@ class ForestTrainer:
     def _level_reduce(self, st: "_FitState", lv: "_Level") -> None:
         """The level histograms summed over ranks: one fused all-reduce, or (large int64 levels) a reduce-scatter
         by feature -- lv.rs_slice is then this rank's feature range and prev_hist is cut to it."""
-        lv.rs_slice = None
         if lv.reduced:
             return
         if self._rs_want(lv.Hb, st.rs_on):
-            st.rs_on = True
             lv.rs_slice, lv.Hb = self._reduce_scatter_features(lv.Hb, self.data.d)
-            if st.prev_hist is not None and st.prev_hist.shape[1] == self.data.d:
-                st.prev_hist = st.prev_hist[:, lv.rs_slice[0]:lv.rs_slice[1]].contiguous()
+            self._rs_enter(st, lv.rs_slice)
         else:
             with _tr.span("tree.allreduce", cat="comm", bytes=lv.Hb.numel() * 8):
                 self.comm.all_reduce(lv.Hb)  # one fused RCCL all-reduce per level
@@ -1211,6 +1247,8 @@ class _FitState:
 class _Level:
     """One level's tables (``_level_tables``), histograms (``_level_histogram`` / ``_level_reduce``) and host-side
     decisions (``_level_decide``)."""
+    rs_slice = None   # (f0, f1): this rank's feature range once the level was reduce-scattered by feature
+    reduced = False
 
 
 from ...ops import tune as _tune  # noqa: E402  (CDNAML_TUNE overrides of the constants above)

@@ -95,6 +95,23 @@ class _Pending:
         return self.t
 
 
+class _PendingRS:
+    """An in-flight reduce-scatter (Comm.reduce_scatter_async); ``wait()`` -> this rank's slice."""
+
+    def __init__(self, work, w, out, device, comm):
+        self.work, self.w, self.out, self.device, self.comm = work, w, out, device, comm
+
+    def wait(self) -> torch.Tensor:
+        if self.work is not None:
+            with self.comm._guard("reduce_scatter_wait"):
+                self.work.wait()
+            self.work = None
+            if self.out is None:  # gloo: the all-reduced host copy, sliced
+                self.out = self.w[self.comm.rank]
+            self.out = self.out.to(self.device)
+        return self.out
+
+
 class Comm:
     """Communicator bound to this process's device."""
 
@@ -257,6 +274,29 @@ class Comm:
         with self._guard("reduce_scatter"):
             dist.all_reduce(w)
         return w[self.rank].to(t.device)
+
+    def reduce_scatter_async(self, t: torch.Tensor) -> "_PendingRS":
+        """``reduce_scatter`` started on the collective stream; ``wait()`` returns this rank's slice.
+
+        RCCL: ``reduce_scatter_tensor(async_op=True)`` is enqueued behind the work already on the current stream, so
+        kernels launched afterwards (the next slot chunk's histogram) overlap it.  gloo: an async all-reduce of a
+        host copy, sliced on ``wait()`` (the same integer sums)."""
+        if not self.distributed:
+            return _PendingRS(None, None, t[0], None, self)
+        W = self.world_size
+        assert t.shape[0] == W
+        self.calls += 1
+        self.bytes_reduced += t.numel() * t.element_size() // W
+        if self.backend == "nccl":
+            w = self._dev_tensor(t).contiguous()
+            out = torch.empty(w.shape[1:], dtype=w.dtype, device=w.device)
+            with self._guard("reduce_scatter"):
+                work = dist.reduce_scatter_tensor(out, w, async_op=True)
+            return _PendingRS(work, w, out, t.device, self)
+        w = self._dev_tensor(t).contiguous().clone()
+        with self._guard("reduce_scatter"):
+            work = dist.all_reduce(w, async_op=True)
+        return _PendingRS(work, w, None, t.device, self)
 
     def all_gather_tensor(self, t: torch.Tensor) -> torch.Tensor:
         """Same-shape tensors of every rank stacked: [W, *t.shape]."""

@@ -129,6 +129,34 @@ def span(name: str, cat: str = "op", device: Optional[torch.device] = None, **ar
             _state["events"].append(s)
 
 
+def begin(name: str, cat: str = "op", **args) -> Optional[_Span]:
+    """Open a span that :func:`end` closes later -- an interval that does not nest in one ``with`` block (an async
+    collective from issue to wait, while other spans run).  None when tracing is off."""
+    if not _state["enabled"]:
+        return None
+    s = _Span()
+    s.name, s.cat, s.args = name, cat, args
+    s.tid = (threading.get_ident() & 0xFFFF) + 1   # its own track: it overlaps the spans of this thread
+    s.rank = _rank()
+    s.ev0 = s.ev1 = None
+    if torch.cuda.is_available():
+        s.ev0 = torch.cuda.Event(enable_timing=True)
+        s.ev1 = torch.cuda.Event(enable_timing=True)
+        s.ev0.record()
+    s.t_host0 = time.perf_counter()
+    return s
+
+
+def end(s: Optional[_Span]) -> None:
+    if s is None:
+        return
+    if s.ev1 is not None:
+        s.ev1.record()
+    s.t_host1 = time.perf_counter()
+    with _state["lock"]:
+        _state["events"].append(s)
+
+
 def traced(name: Optional[str] = None, cat: str = "op"):
     """Decorator form of :func:`span`."""
     def deco(fn):

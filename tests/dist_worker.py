@@ -167,13 +167,13 @@ def scenario_trees_rs(spark):
 
 
 def scenario_trees_rs_overlap(spark):
-    """Reduce-scatter by feature together with the chunked (overlapped) all-reduce, the overlap left enabled
-    (ADVICE r3): (a) overlap for the shallow levels, reduce-scatter from level 2 on; (b) reduce-scatter from
-    level 0 with an overlap threshold the deeper levels cross -- the overlapped branch must not run once a pass
-    reduce-scatters (its full-d sums would meet the rank's sliced parent histograms).  Both must give the 1-rank
-    forests bit for bit."""
+    """Reduce-scatter by feature COMPOSED with the chunked (overlapped) histograms: (a) overlap
+    with all-reduce for the shallow levels, reduce-scatter from level 2 on; (b) every level from 0 reduce-scatters
+    and the levels past the overlap threshold reduce-scatter chunk by chunk (async, while the next chunk builds,
+    the parents cut to the rank's feature slice); (c) every level overlapped + reduce-scattered, with the RF
+    headline shape scaled down and a depth-8 / 256-bin GBDT.  All must give the 1-rank forests bit for bit."""
     from cdnaml.models.tree import engine
-    seen = {"rs": 0, "ov": 0}
+    seen = {"rs": 0, "ov": 0, "ov_rs": 0}
     o_rs, o_ov = engine.ForestTrainer._reduce_scatter_features, engine.ForestTrainer._hist_overlapped
 
     def rs(self, *a):
@@ -182,6 +182,7 @@ def scenario_trees_rs_overlap(spark):
 
     def ov(self, *a, **k):
         seen["ov"] += 1
+        seen["ov_rs"] += int(bool(k.get("rs")))
         return o_ov(self, *a, **k)
     engine.ForestTrainer._reduce_scatter_features = rs
     engine.ForestTrainer._hist_overlapped = ov
@@ -190,11 +191,46 @@ def scenario_trees_rs_overlap(spark):
     out = {}
     for tag, rs_min, ov_min in (("a", 200000, 100000), ("b", 0, 300000)):
         engine.RS_MIN_BYTES, engine.HIST_OVERLAP_MIN_BYTES = rs_min, ov_min
-        seen.update(rs=0, ov=0)
+        seen.update(rs=0, ov=0, ov_rs=0)
         for k, v in _tree_digests(df).items():
             out[f"{tag}_{k}"] = v
         out[f"{tag}_levels"] = dict(seen)
+    from cdnaml.ml.regression import RandomForestRegressor
+    from cdnaml.ml.xgboost import XgboostRegressor
+    from cdnaml.utils.synthetic import forest_digest
+    engine.RS_MIN_BYTES, engine.HIST_OVERLAP_MIN_BYTES, engine.HIST_OVERLAP = 0, 0, 4
+    seen.update(rs=0, ov=0, ov_rs=0)
+    big = _tree_df(spark, n=6000, d=24, seed=5)
+    for k, est in (("rf", RandomForestRegressor(numTrees=20, maxDepth=5, maxBins=40, seed=42)),
+                   ("gbdt8", XgboostRegressor(n_estimators=3, max_depth=8, max_bin=256, learning_rate=0.3,
+                                              random_state=1))):
+        m = est.fit(big)
+        out[f"c_{k}"] = forest_digest(m._forest)
+    out["c_levels"] = dict(seen)
     return out
+
+
+def scenario_trace_rs_overlap(spark):
+    """A traced fit with every multi-slot level overlapped + reduce-scattered: count the tree.reduce_scatter
+    spans that are in flight when a later tree.hist_chunk span starts (Chrome trace written next to the result)."""
+    from cdnaml.ml.regression import RandomForestRegressor
+    from cdnaml.models.tree import engine
+    from cdnaml.utils import tracing
+    engine.RS_MIN_BYTES, engine.HIST_OVERLAP_MIN_BYTES, engine.HIST_OVERLAP = 0, 0, 4
+    df = _tree_df(spark, n=20000, d=24, seed=5)
+    RandomForestRegressor(numTrees=8, maxDepth=5, maxBins=40, seed=42).fit(df)   # warm-up
+    tracing.reset()
+    tracing.enable()
+    RandomForestRegressor(numTrees=8, maxDepth=5, maxBins=40, seed=42).fit(df)
+    tracing.disable()
+    path = os.path.abspath(f"rs_overlap_trace.rank{spark.comm.rank}.json")
+    tracing.export_chrome_trace(path)
+    with open(path) as f:
+        evs = json.load(f)["traceEvents"]
+    rs = [e for e in evs if e["name"] == "tree.reduce_scatter"]
+    ch = [e for e in evs if e["name"] == "tree.hist_chunk"]
+    overl = sum(1 for a in rs for c in ch if a["ts"] < c["ts"] < a["ts"] + a["dur"])
+    return {"rs_spans": len(rs), "chunk_spans": len(ch), "overlapping": overl, "trace": path}
 
 
 def scenario_trees_rs_nccl(spark):
@@ -223,9 +259,16 @@ def scenario_trees_rs_nccl(spark):
     chunks = [torch.full((j + 1, 2), float(r * 10 + j)) for j in range(W)]
     recv = comm.all_to_all_v(chunks)
     out["a2a_ok"] = bool(all(x.shape == (r + 1, 2) and bool((x == k * 10 + r).all()) for k, x in enumerate(recv)))
+    # the async reduce-scatter (the overlapped chunks of reduce-scatter levels)
+    hs = [comm.reduce_scatter_async(t * (j + 1)) for j in range(3)]
+    out["rs_async_ok"] = bool(all(torch.equal(h.wait(), want * (j + 1)) for j, h in enumerate(hs)))
     comm.barrier()
     res = scenario_trees_rs(spark)
     out.update(res)
+    from cdnaml.models.tree import engine
+    engine.HIST_OVERLAP, engine.HIST_OVERLAP_MIN_BYTES = 3, 0
+    ov = _tree_digests(_tree_df(spark, d=13))
+    out["overlap_same"] = bool(all(ov[k] == res[k] for k in ov))
     rec = comm.all_gather_object(dict(fake_nccl.RECORD))
     out["record_min"] = {k: min(x.get(k, 0) for x in rec) for k in rec[0]}
     out["violations"] = sorted(set(sum(comm.all_gather_object(list(fake_nccl.VIOLATIONS)), [])))
@@ -401,7 +444,7 @@ SCENARIOS = {"frame": scenario_frame, "ml": scenario_ml, "fault": scenario_fault
              "hyperopt": scenario_hyperopt,
              "ooc_uneven": scenario_ooc_uneven,
              "trees_rs_nccl": scenario_trees_rs_nccl,
-             "hyperopt_captured": scenario_hyperopt_captured}
+             "hyperopt_captured": scenario_hyperopt_captured, "trace_rs_overlap": scenario_trace_rs_overlap}
 
 
 def run(name):

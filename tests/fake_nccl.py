@@ -37,6 +37,16 @@ def _tensor_ok(op, *ts):
             _check(t.is_contiguous(), op, f"non-contiguous buffer {tuple(t.shape)} stride {t.stride()}")
 
 
+class _Done:
+    """A completed work handle (the proxy runs the gloo emulation of an async collective synchronously)."""
+
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
 class NcclOverGloo:
     """Proxy module: attribute access falls through to torch.distributed except for the overrides below."""
 
@@ -56,7 +66,7 @@ class NcclOverGloo:
         return _real.all_reduce(t, op=op, group=group, async_op=async_op)
 
     def reduce_scatter_tensor(self, out, inp, op=_real.ReduceOp.SUM, group=None, async_op=False):
-        RECORD["reduce_scatter_tensor"] += 1
+        RECORD["reduce_scatter_tensor_async" if async_op else "reduce_scatter_tensor"] += 1
         W = _real.get_world_size()
         _tensor_ok("reduce_scatter_tensor", out, inp)
         _check(out.dtype == inp.dtype, "reduce_scatter_tensor", f"dtype {out.dtype} vs {inp.dtype}")
@@ -67,7 +77,7 @@ class NcclOverGloo:
         _real.all_reduce(buf, op=op, group=group)
         r = _real.get_rank()
         out.copy_(buf.reshape(W, -1)[r].reshape(out.shape))
-        return None
+        return _Done() if async_op else None
 
     def all_gather_into_tensor(self, out, inp, group=None, async_op=False):
         RECORD["all_gather_into_tensor"] += 1

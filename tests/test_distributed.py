@@ -162,17 +162,28 @@ def test_reduce_scatter_by_feature_forests_identical(tmp_path):
 
 
 def test_reduce_scatter_with_overlap_enabled(tmp_path):
-    """with the chunked all-reduce overlap enabled and both thresholds crossed, the
-    reduce-scatter pass never meets full-d overlapped sums; forests equal the 1-rank fits at W = 2 and 4."""
+    """the chunked overlap composes with reduce-scatter by feature (each slot chunk's
+    histogram reduce-scattered asynchronously while the next builds, the parents cut to the rank's feature slice);
+    forests equal the 1-rank fits at W = 2, 4 and 8, with the RF headline shape scaled down and a depth-8 / 256-bin
+    GBDT overlapped + reduce-scattered at every level."""
     one = _run("trees_rs_overlap", tmp_path, 1)
-    for tag in ("a", "b"):
-        assert one.pop(f"{tag}_levels") == {"rs": 0, "ov": 0}
-    for w in (2, 4):
+    for tag in ("a", "b", "c"):
+        assert one.pop(f"{tag}_levels") == {"rs": 0, "ov": 0, "ov_rs": 0}
+    for w in (2, 4, 8):
         got = _run("trees_rs_overlap", tmp_path, w)
-        la, lb = got.pop("a_levels"), got.pop("b_levels")
-        assert la["ov"] > 0 and la["rs"] > 0, (w, la)   # overlap at the shallow levels, RS below
-        assert lb["rs"] > 0 and lb["ov"] == 0, (w, lb)  # RS from level 0: the overlap branch stays off
+        la, lb, lc = got.pop("a_levels"), got.pop("b_levels"), got.pop("c_levels")
+        assert la["ov"] > la["ov_rs"] > 0, (w, la)          # overlapped all-reduce at the shallow levels, RS below
+        assert lb["rs"] > 0 and lb["ov_rs"] > 0, (w, lb)    # RS from level 0, deeper levels overlapped RS
+        assert lc["ov"] == lc["ov_rs"] > 0, (w, lc)         # every multi-slot level overlapped + RS
         assert got == one, w
+
+
+def test_overlapped_reduce_scatter_trace(tmp_path):
+    """The Chrome trace of a 2-rank gloo fit shows each chunk's tree.reduce_scatter in flight while a later
+    tree.hist_chunk runs (the overlap is real, not serialised)."""
+    got = _run("trace_rs_overlap", tmp_path, 2)
+    assert got["rs_spans"] > 0 and got["chunk_spans"] > 0
+    assert got["overlapping"] > 0, got
 
 
 def test_ooc_fit_with_an_empty_shard(tmp_path):
@@ -196,10 +207,11 @@ def test_rccl_branches_through_recording_fake(tmp_path):
         got = _run("trees_rs_nccl", tmp_path, w)
         assert got.pop("backend") == "nccl"
         assert got.pop("violations") == [], w
-        for k in ("rs_ok", "rs_noncontig_ok", "ag_ok", "ar_async_ok", "a2a_ok"):
+        for k in ("rs_ok", "rs_noncontig_ok", "ag_ok", "ar_async_ok", "a2a_ok", "rs_async_ok", "overlap_same"):
             assert got.pop(k) is True, (w, k)
         rec = got.pop("record_min")
         assert rec.get("reduce_scatter_tensor", 0) > 0 and rec.get("all_gather_into_tensor", 0) > 0, (w, rec)
+        assert rec.get("reduce_scatter_tensor_async", 0) > 0, (w, rec)
         assert rec.get("barrier", 0) > 0, (w, rec)
         assert got.pop("rs_levels") > 0, w
         assert got == one, w
