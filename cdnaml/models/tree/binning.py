@@ -18,6 +18,8 @@ from ..util import IllegalArgumentException
 
 # binning queued on the quantile kernel's device thresholds, checked on the host behind it
 SPEC_THRESHOLDS = True
+# free device memory kept back when building the boosting partition's feature-major bins copy
+FM_HEADROOM = 4 << 30
 
 
 # ============================================================ binning (K3/K4)
@@ -43,12 +45,23 @@ class BinnedData:
             self.bins_rm = K.bins_row_major(self.bins)
         return self.bins_rm
 
-    def feature_major_bins(self) -> torch.Tensor:
-        """[G * 8, n] uint8: byte f * n + r is row r's bin of feature f (built once, kept for the fit's rounds)."""
+    def feature_major_bins(self) -> Optional[torch.Tensor]:
+        """[G * 8, n] uint8: byte f * n + r is row r's bin of feature f (built once, kept for the fit's rounds and
+        released by ``release_fit_copies`` when the boosting fit ends).  None when the device cannot hold the
+        second copy with FM_HEADROOM to spare (the partition then gathers from the [G][n] words: ADVICE r5, a
+        1e8 x 100 fit's copy is ~10 GB next to the bins and usually the row-major copy)."""
         if self.bins_fm is None:
             G, n, _ = self.bins.shape
+            if self.bins.is_cuda:
+                free, _ = torch.cuda.mem_get_info(self.bins.device)
+                if free < G * 8 * n + FM_HEADROOM:
+                    return None
             self.bins_fm = self.bins.permute(0, 2, 1).reshape(G * 8, n).contiguous()
         return self.bins_fm
+
+    def release_fit_copies(self) -> None:
+        """Drop the per-fit feature-major copy (the cached binned data outlives the fit: CV / tuning reuse it)."""
+        self.bins_fm = None
 
     def record_rows(self):
         """(rows, is_seg10) for the record histograms: the seg10 copy when binize wrote one, else the standard

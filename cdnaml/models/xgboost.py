@@ -236,6 +236,7 @@ class _XgbEstimatorBase(Estimator):
                     break
             ck.maybe_save(m + 1, forest, F, {"best": best, "best_round": best_round, "history": history})
         ck.finish()
+        data.release_fit_copies()
         return forest, history
 
     def _apply_l1(self, forest: Forest, t: int):

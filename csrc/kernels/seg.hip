@@ -1403,12 +1403,12 @@ __global__ __launch_bounds__(256) void codes_scatter_w_kernel(const CompactWArgs
 // a wave instruction costs the same whatever number of its lanes is active -- but at the headline's levels 2-4
 // only ~25 % of the (row, tree) slots belong to a built node: 3 of every 4 lanes of every scan, readlane,
 // bpermute and record instruction worked for nothing.  Here the wave first queues its built slots in LDS in row
-// order -- a lane reads 4 consecutive codes with one 8-byte load, counts its built ones, and one DPP scan of
-// those counts places them (row offset | weight << 16 | node << 24) -- and then drains the queue in DENSE groups
-// of 64 entries that gather their labels, run the RANK 1 node ranking (RANK 0 ballots for KB <= 2) and build +
-// store the records.  A group ranks in queue order, so the records and their positions are exactly RANK 0 / 1's
+// order -- a lane reads 4 consecutive codes (one 8-byte load) and their labels (one 16-byte load), counts its
+// built ones, and one DPP scan of those counts places them (row offset | weight << 16 | node << 24, and the
+// label) -- and then drains the queue in DENSE groups of 64 entries that run the RANK 1 node ranking (RANK 0
+// ballots for KB <= 2) and build + store the records.  A group ranks in queue order, so the records and their positions are exactly RANK 0 / 1's
 // (row order inside each (tree, node, wave) run).  Leftovers (< 64) carry to the next trip; the wave's last group
-// is partial.  A/B at the headline (profiles/r6/scatter_queue_ab.md).  LDS: 4 waves x 576 x 4 B = 9 KB per block.
+// is partial.  A/B at the headline (profiles/r6/scatter_queue_ab.md).  LDS: 4 waves x 576 x 8 B = 18 KB per block.
 template <int KB>
 __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs a) {
   constexpr int NW = KB > 4 ? KB / 4 : 1;
@@ -1416,6 +1416,7 @@ __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs
   constexpr int QCAP = NG * 256 + 64;
   __shared__ int s_k[256];
   __shared__ uint32_t s_meta[4][QCAP];
+  __shared__ float s_x1[4][QCAP];
   const int nch = (a.Wv + 3) / 4;
   const int xcd = (int)(blockIdx.x & 7u), slot = (int)(blockIdx.x >> 3);
   const int qc = slot / a.T, t = slot - qc * a.T;
@@ -1433,15 +1434,15 @@ __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs
   const int64_t r_begin = (int64_t)w * a.per_wave;
   const int64_t r_end = r_begin + a.per_wave < a.n ? r_begin + a.per_wave : a.n;
   const uint16_t* rec = a.codes + (int64_t)t * a.n;
-  const float* v1w = a.v1 + r_begin;
   uint32_t* qm = s_meta[wib];
+  float* qx = s_x1[wib];
   // RANK 1 cursors: lane k < KB holds node k's next output position
   int cur = lane < KB ? a.woff[cb + lane] + (a.kstart ? (int)a.kstart[(int64_t)t * KB + lane] : 0) : 0;
   // one dense group of queue entries [e0, e0 + cnt): rank among same-node entries in queue order, store
   auto drain = [&](int e0, int cnt) {
     const bool ok = lane < cnt;
     const uint32_t meta = ok ? qm[e0 + lane] : 0u;
-    const float x1 = ok ? v1w[meta & 0xFFFFu] : 0.f;
+    const float x1 = ok ? qx[e0 + lane] : 0.f;
     const int kk = ok ? (int)((meta >> 24) & 0xFu) : -1;
     int pos = -1;
     if (KB <= 2) {
@@ -1476,10 +1477,12 @@ __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs
       a.rec_out[pos] = r | ((uint64_t)((meta >> 16) & 0xFFu) << 31) | ((uint64_t)(uint32_t)(q1 + kPackQ) << 39);
     }
   };
-  const bool vec = (a.n & 3) == 0 && (reinterpret_cast<uintptr_t>(a.codes) & 7u) == 0;
+  const bool vec = (a.n & 3) == 0 && (reinterpret_cast<uintptr_t>(a.codes) & 7u) == 0 &&
+                   (reinterpret_cast<uintptr_t>(a.v1) & 15u) == 0;
   int nq = 0;  // wave-uniform queue length
   for (int64_t rb = r_begin; rb < r_end; rb += 256 * NG) {
     uint32_t cc[NG][4];
+    float xl[NG][4];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int64_t r = rb + g * 256 + lane * 4;
@@ -1489,9 +1492,17 @@ __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs
         cc[g][1] = c4.x >> 16;
         cc[g][2] = c4.y & 0xFFFFu;
         cc[g][3] = c4.y >> 16;
+        const float4 x4 = *reinterpret_cast<const float4*>(a.v1 + r);
+        xl[g][0] = x4.x;
+        xl[g][1] = x4.y;
+        xl[g][2] = x4.z;
+        xl[g][3] = x4.w;
       } else {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) cc[g][u] = r + u < r_end ? (uint32_t)rec[r + u] : 0xFFu;
+        for (int u = 0; u < 4; ++u) {
+          cc[g][u] = r + u < r_end ? (uint32_t)rec[r + u] : 0xFFu;
+          xl[g][u] = r + u < r_end ? a.v1[r + u] : 0.f;
+        }
       }
     }
 #pragma unroll
@@ -1507,7 +1518,10 @@ __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs
       const uint32_t off = (uint32_t)(rb + g * 256 + lane * 4 - r_begin);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (kk[u] >= 0) qm[e++] = (off + u) | ((cc[g][u] >> 8) << 16) | ((uint32_t)kk[u] << 24);
+        if (kk[u] >= 0) {
+          qm[e] = (off + u) | ((cc[g][u] >> 8) << 16) | ((uint32_t)kk[u] << 24);
+          qx[e++] = xl[g][u];
+        }
       nq += __builtin_amdgcn_readlane((int)inc, 63);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1518,9 +1532,13 @@ __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs
     const int left = nq - e0;
     if (left > 0 && e0 > 0) {
       const uint32_t mv = lane < left ? qm[e0 + lane] : 0u;
+      const float xv = lane < left ? qx[e0 + lane] : 0.f;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      if (lane < left) qm[lane] = mv;
+      if (lane < left) {
+        qm[lane] = mv;
+        qx[lane] = xv;
+      }
     }
     nq = left;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
