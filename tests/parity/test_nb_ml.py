@@ -34,7 +34,15 @@ def test_ml02_linear_regression_i(nb):
     pred = lr_model.transform(va.transform(test))
     ev = RegressionEvaluator(predictionCol="prediction", labelCol="price")
     rmse, r2 = ev.setMetricName("rmse").evaluate(pred), ev.setMetricName("r2").evaluate(pred)
-    assert rmse > 0 and r2 < 1.0
+    # the coefficients of ML 02:112-123 against an fp64 least-squares solve of the same design (Double vectors)
+    tr = train.select("bedrooms", "price").toPandas()
+    ref = np.linalg.lstsq(np.c_[tr.bedrooms.values, np.ones(len(tr))], tr.price.values, rcond=None)[0]
+    np.testing.assert_allclose([lr_model.coefficients[0], lr_model.intercept], ref, rtol=1e-9)
+    # RMSE / R^2 of the evaluator against the textbook formulas on the collected predictions
+    pp = pred.select("price", "prediction").toPandas()
+    e = pp.price.values - pp.prediction.values
+    np.testing.assert_allclose(rmse, np.sqrt(np.mean(e ** 2)), rtol=1e-12)
+    np.testing.assert_allclose(r2, 1 - np.sum(e ** 2) / np.sum((pp.price.values - pp.price.mean()) ** 2), rtol=1e-10)
 
 
 def test_ml03_linear_regression_ii(nb, tmp_path):
@@ -67,6 +75,13 @@ def test_ml03_linear_regression_ii(nb, tmp_path):
     rmodel = Pipeline(stages=[rf, LinearRegression(labelCol="price", featuresCol="features")]).fit(train)
     ev = RegressionEvaluator(labelCol="price", predictionCol="prediction", metricName="r2")
     assert ev.evaluate(rmodel.transform(test)) > 0
+    # ML 03:86-88 prints these coefficients: the one-hot design (cond ~1e6) against fp64 least squares
+    des = rmodel.stages[0].transform(train).select("features", "price").toPandas()
+    Xd = np.stack([np.asarray(v.toArray()) for v in des.features])
+    A = np.c_[Xd, np.ones(len(Xd))]
+    ref = np.linalg.lstsq(A, des.price.values, rcond=None)[0]
+    got = np.r_[rmodel.stages[-1].coefficients.toArray(), rmodel.stages[-1].intercept]
+    np.testing.assert_allclose(A @ got, A @ ref, rtol=0, atol=1e-7 * np.abs(des.price.values).max())
     lt = train.withColumn("log_price", log(col("price")))
     lrf = RFormula(formula="log_price ~ . - price", featuresCol="features", labelCol="log_price",
                    handleInvalid="skip")
@@ -132,7 +147,20 @@ def test_ml07_random_forest_cross_validation(nb, tmp_path):
     cvm = model.stages[-1]
     assert len(cvm.avgMetrics) == 4 and all(m > 0 for m in cvm.avgMetrics)
     best = cvm.bestModel
-    assert cvm.avgMetrics[int(np.argmin(cvm.avgMetrics))] == min(cvm.avgMetrics)
+    # the best model carries the argmin map's params (RMSE: smaller is better) and IS the refit of those params
+    # on the whole training set (ML 07:112: 4 maps x 3 folds + 1 refit)
+    k = int(np.argmin(cvm.avgMetrics))
+    bm = cvm.getEstimatorParamMaps()[k]
+    assert best.getOrDefault("maxDepth") == bm[rf.maxDepth] and best.getNumTrees == bm[rf.numTrees]
+    feats = Pipeline(stages=pipe.getStages()[:2]).fit(train).transform(train)
+    refit = rf.copy(bm).fit(feats)
+    from cdnaml.utils.synthetic import forest_digest
+    assert forest_digest(refit._forest) == forest_digest(best._forest)
+    # deeper / larger forests fit this table better: the grid's metrics are not all equal
+    assert max(cvm.avgMetrics) > min(cvm.avgMetrics)
+    # the same seed reproduces the fold metrics exactly
+    cv2 = CrossValidator(estimator=rf, evaluator=ev, estimatorParamMaps=grid, numFolds=3, seed=42, parallelism=2)
+    assert cv2.fit(feats).avgMetrics == cvm.avgMetrics
     assert len(best.featureImportances.toArray()) == len(idx + nums)
     path = str(tmp_path / "cv_pipeline")
     model.write().overwrite().save(path)
