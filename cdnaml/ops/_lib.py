@@ -102,7 +102,7 @@ _SIGS = {
     "cdna_gram": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int,
                    c_void_p], c_int),
     "cdna_binize": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,
-                     c_int, c_int64, c_int, c_void_p],
+                     c_int, c_int64, c_int, c_int, c_void_p],
                     c_int),
     "cdna_hist4": ([c_int, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,
@@ -188,7 +188,7 @@ _SIGS = {
     "cdna_heap_last_level": ([c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double,
                               c_double, c_void_p, c_int, c_int, c_void_p], c_int),
     "cdna_tree_predict_heap": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
-                                c_double, c_void_p, c_void_p, c_void_p], c_int),
+                                c_double, c_void_p, c_void_p, c_int, c_void_p], c_int),
     "cdna_predict_binned_add": ([c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p,
                                  c_void_p], c_int),
     "cdna_node_compact": ([c_int, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

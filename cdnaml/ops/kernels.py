@@ -364,7 +364,8 @@ def binize(X: torch.Tensor, thr: torch.Tensor, nthr: torch.Tensor, missing: Opti
         if n:
             rc = _lib.lib().cdna_binize(_ptr(X), n, d, X.stride(0), _ptr(thr), _ptr(nthr), tmax, int(miss_on),
                                         miss_val, optr, _ptr(rm) if rm is not None else None,
-                                        -10 if s10 else Gs, ldo, int(BINIZE_LUT), _stream(X.device))
+                                        -10 if s10 else Gs, ldo, int(BINIZE_LUT), int(BINIZE_RESIDENT),
+                                        _stream(X.device))
             if rc == 2:  # the fallback kernel ran: no row-major copy
                 rm = None
             else:
@@ -1044,6 +1045,15 @@ def ordered_tree_sum(contribs, T: int, n: int, K: int, base=None) -> torch.Tenso
     return out
 
 
+# persistent one-round grids (exactly the resident blocks) for the streaming kernels -- binize v5 and the heap
+# predict -- instead of fixed caps of 1024 / 8192 blocks (per-block setup and the uneven last trips are what made
+# them 8-9 % slower per row at the 8-GPU shard size: VERDICT r5 weak #2)
+# (A/B round 6, profiles/r6/headline_ab.md: one persistent round was 0.4 ms SLOWER at the headline and within noise
+# at the 8-GPU shard size, so both stay off)
+BINIZE_RESIDENT = False
+PREDICT_RESIDENT = False
+
+
 def tree_predict_heap(X: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: torch.Tensor,
                       masks: torch.Tensor, base: float = 0.0, dtype=torch.float64) -> Optional[torch.Tensor]:
     """Single-output ensemble prediction over a packed heap forest (int32 [T, 2^(depth+2)-2], ``pack_heap``):
@@ -1066,7 +1076,7 @@ def tree_predict_heap(X: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: t
     rc = _lib.lib().cdna_tree_predict_heap(_ptr(X), n, d, X.stride(0), _ptr(heap.contiguous()), depth,
                                            _ptr(tree_w.double().contiguous()), T, _ptr(m), float(base),
                                            None if f64 else _ptr(out), _ptr(out) if f64 else None,
-                                           _stream(X.device))
+                                           int(PREDICT_RESIDENT), _stream(X.device))
     if rc == 1:  # hipErrorInvalidValue: over the LDS budget
         return None
     _lib.check(rc, "cdna_tree_predict_heap")
@@ -1317,6 +1327,12 @@ def logistic_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b: float,
 
 # ------------------------------------------------------------ segment mode (seg.hip)
 SEG_HIST_CHUNK = 262144
+# lane10 record chunks (levels 2-4 of the headline): at most this many records per block.  The records of a slot
+# are in row order and the work list interleaves the slots by relative position, so smaller chunks keep the ~256
+# concurrently running blocks on a narrower row window (each row line is gathered by ~6.3 slots at the headline:
+# scripts/level_records.py); 16384 blocks per level measured -0.7 ms at 1e8 rows, and the per-rank shape keeps its
+# ~37K-record chunks (SEG_MIN_BLOCKS) -- profiles/r6/headline_ab.md
+LANE10_CHUNK_MAX = 40960
 # row-major bins copy for segment histograms (one cache line per row instead of one per 8-feature group)
 SEG_ROW_MAJOR = True
 SEG_PART_CHUNK = 8192
@@ -1546,7 +1562,12 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
             # the six-items-per-wave kernel spreads a block's items over three copies of every cell (item i of the
             # chunk -> copy i % 3): each copy's 20-bit count holds a third of the chunk
             cap = 3 * cap - 1024
-        chunk = _fill_chunk(segs, min(SEG_HIST_CHUNK * (3 if rm_s10 and LANE10_CHUNK3 else 1), cap), B,
+        top = SEG_HIST_CHUNK * (3 if rm_s10 and LANE10_CHUNK3 else 1)
+        if rm_s10 and int(segs[:, 1].sum()) > 2 * LANE10_CHUNK_MAX * SEG_MIN_BLOCKS:
+            # large levels only: the smaller levels of a shard keep _fill_chunk's round fitting (its chunks grow
+            # to drop a sliver round; capping them cost +0.25 ms at 1.25e7 rows)
+            top = min(top, LANE10_CHUNK_MAX)
+        chunk = _fill_chunk(segs, min(top, cap), B,
                             _num_cus(bins.device) if (SEG_ROUND_FIT and rm_s10 and bins.is_cuda) else 0)
         work = _seg_work(segs, chunk, interleave)
         if len(work) == 0:

@@ -156,4 +156,15 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / nx;
 }
 
+// Blocks that fit the device at once (one "round") for kernel k at this block size / dynamic LDS; 0 when the
+// occupancy query fails.  A persistent (grid-stride) launch of exactly this many blocks reads its per-block setup
+// (staged tables, LDS clears) once per resident block and has no partial last round.
+inline unsigned resident_blocks(const void* k, int threads, size_t lds) {
+  int dev = 0, ncu = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds) != hipSuccess || per_cu <= 0) return 0;
+  return (unsigned)(per_cu * ncu);
+}
+
 }  // namespace cdna

@@ -858,9 +858,10 @@ inline unsigned grid_for(int64_t n, int per, unsigned cap) {
 // ran instead (rm not written).
 // ldo: row stride of out's [G][ldo] word planes (0: n) -- chunks of a streamed fit bin into their row slice of
 // the full bins (out = base + row0, ldo = total rows; rm = row-major base + row0).
+// grid_mode 1: v5 launches exactly the resident blocks (one persistent round) instead of up to 1024.
 CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const float* thr, const int* nthr, int tmax,
                          int miss_on, float miss_val, uint64_t* out, uint64_t* rm, int Gs, int64_t ldo, int lut,
-                         hipStream_t st) {
+                         int grid_mode, hipStream_t st) {
   if (ldo <= 0) ldo = n;
   if (ldo < n) return (int)hipErrorInvalidValue;
   // Gs == -10: rm gets the seg10 row layout (d <= 100, 128-byte rows; binize v5 only, see store_rm)
@@ -886,7 +887,12 @@ CDNA_API int cdna_binize(const float* X, int64_t n, int d, int64_t ldx, const fl
         if (lds > 64 * 1024)
           (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds);
-        hipLaunchKernelGGL(kern, dim3(grid_for(n, 64 * rpl, 1024)), dim3(64 * G), lds, st, X, n, d, ldx, thr, nthr,
+        unsigned grid = grid_for(n, 64 * rpl, 1024);
+        if (grid_mode == 1) {
+          const unsigned res = cdna::resident_blocks(reinterpret_cast<const void*>(kern), 64 * G, lds);
+          if (res > 0 && res < grid) grid = res;
+        }
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * G), lds, st, X, n, d, ldx, thr, nthr,
                            tmax > 0 ? tmax : 1, miss_on, miss_val, out, rm, Gs, ldo);
       };
       auto by_steps = [&](auto c_tag) {
@@ -982,15 +988,22 @@ CDNA_API int cdna_predict_binned_add(const uint64_t* bins, int64_t n, const int4
 
 // heap forest [T][2^(depth+2) - 2] int32 words (predict_heap_kernel), single output; returns
 // hipErrorInvalidValue when it does not fit the LDS budget (the caller then uses cdna_tree_predict).
+// grid_mode 1: exactly the resident blocks (one persistent round: the heap is staged once per resident block and
+// every block walks the same number of 64-row tiles, +-1) instead of up to 8192 blocks.
 CDNA_API int cdna_tree_predict_heap(const float* X, int64_t n, int d, int64_t ldx, const int* heap, int depth,
                                     const double* tree_w, int T, const uint32_t* masks, double base, float* out,
-                                    double* out_d, hipStream_t st) {
+                                    double* out_d, int grid_mode, hipStream_t st) {
   if (n <= 0) return 0;
   if (depth < 0 || depth > 12) return (int)hipErrorInvalidValue;
   const size_t wt = ((size_t)4 << depth) - 2;
   const size_t lds = (size_t)T * wt * 4 + (size_t)((T + 1) & ~1) * 8 + (size_t)64 * (d + 1) * 4 + 256 * 8;
   if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(predict_heap_kernel, dim3(grid_for(n, 64, 8192)), dim3(256), lds, st, X, n, d, ldx, heap,
+  unsigned grid = grid_for(n, 64, 8192);
+  if (grid_mode == 1) {
+    const unsigned res = cdna::resident_blocks(reinterpret_cast<const void*>(predict_heap_kernel), 256, lds);
+    if (res > 0 && res < grid) grid = res;
+  }
+  hipLaunchKernelGGL(predict_heap_kernel, dim3(grid), dim3(256), lds, st, X, n, d, ldx, heap,
                      depth, tree_w, T, masks, base, out, out_d);
   return (int)hipGetLastError();
 }
