@@ -12,7 +12,7 @@ Each op dispatches on the device of its inputs:
 from __future__ import annotations
 
 import math
-from typing import Optional
+from typing import Dict, Optional
 
 import numpy as np
 import torch
@@ -1629,51 +1629,16 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
     if n == 0 or s1 <= s0:
         return out
     wm = int(max(1, min(255, wmax)))
-    # each LDS cell copy takes every third item of a wave's stream: rows x wmax / 3 (+ a partial trip per
-    # wave) stays below the 20-bit count field (the wide kernel has one copy: rows x wmax)
-    rows = max(64, min(n, (1 << 20) // (wm + 1) - 64 if wide else 3 * ((1 << 20) // (wm + 1)) - 16 * 64))
-    # CODES_HIST_BLOCKS > 0: shrink the row chunks toward that many blocks (>= 16k rows each).  Off by
-    # default: at the per-rank 1.25e7 shape 4096 blocks ran 21.0-21.3 ms per step vs 20.0-20.1 ms with the
-    # largest chunks (the per-block LDS clear + flush of 100 KB outweighs the emptier last round)
-    S_l = max(1, s1 - s0)
-    if CODES_HIST_BLOCKS > 0:
-        rows = max(min(rows, 16384), min(rows, -(-(n * S_l) // CODES_HIST_BLOCKS)))
-    rows = (rows + 63) // 64 * 64
-    C = (n + rows - 1) // rows
-    bpc = S_l * (-(-d // 64) if wide else 1)  # blocks per row chunk (the wide kernel: one per 64 features)
-    if codes.is_cuda:
-        # at least two rounds of blocks (one block per CU) while blocks keep >= 4096 rows: a boosting level of
-        # 1.25e7 rows in 524k-row chunks would run 48 blocks on 256 CUs
-        C_min = min(-(-2 * _num_cus(codes.device) // bpc), max(1, n // 4096))
-        if C < C_min:
-            C = C_min
-            rows = (-(-n // C) + 63) // 64 * 64
-            C = (n + rows - 1) // rows
-    if CODES_ROUND_FILL and C * bpc < 64 * _num_cus(codes.device):
-        # one block per CU: spread the rows over as many chunks as the rounds of blocks already needed can hold,
-        # so the last round is full instead of a fraction of the chip (1.25e7 rows x 20 trees: 640 blocks in 2.5
-        # rounds -> 760 in 2.97, 19.2 -> 18.9 ms per step; an exact multiple of the CUs, 1280 blocks in 5
-        # rounds, pays each block's 100 KB LDS clear + flush twice as often)
-        ncu = _num_cus(codes.device)
-        rounds = -(-(C * bpc) // ncu)
-        C2 = max(C, (rounds * ncu) // bpc)
-        if C2 > C:
-            rows = (-(-n // C2) + 63) // 64 * 64
-            C = (n + rows - 1) // rows
-    # XCD-aware order: block b runs on XCD b % 8; the slots (trees) of row chunk c are consecutive blocks of
-    # XCD c % 8, so their row-line gathers and label reads share that XCD's L2
-    nq = (C + 7) // 8
-    cq, sl, x = np.meshgrid(np.arange(nq), np.arange(s0, s1), np.arange(8), indexing="ij")  # (cq, slot, x) order
-    c = (cq * 8 + x).reshape(-1)
-    keep = c < C
-    c, sl = c[keep], sl.reshape(-1)[keep]
-    r0 = c * rows
-    work = np.stack([r0, np.minimum(rows, n - r0), sl], 1).astype(np.int32)
     sinfo = np.stack([st, sn], 1).astype(np.int32).reshape(-1)
     v1c = v1.float().contiguous()
+    key = (n, d, B, wm, s0, s1, wide, str(codes.device), CODES_HIST_BLOCKS, CODES_ROUND_FILL)
+    work = _ROOT_WORK.get(key)
+    if work is None:
+        work = _root_work(n, d, wide, wm, s0, s1, codes.device)
+        if len(_ROOT_WORK) > 64:
+            _ROOT_WORK.clear()
+        _ROOT_WORK[key] = work
     if wide:
-        # the kernel pairs the feature blocks of each item on one XCD itself: items in (chunk, slot) order
-        work = work[np.lexsort((work[:, 2], work[:, 0]))]
         wt, si = upload(codes.device, work.reshape(-1), sinfo)
         _lib.check(_lib.lib().cdna_seg_hist_root_wide(_ptr(bins_s10), n, d, B, bins_s10.shape[1] * 8, _ptr(codes),
                                                       _ptr(v1c), float(qs1), _ptr(wt), len(work), _ptr(si), s0,
@@ -1690,6 +1655,60 @@ def seg_hist_codes(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, 
                                              _stream(codes.device)),
                "cdna_seg_hist_root")
     return out
+
+
+# (shape, slot range, device) -> the root / codes histogram work list: the same for every fit of a shard, so its
+# host planning (~100 us of numpy per level, on the critical path between a level's decisions and the next level's
+# first launch at the per-rank shape) runs once
+_ROOT_WORK: Dict[tuple, np.ndarray] = {}
+
+
+def _root_work(n: int, d: int, wide: bool, wm: int, s0: int, s1: int, device) -> np.ndarray:
+    """Work items [m, 3] {row start, rows, slot} of a codes histogram over slots [s0, s1) (see seg_hist_codes)."""
+    # each LDS cell copy takes every third item of a wave's stream: rows x wmax / 3 (+ a partial trip per
+    # wave) stays below the 20-bit count field (the wide kernel has one copy: rows x wmax)
+    rows = max(64, min(n, (1 << 20) // (wm + 1) - 64 if wide else 3 * ((1 << 20) // (wm + 1)) - 16 * 64))
+    # CODES_HIST_BLOCKS > 0: shrink the row chunks toward that many blocks (>= 16k rows each).  Off by
+    # default: at the per-rank 1.25e7 shape 4096 blocks ran 21.0-21.3 ms per step vs 20.0-20.1 ms with the
+    # largest chunks (the per-block LDS clear + flush of 100 KB outweighs the emptier last round)
+    S_l = max(1, s1 - s0)
+    if CODES_HIST_BLOCKS > 0:
+        rows = max(min(rows, 16384), min(rows, -(-(n * S_l) // CODES_HIST_BLOCKS)))
+    rows = (rows + 63) // 64 * 64
+    C = (n + rows - 1) // rows
+    bpc = S_l * (-(-d // 64) if wide else 1)  # blocks per row chunk (the wide kernel: one per 64 features)
+    if device.type == "cuda":
+        # at least two rounds of blocks (one block per CU) while blocks keep >= 4096 rows: a boosting level of
+        # 1.25e7 rows in 524k-row chunks would run 48 blocks on 256 CUs
+        C_min = min(-(-2 * _num_cus(device) // bpc), max(1, n // 4096))
+        if C < C_min:
+            C = C_min
+            rows = (-(-n // C) + 63) // 64 * 64
+            C = (n + rows - 1) // rows
+    if CODES_ROUND_FILL and C * bpc < 64 * _num_cus(device):
+        # one block per CU: spread the rows over as many chunks as the rounds of blocks already needed can hold,
+        # so the last round is full instead of a fraction of the chip (1.25e7 rows x 20 trees: 640 blocks in 2.5
+        # rounds -> 760 in 2.97, 19.2 -> 18.9 ms per step; an exact multiple of the CUs, 1280 blocks in 5
+        # rounds, pays each block's 100 KB LDS clear + flush twice as often)
+        ncu = _num_cus(device)
+        rounds = -(-(C * bpc) // ncu)
+        C2 = max(C, (rounds * ncu) // bpc)
+        if C2 > C:
+            rows = (-(-n // C2) + 63) // 64 * 64
+            C = (n + rows - 1) // rows
+    # XCD-aware order: block b runs on XCD b % 8; the slots (trees) of row chunk c are consecutive blocks of
+    # XCD c % 8, so their row-line gathers and label reads share that XCD's L2
+    nq = (C + 7) // 8
+    cq, sl, x = np.meshgrid(np.arange(nq), np.arange(s0, s1), np.arange(8), indexing="ij")  # (cq, slot, x) order
+    c = (cq * 8 + x).reshape(-1)
+    keep = c < C
+    c, sl = c[keep], sl.reshape(-1)[keep]
+    r0 = c * rows
+    work = np.stack([r0, np.minimum(rows, n - r0), sl], 1).astype(np.int32)
+    if wide:
+        # the kernel pairs the feature blocks of each item on one XCD itself: items in (chunk, slot) order
+        work = work[np.lexsort((work[:, 2], work[:, 0]))]
+    return work
 
 
 def seg_hist_root(bins_s10: torch.Tensor, d: int, B: int, codes: torch.Tensor, v1: torch.Tensor, qs1: float,
