@@ -2015,6 +2015,9 @@ SCATTER_SCAN_MIN_KB = 4
 # A/B (round 5): 512 / 1024 / 2048 -> 17.7 / 17.6 / 17.5-17.6 ms at the per-rank shape, 131.2-131.5 vs 129.7-129.8
 # ms at the headline for 512 vs 2048
 COMPACT_WAVES = 2048
+# rows per wave at least (a multiple of 256): small shards keep fewer, longer waves (the per-block node table and
+# the per-wave count flush are fixed costs; the queued scatter carries its queue across the wave's trips)
+COMPACT_MIN_PER_WAVE = 256
 
 
 # queued scatter (seg.hip codes_scatter_q_kernel, rank 2): the built row slots queued per wave in LDS and ranked /
@@ -2041,7 +2044,7 @@ def _codes_compact_w(codes, tf_h, bs, tree_of, built, nb_t, kb_need, S, v0, v1, 
     first_slot[1:] = np.cumsum(nb_t)[:-1]
     kmap[built] = bs[built] - first_slot[tree_of[built]]
     assert np.all(kmap[built] >= 0) and np.all(kmap[built] < KB)
-    per_wave = max(256, -(-n // (COMPACT_WAVES * 256)) * 256)
+    per_wave = max(COMPACT_MIN_PER_WAVE, -(-n // (COMPACT_WAVES * 256)) * 256)
     Wv = -(-n // per_wave)
     L = _lib.lib()
     tf, kmap_t = upload(dev, tf_h, kmap)
