@@ -567,7 +567,9 @@ __global__ __launch_bounds__(1024) void seg_hist_lane10_kernel(const SegHistArgs
   const uint64_t* __restrict__ recp = a.rec + start + item;
   // U = 16 items per lane per trip (160 atomics): the trip's record load and gather latencies are exposed
   // once per trip, so the other 15 waves of the CU need ~15 x 160 ds_add_u64 of work to cover them (U = 8:
-  // 13.7 ms per level; a two-set software pipeline did not survive the compiler's loop rotation)
+  // 13.7 ms per level; a two-set software pipeline did not survive the compiler's loop rotation; round 6: the
+  // NEXT trip's records prefetched during this trip's atomics, which fits 128 VGPRs only at U = 12 / 8, measured
+  // 127.0-127.5 / 128.0-128.3 vs 126.3-126.7 ms per headline step -- the gathers in flight per trip matter more)
   for (int i0 = wid * IPW * U; i0 < len; i0 += NW * IPW * U) {
     uint64_t rc[U];
 #pragma unroll
