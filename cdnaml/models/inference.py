@@ -50,6 +50,7 @@ class ForestPredictor:
         self._seen: Dict[tuple, int] = {}
         self.replays = 0
         self.captures = 0
+        self.binned = 0   # calls served from the training tensor's bins (forest.FitBins)
 
     def _arrays(self, dev):
         key = str(dev)
@@ -85,9 +86,31 @@ class ForestPredictor:
         nodes, roots, vals, masks = self.forest.device_arrays(X.device, self.kind)
         return K.tree_predict(X, nodes, roots, tw, vals, masks, self.forest.K, b).to(dtype)
 
+    def _launch_binned(self, X: torch.Tensor, dtype) -> Optional[torch.Tensor]:
+        """The forest's training tensor itself (forest.FitBins): predict from the fit's uint8 bins -- the same
+        branches and fp64 sums as the fp32 path (K.tree_predict_heap_binned), a quarter of the bytes."""
+        fb = getattr(self.forest, "_fit_bins", None)
+        if fb is None or self.kind != "value" or not X.is_cuda or not fb.matches(X):
+            return None
+        from ..ops import kernels as K
+        tw, heap, _ = self._arrays(X.device)
+        if heap is None or fb.bins.device != X.device:
+            return None
+        b0 = 0.0 if self.base is None else float(np.asarray(self.base, np.float64).reshape(-1)[0])
+        out = K.tree_predict_heap_binned(fb.bins, fb.thr_up, fb.d, heap[0], heap[1], tw, b0, dtype=dtype)
+        if out is not None:
+            fb.hits += 1
+            self.binned += 1
+            fb.release()          # one transform per fit: the memory goes back to the next fit
+            self.forest.settle()  # the trainer's deferred node lists, while the GPU predicts
+        return out
+
     def __call__(self, X: torch.Tensor, dtype=torch.float64) -> torch.Tensor:
         """[n, d] features -> [n, K] predictions (a fresh tensor the caller owns): fp64 leaf values, weights and
         sums in one fixed tree order (K.ordered_tree_sum), stored as ``dtype``."""
+        out = self._launch_binned(X, dtype)  # one launch: never graph-captured (a replay cannot re-check X)
+        if out is not None:
+            return out
         if not (GRAPH_PREDICT and X.is_cuda and X.shape[0] >= GRAPH_MIN_ROWS and X.is_contiguous()):
             return self._launch(X, dtype)
         if threading.current_thread() is not threading.main_thread():

@@ -12,6 +12,7 @@ Tree regressors delegate to :mod:`cdnaml.models.tree.engine`.
 from __future__ import annotations
 
 import math
+import weakref
 import zlib
 from typing import Optional
 
@@ -27,7 +28,8 @@ from .linalg import DenseVector, SparseVector
 from .param import NO_DEFAULT, TypeConverters as TC, keyword_init
 from .tree.binning import make_binned
 from .tree.engine import ForestTrainer, TreeParams
-from .tree.forest import Forest
+from .tree import forest as _forest_mod
+from .tree.forest import FitBins, Forest
 from .util import (IllegalArgumentException, categorical_info, global_count, global_offset, gram_fp64_auto,
                    local_batch, local_xyw, require_vector, streamed_columns)
 
@@ -613,7 +615,17 @@ def tree_fit_prepare(est, dataset, classification: bool, pre=None):
         seed = _default_seed(type(est))
     late = pre(n, off, seed, X.device, y) if pre is not None else None
     data = make_binned(session, X, cat, est.getMaxBins(), seed, off, n_global, before_binize=late)
+    data.source_ref = weakref.ref(fcol.values) if src is None else None
     return session, data, y, w, seed, fmeta
+
+
+def attach_fit_bins(forest: Forest, data) -> None:
+    """Give a single-output forest the bins of its training tensor (``FitBins``): a transform of that same,
+    unmodified tensor then predicts from the bins (REUSE_FIT_BINS; numeric features only)."""
+    src = data.source_ref() if data.source_ref is not None else None
+    if (_forest_mod.REUSE_FIT_BINS and src is not None and src.is_cuda and forest.K == 1 and not data.categorical
+            and not data.missing_bin and data.bins is not None and data.bins.is_cuda):
+        forest._fit_bins = FitBins(src, data.bins, data.thresholds, data.nthr, data.d, data.B)
 
 
 def _num_classes(session, y: torch.Tensor, meta_label: Optional[dict]) -> int:
@@ -805,6 +817,7 @@ def _train_forest_regression(est, dataset, num_trees, subset, bootstrap, rate, i
         weights = _combine_weights(weights, w, num_trees)
     trainer = ForestTrainer(session, data, p)
     forest = trainer.train(num_trees, {"v0": None, "v1": early.get("yf", y.float())}, weights)
+    attach_fit_bins(forest, data)
     return forest, data.d
 
 
@@ -914,6 +927,7 @@ def _train_rf_reg(est, dataset, T_):
         bc = None
     forest = ForestTrainer(session, data, p).train(T_, {"v0": None, "v1": early.get("yf", y.float())}, weights,
                                                    codes_pre=bc)
+    attach_fit_bins(forest, data)
     return forest, data.d
 
 

@@ -39,6 +39,7 @@ class BinnedData:
     bins_rm: Optional[torch.Tensor] = None  # lazily built row-major copy [n, G, 8] (segment-mode histograms)
     bins_s10: Optional[torch.Tensor] = None  # seg10 row layout [n, 16, 8] written by binize (K.bins_seg10)
     bins_fm: Optional[torch.Tensor] = None   # lazily built feature-major byte copy [G * 8, n] (boosting partitions)
+    source_ref: Optional[object] = None      # weakref to the frame's feature tensor of the latest fit (FitBins)
 
     def row_major_bins(self) -> torch.Tensor:
         if self.bins_rm is None:

@@ -1083,6 +1083,80 @@ def tree_predict_heap(X: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: t
     return out
 
 
+def bin_upper_edges(thresholds: np.ndarray, nthr: np.ndarray, B: int) -> np.ndarray:
+    """[d, B] fp32: feature f's bin b -> the fp32 threshold t_b the bins were cut with (binize: bin(x) = #{t_j <
+    x}), +inf for b >= nthr[f] (the last bin and NaN).  ``tree_predict_heap_binned``'s dequantisation table."""
+    d = thresholds.shape[0]
+    up = np.full((d, B), np.inf, dtype=np.float32)
+    for f in range(d):
+        k = int(min(max(nthr[f], 0), B, thresholds.shape[1]))
+        up[f, :k] = thresholds[f, :k].astype(np.float32)
+    return up
+
+
+def heap_predict_host(Xf: torch.Tensor, heap: torch.Tensor, depth: int, tree_w: torch.Tensor,
+                      base: float = 0.0) -> torch.Tensor:
+    """Host walk of a packed predict heap (numeric and pass-through slots) on fp32 rows -> [n] fp64, summed in the
+    device kernels' order (``ordered_tree_sum``): the cpu twin of ``tree_predict_heap`` and, on dequantised bins
+    (``bin_upper_edges``), of ``tree_predict_heap_binned``."""
+    Xf = Xf.float().cpu()
+    h = heap.cpu()
+    n, T = Xf.shape[0], h.shape[0]
+    NI = (1 << depth) - 1
+    tw = tree_w.double().cpu()
+    rows = torch.arange(n)
+
+    def contrib(t):
+        slots = h[t, :2 * NI].reshape(max(NI, 0), 2)
+        leaf = h[t, 2 * NI:].contiguous().view(torch.float64)
+        idx = torch.zeros(n, dtype=torch.long)
+        for _ in range(depth):
+            nd = slots[idx]
+            f = nd[:, 0].long()
+            if bool((f < -1).any()):
+                raise ValueError("heap_predict_host: categorical slots are not supported")
+            thr = nd[:, 1].contiguous().view(torch.float32)
+            x = Xf[rows, f.clamp(min=0)]
+            go_left = (f < 0) | (x <= thr)
+            idx = 2 * idx + torch.where(go_left, 1, 2)
+        return (tw[t] * leaf[idx - NI])[:, None]
+    out = ordered_tree_sum(contrib, T, n, 1, torch.tensor([float(base)], dtype=torch.float64))
+    return out[:, 0]
+
+
+def tree_predict_heap_binned(bins: torch.Tensor, thr_up: torch.Tensor, d: int, heap: torch.Tensor, depth: int,
+                             tree_w: torch.Tensor, base: float = 0.0, dtype=torch.float64) -> Optional[torch.Tensor]:
+    """``tree_predict_heap`` over the uint8 bins the features were cut into (trees.hip predict_heap_binned_kernel):
+    bins [G, n, 8] (binize's column groups), thr_up fp32 [d, B] (``bin_upper_edges``).  x <= v <=> t_bin(x) <= v
+    for every threshold v of the binning, so the predictions equal ``tree_predict_heap`` on the fp32 rows bit for
+    bit.  [n, 1] ``dtype``; None when over the kernel's LDS budget.  Numeric / pass-through heap slots only."""
+    G, n, _ = bins.shape
+    T = heap.shape[0]
+    assert heap.dtype == torch.int32 and heap.dim() == 2 and heap.shape[1] == (4 << depth) - 2, \
+        (tuple(heap.shape), depth)
+    assert thr_up.dtype == torch.float32 and thr_up.dim() == 2 and thr_up.shape[0] == d and d <= 8 * G
+    assert tree_w.numel() == T
+    if not _native(bins):
+        b = bins_to_matrix(bins, d).cpu().clamp(max=thr_up.shape[1] - 1)
+        Xq = thr_up.cpu().gather(1, b.t().contiguous()).t()   # [n, d]: each bin's upper edge
+        return heap_predict_host(Xq, heap, depth, tree_w, base).to(dtype)[:, None].to(bins.device)
+    out = torch.empty((n, 1), dtype=dtype, device=bins.device)
+    if n == 0:
+        return out
+    f64 = dtype == torch.float64
+    heap = heap.contiguous()
+    heap_b = torch.empty_like(heap)  # the slots as bin counts (trees.hip heap_to_bins_kernel)
+    rc = _lib.lib().cdna_tree_predict_heap_binned(_ptr(bins.contiguous()), n, G, d, _ptr(thr_up.contiguous()),
+                                                  thr_up.shape[1], _ptr(heap), depth,
+                                                  _ptr(tree_w.double().contiguous()), T, float(base), _ptr(heap_b),
+                                                  None if f64 else _ptr(out), _ptr(out) if f64 else None,
+                                                  _stream(bins.device))
+    if rc == 1:
+        return None
+    _lib.check(rc, "cdna_tree_predict_heap_binned")
+    return out
+
+
 def tree_predict(X: torch.Tensor, nodes: torch.Tensor, roots: torch.Tensor, tree_w: torch.Tensor,
                  values: torch.Tensor, masks: torch.Tensor, K: int, base: Optional[torch.Tensor] = None
                  ) -> torch.Tensor:

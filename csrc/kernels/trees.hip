@@ -815,6 +815,148 @@ __global__ __launch_bounds__(256) void predict_heap_kernel(const float* __restri
   }
 }
 
+// K8 over the training matrix's own bins: a transform of the very feature tensor a regression forest was fit on
+// (models/inference.py ForestPredictor, forest.FitBins) reads the fit's uint8 bins -- 8 bytes per 8 features --
+// instead of the fp32 rows.  bins [G][n] u64 words (binize: byte j of word g = feature 8 g + j's bin), thr_up
+// [d][Bup] fp32: feature f's bin b -> t_b, the b-th sorted threshold the bins were cut with (+inf for b >= nthr).
+// For a threshold v of feature f (every numeric heap slot holds one):  x <= v  <=>  t_bin(x) <= v.  bin(x) =
+// #{t_j < x}, so t_bin(x) is the first threshold >= x: x <= t_bin(x) <= v gives x <= v; x <= v = t_b gives
+// bin(x) <= b, so t_bin(x) <= t_b; NaN and x > t_last take bin nthr -> +inf and go right, as NaN <= v and x <= v
+// are false.  t_b is non-decreasing in b, so t_bin(x) <= v  <=>  bin(x) < k(f, v) = #{b : t_b <= v}:
+// heap_to_bins_kernel rewrites every numeric slot's threshold bits as that count once per call, and the walk
+// compares bytes -- the same branches as predict_heap_kernel on X, the fp64 sums in its order: bit-identical
+// predictions.  Categorical slots are not handled (the host keeps forests with categorical features on the fp32
+// path).  (A first version looked t_bin up in an LDS table at every step -- a third dependent LDS read per step:
+// 8.94 vs 7.88 ms for the fp32 kernel at 1e8 x 100.)
+__global__ __launch_bounds__(256) void heap_to_bins_kernel(const int* __restrict__ heap, int T, int depth,
+                                                           const float* __restrict__ thr_up, int Bup, int d,
+                                                           int* __restrict__ heap_b) {
+  const int NI = (1 << depth) - 1, Wt = 4 * NI + 2;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < T * Wt; i += gridDim.x * 256) {
+    const int w = i % Wt;
+    int v = heap[i];
+    if (w < 2 * NI && (w & 1)) {
+      const int f = heap[i - 1];
+      if (f >= 0 && f < d) {
+        const float t = __int_as_float(v);
+        const float* row = thr_up + (size_t)f * Bup;
+        int lo = 0, hi = Bup;  // first b with row[b] > t (row non-decreasing, +inf padded)
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (row[mid] <= t) lo = mid + 1; else hi = mid;
+        }
+        v = lo;
+      }
+    }
+    heap_b[i] = v;
+  }
+}
+
+// Tile: 64 rows x G words staged in LDS at an odd dword pitch (conflict-free word writes; the walk's byte reads
+// are row per lane), the next tile's words in registers while this tile walks.  heap: heap_to_bins_kernel's.
+__global__ __launch_bounds__(256) void predict_heap_binned_kernel(const uint64_t* __restrict__ bins, int64_t n, int G,
+                                                                  int d, const int* __restrict__ heap, int depth,
+                                                                  const double* __restrict__ tree_w, int T,
+                                                                  double base, float* __restrict__ out,
+                                                                  double* __restrict__ out_d) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int NI = (1 << depth) - 1;
+  const int Wt = 4 * NI + 2;
+  int* sheap = reinterpret_cast<int*>(sm);
+  double* stw = reinterpret_cast<double*>(sm + (size_t)T * Wt);
+  const int pw = 2 * G + 1;                                                        // dwords per staged row
+  uint32_t* sb = reinterpret_cast<uint32_t*>(stw + ((T + 1) & ~1));               // [64][pw]
+  double* part = reinterpret_cast<double*>(sb + ((64 * pw + 1) & ~1));
+  for (int i = threadIdx.x; i < T * Wt; i += 256) sheap[i] = heap[i];
+  for (int i = threadIdx.x; i < T; i += 256) stw[i] = tree_w[i];
+  const int tl = threadIdx.x >> 6, row = threadIdx.x & 63;
+  constexpr int kPre = 4;  // G <= 16 (d <= 128): 64 G words per tile = at most 4 per thread
+  uint64_t pre[kPre];
+  const int nw = 64 * G;
+  const bool use_pre = nw <= kPre * 256;
+  const int64_t stride = (int64_t)gridDim.x * 64;
+  auto fetch = [&](int64_t r0) {
+    if (r0 >= n) return;
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int i = threadIdx.x + k * 256;
+      const int64_t r = r0 + (i & 63);
+      if (i < nw) pre[k] = r < n ? bins[(int64_t)(i >> 6) * n + r] : 0ull;
+    }
+  };
+  if (use_pre) fetch((int64_t)blockIdx.x * 64);
+  for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < n; r0 += stride) {
+    const int rows = (int)((n - r0) < 64 ? (n - r0) : 64);
+    __syncthreads();
+    if (use_pre) {
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < nw) {
+          uint32_t* dst = sb + (i & 63) * pw + 2 * (i >> 6);
+          dst[0] = (uint32_t)pre[k];
+          dst[1] = (uint32_t)(pre[k] >> 32);
+        }
+      }
+    } else {
+      for (int i = threadIdx.x; i < nw; i += 256) {
+        const int64_t r = r0 + (i & 63);
+        const uint64_t w = r < n ? bins[(int64_t)(i >> 6) * n + r] : 0ull;
+        uint32_t* dst = sb + (i & 63) * pw + 2 * (i >> 6);
+        dst[0] = (uint32_t)w;
+        dst[1] = (uint32_t)(w >> 32);
+      }
+    }
+    __syncthreads();
+    if (use_pre) fetch(r0 + stride);
+    double acc = 0.0;
+    if (row < rows) {
+      const uint8_t* xr = reinterpret_cast<const uint8_t*>(sb + row * pw);
+      constexpr int W = 8;
+      for (int tb = tl; tb < T; tb += 4 * W) {
+        int idx[W];
+#pragma unroll
+        for (int u = 0; u < W; ++u) idx[u] = 0;
+        for (int s = 0; s < depth; ++s) {
+#pragma unroll
+          for (int u = 0; u < W; ++u) {
+            const int t = tb + 4 * u;
+            if (t >= T) continue;
+            if (!CDNA_DCHECK(idx[u] < NI, 0x7E11u)) idx[u] = 0;
+            const int2 nd = *reinterpret_cast<const int2*>(sheap + t * Wt + 2 * idx[u]);
+            if (nd.x >= 0 && !CDNA_DCHECK(nd.x < d, 0x7E12u)) continue;
+            // numeric: left iff bin < k; pass-through (-1): left
+            idx[u] = 2 * idx[u] + ((nd.x < 0 || (int)xr[nd.x] < nd.y) ? 1 : 2);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+          const int t = tb + 4 * u;
+          if (t < T) {
+            const int j = idx[u] - NI;
+            if (!CDNA_DCHECK(j >= 0 && j <= NI, 0x7E13u)) continue;
+            const double v = *reinterpret_cast<const double*>(sheap + t * Wt + 2 * NI + 2 * j);
+            const double prod = stw[t] * v;
+            acc = acc + prod;
+          }
+        }
+      }
+    }
+    part[tl * 64 + row] = acc;
+    __syncthreads();
+    if (threadIdx.x < rows) {
+      double v = base;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v = v + part[q * 64 + threadIdx.x];
+      if (out_d)
+        out_d[r0 + threadIdx.x] = v;
+      else
+        out[r0 + threadIdx.x] = (float)v;
+    }
+  }
+}
+
 // Leaf lookup on binned data (for GBDT training-set margin updates):
 // out[r] += scale * value(leaf(r)) for a single tree in the compact
 // level-array form used during training (split on bins).
@@ -1005,6 +1147,26 @@ CDNA_API int cdna_tree_predict_heap(const float* X, int64_t n, int d, int64_t ld
   }
   hipLaunchKernelGGL(predict_heap_kernel, dim3(grid), dim3(256), lds, st, X, n, d, ldx, heap,
                      depth, tree_w, T, masks, base, out, out_d);
+  return (int)hipGetLastError();
+}
+
+// predict_heap_binned_kernel: bins [G][n] u64 (binize's column groups), thr_up [d][Bup] fp32; the heap as
+// cdna_tree_predict_heap (numeric and pass-through slots only), heap_b: scratch of the heap's size (the slots
+// rewritten as bin counts).  hipErrorInvalidValue when over the LDS budget.
+CDNA_API int cdna_tree_predict_heap_binned(const uint64_t* bins, int64_t n, int G, int d, const float* thr_up,
+                                           int Bup, const int* heap, int depth, const double* tree_w, int T,
+                                           double base, int* heap_b, float* out, double* out_d, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (depth < 0 || depth > 12 || G < 1 || d < 1 || d > 8 * G || Bup < 1 || Bup > 256) return (int)hipErrorInvalidValue;
+  const size_t wt = ((size_t)4 << depth) - 2;
+  const size_t lds = (size_t)T * wt * 4 + (size_t)((T + 1) & ~1) * 8 + (size_t)((64 * (2 * G + 1) + 1) & ~1) * 4 +
+                     256 * 8;
+  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
+  const int64_t words = (int64_t)T * (int64_t)wt;
+  hipLaunchKernelGGL(heap_to_bins_kernel, dim3(grid_for(words, 256, 64)), dim3(256), 0, st, heap, T, depth, thr_up,
+                     Bup, d, heap_b);
+  hipLaunchKernelGGL(predict_heap_binned_kernel, dim3(grid_for(n, 64, 8192)), dim3(256), lds, st, bins, n, G, d,
+                     heap_b, depth, tree_w, T, base, out, out_d);
   return (int)hipGetLastError();
 }
 
