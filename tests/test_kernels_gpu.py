@@ -1206,8 +1206,9 @@ def test_wide_codes_histogram_equals_records(dev, d, B):
                                               (100, 40, 3001, float("nan"))])
 def test_binize_v5_matches_reference(dev, d, maxb, n, missing):
     """K4 binize v5 (wave = 64-row tile x 8-feature group, broadcast table reads, [64][17] row-major tile):
-    column-major and padded row-major bins equal the CPU searchsorted reference -- categorical columns, NaN / +-inf, ragged last tile, 1..16 waves per block, 4-8 search steps, XGBoost
-    missing values."""
+    column-major and padded row-major bins equal the CPU searchsorted reference -- categorical columns, NaN / +-inf,
+    ragged last tile, 1..16 waves per block, 4-8 search steps, XGBoost missing values; the seg10 row layout
+    equals the bins' repacking."""
     g = torch.Generator().manual_seed(d + maxb)
     X = torch.randn(n, d, generator=g) * 3
     X[:, 1] = torch.randint(0, 9, (n,), generator=g).float()
@@ -1225,6 +1226,9 @@ def test_binize_v5_matches_reference(dev, d, maxb, n, missing):
     rmc = rm.cpu()
     assert rm is not None and torch.equal(rmc[:, :G], K.bins_row_major(ref)) and not rmc[:, G:].any()
     assert torch.equal(rm, K.bins_row_major(bins))
+    if 80 < d <= 100 and maxb <= 40 and missing is None:
+        b10, s10 = K.binize(X.to(dev), thr.to(dev), nthr.to(dev), want_rm=True, rm_layout="s10")
+        assert torch.equal(b10, bins) and torch.equal(s10, K.bins_seg10(bins, d))
 
 
 def test_fused_expressions_match_operator_path(dev, monkeypatch):
