@@ -701,7 +701,8 @@ __global__ __launch_bounds__(256) void predict_kernel(const float* __restrict__ 
 // predict_kernel: left iff x <= thr (NaN goes right), categorical left iff the category's mask bit is set.
 // Sums in fp64 in predict_kernel's order (lane q = t % 4 ascending, then base + lanes 0..3, no contraction).
 // (Two register sets refilled two tiles ahead with LDS-only barriers, as in binize5, measured 8.38 vs 7.78 ms at
-// 1e8 x 100: kept one set.)
+// 1e8 x 100: kept one set.  predict_heap_binned_kernel's walk -- trees per wave as a template, no per-tree guards --
+// measured 11.5 vs 7.8 ms here and was removed.)
 __global__ __launch_bounds__(256) void predict_heap_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ldx,
                                                            const int* __restrict__ heap, int depth,
                                                            const double* __restrict__ tree_w, int T,
@@ -1141,7 +1142,7 @@ CDNA_API int cdna_tree_predict_heap(const float* X, int64_t n, int d, int64_t ld
   const size_t lds = (size_t)T * wt * 4 + (size_t)((T + 1) & ~1) * 8 + (size_t)64 * (d + 1) * 4 + 256 * 8;
   if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
   unsigned grid = grid_for(n, 64, 8192);
-  if (grid_mode == 1) {
+  if (grid_mode & 1) {
     const unsigned res = cdna::resident_blocks(reinterpret_cast<const void*>(predict_heap_kernel), 256, lds);
     if (res > 0 && res < grid) grid = res;
   }
