@@ -94,14 +94,16 @@ class ForestPredictor:
             return None
         from ..ops import kernels as K
         tw, heap, _ = self._arrays(X.device)
-        if heap is None or fb.bins.device != X.device:
+        if heap is None:
             return None
+        got = fb.take(X)  # one transform per fit: the bins' memory goes back to the next fit
+        if got is None:
+            return None
+        bins, thr_up = got
         b0 = 0.0 if self.base is None else float(np.asarray(self.base, np.float64).reshape(-1)[0])
-        out = K.tree_predict_heap_binned(fb.bins, fb.thr_up, fb.d, heap[0], heap[1], tw, b0, dtype=dtype)
+        out = K.tree_predict_heap_binned(bins, thr_up, fb.d, heap[0], heap[1], tw, b0, dtype=dtype)
         if out is not None:
-            fb.hits += 1
             self.binned += 1
-            fb.release()          # one transform per fit: the memory goes back to the next fit
             self.forest.settle()  # the trainer's deferred node lists, while the GPU predicts
         return out
 

@@ -51,7 +51,8 @@ class FitBins:
         self.bins = bins
         self.d = int(d)
         self.thr_up, = K.upload(bins.device, K.bin_upper_edges(thresholds, nthr, int(B)))
-        weakref.finalize(src, FitBins._release, weakref.ref(self))
+        self._lock = threading.Lock()
+        self._fin = weakref.finalize(src, FitBins._release, weakref.ref(self))
         self.hits = 0
 
     @staticmethod
@@ -63,11 +64,26 @@ class FitBins:
     def release(self) -> None:
         """Drop the bins (stream-ordered: work already queued on them is unaffected)."""
         self.bins = self.thr_up = None
+        self._fin.detach()
 
     def matches(self, X: torch.Tensor) -> bool:
         src = self._ref()
         return (src is not None and self.bins is not None and self._key is not None
                 and _tensor_key(X) == self._key and _tensor_key(src) == self._key)
+
+    def take(self, X: torch.Tensor):
+        """(bins, thr_up) for a transform of X when X is the fit's tensor, released from this object at once (one
+        transform per fit; of two threads transforming the frame together exactly one gets them), else None."""
+        with self._lock:
+            if not self.matches(X):
+                return None
+            out = (self.bins, self.thr_up)
+            self.hits += 1
+            self.release()
+            return out
+
+    def __getstate__(self):
+        raise TypeError("FitBins holds device tensors of one process")
 
 
 # ============================================================ forest storage

@@ -74,6 +74,44 @@ def test_binned_walk_equals_raw_cpu(spark):
                                   K.heap_predict_host(Z, heap, D, tw).numpy())
 
 
+def test_fit_bins_lifecycle():
+    """FitBins (host tensors): matches only the fit's unmodified, live tensor; one take per fit, exactly one of
+    several threads gets the bins; released with the source; never pickled with its forest."""
+    import pickle
+    import threading
+    from cdnaml.models.tree.forest import FitBins, Forest
+    X = torch.randn(100, 13)
+    bins = torch.zeros((2, 100, 8), dtype=torch.uint8)
+    thr = np.sort(np.random.default_rng(0).standard_normal((13, 7)), 1)
+    fb = FitBins(X, bins, thr, np.full(13, 7, np.int32), 13, 8)
+    assert fb.thr_up.shape == (13, 8) and torch.isinf(fb.thr_up[:, 7]).all()
+    assert fb.matches(X) and fb.matches(X.view(100, 13)) and not fb.matches(X.clone())
+    got = []
+    ths = [threading.Thread(target=lambda: got.append(fb.take(X))) for _ in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert sum(g is not None for g in got) == 1 and fb.bins is None and fb.hits == 1
+    assert fb.take(X) is None
+    # an in-place write of the source ends the match
+    Y = torch.randn(50, 13)
+    fy = FitBins(Y, bins, thr, np.full(13, 7, np.int32), 13, 8)
+    Y.add_(0.0)
+    assert not fy.matches(Y) and fy.take(Y) is None
+    # released when the source dies
+    Z = torch.randn(20, 13)
+    fz = FitBins(Z, bins, thr, np.full(13, 7, np.int32), 13, 8)
+    del Z
+    gc.collect()
+    assert fz.bins is None
+    # a forest carrying one pickles without it
+    f = Forest(1)
+    f._fit_bins = fy
+    g = pickle.loads(pickle.dumps(f))
+    assert g._fit_bins is None and f._fit_bins is fy
+
+
 @pytest.mark.gpu
 def test_binned_kernel_equals_fp32_kernel(gpu_device):
     import cdnaml
