@@ -189,6 +189,8 @@ _SIGS = {
                               c_double, c_void_p, c_int, c_int, c_void_p], c_int),
     "cdna_tree_predict_heap": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                 c_double, c_void_p, c_void_p, c_int, c_void_p], c_int),
+    "cdna_fill_chunk": ([c_void_p, c_int, c_int64, c_int, c_int, c_int64], c_int64),
+    "cdna_seg_work": ([c_void_p, c_int, c_int64, c_int, c_void_p, c_int64], c_int64),
     "cdna_tree_predict_heap_binned": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                        c_int, c_double, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "cdna_predict_binned_add": ([c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p,

@@ -1450,6 +1450,27 @@ SEG_LANE_MAX_B = 256
 REC_PAD = 128
 
 
+# the record histograms' host planning (_fill_chunk + _seg_work) in the native library (csrc/kernels/plan.hip): ~250 us
+# of numpy per level -> a few us, off the GPU's critical path at the 8-GPU shard size
+NATIVE_PLAN = True
+
+
+def _seg_plan(segs: np.ndarray, chunk: int, B: int, ncu: int, interleave: bool):
+    """(chunk, work) = (_fill_chunk(segs, chunk, B, ncu), _seg_work(segs, that chunk, interleave)), natively."""
+    segs = np.ascontiguousarray(np.asarray(segs, dtype=np.int64).reshape(-1, 3))
+    k = len(segs)
+    mb = SEG_MIN_BLOCKS if B <= 64 else min(SEG_MIN_BLOCKS, SEG_MIN_BLOCKS_WIDE)
+    L = _lib.lib()
+    lens = np.ascontiguousarray(segs[:, 1])
+    c = int(L.cdna_fill_chunk(lens.ctypes.data, k, int(chunk), int(B), int(ncu), int(mb)))
+    total = int(lens.clip(min=0).sum())
+    cap = total // max(1, c) + k + 1
+    out = np.empty((cap, 3), dtype=np.int32)
+    m = int(L.cdna_seg_work(segs.ctypes.data, k, c, int(bool(interleave)), out.ctypes.data, cap))
+    assert m >= 0, (m, cap)
+    return c, out[:m]
+
+
 def _fill_chunk(segs: np.ndarray, chunk: int, B: int = 0, ncu: int = 0) -> int:
     """Shrink the rows-per-block chunk so a level with few rows still launches ~SEG_MIN_BLOCKS blocks
     (at 1.25e7 rows per GPU a level's 95K-row chunks made only ~100 blocks for 256 CUs).  With 2048 instead of
@@ -1641,9 +1662,12 @@ def _seg_hist_rec(bins, d, B, rec, segs, S, wmax, scales, bins_rm, interleave, r
             # large levels only: the smaller levels of a shard keep _fill_chunk's round fitting (its chunks grow
             # to drop a sliver round; capping them cost +0.25 ms at 1.25e7 rows)
             top = min(top, LANE10_CHUNK_MAX)
-        chunk = _fill_chunk(segs, min(top, cap), B,
-                            _num_cus(bins.device) if (SEG_ROUND_FIT and rm_s10 and bins.is_cuda) else 0)
-        work = _seg_work(segs, chunk, interleave)
+        ncu = _num_cus(bins.device) if (SEG_ROUND_FIT and rm_s10 and bins.is_cuda) else 0
+        if NATIVE_PLAN:
+            chunk, work = _seg_plan(segs, min(top, cap), B, ncu, interleave)
+        else:
+            chunk = _fill_chunk(segs, min(top, cap), B, ncu)
+            work = _seg_work(segs, chunk, interleave)
         if len(work) == 0:
             if out is not None:
                 return out

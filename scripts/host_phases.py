@@ -31,8 +31,26 @@ def wrap(cls, name):
 for n in ("_level_tables", "_level_histogram", "_level_reduce", "_level_decide", "_level_advance", "_fit_paths",
           "_fit_rows", "_fit_finish"):
     wrap(engine.ForestTrainer, n)
-for n in ("seg_hist_codes", "codes_compact", "seg_hist", "partition_codes", "split_decode", "split_scan"):
+for n in ("seg_hist_codes", "codes_compact", "seg_hist", "partition_codes", "split_decode", "split_scan",
+          "_codes_compact_w", "_seg_hist_rec", "upload"):
     wrap(K, n)
+_ev_sync = torch.cuda.Event.synchronize
+
+
+SPIN = os.environ.get("SPIN", "0") == "1"
+
+
+def _sync(self):
+    t = time.perf_counter()
+    if SPIN:
+        while not self.query():
+            pass
+    else:
+        _ev_sync(self)
+    log.append(("event.synchronize", t, time.perf_counter()))
+
+
+torch.cuda.Event.synchronize = _sync
 
 rows = int(float(os.environ.get("ROWS", "1.25e7")))
 spark = cdnaml.SparkSession.builder.getOrCreate()
@@ -45,6 +63,6 @@ for _ in range(3):
     rf.fit(df)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-print(f"fit wall {1e3 * (t1 - t0):.2f} ms")
+print(f"fit wall {1e3 * (t1 - t0):.2f} ms (SPIN={int(SPIN)})")
 for name, a, b in log:
     print(f"{1e6 * (a - t0):9.1f} us +{1e6 * (b - a):8.1f} us  {name}")

@@ -232,3 +232,27 @@ def test_col_moments_reference_semantics():
     full = K.col_moments(X)
     assert torch.allclose(merged[0], full[0])
 
+
+
+def test_native_seg_plan_matches_numpy():
+    """csrc/kernels/plan.hip (host code of the native library): the record histograms' chunk and work list equal
+    the numpy _fill_chunk + _seg_work bit for bit (same chunk, same items in the same interleaved order)."""
+    import numpy as np
+    from cdnaml.ops import kernels as K
+    rng = np.random.default_rng(5)
+    cases = 0
+    for S in (1, 2, 3, 40, 80, 160, 700):
+        for scale in (1e3, 3e5, 2e6, 2e7):
+            lens = rng.integers(0, int(scale), S)
+            lens[rng.random(S) < 0.1] = 0
+            segs = np.stack([np.concatenate([[0], np.cumsum(lens)[:-1]]), lens, np.arange(S)], 1)
+            for chunk in (8192, 40960, 786000):
+                for B, ncu in ((40, 256), (40, 0), (128, 256)):
+                    for inter in (False, True):
+                        c_ref = K._fill_chunk(segs, chunk, B, ncu)
+                        w_ref = K._seg_work(segs, c_ref, inter)
+                        c, w = K._seg_plan(segs, chunk, B, ncu, inter)
+                        assert c == c_ref, (S, scale, chunk, B, ncu)
+                        np.testing.assert_array_equal(w, w_ref)
+                        cases += 1
+    assert cases > 500
