@@ -797,6 +797,14 @@ def _early_side_work(num_trees, bootstrap, rate, want_label_max=True, codes_ok=F
     return pre, early
 
 
+def _label_f32(early, y):
+    """The fp32 label queued on the side stream (``early["yf"]``), else a cast of ``y`` (never both: a
+    ``dict.get(k, y.float())`` default is evaluated eagerly -- a full extra cast of the label per fit, 0.27 ms at
+    1e8 rows)."""
+    yf = early.get("yf")
+    return yf if yf is not None else y.float()
+
+
 def _join_early(early, dev):
     for k in ("yf", "w"):
         if k in early:
@@ -816,7 +824,7 @@ def _train_forest_regression(est, dataset, num_trees, subset, bootstrap, rate, i
     if w is not None:
         weights = _combine_weights(weights, w, num_trees)
     trainer = ForestTrainer(session, data, p)
-    forest = trainer.train(num_trees, {"v0": None, "v1": early.get("yf", y.float())}, weights)
+    forest = trainer.train(num_trees, {"v0": None, "v1": _label_f32(early, y)}, weights)
     attach_fit_bins(forest, data)
     return forest, data.d
 
@@ -925,7 +933,7 @@ def _train_rf_reg(est, dataset, T_):
     if w is not None:
         weights = _combine_weights(bc.weights() if bc is not None else weights, w, T_)
         bc = None
-    forest = ForestTrainer(session, data, p).train(T_, {"v0": None, "v1": early.get("yf", y.float())}, weights,
+    forest = ForestTrainer(session, data, p).train(T_, {"v0": None, "v1": _label_f32(early, y)}, weights,
                                                    codes_pre=bc)
     attach_fit_bins(forest, data)
     return forest, data.d

@@ -18,6 +18,8 @@ from ..util import IllegalArgumentException
 
 # binning queued on the quantile kernel's device thresholds, checked on the host behind it
 SPEC_THRESHOLDS = True
+# one-rank quantile sample gathered on the device behind the Philox selection (no host count round trip)
+SAMPLE_FUSED = True
 # free device memory kept back when building the boosting partition's feature-major bins copy
 FM_HEADROOM = 4 << 30
 
@@ -196,14 +198,23 @@ class ChunkedRows:
         return iter(self.it_fn())
 
 
-def _global_sample(session, X, max_bins: int, seed: int, row_offset: int, n_global: int):
+def _global_sample(session, X, max_bins: int, seed: int, row_offset: int, n_global: int, fused: bool = False):
     """Rows sampled by Philox keyed on the GLOBAL row id (the same rows whatever the GPU count), gathered
     from every rank: the split-candidate sample (a row set: its order is not defined).  ``X`` may be a
-    :class:`ChunkedRows` stream (the same rows, sampled chunk by chunk)."""
+    :class:`ChunkedRows` stream (the same rows, sampled chunk by chunk).
+
+    fused (one rank, resident fp32 X on the GPU): ``(samp, ok)`` -- the sample as fp64 rows padded with NaN rows to
+    a fixed capacity, with no host round trip (``K.sample_gather``: the quantile kernel counts non-NaN values only,
+    so the thresholds are the exact sample's); ``ok()`` is False in the (12-sigma) case the capacity overflowed,
+    then the caller takes the exact sample.  Otherwise the sample itself."""
     comm = session.comm
     n = X.shape[0]
     target = max(max_bins * max_bins, 10000)
     frac = min(1.0, target / max(n_global, 1))
+    if fused and SAMPLE_FUSED and frac < 1.0 and not comm.distributed and not isinstance(X, ChunkedRows):
+        r = K.sample_gather(X, seed ^ 0x5BD1E995, row_offset, 3, frac)
+        if r is not None:
+            return r
     if isinstance(X, ChunkedRows) and X.host_it_fn is not None and frac < 1.0:
         # the sampled rows (the same Philox draws on the device) gathered from the host chunks: a few thousand
         # rows cross PCIe instead of the whole frame
@@ -334,9 +345,11 @@ def _make_binned(session, X, categorical: Dict[int, int], max_bins: int, seed: i
     if max_bins > 256:
         raise IllegalArgumentException("maxBins must be <= 256 on this engine (uint8 bins)")
     n = X.shape[0]
-    samp = _global_sample(session, X, max_bins, seed, row_offset, n_global)
+    spec = SPEC_THRESHOLDS and not categorical and X.is_cuda and not isinstance(X, ChunkedRows)
+    samp = _global_sample(session, X, max_bins, seed, row_offset, n_global, fused=spec)
+    samp, samp_ok = samp if isinstance(samp, tuple) else (samp, lambda: True)
     s10 = _seg10_ok(X, d, max_bins)
-    if SPEC_THRESHOLDS and not categorical and X.is_cuda and not isinstance(X, ChunkedRows):
+    if spec:
         # the binning queued straight on the K3 kernel's device thresholds; the host checks behind it that every
         # feature had more than max_bins distinct sample values (then the thresholds are exactly the host path's)
         # -- no device -> host -> device round trip between the quantile kernel and the binning
@@ -348,12 +361,14 @@ def _make_binned(session, X, categorical: Dict[int, int], max_bins: int, seed: i
             with _tr.span("tree.binize"):
                 bins, rm = K.binize(X, thr_d.float(), nthr_d, want_rm=True, rm_layout="s10" if s10 else "std")
             thr, ints = pend.get()
-            if bool((ints[1] > max_bins).all()):
+            if samp_ok() and bool((ints[1] > max_bins).all()):
                 thr, nthr = thr.copy(), ints[0].copy()
                 if s10:
                     return BinnedData(X, bins, thr, nthr, {}, n, n_global, row_offset, d, max_bins, False, None, rm)
                 return BinnedData(X, bins, thr, nthr, {}, n, n_global, row_offset, d, max_bins, False, rm)
             del bins, rm  # a feature with few distinct values: the host path below, then bin again
+    if not samp_ok():  # the fused sample's capacity overflowed: the exact sample
+        samp = _global_sample(session, X, max_bins, seed, row_offset, n_global)
     with _tr.span("tree.find_thresholds"):
         thr, nthr = find_thresholds_t(samp.double(), max_bins, categorical)
     thr_t = torch.from_numpy(thr.astype(np.float32)).to(X.device)

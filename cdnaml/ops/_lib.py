@@ -189,6 +189,7 @@ _SIGS = {
                               c_double, c_void_p, c_int, c_int, c_void_p], c_int),
     "cdna_tree_predict_heap": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                 c_double, c_void_p, c_void_p, c_int, c_void_p], c_int),
+    "cdna_sample_gather": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "cdna_fill_chunk": ([c_void_p, c_int, c_int64, c_int, c_int, c_int64], c_int64),
     "cdna_seg_work": ([c_void_p, c_int, c_int64, c_int, c_void_p, c_int64], c_int64),
     "cdna_tree_predict_heap_binned": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,

@@ -515,6 +515,38 @@ def sample_rows(n: int, seed: int, offset: int, stream: int, frac: float, device
     return torch.sort(idx[:c]).values if ordered else idx[:c]
 
 
+def sample_gather(X: torch.Tensor, seed: int, offset: int, stream: int, frac: float):
+    """``X[sample_rows(...)]`` as an fp64 [cap, d] sample without a host round trip: the rows of the Philox sample
+    (arbitrary order) then NaN rows up to the capacity (misc.hip sample_gather_kernel).  -> (samp, ok) where
+    ``ok()`` (call it once the work behind the sample is queued) tells whether every sampled row fitted the capacity
+    (else the caller redoes the exact path); None where the kernels do not apply."""
+    n, d = X.shape
+    if not _native(X) or n == 0 or X.dtype != torch.float32 or X.stride(1) != 1:
+        return None
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    exp_ = n * frac
+    cap = int(exp_ + 12.0 * math.sqrt(exp_ + 1.0) + 1024)
+    dev = X.device
+    idx = torch.empty(cap, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)
+    st = _stream(dev)
+    L = _lib.lib()
+    _lib.check(L.cdna_sample_rows(n, seed, int(offset), int(stream) & 0xFFFFFFFF, float(frac), _ptr(idx), cap,
+                                  _ptr(cnt), st), "cdna_sample_rows")
+    samp = torch.empty((cap, d), dtype=torch.float64, device=dev)
+    _lib.check(L.cdna_sample_gather(_ptr(X), X.stride(0), d, _ptr(idx), _ptr(cnt), cap, _ptr(samp), st),
+               "cdna_sample_gather")
+    host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+    host.copy_(cnt, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+
+    def ok() -> bool:
+        ev.synchronize()
+        return int(host[0]) <= cap
+    return samp, ok
+
+
 def prefetch_max(t: torch.Tensor, absval: bool = False, stream=None) -> None:
     """Queue max(t) (max |t|) on ``stream`` (default: current) and attach it to the tensor object itself (never
     keyed by address: a recycled allocation must not inherit a stale value) for packed_scale_global /

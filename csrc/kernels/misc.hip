@@ -492,6 +492,23 @@ __global__ __launch_bounds__(256) void sample_rows_kernel(int64_t n, uint64_t se
   }
 }
 
+// The sampled rows of X as the fp64 quantile sample, straight from sample_rows_kernel's device ids and count:
+// out [cap][d], row i = X[idx[i]] for i < min(*count, cap), NaN beyond (the quantile kernel sorts NaN last and
+// counts only the non-NaN values, so the padding changes no threshold).  No host round trip for the count between
+// the two kernels, and no separate gather / cast launches.
+__global__ __launch_bounds__(256) void sample_gather_kernel(const float* __restrict__ X, int64_t ldx, int d,
+                                                            const int64_t* __restrict__ idx,
+                                                            const unsigned* __restrict__ count, int64_t cap,
+                                                            double* __restrict__ out) {
+  const int64_t c = (int64_t)*count < cap ? (int64_t)*count : cap;
+  const int64_t total = cap * (int64_t)d;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t i = e / d;
+    const int f = (int)(e - i * d);
+    out[e] = i < c ? (double)X[idx[i] * ldx + f] : __builtin_nan("");
+  }
+}
+
 // Per-node feature subsets (featureSubsetStrategy) as bit words [A, W]: node a keeps the k features with the
 // smallest splitmix64(base[a] + f * 0xD6E8FEB86659FD93) -- the host formula of engine.ForestTrainer._feature_masks
 // (base[a] = its seed / tree / heap-key mix, computed on the host).  splitmix64 is a bijection and the inputs of a
@@ -550,6 +567,15 @@ CDNA_API int cdna_sample_rows(int64_t n, uint64_t seed, uint64_t offset, uint32_
   if (e != hipSuccess || n <= 0) return (int)e;
   hipLaunchKernelGGL(sample_rows_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, n, seed, offset, stream, frac,
                      idx, cap, count);
+  return (int)hipGetLastError();
+}
+
+CDNA_API int cdna_sample_gather(const float* X, int64_t ldx, int d, const int64_t* idx, const unsigned* count,
+                                int64_t cap, double* out, hipStream_t st) {
+  if (cap <= 0 || d <= 0) return 0;
+  const int64_t total = cap * (int64_t)d;
+  hipLaunchKernelGGL(sample_gather_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, X, ldx, d, idx, count,
+                     cap, out);
   return (int)hipGetLastError();
 }
 

@@ -187,3 +187,32 @@ def test_transform_of_fit_frame_uses_bins(gpu_device):
 def frame_pred(model, frame):
     parts = model.transform(frame)._plan.execute()
     return torch.cat([b.columns["prediction"].values for b in parts])
+
+
+@pytest.mark.gpu
+def test_fused_sample_same_thresholds(gpu_device, monkeypatch):
+    """The one-rank quantile sample gathered on the device (K.sample_gather: NaN-padded to a fixed capacity, no
+    host count) gives the exact sample's thresholds and bins; a capacity overflow falls back to the exact sample."""
+    import cdnaml
+    from cdnaml.models.tree import binning as BN
+    spark = cdnaml.SparkSession.builder.getOrCreate()
+    g = torch.Generator().manual_seed(4)
+    X = torch.randn(300000, 24, generator=g)
+    X[:, 3] = torch.randint(0, 5000, (300000,), generator=g).float()
+    Xd = X.to(gpu_device)
+    outs = {}
+    for mode in ("fused", "exact", "overflow"):
+        monkeypatch.setattr(BN, "SAMPLE_FUSED", mode != "exact")
+        if mode == "overflow":
+            real = K.sample_gather
+
+            def fake(*a, **k):
+                samp, _ = real(*a, **k)
+                return samp, (lambda: False)
+            monkeypatch.setattr(K, "sample_gather", fake)
+        data = BN._make_binned(spark, Xd, {}, 40, 7, 0, 300000)
+        outs[mode] = (data.thresholds.copy(), data.nthr.copy(), data.bins.cpu())
+    for mode in ("fused", "overflow"):
+        np.testing.assert_array_equal(outs[mode][0], outs["exact"][0])
+        np.testing.assert_array_equal(outs[mode][1], outs["exact"][1])
+        assert torch.equal(outs[mode][2], outs["exact"][2])
