@@ -2153,11 +2153,14 @@ COMPACT_MIN_PER_WAVE = 256
 # queued scatter (seg.hip codes_scatter_q_kernel, rank 2): the built row slots queued per wave in LDS and ranked /
 # stored in dense groups of 64 (packed records, per_wave <= 65536); identical records to ranks 0 / 1
 SCATTER_QUEUE = True
+# the queued scatter with its code / label loads one trip ahead (two register sets; rank 3): 120.9 / 120.9 vs
+# 121.6 / 121.6 ms per headline step, scatter 7.7 vs ~8.2 ms (profiles/r6/headline_ab.md)
+SCATTER_PREFETCH = True
 
 
 def _scatter_rank(KB: int, rec: bool = False, per_wave: int = 0) -> int:
     if SCATTER_QUEUE and rec and per_wave <= 65536:
-        return 2
+        return 3 if SCATTER_PREFETCH else 2
     return 0 if (SCATTER_RANK == 1 and KB < SCATTER_SCAN_MIN_KB) else SCATTER_RANK
 
 

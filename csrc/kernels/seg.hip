@@ -1411,7 +1411,10 @@ __global__ __launch_bounds__(256) void codes_scatter_w_kernel(const CompactWArgs
 // ballots for KB <= 2) and build + store the records.  A group ranks in queue order, so the records and their positions are exactly RANK 0 / 1's
 // (row order inside each (tree, node, wave) run).  Leftovers (< 64) carry to the next trip; the wave's last group
 // is partial.  A/B at the headline (profiles/r6/scatter_queue_ab.md).  LDS: 4 waves x 576 x 8 B = 18 KB per block.
-template <int KB>
+// PF (rank 3): two register sets of codes / labels, each consumed and refilled two trips ahead, so a trip's loads
+// are in flight while the previous trip queues and drains (PMC of the one-set loop: 56 % of wave cycles waiting,
+// 14 % VALU busy; 8.2 -> 7.7 ms per headline step).
+template <int KB, bool PF>
 __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs a) {
   constexpr int NW = KB > 4 ? KB / 4 : 1;
   constexpr int NG = 2;                  // 256-row groups per trip (4 consecutive rows per lane)
@@ -1482,9 +1485,8 @@ __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs
   const bool vec = (a.n & 3) == 0 && (reinterpret_cast<uintptr_t>(a.codes) & 7u) == 0 &&
                    (reinterpret_cast<uintptr_t>(a.v1) & 15u) == 0;
   int nq = 0;  // wave-uniform queue length
-  for (int64_t rb = r_begin; rb < r_end; rb += 256 * NG) {
-    uint32_t cc[NG][4];
-    float xl[NG][4];
+  // one trip = NG x 256 rows: 4 consecutive codes + labels per lane (8-byte / 16-byte loads)
+  auto load = [&](int64_t rb, uint32_t (&cc)[NG][4], float (&xl)[NG][4]) {
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int64_t r = rb + g * 256 + lane * 4;
@@ -1507,6 +1509,8 @@ __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs
         }
       }
     }
+  };
+  auto trip = [&](int64_t rb, const uint32_t (&cc)[NG][4], const float (&xl)[NG][4]) {
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       int kk[4], cnt = 0;
@@ -1545,6 +1549,28 @@ __global__ __launch_bounds__(256) void codes_scatter_q_kernel(const CompactWArgs
     nq = left;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+  };
+  constexpr int64_t TRIP = 256 * NG;
+  if (PF) {
+    // two register sets, each consumed and then refilled two trips ahead (no register copy at the back-edge):
+    // a trip's code / label loads are in flight while the previous trip queues and drains
+    uint32_t ca[NG][4], cb2[NG][4];
+    float xa[NG][4], xb[NG][4];
+    load(r_begin, ca, xa);
+    load(r_begin + TRIP, cb2, xb);
+    for (int64_t rb = r_begin; rb < r_end; rb += 2 * TRIP) {
+      trip(rb, ca, xa);
+      load(rb + 2 * TRIP, ca, xa);
+      if (rb + TRIP < r_end) trip(rb + TRIP, cb2, xb);  // wave-uniform
+      load(rb + 3 * TRIP, cb2, xb);
+    }
+  } else {
+    for (int64_t rb = r_begin; rb < r_end; rb += TRIP) {
+      uint32_t cc[NG][4];
+      float xl[NG][4];
+      load(rb, cc, xl);
+      trip(rb, cc, xl);
+    }
   }
   if (nq > 0) drain(0, nq);
 }
@@ -2016,17 +2042,18 @@ CDNA_API int cdna_codes_compact_w(int pass, int KB, const uint16_t* codes, int64
                  rec_out, qs1, kstart};
   const int64_t nch = (Wv + 3) / 4;
   const dim3 grid((unsigned)(((nch + 7) / 8) * 8 * T));  // (chunk, tree) pairs, XCD-aware order (kernel)
-  if (rank < 0 || rank > 2) return (int)hipErrorInvalidValue;
-  // rank 2 (queued): packed records only, row offsets inside a wave's range in 16 bits
-  if (pass == 2 && rank == 2 && (!rec_out || per_wave > 65536)) return (int)hipErrorInvalidValue;
-  auto go = [&](auto k1, auto k2r0, auto k2r1, auto k2q) {
+  if (rank < 0 || rank > 3) return (int)hipErrorInvalidValue;
+  // rank 2 / 3 (queued; 3: loads one trip ahead): packed records only, row offsets inside a wave's range in 16 bits
+  if (pass == 2 && rank >= 2 && (!rec_out || per_wave > 65536)) return (int)hipErrorInvalidValue;
+  auto go = [&](auto k1, auto k2r0, auto k2r1, auto k2q, auto k2qp) {
     if (pass == 1) hipLaunchKernelGGL(k1, grid, dim3(256), 0, st, a);
     else if (rank == 0) hipLaunchKernelGGL(k2r0, grid, dim3(256), 0, st, a);
     else if (rank == 1) hipLaunchKernelGGL(k2r1, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k2q, grid, dim3(256), 0, st, a);
+    else if (rank == 2) hipLaunchKernelGGL(k2q, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k2qp, grid, dim3(256), 0, st, a);
   };
 #define CDNA_CW(K) go(codes_count_w_kernel<K>, codes_scatter_w_kernel<K, 0>, codes_scatter_w_kernel<K, 1>, \
-                      codes_scatter_q_kernel<K>)
+                      codes_scatter_q_kernel<K, false>, codes_scatter_q_kernel<K, true>)
   switch (KB) {
     case 1: CDNA_CW(1); break;
     case 2: CDNA_CW(2); break;

@@ -545,18 +545,20 @@ def test_seg_partition_implicit_level0(dev):
     assert int(ref[3].min()) > 0  # out-of-bag rows dropped
 
 
-@pytest.mark.parametrize("rank", [None, 0, 1, 2])
+@pytest.mark.parametrize("rank", [None, 0, 1, 2, 3])
 @pytest.mark.parametrize("max_loc", [9, 17])
 @pytest.mark.parametrize("waves", [2048, 4])
 def test_codes_compact(dev, monkeypatch, rank, max_loc, waves):
     """Rows of built nodes gathered into slot segments: same (row, v1, w) multiset per slot as the reference.
     rank None = the atomic (not wave-owned) kernel; else the wave-owned kernel ranking a node's lanes by ballots
     (0) or a DPP prefix scan (1; from one built node up), both stable: exactly the reference order; 2 = the queued
-    scatter of packed records (codes_scatter_q_kernel), the same records.  max_loc 17 reaches 16 built nodes per
-    tree (KB = 16); waves 4 gives each wave ~25 trips (the queue's carry between trips)."""
+    scatter of packed records (codes_scatter_q_kernel), the same records; 3 = the queued scatter loading one trip
+    ahead.  max_loc 17 reaches 16 built nodes per tree (KB = 16); waves 4 gives each wave ~25 trips (the queue's
+    carry between trips)."""
     monkeypatch.setattr(K, "COMPACT_W", rank is not None)
     monkeypatch.setattr(K, "COMPACT_WAVES", waves)
-    monkeypatch.setattr(K, "SCATTER_QUEUE", rank == 2)
+    monkeypatch.setattr(K, "SCATTER_QUEUE", rank in (2, 3))
+    monkeypatch.setattr(K, "SCATTER_PREFETCH", rank == 3)
     if rank is not None:
         monkeypatch.setattr(K, "SCATTER_RANK", min(rank, 1))
         monkeypatch.setattr(K, "SCATTER_SCAN_MIN_KB", 1)
