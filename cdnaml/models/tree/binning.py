@@ -359,7 +359,7 @@ def _make_binned(session, X, categorical: Dict[int, int], max_bins: int, seed: i
             thr_d, nthr_d, pend = q
             before_binize()
             with _tr.span("tree.binize"):
-                bins, rm = K.binize(X, thr_d.float(), nthr_d, want_rm=True, rm_layout="s10" if s10 else "std")
+                bins, rm = K.binize(X, thr_d, nthr_d, want_rm=True, rm_layout="s10" if s10 else "std")
             thr, ints = pend.get()
             if samp_ok() and bool((ints[1] > max_bins).all()):
                 thr, nthr = thr.copy(), ints[0].copy()

@@ -97,7 +97,8 @@ def build(force: bool = False, verbose: bool = False, debug: bool = DEBUG) -> st
 _SIGS = {
     # name: (argtypes, restype)
     "cdna_gram_workspace": ([c_int64, c_int, c_int], c_int64),
-    "cdna_quantile_thresholds": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "cdna_quantile_thresholds": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p],
                                  c_int),
     "cdna_gram": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int,
                    c_void_p], c_int),
@@ -189,7 +190,8 @@ _SIGS = {
                               c_double, c_void_p, c_int, c_int, c_void_p], c_int),
     "cdna_tree_predict_heap": ([c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                 c_double, c_void_p, c_void_p, c_int, c_void_p], c_int),
-    "cdna_sample_gather": ([c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p], c_int),
+    "cdna_sample_gather": ([c_void_p, c_int64, c_int64, c_int, c_uint64, c_uint64, c_uint32, c_double, c_void_p,
+                            c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "cdna_fill_chunk": ([c_void_p, c_int, c_int64, c_int, c_int, c_int64], c_int64),
     "cdna_seg_work": ([c_void_p, c_int, c_int64, c_int, c_void_p, c_int64], c_int64),
     "cdna_tree_predict_heap_binned": ([c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,

@@ -271,7 +271,7 @@ def quantile_thresholds(samp: torch.Tensor, max_bins: int):
     thr = torch.empty((d, max_bins - 1), dtype=torch.float64, device=dev)
     ints = torch.empty((2, d), dtype=torch.int32, device=dev)
     _lib.check(_lib.lib().cdna_quantile_thresholds(_ptr(samp), s, d, max_bins, _ptr(sorted_), _ptr(thr),
-                                                   _ptr(ints[0]), _ptr(ints[1]), _stream(dev)),
+                                                   _ptr(ints[0]), _ptr(ints[1]), None, _stream(dev)),
                "cdna_quantile_thresholds")
     ih = ints.cpu().numpy()
     return thr.cpu().numpy(), ih[0].copy(), ih[1].copy(), sorted_
@@ -293,10 +293,11 @@ class _HostCopies:
 
 
 def quantile_thresholds_dev(samp: torch.Tensor, max_bins: int):
-    """K3 without a host round trip: (thr [d, max_bins-1] fp64, nthr [d] int32 -- both device tensors --, pending
-    host copies of (thr, nthr, kdist)), or None where :func:`quantile_thresholds` does not apply.  The binning can be
-    queued on the device thresholds at once; they equal the host path's only where every feature has more than
-    ``max_bins`` distinct values (kdist), which the caller checks on the host copy once it has queued the binning."""
+    """K3 without a host round trip: (thr [d, max_bins-1] fp32, nthr [d] int32 -- both device tensors, the fp32
+    thresholds written by the kernel itself for the binning --, pending host copies of (thr fp64, nthr, kdist)), or
+    None where :func:`quantile_thresholds` does not apply.  The binning can be queued on the device thresholds at
+    once; they equal the host path's only where every feature has more than ``max_bins`` distinct values (kdist),
+    which the caller checks on the host copy once it has queued the binning."""
     s, d = samp.shape
     if not _native(samp) or s == 0 or s > QUANTILE_MAX_S or not (2 <= max_bins <= 257):
         return None
@@ -305,10 +306,11 @@ def quantile_thresholds_dev(samp: torch.Tensor, max_bins: int):
     sorted_ = torch.empty((d, s), dtype=torch.float64, device=dev)
     thr = torch.empty((d, max_bins - 1), dtype=torch.float64, device=dev)
     ints = torch.empty((2, d), dtype=torch.int32, device=dev)
+    thr32 = torch.empty((d, max_bins - 1), dtype=torch.float32, device=dev)
     _lib.check(_lib.lib().cdna_quantile_thresholds(_ptr(samp), s, d, max_bins, _ptr(sorted_), _ptr(thr),
-                                                   _ptr(ints[0]), _ptr(ints[1]), _stream(dev)),
+                                                   _ptr(ints[0]), _ptr(ints[1]), _ptr(thr32), _stream(dev)),
                "cdna_quantile_thresholds")
-    return thr, ints[0], _HostCopies(thr, ints)
+    return thr32, ints[0], _HostCopies(thr, ints)
 
 
 # --------------------------------------------------------------------- K4
@@ -527,23 +529,20 @@ def sample_gather(X: torch.Tensor, seed: int, offset: int, stream: int, frac: fl
     exp_ = n * frac
     cap = int(exp_ + 12.0 * math.sqrt(exp_ + 1.0) + 1024)
     dev = X.device
-    idx = torch.empty(cap, dtype=torch.int64, device=dev)
-    cnt = torch.empty(1, dtype=torch.int32, device=dev)
-    st = _stream(dev)
-    L = _lib.lib()
-    _lib.check(L.cdna_sample_rows(n, seed, int(offset), int(stream) & 0xFFFFFFFF, float(frac), _ptr(idx), cap,
-                                  _ptr(cnt), st), "cdna_sample_rows")
+    idx = torch.empty(8 * cap, dtype=torch.int64, device=dev)  # 8 regions of cap ids (misc.hip)
+    cnt = torch.empty(8, dtype=torch.int32, device=dev)
     samp = torch.empty((cap, d), dtype=torch.float64, device=dev)
-    _lib.check(L.cdna_sample_gather(_ptr(X), X.stride(0), d, _ptr(idx), _ptr(cnt), cap, _ptr(samp), st),
-               "cdna_sample_gather")
-    host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+    _lib.check(_lib.lib().cdna_sample_gather(_ptr(X), n, X.stride(0), d, seed, int(offset) & 0xFFFFFFFFFFFFFFFF,
+                                             int(stream) & 0xFFFFFFFF, float(frac), _ptr(idx), _ptr(cnt), cap,
+                                             _ptr(samp), _stream(dev)), "cdna_sample_gather")
+    host = torch.empty(8, dtype=torch.int32, pin_memory=True)
     host.copy_(cnt, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
 
     def ok() -> bool:
         ev.synchronize()
-        return int(host[0]) <= cap
+        return int(host.to(torch.int64).sum()) <= cap
     return samp, ok
 
 

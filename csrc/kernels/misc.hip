@@ -492,20 +492,81 @@ __global__ __launch_bounds__(256) void sample_rows_kernel(int64_t n, uint64_t se
   }
 }
 
-// The sampled rows of X as the fp64 quantile sample, straight from sample_rows_kernel's device ids and count:
-// out [cap][d], row i = X[idx[i]] for i < min(*count, cap), NaN beyond (the quantile kernel sorts NaN last and
-// counts only the non-NaN values, so the padding changes no threshold).  No host round trip for the count between
-// the two kernels, and no separate gather / cast launches.
+// sample_rows_kernel's selection with the kept ids buffered per BLOCK in LDS and claimed with one atomic per block
+// on one of 8 counters (the block's blockIdx % 8: its XCD under round-robin placement -- speed only): region r of
+// idx [8][rcap] holds counter r's ids.  sample_rows_kernel claims slots with one atomic per wave with a kept row on
+// ONE counter: ~10,000 same-address atomics for a 1e4-row sample, serialised at ~11 ns each (108 us of its 116 us
+// at 1.25e7 rows).  counts[8] are zeroed by the caller.
+__global__ __launch_bounds__(256) void sample_rows_blk_kernel(int64_t n, uint64_t seed, uint64_t offset,
+                                                              uint32_t stream, double frac,
+                                                              int64_t* __restrict__ idx, int64_t rcap,
+                                                              unsigned* __restrict__ counts) {
+  constexpr int SB = 1024;
+  __shared__ int64_t s_rows[SB];
+  __shared__ unsigned s_n, s_base;
+  if (threadIdx.x == 0) s_n = 0u;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int region = (int)(blockIdx.x & 7u);
+  auto flush = [&]() {  // block-uniform
+    __syncthreads();
+    const unsigned m = s_n;
+    if (m) {
+      if (threadIdx.x == 0) s_base = atomicAdd(&counts[region], m);
+      __syncthreads();
+      const unsigned base = s_base;
+      for (unsigned i = threadIdx.x; i < m; i += 256)
+        if ((int64_t)base + i < rcap) idx[(int64_t)region * rcap + base + i] = s_rows[i];
+      __syncthreads();
+      if (threadIdx.x == 0) s_n = 0u;
+    }
+    __syncthreads();
+  };
+  for (int64_t rb = (int64_t)blockIdx.x * 256; rb < n; rb += (int64_t)gridDim.x * 256) {
+    if (s_n + 256u > (unsigned)SB) flush();  // s_n is only written between barriers: the test is block-uniform
+    const int64_t r = rb + threadIdx.x;
+    const bool keep = r < n && cdna::philox_uniform(seed, offset + (uint64_t)r, stream) < frac;
+    const uint64_t mk = __builtin_amdgcn_ballot_w64(keep);
+    if (mk) {
+      unsigned slot = 0u;
+      if (lane == 0) slot = atomicAdd(&s_n, (unsigned)__builtin_popcountll(mk));
+      slot = (unsigned)__shfl((int)slot, 0);
+      const unsigned below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+      if (keep) s_rows[slot + below] = r;
+    }
+    __syncthreads();
+  }
+  flush();
+}
+
+// The sampled rows of X as the fp64 quantile sample, straight from sample_rows_blk_kernel's device ids and counts:
+// out [cap][d], row i = X[id i] for i < min(total, cap) (ids taken region by region), NaN beyond (the quantile
+// kernel sorts NaN last and counts only the non-NaN values, so the padding changes no threshold).  No host round
+// trip for the count between the two kernels, and no separate gather / cast launches.
 __global__ __launch_bounds__(256) void sample_gather_kernel(const float* __restrict__ X, int64_t ldx, int d,
                                                             const int64_t* __restrict__ idx,
-                                                            const unsigned* __restrict__ count, int64_t cap,
-                                                            double* __restrict__ out) {
-  const int64_t c = (int64_t)*count < cap ? (int64_t)*count : cap;
+                                                            const unsigned* __restrict__ counts, int64_t rcap,
+                                                            int64_t cap, double* __restrict__ out) {
+  int64_t pre[9];
+  pre[0] = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int64_t c = (int64_t)counts[q] < rcap ? (int64_t)counts[q] : rcap;
+    pre[q + 1] = pre[q] + c;
+  }
+  const int64_t c = pre[8] < cap ? pre[8] : cap;
   const int64_t total = cap * (int64_t)d;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int64_t i = e / d;
     const int f = (int)(e - i * d);
-    out[e] = i < c ? (double)X[idx[i] * ldx + f] : __builtin_nan("");
+    double v = __builtin_nan("");
+    if (i < c) {
+      int q = 0;
+#pragma unroll
+      for (int k = 1; k < 8; ++k) q += i >= pre[k] ? 1 : 0;
+      v = (double)X[idx[(int64_t)q * rcap + (i - pre[q])] * ldx + f];
+    }
+    out[e] = v;
   }
 }
 
@@ -570,12 +631,20 @@ CDNA_API int cdna_sample_rows(int64_t n, uint64_t seed, uint64_t offset, uint32_
   return (int)hipGetLastError();
 }
 
-CDNA_API int cdna_sample_gather(const float* X, int64_t ldx, int d, const int64_t* idx, const unsigned* count,
-                                int64_t cap, double* out, hipStream_t st) {
-  if (cap <= 0 || d <= 0) return 0;
+// The fused quantile sample: sample_rows_blk_kernel (ids into idx [8][cap], counts [8] zeroed here) then
+// sample_gather_kernel (out [cap][d] fp64, NaN-padded).  counts[8] stay on the device for the caller's check.
+CDNA_API int cdna_sample_gather(const float* X, int64_t n, int64_t ldx, int d, uint64_t seed, uint64_t offset,
+                                uint32_t stream, double frac, int64_t* idx, unsigned* counts, int64_t cap,
+                                double* out, hipStream_t st) {
+  if (cap <= 0 || d <= 0 || !counts) return (int)hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(counts, 0, 8 * sizeof(unsigned), st);
+  if (e != hipSuccess) return (int)e;
+  if (n > 0)
+    hipLaunchKernelGGL(sample_rows_blk_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, n, seed, offset,
+                       stream, frac, idx, cap, counts);
   const int64_t total = cap * (int64_t)d;
-  hipLaunchKernelGGL(sample_gather_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, X, ldx, d, idx, count,
-                     cap, out);
+  hipLaunchKernelGGL(sample_gather_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, X, ldx, d, idx, counts,
+                     cap, cap, out);
   return (int)hipGetLastError();
 }
 

@@ -36,7 +36,7 @@ template <bool RADIX>
 __global__ __launch_bounds__(kQThreads) void quantile_kernel(const double* __restrict__ samp, int s, int d,
                                                              int max_bins, double* __restrict__ sorted,
                                                              double* __restrict__ thr, int* __restrict__ nthr,
-                                                             int* __restrict__ kdist) {
+                                                             int* __restrict__ kdist, float* __restrict__ thr32) {
   extern __shared__ double sv[];  // [P] (radix: the sort's storage first, then [s] sorted values)
   __shared__ int red_nn[kQThreads / 64], red_k[kQThreads / 64];
   __shared__ double cand[256];
@@ -126,6 +126,8 @@ __global__ __launch_bounds__(kQThreads) void quantile_kernel(const double* __res
       kdist[f] = kd;
       nthr[f] = 0;
     }
+    if (thr32)
+      for (int i = threadIdx.x; i < nb; i += kQThreads) thr32[(int64_t)f * nb + i] = 0.f;
     return;  // host path (few distinct values / categorical / empty)
   }
   // the quantile candidates (same operation order as the torch path)
@@ -161,9 +163,13 @@ __global__ __launch_bounds__(kQThreads) void quantile_kernel(const double* __res
         const double p = cand[i - 1];
         if (x == p || (x != x && p != p)) continue;
       }
+      if (thr32) thr32[(int64_t)f * nb + c] = (float)x;
       thr[(int64_t)f * nb + c++] = x;
     }
-    for (int i = c; i < nb; ++i) thr[(int64_t)f * nb + i] = 0.0;
+    for (int i = c; i < nb; ++i) {
+      thr[(int64_t)f * nb + i] = 0.0;
+      if (thr32) thr32[(int64_t)f * nb + i] = 0.f;
+    }
     nthr[f] = c;
     kdist[f] = kd;
   }
@@ -172,9 +178,10 @@ __global__ __launch_bounds__(kQThreads) void quantile_kernel(const double* __res
 }  // namespace
 
 // samp [s][d] fp64 row-major.  Outputs: sorted [d][s], thr [d][max_bins-1], nthr [d], kdist [d] (features with
-// kdist <= max_bins need the host path).  Returns hipErrorInvalidValue when s exceeds the LDS capacity.
+// kdist <= max_bins need the host path), thr32 (optional) = (float)thr for the binning kernel.  Returns
+// hipErrorInvalidValue when s exceeds the LDS capacity.
 CDNA_API int cdna_quantile_thresholds(const double* samp, int s, int d, int max_bins, double* sorted, double* thr,
-                                      int* nthr, int* kdist, hipStream_t st) {
+                                      int* nthr, int* kdist, float* thr32, hipStream_t st) {
   if (d <= 0 || s <= 0) return 0;
   if (s > kQMaxS || max_bins < 2 || max_bins > 257) return (int)hipErrorInvalidValue;
   int P = 1;
@@ -186,7 +193,8 @@ CDNA_API int cdna_quantile_thresholds(const double* samp, int s, int d, int max_
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds);
-    hipLaunchKernelGGL(kern, dim3(d), dim3(kQThreads), lds, st, samp, s, d, max_bins, sorted, thr, nthr, kdist);
+    hipLaunchKernelGGL(kern, dim3(d), dim3(kQThreads), lds, st, samp, s, d, max_bins, sorted, thr, nthr, kdist,
+                       thr32);
   };
   if (radix) launch(quantile_kernel<true>);
   else launch(quantile_kernel<false>);

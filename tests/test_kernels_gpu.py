@@ -160,6 +160,16 @@ def test_quantile_thresholds_kernel(dev, max_bins, s, f32):
     thr_h, nthr_h = find_thresholds(samp.numpy(), 37, max_bins, cats)
     assert np.array_equal(nthr_d, nthr_h)
     assert np.array_equal(thr_d, thr_h, equal_nan=True)
+    # the device-threshold path: the kernel's own fp32 copy is the fp64 thresholds rounded (the binning's input)
+    qd = K.quantile_thresholds_dev(samp.to(dev), max_bins)
+    if qd is not None:
+        t32, n32, pend = qd
+        t64, ints = pend.get()
+        assert t32.dtype == torch.float32 and np.array_equal(n32.cpu().numpy(), ints[0])
+        t32h = t32.cpu().numpy()
+        for f in range(37):  # the thresholds in use (nthr of them; the host path redoes the others)
+            k = int(ints[0][f])
+            assert np.array_equal(t32h[f, :k], t64[f, :k].astype(np.float32)), f
 
 
 @pytest.mark.parametrize("d", [21, 100])
