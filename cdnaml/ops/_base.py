@@ -41,17 +41,16 @@ class _PinnedRing:
     def take(self, nbytes: int):
         """(slot index, pinned uint8 view of nbytes) -- call ``done(slot, stream)`` once the copy is queued."""
         with self.lock:
-            if len(self.slots) < PINNED_RING:
-                self.slots.append([torch.empty(max(PINNED_SLOT, nbytes), dtype=torch.uint8, pin_memory=True), None])
-                k = len(self.slots) - 1
-            else:
-                k = self.i
-                self.i = (self.i + 1) % PINNED_RING
-                ev = self.slots[k][1]
-                if ev is not None and not ev.query():
-                    ev.synchronize()  # the slot's previous copy (PINNED_RING uploads ago) is still queued
-                if self.slots[k][0].numel() < nbytes:
-                    self.slots[k][0] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            if not self.slots:  # every slot at the first upload: the allocations stay out of later (timed) steps
+                self.slots = [[torch.empty(PINNED_SLOT, dtype=torch.uint8, pin_memory=True), None]
+                              for _ in range(PINNED_RING)]
+            k = self.i
+            self.i = (self.i + 1) % PINNED_RING
+            ev = self.slots[k][1]
+            if ev is not None and not ev.query():
+                ev.synchronize()  # the slot's previous copy (PINNED_RING uploads ago) is still queued
+            if self.slots[k][0].numel() < nbytes:
+                self.slots[k][0] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
             return k, self.slots[k][0][:nbytes]
 
     def done(self, k: int, stream) -> None:
