@@ -39,12 +39,12 @@ class FitBins:
     ``matches(X)``: X is the fit's source tensor -- same storage pointer, shape, strides, dtype and device, the
     source still alive (a weak reference: freed memory reused by another tensor never matches) and its version
     counter unchanged since the fit (an in-place write drops the match; DataFrames are immutable, and a write through
-    an alias that bypasses the version counter -- ``.data``, a DLPack / numpy view -- is not seen).  The bins serve ONE
-    transform (a fit is
-    typically followed by one pass over its own frame) and are released after it, or as soon as the source tensor
-    dies, so a kept model does not pin a second copy of the matrix: the next fit reuses their memory (holding them
-    across fits made the allocator map a fresh 10 GB segment at 1e8 x 100, a 240 ms stall).  Forests with
-    categorical features or missing-value bins are never given one."""
+    an alias that bypasses the version counter -- ``.data``, a DLPack / numpy view -- is not seen).
+
+    The bins serve ONE transform (a fit is typically followed by one pass over its own frame) and are released after
+    it, or as soon as the source tensor dies, so a kept model does not pin a second copy of the matrix: the next fit
+    reuses their memory (holding them across fits made the allocator map a fresh 10 GB segment at 1e8 x 100, a
+    240 ms stall).  Forests with categorical features or missing-value bins are never given one."""
 
     def __init__(self, src: torch.Tensor, bins: torch.Tensor, thresholds: np.ndarray, nthr: np.ndarray, d: int,
                  B: int):
